@@ -1,0 +1,101 @@
+// Shared helpers for the posekern HIP kernels (gfx950 / CDNA4, wave64).
+//
+// Every translation unit is compiled with -ffp-contract=off: kernels that must be
+// bit-exact against the CPU oracle (FPS, ball query, crop formation) rely on each
+// product and sum being rounded separately, exactly like numpy / torch-CPU do.
+// Kernels that want fused multiply-adds spell them out with fma()/fmaf().
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PK_OK 0
+#define PK_ERR_ARG 1000      // invalid argument (shape / size / null pointer)
+#define PK_ERR_CAPACITY 1001 // a variable-size output exceeded the caller's capacity
+
+#define PK_CHECK_LAUNCH()                                   \
+  do {                                                      \
+    hipError_t e__ = hipGetLastError();                     \
+    if (e__ != hipSuccess) return (int)e__;                 \
+  } while (0)
+
+#define PK_REQUIRE(cond)            \
+  do {                              \
+    if (!(cond)) return PK_ERR_ARG; \
+  } while (0)
+
+namespace pk {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    uint64_t o = __shfl_xor(v, off);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    uint64_t o = __shfl_xor(v, off);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int wave_sum_i32(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum_f32(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// Inclusive prefix sum across a wave (Hillis-Steele on shuffles).
+__device__ __forceinline__ int wave_inclusive_scan_i32(int v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    int o = __shfl_up(v, off);
+    if (lane >= off) v += o;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int64_t wave_inclusive_scan_i64(int64_t v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    int64_t o = __shfl_up(v, off);
+    if (lane >= off) v += o;
+  }
+  return v;
+}
+
+// Bits of a non-negative float are monotone as an unsigned integer.
+__device__ __forceinline__ uint32_t f32_bits(float f) { return __float_as_uint(f); }
+
+// Order-preserving map of any float to uint32 (for min/max keys on signed values).
+__device__ __forceinline__ uint32_t f32_ordered(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace pk

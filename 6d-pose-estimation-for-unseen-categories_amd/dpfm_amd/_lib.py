@@ -1,0 +1,76 @@
+"""ctypes binding of libposekern.so (the C-ABI declared in include/posekern.h).
+
+The library is built in-tree by `make -C 6d-pose-estimation-for-unseen-categories_amd`
+(or __graft_entry__.build()). There is no CPU fallback: if the library is missing or
+a tensor is not on a HIP device, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch  # noqa: F401  (loads torch's HIP runtime first so the library binds to it)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libposekern.so")
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_U64 = ctypes.c_uint64
+_D = ctypes.c_double
+_F = ctypes.c_float
+
+# name -> argtypes, mirroring include/posekern.h one for one.
+SIGNATURES = {
+    "pk_fps": [_P, _P, _I, _I, _P, _P, _P, _I, _P],
+    "pk_ball_query_mask": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P],
+    "pk_ball_query_pairs": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _I64, _P, _P, _P, _P],
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class PoseKernError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PoseKernError(
+                f"libposekern.so not found at {LIB_PATH}: build it with "
+                "`make -C 6d-pose-estimation-for-unseen-categories_amd` (no CPU fallback exists)")
+        l = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(l, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        _lib = l
+    return _lib
+
+
+_ERRORS = {1000: "invalid argument", 1001: "output capacity exceeded"}
+
+
+def call(name: str, *args) -> None:
+    status = getattr(lib(), name)(*args)
+    if status != 0:
+        msg = _ERRORS.get(status, f"hipError_t {status}")
+        raise PoseKernError(f"{name} failed: {msg}")
+
+
+def ptr(t: Optional[torch.Tensor]):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise PoseKernError("posekern ops take HIP device tensors only (no CPU fallback)")
+    if not t.is_contiguous():
+        raise PoseKernError("posekern ops need contiguous tensors")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream(device: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,379 @@
+"""Literal CPU restatements of the reference hot path — TEST INFRASTRUCTURE ONLY.
+
+Each function cites the /root/reference file:line it restates. Upstream code from
+the un-vendored DPFM submodule and Open3D is restated from their public sources
+ and is marked "parity unpinned".
+
+Nothing here is imported by the product package.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+# --------------------------------------------------------------------------------------
+# H1  crop formation: dataset/object.py:52-88
+# --------------------------------------------------------------------------------------
+
+
+def erode_seg_mask(mask: np.ndarray, kernel_size: int = 3) -> np.ndarray:
+    """dataset/object.py:52-71 — cv2.erode(uint8*255, plus-shaped 3x3, iterations=1).
+
+    OpenCV's default border for erosion (BORDER_CONSTANT with
+    morphologyDefaultBorderValue) never erodes at the image edge, so pixels outside
+    the image are ignored. OpenCV itself is absent here: parity unpinned, exact by
+    construction for a binary min filter.
+    """
+    assert kernel_size == 3
+    m = mask.astype(bool)
+    out = m.copy()
+    out[1:, :] &= m[:-1, :]
+    out[:-1, :] &= m[1:, :]
+    out[:, 1:] &= m[:, :-1]
+    out[:, :-1] &= m[:, 1:]
+    return out
+
+
+def dpt_2_pcld(dpt: np.ndarray, cam_scale: float, K: np.ndarray, mask: np.ndarray) -> np.ndarray:
+    """dataset/object.py:73-88 (erosion at :80). Returns f64 [P,3] in cm, row-major pixel order."""
+    idx = np.indices(dpt.shape[:2])
+    xmap = idx[0]
+    ymap = idx[1]
+    if len(dpt.shape) > 2:
+        dpt = dpt[:, :, 0]
+    dpt = dpt.astype(np.float32) / np.float32(cam_scale)
+    mask = erode_seg_mask(mask, 3)
+    dpt = dpt[mask]
+    row = (ymap[mask] - K[0, 2]) * dpt.astype(np.float64) / K[0, 0]
+    col = (xmap[mask] - K[1, 2]) * dpt.astype(np.float64) / K[1, 1]
+    dpt_3d = np.concatenate((row[..., None], col[..., None], dpt.astype(np.float64)[..., None]), axis=1)
+    return dpt_3d * 100
+
+
+# --------------------------------------------------------------------------------------
+# H2  statistical outlier removal: dataset/object.py:33-50 -> Open3D 0.17
+#     PointCloud::RemoveStatisticalOutliers(nb_neighbors=20, std_ratio=0.3)
+#     (parity unpinned: Open3D absent; restated per SURVEY.md Appendix A)
+# --------------------------------------------------------------------------------------
+
+
+def sor_avg_distances(pcd: np.ndarray, nb_neighbors: int = 20) -> np.ndarray:
+    """Per point: mean of sqrt(squared distance) to its nb nearest points (self included),
+    squared distances as ((dx²+dy²)+dz²) in fp64, summed in ascending order."""
+    n = pcd.shape[0]
+    k = min(nb_neighbors, n)
+    out = np.empty(n, dtype=np.float64)
+    for s in range(0, n, 512):
+        d = pcd[s:s + 512, None, :] - pcd[None, :, :]
+        sq = (d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]
+        part = np.partition(sq, k - 1, axis=1)[:, :k]
+        part.sort(axis=1)
+        r = np.sqrt(part)
+        acc = np.zeros(r.shape[0])
+        for c in range(k):  # std::accumulate, left to right
+            acc = acc + r[:, c]
+        out[s:s + 512] = acc / k
+    return out
+
+
+def remove_outliers_indices(pcd: np.ndarray, nb_neighbors: int = 20, std_ratio: float = 0.3) -> np.ndarray:
+    avg = sor_avg_distances(pcd, nb_neighbors)
+    valid = avg.shape[0]
+    if valid == 0:
+        return np.zeros(0, dtype=np.int64)
+    mean = 0.0
+    for a in avg:  # accumulate, skipping non-positive entries
+        if a > 0:
+            mean = mean + a
+    mean = mean / valid
+    sq = 0.0
+    for a in avg:
+        sq = sq + ((a - mean) * (a - mean) if a > 0 else 0.0)
+    std = math.sqrt(sq / (valid - 1)) if valid > 1 else float("nan")
+    thr = mean + std_ratio * std
+    return np.nonzero((avg > 0) & (avg < thr))[0].astype(np.int64)
+
+
+def remove_outliers(pcd: np.ndarray) -> np.ndarray:
+    """dataset/object.py:33-50."""
+    return pcd[remove_outliers_indices(pcd, 20, 0.3)]
+
+
+# --------------------------------------------------------------------------------------
+# H3  farthest point sampling: upstream DPFM dpfm/utils.py::farthest_point_sample,
+#     called at dataset/object.py:145-148 (parity unpinned; Appendix A)
+# --------------------------------------------------------------------------------------
+
+
+def farthest_point_sample(xyz: torch.Tensor, ratio: float, start: int, npoint: int | None = None) -> torch.Tensor:
+    """Literal torch-CPU restatement. xyz f32 [3, N]; `start` replaces torch.randint(0, N)."""
+    xyz = xyz.t().unsqueeze(0)
+    B, N, C = xyz.shape
+    if npoint is None:
+        npoint = int(ratio * N)
+    centroids = torch.zeros(B, npoint, dtype=torch.long)
+    distance = torch.ones(B, N) * 1e10
+    farthest = torch.tensor([start], dtype=torch.long)
+    batch_indices = torch.arange(B, dtype=torch.long)
+    for i in range(npoint):
+        centroids[:, i] = farthest
+        centroid = xyz[batch_indices, farthest, :].view(B, 1, 3)
+        dist = torch.sum((xyz - centroid) ** 2, -1)
+        mask = dist < distance
+        distance[mask] = dist[mask]
+        farthest = torch.max(distance, -1)[1]
+    return centroids[0]
+
+
+def fps_npoint(n: int) -> int:
+    """dataset/object.py:145-147: ratio = 2000/N, npoint = int(ratio * N) (1999 or 2000)."""
+    ratio = 2000 / n
+    return int(ratio * n)
+
+
+# --------------------------------------------------------------------------------------
+# H4  transform: dataset/object.py:304-309 (inv=True -> object frame, "align_pc")
+# --------------------------------------------------------------------------------------
+
+
+def transform(pc: np.ndarray, R: np.ndarray, t: np.ndarray, inv: bool = False) -> np.ndarray:
+    """`pc @ R + (-t @ R)` for inv, `pc @ R.T + t` otherwise; the 3-term dot products are
+    evaluated left to right with separately rounded products (BLAS-order independent)."""
+    pc = np.asarray(pc, dtype=np.float64)
+    R = np.asarray(R, dtype=np.float64)
+    t = np.asarray(t, dtype=np.float64).reshape(3)
+    M = R if inv else R.T
+    if inv:
+        nt = -1.0 * t
+        tt = np.array([(nt[0] * R[0, j] + nt[1] * R[1, j]) + nt[2] * R[2, j] for j in range(3)])
+    else:
+        tt = t
+    out = np.empty_like(pc)
+    for j in range(3):
+        out[:, j] = ((pc[:, 0] * M[0, j] + pc[:, 1] * M[1, j]) + pc[:, 2] * M[2, j]) + tt[j]
+    return out
+
+
+# --------------------------------------------------------------------------------------
+# H5  ball query: dataset/object.py:281-288 find_positives, :311-317 get_overlap
+# --------------------------------------------------------------------------------------
+
+
+def find_positives(pc1: np.ndarray, pc2: np.ndarray, r: float = 0.2) -> np.ndarray:
+    distances = np.linalg.norm(pc1[:, np.newaxis] - pc2, axis=2)
+    mask = distances <= r
+    return np.argwhere(mask.astype(bool))
+
+
+def find_positives_mask(pc1: np.ndarray, pc2: np.ndarray, r: float) -> np.ndarray:
+    return np.linalg.norm(pc1[:, np.newaxis] - pc2, axis=2) <= r
+
+
+def get_overlap(l_1: int, l_2: int, p: np.ndarray):
+    overlap_12 = np.zeros((l_1), dtype=np.byte)
+    overlap_21 = np.zeros((l_2), dtype=np.byte)
+    overlap_12[p[:, 0]] = 1
+    overlap_21[p[:, 1]] = 1
+    return overlap_12, overlap_21
+
+
+# --------------------------------------------------------------------------------------
+# H10 / H11  fmap -> point map: fmap2pointmap_solvers/naive.py:6-34,
+#            spacial_filtering.py:5-75
+# --------------------------------------------------------------------------------------
+
+
+def naive_nn_query(feat_x: torch.Tensor, feat_y: torch.Tensor, dim: int = -2) -> torch.Tensor:
+    dist = torch.cdist(feat_x, feat_y)
+    return dist.argmin(dim=dim)
+
+
+def naive_fmap2pointmap(C12, evecs_x, evecs_y, **kwargs):
+    if C12.dim() == 3:
+        C12 = C12.squeeze(0)
+    pp = naive_nn_query(torch.matmul(evecs_x, C12.t()), evecs_y)
+    return torch.stack([pp, torch.linspace(0, pp.shape[0] - 1, pp.shape[0], device=pp.device).type(torch.int16)], 0)
+
+
+def topk_nn_query(feat_x, feat_y, K: int = 5):
+    """spacial_filtering.py:20-38 (sort along V1, first K rows per column, PC-major)."""
+    dist = torch.cdist(feat_x, feat_y)
+    _, idx = dist.sort(dim=-2, stable=True)
+    idx = idx.t()[:, :K]
+    idx_p = torch.linspace(0, idx.shape[0] - 1, idx.shape[0]).type(torch.int16).unsqueeze(1).repeat(1, K)
+    return torch.stack([idx, idx_p], 0).reshape(2, -1)
+
+
+def euclidean_distance(tensor):
+    squared_distances = torch.sum((tensor[:, None] - tensor) ** 2, dim=2)
+    return torch.sqrt(squared_distances)
+
+
+def rigidity_scores(CAD, PC, p_pred):
+    B = euclidean_distance(PC[p_pred[1]])
+    A = euclidean_distance(CAD[p_pred[0]])
+    return torch.absolute(A - B).mean(0)
+
+
+def spacial_filtering(CAD, PC, p_pred, diam_cad, return_scores: bool = False):
+    """spacial_filtering.py:51-75."""
+    scores = []
+    s = rigidity_scores(CAD, PC, p_pred)
+    scores.append(s)
+    p_pred = p_pred[:, s < 0.3 * diam_cad]
+    s = rigidity_scores(CAD, PC, p_pred)
+    scores.append(s)
+    p_pred = p_pred[:, s < 0.15 * diam_cad]
+    s = rigidity_scores(CAD, PC, p_pred)
+    scores.append(s)
+    if (s < 0.055 * diam_cad).sum() == 0:
+        p_pred = p_pred[:, s < 0.065 * diam_cad]
+    else:
+        p_pred = p_pred[:, s < 0.055 * diam_cad]
+    if return_scores:
+        return p_pred, scores
+    return p_pred
+
+
+def spacial_filtering_fmap2pointmap(C12, evecs_x, evecs_y, CAD, PC, diam_cad):
+    if C12.dim() == 3:
+        C12 = C12.squeeze(0)
+    pp = topk_nn_query(torch.matmul(evecs_x[:], C12.t()), evecs_y[:])
+    return spacial_filtering(CAD, PC, pp, diam_cad)
+
+
+# --------------------------------------------------------------------------------------
+# H12  inlier ratio: utils/utils.py:81-105 ; H15 C_gt: utils/utils.py:67-79
+# --------------------------------------------------------------------------------------
+
+
+def compute_inlier_ratio(pred_corr, CAD, PC_aligned, threshold):
+    total_corr = len(pred_corr)
+    if total_corr == 0:
+        return 0
+    CAD = CAD[pred_corr[:, 0]]
+    PC_aligned = PC_aligned[pred_corr[:, 1]]
+    sq_dist = torch.square(CAD - PC_aligned).sum(-1) ** 0.5
+    inliers = (sq_dist < (threshold)).sum()
+    return inliers / total_corr
+
+
+def C_from_sparse_P(P, evecs1, evecs2):
+    evec_1_a, evec_2_a = evecs1[P[:, 0]], evecs2[P[:, 1]]
+    return torch.linalg.lstsq(evec_2_a, evec_1_a)[0][:evec_1_a.size(-1)]
+
+
+# --------------------------------------------------------------------------------------
+# H13  RANSAC + Umeyama: scripts/test_RANSAC.py:288-310 -> Open3D 0.17
+#      registration_ransac_based_on_correspondence + Eigen::umeyama (Appendix A).
+#      Hypothesis index sets are inputs (Open3D's RNG is not reproducible).
+# --------------------------------------------------------------------------------------
+
+
+def umeyama(src: np.ndarray, dst: np.ndarray) -> np.ndarray:
+    """Eigen::umeyama(src[3,n], dst[3,n], with_scaling=false) -> 4x4."""
+    n = src.shape[1]
+    one_over_n = 1.0 / n
+    src_mean = src.sum(axis=1) * one_over_n
+    dst_mean = dst.sum(axis=1) * one_over_n
+    src_demean = src - src_mean[:, None]
+    dst_demean = dst - dst_mean[:, None]
+    sigma = one_over_n * dst_demean @ src_demean.T
+    U, S, Vt = np.linalg.svd(sigma)
+    D = np.ones(3)
+    if np.linalg.det(U) * np.linalg.det(Vt.T) < 0:
+        D[2] = -1
+    T = np.eye(4)
+    T[:3, :3] = U @ np.diag(D) @ Vt
+    T[:3, 3] = dst_mean - T[:3, :3] @ src_mean
+    return T
+
+
+def ransac_evaluate(src: np.ndarray, dst: np.ndarray, corres: np.ndarray, T: np.ndarray, max_dist: float):
+    """Open3D EvaluateRANSACBasedOnCorrespondence: fitness, inlier_rmse."""
+    s = src[corres[:, 0]]
+    p = (s @ T[:3, :3].T) + T[:3, 3]
+    d = p - dst[corres[:, 1]]
+    dis2 = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+    inl = dis2 < max_dist * max_dist
+    good = int(inl.sum())
+    if good == 0:
+        return 0.0, 0.0
+    return good / corres.shape[0], math.sqrt(float(dis2[inl].sum()) / good)
+
+
+def ransac_registration(src, dst, corres, hyps, max_dist=0.05):
+    """Best hypothesis by (fitness desc, rmse asc, index asc). hyps: int [H,4] row ids into corres."""
+    best = (-1.0, 0.0, -1, np.eye(4))
+    if corres.shape[0] < 4 or max_dist <= 0:
+        return np.eye(4), 0.0, 0.0, -1
+    for h in range(hyps.shape[0]):
+        c = corres[hyps[h]]
+        T = umeyama(src[c[:, 0]].T, dst[c[:, 1]].T)
+        f, r = ransac_evaluate(src, dst, corres, T, max_dist)
+        if f > best[0] or (f == best[0] and r < best[1]):
+            best = (f, r, h, T)
+    return best[3], best[0], best[1], best[2]
+
+
+# --------------------------------------------------------------------------------------
+# H14  pose metrics: scripts/test_RANSAC.py:77-81, 154-238
+# --------------------------------------------------------------------------------------
+
+
+def pose_transform(pcd, pose):
+    """test_RANSAC.py:154-160."""
+    pcd_ = pcd @ pose[:3, :3].T
+    return pcd_ + pose[:3:, -1]
+
+
+def add(T_est, T_gt, pcd, diameter, percentage=0.1):
+    """test_RANSAC.py:162-173."""
+    pts_est = pose_transform(pcd, T_est)
+    pts_gt = pose_transform(pcd, T_gt)
+    e = np.linalg.norm(pts_est - pts_gt, axis=1).mean()
+    return e, int(e < diameter * percentage)
+
+
+def compute_add_score(pts3d, diameter, pose_gt, pose_pred, percentage=0.1):
+    """test_RANSAC.py:186-201 (per-row "xyz direction" quirk, count = 3)."""
+    R_gt, t_gt = pose_gt[:3, :3], pose_gt[:3, 3]
+    R_pred, t_pred = pose_pred[:3, :3], pose_pred[:3, 3]
+    count = R_gt.shape[0]
+    mean_distances = np.zeros((count,), dtype=np.float32)
+    for i in range(count):
+        a = R_gt[i].reshape((1, 3)).dot(pts3d.transpose()) + t_gt[i]
+        b = R_pred[i].reshape((1, 3)).dot(pts3d.transpose()) + t_pred[i]
+        mean_distances[i] = np.mean(np.linalg.norm(a - b, axis=0))
+    threshold = diameter * percentage
+    return (mean_distances < threshold).sum() / count
+
+
+def compute_adds_score(pts3d, diameter, pose_gt, pose_pred, percentage=0.1):
+    """test_RANSAC.py:203-222 — 1-NN (KDTree) on the per-row 1-D projections."""
+    R_gt, t_gt = pose_gt[:3, :3], pose_gt[:3, 3]
+    R_pred, t_pred = pose_pred[:3, :3], pose_pred[:3, 3]
+    count = R_gt.shape[0]
+    mean_distances = np.zeros((count,), dtype=np.float32)
+    for i in range(count):
+        if np.isnan(np.sum(t_pred[i])):
+            mean_distances[i] = np.inf
+            continue
+        a = (R_gt[i].reshape((1, 3)).dot(pts3d.transpose()) + t_gt[i]).ravel()
+        b = (R_pred[i].reshape((1, 3)).dot(pts3d.transpose()) + t_pred[i]).ravel()
+        sa = np.sort(a)
+        pos = np.clip(np.searchsorted(sa, b), 1, len(sa) - 1)
+        d0 = b - sa[pos - 1]
+        d1 = sa[pos] - b
+        # sklearn KDTree reports sqrt(rdist) with rdist = d*d
+        d = np.minimum(np.sqrt(d0 * d0), np.sqrt(d1 * d1))
+        mean_distances[i] = np.mean(d)
+    threshold = diameter * percentage
+    return (mean_distances < threshold).sum() / count
+
+
+def get_angular_error(R_exp, R_est):
+    """test_RANSAC.py:77-81."""
+    return abs(np.arccos(min(max(((np.matmul(R_exp.T, R_est)).trace() - 1) / 2, -1.0), 1.0)))

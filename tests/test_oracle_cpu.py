@@ -1,0 +1,134 @@
+"""CPU: the oracle's restatements agree with each other (torch literal vs C vs numpy)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dpfm_oracle as O
+from _util import c_fps, c_ball_query, boundary_cloud
+
+
+@pytest.mark.parametrize("n,npoint,dups", [(50, 50, 0), (300, 64, 0), (257, 100, 40), (2345, 2000, 0)])
+def test_fps_torch_literal_matches_c(coracle, n, npoint, dups):
+    rng = np.random.default_rng(n)
+    xyz = (rng.normal(size=(n, 3)) * 7 + np.array([0, 0, 110])).astype(np.float32)
+    if dups:  # exact duplicates exercise the first-index tie rule
+        xyz[rng.integers(0, n, dups)] = xyz[rng.integers(0, n, dups)]
+    start = int(rng.integers(0, n))
+    ref = O.farthest_point_sample(torch.from_numpy(xyz).t(), ratio=npoint / n, start=start, npoint=npoint).numpy()
+    got = c_fps(coracle, xyz, start, npoint)
+    np.testing.assert_array_equal(ref, got)
+
+
+def test_fps_npoint_rounding():
+    # dataset/object.py:146-147: int(2000/N * N) is 1999 for some N (as the published crops show)
+    vals = {O.fps_npoint(n) for n in range(2001, 6000)}
+    assert vals == {1999, 2000}
+
+
+def test_torch_sum3_is_left_to_right():
+    rng = np.random.default_rng(0)
+    a = rng.normal(size=(100000, 3)).astype(np.float32) * 100
+    t = torch.sum(torch.from_numpy(a) ** 2, -1).numpy()
+    m = (a[:, 0] * a[:, 0] + a[:, 1] * a[:, 1]) + a[:, 2] * a[:, 2]
+    np.testing.assert_array_equal(t, m)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_ball_query_numpy_matches_c_and_threshold(coracle, seed):
+    import importlib
+    ops = importlib.import_module("dpfm_amd.ops")
+    rng = np.random.default_rng(seed)
+    r = 0.05 * 13.7
+    pc1, pc2 = boundary_cloud(rng, 400, 300, r)
+    ref = O.find_positives(pc1, pc2, r)
+    pairs, o12, o21 = c_ball_query(coracle, pc1, pc2, r)
+    np.testing.assert_array_equal(ref, pairs)
+    e12, e21 = O.get_overlap(400, 300, ref)
+    np.testing.assert_array_equal(e12, o12)
+    np.testing.assert_array_equal(e21, o21)
+    # sqrt(s) <= r  <=>  s <= T(r) on the numpy sums (the kernel's test)
+    d = pc1[:, None] - pc2
+    s = (d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]
+    np.testing.assert_array_equal(np.argwhere(s <= ops.ball_threshold(r)), ref)
+
+
+def test_ball_threshold_exact():
+    import importlib
+    ops = importlib.import_module("dpfm_amd.ops")
+    rng = np.random.default_rng(3)
+    for r in list(rng.uniform(0.1, 2.0, 200)) + [0.5, 0.25, 1.0, 0.7]:
+        T = ops.ball_threshold(r)
+        assert math.sqrt(T) <= r
+        assert math.sqrt(math.nextafter(T, math.inf)) > r
+
+
+def test_erode_plus_kernel():
+    m = np.zeros((6, 7), bool)
+    m[1:5, 1:6] = True
+    m[0, 3] = True
+    e = O.erode_seg_mask(m)
+    exp = np.zeros_like(m)
+    exp[2:4, 2:5] = True
+    exp[1, 3] = True  # plus kernel: (1,3) sees (0,3),(2,3),(1,2),(1,4) all set
+    np.testing.assert_array_equal(e, exp)
+    # border pixels are not eroded by the image edge (cv2 default border)
+    full = np.ones((4, 4), bool)
+    assert O.erode_seg_mask(full).all()
+
+
+def test_transform_inverse_roundtrip():
+    rng = np.random.default_rng(5)
+    from dpfm_amd.dataset.synthetic import random_rotation
+    R = random_rotation(rng)
+    t = rng.normal(size=3) * 50
+    obj = rng.normal(size=(100, 3)) * 5
+    cam = O.transform(obj, R, t, inv=False)
+    back = O.transform(cam, R, t, inv=True)
+    np.testing.assert_allclose(back, obj, atol=1e-10)
+
+
+def test_umeyama_recovers_rigid_transform(coracle):
+    import ctypes
+    from _util import cp
+    from dpfm_amd.dataset.synthetic import random_rotation
+    rng = np.random.default_rng(7)
+    for _ in range(20):
+        R = random_rotation(rng)
+        t = rng.normal(size=3) * 30
+        src = np.ascontiguousarray(rng.normal(size=(4, 3)) * 5)
+        dst = np.ascontiguousarray(src @ R.T + t)
+        T = O.umeyama(src.T, dst.T)
+        np.testing.assert_allclose(T[:3, :3], R, atol=1e-9)
+        np.testing.assert_allclose(T[:3, 3], t, atol=1e-8)
+        Rc = np.zeros(9)
+        tc = np.zeros(3)
+        coracle.oc_umeyama(cp(src), cp(dst), 4, cp(Rc), cp(tc))
+        np.testing.assert_allclose(Rc.reshape(3, 3), R, atol=1e-9)
+        np.testing.assert_allclose(tc, t, atol=1e-8)
+
+
+def test_ransac_c_matches_python(coracle):
+    from _util import cp
+    from dpfm_amd.dataset.synthetic import random_rotation
+    rng = np.random.default_rng(11)
+    R = random_rotation(rng)
+    t = rng.normal(size=3) * 30
+    src = rng.normal(size=(200, 3)) * 5
+    dst = src @ R.T + t
+    n = 150
+    corres = np.stack([rng.integers(0, 200, n), rng.integers(0, 200, n)], 1).astype(np.int32)
+    good = rng.random(n) < 0.4
+    corres[good, 1] = corres[good, 0]
+    dst = np.ascontiguousarray(dst + rng.normal(size=dst.shape) * 0.01)
+    H = 300
+    hyps = np.array([[coracle.oc_hyp_index(42, h, j, n) for j in range(4)] for h in range(H)], dtype=np.int32)
+    Tp, f, rm, hb = O.ransac_registration(src, dst, corres, hyps, 0.05)
+    T = np.zeros(16)
+    st = np.zeros(3)
+    coracle.oc_ransac(cp(np.ascontiguousarray(src)), cp(dst), cp(np.ascontiguousarray(corres)), n, None, 42, H, 0.05,
+                      cp(T), cp(st))
+    assert int(st[2]) == hb
+    assert st[0] == f
+    np.testing.assert_allclose(T.reshape(4, 4), Tp, atol=1e-9)
