@@ -94,6 +94,109 @@ __global__ __launch_bounds__(kBqThreads) void bq_mask_kernel(
   }
 }
 
+// fp32-screened variant (the default). Coordinates are centred on the crop's first CAD
+// point in fp64 and rounded to fp32 once per point. Each pair's squared distance is
+// evaluated in fp32 by the expansion s32 = (|a|² + |b|²) - 2 a·b (one add + three FMAs
+// with -2b and |b|² precomputed per column) and classified against
+// [thr2 - margin, thr2 + margin]; only pairs inside that band are recomputed with the
+// exact fp64 recipe, so the mask stays bit-exact. `margin` bounds |s32 - s64| for any
+// pair that can land on either side of thr2 (DESIGN.md §Ball query has the derivation).
+//
+// grid (ceil(n1max / 64), B), block 256 = 4 waves; a wave owns 16 CAD rows and walks
+// every 1024-column chunk of the crop (lane = 16 consecutive columns, one 16-B store
+// per row and chunk), so row counts are complete per wave: plain stores, no atomics.
+__global__ __launch_bounds__(kBqThreads) void bq_mask_f32_kernel(
+    const double* __restrict__ cad, const int64_t* __restrict__ cad_off,
+    const double* __restrict__ pc, const int64_t* __restrict__ pc_off,
+    const double* __restrict__ thr2v, int n1max, int ld, uint8_t* __restrict__ mask,
+    int32_t* __restrict__ rowcount) {
+  const int b = blockIdx.y;
+  const int64_t c0 = cad_off[b], p0 = pc_off[b];
+  const int n1 = (int)(cad_off[b + 1] - c0);
+  const int n2 = (int)(pc_off[b + 1] - p0);
+  const double thr2 = thr2v[b];
+  const int lane = pk::lane_id();
+  const int row0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kRowsPerBlock + pk::wave_id() * kRowsPerWave);
+  if (row0 >= n1max) return;
+  const double ox = n1 > 0 ? cad[c0 * 3 + 0] : 0.0;
+  const double oy = n1 > 0 ? cad[c0 * 3 + 1] : 0.0;
+  const double oz = n1 > 0 ? cad[c0 * 3 + 2] : 0.0;
+  const float u = 5.9604645e-8f;  // 2^-24
+  const float thr2f = (float)thr2;
+  const float R = sqrtf(thr2f) * 1.001f;
+  const int ncols = mask != nullptr ? ld : n2;
+
+  __shared__ int cnt_s[kBqThreads / pk::kWave][kRowsPerWave];  // per-wave row totals
+  int* cnt = cnt_s[pk::wave_id()];
+  if (lane < kRowsPerWave) cnt[lane] = 0;
+
+  for (int jc = 0; jc < ncols; jc += kColsPerWave) {
+    const int j0 = jc + lane * kColsPerLane;
+    float mx[kColsPerLane], my[kColsPerLane], mz[kColsPerLane], b2[kColsPerLane];
+    float bm = 0.f;
+#pragma unroll
+    for (int c = 0; c < kColsPerLane; ++c) {
+      const int j = j0 + c;
+      if (j < n2) {
+        const double* q = pc + (p0 + j) * 3;
+        const float bx = (float)(q[0] - ox), by = (float)(q[1] - oy), bz = (float)(q[2] - oz);
+        mx[c] = -2.f * bx;
+        my[c] = -2.f * by;
+        mz[c] = -2.f * bz;
+        b2[c] = fmaf(bz, bz, fmaf(by, by, bx * bx));
+        bm = fmaxf(bm, fmaxf(fabsf(bx), fmaxf(fabsf(by), fabsf(bz))));
+      } else {
+        mx[c] = my[c] = mz[c] = 0.f;
+        b2[c] = __builtin_huge_valf();  // never within
+      }
+    }
+#pragma unroll 1
+    for (int r = 0; r < kRowsPerWave; ++r) {
+      const int i = row0 + r;
+      if (i >= n1max) break;
+      uint32_t inm = 0;
+      if (i < n1) {
+        const double* a = cad + (c0 + i) * 3;
+        const double ax64 = a[0], ay64 = a[1], az64 = a[2];
+        const float ax = (float)(ax64 - ox), ay = (float)(ay64 - oy), az = (float)(az64 - oz);
+        const float a2 = fmaf(az, az, fmaf(ay, ay, ax * ax));
+        const float S = fmaxf(fabsf(ax), fmaxf(fabsf(ay), fabsf(az))) + bm;
+        const float E0 = 1.01f * u * S;
+        const float margin = 2.f * (3.f * E0 * (2.f * R + E0) + 21.f * u * S * S + 2.f * u * thr2f) + 1e-30f;
+        const float lo = thr2f - margin, hi = thr2f + margin;
+        uint32_t him = 0;
+#pragma unroll
+        for (int c = 0; c < kColsPerLane; ++c) {
+          const float sq = fmaf(ax, mx[c], fmaf(ay, my[c], fmaf(az, mz[c], a2 + b2[c])));
+          inm |= (sq <= lo ? 1u : 0u) << c;
+          him |= (sq <= hi ? 1u : 0u) << c;
+        }
+        uint32_t amb = him & ~inm;
+        if (__builtin_expect(amb != 0, 0)) {  // rare: exact fp64 recheck of the band
+          while (amb) {
+            const int c = __ffs(amb) - 1;
+            amb &= amb - 1;
+            const double* q = pc + (p0 + j0 + c) * 3;
+            if (within(ax64, ay64, az64, q[0], q[1], q[2], thr2)) inm |= 1u << c;
+          }
+        }
+        const int tot = pk::wave_sum_i32_s(__popc(inm));
+        if (lane == 0) cnt[r] += tot;  // same wave only: program order, no barrier
+      }
+      if (mask != nullptr && j0 < ld) {
+        // spread 4 mask bits into 4 bytes: (nibble * 0x204081) & 0x01010101
+        const uint32_t w0 = ((inm & 0xfu) * 0x204081u) & 0x01010101u;
+        const uint32_t w1 = (((inm >> 4) & 0xfu) * 0x204081u) & 0x01010101u;
+        const uint32_t w2 = (((inm >> 8) & 0xfu) * 0x204081u) & 0x01010101u;
+        const uint32_t w3 = (((inm >> 12) & 0xfu) * 0x204081u) & 0x01010101u;
+        uint4* dst = reinterpret_cast<uint4*>(mask + ((int64_t)b * n1max + i) * ld + j0);
+        *dst = make_uint4(w0, w1, w2, w3);
+      }
+    }
+  }
+  if (lane < kRowsPerWave && row0 + lane < n1max) rowcount[(int64_t)b * n1max + row0 + lane] = cnt[lane];
+}
+
 // Count-only variant (no mask); same arithmetic.
 __global__ __launch_bounds__(kBqThreads) void bq_count_kernel(
     const double* __restrict__ cad, const int64_t* __restrict__ cad_off,
@@ -233,18 +336,24 @@ extern "C" int pk_ball_query_mask(const double* cad, const int64_t* cad_off, con
   PK_REQUIRE(cad && cad_off && pc && pc_off && thr2 && rowcount);
   PK_REQUIRE(mask == nullptr || (ld >= n2max && ld % kColsPerLane == 0));
   hipStream_t s = pk::as_stream(stream);
+  dim3 grid((n1max + kRowsPerBlock - 1) / kRowsPerBlock, B);
+  hipLaunchKernelGGL(bq_mask_f32_kernel, grid, dim3(kBqThreads), 0, s, cad, cad_off, pc, pc_off,
+                     thr2, n1max, ld, mask, rowcount);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+// Development hook (not in include/posekern.h): the all-fp64 mask kernel, for A/B timing.
+extern "C" int pkdev_ball_query_mask64(const double* cad, const int64_t* cad_off, const double* pc,
+                                       const int64_t* pc_off, const double* thr2, int B, int n1max,
+                                       int n2max, uint8_t* mask, int ld, int32_t* rowcount,
+                                       void* stream) {
+  hipStream_t s = pk::as_stream(stream);
   hipError_t e = hipMemsetAsync(rowcount, 0, sizeof(int32_t) * (size_t)B * n1max, s);
   if (e != hipSuccess) return (int)e;
-  const int ncols = mask != nullptr ? ld : n2max;
-  dim3 grid((ncols + kColsPerWave - 1) / kColsPerWave, (n1max + kRowsPerBlock - 1) / kRowsPerBlock, B);
-  if (grid.x == 0) grid.x = 1;
-  if (mask != nullptr) {
-    hipLaunchKernelGGL(bq_mask_kernel, grid, dim3(kBqThreads), 0, s, cad, cad_off, pc, pc_off,
-                       thr2, n1max, ld, mask, rowcount);
-  } else {
-    hipLaunchKernelGGL(bq_count_kernel, grid, dim3(kBqThreads), 0, s, cad, cad_off, pc, pc_off,
-                       thr2, n1max, rowcount);
-  }
+  dim3 grid((ld + kColsPerWave - 1) / kColsPerWave, (n1max + kRowsPerBlock - 1) / kRowsPerBlock, B);
+  hipLaunchKernelGGL(bq_mask_kernel, grid, dim3(kBqThreads), 0, s, cad, cad_off, pc, pc_off, thr2,
+                     n1max, ld, mask, rowcount);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -99,3 +99,67 @@ __device__ __forceinline__ uint32_t f32_ordered(float f) {
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace pk
+
+namespace pk {
+
+// ---- DPP row (16-lane) all-reductions, u32. After the call every lane of a 16-lane
+// row holds the row's reduction. dpp_ctrl: quad_perm[1,0,3,2]=0xB1, quad_perm[2,3,0,1]
+// =0x4E, row_half_mirror=0x141, row_mirror=0x140.
+#define PK_DPP(v, ctrl) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v), ctrl, 0xF, 0xF, false))
+
+__device__ __forceinline__ uint32_t row_max_u32(uint32_t v) {
+  uint32_t o;
+  o = PK_DPP(v, 0xB1); v = o > v ? o : v;
+  o = PK_DPP(v, 0x4E); v = o > v ? o : v;
+  o = PK_DPP(v, 0x141); v = o > v ? o : v;
+  o = PK_DPP(v, 0x140); v = o > v ? o : v;
+  return v;
+}
+
+__device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {
+  uint32_t o;
+  o = PK_DPP(v, 0xB1); v = o < v ? o : v;
+  o = PK_DPP(v, 0x4E); v = o < v ? o : v;
+  o = PK_DPP(v, 0x141); v = o < v ? o : v;
+  o = PK_DPP(v, 0x140); v = o < v ? o : v;
+  return v;
+}
+
+__device__ __forceinline__ uint32_t readlane(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+// Wave-uniform max / min of a u32 (result is a scalar).
+__device__ __forceinline__ uint32_t wave_max_u32_s(uint32_t v) {
+  v = row_max_u32(v);
+  uint32_t a = readlane(v, 0), b = readlane(v, 16), c = readlane(v, 32), d = readlane(v, 48);
+  a = a > b ? a : b;
+  c = c > d ? c : d;
+  return a > c ? a : c;
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32_s(uint32_t v) {
+  v = row_min_u32(v);
+  uint32_t a = readlane(v, 0), b = readlane(v, 16), c = readlane(v, 32), d = readlane(v, 48);
+  a = a < b ? a : b;
+  c = c < d ? c : d;
+  return a < c ? a : c;
+}
+
+}  // namespace pk
+
+namespace pk {
+__device__ __forceinline__ int row_sum_i32(int v) {
+  v += (int)PK_DPP(v, 0xB1);
+  v += (int)PK_DPP(v, 0x4E);
+  v += (int)PK_DPP(v, 0x141);
+  v += (int)PK_DPP(v, 0x140);
+  return v;
+}
+// Wave-uniform sum of an int (scalar result), DPP + readlane (no LDS traffic).
+__device__ __forceinline__ int wave_sum_i32_s(int v) {
+  v = row_sum_i32(v);
+  return (int)(readlane((uint32_t)v, 0) + readlane((uint32_t)v, 16) + readlane((uint32_t)v, 32) +
+               readlane((uint32_t)v, 48));
+}
+}  // namespace pk

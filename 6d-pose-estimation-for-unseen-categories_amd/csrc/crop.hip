@@ -1,0 +1,458 @@
+// H1 / H2 / H4 — crop formation on the device, stream-ordered, no host round trips.
+//
+//  pk_backproject   dataset/object.py:73-88 dpt_2_pcld (+ :52-71 erode_seg_mask, :137
+//                   `seg == 255`): plus-shaped 3x3 erosion (pixels outside the image do
+//                   not erode, cv2's default border), row-major ordered compaction of the
+//                   surviving pixels, back-projection in fp64 exactly as numpy evaluates
+//                     z32 = f32(depth) / f32(cam_scale)
+//                     X = (((u - cx) * f64(z32)) / fx) * 100,  Y likewise,  Z = f64(z32) * 100
+//  pk_sor           dataset/object.py:33-50 -> Open3D RemoveStatisticalOutliers(20, 0.3):
+//                   brute-force kNN-20 (self included) in fp64, per-point mean of the
+//                   sqrt distances summed in ascending order, cloud mean / Bessel std
+//                   accumulated in point order, keep 0 < avg < mean + 0.3 std (ordered).
+//  pk_gather_transform  pcd[idx0] (object.py:148) + transform(pcd, R, t, inv=True)
+//                   (object.py:174, 304-309) -> align_pc f64, plus the f32 copy the model
+//                   consumes (object.py:263 `astype(np.float32)`).
+//  pk_fps_npoint    object.py:145-147 policy: npoint = int(2000/n * n) when n > 2000
+//                   (else n, no FPS), or a fixed npoint (benchmark configs), per crop.
+//  pk_segment_scan / pk_offsets_from_counts  offsets of packed outputs.
+#include "common.hpp"
+
+namespace {
+
+// sqrt rounded to nearest, independent of how the compiler lowers sqrt(double):
+// Tuckerman's test with exact FMA residual signs — s = RN(sqrt(x)) iff
+// s * pred(s) < x <= s * succ(s).
+__device__ __forceinline__ double sqrt_rn(double x) {
+  if (!(x > 0.0) || x == __builtin_huge_val()) return sqrt(x);
+  double s = sqrt(x);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const long long bits = __double_as_longlong(s);  // s > 0 and finite
+    const double dn = __longlong_as_double(bits - 1);
+    const double up = __longlong_as_double(bits + 1);
+    if (fma(s, dn, -x) >= 0.0) {
+      s = dn;
+    } else if (fma(s, up, -x) < 0.0) {
+      s = up;
+    }
+  }
+  return s;
+}
+
+__device__ __forceinline__ bool eroded(const uint8_t* __restrict__ m, int H, int W, int v, int u) {
+  if (m[(int64_t)v * W + u] != 255) return false;
+  if (v > 0 && m[(int64_t)(v - 1) * W + u] != 255) return false;
+  if (v + 1 < H && m[(int64_t)(v + 1) * W + u] != 255) return false;
+  if (u > 0 && m[(int64_t)v * W + u - 1] != 255) return false;
+  if (u + 1 < W && m[(int64_t)v * W + u + 1] != 255) return false;
+  return true;
+}
+
+// grid (H, F), block 256: count eroded pixels per image row.
+__global__ __launch_bounds__(256) void bp_count_kernel(const uint8_t* __restrict__ mask, int H, int W,
+                                                       int32_t* __restrict__ rowcnt) {
+  const int v = blockIdx.x, f = blockIdx.y;
+  const uint8_t* m = mask + (int64_t)f * H * W;
+  int c = 0;
+  for (int u = threadIdx.x; u < W; u += blockDim.x) c += eroded(m, H, W, v, u) ? 1 : 0;
+  c = pk::wave_sum_i32_s(c);
+  __shared__ int ws[4];
+  if (pk::lane_id() == 0) ws[pk::wave_id()] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) rowcnt[(int64_t)f * H + v] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// Generic per-segment exclusive scan of int32 counts -> int64 offsets (+ totals).
+// grid (S), block 1024; segment s covers cnt[s*n .. s*n+n).
+__global__ __launch_bounds__(1024) void seg_scan_kernel(const int32_t* __restrict__ cnt, int n,
+                                                        int64_t* __restrict__ off,
+                                                        int64_t* __restrict__ total) {
+  __shared__ int64_t wsum[16];
+  __shared__ int64_t carry_s;
+  const int s = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) carry_s = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += 1024) {
+    const int i = base + tid;
+    const int64_t v = i < n ? (int64_t)cnt[(int64_t)s * n + i] : 0;
+    const int64_t inc = pk::wave_inclusive_scan_i64(v);
+    if (pk::lane_id() == 63) wsum[pk::wave_id()] = inc;
+    __syncthreads();
+    int64_t pre = carry_s;
+    for (int w = 0; w < pk::wave_id(); ++w) pre += wsum[w];
+    if (i < n) off[(int64_t)s * n + i] = pre + inc - v;
+    __syncthreads();
+    if (tid == 1023) carry_s = pre + inc;
+    __syncthreads();
+  }
+  if (tid == 0 && total) total[s] = carry_s;
+}
+
+// off[0] = 0, off[b+1] = off[b] + counts[b] (one thread; B is a batch size).
+__global__ void offsets_kernel(const int64_t* __restrict__ counts, int B, int64_t* __restrict__ off) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t acc = 0;
+  off[0] = 0;
+  for (int b = 0; b < B; ++b) {
+    acc += counts[b];
+    off[b + 1] = acc;
+  }
+}
+
+// grid (H, F), block 64 (one wave walks the row in 64-pixel chunks, ordered by ballot).
+__global__ __launch_bounds__(64) void bp_write_kernel(
+    const uint16_t* __restrict__ depth, const uint8_t* __restrict__ mask, int H, int W,
+    const double* __restrict__ K, const float* __restrict__ cam_scale,
+    const int64_t* __restrict__ rowoff, const int64_t* __restrict__ frame_off, double* __restrict__ out,
+    int64_t cap) {
+  const int v = blockIdx.x, f = blockIdx.y;
+  const uint8_t* m = mask + (int64_t)f * H * W;
+  const uint16_t* d = depth + (int64_t)f * H * W;
+  const double fx = K[f * 9 + 0], cx = K[f * 9 + 2], fy = K[f * 9 + 4], cy = K[f * 9 + 5];
+  const float cs = cam_scale[f];
+  int64_t o = frame_off[f] + rowoff[(int64_t)f * H + v];
+  const int lane = threadIdx.x;
+  for (int u0 = 0; u0 < W; u0 += 64) {
+    const int u = u0 + lane;
+    const bool keep = u < W && eroded(m, H, W, v, u);
+    const uint64_t bal = __ballot(keep);
+    if (keep) {
+      const int64_t w = o + __popcll(bal & ((1ull << lane) - 1ull));
+      if (w < cap) {
+        const float z32 = (float)d[(int64_t)v * W + u] / cs;  // f32 / f32, correctly rounded
+        const double z = (double)z32;
+        const double X = (((double)u - cx) * z) / fx;
+        const double Y = (((double)v - cy) * z) / fy;
+        out[3 * w + 0] = X * 100.0;
+        out[3 * w + 1] = Y * 100.0;
+        out[3 * w + 2] = z * 100.0;
+      }
+    }
+    o += __popcll(bal);
+  }
+}
+
+// ---------------------------------------------------------------- SOR (H2)
+constexpr int kKnn = 20;
+constexpr int kSorThreads = 256;
+constexpr int kSorTile = 1024;
+
+// grid (ceil(nmax/256), B), block 256: one query point per thread, candidate points
+// staged through LDS in tiles; sorted top-20 in registers (insertion).
+__global__ __launch_bounds__(kSorThreads) void sor_knn_kernel(const double* __restrict__ xyz,
+                                                              const int64_t* __restrict__ off,
+                                                              int knn, double* __restrict__ avg) {
+  __shared__ double tx[kSorTile], ty[kSorTile], tz[kSorTile];
+  const int b = blockIdx.y;
+  const int64_t base = off[b];
+  const int n = (int)(off[b + 1] - base);
+  const int i = blockIdx.x * kSorThreads + threadIdx.x;
+  if (blockIdx.x * kSorThreads >= n) return;
+  const bool act = i < n;
+  const double* p = xyz + base * 3;
+  double qx = 0, qy = 0, qz = 0;
+  if (act) {
+    qx = p[3 * i];
+    qy = p[3 * i + 1];
+    qz = p[3 * i + 2];
+  }
+  double best[kKnn];
+#pragma unroll
+  for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
+  const int kk = knn < n ? knn : n;
+  for (int t0 = 0; t0 < n; t0 += kSorTile) {
+    const int tn = min(kSorTile, n - t0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < tn; j += kSorThreads) {
+      tx[j] = p[3 * (t0 + j)];
+      ty[j] = p[3 * (t0 + j) + 1];
+      tz[j] = p[3 * (t0 + j) + 2];
+    }
+    __syncthreads();
+    if (act) {
+      for (int j = 0; j < tn; ++j) {
+        const double dx = qx - tx[j], dy = qy - ty[j], dz = qz - tz[j];
+        const double s = (dx * dx + dy * dy) + dz * dz;  // nanoflann L2: ((dx²+dy²)+dz²)
+        if (s < best[kKnn - 1]) {
+          double v = s;
+#pragma unroll
+          for (int k = 0; k < kKnn; ++k) {  // bubble v into the sorted list
+            const double lo = fmin(best[k], v), hi = fmax(best[k], v);
+            best[k] = lo;
+            v = hi;
+          }
+        }
+      }
+    }
+  }
+  if (act) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < kKnn; ++k)
+      if (k < kk) acc = acc + sqrt_rn(best[k]);
+    avg[base + i] = kk > 0 ? acc / (double)kk : -1.0;
+  }
+}
+
+// One wave per crop: mean over avg>0, Bessel std, threshold; sequential accumulation in
+// point order like std::accumulate / std::inner_product (lane 0), then ordered keep flags.
+__global__ __launch_bounds__(64) void sor_stats_kernel(const double* __restrict__ avg,
+                                                       const int64_t* __restrict__ off, double std_ratio,
+                                                       double* __restrict__ thr) {
+  const int b = blockIdx.x;
+  const int64_t base = off[b];
+  const int n = (int)(off[b + 1] - base);
+  if (threadIdx.x != 0) return;
+  if (n <= 0) {
+    thr[b] = -1.0;
+    return;
+  }
+  double mean = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double a = avg[base + i];
+    if (a > 0) mean = mean + a;
+  }
+  mean = mean / (double)n;
+  double sq = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double a = avg[base + i];
+    sq = sq + (a > 0 ? (a - mean) * (a - mean) : 0.0);
+  }
+  const double sd = n > 1 ? sqrt_rn(sq / (double)(n - 1)) : __builtin_nan("");
+  thr[b] = mean + std_ratio * sd;
+}
+
+// grid (ceil(nmax/1024), B) block 1024: per-chunk keep counts.
+__global__ __launch_bounds__(1024) void sor_count_kernel(const double* __restrict__ avg,
+                                                         const int64_t* __restrict__ off,
+                                                         const double* __restrict__ thr, int nchunk,
+                                                         int32_t* __restrict__ ccount) {
+  const int b = blockIdx.y;
+  const int64_t base = off[b];
+  const int n = (int)(off[b + 1] - base);
+  const int i = blockIdx.x * 1024 + threadIdx.x;
+  const double t = thr[b];
+  bool keep = false;
+  if (i < n) {
+    const double a = avg[base + i];
+    keep = a > 0 && a < t;
+  }
+  int c = __popcll(__ballot(keep));
+  __shared__ int ws[16];
+  if (pk::lane_id() == 0) ws[pk::wave_id()] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int w = 0; w < 16; ++w) s += ws[w];
+    ccount[(int64_t)b * nchunk + blockIdx.x] = s;
+  }
+}
+
+// Ordered write of kept points: f64 copy (packed by out_off) + f32 copy.
+__global__ __launch_bounds__(1024) void sor_write_kernel(
+    const double* __restrict__ xyz, const double* __restrict__ avg, const int64_t* __restrict__ off,
+    const double* __restrict__ thr, int nchunk, const int64_t* __restrict__ coff,
+    const int64_t* __restrict__ out_off, double* __restrict__ out64, float* __restrict__ out32,
+    int64_t* __restrict__ kept_idx) {
+  const int b = blockIdx.y;
+  const int64_t base = off[b];
+  const int n = (int)(off[b + 1] - base);
+  const int i = blockIdx.x * 1024 + threadIdx.x;
+  const double t = thr[b];
+  bool keep = false;
+  if (i < n) {
+    const double a = avg[base + i];
+    keep = a > 0 && a < t;
+  }
+  const uint64_t bal = __ballot(keep);
+  __shared__ int ws[16];
+  if (pk::lane_id() == 0) ws[pk::wave_id()] = __popcll(bal);
+  __syncthreads();
+  int pre = 0;
+  for (int w = 0; w < pk::wave_id(); ++w) pre += ws[w];
+  if (keep) {
+    const int64_t w = out_off[b] + coff[(int64_t)b * nchunk + blockIdx.x] + pre +
+                      __popcll(bal & ((1ull << pk::lane_id()) - 1ull));
+    const double* q = xyz + (base + i) * 3;
+    if (out64) {
+      out64[3 * w] = q[0];
+      out64[3 * w + 1] = q[1];
+      out64[3 * w + 2] = q[2];
+    }
+    if (out32) {
+      out32[3 * w] = (float)q[0];
+      out32[3 * w + 1] = (float)q[1];
+      out32[3 * w + 2] = (float)q[2];
+    }
+    if (kept_idx) kept_idx[w] = i;  // index local to the input crop
+  }
+}
+
+// npoint policy, start index (hash of seed, crop) and the packed offsets of the result.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ void npoint_kernel(const int64_t* __restrict__ off, int B, int fixed, int limit,
+                              uint64_t seed, int32_t* __restrict__ npoint, int32_t* __restrict__ start,
+                              int64_t* __restrict__ out_off) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t acc = 0;
+  for (int b = 0; b < B; ++b) {
+    const int n = (int)(off[b + 1] - off[b]);
+    int np;
+    if (fixed > 0) {
+      np = fixed;
+    } else if (n > limit) {
+      const double ratio = (double)limit / (double)n;  // object.py:146
+      np = (int)(ratio * (double)n);                   // int(ratio * N) in upstream FPS
+    } else {
+      np = -n;  // no FPS: keep all n points in order (encoded negative)
+    }
+    npoint[b] = np;
+    if (start) start[b] = n > 0 ? (int32_t)(splitmix64(seed ^ splitmix64((uint64_t)b)) % (uint64_t)n) : 0;
+    out_off[b] = acc;
+    acc += np < 0 ? -np : np;
+  }
+  out_off[B] = acc;
+}
+
+// pcd[idx] (f64) -> align = pcd @ R + (-t @ R) with left-to-right 3-term dots, plus f32
+// copy of pcd[idx]. One thread per output point; crop b writes rows out_off[b]..
+__global__ __launch_bounds__(256) void gather_transform_kernel(
+    const double* __restrict__ pcd, const int64_t* __restrict__ off, const int64_t* __restrict__ idx,
+    int idx_stride, const int32_t* __restrict__ npoint, const int64_t* __restrict__ out_off,
+    const double* __restrict__ R, const double* __restrict__ t, double* __restrict__ sel64,
+    double* __restrict__ align64, float* __restrict__ sel32) {
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int np = npoint[b];
+  const int cnt = np < 0 ? -np : np;
+  if (j >= cnt) return;
+  const int64_t src = off[b] + (np < 0 ? j : idx[(int64_t)b * idx_stride + j]);
+  const double x = pcd[3 * src], y = pcd[3 * src + 1], z = pcd[3 * src + 2];
+  const double* Rb = R + 9 * b;  // row-major R_m2c
+  const double* tb = t + 3 * b;
+  const int64_t w = out_off[b] + j;
+  if (sel64) {
+    sel64[3 * w] = x;
+    sel64[3 * w + 1] = y;
+    sel64[3 * w + 2] = z;
+  }
+  if (sel32) {
+    sel32[3 * w] = (float)x;
+    sel32[3 * w + 1] = (float)y;
+    sel32[3 * w + 2] = (float)z;
+  }
+  if (align64) {
+    const double nt0 = -1.0 * tb[0], nt1 = -1.0 * tb[1], nt2 = -1.0 * tb[2];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double tt = (nt0 * Rb[c] + nt1 * Rb[3 + c]) + nt2 * Rb[6 + c];
+      align64[3 * w + c] = ((x * Rb[c] + y * Rb[3 + c]) + z * Rb[6 + c]) + tt;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int pk_backproject(const uint16_t* depth, const uint8_t* mask, int F, int H, int W,
+                              const double* K, const float* cam_scale, int32_t* rowcnt,
+                              int64_t* rowoff, int64_t* count, int64_t* off, double* xyz, int64_t cap,
+                              void* stream) {
+  PK_REQUIRE(F >= 0 && H > 0 && W > 0 && cap >= 0);
+  if (F == 0) return PK_OK;
+  PK_REQUIRE(depth && mask && K && cam_scale && rowcnt && rowoff && count && off && (xyz || cap == 0));
+  hipStream_t s = pk::as_stream(stream);
+  hipLaunchKernelGGL(bp_count_kernel, dim3(H, F), dim3(256), 0, s, mask, H, W, rowcnt);
+  PK_CHECK_LAUNCH();
+  hipLaunchKernelGGL(seg_scan_kernel, dim3(F), dim3(1024), 0, s, rowcnt, H, rowoff, count);
+  PK_CHECK_LAUNCH();
+  hipLaunchKernelGGL(offsets_kernel, dim3(1), dim3(64), 0, s, count, F, off);
+  PK_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bp_write_kernel, dim3(H, F), dim3(64), 0, s, depth, mask, H, W, K, cam_scale,
+                     rowoff, off, xyz, cap);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, int knn,
+                      double std_ratio, double* avg, double* thr, int32_t* ccount, int64_t* coff,
+                      int64_t* kept, int64_t* out_off, double* out64, float* out32,
+                      int64_t* kept_idx, void* stream) {
+  PK_REQUIRE(B >= 0 && nmax >= 0 && knn > 0 && knn <= kKnn);
+  if (B == 0) return PK_OK;
+  PK_REQUIRE(xyz && off && avg && thr && ccount && coff && kept && out_off);
+  hipStream_t s = pk::as_stream(stream);
+  const int nchunk = (nmax + 1023) / 1024;
+  if (nmax > 0) {
+    hipLaunchKernelGGL(sor_knn_kernel, dim3((nmax + kSorThreads - 1) / kSorThreads, B),
+                       dim3(kSorThreads), 0, s, xyz, off, knn, avg);
+    PK_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(sor_stats_kernel, dim3(B), dim3(64), 0, s, avg, off, std_ratio, thr);
+  PK_CHECK_LAUNCH();
+  if (nchunk > 0) {
+    hipLaunchKernelGGL(sor_count_kernel, dim3(nchunk, B), dim3(1024), 0, s, avg, off, thr, nchunk, ccount);
+    PK_CHECK_LAUNCH();
+    hipLaunchKernelGGL(seg_scan_kernel, dim3(B), dim3(1024), 0, s, ccount, nchunk, coff, kept);
+    PK_CHECK_LAUNCH();
+  } else {
+    hipError_t e = hipMemsetAsync(kept, 0, sizeof(int64_t) * B, s);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(offsets_kernel, dim3(1), dim3(64), 0, s, kept, B, out_off);
+  PK_CHECK_LAUNCH();
+  if (nchunk > 0 && (out64 || out32 || kept_idx)) {
+    hipLaunchKernelGGL(sor_write_kernel, dim3(nchunk, B), dim3(1024), 0, s, xyz, avg, off, thr, nchunk,
+                       coff, out_off, out64, out32, kept_idx);
+    PK_CHECK_LAUNCH();
+  }
+  return PK_OK;
+}
+
+extern "C" int pk_offsets_from_counts(const int64_t* counts, int B, int64_t* off, void* stream) {
+  PK_REQUIRE(B >= 0 && counts && off);
+  hipLaunchKernelGGL(offsets_kernel, dim3(1), dim3(64), 0, pk::as_stream(stream), counts, B, off);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_segment_scan(const int32_t* cnt, int S, int n, int64_t* off, int64_t* total,
+                               void* stream) {
+  PK_REQUIRE(S >= 0 && n >= 0);
+  if (S == 0) return PK_OK;
+  PK_REQUIRE(cnt && off);
+  hipLaunchKernelGGL(seg_scan_kernel, dim3(S), dim3(1024), 0, pk::as_stream(stream), cnt, n, off, total);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_fps_npoint(const int64_t* off, int B, int fixed, int limit, uint64_t seed,
+                             int32_t* npoint, int32_t* start, int64_t* out_off, void* stream) {
+  PK_REQUIRE(B >= 0 && limit > 0);
+  if (B == 0) return PK_OK;
+  PK_REQUIRE(off && npoint && out_off);
+  hipLaunchKernelGGL(npoint_kernel, dim3(1), dim3(64), 0, pk::as_stream(stream), off, B, fixed, limit,
+                     seed, npoint, start, out_off);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_gather_transform(const double* pcd, const int64_t* off, int B, const int64_t* idx,
+                                   int idx_stride, const int32_t* npoint, int npmax,
+                                   const int64_t* out_off, const double* R, const double* t,
+                                   double* sel64, double* align64, float* sel32, void* stream) {
+  PK_REQUIRE(B >= 0 && npmax >= 0);
+  if (B == 0 || npmax == 0) return PK_OK;
+  PK_REQUIRE(pcd && off && npoint && out_off && R && t);
+  hipLaunchKernelGGL(gather_transform_kernel, dim3((npmax + 255) / 256, B), dim3(256), 0,
+                     pk::as_stream(stream), pcd, off, idx, idx_stride, npoint, out_off, R, t, sel64,
+                     align64, sel32);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}

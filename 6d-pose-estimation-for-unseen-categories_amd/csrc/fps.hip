@@ -8,38 +8,43 @@
 //   distance[dist < distance] = dist                   (strict <)
 //   farthest = max(distance, -1)[1]                    (first maximal index)
 // The kernel is bit-exact against that recipe: every product and sum is rounded
-// separately (TU compiled with -ffp-contract=off) and the argmax is a max over the
-// 64-bit key (float_bits(distance) << 32 | ~index), so ties go to the lowest index.
+// separately (TU compiled with -ffp-contract=off); the argmax is done in two 32-bit
+// steps (max of the distance bits, then min of the indices holding that max), so ties
+// go to the lowest index exactly like torch.max.
 //
 // Layout: crops are packed back to back, xyz fp32 AoS [total, 3], crop b spans
 // rows [offsets[b], offsets[b+1]). Each thread keeps PPT points (strided by the
-// block size) and their running distances in registers; a structure-of-arrays copy
-// of the crop sits in LDS so the current centroid is a broadcast read. One barrier
-// per iteration (the per-wave maxima are double-buffered in LDS).
+// block size, so a thread's points are in increasing index order) and their running
+// distances in registers; a structure-of-arrays copy of the crop sits in LDS so the
+// current centroid is a broadcast read. Per iteration: branch-free update of the
+// running distances and of the thread's (best, index) pair, DPP row reductions +
+// readlane for the wave result, one LDS slot per wave, ONE barrier (slots are
+// double-buffered), then a 16-lane DPP reduction of the slots that every wave
+// repeats, leaving the next centroid in a scalar register.
 #include "common.hpp"
 
 namespace {
 
-constexpr int kFpsThreads = 1024;
-constexpr int kFpsWaves = kFpsThreads / pk::kWave;
 constexpr int kFpsMaxLds = 13312;  // points whose SoA copy fits in LDS (156 KiB)
 
-template <int PPT, bool LDS>
-__global__ __launch_bounds__(kFpsThreads) void fps_kernel(
+template <int NT, int PPT, bool LDS>
+__global__ __launch_bounds__(NT) void fps_kernel(
     const float* __restrict__ xyz, const int64_t* __restrict__ offsets,
     const int32_t* __restrict__ start, const int32_t* __restrict__ npoint,
     int64_t* __restrict__ out, int out_stride) {
+  constexpr int NW = NT / pk::kWave;
+  static_assert(NW <= 16, "slot reduction assumes <= 16 waves");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
+  const int lane = pk::lane_id();
   const int64_t base = offsets[b];
   const int n = (int)(offsets[b + 1] - base);
   const int np = npoint[b];
   const float* __restrict__ p = xyz + base * 3;
 
-  // slots[2][kFpsWaves] u64 first (16-B aligned), then SoA x/y/z.
-  uint64_t* slots = reinterpret_cast<uint64_t*>(smem);
-  float* sx = reinterpret_cast<float*>(smem + 2 * kFpsWaves * sizeof(uint64_t));
+  uint2* slots = reinterpret_cast<uint2*>(smem);  // [2][16] (bits, index)
+  float* sx = reinterpret_cast<float*>(smem + 2 * 16 * sizeof(uint2));
   const int n_pad = (n + 3) & ~3;
   float* sy = sx + n_pad;
   float* sz = sy + n_pad;
@@ -47,7 +52,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(
   float px[PPT], py[PPT], pz[PPT], pd[PPT];
 #pragma unroll
   for (int k = 0; k < PPT; ++k) {
-    const int idx = tid + k * kFpsThreads;
+    const int idx = tid + k * NT;
     if (idx < n) {
       px[k] = p[3 * idx + 0];
       py[k] = p[3 * idx + 1];
@@ -60,7 +65,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(
       }
     } else {
       px[k] = py[k] = pz[k] = 0.f;
-      pd[k] = -1.f;  // marks an empty slot
+      pd[k] = -1.f;  // empty slot: min(-1, d >= 0) keeps it at -1, never selected
     }
   }
   if (n <= 0 || np <= 0) return;
@@ -80,51 +85,47 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(
       cy = p[3 * far + 1];
       cz = p[3 * far + 2];
     }
-    uint64_t best = 0;
+    float bd = -1.f;
+    int bk = 0;
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
       const float dx = px[k] - cx;
       const float dy = py[k] - cy;
       const float dz = pz[k] - cz;
       const float d = (dx * dx + dy * dy) + dz * dz;  // no contraction (TU flag)
-      if (pd[k] >= 0.f) {
-        pd[k] = d < pd[k] ? d : pd[k];
-        const uint32_t idx = (uint32_t)(tid + k * kFpsThreads);
-        const uint64_t key = ((uint64_t)pk::f32_bits(pd[k]) << 32) | (uint64_t)(~idx);
-        best = key > best ? key : best;
-      }
+      pd[k] = fminf(pd[k], d);                        // == (d < pd ? d : pd): no NaNs
+      const bool gt = pd[k] > bd;                     // strict: lowest k wins ties
+      bd = gt ? pd[k] : bd;
+      bk = gt ? k : bk;
     }
-    best = pk::wave_max_u64(best);
-    uint64_t* s = slots + (i & 1) * kFpsWaves;
-    if (pk::lane_id() == 0) s[pk::wave_id()] = best;
+    const bool valid = bd >= 0.f;
+    const uint32_t bits = valid ? pk::f32_bits(bd) : 0u;
+    const uint32_t gidx = valid ? (uint32_t)(tid + bk * NT) : 0xffffffffu;
+    const uint32_t wmax = pk::wave_max_u32_s(bits);
+    const uint32_t widx = pk::wave_min_u32_s(bits == wmax ? gidx : 0xffffffffu);
+    uint2* s = slots + (i & 1) * 16;
+    if (lane == 0) s[pk::wave_id()] = make_uint2(wmax, widx);
     __syncthreads();
-    const uint4* s4 = reinterpret_cast<const uint4*>(s);
-    uint64_t m = 0;
-#pragma unroll
-    for (int w = 0; w < kFpsWaves / 2; ++w) {
-      const uint4 q = s4[w];
-      const uint64_t a = ((uint64_t)q.y << 32) | q.x;
-      const uint64_t c = ((uint64_t)q.w << 32) | q.z;
-      m = a > m ? a : m;
-      m = c > m ? c : m;
-    }
-    far = (int)(~(uint32_t)(m & 0xffffffffu));
+    uint2 v = make_uint2(0u, 0xffffffffu);
+    if (lane < NW) v = s[lane];
+    const uint32_t m = pk::readlane(pk::row_max_u32(v.x), 0);
+    far = (int)pk::readlane(pk::row_min_u32(v.x == m ? v.y : 0xffffffffu), 0);
   }
 }
 
-template <int PPT>
+template <int NT, int PPT>
 int launch_fps(const float* xyz, const int64_t* offsets, const int32_t* start,
                const int32_t* npoint, int64_t* out, int out_stride, int B, int nmax,
                hipStream_t s) {
+  const size_t slots = 2 * 16 * sizeof(uint2);
   if (nmax <= kFpsMaxLds) {
     const int n_pad = (nmax + 3) & ~3;
-    const size_t lds = 2 * kFpsWaves * sizeof(uint64_t) + 3 * (size_t)n_pad * sizeof(float);
-    hipLaunchKernelGGL((fps_kernel<PPT, true>), dim3(B), dim3(kFpsThreads), lds, s, xyz,
-                       offsets, start, npoint, out, out_stride);
+    const size_t lds = slots + 3 * (size_t)n_pad * sizeof(float);
+    hipLaunchKernelGGL((fps_kernel<NT, PPT, true>), dim3(B), dim3(NT), lds, s, xyz, offsets,
+                       start, npoint, out, out_stride);
   } else {
-    const size_t lds = 2 * kFpsWaves * sizeof(uint64_t);
-    hipLaunchKernelGGL((fps_kernel<PPT, false>), dim3(B), dim3(kFpsThreads), lds, s, xyz,
-                       offsets, start, npoint, out, out_stride);
+    hipLaunchKernelGGL((fps_kernel<NT, PPT, false>), dim3(B), dim3(NT), slots, s, xyz, offsets,
+                       start, npoint, out, out_stride);
   }
   PK_CHECK_LAUNCH();
   return PK_OK;
@@ -139,12 +140,31 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
   if (B == 0) return PK_OK;
   PK_REQUIRE(xyz && offsets && start && npoint && out);
   hipStream_t s = pk::as_stream(stream);
-  const int ppt = (nmax + kFpsThreads - 1) / kFpsThreads;
-  if (ppt <= 1) return launch_fps<1>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
-  if (ppt <= 2) return launch_fps<2>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
-  if (ppt <= 4) return launch_fps<4>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
-  if (ppt <= 8) return launch_fps<8>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
-  if (ppt <= 13) return launch_fps<13>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
-  if (ppt <= 32) return launch_fps<32>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
+#define PK_FPS(NT, PPT) return launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s)
+  if (nmax <= 512) PK_FPS(512, 1);
+  if (nmax <= 1024) PK_FPS(512, 2);
+  if (nmax <= 2048) PK_FPS(512, 4);
+  if (nmax <= 4096) PK_FPS(1024, 4);
+  if (nmax <= 8192) PK_FPS(1024, 8);
+  if (nmax <= 13312) PK_FPS(1024, 13);
+  if (nmax <= 32768) PK_FPS(1024, 32);
+#undef PK_FPS
   return PK_ERR_ARG;  // > 32768 points per crop
+}
+
+// Development hook (not part of include/posekern.h): force the block size / points
+// per thread, for tools/kbench.py's configuration sweeps.
+extern "C" int pkdev_fps_cfg(const float* xyz, const int64_t* offsets, int B, int nmax,
+                             const int32_t* start, const int32_t* npoint, int64_t* out,
+                             int out_stride, int nt, void* stream) {
+  hipStream_t s = pk::as_stream(stream);
+  const int ppt = (nmax + nt - 1) / nt;
+#define PK_FPS(NT, PPT)                                                                   \
+  if (nt == NT && ppt <= PPT)                                                             \
+    return launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
+  PK_FPS(256, 4) PK_FPS(256, 8) PK_FPS(256, 16) PK_FPS(256, 32)
+  PK_FPS(512, 2) PK_FPS(512, 4) PK_FPS(512, 8) PK_FPS(512, 16)
+  PK_FPS(1024, 2) PK_FPS(1024, 4) PK_FPS(1024, 8)
+#undef PK_FPS
+  return PK_ERR_ARG;
 }

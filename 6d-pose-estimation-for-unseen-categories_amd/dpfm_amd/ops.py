@@ -101,3 +101,74 @@ def packed_offsets(sizes: Sequence[int], device) -> torch.Tensor:
     off = np.zeros(len(sizes) + 1, dtype=np.int64)
     off[1:] = np.cumsum(np.asarray(sizes, dtype=np.int64))
     return torch.from_numpy(off).to(device)
+
+
+# ------------------------------------------------------------------------------ H1 / H2 / H4 crops
+
+
+def backproject(depth: torch.Tensor, mask: torch.Tensor, K: torch.Tensor, cam_scale: torch.Tensor,
+                cap: int) -> dict:
+    """dpt_2_pcld for F frames (pk_backproject). depth uint16 [F,H,W] (int16 storage),
+    mask uint8 [F,H,W], K f64 [F,9], cam_scale f32 [F]. Returns packed xyz f64 [cap,3],
+    count int64 [F], off int64 [F+1] (count > cap overflows; see check_capacity)."""
+    F, H, W = depth.shape
+    dev = depth.device
+    rowcnt = torch.empty((F, H), dtype=torch.int32, device=dev)
+    rowoff = torch.empty((F, H), dtype=torch.int64, device=dev)
+    count = torch.empty((F,), dtype=torch.int64, device=dev)
+    off = torch.empty((F + 1,), dtype=torch.int64, device=dev)
+    xyz = torch.empty((cap, 3), dtype=torch.float64, device=dev)
+    call("pk_backproject", ptr(depth), ptr(mask), F, H, W, ptr(K), ptr(cam_scale), ptr(rowcnt), ptr(rowoff),
+         ptr(count), ptr(off), ptr(xyz), int(cap), _lib.stream(dev))
+    return dict(xyz=xyz, count=count, off=off)
+
+
+def sor(xyz: torch.Tensor, off: torch.Tensor, nmax: int, knn: int = 20, std_ratio: float = 0.3,
+        want64: bool = True, want32: bool = True, want_idx: bool = False) -> dict:
+    """remove_outliers for B packed crops (pk_sor). Survivors are packed by out_off."""
+    B = off.numel() - 1
+    dev = xyz.device
+    T = xyz.shape[0]
+    nchunk = max(1, (nmax + 1023) // 1024)
+    avg = torch.empty((T,), dtype=torch.float64, device=dev)
+    thr = torch.empty((B,), dtype=torch.float64, device=dev)
+    ccount = torch.empty((B, nchunk), dtype=torch.int32, device=dev)
+    coff = torch.empty((B, nchunk), dtype=torch.int64, device=dev)
+    kept = torch.empty((B,), dtype=torch.int64, device=dev)
+    out_off = torch.empty((B + 1,), dtype=torch.int64, device=dev)
+    out64 = torch.empty((T, 3), dtype=torch.float64, device=dev) if want64 else None
+    out32 = torch.empty((T, 3), dtype=torch.float32, device=dev) if want32 else None
+    kidx = torch.empty((T,), dtype=torch.int64, device=dev) if want_idx else None
+    call("pk_sor", ptr(xyz), ptr(off), B, int(nmax), int(knn), float(std_ratio), ptr(avg), ptr(thr), ptr(ccount),
+         ptr(coff), ptr(kept), ptr(out_off), ptr(out64), ptr(out32), ptr(kidx), _lib.stream(dev))
+    return dict(avg=avg, thr=thr, kept=kept, off=out_off, xyz64=out64, xyz32=out32, kept_idx=kidx)
+
+
+def fps_npoint(off: torch.Tensor, fixed: int = 0, limit: int = 2000, seed: int = 0) -> dict:
+    B = off.numel() - 1
+    dev = off.device
+    npoint = torch.empty((B,), dtype=torch.int32, device=dev)
+    start = torch.empty((B,), dtype=torch.int32, device=dev)
+    out_off = torch.empty((B + 1,), dtype=torch.int64, device=dev)
+    call("pk_fps_npoint", ptr(off), B, int(fixed), int(limit), ctypes_u64(seed), ptr(npoint), ptr(start),
+         ptr(out_off), _lib.stream(dev))
+    return dict(npoint=npoint, start=start, off=out_off)
+
+
+def ctypes_u64(v: int):
+    import ctypes
+    return ctypes.c_uint64(int(v) & 0xFFFFFFFFFFFFFFFF)
+
+
+def gather_transform(pcd: torch.Tensor, off: torch.Tensor, idx: Optional[torch.Tensor], npoint: torch.Tensor,
+                     npmax: int, out_off: torch.Tensor, R: torch.Tensor, t: torch.Tensor, total_cap: int,
+                     want_sel64: bool = True, want_align: bool = True, want_sel32: bool = True) -> dict:
+    B = off.numel() - 1
+    dev = pcd.device
+    sel64 = torch.empty((total_cap, 3), dtype=torch.float64, device=dev) if want_sel64 else None
+    align = torch.empty((total_cap, 3), dtype=torch.float64, device=dev) if want_align else None
+    sel32 = torch.empty((total_cap, 3), dtype=torch.float32, device=dev) if want_sel32 else None
+    idx_stride = idx.shape[1] if idx is not None else 0
+    call("pk_gather_transform", ptr(pcd), ptr(off), B, ptr(idx), int(idx_stride), ptr(npoint), int(npmax),
+         ptr(out_off), ptr(R), ptr(t), ptr(sel64), ptr(align), ptr(sel32), _lib.stream(dev))
+    return dict(sel64=sel64, align=align, sel32=sel32)

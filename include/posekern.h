@@ -58,6 +58,51 @@ int pk_ball_query_pairs(const double* cad, const int64_t* cad_off, const double*
                         int64_t* pairs, int64_t cap, int64_t* count, int8_t* ov12, int8_t* ov21,
                         void* stream);
 
+/* H1 crop formation. Replaces dataset/object.py:73-88 dpt_2_pcld (with the plus-shaped
+ * erode_seg_mask of :52-71 and `seg == 255` of :137) for F frames at once.
+ *   depth uint16 [F,H,W], mask uint8 [F,H,W] (mask_visib png values; 255 = object)
+ *   K f64 [F,9] row-major intrinsics, cam_scale f32 [F] = 1000 / depth_scale
+ *   rowcnt int32 [F,H], rowoff int64 [F,H] scratch
+ *   count int64 [F] points per frame, off int64 [F+1] packed offsets
+ *   xyz f64 [cap,3] packed back-projected points in cm, row-major pixel order.
+ * Bit-exact vs numpy: z32 = f32(depth)/f32(cam_scale); X = (((u-cx)*z)/fx)*100. */
+int pk_backproject(const uint16_t* depth, const uint8_t* mask, int F, int H, int W,
+                   const double* K, const float* cam_scale, int32_t* rowcnt, int64_t* rowoff,
+                   int64_t* count, int64_t* off, double* xyz, int64_t cap, void* stream);
+
+/* H2 statistical outlier removal. Replaces dataset/object.py:33-50 remove_outliers
+ * (Open3D RemoveStatisticalOutliers(nb_neighbors=20, std_ratio=0.3)).
+ *   xyz f64 [T,3] packed / off, knn <= 20
+ *   avg f64 [T] mean kNN distance, thr f64 [B] keep threshold
+ *   ccount int32 [B, ceil(nmax/1024)], coff int64 (same shape) scratch
+ *   kept int64 [B] survivors, out_off int64 [B+1] their packed offsets
+ *   out64 f64 [T,3], out32 f32 [T,3] (either may be NULL) survivors in input order
+ *   kept_idx int64 [T] (may be NULL) survivor index within its input crop */
+int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, int knn, double std_ratio,
+           double* avg, double* thr, int32_t* ccount, int64_t* coff, int64_t* kept,
+           int64_t* out_off, double* out64, float* out32, int64_t* kept_idx, void* stream);
+
+/* FPS sample-count policy of dataset/object.py:145-147 on device counts (no host sync):
+ * fixed > 0: npoint = fixed; else npoint = int(limit/n * n) if n > limit, else -n
+ * (negative = keep all n points, no FPS). start[b] = splitmix64(seed ^ splitmix64(b))
+ * % n (replaces upstream torch.randint; may be NULL). out_off int64 [B+1]. */
+int pk_fps_npoint(const int64_t* off, int B, int fixed, int limit, uint64_t seed,
+                  int32_t* npoint, int32_t* start, int64_t* out_off, void* stream);
+
+/* H4 pcd[idx0] (dataset/object.py:148) + transform(pcd, R, t, inv=True) (:174, :304-309).
+ *   pcd f64 [T,3] packed / off; idx int64 [B, idx_stride] FPS output (unused when
+ *   npoint[b] < 0); R f64 [B,9] row-major R_m2c, t f64 [B,3] (cm)
+ *   sel64 f64 / align64 f64 / sel32 f32 [sum npoint, 3] packed by out_off (any NULL) */
+int pk_gather_transform(const double* pcd, const int64_t* off, int B, const int64_t* idx,
+                        int idx_stride, const int32_t* npoint, int npmax, const int64_t* out_off,
+                        const double* R, const double* t, double* sel64, double* align64,
+                        float* sel32, void* stream);
+
+/* Packed-layout helpers: per-segment exclusive scan of int32 counts (S segments of n),
+ * and off[b+1] = off[b] + counts[b]. */
+int pk_segment_scan(const int32_t* cnt, int S, int n, int64_t* off, int64_t* total, void* stream);
+int pk_offsets_from_counts(const int64_t* counts, int B, int64_t* off, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

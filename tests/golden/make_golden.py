@@ -1,0 +1,116 @@
+"""Mint tests/golden fixtures from data files the reference itself holds.
+
+Run in the development container (needs /root/reference, read-only):
+    python tests/golden/make_golden.py
+Nothing here imports or runs reference code; it reads PNG / JSON / PLY / TXT data:
+
+  lm_frame.npz   sample-data/lm/train_pbr/000000: depth png, every mask_visib png,
+                 cam_K + depth_scale of scene_camera.json (H1/H2/H3 real-data inputs)
+  pose_metrics.npz  H14 golden vectors: for N published crops of
+                 results_on_{pbr,real}/results_poses_RANSAC, the CAD vertices
+                 (ply/…/cad_i.ply), T_gt and T_pred_ICP recovered at full precision from
+                 cad_i_pose_gt.ply / cad_i_pose_est.ply (the reference wrote those plys as
+                 CAD transformed by the full-precision poses), T_pred as printed, and the
+                 reference's printed metrics (ADD ICP, Add Score ICP thres (xyz direction),
+                 Add-S Score ICP, Error [cm], Error [deg], diameter from models_info.json)
+  p_pred.npy     sample-data/sample_P_pred/p_i0.npy (RANSAC correspondence shape/order)
+"""
+import glob
+import json
+import os
+import re
+
+import numpy as np
+from PIL import Image
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def read_ply_xyz(path):
+    with open(path, "rb") as f:
+        header = b""
+        while not header.endswith(b"end_header\n"):
+            header += f.readline()
+        h = header.decode()
+        n = int(re.search(r"element vertex (\d+)", h).group(1))
+        props = re.findall(r"property (\w+) (\w+)", h.split("element vertex")[1].split("element")[0])
+        assert "binary_little_endian" in h
+        dt = {"double": "<f8", "float": "<f4"}
+        dtype = np.dtype([(name, dt[t]) for t, name in props])
+        data = np.frombuffer(f.read(n * dtype.itemsize), dtype=dtype, count=n)
+    return np.stack([data["x"], data["y"], data["z"]], 1).astype(np.float64)
+
+
+def parse_result_txt(path):
+    txt = open(path).read()
+
+    def num(label):
+        m = re.search(re.escape(label) + r":\s*([-+0-9.eEnaif]+)", txt)
+        return float(m.group(1))
+
+    def mat(label):
+        m = re.search(re.escape(label) + r".*?\n(\[\[.*?\]\])", txt, re.S)
+        return np.array([[float(x) for x in row.replace("[", "").replace("]", "").split()]
+                         for row in m.group(1).strip().split("\n")])
+
+    return dict(obj_id=int(num("Object ID")), add=num("Avg. Euclidean Distance (ADD) [cm]"),
+                add_icp=num("Avg. Euclidean Distance (ADD) ICP"),
+                add_xyz_icp=num("Add Score ICP thres (xyz direction)"),
+                adds_icp=num("Add-S Score ICP"), err_cm=num("Error [cm]"), err_deg=num("Error [deg]"),
+                T_gt=mat("T_gt (Ground Truth Transformation):"),
+                T_pred=mat("T_pred (Predicted Transformation):"),
+                T_icp=mat("T_pred_ICP (Predicted Transformation from ICP):"))
+
+
+def fit_rigid(src, dst):
+    """Least-squares [R|t] with dst = src @ R.T + t (exact data -> exact up to rounding)."""
+    A = np.concatenate([src, np.ones((src.shape[0], 1))], 1)
+    X, *_ = np.linalg.lstsq(A, dst, rcond=None)
+    T = np.eye(4)
+    T[:3, :3] = X[:3].T
+    T[:3, 3] = X[3]
+    return T
+
+
+def main():
+    base = f"{REF}/sample-data/lm/train_pbr/000000"
+    depth = np.asarray(Image.open(f"{base}/depth/000000.png"))
+    masks = np.stack([np.asarray(Image.open(p)) for p in sorted(glob.glob(f"{base}/mask_visib/000000_*.png"))])
+    cam = json.load(open(f"{base}/scene_camera.json"))["0"]
+    np.savez_compressed(f"{OUT}/lm_frame.npz", depth=depth, masks=masks,
+                        K=np.array(cam["cam_K"], dtype=np.float64).reshape(3, 3),
+                        depth_scale=np.float64(cam["depth_scale"]))
+
+    info = json.load(open(f"{REF}/sample-data/lm/models/models_info.json"))
+    rows = []
+    for tree in ("results_on_pbr", "results_on_real"):
+        files = sorted(glob.glob(f"{REF}/{tree}/results_poses_RANSAC/results/*.txt"))
+        for path in files[:4]:
+            name = os.path.basename(path)[:-4]
+            i = name.split("_")[-1]
+            d = f"{REF}/{tree}/results_poses_RANSAC/ply/{name}"
+            if not os.path.exists(f"{d}/cad_{i}.ply"):
+                continue
+            r = parse_result_txt(path)
+            cad = read_ply_xyz(f"{d}/cad_{i}.ply")
+            T_gt = fit_rigid(cad, read_ply_xyz(f"{d}/cad_{i}_pose_gt.ply"))
+            T_icp = fit_rigid(cad, read_ply_xyz(f"{d}/cad_{i}_pose_est.ply"))
+            assert np.allclose(T_gt, r["T_gt"], atol=1e-6), name
+            assert np.allclose(T_icp, r["T_icp"], atol=1e-6), name
+            r.update(cad=cad, T_gt_full=T_gt, T_icp_full=T_icp,
+                     diam=info[str(r["obj_id"])]["diameter"] * 0.1, tree=tree, name=name)
+            rows.append(r)
+    out = {}
+    for k, r in enumerate(rows):
+        for key in ("cad", "T_gt_full", "T_icp_full", "T_pred", "add", "add_icp", "add_xyz_icp", "adds_icp",
+                    "err_cm", "err_deg", "diam", "obj_id"):
+            out[f"{k}_{key}"] = np.asarray(r[key])
+    out["n"] = np.int64(len(rows))
+    np.savez_compressed(f"{OUT}/pose_metrics.npz", **out)
+    np.save(f"{OUT}/p_pred.npy", np.load(f"{REF}/sample-data/sample_P_pred/p_i0.npy"))
+    print(f"wrote lm_frame.npz, pose_metrics.npz ({len(rows)} crops), p_pred.npy")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,117 @@
+"""GPU parity: crop formation (H1 back-projection + erosion, H2 SOR, FPS policy, H4
+gather + transform) vs the oracle, on the reference's LM sample frame and on
+synthetic frames. Bit-exact except where noted."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dpfm_oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _frames():
+    from dpfm_amd.dataset.synthetic import make_frame
+    g = np.load(os.path.join(GOLD, "lm_frame.npz"))
+    depth, masks, K, ds = g["depth"], g["masks"], g["K"], float(g["depth_scale"])
+    frames = []
+    for j in (0, 2, 4, 7, 11, 1, 14):  # includes an empty mask (1) and a tiny one (14)
+        frames.append((depth, masks[j], K, ds))
+    for s in range(3):
+        f = make_frame(s)
+        frames.append((f.depth, f.mask, f.K, f.depth_scale))
+    return frames
+
+
+def test_backproject_bitexact(device):
+    from dpfm_amd import ops
+    fr = _frames()
+    depth = torch.from_numpy(np.stack([f[0].astype(np.int16) for f in fr])).to(device)
+    mask = torch.from_numpy(np.stack([f[1] for f in fr])).to(device)
+    K = torch.from_numpy(np.stack([f[2].reshape(9) for f in fr])).to(device)
+    cs = torch.tensor([1000.0 / f[3] for f in fr], dtype=torch.float32, device=device)
+    out = ops.backproject(depth, mask, K, cs, cap=200000)
+    off = out["off"].cpu().numpy()
+    xyz = out["xyz"].cpu().numpy()
+    for b, (d, m, k, ds) in enumerate(fr):
+        exp = O.dpt_2_pcld(d, 1000 / ds, k, m == 255)
+        got = xyz[off[b]:off[b + 1]]
+        assert got.shape == exp.shape, b
+        np.testing.assert_array_equal(got, exp, err_msg=f"frame {b}")
+
+
+def _packed(arrs, device, dtype=torch.float64):
+    from dpfm_amd import ops
+    return (torch.from_numpy(np.concatenate(arrs, 0)).to(device=device, dtype=dtype),
+            ops.packed_offsets([a.shape[0] for a in arrs], device))
+
+
+def test_sor_matches_oracle(device):
+    from dpfm_amd import ops
+    clouds = [O.dpt_2_pcld(d, 1000 / ds, k, m == 255) for d, m, k, ds in _frames()]
+    clouds = [c for c in clouds if c.shape[0] > 0]
+    clouds.append(np.repeat(clouds[0][:30], 2, axis=0))  # duplicates: zero distances
+    x, off = _packed(clouds, device)
+    res = ops.sor(x, off, max(c.shape[0] for c in clouds), want_idx=True)
+    avg = res["avg"].cpu().numpy()
+    o = off.cpu().numpy()
+    oo = res["off"].cpu().numpy()
+    kidx = res["kept_idx"].cpu().numpy()
+    x64 = res["xyz64"].cpu().numpy()
+    x32 = res["xyz32"].cpu().numpy()
+    for b, c in enumerate(clouds):
+        exp_avg = O.sor_avg_distances(c)
+        np.testing.assert_array_equal(avg[o[b]:o[b + 1]], exp_avg, err_msg=f"avg crop {b}")
+        keep = O.remove_outliers_indices(c)
+        np.testing.assert_array_equal(kidx[oo[b]:oo[b + 1]], keep, err_msg=f"keep crop {b}")
+        np.testing.assert_array_equal(x64[oo[b]:oo[b + 1]], c[keep])
+        np.testing.assert_array_equal(x32[oo[b]:oo[b + 1]], c[keep].astype(np.float32))
+
+
+@pytest.mark.parametrize("fixed", [0, 1024])
+def test_npoint_fps_gather_transform(device, coracle, fixed):
+    from dpfm_amd import ops
+    from dpfm_amd.dataset.synthetic import make_frame, random_rotation
+    from _util import c_fps
+    rng = np.random.default_rng(4)
+    clouds = []
+    for s in range(4):
+        f = make_frame(s)
+        c = O.dpt_2_pcld(f.depth, 1000 / f.depth_scale, f.K, f.mask == 255)
+        clouds.append(c)
+    clouds.append(clouds[0][:1500])  # n <= 2000: no FPS in reference mode
+    x, off = _packed(clouds, device)
+    pol = ops.fps_npoint(off, fixed=fixed, limit=2000, seed=7)
+    npoint = pol["npoint"].cpu().numpy()
+    start = pol["start"].cpu().numpy()
+    for b, c in enumerate(clouds):
+        n = c.shape[0]
+        if fixed:
+            assert npoint[b] == fixed
+        elif n > 2000:
+            assert npoint[b] == O.fps_npoint(n)
+        else:
+            assert npoint[b] == -n
+    x32 = x.to(torch.float32)
+    npmax = int(np.abs(npoint).max())
+    idx = ops.fps_packed(x32, off, max(c.shape[0] for c in clouds), pol["start"], pol["npoint"], npmax)
+    R = np.stack([random_rotation(rng) for _ in clouds])
+    t = rng.normal(size=(len(clouds), 3)) * 40
+    total = int(np.abs(npoint).sum())
+    g = ops.gather_transform(x, off, idx, pol["npoint"], npmax, pol["off"],
+                             torch.from_numpy(R.reshape(-1, 9)).to(device), torch.from_numpy(t).to(device), total)
+    oo = pol["off"].cpu().numpy()
+    idx = idx.cpu().numpy()
+    for b, c in enumerate(clouds):
+        if npoint[b] > 0:
+            exp_idx = c_fps(coracle, c.astype(np.float32), start[b], npoint[b])
+            np.testing.assert_array_equal(idx[b, :npoint[b]], exp_idx)
+            sel = c[exp_idx]
+        else:
+            sel = c
+        np.testing.assert_array_equal(g["sel64"].cpu().numpy()[oo[b]:oo[b + 1]], sel)
+        np.testing.assert_array_equal(g["sel32"].cpu().numpy()[oo[b]:oo[b + 1]], sel.astype(np.float32))
+        np.testing.assert_array_equal(g["align"].cpu().numpy()[oo[b]:oo[b + 1]], O.transform(sel, R[b], t[b], inv=True))

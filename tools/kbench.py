@@ -1,0 +1,67 @@
+"""Quick per-kernel timing (development aid): FPS and ball query at C2/C4 sizes."""
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "6d-pose-estimation-for-unseen-categories_amd")]
+import numpy as np
+import torch
+from dpfm_amd import ops
+
+dev = torch.device("cuda:0")
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+rng = np.random.default_rng(0)
+for B, nin, npt in [(32, 2000, 1024), (32, 4000, 1024), (32, 8000, 1024), (256, 8000, 2048)]:
+    x = torch.from_numpy((rng.normal(size=(B * nin, 3)) * 6 + 100).astype(np.float32)).to(dev)
+    off = ops.packed_offsets([nin] * B, dev)
+    st = torch.zeros(B, dtype=torch.int32, device=dev)
+    npv = torch.full((B,), npt, dtype=torch.int32, device=dev)
+    ms = timeit(lambda: ops.fps_packed(x, off, nin, st, npv, npt), iters=5, warm=1)
+    print(f"fps B={B} n_in={nin} npoint={npt}: {ms:.3f} ms  ({ms*1e3/npt:.3f} us/iter)")
+    import ctypes
+    from dpfm_amd import _lib
+    L = _lib.lib()
+    out = torch.zeros((B, npt), dtype=torch.int64, device=dev)
+    ref = ops.fps_packed(x, off, nin, st, npv, npt)
+    for nt in (256, 512, 1024):
+        f = lambda: L.pkdev_fps_cfg(_lib.ptr(x), _lib.ptr(off), B, nin, _lib.ptr(st), _lib.ptr(npv), _lib.ptr(out), npt, nt, _lib.stream(dev))
+        if f() != 0:
+            continue
+        ms = timeit(f, iters=5, warm=1)
+        print(f"   nt={nt}: {ms:.3f} ms ({ms*1e3/npt:.3f} us/iter) same={torch.equal(out, ref)}")
+
+for B, N in [(32, 1024), (256, 2048)]:
+    cad = torch.from_numpy(rng.normal(size=(B * N, 3)) * 5).to(dev)
+    pc = torch.from_numpy(rng.normal(size=(B * N, 3)) * 5).to(dev)
+    off = ops.packed_offsets([N] * B, dev)
+    thr = torch.full((B,), ops.ball_threshold(0.6), dtype=torch.float64, device=dev)
+    ld = N
+    mask = torch.empty((B, N, ld), dtype=torch.uint8, device=dev)
+    rc = torch.empty((B, N), dtype=torch.int32, device=dev)
+    from dpfm_amd._lib import call, ptr, stream
+    s = stream(dev)
+    f = lambda: call("pk_ball_query_mask", ptr(cad), ptr(off), ptr(pc), ptr(off), ptr(thr), B, N, N, ptr(mask), ld, ptr(rc), s)
+    ms = timeit(f)
+    byts = B * (24 * N + 24 * N + N * N)
+    print(f"ball_query_mask (f32 screen) B={B} N={N}: {ms:.3f} ms, {byts/ms/1e6:.1f} GB/s algorithmic")
+    m1 = mask.clone(); r1 = rc.clone()
+    from dpfm_amd import _lib
+    f64 = lambda: _lib.lib().pkdev_ball_query_mask64(ptr(cad), ptr(off), ptr(pc), ptr(off), ptr(thr), B, N, N, ptr(mask), ld, ptr(rc), s)
+    ms = timeit(f64)
+    print(f"ball_query_mask (all fp64) B={B} N={N}: {ms:.3f} ms, {byts/ms/1e6:.1f} GB/s algorithmic; same={torch.equal(m1, mask) and torch.equal(r1, rc)}")
+    f2 = lambda: ops.ball_query(cad, off, pc, off, [0.6] * B, N, N, 64 * N, thr2=thr)
+    ms = timeit(f2)
+    print(f"ball_query full (mask+scan+pairs) B={B} N={N}: {ms:.3f} ms")
+    f3 = lambda: ops.ball_query(cad, off, pc, off, [0.6] * B, N, N, 64 * N, with_mask=False, thr2=thr)
+    ms = timeit(f3)
+    print(f"ball_query fused (count+scan+pairs, no mask) B={B} N={N}: {ms:.3f} ms")
