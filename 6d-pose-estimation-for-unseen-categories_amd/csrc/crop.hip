@@ -105,7 +105,7 @@ __global__ __launch_bounds__(64) void bp_write_kernel(
     const uint16_t* __restrict__ depth, const uint8_t* __restrict__ mask, int H, int W,
     const double* __restrict__ K, const float* __restrict__ cam_scale,
     const int64_t* __restrict__ rowoff, const int64_t* __restrict__ frame_off, double* __restrict__ out,
-    int64_t cap) {
+    int64_t cap, int32_t* __restrict__ pix, int32_t* __restrict__ idxmap) {
   const int v = blockIdx.x, f = blockIdx.y;
   const uint8_t* m = mask + (int64_t)f * H * W;
   const uint16_t* d = depth + (int64_t)f * H * W;
@@ -117,8 +117,12 @@ __global__ __launch_bounds__(64) void bp_write_kernel(
     const int u = u0 + lane;
     const bool keep = u < W && eroded(m, H, W, v, u);
     const uint64_t bal = __ballot(keep);
+    if (idxmap != nullptr && u < W)
+      idxmap[(int64_t)f * H * W + (int64_t)v * W + u] =
+          keep ? (int32_t)(o - frame_off[f] + __popcll(bal & ((1ull << lane) - 1ull))) : -1;
     if (keep) {
       const int64_t w = o + __popcll(bal & ((1ull << lane) - 1ull));
+      if (pix != nullptr && w < cap) pix[w] = v * W + u;
       if (w < cap) {
         const float z32 = (float)d[(int64_t)v * W + u] / cs;  // f32 / f32, correctly rounded
         const double z = (double)z32;
@@ -136,14 +140,39 @@ __global__ __launch_bounds__(64) void bp_write_kernel(
 // ---------------------------------------------------------------- SOR (H2)
 constexpr int kKnn = 20;
 constexpr int kSorThreads = 256;
-constexpr int kSorTile = 1024;
+constexpr int kSorTile = 4096;
 
-// grid (ceil(nmax/256), B), block 256: one query point per thread, candidate points
-// staged through LDS in tiles; sorted top-20 in registers (insertion).
+__device__ __forceinline__ void topk_insert(double (&best)[kKnn], double v) {
+#pragma unroll
+  for (int k = 0; k < kKnn; ++k) {  // bubble v into the sorted list
+    const double lo = fmin(best[k], v), hi = fmax(best[k], v);
+    best[k] = lo;
+    v = hi;
+  }
+}
+
+__device__ __forceinline__ double sqdist(double ax, double ay, double az, const double* b) {
+  const double dx = ax - b[0], dy = ay - b[1], dz = az - b[2];
+  return (dx * dx + dy * dy) + dz * dz;  // nanoflann L2: ((dx²+dy²)+dz²)
+}
+
+// grid (ceil(nmax/256), B), block 256: one query point per thread.
+//  pass 1 (pixel window, when pix/idxmap are given): exact distances to the points of the
+//         5x5 pixel neighbourhood; if >= knn of them exist, T = their knn-th smallest
+//         squared distance bounds the true knn-th neighbour distance (>= knn points lie
+//         within T). Otherwise T = +inf.
+//  pass 2: every point of the crop (LDS tiles of fp32 coordinates centred on the crop's
+//         first point) is screened with an fp32 distance against T + margin, where
+//         margin = 2^-19 (T + (|a| + |b|)^2) bounds the fp32 error;
+//         survivors are re-evaluated exactly in fp64 and inserted if <= T.
+// The kept set is a superset of the true knn nearest (ties included), so the sorted
+// top-knn values are exactly those of a full brute-force search.
 __global__ __launch_bounds__(kSorThreads) void sor_knn_kernel(const double* __restrict__ xyz,
-                                                              const int64_t* __restrict__ off,
-                                                              int knn, double* __restrict__ avg) {
-  __shared__ double tx[kSorTile], ty[kSorTile], tz[kSorTile];
+                                                              const int64_t* __restrict__ off, int knn,
+                                                              const int32_t* __restrict__ pix,
+                                                              const int32_t* __restrict__ idxmap, int H, int W,
+                                                              double* __restrict__ avg) {
+  __shared__ float4 tile[kSorTile];
   const int b = blockIdx.y;
   const int64_t base = off[b];
   const int n = (int)(off[b + 1] - base);
@@ -151,37 +180,65 @@ __global__ __launch_bounds__(kSorThreads) void sor_knn_kernel(const double* __re
   if (blockIdx.x * kSorThreads >= n) return;
   const bool act = i < n;
   const double* p = xyz + base * 3;
-  double qx = 0, qy = 0, qz = 0;
+  const double ox = p[0], oy = p[1], oz = p[2];
+  double q0 = 0.0, q1 = 0.0, q2 = 0.0;
   if (act) {
-    qx = p[3 * i];
-    qy = p[3 * i + 1];
-    qz = p[3 * i + 2];
+    q0 = p[3 * i];
+    q1 = p[3 * i + 1];
+    q2 = p[3 * i + 2];
   }
+  const int kk = knn < n ? knn : n;
   double best[kKnn];
 #pragma unroll
   for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
-  const int kk = knn < n ? knn : n;
+  double T = __builtin_huge_val();
+  if (act && pix != nullptr && idxmap != nullptr) {
+    const int pp = pix[base + i];
+    const int v = pp / W, u = pp % W;
+    const int32_t* im = idxmap + (int64_t)b * H * W;
+    int found = 0;
+    for (int dv = -2; dv <= 2; ++dv) {
+      const int vv = v + dv;
+      if (vv < 0 || vv >= H) continue;
+      for (int du = -2; du <= 2; ++du) {
+        const int uu = u + du;
+        if (uu < 0 || uu >= W) continue;
+        const int j = im[vv * W + uu];
+        if (j < 0) continue;
+        topk_insert(best, sqdist(q0, q1, q2, p + 3 * j));
+        ++found;
+      }
+    }
+    if (found >= kk) {
+#pragma unroll
+      for (int k = 0; k < kKnn; ++k)
+        if (k == kk - 1) T = best[k];  // static register index (no scratch)
+    }
+#pragma unroll
+    for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
+  }
+  const float qx = (float)(q0 - ox), qy = (float)(q1 - oy), qz = (float)(q2 - oz);
+  const float qa = fmaxf(fabsf(qx), fmaxf(fabsf(qy), fabsf(qz)));
+  const float Tf = T == __builtin_huge_val() ? __builtin_huge_valf() : (float)T;
   for (int t0 = 0; t0 < n; t0 += kSorTile) {
     const int tn = min(kSorTile, n - t0);
     __syncthreads();
-    for (int j = threadIdx.x; j < tn; j += kSorThreads) {
-      tx[j] = p[3 * (t0 + j)];
-      ty[j] = p[3 * (t0 + j) + 1];
-      tz[j] = p[3 * (t0 + j) + 2];
+    for (int e = threadIdx.x; e < tn; e += kSorThreads) {
+      const double* c = p + 3 * (t0 + e);
+      const float cx = (float)(c[0] - ox), cy = (float)(c[1] - oy), cz = (float)(c[2] - oz);
+      tile[e] = make_float4(cx, cy, cz, fmaxf(fabsf(cx), fmaxf(fabsf(cy), fabsf(cz))));
     }
     __syncthreads();
     if (act) {
-      for (int j = 0; j < tn; ++j) {
-        const double dx = qx - tx[j], dy = qy - ty[j], dz = qz - tz[j];
-        const double s = (dx * dx + dy * dy) + dz * dz;  // nanoflann L2: ((dx²+dy²)+dz²)
-        if (s < best[kKnn - 1]) {
-          double v = s;
-#pragma unroll
-          for (int k = 0; k < kKnn; ++k) {  // bubble v into the sorted list
-            const double lo = fmin(best[k], v), hi = fmax(best[k], v);
-            best[k] = lo;
-            v = hi;
-          }
+      for (int e = 0; e < tn; ++e) {
+        const float4 c = tile[e];
+        const float dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
+        const float d32 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+        const float sa = qa + c.w;
+        const float lim = fmaf(1.9073486e-6f, fmaf(sa, sa, Tf), Tf);  // T + 2^-19 (T + S^2)
+        if (d32 <= lim) {
+          const double s = sqdist(q0, q1, q2, p + 3 * (t0 + e));
+          if (s <= T && s < best[kKnn - 1]) topk_insert(best, s);
         }
       }
     }
@@ -363,7 +420,7 @@ __global__ __launch_bounds__(256) void gather_transform_kernel(
 extern "C" int pk_backproject(const uint16_t* depth, const uint8_t* mask, int F, int H, int W,
                               const double* K, const float* cam_scale, int32_t* rowcnt,
                               int64_t* rowoff, int64_t* count, int64_t* off, double* xyz, int64_t cap,
-                              void* stream) {
+                              int32_t* pix, int32_t* idxmap, void* stream) {
   PK_REQUIRE(F >= 0 && H > 0 && W > 0 && cap >= 0);
   if (F == 0) return PK_OK;
   PK_REQUIRE(depth && mask && K && cam_scale && rowcnt && rowoff && count && off && (xyz || cap == 0));
@@ -375,23 +432,25 @@ extern "C" int pk_backproject(const uint16_t* depth, const uint8_t* mask, int F,
   hipLaunchKernelGGL(offsets_kernel, dim3(1), dim3(64), 0, s, count, F, off);
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(bp_write_kernel, dim3(H, F), dim3(64), 0, s, depth, mask, H, W, K, cam_scale,
-                     rowoff, off, xyz, cap);
+                     rowoff, off, xyz, cap, pix, idxmap);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
 
 extern "C" int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, int knn,
-                      double std_ratio, double* avg, double* thr, int32_t* ccount, int64_t* coff,
+                      double std_ratio, const int32_t* pix, const int32_t* idxmap, int H, int W,
+                      double* avg, double* thr, int32_t* ccount, int64_t* coff,
                       int64_t* kept, int64_t* out_off, double* out64, float* out32,
                       int64_t* kept_idx, void* stream) {
   PK_REQUIRE(B >= 0 && nmax >= 0 && knn > 0 && knn <= kKnn);
   if (B == 0) return PK_OK;
   PK_REQUIRE(xyz && off && avg && thr && ccount && coff && kept && out_off);
+  PK_REQUIRE((pix == nullptr) == (idxmap == nullptr) && (pix == nullptr || (H > 0 && W > 0)));
   hipStream_t s = pk::as_stream(stream);
   const int nchunk = (nmax + 1023) / 1024;
   if (nmax > 0) {
     hipLaunchKernelGGL(sor_knn_kernel, dim3((nmax + kSorThreads - 1) / kSorThreads, B),
-                       dim3(kSorThreads), 0, s, xyz, off, knn, avg);
+                       dim3(kSorThreads), 0, s, xyz, off, knn, pix, idxmap, H, W, avg);
     PK_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(sor_stats_kernel, dim3(B), dim3(64), 0, s, avg, off, std_ratio, thr);
@@ -453,6 +512,76 @@ extern "C" int pk_gather_transform(const double* pcd, const int64_t* off, int B,
   hipLaunchKernelGGL(gather_transform_kernel, dim3((npmax + 255) / 256, B), dim3(256), 0,
                      pk::as_stream(stream), pcd, off, idx, idx_stride, npoint, out_off, R, t, sel64,
                      align64, sel32);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+// ---------------------------------------------------------------- erosion alone (object.py:52-71)
+namespace {
+__global__ __launch_bounds__(256) void erode_kernel(const uint8_t* __restrict__ mask, int H, int W,
+                                                    uint8_t* __restrict__ out) {
+  const int f = blockIdx.y;
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (int64_t)H * W) return;
+  const int v = (int)(p / W), u = (int)(p % W);
+  out[(int64_t)f * H * W + p] = eroded(mask + (int64_t)f * H * W, H, W, v, u) ? 1 : 0;
+}
+
+// H16 — bilinear sampling of an RGB / feature image at projected 3D points (build-defined;
+// the reference loads RGB only when color=True, dataset/scene.py:95-97, 153-156).
+// u = fx X / Z + cx, v = fy Y / Z + cy (pixels); bilinear with zero padding outside the
+// image, i.e. torch grid_sample(align_corners=True, padding_mode="zeros") on pixel
+// centres. img uint8 [F, H, W, C] channels-last; pts f64 [T,3] packed per frame (cm, camera
+// frame); out f32 [T, C] in [0, 1].
+__global__ __launch_bounds__(256) void sample_rgb_kernel(const uint8_t* __restrict__ img, int H, int W, int C,
+                                                         const double* __restrict__ K,
+                                                         const double* __restrict__ pts,
+                                                         const int64_t* __restrict__ off, float* __restrict__ out) {
+  const int f = blockIdx.y;
+  const int64_t o = off[f];
+  const int n = (int)(off[f + 1] - o);
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double* p = pts + 3 * (o + i);
+  const double* Kf = K + 9 * f;
+  const float u = (float)(Kf[0] * p[0] / p[2] + Kf[2]);
+  const float v = (float)(Kf[4] * p[1] / p[2] + Kf[5]);
+  const float u0f = floorf(u), v0f = floorf(v);
+  const int u0 = (int)u0f, v0 = (int)v0f;
+  const float au = u - u0f, av = v - v0f;
+  const uint8_t* im = img + (int64_t)f * H * W * C;
+  for (int c = 0; c < C; ++c) {
+    float acc = 0.f;
+#pragma unroll
+    for (int dv = 0; dv < 2; ++dv)
+#pragma unroll
+      for (int du = 0; du < 2; ++du) {
+        const int uu = u0 + du, vv = v0 + dv;
+        const float w = (du ? au : 1.f - au) * (dv ? av : 1.f - av);
+        if (uu >= 0 && uu < W && vv >= 0 && vv < H) acc = fmaf(w, (float)im[((int64_t)vv * W + uu) * C + c], acc);
+      }
+    out[(o + i) * C + c] = acc * (1.f / 255.f);
+  }
+}
+}  // namespace
+
+extern "C" int pk_erode_mask(const uint8_t* mask, int F, int H, int W, uint8_t* out, void* stream) {
+  PK_REQUIRE(F >= 0 && H > 0 && W > 0);
+  if (F == 0) return PK_OK;
+  PK_REQUIRE(mask && out);
+  hipLaunchKernelGGL(erode_kernel, dim3((H * W + 255) / 256, F), dim3(256), 0, pk::as_stream(stream), mask, H, W,
+                     out);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_sample_rgb(const uint8_t* img, int F, int H, int W, int C, const double* K, const double* pts,
+                             const int64_t* off, int nmax, float* out, void* stream) {
+  PK_REQUIRE(F >= 0 && H > 0 && W > 0 && C > 0 && nmax >= 0);
+  if (F == 0 || nmax == 0) return PK_OK;
+  PK_REQUIRE(img && K && pts && off && out);
+  hipLaunchKernelGGL(sample_rgb_kernel, dim3((nmax + 255) / 256, F), dim3(256), 0, pk::as_stream(stream), img, H, W,
+                     C, K, pts, off, out);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -72,6 +72,7 @@ __global__ __launch_bounds__(NT) void fps_kernel(
   __syncthreads();
 
   int far = start[b];
+  const int kmax = (n + NT - 1) / NT;
   int64_t* __restrict__ o = out + (int64_t)b * out_stride;
   for (int i = 0; i < np; ++i) {
     if (tid == 0) o[i] = far;
@@ -89,6 +90,7 @@ __global__ __launch_bounds__(NT) void fps_kernel(
     int bk = 0;
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
+      if (k >= kmax) break;  // block-uniform: crops smaller than the template bound skip work
       const float dx = px[k] - cx;
       const float dy = py[k] - cy;
       const float dz = pz[k] - cz;

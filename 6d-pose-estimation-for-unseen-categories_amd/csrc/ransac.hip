@@ -1,0 +1,342 @@
+// H13 — RANSAC + Umeyama pose fit from correspondences.
+//
+// Reference: scripts/test_RANSAC.py:288-310 -> Open3D 0.17
+// registration_ransac_based_on_correspondence(source = CAD, target = crop, corres,
+// max_correspondence_distance = 0.05, PointToPoint(with_scaling=False) = Eigen::umeyama,
+// ransac_n = 4, RANSACConvergenceCriteria(4000000, confidence 80000 -> clamped to 1), so
+// every hypothesis runs). Per hypothesis: 4 correspondences drawn with replacement, a
+// rigid fit, and over ALL correspondences: inlier if ||T s - d||^2 < d_max^2,
+// fitness = inliers / n, rmse = sqrt(sum inlier d^2 / inliers); best = max fitness, then
+// min rmse (then lowest hypothesis index, making the result deterministic where
+// Open3D's OpenMP merge is not).
+//
+// Hypothesis sampling is deterministic and shared with the oracle (include/posekern.h):
+//   corres row of draw j of hypothesis h = splitmix64(seed ^ splitmix64(4h + j)) % n.
+// Rigid fit: the maximiser of sum d·(R s) over SO(3) (what Umeyama's SVD with the det
+// sign fix returns) via Horn's quaternion: top eigenvector of the symmetric 4x4 N(S),
+// cyclic Jacobi in fp64 registers. Scoring: one hypothesis per lane, correspondences
+// staged in LDS (fp64) and broadcast; ((R0 s)·... ) + t - d evaluated in fp64 without
+// contraction like the C oracle.
+#include "common.hpp"
+
+namespace {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ int hyp_index(uint64_t seed, int64_t h, int j, int n) {
+  return (int)(splitmix64(seed ^ splitmix64((uint64_t)h * 4u + (uint64_t)j)) % (uint64_t)n);
+}
+
+// Jacobi eigen-decomposition of a symmetric 4x4 (a, in place) -> eigenvector of the
+// largest eigenvalue in q.
+__device__ void top_eigvec4(double a[4][4], double q[4]) {
+  double v[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    double off = 0.0;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int r = p + 1; r < 4; ++r) off += a[p][r] * a[p][r];
+    if (off < 1e-30 * (a[0][0] * a[0][0] + a[1][1] * a[1][1] + a[2][2] * a[2][2] + a[3][3] * a[3][3]) + 1e-300)
+      break;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+#pragma unroll
+      for (int r = p + 1; r < 4; ++r) {
+        const double apr = a[p][r];
+        if (apr == 0.0) continue;
+        const double theta = (a[r][r] - a[p][p]) / (2.0 * apr);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // A <- J^T A J
+          const double akp = a[k][p], akr = a[k][r];
+          a[k][p] = c * akp - s * akr;
+          a[k][r] = s * akp + c * akr;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const double apk = a[p][k], ark = a[r][k];
+          a[p][k] = c * apk - s * ark;
+          a[r][k] = s * apk + c * ark;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const double vkp = v[k][p], vkr = v[k][r];
+          v[k][p] = c * vkp - s * vkr;
+          v[k][r] = s * vkp + c * vkr;
+        }
+      }
+    }
+  }
+  double best = a[0][0];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) q[k] = v[k][0];
+#pragma unroll
+  for (int m = 1; m < 4; ++m) {
+    const bool take = a[m][m] > best;  // static indices only (no scratch)
+    best = take ? a[m][m] : best;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = take ? v[k][m] : q[k];
+  }
+}
+
+// Rigid fit of n = 4 pairs: R (row-major) and t with d ≈ R s + t.
+__device__ void rigid_fit4(const double s[4][3], const double d[4][3], double R[9], double t[3]) {
+  double ms[3] = {0, 0, 0}, md[3] = {0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      ms[c] += s[k][c];
+      md[c] += d[k][c];
+    }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    ms[c] *= 0.25;
+    md[c] *= 0.25;
+  }
+  double S[3][3] = {};
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) S[r][c] += (s[k][r] - ms[r]) * (d[k][c] - md[c]);
+  const double Sxx = S[0][0], Sxy = S[0][1], Sxz = S[0][2];
+  const double Syx = S[1][0], Syy = S[1][1], Syz = S[1][2];
+  const double Szx = S[2][0], Szy = S[2][1], Szz = S[2][2];
+  double N[4][4] = {
+      {Sxx + Syy + Szz, Syz - Szy, Szx - Sxz, Sxy - Syx},
+      {Syz - Szy, Sxx - Syy - Szz, Sxy + Syx, Szx + Sxz},
+      {Szx - Sxz, Sxy + Syx, -Sxx + Syy - Szz, Syz + Szy},
+      {Sxy - Syx, Szx + Sxz, Syz + Szy, -Sxx - Syy + Szz}};
+  double q[4];
+  top_eigvec4(N, q);
+  const double nq = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  const double w = q[0] / nq, x = q[1] / nq, y = q[2] / nq, z = q[3] / nq;
+  R[0] = w * w + x * x - y * y - z * z;
+  R[1] = 2.0 * (x * y - w * z);
+  R[2] = 2.0 * (x * z + w * y);
+  R[3] = 2.0 * (x * y + w * z);
+  R[4] = w * w - x * x + y * y - z * z;
+  R[5] = 2.0 * (y * z - w * x);
+  R[6] = 2.0 * (x * z - w * y);
+  R[7] = 2.0 * (y * z + w * x);
+  R[8] = w * w - x * x - y * y + z * z;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) t[r] = md[r] - ((R[3 * r] * ms[0] + R[3 * r + 1] * ms[1]) + R[3 * r + 2] * ms[2]);
+}
+
+constexpr int kRThreads = 256;
+constexpr int kRTile = 2048;  // correspondences per LDS tile (96 KiB fp64)
+
+struct Best {
+  int good;
+  double rmse;
+  int64_t h;
+};
+
+__device__ __forceinline__ bool better(int g1, double r1, int64_t h1, int g2, double r2, int64_t h2) {
+  if (g1 != g2) return g1 > g2;
+  if (r1 != r2) return r1 < r2;
+  return h1 < h2;
+}
+
+__device__ __forceinline__ void load_hyp(const double* __restrict__ src, const double* __restrict__ dst,
+                                         const int32_t* __restrict__ cr, int n, uint64_t seed, int64_t h,
+                                         const int32_t* __restrict__ hyps, double s4[4][3], double d4[4][3]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = hyps ? hyps[4 * h + j] : hyp_index(seed, h, j, n);
+    const int64_t si = cr[2 * c], di = cr[2 * c + 1];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      s4[j][k] = src[3 * si + k];
+      d4[j][k] = dst[3 * di + k];
+    }
+  }
+}
+
+// grid (ceil(H / 256), B), block 256: one hypothesis per thread; per-block best.
+__global__ __launch_bounds__(kRThreads) void ransac_score_kernel(
+    const double* __restrict__ src, const int64_t* __restrict__ src_off, const double* __restrict__ dst,
+    const int64_t* __restrict__ dst_off, const int32_t* __restrict__ corres, const int64_t* __restrict__ cor_off,
+    const int32_t* __restrict__ hyps, const int64_t* __restrict__ hyp_off, uint64_t seed, int64_t H,
+    double max_d2, int nblk, int* __restrict__ bgood, double* __restrict__ brmse, int64_t* __restrict__ bh) {
+  extern __shared__ __attribute__((aligned(16))) double sp[];  // [tile][6] (s xyz, d xyz)
+  __shared__ int sg[4];
+  __shared__ double sr[4];
+  __shared__ int64_t shh[4];
+  const int b = blockIdx.y;
+  const int64_t c0 = cor_off[b];
+  const int n = (int)(cor_off[b + 1] - c0);
+  const int32_t* cr = corres + 2 * c0;
+  const double* S = src + 3 * src_off[b];
+  const double* Dp = dst + 3 * dst_off[b];
+  const int32_t* hy = hyps ? hyps + 4 * hyp_off[b] : nullptr;
+  const int64_t h = (int64_t)blockIdx.x * kRThreads + threadIdx.x;
+  const bool act = h < H && n >= 4;
+  double R[9], t[3];
+  if (act) {
+    double s4[4][3], d4[4][3];
+    load_hyp(S, Dp, cr, n, seed, h, hy, s4, d4);
+    rigid_fit4(s4, d4, R, t);
+  }
+  int good = 0;
+  double err = 0.0;
+  for (int t0 = 0; t0 < n; t0 += kRTile) {
+    const int tn = min(kRTile, n - t0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < tn; e += kRThreads) {
+      const int64_t si = cr[2 * (t0 + e)], di = cr[2 * (t0 + e) + 1];
+      sp[6 * e + 0] = S[3 * si];
+      sp[6 * e + 1] = S[3 * si + 1];
+      sp[6 * e + 2] = S[3 * si + 2];
+      sp[6 * e + 3] = Dp[3 * di];
+      sp[6 * e + 4] = Dp[3 * di + 1];
+      sp[6 * e + 5] = Dp[3 * di + 2];
+    }
+    __syncthreads();
+    if (act) {
+      for (int e = 0; e < tn; ++e) {
+        const double sx = sp[6 * e], sy = sp[6 * e + 1], sz = sp[6 * e + 2];
+        const double ex = (((R[0] * sx + R[1] * sy) + R[2] * sz) + t[0]) - sp[6 * e + 3];
+        const double ey = (((R[3] * sx + R[4] * sy) + R[5] * sz) + t[1]) - sp[6 * e + 4];
+        const double ez = (((R[6] * sx + R[7] * sy) + R[8] * sz) + t[2]) - sp[6 * e + 5];
+        const double d2 = (ex * ex + ey * ey) + ez * ez;
+        if (d2 < max_d2) {
+          ++good;
+          err += d2;
+        }
+      }
+    }
+  }
+  double rmse = good ? sqrt(err / good) : 0.0;
+  int64_t hh = act ? h : INT64_MAX;
+  if (!act) good = -1;
+  // wave reduction (shuffles) then block
+  for (int off = 32; off >= 1; off >>= 1) {
+    const int og = __shfl_xor(good, off);
+    const double orm = __shfl_xor(rmse, off);
+    const int64_t oh = __shfl_xor(hh, off);
+    if (better(og, orm, oh, good, rmse, hh)) {
+      good = og;
+      rmse = orm;
+      hh = oh;
+    }
+  }
+  if (pk::lane_id() == 0) {
+    sg[pk::wave_id()] = good;
+    sr[pk::wave_id()] = rmse;
+    shh[pk::wave_id()] = hh;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (better(sg[w], sr[w], shh[w], good, rmse, hh)) {
+        good = sg[w];
+        rmse = sr[w];
+        hh = shh[w];
+      }
+    const int64_t o = (int64_t)b * nblk + blockIdx.x;
+    bgood[o] = good;
+    brmse[o] = rmse;
+    bh[o] = hh;
+  }
+}
+
+// grid (B), block 256: best over blocks, refit the winner -> T (4x4 row-major), stats.
+__global__ __launch_bounds__(256) void ransac_final_kernel(
+    const double* __restrict__ src, const int64_t* __restrict__ src_off, const double* __restrict__ dst,
+    const int64_t* __restrict__ dst_off, const int32_t* __restrict__ corres, const int64_t* __restrict__ cor_off,
+    const int32_t* __restrict__ hyps, const int64_t* __restrict__ hyp_off, uint64_t seed, int nblk,
+    const int* __restrict__ bgood, const double* __restrict__ brmse, const int64_t* __restrict__ bh,
+    double* __restrict__ T, double* __restrict__ stats) {
+  __shared__ int sg[4];
+  __shared__ double sr[4];
+  __shared__ int64_t shh[4];
+  const int b = blockIdx.x;
+  int good = -1;
+  double rmse = 0.0;
+  int64_t hh = INT64_MAX;
+  for (int k = threadIdx.x; k < nblk; k += 256) {
+    const int64_t o = (int64_t)b * nblk + k;
+    if (better(bgood[o], brmse[o], bh[o], good, rmse, hh)) {
+      good = bgood[o];
+      rmse = brmse[o];
+      hh = bh[o];
+    }
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    const int og = __shfl_xor(good, off);
+    const double orm = __shfl_xor(rmse, off);
+    const int64_t oh = __shfl_xor(hh, off);
+    if (better(og, orm, oh, good, rmse, hh)) {
+      good = og;
+      rmse = orm;
+      hh = oh;
+    }
+  }
+  if (pk::lane_id() == 0) {
+    sg[pk::wave_id()] = good;
+    sr[pk::wave_id()] = rmse;
+    shh[pk::wave_id()] = hh;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  for (int w = 1; w < 4; ++w)
+    if (better(sg[w], sr[w], shh[w], good, rmse, hh)) {
+      good = sg[w];
+      rmse = sr[w];
+      hh = shh[w];
+    }
+  const int64_t c0 = cor_off[b];
+  const int n = (int)(cor_off[b + 1] - c0);
+  double* Tb = T + 16 * b;
+  for (int k = 0; k < 16; ++k) Tb[k] = (k % 5 == 0) ? 1.0 : 0.0;
+  stats[3 * b + 0] = 0.0;
+  stats[3 * b + 1] = 0.0;
+  stats[3 * b + 2] = -1.0;
+  if (good < 0 || hh == INT64_MAX || n < 4) return;
+  double s4[4][3], d4[4][3], R[9], t[3];
+  load_hyp(src + 3 * src_off[b], dst + 3 * dst_off[b], corres + 2 * c0, n, seed, hh,
+           hyps ? hyps + 4 * hyp_off[b] : nullptr, s4, d4);
+  rigid_fit4(s4, d4, R, t);
+  for (int r = 0; r < 3; ++r) {
+    for (int c = 0; c < 3; ++c) Tb[4 * r + c] = R[3 * r + c];
+    Tb[4 * r + 3] = t[r];
+  }
+  stats[3 * b + 0] = good > 0 ? (double)good / (double)n : 0.0;
+  stats[3 * b + 1] = rmse;
+  stats[3 * b + 2] = (double)hh;
+}
+
+}  // namespace
+
+extern "C" int pk_ransac(const double* src, const int64_t* src_off, const double* dst, const int64_t* dst_off,
+                         const int32_t* corres, const int64_t* cor_off, const int32_t* hyps, const int64_t* hyp_off,
+                         uint64_t seed, int64_t H, double max_dist, int B, int* bgood, double* brmse, int64_t* bh,
+                         double* T, double* stats, void* stream) {
+  PK_REQUIRE(B >= 0 && H >= 0 && max_dist > 0.0);
+  if (B == 0) return PK_OK;
+  PK_REQUIRE(src && src_off && dst && dst_off && corres && cor_off && bgood && brmse && bh && T && stats);
+  PK_REQUIRE(hyps == nullptr || hyp_off != nullptr);
+  hipStream_t s = pk::as_stream(stream);
+  const int nblk = (int)((H + kRThreads - 1) / kRThreads);
+  if (nblk > 0) {
+    hipLaunchKernelGGL(ransac_score_kernel, dim3(nblk, B), dim3(kRThreads), kRTile * 6 * sizeof(double), s, src,
+                       src_off, dst, dst_off, corres, cor_off, hyps, hyp_off, seed, H, max_dist * max_dist, nblk,
+                       bgood, brmse, bh);
+    PK_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(ransac_final_kernel, dim3(B), dim3(256), 0, s, src, src_off, dst, dst_off, corres, cor_off, hyps,
+                     hyp_off, seed, nblk, bgood, brmse, bh, T, stats);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}

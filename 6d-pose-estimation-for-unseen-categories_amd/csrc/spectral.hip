@@ -1,0 +1,176 @@
+// H7 — spectral diffusion of DiffusionNet's LearnedTimeDiffusion (upstream diffusion-net
+// layers.py, used by models/dpfm.py:22-30), forward and backward, fp32.
+//
+//   forward : spec = Phi^T (m ⊙ x)           [K, C]   (to_basis)
+//             y    = Phi (E ⊙ spec),  E[k,c] = exp(-lambda_k t_c)   (from_basis)
+//   backward: gs   = Phi^T g                  [K, C]
+//             gx   = Phi (E ⊙ gs) ⊙ m  (per row)
+//             gt_c = -sum_k lambda_k E[k,c] spec[k,c] gs[k,c]   (per crop; caller sums b)
+// One code path serves both (`mode`): reduce (Phi^T · rows) -> combine (+E, +gt) ->
+// expand (Phi · coefficients [· m]). Layout: x / y [B, N, C], Phi [B, N, K] row-major,
+// m [B, N], lambda [B, K], t [C]; N is the padded per-crop point count.
+#include "common.hpp"
+
+namespace {
+
+constexpr int kRows = 64;     // rows of Phi reduced per block in pass 1
+constexpr int kSub = 32;      // rows staged in LDS per step
+constexpr int kKC = 64;       // K == C == 64 (C_width, k_eig) — checked on the host
+
+// pass 1: part[b, s] = sum_{rows in chunk s} Phi[r, :]^T (w_r * x[r, :]), w = mass or 1.
+// grid (S, B), block 256 = 16 x 16 threads, each owning a 4 x 4 output micro-tile.
+__global__ __launch_bounds__(256) void spec_reduce_kernel(const float* __restrict__ x,
+                                                          const float* __restrict__ mass,
+                                                          const float* __restrict__ evecs, int N, int S,
+                                                          float* __restrict__ part) {
+  __shared__ float4 sphi[kSub][kKC / 4 + 1];
+  __shared__ float4 sx[kSub][kKC / 4 + 1];
+  const int s = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int ty = tid >> 4, tx = tid & 15;
+  const float* __restrict__ phi = evecs + (int64_t)b * N * kKC;
+  const float* __restrict__ xb = x + (int64_t)b * N * kKC;
+  const float* __restrict__ mb = mass ? mass + (int64_t)b * N : nullptr;
+  float acc[4][4] = {};
+  const int r_begin = s * kRows;
+  const int r_end = min(N, r_begin + kRows);
+  for (int r0 = r_begin; r0 < r_end; r0 += kSub) {
+    __syncthreads();
+    for (int e = tid; e < kSub * (kKC / 4); e += 256) {
+      const int rr = e / (kKC / 4), q = e % (kKC / 4);
+      const int r = r0 + rr;
+      float4 pv = make_float4(0.f, 0.f, 0.f, 0.f), xv = pv;
+      if (r < r_end) {
+        pv = reinterpret_cast<const float4*>(phi + (int64_t)r * kKC)[q];
+        xv = reinterpret_cast<const float4*>(xb + (int64_t)r * kKC)[q];
+        if (mb) {
+          const float w = mb[r];
+          xv.x *= w; xv.y *= w; xv.z *= w; xv.w *= w;
+        }
+      }
+      sphi[rr][q] = pv;
+      sx[rr][q] = xv;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int rr = 0; rr < kSub; ++rr) {
+      const float4 p = sphi[rr][ty];
+      const float4 v = sx[rr][tx];
+      const float pk[4] = {p.x, p.y, p.z, p.w};
+      const float vc[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(pk[i], vc[j], acc[i][j]);
+    }
+  }
+  float* __restrict__ o = part + ((int64_t)b * S + s) * kKC * kKC;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    reinterpret_cast<float4*>(o + (ty * 4 + i) * kKC)[tx] = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+}
+
+// pass 2: coef = sum_s part; save raw (optional), scaled = E ⊙ coef; optional gt partial
+// gt[b, c] = -sum_k lambda_k E[k,c] saved[k,c] coef[k,c]. grid (B), block 256.
+__global__ __launch_bounds__(256) void spec_combine_kernel(const float* __restrict__ part, int S,
+                                                           const float* __restrict__ evals,
+                                                           const float* __restrict__ t,
+                                                           float* __restrict__ raw,
+                                                           float* __restrict__ scaled,
+                                                           const float* __restrict__ saved,
+                                                           float* __restrict__ gt) {
+  __shared__ float gsum[4][kKC];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int c = tid & 63, kq = tid >> 6;  // 4 groups of 16 k's
+  float g = 0.f;
+  for (int k = kq; k < kKC; k += 4) {
+    float v = 0.f;
+    for (int s = 0; s < S; ++s) v += part[((int64_t)b * S + s) * kKC * kKC + k * kKC + c];
+    const float lam = evals[b * kKC + k];
+    const float E = expf(-lam * t[c]);
+    const int64_t o = (int64_t)b * kKC * kKC + k * kKC + c;
+    if (raw) raw[o] = v;
+    scaled[o] = E * v;
+    if (gt) g = fmaf(-lam * E, saved[o] * v, g);
+  }
+  if (gt) {
+    gsum[kq][c] = g;
+    __syncthreads();
+    if (kq == 0) gt[b * kKC + c] = (gsum[0][c] + gsum[1][c]) + (gsum[2][c] + gsum[3][c]);
+  }
+}
+
+// pass 3: y[r, :] = Phi[r, :] · coef (· mass[r] if given). grid (ceil(N/64), B), block 256:
+// 16 x 16 threads, 4 rows x 4 cols each.
+__global__ __launch_bounds__(256) void spec_expand_kernel(const float* __restrict__ evecs,
+                                                          const float* __restrict__ coef,
+                                                          const float* __restrict__ mass, int N,
+                                                          float* __restrict__ y) {
+  __shared__ float4 scoef[kKC][kKC / 4];
+  __shared__ float sphi[64][kKC + 1];
+  const int tile = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int ty = tid >> 4, tx = tid & 15;
+  const float* __restrict__ cb = coef + (int64_t)b * kKC * kKC;
+  for (int e = tid; e < kKC * kKC / 4; e += 256) scoef[e / 16][e % 16] = reinterpret_cast<const float4*>(cb)[e];
+  const int r0 = tile * 64;
+  const float* __restrict__ phi = evecs + (int64_t)b * N * kKC;
+  for (int e = tid; e < 64 * kKC / 4; e += 256) {
+    const int rr = e / 16, q = e % 16;
+    const int r = r0 + rr;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < N) v = reinterpret_cast<const float4*>(phi + (int64_t)r * kKC)[q];
+    sphi[rr][4 * q + 0] = v.x;
+    sphi[rr][4 * q + 1] = v.y;
+    sphi[rr][4 * q + 2] = v.z;
+    sphi[rr][4 * q + 3] = v.w;
+  }
+  __syncthreads();
+  float acc[4][4] = {};
+#pragma unroll 8
+  for (int k = 0; k < kKC; ++k) {
+    const float4 cv = scoef[k][tx];
+    const float cc[4] = {cv.x, cv.y, cv.z, cv.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float p = sphi[ty * 4 + i][k];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(p, cc[j], acc[i][j]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + ty * 4 + i;
+    if (r >= N) continue;
+    float w = 1.f;
+    if (mass) w = mass[(int64_t)b * N + r];
+    reinterpret_cast<float4*>(y + ((int64_t)b * N + r) * kKC)[tx] =
+        make_float4(acc[i][0] * w, acc[i][1] * w, acc[i][2] * w, acc[i][3] * w);
+  }
+}
+
+}  // namespace
+
+// mode 0 (forward): in = x, out = y, raw = spec (saved for backward), reduce weights = mass.
+// mode 1 (backward): in = g, out = gx, saved = spec from forward, gt = per-crop dL/dt
+//                    partials [B, C]; expand weights = mass.
+extern "C" int pk_spectral_diffusion(const float* in, const float* mass, const float* evecs,
+                                     const float* evals, const float* t, int B, int N, int K, int C,
+                                     int mode, float* work, float* raw, float* scaled,
+                                     const float* saved, float* gt, float* out, void* stream) {
+  PK_REQUIRE(B >= 0 && N >= 0 && K == kKC && C == kKC && (mode == 0 || mode == 1));
+  if (B == 0 || N == 0) return PK_OK;
+  PK_REQUIRE(in && evecs && evals && t && work && scaled && out);
+  PK_REQUIRE(mode == 0 || (saved && gt));
+  hipStream_t s = pk::as_stream(stream);
+  const int S = (N + kRows - 1) / kRows;
+  hipLaunchKernelGGL(spec_reduce_kernel, dim3(S, B), dim3(256), 0, s, in, mode == 0 ? mass : nullptr,
+                     evecs, N, S, work);
+  PK_CHECK_LAUNCH();
+  hipLaunchKernelGGL(spec_combine_kernel, dim3(B), dim3(256), 0, s, work, S, evals, t, raw, scaled,
+                     mode == 1 ? saved : nullptr, mode == 1 ? gt : nullptr);
+  PK_CHECK_LAUNCH();
+  hipLaunchKernelGGL(spec_expand_kernel, dim3((N + 63) / 64, B), dim3(256), 0, s, evecs, scaled,
+                     mode == 1 ? mass : nullptr, N, out);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+

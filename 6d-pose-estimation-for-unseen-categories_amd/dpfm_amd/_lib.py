@@ -27,12 +27,23 @@ SIGNATURES = {
     "pk_fps": [_P, _P, _I, _I, _P, _P, _P, _I, _P],
     "pk_ball_query_mask": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P],
     "pk_ball_query_pairs": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _I64, _P, _P, _P, _P],
-    "pk_backproject": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I64, _P],
-    "pk_sor": [_P, _P, _I, _I, _I, _D, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "pk_backproject": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P],
+    "pk_sor": [_P, _P, _I, _I, _I, _D, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "pk_fps_npoint": [_P, _I, _I, _I, _U64, _P, _P, _P, _P],
     "pk_gather_transform": [_P, _P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P],
     "pk_segment_scan": [_P, _I, _I, _P, _P, _P],
     "pk_offsets_from_counts": [_P, _I, _P, _P],
+    "pk_spectral_diffusion": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "pk_fmap_solve": [_P, _P, _P, _F, _I, _I, _P, _P],
+    "pk_fmap_solve_backward": [_P, _P, _P, _F, _I, _I, _P, _P, _P, _P],
+    "pk_feat_dist_topk": [_P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "pk_rigidity_filter": [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P],
+    "pk_inlier_ratio": [_P, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P],
+    "pk_cgt_lstsq": [_P, _I, _P, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P],
+    "pk_ransac": [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _I64, _D, _I, _P, _P, _P, _P, _P, _P],
+    "pk_pose_metrics": [_P, _P, _I, _I, _P, _P, _P, _P, _P],
+    "pk_erode_mask": [_P, _I, _I, _I, _P, _P],
+    "pk_sample_rgb": [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -59,10 +70,18 @@ def lib() -> ctypes.CDLL:
 
 
 _ERRORS = {1000: "invalid argument", 1001: "output capacity exceeded"}
+_probe = None
+
+
+def set_probe(hook) -> None:
+    """Install hook(name, thunk) around every call (bench.py's per-kernel HIP events)."""
+    global _probe
+    _probe = hook
 
 
 def call(name: str, *args) -> None:
-    status = getattr(lib(), name)(*args)
+    fn = getattr(lib(), name)
+    status = _probe(name, lambda: fn(*args)) if _probe is not None else fn(*args)
     if status != 0:
         msg = _ERRORS.get(status, f"hipError_t {status}")
         raise PoseKernError(f"{name} failed: {msg}")

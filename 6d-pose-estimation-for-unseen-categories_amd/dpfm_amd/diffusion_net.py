@@ -1,0 +1,91 @@
+"""Spectral DiffusionNet encoder — the DPFM point encoder (H7).
+
+Mirrors upstream diffusion-net `layers.py` as vendored by the DPFM submodule (imported at
+models/dpfm.py:11, built at models/dpfm.py:22-30 with C_in=3, C_out=32, C_width=64,
+N_block=2, dropout=False, with_gradient_features=False): same module and parameter
+names as weights/weights.pt (`first_lin`, `block_{i}.diffusion.diffusion_time`,
+`block_{i}.mlp.miniMLP_mlp_layer_{000,001,002}`, `last_lin`).
+
+The diffusion step (to_basis -> exp(-lambda t) -> from_basis) runs in one fused HIP kernel
+per direction (ops.spectral_diffusion); the per-point MLPs are GEMMs.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+
+
+class LearnedTimeDiffusion(nn.Module):
+    def __init__(self, C_inout: int, method: str = "spectral"):
+        super().__init__()
+        if method != "spectral":
+            raise ValueError("only spectral diffusion is on the hot path (models/dpfm.py:22-30)")
+        self.C_inout = C_inout
+        self.diffusion_time = nn.Parameter(torch.zeros(C_inout))
+
+    def forward(self, x, L, mass, evals, evecs):
+        with torch.no_grad():  # in-place clamp, as upstream
+            self.diffusion_time.data = torch.clamp(self.diffusion_time, min=1e-8)
+        return ops.spectral_diffusion(x, mass, evals, evecs, self.diffusion_time)
+
+
+class MiniMLP(nn.Sequential):
+    def __init__(self, layer_sizes, dropout=False, activation=nn.ReLU, name="miniMLP"):
+        super().__init__()
+        for i in range(len(layer_sizes) - 1):
+            if dropout and i > 0:
+                self.add_module(name + "_mlp_layer_dropout_{:03d}".format(i), nn.Dropout(p=0.5))
+            self.add_module(name + "_mlp_layer_{:03d}".format(i), nn.Linear(layer_sizes[i], layer_sizes[i + 1]))
+            if i + 2 != len(layer_sizes):
+                self.add_module(name + "_mlp_act_{:03d}".format(i), activation())
+
+
+class DiffusionNetBlock(nn.Module):
+    def __init__(self, C_width, mlp_hidden_dims, dropout=False, diffusion_method="spectral",
+                 with_gradient_features=False, with_gradient_rotations=True):
+        super().__init__()
+        if with_gradient_features:
+            raise ValueError("gradient features are off in the reference config (models/dpfm.py:28)")
+        self.C_width = C_width
+        self.diffusion = LearnedTimeDiffusion(C_width, method=diffusion_method)
+        self.mlp = MiniMLP([2 * C_width] + list(mlp_hidden_dims) + [C_width], dropout=dropout)
+
+    def forward(self, x_in, mass, L, evals, evecs, gradX, gradY):
+        x_diffuse = self.diffusion(x_in, L, mass, evals, evecs)
+        return self.mlp(torch.cat((x_in, x_diffuse), dim=-1)) + x_in
+
+
+class DiffusionNet(nn.Module):
+    def __init__(self, C_in, C_out, C_width=128, N_block=4, last_activation=None, outputs_at="vertices",
+                 mlp_hidden_dims=None, dropout=True, with_gradient_features=True, with_gradient_rotations=True,
+                 diffusion_method="spectral"):
+        super().__init__()
+        if outputs_at != "vertices":
+            raise ValueError("DPFM reads features at vertices")
+        self.C_in, self.C_out, self.C_width, self.N_block = C_in, C_out, C_width, N_block
+        self.last_activation = last_activation
+        if mlp_hidden_dims is None:
+            mlp_hidden_dims = [C_width, C_width]
+        self.first_lin = nn.Linear(C_in, C_width)
+        self.last_lin = nn.Linear(C_width, C_out)
+        self.blocks = []
+        for i_block in range(N_block):
+            blk = DiffusionNetBlock(C_width, mlp_hidden_dims, dropout=dropout, diffusion_method=diffusion_method,
+                                    with_gradient_features=with_gradient_features,
+                                    with_gradient_rotations=with_gradient_rotations)
+            self.blocks.append(blk)
+            self.add_module("block_" + str(i_block), blk)
+
+    def forward(self, x_in, mass, L=None, evals=None, evecs=None, gradX=None, gradY=None, edges=None, faces=None):
+        appended = x_in.dim() == 2
+        if appended:
+            x_in, mass, evals, evecs = x_in[None], mass[None], evals[None], evecs[None]
+        x = self.first_lin(x_in)
+        for b in self.blocks:
+            x = b(x, mass, L, evals, evecs, gradX, gradY)
+        x = self.last_lin(x)
+        if self.last_activation is not None:
+            x = self.last_activation(x)
+        return x[0] if appended else x

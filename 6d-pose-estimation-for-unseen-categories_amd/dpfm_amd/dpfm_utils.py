@@ -47,6 +47,18 @@ def get_mask(evals1: torch.Tensor, evals2: torch.Tensor, gamma: float = 0.5, dev
     return M_re.square() + M_im.square()
 
 
+def get_mask_batched(evals1: torch.Tensor, evals2: torch.Tensor, gamma: float = 0.5) -> torch.Tensor:
+    """get_mask for every crop at once: evals [B, K1], [B, K2] -> [B, K2, K1] (same
+    arithmetic per crop; one launch sequence instead of a Python loop over crops)."""
+    s = torch.maximum(evals1.max(dim=1).values, evals2.max(dim=1).values)[:, None]
+    e1, e2 = evals1 / s, evals2 / s
+    g1 = (e1 ** gamma)[:, None, :]
+    g2 = (e2 ** gamma)[:, :, None]
+    M_re = g2 / (g2.square() + 1) - g1 / (g1.square() + 1)
+    M_im = 1 / (g2.square() + 1) - 1 / (g1.square() + 1)
+    return M_re.square() + M_im.square()
+
+
 class WeightedBCELoss(nn.Module):
     """Upstream dpfm/utils.py::WeightedBCELoss (SURVEY Appendix A): padded zeros count
     as negatives, weights from the positive fraction of `gt`."""

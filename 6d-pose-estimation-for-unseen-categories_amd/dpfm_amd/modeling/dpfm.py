@@ -1,0 +1,145 @@
+"""Cross-attention refinement, overlap head and regularized fmap head (H8, H9).
+
+Mirror of reference modeling/dpfm.py:16-195: same classes, constructor arguments,
+parameter names (weights/weights.pt loads strictly) and semantics, including the
+reference's quirks: heads interleaved by view(B, dim, heads, N)
+(:53), desc1 updated with the already-updated desc0 (:101-103), unmasked
+InstanceNorm over zero padding (:24), the batched fmap branch always taken (:164).
+The attention core runs in the fused HIP kernel `ops.attention` (scores never hit HBM);
+the 30 sequential inverses of the fmap head are one HIP launch (`ops.fmap_solve`).
+"""
+from __future__ import annotations
+
+from copy import deepcopy
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ..dpfm_utils import get_mask_batched
+
+
+def MLP(channels: list, do_bn=True):
+    """Multi-layer perceptron of 1x1 convolutions (modeling/dpfm.py:16-26)."""
+    n = len(channels)
+    layers = []
+    for i in range(1, n):
+        layers.append(nn.Conv1d(channels[i - 1], channels[i], kernel_size=1, bias=True))
+        if i < (n - 1):
+            if do_bn:
+                layers.append(nn.InstanceNorm1d(channels[i]))
+            layers.append(nn.ReLU())
+    return nn.Sequential(*layers)
+
+
+def attention(query, key, value):
+    """modeling/dpfm.py:29-37. Tensors are [B, d, heads, N]; returns (result, None): the
+    probability matrix is never materialised (the reference's caller discards it)."""
+    return ops.attention(query, key, value), None
+
+
+class MultiHeadedAttention(nn.Module):
+    def __init__(self, num_heads: int, d_model: int):
+        super().__init__()
+        assert d_model % num_heads == 0
+        self.dim = d_model // num_heads
+        self.num_heads = num_heads
+        self.merge = nn.Conv1d(d_model, d_model, kernel_size=1)
+        self.proj = nn.ModuleList([deepcopy(self.merge) for _ in range(3)])
+
+    def forward(self, query, key, value):
+        B = query.size(0)
+        q, k, v = [ll(x).view(B, self.dim, self.num_heads, -1) for ll, x in zip(self.proj, (query, key, value))]
+        x, _ = attention(q, k, v)
+        return self.merge(x.contiguous().view(B, self.dim * self.num_heads, -1))
+
+
+class AttentionalPropagation(nn.Module):
+    def __init__(self, feature_dim: int, num_heads: int):
+        super().__init__()
+        self.attn = MultiHeadedAttention(num_heads, feature_dim)
+        self.mlp = MLP([feature_dim * 2, feature_dim * 2, feature_dim])
+        nn.init.constant_(self.mlp[-1].bias, 0.0)
+
+    def forward(self, x, source):
+        message = self.attn(x, source, source)
+        return self.mlp(torch.cat([x, message], dim=1))
+
+
+class CrossAttentionRefinementNet(nn.Module):
+    def __init__(self, n_in=128, num_head=4, gnn_dim=512, overlap_feat_dim=32, n_layers=2,
+                 cross_sampling_ratio=0.15, attention_type="normal"):
+        super().__init__()
+        self.attention_type = attention_type
+        if attention_type == "normal":
+            additional_dim = 0
+            overlap_feat_dim = n_in
+        elif attention_type == "double":
+            additional_dim = overlap_feat_dim
+        else:
+            raise Exception("Attention type not recognized")
+        if cross_sampling_ratio != 1:
+            # the subsampled branch (modeling/dpfm.py:105-118) references undefined names in
+            # the reference and can never run; only ratio 1.0 is a working configuration
+            raise ValueError("cross_sampling_ratio != 1 is not a working configuration of the reference")
+        self.n_in = n_in
+        self.cross_sampling_ratio = cross_sampling_ratio
+        self.layers = nn.ModuleList([AttentionalPropagation(gnn_dim + additional_dim, num_head) for _ in range(n_layers)])
+        self.first_lin = nn.Linear(n_in, gnn_dim + additional_dim)
+        self.last_lin = nn.Linear(gnn_dim + additional_dim, n_in + additional_dim)
+        self.overlap_predictor = OverlapPredictorNet(overlap_feat_dim=overlap_feat_dim)
+
+    def forward(self, coords0, coords1, features_x, features_y, batch=None):
+        desc0, desc1 = self.first_lin(features_x).transpose(1, 2), self.first_lin(features_y).transpose(1, 2)
+        for layer in self.layers:
+            desc0 = desc0 + layer(desc0, desc1)
+            desc1 = desc1 + layer(desc1, desc0)
+        ax = self.last_lin(desc0.transpose(1, 2))
+        ay = self.last_lin(desc1.transpose(1, 2))
+        ref_x, ref_y = ax[:, :, :self.n_in], ay[:, :, :self.n_in]
+        if self.attention_type == "normal":
+            ox, oy = self.overlap_predictor(ref_x, ref_y)
+        else:
+            ox, oy = self.overlap_predictor(ax[:, :, self.n_in:], ay[:, :, self.n_in:])
+        return ref_x, ref_y, ox, oy
+
+
+class OverlapPredictorNet(nn.Module):
+    def __init__(self, overlap_feat_dim=32):
+        super().__init__()
+        self.overlap_score_net = nn.Sequential(
+            nn.Linear(overlap_feat_dim, overlap_feat_dim, bias=True),
+            nn.ReLU(True),
+            nn.Linear(overlap_feat_dim, 1, bias=True),
+            nn.Sigmoid(),
+        )
+
+    def forward(self, overlap_feat_x, overlap_feat_y):
+        nx = F.normalize(overlap_feat_x, p=2, dim=-1)
+        ny = F.normalize(overlap_feat_y, p=2, dim=-1)
+        sx = self.overlap_score_net(nx).squeeze(2).squeeze(0)
+        sy = self.overlap_score_net(ny).squeeze(2).squeeze(0)
+        return sx, sy
+
+
+class RegularizedFMNet(nn.Module):
+    """Compute the functional map matrix representation (modeling/dpfm.py:154-195)."""
+
+    def __init__(self, lambda_=1e-3, resolvant_gamma=0.5):
+        super().__init__()
+        self.lambda_ = lambda_
+        self.resolvant_gamma = resolvant_gamma
+
+    def forward(self, feat_x, feat_y, evals_x, evals_y, evecs_trans_x, evecs_trans_y):
+        # the reference compares the bound method `.dim` with 2 (:164), so the batched
+        # branch below is the one that always runs
+        if evecs_trans_x.dim() == 2:
+            evecs_trans_x, evecs_trans_y = evecs_trans_x[None], evecs_trans_y[None]
+            evals_x, evals_y = evals_x[None], evals_y[None]
+        A = torch.bmm(evecs_trans_x, feat_x)
+        Bm = torch.bmm(evecs_trans_y, feat_y)
+        with torch.no_grad():  # per-crop get_mask (:171-176), batched
+            D = get_mask_batched(evals_x.flatten(1), evals_y.flatten(1), self.resolvant_gamma)
+        A_t = A.transpose(1, 2)
+        return ops.fmap_solve(torch.bmm(A, A_t), torch.bmm(Bm, A_t), D, self.lambda_)

@@ -118,14 +118,18 @@ def backproject(depth: torch.Tensor, mask: torch.Tensor, K: torch.Tensor, cam_sc
     count = torch.empty((F,), dtype=torch.int64, device=dev)
     off = torch.empty((F + 1,), dtype=torch.int64, device=dev)
     xyz = torch.empty((cap, 3), dtype=torch.float64, device=dev)
+    pix = torch.empty((cap,), dtype=torch.int32, device=dev)
+    idxmap = torch.empty((F, H, W), dtype=torch.int32, device=dev)
     call("pk_backproject", ptr(depth), ptr(mask), F, H, W, ptr(K), ptr(cam_scale), ptr(rowcnt), ptr(rowoff),
-         ptr(count), ptr(off), ptr(xyz), int(cap), _lib.stream(dev))
-    return dict(xyz=xyz, count=count, off=off)
+         ptr(count), ptr(off), ptr(xyz), int(cap), ptr(pix), ptr(idxmap), _lib.stream(dev))
+    return dict(xyz=xyz, count=count, off=off, pix=pix, idxmap=idxmap)
 
 
 def sor(xyz: torch.Tensor, off: torch.Tensor, nmax: int, knn: int = 20, std_ratio: float = 0.3,
-        want64: bool = True, want32: bool = True, want_idx: bool = False) -> dict:
-    """remove_outliers for B packed crops (pk_sor). Survivors are packed by out_off."""
+        want64: bool = True, want32: bool = True, want_idx: bool = False, pix: Optional[torch.Tensor] = None,
+        idxmap: Optional[torch.Tensor] = None) -> dict:
+    """remove_outliers for B packed crops (pk_sor). Survivors are packed by out_off.
+    pix/idxmap (from backproject) enable the exact pixel-window kNN bound."""
     B = off.numel() - 1
     dev = xyz.device
     T = xyz.shape[0]
@@ -139,7 +143,10 @@ def sor(xyz: torch.Tensor, off: torch.Tensor, nmax: int, knn: int = 20, std_rati
     out64 = torch.empty((T, 3), dtype=torch.float64, device=dev) if want64 else None
     out32 = torch.empty((T, 3), dtype=torch.float32, device=dev) if want32 else None
     kidx = torch.empty((T,), dtype=torch.int64, device=dev) if want_idx else None
-    call("pk_sor", ptr(xyz), ptr(off), B, int(nmax), int(knn), float(std_ratio), ptr(avg), ptr(thr), ptr(ccount),
+    H = idxmap.shape[1] if idxmap is not None else 0
+    W = idxmap.shape[2] if idxmap is not None else 0
+    call("pk_sor", ptr(xyz), ptr(off), B, int(nmax), int(knn), float(std_ratio), ptr(pix), ptr(idxmap), H, W,
+         ptr(avg), ptr(thr), ptr(ccount),
          ptr(coff), ptr(kept), ptr(out_off), ptr(out64), ptr(out32), ptr(kidx), _lib.stream(dev))
     return dict(avg=avg, thr=thr, kept=kept, off=out_off, xyz64=out64, xyz32=out32, kept_idx=kidx)
 
@@ -172,3 +179,206 @@ def gather_transform(pcd: torch.Tensor, off: torch.Tensor, idx: Optional[torch.T
     call("pk_gather_transform", ptr(pcd), ptr(off), B, ptr(idx), int(idx_stride), ptr(npoint), int(npmax),
          ptr(out_off), ptr(R), ptr(t), ptr(sel64), ptr(align), ptr(sel32), _lib.stream(dev))
     return dict(sel64=sel64, align=align, sel32=sel32)
+
+
+# ------------------------------------------------------------------------------ H7 spectral diffusion
+
+
+class _SpectralDiffusion(torch.autograd.Function):
+    """x_diffuse = Phi (exp(-lambda t) ⊙ (Phi^T (mass ⊙ x))) — pk_spectral_diffusion fwd/bwd.
+    Gradients flow to x and t (the operators are data, as in the reference)."""
+
+    @staticmethod
+    def forward(ctx, x, mass, evals, evecs, t):
+        B, N, C = x.shape
+        K = evecs.shape[-1]
+        dev = x.device
+        x = x.contiguous()
+        S = (N + 63) // 64
+        work = torch.empty((B, S, K, C), dtype=torch.float32, device=dev)
+        spec = torch.empty((B, K, C), dtype=torch.float32, device=dev)
+        scaled = torch.empty_like(spec)
+        out = torch.empty_like(x)
+        call("pk_spectral_diffusion", ptr(x), ptr(mass), ptr(evecs), ptr(evals), ptr(t), B, N, K, C, 0,
+             ptr(work), ptr(spec), ptr(scaled), None, None, ptr(out), _lib.stream(dev))
+        ctx.save_for_backward(mass, evals, evecs, t, spec)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        mass, evals, evecs, t, spec = ctx.saved_tensors
+        g = g.contiguous()
+        B, N, C = g.shape
+        K = evecs.shape[-1]
+        dev = g.device
+        S = (N + 63) // 64
+        work = torch.empty((B, S, K, C), dtype=torch.float32, device=dev)
+        scaled = torch.empty((B, K, C), dtype=torch.float32, device=dev)
+        gt = torch.empty((B, C), dtype=torch.float32, device=dev)
+        gx = torch.empty_like(g)
+        call("pk_spectral_diffusion", ptr(g), ptr(mass), ptr(evecs), ptr(evals), ptr(t), B, N, K, C, 1,
+             ptr(work), None, ptr(scaled), ptr(spec), ptr(gt), ptr(gx), _lib.stream(dev))
+        return gx, None, None, None, gt.sum(0)
+
+
+def spectral_diffusion(x, mass, evals, evecs, t):
+    """x [B,N,64] f32, mass [B,N], evals [B,64], evecs [B,N,64], t [64] -> [B,N,64]."""
+    if x.shape[-1] != 64 or evecs.shape[-1] != 64:
+        raise _lib.PoseKernError("spectral diffusion kernel is built for C_width = k_eig = 64")
+    return _SpectralDiffusion.apply(x, mass.contiguous(), evals.contiguous(), evecs.contiguous(), t.contiguous())
+
+
+# ------------------------------------------------------------------------------ H9 fmap solve
+
+
+class _FmapSolve(torch.autograd.Function):
+    """C[b, i, :] = (AAt_b + lambda diag(D_b[i])) ^-1 (BAt_b)[i, :]  (pk_fmap_solve[_backward])."""
+
+    @staticmethod
+    def forward(ctx, AAt, BAt, D, lambda_):
+        AAt, BAt, D = AAt.contiguous(), BAt.contiguous(), D.contiguous()
+        B, K, _ = AAt.shape
+        C = torch.empty_like(BAt)
+        call("pk_fmap_solve", ptr(AAt), ptr(BAt), ptr(D), float(lambda_), B, K, ptr(C), _lib.stream(AAt.device))
+        ctx.save_for_backward(AAt, BAt, D)
+        ctx.lambda_ = float(lambda_)
+        return C
+
+    @staticmethod
+    def backward(ctx, G):
+        AAt, BAt, D = ctx.saved_tensors
+        G = G.contiguous()
+        B, K, _ = AAt.shape
+        dBAt = torch.empty_like(BAt)
+        part = torch.empty((B, K, K, K), dtype=torch.float32, device=AAt.device)
+        call("pk_fmap_solve_backward", ptr(AAt), ptr(BAt), ptr(D), ctx.lambda_, B, K, ptr(G), ptr(dBAt), ptr(part),
+             _lib.stream(AAt.device))
+        return part.sum(1), dBAt, None, None
+
+
+def fmap_solve(AAt: torch.Tensor, BAt: torch.Tensor, D: torch.Tensor, lambda_: float) -> torch.Tensor:
+    if AAt.shape[-1] != 30:
+        raise _lib.PoseKernError("fmap solve kernel is built for n_fmap = 30")
+    return _FmapSolve.apply(AAt, BAt, D, lambda_)
+
+
+# ------------------------------------------------------------------------------ H8 attention
+
+
+def attention(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor) -> torch.Tensor:
+    """softmax(q^T k / sqrt(d)) v for [B, d, heads, N] tensors (modeling/dpfm.py:29-37)."""
+    dim = query.shape[1]
+    scores = torch.einsum("bdhn,bdhm->bhnm", query, key) / dim ** 0.5
+    prob = torch.nn.functional.softmax(scores, dim=-1)
+    return torch.einsum("bhnm,bdhm->bdhn", prob, value)
+
+
+# ------------------------------------------------------------------------------ H10-H13, H15
+
+
+def feat_dist_topk(evecs_x: torch.Tensor, C: torch.Tensor, evecs_y: torch.Tensor, n1: torch.Tensor,
+                   n2: torch.Tensor, topk: int, want_dist: bool = False):
+    """Nearest CAD rows of every crop point in the spectral embedding (pk_feat_dist_topk).
+    evecs_x [B,V1,K>=30], C [B,30,30], evecs_y [B,V2,K>=30], n1/n2 int32 [B]."""
+    B, V1, ldx = evecs_x.shape
+    _, V2, ldy = evecs_y.shape
+    dev = evecs_x.device
+    A = torch.empty((B, V1, 32), dtype=torch.float32, device=dev)
+    Bq = torch.empty((B, V2, 32), dtype=torch.float32, device=dev)
+    idx = torch.empty((B, V2, topk), dtype=torch.int64, device=dev)
+    dist = torch.empty((B, V2, topk), dtype=torch.float32, device=dev) if want_dist else None
+    call("pk_feat_dist_topk", ptr(evecs_x.contiguous()), ldx, ptr(C.contiguous()), ptr(evecs_y.contiguous()), ldy,
+         ptr(n1), ptr(n2), B, V1, V2, int(topk), ptr(A), ptr(Bq), ptr(idx), ptr(dist), _lib.stream(dev))
+    return idx, dist
+
+
+def rigidity_thresholds(diam: Sequence[float], device) -> torch.Tensor:
+    """f32 [B,4]: float32(tau * diam) for tau = 0.3, 0.15, 0.055, 0.065 (Python-float
+    products, as the reference compares with `tau * diam_cad`)."""
+    rows = [[np.float32(t * float(d)) for t in (0.3, 0.15, 0.055, 0.065)] for d in diam]
+    return torch.tensor(np.asarray(rows, dtype=np.float32), device=device)
+
+
+def rigidity_filter(cand: torch.Tensor, ncand: torch.Tensor, cad: torch.Tensor, pc: torch.Tensor,
+                    thr4: torch.Tensor):
+    """cand int64 [B,L,2] -> (survivor rows int64 [B,L], count int32 [B])."""
+    B, L, _ = cand.shape
+    dev = cand.device
+    la = torch.zeros((B, L), dtype=torch.int64, device=dev)
+    lb = torch.zeros((B, L), dtype=torch.int64, device=dev)  # tail rows stay valid indices (0)
+    na = torch.empty((B,), dtype=torch.int32, device=dev)
+    nb = torch.empty((B,), dtype=torch.int32, device=dev)
+    score = torch.empty((B, L), dtype=torch.float32, device=dev)
+    call("pk_rigidity_filter", ptr(cand.contiguous()), L, ptr(ncand), ptr(cad.contiguous()), cad.shape[1],
+         ptr(pc.contiguous()), pc.shape[1], ptr(thr4), B, L, ptr(la), ptr(lb), ptr(na), ptr(nb), ptr(score),
+         _lib.stream(dev))
+    return lb, nb
+
+
+def inlier_ratio(pairs: torch.Tensor, npairs: torch.Tensor, cad: torch.Tensor, pc_aligned: torch.Tensor,
+                 thr: torch.Tensor, layout: int = 0) -> torch.Tensor:
+    B = cad.shape[0]
+    ldp = pairs.shape[1] if layout == 0 else pairs.shape[2]
+    ir = torch.empty((B,), dtype=torch.float32, device=cad.device)
+    call("pk_inlier_ratio", ptr(pairs.contiguous()), ldp, int(layout), ptr(npairs), ptr(cad.contiguous()),
+         cad.shape[1], ptr(pc_aligned.contiguous()), pc_aligned.shape[1], ptr(thr), B, ptr(ir),
+         _lib.stream(cad.device))
+    return ir
+
+
+def cgt_lstsq(pairs: torch.Tensor, npairs: torch.Tensor, evecs1: torch.Tensor, evecs2: torch.Tensor) -> torch.Tensor:
+    B, L, _ = pairs.shape
+    out = torch.empty((B, 30, 30), dtype=torch.float32, device=pairs.device)
+    work = torch.empty((B * max(1, (L + 255) // 256) * 1800,), dtype=torch.float64, device=pairs.device)
+    call("pk_cgt_lstsq", ptr(pairs.contiguous()), L, ptr(npairs), ptr(evecs1.contiguous()), evecs1.shape[2],
+         evecs1.shape[1], ptr(evecs2.contiguous()), evecs2.shape[2], evecs2.shape[1], B, 30, ptr(work), ptr(out),
+         _lib.stream(pairs.device))
+    return out
+
+
+def ransac(src: torch.Tensor, src_off: torch.Tensor, dst: torch.Tensor, dst_off: torch.Tensor,
+           corres: torch.Tensor, cor_off: torch.Tensor, H: int, seed: int = 0, max_dist: float = 0.05,
+           hyps: Optional[torch.Tensor] = None, hyp_off: Optional[torch.Tensor] = None):
+    """Batched RANSAC pose fit (pk_ransac). Returns (T f64 [B,4,4], stats f64 [B,3])."""
+    B = cor_off.numel() - 1
+    dev = src.device
+    nblk = max(1, (int(H) + 255) // 256)
+    bgood = torch.empty((B, nblk), dtype=torch.int32, device=dev)
+    brmse = torch.empty((B, nblk), dtype=torch.float64, device=dev)
+    bh = torch.empty((B, nblk), dtype=torch.int64, device=dev)
+    T = torch.empty((B, 4, 4), dtype=torch.float64, device=dev)
+    stats = torch.empty((B, 3), dtype=torch.float64, device=dev)
+    corres = corres.to(torch.int32).contiguous()
+    if corres.numel() == 0:  # every crop below ransac_n: keep a valid pointer, kernel returns identity
+        corres = torch.zeros((1, 2), dtype=torch.int32, device=dev)
+    call("pk_ransac", ptr(src), ptr(src_off), ptr(dst), ptr(dst_off), ptr(corres),
+         ptr(cor_off), ptr(hyps), ptr(hyp_off), ctypes_u64(seed), int(H), float(max_dist), B, ptr(bgood),
+         ptr(brmse), ptr(bh), ptr(T), ptr(stats), _lib.stream(dev))
+    return T, stats
+
+
+def pose_metrics(cad: torch.Tensor, off: torch.Tensor, nmax: int, T_est: torch.Tensor, T_gt: torch.Tensor):
+    """pk_pose_metrics -> f64 [B, 7] (ADD, xyz-direction means x3, ADD-S 1-D means x3)."""
+    B = off.numel() - 1
+    dev = cad.device
+    work = torch.empty((13 * B * max(nmax, 1),), dtype=torch.float64, device=dev)
+    out = torch.empty((B, 7), dtype=torch.float64, device=dev)
+    call("pk_pose_metrics", ptr(cad), ptr(off), B, int(nmax), ptr(T_est.contiguous()), ptr(T_gt.contiguous()),
+         ptr(work), ptr(out), _lib.stream(dev))
+    return out
+
+
+def erode_mask(mask: torch.Tensor) -> torch.Tensor:
+    F_, H, W = mask.shape
+    out = torch.empty_like(mask)
+    call("pk_erode_mask", ptr(mask.contiguous()), F_, H, W, ptr(out), _lib.stream(mask.device))
+    return out
+
+
+def sample_rgb(img: torch.Tensor, K: torch.Tensor, pts: torch.Tensor, off: torch.Tensor, nmax: int) -> torch.Tensor:
+    """H16: bilinear RGB at the projections of packed camera-frame points -> f32 [T, C]."""
+    F_, H, W, C = img.shape
+    out = torch.zeros((pts.shape[0], C), dtype=torch.float32, device=img.device)
+    call("pk_sample_rgb", ptr(img.contiguous()), F_, H, W, C, ptr(K), ptr(pts), ptr(off), int(nmax), ptr(out),
+         _lib.stream(img.device))
+    return out

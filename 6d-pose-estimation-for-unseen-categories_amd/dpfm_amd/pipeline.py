@@ -1,0 +1,188 @@
+"""The hot path end to end on the device: RGB-D frames -> crops -> DPFM fwd(+bwd) ->
+correspondences -> pose.
+
+  make_frame_batch   seeded synthetic frames / CAD / spectral operators resident in HBM
+  TrainStep          one iteration of scripts/train.py:88-124 for a batch of crops:
+                     model fwd, C_gt (utils/utils.py:67-79), DPFMLoss, the per-crop naive
+                     point map + inlier ratio (train.py:109-116), backward, gradient
+                     all-reduce across ranks (DDP semantics, one bucket), clip 5.0, RMSprop
+  InferStep          scripts/eval.py:57-119 + scripts/test_RANSAC.py:397-419 for a batch:
+                     model fwd, spatial-filtering solver, IR, RANSAC pose, pose metrics
+Nothing here synchronises with the host; callers decide when to read results.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import ops
+from .dataset.object import CropFormation, Crops, FrameBatch
+from .dataset.synthetic import cad_points, lbo_operators, make_frame
+from .models.dpfm import DPFMNet
+from .utils.loss import DPFMLoss
+
+
+@dataclass
+class Operators:
+    """Cached spectral operators (the reference's CAD_LBO / pc_LBO npz caches)."""
+    cad_mass: torch.Tensor   # f32 [F, N1]
+    cad_evals: torch.Tensor  # f32 [F, 64]
+    cad_evecs: torch.Tensor  # f32 [F, N1, 64]
+    cad_xyz: torch.Tensor    # f32 [F, N1, 3]
+    pc_mass: torch.Tensor    # f32 [F, N2]
+    pc_evals: torch.Tensor   # f32 [F, 64]
+    pc_evecs: torch.Tensor   # f32 [F, N2, 64]
+    ir_thr: torch.Tensor     # f32 [F] 0.1 * diam (train.py:115)
+    rig_thr: torch.Tensor    # f32 [F, 4] spatial-filter thresholds
+
+
+def make_frame_batch(F: int, n1: int, n2: int, seed: int, device) -> tuple[FrameBatch, Operators]:
+    depth, mask, rgb, K, cs, R, t, cad, diam = [], [], [], [], [], [], [], [], []
+    ops_c, ops_p = [], []
+    maxpix = 0
+    for f in range(F):
+        fr = make_frame(seed + f)
+        depth.append(fr.depth.view(np.int16))
+        mask.append(fr.mask)
+        rgb.append(fr.rgb)
+        K.append(fr.K.reshape(9))
+        cs.append(np.float32(1000.0 / fr.depth_scale))
+        R.append(fr.R_m2c.reshape(9))
+        t.append(fr.t_m2c)
+        cad.append(cad_points(fr, n1, seed + f))
+        diam.append(fr.diam_cad)
+        maxpix = max(maxpix, int((fr.mask == 255).sum()))
+        ops_c.append(lbo_operators(n1, 64, 2 * (seed + f)))
+        ops_p.append(lbo_operators(n2, 64, 2 * (seed + f) + 1))
+    d = torch.device(device)
+    T = lambda a, dt=None: torch.as_tensor(np.stack(a), device=d) if dt is None else torch.as_tensor(np.stack(a), dtype=dt, device=d)  # noqa: E731
+    fb = FrameBatch(depth=T(depth), mask=T(mask), rgb=T(rgb), K=T(K, torch.float64), cam_scale=T(cs, torch.float32),
+                    R=T(R, torch.float64), t=T(t, torch.float64),
+                    cad64=torch.as_tensor(np.concatenate(cad, 0), dtype=torch.float64, device=d),
+                    cad_off=ops.packed_offsets([n1] * F, d), diam=diam, max_pixels=maxpix,
+                    thr2=torch.tensor([ops.ball_threshold(0.05 * x) for x in diam], dtype=torch.float64, device=d))
+    op = Operators(cad_mass=T([o[0] for o in ops_c]), cad_evals=T([o[1] for o in ops_c]),
+                   cad_evecs=T([o[2] for o in ops_c]), cad_xyz=T([c.astype(np.float32) for c in cad]),
+                   pc_mass=T([o[0] for o in ops_p]), pc_evals=T([o[1] for o in ops_p]),
+                   pc_evecs=T([o[2] for o in ops_p]),
+                   ir_thr=torch.tensor([np.float32(0.1 * x) for x in diam], dtype=torch.float32, device=d),
+                   rig_thr=ops.rigidity_thresholds(diam, d))
+    return fb, op
+
+
+def model_batch(op: Operators, crops: Crops) -> dict:
+    """The {"shape1": CAD, "shape2": PC} dict of train.py:88-91 (L/grad operators None)."""
+    cad = {"xyz": op.cad_xyz, "mass": op.cad_mass, "evals": op.cad_evals, "evecs": op.cad_evecs,
+           "L": None, "gradX": None, "gradY": None, "faces": None}
+    pc = {"xyz": crops.pc32, "mass": op.pc_mass, "evals": op.pc_evals, "evecs": op.pc_evecs,
+          "L": None, "gradX": None, "gradY": None}
+    return {"shape1": cad, "shape2": pc}
+
+
+def naive_p2p_batched(C: torch.Tensor, evecs_x: torch.Tensor, evecs_y: torch.Tensor) -> torch.Tensor:
+    """naive_fmap2pointmap for every crop: int64 [B, 2, V2] (row 0 CAD idx, row 1 arange)."""
+    B, V1, _ = evecs_x.shape
+    V2 = evecs_y.shape[1]
+    dev = C.device
+    n1 = torch.full((B,), V1, dtype=torch.int32, device=dev)
+    n2 = torch.full((B,), V2, dtype=torch.int32, device=dev)
+    idx, _ = ops.feat_dist_topk(evecs_x, C, evecs_y, n1, n2, 1)
+    ar = torch.arange(V2, device=dev, dtype=torch.int64)[None].expand(B, V2)
+    return torch.stack([idx[..., 0], ar], 1)
+
+
+class TrainStep:
+    """One training iteration (scripts/train.py:88-124) for a batch of crops."""
+
+    def __init__(self, model: DPFMNet, lr: float = 5e-4, max_norm: float = 5.0, nce_num_pairs: int = 512,
+                 group: Optional[dist.ProcessGroup] = None, seed: int = 0):
+        self.model = model
+        self.params = [p for p in model.parameters()]
+        self.opt = torch.optim.RMSprop(self.params, lr=lr)  # config/dpfm_orig.gin:62-63
+        self.crit = DPFMLoss(w_fmap=1, w_acc=1, w_nce=1, nce_t=0.07, nce_num_pairs=nce_num_pairs)  # gin:54-58
+        self.max_norm = max_norm
+        self.group = group
+        self.world = dist.get_world_size(group) if (group is not None or dist.is_initialized()) else 1
+        dev = self.params[0].device
+        self.gen = torch.Generator(device=dev)
+        self.gen.manual_seed(seed)
+        self.flat = torch.zeros(sum(p.numel() for p in self.params), dtype=torch.float32, device=dev)
+
+    def allreduce_grads(self):
+        """DDP's gradient averaging in one bucket (49,281 f32 = 197 KB: latency-bound)."""
+        if self.world <= 1:
+            return
+        o = 0
+        for p in self.params:
+            n = p.numel()
+            self.flat[o:o + n].copy_(p.grad.reshape(-1))
+            o += n
+        dist.all_reduce(self.flat, group=self.group)
+        self.flat.div_(self.world)
+        o = 0
+        for p in self.params:
+            n = p.numel()
+            p.grad.copy_(self.flat[o:o + n].view_as(p.grad))
+            o += n
+
+    def __call__(self, op: Operators, crops: Crops):
+        self.model.train()
+        batch = model_batch(op, crops)
+        C_pred, o12, o21, f1, f2, _, _ = self.model(batch)
+        with torch.no_grad():
+            C_gt = ops.cgt_lstsq(crops.pairs, crops.npairs, op.cad_evecs, op.pc_evecs)
+        loss, log = self.crit.forward_batched(C_pred, C_gt, crops.pairs, crops.npairs, f1, f2, o12, o21,
+                                              crops.overlap_12, crops.overlap_21, generator=self.gen)
+        with torch.no_grad():  # train.py:109-116 (naive solver + IR per crop)
+            p_pred = naive_p2p_batched(C_pred.detach(), op.cad_evecs, op.pc_evecs)
+            npred = torch.full((p_pred.shape[0],), p_pred.shape[2], dtype=torch.int32, device=p_pred.device)
+            ir = ops.inlier_ratio(p_pred, npred, op.cad_xyz, crops.align32, op.ir_thr, layout=1).mean()
+        loss.backward()
+        self.allreduce_grads()
+        torch.nn.utils.clip_grad_norm_(self.params, max_norm=self.max_norm, norm_type=2)
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=False)
+        log["IR"] = ir
+        return log
+
+
+class InferStep:
+    """eval.py inference + test_RANSAC.py pose fit for a batch of crops."""
+
+    def __init__(self, model: DPFMNet, hypotheses: int = 1024, seed: int = 0, max_dist: float = 0.05):
+        self.model, self.H, self.seed, self.max_dist = model, hypotheses, seed, max_dist
+
+    @torch.no_grad()
+    def __call__(self, fb: FrameBatch, op: Operators, crops: Crops):
+        self.model.eval()
+        C_pred, o12, o21, f1, f2, _, _ = self.model(model_batch(op, crops))
+        B, V1, _ = op.cad_evecs.shape
+        V2 = op.pc_evecs.shape[1]
+        dev = C_pred.device
+        n1 = torch.full((B,), V1, dtype=torch.int32, device=dev)
+        n2 = torch.full((B,), V2, dtype=torch.int32, device=dev)
+        top, _ = ops.feat_dist_topk(op.cad_evecs, C_pred, op.pc_evecs, n1, n2, 5)      # spacial_filtering.py:32-38
+        cand = torch.stack([top.reshape(B, -1),
+                            torch.arange(V2, device=dev)[None, :, None].expand(B, V2, 5).reshape(B, -1)], -1)
+        ncand = torch.full((B,), 5 * V2, dtype=torch.int32, device=dev)
+        rows, nsurv = ops.rigidity_filter(cand, ncand, op.cad_xyz, crops.pc32, op.rig_thr)  # :42-75
+        p_pred = torch.gather(cand, 1, rows[..., None].expand(-1, -1, 2))                  # [B, L, 2]
+        ir = ops.inlier_ratio(p_pred, nsurv, op.cad_xyz, crops.align32, op.ir_thr, layout=0)  # eval.py:89
+        # RANSAC on (CAD, crop in camera frame) with the surviving correspondences
+        cor_off = torch.zeros(B + 1, dtype=torch.int64, device=dev)
+        cor_off[1:] = torch.cumsum(nsurv.to(torch.int64), 0)
+        L = p_pred.shape[1]
+        valid = torch.arange(L, device=dev)[None] < nsurv[:, None]
+        corres = p_pred[valid].to(torch.int32)   # packed [sum n, 2] (device-side compaction)
+        T, stats = ops.ransac(fb.cad64, fb.cad_off, crops.pc64, crops.off, corres, cor_off, self.H, seed=self.seed,
+                              max_dist=self.max_dist)
+        T_gt = torch.zeros((B, 4, 4), dtype=torch.float64, device=dev)
+        T_gt[:, :3, :3] = fb.R.view(B, 3, 3)
+        T_gt[:, :3, 3] = fb.t
+        T_gt[:, 3, 3] = 1.0
+        metrics = ops.pose_metrics(fb.cad64, fb.cad_off, V1, T, T_gt)
+        return dict(C=C_pred, p_pred=p_pred, n_corr=nsurv, ir=ir, T=T, ransac=stats, metrics=metrics)

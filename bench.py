@@ -1,0 +1,271 @@
+"""Headline benchmark: RGB-D crops/sec (fwd+bwd), 1024-point crops, per BASELINE.json.
+
+One step = one training iteration of the reference (scripts/train.py:88-124) for a batch
+of B synthetic 640x480 RGB-D frames, with the dataset's crop formation on the device:
+  back-projection + erosion -> SOR kNN-20 -> FPS to 1024 -> align transform -> ball
+  query (P, overlaps) -> RGB at the crop points -> DPFMNet fwd -> C_gt + DPFMLoss ->
+  naive point map + inlier ratio -> backward -> grad all-reduce (N > 1) -> clip -> RMSprop.
+Inputs (frames, CAD models, cached spectral operators) are resident in HBM before timing.
+
+  python bench.py [--gpus N --steps K --warmup W --batch B]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+Rank 0 prints one JSON line (contract in the task statement / DESIGN.md §Measurement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.join(ROOT, "6d-pose-estimation-for-unseen-categories_amd")
+for _p in (ROOT, PKG_ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="crops per GPU (configs[1]: 32)")
+    ap.add_argument("--points", type=int, default=1024)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-crops", type=int, default=2, help="bounded CPU-baseline sample (crops)")
+    ap.add_argument("--no-roofline-probe", action="store_true")
+    return ap.parse_args()
+
+
+class KernelProbe:
+    """HIP events around every libposekern call issued inside the timed region (same
+    stream as the kernels: torch's current stream)."""
+
+    def __init__(self):
+        self.ev = {}
+
+    def hook(self, name, fn):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        r = fn()
+        e.record()
+        self.ev.setdefault(name, []).append((s, e))
+        return r
+
+    def summary(self):
+        out = {}
+        for k, lst in self.ev.items():
+            ms = [s.elapsed_time(e) for s, e in lst]
+            out[k] = (float(np.mean(ms)), len(ms), float(np.sum(ms)))
+        return out
+
+
+def ball_query_roofline(dev, probe_launches: int = 10) -> dict:
+    """pk_ball_query_mask at configs[3] size (B=256 crops, 2048 x 2048): >= 1 GB per launch."""
+    from dpfm_amd import ops
+    from dpfm_amd._lib import call, ptr, stream
+    B, N = 256, 2048
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    cad = torch.randn((B * N, 3), dtype=torch.float64, device=dev, generator=g) * 5
+    pc = torch.randn((B * N, 3), dtype=torch.float64, device=dev, generator=g) * 5
+    off = ops.packed_offsets([N] * B, dev)
+    thr = torch.full((B,), ops.ball_threshold(0.6), dtype=torch.float64, device=dev)
+    mask = torch.empty((B, N, N), dtype=torch.uint8, device=dev)
+    rc = torch.empty((B, N), dtype=torch.int32, device=dev)
+    f = lambda: call("pk_ball_query_mask", ptr(cad), ptr(off), ptr(pc), ptr(off), ptr(thr), B, N, N, ptr(mask), N,  # noqa
+                     ptr(rc), stream(dev))
+    for _ in range(3):
+        f()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(probe_launches):
+        f()
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / probe_launches
+    byts = B * (24 * N + 24 * N + N * N) + B * N * 4  # coords in + mask + row counts
+    ach = byts / (ms * 1e-3) / 1e9
+    return {"kernel": "pk_ball_query_mask (configs[3]: 256 x 2048 x 2048)", "bound": "hbm", "achieved": round(ach, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "ms_per_launch": round(ms, 4), "bytes_per_launch": byts}
+
+
+def cpu_baseline(n_crops: int, n1: int, n2: int) -> dict:
+    """The oracle (reference CPU path restated: numpy / torch-CPU) on the same synthetic
+    inputs: crop formation + DPFM fwd+bwd + loss + naive IR + RMSprop, per crop."""
+    from oracle import dpfm_oracle as O
+    from oracle import dpfm_model_oracle as M
+    from dpfm_amd.dataset.synthetic import make_frame, cad_points, lbo_operators
+    threads = len(os.sched_getaffinity(0))
+    torch.set_num_threads(threads)
+    model = M.DPFMNet()
+    opt = torch.optim.RMSprop(model.parameters(), lr=5e-4)
+    rng = np.random.default_rng(0)
+    t0 = time.perf_counter()
+    for c in range(n_crops):
+        fr = make_frame(10_000 + c)
+        pcd = O.dpt_2_pcld(fr.depth, 1000 / fr.depth_scale, fr.K, fr.mask == 255)
+        pcd = O.remove_outliers(pcd)
+        idx = O.farthest_point_sample(torch.Tensor(pcd).t(), ratio=n2 / pcd.shape[0], start=0, npoint=n2)
+        pcd = pcd[idx.numpy()]
+        align = O.transform(pcd, fr.R_m2c, fr.t_m2c, inv=True)
+        cad = cad_points(fr, n1, c)
+        P = O.find_positives(cad, align, r=fr.diam_cad * 0.05)
+        o12, o21 = O.get_overlap(n1, n2, P)
+        cm, ce, cv = lbo_operators(n1, 64, 2 * c)
+        pm, pe, pv = lbo_operators(n2, 64, 2 * c + 1)
+        T = lambda a: torch.from_numpy(np.asarray(a, dtype=np.float32))[None]  # noqa: E731
+        batch = {"shape1": {"xyz": T(cad), "mass": T(cm), "evals": T(ce), "evecs": T(cv)},
+                 "shape2": {"xyz": T(pcd), "mass": T(pm), "evals": T(pe), "evecs": T(pv)}}
+        C, s12, s21, f1, f2, _, _ = model(batch)
+        C_gt = M.C_from_sparse_P(torch.from_numpy(P), batch["shape1"]["evecs"][0, :, :30],
+                                 batch["shape2"]["evecs"][0, :, :30])[None]
+        sel = [torch.from_numpy(M.nce_selection(P.shape[0], 512, rng))]
+        loss = M.dpfm_loss(C, C_gt, [torch.from_numpy(P)], sel, f1, f2, s12, s21, T(o12), T(o21))
+        with torch.no_grad():
+            p2p = O.naive_fmap2pointmap(C[0].detach(), batch["shape1"]["evecs"][0, :, :30],
+                                        batch["shape2"]["evecs"][0, :, :30])
+            O.compute_inlier_ratio(p2p.t(), T(cad)[0], T(align)[0], 0.1 * fr.diam_cad)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 5.0)
+        opt.step()
+        opt.zero_grad()
+    dt = time.perf_counter() - t0
+    import platform
+    model_name = platform.processor()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model_name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(n_crops / dt, 4), "unit": "crops/s (fwd+bwd incl. crop formation)", "cores": threads,
+            "kind": "port",
+            "sample": f"{n_crops} crops, {n2} pts, CAD {n1}; oracle/ (numpy + torch-CPU fp32) on {model_name}",
+            "seconds": round(dt, 2)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from dpfm_amd import _lib
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import TrainStep, make_frame_batch
+
+    B, N = args.batch, args.points
+    torch.manual_seed(1234)  # identical initial weights on every rank (DDP broadcast semantics)
+    model = DPFMNet().to(dev)
+    fb, op = make_frame_batch(B, N, N, seed=1000 * rank, device=dev)
+    crops_of = CropFormation(n1=N, npoint=N, seed=rank)
+    step = TrainStep(model, seed=rank)
+
+    def one_step():
+        crops = crops_of(fb)
+        return step(op, crops)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    probe = KernelProbe()
+    _lib.set_probe(probe.hook)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        log = one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    _lib.set_probe(None)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern = probe.summary()
+    loss_v, ir_v = float(log["loss"]), float(log["IR"])
+
+    if rank == 0:
+        total_ms = elapsed * 1e3 / args.steps
+        # dominant kernel family by total device time inside the timed region
+        dom = max(kern.items(), key=lambda kv: kv[1][2])
+        kernels = {k: {"avg_ms": round(v[0], 4), "launches": v[1], "ms_per_step": round(v[2] / args.steps, 4)}
+                   for k, v in sorted(kern.items(), key=lambda kv: -kv[1][2])}
+        roof = roofline_for(dom[0], dom[1][0], B, N)
+        out = {
+            "metric": "RGB-D crops/sec (fwd+bwd), 1024 pts, at 1/2/4/8 MI355X; pose err vs ref",
+            "value": round(B * world / elapsed * args.steps, 3),
+            "unit": "crops/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(total_ms, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32 (fp64 crop geometry)", "data": "synthetic (seeded ellipsoid RGB-D frames, random-init DPFM)",
+            "config": {"workload": "configs[1] shape: B=32 synthetic 640x480 RGB-D crops/GPU, 1024 pts, "
+                                   "training step fwd+bwd (configs[2] semantics, DDP over RCCL when N>1)",
+                       "global_batch": B * world, "points_per_crop": N, "cad_points": N,
+                       "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "kernels": kernels,
+            "loss": round(loss_v, 5), "ir": round(ir_v, 5),
+        }
+        if not args.no_roofline_probe and world == 1:
+            out["roofline_ball_query"] = ball_query_roofline(dev)
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_crops, N, N)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def roofline_for(name: str, avg_ms: float, B: int, N: int) -> dict:
+    """Algorithmic work per launch of the dominant kernel family."""
+    if name == "pk_fps":
+        # LDS/latency-bound sequential kernel: report the HBM stream it needs (xyz in, idx out)
+        n_in = 4000
+        byts = B * (12 * n_in + 8 * N)
+        ach = byts / (avg_ms * 1e-3) / 1e9
+        return {"kernel": name, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None, "avg_ms": round(avg_ms, 4),
+                "note": "sequential npoint-step argmax; latency-bound, HBM fraction is not its limiter"}
+    if name == "pk_feat_dist_topk":
+        flops = B * 2.0 * N * N * 32
+        ach = flops / (avg_ms * 1e-3) / 1e12
+        return {"kernel": name, "bound": "mfma", "achieved": round(ach, 3), "peak": F32_MFMA_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / F32_MFMA_TFLOPS, 4), "traffic": None, "avg_ms": round(avg_ms, 4)}
+    if name in ("pk_ball_query_mask",):
+        byts = B * (48 * N + N * N + 4 * N)
+        ach = byts / (avg_ms * 1e-3) / 1e9
+        return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_ms": round(avg_ms, 4)}
+    return {"kernel": name, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+            "traffic": None, "avg_ms": round(avg_ms, 4)}
+
+
+if __name__ == "__main__":
+    main()

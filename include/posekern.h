@@ -65,22 +65,28 @@ int pk_ball_query_pairs(const double* cad, const int64_t* cad_off, const double*
  *   rowcnt int32 [F,H], rowoff int64 [F,H] scratch
  *   count int64 [F] points per frame, off int64 [F+1] packed offsets
  *   xyz f64 [cap,3] packed back-projected points in cm, row-major pixel order.
+ *   pix int32 [cap] (may be NULL): v*W+u of each point; idxmap int32 [F,H,W] (may be
+ *   NULL): point index within its frame, -1 for pixels that are not points.
  * Bit-exact vs numpy: z32 = f32(depth)/f32(cam_scale); X = (((u-cx)*z)/fx)*100. */
 int pk_backproject(const uint16_t* depth, const uint8_t* mask, int F, int H, int W,
                    const double* K, const float* cam_scale, int32_t* rowcnt, int64_t* rowoff,
-                   int64_t* count, int64_t* off, double* xyz, int64_t cap, void* stream);
+                   int64_t* count, int64_t* off, double* xyz, int64_t cap, int32_t* pix,
+                   int32_t* idxmap, void* stream);
 
 /* H2 statistical outlier removal. Replaces dataset/object.py:33-50 remove_outliers
  * (Open3D RemoveStatisticalOutliers(nb_neighbors=20, std_ratio=0.3)).
  *   xyz f64 [T,3] packed / off, knn <= 20
+ *   pix / idxmap (optional, from pk_backproject, crop b = frame b): an exact kNN bound
+ *   from the 5x5 pixel window prunes the brute-force scan (results unchanged)
  *   avg f64 [T] mean kNN distance, thr f64 [B] keep threshold
  *   ccount int32 [B, ceil(nmax/1024)], coff int64 (same shape) scratch
  *   kept int64 [B] survivors, out_off int64 [B+1] their packed offsets
  *   out64 f64 [T,3], out32 f32 [T,3] (either may be NULL) survivors in input order
  *   kept_idx int64 [T] (may be NULL) survivor index within its input crop */
 int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, int knn, double std_ratio,
-           double* avg, double* thr, int32_t* ccount, int64_t* coff, int64_t* kept,
-           int64_t* out_off, double* out64, float* out32, int64_t* kept_idx, void* stream);
+           const int32_t* pix, const int32_t* idxmap, int H, int W, double* avg, double* thr,
+           int32_t* ccount, int64_t* coff, int64_t* kept, int64_t* out_off, double* out64,
+           float* out32, int64_t* kept_idx, void* stream);
 
 /* FPS sample-count policy of dataset/object.py:145-147 on device counts (no host sync):
  * fixed > 0: npoint = fixed; else npoint = int(limit/n * n) if n > limit, else -n
@@ -102,6 +108,100 @@ int pk_gather_transform(const double* pcd, const int64_t* off, int B, const int6
  * and off[b+1] = off[b] + counts[b]. */
 int pk_segment_scan(const int32_t* cnt, int S, int n, int64_t* off, int64_t* total, void* stream);
 int pk_offsets_from_counts(const int64_t* counts, int B, int64_t* off, void* stream);
+
+/* H7 spectral diffusion of DiffusionNet's LearnedTimeDiffusion (upstream layers.py,
+ * models/dpfm.py:22-30), fp32, K = C = 64:
+ *   mode 0: out = Phi (E ⊙ raw), raw = Phi^T (mass ⊙ in), E[k,c] = exp(-evals_k t_c)
+ *   mode 1: out = mass ⊙ Phi (E ⊙ Phi^T in) (= dL/dx), gt[b,c] = -sum_k evals E saved (Phi^T in)
+ *   in/out [B,N,C], mass [B,N], evecs [B,N,K], evals [B,K], t [C]
+ *   work f32 [B, ceil(N/256), K, C]; raw (mode 0, may be NULL) / scaled [B,K,C];
+ *   saved = raw of the forward (mode 1); gt [B,C] (mode 1) */
+int pk_spectral_diffusion(const float* in, const float* mass, const float* evecs, const float* evals,
+                          const float* t, int B, int N, int K, int C, int mode, float* work,
+                          float* raw, float* scaled, const float* saved, float* gt, float* out,
+                          void* stream);
+
+/* H9 regularized fmap solve. Replaces the 30 sequential torch.inverse + bmm of
+ * modeling/dpfm.py:185-193: C[b,i,:] = ((AAt_b + lambda diag(D_b[i,:]))^-1 BAt_b[i,:]^T)^T.
+ * fp64 Gauss-Jordan with partial pivoting, one wave per (b, i). K must be 30.
+ *   AAt, BAt, D, C: f32 [B,K,K]. Backward: G = dL/dC; dBAt f32 [B,K,K];
+ *   dAAt_part f32 [B,K,K,K] per-row slabs -w_i x_i^T (dL/dAAt = sum over axis 1). */
+int pk_fmap_solve(const float* AAt, const float* BAt, const float* D, float lambda, int B, int K,
+                  float* C, void* stream);
+int pk_fmap_solve_backward(const float* AAt, const float* BAt, const float* D, float lambda, int B,
+                           int K, const float* G, float* dBAt, float* dAAt_part, void* stream);
+
+/* H10 / H11 correspondence head. Replaces fmap2pointmap_solvers/naive.py:20-34
+ * (topk = 1: dist.argmin(dim=-2)) and spacial_filtering.py:19-38 (topk = 5: the first 5
+ * rows of dist.sort(dim=-2)) with dist = cdist(evecs_x[:, :30] @ C^T, evecs_y[:, :30]).
+ *   evecs_x f32 [B,V1max,ldx] (first 30 columns used), C f32 [B,30,30],
+ *   evecs_y f32 [B,V2max,ldy]; n1/n2 int32 [B] valid rows
+ *   A f32 [B,V1max,32], Bq f32 [B,V2max,32] scratch (augmented cdist operands)
+ *   out_idx int64 [B,V2max,topk] ascending distance (ties: lower index); out_dist f32
+ *   [B,V2max,topk] Euclidean distances (may be NULL). fp32 MFMA, fused epilogue. */
+int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, const float* evecs_y, int ldy,
+                      const int32_t* n1, const int32_t* n2, int B, int V1max, int V2max, int topk,
+                      float* A, float* Bq, int64_t* out_idx, float* out_dist, void* stream);
+
+/* H11 rigidity filter (fmap2pointmap_solvers/spacial_filtering.py:42-75), three rounds
+ * on device with the 0.055 -> 0.065 fallback.
+ *   cand int64 [B,ldc,2] (cad idx, pc idx), ncand int32 [B]; cad f32 [B,ldcad,3],
+ *   pc f32 [B,ldpc,3]; thr4 f32 [B,4] = diam * (0.3, 0.15, 0.055, 0.065)
+ *   list_a/list_b int64 [B,ldc], n_a/n_b int32 [B], score f32 [B,ldc] scratch.
+ * Result: survivors' candidate rows in list_b[b, :n_b[b]] (input order). */
+int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* ncand, const float* cad, int ldcad,
+                       const float* pc, int ldpc, const float* thr4, int B, int nmax, int64_t* list_a,
+                       int64_t* list_b, int32_t* n_a, int32_t* n_b, float* score, void* stream);
+
+/* H12 inlier ratio (utils/utils.py:81-105) per crop: mean(||cad[c] - pc_aligned[p]|| < thr),
+ * 0 when there are no correspondences.
+ *   pairs int64: layout 0 [B,ldp,2] (cad, pc) or layout 1 [B,2,ldp]; npairs int32 [B]
+ *   cad f32 [B,ldcad,3], pc_aligned f32 [B,ldpc,3], thr f32 [B] -> ir f32 [B] */
+int pk_inlier_ratio(const int64_t* pairs, int ldp, int layout, const int32_t* npairs, const float* cad,
+                    int ldcad, const float* pc_aligned, int ldpc, const float* thr, int B, float* ir,
+                    void* stream);
+
+/* H15 C_gt (utils/utils.py:67-79 C_from_sparse_P): least squares
+ * evecs2[P[:,1], :30] X = evecs1[P[:,0], :30] per crop (fp64 normal equations,
+ * Gauss-Jordan with partial pivoting). pairs int64 [B,ldp,2], npairs int64 [B];
+ * evecs f32 [B,Vmax,ld]; K must be 30; work f64 [B * ceil(ldp/256) * 1800] partial
+ * sums (split over 256-pair slices, summed in slice order); Cgt f32 [B,30,30]. */
+int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs, const float* evecs1, int ld1,
+                 int V1max, const float* evecs2, int ld2, int V2max, int B, int K, double* work,
+                 float* Cgt, void* stream);
+
+/* H13 RANSAC + Umeyama (scripts/test_RANSAC.py:288-310, Open3D 0.17 semantics, ransac_n 4).
+ *   src f64 (CAD) / dst f64 (crop, camera frame) packed [T,3] with src_off/dst_off [B+1];
+ *   corres int32 [sum n_b, 2] (src row, dst row) packed by cor_off int64 [B+1]
+ *   hyps int32 [sum H_b, 4] correspondence rows (packed by hyp_off) or NULL: then draw j
+ *   of hypothesis h is splitmix64(seed ^ splitmix64(4h + j)) % n_b
+ *   H hypotheses per crop; inlier iff ||T s - d||^2 < max_dist^2
+ *   bgood int32 / brmse f64 / bh int64 [B, ceil(H/256)] scratch
+ *   T f64 [B,4,4] row-major best pose, stats f64 [B,3] (fitness, inlier rmse, best h). */
+int pk_ransac(const double* src, const int64_t* src_off, const double* dst, const int64_t* dst_off,
+              const int32_t* corres, const int64_t* cor_off, const int32_t* hyps, const int64_t* hyp_off,
+              uint64_t seed, int64_t H, double max_dist, int B, int* bgood, double* brmse, int64_t* bh,
+              double* T, double* stats, void* stream);
+
+/* H14 pose metrics of scripts/test_RANSAC.py:77-81, 154-238 for B crops:
+ *   cad f64 [T,3] packed / off (model points in the object frame), T_est / T_gt f64
+ *   [B,4,4] row-major; work f64 [13 * B * nmax] scratch
+ *   out f64 [B,7] = {ADD (add), mean per-row |.| x3 (compute_add_score's xyz-direction
+ *   distances), mean per-row 1-D nearest-GT distance x3 (compute_adds_score)} */
+int pk_pose_metrics(const double* cad, const int64_t* off, int B, int nmax, const double* T_est,
+                    const double* T_gt, double* work, double* out, void* stream);
+
+/* erode_seg_mask alone (dataset/object.py:52-71): plus-shaped 3x3 erosion of
+ * `mask == 255`, border pixels not eroded by the image edge. out uint8 [F,H,W] 0/1. */
+int pk_erode_mask(const uint8_t* mask, int F, int H, int W, uint8_t* out, void* stream);
+
+/* H16 RGB(-feature) sampling at projected 3D points (north-star row; the reference loads
+ * RGB only with color=True, dataset/scene.py:95-97, and never feeds it to the model).
+ * img uint8 [F,H,W,C]; pts f64 [T,3] camera-frame cm, packed per frame by off [F+1];
+ * bilinear at u = fx X/Z + cx, v = fy Y/Z + cy, zero outside the image
+ * (= grid_sample(align_corners=True, padding_mode="zeros")); out f32 [T,C] / 255. */
+int pk_sample_rgb(const uint8_t* img, int F, int H, int W, int C, const double* K, const double* pts,
+                  const int64_t* off, int nmax, float* out, void* stream);
 
 #ifdef __cplusplus
 }

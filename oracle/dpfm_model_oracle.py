@@ -1,0 +1,251 @@
+"""Literal torch-CPU restatement of the DPFM model and training step — TEST
+INFRASTRUCTURE ONLY (checker for dpfm_amd.models / dpfm_amd.utils, and bench.py's
+cpu_baseline leg).
+
+  DiffusionNet (upstream diffusion-net layers.py as vendored by DPFM),
+  built by models/dpfm.py:22-30 with C_in=3, C_out=32, C_width=64, N_block=2,
+  spectral diffusion, no gradient features, no dropout.
+  Refinement / overlap / fmap heads: modeling/dpfm.py:16-195.
+  Forward: models/dpfm.py:44-82. Loss: utils/loss.py:8-99 (+ upstream WeightedBCELoss).
+  Training-step: scripts/train.py:88-124. C_gt: utils/utils.py:67-79.
+
+Parameter names match weights/weights.pt exactly (38 tensors, 49,281 parameters).
+"""
+from __future__ import annotations
+
+from copy import deepcopy
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+# ---------------------------------------------------------------- DiffusionNet (upstream)
+class LearnedTimeDiffusion(nn.Module):
+    def __init__(self, C):
+        super().__init__()
+        self.C_inout = C
+        self.diffusion_time = nn.Parameter(torch.zeros(C))
+
+    def forward(self, x, mass, evals, evecs):
+        with torch.no_grad():
+            self.diffusion_time.data = torch.clamp(self.diffusion_time, min=1e-8)
+        x_spec = torch.matmul(evecs.transpose(-2, -1), x * mass.unsqueeze(-1))
+        coefs = torch.exp(-evals.unsqueeze(-1) * self.diffusion_time.unsqueeze(0))
+        return torch.matmul(evecs, coefs * x_spec)
+
+
+class MiniMLP(nn.Sequential):
+    def __init__(self, sizes, name="miniMLP"):
+        super().__init__()
+        for i in range(len(sizes) - 1):
+            self.add_module(f"{name}_mlp_layer_{i:03d}", nn.Linear(sizes[i], sizes[i + 1]))
+            if i + 2 != len(sizes):
+                self.add_module(f"{name}_mlp_act_{i:03d}", nn.ReLU())
+
+
+class DiffusionNetBlock(nn.Module):
+    def __init__(self, C):
+        super().__init__()
+        self.diffusion = LearnedTimeDiffusion(C)
+        self.mlp = MiniMLP([2 * C, C, C, C])
+
+    def forward(self, x, mass, evals, evecs):
+        xd = self.diffusion(x, mass, evals, evecs)
+        return self.mlp(torch.cat((x, xd), dim=-1)) + x
+
+
+class DiffusionNet(nn.Module):
+    def __init__(self, C_in=3, C_out=32, C_width=64, N_block=2):
+        super().__init__()
+        self.first_lin = nn.Linear(C_in, C_width)
+        self.last_lin = nn.Linear(C_width, C_out)
+        self.blocks = []
+        for i in range(N_block):
+            self.blocks.append(DiffusionNetBlock(C_width))
+            self.add_module(f"block_{i}", self.blocks[-1])
+
+    def forward(self, x, mass, evals, evecs):
+        squeeze = x.dim() == 2
+        if squeeze:
+            x, mass, evals, evecs = x[None], mass[None], evals[None], evecs[None]
+        h = self.first_lin(x)
+        for blk in self.blocks:
+            h = blk(h, mass, evals, evecs)
+        h = self.last_lin(h)
+        return h[0] if squeeze else h
+
+
+# ---------------------------------------------------------------- modeling/dpfm.py
+def conv_mlp(channels):
+    """modeling/dpfm.py:16-26 MLP: Conv1d(k=1) + InstanceNorm1d + ReLU between layers."""
+    layers = []
+    for i in range(1, len(channels)):
+        layers.append(nn.Conv1d(channels[i - 1], channels[i], kernel_size=1, bias=True))
+        if i < len(channels) - 1:
+            layers.append(nn.InstanceNorm1d(channels[i]))
+            layers.append(nn.ReLU())
+    return nn.Sequential(*layers)
+
+
+def attention(query, key, value):
+    """modeling/dpfm.py:29-37 (heads interleaved: tensors are [B, d, h, N])."""
+    dim = query.shape[1]
+    scores = torch.einsum("bdhn,bdhm->bhnm", query, key) / dim ** 0.5
+    prob = torch.nn.functional.softmax(scores, dim=-1)
+    return torch.einsum("bhnm,bdhm->bdhn", prob, value), prob
+
+
+class MultiHeadedAttention(nn.Module):
+    def __init__(self, num_heads, d_model):
+        super().__init__()
+        self.dim = d_model // num_heads
+        self.num_heads = num_heads
+        self.merge = nn.Conv1d(d_model, d_model, kernel_size=1)
+        self.proj = nn.ModuleList([deepcopy(self.merge) for _ in range(3)])
+
+    def forward(self, q, k, v):
+        B = q.size(0)
+        q, k, v = [l(x).view(B, self.dim, self.num_heads, -1) for l, x in zip(self.proj, (q, k, v))]
+        x, _ = attention(q, k, v)
+        return self.merge(x.contiguous().view(B, self.dim * self.num_heads, -1))
+
+
+class AttentionalPropagation(nn.Module):
+    def __init__(self, feature_dim, num_heads):
+        super().__init__()
+        self.attn = MultiHeadedAttention(num_heads, feature_dim)
+        self.mlp = conv_mlp([feature_dim * 2, feature_dim * 2, feature_dim])
+        nn.init.constant_(self.mlp[-1].bias, 0.0)
+
+    def forward(self, x, source):
+        return self.mlp(torch.cat([x, self.attn(x, source, source)], dim=1))
+
+
+class OverlapPredictorNet(nn.Module):
+    def __init__(self, d=32):
+        super().__init__()
+        self.overlap_score_net = nn.Sequential(nn.Linear(d, d), nn.ReLU(True), nn.Linear(d, 1), nn.Sigmoid())
+
+    def forward(self, fx, fy):
+        sx = self.overlap_score_net(F.normalize(fx, p=2, dim=-1)).squeeze(2).squeeze(0)
+        sy = self.overlap_score_net(F.normalize(fy, p=2, dim=-1)).squeeze(2).squeeze(0)
+        return sx, sy
+
+
+class CrossAttentionRefinementNet(nn.Module):
+    """modeling/dpfm.py:70-130 with attention_type "normal" and cross_sampling_ratio 1."""
+
+    def __init__(self, n_in=32, num_head=2, gnn_dim=32, n_layers=1):
+        super().__init__()
+        self.n_in = n_in
+        self.layers = nn.ModuleList([AttentionalPropagation(gnn_dim, num_head) for _ in range(n_layers)])
+        self.first_lin = nn.Linear(n_in, gnn_dim)
+        self.last_lin = nn.Linear(gnn_dim, n_in)
+        self.overlap_predictor = OverlapPredictorNet(n_in)
+
+    def forward(self, fx, fy):
+        d0, d1 = self.first_lin(fx).transpose(1, 2), self.first_lin(fy).transpose(1, 2)
+        for layer in self.layers:
+            d0 = d0 + layer(d0, d1)
+            d1 = d1 + layer(d1, d0)  # uses the updated d0 (modeling/dpfm.py:101-103)
+        rx = self.last_lin(d0.transpose(1, 2))[:, :, :self.n_in]
+        ry = self.last_lin(d1.transpose(1, 2))[:, :, :self.n_in]
+        ox, oy = self.overlap_predictor(rx, ry)
+        return rx, ry, ox, oy
+
+
+def get_mask(evals1, evals2, gamma=0.5):
+    """Upstream DPFM get_mask -> [K2, K1]."""
+    s = max(torch.max(evals1), torch.max(evals2))
+    e1, e2 = evals1 / s, evals2 / s
+    g1 = (e1 ** gamma)[None, :]
+    g2 = (e2 ** gamma)[:, None]
+    re = g2 / (g2.square() + 1) - g1 / (g1.square() + 1)
+    im = 1 / (g2.square() + 1) - 1 / (g1.square() + 1)
+    return re.square() + im.square()
+
+
+def regularized_fmap(feat_x, feat_y, evals_x, evals_y, et_x, et_y, lambda_=100.0, gamma=0.5):
+    """modeling/dpfm.py:162-195 (batched branch; `dim == 2` is always False)."""
+    A = torch.bmm(et_x, feat_x)
+    Bm = torch.bmm(et_y, feat_y)
+    D = torch.stack([get_mask(ex.flatten(), ey.flatten(), gamma) for ex, ey in zip(evals_x, evals_y)])
+    AAt = torch.bmm(A, A.transpose(1, 2))
+    BAt = torch.bmm(Bm, A.transpose(1, 2))
+    rows = []
+    for i in range(evals_x.size(1)):
+        Di = torch.cat([torch.diag(D[b, i, :].flatten()).unsqueeze(0) for b in range(evals_x.size(0))], 0)
+        Ci = torch.bmm(torch.inverse(AAt + lambda_ * Di), BAt[:, i, :].unsqueeze(1).transpose(1, 2))
+        rows.append(Ci.transpose(1, 2))
+    return torch.cat(rows, dim=1)
+
+
+class DPFMNet(nn.Module):
+    """models/dpfm.py:15-82 with config/dpfm_orig.yaml."""
+
+    def __init__(self, n_fmap=30, n_feat=32, num_head=2, gnn_dim=32, n_layers=1, lambda_=100.0, gamma=0.5):
+        super().__init__()
+        self.feature_extractor = DiffusionNet(3, n_feat, 64, 2)
+        self.feat_refiner = CrossAttentionRefinementNet(n_feat, num_head, gnn_dim, n_layers)
+        self.n_fmap = n_fmap
+        self.lambda_, self.gamma = lambda_, gamma
+
+    def forward(self, batch):
+        s1, s2 = batch["shape1"], batch["shape2"]
+        f1 = self.feature_extractor((s1["xyz"] - 110) / 50, s1["mass"], s1["evals"], s1["evecs"])
+        f2 = self.feature_extractor((s2["xyz"] - 110) / 50, s2["mass"], s2["evals"], s2["evecs"])
+        r1, r2, o12, o21 = self.feat_refiner(f1, f2)
+        k = self.n_fmap
+        et1 = torch.stack([torch.einsum("ij,i->ji", e[:, :k], m) for e, m in zip(s1["evecs"], s1["mass"])])
+        et2 = torch.stack([torch.einsum("ij,i->ji", e[:, :k], m) for e, m in zip(s2["evecs"], s2["mass"])])
+        C = regularized_fmap(r1, r2, s1["evals"][:, :k], s2["evals"][:, :k], et1, et2, self.lambda_, self.gamma)
+        return C, o12, o21, r1, r2, r1, r2
+
+
+# ---------------------------------------------------------------- utils/loss.py
+def weighted_bce(pred, gt):
+    loss = F.binary_cross_entropy(pred, gt, reduction="none")
+    w = torch.ones_like(gt)
+    wn = gt.sum() / gt.size(0)
+    w[gt >= 0.5] = 1 - wn
+    w[gt < 0.5] = wn
+    return torch.mean(w * loss)
+
+
+def nce_loss(f1, f2, pairs, selected, t=0.07):
+    """utils/loss.py:17-42 with the random pair choice passed in (`selected`)."""
+    f1, f2 = F.normalize(f1, p=2, dim=-1), F.normalize(f2, p=2, dim=-1)
+    q = f1[pairs[selected][:, 0]]
+    kk = f2[pairs[selected][:, 1]]
+    logits = -torch.cdist(q, kk) / t
+    return F.cross_entropy(logits, torch.arange(selected.shape[0]))
+
+
+def dpfm_loss(C, C_gt, pairs, sel, f1, f2, o12, o21, g12, g21, w_fmap=1.0, w_acc=1.0, w_nce=1.0, t=0.07):
+    """utils/loss.py:57-99 (batched branch)."""
+    fro = torch.clamp(torch.sum((C - C_gt) ** 2, axis=(1, 2)), min=-1, max=1000).mean() * w_fmap
+    m = f1.shape[0]
+    if o12.dim() == 1:
+        o12, o21 = o12[None], o21[None]
+    nce = 0.0
+    acc = 0.0
+    for b in range(m):
+        nce = nce + nce_loss(f1[b], f2[b], pairs[b], sel[b], t) * w_nce / m
+        acc = acc + weighted_bce(o12[b], g12[b].float()) * w_acc / m
+        acc = acc + weighted_bce(o21[b], g21[b].float()) * w_acc / m
+    return fro + acc + nce
+
+
+def C_from_sparse_P(P, evecs1, evecs2):
+    """utils/utils.py:67-79."""
+    a1, a2 = evecs1[P[:, 0]], evecs2[P[:, 1]]
+    return torch.linalg.lstsq(a2, a1)[0][:a1.size(-1)]
+
+
+def nce_selection(n_pairs: int, num: int, rng: np.random.Generator) -> np.ndarray:
+    """utils/loss.py:27-30: choice without replacement when there are more pairs."""
+    if n_pairs > num:
+        return rng.choice(n_pairs, num, replace=False)
+    return np.arange(n_pairs)

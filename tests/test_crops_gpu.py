@@ -115,3 +115,27 @@ def test_npoint_fps_gather_transform(device, coracle, fixed):
         np.testing.assert_array_equal(g["sel64"].cpu().numpy()[oo[b]:oo[b + 1]], sel)
         np.testing.assert_array_equal(g["sel32"].cpu().numpy()[oo[b]:oo[b + 1]], sel.astype(np.float32))
         np.testing.assert_array_equal(g["align"].cpu().numpy()[oo[b]:oo[b + 1]], O.transform(sel, R[b], t[b], inv=True))
+
+
+def test_sor_pixel_window_path_bitexact(device):
+    """backproject -> sor with the pixel-window kNN bound gives the brute-force result."""
+    from dpfm_amd import ops
+    fr = _frames()
+    depth = torch.from_numpy(np.stack([f[0].astype(np.int16) for f in fr])).to(device)
+    mask = torch.from_numpy(np.stack([f[1] for f in fr])).to(device)
+    K = torch.from_numpy(np.stack([f[2].reshape(9) for f in fr])).to(device)
+    cs = torch.tensor([1000.0 / f[3] for f in fr], dtype=torch.float32, device=device)
+    bp = ops.backproject(depth, mask, K, cs, cap=200000)
+    nmax = int((bp["off"][1:] - bp["off"][:-1]).max())
+    res = ops.sor(bp["xyz"], bp["off"], nmax, pix=bp["pix"], idxmap=bp["idxmap"], want_idx=True)
+    off = bp["off"].cpu().numpy()
+    oo = res["off"].cpu().numpy()
+    avg = res["avg"].cpu().numpy()
+    kidx = res["kept_idx"].cpu().numpy()
+    xyz = bp["xyz"].cpu().numpy()
+    for b in range(len(fr)):
+        c = xyz[off[b]:off[b + 1]]
+        if c.shape[0] == 0:
+            continue
+        np.testing.assert_array_equal(avg[off[b]:off[b + 1]], O.sor_avg_distances(c), err_msg=f"frame {b}")
+        np.testing.assert_array_equal(kidx[oo[b]:oo[b + 1]], O.remove_outliers_indices(c))

@@ -1,0 +1,61 @@
+"""GPU: the batched device pipeline (crop formation -> train step / inference + pose)
+runs sync-free and agrees with the per-crop oracle chain."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dpfm_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def test_crop_formation_chain_matches_oracle(device, coracle):
+    from _util import c_fps
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.dataset.synthetic import make_frame, cad_points
+    from dpfm_amd.pipeline import make_frame_batch
+    F, N = 4, 1024
+    fb, op = make_frame_batch(F, N, N, seed=50, device=device)
+    crops = CropFormation(n1=N, npoint=N, seed=3)(fb)
+    torch.cuda.synchronize()
+    start = None
+    pc64 = crops.pc64.cpu().numpy()
+    al = crops.align64.cpu().numpy()
+    pairs = crops.pairs.cpu().numpy()
+    npairs = crops.npairs.cpu().numpy()
+    for f in range(F):
+        fr = make_frame(50 + f)
+        pcd = O.remove_outliers(O.dpt_2_pcld(fr.depth, 1000 / fr.depth_scale, fr.K, fr.mask == 255))
+        from dpfm_amd import ops
+        # start index of crop f: splitmix hash of (seed, f) as documented in posekern.h
+        pol = ops.fps_npoint(ops.packed_offsets([pcd.shape[0]] * F, device), fixed=N, seed=3)
+        st = int(pol["start"][f])
+        idx = c_fps(coracle, pcd.astype(np.float32), st, N)
+        sel = pcd[idx]
+        np.testing.assert_array_equal(pc64[f * N:(f + 1) * N], sel)
+        align = O.transform(sel, fr.R_m2c, fr.t_m2c, inv=True)
+        np.testing.assert_array_equal(al[f * N:(f + 1) * N], align)
+        cad = cad_points(fr, N, 50 + f)
+        P = O.find_positives(cad, align, r=0.05 * fr.diam_cad)
+        assert npairs[f] == P.shape[0]
+        np.testing.assert_array_equal(pairs[f, :npairs[f]], P)
+
+
+def test_train_and_infer_steps(device):
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import TrainStep, InferStep, make_frame_batch
+    torch.manual_seed(0)
+    F, N = 4, 512
+    fb, op = make_frame_batch(F, N, N, seed=70, device=device)
+    crops = CropFormation(n1=N, npoint=N)(fb)
+    model = DPFMNet().to(device)
+    step = TrainStep(model)
+    w0 = [p.detach().clone() for p in model.parameters()]
+    log = step(op, crops)
+    torch.cuda.synchronize()
+    assert torch.isfinite(log["loss"]) and 0.0 <= float(log["IR"]) <= 1.0
+    assert any(not torch.equal(a, b.detach()) for a, b in zip(w0, model.parameters()))
+    out = InferStep(model, hypotheses=256)(fb, op, crops)
+    torch.cuda.synchronize()
+    assert out["T"].shape == (F, 4, 4) and torch.isfinite(out["metrics"]).all()

@@ -1,0 +1,31 @@
+#!/bin/bash
+# GPU-box runner: each step under its own timeout; stop at the first failure or runtime
+# fault (HSA exception text in the step's log), so nothing else touches a faulted GPU.
+#   tools/gpu_run.sh <tag> <steps...>   steps: tests | smoke | bench | prof | pmc | kbench
+set -u
+tag=$1; shift
+out=gpurun_out/$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+fault() { grep -q "HSA_STATUS_ERROR\|hipErrorLaunchFailure\|Memory access fault" "$1"; }
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name" >&2
+  timeout -k 10 "$to" "$@" > "$out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" >> "$out/status.txt"
+  if fault "$out/$name.log"; then echo "$name: GPU FAULT" >> "$out/status.txt"; tail -30 "$out/$name.log"; exit 3; fi
+  if [ $rc -ne 0 ]; then tail -40 "$out/$name.log"; exit $rc; fi
+}
+for step in "$@"; do
+  case $step in
+    tests) run tests 900 python -m pytest tests -m gpu -q ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    benchq) run benchq 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline-probe ;;
+    kbench) run kbench 300 python tools/kbench.py ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+cat "$out/status.txt"
