@@ -158,19 +158,28 @@ __device__ __forceinline__ double sqdist(double ax, double ay, double az, const 
 
 // grid (ceil(nmax/256), B), block 256: one query point per thread.
 //  pass 1 (pixel window, when pix/idxmap are given): exact distances to the points of the
-//         5x5 pixel neighbourhood; if >= knn of them exist, T = their knn-th smallest
+//         5x5 pixel neighbourhood (9x9, 17x17 where that holds fewer than knn points, near
+//         the mask border); if >= knn of them exist, T = their knn-th smallest
 //         squared distance bounds the true knn-th neighbour distance (>= knn points lie
 //         within T). Otherwise T = +inf.
-//  pass 2: every point of the crop (LDS tiles of fp32 coordinates centred on the crop's
-//         first point) is screened with an fp32 distance against T + margin, where
-//         margin = 2^-19 (T + (|a| + |b|)^2) bounds the fp32 error;
-//         survivors are re-evaluated exactly in fp64 and inserted if <= T.
+//  pass 2a (K given, T finite, Z_q > r = sqrt(T)): every crop point within r of the query
+//         lies in the pixel box |du| <= fx r (1 + tx) / Z_q, |dv| <= fy r (1 + ty) / Z_q
+//         (tx = max|u - cx| / fx over the image), +1 px slack for the
+//         rounding of X/Z vs (u - cx)/fx. That box is scanned exactly in fp64.
+//  pass 2b (otherwise, or when the box exceeds kSorMaxBox pixels): every point of the
+//         crop (LDS tiles of fp32 coordinates centred on the crop's first point) is
+//         screened with an fp32 distance against T + margin, where margin = 2^-19 (T +
+//         (|a| + |b|)^2) bounds the fp32 error; survivors are
+//         re-evaluated exactly in fp64 and inserted if <= T.
 // The kept set is a superset of the true knn nearest (ties included), so the sorted
 // top-knn values are exactly those of a full brute-force search.
+constexpr int kSorMaxBox = 1024;
+
 __global__ __launch_bounds__(kSorThreads) void sor_knn_kernel(const double* __restrict__ xyz,
                                                               const int64_t* __restrict__ off, int knn,
                                                               const int32_t* __restrict__ pix,
                                                               const int32_t* __restrict__ idxmap, int H, int W,
+                                                              const double* __restrict__ Kmat,
                                                               double* __restrict__ avg) {
   __shared__ float4 tile[kSorTile];
   const int b = blockIdx.y;
@@ -192,22 +201,26 @@ __global__ __launch_bounds__(kSorThreads) void sor_knn_kernel(const double* __re
 #pragma unroll
   for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
   double T = __builtin_huge_val();
+  bool done = false;
   if (act && pix != nullptr && idxmap != nullptr) {
     const int pp = pix[base + i];
     const int v = pp / W, u = pp % W;
     const int32_t* im = idxmap + (int64_t)b * H * W;
     int found = 0;
-    for (int dv = -2; dv <= 2; ++dv) {
-      const int vv = v + dv;
-      if (vv < 0 || vv >= H) continue;
-      for (int du = -2; du <= 2; ++du) {
-        const int uu = u + du;
-        if (uu < 0 || uu >= W) continue;
-        const int j = im[vv * W + uu];
-        if (j < 0) continue;
-        topk_insert(best, sqdist(q0, q1, q2, p + 3 * j));
-        ++found;
+    for (int R = 2; R <= 8; R *= 2) {  // 5x5, then 9x9, 17x17 near the mask border
+      found = 0;
+#pragma unroll
+      for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
+      for (int vv = max(v - R, 0); vv <= min(v + R, H - 1); ++vv) {
+        const int32_t* row = im + vv * W;
+        for (int uu = max(u - R, 0); uu <= min(u + R, W - 1); ++uu) {
+          const int j = row[uu];
+          if (j < 0) continue;
+          topk_insert(best, sqdist(q0, q1, q2, p + 3 * j));
+          ++found;
+        }
       }
+      if (found >= kk) break;
     }
     if (found >= kk) {
 #pragma unroll
@@ -216,29 +229,58 @@ __global__ __launch_bounds__(kSorThreads) void sor_knn_kernel(const double* __re
     }
 #pragma unroll
     for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
-  }
-  const float qx = (float)(q0 - ox), qy = (float)(q1 - oy), qz = (float)(q2 - oz);
-  const float qa = fmaxf(fabsf(qx), fmaxf(fabsf(qy), fabsf(qz)));
-  const float Tf = T == __builtin_huge_val() ? __builtin_huge_valf() : (float)T;
-  for (int t0 = 0; t0 < n; t0 += kSorTile) {
-    const int tn = min(kSorTile, n - t0);
-    __syncthreads();
-    for (int e = threadIdx.x; e < tn; e += kSorThreads) {
-      const double* c = p + 3 * (t0 + e);
-      const float cx = (float)(c[0] - ox), cy = (float)(c[1] - oy), cz = (float)(c[2] - oz);
-      tile[e] = make_float4(cx, cy, cz, fmaxf(fabsf(cx), fmaxf(fabsf(cy), fabsf(cz))));
+    if (Kmat != nullptr && T < __builtin_huge_val()) {
+      const double* Kb = Kmat + 9 * b;
+      const double fx = Kb[0], cx = Kb[2], fy = Kb[4], cy = Kb[5];
+      const double r = sqrt(T) * (1.0 + 1e-9) + 1e-300;
+      if (fx > 0.0 && fy > 0.0 && q2 > r) {
+        const double tx = fmax(fabs(cx), fabs((double)(W - 1) - cx)) / fx;
+        const double ty = fmax(fabs(cy), fabs((double)(H - 1) - cy)) / fy;
+        const double bu = fx * r * (1.0 + tx) / q2, bv = fy * r * (1.0 + ty) / q2;
+        if (bu < 64.0 && bv < 64.0) {
+          const int ru = (int)ceil(bu * (1.0 + 1e-9)) + 1, rv = (int)ceil(bv * (1.0 + 1e-9)) + 1;
+          if ((2 * ru + 1) * (2 * rv + 1) <= kSorMaxBox) {
+            const int v0 = max(v - rv, 0), v1 = min(v + rv, H - 1);
+            const int u0 = max(u - ru, 0), u1 = min(u + ru, W - 1);
+            for (int vv = v0; vv <= v1; ++vv) {
+              const int32_t* row = im + vv * W;
+              for (int uu = u0; uu <= u1; ++uu) {
+                const int j = row[uu];
+                if (j < 0) continue;
+                const double s = sqdist(q0, q1, q2, p + 3 * j);
+                if (s <= T && s < best[kKnn - 1]) topk_insert(best, s);
+              }
+            }
+            done = true;
+          }
+        }
+      }
     }
-    __syncthreads();
-    if (act) {
-      for (int e = 0; e < tn; ++e) {
-        const float4 c = tile[e];
-        const float dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
-        const float d32 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-        const float sa = qa + c.w;
-        const float lim = fmaf(1.9073486e-6f, fmaf(sa, sa, Tf), Tf);  // T + 2^-19 (T + S^2)
-        if (d32 <= lim) {
-          const double s = sqdist(q0, q1, q2, p + 3 * (t0 + e));
-          if (s <= T && s < best[kKnn - 1]) topk_insert(best, s);
+  }
+  if (__syncthreads_or(act && !done)) {
+    const float qx = (float)(q0 - ox), qy = (float)(q1 - oy), qz = (float)(q2 - oz);
+    const float qa = fmaxf(fabsf(qx), fmaxf(fabsf(qy), fabsf(qz)));
+    const float Tf = T == __builtin_huge_val() ? __builtin_huge_valf() : (float)T;
+    for (int t0 = 0; t0 < n; t0 += kSorTile) {
+      const int tn = min(kSorTile, n - t0);
+      __syncthreads();
+      for (int e = threadIdx.x; e < tn; e += kSorThreads) {
+        const double* c = p + 3 * (t0 + e);
+        const float cx = (float)(c[0] - ox), cy = (float)(c[1] - oy), cz = (float)(c[2] - oz);
+        tile[e] = make_float4(cx, cy, cz, fmaxf(fabsf(cx), fmaxf(fabsf(cy), fabsf(cz))));
+      }
+      __syncthreads();
+      if (act && !done) {
+        for (int e = 0; e < tn; ++e) {
+          const float4 c = tile[e];
+          const float dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
+          const float d32 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+          const float sa = qa + c.w;
+          const float lim = fmaf(1.9073486e-6f, fmaf(sa, sa, Tf), Tf);  // T + 2^-19 (T + S^2)
+          if (d32 <= lim) {
+            const double s = sqdist(q0, q1, q2, p + 3 * (t0 + e));
+            if (s <= T && s < best[kKnn - 1]) topk_insert(best, s);
+          }
         }
       }
     }
@@ -252,32 +294,67 @@ __global__ __launch_bounds__(kSorThreads) void sor_knn_kernel(const double* __re
   }
 }
 
-// One wave per crop: mean over avg>0, Bessel std, threshold; sequential accumulation in
-// point order like std::accumulate / std::inner_product (lane 0), then ordered keep flags.
-__global__ __launch_bounds__(64) void sor_stats_kernel(const double* __restrict__ avg,
-                                                       const int64_t* __restrict__ off, double std_ratio,
-                                                       double* __restrict__ thr) {
+// One block per crop: cloud mean over avg > 0, then the Bessel std, accumulated in point
+// order exactly like std::accumulate / std::inner_product. The block stages the terms
+// (masked values, then the squared deviations) into LDS in parallel; thread 0 adds them in
+// order (adding +0.0 for masked points leaves a +0.0-started positive sum unchanged).
+constexpr int kStatChunk = 4096;
+constexpr int kStatThreads = 256;
+
+__device__ __forceinline__ double seq_sum_lds(const double* __restrict__ v, int m, double acc) {
+  int k = 0;
+  for (; k + 8 <= m; k += 8) {
+    const double a0 = v[k], a1 = v[k + 1], a2 = v[k + 2], a3 = v[k + 3];
+    const double a4 = v[k + 4], a5 = v[k + 5], a6 = v[k + 6], a7 = v[k + 7];
+    acc = acc + a0; acc = acc + a1; acc = acc + a2; acc = acc + a3;
+    acc = acc + a4; acc = acc + a5; acc = acc + a6; acc = acc + a7;
+  }
+  for (; k < m; ++k) acc = acc + v[k];
+  return acc;
+}
+
+__global__ __launch_bounds__(kStatThreads) void sor_stats_kernel(const double* __restrict__ avg,
+                                                                 const int64_t* __restrict__ off,
+                                                                 double std_ratio, double* __restrict__ thr) {
+  __shared__ double buf[kStatChunk];
+  __shared__ double acc_s;
   const int b = blockIdx.x;
   const int64_t base = off[b];
   const int n = (int)(off[b + 1] - base);
-  if (threadIdx.x != 0) return;
   if (n <= 0) {
-    thr[b] = -1.0;
+    if (threadIdx.x == 0) thr[b] = -1.0;
     return;
   }
-  double mean = 0.0;
-  for (int i = 0; i < n; ++i) {
-    const double a = avg[base + i];
-    if (a > 0) mean = mean + a;
+  if (threadIdx.x == 0) acc_s = 0.0;
+  for (int c0 = 0; c0 < n; c0 += kStatChunk) {
+    const int m = min(kStatChunk, n - c0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < m; e += kStatThreads) {
+      const double a = avg[base + c0 + e];
+      buf[e] = a > 0 ? a : 0.0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) acc_s = seq_sum_lds(buf, m, acc_s);
   }
-  mean = mean / (double)n;
-  double sq = 0.0;
-  for (int i = 0; i < n; ++i) {
-    const double a = avg[base + i];
-    sq = sq + (a > 0 ? (a - mean) * (a - mean) : 0.0);
+  __syncthreads();
+  const double mean = acc_s / (double)n;
+  __syncthreads();
+  if (threadIdx.x == 0) acc_s = 0.0;
+  for (int c0 = 0; c0 < n; c0 += kStatChunk) {
+    const int m = min(kStatChunk, n - c0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < m; e += kStatThreads) {
+      const double a = avg[base + c0 + e];
+      buf[e] = a > 0 ? (a - mean) * (a - mean) : 0.0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) acc_s = seq_sum_lds(buf, m, acc_s);
   }
-  const double sd = n > 1 ? sqrt_rn(sq / (double)(n - 1)) : __builtin_nan("");
-  thr[b] = mean + std_ratio * sd;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double sd = n > 1 ? sqrt_rn(acc_s / (double)(n - 1)) : __builtin_nan("");
+    thr[b] = mean + std_ratio * sd;
+  }
 }
 
 // grid (ceil(nmax/1024), B) block 1024: per-chunk keep counts.
@@ -439,7 +516,7 @@ extern "C" int pk_backproject(const uint16_t* depth, const uint8_t* mask, int F,
 
 extern "C" int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, int knn,
                       double std_ratio, const int32_t* pix, const int32_t* idxmap, int H, int W,
-                      double* avg, double* thr, int32_t* ccount, int64_t* coff,
+                      const double* K, double* avg, double* thr, int32_t* ccount, int64_t* coff,
                       int64_t* kept, int64_t* out_off, double* out64, float* out32,
                       int64_t* kept_idx, void* stream) {
   PK_REQUIRE(B >= 0 && nmax >= 0 && knn > 0 && knn <= kKnn);
@@ -450,10 +527,11 @@ extern "C" int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, in
   const int nchunk = (nmax + 1023) / 1024;
   if (nmax > 0) {
     hipLaunchKernelGGL(sor_knn_kernel, dim3((nmax + kSorThreads - 1) / kSorThreads, B),
-                       dim3(kSorThreads), 0, s, xyz, off, knn, pix, idxmap, H, W, avg);
+                       dim3(kSorThreads), 0, s, xyz, off, knn, pix, idxmap, H, W,
+                       pix != nullptr ? K : nullptr, avg);
     PK_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(sor_stats_kernel, dim3(B), dim3(64), 0, s, avg, off, std_ratio, thr);
+  hipLaunchKernelGGL(sor_stats_kernel, dim3(B), dim3(kStatThreads), 0, s, avg, off, std_ratio, thr);
   PK_CHECK_LAUNCH();
   if (nchunk > 0) {
     hipLaunchKernelGGL(sor_count_kernel, dim3(nchunk, B), dim3(1024), 0, s, avg, off, thr, nchunk, ccount);

@@ -28,7 +28,7 @@ SIGNATURES = {
     "pk_ball_query_mask": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P],
     "pk_ball_query_pairs": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _I64, _P, _P, _P, _P],
     "pk_backproject": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P],
-    "pk_sor": [_P, _P, _I, _I, _I, _D, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "pk_sor": [_P, _P, _I, _I, _I, _D, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "pk_fps_npoint": [_P, _I, _I, _I, _U64, _P, _P, _P, _P],
     "pk_gather_transform": [_P, _P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P],
     "pk_segment_scan": [_P, _I, _I, _P, _P, _P],

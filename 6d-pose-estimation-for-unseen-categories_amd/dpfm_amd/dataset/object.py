@@ -167,7 +167,7 @@ class CropFormation:
         F_, H, W = fb.depth.shape
         dev = fb.depth.device
         bp = ops.backproject(fb.depth, fb.mask, fb.K, fb.cam_scale, cap=F_ * fb.max_pixels)
-        so = ops.sor(bp["xyz"], bp["off"], fb.max_pixels, 20, 0.3, pix=bp["pix"], idxmap=bp["idxmap"])
+        so = ops.sor(bp["xyz"], bp["off"], fb.max_pixels, 20, 0.3, pix=bp["pix"], idxmap=bp["idxmap"], K=fb.K)
         pol = ops.fps_npoint(so["off"], fixed=self.npoint, limit=2000, seed=self.seed)
         npmax = self.npoint if self.npoint > 0 else 2000
         idx = ops.fps_packed(so["xyz32"], so["off"], fb.max_pixels, pol["start"], pol["npoint"], npmax)

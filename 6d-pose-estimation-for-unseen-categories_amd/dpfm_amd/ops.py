@@ -127,9 +127,12 @@ def backproject(depth: torch.Tensor, mask: torch.Tensor, K: torch.Tensor, cam_sc
 
 def sor(xyz: torch.Tensor, off: torch.Tensor, nmax: int, knn: int = 20, std_ratio: float = 0.3,
         want64: bool = True, want32: bool = True, want_idx: bool = False, pix: Optional[torch.Tensor] = None,
-        idxmap: Optional[torch.Tensor] = None) -> dict:
+        idxmap: Optional[torch.Tensor] = None, K: Optional[torch.Tensor] = None) -> dict:
     """remove_outliers for B packed crops (pk_sor). Survivors are packed by out_off.
-    pix/idxmap (from backproject) enable the exact pixel-window kNN bound."""
+    pix/idxmap (from backproject) enable the exact pixel-window kNN bound; with the frames'
+    intrinsics K (f64 [B, 9]) only the pixel box that can hold a neighbour is scanned."""
+    if K is not None:
+        K = K.to(dtype=torch.float64).reshape(-1, 9).contiguous()
     B = off.numel() - 1
     dev = xyz.device
     T = xyz.shape[0]
@@ -146,7 +149,7 @@ def sor(xyz: torch.Tensor, off: torch.Tensor, nmax: int, knn: int = 20, std_rati
     H = idxmap.shape[1] if idxmap is not None else 0
     W = idxmap.shape[2] if idxmap is not None else 0
     call("pk_sor", ptr(xyz), ptr(off), B, int(nmax), int(knn), float(std_ratio), ptr(pix), ptr(idxmap), H, W,
-         ptr(avg), ptr(thr), ptr(ccount),
+         ptr(K), ptr(avg), ptr(thr), ptr(ccount),
          ptr(coff), ptr(kept), ptr(out_off), ptr(out64), ptr(out32), ptr(kidx), _lib.stream(dev))
     return dict(avg=avg, thr=thr, kept=kept, off=out_off, xyz64=out64, xyz32=out32, kept_idx=kidx)
 

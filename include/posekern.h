@@ -78,13 +78,16 @@ int pk_backproject(const uint16_t* depth, const uint8_t* mask, int F, int H, int
  *   xyz f64 [T,3] packed / off, knn <= 20
  *   pix / idxmap (optional, from pk_backproject, crop b = frame b): an exact kNN bound
  *   from the 5x5 pixel window prunes the brute-force scan (results unchanged)
+ *   K f64 [B,9] (optional, with pix): camera intrinsics of frame b; bounds the pixel box
+ *   that can hold a point within the kNN radius so only that box is scanned
  *   avg f64 [T] mean kNN distance, thr f64 [B] keep threshold
  *   ccount int32 [B, ceil(nmax/1024)], coff int64 (same shape) scratch
  *   kept int64 [B] survivors, out_off int64 [B+1] their packed offsets
  *   out64 f64 [T,3], out32 f32 [T,3] (either may be NULL) survivors in input order
  *   kept_idx int64 [T] (may be NULL) survivor index within its input crop */
 int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, int knn, double std_ratio,
-           const int32_t* pix, const int32_t* idxmap, int H, int W, double* avg, double* thr,
+           const int32_t* pix, const int32_t* idxmap, int H, int W, const double* K, double* avg,
+           double* thr,
            int32_t* ccount, int64_t* coff, int64_t* kept, int64_t* out_off, double* out64,
            float* out32, int64_t* kept_idx, void* stream);
 

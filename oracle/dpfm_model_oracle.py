@@ -233,8 +233,8 @@ def dpfm_loss(C, C_gt, pairs, sel, f1, f2, o12, o21, g12, g21, w_fmap=1.0, w_acc
     acc = 0.0
     for b in range(m):
         nce = nce + nce_loss(f1[b], f2[b], pairs[b], sel[b], t) * w_nce / m
-        acc = acc + weighted_bce(o12[b], g12[b].float()) * w_acc / m
-        acc = acc + weighted_bce(o21[b], g21[b].float()) * w_acc / m
+        acc = acc + weighted_bce(o12[b], g12[b].to(o12.dtype)) * w_acc / m
+        acc = acc + weighted_bce(o21[b], g21[b].to(o21.dtype)) * w_acc / m
     return fro + acc + nce
 
 

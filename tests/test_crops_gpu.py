@@ -117,8 +117,10 @@ def test_npoint_fps_gather_transform(device, coracle, fixed):
         np.testing.assert_array_equal(g["align"].cpu().numpy()[oo[b]:oo[b + 1]], O.transform(sel, R[b], t[b], inv=True))
 
 
-def test_sor_pixel_window_path_bitexact(device):
-    """backproject -> sor with the pixel-window kNN bound gives the brute-force result."""
+@pytest.mark.parametrize("with_K", [False, True])
+def test_sor_pixel_window_path_bitexact(device, with_K):
+    """backproject -> sor with the pixel-window kNN bound (and, with K, the camera-model
+    pixel box) gives the brute-force result."""
     from dpfm_amd import ops
     fr = _frames()
     depth = torch.from_numpy(np.stack([f[0].astype(np.int16) for f in fr])).to(device)
@@ -127,7 +129,8 @@ def test_sor_pixel_window_path_bitexact(device):
     cs = torch.tensor([1000.0 / f[3] for f in fr], dtype=torch.float32, device=device)
     bp = ops.backproject(depth, mask, K, cs, cap=200000)
     nmax = int((bp["off"][1:] - bp["off"][:-1]).max())
-    res = ops.sor(bp["xyz"], bp["off"], nmax, pix=bp["pix"], idxmap=bp["idxmap"], want_idx=True)
+    res = ops.sor(bp["xyz"], bp["off"], nmax, pix=bp["pix"], idxmap=bp["idxmap"], want_idx=True,
+                  K=K if with_K else None)
     off = bp["off"].cpu().numpy()
     oo = res["off"].cpu().numpy()
     avg = res["avg"].cpu().numpy()

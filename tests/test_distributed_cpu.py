@@ -1,0 +1,138 @@
+"""Multi-rank data parallelism on the CPU (gloo, world_size 2): the bench/training path
+shards crops across ranks and averages gradients in one all-reduce bucket
+(pipeline.TrainStep.allreduce_grads). Checks:
+  - the bucketed all-reduce leaves every rank with the mean of the ranks' gradients,
+    parameter by parameter (flattening order and views are right);
+  - with equal per-rank batches, the averaged per-rank gradients of the reference loss
+    (utils/loss.py:57-99: Frobenius term a batch mean, NCE/BCE scaled by 1/m) equal the
+    gradient of the global batch, i.e. DDP semantics reproduce single-process training.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import dpfm_model_oracle as M
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _crop_batch(seeds, n1=96, n2=80):
+    from dpfm_amd.dataset.synthetic import lbo_operators
+    out = {"shape1": {}, "shape2": {}}
+    pairs, sel, g12, g21 = [], [], [], []
+    for key, n, o in (("shape1", n1, 0), ("shape2", n2, 1)):
+        cols = {"xyz": [], "mass": [], "evals": [], "evecs": []}
+        for s in seeds:
+            rng = np.random.default_rng(100 + 2 * s + o)
+            m, e, v = lbo_operators(n, 64, 2 * s + o)
+            cols["xyz"].append(rng.normal(size=(n, 3)).astype(np.float32) * 5 + 100)
+            cols["mass"].append(m)
+            cols["evals"].append(e)
+            cols["evecs"].append(v)
+        out[key] = {k: torch.from_numpy(np.stack(v)).double() for k, v in cols.items()}
+    for s in seeds:
+        rng = np.random.default_rng(7 + s)
+        P = np.stack([rng.integers(0, n1, 200), rng.integers(0, n2, 200)], 1).astype(np.int64)
+        pairs.append(torch.from_numpy(P))
+        sel.append(torch.from_numpy(M.nce_selection(200, 64, rng)))
+        a = np.zeros(n1, np.float32)
+        a[P[:, 0]] = 1
+        b = np.zeros(n2, np.float32)
+        b[P[:, 1]] = 1
+        g12.append(a)
+        g21.append(b)
+    return out, pairs, sel, torch.from_numpy(np.stack(g12)).double(), torch.from_numpy(np.stack(g21)).double()
+
+
+def _grads(model, seeds):
+    batch, pairs, sel, g12, g21 = _crop_batch(seeds)
+    model.zero_grad()
+    C, o12, o21, f1, f2, _, _ = model(batch)
+    C_gt = torch.stack([M.C_from_sparse_P(P, batch["shape1"]["evecs"][b, :, :30], batch["shape2"]["evecs"][b, :, :30])
+                        for b, P in enumerate(pairs)])
+    M.dpfm_loss(C, C_gt, pairs, sel, f1, f2, o12, o21, g12, g21).backward()
+    return [p.grad.detach().clone() for p in model.parameters()]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _work(rank, world, q)
+    except BaseException as e:  # report instead of leaving the parent waiting
+        q.put(("error", rank, repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _np(ts):  # plain arrays through the queue (no shared-memory tensor handles)
+    return [t.detach().numpy().copy() for t in ts]
+
+
+def _work(rank, world, q):
+    torch.set_num_threads(1)
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import TrainStep
+    torch.manual_seed(0)
+    ref = M.DPFMNet().double()
+    mine = DPFMNet().double()  # parameters only (CPU): the collective path is device-agnostic
+    mine.load_state_dict(ref.state_dict())
+    step = TrainStep(mine)
+    step.flat = step.flat.double()
+    assert step.world == world
+    # (1) bucket mean of arbitrary per-rank gradients
+    g = torch.Generator().manual_seed(rank)
+    local = [torch.randn(p.shape, generator=g, dtype=torch.float64) for p in mine.parameters()]
+    for p, l in zip(mine.parameters(), local):
+        p.grad = l.clone()
+    step.allreduce_grads()
+    q.put(("bucket", rank, _np(p.grad for p in mine.parameters()), _np(local)))
+    # (2) the reference loss on this rank's half of the global batch
+    seeds = [2 * rank, 2 * rank + 1]
+    for p, gr in zip(mine.parameters(), _grads(ref, seeds)):
+        p.grad = gr
+    step.allreduce_grads()
+    q.put(("loss", rank, _np(p.grad for p in mine.parameters()), None))
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gradient_allreduce_matches_global_batch():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = []
+    for _ in range(2 * world):
+        msgs.append(q.get(timeout=240))
+        assert msgs[-1][0] != "error", msgs[-1]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    bucket = {r: (g, l) for kind, r, g, l in msgs if kind == "bucket"}
+    mean = [(a + b) / 2 for a, b in zip(bucket[0][1], bucket[1][1])]
+    for r in range(world):
+        for got, exp in zip(bucket[r][0], mean):
+            np.testing.assert_allclose(got, exp, rtol=1e-12, atol=1e-12)
+    # global batch of 4 crops in one process (same weights, seed 0)
+    torch.manual_seed(0)
+    ref = M.DPFMNet().double()
+    full = _grads(ref, [0, 1, 2, 3])
+    loss = {r: g for kind, r, g, _ in msgs if kind == "loss"}
+    for r in range(world):
+        for got, exp in zip(loss[r], full):
+            np.testing.assert_allclose(got, exp.numpy(), rtol=1e-9, atol=1e-10)

@@ -79,10 +79,13 @@ def test_fmap_solve_fwd_bwd(device):
 
 @pytest.mark.parametrize("N1,N2", [(256, 256), (300, 200)])
 def test_dpfmnet_matches_oracle(device, N1, N2):
-    """Forward outputs and parameter gradients vs the oracle. The fmap head solves ill-
-    conditioned 30x30 systems, so the yardstick is the oracle evaluated in fp64: the HIP
-    path must be at least as close to it as the reference's own fp32 evaluation (x3 + a
-    small absolute floor)."""
+    """Forward outputs and parameter gradients vs the oracle evaluated in fp64 (the truth).
+    Yardstick: the same oracle evaluated in fp32, on the CPU (the reference's own path) and
+    with torch on the GPU; the HIP path must be within 3x the larger of their errors.
+    Gradients are compared as Frobenius norms per parameter (max-abs errors of independent
+    fp32 evaluations fluctuate by several x), with an absolute floor of 1e-6 x the global
+    gradient norm for the parameters whose true gradient vanishes by invariance (biases in
+    front of InstanceNorm / the softmax's key bias)."""
     from dpfm_amd.models.dpfm import DPFMNet
     torch.manual_seed(3)
     ref = M.DPFMNet()
@@ -91,36 +94,32 @@ def test_dpfmnet_matches_oracle(device, N1, N2):
         ref.feature_extractor.block_1.diffusion.diffusion_time.uniform_(-0.001, 12)
     truth = M.DPFMNet().double()
     truth.load_state_dict(ref.state_dict())
+    gref = M.DPFMNet().to(device)
+    gref.load_state_dict(ref.state_dict())
     mine = DPFMNet().to(device)
     mine.load_state_dict(ref.state_dict(), strict=True)
     batch = _inputs(2, N1, N2, seed=5)
     batch64 = {k: {kk: vv.double() for kk, vv in v.items()} for k, v in batch.items()}
-    outs = [truth(batch64), ref(batch), mine(_to(batch, device))]
+    runs = [(truth, batch64), (ref, batch), (gref, _to(batch, device)), (mine, _to(batch, device))]
 
-    names = ["C", "o12", "o21", "f1", "f2"]
-    for n, t, r, d in zip(names, *(o[:5] for o in outs)):
-        t, r, d = t.detach(), r.detach().double(), d.detach().cpu().double()
-        err_ref = (r - t).abs().max().item()
-        err_mine = (d - t).abs().max().item()
-        assert err_mine <= 3 * err_ref + 1e-5 * (1 + t.abs().max().item()), (n, err_mine, err_ref)
+    outs = [m(b) for m, b in runs]
+    for n, t, r, g, d in zip(["C", "o12", "o21", "f1", "f2"], *(o[:5] for o in outs)):
+        t = t.detach()
+        e = [(x.detach().cpu().double() - t).abs().max().item() for x in (r, g, d)]
+        assert e[2] <= 3 * max(e[0], e[1]) + 1e-6 * (1 + t.abs().max().item()), (n, e)
 
-    def grads_of(loss_fn):
-        for m in (truth, ref, mine):
+    def check(loss_fn):
+        grads = []
+        for m, b in runs:
             m.zero_grad()
-        outs = [truth(batch64), ref(batch), mine(_to(batch, device))]
-        for o in outs:
-            loss_fn(o).backward()
-        return [[p.grad.detach().cpu().double() for p in m.parameters()] for m in (truth, ref, mine)]
+            loss_fn(m(b)).backward()
+            grads.append([torch.zeros(p.shape, dtype=torch.float64) if p.grad is None else p.grad.detach().cpu().double()
+                          for p in m.parameters()])
+        floor = 1e-6 * torch.cat([g.reshape(-1) for g in grads[0]]).norm().item()
+        for i, (name, _) in enumerate(truth.named_parameters()):
+            t = grads[0][i]
+            e = [(g[i] - t).norm().item() for g in grads[1:]]
+            assert e[2] <= 3 * max(e[0], e[1]) + floor, (name, e, floor)
 
-    # (a) overlap + feature heads: well conditioned, tight tolerance
-    gt, gr, gd = grads_of(lambda o: o[1].sum() + o[2].sum() + o[3].square().sum() + o[4].square().sum())
-    for (name, _), t, r, d in zip(truth.named_parameters(), gt, gr, gd):
-        err_ref, err_mine = (r - t).abs().max().item(), (d - t).abs().max().item()
-        assert err_mine <= 3 * err_ref + 1e-5 * (1 + t.abs().max().item()), (name, err_mine, err_ref)
-    # (b) through the fmap solve (ill-conditioned 30x30 systems): error vs the fp64 truth at
-    #     most 10x the reference's own fp32 error plus 2% of the gradient scale
-    gt, gr, gd = grads_of(lambda o: o[0].sum())
-    for (name, _), t, r, d in zip(truth.named_parameters(), gt, gr, gd):
-        err_ref, err_mine = (r - t).abs().max().item(), (d - t).abs().max().item()
-        scale = t.abs().max().item()
-        assert err_mine <= max(10 * err_ref, 1e-5) + 0.02 * scale, (name, err_mine, err_ref, scale)
+    check(lambda o: o[1].sum() + o[2].sum() + o[3].square().sum() + o[4].square().sum())  # overlap + features
+    check(lambda o: o[0].sum())                                                          # through the fmap solve

@@ -23,8 +23,10 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     benchq) run benchq 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline-probe ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline-probe
+          find "$out/prof" -type f ! -name "*stats.csv" -delete ;;
     kbench) run kbench 300 python tools/kbench.py ;;
+    diag) run diag 300 python tools/diag_model.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
