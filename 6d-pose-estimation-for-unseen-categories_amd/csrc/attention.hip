@@ -1,0 +1,272 @@
+// H8 — fused multi-head attention of the cross-attention refinement (fwd + bwd).
+//
+// Reference: modeling/dpfm.py:29-37 `attention(query, key, value)` on [B, dim, heads, N]
+// views of the Conv1d projections (:50-54, heads interleaved: channel = d * heads + h):
+//     scores = einsum('bdhn,bdhm->bhnm', q, k) / dim**.5 ;  prob = softmax(scores, -1)
+//     out    = einsum('bhnm,bdhm->bdhn', prob, v)
+// The reference materialises scores and prob ([B, heads, N, M] fp32, twice per layer);
+// here they live only in registers (online softmax, FlashAttention-2 style), in fp32:
+// products on the f32 MFMA (v_mfma_f32_16x16x4_f32), exp via the accurate expf.
+// dim = 16 (gnn_dim 32 / 2 heads, config/dpfm_orig.yaml), so 1/sqrt(dim) = 0.25 exactly.
+//
+// MFMA lane maps (16x16x4): A[i = l & 15][k = l >> 4], B[k = l >> 4][j = l & 15],
+// D[row = 4 (l >> 4) + r][col = l & 15]. A 16x16 D tile of S^T = K Q^T leaves lane l
+// with keys 4g + r (g = l >> 4) of query l & 15, which is directly the B operand of the
+// next contraction over keys when step r pairs key 4g + r with A's lane group g.
+//
+// Kernels (one workgroup = 4 waves x 16 rows = 64 rows of one (crop, head)):
+//   attn_fwd_kernel     queries; streams 64-key tiles of K, V through LDS; writes out
+//                       and lse = m + log(sum) per query (saved for the backward)
+//   attn_bwd_dq_kernel  queries; delta = rowsum(dO * O) then dQ = 0.25 dS K
+//   attn_bwd_dkv_kernel keys; streams 64-query tiles of Q, dO; dV = P^T dO,
+//                       dK = 0.25 dS^T Q with dS = P (dP - delta), dP = dO V^T
+#include "common.hpp"
+
+namespace {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+constexpr int kD = 16;       // head dim
+constexpr int kT = 64;       // rows per tile / per workgroup
+constexpr int kSR = 80;      // LDS stride of [d][row] arrays (bank-conflict-free MFMA reads)
+constexpr int kSC = 20;      // LDS stride of [row][d] arrays
+constexpr float kScale = 0.25f;
+
+__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float grp_max(float v) {  // over the 4 lane groups (same l & 15)
+  v = fmaxf(v, __shfl_xor(v, 16));
+  return fmaxf(v, __shfl_xor(v, 32));
+}
+
+__device__ __forceinline__ float grp_sum(float v) {
+  v += __shfl_xor(v, 16);
+  return v + __shfl_xor(v, 32);
+}
+
+// Stage a 64-row tile of a [D, H, L] slab (row index contiguous) into LDS as [d][row]
+// (stride kSR) and/or [row][d] (stride kSC); rows >= L read as 0.
+__device__ __forceinline__ void stage(const float* __restrict__ src, int HL, int L, int r0,
+                                      float* __restrict__ dr, float* __restrict__ rd) {
+  for (int e = threadIdx.x; e < kD * kT; e += 256) {
+    const int d = e >> 6, r = e & 63;
+    const float x = r0 + r < L ? src[(int64_t)d * HL + r0 + r] : 0.f;
+    if (dr) dr[d * kSR + r] = x;
+    if (rd) rd[r * kSC + d] = x;
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__ q,
+                                                       const float* __restrict__ k,
+                                                       const float* __restrict__ v, int H, int N,
+                                                       int M, float* __restrict__ out,
+                                                       float* __restrict__ lse) {
+  __shared__ float Ks[kD * kSR];
+  __shared__ float Vs[kT * kSC];
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
+  const int qi = blockIdx.x * kT + pk::wave_id() * 16 + c;
+  const float* qb = q + ((int64_t)b * kD * H + h) * N;
+  const float* kb = k + ((int64_t)b * kD * H + h) * M;
+  const float* vb = v + ((int64_t)b * kD * H + h) * M;
+  float qr[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qr[s] = qi < N ? qb[(int64_t)(4 * s + g) * H * N + qi] * kScale : 0.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float m = -__builtin_huge_valf(), l = 0.f;
+  for (int k0 = 0; k0 < M; k0 += kT) {
+    __syncthreads();
+    stage(kb, H * M, M, k0, Ks, nullptr);
+    stage(vb, H * M, M, k0, nullptr, Vs);
+    __syncthreads();
+    f32x4 st[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) st[t] = mfma(Ks[(4 * s + g) * kSR + 16 * t + c], qr[s], st[t]);
+    }
+    float mt = -__builtin_huge_valf();
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (k0 + 16 * t + 4 * g + r >= M) st[t][r] = -__builtin_huge_valf();
+        mt = fmaxf(mt, st[t][r]);
+      }
+    mt = grp_max(mt);
+    const float mn = fmaxf(m, mt);
+    const float alpha = m == -__builtin_huge_valf() ? 0.f : expf(m - mn);
+    m = mn;
+    float ps = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = expf(st[t][r] - mn);
+        st[t][r] = p;
+        ps += p;
+      }
+    l = l * alpha + ps;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] *= alpha;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = mfma(Vs[(16 * t + 4 * g + r) * kSC + c], st[t][r], acc);
+  }
+  l = grp_sum(l);
+  if (qi < N) {
+    const float inv = 1.f / l;
+    float* ob = out + ((int64_t)b * kD * H + h) * N;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ob[(int64_t)(4 * g + r) * H * N + qi] = acc[r] * inv;
+    if (g == 0) lse[((int64_t)b * H + h) * N + qi] = m + logf(l);
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
+    const float* __restrict__ o, const float* __restrict__ dout, const float* __restrict__ lse,
+    int H, int N, int M, float* __restrict__ delta, float* __restrict__ dq) {
+  __shared__ float Ks[kD * kSR];
+  __shared__ float Vs[kD * kSR];
+  __shared__ float KT[kT * kSC];
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
+  const int qi = blockIdx.x * kT + pk::wave_id() * 16 + c;
+  const int64_t qoff = ((int64_t)b * kD * H + h) * N;
+  const float* kb = k + ((int64_t)b * kD * H + h) * M;
+  const float* vb = v + ((int64_t)b * kD * H + h) * M;
+  float qr[4], dor[4];
+  float dl = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int64_t a = qoff + (int64_t)(4 * s + g) * H * N + qi;
+    qr[s] = qi < N ? q[a] * kScale : 0.f;
+    dor[s] = qi < N ? dout[a] : 0.f;
+    dl = fmaf(dor[s], qi < N ? o[a] : 0.f, dl);
+  }
+  dl = grp_sum(dl);  // delta = sum_d dO * O for query qi
+  const float ls = qi < N ? lse[((int64_t)b * H + h) * N + qi] : __builtin_huge_valf();
+  if (qi < N && g == 0) delta[((int64_t)b * H + h) * N + qi] = dl;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < M; k0 += kT) {
+    __syncthreads();
+    stage(kb, H * M, M, k0, Ks, KT);
+    stage(vb, H * M, M, k0, Vs, nullptr);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        st = mfma(Ks[(4 * s + g) * kSR + 16 * t + c], qr[s], st);
+        dp = mfma(Vs[(4 * s + g) * kSR + 16 * t + c], dor[s], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = k0 + 16 * t + 4 * g + r < M ? expf(st[r] - ls) : 0.f;
+        const float ds = p * (dp[r] - dl);
+        acc = mfma(KT[(16 * t + 4 * g + r) * kSC + c], ds, acc);
+      }
+    }
+  }
+  if (qi < N) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dq[qoff + (int64_t)(4 * g + r) * H * N + qi] = acc[r] * kScale;
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
+    const float* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
+    int H, int N, int M, float* __restrict__ dk, float* __restrict__ dv) {
+  __shared__ float Qs[kD * kSR];
+  __shared__ float Os[kD * kSR];  // dO as [d][q]
+  __shared__ float QT[kT * kSC];
+  __shared__ float OT[kT * kSC];  // dO as [q][d]
+  __shared__ float Ls[kT], Ds[kT];
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
+  const int kj = blockIdx.x * kT + pk::wave_id() * 16 + c;
+  const int64_t koff = ((int64_t)b * kD * H + h) * M;
+  const float* qb = q + ((int64_t)b * kD * H + h) * N;
+  const float* gb = dout + ((int64_t)b * kD * H + h) * N;
+  const float* lb = lse + ((int64_t)b * H + h) * N;
+  const float* db = delta + ((int64_t)b * H + h) * N;
+  float kr[4], vr[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int64_t a = koff + (int64_t)(4 * s + g) * H * M + kj;
+    kr[s] = kj < M ? k[a] * kScale : 0.f;
+    vr[s] = kj < M ? v[a] : 0.f;
+  }
+  f32x4 dka = {0.f, 0.f, 0.f, 0.f}, dva = {0.f, 0.f, 0.f, 0.f};
+  for (int q0 = 0; q0 < N; q0 += kT) {
+    __syncthreads();
+    stage(qb, H * N, N, q0, Qs, QT);
+    stage(gb, H * N, N, q0, Os, OT);
+    if (threadIdx.x < kT) {
+      const int qq = q0 + threadIdx.x;
+      Ls[threadIdx.x] = qq < N ? lb[qq] : __builtin_huge_valf();  // exp(s - inf) = 0
+      Ds[threadIdx.x] = qq < N ? db[qq] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        st = mfma(Qs[(4 * s + g) * kSR + 16 * t + c], kr[s], st);  // S[q][key]
+        dp = mfma(Os[(4 * s + g) * kSR + 16 * t + c], vr[s], dp);  // dP[q][key]
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = 16 * t + 4 * g + r;
+        const float p = expf(st[r] - Ls[qq]);
+        const float ds = p * (dp[r] - Ds[qq]);
+        dva = mfma(OT[qq * kSC + c], p, dva);   // dV^T[d][key] += dO^T[d][q] P[q][key]
+        dka = mfma(QT[qq * kSC + c], ds, dka);  // dK^T[d][key] += Q^T[d][q] dS[q][key]
+      }
+    }
+  }
+  if (kj < M) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t a = koff + (int64_t)(4 * g + r) * H * M + kj;
+      dk[a] = dka[r] * kScale;
+      dv[a] = dva[r];
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int pk_attention_fwd(const float* q, const float* k, const float* v, int B, int D, int H,
+                                int N, int M, float* out, float* lse, void* stream) {
+  PK_REQUIRE(B >= 0 && H > 0 && N >= 0 && M >= 0 && D == kD);
+  if (B == 0 || N == 0) return PK_OK;
+  PK_REQUIRE(M > 0 && q && k && v && out && lse);
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3((N + kT - 1) / kT, H, B), dim3(256), 0, pk::as_stream(stream),
+                     q, k, v, H, N, M, out, lse);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_attention_bwd(const float* q, const float* k, const float* v, const float* out,
+                                const float* dout, const float* lse, int B, int D, int H, int N,
+                                int M, float* delta, float* dq, float* dk, float* dv, void* stream) {
+  PK_REQUIRE(B >= 0 && H > 0 && N >= 0 && M >= 0 && D == kD);
+  if (B == 0 || N == 0 || M == 0) return PK_OK;
+  PK_REQUIRE(q && k && v && out && dout && lse && delta && dq && dk && dv);
+  hipStream_t s = pk::as_stream(stream);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((N + kT - 1) / kT, H, B), dim3(256), 0, s, q, k, v, out, dout,
+                     lse, H, N, M, delta, dq);
+  PK_CHECK_LAUNCH();
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel, dim3((M + kT - 1) / kT, H, B), dim3(256), 0, s, q, k, v, dout, lse,
+                     delta, H, N, M, dk, dv);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}

@@ -96,6 +96,11 @@ __device__ __forceinline__ uint32_t f32_ordered(float f) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+// Inverse of f32_ordered.
+__device__ __forceinline__ float f32_unordered(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace pk

@@ -90,21 +90,145 @@ __global__ __launch_bounds__(NT) void fps_kernel(
     int bk = 0;
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
-      if (k >= kmax) break;  // block-uniform: crops smaller than the template bound skip work
-      const float dx = px[k] - cx;
-      const float dy = py[k] - cy;
-      const float dz = pz[k] - cz;
-      const float d = (dx * dx + dy * dy) + dz * dz;  // no contraction (TU flag)
-      pd[k] = fminf(pd[k], d);                        // == (d < pd ? d : pd): no NaNs
-      const bool gt = pd[k] > bd;                     // strict: lowest k wins ties
-      bd = gt ? pd[k] : bd;
-      bk = gt ? k : bk;
+      if (k < kmax) {  // block-uniform: crops smaller than the template bound skip work
+        const float dx = px[k] - cx;
+        const float dy = py[k] - cy;
+        const float dz = pz[k] - cz;
+        const float d = (dx * dx + dy * dy) + dz * dz;  // no contraction (TU flag)
+        pd[k] = fminf(pd[k], d);                        // == (d < pd ? d : pd): no NaNs
+        const bool gt = pd[k] > bd;                     // strict: lowest k wins ties
+        bd = gt ? pd[k] : bd;
+        bk = gt ? k : bk;
+      }
     }
     const bool valid = bd >= 0.f;
     const uint32_t bits = valid ? pk::f32_bits(bd) : 0u;
     const uint32_t gidx = valid ? (uint32_t)(tid + bk * NT) : 0xffffffffu;
     const uint32_t wmax = pk::wave_max_u32_s(bits);
     const uint32_t widx = pk::wave_min_u32_s(bits == wmax ? gidx : 0xffffffffu);
+    uint2* s = slots + (i & 1) * 16;
+    if (lane == 0) s[pk::wave_id()] = make_uint2(wmax, widx);
+    __syncthreads();
+    uint2 v = make_uint2(0u, 0xffffffffu);
+    if (lane < NW) v = s[lane];
+    const uint32_t m = pk::readlane(pk::row_max_u32(v.x), 0);
+    far = (int)pk::readlane(pk::row_min_u32(v.x == m ? v.y : 0xffffffffu), 0);
+  }
+}
+
+// Pruned variant (the production path). A wave's k-th slot column — indices
+// w*64 + lane + k*NT, 64 consecutive points, a short run of image row in the crop's
+// pixel order — is a bucket with a bounding box and its current max running distance
+// (lane k of the wave holds bucket k's box, max and argmax). Per iteration all buckets of
+// a wave are tested at once (one lane each): if the box lies at computed squared
+// distance lb from the new centroid with lb (1 - 2^-19) >= the bucket max, every point
+// of the bucket has fl(d) >= its running distance (fl(d) >= (1 - 5u) d_true, d_true >=
+// box distance, lb <= (1 + 5u) box distance; 2^-19 > 11u), so fminf leaves it unchanged
+// and the bucket is skipped bit-exactly. Only buckets near the centroid are updated; the
+// wave's best is a reduction over its bucket maxima.
+template <int NT, int PPT>
+__global__ __launch_bounds__(NT) void fps_pruned_kernel(
+    const float* __restrict__ xyz, const int64_t* __restrict__ offsets,
+    const int32_t* __restrict__ start, const int32_t* __restrict__ npoint,
+    int64_t* __restrict__ out, int out_stride) {
+  constexpr int NW = NT / pk::kWave;
+  static_assert(NW <= 16 && PPT <= pk::kWave, "bucket/slot layout limits");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = pk::lane_id();
+  const int64_t base = offsets[b];
+  const int n = (int)(offsets[b + 1] - base);
+  const int np = npoint[b];
+  const float* __restrict__ p = xyz + base * 3;
+
+  uint2* slots = reinterpret_cast<uint2*>(smem);  // [2][16] (bits, index)
+  float* sx = reinterpret_cast<float*>(smem + 2 * 16 * sizeof(uint2));
+  const int n_pad = (n + 3) & ~3;
+  float* sy = sx + n_pad;
+  float* sz = sy + n_pad;
+
+  float px[PPT], py[PPT], pz[PPT], pd[PPT];
+  // lane k: box of bucket k, its max running distance (as bits) and argmax
+  float bx0 = 0.f, bx1 = 0.f, by0 = 0.f, by1 = 0.f, bz0 = 0.f, bz1 = 0.f;
+  uint32_t bmb = 0u, bmi = 0xffffffffu;
+  bool bval = false;
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const int idx = tid + k * NT;
+    const bool ok = idx < n;
+    if (ok) {
+      px[k] = p[3 * idx + 0];
+      py[k] = p[3 * idx + 1];
+      pz[k] = p[3 * idx + 2];
+      pd[k] = 1e10f;
+      sx[idx] = px[k];
+      sy[idx] = py[k];
+      sz[idx] = pz[k];
+    } else {
+      px[k] = py[k] = pz[k] = 0.f;
+      pd[k] = -1.f;  // empty slot: min(-1, d >= 0) keeps it at -1, never selected
+    }
+    const uint64_t any = __ballot(ok);
+    if (any) {  // wave-uniform: bucket k has points
+      const float inf = __builtin_huge_valf();
+      const uint32_t x0 = pk::wave_min_u32_s(pk::f32_ordered(ok ? px[k] : inf));
+      const uint32_t x1 = pk::wave_max_u32_s(pk::f32_ordered(ok ? px[k] : -inf));
+      const uint32_t y0 = pk::wave_min_u32_s(pk::f32_ordered(ok ? py[k] : inf));
+      const uint32_t y1 = pk::wave_max_u32_s(pk::f32_ordered(ok ? py[k] : -inf));
+      const uint32_t z0 = pk::wave_min_u32_s(pk::f32_ordered(ok ? pz[k] : inf));
+      const uint32_t z1 = pk::wave_max_u32_s(pk::f32_ordered(ok ? pz[k] : -inf));
+      if (lane == k) {
+        bx0 = pk::f32_unordered(x0);
+        bx1 = pk::f32_unordered(x1);
+        by0 = pk::f32_unordered(y0);
+        by1 = pk::f32_unordered(y1);
+        bz0 = pk::f32_unordered(z0);
+        bz1 = pk::f32_unordered(z1);
+        bmb = pk::f32_bits(1e10f);
+        bmi = (uint32_t)(pk::wave_id() * pk::kWave + k * NT + (__ffsll((unsigned long long)any) - 1));
+        bval = true;
+      }
+    }
+  }
+  if (n <= 0 || np <= 0) return;
+  __syncthreads();
+
+  int far = start[b];
+  int64_t* __restrict__ o = out + (int64_t)b * out_stride;
+  for (int i = 0; i < np; ++i) {
+    if (tid == 0) o[i] = far;
+    const float cx = sx[far], cy = sy[far], cz = sz[far];
+    // one lane per bucket: can the centroid lower any running distance in it?
+    const float ddx = fmaxf(fmaxf(bx0 - cx, cx - bx1), 0.f);
+    const float ddy = fmaxf(fmaxf(by0 - cy, cy - by1), 0.f);
+    const float ddz = fmaxf(fmaxf(bz0 - cz, cz - bz1), 0.f);
+    const float lb = (ddx * ddx + ddy * ddy) + ddz * ddz;
+    const bool need = bval && !(lb * 0.99999809f >= __uint_as_float(bmb));
+    const uint64_t mask = __ballot(need);
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      if ((mask >> k) & 1ull) {  // wave-uniform (bit k is clear for empty buckets)
+        const float dx = px[k] - cx;
+        const float dy = py[k] - cy;
+        const float dz = pz[k] - cz;
+        const float d = (dx * dx + dy * dy) + dz * dz;  // no contraction (TU flag)
+        pd[k] = fminf(pd[k], d);
+        const bool valid = pd[k] >= 0.f;
+        const uint32_t bits = valid ? pk::f32_bits(pd[k]) : 0u;
+        const uint32_t wmax = pk::wave_max_u32_s(bits);
+        const uint32_t widx = pk::wave_min_u32_s(
+            valid && bits == wmax ? (uint32_t)(tid + k * NT) : 0xffffffffu);
+        if (lane == k) {
+          bmb = wmax;
+          bmi = widx;
+        }
+      }
+    }
+    const uint32_t bb = bval ? bmb : 0u;
+    const uint32_t wmax = PPT <= 16 ? pk::readlane(pk::row_max_u32(bb), 0) : pk::wave_max_u32_s(bb);
+    const uint32_t cand = bval && bb == wmax ? bmi : 0xffffffffu;
+    const uint32_t widx = PPT <= 16 ? pk::readlane(pk::row_min_u32(cand), 0) : pk::wave_min_u32_s(cand);
     uint2* s = slots + (i & 1) * 16;
     if (lane == 0) s[pk::wave_id()] = make_uint2(wmax, widx);
     __syncthreads();
@@ -123,12 +247,27 @@ int launch_fps(const float* xyz, const int64_t* offsets, const int32_t* start,
   if (nmax <= kFpsMaxLds) {
     const int n_pad = (nmax + 3) & ~3;
     const size_t lds = slots + 3 * (size_t)n_pad * sizeof(float);
-    hipLaunchKernelGGL((fps_kernel<NT, PPT, true>), dim3(B), dim3(NT), lds, s, xyz, offsets,
+    hipLaunchKernelGGL((fps_pruned_kernel<NT, PPT>), dim3(B), dim3(NT), lds, s, xyz, offsets,
                        start, npoint, out, out_stride);
   } else {
     hipLaunchKernelGGL((fps_kernel<NT, PPT, false>), dim3(B), dim3(NT), slots, s, xyz, offsets,
                        start, npoint, out, out_stride);
   }
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+// The unpruned kernel at a forced configuration (dev comparisons).
+template <int NT, int PPT>
+int launch_fps_plain(const float* xyz, const int64_t* offsets, const int32_t* start,
+                     const int32_t* npoint, int64_t* out, int out_stride, int B, int nmax,
+                     hipStream_t s) {
+  const size_t slots = 2 * 16 * sizeof(uint2);
+  const int n_pad = (nmax + 3) & ~3;
+  const size_t lds = slots + 3 * (size_t)n_pad * sizeof(float);
+  if (nmax > kFpsMaxLds) return PK_ERR_ARG;
+  hipLaunchKernelGGL((fps_kernel<NT, PPT, true>), dim3(B), dim3(NT), lds, s, xyz, offsets, start,
+                     npoint, out, out_stride);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
@@ -143,30 +282,30 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
   PK_REQUIRE(xyz && offsets && start && npoint && out);
   hipStream_t s = pk::as_stream(stream);
 #define PK_FPS(NT, PPT) return launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s)
-  if (nmax <= 512) PK_FPS(512, 1);
-  if (nmax <= 1024) PK_FPS(512, 2);
-  if (nmax <= 2048) PK_FPS(512, 4);
-  if (nmax <= 4096) PK_FPS(1024, 4);
-  if (nmax <= 8192) PK_FPS(1024, 8);
-  if (nmax <= 13312) PK_FPS(1024, 13);
+  if (nmax <= 1024) PK_FPS(256, 4);
+  if (nmax <= 2048) PK_FPS(256, 8);
+  if (nmax <= 4096) PK_FPS(256, 16);
+  if (nmax <= 8192) PK_FPS(512, 16);
+  if (nmax <= 13312) PK_FPS(512, 26);
   if (nmax <= 32768) PK_FPS(1024, 32);
 #undef PK_FPS
   return PK_ERR_ARG;  // > 32768 points per crop
 }
 
 // Development hook (not part of include/posekern.h): force the block size / points
-// per thread, for tools/kbench.py's configuration sweeps.
+// per thread, pruned (pruned = 1) or plain, for tools/kbench.py's configuration sweeps.
 extern "C" int pkdev_fps_cfg(const float* xyz, const int64_t* offsets, int B, int nmax,
                              const int32_t* start, const int32_t* npoint, int64_t* out,
-                             int out_stride, int nt, void* stream) {
+                             int out_stride, int nt, int pruned, void* stream) {
   hipStream_t s = pk::as_stream(stream);
   const int ppt = (nmax + nt - 1) / nt;
-#define PK_FPS(NT, PPT)                                                                   \
-  if (nt == NT && ppt <= PPT)                                                             \
-    return launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
+#define PK_FPS(NT, PPT)                                                                          \
+  if (nt == NT && ppt <= PPT)                                                                    \
+    return pruned ? launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s) \
+                  : launch_fps_plain<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
   PK_FPS(256, 4) PK_FPS(256, 8) PK_FPS(256, 16) PK_FPS(256, 32)
-  PK_FPS(512, 2) PK_FPS(512, 4) PK_FPS(512, 8) PK_FPS(512, 16)
-  PK_FPS(1024, 2) PK_FPS(1024, 4) PK_FPS(1024, 8)
+  PK_FPS(512, 2) PK_FPS(512, 4) PK_FPS(512, 8) PK_FPS(512, 16) PK_FPS(512, 26)
+  PK_FPS(1024, 2) PK_FPS(1024, 4) PK_FPS(1024, 8) PK_FPS(1024, 13)
 #undef PK_FPS
   return PK_ERR_ARG;
 }

@@ -70,32 +70,45 @@ __global__ __launch_bounds__(256) void spec_reduce_kernel(const float* __restric
 }
 
 // pass 2: coef = sum_s part; save raw (optional), scaled = E ⊙ coef; optional gt partial
-// gt[b, c] = -sum_k lambda_k E[k,c] saved[k,c] coef[k,c]. grid (B), block 256.
-__global__ __launch_bounds__(256) void spec_combine_kernel(const float* __restrict__ part, int S,
-                                                           const float* __restrict__ evals,
-                                                           const float* __restrict__ t,
-                                                           float* __restrict__ raw,
-                                                           float* __restrict__ scaled,
-                                                           const float* __restrict__ saved,
-                                                           float* __restrict__ gt) {
-  __shared__ float gsum[4][kKC];
+// gt[b, c] = -sum_k lambda_k E[k,c] saved[k,c] coef[k,c]. grid (B), block 1024: thread
+// (k-quad, c) sums its 4 rows over the S partials as 4 independent chains.
+__global__ __launch_bounds__(1024) void spec_combine_kernel(const float* __restrict__ part, int S,
+                                                            const float* __restrict__ evals,
+                                                            const float* __restrict__ t,
+                                                            float* __restrict__ raw,
+                                                            float* __restrict__ scaled,
+                                                            const float* __restrict__ saved,
+                                                            float* __restrict__ gt) {
+  __shared__ float gsum[16][kKC];
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int c = tid & 63, kq = tid >> 6;  // 4 groups of 16 k's
+  const int c = tid & 63, k0 = (tid >> 6) * 4;
+  const float* pb = part + (int64_t)b * S * kKC * kKC + k0 * kKC + c;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < S; ++s) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] += pb[(int64_t)s * kKC * kKC + i * kKC];
+  }
   float g = 0.f;
-  for (int k = kq; k < kKC; k += 4) {
-    float v = 0.f;
-    for (int s = 0; s < S; ++s) v += part[((int64_t)b * S + s) * kKC * kKC + k * kKC + c];
+  const float tc = t[c];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = k0 + i;
     const float lam = evals[b * kKC + k];
-    const float E = expf(-lam * t[c]);
+    const float E = expf(-lam * tc);
     const int64_t o = (int64_t)b * kKC * kKC + k * kKC + c;
-    if (raw) raw[o] = v;
-    scaled[o] = E * v;
-    if (gt) g = fmaf(-lam * E, saved[o] * v, g);
+    if (raw) raw[o] = v[i];
+    scaled[o] = E * v[i];
+    if (gt) g = fmaf(-lam * E, saved[o] * v[i], g);
   }
   if (gt) {
-    gsum[kq][c] = g;
+    gsum[tid >> 6][c] = g;
     __syncthreads();
-    if (kq == 0) gt[b * kKC + c] = (gsum[0][c] + gsum[1][c]) + (gsum[2][c] + gsum[3][c]);
+    if (tid < kKC) {
+      float a = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) a += gsum[q][c];
+      gt[b * kKC + c] = a;
+    }
   }
 }
 
@@ -165,7 +178,7 @@ extern "C" int pk_spectral_diffusion(const float* in, const float* mass, const f
   hipLaunchKernelGGL(spec_reduce_kernel, dim3(S, B), dim3(256), 0, s, in, mode == 0 ? mass : nullptr,
                      evecs, N, S, work);
   PK_CHECK_LAUNCH();
-  hipLaunchKernelGGL(spec_combine_kernel, dim3(B), dim3(256), 0, s, work, S, evals, t, raw, scaled,
+  hipLaunchKernelGGL(spec_combine_kernel, dim3(B), dim3(1024), 0, s, work, S, evals, t, raw, scaled,
                      mode == 1 ? saved : nullptr, mode == 1 ? gt : nullptr);
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(spec_expand_kernel, dim3((N + 63) / 64, B), dim3(256), 0, s, evecs, scaled,

@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
+from .layers import Linear
 
 
 class LearnedTimeDiffusion(nn.Module):
@@ -37,7 +38,7 @@ class MiniMLP(nn.Sequential):
         for i in range(len(layer_sizes) - 1):
             if dropout and i > 0:
                 self.add_module(name + "_mlp_layer_dropout_{:03d}".format(i), nn.Dropout(p=0.5))
-            self.add_module(name + "_mlp_layer_{:03d}".format(i), nn.Linear(layer_sizes[i], layer_sizes[i + 1]))
+            self.add_module(name + "_mlp_layer_{:03d}".format(i), Linear(layer_sizes[i], layer_sizes[i + 1]))
             if i + 2 != len(layer_sizes):
                 self.add_module(name + "_mlp_act_{:03d}".format(i), activation())
 
@@ -68,8 +69,8 @@ class DiffusionNet(nn.Module):
         self.last_activation = last_activation
         if mlp_hidden_dims is None:
             mlp_hidden_dims = [C_width, C_width]
-        self.first_lin = nn.Linear(C_in, C_width)
-        self.last_lin = nn.Linear(C_width, C_out)
+        self.first_lin = Linear(C_in, C_width)
+        self.last_lin = Linear(C_width, C_out)
         self.blocks = []
         for i_block in range(N_block):
             blk = DiffusionNetBlock(C_width, mlp_hidden_dims, dropout=dropout, diffusion_method=diffusion_method,

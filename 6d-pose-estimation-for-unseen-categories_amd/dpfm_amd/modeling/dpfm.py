@@ -17,6 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from ..layers import Conv1d, Linear
 from ..dpfm_utils import get_mask_batched
 
 
@@ -25,7 +26,7 @@ def MLP(channels: list, do_bn=True):
     n = len(channels)
     layers = []
     for i in range(1, n):
-        layers.append(nn.Conv1d(channels[i - 1], channels[i], kernel_size=1, bias=True))
+        layers.append(Conv1d(channels[i - 1], channels[i], kernel_size=1, bias=True))
         if i < (n - 1):
             if do_bn:
                 layers.append(nn.InstanceNorm1d(channels[i]))
@@ -45,7 +46,7 @@ class MultiHeadedAttention(nn.Module):
         assert d_model % num_heads == 0
         self.dim = d_model // num_heads
         self.num_heads = num_heads
-        self.merge = nn.Conv1d(d_model, d_model, kernel_size=1)
+        self.merge = Conv1d(d_model, d_model, kernel_size=1)
         self.proj = nn.ModuleList([deepcopy(self.merge) for _ in range(3)])
 
     def forward(self, query, key, value):
@@ -86,8 +87,8 @@ class CrossAttentionRefinementNet(nn.Module):
         self.n_in = n_in
         self.cross_sampling_ratio = cross_sampling_ratio
         self.layers = nn.ModuleList([AttentionalPropagation(gnn_dim + additional_dim, num_head) for _ in range(n_layers)])
-        self.first_lin = nn.Linear(n_in, gnn_dim + additional_dim)
-        self.last_lin = nn.Linear(gnn_dim + additional_dim, n_in + additional_dim)
+        self.first_lin = Linear(n_in, gnn_dim + additional_dim)
+        self.last_lin = Linear(gnn_dim + additional_dim, n_in + additional_dim)
         self.overlap_predictor = OverlapPredictorNet(overlap_feat_dim=overlap_feat_dim)
 
     def forward(self, coords0, coords1, features_x, features_y, batch=None):
@@ -109,9 +110,9 @@ class OverlapPredictorNet(nn.Module):
     def __init__(self, overlap_feat_dim=32):
         super().__init__()
         self.overlap_score_net = nn.Sequential(
-            nn.Linear(overlap_feat_dim, overlap_feat_dim, bias=True),
+            Linear(overlap_feat_dim, overlap_feat_dim, bias=True),
             nn.ReLU(True),
-            nn.Linear(overlap_feat_dim, 1, bias=True),
+            Linear(overlap_feat_dim, 1, bias=True),
             nn.Sigmoid(),
         )
 

@@ -268,12 +268,65 @@ def fmap_solve(AAt: torch.Tensor, BAt: torch.Tensor, D: torch.Tensor, lambda_: f
 # ------------------------------------------------------------------------------ H8 attention
 
 
+class _Attention(torch.autograd.Function):
+    """softmax(q^T k / sqrt(dim)) v per (crop, head), fused (pk_attention_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v):
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        B, D, H, N = q.shape
+        M = k.shape[3]
+        out = torch.empty_like(q)
+        lse = torch.empty((B, H, N), dtype=torch.float32, device=q.device)
+        call("pk_attention_fwd", ptr(q), ptr(k), ptr(v), B, D, H, N, M, ptr(out), ptr(lse), _lib.stream(q.device))
+        ctx.save_for_backward(q, k, v, out, lse)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, lse = ctx.saved_tensors
+        dout = dout.contiguous()
+        B, D, H, N = q.shape
+        M = k.shape[3]
+        delta = torch.empty((B, H, N), dtype=torch.float32, device=q.device)
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        call("pk_attention_bwd", ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse), B, D, H, N, M, ptr(delta),
+             ptr(dq), ptr(dk), ptr(dv), _lib.stream(q.device))
+        return dq, dk, dv
+
+
 def attention(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor) -> torch.Tensor:
-    """softmax(q^T k / sqrt(d)) v for [B, d, heads, N] tensors (modeling/dpfm.py:29-37)."""
-    dim = query.shape[1]
-    scores = torch.einsum("bdhn,bdhm->bhnm", query, key) / dim ** 0.5
-    prob = torch.nn.functional.softmax(scores, dim=-1)
-    return torch.einsum("bhnm,bdhm->bdhn", prob, value)
+    """softmax(q^T k / sqrt(d)) v for [B, d, heads, N] fp32 tensors (modeling/dpfm.py:29-37),
+    fused in HIP (pk_attention_fwd/_bwd); the score matrix never reaches HBM."""
+    if query.shape[1] != 16:
+        raise _lib.PoseKernError("attention kernel is built for dim = 16 (gnn_dim 32, 2 heads)")
+    if query.dtype != torch.float32:
+        raise _lib.PoseKernError("attention kernel computes in fp32")
+    return _Attention.apply(query, key, value)
+
+
+# ------------------------------------------------------------------------------ per-point layers
+
+
+def linear_wgrad(x: torch.Tensor, dy: torch.Tensor, channels_first: bool, want_bias: bool = True):
+    """(dW [O, I], db [O] or None) of y = W x + b over every point (pk_linear_wgrad).
+    channels_first=False: x [..., I], dy [..., O]; True: x [B, I, N], dy [B, O, N]."""
+    x, dy = x.contiguous(), dy.contiguous()
+    if channels_first:
+        Bn, I, N = x.shape
+        O = dy.shape[1]
+        R, layout = Bn * N, 1
+    else:
+        I, O = x.shape[-1], dy.shape[-1]
+        R, N, layout = x.numel() // I, 0, 0
+    dev = x.device
+    S = (R + 127) // 128
+    work = torch.empty((max(S, 1) * (O * I + O),), dtype=torch.float32, device=dev)
+    dw = torch.empty((O, I), dtype=torch.float32, device=dev)
+    db = torch.empty((O,), dtype=torch.float32, device=dev) if want_bias else None
+    call("pk_linear_wgrad", ptr(x), ptr(dy), layout, int(R), I, O, int(N), ptr(work), ptr(dw), ptr(db),
+         _lib.stream(dev))
+    return dw, db
 
 
 # ------------------------------------------------------------------------------ H10-H13, H15

@@ -134,6 +134,27 @@ int pk_fmap_solve(const float* AAt, const float* BAt, const float* D, float lamb
 int pk_fmap_solve_backward(const float* AAt, const float* BAt, const float* D, float lambda, int B,
                            int K, const float* G, float* dBAt, float* dAAt_part, void* stream);
 
+/* H8 fused multi-head attention. Replaces modeling/dpfm.py:29-37 `attention` (einsum
+ * scores / sqrt(dim), softmax over keys, einsum with values) without materialising the
+ * [B, heads, N, M] score/probability tensors. fp32, dim D = 16 only.
+ *   q f32 [B, D, H, N], k / v f32 [B, D, H, M] (heads interleaved as the reference's
+ *   view(B, dim, heads, N) of a [B, D*H, N] projection), out f32 [B, D, H, N],
+ *   lse f32 [B, H, N] log-sum-exp of the scaled scores per query (for the backward).
+ * Backward: dout like out; delta f32 [B, H, N] scratch; dq like q, dk / dv like k. */
+int pk_attention_fwd(const float* q, const float* k, const float* v, int B, int D, int H, int N,
+                     int M, float* out, float* lse, void* stream);
+int pk_attention_bwd(const float* q, const float* k, const float* v, const float* out,
+                     const float* dout, const float* lse, int B, int D, int H, int N, int M,
+                     float* delta, float* dq, float* dk, float* dv, void* stream);
+
+/* Weight/bias gradients of the per-point layers of H7/H8 (DiffusionNet Linear layers,
+ * models/dpfm.py:22-30; refinement Conv1d(k=1), modeling/dpfm.py:16-26,45-54,82-95):
+ * dw[o,i] = sum_r dy[r,o] x[r,i], db[o] = sum_r dy[r,o] over all R = B*N points.
+ *   layout 0: x [R, I], dy [R, O] row-major; layout 1: x [R/N, I, N], dy [R/N, O, N]
+ *   I, O <= 128; work f32 [ceil(R/128) * (O*I + O)]; db may be NULL. */
+int pk_linear_wgrad(const float* x, const float* dy, int layout, int64_t R, int I, int O, int N,
+                    float* work, float* dw, float* db, void* stream);
+
 /* H10 / H11 correspondence head. Replaces fmap2pointmap_solvers/naive.py:20-34
  * (topk = 1: dist.argmin(dim=-2)) and spacial_filtering.py:19-38 (topk = 5: the first 5
  * rows of dist.sort(dim=-2)) with dist = cdist(evecs_x[:, :30] @ C^T, evecs_y[:, :30]).

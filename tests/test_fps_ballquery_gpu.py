@@ -15,13 +15,23 @@ def _packed(arrs, dtype, device):
     return torch.from_numpy(flat).to(device), ops.packed_offsets([a.shape[0] for a in arrs], device)
 
 
-def test_fps_ragged_batch_bitexact(device, coracle):
+@pytest.mark.parametrize("sizes,grid", [
+    ([1, 7, 100, 1024, 2049, 4500, 9000, 13000, 14000], False),  # > 13312: unpruned, global reads
+    ([1, 7, 100, 1024, 2049, 4500, 9000, 13000], False),         # pruned buckets, random order
+    ([500, 3000, 8000, 13312], True),                             # pruned, spatially coherent runs
+])
+def test_fps_ragged_batch_bitexact(device, coracle, sizes, grid):
     from dpfm_amd import ops
     rng = np.random.default_rng(0)
-    sizes = [1, 7, 100, 1024, 2049, 4500, 9000, 13000, 14000]
     crops = []
     for n in sizes:
-        x = (rng.normal(size=(n, 3)) * 6 + np.array([1.0, -2.0, 110.0])).astype(np.float32)
+        if grid:  # row-major samples of a bumpy surface, like back-projected pixels
+            w = int(np.ceil(np.sqrt(n)))
+            v, u = np.divmod(np.arange(n), w)
+            z = 100 + 3 * np.sin(u / 9.0) * np.cos(v / 7.0)
+            x = np.stack([(u - w / 2) * 0.15, (v - w / 2) * 0.15, z], 1).astype(np.float32)
+        else:
+            x = (rng.normal(size=(n, 3)) * 6 + np.array([1.0, -2.0, 110.0])).astype(np.float32)
         if n > 50:  # duplicates -> ties resolved to the lowest index
             x[rng.integers(0, n, n // 10)] = x[rng.integers(0, n, n // 10)]
         crops.append(x)

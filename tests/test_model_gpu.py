@@ -77,6 +77,60 @@ def test_fmap_solve_fwd_bwd(device):
     torch.testing.assert_close(Bd.grad.cpu().double(), Br.grad, rtol=1e-3, atol=1e-3 * float(Br.grad.abs().max()))
 
 
+@pytest.mark.parametrize("shape,channels_first", [((32768, 128, 64), False), ((1000, 3, 64), False),
+                                                  ((4, 7, 32, 1), False), ((3, 32, 300, 64), True),
+                                                  ((2, 64, 1024, 32), True), ((0, 8, 8), False)])
+def test_linear_wgrad(device, shape, channels_first):
+    """pk_linear_wgrad vs fp64: |err| <= 1e-5 * sum_r |dy||x| (the fp32 summation bound)."""
+    from dpfm_amd import ops
+    g = torch.Generator().manual_seed(sum(shape))
+    if channels_first:
+        Bn, I, N, O = shape
+        x = torch.randn(Bn, I, N, generator=g)
+        dy = torch.randn(Bn, O, N, generator=g)
+        exp_w = torch.einsum("bon,bin->oi", dy.double(), x.double())
+        bound = torch.einsum("bon,bin->oi", dy.double().abs(), x.double().abs())
+        exp_b, bnd_b = dy.double().sum((0, 2)), dy.double().abs().sum((0, 2))
+    else:
+        *lead, I, O = shape
+        x = torch.randn(*lead, I, generator=g)
+        dy = torch.randn(*lead, O, generator=g)
+        x2, d2 = x.reshape(-1, I).double(), dy.reshape(-1, O).double()
+        exp_w, bound = d2.t() @ x2, d2.abs().t() @ x2.abs()
+        exp_b, bnd_b = d2.sum(0), d2.abs().sum(0)
+    dw, db = ops.linear_wgrad(x.to(device), dy.to(device), channels_first=channels_first)
+    assert (dw.cpu().double() - exp_w).abs().le(1e-5 * bound + 1e-30).all()
+    assert (db.cpu().double() - exp_b).abs().le(1e-5 * bnd_b + 1e-30).all()
+
+
+@pytest.mark.parametrize("N,M", [(300, 200), (1024, 1024), (64, 1), (17, 130)])
+def test_attention_fwd_bwd(device, N, M):
+    """H8 fused attention vs modeling/dpfm.py:29-37 evaluated in fp64 (truth) and fp32:
+    out and dq/dk/dv within 3x the fp32 reference's own error + 1e-6 of scale."""
+    from dpfm_amd import ops
+    g = torch.Generator().manual_seed(N * 7 + M)
+    B, D, H = 3, 16, 2
+    q = torch.randn(B, D, H, N, generator=g) * 2
+    k = torch.randn(B, D, H, M, generator=g) * 2
+    v = torch.randn(B, D, H, M, generator=g)
+    go = torch.randn(B, D, H, N, generator=g)
+
+    def ref(q, k, v):
+        scores = torch.einsum("bdhn,bdhm->bhnm", q, k) / D ** 0.5
+        return torch.einsum("bhnm,bdhm->bdhn", torch.nn.functional.softmax(scores, dim=-1), v)
+
+    res = []
+    for dt, dev in ((torch.float64, "cpu"), (torch.float32, "cpu"), (torch.float32, device)):
+        ins = [x.detach().clone().to(device=dev, dtype=dt).requires_grad_() for x in (q, k, v)]
+        out = (ops.attention if dev == device else ref)(*ins)
+        (out * go.to(device=dev, dtype=dt)).sum().backward()
+        res.append([t.detach().cpu().double() for t in (out, *(x.grad for x in ins))])
+    scale = max(t.abs().max().item() for t in res[0])  # M = 1: dk vanishes exactly in truth
+    for name, t, r, d in zip(["out", "dq", "dk", "dv"], *res):
+        e_ref, e_mine = (r - t).abs().max().item(), (d - t).abs().max().item()
+        assert e_mine <= 3 * e_ref + 1e-6 * (1 + scale), (name, e_mine, e_ref)
+
+
 @pytest.mark.parametrize("N1,N2", [(256, 256), (300, 200)])
 def test_dpfmnet_matches_oracle(device, N1, N2):
     """Forward outputs and parameter gradients vs the oracle evaluated in fp64 (the truth).

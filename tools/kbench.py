@@ -21,24 +21,38 @@ def timeit(fn, iters=20, warm=3):
     return e0.elapsed_time(e1) / iters
 
 rng = np.random.default_rng(0)
-for B, nin, npt in [(32, 2000, 1024), (32, 4000, 1024), (32, 8000, 1024), (256, 8000, 2048)]:
-    x = torch.from_numpy((rng.normal(size=(B * nin, 3)) * 6 + 100).astype(np.float32)).to(dev)
-    off = ops.packed_offsets([nin] * B, dev)
+from dpfm_amd import _lib  # noqa: E402
+from dpfm_amd.pipeline import make_frame_batch  # noqa: E402
+
+L = _lib.lib()
+# FPS on real crop-formation output (pixel-ordered SOR survivors of synthetic frames)
+for B, npt in [(32, 1024)]:
+    fb, _ = make_frame_batch(B, 1024, 1024, seed=0, device=dev)
+    bp = ops.backproject(fb.depth, fb.mask, fb.K, fb.cam_scale, cap=B * fb.max_pixels)
+    so = ops.sor(bp["xyz"], bp["off"], fb.max_pixels, 20, 0.3, pix=bp["pix"], idxmap=bp["idxmap"], K=fb.K)
+    ms = timeit(lambda: ops.backproject(fb.depth, fb.mask, fb.K, fb.cam_scale, cap=B * fb.max_pixels), iters=5, warm=1)
+    print(f"backproject B={B}: {ms:.3f} ms")
+    ms = timeit(lambda: ops.sor(bp["xyz"], bp["off"], fb.max_pixels, 20, 0.3, pix=bp["pix"], idxmap=bp["idxmap"], K=fb.K),
+                iters=5, warm=1)
+    ms0 = timeit(lambda: ops.sor(bp["xyz"], bp["off"], fb.max_pixels, 20, 0.3, pix=bp["pix"], idxmap=bp["idxmap"]),
+                 iters=3, warm=1)
+    print(f"sor B={B} n={(bp['off'][1:] - bp['off'][:-1]).tolist()[:4]}...: {ms:.3f} ms with K box, {ms0:.3f} ms 5x5 only")
+    x, off = so["xyz32"], so["off"]
+    nin = int((off[1:] - off[:-1]).max())
     st = torch.zeros(B, dtype=torch.int32, device=dev)
     npv = torch.full((B,), npt, dtype=torch.int32, device=dev)
-    ms = timeit(lambda: ops.fps_packed(x, off, nin, st, npv, npt), iters=5, warm=1)
-    print(f"fps B={B} n_in={nin} npoint={npt}: {ms:.3f} ms  ({ms*1e3/npt:.3f} us/iter)")
-    import ctypes
-    from dpfm_amd import _lib
-    L = _lib.lib()
-    out = torch.zeros((B, npt), dtype=torch.int64, device=dev)
     ref = ops.fps_packed(x, off, nin, st, npv, npt)
-    for nt in (256, 512, 1024):
-        f = lambda: L.pkdev_fps_cfg(_lib.ptr(x), _lib.ptr(off), B, nin, _lib.ptr(st), _lib.ptr(npv), _lib.ptr(out), npt, nt, _lib.stream(dev))
-        if f() != 0:
-            continue
-        ms = timeit(f, iters=5, warm=1)
-        print(f"   nt={nt}: {ms:.3f} ms ({ms*1e3/npt:.3f} us/iter) same={torch.equal(out, ref)}")
+    ms = timeit(lambda: ops.fps_packed(x, off, nin, st, npv, npt), iters=5, warm=1)
+    print(f"fps (dispatch) B={B} n_in<={nin} npoint={npt}: {ms:.3f} ms  ({ms*1e3/npt:.3f} us/iter)")
+    out = torch.zeros((B, npt), dtype=torch.int64, device=dev)
+    for pruned in (1, 0):
+        for nt in (256, 512, 1024):
+            f = lambda: L.pkdev_fps_cfg(_lib.ptr(x), _lib.ptr(off), B, nin, _lib.ptr(st), _lib.ptr(npv), _lib.ptr(out),
+                                        npt, nt, pruned, _lib.stream(dev))
+            if f() != 0:
+                continue
+            ms = timeit(f, iters=5, warm=1)
+            print(f"   pruned={pruned} nt={nt}: {ms:.3f} ms ({ms*1e3/npt:.3f} us/iter) same={torch.equal(out, ref)}")
 
 for B, N in [(32, 1024), (256, 2048)]:
     cad = torch.from_numpy(rng.normal(size=(B * N, 3)) * 5).to(dev)
