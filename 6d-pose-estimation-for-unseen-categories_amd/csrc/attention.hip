@@ -6,8 +6,12 @@
 //     out    = einsum('bhnm,bdhm->bdhn', prob, v)
 // The reference materialises scores and prob ([B, heads, N, M] fp32, twice per layer);
 // here they live only in registers (online softmax, FlashAttention-2 style), in fp32:
-// products on the f32 MFMA (v_mfma_f32_16x16x4_f32), exp via the accurate expf.
-// dim = 16 (gnn_dim 32 / 2 heads, config/dpfm_orig.yaml), so 1/sqrt(dim) = 0.25 exactly.
+// products on the f32 MFMA (v_mfma_f32_16x16x4_f32). dim = 16 (gnn_dim 32 / 2 heads,
+// config/dpfm_orig.yaml), so 1/sqrt(dim) = 0.25. Scores are formed in log2 units (one
+// operand pre-scaled by 0.25 log2(e)) so the softmax exponentials are single v_exp_f32
+// (exp2) instructions; the saved lse is a log2-sum-exp2 (internal to these kernels).
+// K/V (resp. Q/dO) tiles are double-buffered: the next tile's global loads are in
+// flight while the current tile is contracted.
 //
 // MFMA lane maps (16x16x4): A[i = l & 15][k = l >> 4], B[k = l >> 4][j = l & 15],
 // D[row = 4 (l >> 4) + r][col = l & 15]. A 16x16 D tile of S^T = K Q^T leaves lane l
@@ -16,7 +20,7 @@
 //
 // Kernels (one workgroup = 4 waves x 16 rows = 64 rows of one (crop, head)):
 //   attn_fwd_kernel     queries; streams 64-key tiles of K, V through LDS; writes out
-//                       and lse = m + log(sum) per query (saved for the backward)
+//                       and lse = m + log2(sum) per query (saved for the backward)
 //   attn_bwd_dq_kernel  queries; delta = rowsum(dO * O) then dQ = 0.25 dS K
 //   attn_bwd_dkv_kernel keys; streams 64-query tiles of Q, dO; dV = P^T dO,
 //                       dK = 0.25 dS^T Q with dS = P (dP - delta), dP = dO V^T
@@ -29,7 +33,7 @@ constexpr int kD = 16;       // head dim
 constexpr int kT = 64;       // rows per tile / per workgroup
 constexpr int kSR = 80;      // LDS stride of [d][row] arrays (bank-conflict-free MFMA reads)
 constexpr int kSC = 20;      // LDS stride of [row][d] arrays
-constexpr float kScale = 0.25f;
+constexpr float kScale = 0.25f;  // 1 / sqrt(dim) for the gradients
 
 __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -45,15 +49,36 @@ __device__ __forceinline__ float grp_sum(float v) {
   return v + __shfl_xor(v, 32);
 }
 
-// Stage a 64-row tile of a [D, H, L] slab (row index contiguous) into LDS as [d][row]
-// (stride kSR) and/or [row][d] (stride kSC); rows >= L read as 0.
-__device__ __forceinline__ void stage(const float* __restrict__ src, int HL, int L, int r0,
-                                      float* __restrict__ dr, float* __restrict__ rd) {
-  for (int e = threadIdx.x; e < kD * kT; e += 256) {
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kScale2 = 0.25f * kLog2e;  // scores in log2 units
+
+__device__ __forceinline__ float exp2_(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// A 64-row tile of a [D, H, L] slab (row index contiguous), 4 elements per thread:
+// element e = tid + 256 j -> (d = e >> 6, row = e & 63); rows >= L read as 0.
+struct Tile {
+  float x[4];
+};
+
+__device__ __forceinline__ Tile load_tile(const float* __restrict__ src, int HL, int L, int r0) {
+  Tile t;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = threadIdx.x + 256 * j;
     const int d = e >> 6, r = e & 63;
-    const float x = r0 + r < L ? src[(int64_t)d * HL + r0 + r] : 0.f;
-    if (dr) dr[d * kSR + r] = x;
-    if (rd) rd[r * kSC + d] = x;
+    t.x[j] = r0 + r < L ? src[(int64_t)d * HL + r0 + r] : 0.f;
+  }
+  return t;
+}
+
+// into LDS as [d][row] (stride kSR) and/or [row][d] (stride kSC)
+__device__ __forceinline__ void store_tile(const Tile& t, float* __restrict__ dr, float* __restrict__ rd) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = threadIdx.x + 256 * j;
+    const int d = e >> 6, r = e & 63;
+    if (dr) dr[d * kSR + r] = t.x[j];
+    if (rd) rd[r * kSC + d] = t.x[j];
   }
 }
 
@@ -72,14 +97,19 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
   const float* vb = v + ((int64_t)b * kD * H + h) * M;
   float qr[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) qr[s] = qi < N ? qb[(int64_t)(4 * s + g) * H * N + qi] * kScale : 0.f;
+  for (int s = 0; s < 4; ++s) qr[s] = qi < N ? qb[(int64_t)(4 * s + g) * H * N + qi] * kScale2 : 0.f;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   float m = -__builtin_huge_valf(), l = 0.f;
+  Tile kt = load_tile(kb, H * M, M, 0), vt = load_tile(vb, H * M, M, 0);
   for (int k0 = 0; k0 < M; k0 += kT) {
     __syncthreads();
-    stage(kb, H * M, M, k0, Ks, nullptr);
-    stage(vb, H * M, M, k0, nullptr, Vs);
+    store_tile(kt, Ks, nullptr);
+    store_tile(vt, nullptr, Vs);
     __syncthreads();
+    if (k0 + kT < M) {  // next tile in flight during this one
+      kt = load_tile(kb, H * M, M, k0 + kT);
+      vt = load_tile(vb, H * M, M, k0 + kT);
+    }
     f32x4 st[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -97,14 +127,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
       }
     mt = grp_max(mt);
     const float mn = fmaxf(m, mt);
-    const float alpha = m == -__builtin_huge_valf() ? 0.f : expf(m - mn);
+    const float alpha = m == -__builtin_huge_valf() ? 0.f : exp2_(m - mn);
     m = mn;
     float ps = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = expf(st[t][r] - mn);
+        const float p = exp2_(st[t][r] - mn);
         st[t][r] = p;
         ps += p;
       }
@@ -122,7 +152,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
     float* ob = out + ((int64_t)b * kD * H + h) * N;
 #pragma unroll
     for (int r = 0; r < 4; ++r) ob[(int64_t)(4 * g + r) * H * N + qi] = acc[r] * inv;
-    if (g == 0) lse[((int64_t)b * H + h) * N + qi] = m + logf(l);
+    if (g == 0) lse[((int64_t)b * H + h) * N + qi] = m + log2f(l);
   }
 }
 
@@ -144,7 +174,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int64_t a = qoff + (int64_t)(4 * s + g) * H * N + qi;
-    qr[s] = qi < N ? q[a] * kScale : 0.f;
+    qr[s] = qi < N ? q[a] * kScale2 : 0.f;
     dor[s] = qi < N ? dout[a] : 0.f;
     dl = fmaf(dor[s], qi < N ? o[a] : 0.f, dl);
   }
@@ -152,11 +182,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
   const float ls = qi < N ? lse[((int64_t)b * H + h) * N + qi] : __builtin_huge_valf();
   if (qi < N && g == 0) delta[((int64_t)b * H + h) * N + qi] = dl;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  Tile kt = load_tile(kb, H * M, M, 0), vt = load_tile(vb, H * M, M, 0);
   for (int k0 = 0; k0 < M; k0 += kT) {
     __syncthreads();
-    stage(kb, H * M, M, k0, Ks, KT);
-    stage(vb, H * M, M, k0, Vs, nullptr);
+    store_tile(kt, Ks, KT);
+    store_tile(vt, Vs, nullptr);
     __syncthreads();
+    if (k0 + kT < M) {
+      kt = load_tile(kb, H * M, M, k0 + kT);
+      vt = load_tile(vb, H * M, M, k0 + kT);
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
@@ -167,7 +202,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = k0 + 16 * t + 4 * g + r < M ? expf(st[r] - ls) : 0.f;
+        const float p = k0 + 16 * t + 4 * g + r < M ? exp2_(st[r] - ls) : 0.f;
         const float ds = p * (dp[r] - dl);
         acc = mfma(KT[(16 * t + 4 * g + r) * kSC + c], ds, acc);
       }
@@ -200,32 +235,37 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int64_t a = koff + (int64_t)(4 * s + g) * H * M + kj;
-    kr[s] = kj < M ? k[a] * kScale : 0.f;
+    kr[s] = kj < M ? k[a] * kScale2 : 0.f;
     vr[s] = kj < M ? v[a] : 0.f;
   }
   f32x4 dka = {0.f, 0.f, 0.f, 0.f}, dva = {0.f, 0.f, 0.f, 0.f};
+  Tile qt = load_tile(qb, H * N, N, 0), gt = load_tile(gb, H * N, N, 0);
   for (int q0 = 0; q0 < N; q0 += kT) {
     __syncthreads();
-    stage(qb, H * N, N, q0, Qs, QT);
-    stage(gb, H * N, N, q0, Os, OT);
+    store_tile(qt, Qs, QT);
+    store_tile(gt, Os, OT);
     if (threadIdx.x < kT) {
       const int qq = q0 + threadIdx.x;
-      Ls[threadIdx.x] = qq < N ? lb[qq] : __builtin_huge_valf();  // exp(s - inf) = 0
+      Ls[threadIdx.x] = qq < N ? lb[qq] : __builtin_huge_valf();  // exp2(s - inf) = 0
       Ds[threadIdx.x] = qq < N ? db[qq] : 0.f;
     }
     __syncthreads();
+    if (q0 + kT < N) {
+      qt = load_tile(qb, H * N, N, q0 + kT);
+      gt = load_tile(gb, H * N, N, q0 + kT);
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        st = mfma(Qs[(4 * s + g) * kSR + 16 * t + c], kr[s], st);  // S[q][key]
+        st = mfma(Qs[(4 * s + g) * kSR + 16 * t + c], kr[s], st);  // S[q][key] (log2 units)
         dp = mfma(Os[(4 * s + g) * kSR + 16 * t + c], vr[s], dp);  // dP[q][key]
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = 16 * t + 4 * g + r;
-        const float p = expf(st[r] - Ls[qq]);
+        const float p = exp2_(st[r] - Ls[qq]);
         const float ds = p * (dp[r] - Ds[qq]);
         dva = mfma(OT[qq * kSC + c], p, dva);   // dV^T[d][key] += dO^T[d][q] P[q][key]
         dka = mfma(QT[qq * kSC + c], ds, dka);  // dK^T[d][key] += Q^T[d][q] dS[q][key]

@@ -152,111 +152,196 @@ __global__ __launch_bounds__(256) void ir_kernel(const int64_t* __restrict__ pai
 }
 
 // ---------------------------------------------------------------- C_gt (normal equations)
+// Least squares A X = Bm with A = e2[P[:,1], :30], Bm = e1[P[:,0], :30] (utils.py:67-79)
+// via the normal equations G X = H in fp64, G = A^T A, H = A^T Bm:
+//   G = sum_j cnt_j e2[j]^T e2[j]   (cnt_j = pairs with crop index j: V2 rows, not P)
+//   H = sum_p e2[j_p]^T e1[i_p]     (64-pair slices, one partial per slice)
+// fp32 inputs, fp64 products and sums; partials reduced in slice order (deterministic),
+// then one wave per crop runs Gauss-Jordan with partial pivoting, rows in registers.
 constexpr int kF = 30;
+constexpr int kCgtRows = 64;   // pairs (H) or crop rows (G) per partial slice
+constexpr int kFF = kF * kF;
 
-constexpr int kCgtPairs = 256;  // pairs per partial-sum block
-constexpr int kGH = kF * 2 * kF;   // 30 x 60 entries of [G | H]
+// grid (ceil(ldp/256), B): cnt[b, j] += 1 for every pair of crop b (integer atomics).
+__global__ __launch_bounds__(256) void cgt_count_kernel(const int64_t* __restrict__ pairs, int ldp,
+                                                        const int64_t* __restrict__ npairs, int V2max,
+                                                        int32_t* __restrict__ cnt) {
+  const int b = blockIdx.y;
+  const int64_t n = npairs[b] < ldp ? npairs[b] : ldp;
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  const int64_t j = pairs[((int64_t)b * ldp + p) * 2 + 1];
+  atomicAdd(&cnt[(int64_t)b * V2max + j], 1);
+}
 
-// grid (ceil(ldp / 256), B), block 256: partial [G | H] = A^T [A | Bm] over 256 pairs of
-// crop b (A = e2[p1], Bm = e1[p0], fp32 inputs, exact products, fp64 accumulation).
+// grid (SH + SG, B), block 256. Slice s < SH: H partial over pairs [64 s, 64 s + 64);
+// s >= SH: G partial over crop rows [64 (s - SH), ...). Rows staged in LDS as fp64
+// (u = e2 row, v = e1 row or cnt * e2 row); wave w takes rows w, w+4, ...; lane
+// (kb, lb) owns the 4 x 4 block rows 4kb.., cols 4lb..; waves combined in fixed order.
 __global__ __launch_bounds__(256) void cgt_partial_kernel(const int64_t* __restrict__ pairs, int ldp,
                                                           const int64_t* __restrict__ npairs,
                                                           const float* __restrict__ e1, int ld1, int V1max,
                                                           const float* __restrict__ e2, int ld2, int V2max,
-                                                          double* __restrict__ part) {
-  __shared__ float r1[64][kF], r2[64][kF];
-  const int b = blockIdx.y, s = blockIdx.x, tid = threadIdx.x;
-  const int64_t n = npairs[b] < ldp ? npairs[b] : ldp;
-  const int64_t p_begin = (int64_t)s * kCgtPairs;
-  if (p_begin >= n) return;
-  const int64_t p_end = min(n, p_begin + kCgtPairs);
-  double acc[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) acc[q] = 0.0;
-  const int64_t* P = pairs + (int64_t)b * ldp * 2;
-  for (int64_t p0 = p_begin; p0 < p_end; p0 += 64) {
-    const int pn = (int)min((int64_t)64, p_end - p0);
-    __syncthreads();
-    for (int e = tid; e < 64 * kF; e += 256) {
-      const int r = e / kF, k = e % kF;
-      float a = 0.f, c = 0.f;
-      if (r < pn) {
-        const int64_t i0 = P[2 * (p0 + r)], i1 = P[2 * (p0 + r) + 1];
-        c = e1[((int64_t)b * V1max + i0) * ld1 + k];
-        a = e2[((int64_t)b * V2max + i1) * ld2 + k];
+                                                          const int32_t* __restrict__ cnt, int SH,
+                                                          double* __restrict__ partH,
+                                                          double* __restrict__ partG) {
+  __shared__ double UV[2 * kCgtRows * 32];  // U rows, then V rows; reused for the wave combine
+  double(*U)[32] = reinterpret_cast<double(*)[32]>(UV);
+  double(*V)[32] = reinterpret_cast<double(*)[32]>(UV + kCgtRows * 32);
+  double(*red)[kFF] = reinterpret_cast<double(*)[kFF]>(UV);
+  static_assert(4 * kFF <= 2 * kCgtRows * 32, "combine buffer fits in the staging buffer");
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const bool isH = (int)blockIdx.x < SH;
+  const int s = isH ? blockIdx.x : blockIdx.x - SH;
+  const int64_t n = isH ? (npairs[b] < ldp ? npairs[b] : ldp) : V2max;
+  const int64_t r0 = (int64_t)s * kCgtRows;
+  if (r0 >= n) return;  // inactive slice: the reduction skips it
+  const int rn = (int)min((int64_t)kCgtRows, n - r0);
+  for (int e = tid; e < kCgtRows * 32; e += 256) {
+    const int r = e >> 5, k = e & 31;
+    double u = 0.0, v = 0.0;
+    if (r < rn && k < kF) {
+      if (isH) {
+        const int64_t* P = pairs + ((int64_t)b * ldp + r0 + r) * 2;
+        u = (double)e2[((int64_t)b * V2max + P[1]) * ld2 + k];
+        v = (double)e1[((int64_t)b * V1max + P[0]) * ld1 + k];
+      } else {
+        const int64_t j = r0 + r;
+        u = (double)e2[((int64_t)b * V2max + j) * ld2 + k];
+        v = u * (double)cnt[(int64_t)b * V2max + j];
       }
-      r2[r][k] = a;
-      r1[r][k] = c;
     }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = tid + 256 * q;
-      if (e >= kGH) break;
-      const int row = e / (2 * kF), col = e % (2 * kF);
-      double sacc = acc[q];
-      for (int r = 0; r < pn; ++r) {
-        const double u = (double)r2[r][row];
-        const double v = col < kF ? (double)r2[r][col] : (double)r1[r][col - kF];
-        sacc = fma(u, v, sacc);
-      }
-      acc[q] = sacc;
-    }
+    U[r][k] = u;
+    V[r][k] = v;
   }
-  const int S = gridDim.x;
+  __syncthreads();
+  const int w = pk::wave_id(), lane = pk::lane_id();
+  const int kb = lane >> 3, lb = lane & 7;
+  double acc[4][4];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int e = tid + 256 * q;
-    if (e < kGH) part[((int64_t)b * S + s) * kGH + e] = acc[q];
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+  for (int r = w; r < rn; r += 4) {
+    double u[4], v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      u[i] = U[r][4 * kb + i];
+      v[i] = V[r][4 * lb + i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = fma(u[i], v[j], acc[i][j]);
+  }
+  __syncthreads();  // staging buffer becomes the combine buffer
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 4 * kb + i, l = 4 * lb + j;
+      if (k < kF && l < kF) red[w][k * kF + l] = acc[i][j];
+    }
+  __syncthreads();
+  double* out = (isH ? partH + ((int64_t)b * SH + s) * kFF
+                     : partG + ((int64_t)b * gridDim.x - (int64_t)b * SH + s) * kFF);
+  for (int e = tid; e < kFF; e += 256) out[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+}
+
+// grid (ceil(1800 / 64), B), block 256: GH[b] = [G | H] (30 x 60), partials summed over the
+// active slices in 4 quarters + a fixed-order combine.
+__global__ __launch_bounds__(256) void cgt_reduce_kernel(const double* __restrict__ partH,
+                                                         const double* __restrict__ partG, int SH, int SG,
+                                                         const int64_t* __restrict__ npairs, int ldp,
+                                                         int V2max, double* __restrict__ GH) {
+  __shared__ double q4[4][64];
+  const int b = blockIdx.y;
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63), qtr = threadIdx.x >> 6;
+  double v = 0.0;
+  const bool valid = e < 2 * kFF;
+  if (valid) {
+    const bool isG = e < kFF;  // row-major [G | H]: entry (k, c) -> G if c < 30
+    const int ee = isG ? e : e - kFF;
+    const int64_t n = isG ? V2max : (npairs[b] < ldp ? npairs[b] : ldp);
+    const int S = isG ? SG : SH;
+    const int active = (int)min((int64_t)S, (n + kCgtRows - 1) / kCgtRows);
+    const double* p = (isG ? partG + (int64_t)b * SG * kFF : partH + (int64_t)b * SH * kFF) + ee;
+    const int s0 = (active * qtr) / 4, s1 = (active * (qtr + 1)) / 4;
+    double a0 = 0.0, a1 = 0.0;
+    int s = s0;
+    for (; s + 2 <= s1; s += 2) {
+      a0 += p[(int64_t)s * kFF];
+      a1 += p[(int64_t)(s + 1) * kFF];
+    }
+    if (s < s1) a0 += p[(int64_t)s * kFF];
+    v = a0 + a1;
+  }
+  q4[qtr][threadIdx.x & 63] = v;
+  __syncthreads();
+  if (qtr == 0 && valid) {
+    const int t = threadIdx.x;
+    const double r = (q4[0][t] + q4[1][t]) + (q4[2][t] + q4[3][t]);
+    const bool isG = e < kFF;
+    const int ee = isG ? e : e - kFF;
+    const int k = ee / kF, c = ee - k * kF;
+    GH[(int64_t)b * 2 * kFF + k * 2 * kF + (isG ? c : kF + c)] = r;
   }
 }
 
-// grid (B), block 256: sum the active partials (in slice order), then one wave solves
-// G X = H by Gauss-Jordan with partial pivoting; C_gt = X.
-__global__ __launch_bounds__(256) void cgt_solve_kernel(const double* __restrict__ part, int S,
-                                                        const int64_t* __restrict__ npairs, int ldp,
-                                                        float* __restrict__ Cgt) {
-  __shared__ double GH[kF][2 * kF + 1];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int64_t n = npairs[b] < ldp ? npairs[b] : ldp;
-  const int active = (int)((n + kCgtPairs - 1) / kCgtPairs);
-  for (int e = tid; e < kGH; e += 256) {
-    double v = 0.0;
-    for (int s = 0; s < active && s < S; ++s) v += part[((int64_t)b * S + s) * kGH + e];
-    GH[e / (2 * kF)][e % (2 * kF)] = v;
-  }
-  __syncthreads();
-  if (tid >= 64) return;
-  const int lane = tid;
-  bool used = lane >= kF;
+// grid (B), block 64 (one wave): Gauss-Jordan with partial pivoting on [G | H]. Lane l holds
+// row r = l & 31 (r < 30), columns 30 h .. 30 h + 29 with h = l >> 5, in registers.
+__global__ __launch_bounds__(64) void cgt_solve_kernel(const double* __restrict__ GH, float* __restrict__ Cgt) {
+  __shared__ double piv_s[2 * kF];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int r = lane & 31, h = lane >> 5;
+  const bool row_ok = r < kF;
+  double a[kF];
+#pragma unroll
+  for (int c = 0; c < kF; ++c) a[c] = row_ok ? GH[(int64_t)b * 2 * kFF + r * 2 * kF + h * kF + c] : 0.0;
+  bool used = !row_ok;
   int var = -1;
   for (int k = 0; k < kF; ++k) {
-    const double a = used ? -1.0 : fabs(GH[lane][k]);
-    uint32_t hi = used ? 0u : (uint32_t)(__double_as_longlong(a) >> 32);
-    const uint32_t mhi = pk::wave_max_u32_s(hi);
-    const uint32_t lo = (uint32_t)(__double_as_longlong(a) & 0xffffffffull);
-    const uint32_t mlo = pk::wave_max_u32_s((!used && hi == mhi) ? lo : 0u);
-    const uint64_t bal = __ballot(!used && hi == mhi && lo == mlo);
-    const int p = bal ? (__ffsll((unsigned long long)bal) - 1) : 0;
-    const double piv = GH[p][k];
-    const double f = (lane != p && lane < kF) ? GH[lane][k] / piv : 0.0;
-    __builtin_amdgcn_s_barrier();  // single wave: keeps the reads above ahead of the writes
-    for (int c = 0; c < 2 * kF; ++c) {
-      if (lane < kF) {
-        const double pc = GH[p][c];
-        if (lane != p) GH[lane][c] = fma(-f, pc, GH[lane][c]);
+    // pivot: max |G[r][k]| over unused rows (half-0 lanes), lowest row on ties
+    double ak = 0.0;  // a[k] through static indices (no scratch)
+#pragma unroll
+    for (int c = 0; c < kF; ++c) ak = c == k ? a[c] : ak;
+    double key = (h == 0 && !used) ? fabs(ak) : -1.0;
+    int who = r;
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) {
+      const double ok = __shfl_xor(key, off);
+      const int ow = __shfl_xor(who, off);
+      if (ok > key || (ok == key && ow < who)) {
+        key = ok;
+        who = ow;
       }
     }
-    __builtin_amdgcn_s_barrier();
-    if (lane == p) {
-      for (int c = 0; c < 2 * kF; ++c) GH[lane][c] = GH[lane][c] / piv;
+    const int p = __shfl(who, 0);
+    const double pivot = __shfl(ak, p);  // G[p][k] from half 0
+    const double f0 = (row_ok && r != p) ? ak / pivot : 0.0;
+    const double f = __shfl(f0, r);        // half-1 lanes take their row's factor
+    if (r == p) {
+#pragma unroll
+      for (int c = 0; c < kF; ++c) piv_s[h * kF + c] = a[c];
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    if (row_ok && r != p) {
+#pragma unroll
+      for (int c = 0; c < kF; ++c) a[c] = fma(-f, piv_s[h * kF + c], a[c]);
+    }
+    if (r == p) {
+#pragma unroll
+      for (int c = 0; c < kF; ++c) a[c] = a[c] / pivot;
       used = true;
       var = k;
     }
-    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_wave_barrier();
   }
-  if (var >= 0)
-    for (int c = 0; c < kF; ++c) Cgt[((int64_t)b * kF + var) * kF + c] = (float)GH[lane][kF + c];
+  if (h == 1 && var >= 0) {
+#pragma unroll
+    for (int c = 0; c < kF; ++c) Cgt[((int64_t)b * kF + var) * kF + c] = (float)a[c];
+  }
 }
 
 }  // namespace
@@ -309,20 +394,39 @@ extern "C" int pk_inlier_ratio(const int64_t* pairs, int ldp, int layout, const 
   return PK_OK;
 }
 
+extern "C" int64_t pk_cgt_lstsq_work_size(int ldp, int V2max, int B) {
+  const int64_t SH = ldp > 0 ? (ldp + kCgtRows - 1) / kCgtRows : 0;
+  const int64_t SG = (V2max + kCgtRows - 1) / kCgtRows;
+  return (int64_t)B * ((SH + SG) * kFF + 2 * kFF) + ((int64_t)B * V2max + 1) / 2;
+}
+
 extern "C" int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs, const float* evecs1, int ld1,
                             int V1max, const float* evecs2, int ld2, int V2max, int B, int K, double* work,
                             float* Cgt, void* stream) {
-  PK_REQUIRE(B >= 0 && K == kF && ld1 >= kF && ld2 >= kF && ldp >= 0);
+  PK_REQUIRE(B >= 0 && K == kF && ld1 >= kF && ld2 >= kF && ldp >= 0 && V2max > 0);
   if (B == 0) return PK_OK;
   PK_REQUIRE(pairs && npairs && evecs1 && evecs2 && work && Cgt);
   hipStream_t s = pk::as_stream(stream);
-  const int S = ldp > 0 ? (ldp + kCgtPairs - 1) / kCgtPairs : 1;
+  const int SH = ldp > 0 ? (ldp + kCgtRows - 1) / kCgtRows : 0;
+  const int SG = (V2max + kCgtRows - 1) / kCgtRows;
+  double* partH = work;
+  double* partG = partH + (int64_t)B * SH * kFF;
+  double* GH = partG + (int64_t)B * SG * kFF;
+  int32_t* cnt = reinterpret_cast<int32_t*>(GH + (int64_t)B * 2 * kFF);
+  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(int32_t) * (size_t)B * V2max, s);
+  if (e != hipSuccess) return (int)e;
   if (ldp > 0) {
-    hipLaunchKernelGGL(cgt_partial_kernel, dim3(S, B), dim3(256), 0, s, pairs, ldp, npairs, evecs1, ld1, V1max, evecs2,
-                       ld2, V2max, work);
+    hipLaunchKernelGGL(cgt_count_kernel, dim3((ldp + 255) / 256, B), dim3(256), 0, s, pairs, ldp, npairs, V2max,
+                       cnt);
     PK_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(cgt_solve_kernel, dim3(B), dim3(256), 0, s, work, S, npairs, ldp, Cgt);
+  hipLaunchKernelGGL(cgt_partial_kernel, dim3(SH + SG, B), dim3(256), 0, s, pairs, ldp, npairs, evecs1, ld1,
+                     V1max, evecs2, ld2, V2max, cnt, SH, partH, partG);
+  PK_CHECK_LAUNCH();
+  hipLaunchKernelGGL(cgt_reduce_kernel, dim3((2 * kFF + 63) / 64, B), dim3(256), 0, s, partH, partG, SH, SG,
+                     npairs, ldp, V2max, GH);
+  PK_CHECK_LAUNCH();
+  hipLaunchKernelGGL(cgt_solve_kernel, dim3(B), dim3(64), 0, s, GH, Cgt);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

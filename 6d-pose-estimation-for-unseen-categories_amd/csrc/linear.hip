@@ -20,7 +20,7 @@ constexpr int kChunk = 32;          // rows staged per step (8 MFMA k-steps)
 constexpr int kSlice = 128;         // rows per workgroup
 constexpr int kMaxC = 128;          // I, O <= 128
 constexpr int kStride = kMaxC + 16; // LDS row stride (mod 64 = 16: conflict-free A/B reads)
-constexpr int kMaxTilesPerWave = 16;
+constexpr int kMaxTilesPerWave = 8;  // O * I <= 128 * 64
 
 __device__ __forceinline__ float load_rc(const float* __restrict__ p, int layout, int C, int N, int64_t r,
                                          int c) {
@@ -29,21 +29,28 @@ __device__ __forceinline__ float load_rc(const float* __restrict__ p, int layout
   return p[(b * C + c) * N + n];
 }
 
-// Stage rows [r0, r0 + kChunk) of a [R, C] operand into s[row][c] (zero padded).
+// Stage rows [r0, r0 + kChunk) of a [R, C] operand into s[row][c] (zero padded). All
+// global loads of the chunk are issued before the first LDS store (one wait per chunk).
 __device__ __forceinline__ void stage_rows(const float* __restrict__ p, int layout, int C, int N, int64_t R,
                                            int64_t r0, float* __restrict__ s) {
   const int cp = (C + 15) & ~15;
-  for (int e = threadIdx.x; e < kChunk * cp; e += 256) {
-    int row, c;
-    if (layout == 0) {
-      row = e / cp;
-      c = e - row * cp;
-    } else {  // channels-first: consecutive threads walk rows (contiguous in memory)
-      c = e / kChunk;
-      row = e - c * kChunk;
-    }
+  const int total = kChunk * cp;
+  constexpr int kPer = kChunk * kMaxC / 256;
+  float v[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int e = threadIdx.x + q * 256;
+    const int row = layout == 0 ? e / cp : e % kChunk;  // channels-first: threads walk rows
+    const int c = layout == 0 ? e % cp : e / kChunk;    // (contiguous in memory)
     const int64_t r = r0 + row;
-    s[row * kStride + c] = (c < C && r < R) ? load_rc(p, layout, C, N, r, c) : 0.f;
+    v[q] = (e < total && c < C && r < R) ? load_rc(p, layout, C, N, r, c) : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int e = threadIdx.x + q * 256;
+    const int row = layout == 0 ? e / cp : e % kChunk;
+    const int c = layout == 0 ? e % cp : e / kChunk;
+    if (e < total) s[row * kStride + c] = v[q];
   }
 }
 
@@ -103,29 +110,41 @@ __global__ __launch_bounds__(256) void wgrad_partial_kernel(const float* __restr
   if (threadIdx.x < O) partb[(int64_t)s * O + threadIdx.x] = bacc;
 }
 
-// dw[e] = sum_s part[s, e] (e < O*I), db[o] = sum_s partb[s, o]; slice order.
+// dw[e] = sum_s part[s, e] (e < O*I), db[o] = sum_s partb[s, o]. Block = 64 outputs x
+// 4 slice quarters (4 interleaved chains each), combined in a fixed order: deterministic.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
                                                            const float* __restrict__ partb, int S,
                                                            int OI, int O, float* __restrict__ dw,
                                                            float* __restrict__ db) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
+  __shared__ float red[4][64];
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int qtr = threadIdx.x >> 6;
   const bool is_w = e < OI;
   const bool is_b = !is_w && e < OI + O && db != nullptr;
-  if (!is_w && !is_b) return;
-  const float* p = is_w ? part + e : partb + (e - OI);
-  const int64_t st = is_w ? OI : O;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int s = 0;
-  for (; s + 4 <= S; s += 4) {  // four interleaved chains, combined in a fixed order
-    a0 += p[(int64_t)s * st];
-    a1 += p[(int64_t)(s + 1) * st];
-    a2 += p[(int64_t)(s + 2) * st];
-    a3 += p[(int64_t)(s + 3) * st];
+  float v = 0.f;
+  if (is_w || is_b) {
+    const float* p = is_w ? part + e : partb + (e - OI);
+    const int64_t st = is_w ? OI : O;
+    const int s0 = (S * qtr) / 4, s1 = (S * (qtr + 1)) / 4;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int s = s0;
+    for (; s + 4 <= s1; s += 4) {
+      a0 += p[(int64_t)s * st];
+      a1 += p[(int64_t)(s + 1) * st];
+      a2 += p[(int64_t)(s + 2) * st];
+      a3 += p[(int64_t)(s + 3) * st];
+    }
+    for (; s < s1; ++s) a0 += p[(int64_t)s * st];
+    v = (a0 + a1) + (a2 + a3);
   }
-  for (; s < S; ++s) a0 += p[(int64_t)s * st];
-  const float v = (a0 + a1) + (a2 + a3);
-  if (is_w) dw[e] = v;
-  else db[e - OI] = v;
+  red[qtr][threadIdx.x & 63] = v;
+  __syncthreads();
+  if (qtr == 0 && (is_w || is_b)) {
+    const int t = threadIdx.x;
+    const float r = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    if (is_w) dw[e] = r;
+    else db[e - OI] = r;
+  }
 }
 
 }  // namespace
@@ -149,7 +168,7 @@ extern "C" int pk_linear_wgrad(const float* x, const float* dy, int layout, int6
   hipLaunchKernelGGL(wgrad_partial_kernel, dim3(S), dim3(256), 0, s, x, dy, layout, R, I, O, N, part, partb);
   PK_CHECK_LAUNCH();
   const int total = O * I + O;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, s, part, partb, S, O * I, O,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(256), 0, s, part, partb, S, O * I, O,
                      dw, db);
   PK_CHECK_LAUNCH();
   return PK_OK;

@@ -42,12 +42,15 @@ SIGNATURES = {
     "pk_feat_dist_topk": [_P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "pk_rigidity_filter": [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P],
     "pk_inlier_ratio": [_P, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P],
+    "pk_cgt_lstsq_work_size": [_I, _I, _I],
     "pk_cgt_lstsq": [_P, _I, _P, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P],
     "pk_ransac": [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _I64, _D, _I, _P, _P, _P, _P, _P, _P],
     "pk_pose_metrics": [_P, _P, _I, _I, _P, _P, _P, _P, _P],
     "pk_erode_mask": [_P, _I, _I, _I, _P, _P],
     "pk_sample_rgb": [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],
 }
+
+RESTYPES = {"pk_cgt_lstsq_work_size": _I64}  # everything else returns an int status
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -67,7 +70,7 @@ def lib() -> ctypes.CDLL:
         for name, argtypes in SIGNATURES.items():
             fn = getattr(l, name)
             fn.argtypes = argtypes
-            fn.restype = ctypes.c_int
+            fn.restype = RESTYPES.get(name, ctypes.c_int)
         _lib = l
     return _lib
 
@@ -77,14 +80,15 @@ _probe = None
 
 
 def set_probe(hook) -> None:
-    """Install hook(name, thunk) around every call (bench.py's per-kernel HIP events)."""
+    """Install hook(name, thunk, work) around every call (bench.py's per-kernel HIP events).
+    `work` is the launch's algorithmic work ("hbm", bytes) / ("mfma", flops) or None."""
     global _probe
     _probe = hook
 
 
-def call(name: str, *args) -> None:
+def call(name: str, *args, work=None) -> None:
     fn = getattr(lib(), name)
-    status = _probe(name, lambda: fn(*args)) if _probe is not None else fn(*args)
+    status = _probe(name, lambda: fn(*args), work) if _probe is not None else fn(*args)
     if status != 0:
         msg = _ERRORS.get(status, f"hipError_t {status}")
         raise PoseKernError(f"{name} failed: {msg}")

@@ -27,8 +27,8 @@ class LearnedTimeDiffusion(nn.Module):
         self.diffusion_time = nn.Parameter(torch.zeros(C_inout))
 
     def forward(self, x, L, mass, evals, evecs):
-        with torch.no_grad():  # in-place clamp, as upstream
-            self.diffusion_time.data = torch.clamp(self.diffusion_time, min=1e-8)
+        with torch.no_grad():  # in-place clamp, as upstream; clamp_ keeps
+            self.diffusion_time.data.clamp_(min=1e-8)  # the storage (HIP-graph replays)
         return ops.spectral_diffusion(x, mass, evals, evecs, self.diffusion_time)
 
 

@@ -36,7 +36,8 @@ def fps_packed(xyz: torch.Tensor, offsets: torch.Tensor, nmax: int, start: torch
     B = offsets.numel() - 1
     out = torch.zeros((B, out_stride), dtype=torch.int64, device=xyz.device)
     call("pk_fps", ptr(xyz), ptr(offsets), B, int(nmax), ptr(start.to(torch.int32).contiguous()),
-         ptr(npoint.to(torch.int32).contiguous()), ptr(out), int(out_stride), _lib.stream(xyz.device))
+         ptr(npoint.to(torch.int32).contiguous()), ptr(out), int(out_stride), _lib.stream(xyz.device),
+         work=("hbm", 12 * xyz.shape[0] + 8 * B * int(out_stride)))
     return out
 
 
@@ -77,7 +78,8 @@ def ball_query(cad: torch.Tensor, cad_off: torch.Tensor, pc: torch.Tensor, pc_of
     rowcount = torch.empty((B, n1max), dtype=torch.int32, device=dev)
     s = _lib.stream(dev)
     call("pk_ball_query_mask", ptr(cad), ptr(cad_off), ptr(pc), ptr(pc_off), ptr(thr2), B, int(n1max),
-         int(n2max), ptr(mask), int(ld), ptr(rowcount), s)
+         int(n2max), ptr(mask), int(ld), ptr(rowcount), s,
+         work=("hbm", 24 * (cad.shape[0] + pc.shape[0]) + B * int(n1max) * int(n2max) + 4 * B * int(n1max)))
     rowoff = torch.empty((B, n1max), dtype=torch.int64, device=dev)
     pairs = torch.empty((B, cap, 2), dtype=torch.int64, device=dev)
     count = torch.empty((B,), dtype=torch.int64, device=dev)
@@ -121,7 +123,8 @@ def backproject(depth: torch.Tensor, mask: torch.Tensor, K: torch.Tensor, cam_sc
     pix = torch.empty((cap,), dtype=torch.int32, device=dev)
     idxmap = torch.empty((F, H, W), dtype=torch.int32, device=dev)
     call("pk_backproject", ptr(depth), ptr(mask), F, H, W, ptr(K), ptr(cam_scale), ptr(rowcnt), ptr(rowoff),
-         ptr(count), ptr(off), ptr(xyz), int(cap), ptr(pix), ptr(idxmap), _lib.stream(dev))
+         ptr(count), ptr(off), ptr(xyz), int(cap), ptr(pix), ptr(idxmap), _lib.stream(dev),
+         work=("hbm", 7 * F * H * W))
     return dict(xyz=xyz, count=count, off=off, pix=pix, idxmap=idxmap)
 
 
@@ -150,7 +153,8 @@ def sor(xyz: torch.Tensor, off: torch.Tensor, nmax: int, knn: int = 20, std_rati
     W = idxmap.shape[2] if idxmap is not None else 0
     call("pk_sor", ptr(xyz), ptr(off), B, int(nmax), int(knn), float(std_ratio), ptr(pix), ptr(idxmap), H, W,
          ptr(K), ptr(avg), ptr(thr), ptr(ccount),
-         ptr(coff), ptr(kept), ptr(out_off), ptr(out64), ptr(out32), ptr(kidx), _lib.stream(dev))
+         ptr(coff), ptr(kept), ptr(out_off), ptr(out64), ptr(out32), ptr(kidx), _lib.stream(dev),
+         work=("hbm", 68 * xyz.shape[0]))
     return dict(avg=avg, thr=thr, kept=kept, off=out_off, xyz64=out64, xyz32=out32, kept_idx=kidx)
 
 
@@ -203,7 +207,8 @@ class _SpectralDiffusion(torch.autograd.Function):
         scaled = torch.empty_like(spec)
         out = torch.empty_like(x)
         call("pk_spectral_diffusion", ptr(x), ptr(mass), ptr(evecs), ptr(evals), ptr(t), B, N, K, C, 0,
-             ptr(work), ptr(spec), ptr(scaled), None, None, ptr(out), _lib.stream(dev))
+             ptr(work), ptr(spec), ptr(scaled), None, None, ptr(out), _lib.stream(dev),
+             work=("hbm", 16 * B * N * 64))  # Phi read twice + x in + y out, f32
         ctx.save_for_backward(mass, evals, evecs, t, spec)
         return out
 
@@ -220,7 +225,8 @@ class _SpectralDiffusion(torch.autograd.Function):
         gt = torch.empty((B, C), dtype=torch.float32, device=dev)
         gx = torch.empty_like(g)
         call("pk_spectral_diffusion", ptr(g), ptr(mass), ptr(evecs), ptr(evals), ptr(t), B, N, K, C, 1,
-             ptr(work), None, ptr(scaled), ptr(spec), ptr(gt), ptr(gx), _lib.stream(dev))
+             ptr(work), None, ptr(scaled), ptr(spec), ptr(gt), ptr(gx), _lib.stream(dev),
+             work=("hbm", 16 * B * N * 64))
         return gx, None, None, None, gt.sum(0)
 
 
@@ -278,7 +284,8 @@ class _Attention(torch.autograd.Function):
         M = k.shape[3]
         out = torch.empty_like(q)
         lse = torch.empty((B, H, N), dtype=torch.float32, device=q.device)
-        call("pk_attention_fwd", ptr(q), ptr(k), ptr(v), B, D, H, N, M, ptr(out), ptr(lse), _lib.stream(q.device))
+        call("pk_attention_fwd", ptr(q), ptr(k), ptr(v), B, D, H, N, M, ptr(out), ptr(lse), _lib.stream(q.device),
+             work=("mfma", 2 * 2 * N * M * D * B * H))  # S = Q K^T, O = P V
         ctx.save_for_backward(q, k, v, out, lse)
         return out
 
@@ -291,7 +298,8 @@ class _Attention(torch.autograd.Function):
         delta = torch.empty((B, H, N), dtype=torch.float32, device=q.device)
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         call("pk_attention_bwd", ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse), B, D, H, N, M, ptr(delta),
-             ptr(dq), ptr(dk), ptr(dv), _lib.stream(q.device))
+             ptr(dq), ptr(dk), ptr(dv), _lib.stream(q.device),
+             work=("mfma", 7 * 2 * N * M * D * B * H))  # S, dP, dQ | S, dP, dV, dK
         return dq, dk, dv
 
 
@@ -325,7 +333,8 @@ def linear_wgrad(x: torch.Tensor, dy: torch.Tensor, channels_first: bool, want_b
     dw = torch.empty((O, I), dtype=torch.float32, device=dev)
     db = torch.empty((O,), dtype=torch.float32, device=dev) if want_bias else None
     call("pk_linear_wgrad", ptr(x), ptr(dy), layout, int(R), I, O, int(N), ptr(work), ptr(dw), ptr(db),
-         _lib.stream(dev))
+         _lib.stream(dev),
+         work=("mfma", 2 * int(R) * I * O))
     return dw, db
 
 
@@ -344,7 +353,8 @@ def feat_dist_topk(evecs_x: torch.Tensor, C: torch.Tensor, evecs_y: torch.Tensor
     idx = torch.empty((B, V2, topk), dtype=torch.int64, device=dev)
     dist = torch.empty((B, V2, topk), dtype=torch.float32, device=dev) if want_dist else None
     call("pk_feat_dist_topk", ptr(evecs_x.contiguous()), ldx, ptr(C.contiguous()), ptr(evecs_y.contiguous()), ldy,
-         ptr(n1), ptr(n2), B, V1, V2, int(topk), ptr(A), ptr(Bq), ptr(idx), ptr(dist), _lib.stream(dev))
+         ptr(n1), ptr(n2), B, V1, V2, int(topk), ptr(A), ptr(Bq), ptr(idx), ptr(dist), _lib.stream(dev),
+         work=("mfma", 2 * B * V1 * V2 * 32))
     return idx, dist
 
 
@@ -385,7 +395,8 @@ def inlier_ratio(pairs: torch.Tensor, npairs: torch.Tensor, cad: torch.Tensor, p
 def cgt_lstsq(pairs: torch.Tensor, npairs: torch.Tensor, evecs1: torch.Tensor, evecs2: torch.Tensor) -> torch.Tensor:
     B, L, _ = pairs.shape
     out = torch.empty((B, 30, 30), dtype=torch.float32, device=pairs.device)
-    work = torch.empty((B * max(1, (L + 255) // 256) * 1800,), dtype=torch.float64, device=pairs.device)
+    nwork = _lib.lib().pk_cgt_lstsq_work_size(L, evecs2.shape[1], B)
+    work = torch.empty((nwork,), dtype=torch.float64, device=pairs.device)
     call("pk_cgt_lstsq", ptr(pairs.contiguous()), L, ptr(npairs), ptr(evecs1.contiguous()), evecs1.shape[2],
          evecs1.shape[1], ptr(evecs2.contiguous()), evecs2.shape[2], evecs2.shape[1], B, 30, ptr(work), ptr(out),
          _lib.stream(pairs.device))

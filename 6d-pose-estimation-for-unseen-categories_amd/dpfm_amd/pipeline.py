@@ -96,13 +96,19 @@ def naive_p2p_batched(C: torch.Tensor, evecs_x: torch.Tensor, evecs_y: torch.Ten
 
 
 class TrainStep:
-    """One training iteration (scripts/train.py:88-124) for a batch of crops."""
+    """One training iteration (scripts/train.py:88-124) for a batch of crops.
+
+    Split in two phases so a HIP graph can hold everything but the collective:
+    `forward_backward` (model, C_gt, loss, naive IR, backward) and `apply` (gradient
+    all-reduce across ranks, clip 5.0, RMSprop, grads reset to None as the next
+    backward re-creates them)."""
 
     def __init__(self, model: DPFMNet, lr: float = 5e-4, max_norm: float = 5.0, nce_num_pairs: int = 512,
-                 group: Optional[dist.ProcessGroup] = None, seed: int = 0):
+                 group: Optional[dist.ProcessGroup] = None, seed: int = 0, capturable: bool = False):
         self.model = model
         self.params = [p for p in model.parameters()]
-        self.opt = torch.optim.RMSprop(self.params, lr=lr)  # config/dpfm_orig.gin:62-63
+        # config/dpfm_orig.gin:62-63; capturable keeps the step count on the device
+        self.opt = torch.optim.RMSprop(self.params, lr=lr, capturable=capturable)
         self.crit = DPFMLoss(w_fmap=1, w_acc=1, w_nce=1, nce_t=0.07, nce_num_pairs=nce_num_pairs)  # gin:54-58
         self.max_norm = max_norm
         self.group = group
@@ -112,24 +118,26 @@ class TrainStep:
         self.gen.manual_seed(seed)
         self.flat = torch.zeros(sum(p.numel() for p in self.params), dtype=torch.float32, device=dev)
 
-    def allreduce_grads(self):
-        """DDP's gradient averaging in one bucket (49,281 f32 = 197 KB: latency-bound)."""
+    def allreduce_grads(self, grads=None):
+        """DDP's gradient averaging in one bucket (49,281 f32 = 197 KB: latency-bound).
+        `grads` defaults to the parameters' .grad tensors."""
         if self.world <= 1:
             return
+        grads = grads if grads is not None else [p.grad for p in self.params]
         o = 0
-        for p in self.params:
-            n = p.numel()
-            self.flat[o:o + n].copy_(p.grad.reshape(-1))
+        for g in grads:
+            n = g.numel()
+            self.flat[o:o + n].copy_(g.reshape(-1))
             o += n
         dist.all_reduce(self.flat, group=self.group)
         self.flat.div_(self.world)
         o = 0
-        for p in self.params:
-            n = p.numel()
-            p.grad.copy_(self.flat[o:o + n].view_as(p.grad))
+        for g in grads:
+            n = g.numel()
+            g.copy_(self.flat[o:o + n].view_as(g))
             o += n
 
-    def __call__(self, op: Operators, crops: Crops):
+    def forward_backward(self, op: Operators, crops: Crops) -> dict:
         self.model.train()
         batch = model_batch(op, crops)
         C_pred, o12, o21, f1, f2, _, _ = self.model(batch)
@@ -142,12 +150,136 @@ class TrainStep:
             npred = torch.full((p_pred.shape[0],), p_pred.shape[2], dtype=torch.int32, device=p_pred.device)
             ir = ops.inlier_ratio(p_pred, npred, op.cad_xyz, crops.align32, op.ir_thr, layout=1).mean()
         loss.backward()
-        self.allreduce_grads()
-        torch.nn.utils.clip_grad_norm_(self.params, max_norm=self.max_norm, norm_type=2)
-        self.opt.step()
-        self.opt.zero_grad(set_to_none=False)
         log["IR"] = ir
         return log
+
+    def apply(self, allreduce: bool = True, reset: bool = True):
+        if allreduce:
+            self.allreduce_grads()
+        torch.nn.utils.clip_grad_norm_(self.params, max_norm=self.max_norm, norm_type=2)
+        self.opt.step()
+        if reset:  # (a captured backward that started from None grads overwrites them instead)
+            self.opt.zero_grad(set_to_none=True)
+
+    def __call__(self, op: Operators, crops: Crops):
+        log = self.forward_backward(op, crops)
+        self.apply()
+        return log
+
+
+class GraphedTrainStep:
+    """Crop formation + a training step captured once into HIP graphs and replayed.
+
+    The eager step issues ~700 launches (libposekern + torch); replaying a graph turns
+    them into one submission, so the step runs at device speed. Inputs are static: `fb`
+    and `op` stay resident and are re-read on every replay (copy new frames into them to
+    feed new data). With one rank the whole step is one graph; with several ranks the
+    RCCL all-reduce runs eagerly between graph A (crops -> backward) and graph B
+    (clip + RMSprop), so no collective is captured."""
+
+    def __init__(self, crop_formation: CropFormation, step: TrainStep, fb: FrameBatch, op: Operators,
+                 warmup: int = 3):
+        self.crops_of, self.step, self.fb, self.op = crop_formation, step, fb, op
+        self.split = step.world > 1
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up outside capture (allocator, optimizer state)
+            for _ in range(warmup):
+                step.forward_backward(op, crop_formation(fb))
+                step.apply()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph_a = torch.cuda.CUDAGraph()
+        self.graph_a.register_generator_state(step.gen)
+        # grads are None here, so the captured backward writes (not accumulates) them
+        with torch.cuda.graph(self.graph_a):
+            self.log = step.forward_backward(op, crop_formation(fb))
+            if not self.split:
+                step.apply(allreduce=False, reset=False)
+        self.graph_b = None
+        if self.split:
+            self.graph_b = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_b, pool=self.graph_a.pool()):
+                step.apply(allreduce=False, reset=False)
+
+    def __call__(self) -> dict:
+        self.graph_a.replay()
+        if self.split:
+            self.step.allreduce_grads()
+            self.graph_b.replay()
+        return self.log
+
+
+class PipelinedTrainer:
+    """Crop formation of batch i+1 overlapped with the training step on batch i.
+
+    Crop formation (back-projection, SOR, FPS, ball query: ~2 ms of mostly latency-bound,
+    one-workgroup-per-crop kernels at B = 32) and the model step (wide kernels) run on
+    two streams, as the reference overlaps its DataLoader workers with training. Two
+    crop buffers ping-pong: graph C_k forms crops into buffer k on the side stream, graph
+    T_k trains on buffer k on the main stream; events order C_k after T_k of the previous
+    use and T_k after C_k. Every piece is a HIP graph replay. With several ranks each
+    T_k is split around the eager RCCL all-reduce, as in GraphedTrainStep."""
+
+    def __init__(self, crop_formation: CropFormation, step: TrainStep, fb: FrameBatch, op: Operators,
+                 warmup: int = 3):
+        self.step, self.split = step, step.world > 1
+        self.main = torch.cuda.current_stream()
+        self.side = torch.cuda.Stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(self.main)
+        with torch.cuda.stream(side):  # warm-up outside capture
+            for _ in range(warmup):
+                step.forward_backward(op, crop_formation(fb))
+                step.apply()
+        self.main.wait_stream(side)
+        torch.cuda.synchronize()
+        self.crop_graphs, self.crops, self.train_a, self.train_b, self.grads, self.logs = [], [], [], [], [], []
+        for k in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.crops.append(crop_formation(fb))
+            self.crop_graphs.append(g)
+        for k in range(2):
+            step.opt.zero_grad(set_to_none=True)  # each training graph owns its gradients
+            ga = torch.cuda.CUDAGraph()
+            ga.register_generator_state(step.gen)
+            with torch.cuda.graph(ga):
+                self.logs.append(step.forward_backward(op, self.crops[k]))
+                if not self.split:
+                    step.apply(allreduce=False, reset=False)
+            self.grads.append([p.grad for p in step.params])
+            gb = None
+            if self.split:
+                gb = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gb, pool=ga.pool()):
+                    step.apply(allreduce=False, reset=False)
+            self.train_a.append(ga)
+            self.train_b.append(gb)
+        self.formed = [torch.cuda.Event(), torch.cuda.Event()]   # C_k done
+        self.consumed = [torch.cuda.Event(), torch.cuda.Event()]  # T_k done reading buffer k
+        for k in range(2):
+            self.consumed[k].record(self.main)
+        self.i = 0
+        self._form(0)
+
+    def _form(self, k):
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(self.consumed[k])
+            self.crop_graphs[k].replay()
+            self.formed[k].record(self.side)
+
+    def __call__(self) -> dict:
+        k = self.i & 1
+        self._form(k ^ 1)                      # next batch's crops, concurrently
+        self.main.wait_event(self.formed[k])
+        self.train_a[k].replay()
+        if self.split:
+            self.step.allreduce_grads(self.grads[k])
+            self.train_b[k].replay()
+        self.consumed[k].record(self.main)
+        self.i += 1
+        return self.logs[k]
 
 
 class InferStep:
@@ -176,8 +308,13 @@ class InferStep:
         cor_off = torch.zeros(B + 1, dtype=torch.int64, device=dev)
         cor_off[1:] = torch.cumsum(nsurv.to(torch.int64), 0)
         L = p_pred.shape[1]
-        valid = torch.arange(L, device=dev)[None] < nsurv[:, None]
-        corres = p_pred[valid].to(torch.int32)   # packed [sum n, 2] (device-side compaction)
+        ar = torch.arange(L, device=dev)[None]
+        valid = ar < nsurv[:, None]
+        # packed [sum n, 2] without reading the total on the host: crop b's i-th survivor goes
+        # to row cor_off[b] + i of a B*L-row buffer (+1 spill row for the invalid slots)
+        pos = torch.where(valid, cor_off[:-1, None] + ar, torch.full_like(ar, B * L)).reshape(-1)
+        corres = torch.zeros((B * L + 1, 2), dtype=torch.int32, device=dev)
+        corres.index_copy_(0, pos, p_pred.reshape(-1, 2).to(torch.int32))
         T, stats = ops.ransac(fb.cad64, fb.cad_off, crops.pc64, crops.off, corres, cor_off, self.H, seed=self.seed,
                               max_dist=self.max_dist)
         T_gt = torch.zeros((B, 4, 4), dtype=torch.float64, device=dev)

@@ -43,29 +43,38 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-crops", type=int, default=2, help="bounded CPU-baseline sample (crops)")
     ap.add_argument("--no-roofline-probe", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no HIP graph: launch every kernel from Python")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="graph mode without overlapping crop formation of the next batch")
+    ap.add_argument("--probe-steps", type=int, default=2, help="eager steps after timing for the kernel breakdown")
     return ap.parse_args()
 
 
 class KernelProbe:
-    """HIP events around every libposekern call issued inside the timed region (same
-    stream as the kernels: torch's current stream)."""
+    """HIP events around every libposekern call (same stream as the kernels: torch's
+    current stream), with the algorithmic work each launch declares (ops.py `work=`)."""
 
     def __init__(self):
         self.ev = {}
 
-    def hook(self, name, fn):
+    def hook(self, name, fn, work=None):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         r = fn()
         e.record()
-        self.ev.setdefault(name, []).append((s, e))
+        self.ev.setdefault(name, []).append((s, e, work))
         return r
 
     def summary(self):
+        """name -> dict(avg_ms, launches, total_ms, bound, work) (work summed, or None)."""
         out = {}
         for k, lst in self.ev.items():
-            ms = [s.elapsed_time(e) for s, e in lst]
-            out[k] = (float(np.mean(ms)), len(ms), float(np.sum(ms)))
+            ms = [s.elapsed_time(e) for s, e, _ in lst]
+            works = [w for _, _, w in lst]
+            known = all(w is not None for w in works)
+            out[k] = dict(avg_ms=float(np.mean(ms)), launches=len(ms), total_ms=float(np.sum(ms)),
+                          bound=works[0][0] if known else None,
+                          work=float(sum(w[1] for w in works)) if known else None)
         return out
 
 
@@ -97,7 +106,8 @@ def ball_query_roofline(dev, probe_launches: int = 10) -> dict:
     byts = B * (24 * N + 24 * N + N * N) + B * N * 4  # coords in + mask + row counts
     ach = byts / (ms * 1e-3) / 1e9
     return {"kernel": "pk_ball_query_mask (configs[3]: 256 x 2048 x 2048)", "bound": "hbm", "achieved": round(ach, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": pmc_traffic("pk_ball_query_mask@configs3_probe"),
             "ms_per_launch": round(ms, 4), "bytes_per_launch": byts}
 
 
@@ -173,18 +183,22 @@ def main():
     from dpfm_amd import _lib
     from dpfm_amd.dataset.object import CropFormation
     from dpfm_amd.models.dpfm import DPFMNet
-    from dpfm_amd.pipeline import TrainStep, make_frame_batch
+    from dpfm_amd.pipeline import GraphedTrainStep, PipelinedTrainer, TrainStep, make_frame_batch
 
     B, N = args.batch, args.points
     torch.manual_seed(1234)  # identical initial weights on every rank (DDP broadcast semantics)
     model = DPFMNet().to(dev)
     fb, op = make_frame_batch(B, N, N, seed=1000 * rank, device=dev)
     crops_of = CropFormation(n1=N, npoint=N, seed=rank)
-    step = TrainStep(model, seed=rank)
+    step = TrainStep(model, seed=rank, capturable=not args.eager)
 
-    def one_step():
-        crops = crops_of(fb)
-        return step(op, crops)
+    if args.eager:
+        def one_step():
+            return step(op, crops_of(fb))
+    elif args.no_overlap:  # warm-up + capture (untimed), then every step is a graph replay
+        one_step = GraphedTrainStep(crops_of, step, fb, op, warmup=3)
+    else:  # same, with crop formation of the next batch on a second stream
+        one_step = PipelinedTrainer(crops_of, step, fb, op, warmup=3)
 
     for _ in range(args.warmup):
         one_step()
@@ -192,7 +206,8 @@ def main():
     if world > 1:
         dist.barrier()
     probe = KernelProbe()
-    _lib.set_probe(probe.hook)
+    if args.eager:
+        _lib.set_probe(probe.hook)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -207,16 +222,28 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern = probe.summary()
     loss_v, ir_v = float(log["loss"]), float(log["IR"])
+    probe_steps = args.steps
+    if not args.eager:
+        # per-kernel HIP events cannot sit inside a graph: time the same step eagerly, on
+        # the same resident inputs, right after the timed region (not part of `value`)
+        _lib.set_probe(probe.hook)
+        for _ in range(args.probe_steps):
+            step(op, crops_of(fb))
+        torch.cuda.synchronize()
+        _lib.set_probe(None)
+        probe_steps = args.probe_steps
+    kern = probe.summary()
 
     if rank == 0:
         total_ms = elapsed * 1e3 / args.steps
-        # dominant kernel family by total device time inside the timed region
-        dom = max(kern.items(), key=lambda kv: kv[1][2])
-        kernels = {k: {"avg_ms": round(v[0], 4), "launches": v[1], "ms_per_step": round(v[2] / args.steps, 4)}
-                   for k, v in sorted(kern.items(), key=lambda kv: -kv[1][2])}
-        roof = roofline_for(dom[0], dom[1][0], B, N)
+        # dominant kernel family by total device time in the probed steps
+        dom = max(kern.items(), key=lambda kv: kv[1]["total_ms"])
+        kernels = {k: {"avg_ms": round(v["avg_ms"], 4), "launches": v["launches"],
+                       "ms_per_step": round(v["total_ms"] / max(probe_steps, 1), 4)}
+                   for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"])}
+        roof = roofline_for(dom[0], dom[1])
+        mfma_fams = {k: roofline_for(k, v) for k, v in kern.items() if v["bound"] == "mfma"}
         out = {
             "metric": "RGB-D crops/sec (fwd+bwd), 1024 pts, at 1/2/4/8 MI355X; pose err vs ref",
             "value": round(B * world / elapsed * args.steps, 3),
@@ -227,9 +254,13 @@ def main():
             "dtype": "fp32 (fp64 crop geometry)", "data": "synthetic (seeded ellipsoid RGB-D frames, random-init DPFM)",
             "config": {"workload": "configs[1] shape: B=32 synthetic 640x480 RGB-D crops/GPU, 1024 pts, "
                                    "training step fwd+bwd (configs[2] semantics, DDP over RCCL when N>1)",
+                       "execution": "eager" if args.eager else ("hip-graph" if args.no_overlap else
+                                                                 "hip-graph, crop formation overlapped"),
                        "global_batch": B * world, "points_per_crop": N, "cad_points": N,
                        "parallelism": f"dp{world}"},
             "roofline": roof,
+            "roofline_mfma_kernels": {k: {"achieved": v["achieved"], "frac": v["frac"], "unit": v["unit"]}
+                                      for k, v in mfma_fams.items()},
             "kernels": kernels,
             "loss": round(loss_v, 5), "ir": round(ir_v, 5),
         }
@@ -243,28 +274,41 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline_for(name: str, avg_ms: float, B: int, N: int) -> dict:
-    """Algorithmic work per launch of the dominant kernel family."""
+def pmc_traffic(name: str):
+    """HBM bytes per launch of a kernel family from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, made by tools/pmc_summary.py from separate FETCH_SIZE and
+    WRITE_SIZE runs of this benchmark), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            v = json.load(f).get(name)
+    except (OSError, ValueError):
+        return None
+    return None if v is None else round(v["traffic_bytes_per_launch"], 1)
+
+
+def roofline_for(name: str, k: dict) -> dict:
+    """Roofline of one kernel family from the probe: achieved = its declared algorithmic
+    work (bytes for HBM-bound kernels, flops for MFMA kernels) summed over
+    its launches / its summed launch time."""
+    base = {"kernel": name, "avg_ms": round(k["avg_ms"], 4), "launches_per_step_probe": k["launches"],
+            "work_per_launch": None if k["work"] is None else k["work"] / k["launches"]}
+    traffic = pmc_traffic(name)
+    if k["work"] is None:
+        return dict(base, bound="hbm", achieved=None, peak=HBM_PEAK_GBS, unit="GB/s", frac=None, traffic=traffic)
+    sec = k["total_ms"] * 1e-3
+    if k["bound"] == "mfma":
+        ach = k["work"] / sec / 1e12
+        r = dict(base, bound="mfma", achieved=round(ach, 3), peak=F32_MFMA_TFLOPS, unit="TFLOP/s",
+                 frac=round(ach / F32_MFMA_TFLOPS, 4), traffic=traffic)
+    else:
+        ach = k["work"] / sec / 1e9
+        r = dict(base, bound="hbm", achieved=round(ach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
+                 frac=round(ach / HBM_PEAK_GBS, 6), traffic=traffic)
     if name == "pk_fps":
-        # LDS/latency-bound sequential kernel: report the HBM stream it needs (xyz in, idx out)
-        n_in = 4000
-        byts = B * (12 * n_in + 8 * N)
-        ach = byts / (avg_ms * 1e-3) / 1e9
-        return {"kernel": name, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None, "avg_ms": round(avg_ms, 4),
-                "note": "sequential npoint-step argmax; latency-bound, HBM fraction is not its limiter"}
-    if name == "pk_feat_dist_topk":
-        flops = B * 2.0 * N * N * 32
-        ach = flops / (avg_ms * 1e-3) / 1e12
-        return {"kernel": name, "bound": "mfma", "achieved": round(ach, 3), "peak": F32_MFMA_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / F32_MFMA_TFLOPS, 4), "traffic": None, "avg_ms": round(avg_ms, 4)}
-    if name in ("pk_ball_query_mask",):
-        byts = B * (48 * N + N * N + 4 * N)
-        ach = byts / (avg_ms * 1e-3) / 1e9
-        return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_ms": round(avg_ms, 4)}
-    return {"kernel": name, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-            "traffic": None, "avg_ms": round(avg_ms, 4)}
+        r["note"] = ("sequential npoint-step argmax, one workgroup per crop: latency-bound; the HBM "
+                     "fraction is reported for completeness, not as its limiter")
+    return r
 
 
 if __name__ == "__main__":

@@ -151,7 +151,7 @@ int pk_attention_bwd(const float* q, const float* k, const float* v, const float
  * models/dpfm.py:22-30; refinement Conv1d(k=1), modeling/dpfm.py:16-26,45-54,82-95):
  * dw[o,i] = sum_r dy[r,o] x[r,i], db[o] = sum_r dy[r,o] over all R = B*N points.
  *   layout 0: x [R, I], dy [R, O] row-major; layout 1: x [R/N, I, N], dy [R/N, O, N]
- *   I, O <= 128; work f32 [ceil(R/128) * (O*I + O)]; db may be NULL. */
+ *   I, O <= 128, O * I <= 8192; work f32 [ceil(R/128) * (O*I + O)]; db may be NULL. */
 int pk_linear_wgrad(const float* x, const float* dy, int layout, int64_t R, int I, int O, int N,
                     float* work, float* dw, float* db, void* stream);
 
@@ -186,10 +186,11 @@ int pk_inlier_ratio(const int64_t* pairs, int ldp, int layout, const int32_t* np
                     void* stream);
 
 /* H15 C_gt (utils/utils.py:67-79 C_from_sparse_P): least squares
- * evecs2[P[:,1], :30] X = evecs1[P[:,0], :30] per crop (fp64 normal equations,
- * Gauss-Jordan with partial pivoting). pairs int64 [B,ldp,2], npairs int64 [B];
- * evecs f32 [B,Vmax,ld]; K must be 30; work f64 [B * ceil(ldp/256) * 1800] partial
- * sums (split over 256-pair slices, summed in slice order); Cgt f32 [B,30,30]. */
+ * evecs2[P[:,1], :30] X = evecs1[P[:,0], :30] per crop (fp64 normal equations: G from the
+ * per-row pair counts, H over 64-pair slices; Gauss-Jordan with partial pivoting).
+ * pairs int64 [B,ldp,2] (any order), npairs int64 [B]; evecs f32 [B,Vmax,ld]; K must be
+ * 30; work f64 [pk_cgt_lstsq_work_size(ldp, V2max, B)]; Cgt f32 [B,30,30]. */
+int64_t pk_cgt_lstsq_work_size(int ldp, int V2max, int B);
 int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs, const float* evecs1, int ld1,
                  int V1max, const float* evecs2, int ld2, int V2max, int B, int K, double* work,
                  float* Cgt, void* stream);

@@ -13,7 +13,7 @@ HEADER = os.path.join(ROOT, "include", "posekern.h")
 def header_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return re.findall(r"\bint\s+(pk_\w+)\s*\(([^;]*)\)\s*;", src)
+    return re.findall(r"\b(?:int|int64_t)\s+(pk_\w+)\s*\(([^;]*)\)\s*;", src)
 
 
 def test_header_declares_entry_points():

@@ -23,10 +23,17 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     benchq) run benchq 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    benche) run benche 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline-probe --eager ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline-probe
           find "$out/prof" -type f ! -name "*stats.csv" -delete ;;
     kbench) run kbench 300 python tools/kbench.py ;;
+    pmc) run pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$out/pmcf" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager --probe-steps 1
+         run pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$out/pmcw" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager --probe-steps 1
+         python tools/pmc_summary.py "$out/pmcf" "$out/pmcw" "$out/pmc_traffic.json" > "$out/pmc_summary.log" 2>&1
+         find "$out/pmcf" "$out/pmcw" -type f -name "*.csv" -size +2M -delete ;;
     diag) run diag 300 python tools/diag_model.py ;;
+    gdiag) run gdiag 300 python tools/graph_diag.py ;;
+    gdiag_rocblas) run gdiag_rocblas 300 python tools/graph_diag.py cublas ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,0 +1,81 @@
+"""Summarise rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE, one counter per pass, as
+MI355X_MICROARCH.md's rocprofv3 section requires) into per-kernel-family HBM traffic per
+launch.
+
+  python tools/pmc_summary.py <fetch_dir> <write_dir> <out.json>
+
+Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE is in KiB and on gfx950
+reports half the bytes of 16-B-per-lane coalesced reads, so it is doubled; WRITE_SIZE
+(KiB) is exact for 16-B-per-lane stores. Both are L2 memory-side request counters,
+with Infinity-Cache hits counted, so this is an upper bound on HBM bytes.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+# libposekern entry point -> device kernels it launches (substring match on the name)
+FAMILIES = {
+    "pk_fps": ["fps_pruned_kernel", "fps_kernel"],
+    "pk_sor": ["sor_knn_kernel", "sor_stats_kernel", "sor_count_kernel", "sor_write_kernel"],
+    "pk_ball_query_mask": ["bq_mask_f32_kernel"],
+    "pk_backproject": ["bp_count_kernel", "bp_write_kernel"],
+    "pk_spectral_diffusion": ["spec_reduce_kernel", "spec_combine_kernel", "spec_expand_kernel"],
+    "pk_attention_fwd": ["attn_fwd_kernel"],
+    "pk_attention_bwd": ["attn_bwd_dq_kernel", "attn_bwd_dkv_kernel"],
+    "pk_linear_wgrad": ["wgrad_partial_kernel", "wgrad_reduce_kernel"],
+    "pk_feat_dist_topk": ["fd_prep_kernel", "fd_main_kernel"],
+    "pk_cgt_lstsq": ["cgt_count_kernel", "cgt_partial_kernel", "cgt_reduce_kernel", "cgt_solve_kernel"],
+}
+# (the first kernel of each family is counted once per family launch)
+
+
+def read(dirpath, counter, min_grid=0, max_grid=None):
+    """kernel name -> (dispatches, summed counter value), dispatches filtered by grid size."""
+    tot = defaultdict(lambda: [0, 0.0])
+    for f in glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                grid = int(float(row.get("Grid_Size", 0) or 0))
+                if grid < min_grid or (max_grid is not None and grid > max_grid):
+                    continue
+                t = tot[row["Kernel_Name"]]
+                t[0] += 1
+                t[1] += float(row["Counter_Value"])
+    return tot
+
+
+# bench.py's configs[3]-size ball-query probe (256 x 2048 x 2048) runs the mask kernel on a
+# grid of 2 x 32 x 256 workgroups of 256 threads; the in-step launches are far smaller
+PROBE_GRID = 2 * 32 * 256 * 256
+
+
+def main():
+    fetch_dir, write_dir, out = sys.argv[1:4]
+    res = {}
+    for fam, names, lo, hi in [(f, n, 0, PROBE_GRID - 1) for f, n in FAMILIES.items()] + \
+            [("pk_ball_query_mask@configs3_probe", FAMILIES["pk_ball_query_mask"], PROBE_GRID, None)]:
+        fetch, write = read(fetch_dir, "FETCH_SIZE", lo, hi), read(write_dir, "WRITE_SIZE", lo, hi)
+        def summed(tab, names=names):
+            n_lead = sum(c for k, (c, _) in tab.items() if names[0] in k)
+            v = sum(s for k, (_, s) in tab.items() if any(nm in k for nm in names))
+            return n_lead, v
+        nf, fb = summed(fetch)
+        nw, wb = summed(write)
+        if nf == 0 or nw == 0:
+            continue
+        fetch_b = 2.0 * fb * 1024 / nf   # KiB -> B, gfx950 x2 read correction, per launch
+        write_b = wb * 1024 / nw
+        res[fam] = {"fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
+                    "traffic_bytes_per_launch": fetch_b + write_b, "launches": nf}
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
