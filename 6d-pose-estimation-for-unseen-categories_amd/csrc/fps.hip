@@ -217,18 +217,22 @@ __global__ __launch_bounds__(NT) void fps_pruned_kernel(
         const bool valid = pd[k] >= 0.f;
         const uint32_t bits = valid ? pk::f32_bits(pd[k]) : 0u;
         const uint32_t wmax = pk::wave_max_u32_s(bits);
-        const uint32_t widx = pk::wave_min_u32_s(
-            valid && bits == wmax ? (uint32_t)(tid + k * NT) : 0xffffffffu);
+        // lanes hold the bucket's indices in increasing order: the first lane at the max
+        // is the lowest index (torch.max's tie rule), no second reduction needed
+        const uint64_t at = __ballot(valid && bits == wmax);
+        const uint32_t widx = (uint32_t)(pk::wave_id() * pk::kWave + k * NT + (__ffsll((unsigned long long)at) - 1));
         if (lane == k) {
           bmb = wmax;
           bmi = widx;
         }
       }
     }
+    // best bucket of the wave: lane k = bucket k and buckets are in increasing index order,
+    // so the first lane at the max holds the lowest index
     const uint32_t bb = bval ? bmb : 0u;
     const uint32_t wmax = PPT <= 16 ? pk::readlane(pk::row_max_u32(bb), 0) : pk::wave_max_u32_s(bb);
-    const uint32_t cand = bval && bb == wmax ? bmi : 0xffffffffu;
-    const uint32_t widx = PPT <= 16 ? pk::readlane(pk::row_min_u32(cand), 0) : pk::wave_min_u32_s(cand);
+    const uint64_t top = __ballot(bval && bb == wmax);
+    const uint32_t widx = top ? pk::readlane(bmi, __ffsll((unsigned long long)top) - 1) : 0xffffffffu;
     uint2* s = slots + (i & 1) * 16;
     if (lane == 0) s[pk::wave_id()] = make_uint2(wmax, widx);
     __syncthreads();

@@ -47,8 +47,15 @@ class DPFMNet(nn.Module):
         verts2, mass2, evals2, evecs2 = s2["xyz"], s2["mass"], s2["evals"], s2["evecs"]
         features1, features2 = (verts1 - 110) / 50, (verts2 - 110) / 50  # models/dpfm.py:53
 
-        feat1 = self.feature_extractor(features1, mass1, evals=evals1, evecs=evecs1)
-        feat2 = self.feature_extractor(features2, mass2, evals=evals2, evecs=evecs2)
+        if features1.dim() == 3 and features1.shape == features2.shape and evecs1.shape == evecs2.shape:
+            # same weights, per-crop operations: one pass over both shapes (2B crops)
+            B = features1.shape[0]
+            feat = self.feature_extractor(torch.cat((features1, features2), 0), torch.cat((mass1, mass2), 0),
+                                          evals=torch.cat((evals1, evals2), 0), evecs=torch.cat((evecs1, evecs2), 0))
+            feat1, feat2 = feat[:B], feat[B:]
+        else:
+            feat1 = self.feature_extractor(features1, mass1, evals=evals1, evecs=evecs1)
+            feat2 = self.feature_extractor(features2, mass2, evals=evals2, evecs=evecs2)
 
         ref_feat1, ref_feat2, overlap_score12, overlap_score21 = self.feat_refiner(verts1, verts2, feat1, feat2, batch)
         use_feat1, use_feat2 = (ref_feat1, ref_feat2) if self.robust else (feat1, feat2)

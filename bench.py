@@ -251,12 +251,13 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(total_ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32 (fp64 crop geometry)", "data": "synthetic (seeded ellipsoid RGB-D frames, random-init DPFM)",
+            "dtype": "fp32", "data": "synthetic (seeded ellipsoid RGB-D frames, random-init DPFM)",
             "config": {"workload": "configs[1] shape: B=32 synthetic 640x480 RGB-D crops/GPU, 1024 pts, "
                                    "training step fwd+bwd (configs[2] semantics, DDP over RCCL when N>1)",
                        "execution": "eager" if args.eager else ("hip-graph" if args.no_overlap else
                                                                  "hip-graph, crop formation overlapped"),
                        "global_batch": B * world, "points_per_crop": N, "cad_points": N,
+                       "precision": "model fp32 (f32 MFMA); crop geometry / C_gt normal equations fp64",
                        "parallelism": f"dp{world}"},
             "roofline": roof,
             "roofline_mfma_kernels": {k: {"achieved": v["achieved"], "frac": v["frac"], "unit": v["unit"]}
