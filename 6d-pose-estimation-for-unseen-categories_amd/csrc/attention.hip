@@ -7,9 +7,11 @@
 // The reference materialises scores and prob ([B, heads, N, M] fp32, twice per layer);
 // here they live only in registers (online softmax, FlashAttention-2 style), in fp32:
 // products on the f32 MFMA (v_mfma_f32_16x16x4_f32). dim = 16 (gnn_dim 32 / 2 heads,
-// config/dpfm_orig.yaml), so 1/sqrt(dim) = 0.25. Scores are formed in log2 units (one
-// operand pre-scaled by 0.25 log2(e)) so the softmax exponentials are single v_exp_f32
-// (exp2) instructions; the saved lse is a log2-sum-exp2 (internal to these kernels).
+// config/dpfm_orig.yaml), so 1/sqrt(dim) = 0.25 (an exact pre-scale of one operand).
+// Softmax terms are exp2((s - m) * log2 e) on v_exp_f32: the scaling multiplies the
+// small difference s - m, not s, so no extra rounding proportional to |s| enters. The
+// forward saves per query the row max m and 1 / sum (ms [B, heads, N, 2]); the backward
+// rebuilds P = exp2((s - m) log2 e) / sum exactly as the reference's softmax does.
 // K/V (resp. Q/dO) tiles are double-buffered: the next tile's global loads are in
 // flight while the current tile is contracted.
 //
@@ -20,7 +22,7 @@
 //
 // Kernels (one workgroup = 4 waves x 16 rows = 64 rows of one (crop, head)):
 //   attn_fwd_kernel     queries; streams 64-key tiles of K, V through LDS; writes out
-//                       and lse = m + log2(sum) per query (saved for the backward)
+//                       and (m, 1 / sum) per query (saved for the backward)
 //   attn_bwd_dq_kernel  queries; delta = rowsum(dO * O) then dQ = 0.25 dS K
 //   attn_bwd_dkv_kernel keys; streams 64-query tiles of Q, dO; dV = P^T dO,
 //                       dK = 0.25 dS^T Q with dS = P (dP - delta), dP = dO V^T
@@ -50,7 +52,6 @@ __device__ __forceinline__ float grp_sum(float v) {
 }
 
 constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kScale2 = 0.25f * kLog2e;  // scores in log2 units
 
 __device__ __forceinline__ float exp2_(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
   const float* vb = v + ((int64_t)b * kD * H + h) * M;
   float qr[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) qr[s] = qi < N ? qb[(int64_t)(4 * s + g) * H * N + qi] * kScale2 : 0.f;
+  for (int s = 0; s < 4; ++s) qr[s] = qi < N ? qb[(int64_t)(4 * s + g) * H * N + qi] * kScale : 0.f;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   float m = -__builtin_huge_valf(), l = 0.f;
   Tile kt = load_tile(kb, H * M, M, 0), vt = load_tile(vb, H * M, M, 0);
@@ -127,14 +128,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
       }
     mt = grp_max(mt);
     const float mn = fmaxf(m, mt);
-    const float alpha = m == -__builtin_huge_valf() ? 0.f : exp2_(m - mn);
+    const float alpha = m == -__builtin_huge_valf() ? 0.f : exp2_((m - mn) * kLog2e);
     m = mn;
     float ps = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2_(st[t][r] - mn);
+        const float p = exp2_((st[t][r] - mn) * kLog2e);
         st[t][r] = p;
         ps += p;
       }
@@ -152,7 +153,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
     float* ob = out + ((int64_t)b * kD * H + h) * N;
 #pragma unroll
     for (int r = 0; r < 4; ++r) ob[(int64_t)(4 * g + r) * H * N + qi] = acc[r] * inv;
-    if (g == 0) lse[((int64_t)b * H + h) * N + qi] = m + log2f(l);
+    if (g == 0) {
+      float2* ms = reinterpret_cast<float2*>(lse) + ((int64_t)b * H + h) * N + qi;
+      *ms = make_float2(m, inv);
+    }
   }
 }
 
@@ -174,12 +178,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int64_t a = qoff + (int64_t)(4 * s + g) * H * N + qi;
-    qr[s] = qi < N ? q[a] * kScale2 : 0.f;
+    qr[s] = qi < N ? q[a] * kScale : 0.f;
     dor[s] = qi < N ? dout[a] : 0.f;
     dl = fmaf(dor[s], qi < N ? o[a] : 0.f, dl);
   }
   dl = grp_sum(dl);  // delta = sum_d dO * O for query qi
-  const float ls = qi < N ? lse[((int64_t)b * H + h) * N + qi] : __builtin_huge_valf();
+  const float2 ms = qi < N ? reinterpret_cast<const float2*>(lse)[((int64_t)b * H + h) * N + qi]
+                           : make_float2(__builtin_huge_valf(), 0.f);
   if (qi < N && g == 0) delta[((int64_t)b * H + h) * N + qi] = dl;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   Tile kt = load_tile(kb, H * M, M, 0), vt = load_tile(vb, H * M, M, 0);
@@ -202,7 +207,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = k0 + 16 * t + 4 * g + r < M ? exp2_(st[r] - ls) : 0.f;
+        const float p = k0 + 16 * t + 4 * g + r < M ? exp2_((st[r] - ms.x) * kLog2e) * ms.y : 0.f;
         const float ds = p * (dp[r] - dl);
         acc = mfma(KT[(16 * t + 4 * g + r) * kSC + c], ds, acc);
       }
@@ -222,20 +227,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
   __shared__ float Os[kD * kSR];  // dO as [d][q]
   __shared__ float QT[kT * kSC];
   __shared__ float OT[kT * kSC];  // dO as [q][d]
-  __shared__ float Ls[kT], Ds[kT];
+  __shared__ float Ls[kT], Is[kT], Ds[kT];
   const int h = blockIdx.y, b = blockIdx.z;
   const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
   const int kj = blockIdx.x * kT + pk::wave_id() * 16 + c;
   const int64_t koff = ((int64_t)b * kD * H + h) * M;
   const float* qb = q + ((int64_t)b * kD * H + h) * N;
   const float* gb = dout + ((int64_t)b * kD * H + h) * N;
-  const float* lb = lse + ((int64_t)b * H + h) * N;
+  const float2* lb = reinterpret_cast<const float2*>(lse) + ((int64_t)b * H + h) * N;
   const float* db = delta + ((int64_t)b * H + h) * N;
   float kr[4], vr[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int64_t a = koff + (int64_t)(4 * s + g) * H * M + kj;
-    kr[s] = kj < M ? k[a] * kScale2 : 0.f;
+    kr[s] = kj < M ? k[a] * kScale : 0.f;
     vr[s] = kj < M ? v[a] : 0.f;
   }
   f32x4 dka = {0.f, 0.f, 0.f, 0.f}, dva = {0.f, 0.f, 0.f, 0.f};
@@ -246,7 +251,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
     store_tile(gt, Os, OT);
     if (threadIdx.x < kT) {
       const int qq = q0 + threadIdx.x;
-      Ls[threadIdx.x] = qq < N ? lb[qq] : __builtin_huge_valf();  // exp2(s - inf) = 0
+      const float2 ms = qq < N ? lb[qq] : make_float2(__builtin_huge_valf(), 0.f);  // exp2(-inf) = 0
+      Ls[threadIdx.x] = ms.x;
+      Is[threadIdx.x] = ms.y;
       Ds[threadIdx.x] = qq < N ? db[qq] : 0.f;
     }
     __syncthreads();
@@ -259,13 +266,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
       f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        st = mfma(Qs[(4 * s + g) * kSR + 16 * t + c], kr[s], st);  // S[q][key] (log2 units)
+        st = mfma(Qs[(4 * s + g) * kSR + 16 * t + c], kr[s], st);  // S[q][key]
         dp = mfma(Os[(4 * s + g) * kSR + 16 * t + c], vr[s], dp);  // dP[q][key]
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = 16 * t + 4 * g + r;
-        const float p = exp2_(st[r] - Ls[qq]);
+        const float p = exp2_((st[r] - Ls[qq]) * kLog2e) * Is[qq];
         const float ds = p * (dp[r] - Ds[qq]);
         dva = mfma(OT[qq * kSC + c], p, dva);   // dV^T[d][key] += dO^T[d][q] P[q][key]
         dka = mfma(QT[qq * kSC + c], ds, dka);  // dK^T[d][key] += Q^T[d][q] dS[q][key]

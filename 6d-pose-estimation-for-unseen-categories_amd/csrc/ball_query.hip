@@ -197,6 +197,203 @@ __global__ __launch_bounds__(kBqThreads) void bq_mask_f32_kernel(
   if (lane < kRowsPerWave && row0 + lane < n1max) rowcount[(int64_t)b * n1max + row0 + lane] = cnt[lane];
 }
 
+// ---------------------------------------------------------------------------------
+// Streaming mask kernel (the default for n2max < 65536).
+//
+// Same fp32 screen + exact fp64 band recheck as bq_mask_f32_kernel, re-arranged so
+// that the per-pair VALU work is ~6 instructions and the kernel runs at the mask-write
+// (HBM) rate:
+//   * per workgroup, the crop's columns are converted ONCE into LDS as float4
+//     {-2bx, -2by, -2bz, |b|^2} (lane-major slots: conflict-free ds_read_b128), and
+//     the 64 rows' per-row constants {ax, ay, az, lo'', W} once by wave 0;
+//   * per pair: q = fma-chain(|b|^2; a.(-2b)) (3 FMA), d = q - lo'' (1 sub) where
+//     lo'' = nextafter(fl(lo - |a|^2), +inf); "in" <=> q <= fl(lo - |a|^2) <=> sign(d);
+//     the in-bits of 4 columns are gathered into one 4-byte word by two v_perm_b32
+//     sign-replicating selects;
+//   * ambiguity: a lane tracks min_u32(bits(d)); non-negative floats order as their
+//     bits and negative ones sort above them, so one unsigned compare against
+//     bits(W), W = fl(hi'' - lo''), flags any pair in (lo, hi] (rare -> fp64 recheck);
+//   * row counts accumulate two rows per register (16-bit fields) and are reduced
+//     across the wave once per 16 rows;
+//   * blocks are renumbered so that a crop's row blocks land on one XCD (shared L2
+//     for its column data).
+// The classification is the one bq_mask_f32_kernel proves exact: the
+// margin is unchanged, and moving |a|^2 to the threshold side replaces one rounding
+// of (|a|^2 + |b|^2) by one rounding of (lo - |a|^2), covered by the 2u*thr2 term.
+constexpr int kStageCols = 2048;  // columns converted into LDS per stage (32 KiB)
+using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
+
+__device__ __forceinline__ float next_up(float x) {  // nextafter(x, +inf) for finite x
+  const uint32_t b = __float_as_uint(x);
+  if (x == 0.f) return __uint_as_float(1u);  // +-0 -> smallest positive subnormal
+  return __uint_as_float(x > 0.f ? b + 1u : b - 1u);
+}
+
+__global__ __launch_bounds__(kBqThreads) void bq_mask_stream_kernel(
+    const double* __restrict__ cad, const int64_t* __restrict__ cad_off,
+    const double* __restrict__ pc, const int64_t* __restrict__ pc_off,
+    const double* __restrict__ thr2v, int n1max, int ld, int nrb, uint8_t* __restrict__ mask,
+    int32_t* __restrict__ rowcount) {
+  __shared__ __attribute__((aligned(16))) float4 scol[kStageCols];
+  __shared__ __attribute__((aligned(16))) float4 srow[kRowsPerBlock];
+  __shared__ uint32_t srowW[kRowsPerBlock];
+  __shared__ uint32_t sbm[kBqThreads / pk::kWave];
+
+  // XCD-aware renumbering: hardware block L runs on XCD L % 8; give each XCD a
+  // contiguous range of logical blocks (bijective for any grid size).
+  const int G = gridDim.x, L = blockIdx.x;
+  const int q8 = G >> 3, r8 = G & 7, x8 = L & 7;
+  const int logical = x8 * q8 + min(x8, r8) + (L >> 3);
+  const int b = logical / nrb;
+  const int rb = logical - b * nrb;
+
+  const int64_t c0 = cad_off[b], p0 = pc_off[b];
+  const int n1 = (int)(cad_off[b + 1] - c0);
+  const int n2 = (int)(pc_off[b + 1] - p0);
+  const double thr2 = thr2v[b];
+  const int tid = threadIdx.x, lane = pk::lane_id(), wave = pk::wave_id();
+  const int rowblk0 = rb * kRowsPerBlock;
+  const int row0 = rowblk0 + wave * kRowsPerWave;
+  const double ox = n1 > 0 ? cad[c0 * 3 + 0] : 0.0;
+  const double oy = n1 > 0 ? cad[c0 * 3 + 1] : 0.0;
+  const double oz = n1 > 0 ? cad[c0 * 3 + 2] : 0.0;
+  const float u = 5.9604645e-8f;  // 2^-24
+  const float thr2f = (float)thr2;
+  const float R = sqrtf(thr2f) * 1.001f;
+  const int ncols = mask != nullptr ? ld : n2;
+
+  uint32_t mine = 0;  // lane r < 16: in-pairs of row row0 + r
+
+  for (int s0 = 0; s0 < ncols; s0 += kStageCols) {
+    const int scols = min(kStageCols, ncols - s0);
+    const int spad = (scols + kColsPerWave - 1) & ~(kColsPerWave - 1);
+    __syncthreads();  // previous stage's readers are done with scol / srow
+    // ---- columns -> LDS. Column jj (stage-relative) of chunk k = jj / 1024 sits in
+    // slot k*1024 + (jj % 16) * 64 + (jj % 1024) / 16: lane l's c-th column is
+    // contiguous across lanes for every c. Slots past the crop get never-within padding.
+    float bm = 0.f;
+    for (int jj = tid; jj < spad; jj += kBqThreads) {
+      const int j = s0 + jj;
+      float4 v;
+      if (j < n2) {
+        const double* qd = pc + (p0 + j) * 3;
+        const float bx = (float)(qd[0] - ox), by = (float)(qd[1] - oy), bz = (float)(qd[2] - oz);
+        v = make_float4(-2.f * bx, -2.f * by, -2.f * bz, fmaf(bz, bz, fmaf(by, by, bx * bx)));
+        bm = fmaxf(bm, fmaxf(fabsf(bx), fmaxf(fabsf(by), fabsf(bz))));
+      } else {
+        v = make_float4(0.f, 0.f, 0.f, __builtin_huge_valf());
+      }
+      const int k = jj >> 10, w = jj & 1023;
+      scol[(k << 10) + ((w & 15) << 6) + (w >> 4)] = v;
+    }
+    uint32_t bmb = pk::wave_max_u32_s(__float_as_uint(bm));  // bm >= 0: bits order = value order
+    if (lane == 0) sbm[wave] = bmb;
+    __syncthreads();
+    bmb = max(max(sbm[0], sbm[1]), max(sbm[2], sbm[3]));
+    // ---- per-row constants (wave 0), with this stage's column bound
+    if (wave == 0) {
+      const int i = rowblk0 + lane;
+      float4 rv = make_float4(0.f, 0.f, 0.f, -__builtin_huge_valf());  // padding row: d = +inf
+      uint32_t wb = 0u;
+      if (i < n1) {
+        const double* a = cad + (c0 + i) * 3;
+        const float ax = (float)(a[0] - ox), ay = (float)(a[1] - oy), az = (float)(a[2] - oz);
+        const float a2 = fmaf(az, az, fmaf(ay, ay, ax * ax));
+        const float S = fmaxf(fabsf(ax), fmaxf(fabsf(ay), fabsf(az))) + __uint_as_float(bmb);
+        const float E0 = 1.01f * u * S;
+        const float margin = 2.f * (3.f * E0 * (2.f * R + E0) + 21.f * u * S * S + 2.f * u * thr2f) + 1e-30f;
+        const float lo_r = (thr2f - margin) - a2;
+        const float hi_r = (thr2f + margin) - a2;
+        const float lo2 = next_up(lo_r);
+        const float W = hi_r - lo2;
+        rv = make_float4(ax, ay, az, lo2);
+        wb = W > 0.f ? __float_as_uint(W) : 0u;
+      }
+      srow[lane] = rv;
+      srowW[lane] = wb;
+    }
+    __syncthreads();
+    if (row0 >= n1max) continue;  // every barrier above stays uniform
+
+    for (int ch = 0; ch < scols; ch += kColsPerWave) {
+      const int j0 = s0 + ch + lane * kColsPerLane;  // first column of this lane
+      float mx[kColsPerLane], my[kColsPerLane], mz[kColsPerLane], b2[kColsPerLane];
+#pragma unroll
+      for (int c = 0; c < kColsPerLane; ++c) {
+        const float4 v = scol[ch + (c << 6) + lane];
+        mx[c] = v.x;
+        my[c] = v.y;
+        mz[c] = v.z;
+        b2[c] = v.w;
+      }
+      const bool store = mask != nullptr && (ch + lane * kColsPerLane) < scols;
+#pragma unroll 1
+      for (int rp = 0; rp < kRowsPerWave; rp += 2) {
+      uint32_t pair_cnt = 0;  // this lane's in-pairs of rows rp (low 16 bits) and rp+1 (high)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = rp + h;
+        const int i = row0 + r;
+        if (i >= n1max) break;  // wave-uniform
+        const float4 rv = srow[wave * kRowsPerWave + r];
+        const uint32_t Wb = srowW[wave * kRowsPerWave + r];
+        float d[kColsPerLane];
+        uint32_t mn = 0xffffffffu;
+#pragma unroll
+        for (int c = 0; c < kColsPerLane; ++c) {
+          const float qv = fmaf(rv.x, mx[c], fmaf(rv.y, my[c], fmaf(rv.z, mz[c], b2[c])));
+          d[c] = qv - rv.w;
+          mn = min(mn, __float_as_uint(d[c]));
+        }
+        // 0x01 where sign(d) = 1 (in). v_perm_b32 selectors 9 / 11 replicate the sign
+        // bit of src1 / src0 into a byte; 12 gives 0x00.
+        uint32_t w[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const uint32_t lo = __builtin_amdgcn_perm(__float_as_uint(d[4 * m + 1]), __float_as_uint(d[4 * m]),
+                                                    0x0c0c0b09u);
+          const uint32_t hi = __builtin_amdgcn_perm(__float_as_uint(d[4 * m + 3]), __float_as_uint(d[4 * m + 2]),
+                                                    0x0b090c0cu);
+          w[m] = (lo | hi) & 0x01010101u;
+        }
+        if (__builtin_expect(mn <= Wb, 0)) {  // rare: exact fp64 recheck of the band
+          uint32_t amb = 0;
+#pragma unroll
+          for (int c = 0; c < kColsPerLane; ++c) amb |= (__float_as_uint(d[c]) <= Wb ? 1u : 0u) << c;
+          const double* a = cad + (c0 + i) * 3;
+          const double ax64 = a[0], ay64 = a[1], az64 = a[2];
+          uint32_t fix = 0, todo = amb;
+          while (todo) {
+            const int c = __ffs(todo) - 1;
+            todo &= todo - 1;
+            const double* qd = pc + (p0 + j0 + c) * 3;
+            fix |= (within(ax64, ay64, az64, qd[0], qd[1], qd[2], thr2) ? 1u : 0u) << c;
+          }
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {  // spread 4 bits to 4 bytes: (nibble * 0x204081) & 0x01010101
+            const uint32_t clr = ((((amb >> (4 * m)) & 0xfu) * 0x204081u) & 0x01010101u) * 0xffu;
+            const uint32_t set = (((fix >> (4 * m)) & 0xfu) * 0x204081u) & 0x01010101u;
+            w[m] = (w[m] & ~clr) | set;
+          }
+        }
+        pair_cnt += (uint32_t)(__popc(w[0]) + __popc(w[1]) + __popc(w[2]) + __popc(w[3])) << (h * 16);
+        if (store) {
+          u32x4* dst = reinterpret_cast<u32x4*>(mask + ((int64_t)b * n1max + i) * ld + j0);
+          const u32x4 val = {w[0], w[1], w[2], w[3]};
+          __builtin_nontemporal_store(val, dst);
+        }
+      }
+      // both rows' totals at once (16-bit fields: a row holds < 65536 pairs); lane r
+      // keeps row r's running count
+      const uint32_t t = (uint32_t)pk::wave_sum_i32_s((int)pair_cnt);
+      if ((lane >> 1) == (rp >> 1)) mine += (lane & 1) ? (t >> 16) : (t & 0xffffu);
+      }
+    }
+  }
+  if (row0 >= n1max) return;
+  if (lane < kRowsPerWave && row0 + lane < n1max) rowcount[(int64_t)b * n1max + row0 + lane] = (int32_t)mine;
+}
+
 // Count-only variant (no mask); same arithmetic.
 __global__ __launch_bounds__(kBqThreads) void bq_count_kernel(
     const double* __restrict__ cad, const int64_t* __restrict__ cad_off,
@@ -336,6 +533,25 @@ extern "C" int pk_ball_query_mask(const double* cad, const int64_t* cad_off, con
   PK_REQUIRE(cad && cad_off && pc && pc_off && thr2 && rowcount);
   PK_REQUIRE(mask == nullptr || (ld >= n2max && ld % kColsPerLane == 0));
   hipStream_t s = pk::as_stream(stream);
+  const int nrb = (n1max + kRowsPerBlock - 1) / kRowsPerBlock;
+  if (n2max < 65536 && (int64_t)nrb * B < (1ll << 31)) {
+    hipLaunchKernelGGL(bq_mask_stream_kernel, dim3(nrb * B), dim3(kBqThreads), 0, s, cad, cad_off, pc,
+                       pc_off, thr2, n1max, ld, nrb, mask, rowcount);
+  } else {
+    dim3 grid(nrb, B);
+    hipLaunchKernelGGL(bq_mask_f32_kernel, grid, dim3(kBqThreads), 0, s, cad, cad_off, pc, pc_off,
+                       thr2, n1max, ld, mask, rowcount);
+  }
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+// Development hook (not in include/posekern.h): the previous fp32-screen kernel, for A/B timing.
+extern "C" int pkdev_ball_query_mask_v1(const double* cad, const int64_t* cad_off, const double* pc,
+                                        const int64_t* pc_off, const double* thr2, int B, int n1max,
+                                        int n2max, uint8_t* mask, int ld, int32_t* rowcount,
+                                        void* stream) {
+  hipStream_t s = pk::as_stream(stream);
   dim3 grid((n1max + kRowsPerBlock - 1) / kRowsPerBlock, B);
   hipLaunchKernelGGL(bq_mask_f32_kernel, grid, dim3(kBqThreads), 0, s, cad, cad_off, pc, pc_off,
                      thr2, n1max, ld, mask, rowcount);
@@ -349,7 +565,7 @@ extern "C" int pkdev_ball_query_mask64(const double* cad, const int64_t* cad_off
                                        int n2max, uint8_t* mask, int ld, int32_t* rowcount,
                                        void* stream) {
   hipStream_t s = pk::as_stream(stream);
-  hipError_t e = hipMemsetAsync(rowcount, 0, sizeof(int32_t) * (size_t)B * n1max, s);
+  hipError_t e = pk::zero_async(rowcount, sizeof(int32_t) * (size_t)B * n1max, s);
   if (e != hipSuccess) return (int)e;
   dim3 grid((ld + kColsPerWave - 1) / kColsPerWave, (n1max + kRowsPerBlock - 1) / kRowsPerBlock, B);
   hipLaunchKernelGGL(bq_mask_kernel, grid, dim3(kBqThreads), 0, s, cad, cad_off, pc, pc_off, thr2,
@@ -371,11 +587,11 @@ extern "C" int pk_ball_query_pairs(const double* cad, const int64_t* cad_off, co
   PK_REQUIRE(mask == nullptr || (ld >= n2max && ld % kColsPerLane == 0));
   hipStream_t s = pk::as_stream(stream);
   if (ov21 != nullptr) {
-    hipError_t e = hipMemsetAsync(ov21, 0, (size_t)B * n2max, s);
+    hipError_t e = pk::zero_async(ov21, (size_t)B * n2max, s);
     if (e != hipSuccess) return (int)e;
   }
   if (n1max == 0) {
-    hipError_t e = hipMemsetAsync(count, 0, sizeof(int64_t) * B, s);
+    hipError_t e = pk::zero_async(count, sizeof(int64_t) * B, s);
     return e == hipSuccess ? PK_OK : (int)e;
   }
   hipLaunchKernelGGL(bq_scan_kernel, dim3(B), dim3(1024), 0, s, rowcount, n1max, rowoff, count);

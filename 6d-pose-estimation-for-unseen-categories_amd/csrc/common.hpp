@@ -168,3 +168,27 @@ __device__ __forceinline__ int wave_sum_i32_s(int v) {
                readlane((uint32_t)v, 48));
 }
 }  // namespace pk
+
+namespace pk {
+// Zero-fill on the stream with a kernel instead of hipMemsetAsync: memset nodes captured
+// into a HIP graph were observed not to order correctly against the kernels around them
+// on replay (ROCm 7.2, tools/replay_diag3.py), so no libposekern entry point issues one.
+namespace {  // one copy per translation unit
+__global__ void zero_fill_kernel(uint8_t* __restrict__ p, size_t n) {
+  const size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (i + 16 <= n && (((uintptr_t)p) & 15) == 0) {
+    *reinterpret_cast<uint4*>(p + i) = make_uint4(0u, 0u, 0u, 0u);
+  } else {
+    for (size_t k = i; k < n && k < i + 16; ++k) p[k] = 0;
+  }
+}
+
+inline hipError_t zero_async(void* p, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  const size_t threads = (bytes + 15) / 16;
+  const unsigned blocks = (unsigned)((threads + 255) / 256);
+  hipLaunchKernelGGL(zero_fill_kernel, dim3(blocks), dim3(256), 0, s, static_cast<uint8_t*>(p), bytes);
+  return hipGetLastError();
+}
+}  // namespace
+}  // namespace pk

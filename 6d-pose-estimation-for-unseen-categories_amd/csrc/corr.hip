@@ -413,7 +413,7 @@ extern "C" int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs
   double* partG = partH + (int64_t)B * SH * kFF;
   double* GH = partG + (int64_t)B * SG * kFF;
   int32_t* cnt = reinterpret_cast<int32_t*>(GH + (int64_t)B * 2 * kFF);
-  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(int32_t) * (size_t)B * V2max, s);
+  hipError_t e = pk::zero_async(cnt, sizeof(int32_t) * (size_t)B * V2max, s);
   if (e != hipSuccess) return (int)e;
   if (ldp > 0) {
     hipLaunchKernelGGL(cgt_count_kernel, dim3((ldp + 255) / 256, B), dim3(256), 0, s, pairs, ldp, npairs, V2max,
@@ -427,6 +427,81 @@ extern "C" int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs
                      npairs, ldp, V2max, GH);
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(cgt_solve_kernel, dim3(B), dim3(64), 0, s, GH, Cgt);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+// ---------------------------------------------------------------- NCE pair selection
+// utils/loss.py:27-30: per crop, `num` distinct rows of its pair list drawn uniformly
+// without replacement (np.random.choice(P, num, replace=False)), all rows when the crop
+// has fewer. Drawn on the device with a keyed pseudo-random bijection of [0, m)
+// (m = min(count, cap)): position i < min(num, m) takes row perm(i), so rows are
+// distinct by construction; perm = cycle-walked composition of invertible maps on
+// [0, 2^p) (odd multiply + add mod 2^p, xor-shift right). No sort, no memset, no host
+// RNG: capture-safe. The key mixes (seed, *ctr, crop); *ctr advances by one per call.
+namespace {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ uint32_t perm_step(uint32_t x, uint32_t mask, int sh, const uint32_t (&k)[3]) {
+  x = (x * 0x9E3779B1u + k[0]) & mask;
+  x ^= x >> sh;
+  x = (x * 0x85EBCA77u + k[1]) & mask;
+  x ^= x >> sh;
+  x = (x * 0xC2B2AE3Du + k[2]) & mask;
+  x ^= x >> sh;
+  return x;
+}
+
+// grid (ceil(k / 256), B), block 256
+__global__ __launch_bounds__(256) void nce_select_kernel(const int64_t* __restrict__ count, int64_t cap, int k,
+                                                         uint64_t seed, const int64_t* __restrict__ ctr,
+                                                         int64_t* __restrict__ rows, uint8_t* __restrict__ valid) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= k) return;
+  const int64_t m64 = count[b] < cap ? count[b] : cap;
+  const uint32_t m = (uint32_t)(m64 > 0 ? m64 : 0);
+  const int64_t o = (int64_t)b * k + i;
+  if ((uint32_t)i >= m) {  // fewer pairs than draws: the tail is padding
+    rows[o] = 0;
+    valid[o] = 0;
+    return;
+  }
+  int p = 1;
+  while ((1u << p) < m) ++p;
+  const uint32_t mask = (p >= 32) ? 0xffffffffu : ((1u << p) - 1u);
+  const int sh = (p + 1) / 2;
+  const uint64_t h = splitmix64(seed ^ splitmix64((uint64_t)ctr[0] * 0x100000001B3ull + (uint64_t)b));
+  const uint32_t kk[3] = {(uint32_t)h, (uint32_t)(h >> 32), (uint32_t)splitmix64(h)};
+  uint32_t y = (uint32_t)i;
+  do {
+    y = perm_step(y, mask, sh, kk);
+  } while (y >= m);  // cycle walking: terminates on i's own cycle
+  rows[o] = (int64_t)y;
+  valid[o] = 1;
+}
+
+__global__ void ctr_advance_kernel(int64_t* ctr) { ctr[0] += 1; }
+
+}  // namespace
+
+extern "C" int pk_nce_select(const int64_t* count, int B, int64_t cap, int num, uint64_t seed, int64_t* ctr,
+                             int64_t* rows, uint8_t* valid, void* stream) {
+  PK_REQUIRE(B >= 0 && cap >= 0 && num >= 0 && cap < (1ll << 31));
+  const int k = (int)(num < cap ? num : cap);
+  if (B == 0 || k == 0) return PK_OK;
+  PK_REQUIRE(count && ctr && rows && valid);
+  hipStream_t s = pk::as_stream(stream);
+  hipLaunchKernelGGL(nce_select_kernel, dim3((k + 255) / 256, B), dim3(256), 0, s, count, cap, k, seed, ctr, rows,
+                     valid);
+  PK_CHECK_LAUNCH();
+  hipLaunchKernelGGL(ctr_advance_kernel, dim3(1), dim3(1), 0, s, ctr);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -539,7 +539,7 @@ extern "C" int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, in
     hipLaunchKernelGGL(seg_scan_kernel, dim3(B), dim3(1024), 0, s, ccount, nchunk, coff, kept);
     PK_CHECK_LAUNCH();
   } else {
-    hipError_t e = hipMemsetAsync(kept, 0, sizeof(int64_t) * B, s);
+    hipError_t e = pk::zero_async(kept, sizeof(int64_t) * B, s);
     if (e != hipSuccess) return (int)e;
   }
   hipLaunchKernelGGL(offsets_kernel, dim3(1), dim3(64), 0, s, kept, B, out_off);

@@ -12,10 +12,16 @@
 // column a running argmin (or sorted top-5) in the epilogue; sqrt is monotone and is
 // applied to the emitted distances only. Ties resolve to the lowest row index.
 //
-// Layout: per crop, rows i < n1[b] of evecs_x [B, V1max, ldx], C [B, 30, 30], rows
-// j < n2[b] of evecs_y [B, V2max, ldy]. Pass 1 (prep) builds the augmented operands
-// A [B, V1max, 32], Bq [B, V2max, 32]; pass 2 tiles 64 columns per workgroup (16 per
-// wave) and streams all rows through LDS in 64-row chunks.
+// Pass 1 (prep) writes both augmented operands straight into MFMA operand order:
+// for a 16-row tile T, lane l = 16 g + c (g = k mod 4 group, c = row in tile) owns the
+// 8 floats k = 4 s + g, s = 0..7, of row 16 T + c — so pass 2 loads one operand set
+// with two 16-byte loads per lane and no LDS, no transposes, no barriers.
+//   A  [B, T1, 64 lanes, 8]  T1 = ceil16(V1max) / 16   (x side, rows reduced over)
+//   Bq [B, T2, 64 lanes, 8]  T2 = ceil16(V2max) / 16   (y side, one column set per wave)
+// Pass 2: a wave owns 16 columns (its B operand stays in 8 VGPRs) and streams every
+// row tile of A through registers, two tiles per step on independent accumulators
+// with the next two tiles' loads in flight, so the matrix pipe issues back to back
+// while the other wave on the SIMD runs its epilogue.
 #include "common.hpp"
 
 namespace {
@@ -24,59 +30,75 @@ constexpr int kF = 30;   // n_fmap
 constexpr int kK = 32;   // augmented contraction length
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 
-// grid (ceil(max(V1,V2)/256), B, 2): z = 0 -> A rows (x side), z = 1 -> B rows (y side).
+// grid (ceil(max(T1, T2) * 16 / 64), B, 2), block 256: thread = (row r = tid / 4, group
+// g = tid % 4) computes the 8 augmented entries k = 4 s + g of its row.
+//   z = 0 (x side): emb = x C^T; entries -2 emb[k] (k < 30), |emb|^2 (k = 30), 1 (k = 31)
+//   z = 1 (y side): y[k] (k < 30), 1 (k = 30), |y|^2 (k = 31)
+// |.|^2 is the fmaf chain over k = 0..29 in order (the 4 lanes of a row exchange their
+// values). Rows r >= n[b] (and the tile padding up to 16) are written as zeros.
 __global__ __launch_bounds__(256) void fd_prep_kernel(const float* __restrict__ ex, int ldx,
                                                       const float* __restrict__ C,
                                                       const float* __restrict__ ey, int ldy,
                                                       const int32_t* __restrict__ n1,
-                                                      const int32_t* __restrict__ n2, int V1max,
-                                                      int V2max, float* __restrict__ A,
+                                                      const int32_t* __restrict__ n2, int V1max, int V2max,
+                                                      int T1, int T2, float* __restrict__ A,
                                                       float* __restrict__ Bq) {
   const int b = blockIdx.y;
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  __shared__ float sC[kF * kF];
-  if (blockIdx.z == 0) {
-    for (int e = threadIdx.x; e < kF * kF; e += 256) sC[e] = C[(int64_t)b * kF * kF + e];
+  const int g = threadIdx.x & 3;
+  const int r = blockIdx.x * 64 + (threadIdx.x >> 2);
+  const bool xside = blockIdx.z == 0;
+  const int T = xside ? T1 : T2;
+  __shared__ float sC[32 * kF];  // rows 30, 31 zero (entries k = 30, 31 are set below)
+  if (xside) {
+    for (int e = threadIdx.x; e < 32 * kF; e += 256) sC[e] = e < kF * kF ? C[(int64_t)b * kF * kF + e] : 0.f;
     __syncthreads();
-    if (r >= V1max) return;
-    float* o = A + ((int64_t)b * V1max + r) * kK;
-    if (r >= n1[b]) {
-      for (int c = 0; c < kK; ++c) o[c] = 0.f;
-      return;
-    }
-    const float* e = ex + ((int64_t)b * V1max + r) * ldx;
-    float x[kF];
-#pragma unroll
-    for (int k = 0; k < kF; ++k) x[k] = e[k];
-    float nrm = 0.f;
-#pragma unroll
-    for (int c = 0; c < kF; ++c) {
-      float s = 0.f;
-#pragma unroll
-      for (int k = 0; k < kF; ++k) s = fmaf(x[k], sC[c * kF + k], s);  // emb = x C^T
-      o[c] = -2.f * s;
-      nrm = fmaf(s, s, nrm);
-    }
-    o[kF] = nrm;
-    o[kF + 1] = 1.f;
-  } else {
-    if (r >= V2max) return;
-    float* o = Bq + ((int64_t)b * V2max + r) * kK;
-    if (r >= n2[b]) {
-      for (int c = 0; c < kK; ++c) o[c] = 0.f;
-      return;
-    }
-    const float* e = ey + ((int64_t)b * V2max + r) * ldy;
-    float nrm = 0.f;
-#pragma unroll
-    for (int k = 0; k < kF; ++k) {
-      const float y = e[k];
-      o[k] = y;
-      nrm = fmaf(y, y, nrm);
-    }
-    o[kF] = 1.f;
-    o[kF + 1] = nrm;
   }
+  if (r >= T * 16) return;  // whole rows (4 adjacent lanes) leave together
+  const int nvalid = xside ? n1[b] : n2[b];
+  const bool valid = r < nvalid;
+  float e[8];  // emb (x side) or y (y side) at k = 4 s + g
+  if (xside) {
+    const float* er = ex + ((int64_t)b * V1max + (valid ? r : 0)) * ldx;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) e[s] = 0.f;
+#pragma unroll 2
+    for (int k = 0; k < kF; ++k) {  // emb[c] = sum_k x[k] C[c][k], fmaf chain in k order
+      const float xk = valid ? er[k] : 0.f;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) e[s] = fmaf(xk, sC[(4 * s + g) * kF + k], e[s]);
+    }
+  } else {
+    const float* er = ey + ((int64_t)b * V2max + (valid ? r : 0)) * ldy;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int c = 4 * s + g;
+      e[s] = (valid && c < kF) ? er[c] : 0.f;
+    }
+  }
+  float nrm = 0.f;
+  const int base = threadIdx.x & ~3;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const float q = __shfl(e[s], base | gg);
+      if (4 * s + gg < kF) nrm = fmaf(q, q, nrm);
+    }
+  }
+  float v[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) v[s] = xside ? -2.f * e[s] : e[s];
+  if (!valid) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) v[s] = 0.f;
+  } else if (g >= 2) {  // k = 30, 31
+    v[7] = (xside == (g == 2)) ? nrm : 1.f;
+  }
+  const int tile = r >> 4, c16 = r & 15;
+  float* dst = (xside ? A + (int64_t)b * T1 * 512 : Bq + (int64_t)b * T2 * 512) +
+               ((int64_t)tile * 64 + g * 16 + c16) * 8;
+  reinterpret_cast<float4*>(dst)[0] = make_float4(v[0], v[1], v[2], v[3]);
+  reinterpret_cast<float4*>(dst)[1] = make_float4(v[4], v[5], v[6], v[7]);
 }
 
 template <int TOPK>
@@ -92,6 +114,12 @@ struct TopK {
   }
   // rows arrive in increasing index order: strict < keeps the lowest index on ties
   __device__ __forceinline__ void push(float x, int idx) {
+    if (TOPK == 1) {
+      const bool lt = x < v[0];
+      v[0] = lt ? x : v[0];
+      i[0] = lt ? idx : i[0];
+      return;
+    }
     if (!(x < v[TOPK - 1])) return;
     float cv = x;
     int ci = idx;
@@ -126,58 +154,65 @@ struct TopK {
   }
 };
 
-constexpr int kRowsChunk = 64;
-constexpr int kLdsRow = kK + 4;  // padded row (floats)
+__device__ __forceinline__ void load_tile(const float* __restrict__ At, int t, int lane, float (&a)[8]) {
+  const float4* p = reinterpret_cast<const float4*>(At + ((int64_t)t * 64 + lane) * 8);
+  const float4 u = p[0], w = p[1];
+  a[0] = u.x; a[1] = u.y; a[2] = u.z; a[3] = u.w;
+  a[4] = w.x; a[5] = w.y; a[6] = w.z; a[7] = w.w;
+}
 
-// grid (ceil(V2max/64), B), block 256 (4 waves x 16 columns).
+template <int TOPK>
+__device__ __forceinline__ void epilogue(const f32x4& acc, int ibase, int N1, bool partial, TopK<TOPK>& best) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = ibase + r;
+    float v = fmaxf(acc[r], 1e-30f);  // clamp_min(1e-30) (cdist mm path)
+    if (partial && i >= N1) v = __builtin_huge_valf();
+    best.push(v, i);
+  }
+}
+
+// grid (ceil(T2 / 4), B), block 256: wave w owns column tile 4 * blockIdx.x + w.
 template <int TOPK>
 __global__ __launch_bounds__(256) void fd_main_kernel(const float* __restrict__ A, const float* __restrict__ Bq,
                                                       const int32_t* __restrict__ n1,
-                                                      const int32_t* __restrict__ n2, int V1max, int V2max,
+                                                      const int32_t* __restrict__ n2, int T1, int T2, int V2max,
                                                       int64_t* __restrict__ out_idx,
                                                       float* __restrict__ out_dist) {
-  __shared__ __attribute__((aligned(16))) float sA[kRowsChunk * kLdsRow];
   const int b = blockIdx.y;
   const int lane = pk::lane_id(), wave = pk::wave_id();
   const int g = lane >> 4, c16 = lane & 15;
-  const int j = blockIdx.x * 64 + wave * 16 + c16;
+  const int ct = blockIdx.x * 4 + wave;
+  if (ct >= T2) return;
+  const int j = ct * 16 + c16;
   const int N1 = n1[b], N2 = n2[b];
-  // B operand: lane supplies Bq[j][4s + g] for step s
   float bop[8];
-  {
-    const float* br = Bq + ((int64_t)b * V2max + min(j, V2max - 1)) * kK;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) bop[s] = br[4 * s + g];
-  }
+  load_tile(Bq + (int64_t)b * T2 * 512, ct, lane, bop);
+  const float* At = A + (int64_t)b * T1 * 512;
+  const int nt = (N1 + 15) >> 4;  // row tiles holding valid rows
   TopK<TOPK> best;
   best.init();
-  for (int i0 = 0; i0 < N1; i0 += kRowsChunk) {
-    __syncthreads();
-    // stage rows [i0, i0+64) of A as [row][g][s] (k = 4s + g) so a lane's 8 operands are contiguous
-    for (int e = threadIdx.x; e < kRowsChunk * kK; e += 256) {
-      const int rr = e / kK, k = e % kK;
-      const int i = i0 + rr;
-      const float v = i < N1 ? A[((int64_t)b * V1max + i) * kK + k] : 0.f;
-      sA[rr * kLdsRow + (k & 3) * 8 + (k >> 2)] = v;
+  float a0[8], a1[8], p0[8], p1[8];
+  if (nt > 0) load_tile(At, 0, lane, p0);
+  if (nt > 1) load_tile(At, 1, lane, p1);
+  for (int t = 0; t < nt; t += 2) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      a0[s] = p0[s];
+      a1[s] = p1[s];
     }
-    __syncthreads();
+    if (t + 2 < nt) load_tile(At, t + 2, lane, p0);
+    if (t + 3 < nt) load_tile(At, t + 3, lane, p1);
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < kRowsChunk / 16; ++t) {
-      const float4* ap = reinterpret_cast<const float4*>(&sA[(t * 16 + c16) * kLdsRow + g * 8]);
-      const float4 a0 = ap[0], a1 = ap[1];
-      const float aop[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(aop[s], bop[s], acc, 0, 0, 0);
-      // lane holds D[i0 + 16t + 4g + r][j]
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = i0 + t * 16 + 4 * g + r;
-        float v = fmaxf(acc[r], 1e-30f);  // clamp_min(1e-30) (cdist mm path)
-        if (i >= N1) v = __builtin_huge_valf();
-        best.push(v, i);
-      }
+    for (int s = 0; s < 8; ++s) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], bop[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], bop[s], acc1, 0, 0, 0);
     }
+    // lane holds D[16 t + 4 g + r][j] (acc0) and D[16 (t+1) + 4 g + r][j] (acc1)
+    const bool last = t + 2 >= nt;
+    epilogue<TOPK>(acc0, t * 16 + 4 * g, N1, last, best);
+    if (t + 1 < nt) epilogue<TOPK>(acc1, (t + 1) * 16 + 4 * g, N1, last, best);
   }
   // merge the 4 lane groups of each column (lanes c16, c16+16, c16+32, c16+48)
 #pragma unroll
@@ -210,16 +245,17 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
   if (B == 0 || V2max == 0) return PK_OK;
   PK_REQUIRE(evecs_x && C && evecs_y && n1 && n2 && A && Bq && out_idx);
   hipStream_t s = pk::as_stream(stream);
-  const int vm = V1max > V2max ? V1max : V2max;
-  hipLaunchKernelGGL(fd_prep_kernel, dim3((vm + 255) / 256, B, 2), dim3(256), 0, s, evecs_x, ldx, C, evecs_y, ldy,
-                     n1, n2, V1max, V2max, A, Bq);
+  const int T1 = (V1max + 15) / 16, T2 = (V2max + 15) / 16;
+  const int rows = (T1 > T2 ? T1 : T2) * 16;
+  hipLaunchKernelGGL(fd_prep_kernel, dim3((rows + 63) / 64, B, 2), dim3(256), 0, s, evecs_x, ldx, C, evecs_y, ldy,
+                     n1, n2, V1max, V2max, T1, T2, A, Bq);
   PK_CHECK_LAUNCH();
   if (topk == 1)
-    hipLaunchKernelGGL(fd_main_kernel<1>, dim3((V2max + 63) / 64, B), dim3(256), 0, s, A, Bq, n1, n2, V1max,
-                       V2max, out_idx, out_dist);
+    hipLaunchKernelGGL(fd_main_kernel<1>, dim3((T2 + 3) / 4, B), dim3(256), 0, s, A, Bq, n1, n2, T1, T2, V2max,
+                       out_idx, out_dist);
   else
-    hipLaunchKernelGGL(fd_main_kernel<5>, dim3((V2max + 63) / 64, B), dim3(256), 0, s, A, Bq, n1, n2, V1max,
-                       V2max, out_idx, out_dist);
+    hipLaunchKernelGGL(fd_main_kernel<5>, dim3((T2 + 3) / 4, B), dim3(256), 0, s, A, Bq, n1, n2, T1, T2, V2max,
+                       out_idx, out_dist);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -158,8 +158,8 @@ extern "C" int pk_linear_wgrad(const float* x, const float* dy, int layout, int6
   hipStream_t s = pk::as_stream(stream);
   const int S = (int)((R + kSlice - 1) / kSlice);
   if (S == 0) {
-    hipError_t e = hipMemsetAsync(dw, 0, sizeof(float) * O * I, s);
-    if (e == hipSuccess && db) e = hipMemsetAsync(db, 0, sizeof(float) * O, s);
+    hipError_t e = pk::zero_async(dw, sizeof(float) * O * I, s);
+    if (e == hipSuccess && db) e = pk::zero_async(db, sizeof(float) * O, s);
     return e == hipSuccess ? PK_OK : (int)e;
   }
   PK_REQUIRE(x && dy && work);

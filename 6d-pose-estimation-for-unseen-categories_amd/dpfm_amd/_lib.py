@@ -43,6 +43,7 @@ SIGNATURES = {
     "pk_rigidity_filter": [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P],
     "pk_inlier_ratio": [_P, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P],
     "pk_cgt_lstsq_work_size": [_I, _I, _I],
+    "pk_nce_select": [_P, _I, _I64, _I, ctypes.c_uint64, _P, _P, _P, _P],
     "pk_cgt_lstsq": [_P, _I, _P, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P],
     "pk_ransac": [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _I64, _D, _I, _P, _P, _P, _P, _P, _P],
     "pk_pose_metrics": [_P, _P, _I, _I, _P, _P, _P, _P, _P],

@@ -283,7 +283,7 @@ class _Attention(torch.autograd.Function):
         B, D, H, N = q.shape
         M = k.shape[3]
         out = torch.empty_like(q)
-        lse = torch.empty((B, H, N), dtype=torch.float32, device=q.device)
+        lse = torch.empty((B, H, N, 2), dtype=torch.float32, device=q.device)  # (row max, 1/sum)
         call("pk_attention_fwd", ptr(q), ptr(k), ptr(v), B, D, H, N, M, ptr(out), ptr(lse), _lib.stream(q.device),
              work=("mfma", 2 * 2 * N * M * D * B * H))  # S = Q K^T, O = P V
         ctx.save_for_backward(q, k, v, out, lse)
@@ -348,14 +348,27 @@ def feat_dist_topk(evecs_x: torch.Tensor, C: torch.Tensor, evecs_y: torch.Tensor
     B, V1, ldx = evecs_x.shape
     _, V2, ldy = evecs_y.shape
     dev = evecs_x.device
-    A = torch.empty((B, V1, 32), dtype=torch.float32, device=dev)
-    Bq = torch.empty((B, V2, 32), dtype=torch.float32, device=dev)
+    # augmented operands in MFMA operand-tile order, rows padded to a multiple of 16
+    A = torch.empty((B, (V1 + 15) // 16 * 16, 32), dtype=torch.float32, device=dev)
+    Bq = torch.empty((B, (V2 + 15) // 16 * 16, 32), dtype=torch.float32, device=dev)
     idx = torch.empty((B, V2, topk), dtype=torch.int64, device=dev)
     dist = torch.empty((B, V2, topk), dtype=torch.float32, device=dev) if want_dist else None
     call("pk_feat_dist_topk", ptr(evecs_x.contiguous()), ldx, ptr(C.contiguous()), ptr(evecs_y.contiguous()), ldy,
          ptr(n1), ptr(n2), B, V1, V2, int(topk), ptr(A), ptr(Bq), ptr(idx), ptr(dist), _lib.stream(dev),
          work=("mfma", 2 * B * V1 * V2 * 32))
     return idx, dist
+
+
+def nce_select(counts: torch.Tensor, cap: int, num: int, seed: int, ctr: torch.Tensor):
+    """pk_nce_select: rows int64 [B, k], valid bool [B, k], k = min(num, cap); advances ctr."""
+    B = counts.shape[0]
+    k = min(int(num), int(cap))
+    dev = counts.device
+    rows = torch.empty((B, k), dtype=torch.int64, device=dev)
+    valid = torch.empty((B, k), dtype=torch.bool, device=dev)
+    call("pk_nce_select", ptr(counts), B, int(cap), int(num), ctypes_u64(seed), ptr(ctr), ptr(rows), ptr(valid),
+         _lib.stream(dev))
+    return rows, valid
 
 
 def rigidity_thresholds(diam: Sequence[float], device) -> torch.Tensor:

@@ -118,6 +118,31 @@ class TrainStep:
         self.gen.manual_seed(seed)
         self.flat = torch.zeros(sum(p.numel() for p in self.params), dtype=torch.float32, device=dev)
 
+    def nce_counter(self) -> torch.Tensor:
+        """The device step counter keying this step's NCE pair draws (utils/loss.py)."""
+        from .utils.loss import _NCE_CTR
+        dev = self.params[0].device
+        key = (id(self.gen), str(dev))
+        if key not in _NCE_CTR:
+            _NCE_CTR[key] = torch.zeros(1, dtype=torch.int64, device=dev)
+        return _NCE_CTR[key]
+
+    @torch.no_grad()
+    def load_state_from(self, other: "TrainStep") -> None:
+        """Copy parameters, optimizer state and the NCE draw counter of `other` in place
+        (tensor storages are kept, so a captured graph over `self` stays valid)."""
+        for p, q in zip(self.params, other.params):
+            p.copy_(q)
+        for p, q in zip(self.params, other.params):
+            sp, sq = self.opt.state.get(p, {}), other.opt.state.get(q, {})
+            for k, v in sq.items():
+                if k in sp and torch.is_tensor(sp[k]):
+                    sp[k].copy_(v)
+                else:
+                    sp[k] = v.clone() if torch.is_tensor(v) else v
+            self.opt.state[p] = sp
+        self.nce_counter().copy_(other.nce_counter())
+
     def allreduce_grads(self, grads=None):
         """DDP's gradient averaging in one bucket (49,281 f32 = 197 KB: latency-bound).
         `grads` defaults to the parameters' .grad tensors."""

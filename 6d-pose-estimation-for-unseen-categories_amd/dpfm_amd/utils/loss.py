@@ -14,19 +14,25 @@ from ..dpfm_utils import FrobeniusLoss
 __all__ = ["FrobeniusLoss", "NCESoftmaxLoss", "DPFMLoss", "nce_select"]
 
 
+_NCE_CTR: dict = {}
+
+
 def nce_select(counts: torch.Tensor, cap: int, num: int, generator: Optional[torch.Generator] = None):
     """Per crop, `num` distinct pair rows drawn uniformly without replacement when the crop
     has more than `num` pairs, all rows otherwise (utils/loss.py:27-30). Returns
-    (rows int64 [B, num], valid bool [B, num])."""
-    B = counts.shape[0]
+    (rows int64 [B, min(num, cap)], valid bool [B, min(num, cap)]).
+
+    Drawn by pk_nce_select (keyed bijection on the device: no sort, no memset, no host
+    RNG, so it can sit inside a HIP graph). The key is the generator's seed plus a
+    device step counter owned by that generator, advanced by every call."""
+    from .. import ops
     dev = counts.device
-    keys = torch.rand((B, cap), device=dev, generator=generator)
-    col = torch.arange(cap, device=dev)[None]
-    keys = torch.where(col < counts[:, None], keys, torch.full_like(keys, 2.0))
-    k = min(num, cap)
-    rows = torch.topk(keys, k, dim=1, largest=False).indices
-    valid = torch.arange(k, device=dev)[None] < torch.clamp(counts, max=num)[:, None]
-    return rows, valid
+    seed = int(generator.initial_seed()) if generator is not None else 0
+    key = (id(generator), str(dev))
+    ctr = _NCE_CTR.get(key)
+    if ctr is None:
+        ctr = _NCE_CTR[key] = torch.zeros(1, dtype=torch.int64, device=dev)
+    return ops.nce_select(counts.to(torch.int64).contiguous(), int(cap), int(num), seed, ctr)
 
 
 class NCESoftmaxLoss(nn.Module):
@@ -39,6 +45,9 @@ class NCESoftmaxLoss(nn.Module):
         """Per-crop NCE loss [B]: pairs [B, cap, 2], rows/valid from nce_select."""
         f1n, f2n = F.normalize(f1, p=2, dim=-1), F.normalize(f2, p=2, dim=-1)
         sel = torch.gather(pairs, 1, rows[..., None].expand(-1, -1, 2))
+        # rows past a crop's pair count select unwritten slots of the pair buffer: point
+        # them at row 0 so the feature gathers stay in bounds (their terms are masked)
+        sel = torch.where(valid[..., None], sel, torch.zeros_like(sel))
         q = torch.gather(f1n, 1, sel[..., 0:1].expand(-1, -1, f1n.shape[-1]))
         k = torch.gather(f2n, 1, sel[..., 1:2].expand(-1, -1, f2n.shape[-1]))
         logits = -torch.cdist(q, k) / self.nce_t
@@ -57,10 +66,27 @@ class NCESoftmaxLoss(nn.Module):
         return self.forward_batched(features_1.squeeze(0)[None], features_2.squeeze(0)[None], pairs, rows, valid)[0]
 
 
+class _BCE(torch.autograd.Function):
+    """F.binary_cross_entropy(reduction='none') with ATen's formulas (log terms clamped at
+    -100; gradient (x - t) / max(x (1 - x), 1e-12)) but without the library kernel's
+    device-side range assert, which inside a HIP graph aborts the whole queue instead of
+    surfacing as a NaN loss."""
+
+    @staticmethod
+    def forward(ctx, x, t):
+        ctx.save_for_backward(x, t)
+        return (t - 1) * torch.clamp(torch.log1p(-x), min=-100) - t * torch.clamp(torch.log(x), min=-100)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, t = ctx.saved_tensors
+        return g * (x - t) / torch.clamp((1 - x) * x, min=1e-12), None
+
+
 def weighted_bce_batched(pred, gt):
     """Upstream WeightedBCELoss per crop: pred/gt [B, N] -> [B] (padding counts, as in the
     reference where collate pads the overlap masks)."""
-    loss = F.binary_cross_entropy(pred, gt, reduction="none")
+    loss = _BCE.apply(pred, gt)
     w_neg = gt.sum(1, keepdim=True) / gt.shape[1]
     w = torch.where(gt >= 0.5, 1 - w_neg, w_neg)
     return (w * loss).mean(1)

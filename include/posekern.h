@@ -139,7 +139,7 @@ int pk_fmap_solve_backward(const float* AAt, const float* BAt, const float* D, f
  * [B, heads, N, M] score/probability tensors. fp32, dim D = 16 only.
  *   q f32 [B, D, H, N], k / v f32 [B, D, H, M] (heads interleaved as the reference's
  *   view(B, dim, heads, N) of a [B, D*H, N] projection), out f32 [B, D, H, N],
- *   lse f32 [B, H, N] log-sum-exp of the scaled scores per query (for the backward).
+ *   lse f32 [B, H, N, 2]: per query the row max m and 1 / sum of exp(s - m) (for the backward).
  * Backward: dout like out; delta f32 [B, H, N] scratch; dq like q, dk / dv like k. */
 int pk_attention_fwd(const float* q, const float* k, const float* v, int B, int D, int H, int N,
                      int M, float* out, float* lse, void* stream);
@@ -160,7 +160,8 @@ int pk_linear_wgrad(const float* x, const float* dy, int layout, int64_t R, int 
  * rows of dist.sort(dim=-2)) with dist = cdist(evecs_x[:, :30] @ C^T, evecs_y[:, :30]).
  *   evecs_x f32 [B,V1max,ldx] (first 30 columns used), C f32 [B,30,30],
  *   evecs_y f32 [B,V2max,ldy]; n1/n2 int32 [B] valid rows
- *   A f32 [B,V1max,32], Bq f32 [B,V2max,32] scratch (augmented cdist operands)
+ *   A f32 [B,ceil16(V1max),32], Bq f32 [B,ceil16(V2max),32] scratch (augmented cdist
+ *   operands, written in MFMA operand-tile order)
  *   out_idx int64 [B,V2max,topk] ascending distance (ties: lower index); out_dist f32
  *   [B,V2max,topk] Euclidean distances (may be NULL). fp32 MFMA, fused epilogue. */
 int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, const float* evecs_y, int ldy,
@@ -191,6 +192,14 @@ int pk_inlier_ratio(const int64_t* pairs, int ldp, int layout, const int32_t* np
  * pairs int64 [B,ldp,2] (any order), npairs int64 [B]; evecs f32 [B,Vmax,ld]; K must be
  * 30; work f64 [pk_cgt_lstsq_work_size(ldp, V2max, B)]; Cgt f32 [B,30,30]. */
 int64_t pk_cgt_lstsq_work_size(int ldp, int V2max, int B);
+
+/* NCE pair selection (utils/loss.py:27-30: np.random.choice(P, num, replace=False) per
+ * crop, every row when P <= num). count int64 [B] pair-list lengths (capped at cap);
+ * k = min(num, cap); rows int64 [B, k] distinct rows of [0, min(count, cap)) drawn by a
+ * keyed pseudo-random bijection, valid uint8 [B, k] (0 on the padding tail, whose rows
+ * are 0). ctr int64 [1] device step counter mixed into the key, incremented per call. */
+int pk_nce_select(const int64_t* count, int B, int64_t cap, int num, uint64_t seed, int64_t* ctr,
+                  int64_t* rows, uint8_t* valid, void* stream);
 int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs, const float* evecs1, int ld1,
                  int V1max, const float* evecs2, int ld2, int V2max, int B, int K, double* work,
                  float* Cgt, void* stream);

@@ -3,6 +3,8 @@ import os
 import subprocess
 import sys
 
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")  # see dpfm_amd/__init__.py (HIP-graph memset replays)
+
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -19,7 +19,7 @@ run() {  # name timeout cmd...
 }
 for step in "$@"; do
   case $step in
-    tests) run tests 900 python -m pytest tests -m gpu -q ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     benchq) run benchq 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
@@ -32,6 +32,15 @@ for step in "$@"; do
          python tools/pmc_summary.py "$out/pmcf" "$out/pmcw" "$out/pmc_traffic.json" > "$out/pmc_summary.log" 2>&1
          find "$out/pmcf" "$out/pmcw" -type f -name "*.csv" -size +2M -delete ;;
     diag) run diag 300 python tools/diag_model.py ;;
+    tprof) run tprof 300 python tools/torch_prof.py "$tag" ;;
+    rdiag) run rdiag 300 python tools/replay_diag.py default ;;
+    rdiag2) run rdiag2 300 python tools/replay_diag2.py ;;
+    rdiag3) run rdiag3 300 python tools/replay_diag3.py ;;
+    gdump) run gdump 300 python tools/graph_dump.py "$tag" ;;
+    mprobe) run mprobe 300 python tools/memset_graph_probe.py ;;
+    mprobe_nopc) DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run mprobe_nopc 300 python tools/memset_graph_probe.py ;;
+    gtrace) run gtrace 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d "$out/gtrace" -o run -- python tools/graph_dump.py "$tag" ;;
+    rdiag_rocblas) run rdiag_rocblas 300 python tools/replay_diag.py cublas ;;
     gdiag) run gdiag 300 python tools/graph_diag.py ;;
     gdiag_rocblas) run gdiag_rocblas 300 python tools/graph_diag.py cublas ;;
     *) echo "unknown step $step"; exit 2 ;;

@@ -91,8 +91,13 @@ g, out_c = capture(lambda: cf(fb))
 g.replay()
 torch.cuda.synchronize()
 okc = True
-for name in ("pc64", "align64", "pairs", "npairs", "overlap_12", "overlap_21", "off", "kept"):
+for name in ("pc64", "align64", "npairs", "overlap_12", "overlap_21", "off", "kept"):
     okc &= cmp(name, getattr(ref_c, name).double(), getattr(out_c, name).double(), exact=True)
+# pair lists: only the first npairs[b] rows are written (the rest of the buffer is scratch)
+cap = ref_c.pairs.shape[1]
+valid = torch.arange(cap, device=dev)[None] < torch.clamp(ref_c.npairs, max=cap)[:, None]
+okc &= cmp("pairs[:npairs]", (ref_c.pairs * valid[..., None]).double(), (out_c.pairs * valid[..., None]).double(),
+           exact=True)
 stage("C crop formation", okc)
 
 # D / E: the real step (same RNG stream on both sides; warm-ups on a side stream)

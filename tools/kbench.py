@@ -73,6 +73,17 @@ for B, N in [(32, 1024), (256, 2048)]:
     f64 = lambda: _lib.lib().pkdev_ball_query_mask64(ptr(cad), ptr(off), ptr(pc), ptr(off), ptr(thr), B, N, N, ptr(mask), ld, ptr(rc), s)
     ms = timeit(f64)
     print(f"ball_query_mask (all fp64) B={B} N={N}: {ms:.3f} ms, {byts/ms/1e6:.1f} GB/s algorithmic; same={torch.equal(m1, mask) and torch.equal(r1, rc)}")
+    fv1 = lambda: _lib.lib().pkdev_ball_query_mask_v1(ptr(cad), ptr(off), ptr(pc), ptr(off), ptr(thr), B, N, N, ptr(mask), ld, ptr(rc), s)
+    ms = timeit(fv1)
+    print(f"ball_query_mask (v1 f32 screen) B={B} N={N}: {ms:.3f} ms, {byts/ms/1e6:.1f} GB/s algorithmic; same={torch.equal(m1, mask) and torch.equal(r1, rc)}")
+    # dense case: a large share of the pairs within r, many near the boundary
+    thr_d = torch.full((B,), ops.ball_threshold(8.0), dtype=torch.float64, device=dev)
+    fd = lambda: call("pk_ball_query_mask", ptr(cad), ptr(off), ptr(pc), ptr(off), ptr(thr_d), B, N, N, ptr(mask), ld, ptr(rc), s)
+    ms = timeit(fd)
+    md = mask.clone(); rd = rc.clone()
+    _lib.lib().pkdev_ball_query_mask64(ptr(cad), ptr(off), ptr(pc), ptr(off), ptr(thr_d), B, N, N, ptr(mask), ld, ptr(rc), s)
+    print(f"ball_query_mask dense (r=8, {float(rd.double().mean())/N:.3f} in) B={B} N={N}: {ms:.3f} ms, "
+          f"{byts/ms/1e6:.1f} GB/s; same as fp64={torch.equal(md, mask) and torch.equal(rd, rc)}")
     f2 = lambda: ops.ball_query(cad, off, pc, off, [0.6] * B, N, N, 64 * N, thr2=thr)
     ms = timeit(f2)
     print(f"ball_query full (mask+scan+pairs) B={B} N={N}: {ms:.3f} ms")

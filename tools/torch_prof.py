@@ -1,0 +1,42 @@
+"""Development aid: which torch op (and input shapes) launches which device kernels in one
+eager training step (bench.py's workload), via torch.profiler. Writes the op table and
+the per-kernel table to gpurun_out/<tag>/torch_prof_*.txt.
+
+  python tools/torch_prof.py [tag] [batch]
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "6d-pose-estimation-for-unseen-categories_amd")]
+import torch  # noqa: E402
+from torch.profiler import ProfilerActivity, profile  # noqa: E402
+
+from dpfm_amd.dataset.object import CropFormation  # noqa: E402
+from dpfm_amd.models.dpfm import DPFMNet  # noqa: E402
+from dpfm_amd.pipeline import TrainStep, make_frame_batch  # noqa: E402
+
+tag = sys.argv[1] if len(sys.argv) > 1 else "tprof"
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+out = os.path.join(ROOT, "gpurun_out", tag)
+os.makedirs(out, exist_ok=True)
+dev = torch.device("cuda:0")
+torch.manual_seed(1234)
+model = DPFMNet().to(dev)
+fb, op = make_frame_batch(B, 1024, 1024, seed=0, device=dev)
+crops_of = CropFormation(n1=1024, npoint=1024, seed=0)
+step = TrainStep(model, seed=0)
+for _ in range(3):
+    step(op, crops_of(fb))
+torch.cuda.synchronize()
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+    for _ in range(2):
+        step(op, crops_of(fb))
+    torch.cuda.synchronize()
+with open(os.path.join(out, "torch_prof_ops.txt"), "w") as f:
+    f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=80,
+                                                               max_name_column_width=60,
+                                                               max_shapes_column_width=80))
+with open(os.path.join(out, "torch_prof_kernels.txt"), "w") as f:
+    f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60, max_name_column_width=90))
+print("ok", out)
