@@ -111,43 +111,225 @@ __global__ __launch_bounds__(256) void wgrad_partial_kernel(const float* __restr
 }
 
 // dw[e] = sum_s part[s, e] (e < O*I), db[o] = sum_s partb[s, o]. Block = 64 outputs x
-// 4 slice quarters (4 interleaved chains each), combined in a fixed order: deterministic.
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
-                                                           const float* __restrict__ partb, int S,
-                                                           int OI, int O, float* __restrict__ dw,
-                                                           float* __restrict__ db) {
-  __shared__ float red[4][64];
+// 16 slice groups (two interleaved chains each), combined by a fixed pairwise tree:
+// deterministic, and 16 loads in flight per output instead of a serial walk over S.
+constexpr int kRedGroups = 16;
+__global__ __launch_bounds__(64 * kRedGroups) void wgrad_reduce_kernel(const float* __restrict__ part,
+                                                                       const float* __restrict__ partb, int S,
+                                                                       int OI, int O, float* __restrict__ dw,
+                                                                       float* __restrict__ db) {
+  __shared__ float red[kRedGroups][64];
   const int e = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int qtr = threadIdx.x >> 6;
+  const int grp = threadIdx.x >> 6;
   const bool is_w = e < OI;
   const bool is_b = !is_w && e < OI + O && db != nullptr;
   float v = 0.f;
   if (is_w || is_b) {
     const float* p = is_w ? part + e : partb + (e - OI);
     const int64_t st = is_w ? OI : O;
-    const int s0 = (S * qtr) / 4, s1 = (S * (qtr + 1)) / 4;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    const int s0 = (S * grp) / kRedGroups, s1 = (S * (grp + 1)) / kRedGroups;
+    float a0 = 0.f, a1 = 0.f;
     int s = s0;
-    for (; s + 4 <= s1; s += 4) {
+    for (; s + 2 <= s1; s += 2) {
       a0 += p[(int64_t)s * st];
       a1 += p[(int64_t)(s + 1) * st];
-      a2 += p[(int64_t)(s + 2) * st];
-      a3 += p[(int64_t)(s + 3) * st];
     }
-    for (; s < s1; ++s) a0 += p[(int64_t)s * st];
-    v = (a0 + a1) + (a2 + a3);
+    if (s < s1) a0 += p[(int64_t)s * st];
+    v = a0 + a1;
   }
-  red[qtr][threadIdx.x & 63] = v;
+  red[grp][threadIdx.x & 63] = v;
   __syncthreads();
-  if (qtr == 0 && (is_w || is_b)) {
-    const int t = threadIdx.x;
-    const float r = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+#pragma unroll
+  for (int half = kRedGroups / 2; half >= 1; half >>= 1) {
+    if (grp < half) red[grp][threadIdx.x & 63] += red[grp + half][threadIdx.x & 63];
+    __syncthreads();
+  }
+  if (grp == 0 && (is_w || is_b)) {
+    const float r = red[0][threadIdx.x & 63];
     if (is_w) dw[e] = r;
     else db[e - OI] = r;
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Direct-load variant (the default): v_mfma_f32_32x32x2_f32 takes its operands straight
+// from global memory, no LDS staging and no barriers in the row loop.
+//   A[m][k] = dY[row k][o0 + m], B[k][n] = X[row k][i0 + n]  ->  D = dW tile [32 x 32]
+// Lane l supplies A[l & 31][l >> 5] and B[l >> 5][l & 31], i.e. one value of row
+// r(step, h = l >> 5) at channel (l & 31). Rows are taken in batches of 16 (8 k-steps):
+//   layout 0 ([R, C]): r = rb + 2 s + h       (32 lanes read 128 contiguous bytes)
+//   layout 1 ([Bn, C, N], N % 16 == 0): r = rb + 8 h + s  (a lane's 8 rows are 8
+//            consecutive n of one channel: two 16-byte loads)
+// Both operands use the same r(s, h), so the contraction is the same sum over rows.
+// Workgroup = one row slice; its 4 waves split the 32x32 output tiles (T = To * Ti <= 16)
+// and, when there are fewer than 4 tiles, the slice's batches; wave row groups are
+// combined through LDS in a fixed order (deterministic). Bias = row sums of the A values
+// of the tiles with ti == 0.
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+template <int LAYOUT>
+__device__ __forceinline__ void load8(const float* __restrict__ p, int C, int c, int N, int64_t rb, int64_t r1,
+                                      int h, float (&v)[8]) {
+  if (LAYOUT == 0) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int64_t r = rb + 2 * s + h;
+      v[s] = (c < C && r < r1) ? p[r * C + c] : 0.f;
+    }
+  } else {
+    if (c < C) {
+      const int64_t b = rb / N;
+      const int64_t n = rb - b * N + 8 * h;
+      const float4* q = reinterpret_cast<const float4*>(p + (b * C + c) * N + n);
+      const float4 u = q[0], w = q[1];
+      v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
+      v[4] = w.x; v[5] = w.y; v[6] = w.z; v[7] = w.w;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) v[s] = 0.f;
+    }
+  }
+}
+
+// Operands of one 16-row batch for a wave's J tiles.
+template <int J>
+struct WgradBatch {
+  float a[J][8], b[J][8];
+};
+
+template <int LAYOUT, int J>
+__device__ __forceinline__ void wgrad_load(WgradBatch<J>& B, const float* __restrict__ x, const float* __restrict__ dy,
+                                           int I, int O, int N, int Ti, int T, int tw, int WT, int m, int h,
+                                           int64_t rb, int64_t r1) {
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int t = tw + WT * j;
+    if (t < T) {
+      const int to = t / Ti, ti = t - to * Ti;
+      load8<LAYOUT>(dy, O, to * 32 + m, N, rb, r1, h, B.a[j]);
+      load8<LAYOUT>(x, I, ti * 32 + m, N, rb, r1, h, B.b[j]);
+    }
+  }
+}
+
+template <int J>
+__device__ __forceinline__ void wgrad_mma(const WgradBatch<J>& B, f32x16 (&acc)[J], float (&bs)[J], int Ti, int T,
+                                          int tw, int WT) {
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int t = tw + WT * j;
+    if (t < T) {
+#pragma unroll
+      for (int st = 0; st < 8; ++st) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(B.a[j][st], B.b[j][st], acc[j], 0, 0, 0);
+      if (t % Ti == 0) {
+#pragma unroll
+        for (int st = 0; st < 8; ++st) bs[j] += B.a[j][st];
+      }
+    }
+  }
+}
+
+// 8 waves per workgroup: WT = min(T, 8) tile lanes x WR = 8 / WT row groups; J tiles per
+// wave (J = 2 only for T = 16). The next batch's loads are issued before the current
+// batch's MFMAs (two register buffers, statically indexed).
+constexpr int kV2Waves = 8;
+
+template <int LAYOUT, int J>
+__global__ __launch_bounds__(64 * kV2Waves) void wgrad_v2_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ dy, int64_t R, int I,
+                                                                 int O, int N, int SL, float* __restrict__ part,
+                                                                 float* __restrict__ partb) {
+  __shared__ float comb[kV2Waves][16 * 64];
+  __shared__ float combb[kV2Waves][64];
+  const int s = blockIdx.x;
+  const int lane = pk::lane_id(), w = pk::wave_id();
+  const int m = lane & 31, h = lane >> 5;
+  const int To = (O + 31) >> 5, Ti = (I + 31) >> 5, T = To * Ti;
+  const int WT = T < kV2Waves ? T : kV2Waves;
+  const int WR = kV2Waves / WT;
+  const int tw = w % WT, g = w / WT;
+  const bool active = g < WR;
+  f32x16 acc[J];
+  float bs[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    bs[j] = 0.f;
+  }
+  const int64_t r0 = (int64_t)s * SL;
+  const int64_t r1 = r0 + SL < R ? r0 + SL : R;
+  const int nb = (int)((r1 - r0 + 15) / 16);
+  if (active) {
+    WgradBatch<J> b0, b1;
+    int q = g;
+    if (q < nb) wgrad_load<LAYOUT, J>(b0, x, dy, I, O, N, Ti, T, tw, WT, m, h, r0 + 16ll * q, r1);
+    for (; q < nb; q += 2 * WR) {
+      const bool has1 = q + WR < nb;
+      if (has1) wgrad_load<LAYOUT, J>(b1, x, dy, I, O, N, Ti, T, tw, WT, m, h, r0 + 16ll * (q + WR), r1);
+      wgrad_mma<J>(b0, acc, bs, Ti, T, tw, WT);
+      if (has1) {
+        if (q + 2 * WR < nb) wgrad_load<LAYOUT, J>(b0, x, dy, I, O, N, Ti, T, tw, WT, m, h, r0 + 16ll * (q + 2 * WR), r1);
+        wgrad_mma<J>(b1, acc, bs, Ti, T, tw, WT);
+      }
+    }
+  }
+  // combine row groups (only when WT < 8, i.e. one tile per wave) in group order
+  if (WR > 1) {
+    if (active) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) comb[w][e * 64 + lane] = acc[0][e];
+      combb[w][lane] = bs[0];
+    }
+    __syncthreads();
+    if (!active || g != 0) return;
+    for (int gg = 1; gg < WR; ++gg) {
+      const int src = tw + WT * gg;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[0][e] += comb[src][e * 64 + lane];
+      bs[0] += combb[src][lane];
+    }
+  }
+  if (!active) return;
+  float* __restrict__ ps = part + (int64_t)s * O * I;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int t = tw + WT * j;
+    if (t < T) {
+      const int to = t / Ti, ti = t - to * Ti;
+      const int i = ti * 32 + m;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int o = to * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (o < O && i < I) ps[(int64_t)o * I + i] = acc[j][e];
+      }
+      if (ti == 0) {
+        const float tot = bs[j] + __shfl_xor(bs[j], 32);  // the two row halves
+        const int o = to * 32 + m;
+        if (h == 0 && o < O) partb[(int64_t)s * O + o] = tot;
+      }
+    }
+  }
+}
+
 }  // namespace
+
+// Development hook (not in include/posekern.h): the LDS-staged slice kernel, for A/B timing.
+extern "C" int pkdev_linear_wgrad_v1(const float* x, const float* dy, int layout, int64_t R, int I, int O, int N,
+                                     float* work, float* dw, float* db, void* stream) {
+  hipStream_t s = pk::as_stream(stream);
+  const int S = (int)((R + kSlice - 1) / kSlice);
+  if (S == 0) return PK_ERR_ARG;
+  float* part = work;
+  float* partb = work + (int64_t)S * O * I;
+  hipLaunchKernelGGL(wgrad_partial_kernel, dim3(S), dim3(256), 0, s, x, dy, layout, R, I, O, N, part, partb);
+  PK_CHECK_LAUNCH();
+  const int total = O * I + O;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(64 * kRedGroups), 0, s, part, partb, S, O * I, O,
+                     dw, db);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
 
 extern "C" int pk_linear_wgrad(const float* x, const float* dy, int layout, int64_t R, int I, int O, int N,
                                float* work, float* dw, float* db, void* stream) {
@@ -164,12 +346,36 @@ extern "C" int pk_linear_wgrad(const float* x, const float* dy, int layout, int6
   }
   PK_REQUIRE(x && dy && work);
   float* part = work;
-  float* partb = work + (int64_t)S * O * I;
-  hipLaunchKernelGGL(wgrad_partial_kernel, dim3(S), dim3(256), 0, s, x, dy, layout, R, I, O, N, part, partb);
+  // direct-load kernel: slices of >= 128 rows (so S never exceeds the documented work
+  // size), ~320 slices for the large calls; channels-first needs N % 16 == 0
+  int S2 = S;
+  if (layout == 0 || N % 16 == 0) {
+    int64_t SL = (R + 319) / 320;
+    SL = (SL + 15) / 16 * 16;
+    if (SL < kSlice) SL = kSlice;
+    S2 = (int)((R + SL - 1) / SL);
+    float* partb = work + (int64_t)S2 * O * I;
+    const int T = ((O + 31) / 32) * ((I + 31) / 32);
+    const int J = T <= kV2Waves ? 1 : 2;
+#define PK_WGRAD_V2(L, JJ)                                                                                   \
+  hipLaunchKernelGGL((wgrad_v2_kernel<L, JJ>), dim3(S2), dim3(64 * kV2Waves), 0, s, x, dy, R, I, O, N, (int)SL, \
+                     part, partb)
+    if (layout == 0) {
+      if (J == 1) PK_WGRAD_V2(0, 1);
+      else PK_WGRAD_V2(0, 2);
+    } else {
+      if (J == 1) PK_WGRAD_V2(1, 1);
+      else PK_WGRAD_V2(1, 2);
+    }
+#undef PK_WGRAD_V2
+  } else {
+    float* partb = work + (int64_t)S * O * I;
+    hipLaunchKernelGGL(wgrad_partial_kernel, dim3(S), dim3(256), 0, s, x, dy, layout, R, I, O, N, part, partb);
+  }
   PK_CHECK_LAUNCH();
   const int total = O * I + O;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(256), 0, s, part, partb, S, O * I, O,
-                     dw, db);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(64 * kRedGroups), 0, s, part,
+                     work + (int64_t)S2 * O * I, S2, O * I, O, dw, db);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -27,6 +27,8 @@ for step in "$@"; do
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline-probe
           find "$out/prof" -type f ! -name "*stats.csv" -delete ;;
     kbench) run kbench 300 python tools/kbench.py ;;
+    kprof) run kprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kprof" -o run -- python tools/kbench.py
+          find "$out/kprof" -type f ! -name "*stats.csv" -delete ;;
     pmc) run pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$out/pmcf" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager --probe-steps 1
          run pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$out/pmcw" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager --probe-steps 1
          python tools/pmc_summary.py "$out/pmcf" "$out/pmcw" "$out/pmc_traffic.json" > "$out/pmc_summary.log" 2>&1

@@ -90,3 +90,29 @@ for B, N in [(32, 1024), (256, 2048)]:
     f3 = lambda: ops.ball_query(cad, off, pc, off, [0.6] * B, N, N, 64 * N, with_mask=False, thr2=thr)
     ms = timeit(f3)
     print(f"ball_query fused (count+scan+pairs, no mask) B={B} N={N}: {ms:.3f} ms")
+
+# per-point layer weight gradients: direct-load MFMA kernel vs the LDS-staged v1
+L.pkdev_linear_wgrad_v1.argtypes = _lib.SIGNATURES["pk_linear_wgrad"]
+for (R_or_B, I, O, N, cf) in [(65536, 128, 64, 0, False), (65536, 64, 64, 0, False), (65536, 64, 32, 0, False),
+                              (32, 64, 64, 1024, True), (32, 32, 32, 1024, True)]:
+    if cf:
+        x = torch.randn(R_or_B, I, N, device=dev)
+        dy = torch.randn(R_or_B, O, N, device=dev)
+        R = R_or_B * N
+    else:
+        x = torch.randn(R_or_B, I, device=dev)
+        dy = torch.randn(R_or_B, O, device=dev)
+        R = R_or_B
+    dw, db = ops.linear_wgrad(x, dy, channels_first=cf)
+    ms2 = timeit(lambda: ops.linear_wgrad(x, dy, channels_first=cf))
+    S = (R + 127) // 128
+    work = torch.empty((S * (O * I + O),), device=dev)
+    dw1 = torch.empty((O, I), device=dev)
+    db1 = torch.empty((O,), device=dev)
+    f1 = lambda: L.pkdev_linear_wgrad_v1(_lib.ptr(x), _lib.ptr(dy), int(cf), R, I, O, N, _lib.ptr(work), _lib.ptr(dw1),
+                                         _lib.ptr(db1), _lib.stream(dev))
+    ms1 = timeit(f1)
+    rel = float((dw - dw1).abs().max() / dw1.abs().max())
+    fl = 2.0 * R * I * O
+    print(f"linear_wgrad R={R} I={I} O={O} {'cf' if cf else 'cl'}: v2 {ms2*1e3:.1f} us ({fl/ms2/1e9:.1f} TF/s) "
+          f"v1 {ms1*1e3:.1f} us; max rel diff {rel:.2e}")
