@@ -239,8 +239,15 @@ def main():
 
     if rank == 0:
         total_ms = elapsed * 1e3 / args.steps
-        # dominant kernel family by total device time in the probed steps
-        dom = max(kern.items(), key=lambda kv: kv[1]["total_ms"])
+        # dominant kernel family on the critical path: in the pipelined execution crop
+        # formation runs on a second stream under the training step, so the training
+        # kernels bound the step; the crop-formation families are reported beside it
+        crop_fams = {"pk_backproject", "pk_sor", "pk_fps_npoint", "pk_fps", "pk_gather_transform",
+                     "pk_ball_query_mask", "pk_ball_query_pairs", "pk_sample_rgb", "pk_erode_mask"}
+        train_k = {k: v for k, v in kern.items() if k not in crop_fams} or kern
+        dom = max(train_k.items(), key=lambda kv: kv[1]["total_ms"])
+        crop_k = {k: v for k, v in kern.items() if k in crop_fams}
+        dom_crop = max(crop_k.items(), key=lambda kv: kv[1]["total_ms"]) if crop_k else None
         kernels = {k: {"avg_ms": round(v["avg_ms"], 4), "launches": v["launches"],
                        "ms_per_step": round(v["total_ms"] / max(probe_steps, 1), 4)}
                    for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"])}
@@ -262,6 +269,10 @@ def main():
                        "precision": "model fp32 (f32 MFMA); crop geometry / C_gt normal equations fp64",
                        "parallelism": f"dp{world}"},
             "roofline": roof,
+            "roofline_crop_formation": (dict(roofline_for(dom_crop[0], dom_crop[1]),
+                                             stream="side (overlapped with the training step)")
+                                        if dom_crop is not None and not args.no_overlap and not args.eager else
+                                        (roofline_for(dom_crop[0], dom_crop[1]) if dom_crop else None)),
             "roofline_mfma_kernels": {k: {"achieved": v["achieved"], "frac": v["frac"], "unit": v["unit"]}
                                       for k, v in mfma_fams.items()},
             "kernels": kernels,

@@ -20,12 +20,12 @@ from collections import defaultdict
 FAMILIES = {
     "pk_fps": ["fps_pruned_kernel", "fps_kernel"],
     "pk_sor": ["sor_knn_kernel", "sor_stats_kernel", "sor_count_kernel", "sor_write_kernel"],
-    "pk_ball_query_mask": ["bq_mask_f32_kernel"],
+    "pk_ball_query_mask": ["bq_mask_stream_kernel", "bq_mask_f32_kernel"],
     "pk_backproject": ["bp_count_kernel", "bp_write_kernel"],
     "pk_spectral_diffusion": ["spec_reduce_kernel", "spec_combine_kernel", "spec_expand_kernel"],
     "pk_attention_fwd": ["attn_fwd_kernel"],
     "pk_attention_bwd": ["attn_bwd_dq_kernel", "attn_bwd_dkv_kernel"],
-    "pk_linear_wgrad": ["wgrad_partial_kernel", "wgrad_reduce_kernel"],
+    "pk_linear_wgrad": ["wgrad_v2_kernel", "wgrad_partial_kernel", "wgrad_reduce_kernel"],
     "pk_feat_dist_topk": ["fd_prep_kernel", "fd_main_kernel"],
     "pk_cgt_lstsq": ["cgt_count_kernel", "cgt_partial_kernel", "cgt_reduce_kernel", "cgt_solve_kernel"],
 }
@@ -50,8 +50,8 @@ def read(dirpath, counter, min_grid=0, max_grid=None):
 
 
 # bench.py's configs[3]-size ball-query probe (256 x 2048 x 2048) runs the mask kernel on a
-# grid of 2 x 32 x 256 workgroups of 256 threads; the in-step launches are far smaller
-PROBE_GRID = 2 * 32 * 256 * 256
+# grid of 32 x 256 workgroups of 256 threads; the in-step launches are far smaller
+PROBE_GRID = 32 * 256 * 256
 
 
 def main():
