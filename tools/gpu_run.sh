@@ -29,12 +29,16 @@ for step in "$@"; do
     kbench) run kbench 300 python tools/kbench.py ;;
     kprof) run kprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kprof" -o run -- python tools/kbench.py
           find "$out/kprof" -type f ! -name "*stats.csv" -delete ;;
+    pmcm) run pmcm 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$out/pmcm" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager --probe-steps 1
+          python tools/mfma_util.py "$out/pmcm" fd_main_kernel attn_fwd attn_bwd wgrad_v2 > "$out/mfma_util_step.json" 2>&1
+          find "$out/pmcm" -type f -name "*.csv" -size +2M -delete ;;
     pmc) run pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$out/pmcf" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager --probe-steps 1
          run pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$out/pmcw" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager --probe-steps 1
          python tools/pmc_summary.py "$out/pmcf" "$out/pmcw" "$out/pmc_traffic.json" > "$out/pmc_summary.log" 2>&1
          find "$out/pmcf" "$out/pmcw" -type f -name "*.csv" -size +2M -delete ;;
     fdb) run fdb 300 python tools/fd_bench.py ;;
     fdpmc) run fdpmc1 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$out/fdpmc1" -o run -- python tools/fd_bench.py 2
+           python tools/mfma_util.py "$out/fdpmc1" fd_main_kernel fd_prep_kernel > "$out/mfma_util.json" 2>&1
            run fdpmc2 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$out/fdpmc2" -o run -- python tools/fd_bench.py 2 ;;
     diag) run diag 300 python tools/diag_model.py ;;
     tprof) run tprof 300 python tools/torch_prof.py "$tag" ;;

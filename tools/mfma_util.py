@@ -1,0 +1,40 @@
+"""MFMA utilisation per kernel from a rocprofv3 --pmc pass holding SQ_VALU_MFMA_BUSY_CYCLES
+and GRBM_GUI_ACTIVE (rocprofv3's own MfmaUtil expression: sum over SIMDs of the MFMA-busy
+cycles / (max over instances of GRBM_GUI_ACTIVE x 1024 SIMDs)).
+
+  python tools/mfma_util.py <pmc dir> [kernel-name substring ...]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+SIMDS = 1024  # 256 CUs x 4 SIMDs (MI355X)
+
+
+def main():
+    d = sys.argv[1]
+    keys = sys.argv[2:] or ["fd_main_kernel", "attn_", "wgrad_v2"]
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    names, grids = {}, {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            did = r["Dispatch_Id"]
+            names[did], grids[did] = r["Kernel_Name"], r.get("Grid_Size", "")
+            per[did][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = collections.defaultdict(list)
+    for did, c in per.items():
+        n = names[did]
+        k = next((k for k in keys if k in n), None)
+        if k is None or "SQ_VALU_MFMA_BUSY_CYCLES" not in c or "GRBM_GUI_ACTIVE" not in c:
+            continue
+        busy, gui = sum(c["SQ_VALU_MFMA_BUSY_CYCLES"]), max(c["GRBM_GUI_ACTIVE"])
+        out[(n.split("(")[0][-60:], grids[did])].append(busy / (gui * SIMDS))
+    res = {f"{n} grid={g}": {"mfma_util": round(sum(v) / len(v), 4), "dispatches": len(v)} for (n, g), v in out.items()}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
