@@ -219,7 +219,7 @@ __device__ __forceinline__ void lanegroup_merge(TopK<TOPK>& best) {
   }
 }
 
-// grid (ceil(T2 / CW), B), block 64 RP: the block owns CW column tiles (their B operands
+// grid (B * ceil(T2 / CW)), block 64 RP: the block owns CW column tiles (their B operands
 // stay in registers, so every A tile load feeds 8 CW MFMAs) and wave q takes the q-th of
 // RP parts of the row tiles; the parts merge through LDS (ties: lower row first). One
 // step = two row tiles x CW column tiles on 2 CW independent accumulators, the next
@@ -232,10 +232,25 @@ __global__ __launch_bounds__(64 * RP) void fd_main_kernel(const float* __restric
                                                           float* __restrict__ out_dist) {
   __shared__ float xv[RP][CW][16][TOPK];
   __shared__ int xi[RP][CW][16][TOPK];
-  const int b = blockIdx.y;
+  // 1-D grid of B x NC blocks (NC = column groups per crop), renumbered so that all blocks
+  // of crop b run on XCD b % 8 (hardware block L lands on XCD L % 8): a crop's A operand
+  // (128 KiB at V1 = 1024) is then read from one XCD's L2 instead of all eight.
+  const int NC = (T2 + CW - 1) / CW;
+  const int B = (int)(gridDim.x / NC);
+  int b, cg;
+  {
+    const int L = blockIdx.x, x8 = L & 7, k = L >> 3;
+    if ((B & 7) == 0) {
+      b = x8 + 8 * (k / NC);
+      cg = k - (k / NC) * NC;
+    } else {
+      b = L / NC;
+      cg = L - b * NC;
+    }
+  }
   const int lane = pk::lane_id(), q = pk::wave_id();
   const int g = lane >> 4, c16 = lane & 15;
-  const int ct0 = blockIdx.x * CW;
+  const int ct0 = cg * CW;
   const int N1 = n1[b], N2 = n2[b];
   const int nt = (N1 + 15) >> 4;  // row tiles holding valid rows
   const int t_begin = (nt * q) / RP, t_end = (nt * (q + 1)) / RP;
@@ -364,7 +379,7 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
   hipLaunchKernelGGL(fd_prep_kernel, dim3((rows + 63) / 64, B, 2), dim3(256), 0, s, evecs_x, ldx, C, evecs_y, ldy,
                      n1, n2, V1max, V2max, T1, T2, A, Bq);
   PK_CHECK_LAUNCH();
-  const dim3 grid((T2 + kFdCW - 1) / kFdCW, B), block(64 * kFdRP);
+  const dim3 grid(((T2 + kFdCW - 1) / kFdCW) * B), block(64 * kFdRP);
   if (topk == 1)
     hipLaunchKernelGGL((fd_main_kernel<1, kFdCW, kFdRP>), grid, block, 0, s, A, Bq, n1, n2, T1, T2, V2max, out_idx,
                        out_dist);
@@ -380,7 +395,7 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
 extern "C" int pkdev_fd_main_noepi(const float* A, const float* Bq, const int32_t* n1, const int32_t* n2, int B,
                                    int V1max, int V2max, int64_t* out_idx, int noload, void* stream) {
   const int T1 = (V1max + 15) / 16, T2 = (V2max + 15) / 16;
-  const dim3 grid((T2 + kFdCW - 1) / kFdCW, B), block(64 * kFdRP);
+  const dim3 grid(((T2 + kFdCW - 1) / kFdCW) * B), block(64 * kFdRP);
   if (noload)
     hipLaunchKernelGGL((fd_main_kernel<1, kFdCW, kFdRP, true, true>), grid, block, 0, pk::as_stream(stream), A, Bq, n1,
                        n2, T1, T2, V2max, out_idx, nullptr);
