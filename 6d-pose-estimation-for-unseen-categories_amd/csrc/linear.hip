@@ -379,3 +379,366 @@ extern "C" int pk_linear_wgrad(const float* x, const float* dy, int layout, int6
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
+
+namespace {
+
+// ---------------------------------------------------------------------------------
+// Per-point layer products (forward and input gradient) of the same layers:
+//   forward   y = x W^T (+ b) (then ReLU if asked)       W [O, I]
+//   dgrad     dx = dy W            (= the forward with the weight transposed, no bias)
+// in both layouts (0: [R, C] rows, nn.Linear; 1: [Bn, C, N], Conv1d(k=1)). I, O <= 128.
+// One wave computes 32 points x all outputs on v_mfma_f32_32x32x2_f32 (up to four 32x32
+// accumulators); the weight sits in LDS, the points' operands are loaded straight from
+// global memory once. Contraction index k is split in halves across the lane halves
+// (k = h * KH + s at step s), so a lane reads one contiguous half-row (layout 0) or the
+// same column of KH consecutive channel rows (layout 1, 128-B coalesced across lanes).
+// Replaces the library GEMM + separate bias / transpose kernels of these tall-skinny
+// shapes (32k-65k points x <= 128 channels).
+constexpr int kLfMaxC = 128;
+
+template <int LAYOUT>
+__global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ bias, int64_t R, int N, int Cin,
+                                                         int Cout, int transw, int relu, float* __restrict__ y) {
+  // weight as Ws[out][k], out < Cout, k < KP (zero padded); row stride KP + 1 (odd);
+  // dynamic LDS of Cout * (KP + 1) floats (<= 64.5 KiB)
+  extern __shared__ float Ws[];
+  const int KP = (Cin + 3) & ~3, KH = KP >> 1, ST = KP + 1;
+  for (int e = threadIdx.x; e < Cout * KP; e += 256) {
+    const int o = e / KP, k = e - o * KP;
+    float v = 0.f;
+    if (k < Cin) v = transw ? w[(int64_t)k * Cout + o] : w[(int64_t)o * Cin + k];
+    Ws[o * ST + k] = v;
+  }
+  __syncthreads();
+  const int lane = pk::lane_id(), wave = pk::wave_id();
+  const int m = lane & 31, h = lane >> 5;
+  const int TO = (Cout + 31) >> 5;
+  // 32 points per wave: rows r0 .. r0 + 31 of the flattened point index
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * 32;
+  if (r0 >= R) return;
+  const int64_t r = r0 + m;  // this lane's point (its A / B operand column)
+  const bool ok = r < R;
+  int64_t bb = 0, nn = 0;
+  if (LAYOUT == 1) {
+    bb = r / N;
+    nn = r - bb * N;
+  }
+  float xa[kLfMaxC / 2];
+#pragma unroll
+  for (int s = 0; s < kLfMaxC / 2; ++s) {
+    if (s < KH) {
+      const int k = h * KH + s;
+      float v = 0.f;
+      if (ok && k < Cin) v = LAYOUT == 0 ? x[r * Cin + k] : x[(bb * Cin + k) * N + nn];
+      xa[s] = v;
+    }
+  }
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+  // layout 0: D[point m][out n] = sum_k x[m][k] W[n][k]  (A = points, B = weight)
+  // layout 1: D[out m][point n] = sum_k W[m][k] x[k][n]  (A = weight, B = points)
+#pragma unroll
+  for (int s = 0; s < kLfMaxC / 2; ++s) {
+    if (s < KH) {
+      const int k = h * KH + s;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t < TO) {
+          const int o = t * 32 + m;
+          const float wv = o < Cout ? Ws[o * ST + k] : 0.f;
+          acc[t] = LAYOUT == 0 ? __builtin_amdgcn_mfma_f32_32x32x2f32(xa[s], wv, acc[t], 0, 0, 0)
+                               : __builtin_amdgcn_mfma_f32_32x32x2f32(wv, xa[s], acc[t], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // D element (row 8 (e / 4) + 4 h + e % 4, column m)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t < TO) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int rr = 8 * (e >> 2) + 4 * h + (e & 3);
+        if (LAYOUT == 0) {
+          const int64_t pr = r0 + rr;
+          const int o = t * 32 + m;
+          if (pr < R && o < Cout) {
+            float v = acc[t][e] + (bias != nullptr ? bias[o] : 0.f);
+            if (relu) v = fmaxf(v, 0.f);
+            y[pr * Cout + o] = v;
+          }
+        } else {
+          const int o = t * 32 + rr;
+          if (ok && o < Cout) {
+            float v = acc[t][e] + (bias != nullptr ? bias[o] : 0.f);
+            if (relu) v = fmaxf(v, 0.f);
+            y[(bb * Cout + o) * N + nn] = v;
+          }
+        }
+      }
+    }
+  }
+}
+
+// Row layout (0) with Cin % 16 == 0: one wave computes 16 points x all outputs per tile on
+// v_mfma_f32_16x16x4_f32 and walks tiles grid-stride, loading the next tile's operands
+// while the current tile's MFMAs run. Contraction index at step (q, i) for lane group g:
+// k = 16 q + 4 g + i, so each lane's operands are float4s of its own point row (one load
+// instruction covers 16 rows x 64 contiguous bytes) and the weight row chunk is one
+// ds_read_b128 from Ws[o][k] (row stride KP + 4: conflict-free over 8-lane phases).
+
+template <int Q>
+__device__ __forceinline__ void lr_load(const float* __restrict__ x, int64_t row, int64_t R, int g, f32x4 (&xa)[Q]) {
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    xa[q] = row < R ? *reinterpret_cast<const f32x4*>(x + row * (16 * Q) + 16 * q + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// Weight staging shared by the MFMA per-point kernels: Ws[o][k] (o < 16 TO, zero rows past
+// Cout; row stride 16 Q + 4), from W [Cout, 16 Q] or, with transw, from W^T's [16 Q, Cout].
+template <int Q, int TO>
+__device__ __forceinline__ void lr_stage(const float* __restrict__ w, int Cout, int transw, float* Ws) {
+  constexpr int CI = 16 * Q, ST = CI + 4;
+  if (!transw) {  // W [Cout, CI] rows: float4 reads, all issued before the LDS writes
+    constexpr int NV = TO * 16 * CI / 4, PER = (NV + 255) / 256;
+    f32x4 v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = threadIdx.x + 256 * i, o = e / (CI / 4);
+      v[i] = (e < NV && o < Cout) ? *reinterpret_cast<const f32x4*>(w + 4 * (int64_t)e) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = threadIdx.x + 256 * i, o = e / (CI / 4), k4 = e - o * (CI / 4);
+      if (e < NV) *reinterpret_cast<f32x4*>(&Ws[o * ST + 4 * k4]) = v[i];
+    }
+  } else {  // W^T from a [CI, Cout] tensor: read along Cout
+    constexpr int NE = TO * 16 * CI, PER = (NE + 255) / 256;
+    float v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = threadIdx.x + 256 * i, k = e / (TO * 16), o = e - k * (TO * 16);
+      v[i] = (e < NE && o < Cout) ? w[(int64_t)k * Cout + o] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = threadIdx.x + 256 * i, k = e / (TO * 16), o = e - k * (TO * 16);
+      if (e < NE) Ws[o * ST + k] = v[i];
+    }
+  }
+}
+
+template <int Q, int TO>  // Cin = 16 Q, Cout <= 16 TO
+__global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                              const float* __restrict__ bias, int64_t R, int Cin,
+                                                              int Cout, int transw, int relu, float* __restrict__ y) {
+  extern __shared__ float Ws[];  // [16 TO][Cin + 4]
+  constexpr int CI = 16 * Q, ST = CI + 4;
+  const int lane = pk::lane_id(), m = lane & 15, g = lane >> 4;
+  const int64_t T = (R + 15) >> 4, stride = (int64_t)gridDim.x * 4;
+  int64_t tile = (int64_t)blockIdx.x * 4 + pk::wave_id();
+  // the first tile's operands are in flight while the weight is staged
+  f32x4 cur[Q], nxt[Q];
+  lr_load<Q>(x, tile < T ? tile * 16 + m : R, R, g, cur);
+  lr_stage<Q, TO>(w, Cout, transw, Ws);
+  __syncthreads();
+  if (tile >= T) return;
+  float bv[TO];
+#pragma unroll
+  for (int t = 0; t < TO; ++t) {
+    const int o = t * 16 + m;
+    bv[t] = (bias != nullptr && o < Cout) ? bias[o] : 0.f;
+  }
+  for (;;) {
+    const int64_t tn = tile + stride;
+    if (tn < T) lr_load<Q>(x, tn * 16 + m, R, g, nxt);
+    f32x4 acc[TO];
+#pragma unroll
+    for (int t = 0; t < TO; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      {
+        f32x4 wv[TO];
+#pragma unroll
+        for (int t = 0; t < TO; ++t)
+          wv[t] = *reinterpret_cast<const f32x4*>(&Ws[(t * 16 + m) * ST + 16 * q + 4 * g]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int t = 0; t < TO; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[q][i], wv[t][i], acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);  // keep the weight reads per chunk (no hoisting of all Q x TO)
+      }
+    }
+    // D[point 4 g + r][out t * 16 + m]
+#pragma unroll
+    for (int t = 0; t < TO; ++t) {
+      {
+        const int o = t * 16 + m;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t pr = tile * 16 + 4 * g + r;
+          if (pr < R && o < Cout) {
+            float v = acc[t][r] + bv[t];
+            if (relu) v = fmaxf(v, 0.f);
+            y[pr * Cout + o] = v;
+          }
+        }
+      }
+    }
+    if (tn >= T) break;
+    tile = tn;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) cur[q] = nxt[q];
+  }
+}
+
+// Channels-first layout (1) [Bn, C, N] with Cin in {16, 32, 64, 128} and N % (16 SUB) == 0:
+// one wave computes 16 SUB consecutive points of one item x all outputs. A = weight
+// (Ws[o][k] chunks, ds_read_b128), B = points: lane (j, g) loads its SUB consecutive points
+// as one vector per channel row k = 16 q + 4 g + i, and element u of that
+// vector is column j of point sub-tile u (sub-tile u holds points SUB j + u), so loads and
+// the D stores (float SUB vectors of consecutive points) are both contiguous per lane.
+template <int SUB> struct LcVec;
+template <> struct LcVec<1> { using T = float; };
+template <> struct LcVec<2> { using T = __attribute__((ext_vector_type(2))) float; };
+template <> struct LcVec<4> { using T = f32x4; };
+
+template <int Q, int TO, int SUB>
+__global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                            const float* __restrict__ bias, int64_t R, int N, int Cout,
+                                                            int transw, int relu, float* __restrict__ y) {
+  using V = typename LcVec<SUB>::T;
+  extern __shared__ float Ws[];
+  constexpr int CI = 16 * Q, ST = CI + 4, P = 16 * SUB;
+  const int lane = pk::lane_id(), m = lane & 15, g = lane >> 4;
+  const int64_t T = R / P;
+  const int64_t tile = (int64_t)blockIdx.x * 4 + pk::wave_id();
+  // the tile's operands are in flight while the weight is staged
+  V xv[Q][4];
+  int64_t bb = 0, n0 = 0;
+  if (tile < T) {
+    const int64_t p0 = tile * P;
+    bb = p0 / N;
+    n0 = p0 - bb * N;
+    const float* xb = x + bb * CI * (int64_t)N + n0 + SUB * m;
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xv[q][i] = *reinterpret_cast<const V*>(xb + (int64_t)(16 * q + 4 * g + i) * N);
+  }
+  lr_stage<Q, TO>(w, Cout, transw, Ws);
+  __syncthreads();
+  if (tile >= T) return;
+  f32x4 acc[TO][SUB];
+#pragma unroll
+  for (int t = 0; t < TO; ++t)
+#pragma unroll
+    for (int u = 0; u < SUB; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    f32x4 wv[TO];
+#pragma unroll
+    for (int t = 0; t < TO; ++t) wv[t] = *reinterpret_cast<const f32x4*>(&Ws[(t * 16 + m) * ST + 16 * q + 4 * g]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int u = 0; u < SUB; ++u)
+#pragma unroll
+        for (int t = 0; t < TO; ++t) {
+          float b;
+          if constexpr (SUB == 1) b = xv[q][i]; else b = xv[q][i][u];
+          acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[t][i], b, acc[t][u], 0, 0, 0);
+        }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // D[out t * 16 + 4 g + r][column m of sub-tile u] = point n0 + SUB m + u
+  float* yb = y + bb * Cout * (int64_t)N + n0 + SUB * m;
+#pragma unroll
+  for (int t = 0; t < TO; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = t * 16 + 4 * g + r;
+      if (o < Cout) {
+        const float bo = bias != nullptr ? bias[o] : 0.f;
+        V v;
+#pragma unroll
+        for (int u = 0; u < SUB; ++u) {
+          float e = acc[t][u][r] + bo;
+          if (relu) e = fmaxf(e, 0.f);
+          if constexpr (SUB == 1) v = e; else v[u] = e;
+        }
+        *reinterpret_cast<V*>(yb + (int64_t)o * N) = v;
+      }
+    }
+}
+
+}  // namespace
+
+extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, int layout, int64_t R, int N,
+                             int Cin, int Cout, int transw, int relu, float* y, void* stream) {
+  PK_REQUIRE((layout == 0 || layout == 1) && R >= 0 && Cin > 0 && Cout > 0 && Cin <= kLfMaxC && Cout <= kLfMaxC);
+  PK_REQUIRE(layout == 0 || (N > 0 && R % N == 0));
+  if (R == 0) return PK_OK;
+  PK_REQUIRE(x && w && y);
+  if (layout == 0 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128)) {
+    // 16-point tiles, 4 per block, at most two blocks per CU's worth of waves in flight
+    const int64_t tiles = (R + 15) / 16;
+    const unsigned blocks = (unsigned)std::min<int64_t>((tiles + 3) / 4, 512);
+    const int TO = Cout <= 16 ? 1 : Cout <= 32 ? 2 : Cout <= 64 ? 4 : 8;
+    auto pick = [&](auto q) {
+      constexpr int Q = decltype(q)::value;
+      return TO == 1 ? linear_fwd_rows_kernel<Q, 1>
+             : TO == 2 ? linear_fwd_rows_kernel<Q, 2>
+             : TO == 4 ? linear_fwd_rows_kernel<Q, 4> : linear_fwd_rows_kernel<Q, 8>;
+    };
+    auto kern = Cin == 16 ? pick(std::integral_constant<int, 1>{})
+                : Cin == 32 ? pick(std::integral_constant<int, 2>{})
+                : Cin == 64 ? pick(std::integral_constant<int, 4>{}) : pick(std::integral_constant<int, 8>{});
+    const size_t lds = sizeof(float) * (size_t)(16 * TO) * (Cin + 4);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, pk::as_stream(stream), x, w, bias, R, Cin, Cout, transw,
+                       relu, y);
+    PK_CHECK_LAUNCH();
+    return PK_OK;
+  }
+  if (layout == 1 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128) && N % 16 == 0) {
+    // points per wave: 16 SUB, as many as keep >= 1024 waves and <= 64 operand VGPRs
+    int sub = R >= 131072 ? 4 : R >= 32768 ? 2 : 1;
+    sub = std::min(sub, 256 / Cin);
+    while (N % (16 * sub)) sub >>= 1;
+    const int TO = Cout <= 16 ? 1 : Cout <= 32 ? 2 : Cout <= 64 ? 4 : 8;
+    auto pick = [&](auto q, auto u) {
+      constexpr int Q = decltype(q)::value, U = decltype(u)::value;
+      return TO == 1 ? linear_fwd_cf_kernel<Q, 1, U>
+             : TO == 2 ? linear_fwd_cf_kernel<Q, 2, U>
+             : TO == 4 ? linear_fwd_cf_kernel<Q, 4, U> : linear_fwd_cf_kernel<Q, 8, U>;
+    };
+    auto pickq = [&](auto u) {
+      return Cin == 16 ? pick(std::integral_constant<int, 1>{}, u)
+             : Cin == 32 ? pick(std::integral_constant<int, 2>{}, u)
+             : Cin == 64 ? pick(std::integral_constant<int, 4>{}, u) : pick(std::integral_constant<int, 8>{}, u);
+    };
+    auto kern = sub == 4 ? pickq(std::integral_constant<int, 4>{})
+                : sub == 2 ? pickq(std::integral_constant<int, 2>{}) : pickq(std::integral_constant<int, 1>{});
+    const int64_t tiles = R / (16 * sub);
+    const size_t lds = sizeof(float) * (size_t)(16 * TO) * (Cin + 4);
+    hipLaunchKernelGGL(kern, dim3((unsigned)((tiles + 3) / 4)), dim3(256), lds, pk::as_stream(stream), x, w, bias, R,
+                       N, Cout, transw, relu, y);
+    PK_CHECK_LAUNCH();
+    return PK_OK;
+  }
+  const unsigned blocks = (unsigned)((R + 127) / 128);
+  const size_t lds = sizeof(float) * (size_t)Cout * (((Cin + 3) & ~3) + 1);
+  if (layout == 0)
+    hipLaunchKernelGGL(linear_fwd_kernel<0>, dim3(blocks), dim3(256), lds, pk::as_stream(stream), x, w, bias, R, N,
+                       Cin, Cout, transw, relu, y);
+  else
+    hipLaunchKernelGGL(linear_fwd_kernel<1>, dim3(blocks), dim3(256), lds, pk::as_stream(stream), x, w, bias, R, N,
+                       Cin, Cout, transw, relu, y);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}

@@ -39,6 +39,7 @@ SIGNATURES = {
     "pk_attention_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P],
     "pk_attention_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "pk_linear_wgrad": [_P, _P, _I, _I64, _I, _I, _I, _P, _P, _P, _P],
+    "pk_linear_fwd": [_P, _P, _P, _I, _I64, _I, _I, _I, _I, _I, _P, _P],
     "pk_feat_dist_topk": [_P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "pk_rigidity_filter": [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P],
     "pk_inlier_ratio": [_P, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P],

@@ -2,10 +2,11 @@
 
 `Linear` and `Conv1d` are drop-in subclasses of torch.nn.Linear / Conv1d(kernel_size=1):
 same constructor, parameter names and state_dict keys (weights/weights.pt loads
-unchanged). Forward and input-gradient products are large-M GEMMs (hipBLASLt); the
-weight / bias gradients — a reduction over all B*N points into a <= 128 x 128 matrix,
-which a library GEMM runs on a handful of output tiles — go to pk_linear_wgrad, which
-splits the points across the whole chip (ops.linear_wgrad).
+unchanged). All three products run in HIP on the f32 MFMA: the forward (bias fused) and
+the input gradient in pk_linear_fwd (32 points x all outputs per wave, weight in LDS,
+either layout, so no transposes or bias kernels), the weight / bias gradients — a
+reduction over all B*N points into a <= 128 x 128 matrix — in pk_linear_wgrad, which
+splits the points across the whole chip.
 """
 from __future__ import annotations
 
@@ -21,22 +22,15 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
-        O, I = weight.shape
         # a fresh (non-view) output: the reference applies in-place ReLUs to it (:112-116)
-        y = torch.empty(x.shape[:-1] + (O,), dtype=x.dtype, device=x.device)
-        x2, y2 = x.reshape(-1, I), y.view(-1, O)
-        if bias is not None:
-            torch.addmm(bias, x2, weight.t(), out=y2)
-        else:
-            torch.mm(x2, weight.t(), out=y2)
-        return y
+        return ops.linear_fwd(x, weight, bias, channels_first=False)
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.matmul(dy, weight)
+            dx = ops.linear_fwd(dy, weight, None, channels_first=False, transw=True)  # dy W
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             dw, db = ops.linear_wgrad(x, dy, channels_first=False, want_bias=ctx.has_bias)
         return dx, dw, db
@@ -47,18 +41,15 @@ class _Conv1x1Fn(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
-        # y[b] = W x[b] (+ b): a batched GEMM (no MIOpen convolution on the path)
-        y = torch.bmm(weight[:, :, 0].expand(x.shape[0], -1, -1), x)
-        if bias is not None:
-            y.add_(bias[:, None])
-        return y
+        # y[b] = W x[b] (+ b) over every point, bias fused (no MIOpen convolution)
+        return ops.linear_fwd(x, weight[:, :, 0], bias, channels_first=True)
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.matmul(weight[:, :, 0].t(), dy)
+            dx = ops.linear_fwd(dy, weight[:, :, 0], None, channels_first=True, transw=True)  # W^T dy
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             dw, db = ops.linear_wgrad(x, dy, channels_first=True, want_bias=ctx.has_bias)
             dw = dw[:, :, None]

@@ -338,6 +338,28 @@ def linear_wgrad(x: torch.Tensor, dy: torch.Tensor, channels_first: bool, want_b
     return dw, db
 
 
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], channels_first: bool,
+               transw: bool = False, relu: bool = False) -> torch.Tensor:
+    """pk_linear_fwd: y = x W^T (+ b) over every point (W [Cout, Cin], or W^T read from a
+    [Cin, Cout] tensor when transw). channels_first=False: x [..., Cin] -> [..., Cout];
+    True: x [B, Cin, N] -> [B, Cout, N]."""
+    x = x.contiguous()
+    w = w.contiguous()
+    Cout, Cin = (w.shape[1], w.shape[0]) if transw else (w.shape[0], w.shape[1])
+    if channels_first:
+        Bn, C, N = x.shape
+        R, layout = Bn * N, 1
+        y = torch.empty((Bn, Cout, N), dtype=x.dtype, device=x.device)
+    else:
+        C, N, layout = x.shape[-1], 0, 0
+        R = x.numel() // max(C, 1)
+        y = torch.empty(x.shape[:-1] + (Cout,), dtype=x.dtype, device=x.device)
+    assert C == Cin, (C, Cin)
+    call("pk_linear_fwd", ptr(x), ptr(w), ptr(bias), layout, int(R), int(N), int(Cin), int(Cout), int(transw),
+         int(relu), ptr(y), _lib.stream(x.device), work=("mfma", 2 * int(R) * Cin * Cout))
+    return y
+
+
 # ------------------------------------------------------------------------------ H10-H13, H15
 
 

@@ -234,8 +234,13 @@ def main():
     if not args.eager:
         # per-kernel HIP events cannot sit inside a graph: time the same step eagerly, on
         # the same resident inputs, right after the timed region (not part of `value`)
+        # A device-side sleep heads each probe step so the host enqueues the whole step
+        # before the GPU starts it: the events then bracket device time only, not host
+        # launch gaps (an eager step is host-bound).
         _lib.set_probe(probe.hook)
         for _ in range(args.probe_steps):
+            torch.cuda.synchronize()
+            torch.cuda._sleep(int(2.5e8))  # ~0.1 s of GPU clock cycles
             step(op, crops_of(fb))
         torch.cuda.synchronize()
         _lib.set_probe(None)

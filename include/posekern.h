@@ -155,6 +155,16 @@ int pk_attention_bwd(const float* q, const float* k, const float* v, const float
 int pk_linear_wgrad(const float* x, const float* dy, int layout, int64_t R, int I, int O, int N,
                     float* work, float* dw, float* db, void* stream);
 
+/* Forward / input gradient of the same per-point layers (nn.Linear at models/dpfm.py:22-30
+ * and modeling/dpfm.py:16-26,90-91,113-116; Conv1d(k=1) at modeling/dpfm.py:16-26,49-50):
+ *   y = x W^T (+ bias) (ReLU if relu), W f32 [Cout, Cin]; with transw = 1 the weight is
+ *   read as W^T (W stored [Cin, Cout]): the input gradient dx = dy W of a layer is
+ *   pk_linear_fwd(dy, W, NULL, ..., Cin = O, Cout = I, transw = 1).
+ *   layout 0: x [R, Cin] -> y [R, Cout]; layout 1: x [R/N, Cin, N] -> y [R/N, Cout, N].
+ *   Cin, Cout <= 128; bias may be NULL. */
+int pk_linear_fwd(const float* x, const float* w, const float* bias, int layout, int64_t R, int N, int Cin,
+                  int Cout, int transw, int relu, float* y, void* stream);
+
 /* H10 / H11 correspondence head. Replaces fmap2pointmap_solvers/naive.py:20-34
  * (topk = 1: dist.argmin(dim=-2)) and spacial_filtering.py:19-38 (topk = 5: the first 5
  * rows of dist.sort(dim=-2)) with dist = cdist(evecs_x[:, :30] @ C^T, evecs_y[:, :30]).

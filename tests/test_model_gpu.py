@@ -177,3 +177,40 @@ def test_dpfmnet_matches_oracle(device, N1, N2):
 
     check(lambda o: o[1].sum() + o[2].sum() + o[3].square().sum() + o[4].square().sum())  # overlap + features
     check(lambda o: o[0].sum())                                                          # through the fmap solve
+
+
+@pytest.mark.parametrize("shape,channels_first,transw", [((65536, 128, 64), False, False), ((1000, 3, 64), False, False),
+                                                          ((4, 7, 32, 1), False, False), ((3, 32, 300, 64), True, False),
+                                                          ((2, 64, 1024, 32), True, False), ((4096, 64, 128), False, True),
+                                                          ((2, 64, 512, 32), True, True), ((0, 8, 8), False, False),
+                                                          ((32, 64, 1024, 64), True, False), ((64, 32, 2048, 128), True, False),
+                                                          ((32, 128, 1024, 64), True, True), ((3, 16, 48, 5), True, False),
+                                                          ((5000, 32, 1), False, False), ((777, 16, 100), False, True)])
+def test_linear_fwd(device, shape, channels_first, transw):
+    """pk_linear_fwd (per-point layer forward, bias fused; transw = the input gradient dy W)
+    vs fp64: |err| <= 1e-5 * sum_k |x||w| + 1e-6 |b|."""
+    from dpfm_amd import ops
+    g = torch.Generator().manual_seed(sum(shape) + 7 * transw)
+    if channels_first:
+        Bn, I, N, O = shape
+        x = torch.randn(Bn, I, N, generator=g)
+    else:
+        *lead, I, O = shape
+        x = torch.randn(*lead, I, generator=g)
+    w = torch.randn(O, I, generator=g) * 0.2
+    b = None if transw else torch.randn(O, generator=g)
+    w_arg = w.t().contiguous() if transw else w  # transw: the kernel reads W^T of a [Cin, Cout] tensor
+    y = ops.linear_fwd(x.to(device), w_arg.to(device), None if b is None else b.to(device),
+                       channels_first=channels_first, transw=transw).cpu().double()
+    xd, wd = x.double(), w.double()
+    if channels_first:
+        exp = torch.einsum("oi,bin->bon", wd, xd)
+        bound = torch.einsum("oi,bin->bon", wd.abs(), xd.abs())
+        if b is not None:
+            exp = exp + b.double()[None, :, None]
+    else:
+        exp, bound = xd @ wd.t(), xd.abs() @ wd.abs().t()
+        if b is not None:
+            exp = exp + b.double()
+    assert y.shape == exp.shape
+    assert (y - exp).abs().le(1e-5 * bound + 1e-6 * (0 if b is None else b.abs().max().item()) + 1e-30).all()

@@ -116,3 +116,22 @@ for (R_or_B, I, O, N, cf) in [(65536, 128, 64, 0, False), (65536, 64, 64, 0, Fal
     fl = 2.0 * R * I * O
     print(f"linear_wgrad R={R} I={I} O={O} {'cf' if cf else 'cl'}: v2 {ms2*1e3:.1f} us ({fl/ms2/1e9:.1f} TF/s) "
           f"v1 {ms1*1e3:.1f} us; max rel diff {rel:.2e}")
+
+# per-point layer forward / input gradient: pk_linear_fwd vs the library GEMM (+ bias)
+for (R_or_B, I, O, N, cf) in [(65536, 128, 64, 0, False), (65536, 64, 128, 0, False), (65536, 3, 64, 0, False),
+                              (32, 64, 64, 1024, True), (32, 32, 64, 1024, True), (32, 128, 32, 1024, True)]:
+    x = torch.randn(R_or_B, I, N, device=dev) if cf else torch.randn(R_or_B, I, device=dev)
+    w = torch.randn(O, I, device=dev)
+    b = torch.randn(O, device=dev)
+    R = R_or_B * (N if cf else 1)
+    y = ops.linear_fwd(x, w, b, channels_first=cf)
+    if cf:
+        ref = lambda: torch.bmm(w.expand(R_or_B, -1, -1), x).add_(b[:, None])
+    else:
+        ref = lambda: torch.addmm(b, x, w.t())
+    rel = float((y - ref()).abs().max() / ref().abs().max())
+    ms = timeit(lambda: ops.linear_fwd(x, w, b, channels_first=cf))
+    msr = timeit(ref)
+    bts = 4.0 * R * (I + O)
+    print(f"linear_fwd R={R} I={I} O={O} {'cf' if cf else 'cl'}: {ms*1e3:.1f} us ({bts/ms/1e6:.0f} GB/s) "
+          f"torch {msr*1e3:.1f} us; max rel diff {rel:.2e}", flush=True)
