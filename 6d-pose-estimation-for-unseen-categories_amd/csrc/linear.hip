@@ -12,6 +12,9 @@
 // Layouts: 0 = rows x channels ([R, C] row-major, nn.Linear), 1 = channels-first
 // ([Bn, C, N], Conv1d with kernel 1; row r = (r / N, r % N)).
 #include "common.hpp"
+#include "../../include/posekern.h"
+
+#include <vector>
 
 namespace {
 
@@ -117,7 +120,7 @@ constexpr int kRedGroups = 16;
 __global__ __launch_bounds__(64 * kRedGroups) void wgrad_reduce_kernel(const float* __restrict__ part,
                                                                        const float* __restrict__ partb, int S,
                                                                        int OI, int O, float* __restrict__ dw,
-                                                                       float* __restrict__ db) {
+                                                                       float* __restrict__ db, int accumulate) {
   __shared__ float red[kRedGroups][64];
   const int e = blockIdx.x * 64 + (threadIdx.x & 63);
   const int grp = threadIdx.x >> 6;
@@ -146,8 +149,8 @@ __global__ __launch_bounds__(64 * kRedGroups) void wgrad_reduce_kernel(const flo
   }
   if (grp == 0 && (is_w || is_b)) {
     const float r = red[0][threadIdx.x & 63];
-    if (is_w) dw[e] = r;
-    else db[e - OI] = r;
+    float* dst = is_w ? dw + e : db + (e - OI);
+    *dst = accumulate ? *dst + r : r;  // += : a weight used by several layers' calls
   }
 }
 
@@ -234,14 +237,13 @@ __device__ __forceinline__ void wgrad_mma(const WgradBatch<J>& B, f32x16 (&acc)[
 // batch's MFMAs (two register buffers, statically indexed).
 constexpr int kV2Waves = 8;
 
+// Slice s of one problem; comb / combb: the workgroup's [kV2Waves][16 * 64] / [kV2Waves][64]
+// LDS (declared by the calling kernel, so a kernel instantiating both layouts allocates it once).
 template <int LAYOUT, int J>
-__global__ __launch_bounds__(64 * kV2Waves) void wgrad_v2_kernel(const float* __restrict__ x,
-                                                                 const float* __restrict__ dy, int64_t R, int I,
-                                                                 int O, int N, int SL, float* __restrict__ part,
-                                                                 float* __restrict__ partb) {
-  __shared__ float comb[kV2Waves][16 * 64];
-  __shared__ float combb[kV2Waves][64];
-  const int s = blockIdx.x;
+__device__ __forceinline__ void wgrad_v2_body(const float* __restrict__ x, const float* __restrict__ dy, int64_t R,
+                                              int I, int O, int N, int SL, float* __restrict__ part,
+                                              float* __restrict__ partb, int s, float (*comb)[16 * 64],
+                                              float (*combb)[64]) {
   const int lane = pk::lane_id(), w = pk::wave_id();
   const int m = lane & 31, h = lane >> 5;
   const int To = (O + 31) >> 5, Ti = (I + 31) >> 5, T = To * Ti;
@@ -312,6 +314,118 @@ __global__ __launch_bounds__(64 * kV2Waves) void wgrad_v2_kernel(const float* __
   }
 }
 
+template <int LAYOUT, int J>
+__global__ __launch_bounds__(64 * kV2Waves) void wgrad_v2_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ dy, int64_t R, int I,
+                                                                 int O, int N, int SL, float* __restrict__ part,
+                                                                 float* __restrict__ partb) {
+  __shared__ float comb[kV2Waves][16 * 64];
+  __shared__ float combb[kV2Waves][64];
+  wgrad_v2_body<LAYOUT, J>(x, dy, R, I, O, N, SL, part, partb, blockIdx.x, comb, combb);
+}
+
+// ---------------------------------------------------------------------------------
+// Grouped weight gradients: every per-point layer of a backward pass in two launches
+// (partials, then reduction) instead of two launches per layer. The problem tables travel
+// as kernel arguments (captured into a HIP graph node by value). Block b belongs to the
+// problem whose [blk0, blk0 + S) holds b; each problem runs the same slice body as
+// pk_linear_wgrad. An output fed by two calls of one forward (a shared layer) reduces both
+// partial sets, first call first: r = reduce(seg 0) + reduce(seg 1), the same rounding as
+// autograd's grad = grad_0 + grad_1.
+constexpr int kGroupMax = 32;
+
+struct WgradProblem {
+  const float* x;
+  const float* dy;
+  float* part;   // S * O * I weight partials, then S * O bias partials
+  int64_t R;
+  int I, O, N, layout, SL, S, blk0, pad;
+};
+struct WgradProblems {
+  int G;
+  WgradProblem p[kGroupMax];
+};
+
+__global__ __launch_bounds__(64 * kV2Waves) void wgrad_grouped_kernel(const WgradProblems tab) {
+  __shared__ float comb[kV2Waves][16 * 64];
+  __shared__ float combb[kV2Waves][64];
+  const int b = blockIdx.x;
+  int g = 0;
+  while (g + 1 < tab.G && b >= tab.p[g + 1].blk0) ++g;  // block-uniform scan (G <= 32)
+  const WgradProblem& P = tab.p[g];
+  const int s = b - P.blk0;
+  float* partb = P.part + (int64_t)P.S * P.O * P.I;
+  if (P.layout == 0) wgrad_v2_body<0, 1>(P.x, P.dy, P.R, P.I, P.O, P.N, P.SL, P.part, partb, s, comb, combb);
+  else wgrad_v2_body<1, 1>(P.x, P.dy, P.R, P.I, P.O, P.N, P.SL, P.part, partb, s, comb, combb);
+}
+
+struct WgradOut {
+  const float* part[2];  // partial sets of the (up to two) calls feeding this output
+  float* dw;
+  float* db;
+  int S[2];
+  int nseg, OI, O, blk0;
+};
+struct WgradOuts {
+  int G;
+  WgradOut p[kGroupMax];
+};
+
+// The tree of wgrad_reduce_kernel for output element e of one partial set (all threads of
+// the block call it; red = the block's [kRedGroups][64] LDS).
+__device__ __forceinline__ float wgrad_tree(const float* __restrict__ part, int S, int OI, int O, int e,
+                                            float (*red)[64]) {
+  const int grp = threadIdx.x >> 6;
+  const bool is_w = e < OI, is_b = !is_w && e < OI + O;
+  float v = 0.f;
+  if (is_w || is_b) {
+    const float* p = is_w ? part + e : part + (int64_t)S * OI + (e - OI);
+    const int64_t st = is_w ? OI : O;
+    const int s0 = (S * grp) / kRedGroups, s1 = (S * (grp + 1)) / kRedGroups;
+    float a0 = 0.f, a1 = 0.f;
+    int s = s0;
+    for (; s + 2 <= s1; s += 2) {
+      a0 += p[(int64_t)s * st];
+      a1 += p[(int64_t)(s + 1) * st];
+    }
+    if (s < s1) a0 += p[(int64_t)s * st];
+    v = a0 + a1;
+  }
+  __syncthreads();  // red reused across calls
+  red[grp][threadIdx.x & 63] = v;
+  __syncthreads();
+#pragma unroll
+  for (int half = kRedGroups / 2; half >= 1; half >>= 1) {
+    if (grp < half) red[grp][threadIdx.x & 63] += red[grp + half][threadIdx.x & 63];
+    __syncthreads();
+  }
+  return red[0][threadIdx.x & 63];
+}
+
+__global__ __launch_bounds__(64 * kRedGroups) void wgrad_grouped_reduce_kernel(const WgradOuts tab) {
+  __shared__ float red[kRedGroups][64];
+  const int b = blockIdx.x;
+  int g = 0;
+  while (g + 1 < tab.G && b >= tab.p[g + 1].blk0) ++g;
+  const WgradOut& P = tab.p[g];
+  const int e = (b - P.blk0) * 64 + (threadIdx.x & 63);
+  float r = wgrad_tree(P.part[0], P.S[0], P.OI, P.O, e, red);
+  if (P.nseg > 1) r = r + wgrad_tree(P.part[1], P.S[1], P.OI, P.O, e, red);
+  if ((threadIdx.x >> 6) == 0 && e < P.OI + P.O) {
+    if (e < P.OI) P.dw[e] = r;
+    else if (P.db) P.db[e - P.OI] = r;
+  }
+}
+
+// Rows per slice of a grouped problem: ~kGroupSlices slices (whole 16-row batches, >= 128
+// rows); the group supplies the parallelism the single-layer launch gets from ~320 slices.
+constexpr int kGroupSlices = 64;
+inline int64_t grouped_slice_rows(int64_t R) {
+  int64_t SL = (R + kGroupSlices - 1) / kGroupSlices;
+  SL = (SL + 15) / 16 * 16;
+  return SL < kSlice ? kSlice : SL;
+}
+
 }  // namespace
 
 // Development hook (not in include/posekern.h): the LDS-staged slice kernel, for A/B timing.
@@ -326,13 +440,13 @@ extern "C" int pkdev_linear_wgrad_v1(const float* x, const float* dy, int layout
   PK_CHECK_LAUNCH();
   const int total = O * I + O;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(64 * kRedGroups), 0, s, part, partb, S, O * I, O,
-                     dw, db);
+                     dw, db, 0);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
 
 extern "C" int pk_linear_wgrad(const float* x, const float* dy, int layout, int64_t R, int I, int O, int N,
-                               float* work, float* dw, float* db, void* stream) {
+                               float* work, float* dw, float* db, int accumulate, void* stream) {
   PK_REQUIRE((layout == 0 || layout == 1) && R >= 0 && I > 0 && O > 0 && I <= kMaxC && O <= kMaxC);
   PK_REQUIRE(layout == 0 || N > 0);
   PK_REQUIRE(((I + 15) / 16) * ((O + 15) / 16) <= 4 * kMaxTilesPerWave);
@@ -340,6 +454,7 @@ extern "C" int pk_linear_wgrad(const float* x, const float* dy, int layout, int6
   hipStream_t s = pk::as_stream(stream);
   const int S = (int)((R + kSlice - 1) / kSlice);
   if (S == 0) {
+    if (accumulate) return PK_OK;  // no rows: nothing to add
     hipError_t e = pk::zero_async(dw, sizeof(float) * O * I, s);
     if (e == hipSuccess && db) e = pk::zero_async(db, sizeof(float) * O, s);
     return e == hipSuccess ? PK_OK : (int)e;
@@ -375,7 +490,7 @@ extern "C" int pk_linear_wgrad(const float* x, const float* dy, int layout, int6
   PK_CHECK_LAUNCH();
   const int total = O * I + O;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(64 * kRedGroups), 0, s, part,
-                     work + (int64_t)S2 * O * I, S2, O * I, O, dw, db);
+                     work + (int64_t)S2 * O * I, S2, O * I, O, dw, db, accumulate);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
@@ -741,4 +856,117 @@ extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, 
                        Cin, Cout, transw, relu, y);
   PK_CHECK_LAUNCH();
   return PK_OK;
+}
+
+extern "C" int64_t pk_linear_wgrad_grouped_work(const pk_wgrad_call* calls, int n) {
+  if (n < 0 || (n > 0 && calls == nullptr)) return -1;
+  int64_t tot = 0;
+  for (int c = 0; c < n; ++c) {
+    const pk_wgrad_call& k = calls[c];
+    if (k.R <= 0) continue;
+    const int64_t S = (k.R + grouped_slice_rows(k.R) - 1) / grouped_slice_rows(k.R);
+    tot += S * ((int64_t)k.O * k.I + k.O);
+  }
+  return tot;
+}
+
+extern "C" int pk_linear_wgrad_grouped(const pk_wgrad_call* calls, int n, float* work, int64_t work_elems,
+                                       void* stream) {
+  PK_REQUIRE(n >= 0 && (n == 0 || calls != nullptr));
+  hipStream_t st = pk::as_stream(stream);
+  // validate; a call with accumulate = 1 must name the dw (and db) of an earlier call
+  std::vector<int> first(n, -1), second(n, -1);
+  for (int c = 0; c < n; ++c) {
+    const pk_wgrad_call& k = calls[c];
+    PK_REQUIRE(k.dw && k.R >= 0 && k.I > 0 && k.O > 0 && k.I <= kMaxC && k.O <= kMaxC);
+    PK_REQUIRE(((k.O + 31) / 32) * ((k.I + 31) / 32) <= kV2Waves);  // one 32x32 tile per wave
+    PK_REQUIRE(k.layout == 0 || (k.layout == 1 && k.N > 0 && k.N % 16 == 0));
+    PK_REQUIRE(k.R == 0 || (k.x && k.dy));
+    if (k.accumulate) {
+      int f = -1;
+      for (int q = 0; q < c; ++q)
+        if (calls[q].dw == k.dw && !calls[q].accumulate) f = q;
+      PK_REQUIRE(f >= 0 && second[f] < 0 && calls[f].I == k.I && calls[f].O == k.O && calls[f].db == k.db);
+      second[f] = c;
+    }
+  }
+  const int64_t need = pk_linear_wgrad_grouped_work(calls, n);
+  PK_REQUIRE(need <= work_elems && (need == 0 || work != nullptr));
+  std::vector<int64_t> S(n, 0), SLv(n, 0), off(n, 0);
+  int64_t o = 0;
+  for (int c = 0; c < n; ++c) {
+    const pk_wgrad_call& k = calls[c];
+    if (k.R <= 0) continue;
+    SLv[c] = grouped_slice_rows(k.R);
+    S[c] = (k.R + SLv[c] - 1) / SLv[c];
+    off[c] = o;
+    o += S[c] * ((int64_t)k.O * k.I + k.O);
+  }
+  // partials: chunks of <= kGroupMax problems
+  WgradProblems tp{};
+  int blocks = 0;
+  auto flush_p = [&]() -> int {
+    if (tp.G == 0) return PK_OK;
+    hipLaunchKernelGGL(wgrad_grouped_kernel, dim3(blocks), dim3(64 * kV2Waves), 0, st, tp);
+    PK_CHECK_LAUNCH();
+    tp.G = 0;
+    blocks = 0;
+    return PK_OK;
+  };
+  for (int c = 0; c < n; ++c) {
+    const pk_wgrad_call& k = calls[c];
+    if (S[c] == 0) continue;
+    WgradProblem& P = tp.p[tp.G++];
+    P = WgradProblem{k.x, k.dy, work + off[c], k.R, k.I, k.O, k.N, k.layout, (int)SLv[c], (int)S[c], blocks, 0};
+    blocks += (int)S[c];
+    if (tp.G == kGroupMax) {
+      const int rc = flush_p();
+      if (rc != PK_OK) return rc;
+    }
+  }
+  int rc = flush_p();
+  if (rc != PK_OK) return rc;
+  // reductions: one output per non-accumulating call (plus its accumulating partner)
+  WgradOuts to{};
+  blocks = 0;
+  auto flush_r = [&]() -> int {
+    if (to.G == 0) return PK_OK;
+    hipLaunchKernelGGL(wgrad_grouped_reduce_kernel, dim3(blocks), dim3(64 * kRedGroups), 0, st, to);
+    PK_CHECK_LAUNCH();
+    to.G = 0;
+    blocks = 0;
+    return PK_OK;
+  };
+  for (int c = 0; c < n; ++c) {
+    const pk_wgrad_call& k = calls[c];
+    if (k.accumulate) continue;
+    int segs[2] = {c, second[c]};
+    WgradOut W{};
+    W.dw = k.dw;
+    W.db = k.db;
+    W.OI = k.O * k.I;
+    W.O = k.O;
+    W.nseg = 0;
+    for (int q = 0; q < 2; ++q) {
+      const int cc = segs[q];
+      if (cc < 0 || S[cc] == 0) continue;  // no rows: contributes zero
+      W.part[W.nseg] = work + off[cc];
+      W.S[W.nseg] = (int)S[cc];
+      ++W.nseg;
+    }
+    if (W.nseg == 0) {  // no rows in any feeding call: the gradient is zero
+      hipError_t e = pk::zero_async(k.dw, sizeof(float) * k.O * k.I, st);
+      if (e == hipSuccess && k.db) e = pk::zero_async(k.db, sizeof(float) * k.O, st);
+      if (e != hipSuccess) return (int)e;
+      continue;
+    }
+    W.blk0 = blocks;
+    to.p[to.G++] = W;
+    blocks += (W.OI + W.O + 63) / 64;
+    if (to.G == kGroupMax) {
+      rc = flush_r();
+      if (rc != PK_OK) return rc;
+    }
+  }
+  return flush_r();
 }

@@ -38,7 +38,9 @@ SIGNATURES = {
     "pk_fmap_solve_backward": [_P, _P, _P, _F, _I, _I, _P, _P, _P, _P],
     "pk_attention_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P],
     "pk_attention_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
-    "pk_linear_wgrad": [_P, _P, _I, _I64, _I, _I, _I, _P, _P, _P, _P],
+    "pk_linear_wgrad": [_P, _P, _I, _I64, _I, _I, _I, _P, _P, _P, _I, _P],
+    "pk_linear_wgrad_grouped_work": [_P, _I],
+    "pk_linear_wgrad_grouped": [_P, _I, _P, _I64, _P],
     "pk_linear_fwd": [_P, _P, _P, _I, _I64, _I, _I, _I, _I, _I, _P, _P],
     "pk_feat_dist_topk": [_P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "pk_rigidity_filter": [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P],
@@ -52,9 +54,16 @@ SIGNATURES = {
     "pk_sample_rgb": [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],
 }
 
-RESTYPES = {"pk_cgt_lstsq_work_size": _I64}  # everything else returns an int status
+RESTYPES = {"pk_cgt_lstsq_work_size": _I64, "pk_linear_wgrad_grouped_work": _I64}  # everything else returns an int status
 
 _lib: Optional[ctypes.CDLL] = None
+
+
+class WgradCall(ctypes.Structure):
+    """pk_wgrad_call (include/posekern.h)."""
+    _fields_ = [("x", _P), ("dy", _P), ("dw", _P), ("db", _P), ("R", _I64), ("I", ctypes.c_int32),
+                ("O", ctypes.c_int32), ("N", ctypes.c_int32), ("layout", ctypes.c_int32),
+                ("accumulate", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
 class PoseKernError(RuntimeError):

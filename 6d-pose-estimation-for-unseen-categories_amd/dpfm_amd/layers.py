@@ -16,12 +16,79 @@ import torch.nn.functional as F
 
 from . import ops
 
+_SIDE = None  # the active GroupedWgrad (TrainStep's backward), or None
+
+
+class GroupedWgrad:
+    """Weight gradients of all per-point layers of one backward in two launches.
+
+    Each layer's backward records (x, dy) instead of launching pk_linear_wgrad (two
+    launches per layer, 56 per training step, each too small to fill the chip) and returns
+    None for its weight / bias so autograd leaves their .grad alone. `end()` issues one
+    grouped pk_linear_wgrad_grouped on the same stream, writing into persistent .grad
+    buffers; a weight used twice in the forward (the refinement layer, modeling/dpfm.py:
+    100-104; first/last_lin on both shapes) accumulates in autograd's order. Everything
+    stays on one stream: a single-stream HIP graph replays without cross-queue
+    dependencies (a forked side stream measured slower on MI355X)."""
+
+    def __init__(self, params):
+        self.params = [p for p in params]
+        self.bufs = {id(p): torch.zeros_like(p, memory_format=torch.contiguous_format) for p in self.params}
+        self.seen = set()
+        self.calls = []
+
+    def begin(self):
+        global _SIDE
+        for p in self.params:
+            p.grad = self.bufs[id(p)]
+        self.seen = set()
+        self.calls = []
+        _SIDE = self
+
+    def owns(self, p) -> bool:
+        return id(p) in self.bufs
+
+    def launch(self, x, dy, weight, bias, channels_first: bool):
+        acc = id(weight) in self.seen
+        self.seen.add(id(weight))
+        if bias is not None:
+            self.seen.add(id(bias))
+        dw = self.bufs[id(weight)]
+        db = self.bufs[id(bias)] if bias is not None else None
+        self.calls.append((x, dy, channels_first, dw.view(dw.shape[0], -1), db, acc))
+
+    @staticmethod
+    def _groupable(c) -> bool:
+        x, dy, cf, dw, _, _ = c
+        O, I = dw.shape
+        return ((O + 31) // 32) * ((I + 31) // 32) <= 8 and (not cf or x.shape[-1] % 16 == 0)
+
+    def end(self, run: bool = True):
+        global _SIDE
+        _SIDE = None
+        if run:
+            if all(self._groupable(c) for c in self.calls):
+                ops.linear_wgrad_grouped(self.calls)
+            else:  # a shape outside the grouped kernel's range: one launch pair per call, in order
+                for x, dy, cf, dw, db, acc in self.calls:
+                    ops.linear_wgrad(x, dy, channels_first=cf, want_bias=db is not None, dw=dw, db=db,
+                                     accumulate=acc)
+            for p in self.params:  # a layer the forward did not use gets a zero gradient
+                if id(p) not in self.seen:
+                    p.grad.zero_()
+        self.calls = []
+
+
+def _side_owns(weight, bias) -> bool:
+    return _SIDE is not None and _SIDE.owns(weight) and (bias is None or _SIDE.owns(bias))
+
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        ctx.param, ctx.bias = weight, bias  # the Parameter objects (SideWgrad's buffer keys)
         # a fresh (non-view) output: the reference applies in-place ReLUs to it (:112-116)
         return ops.linear_fwd(x, weight, bias, channels_first=False)
 
@@ -32,7 +99,10 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = ops.linear_fwd(dy, weight, None, channels_first=False, transw=True)  # dy W
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            dw, db = ops.linear_wgrad(x, dy, channels_first=False, want_bias=ctx.has_bias)
+            if _side_owns(ctx.param, ctx.bias):
+                _SIDE.launch(x, dy, ctx.param, ctx.bias, channels_first=False)
+            else:
+                dw, db = ops.linear_wgrad(x, dy, channels_first=False, want_bias=ctx.has_bias)
         return dx, dw, db
 
 
@@ -41,6 +111,7 @@ class _Conv1x1Fn(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        ctx.param, ctx.bias = weight, bias  # the Parameter objects (SideWgrad's buffer keys)
         # y[b] = W x[b] (+ b) over every point, bias fused (no MIOpen convolution)
         return ops.linear_fwd(x, weight[:, :, 0], bias, channels_first=True)
 
@@ -51,8 +122,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = ops.linear_fwd(dy, weight[:, :, 0], None, channels_first=True, transw=True)  # W^T dy
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            dw, db = ops.linear_wgrad(x, dy, channels_first=True, want_bias=ctx.has_bias)
-            dw = dw[:, :, None]
+            if _side_owns(ctx.param, ctx.bias):
+                _SIDE.launch(x, dy, ctx.param, ctx.bias, channels_first=True)
+            else:
+                dw, db = ops.linear_wgrad(x, dy, channels_first=True, want_bias=ctx.has_bias)
+                dw = dw[:, :, None]
         return dx, dw, db
 
 

@@ -316,9 +316,12 @@ def attention(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor) -> to
 # ------------------------------------------------------------------------------ per-point layers
 
 
-def linear_wgrad(x: torch.Tensor, dy: torch.Tensor, channels_first: bool, want_bias: bool = True):
+def linear_wgrad(x: torch.Tensor, dy: torch.Tensor, channels_first: bool, want_bias: bool = True,
+                 dw: Optional[torch.Tensor] = None, db: Optional[torch.Tensor] = None, accumulate: bool = False):
     """(dW [O, I], db [O] or None) of y = W x + b over every point (pk_linear_wgrad).
-    channels_first=False: x [..., I], dy [..., O]; True: x [B, I, N], dy [B, O, N]."""
+    channels_first=False: x [..., I], dy [..., O]; True: x [B, I, N], dy [B, O, N].
+    `dw` / `db` (contiguous, O*I / O elements) are written in place when given, and added
+    to when `accumulate` (a weight used by several calls of one forward)."""
     x, dy = x.contiguous(), dy.contiguous()
     if channels_first:
         Bn, I, N = x.shape
@@ -330,12 +333,53 @@ def linear_wgrad(x: torch.Tensor, dy: torch.Tensor, channels_first: bool, want_b
     dev = x.device
     S = (R + 127) // 128
     work = torch.empty((max(S, 1) * (O * I + O),), dtype=torch.float32, device=dev)
-    dw = torch.empty((O, I), dtype=torch.float32, device=dev)
-    db = torch.empty((O,), dtype=torch.float32, device=dev) if want_bias else None
-    call("pk_linear_wgrad", ptr(x), ptr(dy), layout, int(R), I, O, int(N), ptr(work), ptr(dw), ptr(db),
-         _lib.stream(dev),
+    if dw is None:
+        dw = torch.empty((O, I), dtype=torch.float32, device=dev)
+    if db is None and want_bias:
+        db = torch.empty((O,), dtype=torch.float32, device=dev)
+    if dw.numel() != O * I or not dw.is_contiguous() or (db is not None and (db.numel() != O or not db.is_contiguous())):
+        raise _lib.PoseKernError("linear_wgrad: output buffers must be contiguous [O, I] / [O]")
+    call("pk_linear_wgrad", ptr(x), ptr(dy), layout, int(R), I, O, int(N), ptr(work), ptr(dw),
+         ptr(db if want_bias else None), int(accumulate), _lib.stream(dev),
          work=("mfma", 2 * int(R) * I * O))
     return dw, db
+
+
+def linear_wgrad_grouped(calls) -> None:
+    """pk_linear_wgrad_grouped: weight / bias gradients of many per-point layers in two
+    launches. calls: list of (x, dy, channels_first, dw, db_or_None, accumulate) with dw / db
+    contiguous output buffers; a call with accumulate=True adds to the buffers of the one
+    earlier call naming the same dw. Inputs must stay alive until the launches complete
+    (stream order), as for any stream-ordered op."""
+    if not calls:
+        return
+    arr = (_lib.WgradCall * len(calls))()
+    flops = 0
+    keep = []
+    for k, (x, dy, cf, dw, db, acc) in enumerate(calls):
+        x, dy = x.contiguous(), dy.contiguous()
+        keep += [x, dy]
+        if cf:
+            Bn, I, N = x.shape
+            O, R, layout = dy.shape[1], Bn * N, 1
+        else:
+            I, O = x.shape[-1], dy.shape[-1]
+            R, N, layout = x.numel() // I, 0, 0
+        if dw.numel() != O * I or not dw.is_contiguous() or (db is not None and (db.numel() != O or not db.is_contiguous())):
+            raise _lib.PoseKernError("linear_wgrad_grouped: output buffers must be contiguous [O, I] / [O]")
+        arr[k] = _lib.WgradCall(ptr(x).value, ptr(dy).value, ptr(dw).value, ptr(db).value if db is not None else None,
+                                int(R), I, O, int(N), layout, int(bool(acc)), 0)
+        flops += 2 * int(R) * I * O
+    n_work = _lib.lib().pk_linear_wgrad_grouped_work(arr, len(calls))
+    if n_work < 0:
+        raise _lib.PoseKernError("linear_wgrad_grouped: invalid call list")
+    dev = calls[0][0].device
+    work = torch.empty((max(int(n_work), 1),), dtype=torch.float32, device=dev)
+    call("pk_linear_wgrad_grouped", arr, len(calls), ptr(work), int(n_work), _lib.stream(dev),
+         work=("mfma", flops))
+    # the work buffer and any contiguous() copies are freed on this stream after the launches
+    # (the caching allocator reuses them only for later work on the same stream)
+    del keep
 
 
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], channels_first: bool,

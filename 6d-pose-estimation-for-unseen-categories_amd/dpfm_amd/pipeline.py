@@ -12,6 +12,7 @@ Nothing here synchronises with the host; callers decide when to read results.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -23,7 +24,14 @@ from . import ops
 from .dataset.object import CropFormation, Crops, FrameBatch
 from .dataset.synthetic import cad_points, lbo_operators, make_frame
 from .models.dpfm import DPFMNet
+from .layers import Conv1d, GroupedWgrad, Linear
 from .utils.loss import DPFMLoss
+
+
+def _on(stream):
+    """torch.cuda.stream(stream), or a no-op context for None."""
+    import contextlib
+    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
 
 
 @dataclass
@@ -104,7 +112,8 @@ class TrainStep:
     backward re-creates them)."""
 
     def __init__(self, model: DPFMNet, lr: float = 5e-4, max_norm: float = 5.0, nce_num_pairs: int = 512,
-                 group: Optional[dist.ProcessGroup] = None, seed: int = 0, capturable: bool = False):
+                 group: Optional[dist.ProcessGroup] = None, seed: int = 0, capturable: bool = False,
+                 overlap: bool = True, grouped: bool = True):
         self.model = model
         self.params = [p for p in model.parameters()]
         # config/dpfm_orig.gin:62-63; capturable keeps the step count on the device
@@ -117,6 +126,18 @@ class TrainStep:
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed)
         self.flat = torch.zeros(sum(p.numel() for p in self.params), dtype=torch.float32, device=dev)
+        # grouped=True (HIP devices): the per-point layers' weight gradients are recorded during
+        # backward and computed in one grouped launch pair at its end (layers.GroupedWgrad).
+        # overlap=True (development knob PK_STEP_OVERLAP=aux): C_gt and the naive point map +
+        # IR on an auxiliary stream beside the model. Off by default: a HIP graph with a
+        # forked stream replayed ~1 ms/step slower than the serial one on MI355X.
+        mode = os.environ.get("PK_STEP_OVERLAP", "none")
+        self.overlap = overlap and dev.type == "cuda" and mode == "aux"
+        self.aux = torch.cuda.Stream(dev) if self.overlap else None
+        self.side = None
+        if grouped and dev.type == "cuda":
+            lin = [p for m in model.modules() if isinstance(m, (Linear, Conv1d)) for p in m.parameters(recurse=False)]
+            self.side = GroupedWgrad(lin)
 
     def nce_counter(self) -> torch.Tensor:
         """The device step counter keying this step's NCE pair draws (utils/loss.py)."""
@@ -165,16 +186,35 @@ class TrainStep:
     def forward_backward(self, op: Operators, crops: Crops) -> dict:
         self.model.train()
         batch = model_batch(op, crops)
-        C_pred, o12, o21, f1, f2, _, _ = self.model(batch)
-        with torch.no_grad():
+        main = torch.cuda.current_stream() if self.overlap else None
+        if self.overlap:  # C_gt needs only the crops: beside the model forward
+            self.aux.wait_stream(main)
+        with torch.no_grad(), _on(self.aux):
             C_gt = ops.cgt_lstsq(crops.pairs, crops.npairs, op.cad_evecs, op.pc_evecs)
+        C_pred, o12, o21, f1, f2, _, _ = self.model(batch)
+        if self.overlap:
+            main.wait_stream(self.aux)
+            C_gt.record_stream(main)
         loss, log = self.crit.forward_batched(C_pred, C_gt, crops.pairs, crops.npairs, f1, f2, o12, o21,
                                               crops.overlap_12, crops.overlap_21, generator=self.gen)
-        with torch.no_grad():  # train.py:109-116 (naive solver + IR per crop)
+        if self.overlap:  # the point map + IR read only C_pred: beside the backward
+            self.aux.wait_stream(main)
+        with torch.no_grad(), _on(self.aux):  # train.py:109-116 (naive solver + IR per crop)
             p_pred = naive_p2p_batched(C_pred.detach(), op.cad_evecs, op.pc_evecs)
             npred = torch.full((p_pred.shape[0],), p_pred.shape[2], dtype=torch.int32, device=p_pred.device)
             ir = ops.inlier_ratio(p_pred, npred, op.cad_xyz, crops.align32, op.ir_thr, layout=1).mean()
-        loss.backward()
+        if self.side is not None:
+            self.side.begin()
+        ok = False
+        try:
+            loss.backward()
+            ok = True
+        finally:
+            if self.side is not None:
+                self.side.end(run=ok)
+        if self.overlap:
+            main.wait_stream(self.aux)
+            ir.record_stream(main)
         log["IR"] = ir
         return log
 

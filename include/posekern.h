@@ -151,9 +151,32 @@ int pk_attention_bwd(const float* q, const float* k, const float* v, const float
  * models/dpfm.py:22-30; refinement Conv1d(k=1), modeling/dpfm.py:16-26,45-54,82-95):
  * dw[o,i] = sum_r dy[r,o] x[r,i], db[o] = sum_r dy[r,o] over all R = B*N points.
  *   layout 0: x [R, I], dy [R, O] row-major; layout 1: x [R/N, I, N], dy [R/N, O, N]
- *   I, O <= 128, O * I <= 8192; work f32 [ceil(R/128) * (O*I + O)]; db may be NULL. */
+ *   I, O <= 128, O * I <= 8192; work f32 [ceil(R/128) * (O*I + O)]; db may be NULL.
+ *   accumulate = 1 adds to dw / db instead of overwriting them (a weight shared by several
+ *   calls of one forward, e.g. the refinement layer applied twice at modeling/dpfm.py:100-104,
+ *   accumulates its gradient the way autograd's AccumulateGrad does). */
 int pk_linear_wgrad(const float* x, const float* dy, int layout, int64_t R, int I, int O, int N,
-                    float* work, float* dw, float* db, void* stream);
+                    float* work, float* dw, float* db, int accumulate, void* stream);
+
+/* Grouped weight gradients: every pk_linear_wgrad of one backward pass in two launches
+ * (all layers' slice partials, then all reductions) instead of two per layer. `calls` is a
+ * HOST array read during the call (its contents are baked into the launches' kernel
+ * arguments, so a HIP-graph capture replays them). Per call as pk_linear_wgrad, with
+ * (O/32 rounded up) * (I/32 rounded up) <= 8 and N % 16 == 0 for layout 1. A call with
+ * accumulate = 1 adds to the dw / db of the one earlier call (accumulate = 0) naming the
+ * same dw: r = partials(earlier) + partials(later), autograd's accumulation order for a
+ * layer applied twice (modeling/dpfm.py:100-104). work: f32, pk_linear_wgrad_grouped_work()
+ * elements (host-computed from the calls). */
+typedef struct pk_wgrad_call {
+  const float* x;
+  const float* dy;
+  float* dw;
+  float* db;
+  int64_t R;
+  int32_t I, O, N, layout, accumulate, pad;
+} pk_wgrad_call;
+int64_t pk_linear_wgrad_grouped_work(const pk_wgrad_call* calls, int n);
+int pk_linear_wgrad_grouped(const pk_wgrad_call* calls, int n, float* work, int64_t work_elems, void* stream);
 
 /* Forward / input gradient of the same per-point layers (nn.Linear at models/dpfm.py:22-30
  * and modeling/dpfm.py:16-26,90-91,113-116; Conv1d(k=1) at modeling/dpfm.py:16-26,49-50):

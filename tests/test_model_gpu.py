@@ -103,6 +103,47 @@ def test_linear_wgrad(device, shape, channels_first):
     assert (db.cpu().double() - exp_b).abs().le(1e-5 * bnd_b + 1e-30).all()
 
 
+def test_linear_wgrad_grouped(device):
+    """pk_linear_wgrad_grouped (every layer of a backward in two launches) vs fp64 per call:
+    both layouts, a shared layer fed by two calls (accumulate), an empty call, a layer
+    whose only call is empty (zero gradient), and > 32 calls (several table chunks)."""
+    from dpfm_amd import ops
+    g = torch.Generator().manual_seed(11)
+    specs = [  # (lead shape, I, O, channels_first, shared-with index or None)
+        ((64, 1024), 128, 64, False, None), ((64, 1024), 64, 64, False, None), ((3, 700), 3, 64, False, None),
+        ((32, 1024), 32, 32, True, None), ((32, 1024), 64, 32, True, None), ((32, 1024), 32, 32, True, 3),
+        ((0,), 16, 8, False, None), ((5, 33), 64, 32, False, None), ((2, 1024), 64, 64, True, 1 << 30),
+    ]
+    specs = specs + [((7, 48), 32, 32, False, None)] * 30
+    calls, exp = [], {}
+    for k, (lead, I, O, cf, shared) in enumerate(specs):
+        if cf:
+            Bn, N = lead
+            x, dy = torch.randn(Bn, I, N, generator=g), torch.randn(Bn, O, N, generator=g)
+            ew, eb = torch.einsum("bon,bin->oi", dy.double(), x.double()), dy.double().sum((0, 2))
+            bw = torch.einsum("bon,bin->oi", dy.double().abs(), x.double().abs())
+        else:
+            x, dy = torch.randn(*lead, I, generator=g), torch.randn(*lead, O, generator=g)
+            x2, d2 = x.reshape(-1, I).double(), dy.reshape(-1, O).double()
+            ew, eb, bw = d2.t() @ x2, d2.sum(0), d2.abs().t() @ x2.abs()
+        if shared is not None and shared < len(calls):
+            dw, db = calls[shared][3], calls[shared][4]
+            e = exp[shared]
+            exp[shared] = (e[0] + ew, e[1] + eb, e[2] + bw)
+            calls.append((x.to(device), dy.to(device), cf, dw, db, True))
+        else:
+            dw = torch.full((O, I), float("nan"), device=device)
+            db = torch.full((O,), float("nan"), device=device)
+            exp[k] = (ew, eb, bw)
+            calls.append((x.to(device), dy.to(device), cf, dw, db, False))
+    ops.linear_wgrad_grouped(calls)
+    torch.cuda.synchronize()
+    for k, (ew, eb, bw) in exp.items():
+        dw, db = calls[k][3].cpu().double(), calls[k][4].cpu().double()
+        assert (dw - ew).abs().le(1e-5 * bw + 1e-30).all(), k
+        assert (db - eb).abs().le(1e-5 * bw.max() + 1e-30).all(), k
+
+
 @pytest.mark.parametrize("N,M", [(300, 200), (1024, 1024), (64, 1), (17, 130)])
 def test_attention_fwd_bwd(device, N, M):
     """H8 fused attention vs modeling/dpfm.py:29-37 evaluated in fp64 (truth) and fp32:

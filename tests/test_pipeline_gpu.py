@@ -61,6 +61,75 @@ def test_train_and_infer_steps(device):
     assert out["T"].shape == (F, 4, 4) and torch.isfinite(out["metrics"]).all()
 
 
+def test_grouped_wgrad_step_matches_serial(device):
+    """TrainStep's grouped weight gradients (layers.GroupedWgrad: every per-point layer's
+    dW / db recorded during backward, computed in one pk_linear_wgrad_grouped launch pair,
+    shared layers accumulating). The recorded (x, dy) of every call are checked against an
+    fp64 recomputation within the fp32 summation bound 1e-5 * sum_r |dy||x|; every layer
+    parameter is fed; the per-layer autograd path agrees within 2x that bound plus its own
+    run-to-run spread (torch ops without deterministic kernels)."""
+    from dpfm_amd import layers
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import TrainStep, make_frame_batch
+    F, N = 4, 512
+    fb, op = make_frame_batch(F, N, N, seed=90, device=device)
+    crops = CropFormation(n1=N, npoint=N)(fb)
+    models = []
+    for _ in range(3):
+        torch.manual_seed(3)
+        models.append(DPFMNet().to(device))
+    steps = [TrainStep(models[0], seed=2, grouped=False), TrainStep(models[1], seed=2, grouped=False),
+             TrainStep(models[2], seed=2, grouped=True)]
+    assert steps[2].side is not None and len(steps[2].side.params) > 30 and steps[0].side is None
+    rec = []
+    orig = layers.ops.linear_wgrad_grouped
+
+    def spy(calls):
+        rec.extend((c[0].detach().clone(), c[1].detach().clone(), c[2], c[3], c[4], c[5]) for c in calls)
+        return orig(calls)
+
+    layers.ops.linear_wgrad_grouped = spy
+    try:
+        for s in steps:
+            s.forward_backward(op, crops)
+    finally:
+        layers.ops.linear_wgrad_grouped = orig
+    torch.cuda.synchronize()
+    # fp64 truth and bound per output buffer from the recorded calls
+    truth = {}
+    for x, dy, cf, dw, db, acc in rec:
+        if cf:
+            X, D = x.transpose(1, 2).reshape(-1, x.shape[1]).double(), dy.transpose(1, 2).reshape(-1, dy.shape[1]).double()
+        else:
+            X, D = x.reshape(-1, x.shape[-1]).double(), dy.reshape(-1, dy.shape[-1]).double()
+        key = dw.data_ptr()
+        assert acc == (key in truth)
+        t = (D.t() @ X, D.abs().t() @ X.abs(), D.sum(0), D.abs().sum(0), dw, db)
+        if key in truth:
+            u = truth[key]
+            t = (u[0] + t[0], u[1] + t[1], u[2] + t[2], u[3] + t[3], dw, db)
+        truth[key] = t
+    n_params = 0
+    for (n, p0), p1, p2 in zip(models[0].named_parameters(), models[1].parameters(), models[2].parameters()):
+        g0, g1, g2 = p0.grad, p1.grad, p2.grad
+        assert g2 is not None, n
+        hit = [t for t in truth.values() if t[4].data_ptr() == g2.data_ptr() or
+               (t[5] is not None and t[5].data_ptr() == g2.data_ptr())]
+        if not hit:  # not a per-point layer parameter (diffusion_time): plain autograd
+            assert n.endswith("diffusion_time"), n
+            continue
+        n_params += 1
+        w, bw, b, bb, dw, db = hit[0]
+        is_w = dw.data_ptr() == g2.data_ptr()
+        ref, bound = (w, bw) if is_w else (b, bb)
+        ref, bound = ref.reshape(g2.shape), bound.reshape(g2.shape)
+        assert (g2.double() - ref).abs().le(1e-5 * bound + 1e-30).all(), n
+        spread = (g0 - g1).abs().max().item()
+        assert (g0.double() - g2.double()).abs().le(2e-5 * bound + 4 * spread + 1e-30).all(), (n, spread)
+    assert n_params == len(steps[2].side.params)
+
+
 def test_graphed_train_step_matches_eager(device):
     """The HIP-graph replay of crop formation + training step (GraphedTrainStep) follows
     the same trajectory as the eager step from the same state (same RNG stream)."""

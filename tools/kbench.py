@@ -92,7 +92,7 @@ for B, N in [(32, 1024), (256, 2048)]:
     print(f"ball_query fused (count+scan+pairs, no mask) B={B} N={N}: {ms:.3f} ms")
 
 # per-point layer weight gradients: direct-load MFMA kernel vs the LDS-staged v1
-L.pkdev_linear_wgrad_v1.argtypes = _lib.SIGNATURES["pk_linear_wgrad"]
+L.pkdev_linear_wgrad_v1.argtypes = [c for i, c in enumerate(_lib.SIGNATURES["pk_linear_wgrad"]) if i != 10]  # no accumulate arg
 for (R_or_B, I, O, N, cf) in [(65536, 128, 64, 0, False), (65536, 64, 64, 0, False), (65536, 64, 32, 0, False),
                               (32, 64, 64, 1024, True), (32, 32, 32, 1024, True)]:
     if cf:
