@@ -437,6 +437,47 @@ def nce_select(counts: torch.Tensor, cap: int, num: int, seed: int, ctr: torch.T
     return rows, valid
 
 
+class _NCELoss(torch.autograd.Function):
+    """Per-crop NCE loss [B] with gradients computed in the forward pass (pk_nce_loss):
+    the backward only scales them by the incoming per-crop gradient."""
+
+    @staticmethod
+    def forward(ctx, f1, f2, pairs, rows, valid, nce_t, want):
+        B, N1, C = f1.shape
+        N2 = f2.shape[1]
+        S = rows.shape[1]
+        dev = f1.device
+        f1c, f2c = f1.detach().contiguous(), f2.detach().contiguous()
+        lse = torch.empty((B, max(S, 1)), dtype=torch.float32, device=dev)
+        term = torch.empty_like(lse)
+        loss = torch.empty((B,), dtype=torch.float32, device=dev)
+        g1 = torch.empty_like(f1c) if want else None
+        g2 = torch.empty_like(f2c) if want else None
+        call("pk_nce_loss", ptr(f1c), ptr(f2c), B, int(N1), int(N2), int(C), ptr(pairs), int(pairs.shape[1]),
+             ptr(rows), ptr(valid), int(S), float(nce_t), ptr(lse), ptr(term), ptr(loss), ptr(g1), ptr(g2),
+             _lib.stream(dev), work=None)
+        ctx.save_for_backward(g1, g2)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        g1, g2 = ctx.saved_tensors
+        s = gl.reshape(-1, 1, 1)
+        return (g1 * s if ctx.needs_input_grad[0] else None, g2 * s if ctx.needs_input_grad[1] else None,
+                None, None, None, None, None)
+
+
+def nce_loss(f1: torch.Tensor, f2: torch.Tensor, pairs: torch.Tensor, rows: torch.Tensor, valid: torch.Tensor,
+             nce_t: float) -> torch.Tensor:
+    """utils/loss.py:17-40 for every crop at once: f1 [B, N1, 32], f2 [B, N2, 32], pairs int64
+    [B, cap, 2], rows int64 / valid bool [B, S <= 512] from nce_select -> loss f32 [B]."""
+    if f1.dtype != torch.float32 or f1.shape[-1] != 32:
+        raise _lib.PoseKernError("pk_nce_loss takes f32 features of width 32")
+    want = torch.is_grad_enabled() and (f1.requires_grad or f2.requires_grad)  # (forward runs under no_grad)
+    return _NCELoss.apply(f1, f2, pairs.contiguous(), rows.contiguous(), valid.contiguous().view(torch.uint8), nce_t,
+                          want)
+
+
 def rigidity_thresholds(diam: Sequence[float], device) -> torch.Tensor:
     """f32 [B,4]: float32(tau * diam) for tau = 0.3, 0.15, 0.055, 0.065 (Python-float
     products, as the reference compares with `tau * diam_cad`)."""

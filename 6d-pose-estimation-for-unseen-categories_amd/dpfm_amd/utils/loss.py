@@ -42,7 +42,12 @@ class NCESoftmaxLoss(nn.Module):
         self.nce_num_pairs = nce_num_pairs
 
     def forward_batched(self, f1, f2, pairs, rows, valid):
-        """Per-crop NCE loss [B]: pairs [B, cap, 2], rows/valid from nce_select."""
+        """Per-crop NCE loss [B]: pairs [B, cap, 2], rows/valid from nce_select. On HIP
+        devices one fused kernel pair (ops.nce_loss); the torch composition below is the
+        host-side restatement kept for CPU tensors (the gloo multi-process tests)."""
+        if f1.is_cuda:
+            from .. import ops
+            return ops.nce_loss(f1, f2, pairs, rows, valid, self.nce_t)
         f1n, f2n = F.normalize(f1, p=2, dim=-1), F.normalize(f2, p=2, dim=-1)
         sel = torch.gather(pairs, 1, rows[..., None].expand(-1, -1, 2))
         # rows past a crop's pair count select unwritten slots of the pair buffer: point

@@ -255,3 +255,80 @@ def test_linear_fwd(device, shape, channels_first, transw):
             exp = exp + b.double()
     assert y.shape == exp.shape
     assert (y - exp).abs().le(1e-5 * bound + 1e-6 * (0 if b is None else b.abs().max().item()) + 1e-30).all()
+
+
+def test_dpfm_loss_matches_oracle(device):
+    """H15 DPFMLoss (Frobenius + fused NCE kernel pk_nce_loss + weighted BCE, batched over
+    crops) vs the reference loss restated in fp64 on the CPU (utils/loss.py:8-99), on the
+    same NCE pair draw: loss within 1e-4 relative, every input gradient within 1e-4 of its
+    scale. Crops with more pairs than 512 (draw without replacement), fewer, exactly 512,
+    and repeated CAD / crop indices (one point in several pairs)."""
+    from dpfm_amd import ops
+    from dpfm_amd.utils.loss import DPFMLoss
+    g = torch.Generator().manual_seed(5)
+    B, N1, N2 = 4, 700, 600
+    counts = [1500, 300, 512, 2000]
+    cap = max(counts)
+    pairs = torch.zeros((B, cap, 2), dtype=torch.int64)
+    for b, c in enumerate(counts):
+        flat = torch.randperm(N1 * N2, generator=g)[:c]
+        pairs[b, :c, 0] = flat // N2
+        pairs[b, :c, 1] = flat % N2
+        if b == 3:  # many pairs on a few CAD points
+            pairs[b, :c, 0] = pairs[b, :c, 0] % 37
+    f1 = torch.randn(B, N1, 32, generator=g)
+    f2 = torch.randn(B, N2, 32, generator=g)
+    C = torch.randn(B, 30, 30, generator=g)
+    C_gt = torch.randn(B, 30, 30, generator=g)
+    o12 = torch.rand(B, N1, generator=g) * 0.98 + 0.01
+    o21 = torch.rand(B, N2, generator=g) * 0.98 + 0.01
+    g12 = (torch.rand(B, N1, generator=g) < 0.4).to(torch.int8)
+    g21 = (torch.rand(B, N2, generator=g) < 0.6).to(torch.int8)
+    npairs = torch.tensor(counts, dtype=torch.int64)
+    ctr = torch.zeros(1, dtype=torch.int64, device=device)
+    rows, valid = ops.nce_select(npairs.to(device), cap, 512, 9, ctr)
+    sel = [rows[b][valid[b]].cpu() for b in range(B)]
+    assert [len(s) for s in sel] == [512, 300, 512, 512]
+    # device (fp32)
+    dv = [t.to(device).requires_grad_(True) for t in (C, f1, f2, o12, o21)]
+    crit = DPFMLoss(w_fmap=1, w_acc=1, w_nce=1, nce_t=0.07, nce_num_pairs=512)
+    loss, _ = crit.forward_batched(dv[0], C_gt.to(device), pairs.to(device), npairs.to(device), dv[1], dv[2],
+                                   dv[3], dv[4], g12.to(device), g21.to(device), selection=(rows, valid))
+    loss.backward()
+    # oracle (fp64, CPU)
+    rv = [t.double().requires_grad_(True) for t in (C, f1, f2, o12, o21)]
+    plist = [pairs[b, :counts[b]] for b in range(B)]
+    ref = M.dpfm_loss(rv[0], C_gt.double(), plist, sel, rv[1], rv[2], rv[3], rv[4], g12, g21)
+    ref.backward()
+    assert abs(float(loss) - float(ref)) <= 1e-4 * abs(float(ref)), (float(loss), float(ref))
+    for name, a, r in zip(("C", "f1", "f2", "o12", "o21"), dv, rv):
+        ga, gr = a.grad.cpu().double(), r.grad
+        scale = float(gr.abs().max())
+        assert (ga - gr).abs().max().item() <= 1e-4 * scale + 1e-9, (name, (ga - gr).abs().max().item(), scale)
+
+
+def test_nce_loss_edge_cases(device):
+    """pk_nce_loss: a crop without pairs has loss 0 and zero gradients; no-grad calls skip
+    the gradient pass and give the same loss."""
+    from dpfm_amd import ops
+    g = torch.Generator().manual_seed(8)
+    B, N = 3, 64
+    counts = torch.tensor([0, 5, 64], dtype=torch.int64)
+    pairs = torch.zeros((B, 64, 2), dtype=torch.int64)
+    for b in range(B):
+        pairs[b, :, 0] = torch.randperm(N, generator=g)
+        pairs[b, :, 1] = torch.randperm(N, generator=g)
+    ctr = torch.zeros(1, dtype=torch.int64, device=device)
+    rows, valid = ops.nce_select(counts.to(device), 64, 512, 1, ctr)
+    f1 = torch.randn(B, N, 32, generator=g).to(device).requires_grad_(True)
+    f2 = torch.randn(B, N, 32, generator=g).to(device).requires_grad_(True)
+    loss = ops.nce_loss(f1, f2, pairs.to(device), rows, valid, 0.07)
+    loss.sum().backward()
+    assert float(loss[0]) == 0.0 and float(f1.grad[0].abs().max()) == 0.0 and float(f2.grad[0].abs().max()) == 0.0
+    with torch.no_grad():
+        l2 = ops.nce_loss(f1, f2, pairs.to(device), rows, valid, 0.07)
+    assert torch.equal(loss.detach(), l2)
+    for b in (1, 2):
+        s = rows[b][valid[b]].cpu()
+        r = M.nce_loss(f1[b].detach().cpu().double(), f2[b].detach().cpu().double(), pairs[b, :int(counts[b])], s)
+        assert abs(float(loss[b]) - float(r)) <= 1e-4 * abs(float(r))
