@@ -382,6 +382,28 @@ def linear_wgrad_grouped(calls) -> None:
     del keep
 
 
+def clip_rmsprop(params, grads, square_avg, steps, max_norm: float, lr: float, alpha: float, eps: float,
+                 norm_out: Optional[torch.Tensor] = None) -> None:
+    """clip_grad_norm_(max_norm) + RMSprop step (no momentum / centering / weight decay) over
+    lists of f32 device tensors, in two launches (pk_clip_rmsprop). Updates params, grads
+    (clipped), square_avg and steps in place."""
+    import ctypes
+    n = len(params)
+    if not (len(grads) == len(square_avg) == n and (steps is None or len(steps) == n)):
+        raise _lib.PoseKernError("clip_rmsprop: list lengths differ")
+    for t in list(params) + list(grads) + list(square_avg):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise _lib.PoseKernError("clip_rmsprop: f32 contiguous tensors only")
+    P = ctypes.c_void_p * n
+    arr = lambda ts: P(*[ptr(t).value for t in ts])  # noqa: E731
+    numel = (ctypes.c_int64 * n)(*[t.numel() for t in params])
+    dev = params[0].device
+    work = torch.empty((64,), dtype=torch.float32, device=dev)
+    call("pk_clip_rmsprop", arr(params), arr(grads), arr(square_avg), arr(steps) if steps is not None else None,
+         numel, n, float(max_norm), float(lr), float(alpha), float(1.0 - alpha), float(eps), ptr(work),
+         ptr(norm_out), _lib.stream(dev), work=None)
+
+
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], channels_first: bool,
                transw: bool = False, relu: bool = False) -> torch.Tensor:
     """pk_linear_fwd: y = x W^T (+ b) over every point (W [Cout, Cin], or W^T read from a

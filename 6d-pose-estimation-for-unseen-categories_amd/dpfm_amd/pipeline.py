@@ -113,7 +113,7 @@ class TrainStep:
 
     def __init__(self, model: DPFMNet, lr: float = 5e-4, max_norm: float = 5.0, nce_num_pairs: int = 512,
                  group: Optional[dist.ProcessGroup] = None, seed: int = 0, capturable: bool = False,
-                 overlap: bool = True, grouped: bool = True):
+                 overlap: bool = True, grouped: bool = True, fused_opt: bool = True):
         self.model = model
         self.params = [p for p in model.parameters()]
         # config/dpfm_orig.gin:62-63; capturable keeps the step count on the device
@@ -126,6 +126,8 @@ class TrainStep:
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed)
         self.flat = torch.zeros(sum(p.numel() for p in self.params), dtype=torch.float32, device=dev)
+        # clip + RMSprop in one HIP launch on HIP devices (torch's optimizer keeps the state)
+        self.fused_opt = fused_opt and dev.type == "cuda" and len(self.params) <= 96
         # grouped=True (HIP devices): the per-point layers' weight gradients are recorded during
         # backward and computed in one grouped launch pair at its end (layers.GroupedWgrad).
         # overlap=True (development knob PK_STEP_OVERLAP=aux): C_gt and the naive point map +
@@ -218,11 +220,32 @@ class TrainStep:
         log["IR"] = ir
         return log
 
+    def _fused_state(self):
+        """The optimizer's per-parameter state (RMSprop's lazy init: step, square_avg),
+        created in place if missing, so torch's optimizer object keeps owning it."""
+        steps, sqs = [], []
+        for p in self.params:
+            st = self.opt.state[p]
+            if len(st) == 0:
+                st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                st["square_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            steps.append(st["step"])
+            sqs.append(st["square_avg"])
+        return steps, sqs
+
     def apply(self, allreduce: bool = True, reset: bool = True):
         if allreduce:
             self.allreduce_grads()
-        torch.nn.utils.clip_grad_norm_(self.params, max_norm=self.max_norm, norm_type=2)
-        self.opt.step()
+        grp = self.opt.param_groups[0]
+        fused = (self.fused_opt and len(self.opt.param_groups) == 1 and grp["momentum"] == 0 and not grp["centered"]
+                 and grp["weight_decay"] == 0 and all(p.grad is not None for p in self.params))
+        if fused:  # clip_grad_norm_ + RMSprop.step in one launch (pk_clip_rmsprop)
+            steps, sqs = self._fused_state()
+            ops.clip_rmsprop(self.params, [p.grad for p in self.params], sqs, steps, self.max_norm, grp["lr"],
+                             grp["alpha"], grp["eps"])
+        else:
+            torch.nn.utils.clip_grad_norm_(self.params, max_norm=self.max_norm, norm_type=2)
+            self.opt.step()
         if reset:  # (a captured backward that started from None grads overwrites them instead)
             self.opt.zero_grad(set_to_none=True)
 

@@ -178,6 +178,17 @@ typedef struct pk_wgrad_call {
 int64_t pk_linear_wgrad_grouped_work(const pk_wgrad_call* calls, int n);
 int pk_linear_wgrad_grouped(const pk_wgrad_call* calls, int n, float* work, int64_t work_elems, void* stream);
 
+/* Optimizer tail of one training step (scripts/train.py:121-124): clip_grad_norm_(max_norm)
+ * over every gradient, then RMSprop (config/dpfm_orig.gin:62-63: no momentum, not centered,
+ * no weight decay) — two launches. work: f32 [64] scratch (partial norms). HOST arrays of n <= 96 device pointers: params, grads
+ * (clipped in place), square_avg state, steps (f32 [1] counters, +1 each; may be NULL) and
+ * numel (host int64). one_minus_alpha = float(1 - alpha) computed in double by the caller
+ * (torch passes value = 1 - alpha as a Python float). norm_out (f32 [1], may be NULL)
+ * receives the total gradient norm before clipping. */
+int pk_clip_rmsprop(float* const* params, float* const* grads, float* const* square_avg, float* const* steps,
+                    const int64_t* numel, int n, float max_norm, float lr, float alpha, float one_minus_alpha,
+                    float eps, float* work, float* norm_out, void* stream);
+
 /* Forward / input gradient of the same per-point layers (nn.Linear at models/dpfm.py:22-30
  * and modeling/dpfm.py:16-26,90-91,113-116; Conv1d(k=1) at modeling/dpfm.py:16-26,49-50):
  *   y = x W^T (+ bias) (ReLU if relu), W f32 [Cout, Cin]; with transw = 1 the weight is

@@ -193,3 +193,35 @@ def test_pipelined_trainer_matches_eager(device):
         assert torch.allclose(le["loss"], lp["loss"], rtol=1e-4, atol=1e-5), (le["loss"], lp["loss"])
     for a, b in zip(m_eager.parameters(), m_pipe.parameters()):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=5e-3)
+
+
+@pytest.mark.parametrize("scale", [10.0, 1e-3])
+def test_fused_clip_rmsprop_matches_torch(device, scale):
+    """pk_clip_rmsprop (TrainStep.apply's clip_grad_norm_(5.0) + RMSprop(5e-4) in one launch)
+    vs torch's clip_grad_norm_ + RMSprop.step over three steps with fresh gradients each
+    step, clipping active (scale 10) and inactive (1e-3): parameters, clipped gradients and
+    square_avg within fp32 rounding (2e-6 relative to each tensor's scale)."""
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import TrainStep
+    torch.manual_seed(4)
+    ma, mb = DPFMNet().to(device), DPFMNet().to(device)
+    mb.load_state_dict(ma.state_dict())
+    sa, sb = TrainStep(ma, fused_opt=True), TrainStep(mb, fused_opt=False)
+    assert sa.fused_opt and not sb.fused_opt
+    g = torch.Generator(device=device).manual_seed(1)
+    for it in range(3):
+        for p, q in zip(ma.parameters(), mb.parameters()):
+            gr = torch.randn(p.shape, device=device, generator=g) * scale
+            p.grad, q.grad = gr.clone(), gr.clone()
+        ga = [p.grad for p in ma.parameters()]
+        gb = [q.grad for q in mb.parameters()]
+        sa.apply(reset=False)
+        sb.apply(reset=False)
+        torch.cuda.synchronize()
+        for (n, p), q, x, y in zip(ma.named_parameters(), mb.parameters(), ga, gb):
+            tol = 2e-6 * max(float(q.detach().abs().max()), 1e-30)
+            assert (p.detach() - q.detach()).abs().max().item() <= tol, (it, n)
+            assert (x - y).abs().max().item() <= 2e-6 * float(y.abs().max()) + 1e-30, (it, n)
+            sqa, sqb = sa.opt.state[p]["square_avg"], sb.opt.state[q]["square_avg"]
+            assert (sqa - sqb).abs().max().item() <= 2e-6 * float(sqb.abs().max()) + 1e-30, (it, n)
+        assert float(sa.opt.state[next(ma.parameters())]["step"]) == it + 1
