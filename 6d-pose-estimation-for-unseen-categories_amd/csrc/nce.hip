@@ -39,18 +39,23 @@ constexpr int kLdW = kC + 4;                  // own rows: 16-B aligned (broadca
 
 // normalized feature row of pair slot `slot` (side 0: f1 via pairs[.., 0]; side 1: f2 via
 // pairs[.., 1]) and its pre-normalization norm
-__device__ __forceinline__ const float* nce_row_ptr(const float* __restrict__ f, int64_t N, const int64_t* __restrict__ pairs,
-                                                    int cap, const int64_t* __restrict__ rows, int S, int b, int slot,
+struct FeatView {  // f[b, n, c] = base[b * sb + n * sn + c * sc] (rows or channels-first storage)
+  const float* base;
+  int64_t sb, sn, sc;
+};
+
+__device__ __forceinline__ const float* nce_row_ptr(const FeatView& f, const int64_t* __restrict__ pairs, int cap,
+                                                    const int64_t* __restrict__ rows, int S, int b, int slot,
                                                     int side, int64_t* idx_out) {
   const int64_t r = rows[(int64_t)b * S + slot];
   const int64_t idx = pairs[((int64_t)b * cap + r) * 2 + side];
   *idx_out = idx;
-  return f + ((int64_t)b * N + idx) * kC;
+  return f.base + (int64_t)b * f.sb + idx * f.sn;
 }
 
 template <bool COLS>
 __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
-    const float* __restrict__ f1, const float* __restrict__ f2, int64_t N1, int64_t N2,
+    const FeatView f1, const FeatView f2, int64_t N1, int64_t N2,
     const int64_t* __restrict__ pairs, int cap, const int64_t* __restrict__ rows,
     const uint8_t* __restrict__ valid, int S, float inv_t, float* __restrict__ lse,
     float* __restrict__ term, float* __restrict__ loss, float* __restrict__ g_own) {
@@ -65,8 +70,8 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
   const int lane = pk::lane_id(), w = pk::wave_id();
   const uint8_t* __restrict__ vb = valid + (int64_t)b * S;
   // own side: rows pass = queries (f1, pairs[..,0]); column pass = keys (f2, pairs[..,1])
-  const float* __restrict__ f_own = COLS ? f2 : f1;
-  const float* __restrict__ f_oth = COLS ? f1 : f2;
+  const FeatView f_own = COLS ? f2 : f1;
+  const FeatView f_oth = COLS ? f1 : f2;
   const int64_t N_own = COLS ? N2 : N1, N_oth = COLS ? N1 : N2;
   const int side_own = COLS ? 1 : 0;
 
@@ -82,12 +87,9 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
     float ss = 0.f;
     const bool ok = o < S && vb[o] != 0;
     int64_t idx = 0;
-    const float* p = ok ? nce_row_ptr(f_oth, N_oth, pairs, cap, rows, S, b, o, 1 - side_own, &idx) : nullptr;
+    const float* p = ok ? nce_row_ptr(f_oth, pairs, cap, rows, S, b, o, 1 - side_own, &idx) : nullptr;
 #pragma unroll
-    for (int c = 0; c < kC; c += 4) {
-      const float4 q = ok ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      x[c] = q.x; x[c + 1] = q.y; x[c + 2] = q.z; x[c + 3] = q.w;
-    }
+    for (int c = 0; c < kC; ++c) x[c] = ok ? p[c * f_oth.sc] : 0.f;
 #pragma unroll
     for (int c = 0; c < kC; ++c) ss = fmaf(x[c], x[c], ss);
     const float nc = fmaxf(sqrtf(ss), 1e-12f);
@@ -101,12 +103,9 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
     const bool ok = a < S && vb[a] != 0;
     int64_t idx = 0;
     float x[kC];
-    const float* p = ok ? nce_row_ptr(f_own, N_own, pairs, cap, rows, S, b, a, side_own, &idx) : nullptr;
+    const float* p = ok ? nce_row_ptr(f_own, pairs, cap, rows, S, b, a, side_own, &idx) : nullptr;
 #pragma unroll
-    for (int c = 0; c < kC; c += 4) {
-      const float4 q = ok ? *reinterpret_cast<const float4*>(p + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      x[c] = q.x; x[c + 1] = q.y; x[c + 2] = q.z; x[c + 3] = q.w;
-    }
+    for (int c = 0; c < kC; ++c) x[c] = ok ? p[c * f_own.sc] : 0.f;
     float ss = 0.f;
 #pragma unroll
     for (int c = 0; c < kC; ++c) ss = fmaf(x[c], x[c], ss);
@@ -290,7 +289,8 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
 
 }  // namespace
 
-extern "C" int pk_nce_loss(const float* f1, const float* f2, int B, int64_t N1, int64_t N2, int C,
+extern "C" int pk_nce_loss(const float* f1, const int64_t* st1, const float* f2, const int64_t* st2, int B,
+                           int64_t N1, int64_t N2, int C,
                            const int64_t* pairs, int cap, const int64_t* rows, const uint8_t* valid, int S,
                            float nce_t, float* lse, float* term, float* loss, float* g1, float* g2,
                            void* stream) {
@@ -308,10 +308,12 @@ extern "C" int pk_nce_loss(const float* f1, const float* f2, int B, int64_t N1, 
   PK_REQUIRE(f1 && f2 && pairs && rows && valid && lse && term && cap > 0);
   const float inv_t = 1.f / nce_t;
   const dim3 grid((S + kTile - 1) / kTile, B);
-  hipLaunchKernelGGL(nce_pass_kernel<false>, grid, dim3(64 * kWaves), 0, s, f1, f2, N1, N2, pairs, cap, rows, valid,
+  const FeatView v1{f1, st1 ? st1[0] : N1 * kC, st1 ? st1[1] : kC, st1 ? st1[2] : 1};
+  const FeatView v2{f2, st2 ? st2[0] : N2 * kC, st2 ? st2[1] : kC, st2 ? st2[2] : 1};
+  hipLaunchKernelGGL(nce_pass_kernel<false>, grid, dim3(64 * kWaves), 0, s, v1, v2, N1, N2, pairs, cap, rows, valid,
                      S, inv_t, lse, term, loss, g1);
   PK_CHECK_LAUNCH();
-  hipLaunchKernelGGL(nce_pass_kernel<true>, grid, dim3(64 * kWaves), 0, s, f1, f2, N1, N2, pairs, cap, rows, valid,
+  hipLaunchKernelGGL(nce_pass_kernel<true>, grid, dim3(64 * kWaves), 0, s, v1, v2, N1, N2, pairs, cap, rows, valid,
                      S, inv_t, lse, term, loss, g2);
   PK_CHECK_LAUNCH();
   return PK_OK;

@@ -14,6 +14,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from typing import Optional
+
 from . import ops
 
 _SIDE = None  # the active GroupedWgrad (TrainStep's backward), or None
@@ -83,58 +85,61 @@ def _side_owns(weight, bias) -> bool:
     return _SIDE is not None and _SIDE.owns(weight) and (bias is None or _SIDE.owns(bias))
 
 
-class _LinearFn(torch.autograd.Function):
+class _PointwiseFn(torch.autograd.Function):
+    """y = x W^T (+ b) over every point of x in its NATIVE layout: cf=False rows [..., C],
+    cf=True channels-first [B, C, N]. The modules below pick the native layout from the
+    input's strides (a transposed view of a contiguous tensor runs on that tensor), so the
+    reference's transposes (modeling/dpfm.py:90-91, 113-116) cost no copies."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, cf):
+        w2 = weight.view(weight.shape[0], -1)
         ctx.save_for_backward(x, weight)
-        ctx.has_bias = bias is not None
-        ctx.param, ctx.bias = weight, bias  # the Parameter objects (SideWgrad's buffer keys)
+        ctx.has_bias, ctx.cf = bias is not None, cf
+        ctx.param, ctx.bias = weight, bias  # the Parameter objects (GroupedWgrad's buffer keys)
         # a fresh (non-view) output: the reference applies in-place ReLUs to it (:112-116)
-        return ops.linear_fwd(x, weight, bias, channels_first=False)
+        return ops.linear_fwd(x, w2, bias, channels_first=cf)
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
+        w2 = weight.view(weight.shape[0], -1)
+        cf = ctx.cf
+        dy = dy.contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = ops.linear_fwd(dy, weight, None, channels_first=False, transw=True)  # dy W
+            dx = ops.linear_fwd(dy, w2, None, channels_first=cf, transw=True)  # dy W (rows) / W^T dy (cf)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             if _side_owns(ctx.param, ctx.bias):
-                _SIDE.launch(x, dy, ctx.param, ctx.bias, channels_first=False)
+                _SIDE.launch(x, dy, ctx.param, ctx.bias, channels_first=cf)
             else:
-                dw, db = ops.linear_wgrad(x, dy, channels_first=False, want_bias=ctx.has_bias)
-        return dx, dw, db
+                dw, db = ops.linear_wgrad(x, dy, channels_first=cf, want_bias=ctx.has_bias)
+                dw = dw.view(weight.shape)
+        return dx, dw, db, None
 
 
-class _Conv1x1Fn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, weight, bias):
-        ctx.save_for_backward(x, weight)
-        ctx.has_bias = bias is not None
-        ctx.param, ctx.bias = weight, bias  # the Parameter objects (SideWgrad's buffer keys)
-        # y[b] = W x[b] (+ b) over every point, bias fused (no MIOpen convolution)
-        return ops.linear_fwd(x, weight[:, :, 0], bias, channels_first=True)
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = ops.linear_fwd(dy, weight[:, :, 0], None, channels_first=True, transw=True)  # W^T dy
-        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            if _side_owns(ctx.param, ctx.bias):
-                _SIDE.launch(x, dy, ctx.param, ctx.bias, channels_first=True)
-            else:
-                dw, db = ops.linear_wgrad(x, dy, channels_first=True, want_bias=ctx.has_bias)
-                dw = dw[:, :, None]
-        return dx, dw, db
+def _pointwise(x, weight, bias, sem_cf: bool, out_cf: Optional[bool] = None):
+    """Apply the layer to x of semantic layout sem_cf (False: [..., C]; True: [B, C, N]).
+    out_cf: force the output storage layout (None: the native layout of the input)."""
+    if not x.is_cuda:
+        raise ops._lib.PoseKernError("dpfm_amd layers run on HIP devices only (no CPU fallback)")
+    if x.dim() == 3 and not x.is_contiguous() and x.transpose(1, 2).is_contiguous():
+        base, native_cf = x.transpose(1, 2), not sem_cf
+    else:
+        base, native_cf = x.contiguous(), sem_cf
+    y = _PointwiseFn.apply(base, weight, bias, native_cf)
+    if out_cf is not None and out_cf != native_cf and y.dim() == 3:
+        y = y.transpose(1, 2).contiguous().transpose(1, 2)  # same values, other storage order
+    return y if native_cf == sem_cf else y.transpose(1, 2)
 
 
 class Linear(nn.Linear):
+    """nn.Linear over every point; `out_cf = True` stores the [B, N, C] output
+    channels-first (a transposed view of a [B, C, N] tensor) for a channels-first consumer."""
+    out_cf: Optional[bool] = None
+
     def forward(self, x):
-        if not x.is_cuda:
-            raise ops._lib.PoseKernError("dpfm_amd layers run on HIP devices only (no CPU fallback)")
-        return _LinearFn.apply(x, self.weight, self.bias)
+        return _pointwise(x, self.weight, self.bias, sem_cf=False, out_cf=self.out_cf)
 
 
 class Conv1d(nn.Conv1d):
@@ -144,6 +149,4 @@ class Conv1d(nn.Conv1d):
             raise ValueError("only the reference's pointwise Conv1d(kernel_size=1) is supported")
 
     def forward(self, x):
-        if not x.is_cuda:
-            raise ops._lib.PoseKernError("dpfm_amd layers run on HIP devices only (no CPU fallback)")
-        return _Conv1x1Fn.apply(x, self.weight, self.bias)
+        return _pointwise(x, self.weight, self.bias, sem_cf=True)

@@ -88,6 +88,7 @@ class CrossAttentionRefinementNet(nn.Module):
         self.cross_sampling_ratio = cross_sampling_ratio
         self.layers = nn.ModuleList([AttentionalPropagation(gnn_dim + additional_dim, num_head) for _ in range(n_layers)])
         self.first_lin = Linear(n_in, gnn_dim + additional_dim)
+        self.first_lin.out_cf = True  # desc = first_lin(x).transpose(1, 2) is then contiguous
         self.last_lin = Linear(gnn_dim + additional_dim, n_in + additional_dim)
         self.overlap_predictor = OverlapPredictorNet(overlap_feat_dim=overlap_feat_dim)
 

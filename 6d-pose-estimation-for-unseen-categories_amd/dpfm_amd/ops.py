@@ -469,13 +469,19 @@ class _NCELoss(torch.autograd.Function):
         N2 = f2.shape[1]
         S = rows.shape[1]
         dev = f1.device
-        f1c, f2c = f1.detach().contiguous(), f2.detach().contiguous()
+        import ctypes
+        f1c, f2c = f1.detach(), f2.detach()
+        if f1c.stride(-1) != 1 and f1c.stride(1) != 1:  # neither rows nor channels-first storage
+            f1c = f1c.contiguous()
+        if f2c.stride(-1) != 1 and f2c.stride(1) != 1:
+            f2c = f2c.contiguous()
+        st = lambda t: (ctypes.c_int64 * 3)(*t.stride())  # noqa: E731
         lse = torch.empty((B, max(S, 1)), dtype=torch.float32, device=dev)
         term = torch.empty_like(lse)
         loss = torch.empty((B,), dtype=torch.float32, device=dev)
-        g1 = torch.empty_like(f1c) if want else None
-        g2 = torch.empty_like(f2c) if want else None
-        call("pk_nce_loss", ptr(f1c), ptr(f2c), B, int(N1), int(N2), int(C), ptr(pairs), int(pairs.shape[1]),
+        g1 = torch.empty((B, N1, C), dtype=torch.float32, device=dev) if want else None
+        g2 = torch.empty((B, N2, C), dtype=torch.float32, device=dev) if want else None
+        call("pk_nce_loss", ctypes.c_void_p(f1c.data_ptr()), st(f1c), ctypes.c_void_p(f2c.data_ptr()), st(f2c), B, int(N1), int(N2), int(C), ptr(pairs), int(pairs.shape[1]),
              ptr(rows), ptr(valid), int(S), float(nce_t), ptr(lse), ptr(term), ptr(loss), ptr(g1), ptr(g2),
              _lib.stream(dev), work=None)
         ctx.save_for_backward(g1, g2)

@@ -261,13 +261,13 @@ def main():
         crop_fams = {"pk_backproject", "pk_sor", "pk_fps_npoint", "pk_fps", "pk_gather_transform",
                      "pk_ball_query_mask", "pk_ball_query_pairs", "pk_sample_rgb", "pk_erode_mask"}
         train_k = {k: v for k, v in kern.items() if k not in crop_fams} or kern
-        dom = max(train_k.items(), key=lambda kv: kv[1]["total_ms"])
+        dom = max(train_k.items(), key=lambda kv: kv[1]["total_ms"]) if train_k else None
         crop_k = {k: v for k, v in kern.items() if k in crop_fams}
         dom_crop = max(crop_k.items(), key=lambda kv: kv[1]["total_ms"]) if crop_k else None
         kernels = {k: {"avg_ms": round(v["avg_ms"], 4), "launches": v["launches"],
                        "ms_per_step": round(v["total_ms"] / max(probe_steps, 1), 4)}
                    for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"])}
-        roof = roofline_for(dom[0], dom[1])
+        roof = roofline_for(dom[0], dom[1]) if dom is not None else None  # None: --probe-steps 0
         mfma_fams = {k: roofline_for(k, v) for k, v in kern.items() if v["bound"] == "mfma"}
         out = {
             "metric": "RGB-D crops/sec (fwd+bwd), 1024 pts, at 1/2/4/8 MI355X; pose err vs ref",

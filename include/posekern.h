@@ -249,11 +249,14 @@ int pk_nce_select(const int64_t* count, int B, int64_t cap, int num, uint64_t se
  * pairs[b] (int64 [B, cap, 2]: CAD index, crop index) when valid[b,a] (uint8);
  *   q_a = normalize(f1[b, pairs[..,0]]), k_a = normalize(f2[b, pairs[..,1]]),
  *   logits = -cdist(q, k) / nce_t, loss[b] = mean over valid a of CE(logits[a], a)
- * (0 for a crop without valid slots). f1 f32 [B, N1, C], f2 f32 [B, N2, C], C = 32,
+ * (0 for a crop without valid slots). f1 f32 [B, N1, C], f2 f32 [B, N2, C], C = 32, element
+ * strides st1 / st2 = HOST int64[3] {batch, point, channel} (NULL: contiguous rows), so a
+ * channels-first [B, C, N] storage is read in place;
  * S <= 512. lse / term f32 [B, S] scratch. g1 / g2 (both or neither) f32 [B, N1|N2, C]
  * receive d loss[b] / d f1[b], f2[b] (zero-filled, then accumulated with f32 atomics,
  * as torch's gather backward). */
-int pk_nce_loss(const float* f1, const float* f2, int B, int64_t N1, int64_t N2, int C, const int64_t* pairs,
+int pk_nce_loss(const float* f1, const int64_t* st1, const float* f2, const int64_t* st2, int B, int64_t N1,
+                int64_t N2, int C, const int64_t* pairs,
                 int cap, const int64_t* rows, const uint8_t* valid, int S, float nce_t, float* lse, float* term,
                 float* loss, float* g1, float* g2, void* stream);
 int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs, const float* evecs1, int ld1,

@@ -328,6 +328,14 @@ def test_nce_loss_edge_cases(device):
     with torch.no_grad():
         l2 = ops.nce_loss(f1, f2, pairs.to(device), rows, valid, 0.07)
     assert torch.equal(loss.detach(), l2)
+    # channels-first storage (the refinement net's ref_feat layout) is read in place
+    cf = lambda t: t.detach().transpose(1, 2).contiguous().transpose(1, 2).requires_grad_(True)  # noqa: E731
+    f1c, f2c = cf(f1), cf(f2)
+    assert not f1c.is_contiguous()
+    l3 = ops.nce_loss(f1c, f2c, pairs.to(device), rows, valid, 0.07)
+    l3.sum().backward()
+    assert torch.equal(loss.detach(), l3.detach())
+    assert torch.allclose(f1c.grad, f1.grad, rtol=0, atol=1e-7) and torch.allclose(f2c.grad, f2.grad, rtol=0, atol=1e-7)
     for b in (1, 2):
         s = rows[b][valid[b]].cpu()
         r = M.nce_loss(f1[b].detach().cpu().double(), f2[b].detach().cpu().double(), pairs[b, :int(counts[b])], s)

@@ -1,0 +1,42 @@
+"""Summarise a rocprofv3 kernel trace of bench.py's replayed steps: busy time per queue,
+idle gaps, and the top kernels by total time over the last 10 steps' window."""
+import csv, sys, collections
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+# the timed window: the last `steps` steps (bench.py's ms_per_step from its JSON line)
+import json, re
+bench = next(json.loads(l) for l in reversed(open(sys.argv[2]).read().splitlines()) if l.startswith('{"metric"'))
+steps = int(bench["steps"])
+t1 = max(int(r["End_Timestamp"]) for r in rows)
+lo = t1 - int(steps * bench["ms_per_step"] * 1e6)
+print(f"ms_per_step {bench['ms_per_step']} x {steps}")
+win = [r for r in rows if int(r["Start_Timestamp"]) >= lo]
+span = (int(win[-1]["End_Timestamp"]) - int(win[0]["Start_Timestamp"])) / 1e6
+byq = collections.defaultdict(list)
+for r in win:
+    byq[r.get("Queue_Id", r.get("Stream_Id", "?"))].append(r)
+print(f"window {span:.3f} ms, {len(win)} kernels ({len(win)/steps:.0f} per step)")
+for q, rs in byq.items():
+    busy = 0
+    end = None
+    gaps = []
+    for r in rs:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if end is not None and s > end:
+            gaps.append(s - end)
+        busy += e - s
+        end = max(end or 0, e)
+    print(f"queue {q}: {len(rs)/steps:.0f} kernels/step, busy {busy/1e6/steps:.3f} ms/step, gaps {sum(gaps)/1e6/steps:.3f} ms/step, "
+          f"mean gap {sum(gaps)/max(len(gaps),1)/1e3:.2f} us")
+tot = collections.defaultdict(lambda: [0, 0])
+for r in win:
+    n = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+    if n.startswith("at::native"):  # keep the functor: which elementwise op
+        m = re.findall(r"at::native::(?:\(anonymous namespace\)::)?([A-Za-z_]+(?:Functor[A-Za-z_]*)?|[a-z_]+_kernel[a-z_]*)", r["Kernel_Name"])
+        n = "/".join(dict.fromkeys(m[:4]))[:110]
+    else:
+        n = re.split(r"[(<]", n)[0][:90]
+    tot[n][0] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    tot[n][1] += 1
+for n, (t, c) in sorted(tot.items(), key=lambda kv: -kv[1][0])[:45]:
+    print(f"{t/1e3/steps:8.1f} us/step {c/steps:6.1f}/step  {n}")
