@@ -1,0 +1,170 @@
+// H8 refinement MLP's InstanceNorm1d(C) + ReLU (modeling/dpfm.py:16-26: Conv1d -> InstanceNorm1d
+// (affine=False, eps 1e-5, statistics over all N points of a crop, padding included) -> ReLU),
+// forward and backward fused: one wave per (crop, channel) row of the channels-first
+// [B, C, N] activation. torch runs batch_norm_collect_statistics + transform + threshold
+// forward and threshold_backward + batch_norm_backward (+ its reductions) backward.
+//   forward   mean = sum x / N, var = sum (x - mean)^2 / N (biased, two passes over the row
+//             held in registers), invstd = 1 / sqrt(var + eps), y = max((x - mean) invstd, 0)
+//   backward  g = dy [xhat > 0], dx = invstd (g - mean(g) - xhat mean(g xhat))
+#include "common.hpp"
+
+namespace {
+
+constexpr int kMaxPerLane = 32;  // N <= 2048 held in registers (64 lanes x 32)
+
+template <int PER>
+__global__ __launch_bounds__(256) void instnorm_relu_fwd_kernel(const float* __restrict__ x, int64_t rows, int N,
+                                                                float eps, float* __restrict__ y,
+                                                                float* __restrict__ mean_out,
+                                                                float* __restrict__ invstd_out) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + pk::wave_id();
+  if (r >= rows) return;
+  const int lane = pk::lane_id();
+  const float* __restrict__ xr = x + r * N;
+  float v[PER];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int n = lane + 64 * k;
+    v[k] = n < N ? xr[n] : 0.f;
+    s += v[k];
+  }
+  const float mean = pk::wave_sum_f32(s) / (float)N;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int n = lane + 64 * k;
+    const float d = v[k] - mean;
+    q += n < N ? d * d : 0.f;
+  }
+  const float var = pk::wave_sum_f32(q) / (float)N;
+  const float invstd = 1.f / sqrtf(var + eps);
+  float* __restrict__ yr = y + r * N;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int n = lane + 64 * k;
+    if (n < N) yr[n] = fmaxf((v[k] - mean) * invstd, 0.f);
+  }
+  if (lane == 0) {
+    mean_out[r] = mean;
+    invstd_out[r] = invstd;
+  }
+}
+
+template <int PER>
+__global__ __launch_bounds__(256) void instnorm_relu_bwd_kernel(const float* __restrict__ x,
+                                                                const float* __restrict__ dy,
+                                                                const float* __restrict__ mean_in,
+                                                                const float* __restrict__ invstd_in, int64_t rows,
+                                                                int N, float* __restrict__ dx) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + pk::wave_id();
+  if (r >= rows) return;
+  const int lane = pk::lane_id();
+  const float mean = mean_in[r], invstd = invstd_in[r];
+  const float* __restrict__ xr = x + r * N;
+  const float* __restrict__ gr = dy + r * N;
+  float xh[PER], g[PER];
+  float sg = 0.f, sgx = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int n = lane + 64 * k;
+    const float xv = n < N ? xr[n] : 0.f;
+    const float gv = n < N ? gr[n] : 0.f;
+    xh[k] = (xv - mean) * invstd;
+    g[k] = xh[k] > 0.f ? gv : 0.f;  // ReLU backward on the normalized value (= the output)
+    sg += g[k];
+    sgx += g[k] * xh[k];
+  }
+  const float mg = pk::wave_sum_f32(sg) / (float)N;
+  const float mgx = pk::wave_sum_f32(sgx) / (float)N;
+  float* __restrict__ dr = dx + r * N;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int n = lane + 64 * k;
+    if (n < N) dr[n] = invstd * ((g[k] - mg) - xh[k] * mgx);
+  }
+}
+
+// rows longer than the register tile (N > 2048, e.g. 4096-point crops): the same arithmetic
+// re-reading the row from memory (L2-resident) for each pass
+__global__ __launch_bounds__(256) void instnorm_relu_fwd_long_kernel(const float* __restrict__ x, int64_t rows, int N,
+                                                                     float eps, float* __restrict__ y,
+                                                                     float* __restrict__ mean_out,
+                                                                     float* __restrict__ invstd_out) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + pk::wave_id();
+  if (r >= rows) return;
+  const int lane = pk::lane_id();
+  const float* __restrict__ xr = x + r * N;
+  float s = 0.f;
+  for (int n = lane; n < N; n += 64) s += xr[n];
+  const float mean = pk::wave_sum_f32(s) / (float)N;
+  float q = 0.f;
+  for (int n = lane; n < N; n += 64) {
+    const float d = xr[n] - mean;
+    q += d * d;
+  }
+  const float invstd = 1.f / sqrtf(pk::wave_sum_f32(q) / (float)N + eps);
+  for (int n = lane; n < N; n += 64) y[r * N + n] = fmaxf((xr[n] - mean) * invstd, 0.f);
+  if (lane == 0) {
+    mean_out[r] = mean;
+    invstd_out[r] = invstd;
+  }
+}
+
+__global__ __launch_bounds__(256) void instnorm_relu_bwd_long_kernel(const float* __restrict__ x,
+                                                                     const float* __restrict__ dy,
+                                                                     const float* __restrict__ mean_in,
+                                                                     const float* __restrict__ invstd_in,
+                                                                     int64_t rows, int N, float* __restrict__ dx) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + pk::wave_id();
+  if (r >= rows) return;
+  const int lane = pk::lane_id();
+  const float mean = mean_in[r], invstd = invstd_in[r];
+  const float* __restrict__ xr = x + r * N;
+  const float* __restrict__ gr = dy + r * N;
+  float sg = 0.f, sgx = 0.f;
+  for (int n = lane; n < N; n += 64) {
+    const float xh = (xr[n] - mean) * invstd;
+    const float g = xh > 0.f ? gr[n] : 0.f;
+    sg += g;
+    sgx += g * xh;
+  }
+  const float mg = pk::wave_sum_f32(sg) / (float)N, mgx = pk::wave_sum_f32(sgx) / (float)N;
+  for (int n = lane; n < N; n += 64) {
+    const float xh = (xr[n] - mean) * invstd;
+    const float g = xh > 0.f ? gr[n] : 0.f;
+    dx[r * N + n] = invstd * ((g - mg) - xh * mgx);
+  }
+}
+
+}  // namespace
+
+extern "C" int pk_instnorm_relu_fwd(const float* x, int64_t rows, int N, float eps, float* y, float* mean,
+                                    float* invstd, void* stream) {
+  PK_REQUIRE(rows >= 0 && N > 0);
+  if (rows == 0) return PK_OK;
+  PK_REQUIRE(x && y && mean && invstd);
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t s = pk::as_stream(stream);
+  if (N <= 512) hipLaunchKernelGGL(instnorm_relu_fwd_kernel<8>, grid, dim3(256), 0, s, x, rows, N, eps, y, mean, invstd);
+  else if (N <= 1024) hipLaunchKernelGGL(instnorm_relu_fwd_kernel<16>, grid, dim3(256), 0, s, x, rows, N, eps, y, mean, invstd);
+  else if (N <= 2048) hipLaunchKernelGGL(instnorm_relu_fwd_kernel<32>, grid, dim3(256), 0, s, x, rows, N, eps, y, mean, invstd);
+  else hipLaunchKernelGGL(instnorm_relu_fwd_long_kernel, grid, dim3(256), 0, s, x, rows, N, eps, y, mean, invstd);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_instnorm_relu_bwd(const float* x, const float* dy, const float* mean, const float* invstd,
+                                    int64_t rows, int N, float* dx, void* stream) {
+  PK_REQUIRE(rows >= 0 && N > 0);
+  if (rows == 0) return PK_OK;
+  PK_REQUIRE(x && dy && mean && invstd && dx);
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t s = pk::as_stream(stream);
+  if (N <= 512) hipLaunchKernelGGL(instnorm_relu_bwd_kernel<8>, grid, dim3(256), 0, s, x, dy, mean, invstd, rows, N, dx);
+  else if (N <= 1024) hipLaunchKernelGGL(instnorm_relu_bwd_kernel<16>, grid, dim3(256), 0, s, x, dy, mean, invstd, rows, N, dx);
+  else if (N <= 2048) hipLaunchKernelGGL(instnorm_relu_bwd_kernel<32>, grid, dim3(256), 0, s, x, dy, mean, invstd, rows, N, dx);
+  else hipLaunchKernelGGL(instnorm_relu_bwd_long_kernel, grid, dim3(256), 0, s, x, dy, mean, invstd, rows, N, dx);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}

@@ -21,6 +21,18 @@ from ..layers import Conv1d, Linear
 from ..dpfm_utils import get_mask_batched
 
 
+class InstanceNormReLU(nn.InstanceNorm1d):
+    """nn.InstanceNorm1d(C) (affine=False, no running stats: no parameters or buffers, so
+    state_dict keys are unchanged) followed by the ReLU of the next Sequential slot, fused in
+    one HIP kernel per direction (ops.instnorm_relu); the slot after it holds an Identity so
+    the Sequential's indices (mlp.0 / mlp.3) match the reference's."""
+
+    def forward(self, x):
+        if self.affine or self.track_running_stats:
+            raise ValueError("the reference's InstanceNorm1d is affine=False, track_running_stats=False")
+        return ops.instnorm_relu(x, self.eps)
+
+
 def MLP(channels: list, do_bn=True):
     """Multi-layer perceptron of 1x1 convolutions (modeling/dpfm.py:16-26)."""
     n = len(channels)
@@ -29,8 +41,10 @@ def MLP(channels: list, do_bn=True):
         layers.append(Conv1d(channels[i - 1], channels[i], kernel_size=1, bias=True))
         if i < (n - 1):
             if do_bn:
-                layers.append(nn.InstanceNorm1d(channels[i]))
-            layers.append(nn.ReLU())
+                layers.append(InstanceNormReLU(channels[i]))
+                layers.append(nn.Identity())  # the ReLU, applied inside InstanceNormReLU
+            else:
+                layers.append(nn.ReLU())
     return nn.Sequential(*layers)
 
 

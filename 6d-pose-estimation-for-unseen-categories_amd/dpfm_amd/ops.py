@@ -404,6 +404,37 @@ def clip_rmsprop(params, grads, square_avg, steps, max_norm: float, lr: float, a
          ptr(norm_out), _lib.stream(dev), work=None)
 
 
+class _InstNormReLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, eps):
+        B, C, N = x.shape
+        y = torch.empty_like(x)
+        mean = torch.empty((B * C,), dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        call("pk_instnorm_relu_fwd", ptr(x), B * C, N, float(eps), ptr(y), ptr(mean), ptr(invstd),
+             _lib.stream(x.device), work=("hbm", 8 * B * C * N))
+        ctx.save_for_backward(x, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, invstd = ctx.saved_tensors
+        B, C, N = x.shape
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        call("pk_instnorm_relu_bwd", ptr(x), ptr(dy), ptr(mean), ptr(invstd), B * C, N, ptr(dx),
+             _lib.stream(x.device), work=("hbm", 12 * B * C * N))
+        return dx, None
+
+
+def instnorm_relu(x: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    """relu(InstanceNorm1d(C, affine=False, eps)(x)) for channels-first f32 x [B, C, N], fused
+    forward and backward (pk_instnorm_relu_fwd/_bwd)."""
+    if x.dim() != 3 or x.dtype != torch.float32:
+        raise _lib.PoseKernError("instnorm_relu takes f32 [B, C, N]")
+    return _InstNormReLU.apply(x.contiguous(), eps)
+
+
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], channels_first: bool,
                transw: bool = False, relu: bool = False) -> torch.Tensor:
     """pk_linear_fwd: y = x W^T (+ b) over every point (W [Cout, Cin], or W^T read from a

@@ -189,6 +189,15 @@ int pk_clip_rmsprop(float* const* params, float* const* grads, float* const* squ
                     const int64_t* numel, int n, float max_norm, float lr, float alpha, float one_minus_alpha,
                     float eps, float* work, float* norm_out, void* stream);
 
+/* H8 refinement MLP's InstanceNorm1d(C, affine=False, eps) + ReLU (modeling/dpfm.py:16-26),
+ * fused, on a channels-first activation viewed as rows = B*C rows of N points:
+ *   fwd: y = max((x - mean) * invstd, 0) per row (biased variance), mean / invstd f32 [rows]
+ *   bwd: dx from dy (the gradient of y), x and the saved mean / invstd. */
+int pk_instnorm_relu_fwd(const float* x, int64_t rows, int N, float eps, float* y, float* mean, float* invstd,
+                         void* stream);
+int pk_instnorm_relu_bwd(const float* x, const float* dy, const float* mean, const float* invstd, int64_t rows,
+                         int N, float* dx, void* stream);
+
 /* Forward / input gradient of the same per-point layers (nn.Linear at models/dpfm.py:22-30
  * and modeling/dpfm.py:16-26,90-91,113-116; Conv1d(k=1) at modeling/dpfm.py:16-26,49-50):
  *   y = x W^T (+ bias) (ReLU if relu), W f32 [Cout, Cin]; with transw = 1 the weight is
