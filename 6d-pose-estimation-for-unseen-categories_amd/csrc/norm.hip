@@ -168,3 +168,66 @@ extern "C" int pk_instnorm_relu_bwd(const float* x, const float* dy, const float
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
+
+// ---------------------------------------------------------------------------------
+// H15 overlap term: upstream DPFM WeightedBCELoss per crop (restated in oracle/
+// dpfm_model_oracle.py::weighted_bce; called from utils/loss.py:79-83), loss and gradient
+// in one pass, one workgroup per (crop, tensor):
+//   wn = sum_n t_n / N;  w_n = t_n >= 0.5 ? 1 - wn : wn
+//   bce_n = (t_n - 1) max(log1p(-p_n), -100) - t_n max(log p_n, -100)   (ATen's formula)
+//   loss = sum_n w_n bce_n / N;  dloss/dp_n = w_n (p_n - t_n) / max(p_n (1 - p_n), 1e-12) / N
+// Sums in a fixed order (deterministic).
+namespace {
+
+constexpr int kBceThreads = 256;
+
+__device__ __forceinline__ float block_sum_f32(float v, float* red) {
+  v = pk::wave_sum_f32(v);
+  __syncthreads();
+  if (pk::lane_id() == 0) red[pk::wave_id()] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int w = 0; w < kBceThreads / 64; ++w) s += red[w];
+  return s;
+}
+
+__global__ __launch_bounds__(kBceThreads) void wbce_kernel(const float* __restrict__ p0, const int8_t* __restrict__ t0,
+                                                           int N0, const float* __restrict__ p1,
+                                                           const int8_t* __restrict__ t1, int N1, int B,
+                                                           float* __restrict__ loss, float* __restrict__ g0,
+                                                           float* __restrict__ g1) {
+  __shared__ float red[kBceThreads / 64];
+  const int b = blockIdx.x % B, which = blockIdx.x / B;
+  const int N = which ? N1 : N0;
+  const float* __restrict__ p = (which ? p1 : p0) + (int64_t)b * N;
+  const int8_t* __restrict__ t = (which ? t1 : t0) + (int64_t)b * N;
+  float* __restrict__ g = g0 ? (which ? g1 : g0) + (int64_t)b * N : nullptr;
+  float st = 0.f;
+  for (int n = threadIdx.x; n < N; n += kBceThreads) st += (float)t[n];
+  const float wn = block_sum_f32(st, red) / (float)N;
+  float sl = 0.f;
+  const float invN = 1.f / (float)N;
+  for (int n = threadIdx.x; n < N; n += kBceThreads) {
+    const float pv = p[n], tv = (float)t[n];
+    const float w = tv >= 0.5f ? 1.f - wn : wn;
+    const float l = (tv - 1.f) * fmaxf(log1pf(-pv), -100.f) - tv * fmaxf(logf(pv), -100.f);
+    sl += w * l;
+    if (g) g[n] = w * invN * ((pv - tv) / fmaxf((1.f - pv) * pv, 1e-12f));
+  }
+  const float s = block_sum_f32(sl, red);
+  if (threadIdx.x == 0) loss[which * B + b] = s * invN;
+}
+
+}  // namespace
+
+extern "C" int pk_wbce(const float* p12, const int8_t* t12, int N1, const float* p21, const int8_t* t21, int N2,
+                       int B, float* loss, float* g12, float* g21, void* stream) {
+  PK_REQUIRE(B >= 0 && N1 > 0 && N2 > 0 && (g12 == nullptr) == (g21 == nullptr));
+  if (B == 0) return PK_OK;
+  PK_REQUIRE(p12 && t12 && p21 && t21 && loss);
+  hipLaunchKernelGGL(wbce_kernel, dim3(2 * B), dim3(kBceThreads), 0, pk::as_stream(stream), p12, t12, N1, p21, t21,
+                     N2, B, loss, g12, g21);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}

@@ -435,6 +435,34 @@ def instnorm_relu(x: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
     return _InstNormReLU.apply(x.contiguous(), eps)
 
 
+class _WBCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, p12, p21, t12, t21, want):
+        B, N1 = p12.shape
+        N2 = p21.shape[1]
+        loss = torch.empty((2, B), dtype=torch.float32, device=p12.device)
+        g12 = torch.empty_like(p12) if want else None
+        g21 = torch.empty_like(p21) if want else None
+        call("pk_wbce", ptr(p12), ptr(t12), N1, ptr(p21), ptr(t21), N2, B, ptr(loss), ptr(g12), ptr(g21),
+             _lib.stream(p12.device), work=None)
+        ctx.save_for_backward(g12, g21)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        g12, g21 = ctx.saved_tensors
+        return g12 * gl[0][:, None], g21 * gl[1][:, None], None, None, None
+
+
+def weighted_bce_pair(p12: torch.Tensor, p21: torch.Tensor, t12: torch.Tensor, t21: torch.Tensor) -> torch.Tensor:
+    """Upstream WeightedBCELoss for both overlap directions of every crop (pk_wbce): p f32
+    [B, N], t 0/1 masks [B, N] -> loss f32 [2, B] (row 0: p12, row 1: p21)."""
+    def mask(t):
+        return (t if t.dtype == torch.int8 else (t >= 0.5).to(torch.int8)).contiguous()
+    want = torch.is_grad_enabled() and (p12.requires_grad or p21.requires_grad)
+    return _WBCE.apply(p12.contiguous(), p21.contiguous(), mask(t12), mask(t21), want)
+
+
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], channels_first: bool,
                transw: bool = False, relu: bool = False) -> torch.Tensor:
     """pk_linear_fwd: y = x W^T (+ b) over every point (W [Cout, Cin], or W^T read from a

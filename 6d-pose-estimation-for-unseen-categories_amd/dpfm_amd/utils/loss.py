@@ -42,12 +42,16 @@ class NCESoftmaxLoss(nn.Module):
         self.nce_num_pairs = nce_num_pairs
 
     def forward_batched(self, f1, f2, pairs, rows, valid):
-        """Per-crop NCE loss [B]: pairs [B, cap, 2], rows/valid from nce_select. On HIP
-        devices one fused kernel pair (ops.nce_loss); the torch composition below is the
-        host-side restatement kept for CPU tensors (the gloo multi-process tests)."""
-        if f1.is_cuda:
-            from .. import ops
-            return ops.nce_loss(f1, f2, pairs, rows, valid, self.nce_t)
+        """Per-crop NCE loss [B]: pairs [B, cap, 2], rows/valid from nce_select; one fused
+        kernel pair (ops.nce_loss)."""
+        from .. import ops
+        if not f1.is_cuda:
+            raise ops._lib.PoseKernError("NCESoftmaxLoss runs on HIP devices only (no CPU fallback)")
+        return ops.nce_loss(f1, f2, pairs, rows, valid, self.nce_t)
+
+    def forward_batched_torch(self, f1, f2, pairs, rows, valid):
+        """The same per-crop NCE loss composed of torch ops (development comparison only;
+        the training step uses the fused kernel above)."""
         f1n, f2n = F.normalize(f1, p=2, dim=-1), F.normalize(f2, p=2, dim=-1)
         sel = torch.gather(pairs, 1, rows[..., None].expand(-1, -1, 2))
         # rows past a crop's pair count select unwritten slots of the pair buffer: point
@@ -116,8 +120,11 @@ class DPFMLoss(nn.Module):
             npairs, pairs.shape[1], self.nce_softmax_loss.nce_num_pairs, generator)
         nce = self.nce_softmax_loss.forward_batched(feat1, feat2, pairs, rows, valid)
         nce_loss = (nce * self.w_nce / m).sum()
-        acc_loss = ((weighted_bce_batched(o12, gt12.float()) + weighted_bce_batched(o21, gt21.float()))
-                    * self.w_acc / m).sum()
+        from .. import ops
+        if not o12.is_cuda:
+            raise ops._lib.PoseKernError("DPFMLoss runs on HIP devices only (no CPU fallback)")
+        wb = ops.weighted_bce_pair(o12, o21, gt12, gt21)  # both directions, loss + gradient, one launch
+        acc_loss = ((wb[0] + wb[1]) * self.w_acc / m).sum()
         loss = fmap_loss + acc_loss + nce_loss
         return loss, {"nce_loss": nce_loss.detach(), "acc_loss": acc_loss.detach(),
                       "fmap_loss": fmap_loss.detach(), "loss": loss.detach()}

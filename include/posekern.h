@@ -198,6 +198,13 @@ int pk_instnorm_relu_fwd(const float* x, int64_t rows, int N, float eps, float* 
 int pk_instnorm_relu_bwd(const float* x, const float* dy, const float* mean, const float* invstd, int64_t rows,
                          int N, float* dx, void* stream);
 
+/* H15 overlap term: upstream WeightedBCELoss (utils/loss.py:79-83) for both directions of
+ * B crops in one launch. p12 f32 [B, N1] / p21 [B, N2] sigmoid outputs, t12 / t21 int8 0/1
+ * masks; loss f32 [2, B] (row 0: 12, row 1: 21); g12 / g21 (both or neither) receive
+ * d loss[., b] / d p. */
+int pk_wbce(const float* p12, const int8_t* t12, int N1, const float* p21, const int8_t* t21, int N2, int B,
+            float* loss, float* g12, float* g21, void* stream);
+
 /* Forward / input gradient of the same per-point layers (nn.Linear at models/dpfm.py:22-30
  * and modeling/dpfm.py:16-26,90-91,113-116; Conv1d(k=1) at modeling/dpfm.py:16-26,49-50):
  *   y = x W^T (+ bias) (ReLU if relu), W f32 [Cout, Cin]; with transw = 1 the weight is
