@@ -231,3 +231,75 @@ extern "C" int pk_wbce(const float* p12, const int8_t* t12, int N1, const float*
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
+
+// ---------------------------------------------------------------------------------
+// F.normalize(x, p=2, dim=-1, eps=1e-12) over the channel dim of [B, N, C] features stored
+// rows or channels-first (the overlap head's input, modeling/dpfm.py:140-145), forward and
+// backward: one thread per point, element (b, n, c) at b * sb + n * sn + c * sc (the output
+// and gradients use the same strides as the input).
+//   y = x / max(||x||, eps);  dx = (dy - y (y . dy)) / ||x||  (dy / eps where clamped)
+namespace {
+
+struct L2View {
+  int64_t sb, sn, sc;
+};
+
+__global__ __launch_bounds__(256) void l2norm_fwd_kernel(const float* __restrict__ x, L2View v, int B, int N, int C,
+                                                         float* __restrict__ y, float* __restrict__ nrm) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)B * N) return;
+  const int64_t b = i / N, n = i - b * N;
+  const int64_t o = b * v.sb + n * v.sn;
+  float s = 0.f;
+  for (int c = 0; c < C; ++c) {
+    const float a = x[o + c * v.sc];
+    s += a * a;
+  }
+  const float nr = sqrtf(s);
+  const float d = fmaxf(nr, 1e-12f);
+  for (int c = 0; c < C; ++c) y[o + c * v.sc] = x[o + c * v.sc] / d;
+  nrm[i] = nr;
+}
+
+__global__ __launch_bounds__(256) void l2norm_bwd_kernel(const float* __restrict__ y, const float* __restrict__ dy,
+                                                         const float* __restrict__ nrm, L2View v, int B, int N, int C,
+                                                         float* __restrict__ dx) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)B * N) return;
+  const int64_t b = i / N, n = i - b * N;
+  const int64_t o = b * v.sb + n * v.sn;
+  const float nr = nrm[i];
+  float yd = 0.f;
+  for (int c = 0; c < C; ++c) yd += y[o + c * v.sc] * dy[o + c * v.sc];
+  if (nr > 1e-12f) {
+    for (int c = 0; c < C; ++c) dx[o + c * v.sc] = (dy[o + c * v.sc] - y[o + c * v.sc] * yd) / nr;
+  } else {
+    for (int c = 0; c < C; ++c) dx[o + c * v.sc] = dy[o + c * v.sc] / 1e-12f;
+  }
+}
+
+}  // namespace
+
+extern "C" int pk_l2_normalize_fwd(const float* x, const int64_t* strides, int B, int N, int C, float* y, float* nrm,
+                                   void* stream) {
+  PK_REQUIRE(B >= 0 && N >= 0 && C > 0 && strides);
+  if ((int64_t)B * N == 0) return PK_OK;
+  PK_REQUIRE(x && y && nrm);
+  const L2View v{strides[0], strides[1], strides[2]};
+  hipLaunchKernelGGL(l2norm_fwd_kernel, dim3((unsigned)(((int64_t)B * N + 255) / 256)), dim3(256), 0,
+                     pk::as_stream(stream), x, v, B, N, C, y, nrm);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_l2_normalize_bwd(const float* y, const float* dy, const float* nrm, const int64_t* strides, int B,
+                                   int N, int C, float* dx, void* stream) {
+  PK_REQUIRE(B >= 0 && N >= 0 && C > 0 && strides);
+  if ((int64_t)B * N == 0) return PK_OK;
+  PK_REQUIRE(y && dy && nrm && dx);
+  const L2View v{strides[0], strides[1], strides[2]};
+  hipLaunchKernelGGL(l2norm_bwd_kernel, dim3((unsigned)(((int64_t)B * N + 255) / 256)), dim3(256), 0,
+                     pk::as_stream(stream), y, dy, nrm, v, B, N, C, dx);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}

@@ -132,8 +132,9 @@ class OverlapPredictorNet(nn.Module):
         )
 
     def forward(self, overlap_feat_x, overlap_feat_y):
-        nx = F.normalize(overlap_feat_x, p=2, dim=-1)
-        ny = F.normalize(overlap_feat_y, p=2, dim=-1)
+        # F.normalize(., p=2, dim=-1) (modeling/dpfm.py:140-141), fused, storage order kept
+        nx = ops.l2_normalize(overlap_feat_x) if overlap_feat_x.dim() == 3 else F.normalize(overlap_feat_x, p=2, dim=-1)
+        ny = ops.l2_normalize(overlap_feat_y) if overlap_feat_y.dim() == 3 else F.normalize(overlap_feat_y, p=2, dim=-1)
         sx = self.overlap_score_net(nx).squeeze(2).squeeze(0)
         sy = self.overlap_score_net(ny).squeeze(2).squeeze(0)
         return sx, sy

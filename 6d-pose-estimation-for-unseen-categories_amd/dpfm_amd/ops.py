@@ -463,6 +463,56 @@ def weighted_bce_pair(p12: torch.Tensor, p21: torch.Tensor, t12: torch.Tensor, t
     return _WBCE.apply(p12.contiguous(), p21.contiguous(), mask(t12), mask(t21), want)
 
 
+def _l2_layout(x: torch.Tensor):
+    """(tensor, strides) with unit stride on the channel or the point dim (copy otherwise)."""
+    import ctypes
+    if x.stride(-1) != 1 and x.stride(1) != 1:
+        x = x.contiguous()
+    return x, (ctypes.c_int64 * 3)(*x.stride())
+
+
+class _L2Normalize(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        B, N, C = x.shape
+        y = torch.empty_strided(x.shape, x.stride(), dtype=x.dtype, device=x.device)
+        nrm = torch.empty((B * N,), dtype=torch.float32, device=x.device)
+        _, st = _l2_layout(x)
+        call("pk_l2_normalize_fwd", ctypes_ptr(x), st, B, N, C, ctypes_ptr(y), ptr(nrm), _lib.stream(x.device),
+             work=("hbm", 8 * B * N * C))
+        ctx.save_for_backward(y, nrm)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, nrm = ctx.saved_tensors
+        B, N, C = y.shape
+        if dy.stride() != y.stride():
+            dy = torch.empty_strided(y.shape, y.stride(), dtype=dy.dtype, device=dy.device).copy_(dy)
+        dx = torch.empty_strided(y.shape, y.stride(), dtype=y.dtype, device=y.device)
+        _, st = _l2_layout(y)
+        call("pk_l2_normalize_bwd", ctypes_ptr(y), ctypes_ptr(dy), ptr(nrm), st, B, N, C, ctypes_ptr(dx),
+             _lib.stream(y.device), work=("hbm", 12 * B * N * C))
+        return dx
+
+
+def ctypes_ptr(t: torch.Tensor):
+    """Device pointer of a (possibly non-contiguous, strides passed separately) tensor."""
+    import ctypes
+    if not t.is_cuda:
+        raise _lib.PoseKernError("posekern ops take HIP device tensors only (no CPU fallback)")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def l2_normalize(x: torch.Tensor) -> torch.Tensor:
+    """F.normalize(x, p=2, dim=-1) for f32 [B, N, C] in rows or channels-first storage, fused
+    forward and backward (pk_l2_normalize_fwd/_bwd); the output keeps x's storage order."""
+    if x.dim() != 3 or x.dtype != torch.float32:
+        raise _lib.PoseKernError("l2_normalize takes f32 [B, N, C]")
+    x, _ = _l2_layout(x)
+    return _L2Normalize.apply(x)
+
+
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], channels_first: bool,
                transw: bool = False, relu: bool = False) -> torch.Tensor:
     """pk_linear_fwd: y = x W^T (+ b) over every point (W [Cout, Cin], or W^T read from a

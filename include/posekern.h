@@ -205,6 +205,15 @@ int pk_instnorm_relu_bwd(const float* x, const float* dy, const float* mean, con
 int pk_wbce(const float* p12, const int8_t* t12, int N1, const float* p21, const int8_t* t21, int N2, int B,
             float* loss, float* g12, float* g21, void* stream);
 
+/* F.normalize(x, p=2, dim=-1) over the C channels of [B, N, C] features (overlap head,
+ * modeling/dpfm.py:140-145), forward and backward. strides = HOST int64[3] element strides
+ * {batch, point, channel} shared by x / y / dy / dx (rows or channels-first storage);
+ * nrm f32 [B * N] = ||x|| per point (saved by the forward for the backward). */
+int pk_l2_normalize_fwd(const float* x, const int64_t* strides, int B, int N, int C, float* y, float* nrm,
+                        void* stream);
+int pk_l2_normalize_bwd(const float* y, const float* dy, const float* nrm, const int64_t* strides, int B, int N,
+                        int C, float* dx, void* stream);
+
 /* Forward / input gradient of the same per-point layers (nn.Linear at models/dpfm.py:22-30
  * and modeling/dpfm.py:16-26,90-91,113-116; Conv1d(k=1) at modeling/dpfm.py:16-26,49-50):
  *   y = x W^T (+ bias) (ReLU if relu), W f32 [Cout, Cin]; with transw = 1 the weight is

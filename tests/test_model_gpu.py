@@ -358,3 +358,27 @@ def test_instnorm_relu_fwd_bwd(device, B, C, N):
     yd.backward(dy.to(device))
     assert (yd.detach().cpu().double() - yr.detach()).abs().max().item() <= 1e-5 * yr.abs().max().item()
     assert (xd.grad.cpu().double() - xr.grad).abs().max().item() <= 1e-5 * xr.grad.abs().max().item()
+
+
+@pytest.mark.parametrize("cf", [False, True])
+def test_l2_normalize_fwd_bwd(device, cf):
+    """Fused F.normalize(x, p=2, dim=-1) (overlap head, modeling/dpfm.py:140-141) vs torch in
+    fp64, rows and channels-first storage, including an all-zero point (the eps clamp)."""
+    from dpfm_amd import ops
+    g = torch.Generator().manual_seed(3 + cf)
+    x = torch.randn(3, 257, 32, generator=g)
+    x[1, 7] = 0.0
+    dy = torch.randn(3, 257, 32, generator=g)
+    xr = x.double().requires_grad_(True)
+    yr = torch.nn.functional.normalize(xr, p=2, dim=-1)
+    yr.backward(dy.double())
+    xd = x.to(device)
+    if cf:
+        xd = xd.transpose(1, 2).contiguous().transpose(1, 2)
+    xd.requires_grad_(True)
+    yd = ops.l2_normalize(xd)
+    assert yd.stride() == xd.stride()
+    yd.backward(dy.to(device))
+    assert (yd.detach().cpu().double() - yr.detach()).abs().max().item() <= 1e-6
+    scale = xr.grad.abs().max().item()
+    assert (xd.grad.cpu().double() - xr.grad).abs().max().item() <= 1e-5 * scale
