@@ -244,37 +244,45 @@ struct L2View {
   int64_t sb, sn, sc;
 };
 
+template <int CC>  // CC > 0: compile-time channel count (all loads in flight); 0: runtime C
 __global__ __launch_bounds__(256) void l2norm_fwd_kernel(const float* __restrict__ x, L2View v, int B, int N, int C,
                                                          float* __restrict__ y, float* __restrict__ nrm) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)B * N) return;
+  const int Cn = CC > 0 ? CC : C;
   const int64_t b = i / N, n = i - b * N;
   const int64_t o = b * v.sb + n * v.sn;
   float s = 0.f;
-  for (int c = 0; c < C; ++c) {
+#pragma unroll
+  for (int c = 0; c < Cn; ++c) {
     const float a = x[o + c * v.sc];
     s += a * a;
   }
   const float nr = sqrtf(s);
   const float d = fmaxf(nr, 1e-12f);
-  for (int c = 0; c < C; ++c) y[o + c * v.sc] = x[o + c * v.sc] / d;
+#pragma unroll
+  for (int c = 0; c < Cn; ++c) y[o + c * v.sc] = x[o + c * v.sc] / d;
   nrm[i] = nr;
 }
 
+template <int CC>
 __global__ __launch_bounds__(256) void l2norm_bwd_kernel(const float* __restrict__ y, const float* __restrict__ dy,
                                                          const float* __restrict__ nrm, L2View v, int B, int N, int C,
                                                          float* __restrict__ dx) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)B * N) return;
+  const int Cn = CC > 0 ? CC : C;
   const int64_t b = i / N, n = i - b * N;
   const int64_t o = b * v.sb + n * v.sn;
   const float nr = nrm[i];
   float yd = 0.f;
-  for (int c = 0; c < C; ++c) yd += y[o + c * v.sc] * dy[o + c * v.sc];
-  if (nr > 1e-12f) {
-    for (int c = 0; c < C; ++c) dx[o + c * v.sc] = (dy[o + c * v.sc] - y[o + c * v.sc] * yd) / nr;
-  } else {
-    for (int c = 0; c < C; ++c) dx[o + c * v.sc] = dy[o + c * v.sc] / 1e-12f;
+#pragma unroll
+  for (int c = 0; c < Cn; ++c) yd += y[o + c * v.sc] * dy[o + c * v.sc];
+  const bool clamped = !(nr > 1e-12f);
+#pragma unroll
+  for (int c = 0; c < Cn; ++c) {
+    const float g = dy[o + c * v.sc];
+    dx[o + c * v.sc] = clamped ? g / 1e-12f : (g - y[o + c * v.sc] * yd) / nr;
   }
 }
 
@@ -286,8 +294,9 @@ extern "C" int pk_l2_normalize_fwd(const float* x, const int64_t* strides, int B
   if ((int64_t)B * N == 0) return PK_OK;
   PK_REQUIRE(x && y && nrm);
   const L2View v{strides[0], strides[1], strides[2]};
-  hipLaunchKernelGGL(l2norm_fwd_kernel, dim3((unsigned)(((int64_t)B * N + 255) / 256)), dim3(256), 0,
-                     pk::as_stream(stream), x, v, B, N, C, y, nrm);
+  const dim3 grid((unsigned)(((int64_t)B * N + 255) / 256));
+  if (C == 32) hipLaunchKernelGGL(l2norm_fwd_kernel<32>, grid, dim3(256), 0, pk::as_stream(stream), x, v, B, N, C, y, nrm);
+  else hipLaunchKernelGGL(l2norm_fwd_kernel<0>, grid, dim3(256), 0, pk::as_stream(stream), x, v, B, N, C, y, nrm);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
@@ -298,8 +307,9 @@ extern "C" int pk_l2_normalize_bwd(const float* y, const float* dy, const float*
   if ((int64_t)B * N == 0) return PK_OK;
   PK_REQUIRE(y && dy && nrm && dx);
   const L2View v{strides[0], strides[1], strides[2]};
-  hipLaunchKernelGGL(l2norm_bwd_kernel, dim3((unsigned)(((int64_t)B * N + 255) / 256)), dim3(256), 0,
-                     pk::as_stream(stream), y, dy, nrm, v, B, N, C, dx);
+  const dim3 grid((unsigned)(((int64_t)B * N + 255) / 256));
+  if (C == 32) hipLaunchKernelGGL(l2norm_bwd_kernel<32>, grid, dim3(256), 0, pk::as_stream(stream), y, dy, nrm, v, B, N, C, dx);
+  else hipLaunchKernelGGL(l2norm_bwd_kernel<0>, grid, dim3(256), 0, pk::as_stream(stream), y, dy, nrm, v, B, N, C, dx);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

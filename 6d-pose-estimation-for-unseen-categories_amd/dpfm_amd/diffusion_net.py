@@ -38,9 +38,14 @@ class MiniMLP(nn.Sequential):
         for i in range(len(layer_sizes) - 1):
             if dropout and i > 0:
                 self.add_module(name + "_mlp_layer_dropout_{:03d}".format(i), nn.Dropout(p=0.5))
-            self.add_module(name + "_mlp_layer_{:03d}".format(i), Linear(layer_sizes[i], layer_sizes[i + 1]))
+            lin = Linear(layer_sizes[i], layer_sizes[i + 1])
+            self.add_module(name + "_mlp_layer_{:03d}".format(i), lin)
             if i + 2 != len(layer_sizes):
-                self.add_module(name + "_mlp_act_{:03d}".format(i), activation())
+                if activation is nn.ReLU:  # fused into the layer's epilogue (same module names)
+                    lin.relu_out = True
+                    self.add_module(name + "_mlp_act_{:03d}".format(i), nn.Identity())
+                else:
+                    self.add_module(name + "_mlp_act_{:03d}".format(i), activation())
 
 
 class DiffusionNetBlock(nn.Module):

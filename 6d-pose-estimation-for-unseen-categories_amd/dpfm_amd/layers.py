@@ -92,20 +92,24 @@ class _PointwiseFn(torch.autograd.Function):
     reference's transposes (modeling/dpfm.py:90-91, 113-116) cost no copies."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, cf):
+    def forward(ctx, x, weight, bias, cf, relu):
         w2 = weight.view(weight.shape[0], -1)
-        ctx.save_for_backward(x, weight)
-        ctx.has_bias, ctx.cf = bias is not None, cf
+        ctx.has_bias, ctx.cf, ctx.relu = bias is not None, cf, relu
         ctx.param, ctx.bias = weight, bias  # the Parameter objects (GroupedWgrad's buffer keys)
-        # a fresh (non-view) output: the reference applies in-place ReLUs to it (:112-116)
-        return ops.linear_fwd(x, w2, bias, channels_first=cf)
+        # a fresh (non-view) output: the reference applies in-place ReLUs to it (:112-116);
+        # relu=True applies the following nn.ReLU in the kernel's epilogue instead
+        y = ops.linear_fwd(x, w2, bias, channels_first=cf, relu=relu)
+        ctx.save_for_backward(x, weight, y if relu else None)
+        return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
+        x, weight, y = ctx.saved_tensors
         w2 = weight.view(weight.shape[0], -1)
         cf = ctx.cf
         dy = dy.contiguous()
+        if ctx.relu:  # the fused ReLU's backward (aten's ReluBackward: threshold_backward on the output)
+            dy = torch.ops.aten.threshold_backward(dy, y, 0.0)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = ops.linear_fwd(dy, w2, None, channels_first=cf, transw=True)  # dy W (rows) / W^T dy (cf)
@@ -115,10 +119,10 @@ class _PointwiseFn(torch.autograd.Function):
             else:
                 dw, db = ops.linear_wgrad(x, dy, channels_first=cf, want_bias=ctx.has_bias)
                 dw = dw.view(weight.shape)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
-def _pointwise(x, weight, bias, sem_cf: bool, out_cf: Optional[bool] = None):
+def _pointwise(x, weight, bias, sem_cf: bool, out_cf: Optional[bool] = None, relu: bool = False):
     """Apply the layer to x of semantic layout sem_cf (False: [..., C]; True: [B, C, N]).
     out_cf: force the output storage layout (None: the native layout of the input)."""
     if not x.is_cuda:
@@ -127,7 +131,7 @@ def _pointwise(x, weight, bias, sem_cf: bool, out_cf: Optional[bool] = None):
         base, native_cf = x.transpose(1, 2), not sem_cf
     else:
         base, native_cf = x.contiguous(), sem_cf
-    y = _PointwiseFn.apply(base, weight, bias, native_cf)
+    y = _PointwiseFn.apply(base, weight, bias, native_cf, relu)
     if out_cf is not None and out_cf != native_cf and y.dim() == 3:
         y = y.transpose(1, 2).contiguous().transpose(1, 2)  # same values, other storage order
     return y if native_cf == sem_cf else y.transpose(1, 2)
@@ -135,11 +139,14 @@ def _pointwise(x, weight, bias, sem_cf: bool, out_cf: Optional[bool] = None):
 
 class Linear(nn.Linear):
     """nn.Linear over every point; `out_cf = True` stores the [B, N, C] output
-    channels-first (a transposed view of a [B, C, N] tensor) for a channels-first consumer."""
+    channels-first (a transposed view of a [B, C, N] tensor) for a channels-first consumer;
+    `relu_out = True` applies the ReLU that follows the layer in the reference (the module
+    holding that ReLU is then an nn.Identity, so state_dict keys are unchanged)."""
     out_cf: Optional[bool] = None
+    relu_out: bool = False
 
     def forward(self, x):
-        return _pointwise(x, self.weight, self.bias, sem_cf=False, out_cf=self.out_cf)
+        return _pointwise(x, self.weight, self.bias, sem_cf=False, out_cf=self.out_cf, relu=self.relu_out)
 
 
 class Conv1d(nn.Conv1d):

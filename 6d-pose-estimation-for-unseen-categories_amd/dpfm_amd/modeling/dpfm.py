@@ -126,10 +126,11 @@ class OverlapPredictorNet(nn.Module):
         super().__init__()
         self.overlap_score_net = nn.Sequential(
             Linear(overlap_feat_dim, overlap_feat_dim, bias=True),
-            nn.ReLU(True),
+            nn.Identity(),  # the reference's nn.ReLU(True), applied in layer 0's epilogue
             Linear(overlap_feat_dim, 1, bias=True),
             nn.Sigmoid(),
         )
+        self.overlap_score_net[0].relu_out = True
 
     def forward(self, overlap_feat_x, overlap_feat_y):
         # F.normalize(., p=2, dim=-1) (modeling/dpfm.py:140-141), fused, storage order kept

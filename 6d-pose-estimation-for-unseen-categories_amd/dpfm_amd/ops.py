@@ -530,8 +530,11 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], c
         R = x.numel() // max(C, 1)
         y = torch.empty(x.shape[:-1] + (Cout,), dtype=x.dtype, device=x.device)
     assert C == Cin, (C, Cin)
+    # a point moves 4 (Cin + Cout) bytes for 2 Cin Cout flops: <= 21 flop/B for these layers,
+    # at or below the f32 MFMA ridge (157.3 TFLOP/s / 8 TB/s = 19.7): HBM-bound (flops beside)
     call("pk_linear_fwd", ptr(x), ptr(w), ptr(bias), layout, int(R), int(N), int(Cin), int(Cout), int(transw),
-         int(relu), ptr(y), _lib.stream(x.device), work=("mfma", 2 * int(R) * Cin * Cout))
+         int(relu), ptr(y), _lib.stream(x.device),
+         work=("hbm", 4 * int(R) * (Cin + Cout) + 4 * Cin * Cout, 2 * int(R) * Cin * Cout))
     return y
 
 

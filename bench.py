@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=32, help="crops per GPU (configs[1]: 32)")
     ap.add_argument("--points", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-crops", type=int, default=6, help="bounded CPU-baseline sample (crops)")
+    ap.add_argument("--cpu-crops", type=int, default=30, help="bounded CPU-baseline sample (crops)")
     ap.add_argument("--no-roofline-probe", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP graph: launch every kernel from Python")
     ap.add_argument("--no-overlap", action="store_true",
@@ -76,7 +76,8 @@ class KernelProbe:
             known = all(w is not None for w in works)
             out[k] = dict(avg_ms=float(np.mean(ms)), launches=len(ms), total_ms=float(np.sum(ms)),
                           bound=works[0][0] if known else None,
-                          work=float(sum(w[1] for w in works)) if known else None)
+                          work=float(sum(w[1] for w in works)) if known else None,
+                          flops=float(sum(w[2] for w in works)) if known and all(len(w) > 2 for w in works) else None)
         return out
 
 
@@ -335,6 +336,12 @@ def roofline_for(name: str, k: dict) -> dict:
         ach = k["work"] / sec / 1e9
         r = dict(base, bound="hbm", achieved=round(ach, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                  frac=round(ach / HBM_PEAK_GBS, 6), traffic=traffic)
+    if k.get("flops") is not None:  # HBM-bound family that also declares its MFMA flops
+        r["mfma_achieved_tflops"] = round(k["flops"] / sec / 1e12, 3)
+        r["mfma_frac"] = round(k["flops"] / sec / 1e12 / F32_MFMA_TFLOPS, 4)
+        r["note"] = ("per-point layers: 2 Cin Cout flop per 4 (Cin + Cout) B of a point, <= 21 flop/B, at or "
+                     "below the f32 MFMA ridge (157.3 / 8 = 19.7 flop/B): bound by HBM; "
+                     "each launch moves 4-50 MB, so launch ramp and tail are a large share")
     if name == "pk_fps":
         r["note"] = ("sequential npoint-step argmax, one workgroup per crop: latency-bound; the HBM "
                      "fraction is reported for completeness, not as its limiter")

@@ -28,7 +28,18 @@ FAMILIES = {
     "pk_linear_wgrad": ["wgrad_v2_kernel", "wgrad_partial_kernel", "wgrad_reduce_kernel"],
     "pk_feat_dist_topk": ["fd_prep_kernel", "fd_main_kernel"],
     "pk_cgt_lstsq": ["cgt_count_kernel", "cgt_partial_kernel", "cgt_reduce_kernel", "cgt_solve_kernel"],
+    "pk_linear_fwd": ["linear_fwd_rows_kernel", "linear_fwd_cf_kernel", "linear_fwd_kernel"],
+    "pk_linear_wgrad_grouped": ["wgrad_grouped_kernel", "wgrad_grouped_reduce_kernel"],
+    "pk_nce_loss": ["nce_pass_kernel<false>", "nce_pass_kernel<true>", "zero_fill_kernel"],
+    "pk_clip_rmsprop": ["grad_sumsq_kernel", "clip_rmsprop_kernel"],
+    "pk_instnorm_relu_fwd": ["instnorm_relu_fwd"],
+    "pk_instnorm_relu_bwd": ["instnorm_relu_bwd"],
+    "pk_wbce": ["wbce_kernel"],
+    "pk_l2_normalize_fwd": ["l2norm_fwd_kernel"],
+    "pk_l2_normalize_bwd": ["l2norm_bwd_kernel"],
 }
+# families whose launches are ONE of several kernels (every dispatch is a family launch)
+ANY_LEAD = {"pk_linear_fwd"}
 # (the first kernel of each family is counted once per family launch)
 
 
@@ -60,8 +71,9 @@ def main():
     for fam, names, lo, hi in [(f, n, 0, PROBE_GRID - 1) for f, n in FAMILIES.items()] + \
             [("pk_ball_query_mask@configs3_probe", FAMILIES["pk_ball_query_mask"], PROBE_GRID, None)]:
         fetch, write = read(fetch_dir, "FETCH_SIZE", lo, hi), read(write_dir, "WRITE_SIZE", lo, hi)
-        def summed(tab, names=names):
-            n_lead = sum(c for k, (c, _) in tab.items() if names[0] in k)
+        def summed(tab, names=names, fam=fam):
+            lead = names if fam in ANY_LEAD else names[:1]
+            n_lead = sum(c for k, (c, _) in tab.items() if any(nm in k for nm in lead))
             v = sum(s for k, (_, s) in tab.items() if any(nm in k for nm in names))
             return n_lead, v
         nf, fb = summed(fetch)
