@@ -792,6 +792,85 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
     }
 }
 
+// Thin layers (Cin <= 4 or Cout <= 4: DiffusionNet's first_lin 3 -> 64, the overlap head's
+// 32 -> 1 and its input gradient 1 -> 32): too little contraction for MFMA tiles, so plain
+// FMAs with the weight in LDS, organised for coalesced memory traffic.
+//   rows layout: thread = (point, 4 consecutive outputs), one float4 store per thread
+//   channels-first: thread = point n of an item, Cout coalesced row stores
+constexpr int kThinMaxW = 4096;  // Cout * Cin floats in LDS
+
+template <int LAYOUT, int CINT>  // CINT: compile-time Cin (1..4), or 0 (runtime Cin, Cout <= 4)
+__global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, int64_t R, int N, int Cin_,
+                                                          int Cout, int transw, int relu, float* __restrict__ y) {
+  __shared__ float Ws[kThinMaxW];  // Ws[o * Cin + k]
+  __shared__ float bs[kLfMaxC];
+  const int Cin = CINT > 0 ? CINT : Cin_;
+  for (int e = threadIdx.x; e < Cout * Cin; e += 256) {
+    const int o = e / Cin, k = e - o * Cin;
+    Ws[e] = transw ? w[(int64_t)k * Cout + o] : w[e];
+  }
+  for (int o = threadIdx.x; o < Cout; o += 256) bs[o] = bias ? bias[o] : 0.f;
+  __syncthreads();
+  if (LAYOUT == 0) {
+    const int G = (Cout + 3) >> 2;  // output quads per point
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= R * G) return;
+    const int64_t r = t / G;
+    const int o0 = (int)(t - r * G) * 4;
+    float acc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = o0 + u < Cout ? bs[o0 + u] : 0.f;
+#pragma unroll 4
+    for (int k = 0; k < Cin; ++k) {
+      const float xv = x[r * Cin + k];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (o0 + u < Cout) acc[u] = fmaf(xv, Ws[(o0 + u) * Cin + k], acc[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = relu ? fmaxf(acc[u], 0.f) : acc[u];
+    if ((Cout & 3) == 0) {
+      *reinterpret_cast<float4*>(y + r * Cout + o0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (o0 + u < Cout) y[r * Cout + o0 + u] = acc[u];
+    }
+  } else {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= R) return;
+    const int64_t b = t / N, n = t - b * N;
+    const float* __restrict__ xb = x + b * Cin * (int64_t)N + n;
+    float* __restrict__ yb = y + b * Cout * (int64_t)N + n;
+    if (CINT > 0) {  // few inputs in registers, one coalesced row store per output
+      float xv[CINT > 0 ? CINT : 1];
+#pragma unroll
+      for (int k = 0; k < CINT; ++k) xv[k] = xb[(int64_t)k * N];
+      for (int o = 0; o < Cout; ++o) {
+        float a = bs[o];
+#pragma unroll
+        for (int k = 0; k < CINT; ++k) a = fmaf(xv[k], Ws[o * CINT + k], a);
+        yb[(int64_t)o * N] = relu ? fmaxf(a, 0.f) : a;
+      }
+    } else {  // Cout <= 4: one coalesced row load per input channel
+      float acc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = u < Cout ? bs[u] : 0.f;
+#pragma unroll 8
+      for (int k = 0; k < Cin; ++k) {
+        const float xv = xb[(int64_t)k * N];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (u < Cout) acc[u] = fmaf(xv, Ws[u * Cin + k], acc[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (u < Cout) yb[(int64_t)u * N] = relu ? fmaxf(acc[u], 0.f) : acc[u];
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, int layout, int64_t R, int N,
@@ -800,6 +879,24 @@ extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, 
   PK_REQUIRE(layout == 0 || (N > 0 && R % N == 0));
   if (R == 0) return PK_OK;
   PK_REQUIRE(x && w && y);
+  if ((Cin <= 4 || Cout <= 4) && Cin * Cout <= kThinMaxW) {
+    const int64_t threads = layout == 0 ? R * ((Cout + 3) / 4) : R;
+    const dim3 grid((unsigned)((threads + 255) / 256));
+#define PK_THIN(L, C)                                                                                           \
+  hipLaunchKernelGGL((linear_thin_kernel<L, C>), grid, dim3(256), 0, pk::as_stream(stream), x, w, bias, R, N, Cin, \
+                     Cout, transw, relu, y)
+    const int ct = Cin <= 4 ? Cin : 0;  // Cin > 4 here means Cout <= 4
+    if (layout == 0) {
+      if (ct == 1) PK_THIN(0, 1); else if (ct == 2) PK_THIN(0, 2); else if (ct == 3) PK_THIN(0, 3);
+      else if (ct == 4) PK_THIN(0, 4); else PK_THIN(0, 0);
+    } else {
+      if (ct == 1) PK_THIN(1, 1); else if (ct == 2) PK_THIN(1, 2); else if (ct == 3) PK_THIN(1, 3);
+      else if (ct == 4) PK_THIN(1, 4); else PK_THIN(1, 0);
+    }
+#undef PK_THIN
+    PK_CHECK_LAUNCH();
+    return PK_OK;
+  }
   if (layout == 0 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128)) {
     // 16-point tiles, 4 per block, at most two blocks per CU's worth of waves in flight
     const int64_t tiles = (R + 15) / 16;

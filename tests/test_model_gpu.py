@@ -226,7 +226,10 @@ def test_dpfmnet_matches_oracle(device, N1, N2):
                                                           ((2, 64, 512, 32), True, True), ((0, 8, 8), False, False),
                                                           ((32, 64, 1024, 64), True, False), ((64, 32, 2048, 128), True, False),
                                                           ((32, 128, 1024, 64), True, True), ((3, 16, 48, 5), True, False),
-                                                          ((5000, 32, 1), False, False), ((777, 16, 100), False, True)])
+                                                          ((5000, 32, 1), False, False), ((777, 16, 100), False, True),
+                                                          ((32, 32, 1024, 1), True, False), ((32, 1, 1024, 32), True, True),
+                                                          ((3, 2, 100, 7), True, False), ((10, 33, 3), False, True),
+                                                          ((2, 40, 64, 3), True, True), ((65536, 3, 64), False, False)])
 def test_linear_fwd(device, shape, channels_first, transw):
     """pk_linear_fwd (per-point layer forward, bias fused; transw = the input gradient dy W)
     vs fp64: |err| <= 1e-5 * sum_k |x||w| + 1e-6 |b|."""
