@@ -11,6 +11,8 @@ per direction (ops.spectral_diffusion); the per-point MLPs are GEMMs.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -48,6 +50,45 @@ class MiniMLP(nn.Sequential):
                     self.add_module(name + "_mlp_act_{:03d}".format(i), activation())
 
 
+class _BlockMLPFn(torch.autograd.Function):
+    """mlp(cat[x_in, x_diffuse]) + x_in for the configured MiniMLP (128 -> 64 -> 64 -> 64, ReLU
+    between): forward in one fused launch (ops.mlp3_fwd); backward through the per-layer
+    input-gradient kernels, the ReLU masks on the saved h1 / h2, and the weight gradients
+    recorded for the grouped launch (layers.GroupedWgrad) or computed per layer."""
+
+    @staticmethod
+    def forward(ctx, x_in, x_diff, w1, b1, w2, b2, w3, b3):
+        cat, h1, h2, y = ops.mlp3_fwd(x_in, x_diff, w1, b1, w2, b2, w3, b3)
+        ctx.save_for_backward(cat, h1, h2, w1, w2, w3)
+        ctx.params = (w1, b1, w2, b2, w3, b3)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import layers
+        cat, h1, h2, w1, w2, w3 = ctx.saved_tensors
+        P = ctx.params
+        dy = dy.contiguous()
+        grads = [None] * 6
+
+        def wgrad(x, d, k):  # layer k (0..2): weight P[2k], bias P[2k + 1]
+            if layers._side_owns(P[2 * k], P[2 * k + 1]):
+                layers._SIDE.launch(x, d, P[2 * k], P[2 * k + 1], channels_first=False)
+            else:
+                grads[2 * k], grads[2 * k + 1] = ops.linear_wgrad(x, d, channels_first=False, want_bias=True)
+
+        wgrad(h2, dy, 2)
+        d2 = torch.ops.aten.threshold_backward(ops.linear_fwd(dy, w3, None, channels_first=False, transw=True), h2, 0.0)
+        wgrad(h1, d2, 1)
+        d1 = torch.ops.aten.threshold_backward(ops.linear_fwd(d2, w2, None, channels_first=False, transw=True), h1, 0.0)
+        wgrad(cat, d1, 0)
+        dcat = ops.linear_fwd(d1, w1, None, channels_first=False, transw=True)
+        C = dy.shape[-1]
+        dx_in = dcat[..., :C] + dy  # the residual
+        dx_diff = dcat[..., C:].contiguous()
+        return (dx_in, dx_diff, *grads)
+
+
 class DiffusionNetBlock(nn.Module):
     def __init__(self, C_width, mlp_hidden_dims, dropout=False, diffusion_method="spectral",
                  with_gradient_features=False, with_gradient_rotations=True):
@@ -58,8 +99,23 @@ class DiffusionNetBlock(nn.Module):
         self.diffusion = LearnedTimeDiffusion(C_width, method=diffusion_method)
         self.mlp = MiniMLP([2 * C_width] + list(mlp_hidden_dims) + [C_width], dropout=dropout)
 
+    # The fused block forward (pk_mlp3_fwd) is opt-in: on MI355X it measured no faster than the
+    # per-layer kernels it replaces (46 us vs 20 + 12 + 12 us of layer launches plus the concat
+    # and the residual add: one 8-wave block per CU, 103 KB of LDS), DESIGN.md §3
+    fused_mlp = os.environ.get("PK_FUSED_BLOCK_MLP", "0") == "1"
+
+    def _fusable(self, x_in) -> bool:
+        lins = [m for m in self.mlp if isinstance(m, Linear)]
+        return (self.fused_mlp and x_in.is_cuda and len(lins) == 3 and self.C_width == 64 and len(self.mlp) == 5
+                and all(l.relu_out for l in lins[:2]) and not lins[2].relu_out
+                and all(l.bias is not None for l in lins)
+                and [tuple(l.weight.shape) for l in lins] == [(64, 128), (64, 64), (64, 64)])
+
     def forward(self, x_in, mass, L, evals, evecs, gradX, gradY):
         x_diffuse = self.diffusion(x_in, L, mass, evals, evecs)
+        if self._fusable(x_in):  # the configured block: one fused forward launch
+            l0, l1, l2 = [m for m in self.mlp if isinstance(m, Linear)]
+            return _BlockMLPFn.apply(x_in, x_diffuse, l0.weight, l0.bias, l1.weight, l1.bias, l2.weight, l2.bias)
         return self.mlp(torch.cat((x_in, x_diffuse), dim=-1)) + x_in
 
 

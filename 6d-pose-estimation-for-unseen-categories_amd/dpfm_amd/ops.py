@@ -513,6 +513,24 @@ def l2_normalize(x: torch.Tensor) -> torch.Tensor:
     return _L2Normalize.apply(x)
 
 
+def mlp3_fwd(x_in: torch.Tensor, x_diff: torch.Tensor, w1, b1, w2, b2, w3, b3):
+    """pk_mlp3_fwd: (cat, h1, h2, y) of the DiffusionNet block MLP with its residual."""
+    x_in, x_diff = x_in.contiguous(), x_diff.contiguous()
+    C = x_in.shape[-1]
+    R = x_in.numel() // C
+    lead = x_in.shape[:-1]
+    dev = x_in.device
+    cat = torch.empty(lead + (2 * C,), dtype=torch.float32, device=dev)
+    h1 = torch.empty(lead + (C,), dtype=torch.float32, device=dev)
+    h2 = torch.empty_like(h1)
+    y = torch.empty_like(h1)
+    byts = 4 * R * (2 * C + 2 * C + 3 * C + C)  # reads x_in, x_diff (+x_in again), writes cat, h1, h2, y
+    call("pk_mlp3_fwd", ptr(x_in), ptr(x_diff), ptr(w1.contiguous()), ptr(b1), ptr(w2.contiguous()), ptr(b2),
+         ptr(w3.contiguous()), ptr(b3), int(R), int(C), ptr(cat), ptr(h1), ptr(h2), ptr(y), _lib.stream(dev),
+         work=("hbm", byts, 2 * R * C * (2 * C + C + C)))
+    return cat, h1, h2, y
+
+
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], channels_first: bool,
                transw: bool = False, relu: bool = False) -> torch.Tensor:
     """pk_linear_fwd: y = x W^T (+ b) over every point (W [Cout, Cin], or W^T read from a

@@ -214,6 +214,15 @@ int pk_l2_normalize_fwd(const float* x, const int64_t* strides, int B, int N, in
 int pk_l2_normalize_bwd(const float* y, const float* dy, const float* nrm, const int64_t* strides, int B, int N,
                         int C, float* dx, void* stream);
 
+/* H7 DiffusionNet block MLP forward, fused (upstream DiffusionNetBlock.forward at
+ * models/dpfm.py:22-30: mlp(cat[x_in, x_diffuse]) + x_in, MiniMLP 128 -> 64 -> ReLU -> 64 ->
+ * ReLU -> 64). x_in / x_diff f32 [R, C], C = 64; W1 [64, 128], W2 / W3 [64, 64], biases
+ * [64]; writes cat [R, 128], h1 / h2 [R, 64] (post-ReLU, kept for the backward) and
+ * y [R, 64] = h2 W3^T + b3 + x_in. */
+int pk_mlp3_fwd(const float* x_in, const float* x_diff, const float* w1, const float* b1, const float* w2,
+                const float* b2, const float* w3, const float* b3, int64_t R, int C, float* cat, float* h1, float* h2,
+                float* y, void* stream);
+
 /* Forward / input gradient of the same per-point layers (nn.Linear at models/dpfm.py:22-30
  * and modeling/dpfm.py:16-26,90-91,113-116; Conv1d(k=1) at modeling/dpfm.py:16-26,49-50):
  *   y = x W^T (+ bias) (ReLU if relu), W f32 [Cout, Cin]; with transw = 1 the weight is
