@@ -113,7 +113,10 @@ class CrossAttentionRefinementNet(nn.Module):
             desc1 = desc1 + layer(desc1, desc0)
         ax = self.last_lin(desc0.transpose(1, 2))
         ay = self.last_lin(desc1.transpose(1, 2))
-        ref_x, ref_y = ax[:, :, :self.n_in], ay[:, :, :self.n_in]
+        if ax.shape[-1] == self.n_in:  # "normal" attention: the whole width (no slice, whose
+            ref_x, ref_y = ax, ay     # backward would zero-fill and copy)
+        else:
+            ref_x, ref_y = ax[:, :, :self.n_in], ay[:, :, :self.n_in]
         if self.attention_type == "normal":
             ox, oy = self.overlap_predictor(ref_x, ref_y)
         else:

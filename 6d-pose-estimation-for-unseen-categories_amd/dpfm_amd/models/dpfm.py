@@ -23,6 +23,17 @@ DEFAULT_CFG = {  # config/dpfm_orig.yaml
 }
 
 
+def _cat0(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """torch.cat((a, b), 0), without a copy when b directly follows a in one storage (the
+    device pipeline keeps the CAD and crop operators of a batch in one buffer)."""
+    if (a.is_contiguous() and b.is_contiguous() and a.dtype == b.dtype and a.device == b.device
+            and a.shape[1:] == b.shape[1:]
+            and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
+            and b.storage_offset() == a.storage_offset() + a.numel()):
+        return a.as_strided((a.shape[0] + b.shape[0],) + tuple(a.shape[1:]), a.stride())
+    return torch.cat((a, b), 0)
+
+
 class DPFMNet(nn.Module):
     """Compute the functional map matrix representation."""
 
@@ -50,9 +61,9 @@ class DPFMNet(nn.Module):
         if features1.dim() == 3 and features1.shape == features2.shape and evecs1.shape == evecs2.shape:
             # same weights, per-crop operations: one pass over both shapes (2B crops)
             B = features1.shape[0]
-            feat = self.feature_extractor(torch.cat((features1, features2), 0), torch.cat((mass1, mass2), 0),
-                                          evals=torch.cat((evals1, evals2), 0), evecs=torch.cat((evecs1, evecs2), 0))
-            feat1, feat2 = feat[:B], feat[B:]
+            feat = self.feature_extractor(torch.cat((features1, features2), 0), _cat0(mass1, mass2),
+                                          evals=_cat0(evals1, evals2), evecs=_cat0(evecs1, evecs2))
+            feat1, feat2 = torch.chunk(feat, 2, 0)  # backward: one concat (slices: two zero-fills + copies)
         else:
             feat1 = self.feature_extractor(features1, mass1, evals=evals1, evecs=evecs1)
             feat2 = self.feature_extractor(features2, mass2, evals=evals2, evecs=evecs2)

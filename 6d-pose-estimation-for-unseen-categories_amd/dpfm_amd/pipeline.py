@@ -73,10 +73,16 @@ def make_frame_batch(F: int, n1: int, n2: int, seed: int, device) -> tuple[Frame
                     cad64=torch.as_tensor(np.concatenate(cad, 0), dtype=torch.float64, device=d),
                     cad_off=ops.packed_offsets([n1] * F, d), diam=diam, max_pixels=maxpix,
                     thr2=torch.tensor([ops.ball_threshold(0.05 * x) for x in diam], dtype=torch.float64, device=d))
-    op = Operators(cad_mass=T([o[0] for o in ops_c]), cad_evals=T([o[1] for o in ops_c]),
-                   cad_evecs=T([o[2] for o in ops_c]), cad_xyz=T([c.astype(np.float32) for c in cad]),
-                   pc_mass=T([o[0] for o in ops_p]), pc_evals=T([o[1] for o in ops_p]),
-                   pc_evecs=T([o[2] for o in ops_p]),
+    # CAD and crop operators of the batch in ONE buffer each ([CAD; crops] along the batch):
+    # the model's shared encoder pass over both shapes then needs no concatenation copy
+    def joint(k):
+        if ops_c[0][k].shape != ops_p[0][k].shape:  # n1 != n2: separate buffers
+            return T([o[k] for o in ops_c]), T([o[k] for o in ops_p])
+        both = T([o[k] for o in ops_c] + [o[k] for o in ops_p])
+        return both[:F], both[F:]
+    (cm, pm), (ce, pe), (cv, pv) = joint(0), joint(1), joint(2)
+    op = Operators(cad_mass=cm, cad_evals=ce, cad_evecs=cv, cad_xyz=T([c.astype(np.float32) for c in cad]),
+                   pc_mass=pm, pc_evals=pe, pc_evecs=pv,
                    ir_thr=torch.tensor([np.float32(0.1 * x) for x in diam], dtype=torch.float32, device=d),
                    rig_thr=ops.rigidity_thresholds(diam, d))
     return fb, op
