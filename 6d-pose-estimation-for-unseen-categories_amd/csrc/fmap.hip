@@ -127,3 +127,55 @@ extern "C" int pk_fmap_solve_backward(const float* AAt, const float* BAt, const 
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
+
+// ---------------------------------------------------------------------------------
+// H9 resolvent mask (upstream dpfm/utils.py::get_mask, called per crop at
+// modeling/dpfm.py:171-176 and models/dpfm.py:76) for every crop in one launch:
+//   s = max(max evals1, max evals2); g1 = (evals1 / s)^gamma; g2 = (evals2 / s)^gamma
+//   D[j][i] = (g2_j / (g2_j^2 + 1) - g1_i / (g1_i^2 + 1))^2 + (1 / (g2_j^2 + 1) - 1 / (g1_i^2 + 1))^2
+// One workgroup per crop, one thread per (j, i). gamma = 0.5 takes sqrt (as aten's pow).
+namespace {
+
+__global__ __launch_bounds__(1024) void resolvent_mask_kernel(const float* __restrict__ ev1, int ld1,
+                                                              const float* __restrict__ ev2, int ld2, int K,
+                                                              float gamma, float* __restrict__ D) {
+  __shared__ float red[16];
+  __shared__ float g1s[64], g2s[64];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* e1 = ev1 + (int64_t)b * ld1;
+  const float* e2 = ev2 + (int64_t)b * ld2;
+  float mx = -__builtin_huge_valf();
+  if (tid < K) mx = fmaxf(e1[tid], e2[tid]);
+  for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  float s = red[0];
+  for (int w = 1; w < (int)(blockDim.x >> 6); ++w) s = fmaxf(s, red[w]);
+  if (tid < K) {
+    const float a = e1[tid] / s, c = e2[tid] / s;
+    g1s[tid] = gamma == 0.5f ? sqrtf(a) : powf(a, gamma);
+    g2s[tid] = gamma == 0.5f ? sqrtf(c) : powf(c, gamma);
+  }
+  __syncthreads();
+  if (tid < K * K) {
+    const int j = tid / K, i = tid - j * K;
+    const float g1 = g1s[i], g2 = g2s[j];
+    const float q1 = g1 * g1 + 1.f, q2 = g2 * g2 + 1.f;
+    const float re = g2 / q2 - g1 / q1;
+    const float im = 1.f / q2 - 1.f / q1;
+    D[(int64_t)b * K * K + tid] = re * re + im * im;
+  }
+}
+
+}  // namespace
+
+extern "C" int pk_resolvent_mask(const float* evals1, int ld1, const float* evals2, int ld2, int B, int K, float gamma,
+                                 float* D, void* stream) {
+  PK_REQUIRE(B >= 0 && K > 0 && K <= 32 && ld1 >= K && ld2 >= K);
+  if (B == 0) return PK_OK;
+  PK_REQUIRE(evals1 && evals2 && D);
+  hipLaunchKernelGGL(resolvent_mask_kernel, dim3(B), dim3(1024), 0, pk::as_stream(stream), evals1, ld1, evals2, ld2, K,
+                     gamma, D);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}

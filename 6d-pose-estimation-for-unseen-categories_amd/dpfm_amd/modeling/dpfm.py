@@ -160,7 +160,11 @@ class RegularizedFMNet(nn.Module):
             evals_x, evals_y = evals_x[None], evals_y[None]
         A = torch.bmm(evecs_trans_x, feat_x)
         Bm = torch.bmm(evecs_trans_y, feat_y)
-        with torch.no_grad():  # per-crop get_mask (:171-176), batched
-            D = get_mask_batched(evals_x.flatten(1), evals_y.flatten(1), self.resolvant_gamma)
+        with torch.no_grad():  # per-crop get_mask (:171-176), batched, one launch
+            ex, ey = evals_x.flatten(1), evals_y.flatten(1)
+            if ex.is_cuda and ex.dtype == torch.float32 and ex.shape == ey.shape and ex.shape[1] <= 32:
+                D = ops.resolvent_mask(ex, ey, self.resolvant_gamma)
+            else:
+                D = get_mask_batched(ex, ey, self.resolvant_gamma)
         A_t = A.transpose(1, 2)
         return ops.fmap_solve(torch.bmm(A, A_t), torch.bmm(Bm, A_t), D, self.lambda_)

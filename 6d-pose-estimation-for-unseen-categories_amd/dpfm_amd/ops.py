@@ -265,6 +265,20 @@ class _FmapSolve(torch.autograd.Function):
         return part.sum(1), dBAt, None, None
 
 
+def resolvent_mask(evals1: torch.Tensor, evals2: torch.Tensor, gamma: float = 0.5) -> torch.Tensor:
+    """get_mask for every crop in one launch (pk_resolvent_mask): evals [B, >=K] (K = the
+    mask size = evals1.shape[1] unless sliced views are passed) -> D f32 [B, K, K]."""
+    B, K = evals1.shape
+    if evals1.stride(1) != 1 or evals2.stride(1) != 1:
+        evals1, evals2 = evals1.contiguous(), evals2.contiguous()
+    D = torch.empty((B, K, K), dtype=torch.float32, device=evals1.device)
+    import ctypes
+    call("pk_resolvent_mask", ctypes.c_void_p(evals1.data_ptr()), int(evals1.stride(0)),
+         ctypes.c_void_p(evals2.data_ptr()), int(evals2.stride(0)), B, K, float(gamma), ptr(D),
+         _lib.stream(evals1.device))
+    return D
+
+
 def fmap_solve(AAt: torch.Tensor, BAt: torch.Tensor, D: torch.Tensor, lambda_: float) -> torch.Tensor:
     if AAt.shape[-1] != 30:
         raise _lib.PoseKernError("fmap solve kernel is built for n_fmap = 30")

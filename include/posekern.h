@@ -223,6 +223,12 @@ int pk_mlp3_fwd(const float* x_in, const float* x_diff, const float* w1, const f
                 const float* b2, const float* w3, const float* b3, int64_t R, int C, float* cat, float* h1, float* h2,
                 float* y, void* stream);
 
+/* H9 resolvent mask: upstream dpfm/utils.py::get_mask(evals1[:K], evals2[:K], gamma) for every
+ * crop (the per-crop branch that always runs, modeling/dpfm.py:164-182). evals1 / evals2 f32
+ * [B, ld] (first K used, K <= 32); D f32 [B, K, K], D[b][j][i] from evals2[j], evals1[i]. */
+int pk_resolvent_mask(const float* evals1, int ld1, const float* evals2, int ld2, int B, int K, float gamma, float* D,
+                      void* stream);
+
 /* Forward / input gradient of the same per-point layers (nn.Linear at models/dpfm.py:22-30
  * and modeling/dpfm.py:16-26,90-91,113-116; Conv1d(k=1) at modeling/dpfm.py:16-26,49-50):
  *   y = x W^T (+ bias) (ReLU if relu), W f32 [Cout, Cin]; with transw = 1 the weight is

@@ -417,3 +417,19 @@ def test_block_mlp_fused_matches_layers(device):
     assert torch.equal(outs[True][0], outs[False][0])
     for a, b in [(outs[True][1], outs[False][1])] + list(zip(outs[True][2], outs[False][2])):
         assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item() + 1e-12
+
+
+def test_resolvent_mask_matches_get_mask(device):
+    """pk_resolvent_mask (all crops, one launch) vs upstream get_mask per crop (restated in
+    dpfm_utils.get_mask) in fp64, on sliced [:, :30] views of [B, 64] eigenvalues."""
+    from dpfm_amd import ops
+    from dpfm_amd.dpfm_utils import get_mask
+    g = torch.Generator().manual_seed(12)
+    B = 5
+    e1 = torch.sort(torch.rand(B, 64, generator=g) * 3, dim=1)[0]
+    e2 = torch.sort(torch.rand(B, 64, generator=g) * 5, dim=1)[0]
+    e1[:, 0] = 0.0
+    D = ops.resolvent_mask(e1.to(device)[:, :30], e2.to(device)[:, :30], 0.5).cpu().double()
+    for b in range(B):
+        ref = get_mask(e1[b, :30].double(), e2[b, :30].double(), 0.5)
+        assert (D[b] - ref).abs().max().item() <= 1e-6 * ref.abs().max().item() + 1e-12

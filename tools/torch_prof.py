@@ -39,4 +39,12 @@ with open(os.path.join(out, "torch_prof_ops.txt"), "w") as f:
                                                                max_shapes_column_width=80))
 with open(os.path.join(out, "torch_prof_kernels.txt"), "w") as f:
     f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60, max_name_column_width=90))
+with open(os.path.join(out, "torch_prof_glue.txt"), "w") as f:
+    rows = []
+    for e in prof.key_averages(group_by_input_shape=True):
+        dev_us = getattr(e, "self_device_time_total", None) or getattr(e, "self_cuda_time_total", 0)
+        if e.key.startswith("aten::") and dev_us > 0:
+            rows.append((dev_us, e.count, e.key, str(e.input_shapes)[:150]))
+    for r in sorted(rows, reverse=True)[:60]:
+        f.write(f"{r[0]/2:9.1f} us/step {r[1]/2:5.1f}/step  {r[2]:32s} {r[3]}\n")
 print("ok", out)
