@@ -511,10 +511,17 @@ namespace {
 // shapes (32k-65k points x <= 128 channels).
 constexpr int kLfMaxC = 128;
 
+// ReLU backward folded into an input-gradient epilogue: mask = the forward output of the layer
+// whose gradient this is (aten threshold_backward(grad, mask, 0): mask <= 0 -> 0)
+__device__ __forceinline__ float relu_mask(float v, const float* __restrict__ mask, int64_t i) {
+  return (mask != nullptr && mask[i] <= 0.f) ? 0.f : v;
+}
+
 template <int LAYOUT>
 __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                          const float* __restrict__ bias, int64_t R, int N, int Cin,
-                                                         int Cout, int transw, int relu, float* __restrict__ y) {
+                                                         int Cout, int transw, int relu, const float* __restrict__ mask,
+    float* __restrict__ y) {
   // weight as Ws[out][k], out < Cout, k < KP (zero padded); row stride KP + 1 (odd);
   // dynamic LDS of Cout * (KP + 1) floats (<= 64.5 KiB)
   extern __shared__ float Ws[];
@@ -584,14 +591,14 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict
           if (pr < R && o < Cout) {
             float v = acc[t][e] + (bias != nullptr ? bias[o] : 0.f);
             if (relu) v = fmaxf(v, 0.f);
-            y[pr * Cout + o] = v;
+            y[pr * Cout + o] = relu_mask(v, mask, pr * Cout + o);
           }
         } else {
           const int o = t * 32 + rr;
           if (ok && o < Cout) {
             float v = acc[t][e] + (bias != nullptr ? bias[o] : 0.f);
             if (relu) v = fmaxf(v, 0.f);
-            y[(bb * Cout + o) * N + nn] = v;
+            y[(bb * Cout + o) * N + nn] = relu_mask(v, mask, (bb * Cout + o) * N + nn);
           }
         }
       }
@@ -650,7 +657,8 @@ __device__ __forceinline__ void lr_stage(const float* __restrict__ w, int Cout, 
 template <int Q, int TO>  // Cin = 16 Q, Cout <= 16 TO
 __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                               const float* __restrict__ bias, int64_t R, int Cin,
-                                                              int Cout, int transw, int relu, float* __restrict__ y) {
+                                                              int Cout, int transw, int relu, const float* __restrict__ mask,
+    float* __restrict__ y) {
   extern __shared__ float Ws[];  // [16 TO][Cin + 4]
   constexpr int CI = 16 * Q, ST = CI + 4;
   const int lane = pk::lane_id(), m = lane & 15, g = lane >> 4;
@@ -700,7 +708,7 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
           if (pr < R && o < Cout) {
             float v = acc[t][r] + bv[t];
             if (relu) v = fmaxf(v, 0.f);
-            y[pr * Cout + o] = v;
+            y[pr * Cout + o] = relu_mask(v, mask, pr * Cout + o);
           }
         }
       }
@@ -726,7 +734,8 @@ template <> struct LcVec<4> { using T = f32x4; };
 template <int Q, int TO, int SUB>
 __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                             const float* __restrict__ bias, int64_t R, int N, int Cout,
-                                                            int transw, int relu, float* __restrict__ y) {
+                                                            int transw, int relu, const float* __restrict__ mask,
+    float* __restrict__ y) {
   using V = typename LcVec<SUB>::T;
   extern __shared__ float Ws[];
   constexpr int CI = 16 * Q, ST = CI + 4, P = 16 * SUB;
@@ -785,6 +794,7 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
         for (int u = 0; u < SUB; ++u) {
           float e = acc[t][u][r] + bo;
           if (relu) e = fmaxf(e, 0.f);
+          e = relu_mask(e, mask, (yb - y) + (int64_t)o * N + u);
           if constexpr (SUB == 1) v = e; else v[u] = e;
         }
         *reinterpret_cast<V*>(yb + (int64_t)o * N) = v;
@@ -802,7 +812,8 @@ constexpr int kThinMaxW = 4096;  // Cout * Cin floats in LDS
 template <int LAYOUT, int CINT>  // CINT: compile-time Cin (1..4), or 0 (runtime Cin, Cout <= 4)
 __global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ bias, int64_t R, int N, int Cin_,
-                                                          int Cout, int transw, int relu, float* __restrict__ y) {
+                                                          int Cout, int transw, int relu, const float* __restrict__ mask,
+    float* __restrict__ y) {
   __shared__ float Ws[kThinMaxW];  // Ws[o * Cin + k]
   __shared__ float bs[kLfMaxC];
   const int Cin = CINT > 0 ? CINT : Cin_;
@@ -829,7 +840,7 @@ __global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restric
         if (o0 + u < Cout) acc[u] = fmaf(xv, Ws[(o0 + u) * Cin + k], acc[u]);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = relu ? fmaxf(acc[u], 0.f) : acc[u];
+    for (int u = 0; u < 4; ++u) acc[u] = relu_mask(relu ? fmaxf(acc[u], 0.f) : acc[u], mask, r * Cout + o0 + u);
     if ((Cout & 3) == 0) {
       *reinterpret_cast<float4*>(y + r * Cout + o0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
     } else {
@@ -851,7 +862,7 @@ __global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restric
         float a = bs[o];
 #pragma unroll
         for (int k = 0; k < CINT; ++k) a = fmaf(xv[k], Ws[o * CINT + k], a);
-        yb[(int64_t)o * N] = relu ? fmaxf(a, 0.f) : a;
+        yb[(int64_t)o * N] = relu_mask(relu ? fmaxf(a, 0.f) : a, mask, (yb - y) + (int64_t)o * N);
       }
     } else {  // Cout <= 4: one coalesced row load per input channel
       float acc[4];
@@ -866,7 +877,7 @@ __global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restric
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (u < Cout) yb[(int64_t)u * N] = relu ? fmaxf(acc[u], 0.f) : acc[u];
+        if (u < Cout) yb[(int64_t)u * N] = relu_mask(relu ? fmaxf(acc[u], 0.f) : acc[u], mask, (yb - y) + (int64_t)u * N);
     }
   }
 }
@@ -874,7 +885,7 @@ __global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restric
 }  // namespace
 
 extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, int layout, int64_t R, int N,
-                             int Cin, int Cout, int transw, int relu, float* y, void* stream) {
+                             int Cin, int Cout, int transw, int relu, const float* mask, float* y, void* stream) {
   PK_REQUIRE((layout == 0 || layout == 1) && R >= 0 && Cin > 0 && Cout > 0 && Cin <= kLfMaxC && Cout <= kLfMaxC);
   PK_REQUIRE(layout == 0 || (N > 0 && R % N == 0));
   if (R == 0) return PK_OK;
@@ -884,7 +895,7 @@ extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, 
     const dim3 grid((unsigned)((threads + 255) / 256));
 #define PK_THIN(L, C)                                                                                           \
   hipLaunchKernelGGL((linear_thin_kernel<L, C>), grid, dim3(256), 0, pk::as_stream(stream), x, w, bias, R, N, Cin, \
-                     Cout, transw, relu, y)
+                     Cout, transw, relu, mask, y)
     const int ct = Cin <= 4 ? Cin : 0;  // Cin > 4 here means Cout <= 4
     if (layout == 0) {
       if (ct == 1) PK_THIN(0, 1); else if (ct == 2) PK_THIN(0, 2); else if (ct == 3) PK_THIN(0, 3);
@@ -913,7 +924,7 @@ extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, 
                 : Cin == 64 ? pick(std::integral_constant<int, 4>{}) : pick(std::integral_constant<int, 8>{});
     const size_t lds = sizeof(float) * (size_t)(16 * TO) * (Cin + 4);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, pk::as_stream(stream), x, w, bias, R, Cin, Cout, transw,
-                       relu, y);
+                       relu, mask, y);
     PK_CHECK_LAUNCH();
     return PK_OK;
   }
@@ -939,7 +950,7 @@ extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, 
     const int64_t tiles = R / (16 * sub);
     const size_t lds = sizeof(float) * (size_t)(16 * TO) * (Cin + 4);
     hipLaunchKernelGGL(kern, dim3((unsigned)((tiles + 3) / 4)), dim3(256), lds, pk::as_stream(stream), x, w, bias, R,
-                       N, Cout, transw, relu, y);
+                       N, Cout, transw, relu, mask, y);
     PK_CHECK_LAUNCH();
     return PK_OK;
   }
@@ -947,10 +958,10 @@ extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, 
   const size_t lds = sizeof(float) * (size_t)Cout * (((Cin + 3) & ~3) + 1);
   if (layout == 0)
     hipLaunchKernelGGL(linear_fwd_kernel<0>, dim3(blocks), dim3(256), lds, pk::as_stream(stream), x, w, bias, R, N,
-                       Cin, Cout, transw, relu, y);
+                       Cin, Cout, transw, relu, mask, y);
   else
     hipLaunchKernelGGL(linear_fwd_kernel<1>, dim3(blocks), dim3(256), lds, pk::as_stream(stream), x, w, bias, R, N,
-                       Cin, Cout, transw, relu, y);
+                       Cin, Cout, transw, relu, mask, y);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -50,7 +50,7 @@ SIGNATURES = {
     "pk_l2_normalize_bwd": [_P, _P, _P, _P, _I, _I, _I, _P, _P],
     "pk_mlp3_fwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P],
     "pk_resolvent_mask": [_P, _I, _P, _I, _I, _I, _F, _P, _P],
-    "pk_linear_fwd": [_P, _P, _P, _I, _I64, _I, _I, _I, _I, _I, _P, _P],
+    "pk_linear_fwd": [_P, _P, _P, _I, _I64, _I, _I, _I, _I, _I, _P, _P, _P],
     "pk_feat_dist_topk": [_P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "pk_rigidity_filter": [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P],
     "pk_inlier_ratio": [_P, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P],

@@ -19,6 +19,7 @@ from typing import Optional
 from . import ops
 
 _SIDE = None  # the active GroupedWgrad (TrainStep's backward), or None
+FOLD_RELU = True  # fold a producer layer's ReLU backward into the consumer's input gradient
 
 
 class GroupedWgrad:
@@ -99,7 +100,11 @@ class _PointwiseFn(torch.autograd.Function):
         # a fresh (non-view) output: the reference applies in-place ReLUs to it (:112-116);
         # relu=True applies the following nn.ReLU in the kernel's epilogue instead
         y = ops.linear_fwd(x, w2, bias, channels_first=cf, relu=relu)
+        # this layer's input gradient can apply the ReLU backward of the layer that produced x
+        ctx.in_relu = FOLD_RELU and getattr(x, "_pk_relu_out", False)
         ctx.save_for_backward(x, weight, y if relu else None)
+        if relu:
+            y._pk_relu_out = True
         return y
 
     @staticmethod
@@ -108,11 +113,16 @@ class _PointwiseFn(torch.autograd.Function):
         w2 = weight.view(weight.shape[0], -1)
         cf = ctx.cf
         dy = dy.contiguous()
-        if ctx.relu:  # the fused ReLU's backward (aten's ReluBackward: threshold_backward on the output)
+        if ctx.relu and not getattr(dy, "_pk_relu_masked", False):
+            # the fused ReLU's backward (aten's ReluBackward: threshold_backward on the output),
+            # unless the consuming layer already applied it in its input-gradient epilogue
             dy = torch.ops.aten.threshold_backward(dy, y, 0.0)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = ops.linear_fwd(dy, w2, None, channels_first=cf, transw=True)  # dy W (rows) / W^T dy (cf)
+            # dy W (rows) / W^T dy (cf); with in_relu the producer's ReLU backward is folded in
+            dx = ops.linear_fwd(dy, w2, None, channels_first=cf, transw=True, mask=x if ctx.in_relu else None)
+            if ctx.in_relu:
+                dx._pk_relu_masked = True
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             if _side_owns(ctx.param, ctx.bias):
                 _SIDE.launch(x, dy, ctx.param, ctx.bias, channels_first=cf)

@@ -546,7 +546,7 @@ def mlp3_fwd(x_in: torch.Tensor, x_diff: torch.Tensor, w1, b1, w2, b2, w3, b3):
 
 
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], channels_first: bool,
-               transw: bool = False, relu: bool = False) -> torch.Tensor:
+               transw: bool = False, relu: bool = False, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
     """pk_linear_fwd: y = x W^T (+ b) over every point (W [Cout, Cin], or W^T read from a
     [Cin, Cout] tensor when transw). channels_first=False: x [..., Cin] -> [..., Cout];
     True: x [B, Cin, N] -> [B, Cout, N]."""
@@ -564,8 +564,10 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], c
     assert C == Cin, (C, Cin)
     # a point moves 4 (Cin + Cout) bytes for 2 Cin Cout flops: <= 21 flop/B for these layers,
     # at or below the f32 MFMA ridge (157.3 TFLOP/s / 8 TB/s = 19.7): HBM-bound (flops beside)
+    if mask is not None and (mask.shape != y.shape or not mask.is_contiguous()):
+        raise _lib.PoseKernError("linear_fwd: mask must be contiguous and shaped like the output")
     call("pk_linear_fwd", ptr(x), ptr(w), ptr(bias), layout, int(R), int(N), int(Cin), int(Cout), int(transw),
-         int(relu), ptr(y), _lib.stream(x.device),
+         int(relu), ptr(mask), ptr(y), _lib.stream(x.device),
          work=("hbm", 4 * int(R) * (Cin + Cout) + 4 * Cin * Cout, 2 * int(R) * Cin * Cout))
     return y
 

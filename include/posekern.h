@@ -235,9 +235,11 @@ int pk_resolvent_mask(const float* evals1, int ld1, const float* evals2, int ld2
  *   read as W^T (W stored [Cin, Cout]): the input gradient dx = dy W of a layer is
  *   pk_linear_fwd(dy, W, NULL, ..., Cin = O, Cout = I, transw = 1).
  *   layout 0: x [R, Cin] -> y [R, Cout]; layout 1: x [R/N, Cin, N] -> y [R/N, Cout, N].
- *   Cin, Cout <= 128; bias may be NULL. */
+ *   Cin, Cout <= 128; bias may be NULL. mask (may be NULL; same layout as y): outputs where
+ *   mask <= 0 are written as 0 — the ReLU backward (aten threshold_backward) of the layer
+ *   feeding this one, folded into its input gradient (mask = that layer's output). */
 int pk_linear_fwd(const float* x, const float* w, const float* bias, int layout, int64_t R, int N, int Cin,
-                  int Cout, int transw, int relu, float* y, void* stream);
+                  int Cout, int transw, int relu, const float* mask, float* y, void* stream);
 
 /* H10 / H11 correspondence head. Replaces fmap2pointmap_solvers/naive.py:20-34
  * (topk = 1: dist.argmin(dim=-2)) and spacial_filtering.py:19-38 (topk = 5: the first 5

@@ -433,3 +433,28 @@ def test_resolvent_mask_matches_get_mask(device):
     for b in range(B):
         ref = get_mask(e1[b, :30].double(), e2[b, :30].double(), 0.5)
         assert (D[b] - ref).abs().max().item() <= 1e-6 * ref.abs().max().item() + 1e-12
+
+
+def test_relu_backward_folded_into_dgrad(device):
+    """The fused ReLU's backward folded into the next layer's input-gradient epilogue
+    (pk_linear_fwd mask) gives the same DiffusionNet input and parameter gradients, bit for
+    bit, as applying aten threshold_backward separately."""
+    from dpfm_amd import layers
+    from dpfm_amd.diffusion_net import DiffusionNet
+    torch.manual_seed(6)
+    net = DiffusionNet(C_in=3, C_out=32, C_width=64, N_block=2, dropout=False,
+                       with_gradient_features=False).to(device)
+    b = _to(_inputs(2, 512, 512, seed=3), device)["shape1"]
+    x = ((b["xyz"] - 110) / 50).requires_grad_(True)
+    g = torch.Generator().manual_seed(1)
+    dy = torch.randn(2, 512, 32, generator=g).to(device)
+    res = {}
+    for fold in (True, False):
+        layers.FOLD_RELU = fold
+        net.zero_grad(set_to_none=True)
+        x.grad = None
+        net(x, b["mass"], evals=b["evals"], evecs=b["evecs"]).backward(dy)
+        res[fold] = [x.grad.clone()] + [p.grad.clone() for p in net.parameters()]
+    layers.FOLD_RELU = True
+    for a, c in zip(res[True], res[False]):
+        assert torch.equal(a, c)
