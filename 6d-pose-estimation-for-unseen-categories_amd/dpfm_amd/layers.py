@@ -34,9 +34,11 @@ class GroupedWgrad:
     stays on one stream: a single-stream HIP graph replays without cross-queue
     dependencies (a forked side stream measured slower on MI355X)."""
 
-    def __init__(self, params):
+    def __init__(self, params, bufs=None):
         self.params = [p for p in params]
-        self.bufs = {id(p): torch.zeros_like(p, memory_format=torch.contiguous_format) for p in self.params}
+        # persistent .grad buffers (optionally the caller's, e.g. views of one flat buffer)
+        self.bufs = {id(p): (bufs[id(p)] if bufs is not None else
+                             torch.zeros_like(p, memory_format=torch.contiguous_format)) for p in self.params}
         self.seen = set()
         self.calls = []
 

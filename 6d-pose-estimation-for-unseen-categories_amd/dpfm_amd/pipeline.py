@@ -132,6 +132,14 @@ class TrainStep:
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed)
         self.flat = torch.zeros(sum(p.numel() for p in self.params), dtype=torch.float32, device=dev)
+        # HIP devices: every .grad is a view of `flat` (zeroed at the start of each backward),
+        # so DDP's all-reduce is one collective on `flat` with no gather / scatter copies
+        self.flat_grads = dev.type == "cuda"
+        self.gviews = []
+        o = 0
+        for p in self.params:
+            self.gviews.append(self.flat[o:o + p.numel()].view_as(p))
+            o += p.numel()
         # clip + RMSprop in one HIP launch on HIP devices (torch's optimizer keeps the state)
         self.fused_opt = fused_opt and dev.type == "cuda" and len(self.params) <= 96
         # grouped=True (HIP devices): the per-point layers' weight gradients are recorded during
@@ -145,7 +153,8 @@ class TrainStep:
         self.side = None
         if grouped and dev.type == "cuda":
             lin = [p for m in model.modules() if isinstance(m, (Linear, Conv1d)) for p in m.parameters(recurse=False)]
-            self.side = GroupedWgrad(lin)
+            self.side = GroupedWgrad(lin, bufs={id(p): v for p, v in zip(self.params, self.gviews)}
+                                     if self.flat_grads else None)
 
     def nce_counter(self) -> torch.Tensor:
         """The device step counter keying this step's NCE pair draws (utils/loss.py)."""
@@ -176,6 +185,10 @@ class TrainStep:
         """DDP's gradient averaging in one bucket (49,281 f32 = 197 KB: latency-bound).
         `grads` defaults to the parameters' .grad tensors."""
         if self.world <= 1:
+            return
+        if self.flat_grads:  # the gradients ARE views of flat: one collective, one scale
+            dist.all_reduce(self.flat, group=self.group)
+            self.flat.div_(self.world)
             return
         grads = grads if grads is not None else [p.grad for p in self.params]
         o = 0
@@ -211,6 +224,10 @@ class TrainStep:
             p_pred = naive_p2p_batched(C_pred.detach(), op.cad_evecs, op.pc_evecs)
             npred = torch.full((p_pred.shape[0],), p_pred.shape[2], dtype=torch.int32, device=p_pred.device)
             ir = ops.inlier_ratio(p_pred, npred, op.cad_xyz, crops.align32, op.ir_thr, layout=1).mean()
+        if self.flat_grads:  # accumulate into the flat buffer's views (autograd adds in place)
+            self.flat.zero_()
+            for p, v in zip(self.params, self.gviews):
+                p.grad = v
         if self.side is not None:
             self.side.begin()
         ok = False

@@ -30,7 +30,7 @@ for step in "$@"; do
     kprof) run kprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kprof" -o run -- python tools/kbench.py
           find "$out/kprof" -type f ! -name "*stats.csv" -delete ;;
     pmcm) run pmcm 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$out/pmcm" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager --probe-steps 1
-          python tools/mfma_util.py "$out/pmcm" fd_main_kernel attn_fwd attn_bwd wgrad_v2 > "$out/mfma_util_step.json" 2>&1
+          python tools/mfma_util.py "$out/pmcm" fd_main_kernel attn_fwd attn_bwd wgrad_grouped_kernel linear_fwd_rows linear_fwd_cf nce_pass > "$out/mfma_util_step.json" 2>&1
           find "$out/pmcm" -type f -name "*.csv" -size +2M -delete ;;
     pmc) run pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$out/pmcf" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager --probe-steps 1
          run pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$out/pmcw" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager --probe-steps 1

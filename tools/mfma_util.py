@@ -9,6 +9,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 SIMDS = 1024  # 256 CUs x 4 SIMDs (MI355X)
@@ -31,7 +32,8 @@ def main():
         if k is None or "SQ_VALU_MFMA_BUSY_CYCLES" not in c or "GRBM_GUI_ACTIVE" not in c:
             continue
         busy, gui = sum(c["SQ_VALU_MFMA_BUSY_CYCLES"]), max(c["GRBM_GUI_ACTIVE"])
-        out[(n.split("(")[0][-60:], grids[did])].append(busy / (gui * SIMDS))
+        short = re.split(r"[(<]", n.replace("(anonymous namespace)::", "").replace("void ", ""))[0][-60:]
+        out[(short, grids[did])].append(busy / (gui * SIMDS))
     res = {f"{n} grid={g}": {"mfma_util": round(sum(v) / len(v), 4), "dispatches": len(v)} for (n, g), v in out.items()}
     print(json.dumps(res, indent=1))
 
