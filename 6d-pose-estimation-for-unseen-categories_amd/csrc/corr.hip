@@ -288,9 +288,85 @@ __global__ __launch_bounds__(256) void cgt_reduce_kernel(const double* __restric
   }
 }
 
+// Minimum-norm least squares for a rank-deficient (or empty) pair list, the solution
+// torch.linalg.lstsq's CPU driver (LAPACK gelsy: complete orthogonal factorization) returns:
+// X = V diag(w) V^T H with G = V diag(lambda) V^T (cyclic Jacobi, fp64) and w_i = 1/lambda_i
+// for lambda_i > rcond^2 lambda_max (sigma_i > rcond sigma_max of A), else 0; rcond =
+// eps_f32 * max(P, 30), torch's default for f32 inputs. One wave; lane k < 30 owns index k.
+__device__ void cgt_min_norm(const double* __restrict__ gh, int64_t npairs, float* __restrict__ out) {
+  __shared__ double G[kF][kF + 1], V[kF][kF + 1], Hs[kF][kF + 1], Ts[kF][kF + 1];
+  const int k = threadIdx.x;
+  const bool ok = k < kF;
+  if (ok) {
+    for (int c = 0; c < kF; ++c) {
+      G[k][c] = gh[k * 2 * kF + c];
+      Hs[k][c] = gh[k * 2 * kF + kF + c];
+      V[k][c] = k == c ? 1.0 : 0.0;
+    }
+  }
+  __syncthreads();
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    double off = 0.0, dia = 0.0;
+    if (ok)
+      for (int c = 0; c < kF; ++c) {
+        const double g = G[k][c];
+        if (c == k) dia += g * g; else off += g * g;
+      }
+    off = pk::wave_sum_f64(off);
+    dia = pk::wave_sum_f64(dia);
+    if (!(off > 1e-32 * dia)) break;  // converged (also: all-zero G)
+    for (int p = 0; p < kF - 1; ++p)
+      for (int q = p + 1; q < kF; ++q) {
+        const double apq = G[p][q];
+        if (fabs(apq) <= 1e-300) continue;  // uniform: every lane read the same LDS word
+        const double theta = (G[q][q] - G[p][p]) / (2.0 * apq);
+        const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+        __syncthreads();
+        if (ok) {  // A J (columns p, q), V J
+          const double gp = G[k][p], gq = G[k][q];
+          G[k][p] = c * gp - s * gq;
+          G[k][q] = s * gp + c * gq;
+          const double vp = V[k][p], vq = V[k][q];
+          V[k][p] = c * vp - s * vq;
+          V[k][q] = s * vp + c * vq;
+        }
+        __syncthreads();
+        if (ok) {  // J^T (A J) (rows p, q)
+          const double gp = G[p][k], gq = G[q][k];
+          G[p][k] = c * gp - s * gq;
+          G[q][k] = s * gp + c * gq;
+        }
+        __syncthreads();
+      }
+  }
+  double lam = ok ? G[k][k] : 0.0;
+  double lmax = lam;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) lmax = fmax(lmax, __shfl_xor(lmax, o));
+  const double rcond = 1.1920928955078125e-07 * (double)(npairs > kF ? npairs : kF);
+  const double w = (ok && lam > rcond * rcond * lmax && lam > 0.0) ? 1.0 / lam : 0.0;
+  if (ok)  // T = diag(w) V^T H: row k
+    for (int c = 0; c < kF; ++c) {
+      double acc = 0.0;
+      for (int j = 0; j < kF; ++j) acc = fma(V[j][k], Hs[j][c], acc);
+      Ts[k][c] = w * acc;
+    }
+  __syncthreads();
+  if (ok)  // X = V T: row k
+    for (int c = 0; c < kF; ++c) {
+      double acc = 0.0;
+      for (int j = 0; j < kF; ++j) acc = fma(V[k][j], Ts[j][c], acc);
+      out[k * kF + c] = (float)acc;
+    }
+}
+
 // grid (B), block 64 (one wave): Gauss-Jordan with partial pivoting on [G | H]. Lane l holds
-// row r = l & 31 (r < 30), columns 30 h .. 30 h + 29 with h = l >> 5, in registers.
-__global__ __launch_bounds__(64) void cgt_solve_kernel(const double* __restrict__ GH, float* __restrict__ Cgt) {
+// row r = l & 31 (r < 30), columns 30 h .. 30 h + 29 with h = l >> 5, in registers. A crop
+// whose pivots span more than 1e6 (rank-deficient or nearly so: fewer than 30 distinct
+// matched crop rows, or no pairs) takes the minimum-norm path above instead.
+__global__ __launch_bounds__(64) void cgt_solve_kernel(const double* __restrict__ GH, const int64_t* __restrict__ npairs,
+                                                       int ldp, float* __restrict__ Cgt) {
   __shared__ double piv_s[2 * kF];
   const int b = blockIdx.x, lane = threadIdx.x;
   const int r = lane & 31, h = lane >> 5;
@@ -300,6 +376,7 @@ __global__ __launch_bounds__(64) void cgt_solve_kernel(const double* __restrict_
   for (int c = 0; c < kF; ++c) a[c] = row_ok ? GH[(int64_t)b * 2 * kFF + r * 2 * kF + h * kF + c] : 0.0;
   bool used = !row_ok;
   int var = -1;
+  double pmin = __builtin_inf(), pmax = 0.0;
   for (int k = 0; k < kF; ++k) {
     // pivot: max |G[r][k]| over unused rows (half-0 lanes), lowest row on ties
     double ak = 0.0;  // a[k] through static indices (no scratch)
@@ -318,6 +395,8 @@ __global__ __launch_bounds__(64) void cgt_solve_kernel(const double* __restrict_
     }
     const int p = __shfl(who, 0);
     const double pivot = __shfl(ak, p);  // G[p][k] from half 0
+    pmin = fmin(pmin, fabs(pivot));
+    pmax = fmax(pmax, fabs(pivot));
     const double f0 = (row_ok && r != p) ? ak / pivot : 0.0;
     const double f = __shfl(f0, r);        // half-1 lanes take their row's factor
     if (r == p) {
@@ -337,6 +416,11 @@ __global__ __launch_bounds__(64) void cgt_solve_kernel(const double* __restrict_
       var = k;
     }
     __builtin_amdgcn_wave_barrier();
+  }
+  if (!(pmin > 1e-6 * pmax)) {  // wave-uniform: rank-deficient, empty or non-finite
+    const int64_t n = npairs[b] < ldp ? npairs[b] : ldp;
+    cgt_min_norm(GH + (int64_t)b * 2 * kFF, n, Cgt + (int64_t)b * kFF);
+    return;
   }
   if (h == 1 && var >= 0) {
 #pragma unroll
@@ -426,7 +510,7 @@ extern "C" int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs
   hipLaunchKernelGGL(cgt_reduce_kernel, dim3((2 * kFF + 63) / 64, B), dim3(256), 0, s, partH, partG, SH, SG,
                      npairs, ldp, V2max, GH);
   PK_CHECK_LAUNCH();
-  hipLaunchKernelGGL(cgt_solve_kernel, dim3(B), dim3(64), 0, s, GH, Cgt);
+  hipLaunchKernelGGL(cgt_solve_kernel, dim3(B), dim3(64), 0, s, GH, npairs, ldp, Cgt);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -440,7 +440,9 @@ __global__ void npoint_kernel(const int64_t* __restrict__ off, int B, int fixed,
     const int n = (int)(off[b + 1] - off[b]);
     int np;
     if (fixed > 0) {
-      np = fixed;
+      // a fixed target acts as the reference's limit without its int(ratio * n) rounding:
+      // FPS to exactly `fixed` when the crop is larger, every point (in order) otherwise
+      np = n > fixed ? fixed : -n;
     } else if (n > limit) {
       const double ratio = (double)limit / (double)n;  // object.py:146
       np = (int)(ratio * (double)n);                   // int(ratio * N) in upstream FPS
@@ -492,7 +494,42 @@ __global__ __launch_bounds__(256) void gather_transform_kernel(
   }
 }
 
+// collate (dataset/helpers.py:22-50) for one packed field: torch.Tensor(x) (-> f32) then
+// pad_sequence(batch_first=True) with zeros. grid (ceil(ld*C/256), B); crop b's rows
+// [0, min(n_b, ld)) are copied (cast to f32), rows up to ld are zero.
+template <typename T>
+__global__ __launch_bounds__(256) void collate_pad_kernel(const T* __restrict__ src, int C,
+                                                          const int64_t* __restrict__ off, int ld,
+                                                          float* __restrict__ dst, int32_t* __restrict__ counts) {
+  const int b = blockIdx.y;
+  const int64_t o = off[b];
+  const int64_t n = off[b + 1] - o;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (counts != nullptr && blockIdx.x == 0 && threadIdx.x == 0) counts[b] = (int32_t)(n < ld ? n : ld);
+  if (e >= (int64_t)ld * C) return;
+  const int64_t row = e / C;
+  dst[(int64_t)b * ld * C + e] = row < n ? (float)src[o * C + e] : 0.f;
+}
+
 }  // namespace
+
+extern "C" int pk_collate_pad(const void* src, int src_f64, int C, const int64_t* off, int B, int ld, float* dst,
+                              int32_t* counts, void* stream) {
+  PK_REQUIRE(B >= 0 && C > 0 && ld >= 0);
+  if (B == 0) return PK_OK;
+  PK_REQUIRE(off && (dst || ld == 0) && (src || ld == 0));
+  if (ld == 0 && counts == nullptr) return PK_OK;
+  dim3 grid((unsigned)(((int64_t)ld * C + 255) / 256 > 0 ? ((int64_t)ld * C + 255) / 256 : 1), B);
+  hipStream_t s = pk::as_stream(stream);
+  if (src_f64)
+    hipLaunchKernelGGL(collate_pad_kernel<double>, grid, dim3(256), 0, s, static_cast<const double*>(src), C, off, ld,
+                       dst, counts);
+  else
+    hipLaunchKernelGGL(collate_pad_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(src), C, off, ld,
+                       dst, counts);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
 
 extern "C" int pk_backproject(const uint16_t* depth, const uint8_t* mask, int F, int H, int W,
                               const double* K, const float* cam_scale, int32_t* rowcnt,

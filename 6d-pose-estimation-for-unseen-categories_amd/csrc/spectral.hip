@@ -79,16 +79,19 @@ __global__ __launch_bounds__(1024) void spec_combine_kernel(const float* __restr
                                                             float* __restrict__ scaled,
                                                             const float* __restrict__ saved,
                                                             float* __restrict__ gt) {
-  __shared__ float gsum[16][kKC];
+  __shared__ double gsum[16][kKC];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int c = tid & 63, k0 = (tid >> 6) * 4;
   const float* pb = part + (int64_t)b * S * kKC * kKC + k0 * kKC + c;
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  // the S slab partials (64 rows each) are summed in fp64: at N ~ 5000 CAD vertices a serial
+  // fp32 sum over ~80 slabs dominated the error of the diffusion-time gradient, a
+  // cancellation-prone contraction of two such sums
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
   for (int s = 0; s < S; ++s) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] += pb[(int64_t)s * kKC * kKC + i * kKC];
+    for (int i = 0; i < 4; ++i) v[i] += (double)pb[(int64_t)s * kKC * kKC + i * kKC];
   }
-  float g = 0.f;
+  double g = 0.0;
   const float tc = t[c];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -96,18 +99,19 @@ __global__ __launch_bounds__(1024) void spec_combine_kernel(const float* __restr
     const float lam = evals[b * kKC + k];
     const float E = expf(-lam * tc);
     const int64_t o = (int64_t)b * kKC * kKC + k * kKC + c;
-    if (raw) raw[o] = v[i];
-    scaled[o] = E * v[i];
-    if (gt) g = fmaf(-lam * E, saved[o] * v[i], g);
+    const float vf = (float)v[i];
+    if (raw) raw[o] = vf;
+    scaled[o] = E * vf;
+    if (gt) g = fma(-(double)lam * (double)E, (double)saved[o] * v[i], g);
   }
   if (gt) {
     gsum[tid >> 6][c] = g;
     __syncthreads();
     if (tid < kKC) {
-      float a = 0.f;
+      double a = 0.0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) a += gsum[q][c];
-      gt[b * kKC + c] = a;
+      gt[b * kKC + c] = (float)a;
     }
   }
 }

@@ -129,54 +129,91 @@ class FrameBatch:
     cam_scale: torch.Tensor  # f32 [F] = 1000 / depth_scale
     R: torch.Tensor          # f64 [F, 9] R_m2c row-major
     t: torch.Tensor          # f64 [F, 3] t_m2c (cm)
-    cad64: torch.Tensor      # f64 [F * N1, 3] CAD vertices (cm), packed
+    cad64: torch.Tensor      # f64 [sum N1_f, 3] CAD vertices (cm), packed
     cad_off: torch.Tensor    # int64 [F + 1]
     diam: list               # host floats (cm), models_info diameter * 0.1
     max_pixels: int          # host bound on mask pixels per frame (kernel grid sizing)
     thr2: torch.Tensor       # f64 [F] ball-query threshold T(0.05 * diam) (ops.ball_threshold)
+    n1max: int = 0           # largest CAD (collate's padded CAD length)
 
 
 @dataclass
 class Crops:
-    pc64: torch.Tensor       # f64 [F*N2, 3] crop points, camera frame (pcd_depth)
-    pc32: torch.Tensor       # f32 [F, N2, 3] (PC xyz fed to the model, object.py:263)
-    align64: torch.Tensor    # f64 [F*N2, 3] crop in the object frame (align_pc)
-    align32: torch.Tensor    # f32 [F, N2, 3]
+    """One batch of formed crops. Packed fields hold crop b in rows off[b]..off[b+1]; the
+    model-facing fields are collate's zero-padded [F, ld, .] layout (dataset/helpers.py:22-50)."""
+    pc64: torch.Tensor       # f64 packed [*, 3] crop points, camera frame (pcd_depth)
+    pc32: torch.Tensor       # f32 [F, ld, 3] PC xyz fed to the model (object.py:263), zero-padded
+    align64: torch.Tensor    # f64 packed [*, 3] crop in the object frame (align_pc)
+    align32: torch.Tensor    # f32 [F, ld, 3] Obj["align_pc"] after collate
     off: torch.Tensor        # int64 [F + 1] packed offsets of the crops
-    npoint: torch.Tensor     # int32 [F]
+    n2: torch.Tensor         # int32 [F] points per crop (the rows of pc32 that are not padding)
+    ld: int                  # padded crop length (the batch maximum when pad="batch")
+    npoint: torch.Tensor     # int32 [F] FPS policy (negative: every point kept, no FPS)
     pairs: torch.Tensor      # int64 [F, cap, 2] P (CAD idx, PC idx), row-major
-    npairs: torch.Tensor     # int64 [F]
-    overlap_12: torch.Tensor  # int8 [F, N1]
-    overlap_21: torch.Tensor  # int8 [F, N2]
-    rgb: torch.Tensor        # f32 [F*N2, 3] colour at each crop point (H16)
+    npairs: torch.Tensor     # int64 [F] true pair counts (> pair_cap: truncated, see overflow)
+    overlap_12: torch.Tensor  # int8 [F, N1max]
+    overlap_21: torch.Tensor  # int8 [F, ld]
+    rgb: Optional[torch.Tensor]  # f32 [*, C] colour at each packed crop point (H16) or None
     kept: torch.Tensor       # int64 [F] points after outlier removal
+    pair_cap: int = 0
+
+    def overflow(self) -> torch.Tensor:
+        """0-d bool on the device: some crop had more ball-query pairs than pair_cap (its P
+        was truncated). No host sync; `check()` raises on it."""
+        return (self.npairs > self.pair_cap).any()
+
+    def check(self) -> None:
+        """Host-synchronising: raise if a pair list overflowed its capacity."""
+        ops.check_capacity(self.npairs, self.pair_cap, "ball-query pairs (CropFormation pair_cap)")
 
 
 class CropFormation:
-    """Frames -> model-ready crops for a whole batch (fixed npoint, as the benchmark
-    configs; `npoint=0` switches to the reference's int(2000/n*n) policy)."""
+    """Frames -> model-ready crops for a whole batch, with the reference's sample policy
+    (dataset/object.py:145-148) and collate's padding (dataset/helpers.py:22-50).
 
-    def __init__(self, n1: int, npoint: int = 1024, pair_cap: Optional[int] = None, seed: int = 0,
-                 with_mask: bool = True):
-        self.n1, self.npoint = n1, npoint
-        self.pair_cap = pair_cap or 64 * max(npoint, 1)
+    npoint = 0: the reference policy — FPS to int(2000/n*n) points (1999 or 2000) when the
+    crop has more than `limit` = 2000 points, every point otherwise (ragged crops).
+    npoint > 0: a fixed target — FPS to exactly `npoint` when the crop is larger, every
+    point otherwise (the benchmark configs' 1024 / 2048 / 4096-point crops).
+
+    pad = "batch": pad to the largest crop of the batch, exactly collate's pad_sequence
+    (one host read of the per-crop counts; eager use). pad = "fixed": pad to the policy's
+    maximum (npoint, or `limit`), no host synchronisation (HIP-graph capture); identical to
+    collate whenever some crop reaches that maximum, otherwise the model sees more zero
+    padding than the reference would. Default: "fixed" for npoint > 0, "batch" for 0."""
+
+    def __init__(self, n1: int = 0, npoint: int = 1024, pair_cap: Optional[int] = None, seed: int = 0,
+                 with_mask: bool = True, pad: Optional[str] = None, limit: int = 2000, with_rgb: bool = False):
+        self.n1, self.npoint, self.limit = n1, npoint, limit
+        self.npmax = npoint if npoint > 0 else limit
+        self.pair_cap = pair_cap or 64 * self.npmax
         self.seed = seed
         self.with_mask = with_mask
+        self.pad = pad or ("fixed" if npoint > 0 else "batch")
+        if self.pad not in ("batch", "fixed"):
+            raise ValueError("pad must be 'batch' or 'fixed'")
+        self.with_rgb = with_rgb
 
     def __call__(self, fb: FrameBatch) -> Crops:
         F_, H, W = fb.depth.shape
-        dev = fb.depth.device
         bp = ops.backproject(fb.depth, fb.mask, fb.K, fb.cam_scale, cap=F_ * fb.max_pixels)
-        so = ops.sor(bp["xyz"], bp["off"], fb.max_pixels, 20, 0.3, pix=bp["pix"], idxmap=bp["idxmap"], K=fb.K)
-        pol = ops.fps_npoint(so["off"], fixed=self.npoint, limit=2000, seed=self.seed)
-        npmax = self.npoint if self.npoint > 0 else 2000
+        so = ops.sor(bp["xyz"], bp["off"], fb.max_pixels, 20, 0.3, pix=bp["pix"], idxmap=bp["idxmap"], K=fb.K,
+                     want64=True, want32=True)
+        pol = ops.fps_npoint(so["off"], fixed=self.npoint, limit=self.limit, seed=self.seed)
+        npmax = self.npmax
+        if self.pad == "batch":  # collate pads to the batch maximum: read it (host sync)
+            ld = int((pol["off"][1:] - pol["off"][:-1]).max().item()) if F_ > 0 else 0
+        else:
+            ld = npmax
         idx = ops.fps_packed(so["xyz32"], so["off"], fb.max_pixels, pol["start"], pol["npoint"], npmax)
         g = ops.gather_transform(so["xyz64"], so["off"], idx, pol["npoint"], npmax, pol["off"], fb.R, fb.t,
-                                 F_ * npmax)
-        bq = ops.ball_query(fb.cad64, fb.cad_off, g["align"], pol["off"], None, self.n1, npmax, self.pair_cap,
+                                 F_ * npmax, want_sel32=False)
+        pc32, n2 = ops.collate_pad(g["sel64"], pol["off"], ld)       # PC["xyz"]: f32(pcd), padded
+        align32, _ = ops.collate_pad(g["align"], pol["off"], ld)     # Obj["align_pc"]
+        n1max = fb.n1max or self.n1
+        bq = ops.ball_query(fb.cad64, fb.cad_off, g["align"], pol["off"], None, n1max, ld, self.pair_cap,
                             with_mask=self.with_mask, thr2=fb.thr2)
-        rgb = ops.sample_rgb(fb.rgb, fb.K, g["sel64"], pol["off"], npmax)
-        return Crops(pc64=g["sel64"], pc32=g["sel32"].view(F_, npmax, 3), align64=g["align"],
-                     align32=g["align"].float().view(F_, npmax, 3), off=pol["off"], npoint=pol["npoint"],
-                     pairs=bq["pairs"], npairs=bq["count"], overlap_12=bq["overlap_12"], overlap_21=bq["overlap_21"],
-                     rgb=rgb, kept=so["kept"])
+        rgb = ops.sample_rgb(fb.rgb, fb.K, g["sel64"], pol["off"], npmax) if self.with_rgb else None
+        return Crops(pc64=g["sel64"], pc32=pc32, align64=g["align"], align32=align32, off=pol["off"], n2=n2, ld=ld,
+                     npoint=pol["npoint"], pairs=bq["pairs"], npairs=bq["count"], overlap_12=bq["overlap_12"],
+                     overlap_21=bq["overlap_21"], rgb=rgb, kept=so["kept"], pair_cap=self.pair_cap)

@@ -174,6 +174,26 @@ def ctypes_u64(v: int):
     return ctypes.c_uint64(int(v) & 0xFFFFFFFFFFFFFFFF)
 
 
+def collate_pad(src: torch.Tensor, off: torch.Tensor, ld: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """collate (dataset/helpers.py:22-50) of one packed field on the device (pk_collate_pad):
+    src f64 / f32 [T, C] packed by off [B+1] -> (f32 [B, ld, C] zero-padded, counts int32 [B]).
+    ld = the batch maximum count reproduces collate's pad_sequence exactly."""
+    if src.dtype not in (torch.float32, torch.float64):
+        raise _lib.PoseKernError("collate_pad: f32 / f64 sources only")
+    src2 = src.reshape(src.shape[0], -1) if src.dim() != 1 else src[:, None]
+    C = int(src2.shape[1]) if src2.dim() == 2 and src2.shape[1] > 0 else 1
+    B = off.numel() - 1
+    dev = off.device
+    dst = torch.empty((B, int(ld), C), dtype=torch.float32, device=dev)
+    counts = torch.empty((B,), dtype=torch.int32, device=dev)
+    if src2.numel() == 0:  # every crop empty: keep a valid pointer (no row is read)
+        src2 = torch.zeros((1, C), dtype=src.dtype, device=dev)
+    call("pk_collate_pad", ptr(src2.contiguous()), int(src.dtype == torch.float64), C,
+         ptr(off), B, int(ld), ptr(dst) if dst.numel() else None, ptr(counts), _lib.stream(dev),
+         work=("hbm", (src.element_size() + 4) * B * int(ld) * C))
+    return dst, counts
+
+
 def gather_transform(pcd: torch.Tensor, off: torch.Tensor, idx: Optional[torch.Tensor], npoint: torch.Tensor,
                      npmax: int, out_off: torch.Tensor, R: torch.Tensor, t: torch.Tensor, total_cap: int,
                      want_sel64: bool = True, want_align: bool = True, want_sel32: bool = True) -> dict:

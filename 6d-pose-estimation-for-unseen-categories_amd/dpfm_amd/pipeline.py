@@ -46,6 +46,32 @@ class Operators:
     pc_evecs: torch.Tensor   # f32 [F, N2, 64]
     ir_thr: torch.Tensor     # f32 [F] 0.1 * diam (train.py:115)
     rig_thr: torch.Tensor    # f32 [F, 4] spatial-filter thresholds
+    cad_n: Optional[torch.Tensor] = None  # int32 [F] CAD vertices per crop (rows of cad_* not padding)
+
+
+def pad_rows(arrs, ld: Optional[int] = None) -> np.ndarray:
+    """collate's pad_sequence on host arrays: stack along a new batch axis, zero-padding the
+    first axis to `ld` (default: the longest)."""
+    ld = max(a.shape[0] for a in arrs) if ld is None else ld
+    out = np.zeros((len(arrs), ld) + arrs[0].shape[1:], dtype=arrs[0].dtype)
+    for b, a in enumerate(arrs):
+        out[b, :a.shape[0]] = a
+    return out
+
+
+def crop_operators(op: Operators, crops: Crops, seed: int) -> Operators:
+    """Operators whose crop part matches the formed crops' true sizes: per crop the cached
+    pc_LBO of a crop of n2 points (dataset/object.py:240-269; the synthetic stand-in of
+    lbo_operators), zero-padded to crops.ld as collate pads them. Reads the crop sizes
+    (host sync): the reference computes these operators per crop, offline, from the crop."""
+    counts = crops.n2.cpu().numpy().tolist()
+    dev = crops.pc32.device
+    ops_p = [lbo_padded(int(n), 2 * (seed + b) + 1) for b, n in enumerate(counts)]
+    pm = torch.as_tensor(pad_rows([o[0] for o in ops_p], crops.ld), device=dev)
+    pv = torch.as_tensor(pad_rows([o[2] for o in ops_p], crops.ld), device=dev)
+    pe = torch.as_tensor(np.stack([o[1] for o in ops_p]), device=dev)
+    return Operators(cad_mass=op.cad_mass, cad_evals=op.cad_evals, cad_evecs=op.cad_evecs, cad_xyz=op.cad_xyz,
+                     pc_mass=pm, pc_evals=pe, pc_evecs=pv, ir_thr=op.ir_thr, rig_thr=op.rig_thr, cad_n=op.cad_n)
 
 
 def make_frame_batch(F: int, n1: int, n2: int, seed: int, device) -> tuple[FrameBatch, Operators]:
@@ -72,7 +98,8 @@ def make_frame_batch(F: int, n1: int, n2: int, seed: int, device) -> tuple[Frame
                     R=T(R, torch.float64), t=T(t, torch.float64),
                     cad64=torch.as_tensor(np.concatenate(cad, 0), dtype=torch.float64, device=d),
                     cad_off=ops.packed_offsets([n1] * F, d), diam=diam, max_pixels=maxpix,
-                    thr2=torch.tensor([ops.ball_threshold(0.05 * x) for x in diam], dtype=torch.float64, device=d))
+                    thr2=torch.tensor([ops.ball_threshold(0.05 * x) for x in diam], dtype=torch.float64, device=d),
+                    n1max=n1)
     # CAD and crop operators of the batch in ONE buffer each ([CAD; crops] along the batch):
     # the model's shared encoder pass over both shapes then needs no concatenation copy
     def joint(k):
@@ -84,8 +111,63 @@ def make_frame_batch(F: int, n1: int, n2: int, seed: int, device) -> tuple[Frame
     op = Operators(cad_mass=cm, cad_evals=ce, cad_evecs=cv, cad_xyz=T([c.astype(np.float32) for c in cad]),
                    pc_mass=pm, pc_evals=pe, pc_evecs=pv,
                    ir_thr=torch.tensor([np.float32(0.1 * x) for x in diam], dtype=torch.float32, device=d),
-                   rig_thr=ops.rigidity_thresholds(diam, d))
+                   rig_thr=ops.rigidity_thresholds(diam, d),
+                   cad_n=torch.full((F,), n1, dtype=torch.int32, device=d))
     return fb, op
+
+
+def frame_batch(frames: list, device) -> FrameBatch:
+    """FrameBatch from per-frame dicts with the fields the reference's datasets read
+    (dataset/scene.py:125-158, object.py:133-164): depth uint16 [H, W], mask uint8 [H, W]
+    (mask_visib, 255 = object), K [3, 3], depth_scale, R_m2c [3, 3], t_m2c [3] (cm), cad f64
+    [n1, 3] (cm, the decimated CAD vertices; ragged across frames), diam_cad (cm); rgb uint8
+    [H, W, 3] optional."""
+    d = torch.device(device)
+    st = lambda key, dt: torch.as_tensor(np.stack([np.asarray(f[key], dtype=dt) for f in frames]), device=d)  # noqa
+    H, W = np.asarray(frames[0]["depth"]).shape[:2]
+    rgb = [np.asarray(f["rgb"], dtype=np.uint8) if f.get("rgb") is not None else np.zeros((H, W, 3), np.uint8)
+           for f in frames]
+    cads = [np.asarray(f["cad"], dtype=np.float64).reshape(-1, 3) for f in frames]
+    diam = [float(f["diam_cad"]) for f in frames]
+    return FrameBatch(
+        depth=torch.as_tensor(np.stack([np.asarray(f["depth"], dtype=np.uint16).view(np.int16) for f in frames]),
+                              device=d),
+        mask=st("mask", np.uint8), rgb=torch.as_tensor(np.stack(rgb), device=d),
+        K=torch.as_tensor(np.stack([np.asarray(f["K"], np.float64).reshape(9) for f in frames]), device=d),
+        cam_scale=torch.tensor([np.float32(1000.0 / f["depth_scale"]) for f in frames], dtype=torch.float32,
+                               device=d),
+        R=torch.as_tensor(np.stack([np.asarray(f["R_m2c"], np.float64).reshape(9) for f in frames]), device=d),
+        t=torch.as_tensor(np.stack([np.asarray(f["t_m2c"], np.float64).reshape(3) for f in frames]), device=d),
+        cad64=torch.as_tensor(np.concatenate(cads, 0), device=d), cad_off=ops.packed_offsets([len(c) for c in cads], d),
+        diam=diam, max_pixels=max(int((np.asarray(f["mask"]) == 255).sum()) for f in frames),
+        thr2=torch.tensor([ops.ball_threshold(0.05 * x) for x in diam], dtype=torch.float64, device=d),
+        n1max=max(len(c) for c in cads))
+
+
+def lbo_padded(n: int, seed: int, k: int = 64):
+    """Synthetic stand-in of one shape's cached LBO operators (mass [n], evals [k], evecs
+    [n, k]); fewer than k points leave the missing eigenvectors as zero columns."""
+    m, e, v = lbo_operators(max(n, 1), k, seed)
+    if v.shape[1] < k:
+        v = np.concatenate([v, np.zeros((v.shape[0], k - v.shape[1]), np.float32)], 1)
+    return m[:n], e, v[:n]
+
+
+def operators_for(cads: list, crop_counts: list, diam: list, seed: int, device, ld2: Optional[int] = None) -> Operators:
+    """Operators of a ragged batch, padded as collate pads them: CAD b (f64 [n1_b, 3], cm)
+    with lbo_padded(n1_b, 2 (seed + b)), crop b with lbo_padded(n2_b, 2 (seed + b) + 1)."""
+    d = torch.device(device)
+    oc = [lbo_padded(len(c), 2 * (seed + b)) for b, c in enumerate(cads)]
+    op_ = [lbo_padded(int(n), 2 * (seed + b) + 1) for b, n in enumerate(crop_counts)]
+    T = lambda a: torch.as_tensor(a, device=d)  # noqa: E731
+    return Operators(cad_mass=T(pad_rows([o[0] for o in oc])), cad_evals=T(np.stack([o[1] for o in oc])),
+                     cad_evecs=T(pad_rows([o[2] for o in oc])),
+                     cad_xyz=T(pad_rows([np.asarray(c, np.float64).astype(np.float32) for c in cads])),
+                     pc_mass=T(pad_rows([o[0] for o in op_], ld2)), pc_evals=T(np.stack([o[1] for o in op_])),
+                     pc_evecs=T(pad_rows([o[2] for o in op_], ld2)),
+                     ir_thr=torch.tensor([np.float32(0.1 * x) for x in diam], dtype=torch.float32, device=d),
+                     rig_thr=ops.rigidity_thresholds(diam, d),
+                     cad_n=torch.tensor([len(c) for c in cads], dtype=torch.int32, device=d))
 
 
 def model_batch(op: Operators, crops: Crops) -> dict:
@@ -97,13 +179,21 @@ def model_batch(op: Operators, crops: Crops) -> dict:
     return {"shape1": cad, "shape2": pc}
 
 
-def naive_p2p_batched(C: torch.Tensor, evecs_x: torch.Tensor, evecs_y: torch.Tensor) -> torch.Tensor:
-    """naive_fmap2pointmap for every crop: int64 [B, 2, V2] (row 0 CAD idx, row 1 arange)."""
+def _counts(n: Optional[torch.Tensor], B: int, full: int, dev) -> torch.Tensor:
+    return n.to(torch.int32) if n is not None else torch.full((B,), full, dtype=torch.int32, device=dev)
+
+
+def naive_p2p_batched(C: torch.Tensor, evecs_x: torch.Tensor, evecs_y: torch.Tensor,
+                      n1: Optional[torch.Tensor] = None, n2: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """naive_fmap2pointmap for every crop: int64 [B, 2, V2] (row 0 CAD idx, row 1 arange).
+    n1 / n2 (int32 [B]): the rows of the padded evecs that are real points — train.py:110-114
+    keeps the rows whose xyz is non-zero, i.e. drops collate's padding; entries j >= n2[b]
+    of crop b are unspecified."""
     B, V1, _ = evecs_x.shape
     V2 = evecs_y.shape[1]
     dev = C.device
-    n1 = torch.full((B,), V1, dtype=torch.int32, device=dev)
-    n2 = torch.full((B,), V2, dtype=torch.int32, device=dev)
+    n1 = _counts(n1, B, V1, dev)
+    n2 = _counts(n2, B, V2, dev)
     idx, _ = ops.feat_dist_topk(evecs_x, C, evecs_y, n1, n2, 1)
     ar = torch.arange(V2, device=dev, dtype=torch.int64)[None].expand(B, V2)
     return torch.stack([idx[..., 0], ar], 1)
@@ -221,9 +311,11 @@ class TrainStep:
         if self.overlap:  # the point map + IR read only C_pred: beside the backward
             self.aux.wait_stream(main)
         with torch.no_grad(), _on(self.aux):  # train.py:109-116 (naive solver + IR per crop)
-            p_pred = naive_p2p_batched(C_pred.detach(), op.cad_evecs, op.pc_evecs)
-            npred = torch.full((p_pred.shape[0],), p_pred.shape[2], dtype=torch.int32, device=p_pred.device)
+            p_pred = naive_p2p_batched(C_pred.detach(), op.cad_evecs, op.pc_evecs, op.cad_n, crops.n2)
+            npred = _counts(crops.n2, p_pred.shape[0], p_pred.shape[2], p_pred.device)
             ir = ops.inlier_ratio(p_pred, npred, op.cad_xyz, crops.align32, op.ir_thr, layout=1).mean()
+            # P truncated at the pair capacity would train on partial labels: flag it (device bool)
+            log["pair_overflow"] = crops.overflow()
         if self.flat_grads:  # accumulate into the flat buffer's views (autograd adds in place)
             self.flat.zero_()
             for p, v in zip(self.params, self.gviews):
@@ -406,12 +498,13 @@ class InferStep:
         B, V1, _ = op.cad_evecs.shape
         V2 = op.pc_evecs.shape[1]
         dev = C_pred.device
-        n1 = torch.full((B,), V1, dtype=torch.int32, device=dev)
-        n2 = torch.full((B,), V2, dtype=torch.int32, device=dev)
+        # eval.py:85-87: the solver sees only the non-padding rows of each crop
+        n1 = _counts(op.cad_n, B, V1, dev)
+        n2 = _counts(crops.n2, B, V2, dev)
         top, _ = ops.feat_dist_topk(op.cad_evecs, C_pred, op.pc_evecs, n1, n2, 5)      # spacial_filtering.py:32-38
         cand = torch.stack([top.reshape(B, -1),
                             torch.arange(V2, device=dev)[None, :, None].expand(B, V2, 5).reshape(B, -1)], -1)
-        ncand = torch.full((B,), 5 * V2, dtype=torch.int32, device=dev)
+        ncand = 5 * n2
         rows, nsurv = ops.rigidity_filter(cand, ncand, op.cad_xyz, crops.pc32, op.rig_thr)  # :42-75
         p_pred = torch.gather(cand, 1, rows[..., None].expand(-1, -1, 2))                  # [B, L, 2]
         ir = ops.inlier_ratio(p_pred, nsurv, op.cad_xyz, crops.align32, op.ir_thr, layout=0)  # eval.py:89

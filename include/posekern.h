@@ -92,9 +92,10 @@ int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, int knn, doub
            float* out32, int64_t* kept_idx, void* stream);
 
 /* FPS sample-count policy of dataset/object.py:145-147 on device counts (no host sync):
- * fixed > 0: npoint = fixed; else npoint = int(limit/n * n) if n > limit, else -n
- * (negative = keep all n points, no FPS). start[b] = splitmix64(seed ^ splitmix64(b))
- * % n (replaces upstream torch.randint; may be NULL). out_off int64 [B+1]. */
+ * fixed > 0: npoint = fixed if n > fixed, else -n; fixed <= 0: npoint = int(limit/n * n)
+ * if n > limit, else -n (negative = keep all n points in order, no FPS: the reference's
+ * `if pcd.shape[0] > 2000` branch). start[b] = splitmix64(seed ^ splitmix64(b)) % n
+ * (replaces upstream torch.randint; may be NULL). out_off int64 [B+1]. */
 int pk_fps_npoint(const int64_t* off, int B, int fixed, int limit, uint64_t seed,
                   int32_t* npoint, int32_t* start, int64_t* out_off, void* stream);
 
@@ -106,6 +107,14 @@ int pk_gather_transform(const double* pcd, const int64_t* off, int B, const int6
                         int idx_stride, const int32_t* npoint, int npmax, const int64_t* out_off,
                         const double* R, const double* t, double* sel64, double* align64,
                         float* sel32, void* stream);
+
+/* H6 collate (dataset/helpers.py:22-50: torch.Tensor(x) then pad_sequence(batch_first=True))
+ * of one packed per-crop field: src [T, C] f64 (src_f64 = 1) or f32, packed by off [B+1];
+ * dst f32 [B, ld, C] with crop b's first min(n_b, ld) rows cast to f32 and every later row
+ * zero (ld = the batch maximum reproduces collate exactly). counts int32 [B] (may be NULL)
+ * receives min(n_b, ld). */
+int pk_collate_pad(const void* src, int src_f64, int C, const int64_t* off, int B, int ld, float* dst,
+                   int32_t* counts, void* stream);
 
 /* Packed-layout helpers: per-segment exclusive scan of int32 counts (S segments of n),
  * and off[b+1] = off[b] + counts[b]. */

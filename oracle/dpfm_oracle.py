@@ -133,6 +133,37 @@ def fps_npoint(n: int) -> int:
     return int(ratio * n)
 
 
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+def fps_start(seed: int, b: int, n: int) -> int:
+    """The FPS start index that replaces upstream's unseeded torch.randint(0, N) for crop b
+    (the build's documented choice, include/posekern.h pk_fps_npoint)."""
+    return _splitmix64((seed & _M64) ^ _splitmix64(b)) % n if n > 0 else 0
+
+
+def sample_crop(pcd: np.ndarray, seed: int, b: int, fixed: int = 0, limit: int = 2000) -> np.ndarray:
+    """dataset/object.py:145-148 on one outlier-filtered crop: FPS when the crop has more
+    than `limit` points (npoint = int(limit/n * n)), every point otherwise. fixed > 0 is the
+    build's fixed-size variant (FPS to exactly `fixed` when larger, every point otherwise)."""
+    n = pcd.shape[0]
+    if fixed > 0:
+        npoint = fixed if n > fixed else 0
+    else:
+        npoint = int(limit / n * n) if n > limit else 0
+    if npoint == 0:
+        return pcd
+    idx = farthest_point_sample(torch.Tensor(pcd).t(), ratio=0, start=fps_start(seed, b, n), npoint=npoint)
+    return pcd[idx.numpy()]
+
+
 # --------------------------------------------------------------------------------------
 # H4  transform: dataset/object.py:304-309 (inv=True -> object frame, "align_pc")
 # --------------------------------------------------------------------------------------
@@ -177,6 +208,30 @@ def get_overlap(l_1: int, l_2: int, p: np.ndarray):
     overlap_12[p[:, 0]] = 1
     overlap_21[p[:, 1]] = 1
     return overlap_12, overlap_21
+
+
+# --------------------------------------------------------------------------------------
+# H6  batch assembly: dataset/helpers.py:22-50 collate
+# --------------------------------------------------------------------------------------
+
+
+def collate(data):
+    """dataset/helpers.py:22-50 on a list of (CAD, PC, Obj) dicts: every ndarray field of
+    CAD / PC becomes torch.Tensor (f32) padded by pad_sequence(batch_first=True), other CAD
+    / PC fields None; Obj ndarray fields with more than one element are converted the same
+    way and padded, except P which stays a list; everything else becomes a list."""
+    def padded(key, part):
+        return torch.nn.utils.rnn.pad_sequence([torch.Tensor(d[part][key]) for d in data], batch_first=True)
+
+    CAD = {k: padded(k, 0) if isinstance(v, np.ndarray) else None for k, v in data[0][0].items()}
+    PC = {k: padded(k, 1) if isinstance(v, np.ndarray) else None for k, v in data[0][1].items()}
+    Obj = {}
+    for k, v in data[0][2].items():
+        if isinstance(v, np.ndarray) and v.size > 1:
+            Obj[k] = [torch.Tensor(d[2][k]) for d in data] if k == "P" else padded(k, 2)
+        else:
+            Obj[k] = [d[2][k] for d in data]
+    return CAD, PC, Obj
 
 
 # --------------------------------------------------------------------------------------

@@ -109,7 +109,44 @@ def main():
     out["n"] = np.int64(len(rows))
     np.savez_compressed(f"{OUT}/pose_metrics.npz", **out)
     np.save(f"{OUT}/p_pred.npy", np.load(f"{REF}/sample-data/sample_P_pred/p_i0.npy"))
-    print(f"wrote lm_frame.npz, pose_metrics.npz ({len(rows)} crops), p_pred.npy")
+    real_crops(info)
+    print(f"wrote lm_frame.npz, pose_metrics.npz ({len(rows)} crops), p_pred.npy, real_crops.npz")
+
+
+# Real crops of the published PBR/RANSAC results, chosen to span the reference's crop sizes:
+# 200 .. 2000 points (1999 = the int(2000/n * n) rounding of object.py:145-147) on decimated
+# CADs of 4996 / 4998 / 5002 vertices (object.py:171-173).
+REAL_CROPS = ("obj_11_result_263", "obj_6_result_101", "obj_6_result_409", "obj_5_result_249",
+              "obj_11_result_5", "obj_12_result_111", "obj_8_result_196")
+
+
+def real_crops(info):
+    """real_crops.npz: per crop the camera-frame crop pc_i.ply (pcd_depth, f64 cm), T_gt at
+    full precision (fitted from cad_i -> cad_i_pose_gt, checked against the printed matrix),
+    the object's diameter (models_info.json * 0.1) and id; one decimated CAD per object."""
+    base = f"{REF}/results_on_pbr/results_poses_RANSAC"
+    out, cads = {}, {}
+    for k, name in enumerate(REAL_CROPS):
+        i = name.split("_")[-1]
+        d = f"{base}/ply/{name}"
+        r = parse_result_txt(f"{base}/results/{name}.txt")
+        cad = read_ply_xyz(f"{d}/cad_{i}.ply")
+        T_gt = fit_rigid(cad, read_ply_xyz(f"{d}/cad_{i}_pose_gt.ply"))
+        assert np.allclose(T_gt, r["T_gt"], atol=1e-6), name
+        oid = r["obj_id"]
+        if oid in cads:
+            assert np.array_equal(cads[oid], cad), name  # one decimated CAD per object
+        cads[oid] = cad
+        out[f"{k}_pc"] = read_ply_xyz(f"{d}/pc_{i}.ply")
+        out[f"{k}_T_gt"] = T_gt
+        out[f"{k}_obj_id"] = np.int64(oid)
+        out[f"{k}_diam"] = np.float64(info[str(oid)]["diameter"] * 0.1)
+        out[f"{k}_n_corr"] = np.int64(int(re.search(r"Num\. of correspondences:\s*(\d+)",
+                                                    open(f"{base}/results/{name}.txt").read()).group(1)))
+    for oid, cad in cads.items():
+        out[f"cad_{oid}"] = cad
+    out["n"] = np.int64(len(REAL_CROPS))
+    np.savez_compressed(f"{OUT}/real_crops.npz", **out)
 
 
 if __name__ == "__main__":

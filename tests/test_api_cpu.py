@@ -32,3 +32,43 @@ def test_reference_signatures():
     assert list(inspect.signature(C_from_sparse_P).parameters) == ["P", "evecs1", "evecs2"]
     assert list(inspect.signature(compute_inlier_ratio).parameters) == ["pred_corr", "CAD", "PC_aligned", "threshold"]
     assert list(inspect.signature(farthest_point_sample).parameters)[:2] == ["xyz", "ratio"]
+
+
+def _ragged_items(seed=0):
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    items = []
+    for n1, n2 in ((5002, 200), (4996, 1999), (4998, 2000), (5002, 0)):
+        cad = {"xyz": rng.normal(size=(n1, 3)), "mass": rng.random(n1), "evals": rng.random(64),
+               "evecs": rng.normal(size=(n1, 64)).astype(np.float32), "L": None, "gradX": None, "gradY": None,
+               "faces": rng.integers(0, n1, size=(n1 // 2, 3))}
+        pc = {"xyz": rng.normal(size=(n2, 3)).astype(np.float32), "mass": rng.random(n2), "evals": rng.random(64),
+              "evecs": rng.normal(size=(n2, 64)), "L": None, "gradX": None, "gradY": None}
+        P = np.stack([rng.integers(0, n1, 7), rng.integers(0, max(n2, 1), 7)], 1)
+        obj = {"obj_id": 5, "diam_cad": 17.5, "R_m2c": rng.normal(size=(3, 3)), "t_m2c": rng.normal(size=3),
+               "align_pc": rng.normal(size=(n2, 3)), "P": P, "overlap_12": (rng.random(n1) < .3).astype(np.byte),
+               "overlap_21": (rng.random(n2) < .5).astype(np.byte), "cad_path": "x.ply", "visib_fract": 0.7}
+        items.append((cad, pc, obj))
+    return items
+
+
+def test_collate_matches_reference_semantics():
+    """dpfm_amd.dataset.helpers.collate == the oracle's restatement of helpers.py:22-50
+    (bit-exact f32 tensors, ragged crops including an empty one)."""
+    from oracle import dpfm_oracle as O
+    from dpfm_amd.dataset.helpers import collate, collate_noprocess, shape_to_device
+    items = _ragged_items()
+    got, exp = collate(items), O.collate(items)
+    for g, e in zip(got, exp):
+        assert set(g) == set(e)
+        for k in e:
+            if isinstance(e[k], torch.Tensor):
+                assert g[k].dtype == e[k].dtype == torch.float32 and torch.equal(g[k], e[k]), k
+            elif isinstance(e[k], list) and e[k] and isinstance(e[k][0], torch.Tensor):
+                assert all(torch.equal(a, b) for a, b in zip(g[k], e[k])), k
+            else:
+                assert g[k] == e[k], k
+    assert got[1]["xyz"].shape == (4, 2000, 3) and got[0]["evecs"].shape == (4, 5002, 64)
+    batch = shape_to_device({"shape1": got[0], "shape2": got[1]}, "cpu")
+    assert batch["shape1"]["L"] is None
+    assert all("L" not in it[0] for it in collate_noprocess(_ragged_items()))

@@ -178,3 +178,29 @@ def test_sample_rgb_vs_grid_sample(device):
         im = torch.from_numpy(img[f]).permute(2, 0, 1)[None].float() / 255
         ref = torch.nn.functional.grid_sample(im, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
         torch.testing.assert_close(out[200 * f:200 * (f + 1)], ref[0, :, 0].t(), rtol=1e-4, atol=2e-5)
+
+
+def test_cgt_rank_deficient_and_empty(device):
+    """C_from_sparse_P (utils/utils.py:67-79) when the pair list does not determine C_gt:
+    fewer than 30 distinct matched crop rows (rank < 30) and an empty list. torch's CPU lstsq
+    (gelsy) returns the minimum-norm solution there (zeros for no pairs); so does
+    pk_cgt_lstsq's fallback path. A full-rank crop in the same batch keeps the fast path."""
+    ops = _ops()
+    torch.manual_seed(5)
+    V1, V2 = 400, 300
+    e1 = torch.stack([_spectral(V1, 11), _spectral(V1, 12), _spectral(V1, 13)])
+    e2 = torch.stack([_spectral(V2, 14), _spectral(V2, 15), _spectral(V2, 16)])
+    cap = 700
+    pairs = torch.zeros((3, cap, 2), dtype=torch.int64)
+    n = [cap, 200, 0]
+    pairs[0, :, 0] = torch.randint(0, V1, (cap,))
+    pairs[0, :, 1] = torch.randint(0, V2, (cap,))
+    pairs[1, :200, 0] = torch.randint(0, V1, (200,))
+    pairs[1, :200, 1] = torch.randint(0, 12, (200,))  # rank <= 12
+    got = ops.cgt_lstsq(pairs.to(device), torch.tensor(n, device=device), e1.to(device), e2.to(device)).cpu()
+    for b in range(3):
+        P = pairs[b, :n[b]]
+        exp = M.C_from_sparse_P(P, e1[b, :, :30], e2[b, :, :30])
+        scale = max(float(exp.abs().max()), 1e-30)
+        torch.testing.assert_close(got[b], exp, rtol=1e-3, atol=1e-4 * scale)
+    assert torch.equal(got[2], torch.zeros(30, 30))

@@ -132,3 +132,27 @@ def test_ransac_c_matches_python(coracle):
     assert int(st[2]) == hb
     assert st[0] == f
     np.testing.assert_allclose(T.reshape(4, 4), Tp, atol=1e-9)
+
+
+def test_transform_oracle_vs_numpy_literal_real_crops():
+    """H4's oracle evaluates pc @ R + (-t @ R) as left-to-right 3-term dots without FMA (the
+    order the HIP kernel reproduces bit-exactly). The reference's literal numpy expression
+    (object.py:304-307) goes through BLAS, whose order is library-dependent. On the
+    reference's real crops (tests/golden/real_crops.npz) the two differ by at most a few
+    ulps of the coordinates' scale (|x| <= |pc| + |t|), and no find_positives pair flips."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "real_crops.npz"))
+    flips = pairs = 0
+    for k in range(int(g["n"])):
+        T = g[f"{k}_T_gt"]
+        R, t, pc = T[:3, :3].copy(), T[:3, 3].copy(), g[f"{k}_pc"]
+        cad = g[f"cad_{int(g[f'{k}_obj_id'])}"]
+        mine = O.transform(pc, R, t, inv=True)
+        literal = pc @ R + (-1.0 * t.reshape(1, 3) @ R)
+        scale = np.abs(pc).max() + np.abs(t).max()
+        assert np.abs(mine - literal).max() <= 8 * np.finfo(np.float64).eps * scale
+        r = float(g[f"{k}_diam"]) * 0.05
+        a, b = O.find_positives_mask(cad, mine, r), O.find_positives_mask(cad, literal, r)
+        flips += int((a != b).sum())
+        pairs += int(a.sum())
+    assert pairs > 200_000 and flips == 0
