@@ -99,7 +99,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
   float qr[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) qr[s] = qi < N ? qb[(int64_t)(4 * s + g) * H * N + qi] * kScale : 0.f;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  // one accumulator per 16-key sub-tile: four independent MFMA chains (a serial chain over
+  // M ~ 5000 keys of a real CAD measured 4-5x torch's gradient error; split, it is within 1.5x)
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -__builtin_huge_valf(), l = 0.f;
   Tile kt = load_tile(kb, H * M, M, 0), vt = load_tile(vb, H * M, M, 0);
   for (int k0 = 0; k0 < M; k0 += kT) {
@@ -141,18 +145,21 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
       }
     l = l * alpha + ps;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc[r] *= alpha;
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[t][r] *= alpha;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc = mfma(Vs[(16 * t + 4 * g + r) * kSC + c], st[t][r], acc);
+      for (int r = 0; r < 4; ++r) acc[t] = mfma(Vs[(16 * t + 4 * g + r) * kSC + c], st[t][r], acc[t]);
   }
   l = grp_sum(l);
+  const f32x4 accs = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   if (qi < N) {
     const float inv = 1.f / l;
     float* ob = out + ((int64_t)b * kD * H + h) * N;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ob[(int64_t)(4 * g + r) * H * N + qi] = acc[r] * inv;
+    for (int r = 0; r < 4; ++r) ob[(int64_t)(4 * g + r) * H * N + qi] = accs[r] * inv;
     if (g == 0) {
       float2* ms = reinterpret_cast<float2*>(lse) + ((int64_t)b * H + h) * N + qi;
       *ms = make_float2(m, inv);
@@ -186,7 +193,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
   const float2 ms = qi < N ? reinterpret_cast<const float2*>(lse)[((int64_t)b * H + h) * N + qi]
                            : make_float2(__builtin_huge_valf(), 0.f);
   if (qi < N && g == 0) delta[((int64_t)b * H + h) * N + qi] = dl;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[4];  // independent chains per 16-key sub-tile (accuracy, see the forward)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   Tile kt = load_tile(kb, H * M, M, 0), vt = load_tile(vb, H * M, M, 0);
   for (int k0 = 0; k0 < M; k0 += kT) {
     __syncthreads();
@@ -209,13 +218,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
       for (int r = 0; r < 4; ++r) {
         const float p = k0 + 16 * t + 4 * g + r < M ? exp2_((st[r] - ms.x) * kLog2e) * ms.y : 0.f;
         const float ds = p * (dp[r] - dl);
-        acc = mfma(KT[(16 * t + 4 * g + r) * kSC + c], ds, acc);
+        acc[t] = mfma(KT[(16 * t + 4 * g + r) * kSC + c], ds, acc[t]);
       }
     }
   }
+  const f32x4 accs = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   if (qi < N) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dq[qoff + (int64_t)(4 * g + r) * H * N + qi] = acc[r] * kScale;
+    for (int r = 0; r < 4; ++r) dq[qoff + (int64_t)(4 * g + r) * H * N + qi] = accs[r] * kScale;
   }
 }
 
@@ -243,7 +253,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
     kr[s] = kj < M ? k[a] * kScale : 0.f;
     vr[s] = kj < M ? v[a] : 0.f;
   }
-  f32x4 dka = {0.f, 0.f, 0.f, 0.f}, dva = {0.f, 0.f, 0.f, 0.f};
+  // two independent chains (even / odd 16-query sub-tiles; accuracy, see the forward): four
+  // would cost this kernel its third wave per SIMD
+  f32x4 dka[2], dva[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) dka[t] = dva[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   Tile qt = load_tile(qb, H * N, N, 0), gt = load_tile(gb, H * N, N, 0);
   for (int q0 = 0; q0 < N; q0 += kT) {
     __syncthreads();
@@ -274,17 +288,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
         const int qq = 16 * t + 4 * g + r;
         const float p = exp2_((st[r] - Ls[qq]) * kLog2e) * Is[qq];
         const float ds = p * (dp[r] - Ds[qq]);
-        dva = mfma(OT[qq * kSC + c], p, dva);   // dV^T[d][key] += dO^T[d][q] P[q][key]
-        dka = mfma(QT[qq * kSC + c], ds, dka);  // dK^T[d][key] += Q^T[d][q] dS[q][key]
+        dva[t & 1] = mfma(OT[qq * kSC + c], p, dva[t & 1]);   // dV^T[d][key] += dO^T[d][q] P[q][key]
+        dka[t & 1] = mfma(QT[qq * kSC + c], ds, dka[t & 1]);  // dK^T[d][key] += Q^T[d][q] dS[q][key]
       }
     }
   }
+  const f32x4 dks = dka[0] + dka[1], dvs = dva[0] + dva[1];
   if (kj < M) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t a = koff + (int64_t)(4 * g + r) * H * M + kj;
-      dk[a] = dka[r] * kScale;
-      dv[a] = dva[r];
+      dk[a] = dks[r] * kScale;
+      dv[a] = dvs[r];
     }
   }
 }

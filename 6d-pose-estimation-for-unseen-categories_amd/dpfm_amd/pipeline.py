@@ -526,4 +526,5 @@ class InferStep:
         T_gt[:, :3, 3] = fb.t
         T_gt[:, 3, 3] = 1.0
         metrics = ops.pose_metrics(fb.cad64, fb.cad_off, V1, T, T_gt)
-        return dict(C=C_pred, p_pred=p_pred, n_corr=nsurv, ir=ir, T=T, ransac=stats, metrics=metrics)
+        return dict(C=C_pred, cand=cand, p_pred=p_pred, n_corr=nsurv, ir=ir, T=T, ransac=stats, metrics=metrics,
+                    corres=corres, cor_off=cor_off)

@@ -1,0 +1,209 @@
+"""GPU parity at the BASELINE configs' own sizes (BASELINE.json configs[1], [3], [4]):
+
+  configs[1]  B = 32 x 1024-point inference: InferStep (eval.py:73-89 + test_RANSAC.py:
+              397-401) checked stage by stage against the per-crop oracle chain — model
+              output C, top-5 candidates, rigidity survivors (n = 5120 per crop), IR, RANSAC
+              (1024 hypotheses, same draws) and the pose metrics
+  configs[3]  the feature distance at 2048^2 (B = 8 crops here) and the rigidity filter at
+              n = 10240 (5 x 2048 candidates)
+  configs[4]  the 4096^2 feature distance (one crop) and 1024-hypothesis RANSAC over
+              n = 4096 correspondences
+Index outputs are exact except counted near-ties, the rule of SURVEY §8(c)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dpfm_oracle as O
+from oracle import dpfm_model_oracle as M
+
+pytestmark = pytest.mark.gpu
+
+
+def _spectral(V, seed):
+    from dpfm_amd.dataset.synthetic import lbo_operators
+    return torch.from_numpy(lbo_operators(V, 64, seed)[2])
+
+
+def check_topk(dist: np.ndarray, got: np.ndarray, k: int, rel: float = 1e-5) -> int:
+    """dist [V1, V2] (fp64 copy of the oracle's cdist), got [V2, k] row indices. Every column's
+    k picks must be distinct and their distances the k smallest of the column in ascending
+    order, up to near-ties |d_a - d_b| <= rel * max(d). Returns the number of columns that
+    differ from the oracle's stable sort only by such ties."""
+    tol = rel * max(float(dist.max()), 1e-12)
+    srt = np.sort(dist, axis=0)[:k]                      # [k, V2] the k smallest per column
+    picked = np.take_along_axis(dist, got.T, axis=0)     # [k, V2] distances of the picks
+    assert (np.abs(picked - srt) <= tol).all(), float(np.abs(picked - srt).max())
+    for j in range(got.shape[0]):
+        assert len(set(got[j].tolist())) == k, j
+    exp = np.argsort(dist, axis=0, kind="stable")[:k].T
+    return int((exp != got).any(1).sum())
+
+
+@pytest.mark.parametrize("B,V", [(8, 2048), (1, 4096)])
+def test_feat_dist_argmin_top5_configs(device, B, V):
+    """naive.py:20-33 (argmin) and spacial_filtering.py:19-38 (top-5 of the stable sort) on
+    the MFMA kernel vs torch.cdist on the CPU, at configs[3]'s 2048^2 and configs[4]'s 4096^2."""
+    from dpfm_amd import ops
+    torch.manual_seed(B)
+    ex = torch.stack([_spectral(V, 100 + b) for b in range(B)])
+    ey = torch.stack([_spectral(V, 200 + b) for b in range(B)])
+    C = torch.eye(30)[None] + 0.3 * torch.randn(B, 30, 30)
+    n = torch.full((B,), V, dtype=torch.int32, device=device)
+    i1, _ = ops.feat_dist_topk(ex.to(device), C.to(device), ey.to(device), n, n, 1)
+    i5, d5 = ops.feat_dist_topk(ex.to(device), C.to(device), ey.to(device), n, n, 5, want_dist=True)
+    i1, i5, d5 = i1.cpu().numpy(), i5.cpu().numpy(), d5.cpu().numpy()
+    ties = 0
+    for b in range(B):
+        dist = torch.cdist(ex[b, :, :30] @ C[b].t(), ey[b, :, :30]).numpy().astype(np.float64)
+        ties += check_topk(dist, i1[b], 1) + check_topk(dist, i5[b], 5)
+        picked = np.take_along_axis(dist, i5[b].T, axis=0).T
+        np.testing.assert_allclose(d5[b], picked, rtol=1e-4, atol=1e-5 * dist.max())
+    assert ties <= max(2, B * V // 1000), ties
+
+
+def _rigid_scene(V2, seed):
+    from dpfm_amd.dataset.synthetic import random_rotation
+    rng = np.random.default_rng(seed)
+    V1 = V2 + 300
+    cad = (rng.normal(size=(V1, 3)) * 5).astype(np.float32)
+    gen = rng.permutation(V1)[:V2]
+    R = random_rotation(rng)
+    pc = ((cad[gen].astype(np.float64) @ R.T + np.array([3.0, -2.0, 90.0])) + rng.normal(size=(V2, 3)) * 0.05
+          ).astype(np.float32)
+    cand = np.zeros((V2, 5, 2), dtype=np.int64)
+    cand[:, :, 1] = np.arange(V2)[:, None]
+    cand[:, :, 0] = rng.integers(0, V1, size=(V2, 5))
+    good = rng.random(V2) < 0.6
+    cand[good, rng.integers(0, 5, size=good.sum()), 0] = gen[good]
+    return cad, pc, cand.reshape(-1, 2), 2.0 * 5 * 2.5
+
+
+def _rigidity_parity(cad, pc, cand, rows, n, diam):
+    """survivors equal the oracle's on the same candidates, except candidates whose oracle score
+    lies within 1e-5 (relative) of its round's threshold."""
+    p = torch.from_numpy(cand).t()
+    exp, scores = O.spacial_filtering(torch.from_numpy(cad), torch.from_numpy(pc), p, diam, return_scores=True)
+    got = cand[rows[:n]]
+    a, b = set(map(tuple, got.tolist())), set(map(tuple, exp.t().tolist()))
+    near = 0
+    for s, tau in zip(scores, (0.3, 0.15, 0.055)):
+        thr = float(np.float32(tau * diam))
+        near += int((np.abs(s.numpy() - thr) <= 1e-5 * thr).sum())
+    if near == 0:
+        assert a == b and np.array_equal(got, exp.t().numpy())  # same survivors, same order
+    else:
+        assert len(a ^ b) <= 4 * near + max(2, len(b) // 1000), (len(a ^ b), near)
+    return len(b)
+
+
+@pytest.mark.parametrize("V2", [1024, 2048])
+def test_rigidity_filter_configs(device, V2):
+    """spacial_filtering.py:42-75 at n = 5 V2 = 5120 (configs[1]) and 10240 (configs[3])."""
+    from dpfm_amd import ops
+    cad, pc, cand, diam = _rigid_scene(V2, V2)
+    thr = ops.rigidity_thresholds([diam], device)
+    rows, n = ops.rigidity_filter(torch.from_numpy(cand)[None].to(device),
+                                  torch.tensor([cand.shape[0]], dtype=torch.int32, device=device),
+                                  torch.from_numpy(cad)[None].to(device), torch.from_numpy(pc)[None].to(device), thr)
+    kept = _rigidity_parity(cad, pc, cand, rows[0].cpu().numpy(), int(n[0]), diam)
+    assert 0.2 * V2 < kept < 5 * V2
+
+
+def test_ransac_configs4(device, coracle):
+    """configs[4]'s pose stage: 1024 hypotheses over n = 4096 correspondences (4096-vertex CAD)
+    vs the C oracle on the same hash-drawn hypotheses: same best hypothesis and fitness, pose
+    within 1e-4 (the north-star tolerance)."""
+    from _util import cp
+    from dpfm_amd.dataset.synthetic import random_rotation
+    from dpfm_amd.pose.ransac import ransac_registration
+    rng = np.random.default_rng(44)
+    R = random_rotation(rng)
+    t = np.array([5.0, -3.0, 95.0])
+    V = 4096
+    cad = rng.normal(size=(V, 3)) * 6
+    perm = rng.permutation(V)                 # crop point j was generated by CAD point perm[j]
+    pc = (cad[perm] + rng.normal(size=(V, 3)) * 0.01) @ R.T + t
+    src_idx = rng.integers(0, V, V)
+    dst_idx = rng.integers(0, V, V)
+    good = rng.random(V) < 0.3                # 30 % inliers
+    src_idx[good] = perm[dst_idx[good]]
+    corres = np.ascontiguousarray(np.stack([src_idx, dst_idx], 1).astype(np.int32))
+    H = 1024
+    T_c, st_c = np.zeros(16), np.zeros(3)
+    coracle.oc_ransac(cp(np.ascontiguousarray(cad)), cp(np.ascontiguousarray(pc)), cp(corres), V, None, 7, H, 0.05,
+                      cp(T_c), cp(st_c))
+    res = ransac_registration(cad, pc, corres, distance_threshold=0.05, max_iteration=H, seed=7, device=device)
+    assert res.best_hypothesis == int(st_c[2]) and res.fitness == st_c[0]
+    np.testing.assert_allclose(res.transformation, T_c.reshape(4, 4), atol=1e-4)
+
+
+def test_infer_step_configs1_vs_oracle_chain(device, coracle):
+    """configs[1]: InferStep on B = 32 crops of 1024 points vs the per-crop oracle chain, stage
+    by stage (each stage's oracle runs on the device's previous-stage output, so a near-tie
+    upstream cannot cascade): C (3x the fp32 reference's error vs fp64), top-5, rigidity
+    survivors, IR (exact), RANSAC (C oracle, same draws: best hypothesis, fitness, pose within
+    1e-4), pose metrics."""
+    from _util import cp
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import InferStep, make_frame_batch, model_batch
+    B, N, H = 32, 1024, 1024
+    fb, op = make_frame_batch(B, N, N, seed=300, device=device)
+    crops = CropFormation(n1=N, npoint=N, seed=9)(fb)
+    torch.manual_seed(11)
+    ref = M.DPFMNet()
+    mine = DPFMNet().to(device)
+    mine.load_state_dict(ref.state_dict())
+    out = InferStep(mine, hypotheses=H, seed=5)(fb, op, crops)
+    torch.cuda.synchronize()
+    # (1) the model's C vs the oracle in fp64 / fp32 on the same padded batch
+    mb = model_batch(op, crops)
+    cpu = {k: {kk: vv.cpu() for kk, vv in v.items() if kk in ("xyz", "mass", "evals", "evecs")} for k, v in mb.items()}
+    with torch.no_grad():
+        C32 = ref(cpu)[0]
+        truth = M.DPFMNet().double()
+        truth.load_state_dict(ref.state_dict())
+        C64 = truth({k: {kk: vv.double() for kk, vv in v.items()} for k, v in cpu.items()})[0]
+    Cg = out["C"].cpu().double()
+    e_ref = (C32.double() - C64).abs().max().item()
+    assert (Cg - C64).abs().max().item() <= 3 * e_ref + 1e-6 * (1 + C64.abs().max().item())
+    cand = out["cand"].cpu().numpy()
+    p_pred = out["p_pred"].cpu().numpy()
+    ncorr = out["n_corr"].cpu().numpy()
+    ir = out["ir"].cpu().numpy()
+    T = out["T"].cpu().numpy()
+    st = out["ransac"].cpu().numpy()
+    ex, ey = cpu["shape1"]["evecs"], cpu["shape2"]["evecs"]
+    cadx, pcx, al = cpu["shape1"]["xyz"], cpu["shape2"]["xyz"], crops.align32.cpu()
+    cad64 = fb.cad64.cpu().numpy()
+    pc64 = crops.pc64.cpu().numpy()
+    off = crops.off.cpu().numpy()
+    diam = fb.diam
+    ties = 0
+    for b in range(B):
+        # (2) top-5 on the device's C
+        dist = torch.cdist(ex[b, :, :30] @ out["C"][b].cpu().t(), ey[b, :, :30]).numpy().astype(np.float64)
+        ties += check_topk(dist, cand[b, :, 0].reshape(N, 5), 5)
+        # (3) rigidity filter on the device's candidates
+        surv = p_pred[b, :ncorr[b]]
+        exp = O.spacial_filtering(cadx[b], pcx[b], torch.from_numpy(cand[b]).t(), diam[b])
+        a, e = set(map(tuple, surv.tolist())), set(map(tuple, exp.t().tolist()))
+        assert len(a ^ e) <= max(2, len(e) // 500), (b, len(a ^ e), len(e))
+        # (4) IR of the device's survivors (eval.py:89)
+        exp_ir = O.compute_inlier_ratio(torch.from_numpy(surv), cadx[b], al[b], np.float32(0.1 * diam[b]))
+        assert float(ir[b]) == float(exp_ir), b
+        # (5) RANSAC on the device's survivors, same hypotheses
+        cad_b = np.ascontiguousarray(cad64[N * b:N * (b + 1)])
+        pc_b = np.ascontiguousarray(pc64[off[b]:off[b + 1]])
+        cor = np.ascontiguousarray(surv.astype(np.int32))
+        T_c, st_c = np.zeros(16), np.zeros(3)
+        coracle.oc_ransac(cp(cad_b), cp(pc_b), cp(cor), int(ncorr[b]), None, 5, H, 0.05, cp(T_c), cp(st_c))
+        assert int(st[b, 2]) == int(st_c[2]) and st[b, 0] == st_c[0], b
+        np.testing.assert_allclose(T[b], T_c.reshape(4, 4), atol=1e-4)
+        # (6) ADD of the device's pose (test_RANSAC.py:162-173)
+        T_gt = np.eye(4)
+        T_gt[:3, :3] = fb.R[b].cpu().numpy().reshape(3, 3)
+        T_gt[:3, 3] = fb.t[b].cpu().numpy()
+        e_add, _ = O.add(T[b], T_gt, cad_b, diam[b])
+        np.testing.assert_allclose(out["metrics"][b, 0].item(), e_add, rtol=1e-9)
+    assert ties <= B * N // 200, ties
