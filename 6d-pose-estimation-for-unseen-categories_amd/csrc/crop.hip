@@ -432,7 +432,7 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 }
 
 __global__ void npoint_kernel(const int64_t* __restrict__ off, int B, int fixed, int limit,
-                              uint64_t seed, int32_t* __restrict__ npoint, int32_t* __restrict__ start,
+                              uint64_t seed, int64_t base, int32_t* __restrict__ npoint, int32_t* __restrict__ start,
                               int64_t* __restrict__ out_off) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   int64_t acc = 0;
@@ -450,7 +450,7 @@ __global__ void npoint_kernel(const int64_t* __restrict__ off, int B, int fixed,
       np = -n;  // no FPS: keep all n points in order (encoded negative)
     }
     npoint[b] = np;
-    if (start) start[b] = n > 0 ? (int32_t)(splitmix64(seed ^ splitmix64((uint64_t)b)) % (uint64_t)n) : 0;
+    if (start) start[b] = n > 0 ? (int32_t)(splitmix64(seed ^ splitmix64((uint64_t)(base + b))) % (uint64_t)n) : 0;
     out_off[b] = acc;
     acc += np < 0 ? -np : np;
   }
@@ -606,13 +606,13 @@ extern "C" int pk_segment_scan(const int32_t* cnt, int S, int n, int64_t* off, i
   return PK_OK;
 }
 
-extern "C" int pk_fps_npoint(const int64_t* off, int B, int fixed, int limit, uint64_t seed,
+extern "C" int pk_fps_npoint(const int64_t* off, int B, int fixed, int limit, uint64_t seed, int64_t base,
                              int32_t* npoint, int32_t* start, int64_t* out_off, void* stream) {
-  PK_REQUIRE(B >= 0 && limit > 0);
+  PK_REQUIRE(B >= 0 && limit > 0 && base >= 0);
   if (B == 0) return PK_OK;
   PK_REQUIRE(off && npoint && out_off);
   hipLaunchKernelGGL(npoint_kernel, dim3(1), dim3(64), 0, pk::as_stream(stream), off, B, fixed, limit,
-                     seed, npoint, start, out_off);
+                     seed, base, npoint, start, out_off);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

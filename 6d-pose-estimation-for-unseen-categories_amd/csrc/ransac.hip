@@ -135,12 +135,8 @@ __device__ void rigid_fit4(const double s[4][3], const double d[4][3], double R[
 
 constexpr int kRThreads = 256;
 constexpr int kRTile = 2048;  // correspondences per LDS tile (96 KiB fp64)
-
-struct Best {
-  int good;
-  double rmse;
-  int64_t h;
-};
+constexpr int kRChunkMin = 64;  // fewest correspondences a scoring block takes
+constexpr int kRTargetBlocks = 2048;  // scoring grid to aim for (8 blocks per CU)
 
 __device__ __forceinline__ bool better(int g1, double r1, int64_t h1, int g2, double r2, int64_t h2) {
   if (g1 != g2) return g1 > g2;
@@ -163,35 +159,102 @@ __device__ __forceinline__ void load_hyp(const double* __restrict__ src, const d
   }
 }
 
-// grid (ceil(H / 256), B), block 256: one hypothesis per thread; per-block best.
-__global__ __launch_bounds__(kRThreads) void ransac_score_kernel(
+// Scratch of one pk_ransac call (see pk_ransac_work_size): per crop b the fitted poses
+// RT [12][H] (R row-major, then t; hypothesis-contiguous), the per-chunk partial scores
+// pg int32 / pe f64 [C][H], and the per-block bests of the reduction [nhb].
+struct RansacWork {
+  double* RT;
+  int32_t* pg;
+  double* pe;
+  int* bgood;
+  double* brmse;
+  int64_t* bh;
+};
+
+__host__ __device__ inline int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+__host__ __device__ inline RansacWork carve(void* work, int B, int64_t H, int C, int nhb) {
+  char* p = static_cast<char*>(work);
+  RansacWork w;
+  w.RT = reinterpret_cast<double*>(p);
+  p += align256((int64_t)B * 12 * H * 8);
+  w.pe = reinterpret_cast<double*>(p);
+  p += align256((int64_t)B * C * H * 8);
+  w.pg = reinterpret_cast<int32_t*>(p);
+  p += align256((int64_t)B * C * H * 4);
+  w.brmse = reinterpret_cast<double*>(p);
+  p += align256((int64_t)B * nhb * 8);
+  w.bh = reinterpret_cast<int64_t*>(p);
+  p += align256((int64_t)B * nhb * 8);
+  w.bgood = reinterpret_cast<int*>(p);
+  return w;
+}
+
+inline int chunks_for(int B, int64_t H, int nmax) {
+  const int64_t nhb = (H + kRThreads - 1) / kRThreads;
+  const int64_t by_n = (nmax + kRChunkMin - 1) / kRChunkMin;
+  const int64_t want = (kRTargetBlocks + nhb * B - 1) / (nhb * B > 0 ? nhb * B : 1);
+  int64_t C = want < by_n ? want : by_n;
+  return (int)(C < 1 ? 1 : C);
+}
+
+// pass 1 — grid (ceil(H / 256), B): one hypothesis per thread: draw its 4 correspondences,
+// fit [R | t], store it hypothesis-contiguous (coalesced for the scoring pass).
+__global__ __launch_bounds__(kRThreads) void ransac_fit_kernel(
     const double* __restrict__ src, const int64_t* __restrict__ src_off, const double* __restrict__ dst,
     const int64_t* __restrict__ dst_off, const int32_t* __restrict__ corres, const int64_t* __restrict__ cor_off,
     const int32_t* __restrict__ hyps, const int64_t* __restrict__ hyp_off, uint64_t seed, int64_t H,
-    double max_d2, int nblk, int* __restrict__ bgood, double* __restrict__ brmse, int64_t* __restrict__ bh) {
-  extern __shared__ __attribute__((aligned(16))) double sp[];  // [tile][6] (s xyz, d xyz)
-  __shared__ int sg[4];
-  __shared__ double sr[4];
-  __shared__ int64_t shh[4];
+    double* __restrict__ RT) {
   const int b = blockIdx.y;
+  const int64_t h = (int64_t)blockIdx.x * kRThreads + threadIdx.x;
   const int64_t c0 = cor_off[b];
   const int n = (int)(cor_off[b + 1] - c0);
+  if (h >= H || n < 4) return;
+  double s4[4][3], d4[4][3], R[9], t[3];
+  load_hyp(src + 3 * src_off[b], dst + 3 * dst_off[b], corres + 2 * c0, n, seed, h,
+           hyps ? hyps + 4 * hyp_off[b] : nullptr, s4, d4);
+  rigid_fit4(s4, d4, R, t);
+  double* o = RT + (int64_t)b * 12 * H + h;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) o[k * H] = R[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) o[(9 + k) * H] = t[k];
+}
+
+// pass 2 — grid (ceil(H / 256) * C, B): block (hypothesis tile, correspondence chunk c):
+// the chunk's pairs are staged in LDS (fp64) and broadcast; each thread scores its
+// hypothesis over the chunk in order ((R s + t) - d, no contraction, as the C oracle) and
+// writes the chunk's inlier count and error sum. C is sized so one crop's few hypotheses
+// (configs[4]: H = 1024) still fill the chip: 4 tiles x 64 chunks = 256 blocks.
+__global__ __launch_bounds__(kRThreads) void ransac_score_kernel(
+    const double* __restrict__ src, const int64_t* __restrict__ src_off, const double* __restrict__ dst,
+    const int64_t* __restrict__ dst_off, const int32_t* __restrict__ corres, const int64_t* __restrict__ cor_off,
+    int64_t H, double max_d2, int nhb, int C, int tile_len, const double* __restrict__ RT,
+    int32_t* __restrict__ pg, double* __restrict__ pe) {
+  extern __shared__ __attribute__((aligned(16))) double sp[];  // [tile][6] (s xyz, d xyz)
+  const int b = blockIdx.y;
+  const int tile = blockIdx.x % nhb, chunk = blockIdx.x / nhb;
+  const int64_t c0 = cor_off[b];
+  const int n = (int)(cor_off[b + 1] - c0);
+  const int clen = (n + C - 1) / C;
+  const int e0 = chunk * clen, e1 = min(n, e0 + clen);
+  const int64_t h = (int64_t)tile * kRThreads + threadIdx.x;
+  const bool act = h < H && n >= 4;
   const int32_t* cr = corres + 2 * c0;
   const double* S = src + 3 * src_off[b];
   const double* Dp = dst + 3 * dst_off[b];
-  const int32_t* hy = hyps ? hyps + 4 * hyp_off[b] : nullptr;
-  const int64_t h = (int64_t)blockIdx.x * kRThreads + threadIdx.x;
-  const bool act = h < H && n >= 4;
   double R[9], t[3];
   if (act) {
-    double s4[4][3], d4[4][3];
-    load_hyp(S, Dp, cr, n, seed, h, hy, s4, d4);
-    rigid_fit4(s4, d4, R, t);
+    const double* r = RT + (int64_t)b * 12 * H + h;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) R[k] = r[k * H];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t[k] = r[(9 + k) * H];
   }
   int good = 0;
   double err = 0.0;
-  for (int t0 = 0; t0 < n; t0 += kRTile) {
-    const int tn = min(kRTile, n - t0);
+  for (int t0 = e0; t0 < e1; t0 += tile_len) {  // tile_len = the LDS rows allocated
+    const int tn = min(tile_len, e1 - t0);
     __syncthreads();
     for (int e = threadIdx.x; e < tn; e += kRThreads) {
       const int64_t si = cr[2 * (t0 + e)], di = cr[2 * (t0 + e) + 1];
@@ -217,10 +280,41 @@ __global__ __launch_bounds__(kRThreads) void ransac_score_kernel(
       }
     }
   }
-  double rmse = good ? sqrt(err / good) : 0.0;
-  int64_t hh = act ? h : INT64_MAX;
-  if (!act) good = -1;
-  // wave reduction (shuffles) then block
+  if (h < H) {
+    const int64_t o = ((int64_t)b * C + chunk) * H + h;
+    pg[o] = good;
+    pe[o] = err;
+  }
+}
+
+// pass 3 — grid (ceil(H / 256), B): per hypothesis the chunks' counts and error sums in chunk
+// order -> (inliers, rmse); the block's best (fitness desc, rmse asc, index asc).
+__global__ __launch_bounds__(kRThreads) void ransac_reduce_kernel(const int64_t* __restrict__ cor_off, int64_t H,
+                                                                  int nhb, int C, const int32_t* __restrict__ pg,
+                                                                  const double* __restrict__ pe, int* __restrict__ bgood,
+                                                                  double* __restrict__ brmse, int64_t* __restrict__ bh) {
+  __shared__ int sg[4];
+  __shared__ double sr[4];
+  __shared__ int64_t shh[4];
+  const int b = blockIdx.y;
+  const int n = (int)(cor_off[b + 1] - cor_off[b]);
+  const int64_t h = (int64_t)blockIdx.x * kRThreads + threadIdx.x;
+  const bool act = h < H && n >= 4;
+  int good = -1;
+  double rmse = 0.0;
+  int64_t hh = INT64_MAX;
+  if (act) {
+    int g = 0;
+    double err = 0.0;
+    for (int c = 0; c < C; ++c) {
+      const int64_t o = ((int64_t)b * C + c) * H + h;
+      g += pg[o];
+      err += pe[o];
+    }
+    good = g;
+    rmse = g ? sqrt(err / g) : 0.0;
+    hh = h;
+  }
   for (int off = 32; off >= 1; off >>= 1) {
     const int og = __shfl_xor(good, off);
     const double orm = __shfl_xor(rmse, off);
@@ -244,20 +338,20 @@ __global__ __launch_bounds__(kRThreads) void ransac_score_kernel(
         rmse = sr[w];
         hh = shh[w];
       }
-    const int64_t o = (int64_t)b * nblk + blockIdx.x;
+    const int64_t o = (int64_t)b * nhb + blockIdx.x;
     bgood[o] = good;
     brmse[o] = rmse;
     bh[o] = hh;
   }
 }
 
-// grid (B), block 256: best over blocks, refit the winner -> T (4x4 row-major), stats.
-__global__ __launch_bounds__(256) void ransac_final_kernel(
-    const double* __restrict__ src, const int64_t* __restrict__ src_off, const double* __restrict__ dst,
-    const int64_t* __restrict__ dst_off, const int32_t* __restrict__ corres, const int64_t* __restrict__ cor_off,
-    const int32_t* __restrict__ hyps, const int64_t* __restrict__ hyp_off, uint64_t seed, int nblk,
-    const int* __restrict__ bgood, const double* __restrict__ brmse, const int64_t* __restrict__ bh,
-    double* __restrict__ T, double* __restrict__ stats) {
+// grid (B), block 256: best over blocks; the winner's stored pose -> T (4x4 row-major), stats.
+__global__ __launch_bounds__(256) void ransac_final_kernel(const int64_t* __restrict__ cor_off, int64_t H, int nblk,
+                                                           const double* __restrict__ RT,
+                                                           const int* __restrict__ bgood,
+                                                           const double* __restrict__ brmse,
+                                                           const int64_t* __restrict__ bh, double* __restrict__ T,
+                                                           double* __restrict__ stats) {
   __shared__ int sg[4];
   __shared__ double sr[4];
   __shared__ int64_t shh[4];
@@ -296,21 +390,17 @@ __global__ __launch_bounds__(256) void ransac_final_kernel(
       rmse = sr[w];
       hh = shh[w];
     }
-  const int64_t c0 = cor_off[b];
-  const int n = (int)(cor_off[b + 1] - c0);
+  const int n = (int)(cor_off[b + 1] - cor_off[b]);
   double* Tb = T + 16 * b;
   for (int k = 0; k < 16; ++k) Tb[k] = (k % 5 == 0) ? 1.0 : 0.0;
   stats[3 * b + 0] = 0.0;
   stats[3 * b + 1] = 0.0;
   stats[3 * b + 2] = -1.0;
   if (good < 0 || hh == INT64_MAX || n < 4) return;
-  double s4[4][3], d4[4][3], R[9], t[3];
-  load_hyp(src + 3 * src_off[b], dst + 3 * dst_off[b], corres + 2 * c0, n, seed, hh,
-           hyps ? hyps + 4 * hyp_off[b] : nullptr, s4, d4);
-  rigid_fit4(s4, d4, R, t);
-  for (int r = 0; r < 3; ++r) {
-    for (int c = 0; c < 3; ++c) Tb[4 * r + c] = R[3 * r + c];
-    Tb[4 * r + 3] = t[r];
+  const double* r = RT + (int64_t)b * 12 * H + hh;
+  for (int i = 0; i < 3; ++i) {
+    for (int c = 0; c < 3; ++c) Tb[4 * i + c] = r[(3 * i + c) * H];
+    Tb[4 * i + 3] = r[(9 + i) * H];
   }
   stats[3 * b + 0] = good > 0 ? (double)good / (double)n : 0.0;
   stats[3 * b + 1] = rmse;
@@ -319,24 +409,41 @@ __global__ __launch_bounds__(256) void ransac_final_kernel(
 
 }  // namespace
 
+extern "C" int64_t pk_ransac_work_size(int B, int64_t H, int nmax) {
+  if (B <= 0 || H < 0 || nmax < 0) return 0;
+  const int C = chunks_for(B, H, nmax);
+  const int64_t nhb = (H + kRThreads - 1) / kRThreads;
+  return align256((int64_t)B * 12 * H * 8) + align256((int64_t)B * C * H * 8) + align256((int64_t)B * C * H * 4) +
+         2 * align256((int64_t)B * nhb * 8) + align256((int64_t)B * nhb * 4);
+}
+
 extern "C" int pk_ransac(const double* src, const int64_t* src_off, const double* dst, const int64_t* dst_off,
                          const int32_t* corres, const int64_t* cor_off, const int32_t* hyps, const int64_t* hyp_off,
-                         uint64_t seed, int64_t H, double max_dist, int B, int* bgood, double* brmse, int64_t* bh,
+                         uint64_t seed, int64_t H, double max_dist, int B, int nmax, void* work, int64_t work_bytes,
                          double* T, double* stats, void* stream) {
-  PK_REQUIRE(B >= 0 && H >= 0 && max_dist > 0.0);
+  PK_REQUIRE(B >= 0 && H >= 0 && max_dist > 0.0 && nmax >= 0);
   if (B == 0) return PK_OK;
-  PK_REQUIRE(src && src_off && dst && dst_off && corres && cor_off && bgood && brmse && bh && T && stats);
+  PK_REQUIRE(src && src_off && dst && dst_off && corres && cor_off && work && T && stats);
   PK_REQUIRE(hyps == nullptr || hyp_off != nullptr);
+  PK_REQUIRE(work_bytes >= pk_ransac_work_size(B, H, nmax));
   hipStream_t s = pk::as_stream(stream);
-  const int nblk = (int)((H + kRThreads - 1) / kRThreads);
-  if (nblk > 0) {
-    hipLaunchKernelGGL(ransac_score_kernel, dim3(nblk, B), dim3(kRThreads), kRTile * 6 * sizeof(double), s, src,
-                       src_off, dst, dst_off, corres, cor_off, hyps, hyp_off, seed, H, max_dist * max_dist, nblk,
-                       bgood, brmse, bh);
+  const int nhb = (int)((H + kRThreads - 1) / kRThreads);
+  const int C = chunks_for(B, H, nmax);
+  const RansacWork w = carve(work, B, H, C, nhb);
+  if (nhb > 0) {
+    hipLaunchKernelGGL(ransac_fit_kernel, dim3(nhb, B), dim3(kRThreads), 0, s, src, src_off, dst, dst_off, corres,
+                       cor_off, hyps, hyp_off, seed, H, w.RT);
+    PK_CHECK_LAUNCH();
+    const int tile = min(kRTile, (nmax + C - 1) / C > 0 ? (nmax + C - 1) / C : 1);
+    hipLaunchKernelGGL(ransac_score_kernel, dim3(nhb * C, B), dim3(kRThreads), tile * 6 * sizeof(double), s, src,
+                       src_off, dst, dst_off, corres, cor_off, H, max_dist * max_dist, nhb, C, tile, w.RT, w.pg, w.pe);
+    PK_CHECK_LAUNCH();
+    hipLaunchKernelGGL(ransac_reduce_kernel, dim3(nhb, B), dim3(kRThreads), 0, s, cor_off, H, nhb, C, w.pg, w.pe,
+                       w.bgood, w.brmse, w.bh);
     PK_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(ransac_final_kernel, dim3(B), dim3(256), 0, s, src, src_off, dst, dst_off, corres, cor_off, hyps,
-                     hyp_off, seed, nblk, bgood, brmse, bh, T, stats);
+  hipLaunchKernelGGL(ransac_final_kernel, dim3(B), dim3(256), 0, s, cor_off, H, nhb, w.RT, w.bgood, w.brmse, w.bh,
+                     T, stats);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -183,8 +183,10 @@ class CropFormation:
     padding than the reference would. Default: "fixed" for npoint > 0, "batch" for 0."""
 
     def __init__(self, n1: int = 0, npoint: int = 1024, pair_cap: Optional[int] = None, seed: int = 0,
-                 with_mask: bool = True, pad: Optional[str] = None, limit: int = 2000, with_rgb: bool = False):
+                 with_mask: bool = True, pad: Optional[str] = None, limit: int = 2000, with_rgb: bool = False,
+                 base: int = 0):
         self.n1, self.npoint, self.limit = n1, npoint, limit
+        self.base = base  # global index of this batch's first crop (FPS start draws of a rank's shard)
         self.npmax = npoint if npoint > 0 else limit
         self.pair_cap = pair_cap or 64 * self.npmax
         self.seed = seed
@@ -199,7 +201,7 @@ class CropFormation:
         bp = ops.backproject(fb.depth, fb.mask, fb.K, fb.cam_scale, cap=F_ * fb.max_pixels)
         so = ops.sor(bp["xyz"], bp["off"], fb.max_pixels, 20, 0.3, pix=bp["pix"], idxmap=bp["idxmap"], K=fb.K,
                      want64=True, want32=True)
-        pol = ops.fps_npoint(so["off"], fixed=self.npoint, limit=self.limit, seed=self.seed)
+        pol = ops.fps_npoint(so["off"], fixed=self.npoint, limit=self.limit, seed=self.seed, base=self.base)
         npmax = self.npmax
         if self.pad == "batch":  # collate pads to the batch maximum: read it (host sync)
             ld = int((pol["off"][1:] - pol["off"][:-1]).max().item()) if F_ > 0 else 0

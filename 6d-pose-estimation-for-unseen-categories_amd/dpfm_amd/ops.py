@@ -158,13 +158,13 @@ def sor(xyz: torch.Tensor, off: torch.Tensor, nmax: int, knn: int = 20, std_rati
     return dict(avg=avg, thr=thr, kept=kept, off=out_off, xyz64=out64, xyz32=out32, kept_idx=kidx)
 
 
-def fps_npoint(off: torch.Tensor, fixed: int = 0, limit: int = 2000, seed: int = 0) -> dict:
+def fps_npoint(off: torch.Tensor, fixed: int = 0, limit: int = 2000, seed: int = 0, base: int = 0) -> dict:
     B = off.numel() - 1
     dev = off.device
     npoint = torch.empty((B,), dtype=torch.int32, device=dev)
     start = torch.empty((B,), dtype=torch.int32, device=dev)
     out_off = torch.empty((B + 1,), dtype=torch.int64, device=dev)
-    call("pk_fps_npoint", ptr(off), B, int(fixed), int(limit), ctypes_u64(seed), ptr(npoint), ptr(start),
+    call("pk_fps_npoint", ptr(off), B, int(fixed), int(limit), ctypes_u64(seed), int(base), ptr(npoint), ptr(start),
          ptr(out_off), _lib.stream(dev))
     return dict(npoint=npoint, start=start, off=out_off)
 
@@ -689,9 +689,11 @@ def rigidity_filter(cand: torch.Tensor, ncand: torch.Tensor, cad: torch.Tensor, 
     na = torch.empty((B,), dtype=torch.int32, device=dev)
     nb = torch.empty((B,), dtype=torch.int32, device=dev)
     score = torch.empty((B, L), dtype=torch.float32, device=dev)
+    # f32 VALU work of the first (largest) round: per candidate pair two 3-D distances and
+    # |a - b| accumulated, ~20 flops (the later rounds run on its survivors)
     call("pk_rigidity_filter", ptr(cand.contiguous()), L, ptr(ncand), ptr(cad.contiguous()), cad.shape[1],
          ptr(pc.contiguous()), pc.shape[1], ptr(thr4), B, L, ptr(la), ptr(lb), ptr(na), ptr(nb), ptr(score),
-         _lib.stream(dev))
+         _lib.stream(dev), work=("valu32", 20 * B * L * L))
     return lb, nb
 
 
@@ -719,22 +721,24 @@ def cgt_lstsq(pairs: torch.Tensor, npairs: torch.Tensor, evecs1: torch.Tensor, e
 
 def ransac(src: torch.Tensor, src_off: torch.Tensor, dst: torch.Tensor, dst_off: torch.Tensor,
            corres: torch.Tensor, cor_off: torch.Tensor, H: int, seed: int = 0, max_dist: float = 0.05,
-           hyps: Optional[torch.Tensor] = None, hyp_off: Optional[torch.Tensor] = None):
-    """Batched RANSAC pose fit (pk_ransac). Returns (T f64 [B,4,4], stats f64 [B,3])."""
+           hyps: Optional[torch.Tensor] = None, hyp_off: Optional[torch.Tensor] = None,
+           nmax: Optional[int] = None):
+    """Batched RANSAC pose fit (pk_ransac). nmax bounds the correspondences per crop (default:
+    all rows of `corres`). Returns (T f64 [B,4,4], stats f64 [B,3] = fitness, rmse, best h)."""
     B = cor_off.numel() - 1
     dev = src.device
-    nblk = max(1, (int(H) + 255) // 256)
-    bgood = torch.empty((B, nblk), dtype=torch.int32, device=dev)
-    brmse = torch.empty((B, nblk), dtype=torch.float64, device=dev)
-    bh = torch.empty((B, nblk), dtype=torch.int64, device=dev)
-    T = torch.empty((B, 4, 4), dtype=torch.float64, device=dev)
-    stats = torch.empty((B, 3), dtype=torch.float64, device=dev)
     corres = corres.to(torch.int32).contiguous()
     if corres.numel() == 0:  # every crop below ransac_n: keep a valid pointer, kernel returns identity
         corres = torch.zeros((1, 2), dtype=torch.int32, device=dev)
+    nmax = int(corres.shape[0]) if nmax is None else int(nmax)
+    nbytes = int(_lib.lib().pk_ransac_work_size(B, int(H), nmax))
+    work = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+    T = torch.empty((B, 4, 4), dtype=torch.float64, device=dev)
+    stats = torch.empty((B, 3), dtype=torch.float64, device=dev)
+    # fp64 VALU work: ~30 flops per (hypothesis, correspondence) residual + ~6000 per 4-point fit
     call("pk_ransac", ptr(src), ptr(src_off), ptr(dst), ptr(dst_off), ptr(corres),
-         ptr(cor_off), ptr(hyps), ptr(hyp_off), ctypes_u64(seed), int(H), float(max_dist), B, ptr(bgood),
-         ptr(brmse), ptr(bh), ptr(T), ptr(stats), _lib.stream(dev))
+         ptr(cor_off), ptr(hyps), ptr(hyp_off), ctypes_u64(seed), int(H), float(max_dist), B, nmax, ptr(work),
+         nbytes, ptr(T), ptr(stats), _lib.stream(dev), work=("valu64", B * int(H) * (30 * nmax + 6000)))
     return T, stats
 
 

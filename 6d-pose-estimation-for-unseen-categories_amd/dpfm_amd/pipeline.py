@@ -520,7 +520,7 @@ class InferStep:
         corres = torch.zeros((B * L + 1, 2), dtype=torch.int32, device=dev)
         corres.index_copy_(0, pos, p_pred.reshape(-1, 2).to(torch.int32))
         T, stats = ops.ransac(fb.cad64, fb.cad_off, crops.pc64, crops.off, corres, cor_off, self.H, seed=self.seed,
-                              max_dist=self.max_dist)
+                              max_dist=self.max_dist, nmax=L)
         T_gt = torch.zeros((B, 4, 4), dtype=torch.float64, device=dev)
         T_gt[:, :3, :3] = fb.R.view(B, 3, 3)
         T_gt[:, :3, 3] = fb.t
@@ -528,3 +528,56 @@ class InferStep:
         metrics = ops.pose_metrics(fb.cad64, fb.cad_off, V1, T, T_gt)
         return dict(C=C_pred, cand=cand, p_pred=p_pred, n_corr=nsurv, ir=ir, T=T, ransac=stats, metrics=metrics,
                     corres=corres, cor_off=cor_off)
+
+
+class GraphedInfer:
+    """Crop formation + InferStep captured once into a HIP graph and replayed (the inference
+    twin of GraphedTrainStep): frames, CAD models and operators stay resident; every replay
+    re-forms the crops and re-runs the model, correspondence head, RANSAC and metrics. The
+    returned dict's tensors are the graph's static outputs (overwritten by the next replay)."""
+
+    def __init__(self, crop_formation: CropFormation, infer: InferStep, fb: FrameBatch, op: Operators,
+                 warmup: int = 2):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                infer(fb, op, crop_formation(fb))
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = infer(fb, op, crop_formation(fb))
+
+    def __call__(self) -> dict:
+        self.graph.replay()
+        return self.out
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Rank-contiguous partition of n crops (configs[3]: 256 crops over 8 GPUs): rank r takes
+    [r*n//world, (r+1)*n//world)."""
+    return rank * n // world, (rank + 1) * n // world
+
+
+def gather_results(local: dict, keys=("T", "ir", "n_corr", "metrics"), group: Optional[dist.ProcessGroup] = None,
+                   world: int = 1) -> dict:
+    """all_gather of the per-crop results of sharded inference (poses, IR, counts, metrics) so
+    every rank holds the whole batch in global crop order. No collective runs with one rank.
+    Shards may differ in size by one crop: padded to the largest, then trimmed."""
+    if world <= 1:
+        return {k: local[k] for k in keys}
+    out = {}
+    n = torch.tensor([local[keys[0]].shape[0]], device=local[keys[0]].device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(sizes)
+    for k in keys:
+        t = local[k]
+        pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[:t.shape[0]] = t
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad, group=group)
+        out[k] = torch.cat([p[:s] for p, s in zip(parts, sizes)], 0)
+    return out

@@ -33,6 +33,9 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+F32_VALU_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector peak
+F64_VALU_TFLOPS = 78.6    # AMD MI355X datasheet FP64 vector (not in the guide; half the FP32 vector rate)
+BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense BF16
 
 
 def parse():
@@ -49,6 +52,11 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="graph mode without overlapping crop formation of the next batch")
     ap.add_argument("--probe-steps", type=int, default=2, help="eager steps after timing for the kernel breakdown")
+    ap.add_argument("--mode", choices=("train", "infer", "corr4096"), default="train",
+                    help="train: the headline fwd+bwd step (default); infer: configs[1]/[3] inference; "
+                         "corr4096: configs[4] feature distance + RANSAC")
+    ap.add_argument("--hypotheses", type=int, default=1024, help="RANSAC hypotheses per crop (infer/corr4096)")
+    ap.add_argument("--bf16", action="store_true", help="corr4096: bf16 feature-distance operands")
     return ap.parse_args()
 
 
@@ -177,8 +185,15 @@ def cpu_baseline(n_crops: int, n1: int, n2: int) -> dict:
             "seconds": round(dt, 2)}
 
 
-def main():
-    args = parse()
+TRAIN_METRIC = "RGB-D crops/sec (fwd+bwd), 1024 pts, at 1/2/4/8 MI355X; pose err vs ref"
+INFER_METRIC = ("RGB-D crops/sec (inference: crop formation + DPFM fwd + spatial-filter solver + IR + "
+                "RANSAC 1024 hyp + pose metrics)")
+CORR_METRIC = "4096-pt dense correspondence solves/sec (4096^2 feature distance + 1024-hypothesis RANSAC)"
+CROP_FAMS = {"pk_backproject", "pk_sor", "pk_fps_npoint", "pk_fps", "pk_gather_transform", "pk_collate_pad",
+             "pk_ball_query_mask", "pk_ball_query_pairs", "pk_sample_rgb", "pk_erode_mask"}
+
+
+def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -193,26 +208,117 @@ def main():
         dist.init_process_group(backend, rank=rank, world_size=world)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    return world, rank, dev
 
-    from dpfm_amd import _lib
+
+def build_train(args, dev, rank, world):
+    """configs[1] shape (configs[2] semantics for N > 1): one training step per iteration."""
     from dpfm_amd.dataset.object import CropFormation
     from dpfm_amd.models.dpfm import DPFMNet
     from dpfm_amd.pipeline import GraphedTrainStep, PipelinedTrainer, TrainStep, make_frame_batch
-
     B, N = args.batch, args.points
     torch.manual_seed(1234)  # identical initial weights on every rank (DDP broadcast semantics)
     model = DPFMNet().to(dev)
     fb, op = make_frame_batch(B, N, N, seed=1000 * rank, device=dev)
     crops_of = CropFormation(n1=N, npoint=N, seed=rank)
     step = TrainStep(model, seed=rank, capturable=not args.eager)
-
     if args.eager:
-        def one_step():
-            return step(op, crops_of(fb))
+        one_step = lambda: step(op, crops_of(fb))  # noqa: E731
     elif args.no_overlap:  # warm-up + capture (untimed), then every step is a graph replay
         one_step = GraphedTrainStep(crops_of, step, fb, op, warmup=3)
     else:  # same, with crop formation of the next batch on a second stream
         one_step = PipelinedTrainer(crops_of, step, fb, op, warmup=3)
+    config = {"workload": f"configs[1] shape: B={B} synthetic 640x480 RGB-D crops/GPU, {N} pts, training step "
+                          "fwd+bwd (configs[2] semantics, DDP over RCCL when N>1)",
+              "execution": "eager" if args.eager else ("hip-graph" if args.no_overlap else
+                                                       "hip-graph, crop formation overlapped"),
+              "global_batch": B * world, "points_per_crop": N, "cad_points": N,
+              "precision": "model fp32 (f32 MFMA); crop geometry / C_gt normal equations fp64",
+              "parallelism": f"dp{world}"}
+    probe = lambda: step(op, crops_of(fb))  # noqa: E731
+    return one_step, probe, TRAIN_METRIC, B, config
+
+
+def build_infer(args, dev, rank, world):
+    """configs[1] (B = 32 x 1024 pts, 1 GPU) / configs[3] (--points 2048; each rank infers its
+    own shard of the batch, no collective on the data path): one inference pass per iteration."""
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import GraphedInfer, InferStep, make_frame_batch
+    B, N = args.batch, args.points
+    torch.manual_seed(1234)
+    model = DPFMNet().to(dev).eval()
+    fb, op = make_frame_batch(B, N, N, seed=1000 * rank, device=dev)
+    crops_of = CropFormation(n1=N, npoint=N, seed=0, base=rank * B)
+    infer = InferStep(model, hypotheses=args.hypotheses, seed=0)
+    one_step = (lambda: infer(fb, op, crops_of(fb))) if args.eager else GraphedInfer(crops_of, infer, fb, op)
+    name = "configs[3] shard" if N == 2048 else "configs[1]"
+    config = {"workload": f"{name}: B={B} synthetic 640x480 RGB-D crops/GPU, {N} pts, inference (eval.py + "
+                          f"test_RANSAC.py: top-5 + 3-round rigidity filter + IR + RANSAC {args.hypotheses} "
+                          "hypotheses + ADD metrics), batch-sharded across ranks (weak scaling)",
+              "execution": "eager" if args.eager else "hip-graph",
+              "global_batch": B * world, "points_per_crop": N, "cad_points": N, "hypotheses": args.hypotheses,
+              "precision": "model fp32 (f32 MFMA); crop geometry / RANSAC fp64", "parallelism": f"shard{world}"}
+    probe = lambda: infer(fb, op, crops_of(fb))  # noqa: E731
+    return one_step, probe, INFER_METRIC, B, config
+
+
+def build_corr(args, dev, rank, world):
+    """configs[4]: one 4096-point crop vs a 4096-vertex CAD: the naive solver's feature
+    distance (naive.py:20-33, 4096 x 4096 x 30) and RANSAC with 1024 hypotheses over the
+    4096 point-map correspondences (test_RANSAC.py:288-310)."""
+    from dpfm_amd import ops
+    from dpfm_amd.dataset.synthetic import lbo_operators, random_rotation
+    V, H = 4096, args.hypotheses
+    rng = np.random.default_rng(4096 + rank)
+    ex = torch.from_numpy(lbo_operators(V, 64, 1)[2])[None].to(dev)
+    ey = torch.from_numpy(lbo_operators(V, 64, 2)[2])[None].to(dev)
+    C = (torch.eye(30) + 0.1 * torch.randn(30, 30, generator=torch.Generator().manual_seed(3)))[None].to(dev)
+    cad = rng.normal(size=(V, 3)) * 6
+    R = random_rotation(rng)
+    pc = (cad[rng.permutation(V)] + rng.normal(size=(V, 3)) * 0.02) @ R.T + np.array([2.0, -1.0, 90.0])
+    cad_t, pc_t = torch.from_numpy(cad).to(dev), torch.from_numpy(pc).to(dev)
+    off = torch.tensor([0, V], dtype=torch.int64, device=dev)
+    n = torch.full((1,), V, dtype=torch.int32, device=dev)
+    ar = torch.arange(V, dtype=torch.int32, device=dev)
+    bf16 = bool(args.bf16)
+
+    def solve():
+        idx, _ = ops.feat_dist_topk(ex, C, ey, n, n, 1, bf16=bf16) if bf16 else ops.feat_dist_topk(ex, C, ey, n, n, 1)
+        corres = torch.stack([idx[0, :, 0].to(torch.int32), ar], 1)
+        return {"T": ops.ransac(cad_t, off, pc_t, off, corres, off, H, seed=0, nmax=V)[0]}
+
+    one_step = solve
+    if not args.eager:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                solve()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = solve()
+
+        def one_step():
+            g.replay()
+            return out
+    config = {"workload": f"configs[4]: one crop, V1 = V2 = {V}: feature distance {V}x{V}x30 "
+                          f"({'bf16' if bf16 else 'fp32'} MFMA, K padded to 32) + argmin + RANSAC {H} hypotheses "
+                          f"over n = {V} correspondences", "execution": "eager" if args.eager else "hip-graph",
+              "global_batch": world, "points_per_crop": V, "cad_points": V, "hypotheses": H,
+              "precision": ("bf16 operands / f32 accumulate" if bf16 else "fp32") + " distance; fp64 RANSAC",
+              "parallelism": f"replicas{world}"}
+    return one_step, solve, CORR_METRIC, 1, config
+
+
+def main():
+    args = parse()
+    world, rank, dev = setup_dist()
+    from dpfm_amd import _lib
+    build = {"train": build_train, "infer": build_infer, "corr4096": build_corr}[args.mode]
+    one_step, probe_step, metric, units, config = build(args, dev, rank, world)
 
     for _ in range(args.warmup):
         one_step()
@@ -236,7 +342,12 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    loss_v, ir_v = float(log["loss"]), float(log["IR"])
+    extra = {}
+    if args.mode == "train":
+        extra = {"loss": round(float(log["loss"]), 5), "ir": round(float(log["IR"]), 5),
+                 "pair_overflow": bool(log["pair_overflow"])}
+    elif args.mode == "infer":
+        extra = {"mean_ir": round(float(log["ir"].mean()), 5), "mean_corr": round(float(log["n_corr"].float().mean()), 1)}
     probe_steps = args.steps
     if not args.eager:
         # per-kernel HIP events cannot sit inside a graph: time the same step eagerly, on
@@ -248,7 +359,7 @@ def main():
         for _ in range(args.probe_steps):
             torch.cuda.synchronize()
             torch.cuda._sleep(int(2.5e8))  # ~0.1 s of GPU clock cycles
-            step(op, crops_of(fb))
+            probe_step()
         torch.cuda.synchronize()
         _lib.set_probe(None)
         probe_steps = args.probe_steps
@@ -256,53 +367,86 @@ def main():
 
     if rank == 0:
         total_ms = elapsed * 1e3 / args.steps
-        # dominant kernel family on the critical path: in the pipelined execution crop
-        # formation runs on a second stream under the training step, so the training
-        # kernels bound the step; the crop-formation families are reported beside it
-        crop_fams = {"pk_backproject", "pk_sor", "pk_fps_npoint", "pk_fps", "pk_gather_transform",
-                     "pk_ball_query_mask", "pk_ball_query_pairs", "pk_sample_rgb", "pk_erode_mask"}
-        train_k = {k: v for k, v in kern.items() if k not in crop_fams} or kern
-        dom = max(train_k.items(), key=lambda kv: kv[1]["total_ms"]) if train_k else None
-        crop_k = {k: v for k, v in kern.items() if k in crop_fams}
+        # dominant kernel family on the critical path: in the pipelined training execution crop
+        # formation runs on a second stream under the training step, so the training kernels
+        # bound the step; the crop-formation families are reported beside it
+        overlapped = args.mode == "train" and not args.no_overlap and not args.eager
+        main_k = {k: v for k, v in kern.items() if not (overlapped and k in CROP_FAMS)} or kern
+        dom = max(main_k.items(), key=lambda kv: kv[1]["total_ms"]) if main_k else None
+        crop_k = {k: v for k, v in kern.items() if k in CROP_FAMS}
         dom_crop = max(crop_k.items(), key=lambda kv: kv[1]["total_ms"]) if crop_k else None
         kernels = {k: {"avg_ms": round(v["avg_ms"], 4), "launches": v["launches"],
                        "ms_per_step": round(v["total_ms"] / max(probe_steps, 1), 4)}
                    for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"])}
         roof = roofline_for(dom[0], dom[1]) if dom is not None else None  # None: --probe-steps 0
-        mfma_fams = {k: roofline_for(k, v) for k, v in kern.items() if v["bound"] == "mfma"}
+        mfma_fams = {k: roofline_for(k, v) for k, v in kern.items() if v["bound"] in ("mfma", "mfma_bf16")}
         out = {
-            "metric": "RGB-D crops/sec (fwd+bwd), 1024 pts, at 1/2/4/8 MI355X; pose err vs ref",
-            "value": round(B * world / elapsed * args.steps, 3),
-            "unit": "crops/s",
+            "metric": metric,
+            "value": round(units * world / elapsed * args.steps, 3),
+            "unit": "crops/s" if args.mode != "corr4096" else "solves/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(total_ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32", "data": "synthetic (seeded ellipsoid RGB-D frames, random-init DPFM)",
-            "config": {"workload": "configs[1] shape: B=32 synthetic 640x480 RGB-D crops/GPU, 1024 pts, "
-                                   "training step fwd+bwd (configs[2] semantics, DDP over RCCL when N>1)",
-                       "execution": "eager" if args.eager else ("hip-graph" if args.no_overlap else
-                                                                 "hip-graph, crop formation overlapped"),
-                       "global_batch": B * world, "points_per_crop": N, "cad_points": N,
-                       "precision": "model fp32 (f32 MFMA); crop geometry / C_gt normal equations fp64",
-                       "parallelism": f"dp{world}"},
+            "dtype": "bf16" if (args.mode == "corr4096" and args.bf16) else "fp32",
+            "data": "synthetic (seeded ellipsoid RGB-D frames, random-init DPFM)",
+            "config": config,
             "roofline": roof,
             "roofline_crop_formation": (dict(roofline_for(dom_crop[0], dom_crop[1]),
                                              stream="side (overlapped with the training step)")
-                                        if dom_crop is not None and not args.no_overlap and not args.eager else
+                                        if dom_crop is not None and overlapped else
                                         (roofline_for(dom_crop[0], dom_crop[1]) if dom_crop else None)),
             "roofline_mfma_kernels": {k: {"achieved": v["achieved"], "frac": v["frac"], "unit": v["unit"]}
                                       for k, v in mfma_fams.items()},
             "kernels": kernels,
-            "loss": round(loss_v, 5), "ir": round(ir_v, 5),
         }
-        if not args.no_roofline_probe and world == 1:
+        out.update(extra)
+        if args.mode == "train" and not args.no_roofline_probe and world == 1:
             out["roofline_ball_query"] = ball_query_roofline(dev)
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_crops, N, N)
+            if args.mode == "train":
+                out["cpu_baseline"] = cpu_baseline(args.cpu_crops, args.points, args.points)
+            elif args.mode == "corr4096":
+                out["cpu_baseline"] = cpu_ransac_baseline(args.hypotheses)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def cpu_ransac_baseline(H: int, V: int = 4096, sample_h: int = 0) -> dict:
+    """configs[4]'s pose stage on the host: the C/OpenMP restatement of Open3D 0.17's
+    RegistrationRANSACBasedOnCorrespondence loop (oracle/c/oracle.c oc_ransac_o3d: per
+    hypothesis a 4-point Umeyama, the WHOLE source cloud transformed as Open3D's loop does, the
+    correspondences scored), on the same 4096-vertex CAD / 4096 correspondences; H hypotheses
+    timed, the reference's 4x10^6 extrapolated linearly (stated as such)."""
+    import ctypes
+    from dpfm_amd.dataset.synthetic import random_rotation
+    so = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+    lib = ctypes.CDLL(so)
+    P = ctypes.c_void_p
+    lib.oc_ransac_o3d.argtypes = [P, ctypes.c_int, P, P, ctypes.c_int, P, ctypes.c_uint64, ctypes.c_int64,
+                                  ctypes.c_double, P, P]
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    rng = np.random.default_rng(4096)
+    cad = np.ascontiguousarray(rng.normal(size=(V, 3)) * 6)
+    R = random_rotation(rng)
+    pc = np.ascontiguousarray((cad[rng.permutation(V)] + rng.normal(size=(V, 3)) * 0.02) @ R.T + np.array([2.0, -1.0, 90.0]))
+    corres = np.ascontiguousarray(np.stack([rng.integers(0, V, V), np.arange(V)], 1).astype(np.int32))
+    T, st = np.zeros(16), np.zeros(3)
+    cp = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    h = sample_h or H
+    lib.oc_ransac_o3d(cp(cad), V, cp(pc), cp(corres), V, None, 0, 64, 0.05, cp(T), cp(st))  # warm-up
+    t0 = time.perf_counter()
+    lib.oc_ransac_o3d(cp(cad), V, cp(pc), cp(corres), V, None, 0, h, 0.05, cp(T), cp(st))
+    dt = time.perf_counter() - t0
+    import platform
+    return {"value": round(1.0 / (dt * H / h), 4), "unit": "solves/s (RANSAC stage only, H = %d)" % H,
+            "cores": threads, "kind": "port",
+            "sample": f"{h} hypotheses x {V} correspondences, {V}-vertex source transformed per hypothesis "
+                      f"(Open3D's loop), C/OpenMP on {platform.processor() or 'host'}",
+            "seconds": round(dt, 3),
+            "reference_4e6_hypotheses_s_extrapolated": round(dt * 4e6 / h, 1)}
 
 
 def pmc_traffic(name: str):
@@ -328,10 +472,18 @@ def roofline_for(name: str, k: dict) -> dict:
     if k["work"] is None:
         return dict(base, bound="hbm", achieved=None, peak=HBM_PEAK_GBS, unit="GB/s", frac=None, traffic=traffic)
     sec = k["total_ms"] * 1e-3
-    if k["bound"] == "mfma":
+    if k["bound"] in ("mfma", "mfma_bf16"):
         ach = k["work"] / sec / 1e12
-        r = dict(base, bound="mfma", achieved=round(ach, 3), peak=F32_MFMA_TFLOPS, unit="TFLOP/s",
-                 frac=round(ach / F32_MFMA_TFLOPS, 4), traffic=traffic)
+        peak = F32_MFMA_TFLOPS if k["bound"] == "mfma" else BF16_MFMA_TFLOPS
+        r = dict(base, bound="mfma", achieved=round(ach, 3), peak=peak, unit="TFLOP/s",
+                 frac=round(ach / peak, 4), traffic=traffic)
+        if k["bound"] == "mfma_bf16":
+            r["dtype"] = "bf16"
+    elif k["bound"] in ("valu32", "valu64"):
+        ach = k["work"] / sec / 1e12
+        peak = F32_VALU_TFLOPS if k["bound"] == "valu32" else F64_VALU_TFLOPS
+        r = dict(base, bound=k["bound"], achieved=round(ach, 3), peak=peak, unit="TFLOP/s",
+                 frac=round(ach / peak, 4), traffic=traffic)
     else:
         ach = k["work"] / sec / 1e9
         r = dict(base, bound="hbm", achieved=round(ach, 2), peak=HBM_PEAK_GBS, unit="GB/s",

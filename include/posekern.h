@@ -94,9 +94,10 @@ int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, int knn, doub
 /* FPS sample-count policy of dataset/object.py:145-147 on device counts (no host sync):
  * fixed > 0: npoint = fixed if n > fixed, else -n; fixed <= 0: npoint = int(limit/n * n)
  * if n > limit, else -n (negative = keep all n points in order, no FPS: the reference's
- * `if pcd.shape[0] > 2000` branch). start[b] = splitmix64(seed ^ splitmix64(b)) % n
- * (replaces upstream torch.randint; may be NULL). out_off int64 [B+1]. */
-int pk_fps_npoint(const int64_t* off, int B, int fixed, int limit, uint64_t seed,
+ * `if pcd.shape[0] > 2000` branch). start[b] = splitmix64(seed ^ splitmix64(base + b)) % n
+ * (replaces upstream torch.randint; may be NULL; base = the global index of crop 0, so a
+ * rank's shard draws the starts the whole batch would). out_off int64 [B+1]. */
+int pk_fps_npoint(const int64_t* off, int B, int fixed, int limit, uint64_t seed, int64_t base,
                   int32_t* npoint, int32_t* start, int64_t* out_off, void* stream);
 
 /* H4 pcd[idx0] (dataset/object.py:148) + transform(pcd, R, t, inv=True) (:174, :304-309).
@@ -316,15 +317,19 @@ int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs, const flo
 
 /* H13 RANSAC + Umeyama (scripts/test_RANSAC.py:288-310, Open3D 0.17 semantics, ransac_n 4).
  *   src f64 (CAD) / dst f64 (crop, camera frame) packed [T,3] with src_off/dst_off [B+1];
- *   corres int32 [sum n_b, 2] (src row, dst row) packed by cor_off int64 [B+1]
+ *   corres int32 [sum n_b, 2] (src row, dst row) packed by cor_off int64 [B+1]; nmax >= every
+ *   n_b (host bound: sizes the correspondence chunks that spread one crop over the chip)
  *   hyps int32 [sum H_b, 4] correspondence rows (packed by hyp_off) or NULL: then draw j
  *   of hypothesis h is splitmix64(seed ^ splitmix64(4h + j)) % n_b
  *   H hypotheses per crop; inlier iff ||T s - d||^2 < max_dist^2
- *   bgood int32 / brmse f64 / bh int64 [B, ceil(H/256)] scratch
- *   T f64 [B,4,4] row-major best pose, stats f64 [B,3] (fitness, inlier rmse, best h). */
+ *   work: scratch of pk_ransac_work_size(B, H, nmax) bytes (fitted poses, per-chunk scores)
+ *   T f64 [B,4,4] row-major best pose, stats f64 [B,3] (fitness, inlier rmse, best h).
+ * Best = (fitness desc, rmse asc, index asc). A crop's error sum is taken per chunk in
+ * correspondence order, then over chunks in order. */
+int64_t pk_ransac_work_size(int B, int64_t H, int nmax);
 int pk_ransac(const double* src, const int64_t* src_off, const double* dst, const int64_t* dst_off,
               const int32_t* corres, const int64_t* cor_off, const int32_t* hyps, const int64_t* hyp_off,
-              uint64_t seed, int64_t H, double max_dist, int B, int* bgood, double* brmse, int64_t* bh,
+              uint64_t seed, int64_t H, double max_dist, int B, int nmax, void* work, int64_t work_bytes,
               double* T, double* stats, void* stream);
 
 /* H14 pose metrics of scripts/test_RANSAC.py:77-81, 154-238 for B crops:

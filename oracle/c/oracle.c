@@ -236,3 +236,68 @@ int oc_ransac(const double* src, const double* dst, const int32_t* corres /* [n,
   }
   return 0;
 }
+
+/* Open3D 0.17 RegistrationRANSACBasedOnCorrespondence's per-iteration cost shape, for the
+ * CPU baseline (bench.py cpu_ransac_baseline): like oc_ransac, but each hypothesis copies
+ * and transforms the WHOLE source cloud (V1 points; Open3D: `pcd = source;
+ * pcd.Transform(T)`) before scoring the correspondences on the transformed copy. Same
+ * selection rule and draws as oc_ransac. */
+int oc_ransac_o3d(const double* src, int V1, const double* dst, const int32_t* corres, int n,
+                  const int32_t* hyps, uint64_t seed, int64_t H, double max_dist, double* T, double* out_stats) {
+  for (int k = 0; k < 16; ++k) T[k] = (k % 5 == 0) ? 1.0 : 0.0;
+  out_stats[0] = 0.0; out_stats[1] = 0.0; out_stats[2] = -1.0;
+  if (n < 4 || max_dist <= 0.0 || H <= 0) return 0;
+  const double max_d2 = max_dist * max_dist;
+  double best_f = -1.0, best_r = 0.0;
+  int64_t best_h = -1;
+  double best_R[9], best_t[3];
+#pragma omp parallel
+  {
+    double lf = -1.0, lr = 0.0;
+    int64_t lh = -1;
+    double lR[9], lt[3];
+    double* pcd = (double*)malloc(sizeof(double) * 3 * (size_t)V1);
+#pragma omp for schedule(static)
+    for (int64_t h = 0; h < H; ++h) {
+      double s4[12], d4[12];
+      for (int j = 0; j < 4; ++j) {
+        const int32_t c = hyps ? hyps[4 * h + j] : oc_hyp_index(seed, h, j, n);
+        memcpy(s4 + 3 * j, src + 3 * (int64_t)corres[2 * c], 3 * sizeof(double));
+        memcpy(d4 + 3 * j, dst + 3 * (int64_t)corres[2 * c + 1], 3 * sizeof(double));
+      }
+      double R[9], t[3];
+      oc_umeyama(s4, d4, 4, R, t);
+      for (int i = 0; i < V1; ++i) {
+        const double* s = src + 3 * (int64_t)i;
+        for (int r = 0; r < 3; ++r) pcd[3 * i + r] = ((R[3 * r] * s[0] + R[3 * r + 1] * s[1]) + R[3 * r + 2] * s[2]) + t[r];
+      }
+      int good = 0;
+      double err = 0.0;
+      for (int i = 0; i < n; ++i) {
+        const double* p = pcd + 3 * (int64_t)corres[2 * i];
+        const double* d = dst + 3 * (int64_t)corres[2 * i + 1];
+        const double ex = p[0] - d[0], ey = p[1] - d[1], ez = p[2] - d[2];
+        const double d2 = (ex * ex + ey * ey) + ez * ez;
+        if (d2 < max_d2) { ++good; err += d2; }
+      }
+      const double f = good ? (double)good / n : 0.0;
+      const double r = good ? sqrt(err / good) : 0.0;
+      if (f > lf || (f == lf && r < lr)) { lf = f; lr = r; lh = h; memcpy(lR, R, sizeof(lR)); memcpy(lt, t, sizeof(lt)); }
+    }
+    free(pcd);
+#pragma omp critical
+    {
+      if (lh >= 0 && (lf > best_f || (lf == best_f && (lr < best_r || (lr == best_r && lh < best_h))))) {
+        best_f = lf; best_r = lr; best_h = lh; memcpy(best_R, lR, sizeof(lR)); memcpy(best_t, lt, sizeof(lt));
+      }
+    }
+  }
+  if (best_h >= 0) {
+    for (int r = 0; r < 3; ++r) {
+      for (int c = 0; c < 3; ++c) T[4 * r + c] = best_R[3 * r + c];
+      T[4 * r + 3] = best_t[r];
+    }
+    out_stats[0] = best_f; out_stats[1] = best_r; out_stats[2] = (double)best_h;
+  }
+  return 0;
+}

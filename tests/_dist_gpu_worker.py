@@ -37,6 +37,45 @@ def main():
     out = [torch.zeros_like(flat_p) for _ in range(world)]
     dist.all_gather(out, flat_p)
     assert all(torch.equal(out[0], o) for o in out), "parameters diverged across ranks"
+    # (3) the HIP-graph paths bench.py uses for N > 1: graph A (crops -> backward), the eager
+    # flat all-reduce, graph B (clip + RMSprop)
+    from dpfm_amd.pipeline import GraphedTrainStep, PipelinedTrainer
+
+    def same_params(st):
+        flat = torch.cat([p.detach().reshape(-1) for p in st.params]).cpu()
+        got = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(got, flat)
+        return all(torch.equal(got[0], o) for o in got)
+
+    cf = CropFormation(n1=256, npoint=256, seed=rank)
+    torch.manual_seed(1)
+    gstep = TrainStep(DPFMNet().to(dev), seed=rank, capturable=True)
+    g = GraphedTrainStep(cf, gstep, fb, op, warmup=1)
+    assert g.split
+    for _ in range(3):
+        g.graph_a.replay()                       # this rank's gradient into the flat buffer
+        local = gstep.flat.detach().clone().cpu()
+        every = [torch.zeros_like(local) for _ in range(world)]
+        dist.all_gather(every, local)
+        gstep.allreduce_grads()
+        torch.cuda.synchronize()
+        mean = torch.stack(every).mean(0)
+        assert torch.allclose(gstep.flat.cpu(), mean, rtol=1e-6, atol=1e-7 * float(mean.abs().max())), \
+            "graphed step: averaged gradient != mean of the ranks' gradients"
+        g.graph_b.replay()
+        torch.cuda.synchronize()
+        assert same_params(gstep), "graphed step: parameters diverged across ranks"
+    torch.manual_seed(2)
+    pstep = TrainStep(DPFMNet().to(dev), seed=rank, capturable=True)
+    pipe = PipelinedTrainer(cf, pstep, fb, op, warmup=1)
+    for _ in range(4):
+        pipe()
+        torch.cuda.synchronize()
+        assert same_params(pstep), "pipelined trainer: parameters diverged across ranks"
+        flat = pstep.flat.detach().cpu()
+        got = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(got, flat)
+        assert all(torch.equal(got[0], o) for o in got), "pipelined trainer: reduced gradients differ"
     dist.barrier()
     dist.destroy_process_group()
     if rank == 0:

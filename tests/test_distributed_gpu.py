@@ -21,12 +21,24 @@ def _free_port():
     return port
 
 
+def _launch(worker, marker):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "tests", worker)]
+    r = subprocess.run(cmd, env=dict(os.environ), cwd=ROOT, capture_output=True, text=True, timeout=220)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert marker in r.stdout
+
+
 @pytest.mark.timeout(240)
 def test_two_rank_flat_allreduce_on_gpu():
-    env = dict(os.environ)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "tests", "_dist_gpu_worker.py")]
-    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=220)
-    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
-    assert "dist-gpu ok" in r.stdout
+    """flat all-reduce mean; eager, GraphedTrainStep and PipelinedTrainer steps (graph A |
+    eager all-reduce | graph B): the averaged gradient equals the mean of the ranks' own
+    gradients and parameters stay identical across ranks over several replays."""
+    _launch("_dist_gpu_worker.py", "dist-gpu ok")
+
+
+@pytest.mark.timeout(240)
+def test_sharded_inference_equals_single_rank():
+    """configs[3] sharding: 2 ranks x 2 crops give bit-identical poses, IR, correspondence
+    counts, metrics and C to one process over the 4 crops."""
+    _launch("_dist_infer_worker.py", "sharded-infer ok")
