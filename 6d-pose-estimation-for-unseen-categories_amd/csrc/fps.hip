@@ -286,11 +286,13 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
   PK_REQUIRE(xyz && offsets && start && npoint && out);
   hipStream_t s = pk::as_stream(stream);
 #define PK_FPS(NT, PPT) return launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s)
+  // 1024-thread workgroups above 4096 points: measured 0.715 us per FPS step against 0.782
+  // (512 threads) and 1.078 (256) on the configs' crops (n <= 6588, profiles/r01_kbench.txt)
   if (nmax <= 1024) PK_FPS(256, 4);
   if (nmax <= 2048) PK_FPS(256, 8);
   if (nmax <= 4096) PK_FPS(256, 16);
-  if (nmax <= 8192) PK_FPS(512, 16);
-  if (nmax <= 13312) PK_FPS(512, 26);
+  if (nmax <= 8192) PK_FPS(1024, 8);
+  if (nmax <= 13312) PK_FPS(1024, 13);
   if (nmax <= 32768) PK_FPS(1024, 32);
 #undef PK_FPS
   return PK_ERR_ARG;  // > 32768 points per crop

@@ -136,3 +136,39 @@ def test_two_rank_gradient_allreduce_matches_global_batch():
     for r in range(world):
         for got, exp in zip(loss[r], full):
             np.testing.assert_allclose(got, exp.numpy(), rtol=1e-9, atol=1e-10)
+
+
+def _gather_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from dpfm_amd.pipeline import gather_results, shard_range
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    G = 7  # uneven shards: 3 + 4
+    lo, hi = shard_range(G, rank, world)
+    idx = torch.arange(lo, hi)
+    local = {"T": idx.double()[:, None, None].expand(-1, 4, 4).contiguous(), "ir": idx.float() / 10,
+             "n_corr": idx.int(), "metrics": idx.double()[:, None].expand(-1, 7).contiguous()}
+    out = gather_results(local, world=world)
+    q.put((rank, {k: v.clone() for k, v in out.items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_inference_gather_cpu():
+    """configs[3] sharding on gloo / CPU: rank-contiguous shards of a 7-crop batch (3 + 4),
+    the all_gather of per-crop results restores global crop order on every rank."""
+    from dpfm_amd.pipeline import shard_range
+    assert [shard_range(256, r, 8) for r in (0, 7)] == [(0, 32), (224, 256)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        out = res[r]
+        assert torch.equal(out["n_corr"], torch.arange(7).int())
+        assert torch.equal(out["T"][:, 0, 0], torch.arange(7).double())
+        assert torch.equal(out["ir"], torch.arange(7).float() / 10)
