@@ -678,7 +678,54 @@ __global__ __launch_bounds__(256) void sample_rgb_kernel(const uint8_t* __restri
     out[(o + i) * C + c] = acc * (1.f / 255.f);
   }
 }
+
+// H16, f32 backbone features: the same projection and bilinear weights on an f32 feature
+// map [F, C, H, W] (channels-first, as a CNN backbone emits it). Thread = (point, channel),
+// channel fastest, so the [T, C] output rows are written contiguously.
+__global__ __launch_bounds__(256) void sample_feat_kernel(const float* __restrict__ fmap, int C, int H, int W,
+                                                          const double* __restrict__ K,
+                                                          const double* __restrict__ pts,
+                                                          const int64_t* __restrict__ off, int nmax,
+                                                          float* __restrict__ out) {
+  const int f = blockIdx.y;
+  const int64_t o = off[f];
+  const int n = (int)(off[f + 1] - o);
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int i = (int)(e / C), c = (int)(e - (int64_t)i * C);
+  if (i >= n || i >= nmax) return;
+  const double* p = pts + 3 * (o + i);
+  const double* Kf = K + 9 * f;
+  const float u = (float)(Kf[0] * p[0] / p[2] + Kf[2]);
+  const float v = (float)(Kf[4] * p[1] / p[2] + Kf[5]);
+  const float u0f = floorf(u), v0f = floorf(v);
+  const int u0 = (int)u0f, v0 = (int)v0f;
+  const float au = u - u0f, av = v - v0f;
+  const float* pl = fmap + ((int64_t)f * C + c) * H * W;
+  float acc = 0.f;
+#pragma unroll
+  for (int dv = 0; dv < 2; ++dv)
+#pragma unroll
+    for (int du = 0; du < 2; ++du) {
+      const int uu = u0 + du, vv = v0 + dv;
+      const float w = (du ? au : 1.f - au) * (dv ? av : 1.f - av);
+      if (uu >= 0 && uu < W && vv >= 0 && vv < H) acc = fmaf(w, pl[(int64_t)vv * W + uu], acc);
+    }
+  out[(o + i) * C + c] = acc;
+}
 }  // namespace
+
+extern "C" int pk_sample_features(const float* fmap, int F, int C, int H, int W, const double* K, const double* pts,
+                                  const int64_t* off, int nmax, float* out, void* stream) {
+  PK_REQUIRE(F >= 0 && H > 0 && W > 0 && C > 0 && nmax >= 0);
+  if (F == 0 || nmax == 0) return PK_OK;
+  PK_REQUIRE(fmap && K && pts && off && out);
+  const int64_t blocks = ((int64_t)nmax * C + 255) / 256;
+  PK_REQUIRE(blocks < (1LL << 31));
+  hipLaunchKernelGGL(sample_feat_kernel, dim3((unsigned)blocks, F), dim3(256), 0, pk::as_stream(stream), fmap, C, H,
+                     W, K, pts, off, nmax, out);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
 
 extern "C" int pk_erode_mask(const uint8_t* mask, int F, int H, int W, uint8_t* out, void* stream) {
   PK_REQUIRE(F >= 0 && H > 0 && W > 0);

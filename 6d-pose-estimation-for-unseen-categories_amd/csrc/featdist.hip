@@ -7,113 +7,147 @@
 //     spatial: idx = dist.sort(dim=-2)[1].T[:, :5]         (5 nearest i per j)
 // torch.cdist (V > 25) evaluates the mm expansion with K = 32:
 //     [-2 x, |x|^2, 1] · [y, 1, |y|^2]^T, clamp_min(1e-30), sqrt
-// The kernel computes exactly that augmented K = 32 contraction on the f32 MFMA
-// (v_mfma_f32_16x16x4_f32: f32 products, f32 accumulation), clamps, and keeps per
-// column a running argmin (or sorted top-5) in the epilogue; sqrt is monotone and is
-// applied to the emitted distances only. Ties resolve to the lowest row index.
 //
-// Pass 1 (prep) writes both augmented operands straight into MFMA operand order:
-// for a 16-row tile T, lane l = 16 g + c (g = k mod 4 group, c = row in tile) owns the
-// 8 floats k = 4 s + g, s = 0..7, of row 16 T + c — so pass 2 loads one operand set
-// with two 16-byte loads per lane and no LDS, no transposes, no barriers.
-//   A  [B, T1, 64 lanes, 8]  T1 = ceil16(V1max) / 16   (x side, rows reduced over)
-//   Bq [B, T2, 64 lanes, 8]  T2 = ceil16(V2max) / 16   (y side, one column set per wave)
-// Pass 2: a wave owns 32 columns (two B operands in 16 VGPRs) and a quarter of the row
-// tiles of A, streamed through registers two tiles per step (four independent
-// accumulators, 32 MFMAs per A tile pair) with the next two tiles' loads in flight, so
-// the matrix pipe issues back to back while the other waves on the SIMD run their
-// epilogues; the four row parts of a column pair merge through LDS.
+// Precision modes (the contraction only; the selection epilogue is shared):
+//   0 (default, the parity path): exactly that augmented K = 32 contraction on the f32 MFMA
+//     (v_mfma_f32_16x16x4_f32: f32 products, f32 accumulation).
+//   1 bf16: the cross term -2 x·y on v_mfma_f32_16x16x32_bf16 (K = 30 padded to 32, one
+//     instruction per 16 x 16 tile), |x|^2 + |y|^2 added in f32 in the epilogue.
+//   2 bf16x3: the cross term as hi·hi + hi·lo + lo·hi of a two-term bf16 split of both
+//     operands (three bf16 MFMAs, ~16 significant bits), norms in f32 as in mode 1.
+// Modes 1 / 2 are opt-in (configs[4]'s "4096 x 4096 bf16"); tests report their argmin
+// agreement with mode 0.
+//
+// Pass 1 (prep): one thread per row computes the row's operand (x side: emb = x C^T, an fmaf
+// chain over k in order; y side: y) and its squared norm, and writes the operand straight
+// into MFMA operand-tile order (16-row tiles, lane l = 16 g + c holding row c's k values of
+// its group g), so pass 2 moves whole tiles with 16-byte loads and no transposes.
+// Pass 2 (main): a block = 4 waves x CW column tiles (B operands in registers); the crop's
+// row tiles (or the block's share of them, RS row splits) stream through a two-stage LDS
+// ring shared by the 4 waves (one barrier per chunk of CH tiles): every A tile read from L2
+// feeds 4 CW column tiles. Epilogue per 16 x 16 tile: running argmin / sorted top-5 per
+// column (ties: lowest row). With RS > 1 the row parts write partial lists that pass 3
+// merges (same tie rule), so one 4096-point crop (configs[4]) still spreads over the chip.
+#include <algorithm>
+
 #include "common.hpp"
 
 namespace {
 
 constexpr int kF = 30;   // n_fmap
-constexpr int kK = 32;   // augmented contraction length
+constexpr int kK = 32;   // contraction length (K padded)
+constexpr int kCW = 1;   // column tiles per wave
+constexpr int kWaves = 4;
+constexpr int kCols = kWaves * kCW * 16;  // columns per block
+constexpr int kCH = 8;   // row tiles per LDS stage
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 
-// grid (ceil(max(T1, T2) * 16 / 64), B, 2), block 256: thread = (row r = tid / 4, group
-// g = tid % 4) computes the 8 augmented entries k = 4 s + g of its row.
-//   z = 0 (x side): emb = x C^T; entries -2 emb[k] (k < 30), |emb|^2 (k = 30), 1 (k = 31)
-//   z = 1 (y side): y[k] (k < 30), 1 (k = 30), |y|^2 (k = 31)
-// |.|^2 is the fmaf chain over k = 0..29 in order (the 4 lanes of a row exchange their
-// values). Rows r >= n[b] (and the tile padding up to 16) are written as zeros.
+// bytes of one 16-row operand tile per mode (f32: 64 lanes x 8 floats; bf16: 64 x 8 bf16;
+// bf16x3: hi then lo)
+__host__ __device__ constexpr int tile_bytes(int mode) { return mode == 0 ? 2048 : mode == 1 ? 1024 : 2048; }
+
+__device__ __forceinline__ __bf16 to_bf16(float v) { return (__bf16)v; }
+
+// grid (ceil(max(T1, T2) / 4), B, 2), block 256: wave = one 16-row tile of one side (z = 0:
+// x side, 1: y side). Lane (g, c) = (lane >> 4, lane & 15).
+//   x side: emb = x C^T on the f32 MFMA ([16 x 32] x [32 x 32], two 16 x 16 output tiles,
+//           K = 30 zero-padded; an f32 MFMA accumulates as the fmaf chain over k in order),
+//           then through LDS into the operand layout;
+//   y side: y itself.
+// The squared norm of a row is its lane group's 8 values summed per lane, then across the 4
+// lanes of the row (fixed order). Rows >= n (and the tile padding) are written as zeros.
+template <int MODE>
 __global__ __launch_bounds__(256) void fd_prep_kernel(const float* __restrict__ ex, int ldx,
-                                                      const float* __restrict__ C,
-                                                      const float* __restrict__ ey, int ldy,
-                                                      const int32_t* __restrict__ n1,
-                                                      const int32_t* __restrict__ n2, int V1max, int V2max,
-                                                      int T1, int T2, float* __restrict__ A,
-                                                      float* __restrict__ Bq) {
+                                                      const float* __restrict__ C, const float* __restrict__ ey,
+                                                      int ldy, const int32_t* __restrict__ n1,
+                                                      const int32_t* __restrict__ n2, int V1max, int V2max, int T1,
+                                                      int T2, char* __restrict__ A, char* __restrict__ Bq,
+                                                      float* __restrict__ nA, float* __restrict__ nB) {
+  __shared__ float E[4][16][kK + 1];  // per wave: the tile's rows (emb or y), k padded to 32
   const int b = blockIdx.y;
-  const int g = threadIdx.x & 3;
-  const int r = blockIdx.x * 64 + (threadIdx.x >> 2);
   const bool xside = blockIdx.z == 0;
+  const int w = pk::wave_id(), lane = pk::lane_id(), g = lane >> 4, c16 = lane & 15;
   const int T = xside ? T1 : T2;
-  // C transposed per thread group: sCt[k][g][s] = C[4 s + g][k] (0 for rows 30, 31), so a
-  // thread's 8 coefficients of one k are two 16-byte LDS reads
-  __shared__ __attribute__((aligned(16))) float sCt[kF * 4 * 8];
-  if (xside) {
-    for (int e = threadIdx.x; e < kF * 32; e += 256) {
-      const int k = e >> 5, gg = (e >> 3) & 3, ss = e & 7;
-      const int c = 4 * ss + gg;
-      sCt[e] = c < kF ? C[((int64_t)b * kF + c) * kF + k] : 0.f;
-    }
-    __syncthreads();
-  }
-  if (r >= T * 16) return;  // whole rows (4 adjacent lanes) leave together
-  const int nvalid = xside ? n1[b] : n2[b];
-  const bool valid = r < nvalid;
-  float e[8];  // emb (x side) or y (y side) at k = 4 s + g
-  if (xside) {
-    const float* er = ex + ((int64_t)b * V1max + (valid ? r : 0)) * ldx;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) e[s] = 0.f;
-#pragma unroll 6
-    for (int k = 0; k < kF; ++k) {  // emb[c] = sum_k x[k] C[c][k], fmaf chain in k order
-      const float xk = valid ? er[k] : 0.f;
-      const float4* cp = reinterpret_cast<const float4*>(&sCt[(k * 4 + g) * 8]);
-      const float4 c0 = cp[0], c1 = cp[1];
-      e[0] = fmaf(xk, c0.x, e[0]);
-      e[1] = fmaf(xk, c0.y, e[1]);
-      e[2] = fmaf(xk, c0.z, e[2]);
-      e[3] = fmaf(xk, c0.w, e[3]);
-      e[4] = fmaf(xk, c1.x, e[4]);
-      e[5] = fmaf(xk, c1.y, e[5]);
-      e[6] = fmaf(xk, c1.z, e[6]);
-      e[7] = fmaf(xk, c1.w, e[7]);
-    }
-  } else {
-    const float* er = ey + ((int64_t)b * V2max + (valid ? r : 0)) * ldy;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int c = 4 * s + g;
-      e[s] = (valid && c < kF) ? er[c] : 0.f;
-    }
-  }
-  float nrm = 0.f;
-  const int base = threadIdx.x & ~3;
+  const int tile = blockIdx.x * 4 + w;
+  if (tile >= T) return;
+  const int nval = xside ? n1[b] : n2[b];
+  const int r = tile * 16 + c16;
+  const bool valid = r < nval;
+  const float* rowp = xside ? ex + ((int64_t)b * V1max + (valid ? r : 0)) * ldx
+                            : ey + ((int64_t)b * V2max + (valid ? r : 0)) * ldy;
+  // this lane's 8 row values at k = 4 s + g (the f32 MFMA operand layout), 0 past k = 29
+  float xv[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
+    const int k = 4 * s + g;
+    xv[s] = (valid && k < kF) ? rowp[k] : 0.f;
+  }
+  float (*Ew)[kK + 1] = E[w];
+  if (xside) {
+    // D[row 4 g' + q][col c] of output tile n: emb[row][16 n + c] = sum_k x[row][k] C[16 n + c][k]
 #pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      const float q = __shfl(e[s], base | gg);
-      if (4 * s + gg < kF) nrm = fmaf(q, q, nrm);
+    for (int n = 0; n < 2; ++n) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const int cc = 16 * n + c16;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int k = 4 * s + g;
+        const float cv = (cc < kF && k < kF) ? C[((int64_t)b * kF + cc) * kF + k] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s], cv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Ew[4 * g + q][cc] = acc[q];
     }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) Ew[c16][4 * s + g] = xv[s];
   }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  // the lane's operand values (mode 0: k = 4 s + g; bf16 modes: k = 8 g + j) and the row norm
   float v[8];
+  float part = 0.f;
 #pragma unroll
-  for (int s = 0; s < 8; ++s) v[s] = xside ? -2.f * e[s] : e[s];
-  if (!valid) {
-#pragma unroll
-    for (int s = 0; s < 8; ++s) v[s] = 0.f;
-  } else if (g >= 2) {  // k = 30, 31
-    v[7] = (xside == (g == 2)) ? nrm : 1.f;
+  for (int s = 0; s < 8; ++s) {
+    const int k = MODE == 0 ? 4 * s + g : 8 * g + s;
+    v[s] = (valid && k < kF) ? Ew[c16][k] : 0.f;
+    part = fmaf(v[s], v[s], part);
   }
-  const int tile = r >> 4, c16 = r & 15;
-  float* dst = (xside ? A + (int64_t)b * T1 * 512 : Bq + (int64_t)b * T2 * 512) +
-               ((int64_t)tile * 64 + g * 16 + c16) * 8;
-  reinterpret_cast<float4*>(dst)[0] = make_float4(v[0], v[1], v[2], v[3]);
-  reinterpret_cast<float4*>(dst)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  const float p1 = __shfl_xor(part, 16), p2 = __shfl_xor(part, 32), p3 = __shfl_xor(part, 48);
+  const float mine[4] = {part, p1, p2, p3};  // lane group g, g^1, g^2, g^3
+  float nrm = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) nrm += mine[q ^ g];  // groups 0, 1, 2, 3 in that order
+  // padding rows: y side zeros; x side a row whose distance to every column is +inf (mode 0:
+  // the |x|^2 slot; bf16 modes: the norm), so the main pass needs no row mask
+  if (!valid) nrm = xside ? __builtin_huge_valf() : 0.f;
+  char* base = (xside ? A + (int64_t)b * T1 * tile_bytes(MODE) : Bq + (int64_t)b * T2 * tile_bytes(MODE)) +
+               (int64_t)tile * tile_bytes(MODE);
+  if (MODE == 0) {
+    // augmented operand: x side [-2 emb, |emb|^2, 1], y side [y, 1, |y|^2]
+    float o[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) o[s] = xside ? -2.f * v[s] : v[s];
+    if (g >= 2 && valid) o[7] = (xside == (g == 2)) ? nrm : 1.f;  // k = 30 (g = 2), 31 (g = 3)
+    if (g == 2 && xside && !valid) o[7] = nrm;                      // +inf |x|^2 slot
+    float4* d = reinterpret_cast<float4*>(base + (size_t)lane * 32);
+    d[0] = make_float4(o[0], o[1], o[2], o[3]);
+    d[1] = make_float4(o[4], o[5], o[6], o[7]);
+  } else {
+    // bf16 cross-term operand: x side -2 emb, y side y (k < 30, zero pad); k = 8 g + j
+    bf16x8 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float f = xside ? -2.f * v[j] : v[j];
+      const __bf16 h = to_bf16(f);
+      hi[j] = h;
+      lo[j] = to_bf16(f - (float)h);
+    }
+    *reinterpret_cast<bf16x8*>(base + (size_t)lane * 16) = hi;
+    if (MODE == 2) *reinterpret_cast<bf16x8*>(base + 1024 + (size_t)lane * 16) = lo;
+    if (g == 0) (xside ? nA + (int64_t)b * T1 * 16 : nB + (int64_t)b * T2 * 16)[r] = nrm;
+  }
 }
 
 template <int TOPK>
@@ -169,39 +203,11 @@ struct TopK {
   }
 };
 
-__device__ __forceinline__ void load_tile(const float* __restrict__ At, int t, int lane, float (&a)[8]) {
-  const float4* p = reinterpret_cast<const float4*>(At + ((int64_t)t * 64 + lane) * 8);
-  const float4 u = p[0], w = p[1];
-  a[0] = u.x; a[1] = u.y; a[2] = u.z; a[3] = u.w;
-  a[4] = w.x; a[5] = w.y; a[6] = w.z; a[7] = w.w;
-}
-
+// 4 distances of this lane (rows ibase .. ibase + 3 of its column) into the running top-k
 template <int TOPK>
-__device__ __forceinline__ void epilogue(const f32x4& acc, int ibase, int N1, bool partial, TopK<TOPK>& best) {
-  if (TOPK == 1) {
-    // the 4 rows of this lane in one go: min of the clamped values (2 min + 1 max), and
-    // only when it beats the running best (rare once warmed up) find its first row
-    float v[4];
+__device__ __forceinline__ void epilogue(const float (&d)[4], int ibase, TopK<TOPK>& best) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = (partial && ibase + r >= N1) ? __builtin_huge_valf() : acc[r];
-    const float mc = fmaxf(fminf(fminf(v[0], v[1]), fminf(v[2], v[3])), 1e-30f);  // clamp_min(1e-30)
-    if (mc < best.v[0]) {
-      int r = 3;
-      if (fmaxf(v[2], 1e-30f) == mc) r = 2;
-      if (fmaxf(v[1], 1e-30f) == mc) r = 1;
-      if (fmaxf(v[0], 1e-30f) == mc) r = 0;
-      best.v[0] = mc;
-      best.i[0] = ibase + r;
-    }
-    return;
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int i = ibase + r;
-    float v = fmaxf(acc[r], 1e-30f);  // clamp_min(1e-30) (cdist mm path)
-    if (partial && i >= N1) v = __builtin_huge_valf();
-    best.push(v, i);
-  }
+  for (int r = 0; r < 4; ++r) best.push(fmaxf(d[r], 1e-30f), ibase + r);  // clamp_min(1e-30) (cdist mm path)
 }
 
 template <int TOPK>
@@ -219,189 +225,362 @@ __device__ __forceinline__ void lanegroup_merge(TopK<TOPK>& best) {
   }
 }
 
-// grid (B * ceil(T2 / CW)), block 64 RP: the block owns CW column tiles (their B operands
-// stay in registers, so every A tile load feeds 8 CW MFMAs) and wave q takes the q-th of
-// RP parts of the row tiles; the parts merge through LDS (ties: lower row first). One
-// step = two row tiles x CW column tiles on 2 CW independent accumulators, the next
-// step's A tiles in flight (two register sets, written out twice so nothing is copied).
-template <int TOPK, int CW, int RP, bool NOEPI = false, bool NOLOAD = false>
-__global__ __launch_bounds__(64 * RP) void fd_main_kernel(const float* __restrict__ A, const float* __restrict__ Bq,
-                                                          const int32_t* __restrict__ n1,
-                                                          const int32_t* __restrict__ n2, int T1, int T2, int V2max,
-                                                          int64_t* __restrict__ out_idx,
-                                                          float* __restrict__ out_dist) {
-  __shared__ float xv[RP][CW][16][TOPK];
-  __shared__ int xi[RP][CW][16][TOPK];
-  // 1-D grid of B x NC blocks (NC = column groups per crop), renumbered so that all blocks
-  // of crop b run on XCD b % 8 (hardware block L lands on XCD L % 8): a crop's A operand
-  // (128 KiB at V1 = 1024) is then read from one XCD's L2 instead of all eight.
-  const int NC = (T2 + CW - 1) / CW;
-  const int B = (int)(gridDim.x / NC);
-  int b, cg;
-  {
-    const int L = blockIdx.x, x8 = L & 7, k = L >> 3;
+// One 16 x 16 tile (rows of A tile `a`, this wave's column tile) -> 4 values per lane
+// (rows 4 g + r, column c16).
+template <int MODE>
+struct Frag;
+template <> struct Frag<0> { float a[8]; };
+template <> struct Frag<1> { bf16x8 hi; float n[4]; };
+template <> struct Frag<2> { bf16x8 hi, lo; float n[4]; };
+
+template <int MODE>
+__device__ __forceinline__ void read_frag(const char* __restrict__ tile, const float* __restrict__ ntile, int lane,
+                                          Frag<MODE>& f) {
+  if constexpr (MODE == 0) {
+    const float4* p = reinterpret_cast<const float4*>(tile + lane * 32);
+    const float4 u = p[0], w = p[1];
+    f.a[0] = u.x; f.a[1] = u.y; f.a[2] = u.z; f.a[3] = u.w;
+    f.a[4] = w.x; f.a[5] = w.y; f.a[6] = w.z; f.a[7] = w.w;
+  } else {
+    f.hi = *reinterpret_cast<const bf16x8*>(tile + lane * 16);
+    if constexpr (MODE == 2) f.lo = *reinterpret_cast<const bf16x8*>(tile + 1024 + lane * 16);
+    const float4 n = *reinterpret_cast<const float4*>(ntile + 4 * (lane >> 4));
+    f.n[0] = n.x; f.n[1] = n.y; f.n[2] = n.z; f.n[3] = n.w;
+  }
+}
+
+template <int MODE>
+struct BOp;
+template <> struct BOp<0> { float b[8]; };
+template <> struct BOp<1> { bf16x8 hi; float n; };
+template <> struct BOp<2> { bf16x8 hi, lo; float n; };
+
+template <int MODE>
+__device__ __forceinline__ void tile_dist(const Frag<MODE>& a, const BOp<MODE>& b, float (&d)[4]) {
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (MODE == 0) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.a[s], b.b[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) d[r] = acc[r];
+  } else {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, acc, 0, 0, 0);
+    if constexpr (MODE == 2) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo, b.hi, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) d[r] = (acc[r] + a.n[r]) + b.n;  // |x|^2 - 2 x.y + |y|^2
+  }
+}
+
+// Top-1 running state of a lane: per row offset r (rows 16 t + 4 g + r of its column) the
+// smallest clamped distance so far, as its f32 bit pattern (clamped values are positive, so
+// their bit patterns order as the values do), and the tile t holding it. Per distance: integer
+// max (the clamp), difference, sign mask, bit-select, integer min — no compare-to-VCC, so the
+// four chains interleave with each other and the MFMAs without hazard stalls. Ties stay with
+// the earliest tile because tiles arrive in increasing order and only a strictly smaller key
+// moves the tile.
+struct Top1x4 {
+  int k[4];
+  int t[4];
+};
+
+// kCH row tiles of one LDS chunk against this wave's column tile
+template <int MODE>
+__device__ __forceinline__ void chunk_dist(const char* rb, const float* nb, const BOp<MODE>& bo, int lane,
+                                           float (&d)[kCH][4]) {
+#pragma unroll
+  for (int t = 0; t < kCH; ++t) {
+    Frag<MODE> f;
+    read_frag<MODE>(rb + tile_bytes(MODE) * t, nb + t * 16, lane, f);
+    tile_dist<MODE>(f, bo, d[t]);
+  }
+}
+
+// the selection over one chunk's distances (tiles c0 .. c0 + kCH - 1)
+template <int TOPK>
+__device__ __forceinline__ void chunk_select(const float (&d)[kCH][4], int c0, int g, TopK<TOPK>& best, Top1x4& b4) {
+  if constexpr (TOPK == 1) {
+    constexpr int kClamp = 0x0da24260;  // bits of 1e-30f: clamp_min(1e-30) (cdist mm path)
+#pragma unroll
+    for (int t = 0; t < kCH; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = max(__float_as_int(d[t][r]), kClamp);
+        const int m = (key - b4.k[r]) >> 31;  // -1 iff key < best (both in [kClamp, 0x7fffffff])
+        b4.t[r] = (m & (c0 + t)) | (~m & b4.t[r]);
+        b4.k[r] = min(key, b4.k[r]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < kCH; ++t) epilogue<TOPK>(d[t], (c0 + t) * 16 + 4 * g, best);
+  }
+}
+
+// grid (B * NCG * RS) (1-D, XCD-aware), block 256. Block = (crop b, column group cg: wave w
+// takes column tile 4 cg + w, row split rs: row tiles [tb, te) of the crop's valid ones).
+template <int TOPK, int MODE>
+__global__ __launch_bounds__(64 * kWaves) void fd_main_kernel(
+    const char* __restrict__ A, const char* __restrict__ Bq, const float* __restrict__ nA,
+    const float* __restrict__ nB, const int32_t* __restrict__ n1, const int32_t* __restrict__ n2, int T1, int T2,
+    int V2max, int NCG, int RS, int64_t* __restrict__ out_idx, float* __restrict__ out_dist,
+    float* __restrict__ part_v, int32_t* __restrict__ part_i) {
+  constexpr int TB = tile_bytes(MODE);
+  __shared__ __attribute__((aligned(16))) char ring[2][kCH][TB];
+  __shared__ __attribute__((aligned(16))) float nring[2][kCH][16];
+  const int per = NCG * RS;
+  const int B = (int)(gridDim.x / per);
+  int b, k;
+  {  // all blocks of crop b on XCD b % 8 (hardware block L lands on XCD L % 8) when B % 8 == 0
+    const int L = blockIdx.x;
     if ((B & 7) == 0) {
-      b = x8 + 8 * (k / NC);
-      cg = k - (k / NC) * NC;
+      const int x8 = L & 7, q = L >> 3;
+      b = x8 + 8 * (q / per);
+      k = q - (q / per) * per;
     } else {
-      b = L / NC;
-      cg = L - b * NC;
+      b = L / per;
+      k = L - b * per;
     }
   }
-  const int lane = pk::lane_id(), q = pk::wave_id();
+  const int cg = k % NCG, rs = k / NCG;
+  const int lane = pk::lane_id(), w = pk::wave_id();
   const int g = lane >> 4, c16 = lane & 15;
-  const int ct0 = cg * CW;
+  const int ct = cg * kWaves + w;  // this wave's column tile
   const int N1 = n1[b], N2 = n2[b];
-  const int nt = (N1 + 15) >> 4;  // row tiles holding valid rows
-  const int t_begin = (nt * q) / RP, t_end = (nt * (q + 1)) / RP;
-  TopK<TOPK> best[CW];
-  float bop[CW][8];
-#pragma unroll
-  for (int c = 0; c < CW; ++c) {
-    best[c].init();
-    if (ct0 + c < T2) load_tile(Bq + (int64_t)b * T2 * 512, ct0 + c, lane, bop[c]);
-    else {
-#pragma unroll
-      for (int s = 0; s < 8; ++s) bop[c][s] = 0.f;
-    }
-  }
-  const float* At = A + (int64_t)b * T1 * 512;
-  float p0[8], p1[8], q0[8], q1[8];
-  const bool ragged = (N1 & 15) != 0;  // only then does the last tile need row masking
-  auto step = [&](int t, const float (&a0)[8], const float (&a1)[8]) {
-    f32x4 c0[CW], c1[CW];
-#pragma unroll
-    for (int c = 0; c < CW; ++c) c0[c] = c1[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-#pragma unroll
-      for (int c = 0; c < CW; ++c) {
-        c0[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], bop[c][s], c0[c], 0, 0, 0);
-        c1[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], bop[c][s], c1[c], 0, 0, 0);
-      }
-    }
-    // lane holds D[16 t + 4 g + r][col] (c0) and D[16 (t+1) + 4 g + r][col] (c1)
-    const bool two = t + 1 < t_end;
-    if (NOEPI) {  // development variant: MFMA + operand streaming only
-#pragma unroll
-      for (int c = 0; c < CW; ++c) best[c].v[0] += c0[c][0] + c1[c][3];
-      return;
-    }
-    if (ragged && t + 2 >= nt) {  // wave-uniform: the crop's last, partial tile
-#pragma unroll
-      for (int c = 0; c < CW; ++c) {
-        epilogue<TOPK>(c0[c], t * 16 + 4 * g, N1, true, best[c]);
-        if (two) epilogue<TOPK>(c1[c], (t + 1) * 16 + 4 * g, N1, true, best[c]);
-      }
+  const int nt = (N1 + 15) >> 4;
+  const int tb = (nt * rs) / RS, te = (nt * (rs + 1)) / RS;
+  const bool col_ok = ct < T2 && ct * 16 < N2;
+  BOp<MODE> bo;
+  if (col_ok) {
+    const char* bt = Bq + ((int64_t)b * T2 + ct) * TB;
+    if constexpr (MODE == 0) {
+      const float4* p = reinterpret_cast<const float4*>(bt + lane * 32);
+      const float4 u = p[0], v = p[1];
+      bo.b[0] = u.x; bo.b[1] = u.y; bo.b[2] = u.z; bo.b[3] = u.w;
+      bo.b[4] = v.x; bo.b[5] = v.y; bo.b[6] = v.z; bo.b[7] = v.w;
     } else {
+      bo.hi = *reinterpret_cast<const bf16x8*>(bt + lane * 16);
+      if constexpr (MODE == 2) bo.lo = *reinterpret_cast<const bf16x8*>(bt + 1024 + lane * 16);
+      bo.n = nB[((int64_t)b * T2 + ct) * 16 + c16];
+    }
+  } else {
+    if constexpr (MODE == 0) {
 #pragma unroll
-      for (int c = 0; c < CW; ++c) {
-        epilogue<TOPK>(c0[c], t * 16 + 4 * g, N1, false, best[c]);
-        if (two) epilogue<TOPK>(c1[c], (t + 1) * 16 + 4 * g, N1, false, best[c]);
+      for (int s = 0; s < 8; ++s) bo.b[s] = 0.f;
+    } else {
+      bo.hi = bf16x8{};
+      if constexpr (MODE == 2) bo.lo = bf16x8{};
+      bo.n = 0.f;
+    }
+  }
+  TopK<TOPK> best;
+  best.init();
+  Top1x4 b4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    b4.k[r] = 0x7f800000;  // +inf: never replaced by an equal key
+    b4.t[r] = 0x7fffffff;
+  }
+  const char* At = A + (int64_t)b * T1 * TB;
+  const float* nAt = MODE != 0 ? nA + (int64_t)b * T1 * 16 : nullptr;
+  // staging: a chunk of kCH tiles = kCH * TB bytes, 16 B per thread per step
+  constexpr int VPT = kCH * TB / 16 / (64 * kWaves);  // float4s per thread per chunk
+  float4 stage[VPT];
+  float nst = 0.f;  // one norm per thread (threads < kCH * 16)
+  auto gload = [&](int c0, int cn) {
+    const float4* src = reinterpret_cast<const float4*>(At + (int64_t)c0 * TB);
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+      const int e = threadIdx.x + 64 * kWaves * v;
+      if (e < cn * TB / 16) {
+        stage[v] = src[e];
+      } else {  // past the row part: padding rows (+inf |x|^2 slot in mode 0: lane group 2, k = 30)
+        const int q = e % (TB / 16);
+        const bool inf_slot = MODE == 0 && (q & 1) && (q >> 5) == 2;
+        stage[v] = make_float4(0.f, 0.f, 0.f, inf_slot ? __builtin_huge_valf() : 0.f);
       }
     }
+    if (MODE != 0 && threadIdx.x < kCH * 16)
+      nst = threadIdx.x < cn * 16 ? nAt[(int64_t)c0 * 16 + threadIdx.x] : __builtin_huge_valf();
   };
-  if (t_begin < t_end) load_tile(At, t_begin, lane, p0);
-  if (t_begin + 1 < t_end) load_tile(At, t_begin + 1, lane, p1);
-  if (NOLOAD) {  // development variant: operands loaded once, reused every step
+  auto lstore = [&](int buf) {
+    float4* dst = reinterpret_cast<float4*>(&ring[buf][0][0]);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      q0[s] = p0[s];
-      q1[s] = p1[s];
-    }
-  }
-  for (int t = t_begin; t < t_end; t += 4) {
-    if (!NOLOAD && t + 2 < t_end) load_tile(At, t + 2, lane, q0);
-    if (!NOLOAD && t + 3 < t_end) load_tile(At, t + 3, lane, q1);
-    step(t, p0, p1);
-    if (t + 2 >= t_end) break;
-    if (!NOLOAD && t + 4 < t_end) load_tile(At, t + 4, lane, p0);
-    if (!NOLOAD && t + 5 < t_end) load_tile(At, t + 5, lane, p1);
-    step(t + 2, q0, q1);
-  }
-#pragma unroll
-  for (int c = 0; c < CW; ++c) {
-    lanegroup_merge<TOPK>(best[c]);
-    if (g == 0) {
-#pragma unroll
-      for (int k = 0; k < TOPK; ++k) {
-        xv[q][c][c16][k] = best[c].v[k];
-        xi[q][c][c16][k] = best[c].i[k];
-      }
-    }
+    for (int v = 0; v < VPT; ++v) dst[threadIdx.x + 64 * kWaves * v] = stage[v];
+    if (MODE != 0 && threadIdx.x < kCH * 16) (&nring[buf][0][0])[threadIdx.x] = nst;
+  };
+  const int nch = (te - tb + kCH - 1) / kCH;
+  if (nch > 0) {
+    gload(tb, min(kCH, te - tb));
+    lstore(0);
   }
   __syncthreads();
-  // lanes 16 cw + c16 of wave 0 (cw < CW) finish column tile ct0 + cw
-  const int cw = lane >> 4;
-  if (q != 0 || cw >= CW || ct0 + cw >= T2) return;
-  TopK<TOPK> fin;
+  // software pipeline: the selection over chunk ci - 1 (registers) runs beside the MFMAs of
+  // chunk ci; dp starts as +inf (never selected)
+  float dp[kCH][4];
 #pragma unroll
-  for (int k = 0; k < TOPK; ++k) {
-    fin.v[k] = xv[0][cw][c16][k];
-    fin.i[k] = xi[0][cw][c16][k];
+  for (int t = 0; t < kCH; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dp[t][r] = __builtin_huge_valf();
+  int cp = 0;
+  for (int ci = 0; ci < nch; ++ci) {
+    const int c0 = tb + ci * kCH;
+    if (ci + 1 < nch) gload(c0 + kCH, min(kCH, te - c0 - kCH));
+    if (col_ok) {
+      float d[kCH][4];
+      chunk_dist<MODE>(&ring[ci & 1][0][0], &nring[ci & 1][0][0], bo, lane, d);
+      chunk_select<TOPK>(dp, cp, g, best, b4);
+#pragma unroll
+      for (int t = 0; t < kCH; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dp[t][r] = d[t][r];
+      cp = c0;
+    }
+    if (ci + 1 < nch) lstore((ci + 1) & 1);
+    __syncthreads();
   }
+  if (!col_ok) return;
+  chunk_select<TOPK>(dp, cp, g, best, b4);
+  if constexpr (TOPK == 1) {  // the 4 row offsets: smallest value, ties lowest row
 #pragma unroll
-  for (int qq = 1; qq < RP; ++qq) {
+    for (int r = 0; r < 4; ++r) {
+      const int row = b4.t[r] == 0x7fffffff ? 0x7fffffff : b4.t[r] * 16 + 4 * g + r;
+      const float v = __int_as_float(b4.k[r]);
+      const bool take = v < best.v[0] || (v == best.v[0] && row < best.i[0]);
+      best.v[0] = take ? v : best.v[0];
+      best.i[0] = take ? row : best.i[0];
+    }
+  }
+  lanegroup_merge<TOPK>(best);
+  const int j = ct * 16 + c16;
+  if (g != 0 || j >= N2) return;
+  if (RS == 1) {
+    const int64_t o = ((int64_t)b * V2max + j) * TOPK;
+#pragma unroll
+    for (int q = 0; q < TOPK; ++q) {
+      out_idx[o + q] = best.i[q] == 0x7fffffff ? -1 : best.i[q];
+      if (out_dist) out_dist[o + q] = sqrtf(best.v[q]);
+    }
+  } else {
+    const int64_t o = (((int64_t)b * RS + rs) * V2max + j) * TOPK;
+#pragma unroll
+    for (int q = 0; q < TOPK; ++q) {
+      part_v[o + q] = best.v[q];
+      part_i[o + q] = best.i[q];
+    }
+  }
+}
+
+// pass 3 (RS > 1): grid (ceil(V2max / 256), B): merge the RS partial lists of each column in
+// row-split order (ties: lower row).
+template <int TOPK>
+__global__ __launch_bounds__(256) void fd_merge_kernel(const float* __restrict__ part_v,
+                                                       const int32_t* __restrict__ part_i,
+                                                       const int32_t* __restrict__ n2, int V2max, int RS,
+                                                       int64_t* __restrict__ out_idx, float* __restrict__ out_dist) {
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n2[b]) return;
+  TopK<TOPK> best;
+  best.init();
+  for (int rs = 0; rs < RS; ++rs) {
+    const int64_t o = (((int64_t)b * RS + rs) * V2max + j) * TOPK;
     float ov[TOPK];
     int oi[TOPK];
 #pragma unroll
-    for (int k = 0; k < TOPK; ++k) {
-      ov[k] = xv[qq][cw][c16][k];
-      oi[k] = xi[qq][cw][c16][k];
+    for (int q = 0; q < TOPK; ++q) {
+      ov[q] = part_v[o + q];
+      oi[q] = part_i[o + q];
     }
-    fin.merge(ov, oi);
+    best.merge(ov, oi);
   }
-  const int j = (ct0 + cw) * 16 + c16;
-  if (j < N2) {
-    const int64_t o = ((int64_t)b * V2max + j) * TOPK;
+  const int64_t o = ((int64_t)b * V2max + j) * TOPK;
 #pragma unroll
-    for (int k = 0; k < TOPK; ++k) {
-      out_idx[o + k] = fin.i[k] == 0x7fffffff ? -1 : fin.i[k];
-      if (out_dist) out_dist[o + k] = sqrtf(fin.v[k]);
-    }
+  for (int q = 0; q < TOPK; ++q) {
+    out_idx[o + q] = best.i[q] == 0x7fffffff ? -1 : best.i[q];
+    if (out_dist) out_dist[o + q] = sqrtf(best.v[q]);
   }
 }
 
-constexpr int kFdCW = 2;  // column tiles per wave (4 measured slower: 136 VGPRs)
-constexpr int kFdRP = 4;  // row parts (waves) per block
+struct FdPlan {
+  int T1, T2, NCG, RS;
+  int64_t a_bytes, b_bytes, na_bytes, nb_bytes, pv_bytes, pi_bytes;
+};
+
+inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+inline FdPlan fd_plan(int B, int V1max, int V2max, int topk, int mode) {
+  FdPlan p{};
+  p.T1 = (V1max + 15) / 16;
+  p.T2 = (V2max + 15) / 16;
+  p.NCG = (p.T2 + kWaves * kCW - 1) / (kWaves * kCW);
+  const int64_t blocks = (int64_t)B * p.NCG;
+  int rs = blocks >= 512 ? 1 : (int)((512 + blocks - 1) / blocks);
+  const int max_rs = std::max(1, p.T1 / (2 * kCH));  // at least two chunks per row part
+  p.RS = std::min(rs, max_rs);
+  const int TB = tile_bytes(mode);
+  p.a_bytes = al256((int64_t)B * p.T1 * TB);
+  p.b_bytes = al256((int64_t)B * p.T2 * TB);
+  p.na_bytes = mode ? al256((int64_t)B * p.T1 * 16 * 4) : 0;
+  p.nb_bytes = mode ? al256((int64_t)B * p.T2 * 16 * 4) : 0;
+  p.pv_bytes = p.RS > 1 ? al256((int64_t)B * p.RS * V2max * topk * 4) : 0;
+  p.pi_bytes = p.pv_bytes;
+  return p;
+}
 
 }  // namespace
 
-extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, const float* evecs_y, int ldy,
-                                 const int32_t* n1, const int32_t* n2, int B, int V1max, int V2max, int topk,
-                                 float* A, float* Bq, int64_t* out_idx, float* out_dist, void* stream) {
-  PK_REQUIRE(B >= 0 && V1max >= 0 && V2max >= 0 && ldx >= kF && ldy >= kF && (topk == 1 || topk == 5));
-  if (B == 0 || V2max == 0) return PK_OK;
-  PK_REQUIRE(evecs_x && C && evecs_y && n1 && n2 && A && Bq && out_idx);
-  hipStream_t s = pk::as_stream(stream);
-  const int T1 = (V1max + 15) / 16, T2 = (V2max + 15) / 16;
-  const int rows = (T1 > T2 ? T1 : T2) * 16;
-  hipLaunchKernelGGL(fd_prep_kernel, dim3((rows + 63) / 64, B, 2), dim3(256), 0, s, evecs_x, ldx, C, evecs_y, ldy,
-                     n1, n2, V1max, V2max, T1, T2, A, Bq);
-  PK_CHECK_LAUNCH();
-  const dim3 grid(((T2 + kFdCW - 1) / kFdCW) * B), block(64 * kFdRP);
-  if (topk == 1)
-    hipLaunchKernelGGL((fd_main_kernel<1, kFdCW, kFdRP>), grid, block, 0, s, A, Bq, n1, n2, T1, T2, V2max, out_idx,
-                       out_dist);
-  else
-    hipLaunchKernelGGL((fd_main_kernel<5, kFdCW, kFdRP>), grid, block, 0, s, A, Bq, n1, n2, T1, T2, V2max, out_idx,
-                       out_dist);
-  PK_CHECK_LAUNCH();
-  return PK_OK;
+extern "C" int64_t pk_feat_dist_work_size(int B, int V1max, int V2max, int topk, int mode) {
+  if (B < 0 || V1max < 0 || V2max < 0 || !(topk == 1 || topk == 5) || mode < 0 || mode > 2) return -1;
+  const FdPlan p = fd_plan(B, V1max, V2max, topk, mode);
+  return p.a_bytes + p.b_bytes + p.na_bytes + p.nb_bytes + p.pv_bytes + p.pi_bytes;
 }
 
-// Development hook (not in include/posekern.h): the main pass without its top-k epilogue,
-// on operands already prepared by pk_feat_dist_topk (A, Bq), to time the MFMA pipeline.
-extern "C" int pkdev_fd_main_noepi(const float* A, const float* Bq, const int32_t* n1, const int32_t* n2, int B,
-                                   int V1max, int V2max, int64_t* out_idx, int noload, void* stream) {
-  const int T1 = (V1max + 15) / 16, T2 = (V2max + 15) / 16;
-  const dim3 grid(((T2 + kFdCW - 1) / kFdCW) * B), block(64 * kFdRP);
-  if (noload)
-    hipLaunchKernelGGL((fd_main_kernel<1, kFdCW, kFdRP, true, true>), grid, block, 0, pk::as_stream(stream), A, Bq, n1,
-                       n2, T1, T2, V2max, out_idx, nullptr);
-  else
-    hipLaunchKernelGGL((fd_main_kernel<1, kFdCW, kFdRP, true>), grid, block, 0, pk::as_stream(stream), A, Bq, n1, n2,
-                       T1, T2, V2max, out_idx, nullptr);
+extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, const float* evecs_y, int ldy,
+                                 const int32_t* n1, const int32_t* n2, int B, int V1max, int V2max, int topk,
+                                 int mode, void* work, int64_t work_bytes, int64_t* out_idx, float* out_dist,
+                                 void* stream) {
+  PK_REQUIRE(B >= 0 && V1max >= 0 && V2max >= 0 && ldx >= kF && ldy >= kF && (topk == 1 || topk == 5));
+  PK_REQUIRE(mode >= 0 && mode <= 2);
+  if (B == 0 || V2max == 0) return PK_OK;
+  PK_REQUIRE(evecs_x && C && evecs_y && n1 && n2 && work && out_idx);
+  PK_REQUIRE(work_bytes >= pk_feat_dist_work_size(B, V1max, V2max, topk, mode));
+  hipStream_t s = pk::as_stream(stream);
+  const FdPlan p = fd_plan(B, V1max, V2max, topk, mode);
+  char* wp = static_cast<char*>(work);
+  char* A = wp;
+  char* Bq = A + p.a_bytes;
+  float* nA = mode ? reinterpret_cast<float*>(Bq + p.b_bytes) : nullptr;
+  float* nB = mode ? reinterpret_cast<float*>(Bq + p.b_bytes + p.na_bytes) : nullptr;
+  float* pv = p.RS > 1 ? reinterpret_cast<float*>(Bq + p.b_bytes + p.na_bytes + p.nb_bytes) : nullptr;
+  int32_t* pi = p.RS > 1 ? reinterpret_cast<int32_t*>(reinterpret_cast<char*>(pv) + p.pv_bytes) : nullptr;
+  const dim3 pg((std::max(p.T1, p.T2) + 3) / 4, B, 2);
+#define PK_FD_PREP(M)                                                                                              \
+  hipLaunchKernelGGL(fd_prep_kernel<M>, pg, dim3(256), 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, n2, V1max, V2max, \
+                     p.T1, p.T2, A, Bq, nA, nB)
+  if (mode == 0) PK_FD_PREP(0); else if (mode == 1) PK_FD_PREP(1); else PK_FD_PREP(2);
+#undef PK_FD_PREP
   PK_CHECK_LAUNCH();
+  const dim3 grid((unsigned)((int64_t)B * p.NCG * p.RS)), block(64 * kWaves);
+#define PK_FD_MAIN(K, M)                                                                                        \
+  hipLaunchKernelGGL((fd_main_kernel<K, M>), grid, block, 0, s, A, Bq, nA, nB, n1, n2, p.T1, p.T2, V2max, p.NCG, \
+                     p.RS, out_idx, out_dist, pv, pi)
+  if (topk == 1) {
+    if (mode == 0) PK_FD_MAIN(1, 0); else if (mode == 1) PK_FD_MAIN(1, 1); else PK_FD_MAIN(1, 2);
+  } else {
+    if (mode == 0) PK_FD_MAIN(5, 0); else if (mode == 1) PK_FD_MAIN(5, 1); else PK_FD_MAIN(5, 2);
+  }
+#undef PK_FD_MAIN
+  PK_CHECK_LAUNCH();
+  if (p.RS > 1) {
+    const dim3 mg((V2max + 255) / 256, B);
+    if (topk == 1)
+      hipLaunchKernelGGL(fd_merge_kernel<1>, mg, dim3(256), 0, s, pv, pi, n2, V2max, p.RS, out_idx, out_dist);
+    else
+      hipLaunchKernelGGL(fd_merge_kernel<5>, mg, dim3(256), 0, s, pv, pi, n2, V2max, p.RS, out_idx, out_dist);
+    PK_CHECK_LAUNCH();
+  }
   return PK_OK;
 }

@@ -52,7 +52,8 @@ SIGNATURES = {
     "pk_mlp3_fwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P],
     "pk_resolvent_mask": [_P, _I, _P, _I, _I, _I, _F, _P, _P],
     "pk_linear_fwd": [_P, _P, _P, _I, _I64, _I, _I, _I, _I, _I, _P, _P, _P],
-    "pk_feat_dist_topk": [_P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "pk_feat_dist_work_size": [_I, _I, _I, _I, _I],
+    "pk_feat_dist_topk": [_P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I64, _P, _P, _P],
     "pk_rigidity_filter": [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P],
     "pk_inlier_ratio": [_P, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P],
     "pk_cgt_lstsq_work_size": [_I, _I, _I],
@@ -63,9 +64,11 @@ SIGNATURES = {
     "pk_pose_metrics": [_P, _P, _I, _I, _P, _P, _P, _P, _P],
     "pk_erode_mask": [_P, _I, _I, _I, _P, _P],
     "pk_sample_rgb": [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],
+    "pk_sample_features": [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],
 }
 
-RESTYPES = {"pk_cgt_lstsq_work_size": _I64, "pk_linear_wgrad_grouped_work": _I64, "pk_ransac_work_size": _I64}  # everything else returns an int status
+RESTYPES = {"pk_cgt_lstsq_work_size": _I64, "pk_linear_wgrad_grouped_work": _I64, "pk_ransac_work_size": _I64,
+            "pk_feat_dist_work_size": _I64}  # everything else returns an int status
 
 _lib: Optional[ctypes.CDLL] = None
 

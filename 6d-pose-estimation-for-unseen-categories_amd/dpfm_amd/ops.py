@@ -595,21 +595,28 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], c
 # ------------------------------------------------------------------------------ H10-H13, H15
 
 
+FD_MODES = {"fp32": 0, "bf16": 1, "bf16x3": 2}
+
+
 def feat_dist_topk(evecs_x: torch.Tensor, C: torch.Tensor, evecs_y: torch.Tensor, n1: torch.Tensor,
-                   n2: torch.Tensor, topk: int, want_dist: bool = False):
+                   n2: torch.Tensor, topk: int, want_dist: bool = False, precision: str = "fp32"):
     """Nearest CAD rows of every crop point in the spectral embedding (pk_feat_dist_topk).
-    evecs_x [B,V1,K>=30], C [B,30,30], evecs_y [B,V2,K>=30], n1/n2 int32 [B]."""
+    evecs_x [B,V1,K>=30], C [B,30,30], evecs_y [B,V2,K>=30], n1/n2 int32 [B].
+    precision: "fp32" (the parity path: torch.cdist's augmented contraction on the f32 MFMA),
+    "bf16" or "bf16x3" (opt-in: bf16 MFMA cross term, f32 norms)."""
     B, V1, ldx = evecs_x.shape
     _, V2, ldy = evecs_y.shape
     dev = evecs_x.device
-    # augmented operands in MFMA operand-tile order, rows padded to a multiple of 16
-    A = torch.empty((B, (V1 + 15) // 16 * 16, 32), dtype=torch.float32, device=dev)
-    Bq = torch.empty((B, (V2 + 15) // 16 * 16, 32), dtype=torch.float32, device=dev)
+    mode = FD_MODES[precision]
+    nbytes = int(_lib.lib().pk_feat_dist_work_size(B, V1, V2, int(topk), mode))
+    if nbytes < 0:
+        raise _lib.PoseKernError("feat_dist_topk: invalid shape / topk / precision")
+    work = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
     idx = torch.empty((B, V2, topk), dtype=torch.int64, device=dev)
     dist = torch.empty((B, V2, topk), dtype=torch.float32, device=dev) if want_dist else None
     call("pk_feat_dist_topk", ptr(evecs_x.contiguous()), ldx, ptr(C.contiguous()), ptr(evecs_y.contiguous()), ldy,
-         ptr(n1), ptr(n2), B, V1, V2, int(topk), ptr(A), ptr(Bq), ptr(idx), ptr(dist), _lib.stream(dev),
-         work=("mfma", 2 * B * V1 * V2 * 32))
+         ptr(n1), ptr(n2), B, V1, V2, int(topk), mode, ptr(work), nbytes, ptr(idx), ptr(dist), _lib.stream(dev),
+         work=("mfma" if mode == 0 else "mfma_bf16", 2 * B * V1 * V2 * 32))
     return idx, dist
 
 
@@ -766,4 +773,18 @@ def sample_rgb(img: torch.Tensor, K: torch.Tensor, pts: torch.Tensor, off: torch
     out = torch.zeros((pts.shape[0], C), dtype=torch.float32, device=img.device)
     call("pk_sample_rgb", ptr(img.contiguous()), F_, H, W, C, ptr(K), ptr(pts), ptr(off), int(nmax), ptr(out),
          _lib.stream(img.device))
+    return out
+
+
+def sample_features(fmap: torch.Tensor, K: torch.Tensor, pts: torch.Tensor, off: torch.Tensor,
+                    nmax: int) -> torch.Tensor:
+    """H16: bilinear sample of an f32 feature map [F, C, H, W] at the projections of packed
+    camera-frame points (grid_sample(align_corners=True, padding_mode="zeros") on pixel
+    coordinates) -> f32 [T, C]."""
+    if fmap.dtype != torch.float32 or fmap.dim() != 4:
+        raise ValueError("sample_features: fmap must be f32 [F, C, H, W]")
+    F_, C, H, W = fmap.shape
+    out = torch.zeros((pts.shape[0], C), dtype=torch.float32, device=fmap.device)
+    call("pk_sample_features", ptr(fmap.contiguous()), F_, C, H, W, ptr(K), ptr(pts), ptr(off), int(nmax), ptr(out),
+         _lib.stream(fmap.device))
     return out

@@ -56,7 +56,8 @@ def parse():
                     help="train: the headline fwd+bwd step (default); infer: configs[1]/[3] inference; "
                          "corr4096: configs[4] feature distance + RANSAC")
     ap.add_argument("--hypotheses", type=int, default=1024, help="RANSAC hypotheses per crop (infer/corr4096)")
-    ap.add_argument("--bf16", action="store_true", help="corr4096: bf16 feature-distance operands")
+    ap.add_argument("--fd-precision", choices=("fp32", "bf16", "bf16x3"), default="fp32",
+                    help="corr4096: feature-distance contraction precision (fp32 = the parity path)")
     return ap.parse_args()
 
 
@@ -281,10 +282,10 @@ def build_corr(args, dev, rank, world):
     off = torch.tensor([0, V], dtype=torch.int64, device=dev)
     n = torch.full((1,), V, dtype=torch.int32, device=dev)
     ar = torch.arange(V, dtype=torch.int32, device=dev)
-    bf16 = bool(args.bf16)
+    bf16 = args.fd_precision != "fp32"
 
     def solve():
-        idx, _ = ops.feat_dist_topk(ex, C, ey, n, n, 1, bf16=bf16) if bf16 else ops.feat_dist_topk(ex, C, ey, n, n, 1)
+        idx, _ = ops.feat_dist_topk(ex, C, ey, n, n, 1, precision=args.fd_precision)
         corres = torch.stack([idx[0, :, 0].to(torch.int32), ar], 1)
         return {"T": ops.ransac(cad_t, off, pc_t, off, corres, off, H, seed=0, nmax=V)[0]}
 
@@ -305,10 +306,11 @@ def build_corr(args, dev, rank, world):
             g.replay()
             return out
     config = {"workload": f"configs[4]: one crop, V1 = V2 = {V}: feature distance {V}x{V}x30 "
-                          f"({'bf16' if bf16 else 'fp32'} MFMA, K padded to 32) + argmin + RANSAC {H} hypotheses "
+                          f"({args.fd_precision} MFMA, K padded to 32) + argmin + RANSAC {H} hypotheses "
                           f"over n = {V} correspondences", "execution": "eager" if args.eager else "hip-graph",
               "global_batch": world, "points_per_crop": V, "cad_points": V, "hypotheses": H,
-              "precision": ("bf16 operands / f32 accumulate" if bf16 else "fp32") + " distance; fp64 RANSAC",
+              "precision": (f"{args.fd_precision} cross term / f32 norms and accumulate" if bf16 else "fp32")
+              + " distance; fp64 RANSAC",
               "parallelism": f"replicas{world}"}
     return one_step, solve, CORR_METRIC, 1, config
 
@@ -387,7 +389,7 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(total_ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16" if (args.mode == "corr4096" and args.bf16) else "fp32",
+            "dtype": "bf16" if (args.mode == "corr4096" and args.fd_precision != "fp32") else "fp32",
             "data": "synthetic (seeded ellipsoid RGB-D frames, random-init DPFM)",
             "config": config,
             "roofline": roof,

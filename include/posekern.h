@@ -256,13 +256,15 @@ int pk_linear_fwd(const float* x, const float* w, const float* bias, int layout,
  * rows of dist.sort(dim=-2)) with dist = cdist(evecs_x[:, :30] @ C^T, evecs_y[:, :30]).
  *   evecs_x f32 [B,V1max,ldx] (first 30 columns used), C f32 [B,30,30],
  *   evecs_y f32 [B,V2max,ldy]; n1/n2 int32 [B] valid rows
- *   A f32 [B,ceil16(V1max),32], Bq f32 [B,ceil16(V2max),32] scratch (augmented cdist
- *   operands, written in MFMA operand-tile order)
+ *   mode 0: fp32 MFMA on torch.cdist's augmented K = 32 operands (the parity path);
+ *   mode 1: bf16 MFMA cross term + f32 norms; mode 2: bf16x3 (hi/lo split, three bf16 MFMAs)
+ *   work: scratch of pk_feat_dist_work_size(B, V1max, V2max, topk, mode) bytes
  *   out_idx int64 [B,V2max,topk] ascending distance (ties: lower index); out_dist f32
- *   [B,V2max,topk] Euclidean distances (may be NULL). fp32 MFMA, fused epilogue. */
+ *   [B,V2max,topk] Euclidean distances (may be NULL). Fused selection epilogue. */
+int64_t pk_feat_dist_work_size(int B, int V1max, int V2max, int topk, int mode);
 int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, const float* evecs_y, int ldy,
-                      const int32_t* n1, const int32_t* n2, int B, int V1max, int V2max, int topk,
-                      float* A, float* Bq, int64_t* out_idx, float* out_dist, void* stream);
+                      const int32_t* n1, const int32_t* n2, int B, int V1max, int V2max, int topk, int mode,
+                      void* work, int64_t work_bytes, int64_t* out_idx, float* out_dist, void* stream);
 
 /* H11 rigidity filter (fmap2pointmap_solvers/spacial_filtering.py:42-75), three rounds
  * on device with the 0.055 -> 0.065 fallback.
@@ -351,6 +353,13 @@ int pk_erode_mask(const uint8_t* mask, int F, int H, int W, uint8_t* out, void* 
  * (= grid_sample(align_corners=True, padding_mode="zeros")); out f32 [T,C] / 255. */
 int pk_sample_rgb(const uint8_t* img, int F, int H, int W, int C, const double* K, const double* pts,
                   const int64_t* off, int nmax, float* out, void* stream);
+
+/* H16 (north-star "RGB-backbone feature sampling at projected 3D points"): the same
+ * projection and bilinear weights as pk_sample_rgb on an f32 feature map fmap [F, C, H, W]
+ * (channels-first), zero outside the image (= grid_sample(align_corners=True,
+ * padding_mode="zeros")); out f32 [T, C], no scaling. pts / off / nmax as pk_sample_rgb. */
+int pk_sample_features(const float* fmap, int F, int C, int H, int W, const double* K, const double* pts,
+                       const int64_t* off, int nmax, float* out, void* stream);
 
 #ifdef __cplusplus
 }

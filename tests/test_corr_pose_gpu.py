@@ -180,6 +180,32 @@ def test_sample_rgb_vs_grid_sample(device):
         torch.testing.assert_close(out[200 * f:200 * (f + 1)], ref[0, :, 0].t(), rtol=1e-4, atol=2e-5)
 
 
+def test_sample_features_vs_grid_sample(device):
+    """H16 on an f32 backbone feature map [F, C, H, W] (C = 64): the product kernel against
+    torch grid_sample(align_corners=True, padding_mode="zeros") at the projected points,
+    points projecting inside, on the border and outside the image, ragged frames."""
+    ops = _ops()
+    rng = np.random.default_rng(4)
+    F_, C, H, W = 2, 64, 60, 80
+    fmap = rng.standard_normal((F_, C, H, W)).astype(np.float32)
+    K = np.array([[60.0, 0, 39.5], [0, 60.0, 29.5], [0, 0, 1]])
+    n = [300, 170]
+    pts = [np.concatenate([rng.uniform(-45, 45, (m, 2)), rng.uniform(40, 90, (m, 1))], 1) for m in n]
+    off = torch.tensor([0, n[0], n[0] + n[1]], device=device)
+    out = ops.sample_features(torch.from_numpy(fmap).to(device), torch.from_numpy(np.stack([K.reshape(9)] * 2)).to(device),
+                              torch.from_numpy(np.concatenate(pts)).to(device), off, max(n)).cpu()
+    for f in range(F_):
+        u = K[0, 0] * pts[f][:, 0] / pts[f][:, 2] + K[0, 2]
+        v = K[1, 1] * pts[f][:, 1] / pts[f][:, 2] + K[1, 2]
+        assert ((u < 0) | (u > W - 1)).any() and ((u >= 0) & (u <= W - 1)).any()
+        grid = torch.from_numpy(np.stack([2 * u / (W - 1) - 1, 2 * v / (H - 1) - 1], -1)).float()[None, None]
+        ref = torch.nn.functional.grid_sample(torch.from_numpy(fmap[f])[None], grid, mode="bilinear",
+                                              padding_mode="zeros", align_corners=True)
+        got = out[off[f].item():off[f + 1].item()]
+        # f32 weights from an fp64 projection vs grid_sample's f32 unnormalisation: ~1e-5 abs
+        torch.testing.assert_close(got, ref[0, :, 0].t(), rtol=1e-4, atol=5e-5)
+
+
 def test_cgt_rank_deficient_and_empty(device):
     """C_from_sparse_P (utils/utils.py:67-79) when the pair list does not determine C_gt:
     fewer than 30 distinct matched crop rows (rank < 30) and an empty list. torch's CPU lstsq

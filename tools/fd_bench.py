@@ -1,8 +1,9 @@
-"""Feature-distance + argmin / top-5 (pk_feat_dist_topk) at the BASELINE shapes, for
-timing and PMC passes (MFMA utilisation): configs[1] (32 crops of 1024 x 1024) and
-configs[4] (one 4096 x 4096 crop). Prints achieved TFLOP/s from HIP events.
+"""Feature-distance + argmin / top-5 (pk_feat_dist_topk) at the BASELINE shapes, timed in
+HIP graphs (no host gaps): configs[1] (32 crops of 1024 x 1024) and configs[4] (one 4096 x
+4096 crop), every precision mode. Prints achieved TFLOP/s and, for the bf16 modes, the
+argmin / top-5 agreement with the fp32 path.
 
-  python tools/fd_bench.py [iters]
+  python tools/fd_bench.py [iters] [BxV] [precisions, comma-separated]
 """
 import os
 import sys
@@ -12,58 +13,51 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "6d-pose-estimation-for-unseen-categori
 import torch  # noqa: E402
 
 from dpfm_amd import ops  # noqa: E402
+from dpfm_amd.dataset.synthetic import lbo_operators  # noqa: E402
 
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+only = sys.argv[2] if len(sys.argv) > 2 else None  # e.g. "32x1024"
+precs = sys.argv[3].split(",") if len(sys.argv) > 3 else ["fp32", "bf16x3", "bf16"]
 dev = torch.device("cuda:0")
-g = torch.Generator(device=dev)
-g.manual_seed(0)
-for B, V, topk in [(32, 1024, 1), (32, 1024, 5), (1, 4096, 1), (1, 4096, 5)]:
-    ex = torch.randn(B, V, 64, device=dev, generator=g) * 0.05
-    ey = torch.randn(B, V, 64, device=dev, generator=g) * 0.05
-    C = torch.randn(B, 30, 30, device=dev, generator=g) * 0.3
+for B, V in [(32, 1024), (8, 2048), (1, 4096)]:
+    if only and only != f"{B}x{V}":
+        continue
+    ex = torch.stack([torch.from_numpy(lbo_operators(V, 64, 10 + b)[2]) for b in range(B)]).to(dev)
+    ey = torch.stack([torch.from_numpy(lbo_operators(V, 64, 50 + b)[2]) for b in range(B)]).to(dev)
+    C = (torch.eye(30)[None] + 0.3 * torch.randn(B, 30, 30, generator=torch.Generator().manual_seed(B))).to(dev)
     n = torch.full((B,), V, dtype=torch.int32, device=dev)
-    for _ in range(3):
-        ops.feat_dist_topk(ex, C, ey, n, n, topk)
-    # time inside a HIP graph: no host launch gaps between the timed launches
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    torch.cuda.synchronize()
-    gr = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(gr):
-        for _ in range(iters):
-            ops.feat_dist_topk(ex, C, ey, n, n, topk)
-    gr.replay()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    gr.replay()
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / iters
-    fl = 2.0 * B * V * V * 32
-    if topk == 1:  # main pass alone, and without its epilogue (development hooks)
-        from dpfm_amd import _lib
-        L = _lib.lib()
-        A = torch.empty((B, (V + 15) // 16 * 16, 32), device=dev)
-        Bq = torch.empty_like(A)
-        idx = torch.empty((B, V, 1), dtype=torch.int64, device=dev)
-        _lib.call("pk_feat_dist_topk", _lib.ptr(ex), 64, _lib.ptr(C), _lib.ptr(ey), 64, _lib.ptr(n), _lib.ptr(n), B, V, V,
-                  1, _lib.ptr(A), _lib.ptr(Bq), _lib.ptr(idx), None, _lib.stream(dev))
-        L.pkdev_fd_main_noepi.argtypes = [_lib._P] * 4 + [_lib._I] * 3 + [_lib._P, _lib._I, _lib._P]
-        for noload in (0, 1):
-            gr2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr2):
-                for _ in range(iters):
-                    L.pkdev_fd_main_noepi(_lib.ptr(A), _lib.ptr(Bq), _lib.ptr(n), _lib.ptr(n), B, V, V, _lib.ptr(idx),
-                                          noload, _lib.stream(dev))
-            gr2.replay()
+    ref = {}
+    for topk in ((1,) if only else (1, 5)):
+        for prec in precs:
+            f = lambda: ops.feat_dist_topk(ex, C, ey, n, n, topk, precision=prec)  # noqa: E731
+            for _ in range(3):
+                out = f()
             torch.cuda.synchronize()
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                for _ in range(iters):
+                    f()
+            gr.replay()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            gr2.replay()
+            gr.replay()
             e1.record()
             torch.cuda.synchronize()
-            ms2 = e0.elapsed_time(e1) / iters
-            print(f"   main pass without epilogue{' and A loads' if noload else ''}: {ms2 * 1e3:.1f} us "
-                  f"({fl / ms2 / 1e9:.1f} TFLOP/s)", flush=True)
-    print(f"feat_dist_topk B={B} V={V} topk={topk}: {ms * 1e3:.1f} us/launch (prep + main), "
-          f"{fl / ms / 1e9:.1f} TFLOP/s = {fl / ms / 1e9 / 157.3:.3f} of the f32 MFMA peak", flush=True)
+            ms = e0.elapsed_time(e1) / iters
+            fl = 2.0 * B * V * V * 32
+            peak = 157.3 if prec == "fp32" else 2500.0
+            idx = out[0]
+            if prec == "fp32" or topk not in ref:
+                ref[topk] = idx
+                agree = ""
+            else:
+                a1 = (idx[..., 0] == ref[topk][..., 0]).float().mean().item()
+                agree = f", first-choice agreement with fp32 {a1:.4f}"
+                if topk == 5:
+                    same = (idx.sort(-1).values == ref[5].sort(-1).values).all(-1).float().mean().item()
+                    agree += f", same top-5 set {same:.4f}"
+            print(f"feat_dist_topk B={B} V={V} topk={topk} {prec}: {ms * 1e3:.1f} us/launch (prep + main), "
+                  f"{fl / ms / 1e9:.1f} TFLOP/s = {fl / ms / 1e9 / peak:.3f} of the {'f32' if prec == 'fp32' else 'bf16'}"
+                  f" MFMA peak{agree}", flush=True)
+

@@ -38,5 +38,5 @@ for r in win:
         n = re.split(r"[(<]", n)[0][:90]
     tot[n][0] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     tot[n][1] += 1
-for n, (t, c) in sorted(tot.items(), key=lambda kv: -kv[1][0])[:45]:
+for n, (t, c) in sorted(tot.items(), key=lambda kv: -kv[1][0])[:int(sys.argv[3]) if len(sys.argv) > 3 else 45]:
     print(f"{t/1e3/steps:8.1f} us/step {c/steps:6.1f}/step  {n}")
