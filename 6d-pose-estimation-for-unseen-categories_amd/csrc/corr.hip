@@ -134,8 +134,14 @@ __global__ __launch_bounds__(256) void ir_kernel(const int64_t* __restrict__ pai
   int c = 0;
   for (int k = threadIdx.x; k < n; k += 256) {
     const int64_t* pr = pairs + (int64_t)b * ldp * 2;
-    const int64_t ci = pr[col_cad * (pair_stride == 1 ? ldp : 1) + k * (pair_stride == 1 ? 1 : 2)];
-    const int64_t pi = pr[col_pc * (pair_stride == 1 ? ldp : 1) + k * (pair_stride == 1 ? 1 : 2)];
+    int64_t ci, pi;
+    if (pair_stride == 0) {  // point map: CAD index per crop point k, crop index k
+      ci = pairs[(int64_t)b * ldp + k];
+      pi = k;
+    } else {
+      ci = pr[col_cad * (pair_stride == 1 ? ldp : 1) + k * (pair_stride == 1 ? 1 : 2)];
+      pi = pr[col_pc * (pair_stride == 1 ? ldp : 1) + k * (pair_stride == 1 ? 1 : 2)];
+    }
     const float* a = cad + ((int64_t)b * ldcad + ci) * 3;
     const float* p = pcal + ((int64_t)b * ldpc + pi) * 3;
     const float dx = a[0] - p[0], dy = a[1] - p[1], dz = a[2] - p[2];
@@ -471,11 +477,13 @@ extern "C" int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* n
 extern "C" int pk_inlier_ratio(const int64_t* pairs, int ldp, int layout, const int32_t* npairs, const float* cad,
                                int ldcad, const float* pc_aligned, int ldpc, const float* thr, int B, float* ir,
                                void* stream) {
-  PK_REQUIRE(B >= 0 && (layout == 0 || layout == 1));
+  PK_REQUIRE(B >= 0 && layout >= 0 && layout <= 2);
   if (B == 0) return PK_OK;
   PK_REQUIRE(pairs && npairs && cad && pc_aligned && thr && ir);
-  // layout 0: pairs [B, ldp, 2] (cad, pc); layout 1: [B, 2, ldp] (row 0 cad, row 1 pc)
-  hipLaunchKernelGGL(ir_kernel, dim3(B), dim3(256), 0, pk::as_stream(stream), pairs, ldp, layout == 1 ? 1 : 2, 0, 1,
+  // layout 0: pairs [B, ldp, 2] (cad, pc); layout 1: [B, 2, ldp] (row 0 cad, row 1 pc);
+  // layout 2: [B, ldp] CAD index of crop point k (a point map; pc index = k)
+  hipLaunchKernelGGL(ir_kernel, dim3(B), dim3(256), 0, pk::as_stream(stream), pairs, ldp,
+                     layout == 2 ? 0 : layout == 1 ? 1 : 2, 0, 1,
                      npairs, cad, ldcad, pc_aligned, ldpc, thr, ir);
   PK_CHECK_LAUNCH();
   return PK_OK;

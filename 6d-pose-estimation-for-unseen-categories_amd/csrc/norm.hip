@@ -313,3 +313,28 @@ extern "C" int pk_l2_normalize_bwd(const float* y, const float* dy, const float*
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
+
+// models/dpfm.py:53 + :61-66 (the shared encoder pass): features = cat((v1 - 110) / 50,
+// (v2 - 110) / 50) in one launch. `mul` is the host-rounded reciprocal: torch evaluates a
+// division by a Python scalar on the GPU as a product with the f32 reciprocal, so this is
+// the same rounding as the reference's two elementwise kernels and the concatenation copy.
+namespace {
+__global__ __launch_bounds__(256) void affine_cat_kernel(const float* __restrict__ a, int64_t na,
+                                                         const float* __restrict__ b, int64_t nb, float sub,
+                                                         float mul, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < na) out[i] = (a[i] - sub) * mul;
+  else if (i < na + nb) out[i] = (b[i - na] - sub) * mul;
+}
+}  // namespace
+
+extern "C" int pk_affine_cat(const float* a, int64_t na, const float* b, int64_t nb, float sub, float mul, float* out,
+                             void* stream) {
+  PK_REQUIRE(na >= 0 && nb >= 0);
+  if (na + nb == 0) return PK_OK;
+  PK_REQUIRE(out && (na == 0 || a) && (nb == 0 || b));
+  hipLaunchKernelGGL(affine_cat_kernel, dim3((unsigned)((na + nb + 255) / 256)), dim3(256), 0, pk::as_stream(stream),
+                     a, na, b, nb, sub, mul, out);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}

@@ -19,7 +19,7 @@ constexpr int kKC = 64;       // K == C == 64 (C_width, k_eig) — checked on th
 
 // pass 1: part[b, s] = sum_{rows in chunk s} Phi[r, :]^T (w_r * x[r, :]), w = mass or 1.
 // grid (S, B), block 256 = 16 x 16 threads, each owning a 4 x 4 output micro-tile.
-__global__ __launch_bounds__(256) void spec_reduce_kernel(const float* __restrict__ x,
+__global__ __launch_bounds__(256) void spec_reduce_kernel(const float* __restrict__ x, int ldx,
                                                           const float* __restrict__ mass,
                                                           const float* __restrict__ evecs, int N, int S,
                                                           float* __restrict__ part) {
@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256) void spec_reduce_kernel(const float* __restric
   const int s = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int ty = tid >> 4, tx = tid & 15;
   const float* __restrict__ phi = evecs + (int64_t)b * N * kKC;
-  const float* __restrict__ xb = x + (int64_t)b * N * kKC;
+  const float* __restrict__ xb = x + (int64_t)b * N * ldx;
   const float* __restrict__ mb = mass ? mass + (int64_t)b * N : nullptr;
   float acc[4][4] = {};
   const int r_begin = s * kRows;
@@ -41,7 +41,7 @@ __global__ __launch_bounds__(256) void spec_reduce_kernel(const float* __restric
       float4 pv = make_float4(0.f, 0.f, 0.f, 0.f), xv = pv;
       if (r < r_end) {
         pv = reinterpret_cast<const float4*>(phi + (int64_t)r * kKC)[q];
-        xv = reinterpret_cast<const float4*>(xb + (int64_t)r * kKC)[q];
+        xv = reinterpret_cast<const float4*>(xb + (int64_t)r * ldx)[q];
         if (mb) {
           const float w = mb[r];
           xv.x *= w; xv.y *= w; xv.z *= w; xv.w *= w;
@@ -72,17 +72,22 @@ __global__ __launch_bounds__(256) void spec_reduce_kernel(const float* __restric
 // pass 2: coef = sum_s part; save raw (optional), scaled = E ⊙ coef; optional gt partial
 // gt[b, c] = -sum_k lambda_k E[k,c] saved[k,c] coef[k,c]. grid (B), block 1024: thread
 // (k-quad, c) sums its 4 rows over the S partials as 4 independent chains.
-__global__ __launch_bounds__(1024) void spec_combine_kernel(const float* __restrict__ part, int S,
+// clamp_t: use max(t, 1e-8) (LearnedTimeDiffusion's in-place clamp_(min=1e-8) of the
+// parameter, upstream layers.py) and, in the forward, write it back (block 0; every block
+// computes the same value, so the concurrent reads see either value and use the clamped one).
+// gt (backward): this crop's dL/dt partial, written over the first row of its own partial
+// slab region (already consumed by this block) for the expand pass to sum in crop order.
+__global__ __launch_bounds__(1024) void spec_combine_kernel(float* __restrict__ part, int S,
                                                             const float* __restrict__ evals,
-                                                            const float* __restrict__ t,
+                                                            float* __restrict__ t, int clamp_t, int write_t,
                                                             float* __restrict__ raw,
                                                             float* __restrict__ scaled,
-                                                            const float* __restrict__ saved,
-                                                            float* __restrict__ gt) {
+                                                            const float* __restrict__ saved, int want_gt) {
   __shared__ double gsum[16][kKC];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int c = tid & 63, k0 = (tid >> 6) * 4;
   const float* pb = part + (int64_t)b * S * kKC * kKC + k0 * kKC + c;
+  const float tc = clamp_t ? fmaxf(t[c], 1e-8f) : t[c];
   // the S slab partials (64 rows each) are summed in fp64: at N ~ 5000 CAD vertices a serial
   // fp32 sum over ~80 slabs dominated the error of the diffusion-time gradient, a
   // cancellation-prone contraction of two such sums
@@ -92,7 +97,6 @@ __global__ __launch_bounds__(1024) void spec_combine_kernel(const float* __restr
     for (int i = 0; i < 4; ++i) v[i] += (double)pb[(int64_t)s * kKC * kKC + i * kKC];
   }
   double g = 0.0;
-  const float tc = t[c];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k = k0 + i;
@@ -102,30 +106,39 @@ __global__ __launch_bounds__(1024) void spec_combine_kernel(const float* __restr
     const float vf = (float)v[i];
     if (raw) raw[o] = vf;
     scaled[o] = E * vf;
-    if (gt) g = fma(-(double)lam * (double)E, (double)saved[o] * v[i], g);
+    if (want_gt) g = fma(-(double)lam * (double)E, (double)saved[o] * v[i], g);
   }
-  if (gt) {
+  if (write_t && b == 0 && tid < kKC) t[c] = tc;
+  if (want_gt) {
     gsum[tid >> 6][c] = g;
-    __syncthreads();
+    __syncthreads();  // also orders this block's partial reads before the overwrite below
     if (tid < kKC) {
       double a = 0.0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) a += gsum[q][c];
-      gt[b * kKC + c] = (float)a;
+      part[(int64_t)b * S * kKC * kKC + c] = (float)a;
     }
   }
 }
 
 // pass 3: y[r, :] = Phi[r, :] · coef (· mass[r] if given). grid (ceil(N/64), B), block 256:
 // 16 x 16 threads, 4 rows x 4 cols each.
+// gtb (backward): block (0, 0) also sums the per-crop dL/dt partials in crop order into gt.
 __global__ __launch_bounds__(256) void spec_expand_kernel(const float* __restrict__ evecs,
                                                           const float* __restrict__ coef,
                                                           const float* __restrict__ mass, int N,
-                                                          float* __restrict__ y) {
+                                                          float* __restrict__ y, int ldy,
+                                                          const float* __restrict__ gtb, int64_t gt_stride,
+                                                          float* __restrict__ gt) {
   __shared__ float4 scoef[kKC][kKC / 4];
   __shared__ float sphi[64][kKC + 1];
   const int tile = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int ty = tid >> 4, tx = tid & 15;
+  if (gt && tile == 0 && b == 0 && tid < kKC) {
+    float a = 0.f;
+    for (int q = 0; q < (int)gridDim.y; ++q) a += gtb[(int64_t)q * gt_stride + tid];
+    gt[tid] = a;
+  }
   const float* __restrict__ cb = coef + (int64_t)b * kKC * kKC;
   for (int e = tid; e < kKC * kKC / 4; e += 256) scoef[e / 16][e % 16] = reinterpret_cast<const float4*>(cb)[e];
   const int r0 = tile * 64;
@@ -159,7 +172,7 @@ __global__ __launch_bounds__(256) void spec_expand_kernel(const float* __restric
     if (r >= N) continue;
     float w = 1.f;
     if (mass) w = mass[(int64_t)b * N + r];
-    reinterpret_cast<float4*>(y + ((int64_t)b * N + r) * kKC)[tx] =
+    reinterpret_cast<float4*>(y + ((int64_t)b * N + r) * ldy)[tx] =
         make_float4(acc[i][0] * w, acc[i][1] * w, acc[i][2] * w, acc[i][3] * w);
   }
 }
@@ -167,27 +180,28 @@ __global__ __launch_bounds__(256) void spec_expand_kernel(const float* __restric
 }  // namespace
 
 // mode 0 (forward): in = x, out = y, raw = spec (saved for backward), reduce weights = mass.
-// mode 1 (backward): in = g, out = gx, saved = spec from forward, gt = per-crop dL/dt
-//                    partials [B, C]; expand weights = mass.
-extern "C" int pk_spectral_diffusion(const float* in, const float* mass, const float* evecs,
-                                     const float* evals, const float* t, int B, int N, int K, int C,
-                                     int mode, float* work, float* raw, float* scaled,
-                                     const float* saved, float* gt, float* out, void* stream) {
+// mode 1 (backward): in = g, out = gx, saved = spec from forward, gt = dL/dt [C] summed over
+//                    crops; expand weights = mass.
+extern "C" int pk_spectral_diffusion(const float* in, int ld_in, const float* mass, const float* evecs,
+                                     const float* evals, float* t, int clamp_t, int B, int N, int K, int C,
+                                     int mode, float* work, float* raw, float* scaled, const float* saved,
+                                     float* gt, float* out, int ld_out, void* stream) {
   PK_REQUIRE(B >= 0 && N >= 0 && K == kKC && C == kKC && (mode == 0 || mode == 1));
+  PK_REQUIRE(ld_in >= C && ld_out >= C && ld_in % 4 == 0 && ld_out % 4 == 0);
   if (B == 0 || N == 0) return PK_OK;
   PK_REQUIRE(in && evecs && evals && t && work && scaled && out);
   PK_REQUIRE(mode == 0 || (saved && gt));
   hipStream_t s = pk::as_stream(stream);
   const int S = (N + kRows - 1) / kRows;
-  hipLaunchKernelGGL(spec_reduce_kernel, dim3(S, B), dim3(256), 0, s, in, mode == 0 ? mass : nullptr,
+  hipLaunchKernelGGL(spec_reduce_kernel, dim3(S, B), dim3(256), 0, s, in, ld_in, mode == 0 ? mass : nullptr,
                      evecs, N, S, work);
   PK_CHECK_LAUNCH();
-  hipLaunchKernelGGL(spec_combine_kernel, dim3(B), dim3(1024), 0, s, work, S, evals, t, raw, scaled,
-                     mode == 1 ? saved : nullptr, mode == 1 ? gt : nullptr);
+  hipLaunchKernelGGL(spec_combine_kernel, dim3(B), dim3(1024), 0, s, work, S, evals, t, clamp_t,
+                     (int)(clamp_t && mode == 0), raw, scaled, mode == 1 ? saved : nullptr, (int)(mode == 1));
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(spec_expand_kernel, dim3((N + 63) / 64, B), dim3(256), 0, s, evecs, scaled,
-                     mode == 1 ? mass : nullptr, N, out);
+                     mode == 1 ? mass : nullptr, N, out, ld_out, work, (int64_t)S * kKC * kKC,
+                     mode == 1 ? gt : nullptr);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
-

@@ -34,7 +34,7 @@ SIGNATURES = {
     "pk_collate_pad": [_P, _I, _I, _P, _I, _I, _P, _P, _P],
     "pk_segment_scan": [_P, _I, _I, _P, _P, _P],
     "pk_offsets_from_counts": [_P, _I, _P, _P],
-    "pk_spectral_diffusion": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "pk_spectral_diffusion": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P],
     "pk_fmap_solve": [_P, _P, _P, _F, _I, _I, _P, _P],
     "pk_fmap_solve_backward": [_P, _P, _P, _F, _I, _I, _P, _P, _P, _P],
     "pk_attention_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P],
@@ -43,6 +43,9 @@ SIGNATURES = {
     "pk_linear_wgrad_grouped_work": [_P, _I],
     "pk_linear_wgrad_grouped": [_P, _I, _P, _I64, _P],
     "pk_nce_loss": [_P, _P, _P, _P, _I, _I64, _I64, _I, _P, _I, _P, _P, _I, _F, _P, _P, _P, _P, _P, _P],
+    "pk_affine_cat": [_P, _I64, _P, _I64, _F, _F, _P, _P],
+    "pk_loss_head": [_P, _P, _I, _I, _P, _P, _F, _F, _F, _P, _P, _P, _P],
+    "pk_loss_scale": [_P, _P, _P, _P, _I, _P, _P],
     "pk_clip_rmsprop": [_P, _P, _P, _P, _P, _I, _F, _F, _F, _F, _F, _P, _P, _P],
     "pk_instnorm_relu_fwd": [_P, _I64, _I, _F, _P, _P, _P, _P],
     "pk_instnorm_relu_bwd": [_P, _P, _P, _P, _I64, _I, _P, _P],

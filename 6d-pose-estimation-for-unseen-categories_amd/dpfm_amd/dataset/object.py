@@ -156,10 +156,14 @@ class Crops:
     rgb: Optional[torch.Tensor]  # f32 [*, C] colour at each packed crop point (H16) or None
     kept: torch.Tensor       # int64 [F] points after outlier removal
     pair_cap: int = 0
+    overflow_flag: Optional[torch.Tensor] = None  # 0-d bool formed with the crops (see overflow)
 
     def overflow(self) -> torch.Tensor:
         """0-d bool on the device: some crop had more ball-query pairs than pair_cap (its P
-        was truncated). No host sync; `check()` raises on it."""
+        was truncated). No host sync; `check()` raises on it. CropFormation forms it on its
+        own stream, so the training step only reads it."""
+        if self.overflow_flag is not None:
+            return self.overflow_flag
         return (self.npairs > self.pair_cap).any()
 
     def check(self) -> None:
@@ -218,4 +222,5 @@ class CropFormation:
         rgb = ops.sample_rgb(fb.rgb, fb.K, g["sel64"], pol["off"], npmax) if self.with_rgb else None
         return Crops(pc64=g["sel64"], pc32=pc32, align64=g["align"], align32=align32, off=pol["off"], n2=n2, ld=ld,
                      npoint=pol["npoint"], pairs=bq["pairs"], npairs=bq["count"], overlap_12=bq["overlap_12"],
-                     overlap_21=bq["overlap_21"], rgb=rgb, kept=so["kept"], pair_cap=self.pair_cap)
+                     overlap_21=bq["overlap_21"], rgb=rgb, kept=so["kept"], pair_cap=self.pair_cap,
+                     overflow_flag=(bq["count"] > self.pair_cap).any())

@@ -29,9 +29,10 @@ class LearnedTimeDiffusion(nn.Module):
         self.diffusion_time = nn.Parameter(torch.zeros(C_inout))
 
     def forward(self, x, L, mass, evals, evecs):
-        with torch.no_grad():  # in-place clamp, as upstream; clamp_ keeps
-            self.diffusion_time.data.clamp_(min=1e-8)  # the storage (HIP-graph replays)
-        return ops.spectral_diffusion(x, mass, evals, evecs, self.diffusion_time)
+        # upstream clamps diffusion_time in place (clamp_(min=1e-8)) before
+        # every diffusion; the spectral kernel applies and writes back that clamp itself (same
+        # storage, so HIP-graph replays see it), saving a launch per block
+        return ops.spectral_diffusion(x, mass, evals, evecs, self.diffusion_time, clamp_t=True)
 
 
 class MiniMLP(nn.Sequential):

@@ -20,6 +20,10 @@ from . import ops
 
 _SIDE = None  # the active GroupedWgrad (TrainStep's backward), or None
 FOLD_RELU = True  # fold a producer layer's ReLU backward into the consumer's input gradient
+# input gradients whose producer ReLU mask a consumer already applied: (dx storage pointer,
+# mask storage pointer). Keyed by storage, not by tensor object: autograd hands the producer a
+# transposed view of the consumer's dx for channels-first layers (a new Python object)
+_MASKED = set()
 
 
 class GroupedWgrad:
@@ -44,6 +48,7 @@ class GroupedWgrad:
 
     def begin(self):
         global _SIDE
+        _MASKED.clear()
         for p in self.params:
             p.grad = self.bufs[id(p)]
         self.seen = set()
@@ -95,7 +100,7 @@ class _PointwiseFn(torch.autograd.Function):
     reference's transposes (modeling/dpfm.py:90-91, 113-116) cost no copies."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, cf, relu):
+    def forward(ctx, x, weight, bias, cf, relu, in_relu):
         w2 = weight.view(weight.shape[0], -1)
         ctx.has_bias, ctx.cf, ctx.relu = bias is not None, cf, relu
         ctx.param, ctx.bias = weight, bias  # the Parameter objects (GroupedWgrad's buffer keys)
@@ -103,10 +108,8 @@ class _PointwiseFn(torch.autograd.Function):
         # relu=True applies the following nn.ReLU in the kernel's epilogue instead
         y = ops.linear_fwd(x, w2, bias, channels_first=cf, relu=relu)
         # this layer's input gradient can apply the ReLU backward of the layer that produced x
-        ctx.in_relu = FOLD_RELU and getattr(x, "_pk_relu_out", False)
+        ctx.in_relu = FOLD_RELU and in_relu
         ctx.save_for_backward(x, weight, y if relu else None)
-        if relu:
-            y._pk_relu_out = True
         return y
 
     @staticmethod
@@ -115,7 +118,7 @@ class _PointwiseFn(torch.autograd.Function):
         w2 = weight.view(weight.shape[0], -1)
         cf = ctx.cf
         dy = dy.contiguous()
-        if ctx.relu and not getattr(dy, "_pk_relu_masked", False):
+        if ctx.relu and (dy.data_ptr(), y.data_ptr()) not in _MASKED:
             # the fused ReLU's backward (aten's ReluBackward: threshold_backward on the output),
             # unless the consuming layer already applied it in its input-gradient epilogue
             dy = torch.ops.aten.threshold_backward(dy, y, 0.0)
@@ -124,14 +127,14 @@ class _PointwiseFn(torch.autograd.Function):
             # dy W (rows) / W^T dy (cf); with in_relu the producer's ReLU backward is folded in
             dx = ops.linear_fwd(dy, w2, None, channels_first=cf, transw=True, mask=x if ctx.in_relu else None)
             if ctx.in_relu:
-                dx._pk_relu_masked = True
+                _MASKED.add((dx.data_ptr(), x.data_ptr()))
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             if _side_owns(ctx.param, ctx.bias):
                 _SIDE.launch(x, dy, ctx.param, ctx.bias, channels_first=cf)
             else:
                 dw, db = ops.linear_wgrad(x, dy, channels_first=cf, want_bias=ctx.has_bias)
                 dw = dw.view(weight.shape)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 def _pointwise(x, weight, bias, sem_cf: bool, out_cf: Optional[bool] = None, relu: bool = False):
@@ -143,10 +146,14 @@ def _pointwise(x, weight, bias, sem_cf: bool, out_cf: Optional[bool] = None, rel
         base, native_cf = x.transpose(1, 2), not sem_cf
     else:
         base, native_cf = x.contiguous(), sem_cf
-    y = _PointwiseFn.apply(base, weight, bias, native_cf, relu)
+    in_relu = getattr(x, "_pk_relu_out", False)
+    y = _PointwiseFn.apply(base, weight, bias, native_cf, relu, in_relu)
     if out_cf is not None and out_cf != native_cf and y.dim() == 3:
         y = y.transpose(1, 2).contiguous().transpose(1, 2)  # same values, other storage order
-    return y if native_cf == sem_cf else y.transpose(1, 2)
+    out = y if native_cf == sem_cf else y.transpose(1, 2)
+    if relu:  # marks the tensor the consumer sees (a view object when the layout flips)
+        out._pk_relu_out = True
+    return out
 
 
 class Linear(nn.Linear):

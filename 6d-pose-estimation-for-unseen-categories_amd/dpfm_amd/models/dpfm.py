@@ -11,6 +11,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from .. import ops
 from ..diffusion_net import DiffusionNet
 from ..modeling.dpfm import CrossAttentionRefinementNet, RegularizedFMNet
 
@@ -56,15 +57,19 @@ class DPFMNet(nn.Module):
         s1, s2 = batch["shape1"], batch["shape2"]
         verts1, mass1, evals1, evecs1 = s1["xyz"], s1["mass"], s1["evals"], s1["evecs"]
         verts2, mass2, evals2, evecs2 = s2["xyz"], s2["mass"], s2["evals"], s2["evecs"]
-        features1, features2 = (verts1 - 110) / 50, (verts2 - 110) / 50  # models/dpfm.py:53
-
-        if features1.dim() == 3 and features1.shape == features2.shape and evecs1.shape == evecs2.shape:
-            # same weights, per-crop operations: one pass over both shapes (2B crops)
-            B = features1.shape[0]
-            feat = self.feature_extractor(torch.cat((features1, features2), 0), _cat0(mass1, mass2),
+        if verts1.dim() == 3 and verts1.shape == verts2.shape and evecs1.shape == evecs2.shape:
+            # same weights, per-crop operations: one pass over both shapes (2B crops); the
+            # input features (v - 110) / 50 of both shapes (models/dpfm.py:53) in one launch
+            B = verts1.shape[0]
+            if verts1.is_cuda and verts1.dtype == torch.float32 and not verts1.requires_grad:
+                fcat = ops.affine_cat(verts1, verts2, 110.0, 50.0)
+            else:
+                fcat = torch.cat(((verts1 - 110) / 50, (verts2 - 110) / 50), 0)
+            feat = self.feature_extractor(fcat, _cat0(mass1, mass2),
                                           evals=_cat0(evals1, evals2), evecs=_cat0(evecs1, evecs2))
             feat1, feat2 = torch.chunk(feat, 2, 0)  # backward: one concat (slices: two zero-fills + copies)
         else:
+            features1, features2 = (verts1 - 110) / 50, (verts2 - 110) / 50  # models/dpfm.py:53
             feat1 = self.feature_extractor(features1, mass1, evals=evals1, evecs=evecs1)
             feat2 = self.feature_extractor(features2, mass2, evals=evals2, evecs=evecs2)
 

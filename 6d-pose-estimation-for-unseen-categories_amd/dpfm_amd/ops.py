@@ -213,23 +213,26 @@ def gather_transform(pcd: torch.Tensor, off: torch.Tensor, idx: Optional[torch.T
 
 class _SpectralDiffusion(torch.autograd.Function):
     """x_diffuse = Phi (exp(-lambda t) ⊙ (Phi^T (mass ⊙ x))) — pk_spectral_diffusion fwd/bwd.
-    Gradients flow to x and t (the operators are data, as in the reference)."""
+    Gradients flow to x and t (the operators are data, as in the reference). clamp_t applies
+    LearnedTimeDiffusion's in-place clamp_(min=1e-8) of t inside the kernel."""
 
     @staticmethod
-    def forward(ctx, x, mass, evals, evecs, t):
+    def forward(ctx, x, mass, evals, evecs, t, clamp_t):
         B, N, C = x.shape
         K = evecs.shape[-1]
         dev = x.device
-        x = x.contiguous()
+        if x.stride(-1) != 1 or x.stride(0) != N * x.stride(1) or x.stride(1) % 4:
+            x = x.contiguous()
         S = (N + 63) // 64
         work = torch.empty((B, S, K, C), dtype=torch.float32, device=dev)
         spec = torch.empty((B, K, C), dtype=torch.float32, device=dev)
         scaled = torch.empty_like(spec)
-        out = torch.empty_like(x)
-        call("pk_spectral_diffusion", ptr(x), ptr(mass), ptr(evecs), ptr(evals), ptr(t), B, N, K, C, 0,
-             ptr(work), ptr(spec), ptr(scaled), None, None, ptr(out), _lib.stream(dev),
-             work=("hbm", 16 * B * N * 64))  # Phi read twice + x in + y out, f32
+        out = torch.empty((B, N, C), dtype=torch.float32, device=dev)
+        call("pk_spectral_diffusion", ptr(x), int(x.stride(1)), ptr(mass), ptr(evecs), ptr(evals), ptr(t),
+             int(clamp_t), B, N, K, C, 0, ptr(work), ptr(spec), ptr(scaled), None, None, ptr(out), C,
+             _lib.stream(dev), work=("hbm", 16 * B * N * 64))  # Phi read twice + x in + y out, f32
         ctx.save_for_backward(mass, evals, evecs, t, spec)
+        ctx.clamp_t = clamp_t
         return out
 
     @staticmethod
@@ -242,19 +245,23 @@ class _SpectralDiffusion(torch.autograd.Function):
         S = (N + 63) // 64
         work = torch.empty((B, S, K, C), dtype=torch.float32, device=dev)
         scaled = torch.empty((B, K, C), dtype=torch.float32, device=dev)
-        gt = torch.empty((B, C), dtype=torch.float32, device=dev)
+        gt = torch.empty((C,), dtype=torch.float32, device=dev)
         gx = torch.empty_like(g)
-        call("pk_spectral_diffusion", ptr(g), ptr(mass), ptr(evecs), ptr(evals), ptr(t), B, N, K, C, 1,
-             ptr(work), None, ptr(scaled), ptr(spec), ptr(gt), ptr(gx), _lib.stream(dev),
+        call("pk_spectral_diffusion", ptr(g), C, ptr(mass), ptr(evecs), ptr(evals), ptr(t), int(ctx.clamp_t), B, N,
+             K, C, 1, ptr(work), None, ptr(scaled), ptr(spec), ptr(gt), ptr(gx), C, _lib.stream(dev),
              work=("hbm", 16 * B * N * 64))
-        return gx, None, None, None, gt.sum(0)
+        return gx, None, None, None, gt, None
 
 
-def spectral_diffusion(x, mass, evals, evecs, t):
-    """x [B,N,64] f32, mass [B,N], evals [B,64], evecs [B,N,64], t [64] -> [B,N,64]."""
+def spectral_diffusion(x, mass, evals, evecs, t, clamp_t: bool = False):
+    """x [B,N,64] f32, mass [B,N], evals [B,64], evecs [B,N,64], t [64] -> [B,N,64].
+    clamp_t: first clamp t in place to >= 1e-8 (the reference's LearnedTimeDiffusion)."""
     if x.shape[-1] != 64 or evecs.shape[-1] != 64:
         raise _lib.PoseKernError("spectral diffusion kernel is built for C_width = k_eig = 64")
-    return _SpectralDiffusion.apply(x, mass.contiguous(), evals.contiguous(), evecs.contiguous(), t.contiguous())
+    if clamp_t and not t.is_contiguous():
+        raise _lib.PoseKernError("spectral_diffusion: clamp_t needs the parameter's own contiguous storage")
+    return _SpectralDiffusion.apply(x, mass.contiguous(), evals.contiguous(), evecs.contiguous(),
+                                    t if clamp_t else t.contiguous(), bool(clamp_t))
 
 
 # ------------------------------------------------------------------------------ H9 fmap solve
@@ -679,6 +686,99 @@ def nce_loss(f1: torch.Tensor, f2: torch.Tensor, pairs: torch.Tensor, rows: torc
                           want)
 
 
+def affine_cat(a: torch.Tensor, b: torch.Tensor, sub: float, div: float) -> torch.Tensor:
+    """cat(((a - sub) / div, (b - sub) / div), 0) with torch's GPU rounding (a product with the
+    f32 reciprocal of the scalar divisor), one launch (pk_affine_cat). No gradient: the
+    inputs are data (vertex coordinates)."""
+    a, b = a.detach().contiguous(), b.detach().contiguous()
+    if a.dtype != torch.float32 or b.dtype != torch.float32 or a.shape[1:] != b.shape[1:]:
+        raise _lib.PoseKernError("affine_cat: f32 tensors of equal trailing shape")
+    out = torch.empty((a.shape[0] + b.shape[0],) + tuple(a.shape[1:]), dtype=torch.float32, device=a.device)
+    mul = float(np.float32(1.0) / np.float32(div))
+    call("pk_affine_cat", ptr(a), a.numel(), ptr(b), b.numel(), float(sub), mul, ptr(out), _lib.stream(a.device))
+    return out
+
+
+def _nce_raw(f1, f2, pairs, rows, valid, nce_t, want):
+    """pk_nce_loss: (loss [B], g1, g2) with g the gradients of each crop's loss (None unless want)."""
+    import ctypes
+    B, N1, C = f1.shape
+    N2 = f2.shape[1]
+    S = rows.shape[1]
+    dev = f1.device
+    f1c, f2c = f1.detach(), f2.detach()
+    if f1c.stride(-1) != 1 and f1c.stride(1) != 1:
+        f1c = f1c.contiguous()
+    if f2c.stride(-1) != 1 and f2c.stride(1) != 1:
+        f2c = f2c.contiguous()
+    st = lambda t: (ctypes.c_int64 * 3)(*t.stride())  # noqa: E731
+    lse = torch.empty((B, max(S, 1)), dtype=torch.float32, device=dev)
+    term = torch.empty_like(lse)
+    loss = torch.empty((B,), dtype=torch.float32, device=dev)
+    g1 = torch.empty((B, N1, C), dtype=torch.float32, device=dev) if want else None
+    g2 = torch.empty((B, N2, C), dtype=torch.float32, device=dev) if want else None
+    call("pk_nce_loss", ctypes.c_void_p(f1c.data_ptr()), st(f1c), ctypes.c_void_p(f2c.data_ptr()), st(f2c), B,
+         int(N1), int(N2), int(C), ptr(pairs), int(pairs.shape[1]), ptr(rows), ptr(valid), int(S), float(nce_t),
+         ptr(lse), ptr(term), ptr(loss), ptr(g1), ptr(g2), _lib.stream(dev), work=None)
+    return loss, g1, g2
+
+
+class _DPFMLossFn(torch.autograd.Function):
+    """DPFMLoss.forward (utils/loss.py:44-99) as one autograd node: NCE (pk_nce_loss) and WBCE
+    (pk_wbce) with their input gradients, the scalar head (pk_loss_head: Frobenius term,
+    weights, sums, dloss/dC12); the backward is one grouped scale (pk_loss_scale)."""
+
+    @staticmethod
+    def forward(ctx, C12, f1, f2, o12, o21, C_gt, pairs, rows, valid, t12, t21, w, nce_t):
+        w_fmap, w_acc, w_nce = w
+        want = any(ctx.needs_input_grad[:5])
+        B, K = C12.shape[0], C12.shape[1]
+        dev = C12.device
+        nce, g1, g2 = _nce_raw(f1, f2, pairs, rows, valid, nce_t, want)
+        N1, N2 = o12.shape[1], o21.shape[1]
+        wb = torch.empty((2, B), dtype=torch.float32, device=dev)
+        g12 = torch.empty_like(o12) if want else None
+        g21 = torch.empty_like(o21) if want else None
+        call("pk_wbce", ptr(o12), ptr(t12), N1, ptr(o21), ptr(t21), N2, B, ptr(wb), ptr(g12), ptr(g21),
+             _lib.stream(dev), work=None)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        logs = torch.empty((3,), dtype=torch.float32, device=dev)
+        dC = torch.empty_like(C12)
+        call("pk_loss_head", ptr(C12), ptr(C_gt), B, K, ptr(nce), ptr(wb), float(w_fmap), float(w_acc), float(w_nce),
+             ptr(loss), ptr(logs), ptr(dC), _lib.stream(dev), work=None)
+        ctx.save_for_backward(dC, g1, g2, g12, g21)
+        ctx.scales = (1.0, w_nce / B, w_nce / B, w_acc / B, w_acc / B)
+        ctx.mark_non_differentiable(logs)
+        return loss, logs
+
+    @staticmethod
+    def backward(ctx, gl, _glogs):
+        import ctypes
+        saved = ctx.saved_tensors
+        need = ctx.needs_input_grad[:5]
+        outs = [torch.empty_like(t) if (n and t is not None) else None for t, n in zip(saved, need)]
+        sel = [i for i, o in enumerate(outs) if o is not None]
+        if sel:
+            P = ctypes.c_void_p * len(sel)
+            call("pk_loss_scale", P(*[saved[i].data_ptr() for i in sel]), P(*[outs[i].data_ptr() for i in sel]),
+                 (ctypes.c_int64 * len(sel))(*[saved[i].numel() for i in sel]),
+                 (ctypes.c_float * len(sel))(*[ctx.scales[i] for i in sel]), len(sel), ptr(gl.contiguous()),
+                 _lib.stream(gl.device), work=None)
+        return (*outs, None, None, None, None, None, None, None, None)
+
+
+def dpfm_loss(C12, C_gt, f1, f2, pairs, rows, valid, o12, o21, t12, t21, w_fmap: float, w_acc: float,
+              w_nce: float, nce_t: float):
+    """DPFMLoss.forward for every crop at once -> (loss 0-d, logs f32 [3] = nce, acc, fmap)."""
+    def mask(t):
+        return (t if t.dtype == torch.int8 else (t >= 0.5).to(torch.int8)).contiguous()
+    if f1.dtype != torch.float32 or f1.shape[-1] != 32:
+        raise _lib.PoseKernError("pk_nce_loss takes f32 features of width 32")
+    return _DPFMLossFn.apply(C12.contiguous(), f1, f2, o12.contiguous(), o21.contiguous(), C_gt.contiguous(),
+                             pairs.contiguous(), rows.contiguous(), valid.contiguous().view(torch.uint8),
+                             mask(t12), mask(t21), (float(w_fmap), float(w_acc), float(w_nce)), float(nce_t))
+
+
 def rigidity_thresholds(diam: Sequence[float], device) -> torch.Tensor:
     """f32 [B,4]: float32(tau * diam) for tau = 0.3, 0.15, 0.055, 0.065 (Python-float
     products, as the reference compares with `tau * diam_cad`)."""
@@ -707,7 +807,7 @@ def rigidity_filter(cand: torch.Tensor, ncand: torch.Tensor, cad: torch.Tensor, 
 def inlier_ratio(pairs: torch.Tensor, npairs: torch.Tensor, cad: torch.Tensor, pc_aligned: torch.Tensor,
                  thr: torch.Tensor, layout: int = 0) -> torch.Tensor:
     B = cad.shape[0]
-    ldp = pairs.shape[1] if layout == 0 else pairs.shape[2]
+    ldp = pairs.shape[1] if layout in (0, 2) else pairs.shape[2]
     ir = torch.empty((B,), dtype=torch.float32, device=cad.device)
     call("pk_inlier_ratio", ptr(pairs.contiguous()), ldp, int(layout), ptr(npairs), ptr(cad.contiguous()),
          cad.shape[1], ptr(pc_aligned.contiguous()), pc_aligned.shape[1], ptr(thr), B, ptr(ir),

@@ -311,10 +311,15 @@ class TrainStep:
         if self.overlap:  # the point map + IR read only C_pred: beside the backward
             self.aux.wait_stream(main)
         with torch.no_grad(), _on(self.aux):  # train.py:109-116 (naive solver + IR per crop)
-            p_pred = naive_p2p_batched(C_pred.detach(), op.cad_evecs, op.pc_evecs, op.cad_n, crops.n2)
-            npred = _counts(crops.n2, p_pred.shape[0], p_pred.shape[2], p_pred.device)
-            ir = ops.inlier_ratio(p_pred, npred, op.cad_xyz, crops.align32, op.ir_thr, layout=1).mean()
-            # P truncated at the pair capacity would train on partial labels: flag it (device bool)
+            # naive point map (naive_p2p_batched without materialising its arange row: the IR
+            # kernel reads the map as [B, V2] CAD indices of crop points 0..n2-1)
+            B_, V2_ = op.pc_evecs.shape[0], op.pc_evecs.shape[1]
+            n1 = _counts(op.cad_n, B_, op.cad_evecs.shape[1], C_pred.device)
+            npred = _counts(crops.n2, B_, V2_, C_pred.device)
+            p_map, _ = ops.feat_dist_topk(op.cad_evecs, C_pred.detach(), op.pc_evecs, n1, npred, 1)
+            ir = ops.inlier_ratio(p_map[..., 0], npred, op.cad_xyz, crops.align32, op.ir_thr, layout=2).mean()
+            # P truncated at the pair capacity would train on partial labels: flag it (device
+            # bool, formed with the crops on the crop-formation stream)
             log["pair_overflow"] = crops.overflow()
         if self.flat_grads:  # accumulate into the flat buffer's views (autograd adds in place)
             self.flat.zero_()
@@ -323,8 +328,10 @@ class TrainStep:
         if self.side is not None:
             self.side.begin()
         ok = False
+        if getattr(self, "_seed_grad", None) is None or self._seed_grad.device != loss.device:
+            self._seed_grad = torch.ones((), dtype=loss.dtype, device=loss.device)  # persistent: no fill per step
         try:
-            loss.backward()
+            torch.autograd.backward(loss, grad_tensors=self._seed_grad)
             ok = True
         finally:
             if self.side is not None:

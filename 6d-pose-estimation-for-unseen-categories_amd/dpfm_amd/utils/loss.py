@@ -111,7 +111,23 @@ class DPFMLoss(nn.Module):
     def forward_batched(self, C12, C_gt, pairs, npairs, feat1, feat2, o12, o21, gt12, gt21,
                         generator: Optional[torch.Generator] = None, selection=None):
         """All crops at once. pairs int64 [B, cap, 2] (CAD idx, PC idx), npairs [B];
-        returns (loss, dict of 0-d tensors)."""
+        returns (loss, dict of 0-d tensors). One autograd node (ops.dpfm_loss): the NCE and
+        WBCE kernels with their input gradients plus the fused scalar head."""
+        from .. import ops
+        if not C12.is_cuda:
+            raise ops._lib.PoseKernError("DPFMLoss runs on HIP devices only (no CPU fallback)")
+        if o12.dim() == 1:
+            o12, o21 = o12[None], o21[None]
+        rows, valid = selection if selection is not None else nce_select(
+            npairs, pairs.shape[1], self.nce_softmax_loss.nce_num_pairs, generator)
+        loss, logs = ops.dpfm_loss(C12, C_gt, feat1, feat2, pairs, rows, valid, o12, o21, gt12, gt21,
+                                   self.w_fmap, self.w_acc, self.w_nce, self.nce_softmax_loss.nce_t)
+        return loss, {"nce_loss": logs[0], "acc_loss": logs[1], "fmap_loss": logs[2], "loss": loss.detach()}
+
+    def forward_batched_composed(self, C12, C_gt, pairs, npairs, feat1, feat2, o12, o21, gt12, gt21,
+                                 generator: Optional[torch.Generator] = None, selection=None):
+        """The same loss composed from the per-term kernels and torch ops (development
+        comparison for the fused head)."""
         fmap_loss = self.frob_loss(C12, C_gt) * self.w_fmap
         m = feat1.shape[0]
         if o12.dim() == 1:
@@ -121,8 +137,6 @@ class DPFMLoss(nn.Module):
         nce = self.nce_softmax_loss.forward_batched(feat1, feat2, pairs, rows, valid)
         nce_loss = (nce * self.w_nce / m).sum()
         from .. import ops
-        if not o12.is_cuda:
-            raise ops._lib.PoseKernError("DPFMLoss runs on HIP devices only (no CPU fallback)")
         wb = ops.weighted_bce_pair(o12, o21, gt12, gt21)  # both directions, loss + gradient, one launch
         acc_loss = ((wb[0] + wb[1]) * self.w_acc / m).sum()
         loss = fmap_loss + acc_loss + nce_loss

@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-crops", type=int, default=30, help="bounded CPU-baseline sample (crops)")
     ap.add_argument("--no-roofline-probe", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP graph: launch every kernel from Python")
+    ap.add_argument("--train-only", action="store_true",
+                    help="diagnostic: crops formed once, outside the timed graph (not a headline number)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="graph mode without overlapping crop formation of the next batch")
     ap.add_argument("--probe-steps", type=int, default=2, help="eager steps after timing for the kernel breakdown")
@@ -225,13 +227,17 @@ def build_train(args, dev, rank, world):
     step = TrainStep(model, seed=rank, capturable=not args.eager)
     if args.eager:
         one_step = lambda: step(op, crops_of(fb))  # noqa: E731
+    elif args.train_only:  # diagnostic: the training stream alone, on one fixed crop batch
+        fixed = crops_of(fb)
+        one_step = GraphedTrainStep(lambda _fb: fixed, step, fb, op, warmup=3)
     elif args.no_overlap:  # warm-up + capture (untimed), then every step is a graph replay
         one_step = GraphedTrainStep(crops_of, step, fb, op, warmup=3)
     else:  # same, with crop formation of the next batch on a second stream
         one_step = PipelinedTrainer(crops_of, step, fb, op, warmup=3)
     config = {"workload": f"configs[1] shape: B={B} synthetic 640x480 RGB-D crops/GPU, {N} pts, training step "
                           "fwd+bwd (configs[2] semantics, DDP over RCCL when N>1)",
-              "execution": "eager" if args.eager else ("hip-graph" if args.no_overlap else
+              "execution": "eager" if args.eager else ("hip-graph, training only (diagnostic)" if args.train_only else
+                                                       "hip-graph" if args.no_overlap else
                                                        "hip-graph, crop formation overlapped"),
               "global_batch": B * world, "points_per_crop": N, "cad_points": N,
               "precision": "model fp32 (f32 MFMA); crop geometry / C_gt normal equations fp64",

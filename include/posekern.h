@@ -125,14 +125,16 @@ int pk_offsets_from_counts(const int64_t* counts, int B, int64_t* off, void* str
 /* H7 spectral diffusion of DiffusionNet's LearnedTimeDiffusion (upstream layers.py,
  * models/dpfm.py:22-30), fp32, K = C = 64:
  *   mode 0: out = Phi (E ⊙ raw), raw = Phi^T (mass ⊙ in), E[k,c] = exp(-evals_k t_c)
- *   mode 1: out = mass ⊙ Phi (E ⊙ Phi^T in) (= dL/dx), gt[b,c] = -sum_k evals E saved (Phi^T in)
- *   in/out [B,N,C], mass [B,N], evecs [B,N,K], evals [B,K], t [C]
- *   work f32 [B, ceil(N/256), K, C]; raw (mode 0, may be NULL) / scaled [B,K,C];
- *   saved = raw of the forward (mode 1); gt [B,C] (mode 1) */
-int pk_spectral_diffusion(const float* in, const float* mass, const float* evecs, const float* evals,
-                          const float* t, int B, int N, int K, int C, int mode, float* work,
-                          float* raw, float* scaled, const float* saved, float* gt, float* out,
-                          void* stream);
+ *   mode 1: out = mass ⊙ Phi (E ⊙ Phi^T in) (= dL/dx), gt[c] = -sum_b sum_k evals E saved (Phi^T in)
+ *   in [B,N] rows of row stride ld_in, out rows of row stride ld_out (>= C, multiples of 4: a
+ *   slice of a wider concatenation buffer), mass [B,N], evecs [B,N,K], evals [B,K], t [C];
+ *   clamp_t: use max(t, 1e-8), and in mode 0 write it back into t (the reference's in-place
+ *   diffusion_time.clamp_(min=1e-8) before every diffusion);
+ *   work f32 [B, ceil(N/64), K, C]; raw (mode 0, may be NULL) / scaled [B,K,C];
+ *   saved = raw of the forward (mode 1); gt [C] (mode 1, summed over crops in crop order) */
+int pk_spectral_diffusion(const float* in, int ld_in, const float* mass, const float* evecs, const float* evals,
+                          float* t, int clamp_t, int B, int N, int K, int C, int mode, float* work, float* raw,
+                          float* scaled, const float* saved, float* gt, float* out, int ld_out, void* stream);
 
 /* H9 regularized fmap solve. Replaces the 30 sequential torch.inverse + bmm of
  * modeling/dpfm.py:185-193: C[b,i,:] = ((AAt_b + lambda diag(D_b[i,:]))^-1 BAt_b[i,:]^T)^T.
@@ -215,6 +217,12 @@ int pk_instnorm_relu_bwd(const float* x, const float* dy, const float* mean, con
 int pk_wbce(const float* p12, const int8_t* t12, int N1, const float* p21, const int8_t* t21, int N2, int B,
             float* loss, float* g12, float* g21, void* stream);
 
+/* models/dpfm.py:53,61-66: out = cat((a - sub) * mul, (b - sub) * mul) over na + nb f32
+ * elements (the shared encoder's input features; mul = float32(1) / 50, the reciprocal torch
+ * multiplies by when dividing by a Python scalar on the GPU). */
+int pk_affine_cat(const float* a, int64_t na, const float* b, int64_t nb, float sub, float mul, float* out,
+                  void* stream);
+
 /* F.normalize(x, p=2, dim=-1) over the C channels of [B, N, C] features (overlap head,
  * modeling/dpfm.py:140-145), forward and backward. strides = HOST int64[3] element strides
  * {batch, point, channel} shared by x / y / dy / dx (rows or channels-first storage);
@@ -278,7 +286,8 @@ int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* ncand, const
 
 /* H12 inlier ratio (utils/utils.py:81-105) per crop: mean(||cad[c] - pc_aligned[p]|| < thr),
  * 0 when there are no correspondences.
- *   pairs int64: layout 0 [B,ldp,2] (cad, pc) or layout 1 [B,2,ldp]; npairs int32 [B]
+ *   pairs int64: layout 0 [B,ldp,2] (cad, pc), layout 1 [B,2,ldp], or layout 2 [B,ldp] the CAD
+ *   index of crop point k (a point map: pc index = k); npairs int32 [B]
  *   cad f32 [B,ldcad,3], pc_aligned f32 [B,ldpc,3], thr f32 [B] -> ir f32 [B] */
 int pk_inlier_ratio(const int64_t* pairs, int ldp, int layout, const int32_t* npairs, const float* cad,
                     int ldcad, const float* pc_aligned, int ldpc, const float* thr, int B, float* ir,
@@ -313,6 +322,18 @@ int pk_nce_loss(const float* f1, const int64_t* st1, const float* f2, const int6
                 int64_t N2, int C, const int64_t* pairs,
                 int cap, const int64_t* rows, const uint8_t* valid, int S, float nce_t, float* lse, float* term,
                 float* loss, float* g1, float* g2, void* stream);
+
+/* H15 DPFMLoss scalar head (utils/loss.py:44-99, FrobeniusLoss :8-15), one launch:
+ *   fmap = w_fmap * mean_b clamp(sum (C12_b - Cgt_b)^2, -1, 1000); nce = sum_b nce[b] w_nce / B;
+ *   acc = sum_b (wb[b] + wb[B + b]) w_acc / B; loss[0] = (fmap + acc) + nce;
+ *   logs = {nce, acc, fmap}; dC = dloss/dC12 for a unit incoming gradient.
+ * C12 / Cgt / dC f32 [B,K,K]; nce f32 [B] (pk_nce_loss); wb f32 [2,B] (pk_wbce). B <= 1024. */
+int pk_loss_head(const float* C12, const float* Cgt, int B, int K, const float* nce, const float* wb,
+                 float w_fmap, float w_acc, float w_nce, float* loss, float* logs, float* dC, void* stream);
+/* dst[i] = src[i] * (scale[i] * g[0]) for n <= 8 tensors (HOST pointer tables; numel HOST
+ * int64[n]) in one launch: the loss head's saved input gradients times the incoming one. */
+int pk_loss_scale(const float* const* src, float* const* dst, const int64_t* numel, const float* scale, int n,
+                  const float* g, void* stream);
 int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs, const float* evecs1, int ld1,
                  int V1max, const float* evecs2, int ld2, int V2max, int B, int K, double* work,
                  float* Cgt, void* stream);

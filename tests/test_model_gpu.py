@@ -283,6 +283,8 @@ def test_dpfm_loss_matches_oracle(device):
     f2 = torch.randn(B, N2, 32, generator=g)
     C = torch.randn(B, 30, 30, generator=g)
     C_gt = torch.randn(B, 30, 30, generator=g)
+    # crops 0-1 below FrobeniusLoss's clamp (sum ~ 225 < 1000: gradient flows), 2-3 above it
+    C_gt[:2] = C[:2] + 0.5 * torch.randn(2, 30, 30, generator=g)
     o12 = torch.rand(B, N1, generator=g) * 0.98 + 0.01
     o21 = torch.rand(B, N2, generator=g) * 0.98 + 0.01
     g12 = (torch.rand(B, N1, generator=g) < 0.4).to(torch.int8)
@@ -304,6 +306,7 @@ def test_dpfm_loss_matches_oracle(device):
     ref = M.dpfm_loss(rv[0], C_gt.double(), plist, sel, rv[1], rv[2], rv[3], rv[4], g12, g21)
     ref.backward()
     assert abs(float(loss) - float(ref)) <= 1e-4 * abs(float(ref)), (float(loss), float(ref))
+    assert rv[0].grad[:2].abs().max() > 0 and rv[0].grad[2:].abs().max() == 0  # both clamp regimes covered
     for name, a, r in zip(("C", "f1", "f2", "o12", "o21"), dv, rv):
         ga, gr = a.grad.cpu().double(), r.grad
         scale = float(gr.abs().max())

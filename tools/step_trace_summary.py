@@ -40,3 +40,20 @@ for r in win:
     tot[n][1] += 1
 for n, (t, c) in sorted(tot.items(), key=lambda kv: -kv[1][0])[:int(sys.argv[3]) if len(sys.argv) > 3 else 45]:
     print(f"{t/1e3/steps:8.1f} us/step {c/steps:6.1f}/step  {n}")
+
+# the main queue's kernels of the last step, in issue order (duration, gap before it)
+def short(r):
+    n = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+    if n.startswith("at::native"):
+        m = re.findall(r"at::native::(?:\(anonymous namespace\)::)?([A-Za-z_]+(?:Functor[A-Za-z_]*)?|[a-z_]+_kernel[a-z_]*)", r["Kernel_Name"])
+        return "/".join(dict.fromkeys(m[:4]))[:80]
+    return re.split(r"[(<]", n)[0][:80]
+mq = max(byq.values(), key=len)
+per = len(mq) // steps
+print(f"\n--- main queue, last step ({per} kernels) ---")
+prev = None
+for r in mq[-per:]:
+    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    gap = (s - prev) / 1e3 if prev is not None else 0.0
+    prev = e
+    print(f"{(e - s) / 1e3:7.1f} us  gap {gap:6.1f}  {short(r)}")
