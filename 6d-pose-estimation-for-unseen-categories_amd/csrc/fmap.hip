@@ -179,3 +179,234 @@ extern "C" int pk_resolvent_mask(const float* evals1, int ld1, const float* eval
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
+
+// ---------------------------------------------------------------------------------
+// H9 fmap head around the solve (modeling/dpfm.py:154-176, the batched branch that always
+// runs; models/dpfm.py:66-72 for evecs_trans):
+//   W = evecs[:, :K] * mass (f32 products, the reference's evecs_trans before its transpose)
+//   A = W_x^T F_x, Bm = W_y^T F_y            [K, C] per crop (F = refined features [N, C])
+//   AAt = A A^T, BAt = Bm A^T, D = get_mask(evals_x, evals_y)   -> pk_fmap_solve
+// Forward in one launch per batch (one workgroup per crop: W and F staged through LDS in
+// 64-point chunks, each thread two outputs of A / Bm, then the K x K products and the mask);
+// backward in two: the K x C gradients of A and Bm (dAAt = the solve backward's per-row slabs
+// summed in row order), then dF = (W dA) / (W dBm) per point, written straight into the
+// caller's feature-gradient layout. Replaces the evecs * mass products, four batched GEMMs,
+// the mask launch and, backward, six GEMMs, the slab sum and the gradient additions.
+namespace {
+
+constexpr int kHK = 30, kHC = 32, kHChunk = 64;
+
+struct FeatRef {  // element (b, n, c) at base + b * sb + n * sn + c * sc
+  const float* base;
+  int64_t sb, sn, sc;
+};
+
+__device__ __forceinline__ void head_project(const float* __restrict__ ev, int lde, const float* __restrict__ mass,
+                                             const FeatRef f, int b, int N, float (*Ws)[kHK + 1],
+                                             float (*Fs)[kHC + 1], float (*out)[kHC + 1]) {
+  const int tid = threadIdx.x;
+  const int k = tid >> 4, c = (tid & 15) * 2;  // threads < 480: outputs (k, c), (k, c + 1)
+  float a0 = 0.f, a1 = 0.f;
+  for (int n0 = 0; n0 < N; n0 += kHChunk) {
+    const int m = min(kHChunk, N - n0);
+    __syncthreads();
+    for (int e = tid; e < kHChunk * kHK; e += blockDim.x) {
+      const int r = e / kHK, kk = e - r * kHK;
+      float v = 0.f;
+      if (r < m) {
+        const int64_t n = (int64_t)b * N + n0 + r;
+        v = ev[n * lde + kk] * mass[n];  // f32 product, as evecs[:, :, :k] * mass[:, :, None]
+      }
+      Ws[r][kk] = v;
+    }
+    for (int e = tid; e < kHChunk * kHC; e += blockDim.x) {
+      const int r = e / kHC, cc = e - r * kHC;
+      Fs[r][cc] = r < m ? f.base[(int64_t)b * f.sb + (int64_t)(n0 + r) * f.sn + (int64_t)cc * f.sc] : 0.f;
+    }
+    __syncthreads();
+    if (tid < kHK * 16) {
+      for (int r = 0; r < m; ++r) {
+        const float w = Ws[r][k];
+        a0 = fmaf(w, Fs[r][c], a0);
+        a1 = fmaf(w, Fs[r][c + 1], a1);
+      }
+    }
+  }
+  if (tid < kHK * 16) {
+    out[k][c] = a0;
+    out[k][c + 1] = a1;
+  }
+}
+
+__global__ __launch_bounds__(512) void fmap_head_fwd_kernel(const float* __restrict__ ex, int ldex,
+                                                            const float* __restrict__ mx, const FeatRef fx, int N1,
+                                                            const float* __restrict__ ey, int ldey,
+                                                            const float* __restrict__ my, const FeatRef fy, int N2,
+                                                            const float* __restrict__ evx, int ldvx,
+                                                            const float* __restrict__ evy, int ldvy, float gamma,
+                                                            float* __restrict__ A, float* __restrict__ Bm,
+                                                            float* __restrict__ AAt, float* __restrict__ BAt,
+                                                            float* __restrict__ D) {
+  __shared__ float Ws[kHChunk][kHK + 1];
+  __shared__ float Fs[kHChunk][kHC + 1];
+  __shared__ float As[kHK][kHC + 1], Bs[kHK][kHC + 1];
+  __shared__ float red[8], g1s[kHK], g2s[kHK];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  head_project(ex, ldex, mx, fx, b, N1, Ws, Fs, As);
+  head_project(ey, ldey, my, fy, b, N2, Ws, Fs, Bs);
+  __syncthreads();
+  for (int e = tid; e < kHK * kHC; e += blockDim.x) {
+    const int k = e / kHC, c = e - k * kHC;
+    A[(int64_t)b * kHK * kHC + e] = As[k][c];
+    Bm[(int64_t)b * kHK * kHC + e] = Bs[k][c];
+  }
+  for (int e = tid; e < kHK * kHK; e += blockDim.x) {
+    const int i = e / kHK, j = e - i * kHK;
+    float s = 0.f, t = 0.f;
+#pragma unroll 8
+    for (int c = 0; c < kHC; ++c) {
+      s = fmaf(As[i][c], As[j][c], s);
+      t = fmaf(Bs[i][c], As[j][c], t);
+    }
+    AAt[(int64_t)b * kHK * kHK + e] = s;
+    BAt[(int64_t)b * kHK * kHK + e] = t;
+  }
+  // the resolvent mask (resolvent_mask_kernel's arithmetic)
+  float mxv = -__builtin_huge_valf();
+  if (tid < kHK) mxv = fmaxf(evx[(int64_t)b * ldvx + tid], evy[(int64_t)b * ldvy + tid]);
+  for (int off = 32; off >= 1; off >>= 1) mxv = fmaxf(mxv, __shfl_xor(mxv, off));
+  if ((tid & 63) == 0) red[tid >> 6] = mxv;
+  __syncthreads();
+  float s = red[0];
+  for (int w = 1; w < (int)(blockDim.x >> 6); ++w) s = fmaxf(s, red[w]);
+  if (tid < kHK) {
+    const float a = evx[(int64_t)b * ldvx + tid] / s, c = evy[(int64_t)b * ldvy + tid] / s;
+    g1s[tid] = gamma == 0.5f ? sqrtf(a) : powf(a, gamma);
+    g2s[tid] = gamma == 0.5f ? sqrtf(c) : powf(c, gamma);
+  }
+  __syncthreads();
+  for (int e = tid; e < kHK * kHK; e += blockDim.x) {
+    const int j = e / kHK, i = e - j * kHK;
+    const float g1 = g1s[i], g2 = g2s[j];
+    const float q1 = g1 * g1 + 1.f, q2 = g2 * g2 + 1.f;
+    const float re = g2 / q2 - g1 / q1;
+    const float im = 1.f / q2 - 1.f / q1;
+    D[(int64_t)b * kHK * kHK + e] = re * re + im * im;
+  }
+}
+
+// grid (B), block 512: dAAt = sum_j part[b, j] (row order); dA = (dAAt + dAAt^T) A + dBAt^T Bm;
+// dBm = dBAt A.
+__global__ __launch_bounds__(512) void fmap_head_grad_kernel(const float* __restrict__ part,
+                                                             const float* __restrict__ dBAt,
+                                                             const float* __restrict__ A,
+                                                             const float* __restrict__ Bm,
+                                                             float* __restrict__ dA, float* __restrict__ dBm) {
+  __shared__ float G[kHK][kHK + 1], H[kHK][kHK + 1];
+  __shared__ float As[kHK][kHC + 1], Bs[kHK][kHC + 1];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  for (int e = tid; e < kHK * kHK; e += blockDim.x) {
+    const float* p = part + (int64_t)b * kHK * kHK * kHK + e;
+    float s = 0.f;
+    for (int j = 0; j < kHK; ++j) s += p[(int64_t)j * kHK * kHK];
+    G[e / kHK][e % kHK] = s;
+    H[e / kHK][e % kHK] = dBAt[(int64_t)b * kHK * kHK + e];
+  }
+  for (int e = tid; e < kHK * kHC; e += blockDim.x) {
+    As[e / kHC][e % kHC] = A[(int64_t)b * kHK * kHC + e];
+    Bs[e / kHC][e % kHC] = Bm[(int64_t)b * kHK * kHC + e];
+  }
+  __syncthreads();
+  for (int e = tid; e < kHK * kHC; e += blockDim.x) {
+    const int k = e / kHC, c = e - k * kHC;
+    float da = 0.f, db = 0.f;
+    for (int j = 0; j < kHK; ++j) {
+      da = fmaf(G[k][j] + G[j][k], As[j][c], da);
+      da = fmaf(H[j][k], Bs[j][c], da);
+      db = fmaf(H[k][j], As[j][c], db);
+    }
+    dA[(int64_t)b * kHK * kHC + e] = da;
+    dBm[(int64_t)b * kHK * kHC + e] = db;
+  }
+}
+
+// grid (ceil(Nmax / 64), B, 2), block 256: dF[n, c] = sum_k W[n, k] dA[k, c] for the x side
+// (z = 0) / y side (z = 1), W = evecs * mass; written to dF (element (b, n, c) at b sb + n sn
+// + c sc: the caller's layout). Threads: 64 points x 4 channel groups of 8.
+struct FeatOut {
+  float* base;
+  int64_t sb, sn, sc;
+};
+
+__global__ __launch_bounds__(256) void fmap_head_expand_kernel(const float* __restrict__ ex, int ldex,
+                                                               const float* __restrict__ mx, int N1,
+                                                               const float* __restrict__ ey, int ldey,
+                                                               const float* __restrict__ my, int N2,
+                                                               const float* __restrict__ dA,
+                                                               const float* __restrict__ dBm, FeatOut ox,
+                                                               FeatOut oy) {
+  __shared__ float Gs[kHK][kHC];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const bool xs = blockIdx.z == 0;
+  const int N = xs ? N1 : N2;
+  const int n0 = blockIdx.x * 64;
+  if (n0 >= N) return;
+  const float* g = (xs ? dA : dBm) + (int64_t)b * kHK * kHC;
+  for (int e = tid; e < kHK * kHC; e += 256) Gs[e / kHC][e % kHC] = g[e];
+  __syncthreads();
+  const int n = n0 + (tid & 63), cg = (tid >> 6) * 8;
+  if (n >= N) return;
+  const float* ev = xs ? ex : ey;
+  const int lde = xs ? ldex : ldey;
+  const int64_t row = (int64_t)b * N + n;
+  const float m = (xs ? mx : my)[row];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < kHK; ++k) {
+    const float w = ev[row * lde + k] * m;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = fmaf(w, Gs[k][cg + q], acc[q]);
+  }
+  const FeatOut o = xs ? ox : oy;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o.base[(int64_t)b * o.sb + (int64_t)n * o.sn + (int64_t)(cg + q) * o.sc] = acc[q];
+}
+
+}  // namespace
+
+extern "C" int pk_fmap_head_fwd(const float* evecs_x, int ldex, const float* mass_x, const float* fx,
+                                const int64_t* fx_strides, int N1, const float* evecs_y, int ldey,
+                                const float* mass_y, const float* fy, const int64_t* fy_strides, int N2,
+                                const float* evals_x, int ldvx, const float* evals_y, int ldvy, int B, int K, int C,
+                                float gamma, float* A, float* Bm, float* AAt, float* BAt, float* D, void* stream) {
+  PK_REQUIRE(B >= 0 && K == kHK && C == kHC && N1 > 0 && N2 > 0 && ldex >= K && ldey >= K && ldvx >= K && ldvy >= K);
+  if (B == 0) return PK_OK;
+  PK_REQUIRE(evecs_x && mass_x && fx && fx_strides && evecs_y && mass_y && fy && fy_strides && evals_x && evals_y);
+  PK_REQUIRE(A && Bm && AAt && BAt && D);
+  const FeatRef rx{fx, fx_strides[0], fx_strides[1], fx_strides[2]};
+  const FeatRef ry{fy, fy_strides[0], fy_strides[1], fy_strides[2]};
+  hipLaunchKernelGGL(fmap_head_fwd_kernel, dim3(B), dim3(512), 0, pk::as_stream(stream), evecs_x, ldex, mass_x, rx,
+                     N1, evecs_y, ldey, mass_y, ry, N2, evals_x, ldvx, evals_y, ldvy, gamma, A, Bm, AAt, BAt, D);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_fmap_head_bwd(const float* part, const float* dBAt, const float* A, const float* Bm,
+                                const float* evecs_x, int ldex, const float* mass_x, int N1, const float* evecs_y,
+                                int ldey, const float* mass_y, int N2, int B, int K, int C, float* dA, float* dBm,
+                                float* dfx, const int64_t* dfx_strides, float* dfy, const int64_t* dfy_strides,
+                                void* stream) {
+  PK_REQUIRE(B >= 0 && K == kHK && C == kHC && N1 > 0 && N2 > 0 && ldex >= K && ldey >= K);
+  if (B == 0) return PK_OK;
+  PK_REQUIRE(part && dBAt && A && Bm && evecs_x && mass_x && evecs_y && mass_y && dA && dBm);
+  PK_REQUIRE(dfx && dfx_strides && dfy && dfy_strides);
+  hipStream_t s = pk::as_stream(stream);
+  hipLaunchKernelGGL(fmap_head_grad_kernel, dim3(B), dim3(512), 0, s, part, dBAt, A, Bm, dA, dBm);
+  PK_CHECK_LAUNCH();
+  const FeatOut ox{dfx, dfx_strides[0], dfx_strides[1], dfx_strides[2]};
+  const FeatOut oy{dfy, dfy_strides[0], dfy_strides[1], dfy_strides[2]};
+  const int Nmax = N1 > N2 ? N1 : N2;
+  hipLaunchKernelGGL(fmap_head_expand_kernel, dim3((Nmax + 63) / 64, B, 2), dim3(256), 0, s, evecs_x, ldex, mass_x, N1,
+                     evecs_y, ldey, mass_y, N2, dA, dBm, ox, oy);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}

@@ -243,6 +243,140 @@ __global__ __launch_bounds__(NT) void fps_pruned_kernel(
   }
 }
 
+// Per-lane buckets (crops above the LDS bound of fps_pruned_kernel). Thread t holds PPT CONSECUTIVE points
+// (indices t PPT .. t PPT + PPT - 1: a short run of image row in the crop's pixel order, so a
+// compact box), and the lane's running maximum bd is exactly its bucket maximum — tracked
+// anyway for the argmax, so the skip test costs no reduction. A lane updates its points only
+// when the centroid can lower one of them (box distance lb with lb (1 - 2^-19) < bd; the
+// exactness argument of fps_pruned_kernel), and a wave none of whose lanes needs the centroid
+// skips the whole iteration body, reusing its cached (max, index, coordinates). The block
+// result carries the winner's coordinates (no LDS / global read for the next centroid); one
+// barrier per iteration (double-buffered slots). Ties: first maximal index, as torch.max
+// (strict > over a lane's increasing indices; min index among equal maxima across lanes).
+template <int NT, int PPT>
+__global__ __launch_bounds__(NT) void fps_lane_kernel(
+    const float* __restrict__ xyz, const int64_t* __restrict__ offsets,
+    const int32_t* __restrict__ start, const int32_t* __restrict__ npoint,
+    int64_t* __restrict__ out, int out_stride) {
+  constexpr int NW = NT / pk::kWave;
+  static_assert(NW <= 16, "slot layout limit");
+  __shared__ uint32_t slot_b[2][16], slot_i[2][16];
+  __shared__ float slot_x[2][16], slot_y[2][16], slot_z[2][16];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = pk::lane_id(), w = pk::wave_id();
+  const int64_t base = offsets[b];
+  const int n = (int)(offsets[b + 1] - base);
+  const int np = npoint[b];
+  const float* __restrict__ p = xyz + base * 3;
+
+  float px[PPT], py[PPT], pz[PPT], pd[PPT];
+  const float inf = __builtin_huge_valf();
+  float bx0 = inf, bx1 = -inf, by0 = inf, by1 = -inf, bz0 = inf, bz1 = -inf;
+  const int i0 = tid * PPT;
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const bool ok = i0 + k < n;
+    px[k] = ok ? p[3 * (i0 + k) + 0] : 0.f;
+    py[k] = ok ? p[3 * (i0 + k) + 1] : 0.f;
+    pz[k] = ok ? p[3 * (i0 + k) + 2] : 0.f;
+    pd[k] = ok ? 1e10f : -1.f;  // empty slot: min(-1, d >= 0) keeps it at -1, never selected
+    if (ok) {
+      bx0 = fminf(bx0, px[k]); bx1 = fmaxf(bx1, px[k]);
+      by0 = fminf(by0, py[k]); by1 = fmaxf(by1, py[k]);
+      bz0 = fminf(bz0, pz[k]); bz1 = fmaxf(bz1, pz[k]);
+    }
+  }
+  const bool lval = i0 < n;
+  if (n <= 0 || np <= 0) return;
+
+  // the lane's current maximum running distance, its point and that point's coordinates
+  float bd = lval ? 1e10f : -1.f;
+  int bk = 0;
+  float qx = px[0], qy = py[0], qz = pz[0];
+  int far = start[b];
+  float cx = p[3 * far + 0], cy = p[3 * far + 1], cz = p[3 * far + 2];
+  uint32_t wbits = 0u, widx = 0xffffffffu;
+  float wx = 0.f, wy = 0.f, wz = 0.f;
+  int64_t* __restrict__ o = out + (int64_t)b * out_stride;
+  for (int i = 0; i < np; ++i) {
+    if (tid == 0) o[i] = far;
+    const float ddx = fmaxf(fmaxf(bx0 - cx, cx - bx1), 0.f);
+    const float ddy = fmaxf(fmaxf(by0 - cy, cy - by1), 0.f);
+    const float ddz = fmaxf(fmaxf(bz0 - cz, cz - bz1), 0.f);
+    const float lb = (ddx * ddx + ddy * ddy) + ddz * ddz;
+    const bool need = lval && !(lb * 0.99999809f >= bd);
+    if (__ballot(need)) {  // wave-uniform
+      if (need) {
+        bd = -1.f;
+#pragma unroll
+        for (int k = 0; k < PPT; ++k) {
+          const float dx = px[k] - cx;
+          const float dy = py[k] - cy;
+          const float dz = pz[k] - cz;
+          const float d = (dx * dx + dy * dy) + dz * dz;  // no contraction (TU flag)
+          pd[k] = fminf(pd[k], d);
+          const bool gt = pd[k] > bd;  // strict: lowest index on ties
+          bd = gt ? pd[k] : bd;
+          bk = gt ? k : bk;
+          qx = gt ? px[k] : qx;
+          qy = gt ? py[k] : qy;
+          qz = gt ? pz[k] : qz;
+        }
+      }
+      const bool valid = bd >= 0.f;
+      const uint32_t bits = valid ? pk::f32_bits(bd) : 0u;
+      const uint32_t gidx = valid ? (uint32_t)(i0 + bk) : 0xffffffffu;
+      wbits = pk::wave_max_u32_s(bits);
+      const uint64_t at = __ballot(valid && bits == wbits);
+      int wl;
+      if ((at & (at - 1)) == 0) {  // one lane at the max: lanes hold increasing index runs
+        wl = __ffsll((unsigned long long)at) - 1;
+      } else {  // several lanes: the first one holds the lowest index
+        wl = __ffsll((unsigned long long)at) - 1;
+      }
+      widx = pk::readlane(gidx, wl);
+      wx = __uint_as_float(pk::readlane(__float_as_uint(qx), wl));
+      wy = __uint_as_float(pk::readlane(__float_as_uint(qy), wl));
+      wz = __uint_as_float(pk::readlane(__float_as_uint(qz), wl));
+    }
+    const int par = i & 1;
+    if (lane == 0) {
+      slot_b[par][w] = wbits;
+      slot_i[par][w] = widx;
+      slot_x[par][w] = wx;
+      slot_y[par][w] = wy;
+      slot_z[par][w] = wz;
+    }
+    __syncthreads();
+    uint32_t vb = 0u, vi = 0xffffffffu;
+    float vx = 0.f, vy = 0.f, vz = 0.f;
+    if (lane < NW) {
+      vb = slot_b[par][lane];
+      vi = slot_i[par][lane];
+      vx = slot_x[par][lane];
+      vy = slot_y[par][lane];
+      vz = slot_z[par][lane];
+    }
+    // waves hold increasing index ranges too: the first wave at the max has the lowest index
+    const uint32_t m = pk::readlane(pk::row_max_u32(vb), 0);
+    const int l = __ffsll((unsigned long long)__ballot(lane < NW && vb == m)) - 1;
+    far = (int)pk::readlane(vi, l);
+    cx = __uint_as_float(pk::readlane(__float_as_uint(vx), l));
+    cy = __uint_as_float(pk::readlane(__float_as_uint(vy), l));
+    cz = __uint_as_float(pk::readlane(__float_as_uint(vz), l));
+  }
+}
+
+template <int NT, int PPT>
+int launch_fps_lane(const float* xyz, const int64_t* offsets, const int32_t* start, const int32_t* npoint,
+                    int64_t* out, int out_stride, int B, hipStream_t s) {
+  hipLaunchKernelGGL((fps_lane_kernel<NT, PPT>), dim3(B), dim3(NT), 0, s, xyz, offsets, start, npoint, out,
+                     out_stride);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
 template <int NT, int PPT>
 int launch_fps(const float* xyz, const int64_t* offsets, const int32_t* start,
                const int32_t* npoint, int64_t* out, int out_stride, int B, int nmax,
@@ -286,20 +420,23 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
   PK_REQUIRE(xyz && offsets && start && npoint && out);
   hipStream_t s = pk::as_stream(stream);
 #define PK_FPS(NT, PPT) return launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s)
-  // 1024-thread workgroups above 4096 points: measured 0.715 us per FPS step against 0.782
-  // (512 threads) and 1.078 (256) on the configs' crops (n <= 6588, profiles/r01_kbench.txt)
+  // 1024-thread workgroups above 4096 points: measured 0.712 us per FPS step against 0.78
+  // (512 threads) and 1.09 (256) on the bench's crops (n <= 6588, profiles/r02_kbench_fps.txt)
   if (nmax <= 1024) PK_FPS(256, 4);
   if (nmax <= 2048) PK_FPS(256, 8);
   if (nmax <= 4096) PK_FPS(256, 16);
   if (nmax <= 8192) PK_FPS(1024, 8);
   if (nmax <= 13312) PK_FPS(1024, 13);
-  if (nmax <= 32768) PK_FPS(1024, 32);
 #undef PK_FPS
+  // beyond the LDS copy of the pruned kernel: per-lane buckets, points in registers only
+  if (nmax <= 16384) return launch_fps_lane<1024, 16>(xyz, offsets, start, npoint, out, out_stride, B, s);
+  if (nmax <= 24576) return launch_fps_lane<1024, 24>(xyz, offsets, start, npoint, out, out_stride, B, s);
+  if (nmax <= 32768) return launch_fps<1024, 32>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
   return PK_ERR_ARG;  // > 32768 points per crop
 }
 
 // Development hook (not part of include/posekern.h): force the block size / points
-// per thread, pruned (pruned = 1) or plain, for tools/kbench.py's configuration sweeps.
+// per thread, per-lane buckets (pruned = 3), pruned (1) or plain (0), for tools/kbench.py's sweeps.
 extern "C" int pkdev_fps_cfg(const float* xyz, const int64_t* offsets, int B, int nmax,
                              const int32_t* start, const int32_t* npoint, int64_t* out,
                              int out_stride, int nt, int pruned, void* stream) {
@@ -307,7 +444,8 @@ extern "C" int pkdev_fps_cfg(const float* xyz, const int64_t* offsets, int B, in
   const int ppt = (nmax + nt - 1) / nt;
 #define PK_FPS(NT, PPT)                                                                          \
   if (nt == NT && ppt <= PPT)                                                                    \
-    return pruned ? launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s) \
+    return pruned == 3 ? launch_fps_lane<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, s) \
+           : pruned ? launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s) \
                   : launch_fps_plain<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
   PK_FPS(256, 4) PK_FPS(256, 8) PK_FPS(256, 16) PK_FPS(256, 32)
   PK_FPS(512, 2) PK_FPS(512, 4) PK_FPS(512, 8) PK_FPS(512, 16) PK_FPS(512, 26)

@@ -517,6 +517,50 @@ __device__ __forceinline__ float relu_mask(float v, const float* __restrict__ ma
   return (mask != nullptr && mask[i] <= 0.f) ? 0.f : v;
 }
 
+// Output side of a per-point layer launch (pk_linear_ex): where y goes and what the epilogue
+// folds in. Strides are element strides: rows layout — row stride; channels-first — batch
+// stride (the channel stride is N). v = acc + bias; ReLU; mask (contiguous, the ReLU backward
+// of the producing layer); + add (columns < add_cols); then stored to y (columns < split) or
+// y2 (columns >= split, at column - split), or channels-first when store_cf (rows kernels).
+struct LinEpi {
+  float* y;
+  int64_t sy;
+  float* y2;
+  int64_t sy2;
+  int split;
+  const float* add;
+  int64_t sa;
+  int add_cols;
+  const float* mask;
+  int relu;  // 0 none, 1 ReLU, 2 sigmoid (1 / (1 + exp(-v)))
+  int store_cf;
+  int N;
+  const float* pre;  // thin kernels: input x scaled by pre (1 - pre) first (sigmoid backward)
+  float* pre_out;    // ... and that scaled input written here (same indexing as x)
+};
+
+__device__ __forceinline__ float lin_act(int act, float v) {
+  return act == 1 ? fmaxf(v, 0.f) : act == 2 ? 1.f / (1.f + expf(-v)) : v;
+}
+
+__device__ __forceinline__ float lin_epi(const LinEpi& e, float v, int64_t mask_i) {
+  return relu_mask(lin_act(e.relu, v), e.mask, mask_i);
+}
+
+// rows-layout store of output column o of point r (Cout outputs per point)
+__device__ __forceinline__ void lin_store_row(const LinEpi& e, int64_t r, int o, int Cout, float v) {
+  v = lin_epi(e, v, r * Cout + o);
+  if (e.add != nullptr && o < e.add_cols) v += e.add[r * e.sa + o];
+  if (e.store_cf) {
+    const int64_t b = r / e.N, n = r - b * e.N;
+    e.y[b * e.sy + (int64_t)o * e.N + n] = v;
+  } else if (o >= e.split) {
+    e.y2[r * e.sy2 + (o - e.split)] = v;
+  } else {
+    e.y[r * e.sy + o] = v;
+  }
+}
+
 template <int LAYOUT>
 __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                          const float* __restrict__ bias, int64_t R, int N, int Cin,
@@ -614,10 +658,11 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict
 // ds_read_b128 from Ws[o][k] (row stride KP + 4: conflict-free over 8-lane phases).
 
 template <int Q>
-__device__ __forceinline__ void lr_load(const float* __restrict__ x, int64_t row, int64_t R, int g, f32x4 (&xa)[Q]) {
+__device__ __forceinline__ void lr_load(const float* __restrict__ x, int64_t sx, int64_t row, int64_t R, int g,
+                                        f32x4 (&xa)[Q]) {
 #pragma unroll
   for (int q = 0; q < Q; ++q)
-    xa[q] = row < R ? *reinterpret_cast<const f32x4*>(x + row * (16 * Q) + 16 * q + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+    xa[q] = row < R ? *reinterpret_cast<const f32x4*>(x + row * sx + 16 * q + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
 // Weight staging shared by the MFMA per-point kernels: Ws[o][k] (o < 16 TO, zero rows past
@@ -655,10 +700,10 @@ __device__ __forceinline__ void lr_stage(const float* __restrict__ w, int Cout, 
 }
 
 template <int Q, int TO>  // Cin = 16 Q, Cout <= 16 TO
-__global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __restrict__ x, const float* __restrict__ w,
+__global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __restrict__ x, int64_t sx,
+                                                              const float* __restrict__ w,
                                                               const float* __restrict__ bias, int64_t R, int Cin,
-                                                              int Cout, int transw, int relu, const float* __restrict__ mask,
-    float* __restrict__ y) {
+                                                              int Cout, int transw, LinEpi e) {
   extern __shared__ float Ws[];  // [16 TO][Cin + 4]
   constexpr int CI = 16 * Q, ST = CI + 4;
   const int lane = pk::lane_id(), m = lane & 15, g = lane >> 4;
@@ -666,7 +711,7 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
   int64_t tile = (int64_t)blockIdx.x * 4 + pk::wave_id();
   // the first tile's operands are in flight while the weight is staged
   f32x4 cur[Q], nxt[Q];
-  lr_load<Q>(x, tile < T ? tile * 16 + m : R, R, g, cur);
+  lr_load<Q>(x, sx, tile < T ? tile * 16 + m : R, R, g, cur);
   lr_stage<Q, TO>(w, Cout, transw, Ws);
   __syncthreads();
   if (tile >= T) return;
@@ -678,7 +723,7 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
   }
   for (;;) {
     const int64_t tn = tile + stride;
-    if (tn < T) lr_load<Q>(x, tn * 16 + m, R, g, nxt);
+    if (tn < T) lr_load<Q>(x, sx, tn * 16 + m, R, g, nxt);
     f32x4 acc[TO];
 #pragma unroll
     for (int t = 0; t < TO; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -705,11 +750,7 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t pr = tile * 16 + 4 * g + r;
-          if (pr < R && o < Cout) {
-            float v = acc[t][r] + bv[t];
-            if (relu) v = fmaxf(v, 0.f);
-            y[pr * Cout + o] = relu_mask(v, mask, pr * Cout + o);
-          }
+          if (pr < R && o < Cout) lin_store_row(e, pr, o, Cout, acc[t][r] + bv[t]);
         }
       }
     }
@@ -732,10 +773,10 @@ template <> struct LcVec<2> { using T = __attribute__((ext_vector_type(2))) floa
 template <> struct LcVec<4> { using T = f32x4; };
 
 template <int Q, int TO, int SUB>
-__global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restrict__ x, const float* __restrict__ w,
+__global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restrict__ x, int64_t sx,
+                                                            const float* __restrict__ w,
                                                             const float* __restrict__ bias, int64_t R, int N, int Cout,
-                                                            int transw, int relu, const float* __restrict__ mask,
-    float* __restrict__ y) {
+                                                            int transw, LinEpi e) {
   using V = typename LcVec<SUB>::T;
   extern __shared__ float Ws[];
   constexpr int CI = 16 * Q, ST = CI + 4, P = 16 * SUB;
@@ -749,7 +790,7 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
     const int64_t p0 = tile * P;
     bb = p0 / N;
     n0 = p0 - bb * N;
-    const float* xb = x + bb * CI * (int64_t)N + n0 + SUB * m;
+    const float* xb = x + bb * sx + n0 + SUB * m;
 #pragma unroll
     for (int q = 0; q < Q; ++q)
 #pragma unroll
@@ -781,7 +822,9 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
     __builtin_amdgcn_sched_barrier(0);
   }
   // D[out t * 16 + 4 g + r][column m of sub-tile u] = point n0 + SUB m + u
-  float* yb = y + bb * Cout * (int64_t)N + n0 + SUB * m;
+  const int64_t pn = n0 + SUB * m;
+  float* yb = e.y + bb * e.sy + pn;
+  const int64_t mb = bb * Cout * (int64_t)N + pn;  // contiguous index (mask)
 #pragma unroll
   for (int t = 0; t < TO; ++t)
 #pragma unroll
@@ -790,12 +833,16 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
       if (o < Cout) {
         const float bo = bias != nullptr ? bias[o] : 0.f;
         V v;
+        V av;
+        const bool has_add = e.add != nullptr && o < e.add_cols;
+        if (has_add) av = *reinterpret_cast<const V*>(e.add + bb * e.sa + (int64_t)o * N + pn);
 #pragma unroll
         for (int u = 0; u < SUB; ++u) {
-          float e = acc[t][u][r] + bo;
-          if (relu) e = fmaxf(e, 0.f);
-          e = relu_mask(e, mask, (yb - y) + (int64_t)o * N + u);
-          if constexpr (SUB == 1) v = e; else v[u] = e;
+          float z = lin_epi(e, acc[t][u][r] + bo, mb + (int64_t)o * N + u);
+          if (has_add) {
+            if constexpr (SUB == 1) z += av; else z += av[u];
+          }
+          if constexpr (SUB == 1) v = z; else v[u] = z;
         }
         *reinterpret_cast<V*>(yb + (int64_t)o * N) = v;
       }
@@ -810,10 +857,13 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
 constexpr int kThinMaxW = 4096;  // Cout * Cin floats in LDS
 
 template <int LAYOUT, int CINT>  // CINT: compile-time Cin (1..4), or 0 (runtime Cin, Cout <= 4)
-__global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restrict__ x, const float* __restrict__ w,
+__global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restrict__ x, int64_t sx,
+                                                          const float* __restrict__ w,
                                                           const float* __restrict__ bias, int64_t R, int N, int Cin_,
-                                                          int Cout, int transw, int relu, const float* __restrict__ mask,
-    float* __restrict__ y) {
+                                                          int Cout, int transw, LinEpi e) {
+  const int relu = e.relu;
+  const float* __restrict__ mask = e.mask;
+  float* __restrict__ y = e.y;
   __shared__ float Ws[kThinMaxW];  // Ws[o * Cin + k]
   __shared__ float bs[kLfMaxC];
   const int Cin = CINT > 0 ? CINT : Cin_;
@@ -834,35 +884,49 @@ __global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restric
     for (int u = 0; u < 4; ++u) acc[u] = o0 + u < Cout ? bs[o0 + u] : 0.f;
 #pragma unroll 4
     for (int k = 0; k < Cin; ++k) {
-      const float xv = x[r * Cin + k];
+      float xv = x[r * sx + k];
+      if (e.pre) {
+        const float s = e.pre[r * sx + k];
+        xv = xv * (s * (1.f - s));
+        if (e.pre_out && o0 == 0) e.pre_out[r * sx + k] = xv;
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (o0 + u < Cout) acc[u] = fmaf(xv, Ws[(o0 + u) * Cin + k], acc[u]);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = relu_mask(relu ? fmaxf(acc[u], 0.f) : acc[u], mask, r * Cout + o0 + u);
-    if ((Cout & 3) == 0) {
-      *reinterpret_cast<float4*>(y + r * Cout + o0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    for (int u = 0; u < 4; ++u) acc[u] = relu_mask(lin_act(relu, acc[u]), mask, r * Cout + o0 + u);
+    if ((Cout & 3) == 0 && (e.sy & 3) == 0) {
+      *reinterpret_cast<float4*>(y + r * e.sy + o0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
     } else {
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (o0 + u < Cout) y[r * Cout + o0 + u] = acc[u];
+        if (o0 + u < Cout) y[r * e.sy + o0 + u] = acc[u];
     }
   } else {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= R) return;
     const int64_t b = t / N, n = t - b * N;
-    const float* __restrict__ xb = x + b * Cin * (int64_t)N + n;
-    float* __restrict__ yb = y + b * Cout * (int64_t)N + n;
+    const float* __restrict__ xb = x + b * sx + n;
+    float* __restrict__ yb = y + b * e.sy + n;
+    const int64_t mo = b * Cout * (int64_t)N + n - (yb - y);  // mask index = (yb - y) + mo + o N
     if (CINT > 0) {  // few inputs in registers, one coalesced row store per output
       float xv[CINT > 0 ? CINT : 1];
 #pragma unroll
-      for (int k = 0; k < CINT; ++k) xv[k] = xb[(int64_t)k * N];
+      for (int k = 0; k < CINT; ++k) {
+        xv[k] = xb[(int64_t)k * N];
+        if (e.pre) {
+          const int64_t xi = (xb - x) + (int64_t)k * N;
+          const float s = e.pre[xi];
+          xv[k] = xv[k] * (s * (1.f - s));
+          if (e.pre_out) e.pre_out[xi] = xv[k];
+        }
+      }
       for (int o = 0; o < Cout; ++o) {
         float a = bs[o];
 #pragma unroll
         for (int k = 0; k < CINT; ++k) a = fmaf(xv[k], Ws[o * CINT + k], a);
-        yb[(int64_t)o * N] = relu_mask(relu ? fmaxf(a, 0.f) : a, mask, (yb - y) + (int64_t)o * N);
+        yb[(int64_t)o * N] = relu_mask(lin_act(relu, a), mask, (yb - y) + mo + (int64_t)o * N);
       }
     } else {  // Cout <= 4: one coalesced row load per input channel
       float acc[4];
@@ -870,32 +934,70 @@ __global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restric
       for (int u = 0; u < 4; ++u) acc[u] = u < Cout ? bs[u] : 0.f;
 #pragma unroll 8
       for (int k = 0; k < Cin; ++k) {
-        const float xv = xb[(int64_t)k * N];
+        float xv = xb[(int64_t)k * N];
+        if (e.pre) {
+          const int64_t xi = (xb - x) + (int64_t)k * N;
+          const float s = e.pre[xi];
+          xv = xv * (s * (1.f - s));
+          if (e.pre_out) e.pre_out[xi] = xv;
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           if (u < Cout) acc[u] = fmaf(xv, Ws[u * Cin + k], acc[u]);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (u < Cout) yb[(int64_t)u * N] = relu_mask(relu ? fmaxf(acc[u], 0.f) : acc[u], mask, (yb - y) + (int64_t)u * N);
+        if (u < Cout) yb[(int64_t)u * N] = relu_mask(lin_act(relu, acc[u]), mask, (yb - y) + mo + (int64_t)u * N);
     }
   }
 }
 
 }  // namespace
 
-extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, int layout, int64_t R, int N,
-                             int Cin, int Cout, int transw, int relu, const float* mask, float* y, void* stream) {
+extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
+  PK_REQUIRE(a != nullptr);
+  const int layout = a->layout, Cin = a->Cin, Cout = a->Cout, N = a->N;
+  const int64_t R = a->R;
   PK_REQUIRE((layout == 0 || layout == 1) && R >= 0 && Cin > 0 && Cout > 0 && Cin <= kLfMaxC && Cout <= kLfMaxC);
   PK_REQUIRE(layout == 0 || (N > 0 && R % N == 0));
+  PK_REQUIRE(a->act >= 0 && a->act <= 2);
   if (R == 0) return PK_OK;
-  PK_REQUIRE(x && w && y);
+  PK_REQUIRE(a->x && a->w && a->y);
+  const int split = a->y2 ? a->split : Cout;
+  PK_REQUIRE(split >= 1 && split <= Cout && (a->y2 == nullptr || (layout == 0 && !a->store_cf && split < Cout)));
+  PK_REQUIRE(a->store_cf == 0 || (layout == 0 && N > 0 && R % N == 0));
+  PK_REQUIRE(a->add == nullptr || (a->add_cols >= 1 && a->add_cols <= Cout));
+  // default strides: contiguous
+  const int64_t sx = a->ldx ? a->ldx : (layout == 0 ? Cin : (int64_t)Cin * N);
+  const int64_t sy = a->ldy ? a->ldy : (layout == 0 && !a->store_cf ? split : (int64_t)Cout * N);
+  LinEpi e{};
+  e.y = a->y;
+  e.sy = sy;
+  e.y2 = a->y2;
+  e.sy2 = a->ldy2 ? a->ldy2 : Cout - split;
+  e.split = split;
+  e.add = a->add;
+  e.sa = a->lda ? a->lda : (layout == 0 ? (int64_t)(a->add_cols > 0 ? a->add_cols : Cout) : (int64_t)Cout * N);
+  e.add_cols = a->add ? a->add_cols : 0;
+  e.mask = a->mask;
+  e.relu = a->act;
+  e.store_cf = a->store_cf;
+  e.N = N;
+  e.pre = a->pre;
+  e.pre_out = a->pre_out;
+  const float* x = a->x;
+  const float* w = a->w;
+  const float* bias = a->bias;
+  const int transw = a->transw;
+  hipStream_t st = pk::as_stream(stream);
+  const bool plain_out = e.y2 == nullptr && e.add == nullptr && !e.store_cf;
+  PK_REQUIRE((e.pre == nullptr && e.relu != 2) || ((Cin <= 4 || Cout <= 4) && Cin * Cout <= kThinMaxW));
   if ((Cin <= 4 || Cout <= 4) && Cin * Cout <= kThinMaxW) {
+    PK_REQUIRE(plain_out);  // the thin kernels take strides only
     const int64_t threads = layout == 0 ? R * ((Cout + 3) / 4) : R;
     const dim3 grid((unsigned)((threads + 255) / 256));
 #define PK_THIN(L, C)                                                                                           \
-  hipLaunchKernelGGL((linear_thin_kernel<L, C>), grid, dim3(256), 0, pk::as_stream(stream), x, w, bias, R, N, Cin, \
-                     Cout, transw, relu, mask, y)
+  hipLaunchKernelGGL((linear_thin_kernel<L, C>), grid, dim3(256), 0, st, x, sx, w, bias, R, N, Cin, Cout, transw, e)
     const int ct = Cin <= 4 ? Cin : 0;  // Cin > 4 here means Cout <= 4
     if (layout == 0) {
       if (ct == 1) PK_THIN(0, 1); else if (ct == 2) PK_THIN(0, 2); else if (ct == 3) PK_THIN(0, 3);
@@ -908,7 +1010,7 @@ extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, 
     PK_CHECK_LAUNCH();
     return PK_OK;
   }
-  if (layout == 0 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128)) {
+  if (layout == 0 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128) && sx % 4 == 0) {
     // 16-point tiles, 4 per block, at most two blocks per CU's worth of waves in flight
     const int64_t tiles = (R + 15) / 16;
     const unsigned blocks = (unsigned)std::min<int64_t>((tiles + 3) / 4, 512);
@@ -923,16 +1025,18 @@ extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, 
                 : Cin == 32 ? pick(std::integral_constant<int, 2>{})
                 : Cin == 64 ? pick(std::integral_constant<int, 4>{}) : pick(std::integral_constant<int, 8>{});
     const size_t lds = sizeof(float) * (size_t)(16 * TO) * (Cin + 4);
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, pk::as_stream(stream), x, w, bias, R, Cin, Cout, transw,
-                       relu, mask, y);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, st, x, sx, w, bias, R, Cin, Cout, transw, e);
     PK_CHECK_LAUNCH();
     return PK_OK;
   }
   if (layout == 1 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128) && N % 16 == 0) {
+    PK_REQUIRE(e.y2 == nullptr && !e.store_cf);
     // points per wave: 16 SUB, as many as keep >= 1024 waves and <= 64 operand VGPRs
     int sub = R >= 131072 ? 4 : R >= 32768 ? 2 : 1;
     sub = std::min(sub, 256 / Cin);
     while (N % (16 * sub)) sub >>= 1;
+    // vector loads / stores of SUB points need SUB-aligned batch strides
+    while (sub > 1 && ((sx % sub) || (e.sy % sub) || (e.add && (e.sa % sub)))) sub >>= 1;
     const int TO = Cout <= 16 ? 1 : Cout <= 32 ? 2 : Cout <= 64 ? 4 : 8;
     auto pick = [&](auto q, auto u) {
       constexpr int Q = decltype(q)::value, U = decltype(u)::value;
@@ -949,21 +1053,44 @@ extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, 
                 : sub == 2 ? pickq(std::integral_constant<int, 2>{}) : pickq(std::integral_constant<int, 1>{});
     const int64_t tiles = R / (16 * sub);
     const size_t lds = sizeof(float) * (size_t)(16 * TO) * (Cin + 4);
-    hipLaunchKernelGGL(kern, dim3((unsigned)((tiles + 3) / 4)), dim3(256), lds, pk::as_stream(stream), x, w, bias, R,
-                       N, Cout, transw, relu, mask, y);
+    hipLaunchKernelGGL(kern, dim3((unsigned)((tiles + 3) / 4)), dim3(256), lds, st, x, sx, w, bias, R, N, Cout,
+                       transw, e);
     PK_CHECK_LAUNCH();
     return PK_OK;
   }
+  // generic fallback kernel: contiguous operands only
+  PK_REQUIRE(plain_out && sx == (layout == 0 ? Cin : (int64_t)Cin * N) &&
+             e.sy == (layout == 0 ? Cout : (int64_t)Cout * N));
   const unsigned blocks = (unsigned)((R + 127) / 128);
   const size_t lds = sizeof(float) * (size_t)Cout * (((Cin + 3) & ~3) + 1);
   if (layout == 0)
-    hipLaunchKernelGGL(linear_fwd_kernel<0>, dim3(blocks), dim3(256), lds, pk::as_stream(stream), x, w, bias, R, N,
-                       Cin, Cout, transw, relu, mask, y);
+    hipLaunchKernelGGL(linear_fwd_kernel<0>, dim3(blocks), dim3(256), lds, st, x, w, bias, R, N, Cin, Cout, transw,
+                       e.relu, e.mask, e.y);
   else
-    hipLaunchKernelGGL(linear_fwd_kernel<1>, dim3(blocks), dim3(256), lds, pk::as_stream(stream), x, w, bias, R, N,
-                       Cin, Cout, transw, relu, mask, y);
+    hipLaunchKernelGGL(linear_fwd_kernel<1>, dim3(blocks), dim3(256), lds, st, x, w, bias, R, N, Cin, Cout, transw,
+                       e.relu, e.mask, e.y);
   PK_CHECK_LAUNCH();
   return PK_OK;
+}
+
+extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, int layout, int64_t R, int N,
+                             int Cin, int Cout, int transw, int relu, const float* mask, float* y, void* stream) {
+  pk_linear_args a{};
+  a.x = x;
+  a.w = w;
+  a.bias = bias;
+  a.layout = layout;
+  a.R = R;
+  a.N = N;
+  a.Cin = Cin;
+  a.Cout = Cout;
+  a.transw = transw;
+  a.act = relu ? 1 : 0;
+  a.mask = mask;
+  a.y = y;
+  a.pre = nullptr;
+  a.pre_out = nullptr;
+  return pk_linear_ex(&a, stream);
 }
 
 extern "C" int64_t pk_linear_wgrad_grouped_work(const pk_wgrad_call* calls, int n) {

@@ -19,6 +19,9 @@
 // Column pass: the same per key column o, with the softmax rows' lse from the row pass:
 //   dk_o = k_o sum_a r - sum_a r q_a  -> g2[b, idx2(o)];  block (0, b) also writes
 //   loss[b] = sum_a term[a] / max(n_valid, 1) in a fixed order (deterministic).
+// prenorm: f1 / f2 are already F.normalize'd (the overlap head's l2-normalize writes a rows
+// copy for this term): no normalization here, and g1 / g2 are the gradients with respect to
+// those normalized features (the l2-normalize backward then takes both heads' gradients).
 // Rows past a crop's pair count (valid == 0) contribute nothing; a crop without pairs has
 // loss 0 (the batched host code's clamp(min=1) convention; the reference would give NaN).
 #include "common.hpp"
@@ -57,7 +60,7 @@ template <bool COLS>
 __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
     const FeatView f1, const FeatView f2, int64_t N1, int64_t N2,
     const int64_t* __restrict__ pairs, int cap, const int64_t* __restrict__ rows,
-    const uint8_t* __restrict__ valid, int S, float inv_t, float* __restrict__ lse,
+    const uint8_t* __restrict__ valid, int S, float inv_t, int prenorm, float* __restrict__ lse,
     float* __restrict__ term, float* __restrict__ loss, float* __restrict__ g_own) {
   __shared__ float Os[kMaxS * kLdO];  // the other side's normalized vectors
   __shared__ float lse_s[kMaxS];      // COLS: softmax rows' lse
@@ -92,9 +95,9 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
     for (int c = 0; c < kC; ++c) x[c] = ok ? p[c * f_oth.sc] : 0.f;
 #pragma unroll
     for (int c = 0; c < kC; ++c) ss = fmaf(x[c], x[c], ss);
-    const float nc = fmaxf(sqrtf(ss), 1e-12f);
+    const float nc = prenorm ? 1.f : fmaxf(sqrtf(ss), 1e-12f);
 #pragma unroll
-    for (int c = 0; c < kC; ++c) Os[o * kLdO + c] = ok ? x[c] / nc : 0.f;
+    for (int c = 0; c < kC; ++c) Os[o * kLdO + c] = ok ? (prenorm ? x[c] : x[c] / nc) : 0.f;
     if (COLS) lse_s[o] = o < S ? lse[(int64_t)b * S + o] : 0.f;
   }
   // stage this block's own rows (all their dependent index / feature loads in parallel)
@@ -109,10 +112,10 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
     float ss = 0.f;
 #pragma unroll
     for (int c = 0; c < kC; ++c) ss = fmaf(x[c], x[c], ss);
-    const float nrm = sqrtf(ss);
+    const float nrm = prenorm ? 1.f : sqrtf(ss);
     const float nc = fmaxf(nrm, 1e-12f);
 #pragma unroll
-    for (int c = 0; c < kC; ++c) Ws[threadIdx.x * kLdW + c] = ok ? x[c] / nc : 0.f;
+    for (int c = 0; c < kC; ++c) Ws[threadIdx.x * kLdW + c] = ok ? (prenorm ? x[c] : x[c] / nc) : 0.f;
     wn_s[threadIdx.x] = ok ? nrm : -1.f;  // -1: invalid slot
     widx_s[threadIdx.x] = idx;
   }
@@ -280,7 +283,7 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
       const float vc = lane < kC ? Ws[(a0 + g - blockIdx.x * kTile) * kLdW + c] : 0.f;  // staged row
       const float dv = vc * rs[g] - acc[g];
       const float vdv = pk::wave_sum_f32(lane < kC ? vc * dv : 0.f);
-      const float dx = nrm[g] > 1e-12f ? (dv - vc * vdv) / nrm[g] : dv / 1e-12f;
+      const float dx = prenorm ? dv : nrm[g] > 1e-12f ? (dv - vc * vdv) / nrm[g] : dv / 1e-12f;
       if (lane < kC) atomicAdd(g_own + ((int64_t)b * N_own + idx[g]) * kC + c, dx);
     }
     __builtin_amdgcn_wave_barrier();  // all lanes done reading rbuf before the next group
@@ -292,7 +295,7 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
 extern "C" int pk_nce_loss(const float* f1, const int64_t* st1, const float* f2, const int64_t* st2, int B,
                            int64_t N1, int64_t N2, int C,
                            const int64_t* pairs, int cap, const int64_t* rows, const uint8_t* valid, int S,
-                           float nce_t, float* lse, float* term, float* loss, float* g1, float* g2,
+                           float nce_t, int prenorm, float* lse, float* term, float* loss, float* g1, float* g2,
                            void* stream) {
   PK_REQUIRE(B >= 0 && C == kC && S >= 0 && S <= kMaxS && cap >= 0 && nce_t > 0.f);
   PK_REQUIRE((g1 == nullptr) == (g2 == nullptr));
@@ -311,10 +314,10 @@ extern "C" int pk_nce_loss(const float* f1, const int64_t* st1, const float* f2,
   const FeatView v1{f1, st1 ? st1[0] : N1 * kC, st1 ? st1[1] : kC, st1 ? st1[2] : 1};
   const FeatView v2{f2, st2 ? st2[0] : N2 * kC, st2 ? st2[1] : kC, st2 ? st2[2] : 1};
   hipLaunchKernelGGL(nce_pass_kernel<false>, grid, dim3(64 * kWaves), 0, s, v1, v2, N1, N2, pairs, cap, rows, valid,
-                     S, inv_t, lse, term, loss, g1);
+                     S, inv_t, prenorm, lse, term, loss, g1);
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(nce_pass_kernel<true>, grid, dim3(64 * kWaves), 0, s, v1, v2, N1, N2, pairs, cap, rows, valid,
-                     S, inv_t, lse, term, loss, g2);
+                     S, inv_t, prenorm, lse, term, loss, g2);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -246,7 +246,8 @@ struct L2View {
 
 template <int CC>  // CC > 0: compile-time channel count (all loads in flight); 0: runtime C
 __global__ __launch_bounds__(256) void l2norm_fwd_kernel(const float* __restrict__ x, L2View v, int B, int N, int C,
-                                                         float* __restrict__ y, float* __restrict__ nrm) {
+                                                         float* __restrict__ y, float* __restrict__ nrm,
+                                                         float* __restrict__ y_rows) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)B * N) return;
   const int Cn = CC > 0 ? CC : C;
@@ -261,12 +262,17 @@ __global__ __launch_bounds__(256) void l2norm_fwd_kernel(const float* __restrict
   const float nr = sqrtf(s);
   const float d = fmaxf(nr, 1e-12f);
 #pragma unroll
-  for (int c = 0; c < Cn; ++c) y[o + c * v.sc] = x[o + c * v.sc] / d;
+  for (int c = 0; c < Cn; ++c) {
+    const float q = x[o + c * v.sc] / d;
+    y[o + c * v.sc] = q;
+    if (y_rows) y_rows[i * Cn + c] = q;  // the same values, rows layout [B, N, C]
+  }
   nrm[i] = nr;
 }
 
 template <int CC>
 __global__ __launch_bounds__(256) void l2norm_bwd_kernel(const float* __restrict__ y, const float* __restrict__ dy,
+                                                         const float* __restrict__ dy_rows,
                                                          const float* __restrict__ nrm, L2View v, int B, int N, int C,
                                                          float* __restrict__ dx) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -275,13 +281,19 @@ __global__ __launch_bounds__(256) void l2norm_bwd_kernel(const float* __restrict
   const int64_t b = i / N, n = i - b * N;
   const int64_t o = b * v.sb + n * v.sn;
   const float nr = nrm[i];
+  // the incoming gradient: dy (x's layout) + dy_rows (rows layout), either may be absent
+  auto grad = [&](int c) {
+    float g = dy ? dy[o + c * v.sc] : 0.f;
+    if (dy_rows) g += dy_rows[i * Cn + c];
+    return g;
+  };
   float yd = 0.f;
 #pragma unroll
-  for (int c = 0; c < Cn; ++c) yd += y[o + c * v.sc] * dy[o + c * v.sc];
+  for (int c = 0; c < Cn; ++c) yd += y[o + c * v.sc] * grad(c);
   const bool clamped = !(nr > 1e-12f);
 #pragma unroll
   for (int c = 0; c < Cn; ++c) {
-    const float g = dy[o + c * v.sc];
+    const float g = grad(c);
     dx[o + c * v.sc] = clamped ? g / 1e-12f : (g - y[o + c * v.sc] * yd) / nr;
   }
 }
@@ -289,27 +301,33 @@ __global__ __launch_bounds__(256) void l2norm_bwd_kernel(const float* __restrict
 }  // namespace
 
 extern "C" int pk_l2_normalize_fwd(const float* x, const int64_t* strides, int B, int N, int C, float* y, float* nrm,
-                                   void* stream) {
+                                   float* y_rows, void* stream) {
   PK_REQUIRE(B >= 0 && N >= 0 && C > 0 && strides);
   if ((int64_t)B * N == 0) return PK_OK;
   PK_REQUIRE(x && y && nrm);
   const L2View v{strides[0], strides[1], strides[2]};
   const dim3 grid((unsigned)(((int64_t)B * N + 255) / 256));
-  if (C == 32) hipLaunchKernelGGL(l2norm_fwd_kernel<32>, grid, dim3(256), 0, pk::as_stream(stream), x, v, B, N, C, y, nrm);
-  else hipLaunchKernelGGL(l2norm_fwd_kernel<0>, grid, dim3(256), 0, pk::as_stream(stream), x, v, B, N, C, y, nrm);
+  if (C == 32)
+    hipLaunchKernelGGL(l2norm_fwd_kernel<32>, grid, dim3(256), 0, pk::as_stream(stream), x, v, B, N, C, y, nrm, y_rows);
+  else
+    hipLaunchKernelGGL(l2norm_fwd_kernel<0>, grid, dim3(256), 0, pk::as_stream(stream), x, v, B, N, C, y, nrm, y_rows);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
 
 extern "C" int pk_l2_normalize_bwd(const float* y, const float* dy, const float* nrm, const int64_t* strides, int B,
-                                   int N, int C, float* dx, void* stream) {
+                                   int N, int C, float* dx, const float* dy_rows, void* stream) {
   PK_REQUIRE(B >= 0 && N >= 0 && C > 0 && strides);
   if ((int64_t)B * N == 0) return PK_OK;
-  PK_REQUIRE(y && dy && nrm && dx);
+  PK_REQUIRE(y && (dy || dy_rows) && nrm && dx);
   const L2View v{strides[0], strides[1], strides[2]};
   const dim3 grid((unsigned)(((int64_t)B * N + 255) / 256));
-  if (C == 32) hipLaunchKernelGGL(l2norm_bwd_kernel<32>, grid, dim3(256), 0, pk::as_stream(stream), y, dy, nrm, v, B, N, C, dx);
-  else hipLaunchKernelGGL(l2norm_bwd_kernel<0>, grid, dim3(256), 0, pk::as_stream(stream), y, dy, nrm, v, B, N, C, dx);
+  if (C == 32)
+    hipLaunchKernelGGL(l2norm_bwd_kernel<32>, grid, dim3(256), 0, pk::as_stream(stream), y, dy, dy_rows, nrm, v, B, N,
+                       C, dx);
+  else
+    hipLaunchKernelGGL(l2norm_bwd_kernel<0>, grid, dim3(256), 0, pk::as_stream(stream), y, dy, dy_rows, nrm, v, B, N,
+                       C, dx);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

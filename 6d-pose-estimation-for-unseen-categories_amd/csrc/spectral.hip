@@ -127,7 +127,7 @@ __global__ __launch_bounds__(1024) void spec_combine_kernel(float* __restrict__ 
 __global__ __launch_bounds__(256) void spec_expand_kernel(const float* __restrict__ evecs,
                                                           const float* __restrict__ coef,
                                                           const float* __restrict__ mass, int N,
-                                                          float* __restrict__ y, int ldy,
+                                                          float* __restrict__ y, int ldy, int accumulate,
                                                           const float* __restrict__ gtb, int64_t gt_stride,
                                                           float* __restrict__ gt) {
   __shared__ float4 scoef[kKC][kKC / 4];
@@ -172,8 +172,13 @@ __global__ __launch_bounds__(256) void spec_expand_kernel(const float* __restric
     if (r >= N) continue;
     float w = 1.f;
     if (mass) w = mass[(int64_t)b * N + r];
-    reinterpret_cast<float4*>(y + ((int64_t)b * N + r) * ldy)[tx] =
-        make_float4(acc[i][0] * w, acc[i][1] * w, acc[i][2] * w, acc[i][3] * w);
+    float4* yp = reinterpret_cast<float4*>(y + ((int64_t)b * N + r) * ldy) + tx;
+    float4 v = make_float4(acc[i][0] * w, acc[i][1] * w, acc[i][2] * w, acc[i][3] * w);
+    if (accumulate) {
+      const float4 o = *yp;
+      v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+    }
+    *yp = v;
   }
 }
 
@@ -185,7 +190,7 @@ __global__ __launch_bounds__(256) void spec_expand_kernel(const float* __restric
 extern "C" int pk_spectral_diffusion(const float* in, int ld_in, const float* mass, const float* evecs,
                                      const float* evals, float* t, int clamp_t, int B, int N, int K, int C,
                                      int mode, float* work, float* raw, float* scaled, const float* saved,
-                                     float* gt, float* out, int ld_out, void* stream) {
+                                     float* gt, float* out, int ld_out, int accumulate, void* stream) {
   PK_REQUIRE(B >= 0 && N >= 0 && K == kKC && C == kKC && (mode == 0 || mode == 1));
   PK_REQUIRE(ld_in >= C && ld_out >= C && ld_in % 4 == 0 && ld_out % 4 == 0);
   if (B == 0 || N == 0) return PK_OK;
@@ -200,7 +205,7 @@ extern "C" int pk_spectral_diffusion(const float* in, int ld_in, const float* ma
                      (int)(clamp_t && mode == 0), raw, scaled, mode == 1 ? saved : nullptr, (int)(mode == 1));
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(spec_expand_kernel, dim3((N + 63) / 64, B), dim3(256), 0, s, evecs, scaled,
-                     mode == 1 ? mass : nullptr, N, out, ld_out, work, (int64_t)S * kKC * kKC,
+                     mode == 1 ? mass : nullptr, N, out, ld_out, accumulate, work, (int64_t)S * kKC * kKC,
                      mode == 1 ? gt : nullptr);
   PK_CHECK_LAUNCH();
   return PK_OK;

@@ -22,6 +22,17 @@ _U64 = ctypes.c_uint64
 _D = ctypes.c_double
 _F = ctypes.c_float
 
+
+
+class LinearArgs(ctypes.Structure):
+    """pk_linear_args (include/posekern.h)."""
+    _fields_ = [("x", _P), ("w", _P), ("bias", _P), ("layout", ctypes.c_int32), ("N", ctypes.c_int32),
+                ("R", _I64), ("Cin", ctypes.c_int32), ("Cout", ctypes.c_int32), ("transw", ctypes.c_int32),
+                ("act", ctypes.c_int32), ("mask", _P), ("ldx", _I64), ("y", _P), ("ldy", _I64), ("y2", _P),
+                ("ldy2", _I64), ("split", ctypes.c_int32), ("store_cf", ctypes.c_int32), ("add", _P), ("lda", _I64),
+                ("add_cols", ctypes.c_int32), ("pad", ctypes.c_int32), ("pre", _P), ("pre_out", _P)]
+
+
 # name -> argtypes, mirroring include/posekern.h one for one.
 SIGNATURES = {
     "pk_fps": [_P, _P, _I, _I, _P, _P, _P, _I, _P],
@@ -34,7 +45,11 @@ SIGNATURES = {
     "pk_collate_pad": [_P, _I, _I, _P, _I, _I, _P, _P, _P],
     "pk_segment_scan": [_P, _I, _I, _P, _P, _P],
     "pk_offsets_from_counts": [_P, _I, _P, _P],
-    "pk_spectral_diffusion": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P],
+    "pk_spectral_diffusion": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _P],
+    "pk_linear_ex": [_P, _P],
+    "pk_fmap_head_fwd": [_P, _I, _P, _P, _P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _F, _P, _P, _P, _P,
+                         _P, _P],
+    "pk_fmap_head_bwd": [_P, _P, _P, _P, _P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "pk_fmap_solve": [_P, _P, _P, _F, _I, _I, _P, _P],
     "pk_fmap_solve_backward": [_P, _P, _P, _F, _I, _I, _P, _P, _P, _P],
     "pk_attention_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P],
@@ -42,7 +57,7 @@ SIGNATURES = {
     "pk_linear_wgrad": [_P, _P, _I, _I64, _I, _I, _I, _P, _P, _P, _I, _P],
     "pk_linear_wgrad_grouped_work": [_P, _I],
     "pk_linear_wgrad_grouped": [_P, _I, _P, _I64, _P],
-    "pk_nce_loss": [_P, _P, _P, _P, _I, _I64, _I64, _I, _P, _I, _P, _P, _I, _F, _P, _P, _P, _P, _P, _P],
+    "pk_nce_loss": [_P, _P, _P, _P, _I, _I64, _I64, _I, _P, _I, _P, _P, _I, _F, _I, _P, _P, _P, _P, _P, _P],
     "pk_affine_cat": [_P, _I64, _P, _I64, _F, _F, _P, _P],
     "pk_loss_head": [_P, _P, _I, _I, _P, _P, _F, _F, _F, _P, _P, _P, _P],
     "pk_loss_scale": [_P, _P, _P, _P, _I, _P, _P],
@@ -50,8 +65,8 @@ SIGNATURES = {
     "pk_instnorm_relu_fwd": [_P, _I64, _I, _F, _P, _P, _P, _P],
     "pk_instnorm_relu_bwd": [_P, _P, _P, _P, _I64, _I, _P, _P],
     "pk_wbce": [_P, _P, _I, _P, _P, _I, _I, _P, _P, _P, _P],
-    "pk_l2_normalize_fwd": [_P, _P, _I, _I, _I, _P, _P, _P],
-    "pk_l2_normalize_bwd": [_P, _P, _P, _P, _I, _I, _I, _P, _P],
+    "pk_l2_normalize_fwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P],
+    "pk_l2_normalize_bwd": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P],
     "pk_mlp3_fwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P],
     "pk_resolvent_mask": [_P, _I, _P, _I, _I, _I, _F, _P, _P],
     "pk_linear_fwd": [_P, _P, _P, _I, _I64, _I, _I, _I, _I, _I, _P, _P, _P],

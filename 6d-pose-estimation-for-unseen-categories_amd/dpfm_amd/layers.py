@@ -100,16 +100,27 @@ class _PointwiseFn(torch.autograd.Function):
     reference's transposes (modeling/dpfm.py:90-91, 113-116) cost no copies."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, cf, relu, in_relu):
+    def forward(ctx, x, weight, bias, cf, relu, in_relu, sigmoid=False):
         w2 = weight.view(weight.shape[0], -1)
-        ctx.has_bias, ctx.cf, ctx.relu = bias is not None, cf, relu
+        ctx.has_bias, ctx.cf, ctx.relu, ctx.sigmoid = bias is not None, cf, relu, sigmoid
         ctx.param, ctx.bias = weight, bias  # the Parameter objects (GroupedWgrad's buffer keys)
         # a fresh (non-view) output: the reference applies in-place ReLUs to it (:112-116);
-        # relu=True applies the following nn.ReLU in the kernel's epilogue instead
-        y = ops.linear_fwd(x, w2, bias, channels_first=cf, relu=relu)
+        # relu=True applies the following nn.ReLU in the kernel's epilogue instead, sigmoid=True
+        # the following nn.Sigmoid (the overlap head's last layer, modeling/dpfm.py:132-137)
+        if sigmoid:
+            Cout, Cin = w2.shape
+            if cf:
+                Bn, _, N = x.shape
+                y = torch.empty((Bn, Cout, N), dtype=x.dtype, device=x.device)
+                ops.linear_ex(x, w2, bias, 1, Bn * N, N, Cin, Cout, y=y, act=2)
+            else:
+                y = torch.empty(x.shape[:-1] + (Cout,), dtype=x.dtype, device=x.device)
+                ops.linear_ex(x, w2, bias, 0, x.numel() // Cin, 0, Cin, Cout, y=y, act=2)
+        else:
+            y = ops.linear_fwd(x, w2, bias, channels_first=cf, relu=relu)
         # this layer's input gradient can apply the ReLU backward of the layer that produced x
         ctx.in_relu = FOLD_RELU and in_relu
-        ctx.save_for_backward(x, weight, y if relu else None)
+        ctx.save_for_backward(x, weight, y if (relu or sigmoid) else None)
         return y
 
     @staticmethod
@@ -123,7 +134,23 @@ class _PointwiseFn(torch.autograd.Function):
             # unless the consuming layer already applied it in its input-gradient epilogue
             dy = torch.ops.aten.threshold_backward(dy, y, 0.0)
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
+        if ctx.sigmoid:
+            # the sigmoid's backward dy y (1 - y) folded into the input gradient's prologue, the
+            # scaled dy written out for the weight gradient (pk_linear_ex pre / pre_out)
+            Cout, Cin = w2.shape
+            dz = torch.empty_like(dy)
+            dx = torch.empty_like(x)
+            if cf:
+                Bn, _, N = x.shape
+                ops.linear_ex(dy, w2, None, 1, Bn * N, N, Cout, Cin, y=dx, transw=True,
+                              mask=x if ctx.in_relu else None, pre=y, pre_out=dz)
+            else:
+                ops.linear_ex(dy, w2, None, 0, dy.numel() // Cout, 0, Cout, Cin, y=dx, transw=True,
+                              mask=x if ctx.in_relu else None, pre=y, pre_out=dz)
+            if ctx.in_relu:
+                _MASKED.add((dx.data_ptr(), x.data_ptr()))
+            dy = dz
+        elif ctx.needs_input_grad[0]:
             # dy W (rows) / W^T dy (cf); with in_relu the producer's ReLU backward is folded in
             dx = ops.linear_fwd(dy, w2, None, channels_first=cf, transw=True, mask=x if ctx.in_relu else None)
             if ctx.in_relu:
@@ -134,10 +161,11 @@ class _PointwiseFn(torch.autograd.Function):
             else:
                 dw, db = ops.linear_wgrad(x, dy, channels_first=cf, want_bias=ctx.has_bias)
                 dw = dw.view(weight.shape)
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
-def _pointwise(x, weight, bias, sem_cf: bool, out_cf: Optional[bool] = None, relu: bool = False):
+def _pointwise(x, weight, bias, sem_cf: bool, out_cf: Optional[bool] = None, relu: bool = False,
+               sigmoid: bool = False):
     """Apply the layer to x of semantic layout sem_cf (False: [..., C]; True: [B, C, N]).
     out_cf: force the output storage layout (None: the native layout of the input)."""
     if not x.is_cuda:
@@ -147,7 +175,7 @@ def _pointwise(x, weight, bias, sem_cf: bool, out_cf: Optional[bool] = None, rel
     else:
         base, native_cf = x.contiguous(), sem_cf
     in_relu = getattr(x, "_pk_relu_out", False)
-    y = _PointwiseFn.apply(base, weight, bias, native_cf, relu, in_relu)
+    y = _PointwiseFn.apply(base, weight, bias, native_cf, relu, in_relu, sigmoid)
     if out_cf is not None and out_cf != native_cf and y.dim() == 3:
         y = y.transpose(1, 2).contiguous().transpose(1, 2)  # same values, other storage order
     out = y if native_cf == sem_cf else y.transpose(1, 2)
@@ -163,9 +191,12 @@ class Linear(nn.Linear):
     holding that ReLU is then an nn.Identity, so state_dict keys are unchanged)."""
     out_cf: Optional[bool] = None
     relu_out: bool = False
+    sigmoid_out: bool = False  # the following nn.Sigmoid in the epilogue (thin layers, Cout <= 4)
 
     def forward(self, x):
-        return _pointwise(x, self.weight, self.bias, sem_cf=False, out_cf=self.out_cf, relu=self.relu_out)
+        sig = self.sigmoid_out and (self.out_features <= 4 or self.in_features <= 4)
+        y = _pointwise(x, self.weight, self.bias, sem_cf=False, out_cf=self.out_cf, relu=self.relu_out, sigmoid=sig)
+        return torch.sigmoid(y) if (self.sigmoid_out and not sig) else y
 
 
 class Conv1d(nn.Conv1d):

@@ -131,14 +131,23 @@ class OverlapPredictorNet(nn.Module):
             Linear(overlap_feat_dim, overlap_feat_dim, bias=True),
             nn.Identity(),  # the reference's nn.ReLU(True), applied in layer 0's epilogue
             Linear(overlap_feat_dim, 1, bias=True),
-            nn.Sigmoid(),
+            nn.Identity(),  # the reference's nn.Sigmoid(), applied in layer 2's epilogue
         )
         self.overlap_score_net[0].relu_out = True
+        self.overlap_score_net[2].sigmoid_out = True
 
     def forward(self, overlap_feat_x, overlap_feat_y):
-        # F.normalize(., p=2, dim=-1) (modeling/dpfm.py:140-141), fused, storage order kept
-        nx = ops.l2_normalize(overlap_feat_x) if overlap_feat_x.dim() == 3 else F.normalize(overlap_feat_x, p=2, dim=-1)
-        ny = ops.l2_normalize(overlap_feat_y) if overlap_feat_y.dim() == 3 else F.normalize(overlap_feat_y, p=2, dim=-1)
+        # F.normalize(., p=2, dim=-1) (modeling/dpfm.py:140-141), fused, storage order kept; a rows
+        # copy of the normalized features is attached to the input for the loss's NCE term
+        # (the same normalization, utils/loss.py:23-24), which then reads whole rows
+        nx = ny = None
+        if (torch.is_grad_enabled() and overlap_feat_x.dim() == 3 and overlap_feat_x.is_cuda
+                and overlap_feat_x.shape[-1] == 32):
+            nx, overlap_feat_x._pk_nrows = ops.l2_normalize_two(overlap_feat_x)
+            ny, overlap_feat_y._pk_nrows = ops.l2_normalize_two(overlap_feat_y)
+        if nx is None:
+            nx = ops.l2_normalize(overlap_feat_x) if overlap_feat_x.dim() == 3 else F.normalize(overlap_feat_x, p=2, dim=-1)
+            ny = ops.l2_normalize(overlap_feat_y) if overlap_feat_y.dim() == 3 else F.normalize(overlap_feat_y, p=2, dim=-1)
         sx = self.overlap_score_net(nx).squeeze(2).squeeze(0)
         sy = self.overlap_score_net(ny).squeeze(2).squeeze(0)
         return sx, sy

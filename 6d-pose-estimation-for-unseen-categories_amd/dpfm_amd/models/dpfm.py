@@ -8,6 +8,8 @@ ref_feat1, ref_feat2). state_dict keys equal weights/weights.pt.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -77,6 +79,13 @@ class DPFMNet(nn.Module):
         use_feat1, use_feat2 = (ref_feat1, ref_feat2) if self.robust else (feat1, feat2)
 
         k = self.n_fmap
+        if (evecs1.dim() == 3 and evecs1.is_cuda and k == 30 and use_feat1.shape[-1] == 32
+                and os.environ.get("PK_FUSED_FMAP_HEAD", "1") == "1"):
+            # models/dpfm.py:66-72 + RegularizedFMNet (modeling/dpfm.py:154-195) fused: the
+            # projections, AAt / BAt, the resolvent mask and the solve in two launches
+            C_pred = ops.fmap_head(use_feat1, use_feat2, evecs1, evecs2, mass1, mass2, evals1, evals2,
+                                   self.fmreg_net.lambda_, self.fmreg_net.resolvant_gamma)
+            return C_pred, overlap_score12, overlap_score21, use_feat1, use_feat2, ref_feat1, ref_feat2
         if evecs1.dim() == 3:  # models/dpfm.py:66-72, batched instead of a loop over crops
             evecs_trans1 = (evecs1[:, :, :k] * mass1[:, :, None]).transpose(1, 2)
             evecs_trans2 = (evecs2[:, :, :k] * mass2[:, :, None]).transpose(1, 2)

@@ -229,7 +229,7 @@ class _SpectralDiffusion(torch.autograd.Function):
         scaled = torch.empty_like(spec)
         out = torch.empty((B, N, C), dtype=torch.float32, device=dev)
         call("pk_spectral_diffusion", ptr(x), int(x.stride(1)), ptr(mass), ptr(evecs), ptr(evals), ptr(t),
-             int(clamp_t), B, N, K, C, 0, ptr(work), ptr(spec), ptr(scaled), None, None, ptr(out), C,
+             int(clamp_t), B, N, K, C, 0, ptr(work), ptr(spec), ptr(scaled), None, None, ptr(out), C, 0,
              _lib.stream(dev), work=("hbm", 16 * B * N * 64))  # Phi read twice + x in + y out, f32
         ctx.save_for_backward(mass, evals, evecs, t, spec)
         ctx.clamp_t = clamp_t
@@ -248,7 +248,7 @@ class _SpectralDiffusion(torch.autograd.Function):
         gt = torch.empty((C,), dtype=torch.float32, device=dev)
         gx = torch.empty_like(g)
         call("pk_spectral_diffusion", ptr(g), C, ptr(mass), ptr(evecs), ptr(evals), ptr(t), int(ctx.clamp_t), B, N,
-             K, C, 1, ptr(work), None, ptr(scaled), ptr(spec), ptr(gt), ptr(gx), C, _lib.stream(dev),
+             K, C, 1, ptr(work), None, ptr(scaled), ptr(spec), ptr(gt), ptr(gx), C, 0, _lib.stream(dev),
              work=("hbm", 16 * B * N * 64))
         return gx, None, None, None, gt, None
 
@@ -304,6 +304,67 @@ def resolvent_mask(evals1: torch.Tensor, evals2: torch.Tensor, gamma: float = 0.
          ctypes.c_void_p(evals2.data_ptr()), int(evals2.stride(0)), B, K, float(gamma), ptr(D),
          _lib.stream(evals1.device))
     return D
+
+
+class _FmapHeadFn(torch.autograd.Function):
+    """RegularizedFMNet.forward's batched branch (modeling/dpfm.py:154-195) from the refined
+    features to C: pk_fmap_head_fwd (projections, AAt, BAt, the resolvent mask) + pk_fmap_solve;
+    backward pk_fmap_solve_backward + pk_fmap_head_bwd, whose expansion writes the feature
+    gradients in the features' own storage order."""
+
+    @staticmethod
+    def forward(ctx, fx, fy, evecs_x, evecs_y, mass_x, mass_y, evals_x, evals_y, lambda_, gamma):
+        import ctypes
+        B, N1, Cf = fx.shape
+        N2 = fy.shape[1]
+        dev = fx.device
+        K = 30
+        st = lambda t: (ctypes.c_int64 * 3)(*t.stride())  # noqa: E731
+        A = torch.empty((B, K, Cf), dtype=torch.float32, device=dev)
+        Bm = torch.empty_like(A)
+        AAt = torch.empty((B, K, K), dtype=torch.float32, device=dev)
+        BAt = torch.empty_like(AAt)
+        D = torch.empty_like(AAt)
+        call("pk_fmap_head_fwd", ptr(evecs_x), int(evecs_x.shape[-1]), ptr(mass_x), ctypes.c_void_p(fx.data_ptr()),
+             st(fx), int(N1), ptr(evecs_y), int(evecs_y.shape[-1]), ptr(mass_y), ctypes.c_void_p(fy.data_ptr()),
+             st(fy), int(N2), ctypes.c_void_p(evals_x.data_ptr()), int(evals_x.stride(0)),
+             ctypes.c_void_p(evals_y.data_ptr()), int(evals_y.stride(0)), B, K, Cf, float(gamma), ptr(A), ptr(Bm),
+             ptr(AAt), ptr(BAt), ptr(D), _lib.stream(dev), work=None)
+        Cm = torch.empty_like(BAt)
+        call("pk_fmap_solve", ptr(AAt), ptr(BAt), ptr(D), float(lambda_), B, K, ptr(Cm), _lib.stream(dev))
+        ctx.save_for_backward(evecs_x, evecs_y, mass_x, mass_y, A, Bm, AAt, BAt, D)
+        ctx.lambda_ = float(lambda_)
+        ctx.fshape = (tuple(fx.shape), tuple(fx.stride()), tuple(fy.shape), tuple(fy.stride()))
+        return Cm
+
+    @staticmethod
+    def backward(ctx, G):
+        import ctypes
+        evecs_x, evecs_y, mass_x, mass_y, A, Bm, AAt, BAt, D = ctx.saved_tensors
+        G = G.contiguous()
+        B, K, _ = AAt.shape
+        dev = G.device
+        dBAt = torch.empty_like(BAt)
+        part = torch.empty((B, K, K, K), dtype=torch.float32, device=dev)
+        call("pk_fmap_solve_backward", ptr(AAt), ptr(BAt), ptr(D), ctx.lambda_, B, K, ptr(G), ptr(dBAt), ptr(part),
+             _lib.stream(dev))
+        (sx, tx, sy, ty) = ctx.fshape
+        dfx = torch.empty_strided(sx, tx, dtype=torch.float32, device=dev)  # the features' storage order
+        dfy = torch.empty_strided(sy, ty, dtype=torch.float32, device=dev)
+        dA, dBm = torch.empty_like(A), torch.empty_like(Bm)
+        st = lambda t: (ctypes.c_int64 * 3)(*t.stride())  # noqa: E731
+        call("pk_fmap_head_bwd", ptr(part), ptr(dBAt), ptr(A), ptr(Bm), ptr(evecs_x), int(evecs_x.shape[-1]),
+             ptr(mass_x), int(sx[1]), ptr(evecs_y), int(evecs_y.shape[-1]), ptr(mass_y), int(sy[1]), B, K, A.shape[2],
+             ptr(dA), ptr(dBm), ctypes.c_void_p(dfx.data_ptr()), st(dfx), ctypes.c_void_p(dfy.data_ptr()), st(dfy),
+             _lib.stream(dev))
+        return dfx, dfy, None, None, None, None, None, None, None, None
+
+
+def fmap_head(fx, fy, evecs_x, evecs_y, mass_x, mass_y, evals_x, evals_y, lambda_: float, gamma: float):
+    """C from the refined features (RegularizedFMNet with evecs_trans = (evecs[..., :30] *
+    mass).T), fused: fx [B, N1, 32], fy [B, N2, 32] in rows or channels-first storage."""
+    return _FmapHeadFn.apply(fx, fy, evecs_x.contiguous(), evecs_y.contiguous(), mass_x.contiguous(),
+                             mass_y.contiguous(), evals_x, evals_y, float(lambda_), float(gamma))
 
 
 def fmap_solve(AAt: torch.Tensor, BAt: torch.Tensor, D: torch.Tensor, lambda_: float) -> torch.Tensor:
@@ -519,7 +580,7 @@ class _L2Normalize(torch.autograd.Function):
         y = torch.empty_strided(x.shape, x.stride(), dtype=x.dtype, device=x.device)
         nrm = torch.empty((B * N,), dtype=torch.float32, device=x.device)
         _, st = _l2_layout(x)
-        call("pk_l2_normalize_fwd", ctypes_ptr(x), st, B, N, C, ctypes_ptr(y), ptr(nrm), _lib.stream(x.device),
+        call("pk_l2_normalize_fwd", ctypes_ptr(x), st, B, N, C, ctypes_ptr(y), ptr(nrm), None, _lib.stream(x.device),
              work=("hbm", 8 * B * N * C))
         ctx.save_for_backward(y, nrm)
         return y
@@ -532,7 +593,7 @@ class _L2Normalize(torch.autograd.Function):
             dy = torch.empty_strided(y.shape, y.stride(), dtype=dy.dtype, device=dy.device).copy_(dy)
         dx = torch.empty_strided(y.shape, y.stride(), dtype=y.dtype, device=y.device)
         _, st = _l2_layout(y)
-        call("pk_l2_normalize_bwd", ctypes_ptr(y), ctypes_ptr(dy), ptr(nrm), st, B, N, C, ctypes_ptr(dx),
+        call("pk_l2_normalize_bwd", ctypes_ptr(y), ctypes_ptr(dy), ptr(nrm), st, B, N, C, ctypes_ptr(dx), None,
              _lib.stream(y.device), work=("hbm", 12 * B * N * C))
         return dx
 
@@ -543,6 +604,45 @@ def ctypes_ptr(t: torch.Tensor):
     if not t.is_cuda:
         raise _lib.PoseKernError("posekern ops take HIP device tensors only (no CPU fallback)")
     return ctypes.c_void_p(t.data_ptr())
+
+
+class _L2NormalizeTwo(torch.autograd.Function):
+    """F.normalize(x, dim=-1) returned twice: in x's storage order and as a rows [B, N, C]
+    copy (one launch); the backward takes both incoming gradients in one launch."""
+
+    @staticmethod
+    def forward(ctx, x):
+        B, N, C = x.shape
+        y = torch.empty_strided(x.shape, x.stride(), dtype=x.dtype, device=x.device)
+        y_rows = torch.empty((B, N, C), dtype=x.dtype, device=x.device)
+        nrm = torch.empty((B * N,), dtype=torch.float32, device=x.device)
+        _, st = _l2_layout(x)
+        call("pk_l2_normalize_fwd", ctypes_ptr(x), st, B, N, C, ctypes_ptr(y), ptr(nrm), ptr(y_rows),
+             _lib.stream(x.device), work=("hbm", 12 * B * N * C))
+        ctx.save_for_backward(y, nrm)
+        return y, y_rows
+
+    @staticmethod
+    def backward(ctx, dy, dy_rows):
+        y, nrm = ctx.saved_tensors
+        B, N, C = y.shape
+        if dy is not None and dy.stride() != y.stride():
+            dy = torch.empty_strided(y.shape, y.stride(), dtype=dy.dtype, device=dy.device).copy_(dy)
+        if dy_rows is not None:
+            dy_rows = dy_rows.contiguous()
+        dx = torch.empty_strided(y.shape, y.stride(), dtype=y.dtype, device=y.device)
+        _, st = _l2_layout(y)
+        call("pk_l2_normalize_bwd", ctypes_ptr(y), ctypes_ptr(dy) if dy is not None else None, ptr(nrm), st, B, N, C,
+             ctypes_ptr(dx), ptr(dy_rows), _lib.stream(y.device), work=("hbm", 16 * B * N * C))
+        return dx
+
+
+def l2_normalize_two(x: torch.Tensor):
+    """(F.normalize(x, dim=-1) in x's storage order, the same as a contiguous rows copy)."""
+    if x.dim() != 3 or x.dtype != torch.float32:
+        raise _lib.PoseKernError("l2_normalize takes f32 [B, N, C]")
+    x, _ = _l2_layout(x)
+    return _L2NormalizeTwo.apply(x)
 
 
 def l2_normalize(x: torch.Tensor) -> torch.Tensor:
@@ -597,6 +697,52 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], c
          int(relu), ptr(mask), ptr(y), _lib.stream(x.device),
          work=("hbm", 4 * int(R) * (Cin + Cout) + 4 * Cin * Cout, 2 * int(R) * Cin * Cout))
     return y
+
+
+def _dp(t: Optional[torch.Tensor]) -> Optional[int]:
+    """Device address of a (possibly strided) tensor view, or None."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise _lib.PoseKernError("posekern ops take HIP device tensors only (no CPU fallback)")
+    return t.data_ptr()
+
+
+def linear_ex(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], layout: int, R: int, N: int,
+              Cin: int, Cout: int, y: torch.Tensor, ldx: int = 0, ldy: int = 0, transw: bool = False,
+              relu: bool = False, mask: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None,
+              split: int = 0, ldy2: int = 0, store_cf: bool = False, add: Optional[torch.Tensor] = None,
+              lda: int = 0, add_cols: int = 0, act: Optional[int] = None, pre: Optional[torch.Tensor] = None,
+              pre_out: Optional[torch.Tensor] = None) -> None:
+    """pk_linear_ex: a per-point layer writing into caller-placed (strided) outputs with a
+    residual / accumulation epilogue. x, y, y2, add are the first elements of their (possibly
+    strided) operands; strides as in include/posekern.h (0 = contiguous)."""
+    a = _lib.LinearArgs(x=_dp(x), w=_dp(w.contiguous()), bias=_dp(bias), layout=int(layout), N=int(N), R=int(R),
+                        Cin=int(Cin), Cout=int(Cout), transw=int(transw), act=int(relu) if act is None else int(act),
+                        mask=_dp(mask),
+                        ldx=int(ldx), y=_dp(y), ldy=int(ldy), y2=_dp(y2), ldy2=int(ldy2), split=int(split),
+                        store_cf=int(store_cf), add=_dp(add), lda=int(lda), add_cols=int(add_cols), pre=_dp(pre),
+                        pre_out=_dp(pre_out))
+    import ctypes
+    call("pk_linear_ex", ctypes.addressof(a), _lib.stream(x.device),
+         work=("hbm", 4 * int(R) * (Cin + Cout) + 4 * Cin * Cout, 2 * int(R) * Cin * Cout))
+
+
+def spectral_raw(x: torch.Tensor, ld_in: int, mass, evals, evecs, t, clamp_t: bool, mode: int, out: torch.Tensor,
+                 ld_out: int, saved=None, gt=None, accumulate: bool = False, want_raw: bool = True):
+    """pk_spectral_diffusion on caller-placed rows (row strides ld_in / ld_out): returns the
+    spectral coefficients (mode 0, for the backward) or None."""
+    B, N = mass.shape[0], mass.shape[1]
+    K = evecs.shape[-1]
+    dev = mass.device
+    S = (N + 63) // 64
+    work = torch.empty((B, S, K, 64), dtype=torch.float32, device=dev)
+    scaled = torch.empty((B, K, 64), dtype=torch.float32, device=dev)
+    raw = torch.empty((B, K, 64), dtype=torch.float32, device=dev) if (mode == 0 and want_raw) else None
+    call("pk_spectral_diffusion", _dp(x), int(ld_in), ptr(mass), ptr(evecs), ptr(evals), ptr(t), int(clamp_t), B, N,
+         K, 64, int(mode), ptr(work), ptr(raw), ptr(scaled), ptr(saved), ptr(gt), _dp(out), int(ld_out),
+         int(accumulate), _lib.stream(dev), work=("hbm", 16 * B * N * 64))
+    return raw
 
 
 # ------------------------------------------------------------------------------ H10-H13, H15
@@ -662,7 +808,7 @@ class _NCELoss(torch.autograd.Function):
         g1 = torch.empty((B, N1, C), dtype=torch.float32, device=dev) if want else None
         g2 = torch.empty((B, N2, C), dtype=torch.float32, device=dev) if want else None
         call("pk_nce_loss", ctypes.c_void_p(f1c.data_ptr()), st(f1c), ctypes.c_void_p(f2c.data_ptr()), st(f2c), B, int(N1), int(N2), int(C), ptr(pairs), int(pairs.shape[1]),
-             ptr(rows), ptr(valid), int(S), float(nce_t), ptr(lse), ptr(term), ptr(loss), ptr(g1), ptr(g2),
+             ptr(rows), ptr(valid), int(S), float(nce_t), 0, ptr(lse), ptr(term), ptr(loss), ptr(g1), ptr(g2),
              _lib.stream(dev), work=None)
         ctx.save_for_backward(g1, g2)
         return loss
@@ -699,8 +845,9 @@ def affine_cat(a: torch.Tensor, b: torch.Tensor, sub: float, div: float) -> torc
     return out
 
 
-def _nce_raw(f1, f2, pairs, rows, valid, nce_t, want):
-    """pk_nce_loss: (loss [B], g1, g2) with g the gradients of each crop's loss (None unless want)."""
+def _nce_raw(f1, f2, pairs, rows, valid, nce_t, want, prenorm=False):
+    """pk_nce_loss: (loss [B], g1, g2) with g the gradients of each crop's loss (None unless
+    want); prenorm: f1 / f2 already normalized, g with respect to them."""
     import ctypes
     B, N1, C = f1.shape
     N2 = f2.shape[1]
@@ -719,7 +866,7 @@ def _nce_raw(f1, f2, pairs, rows, valid, nce_t, want):
     g2 = torch.empty((B, N2, C), dtype=torch.float32, device=dev) if want else None
     call("pk_nce_loss", ctypes.c_void_p(f1c.data_ptr()), st(f1c), ctypes.c_void_p(f2c.data_ptr()), st(f2c), B,
          int(N1), int(N2), int(C), ptr(pairs), int(pairs.shape[1]), ptr(rows), ptr(valid), int(S), float(nce_t),
-         ptr(lse), ptr(term), ptr(loss), ptr(g1), ptr(g2), _lib.stream(dev), work=None)
+         int(prenorm), ptr(lse), ptr(term), ptr(loss), ptr(g1), ptr(g2), _lib.stream(dev), work=None)
     return loss, g1, g2
 
 
@@ -729,12 +876,12 @@ class _DPFMLossFn(torch.autograd.Function):
     weights, sums, dloss/dC12); the backward is one grouped scale (pk_loss_scale)."""
 
     @staticmethod
-    def forward(ctx, C12, f1, f2, o12, o21, C_gt, pairs, rows, valid, t12, t21, w, nce_t):
+    def forward(ctx, C12, f1, f2, o12, o21, C_gt, pairs, rows, valid, t12, t21, w, nce_t, prenorm):
         w_fmap, w_acc, w_nce = w
         want = any(ctx.needs_input_grad[:5])
         B, K = C12.shape[0], C12.shape[1]
         dev = C12.device
-        nce, g1, g2 = _nce_raw(f1, f2, pairs, rows, valid, nce_t, want)
+        nce, g1, g2 = _nce_raw(f1, f2, pairs, rows, valid, nce_t, want, prenorm)
         N1, N2 = o12.shape[1], o21.shape[1]
         wb = torch.empty((2, B), dtype=torch.float32, device=dev)
         g12 = torch.empty_like(o12) if want else None
@@ -764,7 +911,7 @@ class _DPFMLossFn(torch.autograd.Function):
                  (ctypes.c_int64 * len(sel))(*[saved[i].numel() for i in sel]),
                  (ctypes.c_float * len(sel))(*[ctx.scales[i] for i in sel]), len(sel), ptr(gl.contiguous()),
                  _lib.stream(gl.device), work=None)
-        return (*outs, None, None, None, None, None, None, None, None)
+        return (*outs, None, None, None, None, None, None, None, None, None)
 
 
 def dpfm_loss(C12, C_gt, f1, f2, pairs, rows, valid, o12, o21, t12, t21, w_fmap: float, w_acc: float,
@@ -774,9 +921,17 @@ def dpfm_loss(C12, C_gt, f1, f2, pairs, rows, valid, o12, o21, t12, t21, w_fmap:
         return (t if t.dtype == torch.int8 else (t >= 0.5).to(torch.int8)).contiguous()
     if f1.dtype != torch.float32 or f1.shape[-1] != 32:
         raise _lib.PoseKernError("pk_nce_loss takes f32 features of width 32")
+    # features whose F.normalize'd rows copy the overlap head already made (l2_normalize_two):
+    # the NCE term reads those rows (coalesced) and its gradient joins the overlap head's in
+    # the one l2-normalize backward
+    n1, n2 = getattr(f1, "_pk_nrows", None), getattr(f2, "_pk_nrows", None)
+    prenorm = n1 is not None and n2 is not None
+    if prenorm:
+        f1, f2 = n1, n2
     return _DPFMLossFn.apply(C12.contiguous(), f1, f2, o12.contiguous(), o21.contiguous(), C_gt.contiguous(),
                              pairs.contiguous(), rows.contiguous(), valid.contiguous().view(torch.uint8),
-                             mask(t12), mask(t21), (float(w_fmap), float(w_acc), float(w_nce)), float(nce_t))
+                             mask(t12), mask(t21), (float(w_fmap), float(w_acc), float(w_nce)), float(nce_t),
+                             bool(prenorm))
 
 
 def rigidity_thresholds(diam: Sequence[float], device) -> torch.Tensor:

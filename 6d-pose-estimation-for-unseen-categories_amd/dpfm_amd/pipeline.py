@@ -435,7 +435,9 @@ class PipelinedTrainer:
                  warmup: int = 3):
         self.step, self.split = step, step.world > 1
         self.main = torch.cuda.current_stream()
-        self.side = torch.cuda.Stream()
+        # crop-formation stream priority (development knob PK_SIDE_PRIORITY: torch's stream
+        # priorities, lower number = higher priority; default 0, the main stream's)
+        self.side = torch.cuda.Stream(priority=int(os.environ.get("PK_SIDE_PRIORITY", "0")))
         side = torch.cuda.Stream()
         side.wait_stream(self.main)
         with torch.cuda.stream(side):  # warm-up outside capture

@@ -188,6 +188,63 @@ def cpu_baseline(n_crops: int, n1: int, n2: int) -> dict:
             "seconds": round(dt, 2)}
 
 
+def cpu_infer_baseline(n_crops: int, n1: int, n2: int, H: int) -> dict:
+    """configs[1] inference on the host, per crop (scripts/eval.py:57-119 + test_RANSAC.py:
+    397-419 restated by oracle/): crop formation, DPFMNet forward (torch-CPU fp32), the
+    spatial-filtering solver (top-5 + three rigidity rounds), IR, the Open3D-shaped RANSAC
+    (oracle/c oc_ransac_o3d, H hypotheses, C/OpenMP) and the ADD metric."""
+    import ctypes
+    from oracle import dpfm_oracle as O
+    from oracle import dpfm_model_oracle as M
+    from dpfm_amd.dataset.synthetic import make_frame, cad_points, lbo_operators
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
+    torch.set_num_threads(threads)
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "liboracle.so"))
+    P = ctypes.c_void_p
+    lib.oc_ransac_o3d.argtypes = [P, ctypes.c_int, P, P, ctypes.c_int, P, ctypes.c_uint64, ctypes.c_int64,
+                                  ctypes.c_double, P, P]
+    cp = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    model = M.DPFMNet().eval()
+    t0 = time.perf_counter()
+    for c in range(-1, n_crops):  # crop -1: untimed warm-up
+        if c == 0:
+            t0 = time.perf_counter()
+        cs = c % 10_000
+        fr = make_frame(20_000 + cs)
+        pcd = O.dpt_2_pcld(fr.depth, 1000 / fr.depth_scale, fr.K, fr.mask == 255)
+        pcd = O.remove_outliers(pcd)
+        idx = O.farthest_point_sample(torch.Tensor(pcd).t(), ratio=n2 / pcd.shape[0], start=0, npoint=n2)
+        pcd = pcd[idx.numpy()]
+        align = O.transform(pcd, fr.R_m2c, fr.t_m2c, inv=True)
+        cad = cad_points(fr, n1, cs)
+        cm, ce, cv = lbo_operators(n1, 64, 2 * cs)
+        pm, pe, pv = lbo_operators(n2, 64, 2 * cs + 1)
+        T = lambda a: torch.from_numpy(np.asarray(a, dtype=np.float32))[None]  # noqa: E731
+        batch = {"shape1": {"xyz": T(cad), "mass": T(cm), "evals": T(ce), "evecs": T(cv)},
+                 "shape2": {"xyz": T(pcd), "mass": T(pm), "evals": T(pe), "evecs": T(pv)}}
+        with torch.no_grad():
+            C = model(batch)[0]
+            corr = O.spacial_filtering_fmap2pointmap(C[0], batch["shape1"]["evecs"][0, :, :30],
+                                                     batch["shape2"]["evecs"][0, :, :30], T(cad)[0], T(pcd)[0],
+                                                     fr.diam_cad)
+            O.compute_inlier_ratio(corr.t().long(), T(cad)[0], T(align)[0], 0.1 * fr.diam_cad)
+        cor = np.ascontiguousarray(corr.t().numpy().astype(np.int32))
+        Tm, st = np.zeros(16), np.zeros(3)
+        cad64, pc64 = np.ascontiguousarray(cad, dtype=np.float64), np.ascontiguousarray(pcd, dtype=np.float64)
+        if cor.shape[0] >= 4:
+            lib.oc_ransac_o3d(cp(cad64), n1, cp(pc64), cp(cor), cor.shape[0], None, 0, H, 0.05, cp(Tm), cp(st))
+        Tgt = np.eye(4)
+        Tgt[:3, :3], Tgt[:3, 3] = fr.R_m2c, fr.t_m2c
+        O.add(Tm.reshape(4, 4), Tgt, cad, fr.diam_cad)
+    dt = time.perf_counter() - t0
+    return {"value": round(n_crops / dt, 4), "unit": "crops/s (inference incl. crop formation and RANSAC)",
+            "cores": threads, "kind": "port",
+            "sample": f"{n_crops} crops after 1 warm-up, {n2} pts, CAD {n1}, RANSAC {H} hypotheses; oracle/ (numpy + "
+                      "torch-CPU fp32, C/OpenMP RANSAC)",
+            "seconds": round(dt, 2)}
+
+
 TRAIN_METRIC = "RGB-D crops/sec (fwd+bwd), 1024 pts, at 1/2/4/8 MI355X; pose err vs ref"
 INFER_METRIC = ("RGB-D crops/sec (inference: crop formation + DPFM fwd + spatial-filter solver + IR + "
                 "RANSAC 1024 hyp + pose metrics)")
@@ -415,6 +472,9 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(args.cpu_crops, args.points, args.points)
             elif args.mode == "corr4096":
                 out["cpu_baseline"] = cpu_ransac_baseline(args.hypotheses)
+            elif args.mode == "infer":
+                out["cpu_baseline"] = cpu_infer_baseline(max(1, args.cpu_crops // 3), args.points, args.points,
+                                                         args.hypotheses)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

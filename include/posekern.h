@@ -131,10 +131,12 @@ int pk_offsets_from_counts(const int64_t* counts, int B, int64_t* off, void* str
  *   clamp_t: use max(t, 1e-8), and in mode 0 write it back into t (the reference's in-place
  *   diffusion_time.clamp_(min=1e-8) before every diffusion);
  *   work f32 [B, ceil(N/64), K, C]; raw (mode 0, may be NULL) / scaled [B,K,C];
- *   saved = raw of the forward (mode 1); gt [C] (mode 1, summed over crops in crop order) */
+ *   saved = raw of the forward (mode 1); gt [C] (mode 1, summed over crops in crop order);
+ *   accumulate: out += result (a gradient summed into an existing one) instead of out = result */
 int pk_spectral_diffusion(const float* in, int ld_in, const float* mass, const float* evecs, const float* evals,
                           float* t, int clamp_t, int B, int N, int K, int C, int mode, float* work, float* raw,
-                          float* scaled, const float* saved, float* gt, float* out, int ld_out, void* stream);
+                          float* scaled, const float* saved, float* gt, float* out, int ld_out, int accumulate,
+                          void* stream);
 
 /* H9 regularized fmap solve. Replaces the 30 sequential torch.inverse + bmm of
  * modeling/dpfm.py:185-193: C[b,i,:] = ((AAt_b + lambda diag(D_b[i,:]))^-1 BAt_b[i,:]^T)^T.
@@ -226,11 +228,14 @@ int pk_affine_cat(const float* a, int64_t na, const float* b, int64_t nb, float 
 /* F.normalize(x, p=2, dim=-1) over the C channels of [B, N, C] features (overlap head,
  * modeling/dpfm.py:140-145), forward and backward. strides = HOST int64[3] element strides
  * {batch, point, channel} shared by x / y / dy / dx (rows or channels-first storage);
- * nrm f32 [B * N] = ||x|| per point (saved by the forward for the backward). */
+ * nrm f32 [B * N] = ||x|| per point (saved by the forward for the backward).
+ * y_rows (may be NULL): the same normalized values also in rows layout [B, N, C] (the NCE
+ * term's gathers read whole rows, utils/loss.py:17-40); dy_rows (may be NULL; dy may be NULL
+ * when it is given): a second incoming gradient in rows layout, summed with dy. */
 int pk_l2_normalize_fwd(const float* x, const int64_t* strides, int B, int N, int C, float* y, float* nrm,
-                        void* stream);
+                        float* y_rows, void* stream);
 int pk_l2_normalize_bwd(const float* y, const float* dy, const float* nrm, const int64_t* strides, int B, int N,
-                        int C, float* dx, void* stream);
+                        int C, float* dx, const float* dy_rows, void* stream);
 
 /* H7 DiffusionNet block MLP forward, fused (upstream DiffusionNetBlock.forward at
  * models/dpfm.py:22-30: mlp(cat[x_in, x_diffuse]) + x_in, MiniMLP 128 -> 64 -> ReLU -> 64 ->
@@ -240,6 +245,24 @@ int pk_l2_normalize_bwd(const float* y, const float* dy, const float* nrm, const
 int pk_mlp3_fwd(const float* x_in, const float* x_diff, const float* w1, const float* b1, const float* w2,
                 const float* b2, const float* w3, const float* b3, int64_t R, int C, float* cat, float* h1, float* h2,
                 float* y, void* stream);
+
+/* H9 fmap head around the solve (modeling/dpfm.py:154-176, models/dpfm.py:66-72), K = 30,
+ * C = 32: W = evecs[:, :K] * mass (f32 products); A = W_x^T F_x, Bm = W_y^T F_y [B,K,C];
+ * AAt = A A^T, BAt = Bm A^T [B,K,K]; D = get_mask(evals_x[:K], evals_y[:K], gamma) [B,K,K].
+ *   evecs f32 [B,N,lde], mass f32 [B,N], F (refined features [B,N,C]) at HOST int64[3]
+ *   element strides {batch, point, channel}; evals f32 [B, ldv].
+ * Backward: part = pk_fmap_solve_backward's dAAt slabs [B,K,K,K], dBAt [B,K,K] ->
+ *   dA, dBm [B,K,C] (scratch outputs) and dF_x = W_x dA, dF_y = W_y dBm written at the
+ *   HOST strides dfx_strides / dfy_strides. */
+int pk_fmap_head_fwd(const float* evecs_x, int ldex, const float* mass_x, const float* fx, const int64_t* fx_strides,
+                     int N1, const float* evecs_y, int ldey, const float* mass_y, const float* fy,
+                     const int64_t* fy_strides, int N2, const float* evals_x, int ldvx, const float* evals_y, int ldvy,
+                     int B, int K, int C, float gamma, float* A, float* Bm, float* AAt, float* BAt, float* D,
+                     void* stream);
+int pk_fmap_head_bwd(const float* part, const float* dBAt, const float* A, const float* Bm, const float* evecs_x,
+                     int ldex, const float* mass_x, int N1, const float* evecs_y, int ldey, const float* mass_y, int N2,
+                     int B, int K, int C, float* dA, float* dBm, float* dfx, const int64_t* dfx_strides, float* dfy,
+                     const int64_t* dfy_strides, void* stream);
 
 /* H9 resolvent mask: upstream dpfm/utils.py::get_mask(evals1[:K], evals2[:K], gamma) for every
  * crop (the per-crop branch that always runs, modeling/dpfm.py:164-182). evals1 / evals2 f32
@@ -258,6 +281,43 @@ int pk_resolvent_mask(const float* evals1, int ld1, const float* evals2, int ld2
  *   feeding this one, folded into its input gradient (mask = that layer's output). */
 int pk_linear_fwd(const float* x, const float* w, const float* bias, int layout, int64_t R, int N, int Cin,
                   int Cout, int transw, int relu, const float* mask, float* y, void* stream);
+
+/* pk_linear_fwd with explicit output placement and epilogue (one launch where torch would
+ * add concatenations, residual adds, slices and transposed copies around the layer):
+ *   ldx: rows layout — x row stride; channels-first — x batch stride (0: contiguous);
+ *   y / ldy: output (same stride meaning; 0: contiguous);
+ *   store_cf (rows layout): y written channels-first [R/N, Cout, N] (ldy = its batch stride);
+ *   y2 / split / ldy2 (rows layout): output columns >= split go to y2 at column - split;
+ *   add / lda / add_cols: y[.., o] += add[.., o] for o < add_cols, after bias / ReLU / mask
+ *   (residual connections, gradient accumulation of a split input);
+ *   act: 0 none, 1 ReLU, 2 sigmoid (thin kernels); mask: contiguous [R, Cout] / [R/N, Cout, N]
+ *   (see pk_linear_fwd);
+ *   pre / pre_out (thin kernels): the input is first scaled elementwise by pre (1 - pre) —
+ *   a following sigmoid's backward (pre = its output) folded into the input gradient — and
+ *   the scaled input written to pre_out (for the weight gradient), same indexing as x.
+ * The thin kernels (Cin or Cout <= 4) take strides only. */
+typedef struct pk_linear_args {
+  const float* x;
+  const float* w;
+  const float* bias;
+  int32_t layout;
+  int32_t N;
+  int64_t R;
+  int32_t Cin, Cout, transw, act;
+  const float* mask;
+  int64_t ldx;
+  float* y;
+  int64_t ldy;
+  float* y2;
+  int64_t ldy2;
+  int32_t split, store_cf;
+  const float* add;
+  int64_t lda;
+  int32_t add_cols, pad;
+  const float* pre;
+  float* pre_out;
+} pk_linear_args;
+int pk_linear_ex(const pk_linear_args* a, void* stream);
 
 /* H10 / H11 correspondence head. Replaces fmap2pointmap_solvers/naive.py:20-34
  * (topk = 1: dist.argmin(dim=-2)) and spacial_filtering.py:19-38 (topk = 5: the first 5
@@ -317,11 +377,13 @@ int pk_nce_select(const int64_t* count, int B, int64_t cap, int num, uint64_t se
  * channels-first [B, C, N] storage is read in place;
  * S <= 512. lse / term f32 [B, S] scratch. g1 / g2 (both or neither) f32 [B, N1|N2, C]
  * receive d loss[b] / d f1[b], f2[b] (zero-filled, then accumulated with f32 atomics,
- * as torch's gather backward). */
+ * as torch's gather backward).  * prenorm = 1: f1 / f2 are already F.normalize'd; g1 / g2 are then the gradients with
+ * respect to the normalized features (no normalize backward).
+ */
 int pk_nce_loss(const float* f1, const int64_t* st1, const float* f2, const int64_t* st2, int B, int64_t N1,
                 int64_t N2, int C, const int64_t* pairs,
-                int cap, const int64_t* rows, const uint8_t* valid, int S, float nce_t, float* lse, float* term,
-                float* loss, float* g1, float* g2, void* stream);
+                int cap, const int64_t* rows, const uint8_t* valid, int S, float nce_t, int prenorm, float* lse,
+                float* term, float* loss, float* g1, float* g2, void* stream);
 
 /* H15 DPFMLoss scalar head (utils/loss.py:44-99, FrobeniusLoss :8-15), one launch:
  *   fmap = w_fmap * mean_b clamp(sum (C12_b - Cgt_b)^2, -1, 1000); nce = sum_b nce[b] w_nce / B;

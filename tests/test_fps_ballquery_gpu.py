@@ -16,7 +16,7 @@ def _packed(arrs, dtype, device):
 
 
 @pytest.mark.parametrize("sizes,grid", [
-    ([1, 7, 100, 1024, 2049, 4500, 9000, 13000, 14000], False),  # > 13312: unpruned, global reads
+    ([1, 7, 100, 1024, 2049, 4500, 9000, 13000, 14000, 20000, 26000], False),  # > 13312: per-lane buckets, plain
     ([1, 7, 100, 1024, 2049, 4500, 9000, 13000], False),         # pruned buckets, random order
     ([500, 3000, 8000, 13312], True),                             # pruned, spatially coherent runs
 ])

@@ -438,10 +438,11 @@ def test_resolvent_mask_matches_get_mask(device):
         assert (D[b] - ref).abs().max().item() <= 1e-6 * ref.abs().max().item() + 1e-12
 
 
-def test_relu_backward_folded_into_dgrad(device):
+def test_relu_backward_folded_into_dgrad(device, monkeypatch):
     """The fused ReLU's backward folded into the next layer's input-gradient epilogue
     (pk_linear_fwd mask) gives the same DiffusionNet input and parameter gradients, bit for
     bit, as applying aten threshold_backward separately."""
+    monkeypatch.setenv("PK_FUSED_ENCODER", "0")  # the per-module path is the one that folds
     from dpfm_amd import layers
     from dpfm_amd.diffusion_net import DiffusionNet
     torch.manual_seed(6)
@@ -461,3 +462,104 @@ def test_relu_backward_folded_into_dgrad(device):
     layers.FOLD_RELU = True
     for a, c in zip(res[True], res[False]):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("B,N", [(3, 256), (2, 333)])
+def test_fused_encoder_matches_module_path(device, B, N, monkeypatch):
+    """The DiffusionNet encoder as one autograd node (_EncoderFn: concatenation-free blocks,
+    residual adds and split input gradients in the layer epilogues, diffusion backward
+    accumulated in place) against the per-module path (PK_FUSED_ENCODER=0) on the same
+    weights: forward bit-identical (same kernels and per-element arithmetic), gradients of
+    every parameter within 2e-5 of their scale (only the order of the residual / diffusion
+    gradient sums differs)."""
+    from dpfm_amd.models.dpfm import DPFMNet
+    torch.manual_seed(11)
+    net = DPFMNet().feature_extractor.to(device)
+    b = _to(_inputs(B, N, N, seed=3), device)["shape1"]
+    x = ((b["xyz"] - 110) / 50).contiguous()
+    g = torch.randn(B, N, 32, device=device)
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PK_FUSED_ENCODER", mode)
+        net.zero_grad(set_to_none=True)
+        for blk in net.blocks:  # above the clamp: both paths see the same diffusion times
+            blk.diffusion.diffusion_time.data.copy_(torch.linspace(0.01, 2.0, 64, device=device))
+        y = net(x, b["mass"], evals=b["evals"], evecs=b["evecs"])
+        (y * g).sum().backward()
+        res[mode] = (y.detach().clone(), {k: p.grad.detach().clone() for k, p in net.named_parameters()})
+    assert torch.equal(res["1"][0], res["0"][0])
+    for k, g0 in res["0"][1].items():
+        g1 = res["1"][1][k]
+        scale = float(g0.abs().max()) + 1e-30
+        assert (g1 - g0).abs().max().item() <= 2e-5 * scale, (k, (g1 - g0).abs().max().item(), scale)
+
+
+def test_nce_on_prenormalized_rows_matches_raw(device):
+    """The NCE term fed the overlap head's F.normalize'd rows copy (ops.l2_normalize_two,
+    pk_nce_loss prenorm = 1, its gradient joining the l2-normalize backward) against the term
+    normalizing the raw channels-first features itself: same loss and feature gradients
+    within f32 rounding of the two norm evaluations (1e-5 of scale)."""
+    from dpfm_amd import ops
+    from dpfm_amd.utils.loss import DPFMLoss
+    g = torch.Generator().manual_seed(12)
+    B, N1, N2 = 3, 300, 260
+    counts = [700, 40, 512]
+    cap = max(counts)
+    pairs = torch.zeros((B, cap, 2), dtype=torch.int64)
+    for b, c in enumerate(counts):
+        flat = torch.randperm(N1 * N2, generator=g)[:c]
+        pairs[b, :c, 0], pairs[b, :c, 1] = flat // N2, flat % N2
+    f1 = torch.randn(B, 32, N1, generator=g).to(device).transpose(1, 2)  # channels-first storage
+    f2 = torch.randn(B, 32, N2, generator=g).to(device).transpose(1, 2)
+    C = torch.randn(B, 30, 30, generator=g).to(device)
+    C_gt = torch.randn(B, 30, 30, generator=g).to(device)
+    o12 = (torch.rand(B, N1, generator=g) * 0.9 + 0.05).to(device)
+    o21 = (torch.rand(B, N2, generator=g) * 0.9 + 0.05).to(device)
+    t12 = (torch.rand(B, N1, generator=g) < 0.5).to(torch.int8).to(device)
+    t21 = (torch.rand(B, N2, generator=g) < 0.5).to(torch.int8).to(device)
+    npairs = torch.tensor(counts, device=device)
+    ctr = torch.zeros(1, dtype=torch.int64, device=device)
+    rows, valid = ops.nce_select(npairs, cap, 512, 3, ctr)
+    crit = DPFMLoss(w_fmap=1, w_acc=1, w_nce=1, nce_t=0.07, nce_num_pairs=512)
+    res = []
+    for pre in (False, True):
+        a1, a2 = f1.detach().clone().requires_grad_(True), f2.detach().clone().requires_grad_(True)
+        if pre:
+            _, a1._pk_nrows = ops.l2_normalize_two(a1)
+            _, a2._pk_nrows = ops.l2_normalize_two(a2)
+        loss, _ = crit.forward_batched(C, C_gt, pairs.to(device), npairs, a1, a2, o12, o21, t12, t21,
+                                       selection=(rows, valid))
+        loss.backward()
+        res.append((float(loss), a1.grad.clone(), a2.grad.clone()))
+    assert abs(res[0][0] - res[1][0]) <= 1e-5 * abs(res[0][0])
+    for k in (1, 2):
+        scale = float(res[0][k].abs().max())
+        assert (res[0][k] - res[1][k]).abs().max().item() <= 1e-5 * scale, k
+
+
+@pytest.mark.parametrize("N1,N2", [(256, 256), (300, 200)])
+def test_fused_fmap_head_matches_module_path(device, N1, N2, monkeypatch):
+    """DPFMNet with the fused fmap head (pk_fmap_head_fwd / _bwd around the solve) against
+    the module path (evecs_trans products, batched GEMMs, resolvent mask, solve) on the same
+    weights and inputs: C_pred within 1e-4 of its scale and every parameter gradient within
+    1e-4 of its scale (f32 summation order of the projections differs)."""
+    from dpfm_amd.models.dpfm import DPFMNet
+    torch.manual_seed(21)
+    net = DPFMNet().to(device)
+    b = _to(_inputs(2, N1, N2, seed=5), device)
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PK_FUSED_FMAP_HEAD", mode)
+        net.zero_grad(set_to_none=True)
+        C = net(b)[0]
+        g = torch.linspace(-1, 1, C.numel(), device=device).view_as(C)
+        (C * g).sum().backward()
+        res[mode] = (C.detach().clone(), {k: p.grad.detach().clone() for k, p in net.named_parameters()
+                                          if p.grad is not None})
+    sc = float(res["0"][0].abs().max())
+    assert (res["1"][0] - res["0"][0]).abs().max().item() <= 1e-4 * sc
+    assert res["1"][1].keys() == res["0"][1].keys()
+    for k, g0 in res["0"][1].items():
+        g1 = res["1"][1][k]
+        scale = float(g0.abs().max()) + 1e-30
+        assert (g1 - g0).abs().max().item() <= 1e-4 * scale, (k, (g1 - g0).abs().max().item(), scale)
