@@ -175,33 +175,6 @@ __device__ __forceinline__ double sqdist(double ax, double ay, double az, const 
 // top-knn values are exactly those of a full brute-force search.
 constexpr int kSorMaxBox = 1024;
 
-// pixel offsets {du, dv} of the 17 x 17 window in order of increasing pixel distance
-__constant__ int8_t kSpiral[289][2] = {
-    {0, 0}, {0, -1}, {-1, 0}, {1, 0}, {0, 1}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}, {0, -2}, {-2, 0}, {2, 0},
-    {0, 2}, {-1, -2}, {1, -2}, {-2, -1}, {2, -1}, {-2, 1}, {2, 1}, {-1, 2}, {1, 2}, {-2, -2}, {2, -2}, {-2, 2},
-    {2, 2}, {0, -3}, {-3, 0}, {3, 0}, {0, 3}, {-1, -3}, {1, -3}, {-3, -1}, {3, -1}, {-3, 1}, {3, 1}, {-1, 3},
-    {1, 3}, {-2, -3}, {2, -3}, {-3, -2}, {3, -2}, {-3, 2}, {3, 2}, {-2, 3}, {2, 3}, {0, -4}, {-4, 0}, {4, 0},
-    {0, 4}, {-1, -4}, {1, -4}, {-4, -1}, {4, -1}, {-4, 1}, {4, 1}, {-1, 4}, {1, 4}, {-3, -3}, {3, -3}, {-3, 3},
-    {3, 3}, {-2, -4}, {2, -4}, {-4, -2}, {4, -2}, {-4, 2}, {4, 2}, {-2, 4}, {2, 4}, {0, -5}, {-3, -4}, {3, -4},
-    {-4, -3}, {4, -3}, {-5, 0}, {5, 0}, {-4, 3}, {4, 3}, {-3, 4}, {3, 4}, {0, 5}, {-1, -5}, {1, -5}, {-5, -1},
-    {5, -1}, {-5, 1}, {5, 1}, {-1, 5}, {1, 5}, {-2, -5}, {2, -5}, {-5, -2}, {5, -2}, {-5, 2}, {5, 2}, {-2, 5},
-    {2, 5}, {-4, -4}, {4, -4}, {-4, 4}, {4, 4}, {-3, -5}, {3, -5}, {-5, -3}, {5, -3}, {-5, 3}, {5, 3}, {-3, 5},
-    {3, 5}, {0, -6}, {-6, 0}, {6, 0}, {0, 6}, {-1, -6}, {1, -6}, {-6, -1}, {6, -1}, {-6, 1}, {6, 1}, {-1, 6},
-    {1, 6}, {-2, -6}, {2, -6}, {-6, -2}, {6, -2}, {-6, 2}, {6, 2}, {-2, 6}, {2, 6}, {-4, -5}, {4, -5}, {-5, -4},
-    {5, -4}, {-5, 4}, {5, 4}, {-4, 5}, {4, 5}, {-3, -6}, {3, -6}, {-6, -3}, {6, -3}, {-6, 3}, {6, 3}, {-3, 6},
-    {3, 6}, {0, -7}, {-7, 0}, {7, 0}, {0, 7}, {-1, -7}, {1, -7}, {-5, -5}, {5, -5}, {-7, -1}, {7, -1}, {-7, 1},
-    {7, 1}, {-5, 5}, {5, 5}, {-1, 7}, {1, 7}, {-4, -6}, {4, -6}, {-6, -4}, {6, -4}, {-6, 4}, {6, 4}, {-4, 6},
-    {4, 6}, {-2, -7}, {2, -7}, {-7, -2}, {7, -2}, {-7, 2}, {7, 2}, {-2, 7}, {2, 7}, {-3, -7}, {3, -7}, {-7, -3},
-    {7, -3}, {-7, 3}, {7, 3}, {-3, 7}, {3, 7}, {-5, -6}, {5, -6}, {-6, -5}, {6, -5}, {-6, 5}, {6, 5}, {-5, 6},
-    {5, 6}, {0, -8}, {-8, 0}, {8, 0}, {0, 8}, {-1, -8}, {1, -8}, {-4, -7}, {4, -7}, {-7, -4}, {7, -4}, {-8, -1},
-    {8, -1}, {-8, 1}, {8, 1}, {-7, 4}, {7, 4}, {-4, 7}, {4, 7}, {-1, 8}, {1, 8}, {-2, -8}, {2, -8}, {-8, -2},
-    {8, -2}, {-8, 2}, {8, 2}, {-2, 8}, {2, 8}, {-6, -6}, {6, -6}, {-6, 6}, {6, 6}, {-3, -8}, {3, -8}, {-8, -3},
-    {8, -3}, {-8, 3}, {8, 3}, {-3, 8}, {3, 8}, {-5, -7}, {5, -7}, {-7, -5}, {7, -5}, {-7, 5}, {7, 5}, {-5, 7},
-    {5, 7}, {-4, -8}, {4, -8}, {-8, -4}, {8, -4}, {-8, 4}, {8, 4}, {-4, 8}, {4, 8}, {-6, -7}, {6, -7}, {-7, -6},
-    {7, -6}, {-7, 6}, {7, 6}, {-6, 7}, {6, 7}, {-5, -8}, {5, -8}, {-8, -5}, {8, -5}, {-8, 5}, {8, 5}, {-5, 8},
-    {5, 8}, {-7, -7}, {7, -7}, {-7, 7}, {7, 7}, {-6, -8}, {6, -8}, {-8, -6}, {8, -6}, {-8, 6}, {8, 6}, {-6, 8},
-    {6, 8}, {-7, -8}, {7, -8}, {-8, -7}, {8, -7}, {-8, 7}, {8, 7}, {-7, 8}, {7, 8}, {-8, -8}, {8, -8}, {-8, 8},
-    {8, 8}};
 
 __global__ __launch_bounds__(kSorThreads) void sor_knn_kernel(const double* __restrict__ xyz,
                                                               const int64_t* __restrict__ off, int knn,
@@ -234,20 +207,27 @@ __global__ __launch_bounds__(kSorThreads) void sor_knn_kernel(const double* __re
     const int pp = pix[base + i];
     const int v = pp / W, u = pp % W;
     const int32_t* im = idxmap + (int64_t)b * H * W;
-    // T = the largest distance to the first kk crop points met walking the window outward
-    // (nearest pixels first): kk actual points lie within sqrt(T), so T bounds the kk-th
-    // nearest neighbour distance (no sorting; the box pass below finds the exact set)
     int found = 0;
-    double tmax = 0.0;
-    for (int c = 0; c < 289 && found < kk; ++c) {
-      const int uu = u + kSpiral[c][0], vv = v + kSpiral[c][1];
-      if (uu < 0 || uu >= W || vv < 0 || vv >= H) continue;
-      const int j = im[vv * W + uu];
-      if (j < 0) continue;
-      tmax = fmax(tmax, sqdist(q0, q1, q2, p + 3 * j));
-      ++found;
+    for (int R = 2; R <= 8; R *= 2) {  // 5x5, then 9x9, 17x17 near the mask border
+      found = 0;
+#pragma unroll
+      for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
+      for (int vv = max(v - R, 0); vv <= min(v + R, H - 1); ++vv) {
+        const int32_t* row = im + vv * W;
+        for (int uu = max(u - R, 0); uu <= min(u + R, W - 1); ++uu) {
+          const int j = row[uu];
+          if (j < 0) continue;
+          topk_insert(best, sqdist(q0, q1, q2, p + 3 * j));
+          ++found;
+        }
+      }
+      if (found >= kk) break;
     }
-    if (found >= kk) T = tmax;
+    if (found >= kk) {
+#pragma unroll
+      for (int k = 0; k < kKnn; ++k)
+        if (k == kk - 1) T = best[k];  // static register index (no scratch)
+    }
 #pragma unroll
     for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
     if (Kmat != nullptr && T < __builtin_huge_val()) {

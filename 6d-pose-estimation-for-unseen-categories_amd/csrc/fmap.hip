@@ -186,80 +186,96 @@ extern "C" int pk_resolvent_mask(const float* evals1, int ld1, const float* eval
 //   W = evecs[:, :K] * mass (f32 products, the reference's evecs_trans before its transpose)
 //   A = W_x^T F_x, Bm = W_y^T F_y            [K, C] per crop (F = refined features [N, C])
 //   AAt = A A^T, BAt = Bm A^T, D = get_mask(evals_x, evals_y)   -> pk_fmap_solve
-// Forward in one launch per batch (one workgroup per crop: W and F staged through LDS in
-// 64-point chunks, each thread two outputs of A / Bm, then the K x K products and the mask);
+// Forward in two launches: 128-point chunks of both sides spread over the chip (W and F staged
+// through LDS, the chunk's 30 x 32 partial product into a work buffer), then one workgroup per
+// crop sums the partials in chunk order and forms the K x K products and the mask;
 // backward in two: the K x C gradients of A and Bm (dAAt = the solve backward's per-row slabs
 // summed in row order), then dF = (W dA) / (W dBm) per point, written straight into the
 // caller's feature-gradient layout. Replaces the evecs * mass products, four batched GEMMs,
 // the mask launch and, backward, six GEMMs, the slab sum and the gradient additions.
 namespace {
 
-constexpr int kHK = 30, kHC = 32, kHChunk = 64;
+constexpr int kHK = 30, kHC = 32;
 
 struct FeatRef {  // element (b, n, c) at base + b * sb + n * sn + c * sc
   const float* base;
   int64_t sb, sn, sc;
 };
 
-__device__ __forceinline__ void head_project(const float* __restrict__ ev, int lde, const float* __restrict__ mass,
-                                             const FeatRef f, int b, int N, float (*Ws)[kHK + 1],
-                                             float (*Fs)[kHC + 1], float (*out)[kHC + 1]) {
-  const int tid = threadIdx.x;
-  const int k = tid >> 4, c = (tid & 15) * 2;  // threads < 480: outputs (k, c), (k, c + 1)
-  float a0 = 0.f, a1 = 0.f;
-  for (int n0 = 0; n0 < N; n0 += kHChunk) {
-    const int m = min(kHChunk, N - n0);
-    __syncthreads();
-    for (int e = tid; e < kHChunk * kHK; e += blockDim.x) {
-      const int r = e / kHK, kk = e - r * kHK;
-      float v = 0.f;
-      if (r < m) {
-        const int64_t n = (int64_t)b * N + n0 + r;
-        v = ev[n * lde + kk] * mass[n];  // f32 product, as evecs[:, :, :k] * mass[:, :, None]
-      }
-      Ws[r][kk] = v;
+constexpr int kPChunk = 128;  // points per partial-projection workgroup
+constexpr int kLdF = kHC + 4;  // 16-B aligned feature rows in LDS
+
+// grid (ceil(N1 / 128) + ceil(N2 / 128), B), block 256: the 30 x 32 partial product W^T F of
+// one 128-point chunk of one side -> part[b, p] (p < P_x: x side chunk p, else y side).
+// Threads 0..239: output (k = tid / 8, channels 4 (tid % 8) .. + 3).
+__global__ __launch_bounds__(256) void fmap_head_part_kernel(const float* __restrict__ ex, int ldex,
+                                                             const float* __restrict__ mx, const FeatRef fx, int N1,
+                                                             const float* __restrict__ ey, int ldey,
+                                                             const float* __restrict__ my, const FeatRef fy, int N2,
+                                                             int Px, float* __restrict__ part) {
+  __shared__ float Ws[kPChunk][kHK + 1];
+  __shared__ __attribute__((aligned(16))) float Fs[kPChunk][kLdF];
+  const int b = blockIdx.y, p = blockIdx.x, tid = threadIdx.x;
+  const bool xs = p < Px;
+  const int N = xs ? N1 : N2, lde = xs ? ldex : ldey;
+  const float* __restrict__ ev = xs ? ex : ey;
+  const float* __restrict__ ms = xs ? mx : my;
+  const FeatRef f = xs ? fx : fy;
+  const int n0 = (xs ? p : p - Px) * kPChunk;
+  const int m = min(kPChunk, N - n0);
+  for (int e = tid; e < kPChunk * kHK; e += 256) {
+    const int r = e / kHK, kk = e - r * kHK;
+    float v = 0.f;
+    if (r < m) {
+      const int64_t n = (int64_t)b * N + n0 + r;
+      v = ev[n * lde + kk] * ms[n];  // f32 product, as evecs[:, :, :k] * mass[:, :, None]
     }
-    for (int e = tid; e < kHChunk * kHC; e += blockDim.x) {
-      const int r = e / kHC, cc = e - r * kHC;
-      Fs[r][cc] = r < m ? f.base[(int64_t)b * f.sb + (int64_t)(n0 + r) * f.sn + (int64_t)cc * f.sc] : 0.f;
-    }
-    __syncthreads();
-    if (tid < kHK * 16) {
-      for (int r = 0; r < m; ++r) {
-        const float w = Ws[r][k];
-        a0 = fmaf(w, Fs[r][c], a0);
-        a1 = fmaf(w, Fs[r][c + 1], a1);
-      }
-    }
+    Ws[r][kk] = v;
   }
-  if (tid < kHK * 16) {
-    out[k][c] = a0;
-    out[k][c + 1] = a1;
+  // consecutive threads walk the unit-stride axis of the features (points for channels-first
+  // storage, channels for rows), so the staging loads coalesce either way
+  const bool pts_fast = f.sn == 1;
+  for (int e = tid; e < kPChunk * kHC; e += 256) {
+    const int r = pts_fast ? e % kPChunk : e / kHC, cc = pts_fast ? e / kPChunk : e % kHC;
+    Fs[r][cc] = r < m ? f.base[(int64_t)b * f.sb + (int64_t)(n0 + r) * f.sn + (int64_t)cc * f.sc] : 0.f;
   }
+  __syncthreads();
+  if (tid >= kHK * 8) return;
+  const int k = tid >> 3, c = (tid & 7) * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = 0; r < m; ++r) {
+    const float w = Ws[r][k];
+    const float4 x = *reinterpret_cast<const float4*>(&Fs[r][c]);
+    acc.x = fmaf(w, x.x, acc.x);
+    acc.y = fmaf(w, x.y, acc.y);
+    acc.z = fmaf(w, x.z, acc.z);
+    acc.w = fmaf(w, x.w, acc.w);
+  }
+  *reinterpret_cast<float4*>(&part[(((int64_t)b * gridDim.x + p) * kHK + k) * kHC + c]) = acc;
 }
 
-__global__ __launch_bounds__(512) void fmap_head_fwd_kernel(const float* __restrict__ ex, int ldex,
-                                                            const float* __restrict__ mx, const FeatRef fx, int N1,
-                                                            const float* __restrict__ ey, int ldey,
-                                                            const float* __restrict__ my, const FeatRef fy, int N2,
+// grid (B), block 512: A / Bm = the chunk partials summed in chunk order; AAt, BAt; the mask
+__global__ __launch_bounds__(512) void fmap_head_fin_kernel(const float* __restrict__ part, int Px, int P,
                                                             const float* __restrict__ evx, int ldvx,
                                                             const float* __restrict__ evy, int ldvy, float gamma,
                                                             float* __restrict__ A, float* __restrict__ Bm,
                                                             float* __restrict__ AAt, float* __restrict__ BAt,
                                                             float* __restrict__ D) {
-  __shared__ float Ws[kHChunk][kHK + 1];
-  __shared__ float Fs[kHChunk][kHC + 1];
   __shared__ float As[kHK][kHC + 1], Bs[kHK][kHC + 1];
   __shared__ float red[8], g1s[kHK], g2s[kHK];
   const int b = blockIdx.x, tid = threadIdx.x;
-  head_project(ex, ldex, mx, fx, b, N1, Ws, Fs, As);
-  head_project(ey, ldey, my, fy, b, N2, Ws, Fs, Bs);
-  __syncthreads();
+  const float* pb = part + (int64_t)b * P * kHK * kHC;
   for (int e = tid; e < kHK * kHC; e += blockDim.x) {
     const int k = e / kHC, c = e - k * kHC;
-    A[(int64_t)b * kHK * kHC + e] = As[k][c];
-    Bm[(int64_t)b * kHK * kHC + e] = Bs[k][c];
+    float sa = 0.f, sb = 0.f;
+    for (int q = 0; q < Px; ++q) sa += pb[(int64_t)q * kHK * kHC + e];
+    for (int q = Px; q < P; ++q) sb += pb[(int64_t)q * kHK * kHC + e];
+    As[k][c] = sa;
+    Bs[k][c] = sb;
+    A[(int64_t)b * kHK * kHC + e] = sa;
+    Bm[(int64_t)b * kHK * kHC + e] = sb;
   }
+  __syncthreads();
   for (int e = tid; e < kHK * kHK; e += blockDim.x) {
     const int i = e / kHK, j = e - i * kHK;
     float s = 0.f, t = 0.f;
@@ -373,19 +389,31 @@ __global__ __launch_bounds__(256) void fmap_head_expand_kernel(const float* __re
 
 }  // namespace
 
+extern "C" int64_t pk_fmap_head_work_len(int B, int N1, int N2) {
+  if (B <= 0 || N1 <= 0 || N2 <= 0) return 0;
+  return (int64_t)B * ((N1 + kPChunk - 1) / kPChunk + (N2 + kPChunk - 1) / kPChunk) * kHK * kHC;
+}
+
 extern "C" int pk_fmap_head_fwd(const float* evecs_x, int ldex, const float* mass_x, const float* fx,
                                 const int64_t* fx_strides, int N1, const float* evecs_y, int ldey,
                                 const float* mass_y, const float* fy, const int64_t* fy_strides, int N2,
                                 const float* evals_x, int ldvx, const float* evals_y, int ldvy, int B, int K, int C,
-                                float gamma, float* A, float* Bm, float* AAt, float* BAt, float* D, void* stream) {
+                                float gamma, float* A, float* Bm, float* AAt, float* BAt, float* D, float* work,
+                                int64_t work_len, void* stream) {
   PK_REQUIRE(B >= 0 && K == kHK && C == kHC && N1 > 0 && N2 > 0 && ldex >= K && ldey >= K && ldvx >= K && ldvy >= K);
   if (B == 0) return PK_OK;
   PK_REQUIRE(evecs_x && mass_x && fx && fx_strides && evecs_y && mass_y && fy && fy_strides && evals_x && evals_y);
-  PK_REQUIRE(A && Bm && AAt && BAt && D);
+  PK_REQUIRE(A && Bm && AAt && BAt && D && work);
+  const int Px = (N1 + kPChunk - 1) / kPChunk, P = Px + (N2 + kPChunk - 1) / kPChunk;
+  PK_REQUIRE(work_len >= pk_fmap_head_work_len(B, N1, N2));
   const FeatRef rx{fx, fx_strides[0], fx_strides[1], fx_strides[2]};
   const FeatRef ry{fy, fy_strides[0], fy_strides[1], fy_strides[2]};
-  hipLaunchKernelGGL(fmap_head_fwd_kernel, dim3(B), dim3(512), 0, pk::as_stream(stream), evecs_x, ldex, mass_x, rx,
-                     N1, evecs_y, ldey, mass_y, ry, N2, evals_x, ldvx, evals_y, ldvy, gamma, A, Bm, AAt, BAt, D);
+  hipStream_t s = pk::as_stream(stream);
+  hipLaunchKernelGGL(fmap_head_part_kernel, dim3(P, B), dim3(256), 0, s, evecs_x, ldex, mass_x, rx, N1, evecs_y, ldey,
+                     mass_y, ry, N2, Px, work);
+  PK_CHECK_LAUNCH();
+  hipLaunchKernelGGL(fmap_head_fin_kernel, dim3(B), dim3(512), 0, s, work, Px, P, evals_x, ldvx, evals_y, ldvy, gamma,
+                     A, Bm, AAt, BAt, D);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -510,6 +510,11 @@ namespace {
 // Replaces the library GEMM + separate bias / transpose kernels of these tall-skinny
 // shapes (32k-65k points x <= 128 channels).
 constexpr int kLfMaxC = 128;
+// rows kernel grid cap (development knob PK_ROWS_BLOCKS at build time; 4 waves per block)
+#ifndef PK_ROWS_BLOCKS
+#define PK_ROWS_BLOCKS 4096
+#endif
+constexpr int kRowsMaxBlocks = PK_ROWS_BLOCKS;
 
 // ReLU backward folded into an input-gradient epilogue: mask = the forward output of the layer
 // whose gradient this is (aten threshold_backward(grad, mask, 0): mask <= 0 -> 0)
@@ -1013,7 +1018,7 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
   if (layout == 0 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128) && sx % 4 == 0) {
     // 16-point tiles, 4 per block, at most two blocks per CU's worth of waves in flight
     const int64_t tiles = (R + 15) / 16;
-    const unsigned blocks = (unsigned)std::min<int64_t>((tiles + 3) / 4, 512);
+    const unsigned blocks = (unsigned)std::min<int64_t>((tiles + 3) / 4, (int64_t)kRowsMaxBlocks);
     const int TO = Cout <= 16 ? 1 : Cout <= 32 ? 2 : Cout <= 64 ? 4 : 8;
     auto pick = [&](auto q) {
       constexpr int Q = decltype(q)::value;

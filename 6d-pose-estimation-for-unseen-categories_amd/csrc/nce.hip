@@ -9,39 +9,44 @@
 // forward and ~35 backward per step (normalize, gathers, cdist, masked log-softmax,
 // diagonal, their backwards, scatter-adds); here it is three launches:
 //   zero(g1, g2) -> row pass -> column pass.
-// Row pass, one wave per 16 query rows a, taken 4 at a time (4 waves per block; grid S/64 x B):
-//   logits of row a against all S keys (8 columns per lane, keys normalized once per block
-//   into LDS), wave max / sum -> lse[a], term[a] = lse[a] - logit[a][a];
-//   dlogit[a][o] = (softmax - [o == a]) / n_valid;  r = -dlogit / (t d);
-//   dq_a = q_a sum_o r - sum_o r k_o  (torch's _euclidean_dist_backward), then through
-//   F.normalize's backward, added into g1[b, idx1(a)] (global f32 atomics: a CAD point can
-//   sit in several pairs, as torch's gather-backward scatter_add).
-// Column pass: the same per key column o, with the softmax rows' lse from the row pass:
-//   dk_o = k_o sum_a r - sum_a r q_a  -> g2[b, idx2(o)];  block (0, b) also writes
+// Each pass is two f32 MFMA contractions (v_mfma_f32_16x16x4f32: exact f32, an fmaf chain
+// over the 32 channels in order, so both passes see bit-identical distances), one wave per
+// 16 own rows (4 waves per block; grid S/64 x B), the other side's S <= 512 normalized
+// vectors staged once per block in LDS:
+//   G^T[512 x 16] = O[512 x 32] . V^T[32 x 16]: lane (row r = lane % 16, group g = lane / 16)
+//     holds its row's distances to partners 16 t + 4 g + v (t < 32, v < 4) in 128 VGPRs;
+//   row pass: max / sum over a row = in-lane over 128, then xor 16, 32 -> lse[a],
+//     term[a] = lse[a] - logit[a][a];  column pass: the softmax rows' lse from the row pass;
+//   r[a][o] = dL/dd = -(softmax - [o == a]) / (n_valid t d)  (0 where d == 0 or invalid),
+//     written over the distances (the A operand of the next product, same register layout);
+//   dQ[16 x 32] = R[16 x 512] . O[512 x 32]  (k-slot g of step (t, v) = partner 16 t + 4 g + v);
+//   dq_a = q_a sum_o r - (R O)_a  (torch's _euclidean_dist_backward), then F.normalize's
+//   backward, added into g_own[b, idx(a)] (global f32 atomics: a CAD point can sit in several
+//   pairs, as torch's gather-backward scatter_add).
+// Column pass: the same per key column o -> g2;  block (0, b) also writes
 //   loss[b] = sum_a term[a] / max(n_valid, 1) in a fixed order (deterministic).
 // prenorm: f1 / f2 are already F.normalize'd (the overlap head's l2-normalize writes a rows
 // copy for this term): no normalization here, and g1 / g2 are the gradients with respect to
-// those normalized features (the l2-normalize backward then takes both heads' gradients).
+// those normalized features (the l2-normalize backward then takes both heads' gradients);
+// such rows are staged with 16-B loads, 8 lanes per row.
 // Rows past a crop's pair count (valid == 0) contribute nothing; a crop without pairs has
 // loss 0 (the batched host code's clamp(min=1) convention; the reference would give NaN).
+#include <cstdint>
+
 #include "common.hpp"
 
 namespace {
 
-typedef float fx2 __attribute__((ext_vector_type(2)));  // v_pk_fma_f32 operands
+typedef float fx4 __attribute__((ext_vector_type(4)));
 
-constexpr int kC = 32;         // feature width (n_feat, config/dpfm_orig.yaml)
-constexpr int kMaxS = 512;     // nce_num_pairs (config/dpfm_orig.gin:58)
-constexpr int kPerLane = kMaxS / pk::kWave;
+constexpr int kC = 32;           // feature width (n_feat, config/dpfm_orig.yaml)
+constexpr int kMaxS = 512;       // nce_num_pairs (config/dpfm_orig.gin:58)
+constexpr int kPT = kMaxS / 16;  // partner tiles of 16
 constexpr int kRowsPerWave = 16;
-constexpr int kGroup = 4;     // rows evaluated together (partner reads amortized over them)
-constexpr int kWaves = 4;     // one wave per SIMD (LDS holds one block per CU): 256 VGPRs + AGPRs each
+constexpr int kWaves = 4;  // one block per CU (LDS), one wave per SIMD
 constexpr int kTile = kRowsPerWave * kWaves;  // rows per block
-constexpr int kLdO = kC + 1;                  // odd LDS row stride: lanes read rows o = lane + 64 j
-constexpr int kLdW = kC + 4;                  // own rows: 16-B aligned (broadcast ds_read_b128)
+constexpr int kLd = kC + 2;  // LDS row stride: the G operand reads (row r, channel 4 s + g) hit distinct banks
 
-// normalized feature row of pair slot `slot` (side 0: f1 via pairs[.., 0]; side 1: f2 via
-// pairs[.., 1]) and its pre-normalization norm
 struct FeatView {  // f[b, n, c] = base[b * sb + n * sn + c * sc] (rows or channels-first storage)
   const float* base;
   int64_t sb, sn, sc;
@@ -56,26 +61,43 @@ __device__ __forceinline__ const float* nce_row_ptr(const FeatView& f, const int
   return f.base + (int64_t)b * f.sb + idx * f.sn;
 }
 
+// one feature row into dst[0..31]: x / max(||x||, 1e-12) (F.normalize, sequential fmaf norm),
+// or as is under prenorm; returns the pre-normalization norm (1 under prenorm)
+__device__ __forceinline__ float stage_row(const float* p, int64_t sc, bool ok, int prenorm, float* dst) {
+  float x[kC];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < kC; ++c) x[c] = ok ? p[c * sc] : 0.f;
+#pragma unroll
+  for (int c = 0; c < kC; ++c) ss = fmaf(x[c], x[c], ss);
+  const float nrm = prenorm ? 1.f : sqrtf(ss);
+  const float nc = fmaxf(nrm, 1e-12f);
+#pragma unroll
+  for (int c = 0; c < kC; ++c) dst[c] = ok ? (prenorm ? x[c] : x[c] / nc) : 0.f;
+  return nrm;
+}
+
 template <bool COLS>
 __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
     const FeatView f1, const FeatView f2, int64_t N1, int64_t N2,
     const int64_t* __restrict__ pairs, int cap, const int64_t* __restrict__ rows,
     const uint8_t* __restrict__ valid, int S, float inv_t, int prenorm, float* __restrict__ lse,
     float* __restrict__ term, float* __restrict__ loss, float* __restrict__ g_own) {
-  __shared__ float Os[kMaxS * kLdO];  // the other side's normalized vectors
-  __shared__ float lse_s[kMaxS];      // COLS: softmax rows' lse
-  __shared__ float4 rbuf[kWaves][kMaxS];  // per wave: r of its kGroup rows, [partner][row]
+  __shared__ __attribute__((aligned(16))) float Os[kMaxS * kLd];  // the other side's normalized vectors
+  __shared__ __attribute__((aligned(16))) float on_s[kMaxS];      // their |u|^2 (+inf: invalid slot)
+  __shared__ __attribute__((aligned(16))) float lse_s[kMaxS];     // COLS: the softmax rows' lse
+  __shared__ float Ws[kTile * kLd];  // this block's own rows, normalized
+  __shared__ float wn_s[kTile];      // their norms (-1: invalid row)
+  __shared__ float vn_s[kTile];      // their |v|^2
+  __shared__ int64_t widx_s[kTile];  // their feature indices
   __shared__ int nv_s[kWaves];
-  __shared__ __attribute__((aligned(16))) float Ws[kTile * kLdW];  // this block's own rows, normalized
-  __shared__ float wn_s[kTile];                                     // their norms (0: invalid row)
-  __shared__ int64_t widx_s[kTile];                                 // their feature indices
   const int b = blockIdx.y;
   const int lane = pk::lane_id(), w = pk::wave_id();
   const uint8_t* __restrict__ vb = valid + (int64_t)b * S;
   // own side: rows pass = queries (f1, pairs[..,0]); column pass = keys (f2, pairs[..,1])
   const FeatView f_own = COLS ? f2 : f1;
   const FeatView f_oth = COLS ? f1 : f2;
-  const int64_t N_own = COLS ? N2 : N1, N_oth = COLS ? N1 : N2;
+  const int64_t N_own = COLS ? N2 : N1;
   const int side_own = COLS ? 1 : 0;
 
   // number of valid slots (identical in every block of the crop)
@@ -83,41 +105,52 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
   for (int o = threadIdx.x; o < S; o += 64 * kWaves) nv += vb[o] ? 1 : 0;
   nv = pk::wave_sum_i32(nv);
   if (lane == 0) nv_s[w] = nv;
-  // stage the other side, normalized as F.normalize: x / max(||x||, 1e-12), with the same
-  // sequential fmaf norm as the own side below (both passes then see identical vectors)
-  for (int o = threadIdx.x; o < kMaxS; o += 64 * kWaves) {  // rows >= S: zeros
-    float x[kC];
-    float ss = 0.f;
-    const bool ok = o < S && vb[o] != 0;
-    int64_t idx = 0;
-    const float* p = ok ? nce_row_ptr(f_oth, pairs, cap, rows, S, b, o, 1 - side_own, &idx) : nullptr;
-#pragma unroll
-    for (int c = 0; c < kC; ++c) x[c] = ok ? p[c * f_oth.sc] : 0.f;
-#pragma unroll
-    for (int c = 0; c < kC; ++c) ss = fmaf(x[c], x[c], ss);
-    const float nc = prenorm ? 1.f : fmaxf(sqrtf(ss), 1e-12f);
-#pragma unroll
-    for (int c = 0; c < kC; ++c) Os[o * kLdO + c] = ok ? (prenorm ? x[c] : x[c] / nc) : 0.f;
-    if (COLS) lse_s[o] = o < S ? lse[(int64_t)b * S + o] : 0.f;
+  // stage the other side (slots >= S and invalid slots: zeros)
+  const bool vec = prenorm && f_oth.sc == 1 && (((uintptr_t)f_oth.base) & 15) == 0 && (f_oth.sn & 3) == 0 &&
+                   (f_oth.sb & 3) == 0;
+  if (vec) {  // normalized rows storage: 8 lanes per row, 16 B each
+    for (int e = threadIdx.x; e < kMaxS * 8; e += 64 * kWaves) {
+      const int o = e >> 3, q = e & 7;
+      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (o < S && vb[o] != 0) {
+        int64_t idx;
+        const float* p = nce_row_ptr(f_oth, pairs, cap, rows, S, b, o, 1 - side_own, &idx);
+        x = *reinterpret_cast<const float4*>(p + 4 * q);
+      }
+      float2* d2 = reinterpret_cast<float2*>(&Os[o * kLd + 4 * q]);  // 8-B aligned (kLd even)
+      d2[0] = make_float2(x.x, x.y);
+      d2[1] = make_float2(x.z, x.w);
+    }
+  } else {
+    for (int o = threadIdx.x; o < kMaxS; o += 64 * kWaves) {
+      const bool ok = o < S && vb[o] != 0;
+      int64_t idx = 0;
+      const float* p = ok ? nce_row_ptr(f_oth, pairs, cap, rows, S, b, o, 1 - side_own, &idx) : nullptr;
+      stage_row(p, f_oth.sc, ok, prenorm, &Os[o * kLd]);
+    }
   }
-  // stage this block's own rows (all their dependent index / feature loads in parallel)
+  // this block's own rows (all their dependent index / feature loads in parallel)
   if (threadIdx.x < kTile) {
     const int a = blockIdx.x * kTile + threadIdx.x;
     const bool ok = a < S && vb[a] != 0;
     int64_t idx = 0;
-    float x[kC];
     const float* p = ok ? nce_row_ptr(f_own, pairs, cap, rows, S, b, a, side_own, &idx) : nullptr;
+    float* dst = &Ws[threadIdx.x * kLd];
+    const float nrm = stage_row(p, f_own.sc, ok, prenorm, dst);
+    float vn = 0.f;
 #pragma unroll
-    for (int c = 0; c < kC; ++c) x[c] = ok ? p[c * f_own.sc] : 0.f;
-    float ss = 0.f;
-#pragma unroll
-    for (int c = 0; c < kC; ++c) ss = fmaf(x[c], x[c], ss);
-    const float nrm = prenorm ? 1.f : sqrtf(ss);
-    const float nc = fmaxf(nrm, 1e-12f);
-#pragma unroll
-    for (int c = 0; c < kC; ++c) Ws[threadIdx.x * kLdW + c] = ok ? (prenorm ? x[c] : x[c] / nc) : 0.f;
-    wn_s[threadIdx.x] = ok ? nrm : -1.f;  // -1: invalid slot
+    for (int c = 0; c < kC; ++c) vn = fmaf(dst[c], dst[c], vn);
+    wn_s[threadIdx.x] = ok ? nrm : -1.f;
+    vn_s[threadIdx.x] = vn;
     widx_s[threadIdx.x] = idx;
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < kMaxS; o += 64 * kWaves) {  // |u|^2: the same fmaf chain in both passes
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < kC; ++c) s = fmaf(Os[o * kLd + c], Os[o * kLd + c], s);
+    on_s[o] = (o < S && vb[o] != 0) ? s : __builtin_huge_valf();
+    if (COLS) lse_s[o] = o < S ? lse[(int64_t)b * S + o] : 0.f;
   }
   __syncthreads();
   nv = 0;
@@ -132,161 +165,123 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
     if (lane == 0) loss[b] = t * sc;
   }
   if (COLS && g_own == nullptr) return;
+  const int a0 = blockIdx.x * kTile + w * kRowsPerWave;  // wave-uniform; no barrier below
+  if (a0 >= S) return;
+  const int r = lane & 15, g = lane >> 4;
+  const int tr = w * kRowsPerWave + r;  // the lane's row within the staged tile
+  const int a = a0 + r;
+  const bool ok = a < S && wn_s[tr] >= 0.f;
+  const float vn = vn_s[tr];
 
-  // |u|^2 of the lane's other-side columns (same expression in both passes)
-  float on[kPerLane];
+  // d[t][v]: distance to partner 16 t + 4 g + v (-1: no logit there)
+  float bv[kC / 4];
 #pragma unroll
-  for (int j = 0; j < kPerLane; ++j) {
-    const int o = lane + pk::kWave * j;
+  for (int s = 0; s < kC / 4; ++s) bv[s] = Ws[tr * kLd + 4 * s + g];
+  float d[kPT][4];
+#pragma unroll
+  for (int t = 0; t < kPT; ++t) {
+    fx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < kC / 4; ++s)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Os[(16 * t + r) * kLd + 4 * s + g], bv[s], acc, 0, 0, 0);
+    const float4 on = *reinterpret_cast<const float4*>(&on_s[16 * t + 4 * g]);
+    const float onv[4] = {on.x, on.y, on.z, on.w};
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const float d2 = fmaxf((vn + onv[v]) - 2.f * acc[v], 0.f);
+      d[t][v] = ok && onv[v] < __builtin_huge_valf() ? __builtin_amdgcn_sqrtf(d2) : -1.f;  // v_sqrt_f32 (1 ulp)
+    }
+  }
+  // row pass: the row's softmax statistics; max logit = -(min d) / t exactly (monotone rounding)
+  float mx = 0.f, is = 0.f, lse_a = 0.f;
+  if (!COLS) {
+    float dm = __builtin_huge_valf();
+#pragma unroll
+    for (int t = 0; t < kPT; ++t)
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        if (d[t][v] >= 0.f) dm = fminf(dm, d[t][v]);
+    dm = fminf(dm, __shfl_xor(dm, 16));
+    dm = fminf(dm, __shfl_xor(dm, 32));
+    mx = ok ? -dm * inv_t : 0.f;
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < kC; ++c) s = fmaf(Os[o * kLdO + c], Os[o * kLdO + c], s);
-    on[j] = s;
+    for (int t = 0; t < kPT; ++t)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) s += d[t][v] >= 0.f ? __expf(-d[t][v] * inv_t - mx) : 0.f;
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    is = __builtin_amdgcn_rcpf(s);
+    lse_a = mx + __logf(s);
   }
-
-  // kGroup rows at a time: every partner vector read from LDS serves kGroup dot products
-  for (int rg = 0; rg < kRowsPerWave; rg += kGroup) {
-    const int a0 = blockIdx.x * kTile + w * kRowsPerWave + rg;  // wave-uniform
-    if (a0 >= S) break;
-    bool ok[kGroup];
-    int64_t idx[kGroup];
-    float v[kGroup][kC], nrm[kGroup], vn[kGroup];
-    bool any = false;
+  // r = dL/dd over the distances; the row pass also picks the diagonal logit
+  const float k_r = -sc * inv_t;
+  float rs = 0.f, ldg = 0.f;
 #pragma unroll
-    for (int g = 0; g < kGroup; ++g) {
-      const int a = a0 + g;
-      const int t = a - blockIdx.x * kTile;  // row within the block's staged tile
-      nrm[g] = wn_s[t];
-      ok[g] = a < S && nrm[g] >= 0.f;
-      any = any || ok[g];
-      idx[g] = widx_s[t];
-      if (!ok[g] && !COLS && a < S && lane == 0) {
-        lse[(int64_t)b * S + a] = 0.f;
-        term[(int64_t)b * S + a] = 0.f;
-      }
-      vn[g] = 0.f;
-#pragma unroll
-      for (int c = 0; c < kC; c += 4) {  // broadcast reads of the staged (normalized) row
-        const float4 q = *reinterpret_cast<const float4*>(&Ws[t * kLdW + c]);
-        v[g][c] = q.x; v[g][c + 1] = q.y; v[g][c + 2] = q.z; v[g][c + 3] = q.w;
-      }
-#pragma unroll
-      for (int c = 0; c < kC; ++c) vn[g] = fmaf(v[g][c], v[g][c], vn[g]);
+  for (int t = 0; t < kPT; ++t) {
+    float lo[4] = {0.f, 0.f, 0.f, 0.f};
+    if (COLS) {
+      const float4 l4 = *reinterpret_cast<const float4*>(&lse_s[16 * t + 4 * g]);
+      lo[0] = l4.x; lo[1] = l4.y; lo[2] = l4.z; lo[3] = l4.w;
     }
-    if (!any) continue;
-    // distances and logits against all S partners (8 per lane); rows paired for packed FMAs
-    float d[kGroup][kPerLane], lg[kGroup][kPerLane];
 #pragma unroll
-    for (int j = 0; j < kPerLane; ++j) {
-      const int o = lane + pk::kWave * j;
-      const bool vo = o < S && vb[o] != 0;
-      fx2 dot01 = {0.f, 0.f}, dot23 = {0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < kC; ++c) {
-        const float u = Os[o * kLdO + c];
-        const fx2 uu = {u, u};
-        dot01 = __builtin_elementwise_fma((fx2){v[0][c], v[1][c]}, uu, dot01);
-        dot23 = __builtin_elementwise_fma((fx2){v[2][c], v[3][c]}, uu, dot23);
-      }
-      const float dot[kGroup] = {dot01.x, dot01.y, dot23.x, dot23.y};
-#pragma unroll
-      for (int g = 0; g < kGroup; ++g) {
-        const float d2 = fmaxf((vn[g] + on[j]) - 2.f * dot[g], 0.f);
-        const bool on_ = vo && ok[g];
-        d[g][j] = on_ ? __builtin_amdgcn_sqrtf(d2) : 0.f;  // v_sqrt_f32 (1 ulp)
-        lg[g][j] = on_ ? -d[g][j] * inv_t : -__builtin_huge_valf();
-      }
+    for (int v = 0; v < 4; ++v) {
+      const float dd = d[t][v];
+      const float lg = -dd * inv_t;
+      const bool diag = 16 * t + 4 * g + v == a;
+      const float p = dd >= 0.f ? (COLS ? __expf(lg - lo[v]) : __expf(lg - mx) * is) : 0.f;
+      if (!COLS && diag) ldg = lg;
+      const float gg = p - (diag ? 1.f : 0.f);
+      const float rr = dd > 0.f ? gg * k_r * __builtin_amdgcn_rcpf(dd) : 0.f;  // implies ok, partner valid
+      rs += rr;
+      d[t][v] = rr;
     }
-    // softmax weights p[g][j] (row pass: this row's softmax; column pass: row o's, from lse)
-    float p[kGroup][kPerLane];
-    if (!COLS) {
-#pragma unroll
-      for (int g = 0; g < kGroup; ++g) {
-        float m = lg[g][0];
-#pragma unroll
-        for (int j = 1; j < kPerLane; ++j) m = fmaxf(m, lg[g][j]);
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-        if (!ok[g]) m = 0.f;  // all -inf: keep exp finite-free (0)
-        const int a = a0 + g;
-        float ld = 0.f;  // logit of the diagonal (a, a): lane a % 64, slot a / 64
-#pragma unroll
-        for (int j = 0; j < kPerLane; ++j)
-          if (j == a / pk::kWave) ld = lg[g][j];
-        ld = __shfl(ld, a % pk::kWave);
-        float s = 0.f;
-#pragma unroll
-        for (int j = 0; j < kPerLane; ++j) {
-          p[g][j] = __expf(lg[g][j] - m);
-          s += p[g][j];
-        }
-        s = pk::wave_sum_f32(s);
-        const float sm = m + __logf(s);
-        const float is = __builtin_amdgcn_rcpf(s);
-#pragma unroll
-        for (int j = 0; j < kPerLane; ++j) p[g][j] *= is;
-        if (!ok[g]) continue;  // wave-uniform
-        if (lane == 0) {
-          lse[(int64_t)b * S + a] = sm;
-          term[(int64_t)b * S + a] = sm - ld;
-        }
-      }
-      if (g_own == nullptr) continue;
-    } else {
-#pragma unroll
-      for (int j = 0; j < kPerLane; ++j) {
-        const float l_oth = lse_s[lane + pk::kWave * j];
-#pragma unroll
-        for (int g = 0; g < kGroup; ++g) p[g][j] = __expf(lg[g][j] - l_oth);
-      }
+  }
+  rs += __shfl_xor(rs, 16);
+  rs += __shfl_xor(rs, 32);
+  if (!COLS) {
+    ldg += __shfl_xor(ldg, 16);  // one group holds it, the others add zeros
+    ldg += __shfl_xor(ldg, 32);
+    if (g == 0 && a < S) {
+      lse[(int64_t)b * S + a] = ok ? lse_a : 0.f;
+      term[(int64_t)b * S + a] = ok ? lse_a - ldg : 0.f;
     }
-    // r[g][o] = dL/dd = -(p - [o == a]) * sc / (t d)   (0 where d == 0 or invalid)
-    float rs[kGroup];
+    if (g_own == nullptr) return;
+  }
+  // (R O)[row 4 g + v][channel 16 h + r]
+  fx4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int g = 0; g < kGroup; ++g) rs[g] = 0.f;
-    const float k_r = -sc * inv_t;
+  for (int t = 0; t < kPT; ++t)
 #pragma unroll
-    for (int j = 0; j < kPerLane; ++j) {
-      const int o = lane + pk::kWave * j;
-      float r4[kGroup];
+    for (int v = 0; v < 4; ++v) {
+      const float* orow = &Os[(16 * t + 4 * g + v) * kLd + r];
 #pragma unroll
-      for (int g = 0; g < kGroup; ++g) {
-        const float gg = p[g][j] - (o == a0 + g ? 1.f : 0.f);
-        const float r = d[g][j] > 0.f ? gg * k_r * __builtin_amdgcn_rcpf(d[g][j]) : 0.f;  // implies ok[g], o valid
-        r4[g] = r;
-        rs[g] += r;
-      }
-      rbuf[w][o] = make_float4(r4[0], r4[1], r4[2], r4[3]);
+      for (int h = 0; h < 2; ++h) acc2[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(d[t][v], orow[16 * h], acc2[h], 0, 0, 0);
     }
-    __builtin_amdgcn_wave_barrier();  // rbuf rows complete (one wave's LDS ops run in order)
+  // dq, then F.normalize backward: (dv - v (v . dv)) / n  (dv / 1e-12 when clamped)
 #pragma unroll
-    for (int g = 0; g < kGroup; ++g) rs[g] = pk::wave_sum_f32(rs[g]);
-    // sum_o r[g][o] u_o[c]: lane (c, half h) over half of the partners, then the two halves
-    const int c = lane & 31, h = lane >> 5;
-    fx2 acc01 = {0.f, 0.f}, acc23 = {0.f, 0.f};
-    const float4* __restrict__ rb = &rbuf[w][h * (kMaxS / 2)];
-    const float* __restrict__ os = &Os[(h * (kMaxS / 2)) * kLdO + c];
-#pragma unroll 8
-    for (int o = 0; o < kMaxS / 2; ++o) {
-      const float4 r = rb[o];
-      const float u = os[o * kLdO];
-      const fx2 uu = {u, u};
-      acc01 = __builtin_elementwise_fma((fx2){r.x, r.y}, uu, acc01);
-      acc23 = __builtin_elementwise_fma((fx2){r.z, r.w}, uu, acc23);
-    }
-    float acc[kGroup] = {acc01.x, acc01.y, acc23.x, acc23.y};
+  for (int v = 0; v < 4; ++v) {
+    const int rw = 4 * g + v;               // row of this accumulator slot
+    const float rs_w = __shfl(rs, rw);      // lane rw holds row rw's sum (group 0)
+    const int trw = w * kRowsPerWave + rw;
+    const bool okw = a0 + rw < S && wn_s[trw] >= 0.f;
+    const float nw = wn_s[trw];
+    float vc[2], dv[2];
 #pragma unroll
-    for (int g = 0; g < kGroup; ++g) {
-      acc[g] += __shfl_xor(acc[g], 32);
-      if (!ok[g]) continue;  // wave-uniform
-      // d/dv, then F.normalize backward: (dv - v (v . dv)) / n  (dv / 1e-12 when clamped)
-      const float vc = lane < kC ? Ws[(a0 + g - blockIdx.x * kTile) * kLdW + c] : 0.f;  // staged row
-      const float dv = vc * rs[g] - acc[g];
-      const float vdv = pk::wave_sum_f32(lane < kC ? vc * dv : 0.f);
-      const float dx = prenorm ? dv : nrm[g] > 1e-12f ? (dv - vc * vdv) / nrm[g] : dv / 1e-12f;
-      if (lane < kC) atomicAdd(g_own + ((int64_t)b * N_own + idx[g]) * kC + c, dx);
+    for (int h = 0; h < 2; ++h) {
+      vc[h] = Ws[trw * kLd + 16 * h + r];
+      dv[h] = vc[h] * rs_w - acc2[h][v];
     }
-    __builtin_amdgcn_wave_barrier();  // all lanes done reading rbuf before the next group
+    float vdv = vc[0] * dv[0] + vc[1] * dv[1];
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) vdv += __shfl_xor(vdv, off);  // the row's 16 lanes
+    if (!okw) continue;
+    const int64_t base = ((int64_t)b * N_own + widx_s[trw]) * kC + r;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float dx = prenorm ? dv[h] : nw > 1e-12f ? (dv[h] - vc[h] * vdv) / nw : dv[h] / 1e-12f;
+      atomicAdd(g_own + base + 16 * h, dx);
+    }
   }
 }
 

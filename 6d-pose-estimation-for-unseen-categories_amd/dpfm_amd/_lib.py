@@ -47,8 +47,9 @@ SIGNATURES = {
     "pk_offsets_from_counts": [_P, _I, _P, _P],
     "pk_spectral_diffusion": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _P],
     "pk_linear_ex": [_P, _P],
+    "pk_fmap_head_work_len": [_I, _I, _I],
     "pk_fmap_head_fwd": [_P, _I, _P, _P, _P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _F, _P, _P, _P, _P,
-                         _P, _P],
+                         _P, _P, _I64, _P],
     "pk_fmap_head_bwd": [_P, _P, _P, _P, _P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "pk_fmap_solve": [_P, _P, _P, _F, _I, _I, _P, _P],
     "pk_fmap_solve_backward": [_P, _P, _P, _F, _I, _I, _P, _P, _P, _P],
@@ -86,7 +87,7 @@ SIGNATURES = {
 }
 
 RESTYPES = {"pk_cgt_lstsq_work_size": _I64, "pk_linear_wgrad_grouped_work": _I64, "pk_ransac_work_size": _I64,
-            "pk_feat_dist_work_size": _I64}  # everything else returns an int status
+            "pk_feat_dist_work_size": _I64, "pk_fmap_head_work_len": _I64}  # everything else returns an int status
 
 _lib: Optional[ctypes.CDLL] = None
 

@@ -325,11 +325,13 @@ class _FmapHeadFn(torch.autograd.Function):
         AAt = torch.empty((B, K, K), dtype=torch.float32, device=dev)
         BAt = torch.empty_like(AAt)
         D = torch.empty_like(AAt)
+        wl = int(_lib.lib().pk_fmap_head_work_len(B, int(N1), int(N2)))
+        work = torch.empty((max(wl, 1),), dtype=torch.float32, device=dev)
         call("pk_fmap_head_fwd", ptr(evecs_x), int(evecs_x.shape[-1]), ptr(mass_x), ctypes.c_void_p(fx.data_ptr()),
              st(fx), int(N1), ptr(evecs_y), int(evecs_y.shape[-1]), ptr(mass_y), ctypes.c_void_p(fy.data_ptr()),
              st(fy), int(N2), ctypes.c_void_p(evals_x.data_ptr()), int(evals_x.stride(0)),
              ctypes.c_void_p(evals_y.data_ptr()), int(evals_y.stride(0)), B, K, Cf, float(gamma), ptr(A), ptr(Bm),
-             ptr(AAt), ptr(BAt), ptr(D), _lib.stream(dev), work=None)
+             ptr(AAt), ptr(BAt), ptr(D), ptr(work), wl, _lib.stream(dev), work=None)
         Cm = torch.empty_like(BAt)
         call("pk_fmap_solve", ptr(AAt), ptr(BAt), ptr(D), float(lambda_), B, K, ptr(Cm), _lib.stream(dev))
         ctx.save_for_backward(evecs_x, evecs_y, mass_x, mass_y, A, Bm, AAt, BAt, D)

@@ -465,6 +465,14 @@ def main():
             "kernels": kernels,
         }
         out.update(extra)
+        if "pk_ransac" in kern and args.mode in ("infer", "corr4096"):
+            rk = kern["pk_ransac"]
+            crops_per_launch = 1 if args.mode == "corr4096" else units
+            r64 = roofline_for("pk_ransac", rk)
+            out["ransac"] = {"hypotheses_per_s": round(args.hypotheses * crops_per_launch / (rk["avg_ms"] * 1e-3), 1),
+                             "ms_per_launch": round(rk["avg_ms"], 4), "hypotheses_per_launch":
+                             args.hypotheses * crops_per_launch, "valu64_achieved_tflops": r64["achieved"],
+                             "valu64_frac": r64["frac"]}
         if args.mode == "train" and not args.no_roofline_probe and world == 1:
             out["roofline_ball_query"] = ball_query_roofline(dev)
         if not args.no_cpu_baseline and world == 1:

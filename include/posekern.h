@@ -253,12 +253,15 @@ int pk_mlp3_fwd(const float* x_in, const float* x_diff, const float* w1, const f
  *   element strides {batch, point, channel}; evals f32 [B, ldv].
  * Backward: part = pk_fmap_solve_backward's dAAt slabs [B,K,K,K], dBAt [B,K,K] ->
  *   dA, dBm [B,K,C] (scratch outputs) and dF_x = W_x dA, dF_y = W_y dBm written at the
- *   HOST strides dfx_strides / dfy_strides. */
+ *   HOST strides dfx_strides / dfy_strides.
+ * work: f32 scratch of pk_fmap_head_work_len(B, N1, N2) floats (the 128-point chunk partials
+ *   of the projections); PK_ERR_ARG when work_len is smaller. */
+int64_t pk_fmap_head_work_len(int B, int N1, int N2);
 int pk_fmap_head_fwd(const float* evecs_x, int ldex, const float* mass_x, const float* fx, const int64_t* fx_strides,
                      int N1, const float* evecs_y, int ldey, const float* mass_y, const float* fy,
                      const int64_t* fy_strides, int N2, const float* evals_x, int ldvx, const float* evals_y, int ldvy,
                      int B, int K, int C, float gamma, float* A, float* Bm, float* AAt, float* BAt, float* D,
-                     void* stream);
+                     float* work, int64_t work_len, void* stream);
 int pk_fmap_head_bwd(const float* part, const float* dBAt, const float* A, const float* Bm, const float* evecs_x,
                      int ldex, const float* mass_x, int N1, const float* evecs_y, int ldey, const float* mass_y, int N2,
                      int B, int K, int C, float* dA, float* dBm, float* dfx, const int64_t* dfx_strides, float* dfy,
