@@ -16,6 +16,9 @@
 //  pk_fps_npoint    object.py:145-147 policy: npoint = int(2000/n * n) when n > 2000
 //                   (else n, no FPS), or a fixed npoint (benchmark configs), per crop.
 //  pk_segment_scan / pk_offsets_from_counts  offsets of packed outputs.
+#include <algorithm>
+#include <climits>
+
 #include "common.hpp"
 
 namespace {
@@ -140,7 +143,7 @@ __global__ __launch_bounds__(64) void bp_write_kernel(
 // ---------------------------------------------------------------- SOR (H2)
 constexpr int kKnn = 20;
 constexpr int kSorThreads = 256;
-constexpr int kSorTile = 4096;
+constexpr int kSorTile = 1024;
 
 __device__ __forceinline__ void topk_insert(double (&best)[kKnn], double v) {
 #pragma unroll
@@ -174,20 +177,58 @@ __device__ __forceinline__ double sqdist(double ax, double ay, double az, const 
 // The kept set is a superset of the true knn nearest (ties included), so the sorted
 // top-knn values are exactly those of a full brute-force search.
 constexpr int kSorMaxBox = 1024;
+#ifndef PK_SOR_BATCH
+#define PK_SOR_BATCH 4
+#endif
+#ifndef PK_SOR_MINW
+#define PK_SOR_MINW 4
+#endif
+constexpr int kSorBatch = PK_SOR_BATCH;  // pixels of a window row gathered together (loads in flight at once)
+
+// distances from the query to the points of pixels uu .. min(uu + 7, u1) of an index-map row;
+// bit t of the result: pixel uu + t holds a point (s[t] valid). All index loads, then all
+// coordinate loads, are issued before the first use (memory-level parallelism).
+__device__ __forceinline__ int sor_gather(const int32_t* __restrict__ row, int uu, int u1,
+                                          const double* __restrict__ p, double q0, double q1, double q2,
+                                          double (&s)[kSorBatch]) {
+  int j[kSorBatch];
+#pragma unroll
+  for (int t = 0; t < kSorBatch; ++t) j[t] = uu + t <= u1 ? row[uu + t] : -1;
+  double c[kSorBatch][3];
+#pragma unroll
+  for (int t = 0; t < kSorBatch; ++t) {
+    const double* pj = p + 3 * (j[t] >= 0 ? j[t] : 0);
+    c[t][0] = pj[0];
+    c[t][1] = pj[1];
+    c[t][2] = pj[2];
+  }
+  int m = 0;
+#pragma unroll
+  for (int t = 0; t < kSorBatch; ++t) {
+    s[t] = sqdist(q0, q1, q2, c[t]);
+    m |= (j[t] >= 0 ? 1 : 0) << t;
+  }
+  return m;
+}
 
 
-__global__ __launch_bounds__(kSorThreads) void sor_knn_kernel(const double* __restrict__ xyz,
-                                                              const int64_t* __restrict__ off, int knn,
-                                                              const int32_t* __restrict__ pix,
-                                                              const int32_t* __restrict__ idxmap, int H, int W,
-                                                              const double* __restrict__ Kmat,
-                                                              double* __restrict__ avg) {
+// grid (tiles x B): workgroup = (crop, 256-query tile), crops interleaved; a persistent grid
+// (fewer workgroups looping over the items) measured slower with no gain in overlap.
+
+__global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const double* __restrict__ xyz,
+                                                                 const int64_t* __restrict__ off, int knn,
+                                                                 const int32_t* __restrict__ pix,
+                                                                 const int32_t* __restrict__ idxmap, int H, int W,
+                                                                 const double* __restrict__ Kmat, int tiles, int B,
+                                                                 double* __restrict__ avg) {
   __shared__ float4 tile[kSorTile];
-  const int b = blockIdx.y;
+  {
+  const int item = blockIdx.x;
+  const int b = item % B, bx = item / B;
   const int64_t base = off[b];
   const int n = (int)(off[b + 1] - base);
-  const int i = blockIdx.x * kSorThreads + threadIdx.x;
-  if (blockIdx.x * kSorThreads >= n) return;
+  const int i = bx * kSorThreads + threadIdx.x;
+  if (bx * kSorThreads >= n) return;  // workgroup-uniform
   const bool act = i < n;
   const double* p = xyz + base * 3;
   const double ox = p[0], oy = p[1], oz = p[2];
@@ -207,29 +248,37 @@ __global__ __launch_bounds__(kSorThreads) void sor_knn_kernel(const double* __re
     const int pp = pix[base + i];
     const int v = pp / W, u = pp % W;
     const int32_t* im = idxmap + (int64_t)b * H * W;
-    int found = 0;
+    int found = 0, Rw = -1;
     for (int R = 2; R <= 8; R *= 2) {  // 5x5, then 9x9, 17x17 near the mask border
       found = 0;
 #pragma unroll
       for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
       for (int vv = max(v - R, 0); vv <= min(v + R, H - 1); ++vv) {
         const int32_t* row = im + vv * W;
-        for (int uu = max(u - R, 0); uu <= min(u + R, W - 1); ++uu) {
-          const int j = row[uu];
-          if (j < 0) continue;
-          topk_insert(best, sqdist(q0, q1, q2, p + 3 * j));
-          ++found;
+        const int u1 = min(u + R, W - 1);
+        for (int uu = max(u - R, 0); uu <= u1; uu += kSorBatch) {
+          double s[kSorBatch];
+          const int m = sor_gather(row, uu, u1, p, q0, q1, q2, s);
+#pragma unroll
+          for (int t = 0; t < kSorBatch; ++t)
+            if ((m >> t) & 1) topk_insert(best, s[t]);
+          found += __builtin_popcount(m);
         }
       }
-      if (found >= kk) break;
+      if (found >= kk) {
+        Rw = R;
+        break;
+      }
     }
-    if (found >= kk) {
+    if (Rw >= 0) {
 #pragma unroll
       for (int k = 0; k < kKnn; ++k)
         if (k == kk - 1) T = best[k];  // static register index (no scratch)
     }
-#pragma unroll
-    for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
+    // pass 2a: best keeps the window's kk smallest (all <= T, real points), and the box scan
+    // adds the box pixels outside that window: the kk smallest of window + box are exact
+    bool box = false;
+    int u0 = 0, u1 = -1, v0 = 0, v1 = -1;
     if (Kmat != nullptr && T < __builtin_huge_val()) {
       const double* Kb = Kmat + 9 * b;
       const double fx = Kb[0], cx = Kb[2], fy = Kb[4], cy = Kb[5];
@@ -241,21 +290,35 @@ __global__ __launch_bounds__(kSorThreads) void sor_knn_kernel(const double* __re
         if (bu < 64.0 && bv < 64.0) {
           const int ru = (int)ceil(bu * (1.0 + 1e-9)) + 1, rv = (int)ceil(bv * (1.0 + 1e-9)) + 1;
           if ((2 * ru + 1) * (2 * rv + 1) <= kSorMaxBox) {
-            const int v0 = max(v - rv, 0), v1 = min(v + rv, H - 1);
-            const int u0 = max(u - ru, 0), u1 = min(u + ru, W - 1);
-            for (int vv = v0; vv <= v1; ++vv) {
-              const int32_t* row = im + vv * W;
-              for (int uu = u0; uu <= u1; ++uu) {
-                const int j = row[uu];
-                if (j < 0) continue;
-                const double s = sqdist(q0, q1, q2, p + 3 * j);
-                if (s <= T && s < best[kKnn - 1]) topk_insert(best, s);
-              }
-            }
-            done = true;
+            box = true;
+            v0 = max(v - rv, 0);
+            v1 = min(v + rv, H - 1);
+            u0 = max(u - ru, 0);
+            u1 = min(u + ru, W - 1);
           }
         }
       }
+    }
+    if (box) {
+      for (int vv = v0; vv <= v1; ++vv) {
+        const int32_t* row = im + vv * W;
+        const bool in_w = vv >= v - Rw && vv <= v + Rw;  // this row's window pixels are in best
+        for (int seg = 0; seg < 2; ++seg) {
+          const int a = in_w ? (seg == 0 ? u0 : max(u0, u + Rw + 1)) : (seg == 0 ? u0 : 1);
+          const int c = in_w ? (seg == 0 ? min(u1, u - Rw - 1) : u1) : (seg == 0 ? u1 : 0);
+          for (int uu = a; uu <= c; uu += kSorBatch) {
+            double s[kSorBatch];
+            const int m = sor_gather(row, uu, c, p, q0, q1, q2, s);
+#pragma unroll
+            for (int t = 0; t < kSorBatch; ++t)
+              if (((m >> t) & 1) && s[t] <= T && s[t] < best[kKnn - 1]) topk_insert(best, s[t]);
+          }
+        }
+      }
+      done = true;
+    } else {
+#pragma unroll
+      for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
     }
   }
   if (__syncthreads_or(act && !done)) {
@@ -293,32 +356,123 @@ __global__ __launch_bounds__(kSorThreads) void sor_knn_kernel(const double* __re
       if (k < kk) acc = acc + sqrt_rn(best[k]);
     avg[base + i] = kk > 0 ? acc / (double)kk : -1.0;
   }
+  }
 }
 
 // One block per crop: cloud mean over avg > 0, then the Bessel std, accumulated in point
-// order exactly like std::accumulate / std::inner_product. The block stages the terms
-// (masked values, then the squared deviations) into LDS in parallel; thread 0 adds them in
-// order (adding +0.0 for masked points leaves a +0.0-started positive sum unchanged).
-constexpr int kStatChunk = 4096;
-constexpr int kStatThreads = 256;
+// order exactly like std::accumulate / std::inner_product: s = s + t_k, k = 0 .. n-1, IEEE
+// double round-to-nearest-even at every step. The terms are >= 0 (masked values, squared
+// deviations), so the running sum only grows, and while it stays in one binade
+// [2^(e-1), 2^e) (ulp U = 2^(e-53), s = S U with the integer S in [2^52, 2^53)) one step is
+//   s + t = (S + r) U rounded to an integer multiple of U,  r = t / U = q + f (q integer):
+//   = (S + q + [f > 1/2]) U   unless f == 1/2 exactly (a tie: the even neighbour, which
+//   depends on S's parity) or the result leaves the binade (rounded at 2U).
+// So a block takes 8192 terms at a time: per term m = q + [f > 1/2] (int64), an exclusive
+// scan gives every term's S before it, and the first term that ties, is >= s, or would reach
+// 2^53 is a break: s = (S + P) U exactly up to it, then that one term is added by the FPU
+// (the true sequential step) and the next round restarts after it. Breaks happen at binade
+// crossings (~log2 n of them: the first 256 terms are added sequentially, where most
+// crossings are) and at exact ties, so a crop takes a handful of rounds instead of n
+// dependent fp64 additions.
+constexpr int kStatThreads = 1024;
+constexpr int kSeqPer = 8;     // terms per thread per round
+constexpr int kSeqWarm = 256;  // first terms added one by one
 
-__device__ __forceinline__ double seq_sum_lds(const double* __restrict__ v, int m, double acc) {
-  int k = 0;
-  for (; k + 8 <= m; k += 8) {
-    const double a0 = v[k], a1 = v[k + 1], a2 = v[k + 2], a3 = v[k + 3];
-    const double a4 = v[k + 4], a5 = v[k + 5], a6 = v[k + 6], a7 = v[k + 7];
-    acc = acc + a0; acc = acc + a1; acc = acc + a2; acc = acc + a3;
-    acc = acc + a4; acc = acc + a5; acc = acc + a6; acc = acc + a7;
+struct SeqShared {
+  double s;
+  int k;
+  int brk;
+  int64_t part[kStatThreads / 64];
+  double s_next;
+};
+
+template <class F>
+__device__ double seq_sum_exact(F term, int n, SeqShared& sh) {
+  const int tid = threadIdx.x, lane = pk::lane_id(), w = pk::wave_id();
+  if (tid == 0) {
+    double s = 0.0;
+    const int m = min(n, kSeqWarm);
+    for (int k = 0; k < m; ++k) s = s + term(k);
+    sh.s = s;
+    sh.k = m;
   }
-  for (; k < m; ++k) acc = acc + v[k];
-  return acc;
+  __syncthreads();
+  while (true) {
+    const double s = sh.s;
+    const int k = sh.k;
+    if (k >= n) break;  // block-uniform
+    __syncthreads();    // everyone has read sh before it changes
+    int e = 0;
+    (void)frexp(s, &e);  // s in [2^(e-1), 2^e) (s == 0: every term breaks, the FPU adds it)
+    const int64_t S = s > 0.0 ? (int64_t)ldexp(s, 53 - e) : 0;
+    const int64_t kTop = (int64_t)1 << 53;
+    const int j0 = k + tid * kSeqPer;
+    int64_t mv[kSeqPer];
+    bool bad[kSeqPer];
+    int64_t tot = 0;
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) {
+      const int j = j0 + i;
+      mv[i] = 0;
+      bad[i] = false;
+      if (j < n) {
+        const double t = term(j);
+        const double r = ldexp(t, 53 - e);
+        if (s == 0.0) {  // 0 + t: exact, but the binade is unknown; zeros leave s at 0
+          bad[i] = t != 0.0;
+        } else if (!(r < 9007199254740992.0)) {  // t >= s (or inf / nan): the FPU step
+          bad[i] = true;
+        } else {
+          const double q = floor(r), f = r - q;
+          bad[i] = f == 0.5;
+          mv[i] = (int64_t)q + (f > 0.5 ? 1 : 0);
+        }
+      }
+      tot += mv[i];
+    }
+    // exclusive scan of the per-thread totals (clamped: a total >= 2^52 already forces a break)
+    const int64_t tc = tot < ((int64_t)1 << 52) ? tot : ((int64_t)1 << 52);
+    const int64_t inc = pk::wave_inclusive_scan_i64(tc);
+    if (lane == 63) sh.part[w] = inc;
+    if (tid == 0) sh.brk = INT_MAX;
+    __syncthreads();
+    int64_t base = inc - tc;
+    for (int q = 0; q < w; ++q) base += sh.part[q];
+    int64_t P = base;
+    int mybrk = INT_MAX;
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) {
+      if (j0 + i < n && mybrk == INT_MAX && (bad[i] || S + P + mv[i] >= kTop)) mybrk = j0 + i;
+      P += mv[i];
+    }
+    if (mybrk != INT_MAX) atomicMin(&sh.brk, mybrk);
+    __syncthreads();
+    const int jb = sh.brk;
+    const int kend = min(k + kStatThreads * kSeqPer, n);
+    // the thread owning the break (or the chunk's last term) publishes the new state
+    if (jb != INT_MAX) {
+      if (jb >= j0 && jb < j0 + kSeqPer) {
+        int64_t Pb = base;
+#pragma unroll
+        for (int i = 0; i < kSeqPer; ++i)
+          if (j0 + i < jb) Pb += mv[i];
+        const double before = s > 0.0 ? ldexp((double)(S + Pb), e - 53) : 0.0;  // exact (S + Pb < 2^53)
+        sh.s = before + term(jb);  // the sequential FPU step
+        sh.k = jb + 1;
+      }
+    } else if (kend - 1 >= j0 && kend - 1 < j0 + kSeqPer) {
+      sh.s = ldexp((double)(S + P), e - 53);
+      sh.k = kend;
+    }
+    __syncthreads();
+  }
+  return sh.s;
 }
 
 __global__ __launch_bounds__(kStatThreads) void sor_stats_kernel(const double* __restrict__ avg,
                                                                  const int64_t* __restrict__ off,
                                                                  double std_ratio, double* __restrict__ thr) {
-  __shared__ double buf[kStatChunk];
-  __shared__ double acc_s;
+  __shared__ SeqShared sh;
   const int b = blockIdx.x;
   const int64_t base = off[b];
   const int n = (int)(off[b + 1] - base);
@@ -326,36 +480,28 @@ __global__ __launch_bounds__(kStatThreads) void sor_stats_kernel(const double* _
     if (threadIdx.x == 0) thr[b] = -1.0;
     return;
   }
-  if (threadIdx.x == 0) acc_s = 0.0;
-  for (int c0 = 0; c0 < n; c0 += kStatChunk) {
-    const int m = min(kStatChunk, n - c0);
-    __syncthreads();
-    for (int e = threadIdx.x; e < m; e += kStatThreads) {
-      const double a = avg[base + c0 + e];
-      buf[e] = a > 0 ? a : 0.0;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) acc_s = seq_sum_lds(buf, m, acc_s);
-  }
+  const double* __restrict__ a = avg + base;
+  const double sum = seq_sum_exact([&](int j) { const double v = a[j]; return v > 0 ? v : 0.0; }, n, sh);
+  const double mean = sum / (double)n;
   __syncthreads();
-  const double mean = acc_s / (double)n;
-  __syncthreads();
-  if (threadIdx.x == 0) acc_s = 0.0;
-  for (int c0 = 0; c0 < n; c0 += kStatChunk) {
-    const int m = min(kStatChunk, n - c0);
-    __syncthreads();
-    for (int e = threadIdx.x; e < m; e += kStatThreads) {
-      const double a = avg[base + c0 + e];
-      buf[e] = a > 0 ? (a - mean) * (a - mean) : 0.0;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) acc_s = seq_sum_lds(buf, m, acc_s);
-  }
-  __syncthreads();
+  const double ss = seq_sum_exact(
+      [&](int j) {
+        const double v = a[j];
+        return v > 0 ? (v - mean) * (v - mean) : 0.0;
+      },
+      n, sh);
   if (threadIdx.x == 0) {
-    const double sd = n > 1 ? sqrt_rn(acc_s / (double)(n - 1)) : __builtin_nan("");
+    const double sd = n > 1 ? sqrt_rn(ss / (double)(n - 1)) : __builtin_nan("");
     thr[b] = mean + std_ratio * sd;
   }
+}
+
+// development entry (tests): out[0] = the ordered sum of v[0..n) (terms >= 0) by seq_sum_exact
+__global__ __launch_bounds__(kStatThreads) void seq_sum_dev_kernel(const double* __restrict__ v, int n,
+                                                                   double* __restrict__ out) {
+  __shared__ SeqShared sh;
+  const double r = seq_sum_exact([&](int j) { return v[j]; }, n, sh);
+  if (threadIdx.x == 0) out[0] = r;
 }
 
 // grid (ceil(nmax/1024), B) block 1024: per-chunk keep counts.
@@ -564,9 +710,10 @@ extern "C" int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, in
   hipStream_t s = pk::as_stream(stream);
   const int nchunk = (nmax + 1023) / 1024;
   if (nmax > 0) {
-    hipLaunchKernelGGL(sor_knn_kernel, dim3((nmax + kSorThreads - 1) / kSorThreads, B),
+    const int tiles = (nmax + kSorThreads - 1) / kSorThreads;
+    hipLaunchKernelGGL(sor_knn_kernel, dim3((unsigned)((int64_t)tiles * B)),
                        dim3(kSorThreads), 0, s, xyz, off, knn, pix, idxmap, H, W,
-                       pix != nullptr ? K : nullptr, avg);
+                       pix != nullptr ? K : nullptr, tiles, B, avg);
     PK_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(sor_stats_kernel, dim3(B), dim3(kStatThreads), 0, s, avg, off, std_ratio, thr);
@@ -745,6 +892,13 @@ extern "C" int pk_sample_rgb(const uint8_t* img, int F, int H, int W, int C, con
   PK_REQUIRE(img && K && pts && off && out);
   hipLaunchKernelGGL(sample_rgb_kernel, dim3((nmax + 255) / 256, F), dim3(256), 0, pk::as_stream(stream), img, H, W,
                      C, K, pts, off, out);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pkdev_seq_sum(const double* v, int n, double* out, void* stream) {
+  PK_REQUIRE(n >= 0 && out && (n == 0 || v));
+  hipLaunchKernelGGL(seq_sum_dev_kernel, dim3(1), dim3(kStatThreads), 0, pk::as_stream(stream), v, n, out);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -434,7 +434,11 @@ class PipelinedTrainer:
     def __init__(self, crop_formation: CropFormation, step: TrainStep, fb: FrameBatch, op: Operators,
                  warmup: int = 3):
         self.step, self.split = step, step.world > 1
-        self.main = torch.cuda.current_stream()
+        # development knob PK_MAIN_PRIORITY: run the training graphs on a stream of that priority
+        mp = os.environ.get("PK_MAIN_PRIORITY")
+        self.main = torch.cuda.Stream(priority=int(mp)) if mp else torch.cuda.current_stream()
+        if mp:
+            self.main.wait_stream(torch.cuda.current_stream())
         # crop-formation stream priority (development knob PK_SIDE_PRIORITY: torch's stream
         # priorities, lower number = higher priority; default 0, the main stream's)
         self.side = torch.cuda.Stream(priority=int(os.environ.get("PK_SIDE_PRIORITY", "0")))
@@ -474,6 +478,17 @@ class PipelinedTrainer:
             self.consumed[k].record(self.main)
         self.i = 0
         self._form(0)
+        # development knob PK_PIPE_THREAD=1: launch the crop graphs from a worker thread (graph
+        # launches block the host; the training stream should not wait behind them)
+        self._jobs = None
+        if os.environ.get("PK_PIPE_THREAD", "0") == "1":
+            import queue
+            import threading
+            self._jobs = queue.Queue()
+            self._queued = [threading.Event(), threading.Event()]
+            self._queued[0].set()
+            self._worker = threading.Thread(target=self._worker_loop, daemon=True)
+            self._worker.start()
 
     def _form(self, k):
         with torch.cuda.stream(self.side):
@@ -481,15 +496,31 @@ class PipelinedTrainer:
             self.crop_graphs[k].replay()
             self.formed[k].record(self.side)
 
+    def _worker_loop(self):
+        torch.cuda.set_device(self.main.device)
+        while True:
+            k = self._jobs.get()
+            if k is None:
+                return
+            self._form(k)
+            self._queued[k].set()
+
     def __call__(self) -> dict:
         k = self.i & 1
-        self._form(k ^ 1)                      # next batch's crops, concurrently
-        self.main.wait_event(self.formed[k])
-        self.train_a[k].replay()
-        if self.split:
-            self.step.allreduce_grads(self.grads[k])
-            self.train_b[k].replay()
-        self.consumed[k].record(self.main)
+        if self._jobs is not None:  # crop graphs launched from a second host thread
+            self._queued[k].wait()             # C_k enqueued (host side) before T_k waits on it
+            self._queued[k].clear()
+            self._queued[k ^ 1].clear()
+            self._jobs.put(k ^ 1)
+        else:
+            self._form(k ^ 1)                  # next batch's crops, concurrently
+        with torch.cuda.stream(self.main):
+            self.main.wait_event(self.formed[k])
+            self.train_a[k].replay()
+            if self.split:
+                self.step.allreduce_grads(self.grads[k])
+                self.train_b[k].replay()
+            self.consumed[k].record(self.main)
         self.i += 1
         return self.logs[k]
 

@@ -142,3 +142,55 @@ def test_sor_pixel_window_path_bitexact(device, with_K):
             continue
         np.testing.assert_array_equal(avg[off[b]:off[b + 1]], O.sor_avg_distances(c), err_msg=f"frame {b}")
         np.testing.assert_array_equal(kidx[oo[b]:oo[b + 1]], O.remove_outliers_indices(c))
+
+
+def _seq_sum(v):
+    s = 0.0
+    for x in v.tolist():
+        s = s + x  # IEEE double, round to nearest even, in order
+    return s
+
+
+def test_sor_ordered_sum_exact(device):
+    """The SOR statistics' ordered fp64 sums (std::accumulate order, object.py:33-50 via
+    Open3D) computed by binade-wise integer scans (crop.hip seq_sum_exact) equal the
+    sequential sum bit for bit: random magnitudes, zeros, exact ties (terms of half an ulp
+    of the running sum), terms larger than the sum, and every binade crossing."""
+    from dpfm_amd import _lib
+    rng = np.random.default_rng(11)
+    cases = [np.zeros(0), np.array([3.0]), rng.random(5), rng.random(256), rng.random(257),
+             rng.random(1000) * 7.3, rng.random(20000) * 0.01 + 1.0, rng.exponential(size=100000),
+             np.concatenate([np.zeros(3000), rng.random(9000)]),
+             np.concatenate([[2.0 ** 52], np.full(3000, 0.5), [1.5, 2.5, 0.5, 3.5]]),
+             np.concatenate([[2.0 ** 40], rng.integers(0, 8, 12000) * 2.0 ** -13]),
+             np.concatenate([rng.random(300), [1e300], rng.random(9000), [1e-300] * 50]),
+             np.ldexp(rng.integers(1, 2 ** 20, 30000).astype(np.float64), rng.integers(-30, 5, 30000)),
+             rng.random(12000) ** 8]
+    for i, v in enumerate(cases):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        t = torch.from_numpy(v).to(device)
+        out = torch.empty(1, dtype=torch.float64, device=device)
+        assert _lib.lib().pkdev_seq_sum(_lib.ptr(t), int(v.size), _lib.ptr(out), _lib.stream(device)) == 0
+        got = float(out.cpu()[0])
+        exp = _seq_sum(v)
+        assert got == exp, (i, got, exp, got - exp)
+
+
+def test_sor_threshold_bitexact(device):
+    """sor's per-crop threshold mean + 0.3 std equals the ordered-sum restatement exactly."""
+    from dpfm_amd import ops
+    import math
+    clouds = [O.dpt_2_pcld(d, 1000 / ds, k, m == 255) for d, m, k, ds in _frames()]
+    clouds = [c for c in clouds if c.shape[0] > 0]
+    x, off = _packed(clouds, device)
+    res = ops.sor(x, off, max(c.shape[0] for c in clouds), want_idx=True)
+    assert "thr" in res
+    thr = res["thr"].cpu().numpy()
+    for b, c in enumerate(clouds):
+        avg = O.sor_avg_distances(c)
+        n = avg.size
+        s = _seq_sum(np.where(avg > 0, avg, 0.0))
+        mean = s / n
+        ss = _seq_sum(np.where(avg > 0, (avg - mean) * (avg - mean), 0.0))
+        exp = mean + 0.3 * math.sqrt(ss / (n - 1))
+        assert thr[b] == exp, (b, thr[b], exp)

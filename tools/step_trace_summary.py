@@ -57,3 +57,27 @@ for r in mq[-per:]:
     gap = (s - prev) / 1e3 if prev is not None else 0.0
     prev = e
     print(f"{(e - s) / 1e3:7.1f} us  gap {gap:6.1f}  {short(r)}")
+
+# other queues over the last two steps, start/end relative to the start of the main queue's
+# second-to-last step (where crop formation overlaps the training step)
+if len(byq) > 1:
+    t0 = int(mq[-2 * per]["Start_Timestamp"])
+    print(f"\n--- main step boundaries (us from t0) ---")
+    for j in (2, 1):
+        a, z = mq[-j * per], mq[-(j - 1) * per - 1]
+        print(f"main step -{j}: {(int(a['Start_Timestamp']) - t0) / 1e3:8.1f} .. {(int(z['End_Timestamp']) - t0) / 1e3:8.1f}")
+    for q, rs in byq.items():
+        if rs is mq:
+            continue
+        print(f"--- queue {q}, kernels starting after t0 ---")
+        for r in rs:
+            s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            if s >= t0:
+                print(f"{(s - t0) / 1e3:8.1f} .. {(e - t0) / 1e3:8.1f}  {(e - s) / 1e3:7.1f} us  {short(r)}")
+    print("--- main queue: kernels starting after t0 with a gap > 10 us before them ---")
+    prev = None
+    for r in mq:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if s >= t0 and prev is not None and s - prev > 10000:
+            print(f"{(s - t0) / 1e3:8.1f}  gap {(s - prev) / 1e3:7.1f}  {short(r)}")
+        prev = e
