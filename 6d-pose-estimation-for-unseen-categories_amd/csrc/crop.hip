@@ -284,9 +284,13 @@ __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const
       const double fx = Kb[0], cx = Kb[2], fy = Kb[4], cy = Kb[5];
       const double r = sqrt(T) * (1.0 + 1e-9) + 1e-300;
       if (fx > 0.0 && fy > 0.0 && q2 > r) {
-        const double tx = fmax(fabs(cx), fabs((double)(W - 1) - cx)) / fx;
-        const double ty = fmax(fabs(cy), fabs((double)(H - 1) - cy)) / fy;
-        const double bu = fx * r * (1.0 + tx) / q2, bv = fy * r * (1.0 + ty) / q2;
+        // a candidate c within r of q: |X_q/Z_q - X_c/Z_c| <= (r/Z_q) sqrt(1 + t_c^2) (Cauchy-
+        // Schwarz on (X_q - X_c) + t_c (Z_c - Z_q)), with |t_c| <= the image bound tx and
+        // |t_c| <= (|t_q| + rho) / (1 - rho), rho = r / Z_q (SOR camera box)
+        const double rho = r / q2;
+        const double tx = fmin(fmax(fabs(cx), fabs((double)(W - 1) - cx)) / fx, (fabs(q0 / q2) + rho) / (1.0 - rho));
+        const double ty = fmin(fmax(fabs(cy), fabs((double)(H - 1) - cy)) / fy, (fabs(q1 / q2) + rho) / (1.0 - rho));
+        const double bu = fx * rho * sqrt(1.0 + tx * tx), bv = fy * rho * sqrt(1.0 + ty * ty);
         if (bu < 64.0 && bv < 64.0) {
           const int ru = (int)ceil(bu * (1.0 + 1e-9)) + 1, rv = (int)ceil(bv * (1.0 + 1e-9)) + 1;
           if ((2 * ru + 1) * (2 * rv + 1) <= kSorMaxBox) {

@@ -425,6 +425,10 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
   if (nmax <= 1024) PK_FPS(256, 4);
   if (nmax <= 2048) PK_FPS(256, 8);
   if (nmax <= 4096) PK_FPS(256, 16);
+#ifdef PK_FPS_LANE_ABOVE_4096  // development variant: per-lane buckets (no LDS point copy) above 4096
+  if (nmax <= 8192) return launch_fps_lane<1024, 8>(xyz, offsets, start, npoint, out, out_stride, B, s);
+  if (nmax <= 13312) return launch_fps_lane<1024, 13>(xyz, offsets, start, npoint, out, out_stride, B, s);
+#endif
   if (nmax <= 8192) PK_FPS(1024, 8);
   if (nmax <= 13312) PK_FPS(1024, 13);
 #undef PK_FPS

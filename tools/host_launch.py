@@ -96,3 +96,29 @@ def crop_only(n=30):
     return (time.perf_counter() - a) / n * 1e3
 print(f"wall per step: train graphs alone {train_only():.3f} ms, with the event pattern {events_only():.3f} ms, "
       f"crop graphs alone {crop_only():.3f} ms", flush=True)
+
+# the two graphs concurrently with no event coupling at all (T_k reads a buffer C_k may be
+# rewriting: timing only): pure interference between the streams
+def uncoupled(n=30):
+    torch.cuda.synchronize()
+    a = time.perf_counter()
+    for i in range(n):
+        k = i & 1
+        with torch.cuda.stream(side):
+            tr.crop_graphs[k ^ 1].replay()
+        tr.train_a[k].replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - a) / n * 1e3
+def coupled_one_way(n=30):  # T waits for C, C never waits for T
+    torch.cuda.synchronize()
+    a = time.perf_counter()
+    for i in range(n):
+        k = i & 1
+        with torch.cuda.stream(side):
+            tr.crop_graphs[k ^ 1].replay()
+            tr.formed[k ^ 1].record(side)
+        main.wait_event(tr.formed[k])
+        tr.train_a[k].replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - a) / n * 1e3
+print(f"uncoupled streams {uncoupled():.3f} ms/step, T waits for C only {coupled_one_way():.3f} ms/step", flush=True)
