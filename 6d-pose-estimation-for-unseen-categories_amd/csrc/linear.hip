@@ -747,15 +747,62 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
         __builtin_amdgcn_sched_barrier(0);  // keep the weight reads per chunk (no hoisting of all Q x TO)
       }
     }
-    // D[point 4 g + r][out t * 16 + m]
+    // D[point 4 g + r][out t * 16 + m]; the epilogue's operand loads (mask, add) for all
+    // TO x 4 outputs are issued before the first use, not one dependent load per store
+    // (workgroup-uniform branches around unconditional loads at clamped indices: no per-load
+    // exec-mask branch, so no wait per load)
+    float mk[TO][4], ad[TO][4];
+    if (e.mask != nullptr) {
 #pragma unroll
-    for (int t = 0; t < TO; ++t) {
-      {
-        const int o = t * 16 + m;
+      for (int t = 0; t < TO; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t pr = tile * 16 + 4 * g + r;
-          if (pr < R && o < Cout) lin_store_row(e, pr, o, Cout, acc[t][r] + bv[t]);
+          const int o = t * 16 + m;
+          const float v = e.mask[(pr < R && o < Cout) ? pr * Cout + o : 0];
+          mk[t][r] = v;
+        }
+    } else {
+#pragma unroll
+      for (int t = 0; t < TO; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mk[t][r] = 1.f;
+    }
+    if (e.add != nullptr) {
+#pragma unroll
+      for (int t = 0; t < TO; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t pr = tile * 16 + 4 * g + r;
+          const int o = t * 16 + m;
+          const bool ok = pr < R && o < e.add_cols;
+          const float v = e.add[ok ? pr * e.sa + o : 0];
+          ad[t][r] = ok ? v : 0.f;
+        }
+    } else {
+#pragma unroll
+      for (int t = 0; t < TO; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ad[t][r] = 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < TO; ++t) {
+      const int o = t * 16 + m;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t pr = tile * 16 + 4 * g + r;
+        if (pr < R && o < Cout) {
+          float v = lin_act(e.relu, acc[t][r] + bv[t]);
+          v = mk[t][r] <= 0.f ? 0.f : v;  // relu_mask
+          v += ad[t][r];  // 0 without add / past add_cols
+          if (e.store_cf) {
+            const int64_t b = pr / e.N, n = pr - b * e.N;
+            e.y[b * e.sy + (int64_t)o * e.N + n] = v;
+          } else if (o >= e.split) {
+            e.y2[pr * e.sy2 + (o - e.split)] = v;
+          } else {
+            e.y[pr * e.sy + o] = v;
+          }
         }
       }
     }
@@ -830,22 +877,58 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
   const int64_t pn = n0 + SUB * m;
   float* yb = e.y + bb * e.sy + pn;
   const int64_t mb = bb * Cout * (int64_t)N + pn;  // contiguous index (mask)
+  // epilogue operands (mask, add) of all TO x 4 output rows loaded before the first use:
+  // workgroup-uniform branches around unconditional loads at clamped rows
+  V mv[TO][4], av[TO][4];
+  float bo4[TO][4];
+#pragma unroll
+  for (int t = 0; t < TO; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = t * 16 + 4 * g + r;
+      bo4[t][r] = 0.f;
+      if (bias != nullptr) {
+        const float b = bias[o < Cout ? o : 0];
+        bo4[t][r] = o < Cout ? b : 0.f;
+      }
+    }
+  if (e.mask != nullptr) {
+#pragma unroll
+    for (int t = 0; t < TO; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = t * 16 + 4 * g + r;
+        mv[t][r] = *reinterpret_cast<const V*>(e.mask + mb + (int64_t)(o < Cout ? o : 0) * N);
+      }
+  }
+  if (e.add != nullptr) {
+#pragma unroll
+    for (int t = 0; t < TO; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = t * 16 + 4 * g + r;
+        av[t][r] = *reinterpret_cast<const V*>(e.add + bb * e.sa + (int64_t)(o < e.add_cols ? o : 0) * N + pn);
+      }
+  }
 #pragma unroll
   for (int t = 0; t < TO; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int o = t * 16 + 4 * g + r;
       if (o < Cout) {
-        const float bo = bias != nullptr ? bias[o] : 0.f;
-        V v;
-        V av;
+        const float bo = bo4[t][r];
         const bool has_add = e.add != nullptr && o < e.add_cols;
-        if (has_add) av = *reinterpret_cast<const V*>(e.add + bb * e.sa + (int64_t)o * N + pn);
+        V v;
 #pragma unroll
         for (int u = 0; u < SUB; ++u) {
-          float z = lin_epi(e, acc[t][u][r] + bo, mb + (int64_t)o * N + u);
+          float z = lin_act(e.relu, acc[t][u][r] + bo);
+          if (e.mask != nullptr) {
+            float mz;
+            if constexpr (SUB == 1) mz = mv[t][r]; else mz = mv[t][r][u];
+            z = mz <= 0.f ? 0.f : z;
+          }
           if (has_add) {
-            if constexpr (SUB == 1) z += av; else z += av[u];
+            if constexpr (SUB == 1) z += av[t][r]; else z += av[t][r][u];
           }
           if constexpr (SUB == 1) v = z; else v[u] = z;
         }
@@ -887,8 +970,29 @@ __global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restric
     float acc[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[u] = o0 + u < Cout ? bs[o0 + u] : 0.f;
+    int k0 = 0;
+    if (CINT == 0 && e.pre == nullptr && ((sx | Cin) & 3) == 0 && (((uintptr_t)x) & 15) == 0) {
+      // wide input rows (e.g. the overlap head's 32 -> 1): 16-B loads, all issued up front
+      const float4* xr = reinterpret_cast<const float4*>(x + r * sx);
+      for (; k0 + 16 <= Cin; k0 += 16) {
+        float4 q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = xr[(k0 >> 2) + j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float xs[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int k = k0 + 4 * j + i;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (o0 + u < Cout) acc[u] = fmaf(xs[i], Ws[(o0 + u) * Cin + k], acc[u]);
+          }
+        }
+      }
+    }
 #pragma unroll 4
-    for (int k = 0; k < Cin; ++k) {
+    for (int k = k0; k < Cin; ++k) {
       float xv = x[r * sx + k];
       if (e.pre) {
         const float s = e.pre[r * sx + k];
@@ -899,8 +1003,13 @@ __global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restric
       for (int u = 0; u < 4; ++u)
         if (o0 + u < Cout) acc[u] = fmaf(xv, Ws[(o0 + u) * Cin + k], acc[u]);
     }
+    float mk[4] = {1.f, 1.f, 1.f, 1.f};
+    if (mask != nullptr) {  // workgroup-uniform; the loads at clamped indices, then one wait
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = relu_mask(lin_act(relu, acc[u]), mask, r * Cout + o0 + u);
+      for (int u = 0; u < 4; ++u) mk[u] = mask[r * Cout + (o0 + u < Cout ? o0 + u : 0)];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = mk[u] <= 0.f ? 0.f : lin_act(relu, acc[u]);
     if ((Cout & 3) == 0 && (e.sy & 3) == 0) {
       *reinterpret_cast<float4*>(y + r * e.sy + o0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
     } else {
