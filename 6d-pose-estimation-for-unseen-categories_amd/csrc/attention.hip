@@ -31,6 +31,7 @@
 namespace {
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
 constexpr int kD = 16;       // head dim
 constexpr int kT = 64;       // rows per tile / per workgroup
 constexpr int kSR = 80;      // LDS stride of [d][row] arrays (bank-conflict-free MFMA reads)
@@ -122,32 +123,46 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
 #pragma unroll
       for (int s = 0; s < 4; ++s) st[t] = mfma(Ks[(4 * s + g) * kSR + 16 * t + c], qr[s], st[t]);
     }
+    if (k0 + kT > M) {  // workgroup-uniform: only a ragged last tile has keys past M
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (k0 + 16 * t + 4 * g + r >= M) st[t][r] = -__builtin_huge_valf();
+    }
     float mt = -__builtin_huge_valf();
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (k0 + 16 * t + 4 * g + r >= M) st[t][r] = -__builtin_huge_valf();
-        mt = fmaxf(mt, st[t][r]);
-      }
+      for (int r = 0; r < 4; ++r) mt = fmaxf(mt, st[t][r]);
     mt = grp_max(mt);
     const float mn = fmaxf(m, mt);
     const float alpha = m == -__builtin_huge_valf() ? 0.f : exp2_((m - mn) * kLog2e);
     m = mn;
-    float ps = 0.f;
+    // (s - m) log2 e on packed f32 pairs (v_pk_add_f32 / v_pk_mul_f32: the same per-element
+    // rounding), row sums in two pair lanes
+    const f32x2 mn2 = {mn, mn}, l2e = {kLog2e, kLog2e};
+    f32x2 ps2 = {0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = exp2_((st[t][r] - mn) * kLog2e);
-        st[t][r] = p;
-        ps += p;
+      for (int r = 0; r < 4; r += 2) {
+        f32x2 d = {st[t][r], st[t][r + 1]};
+        d = (d - mn2) * l2e;
+        const f32x2 p = {exp2_(d.x), exp2_(d.y)};
+        st[t][r] = p.x;
+        st[t][r + 1] = p.y;
+        ps2 += p;
       }
-    l = l * alpha + ps;
+    l = l * alpha + (ps2.x + ps2.y);
+    const f32x2 al2 = {alpha, alpha};
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[t][r] *= alpha;
+    for (int t = 0; t < 4; ++t) {
+      f32x2 a0 = {acc[t][0], acc[t][1]}, a1 = {acc[t][2], acc[t][3]};
+      a0 *= al2;
+      a1 *= al2;
+      acc[t] = f32x4{a0.x, a0.y, a1.x, a1.y};
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
