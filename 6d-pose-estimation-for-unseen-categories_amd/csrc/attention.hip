@@ -229,12 +229,27 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
         st = mfma(Ks[(4 * s + g) * kSR + 16 * t + c], qr[s], st);
         dp = mfma(Vs[(4 * s + g) * kSR + 16 * t + c], dor[s], dp);
       }
+      // packed pairs (v_pk_*: the same per-element rounding as the scalar ops)
+      float pr[4], dsr[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = k0 + 16 * t + 4 * g + r < M ? exp2_((st[r] - ms.x) * kLog2e) * ms.y : 0.f;
-        const float ds = p * (dp[r] - dl);
-        acc[t] = mfma(KT[(16 * t + 4 * g + r) * kSC + c], ds, acc[t]);
+      for (int r = 0; r < 4; r += 2) {
+        f32x2 d = {st[r], st[r + 1]};
+        d = (d - f32x2{ms.x, ms.x}) * f32x2{kLog2e, kLog2e};
+        f32x2 pp = f32x2{exp2_(d.x), exp2_(d.y)} * f32x2{ms.y, ms.y};
+        const f32x2 ds = pp * (f32x2{dp[r], dp[r + 1]} - f32x2{dl, dl});
+        pr[r] = pp.x;
+        pr[r + 1] = pp.y;
+        dsr[r] = ds.x;
+        dsr[r + 1] = ds.y;
       }
+      if (k0 + kT > M) {  // workgroup-uniform: keys past M (ragged last tile) carry no weight
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (k0 + 16 * t + 4 * g + r >= M) dsr[r] = 0.f;
+      }
+      (void)pr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[t] = mfma(KT[(16 * t + 4 * g + r) * kSC + c], dsr[r], acc[t]);
     }
   }
   const f32x4 accs = (acc[0] + acc[1]) + (acc[2] + acc[3]);
@@ -252,7 +267,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
   __shared__ float Os[kD * kSR];  // dO as [d][q]
   __shared__ float QT[kT * kSC];
   __shared__ float OT[kT * kSC];  // dO as [q][d]
-  __shared__ float Ls[kT], Is[kT], Ds[kT];
+  __shared__ __attribute__((aligned(16))) float Ls[kT];
+  __shared__ __attribute__((aligned(16))) float Is[kT];
+  __shared__ __attribute__((aligned(16))) float Ds[kT];
   const int h = blockIdx.y, b = blockIdx.z;
   const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
   const int kj = blockIdx.x * kT + pk::wave_id() * 16 + c;
@@ -298,13 +315,29 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
         st = mfma(Qs[(4 * s + g) * kSR + 16 * t + c], kr[s], st);  // S[q][key]
         dp = mfma(Os[(4 * s + g) * kSR + 16 * t + c], vr[s], dp);  // dP[q][key]
       }
+      // per-query (m, 1 / sum, delta) of queries 16 t + 4 g .. + 3 as 16-B LDS reads; packed pairs
+      const float4 L4 = *reinterpret_cast<const float4*>(&Ls[16 * t + 4 * g]);
+      const float4 I4 = *reinterpret_cast<const float4*>(&Is[16 * t + 4 * g]);
+      const float4 D4 = *reinterpret_cast<const float4*>(&Ds[16 * t + 4 * g]);
+      float pr[4], dsr[4];
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        const f32x2 Lp = r == 0 ? f32x2{L4.x, L4.y} : f32x2{L4.z, L4.w};
+        const f32x2 Ip = r == 0 ? f32x2{I4.x, I4.y} : f32x2{I4.z, I4.w};
+        const f32x2 Dp = r == 0 ? f32x2{D4.x, D4.y} : f32x2{D4.z, D4.w};
+        f32x2 d = (f32x2{st[r], st[r + 1]} - Lp) * f32x2{kLog2e, kLog2e};
+        const f32x2 pp = f32x2{exp2_(d.x), exp2_(d.y)} * Ip;
+        const f32x2 ds = pp * (f32x2{dp[r], dp[r + 1]} - Dp);
+        pr[r] = pp.x;
+        pr[r + 1] = pp.y;
+        dsr[r] = ds.x;
+        dsr[r + 1] = ds.y;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = 16 * t + 4 * g + r;
-        const float p = exp2_((st[r] - Ls[qq]) * kLog2e) * Is[qq];
-        const float ds = p * (dp[r] - Ds[qq]);
-        dva[t & 1] = mfma(OT[qq * kSC + c], p, dva[t & 1]);   // dV^T[d][key] += dO^T[d][q] P[q][key]
-        dka[t & 1] = mfma(QT[qq * kSC + c], ds, dka[t & 1]);  // dK^T[d][key] += Q^T[d][q] dS[q][key]
+        dva[t & 1] = mfma(OT[qq * kSC + c], pr[r], dva[t & 1]);   // dV^T[d][key] += dO^T[d][q] P[q][key]
+        dka[t & 1] = mfma(QT[qq * kSC + c], dsr[r], dka[t & 1]);  // dK^T[d][key] += Q^T[d][q] dS[q][key]
       }
     }
   }
