@@ -1,0 +1,397 @@
+// (f4) Point-to-point ICP refinement after RANSAC, batched over crops.
+//
+// Reference: scripts/test_RANSAC.py:436-446 -> Open3D 0.17 registration_icp(source, target,
+// threshold = 0.2, trans_init = T_RANSAC, TransformationEstimationPointToPoint(),
+// ICPConvergenceCriteria(max_iteration = 2000)) (relative_fitness = relative_rmse = 1e-6, the
+// defaults). Open3D's loop:
+//   result_0 = evaluate(T_0)
+//   for i < max_iteration: U = umeyama(matched source, matched target); T <- U T;
+//                          result_{i+1} = evaluate(T);
+//                          stop if |dfitness| < rel_fitness and |drmse| < rel_rmse
+// evaluate(T): every source point p = T s takes its nearest target point (KD-tree hybrid search,
+// radius = threshold, max_nn = 1: a pair iff d^2 < threshold^2, nanoflann's strict radius test);
+// fitness = pairs / |source|, inlier_rmse = sqrt(sum d^2 / pairs) (0 without pairs); no pairs
+// gives U = I. Deviations (documented, parity unpinned against Open3D): the source is
+// transformed by the accumulated T each iteration (Open3D re-transforms its working copy by
+// every U, compounding roundings), and an exact distance tie goes to the lowest target index
+// (a KD-tree returns either).
+//
+// The reference aligns the CAD to the GT-posed CAD (its target); the host mirror also offers
+// the observed crop as the target (pose refinement without ground truth).
+//
+// Design: the target of each crop is sorted once by x (rank by counting, fp64 keys, index
+// tie-break); a query scans only the x-slab [px - r, px + r] found by binary search, so a
+// 0.2 cm radius on a 10-20 cm object touches a few dozen candidates instead of the whole
+// target. Per iteration two launches: match (grid = source blocks x crops: nearest target,
+// pair test, block partial sums of count, sum d^2, the matched source and target points and
+// their products, shifted by the crop's first target point against cancellation) and update
+// (one wave per crop: partials in block order, the convergence test, Horn's quaternion fit of
+// the centred cross-covariance — pk_rigid, shared with RANSAC — and T <- U T). Converged crops
+// return at the top of both kernels, so a host loop can enqueue iterations in batches and
+// poll a device count of active crops.
+#include "common.hpp"
+#include "rigid.hpp"
+
+namespace {
+
+constexpr int kIThreads = 256;
+constexpr int kNPart = 17;  // count, sum d^2, sum p (3), sum q (3), sum p q^T (9)
+
+struct IcpState {  // per crop, in the work buffer
+  double T[16];
+  double fit, rmse, prev_fit, prev_rmse;
+  int iter, active, converged, pad;
+};
+
+struct IcpWork {
+  IcpState* st;
+  double* sx;     // [B][ntgt_max] sorted x
+  double* sp;     // [B][ntgt_max][3] points in x order
+  int32_t* sidx;  // [B][ntgt_max] original index
+  double* part;   // [B][nblk][kNPart]
+};
+
+__host__ __device__ inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+__host__ __device__ inline IcpWork carve(void* w, int B, int nsrc_max, int ntgt_max) {
+  char* p = static_cast<char*>(w);
+  const int64_t nblk = (nsrc_max + kIThreads - 1) / kIThreads;
+  IcpWork o;
+  o.st = reinterpret_cast<IcpState*>(p);
+  p += al256((int64_t)B * sizeof(IcpState));
+  o.sx = reinterpret_cast<double*>(p);
+  p += al256((int64_t)B * ntgt_max * 8);
+  o.sp = reinterpret_cast<double*>(p);
+  p += al256((int64_t)B * ntgt_max * 24);
+  o.sidx = reinterpret_cast<int32_t*>(p);
+  p += al256((int64_t)B * ntgt_max * 4);
+  o.part = reinterpret_cast<double*>(p);
+  (void)nblk;
+  return o;
+}
+
+inline int64_t work_bytes_for(int B, int nsrc_max, int ntgt_max) {
+  const int64_t nblk = (nsrc_max + kIThreads - 1) / kIThreads;
+  return al256((int64_t)B * sizeof(IcpState)) + al256((int64_t)B * ntgt_max * 8) + al256((int64_t)B * ntgt_max * 24) +
+         al256((int64_t)B * ntgt_max * 4) + al256((int64_t)B * (nblk > 0 ? nblk : 1) * kNPart * 8);
+}
+
+// grid (B): T <- T_init, counters reset.
+__global__ void icp_init_kernel(const double* __restrict__ T_init, IcpState* __restrict__ st) {
+  const int b = blockIdx.x;
+  if (threadIdx.x < 16) st[b].T[threadIdx.x] = T_init[16 * b + threadIdx.x];
+  if (threadIdx.x == 0) {
+    st[b].fit = st[b].rmse = st[b].prev_fit = st[b].prev_rmse = 0.0;
+    st[b].iter = 0;
+    st[b].active = 1;
+    st[b].converged = 0;
+  }
+}
+
+// grid (ceil(ntgt_max / 256), B): each point's rank in (x, index) order by counting over the
+// crop's x values staged through LDS; scatter into the sorted arrays.
+__global__ __launch_bounds__(kIThreads) void icp_sort_kernel(const double* __restrict__ tgt,
+                                                             const int64_t* __restrict__ tgt_off, int ntgt_max,
+                                                             double* __restrict__ sx, double* __restrict__ sp,
+                                                             int32_t* __restrict__ sidx) {
+  constexpr int kTile = 2048;
+  __shared__ double xs[kTile];
+  const int b = blockIdx.y;
+  const int64_t t0 = tgt_off[b];
+  const int nt = (int)(tgt_off[b + 1] - t0);
+  if ((int)blockIdx.x * kIThreads >= nt) return;  // block-uniform
+  const double* T = tgt + 3 * t0;
+  const int i = blockIdx.x * kIThreads + threadIdx.x;
+  const bool own = i < nt;
+  const double xi = own ? T[3 * i] : 0.0;
+  int rank = 0;
+  for (int j0 = 0; j0 < nt; j0 += kTile) {
+    const int jn = min(kTile, nt - j0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < jn; j += kIThreads) xs[j] = T[3 * (j0 + j)];
+    __syncthreads();
+    if (own) {
+      for (int j = 0; j < jn; ++j) {
+        const double xj = xs[j];
+        rank += (xj < xi) || (xj == xi && j0 + j < i);
+      }
+    }
+  }
+  if (!own) return;
+  const int64_t o = (int64_t)b * ntgt_max + rank;
+  sx[o] = xi;
+  sp[3 * o] = xi;
+  sp[3 * o + 1] = T[3 * i + 1];
+  sp[3 * o + 2] = T[3 * i + 2];
+  sidx[o] = i;
+}
+
+__device__ __forceinline__ void block_sum(double v[kNPart], double* __restrict__ out) {
+  __shared__ double red[kIThreads / 64][kNPart];
+#pragma unroll
+  for (int k = 0; k < kNPart; ++k) {
+    double x = v[k];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
+    v[k] = x;
+  }
+  if (pk::lane_id() == 0)
+#pragma unroll
+    for (int k = 0; k < kNPart; ++k) red[pk::wave_id()][k] = v[k];
+  __syncthreads();
+  if (threadIdx.x < kNPart) {
+    double s = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < kIThreads / 64; ++w) s += red[w][threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+}
+
+// grid (nblk, B): nearest target point of each transformed source point inside the x-slab;
+// the block's partial sums of the matched pairs (shifted by the crop's first target point).
+__global__ __launch_bounds__(kIThreads) void icp_match_kernel(
+    const double* __restrict__ src, const int64_t* __restrict__ src_off, const double* __restrict__ tgt,
+    const int64_t* __restrict__ tgt_off, double r, int ntgt_max, int nblk, const IcpState* __restrict__ st,
+    const double* __restrict__ sx, const double* __restrict__ sp, const int32_t* __restrict__ sidx,
+    double* __restrict__ part) {
+  const int b = blockIdx.y;
+  if (!st[b].active) return;  // block-uniform
+  const int64_t s0 = src_off[b];
+  const int ns = (int)(src_off[b + 1] - s0);
+  const int64_t t0 = tgt_off[b];
+  const int nt = (int)(tgt_off[b + 1] - t0);
+  const int i = blockIdx.x * kIThreads + threadIdx.x;
+  double acc[kNPart];
+#pragma unroll
+  for (int k = 0; k < kNPart; ++k) acc[k] = 0.0;
+  if (i < ns && nt > 0) {
+    const double* M = st[b].T;
+    const double* s = src + 3 * (s0 + i);
+    const double x = s[0], y = s[1], z = s[2];
+    const double px = ((M[0] * x + M[1] * y) + M[2] * z) + M[3];
+    const double py = ((M[4] * x + M[5] * y) + M[6] * z) + M[7];
+    const double pz = ((M[8] * x + M[9] * y) + M[10] * z) + M[11];
+    const double* X = sx + (int64_t)b * ntgt_max;
+    const double* Pp = sp + 3 * (int64_t)b * ntgt_max;
+    const int32_t* I = sidx + (int64_t)b * ntgt_max;
+    // first k with X[k] >= px - r
+    const double lo_x = px - r, hi_x = px + r;
+    int lo = 0, hi = nt;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (X[mid] < lo_x) lo = mid + 1;
+      else hi = mid;
+    }
+    double best = INFINITY;
+    int bi = INT32_MAX, bk = -1;
+    for (int k = lo; k < nt; ++k) {
+      const double qx = Pp[3 * k];
+      if (qx > hi_x) break;
+      const double dx = px - qx, dy = py - Pp[3 * k + 1], dz = pz - Pp[3 * k + 2];
+      const double d2 = (dx * dx + dy * dy) + dz * dz;
+      const int id = I[k];
+      if (d2 < best || (d2 == best && id < bi)) {
+        best = d2;
+        bi = id;
+        bk = k;
+      }
+    }
+    if (bk >= 0 && best < r * r) {
+      const double* c = tgt + 3 * t0;  // shift: the crop's first target point
+      const double ax = px - c[0], ay = py - c[1], az = pz - c[2];
+      const double bx = Pp[3 * bk] - c[0], by = Pp[3 * bk + 1] - c[1], bz = Pp[3 * bk + 2] - c[2];
+      acc[0] = 1.0;
+      acc[1] = best;
+      acc[2] = ax; acc[3] = ay; acc[4] = az;
+      acc[5] = bx; acc[6] = by; acc[7] = bz;
+      acc[8] = ax * bx; acc[9] = ax * by; acc[10] = ax * bz;
+      acc[11] = ay * bx; acc[12] = ay * by; acc[13] = ay * bz;
+      acc[14] = az * bx; acc[15] = az * by; acc[16] = az * bz;
+    }
+  }
+  block_sum(acc, part + ((int64_t)b * nblk + blockIdx.x) * kNPart);
+}
+
+// grid (B), one wave: partials in block order -> (fitness, rmse); convergence test against the
+// previous evaluation; otherwise U = rigid fit of the pairs and T <- U T.
+__global__ __launch_bounds__(64) void icp_update_kernel(const int64_t* __restrict__ src_off,
+                                                        const double* __restrict__ tgt,
+                                                        const int64_t* __restrict__ tgt_off, int nblk, int max_iter,
+                                                        double rel_fit, double rel_rmse, IcpState* __restrict__ st,
+                                                        const double* __restrict__ part) {
+  const int b = blockIdx.x;
+  IcpState& S = st[b];
+  if (!S.active) return;
+  const int lane = threadIdx.x;
+  double v = 0.0;
+  if (lane < kNPart)
+    for (int k = 0; k < nblk; ++k) v += part[((int64_t)b * nblk + k) * kNPart + lane];
+  double a[kNPart];
+#pragma unroll
+  for (int k = 0; k < kNPart; ++k) a[k] = __shfl(v, k);
+  if (lane != 0) return;
+  const int ns = (int)(src_off[b + 1] - src_off[b]);
+  const double cnt = a[0];
+  const double fit = (cnt > 0.0 && ns > 0) ? cnt / (double)ns : 0.0;
+  const double rmse = cnt > 0.0 ? sqrt(a[1] / cnt) : 0.0;
+  const int e = S.iter;
+  bool done = false;
+  if (e > 0 && fabs(S.fit - fit) < rel_fit && fabs(S.rmse - rmse) < rel_rmse) {
+    done = true;
+    S.converged = 1;
+  } else if (e >= max_iter) {
+    done = true;
+  }
+  S.prev_fit = S.fit;
+  S.prev_rmse = S.rmse;
+  S.fit = fit;
+  S.rmse = rmse;
+  if (done) {
+    S.active = 0;
+    return;
+  }
+  double U[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+  if (cnt > 0.0) {
+    const double inv = 1.0 / cnt;
+    const double* c = tgt + 3 * tgt_off[b];
+    double ms[3], md[3], Sg[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      ms[k] = a[2 + k] * inv;
+      md[k] = a[5 + k] * inv;
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) Sg[r][q] = a[8 + 3 * r + q] * inv - ms[r] * md[q];
+    double R[9], t[3];
+    pk_rigid::rigid_from_cov(Sg, ms, md, R, t);
+    // t was fitted in shifted coordinates: p - c -> R (p - c) + t = R p + (t + c - R c)
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      U[4 * r + 0] = R[3 * r + 0];
+      U[4 * r + 1] = R[3 * r + 1];
+      U[4 * r + 2] = R[3 * r + 2];
+      U[4 * r + 3] = (t[r] + c[r]) - ((R[3 * r] * c[0] + R[3 * r + 1] * c[1]) + R[3 * r + 2] * c[2]);
+    }
+  }
+  double Tn[16];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      Tn[4 * r + q] = ((U[4 * r] * S.T[q] + U[4 * r + 1] * S.T[4 + q]) + U[4 * r + 2] * S.T[8 + q]) +
+                      U[4 * r + 3] * S.T[12 + q];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) S.T[k] = Tn[k];
+  S.iter = e + 1;
+}
+
+// grid (1): number of crops still iterating.
+__global__ void icp_count_kernel(const IcpState* __restrict__ st, int B, int32_t* __restrict__ out) {
+  int c = 0;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) c += st[b].active;
+  c = pk::wave_sum_i32(c);
+  if (threadIdx.x == 0) *out = c;
+}
+
+// grid (B): T and (fitness, inlier_rmse, iterations, converged).
+__global__ void icp_result_kernel(const IcpState* __restrict__ st, double* __restrict__ T,
+                                  double* __restrict__ stats) {
+  const int b = blockIdx.x;
+  if (threadIdx.x < 16) T[16 * b + threadIdx.x] = st[b].T[threadIdx.x];
+  if (threadIdx.x == 0) {
+    stats[4 * b + 0] = st[b].fit;
+    stats[4 * b + 1] = st[b].rmse;
+    stats[4 * b + 2] = (double)st[b].iter;
+    stats[4 * b + 3] = (double)st[b].converged;
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t pk_icp_work_size(int B, int nsrc_max, int ntgt_max) {
+  if (B <= 0 || nsrc_max < 0 || ntgt_max < 0) return 0;
+  return work_bytes_for(B, nsrc_max, ntgt_max);
+}
+
+extern "C" int pk_icp_init(const double* tgt, const int64_t* tgt_off, const double* T_init, int B, int nsrc_max,
+                           int ntgt_max, void* work, int64_t work_bytes, void* stream) {
+  PK_REQUIRE(B >= 0 && nsrc_max >= 0 && ntgt_max >= 0);
+  if (B == 0) return PK_OK;
+  PK_REQUIRE(tgt && tgt_off && T_init && work);
+  PK_REQUIRE(work_bytes >= work_bytes_for(B, nsrc_max, ntgt_max));
+  hipStream_t s = pk::as_stream(stream);
+  const IcpWork w = carve(work, B, nsrc_max, ntgt_max);
+  hipLaunchKernelGGL(icp_init_kernel, dim3(B), dim3(64), 0, s, T_init, w.st);
+  PK_CHECK_LAUNCH();
+  if (ntgt_max > 0) {
+    hipLaunchKernelGGL(icp_sort_kernel, dim3((ntgt_max + kIThreads - 1) / kIThreads, B), dim3(kIThreads), 0, s, tgt,
+                       tgt_off, ntgt_max, w.sx, w.sp, w.sidx);
+    PK_CHECK_LAUNCH();
+  }
+  return PK_OK;
+}
+
+extern "C" int pk_icp_iterate(const double* src, const int64_t* src_off, const double* tgt, const int64_t* tgt_off,
+                              double max_dist, int max_iter, double rel_fitness, double rel_rmse, int B, int nsrc_max,
+                              int ntgt_max, int steps, void* work, int64_t work_bytes, int32_t* active_count,
+                              void* stream) {
+  PK_REQUIRE(B >= 0 && nsrc_max >= 0 && ntgt_max >= 0 && steps >= 0 && max_iter >= 0 && max_dist > 0.0);
+  if (B == 0) return PK_OK;
+  PK_REQUIRE(src && src_off && tgt && tgt_off && work);
+  PK_REQUIRE(work_bytes >= work_bytes_for(B, nsrc_max, ntgt_max));
+  hipStream_t s = pk::as_stream(stream);
+  const IcpWork w = carve(work, B, nsrc_max, ntgt_max);
+  const int nblk = nsrc_max > 0 ? (nsrc_max + kIThreads - 1) / kIThreads : 1;
+  for (int k = 0; k < steps; ++k) {
+    hipLaunchKernelGGL(icp_match_kernel, dim3(nblk, B), dim3(kIThreads), 0, s, src, src_off, tgt, tgt_off, max_dist,
+                       ntgt_max, nblk, w.st, w.sx, w.sp, w.sidx, w.part);
+    PK_CHECK_LAUNCH();
+    hipLaunchKernelGGL(icp_update_kernel, dim3(B), dim3(64), 0, s, src_off, tgt, tgt_off, nblk, max_iter,
+                       rel_fitness, rel_rmse, w.st, w.part);
+    PK_CHECK_LAUNCH();
+  }
+  if (active_count) {
+    hipLaunchKernelGGL(icp_count_kernel, dim3(1), dim3(64), 0, s, w.st, B, active_count);
+    PK_CHECK_LAUNCH();
+  }
+  return PK_OK;
+}
+
+extern "C" int pk_icp_result(const void* work, int B, double* T, double* stats, void* stream) {
+  PK_REQUIRE(B >= 0);
+  if (B == 0) return PK_OK;
+  PK_REQUIRE(work && T && stats);
+  const IcpWork w = carve(const_cast<void*>(work), B, 0, 0);
+  hipLaunchKernelGGL(icp_result_kernel, dim3(B), dim3(64), 0, pk::as_stream(stream), w.st, T, stats);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+// Blocking driver: init, then batches of `poll` iterations until no crop is active (one
+// 4-byte device-to-host read per batch), then the result. Every crop runs at most
+// max_iter + 1 evaluations.
+extern "C" int pk_icp(const double* src, const int64_t* src_off, const double* tgt, const int64_t* tgt_off,
+                      const double* T_init, double max_dist, int max_iter, double rel_fitness, double rel_rmse, int B,
+                      int nsrc_max, int ntgt_max, int poll, void* work, int64_t work_bytes, int32_t* dev_count,
+                      double* T, double* stats, void* stream) {
+  PK_REQUIRE(poll > 0 && dev_count);
+  int rc = pk_icp_init(tgt, tgt_off, T_init, B, nsrc_max, ntgt_max, work, work_bytes, stream);
+  if (rc) return rc;
+  if (B == 0) return PK_OK;
+  hipStream_t s = pk::as_stream(stream);
+  for (int done = 0; done <= max_iter;) {
+    const int steps = min(poll, max_iter + 1 - done);
+    rc = pk_icp_iterate(src, src_off, tgt, tgt_off, max_dist, max_iter, rel_fitness, rel_rmse, B, nsrc_max, ntgt_max,
+                        steps, work, work_bytes, dev_count, stream);
+    if (rc) return rc;
+    done += steps;
+    int32_t active = 0;
+    hipError_t e = hipMemcpyAsync(&active, dev_count, sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return (int)e;
+    if (active == 0) break;
+  }
+  return pk_icp_result(work, B, T, stats, stream);
+}

@@ -84,10 +84,15 @@ SIGNATURES = {
     "pk_erode_mask": [_P, _I, _I, _I, _P, _P],
     "pk_sample_rgb": [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],
     "pk_sample_features": [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],
+    "pk_icp_work_size": [_I, _I, _I],
+    "pk_icp_init": [_P, _P, _P, _I, _I, _I, _P, _I64, _P],
+    "pk_icp_iterate": [_P, _P, _P, _P, _D, _I, _D, _D, _I, _I, _I, _I, _P, _I64, _P, _P],
+    "pk_icp_result": [_P, _I, _P, _P, _P],
+    "pk_icp": [_P, _P, _P, _P, _P, _D, _I, _D, _D, _I, _I, _I, _I, _P, _I64, _P, _P, _P, _P],
 }
 
 RESTYPES = {"pk_cgt_lstsq_work_size": _I64, "pk_linear_wgrad_grouped_work": _I64, "pk_ransac_work_size": _I64,
-            "pk_feat_dist_work_size": _I64, "pk_fmap_head_work_len": _I64}  # everything else returns an int status
+            "pk_feat_dist_work_size": _I64, "pk_fmap_head_work_len": _I64, "pk_icp_work_size": _I64}  # everything else returns an int status
 
 _lib: Optional[ctypes.CDLL] = None
 

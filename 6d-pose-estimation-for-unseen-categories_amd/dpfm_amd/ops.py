@@ -1006,6 +1006,40 @@ def ransac(src: torch.Tensor, src_off: torch.Tensor, dst: torch.Tensor, dst_off:
     return T, stats
 
 
+def icp(src: torch.Tensor, src_off: torch.Tensor, tgt: torch.Tensor, tgt_off: torch.Tensor, T_init: torch.Tensor,
+        max_dist: float, max_iter: int = 30, rel_fitness: float = 1e-6, rel_rmse: float = 1e-6,
+        nsrc_max: Optional[int] = None, ntgt_max: Optional[int] = None, poll: int = 8):
+    """Batched point-to-point ICP (pk_icp_init / pk_icp_iterate / pk_icp_result). Iterations are
+    enqueued `poll` at a time; between batches the host reads the device count of crops still
+    iterating (one 4-byte read). Returns (T f64 [B,4,4], stats f64 [B,4] = fitness, inlier rmse,
+    updates, converged)."""
+    B = src_off.numel() - 1
+    dev = src.device
+    if nsrc_max is None:
+        nsrc_max = int((src_off[1:] - src_off[:-1]).max()) if B else 0
+    if ntgt_max is None:
+        ntgt_max = int((tgt_off[1:] - tgt_off[:-1]).max()) if B else 0
+    T0 = T_init.to(dtype=torch.float64).reshape(B, 16).contiguous()
+    nbytes = int(_lib.lib().pk_icp_work_size(B, int(nsrc_max), int(ntgt_max)))
+    work = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros((1,), dtype=torch.int32, device=dev)
+    s = _lib.stream(dev)
+    call("pk_icp_init", ptr(tgt), ptr(tgt_off), ptr(T0), B, int(nsrc_max), int(ntgt_max), ptr(work), nbytes, s)
+    done = 0
+    while B and done <= max_iter:
+        steps = min(int(poll), max_iter + 1 - done)
+        call("pk_icp_iterate", ptr(src), ptr(src_off), ptr(tgt), ptr(tgt_off), float(max_dist), int(max_iter),
+             float(rel_fitness), float(rel_rmse), B, int(nsrc_max), int(ntgt_max), steps, ptr(work), nbytes,
+             ptr(cnt), s, work=("hbm", steps * int(src.shape[0]) * 48))  # upper bound: source + matched target rows
+        done += steps
+        if int(cnt.item()) == 0:
+            break
+    T = torch.empty((B, 4, 4), dtype=torch.float64, device=dev)
+    stats = torch.empty((B, 4), dtype=torch.float64, device=dev)
+    call("pk_icp_result", ptr(work), B, ptr(T), ptr(stats), s)
+    return T, stats
+
+
 def pose_metrics(cad: torch.Tensor, off: torch.Tensor, nmax: int, T_est: torch.Tensor, T_gt: torch.Tensor):
     """pk_pose_metrics -> f64 [B, 7] (ADD, xyz-direction means x3, ADD-S 1-D means x3)."""
     B = off.numel() - 1

@@ -54,9 +54,11 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="graph mode without overlapping crop formation of the next batch")
     ap.add_argument("--probe-steps", type=int, default=2, help="eager steps after timing for the kernel breakdown")
-    ap.add_argument("--mode", choices=("train", "infer", "corr4096"), default="train",
+    ap.add_argument("--mode", choices=("train", "infer", "corr4096", "icp"), default="train",
                     help="train: the headline fwd+bwd step (default); infer: configs[1]/[3] inference; "
-                         "corr4096: configs[4] feature distance + RANSAC")
+                         "corr4096: configs[4] feature distance + RANSAC; icp: the (f4) ICP refinement")
+    ap.add_argument("--icp-target", choices=("gt_cad", "crop"), default="gt_cad",
+                    help="icp: the reference's target (CAD under T_gt) or the observed crop")
     ap.add_argument("--hypotheses", type=int, default=1024, help="RANSAC hypotheses per crop (infer/corr4096)")
     ap.add_argument("--fd-precision", choices=("fp32", "bf16", "bf16x3"), default="fp32",
                     help="corr4096: feature-distance contraction precision (fp32 = the parity path)")
@@ -249,6 +251,7 @@ TRAIN_METRIC = "RGB-D crops/sec (fwd+bwd), 1024 pts, at 1/2/4/8 MI355X; pose err
 INFER_METRIC = ("RGB-D crops/sec (inference: crop formation + DPFM fwd + spatial-filter solver + IR + "
                 "RANSAC 1024 hyp + pose metrics)")
 CORR_METRIC = "4096-pt dense correspondence solves/sec (4096^2 feature distance + 1024-hypothesis RANSAC)"
+ICP_METRIC = "ICP refinements/sec (point-to-point after RANSAC, ~5000-vertex CAD, threshold 0.2 cm, <= 2000 iterations)"
 CROP_FAMS = {"pk_backproject", "pk_sor", "pk_fps_npoint", "pk_fps", "pk_gather_transform", "pk_collate_pad",
              "pk_ball_query_mask", "pk_ball_query_pairs", "pk_sample_rgb", "pk_erode_mask"}
 
@@ -378,11 +381,106 @@ def build_corr(args, dev, rank, world):
     return one_step, solve, CORR_METRIC, 1, config
 
 
+def icp_workload(B: int, rank: int, target: str):
+    """(f4) workload per rank: B CADs of 5000 surface points (ellipsoids, semi-axes 4-8 cm, the
+    reference's decimated CAD size), a random T_gt per crop, init = T_gt perturbed by 3 degrees
+    and ~0.1 cm (a RANSAC-quality start); target = the CAD under T_gt (test_RANSAC.py:426-436)
+    or a 2000-point noisy partial view of it (the observed-crop variant)."""
+    from dpfm_amd.dataset.synthetic import random_rotation
+    rng = np.random.default_rng(777 + rank)
+    srcs, tgts, T0s = [], [], []
+    for b in range(B):
+        ax = rng.uniform(4, 8, size=3)
+        u = rng.normal(size=(5000, 3))
+        src = u / np.linalg.norm(u, axis=1, keepdims=True) * ax
+        R = random_rotation(rng)
+        t = rng.normal(size=3) * 10 + np.array([0, 0, 90.0])
+        Tg = np.eye(4)
+        Tg[:3, :3], Tg[:3, 3] = R, t
+        tgt = src @ R.T + t
+        if target == "crop":
+            vis = (src @ R.T)[:, 2] < 0  # the half facing the camera
+            idx = np.flatnonzero(vis)[:2000]
+            tgt = tgt[idx] + rng.normal(size=(idx.size, 3)) * 0.02
+        a = np.deg2rad(3.0)
+        k = rng.normal(size=3)
+        k /= np.linalg.norm(k)
+        K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+        D = np.eye(4)
+        D[:3, :3] = np.eye(3) + np.sin(a) * K + (1 - np.cos(a)) * K @ K
+        D[:3, 3] = t - D[:3, :3] @ t + rng.normal(size=3) * 0.1
+        srcs.append(src)
+        tgts.append(np.ascontiguousarray(tgt))
+        T0s.append(D @ Tg)
+    return srcs, tgts, T0s
+
+
+def build_icp(args, dev, rank, world):
+    """(f4): batched ICP of B crops per rank (test_RANSAC.py:436-446), crops sharded across
+    ranks with no collective. One step = the whole refinement of the batch, including the
+    host's convergence polls (one 4-byte read per 8 evaluations)."""
+    from dpfm_amd import ops
+    B = args.batch
+    srcs, tgts, T0s = icp_workload(B, rank, args.icp_target)
+    cat = lambda a: torch.from_numpy(np.ascontiguousarray(np.concatenate(a, 0))).to(dev)  # noqa: E731
+    offs = lambda a: torch.from_numpy(np.concatenate([[0], np.cumsum([x.shape[0] for x in a])])).to(dev)  # noqa
+    s, so, t, to = cat(srcs), offs(srcs), cat(tgts), offs(tgts)
+    T0 = torch.from_numpy(np.stack(T0s)).to(dev)
+    nsm, ntm = max(x.shape[0] for x in srcs), max(x.shape[0] for x in tgts)
+    state = {}
+
+    def one_step():
+        T, st = ops.icp(s, so, t, to, T0, 0.2, 2000, nsrc_max=nsm, ntgt_max=ntm)
+        state["stats"] = st
+        return {"T": T, "stats": st}
+    config = {"workload": f"(f4) ICP: B={B} crops/GPU, source = 5000-point CAD, target = "
+                          + ("the CAD under T_gt (the reference's)" if args.icp_target == "gt_cad" else
+                             "a 2000-point noisy partial view (observed-crop variant)")
+                          + ", threshold 0.2 cm, max_iteration 2000, relative fitness / rmse 1e-6, init = T_gt "
+                            "perturbed by 3 deg", "execution": "eager, host polls convergence every 8 evaluations",
+              "global_batch": B * world, "points_per_crop": 5000, "precision": "fp64",
+              "parallelism": f"shard{world}"}
+    return one_step, one_step, ICP_METRIC, B, config
+
+
+def cpu_icp_baseline(n_crops: int, target: str) -> dict:
+    """The same ICP loop on the host the way Open3D runs it: a KD-tree nearest-neighbour query
+    per evaluation (scipy cKDTree, C++, `workers` threads, distance_upper_bound = threshold)
+    and an SVD Umeyama, on the first n_crops crops of the same workload."""
+    from scipy.spatial import cKDTree
+    from oracle import dpfm_oracle as O
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
+    srcs, tgts, T0s = icp_workload(n_crops, 0, target)
+    iters = 0
+    t0 = time.perf_counter()
+    for src, tgt, T in zip(srcs, tgts, T0s):
+        tree = cKDTree(tgt)
+
+        def evaluate(T):
+            p = src @ T[:3, :3].T + T[:3, 3]
+            d, j = tree.query(p, k=1, distance_upper_bound=0.2, workers=threads)
+            ok = np.isfinite(d) & (d < 0.2)
+            n = int(ok.sum())
+            return p[ok], tgt[j[ok]], (n / len(p) if n else 0.0), (float(np.sqrt((d[ok] ** 2).sum() / n)) if n else 0.0)
+        P, Q, fit, rmse = evaluate(T)
+        for it in range(2000):
+            T = (O.umeyama(P.T, Q.T) if len(P) else np.eye(4)) @ T
+            pf, pr = fit, rmse
+            P, Q, fit, rmse = evaluate(T)
+            iters += 1
+            if abs(pf - fit) < 1e-6 and abs(pr - rmse) < 1e-6:
+                break
+    dt = time.perf_counter() - t0
+    return {"value": round(n_crops / dt, 4), "unit": "refinements/s", "cores": threads, "kind": "port",
+            "sample": f"{n_crops} crops ({iters} ICP updates), scipy cKDTree + numpy SVD Umeyama (Open3D's loop shape)",
+            "seconds": round(dt, 3)}
+
+
 def main():
     args = parse()
     world, rank, dev = setup_dist()
     from dpfm_amd import _lib
-    build = {"train": build_train, "infer": build_infer, "corr4096": build_corr}[args.mode]
+    build = {"train": build_train, "infer": build_infer, "corr4096": build_corr, "icp": build_icp}[args.mode]
     one_step, probe_step, metric, units, config = build(args, dev, rank, world)
 
     for _ in range(args.warmup):
@@ -413,6 +511,11 @@ def main():
                  "pair_overflow": bool(log["pair_overflow"])}
     elif args.mode == "infer":
         extra = {"mean_ir": round(float(log["ir"].mean()), 5), "mean_corr": round(float(log["n_corr"].float().mean()), 1)}
+    elif args.mode == "icp":
+        st = log["stats"].cpu().numpy()
+        extra = {"icp": {"mean_fitness": round(float(st[:, 0].mean()), 5), "mean_rmse": round(float(st[:, 1].mean()), 6),
+                         "mean_updates": round(float(st[:, 2].mean()), 2), "max_updates": int(st[:, 2].max()),
+                         "converged": int(st[:, 3].sum())}}
     probe_steps = args.steps
     if not args.eager:
         # per-kernel HIP events cannot sit inside a graph: time the same step eagerly, on
@@ -448,7 +551,7 @@ def main():
         out = {
             "metric": metric,
             "value": round(units * world / elapsed * args.steps, 3),
-            "unit": "crops/s" if args.mode != "corr4096" else "solves/s",
+            "unit": {"corr4096": "solves/s", "icp": "refinements/s"}.get(args.mode, "crops/s"),
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(total_ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -480,6 +583,8 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(args.cpu_crops, args.points, args.points)
             elif args.mode == "corr4096":
                 out["cpu_baseline"] = cpu_ransac_baseline(args.hypotheses)
+            elif args.mode == "icp":
+                out["cpu_baseline"] = cpu_icp_baseline(32, args.icp_target)
             elif args.mode == "infer":
                 out["cpu_baseline"] = cpu_infer_baseline(max(1, args.cpu_crops // 3), args.points, args.points,
                                                          args.hypotheses)

@@ -447,6 +447,35 @@ int pk_sample_rgb(const uint8_t* img, int F, int H, int W, int C, const double* 
 int pk_sample_features(const float* fmap, int F, int C, int H, int W, const double* K, const double* pts,
                        const int64_t* off, int nmax, float* out, void* stream);
 
+/* (f4) Point-to-point ICP after RANSAC (scripts/test_RANSAC.py:436-446: Open3D 0.17
+ * registration_icp(source, target, threshold 0.2, trans_init = T_RANSAC, PointToPoint,
+ * ICPConvergenceCriteria(max_iteration 2000), relative fitness / rmse 1e-6)), batched.
+ *   src f64 [Ts,3] packed by src_off [B+1] (the CAD), tgt f64 [Tt,3] packed by tgt_off [B+1]
+ *   (the reference's GT-posed CAD, or the observed crop); T_init f64 [B,4,4] row-major;
+ *   nsrc_max / ntgt_max >= every crop's sizes (host bounds: grid and scratch sizing).
+ * Per evaluation every source point T s takes its nearest target point (ties: lowest index);
+ * a pair iff d^2 < max_dist^2; fitness = pairs / |src|, rmse = sqrt(sum d^2 / pairs) (0 without
+ * pairs). Update: Umeyama (no scaling) of the pairs (identity without pairs), T <- U T. Stop
+ * when |dfitness| < rel_fitness and |drmse| < rel_rmse, or after max_iter updates.
+ *   pk_icp_init       sorts each crop's target by x (slab search) and loads T_init;
+ *   pk_icp_iterate    enqueues `steps` evaluations (converged crops return at once) and, if
+ *                     active_count != NULL, writes the number of crops still iterating (int32,
+ *                     device) — a host loop polls it; capture-safe (no host synchronisation);
+ *   pk_icp_result     T f64 [B,4,4], stats f64 [B,4] = (fitness, inlier rmse, updates, converged);
+ *   pk_icp            blocking driver of the three: polls dev_count (int32, device) every `poll`
+ *                     evaluations (one 4-byte read and a stream synchronisation each).
+ * work: pk_icp_work_size(B, nsrc_max, ntgt_max) bytes, kept between the calls of one run. */
+int64_t pk_icp_work_size(int B, int nsrc_max, int ntgt_max);
+int pk_icp_init(const double* tgt, const int64_t* tgt_off, const double* T_init, int B, int nsrc_max, int ntgt_max,
+                void* work, int64_t work_bytes, void* stream);
+int pk_icp_iterate(const double* src, const int64_t* src_off, const double* tgt, const int64_t* tgt_off,
+                   double max_dist, int max_iter, double rel_fitness, double rel_rmse, int B, int nsrc_max,
+                   int ntgt_max, int steps, void* work, int64_t work_bytes, int32_t* active_count, void* stream);
+int pk_icp_result(const void* work, int B, double* T, double* stats, void* stream);
+int pk_icp(const double* src, const int64_t* src_off, const double* tgt, const int64_t* tgt_off, const double* T_init,
+           double max_dist, int max_iter, double rel_fitness, double rel_rmse, int B, int nsrc_max, int ntgt_max,
+           int poll, void* work, int64_t work_bytes, int32_t* dev_count, double* T, double* stats, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

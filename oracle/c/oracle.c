@@ -10,6 +10,8 @@
  *                  RegistrationRANSACBasedOnCorrespondence with
  *                  Eigen::umeyama(with_scaling=false); OpenMP over hypotheses
  *  oc_hyp_index    the documented hypothesis hash of include/posekern.h
+ *  oc_icp          scripts/test_RANSAC.py:436-446 -> Open3D 0.17 RegistrationICP,
+ *                  point-to-point (semantics of csrc/icp.hip, brute-force nearest target)
  */
 #include <math.h>
 #include <stdint.h>
@@ -123,6 +125,8 @@ static void svd3(const double A[9], double U[9], double S[3], double V[9]) {
     const int j = order[c];
     if (S[j] > 1e-12 * (S[order[0]] + 1e-300)) {
       for (int k = 0; k < 3; ++k) Uc[c][k] = a[3 * k + j] / S[j];
+    } else if (c == 0) { /* rank 0 (all-zero sigma): U = I */
+      Uc[0][0] = 1.0; Uc[0][1] = 0.0; Uc[0][2] = 0.0;
     } else if (c == 2) {
       Uc[2][0] = Uc[0][1] * Uc[1][2] - Uc[0][2] * Uc[1][1];
       Uc[2][1] = Uc[0][2] * Uc[1][0] - Uc[0][0] * Uc[1][2];
@@ -299,5 +303,76 @@ int oc_ransac_o3d(const double* src, int V1, const double* dst, const int32_t* c
     }
     out_stats[0] = best_f; out_stats[1] = best_r; out_stats[2] = (double)best_h;
   }
+  return 0;
+}
+
+/* ---------------------------------------------------------------- ICP */
+/* One evaluation of Open3D's GetRegistrationResultAndCorrespondences: every source point
+ * p = T s takes its nearest target point (exact fp64 distance, first index on ties); a pair iff
+ * d^2 < r^2. Fills the matched points (p, q) and returns the pair count; *err = sum d^2. */
+static int icp_eval(const double* src, int ns, const double* tgt, int nt, const double T[16], double r2,
+                    double* mp, double* mq, double* err) {
+  int cnt = 0;
+  double e = 0.0;
+  for (int i = 0; i < ns; ++i) {
+    const double* s = src + 3 * (int64_t)i;
+    double p[3];
+    for (int k = 0; k < 3; ++k) p[k] = ((T[4 * k] * s[0] + T[4 * k + 1] * s[1]) + T[4 * k + 2] * s[2]) + T[4 * k + 3];
+    double best = INFINITY;
+    int bj = -1;
+    for (int j = 0; j < nt; ++j) {
+      const double dx = p[0] - tgt[3 * j], dy = p[1] - tgt[3 * j + 1], dz = p[2] - tgt[3 * j + 2];
+      const double d2 = (dx * dx + dy * dy) + dz * dz;
+      if (d2 < best) { best = d2; bj = j; }
+    }
+    if (bj >= 0 && best < r2) {
+      memcpy(mp + 3 * cnt, p, sizeof(p));
+      memcpy(mq + 3 * cnt, tgt + 3 * bj, 3 * sizeof(double));
+      e += best;
+      ++cnt;
+    }
+  }
+  *err = e;
+  return cnt;
+}
+
+/* Open3D RegistrationICP loop: result_0 = eval(T0); then up to max_iter times: U = umeyama of the
+ * pairs (identity without pairs), T <- U T, result = eval(T), stop when both relative criteria
+ * hold. T: 4x4 row-major in/out (init in T_init); stats: fitness, rmse, updates, converged. */
+int oc_icp(const double* src, int ns, const double* tgt, int nt, const double* T_init, double max_dist,
+           int max_iter, double rel_fit, double rel_rmse, double* T, double* stats) {
+  double* mp = (double*)malloc(sizeof(double) * 3 * (size_t)(ns > 0 ? ns : 1));
+  double* mq = (double*)malloc(sizeof(double) * 3 * (size_t)(ns > 0 ? ns : 1));
+  if (!mp || !mq) { free(mp); free(mq); return -1; }
+  memcpy(T, T_init, 16 * sizeof(double));
+  const double r2 = max_dist * max_dist;
+  double err;
+  int cnt = icp_eval(src, ns, tgt, nt, T, r2, mp, mq, &err);
+  double fit = (cnt > 0 && ns > 0) ? (double)cnt / ns : 0.0;
+  double rmse = cnt > 0 ? sqrt(err / cnt) : 0.0;
+  int it = 0, conv = 0;
+  for (; it < max_iter; ++it) {
+    double U[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    if (cnt > 0) {
+      double R[9], t[3];
+      oc_umeyama(mp, mq, cnt, R, t);
+      for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) U[4 * r + c] = R[3 * r + c];
+        U[4 * r + 3] = t[r];
+      }
+    }
+    double Tn[16];
+    for (int r = 0; r < 4; ++r)
+      for (int c = 0; c < 4; ++c)
+        Tn[4 * r + c] = ((U[4 * r] * T[c] + U[4 * r + 1] * T[4 + c]) + U[4 * r + 2] * T[8 + c]) + U[4 * r + 3] * T[12 + c];
+    memcpy(T, Tn, sizeof(Tn));
+    const double pf = fit, pr = rmse;
+    cnt = icp_eval(src, ns, tgt, nt, T, r2, mp, mq, &err);
+    fit = (cnt > 0 && ns > 0) ? (double)cnt / ns : 0.0;
+    rmse = cnt > 0 ? sqrt(err / cnt) : 0.0;
+    if (fabs(pf - fit) < rel_fit && fabs(pr - rmse) < rel_rmse) { ++it; conv = 1; break; }
+  }
+  stats[0] = fit; stats[1] = rmse; stats[2] = (double)it; stats[3] = (double)conv;
+  free(mp); free(mq);
   return 0;
 }

@@ -346,6 +346,42 @@ def umeyama(src: np.ndarray, dst: np.ndarray) -> np.ndarray:
     return T
 
 
+def registration_icp(source: np.ndarray, target: np.ndarray, max_dist: float, init: np.ndarray,
+                     max_iteration: int = 30, relative_fitness: float = 1e-6, relative_rmse: float = 1e-6):
+    """scripts/test_RANSAC.py:436-446 -> Open3D 0.17 RegistrationICP with
+    TransformationEstimationPointToPoint (parity unpinned: Open3D is absent). Per evaluation
+    every source point T s takes its nearest target point (first index on exact ties; a KD-tree
+    may return either), a pair iff d^2 < max_dist^2 (nanoflann's strict radius test);
+    fitness = pairs / |source|, rmse = sqrt(sum d^2 / pairs). Update: umeyama of the pairs
+    (identity without pairs), T <- U T; stop when |dfitness| < relative_fitness and
+    |drmse| < relative_rmse. Returns (T, fitness, rmse, updates, converged)."""
+    T = np.array(init, dtype=np.float64).reshape(4, 4)
+
+    def evaluate(T):
+        p = source @ T[:3, :3].T + T[:3, 3]
+        d2 = ((p[:, None, :] - target[None, :, :]) ** 2).sum(-1)
+        j = d2.argmin(1)
+        best = d2[np.arange(len(p)), j]
+        ok = best < max_dist * max_dist
+        n = int(ok.sum())
+        fit = n / len(p) if n else 0.0
+        rmse = math.sqrt(best[ok].sum() / n) if n else 0.0
+        return p[ok], target[j[ok]], fit, rmse
+
+    P, Q, fit, rmse = evaluate(T)
+    it, conv = 0, False
+    while it < max_iteration:
+        U = umeyama(P.T, Q.T) if len(P) else np.eye(4)
+        T = U @ T
+        pf, pr = fit, rmse
+        P, Q, fit, rmse = evaluate(T)
+        it += 1
+        if abs(pf - fit) < relative_fitness and abs(pr - rmse) < relative_rmse:
+            conv = True
+            break
+    return T, fit, rmse, it, conv
+
+
 def ransac_evaluate(src: np.ndarray, dst: np.ndarray, corres: np.ndarray, T: np.ndarray, max_dist: float):
     """Open3D EvaluateRANSACBasedOnCorrespondence: fitness, inlier_rmse."""
     s = src[corres[:, 0]]

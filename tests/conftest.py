@@ -34,6 +34,7 @@ def coracle():
     lib.oc_hyp_index.restype = ctypes.c_int32
     lib.oc_umeyama.argtypes = [P, P, I, P, P]
     lib.oc_ransac.argtypes = [P, P, P, I, P, U64, I64, D, P, P]
+    lib.oc_icp.argtypes = [P, I, P, I, P, D, I, D, D, P, P]
     return lib
 
 

@@ -1,0 +1,153 @@
+"""(f4) ICP after RANSAC on the GPU (csrc/icp.hip) against the C oracle oc_icp, which the CPU
+suite pins against the numpy restatement of Open3D's loop (test_oracle_cpu.py::test_icp_*).
+
+  * ragged synthetic batch (200-2000 source points, 300-2400 target points), perturbed
+    initial poses, 2000-iteration budget: same update count and convergence flag per crop,
+    fitness equal, rmse and T within 1e-9 (the GPU sums pairs in a block tree, the oracle
+    sequentially; no pair decision flips on these inputs);
+  * the reference's own setting on its real data (tests/golden/real_crops.npz): source = CAD
+    (~5000 vertices), target = the CAD under T_gt (test_RANSAC.py:426-436), threshold 0.2,
+    init = T_gt perturbed; and the build's crop-target variant (CAD against the observed crop);
+  * edge cases: no pair within the radius, an empty target, max_iteration 0, and the blocking
+    C entry point pk_icp against the host-polled loop.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from _util import cp
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _perturb(rng, T, deg, shift, center):
+    ax = rng.normal(size=3)
+    ax /= np.linalg.norm(ax)
+    a = np.deg2rad(deg)
+    K = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+    dR = np.eye(3) + np.sin(a) * K + (1 - np.cos(a)) * K @ K
+    D = np.eye(4)
+    D[:3, :3] = dR
+    D[:3, 3] = center - dR @ center + rng.normal(size=3) * shift
+    return D @ T
+
+
+def _oracle(coracle, src, tgt, T0, r, max_it):
+    T = np.zeros(16)
+    st = np.zeros(4)
+    coracle.oc_icp(cp(np.ascontiguousarray(src)), src.shape[0], cp(np.ascontiguousarray(tgt)), tgt.shape[0],
+                   cp(np.ascontiguousarray(T0)), r, max_it, 1e-6, 1e-6, cp(T), cp(st))
+    return T.reshape(4, 4), st
+
+
+def _pack(arrs, device):
+    off = np.concatenate([[0], np.cumsum([a.shape[0] for a in arrs])]).astype(np.int64)
+    cat = np.concatenate(arrs, 0) if sum(a.shape[0] for a in arrs) else np.zeros((1, 3))
+    return (torch.from_numpy(np.ascontiguousarray(cat, dtype=np.float64)).to(device),
+            torch.from_numpy(off).to(device))
+
+
+def _check(coracle, srcs, tgts, T0s, r, max_it, device, **kw):
+    from dpfm_amd import ops
+    s, so = _pack(srcs, device)
+    t, to = _pack(tgts, device)
+    T0 = torch.from_numpy(np.stack(T0s)).to(device)
+    T, st = ops.icp(s, so, t, to, T0, r, max_it, **kw)
+    T = T.cpu().numpy()
+    st = st.cpu().numpy()
+    for b in range(len(srcs)):
+        To, sto = _oracle(coracle, srcs[b], tgts[b], T0s[b], r, max_it)
+        assert st[b, 2] == sto[2] and st[b, 3] == sto[3], (b, st[b], sto)
+        assert st[b, 0] == sto[0], (b, st[b], sto)
+        assert abs(st[b, 1] - sto[1]) <= 1e-9, (b, st[b], sto)
+        np.testing.assert_allclose(T[b], To, atol=1e-9, err_msg=f"crop {b}")
+    return T, st
+
+
+def test_icp_ragged_batch_matches_oracle(coracle, device):
+    rng = np.random.default_rng(0)
+    srcs, tgts, T0s = [], [], []
+    for b, ns in enumerate([200, 731, 1024, 1999, 2000, 357]):
+        nt = int(ns * rng.uniform(0.8, 1.2)) + 100
+        tgt = rng.normal(size=(nt, 3)) * np.array([5.0, 3.0, 2.5]) + np.array([0, 0, 90.0])
+        src = tgt[rng.permutation(nt)[:ns]] + rng.normal(size=(ns, 3)) * 0.03
+        # source in its own frame: undo a random pose, then start ICP near it
+        from dpfm_amd.dataset.synthetic import random_rotation
+        R = random_rotation(rng)
+        tt = rng.normal(size=3) * 10
+        src_obj = (src - tt) @ R  # src = R src_obj + tt
+        Tg = np.eye(4)
+        Tg[:3, :3] = R
+        Tg[:3, 3] = tt
+        T0s.append(_perturb(rng, Tg, 3.0 + b, 0.2, src.mean(0)))
+        srcs.append(np.ascontiguousarray(src_obj))
+        tgts.append(np.ascontiguousarray(tgt))
+    T, st = _check(coracle, srcs, tgts, T0s, 0.5, 2000, device)
+    assert (st[:, 3] == 1).all() and (st[:, 0] > 0.8).all()
+
+
+@pytest.mark.parametrize("target", ["gt_cad", "crop"])
+def test_icp_real_crops_matches_oracle(coracle, device, target):
+    g = np.load(os.path.join(GOLD, "real_crops.npz"))
+    rng = np.random.default_rng(3)
+    srcs, tgts, T0s = [], [], []
+    for i in (0, 4):
+        cad = g[f"cad_{int(g[f'{i}_obj_id'])}"]
+        Tg = g[f"{i}_T_gt"]
+        if target == "gt_cad":  # test_RANSAC.py:426-436 (the reference's ICP target)
+            tgt = cad @ Tg[:3, :3].T + Tg[:3, 3]
+        else:
+            tgt = g[f"{i}_pc"]
+        srcs.append(np.ascontiguousarray(cad))
+        tgts.append(np.ascontiguousarray(tgt))
+        T0s.append(_perturb(rng, Tg, 2.0, 0.1, tgt.mean(0)))
+    _check(coracle, srcs, tgts, T0s, 0.2, 2000, device)
+
+
+def test_icp_edge_cases(coracle, device):
+    from dpfm_amd import ops
+    rng = np.random.default_rng(9)
+    tgt = rng.normal(size=(500, 3)) * 3
+    src = np.ascontiguousarray(tgt[:300] + 0.01)
+    far = np.eye(4)
+    far[:3, 3] = 100.0
+    near = np.eye(4)
+    # no pairs / empty target / normal crop in one batch
+    _check(coracle, [src, src, src], [tgt, np.zeros((0, 3)), tgt], [far, near, near], 0.2, 50, device)
+    # max_iteration 0: the initial evaluation only
+    _check(coracle, [src], [tgt], [near], 0.2, 0, device)
+    # poll granularity does not change the result
+    s, so = _pack([src], device)
+    t, to = _pack([tgt], device)
+    T0 = torch.from_numpy(near[None]).to(device)
+    Ta, sa = ops.icp(s, so, t, to, T0, 0.2, 100, poll=1)
+    Tb, sb = ops.icp(s, so, t, to, T0, 0.2, 100, poll=64)
+    assert torch.equal(Ta, Tb) and torch.equal(sa, sb)
+
+
+def test_pk_icp_blocking_entry_matches_polled(device):
+    from dpfm_amd import _lib, ops
+    rng = np.random.default_rng(4)
+    tgts = [rng.normal(size=(n, 3)) * 4 for n in (800, 1200)]
+    srcs = [np.ascontiguousarray(t[: n // 2] + rng.normal(size=(n // 2, 3)) * 0.02) for t, n in zip(tgts, (800, 1200))]
+    s, so = _pack(srcs, device)
+    t, to = _pack(tgts, device)
+    T0 = torch.eye(4, dtype=torch.float64, device=device).repeat(2, 1, 1)
+    T0[:, :3, 3] = 0.1
+    Ta, sa = ops.icp(s, so, t, to, T0, 0.3, 200)
+    B, nsm, ntm = 2, 600, 1200
+    nbytes = int(_lib.lib().pk_icp_work_size(B, nsm, ntm))
+    work = torch.empty((nbytes,), dtype=torch.uint8, device=device)
+    cnt = torch.zeros((1,), dtype=torch.int32, device=device)
+    Tb = torch.empty((B, 4, 4), dtype=torch.float64, device=device)
+    sb = torch.empty((B, 4), dtype=torch.float64, device=device)
+    p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    rc = _lib.lib().pk_icp(p(s), p(so), p(t), p(to), p(T0.contiguous()), 0.3, 200, 1e-6, 1e-6, B, nsm, ntm, 8, p(work),
+                           nbytes, p(cnt), p(Tb), p(sb), _lib.stream(device))
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.equal(Ta, Tb) and torch.equal(sa, sb)

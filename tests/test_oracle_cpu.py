@@ -156,3 +156,51 @@ def test_transform_oracle_vs_numpy_literal_real_crops():
         flips += int((a != b).sum())
         pairs += int(a.sum())
     assert pairs > 200_000 and flips == 0
+
+
+def _icp_case(rng, ns=300, nt=400, deg=4.0, shift=0.3):
+    from dpfm_amd.dataset.synthetic import random_rotation
+    tgt = rng.normal(size=(nt, 3)) * np.array([4.0, 3.0, 2.0]) + np.array([1.0, -2.0, 80.0])
+    src = np.ascontiguousarray(tgt[rng.permutation(nt)[:ns]] + rng.normal(size=(ns, 3)) * 0.02)
+    ax = rng.normal(size=3)
+    ax /= np.linalg.norm(ax)
+    a = np.deg2rad(deg)
+    K = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+    R = np.eye(3) + np.sin(a) * K + (1 - np.cos(a)) * K @ K
+    c = src.mean(0)
+    T0 = np.eye(4)
+    T0[:3, :3] = R
+    T0[:3, 3] = c - R @ c + rng.normal(size=3) * shift
+    return src, np.ascontiguousarray(tgt), T0
+
+
+@pytest.mark.parametrize("seed,max_it", [(0, 30), (1, 2000), (2, 3), (3, 0)])
+def test_icp_c_matches_python(coracle, seed, max_it):
+    """(f4) oc_icp (the GPU parity checker) against the numpy restatement of Open3D's ICP loop."""
+    from _util import cp
+    rng = np.random.default_rng(seed)
+    src, tgt, T0 = _icp_case(rng)
+    Tp, fp, rp, itp, cvp = O.registration_icp(src, tgt, 0.5, T0, max_it)
+    T = np.zeros(16)
+    st = np.zeros(4)
+    coracle.oc_icp(cp(src), src.shape[0], cp(tgt), tgt.shape[0], cp(np.ascontiguousarray(T0)), 0.5, max_it, 1e-6, 1e-6,
+                   cp(T), cp(st))
+    assert int(st[2]) == itp and bool(st[3]) == cvp
+    assert abs(st[0] - fp) < 1e-12 and abs(st[1] - rp) < 1e-9
+    np.testing.assert_allclose(T.reshape(4, 4), Tp, atol=1e-9)
+    if max_it >= 30:
+        assert fp > 0.9 and cvp  # a 4 degree / 3 mm perturbation is recovered
+
+
+def test_icp_c_no_pairs_and_empty_target(coracle):
+    from _util import cp
+    rng = np.random.default_rng(5)
+    src, tgt, T0 = _icp_case(rng)
+    T0[:3, 3] += 100.0  # far away: no pair within the radius
+    for nt in (tgt.shape[0], 0):
+        T = np.zeros(16)
+        st = np.zeros(4)
+        coracle.oc_icp(cp(src), src.shape[0], cp(tgt), nt, cp(np.ascontiguousarray(T0)), 0.5, 50, 1e-6, 1e-6,
+                       cp(T), cp(st))
+        np.testing.assert_array_equal(T.reshape(4, 4), T0)
+        assert st[0] == 0.0 and st[1] == 0.0 and st[2] == 1 and st[3] == 1
