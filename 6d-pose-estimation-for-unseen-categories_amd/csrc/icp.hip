@@ -20,9 +20,10 @@
 // the observed crop as the target (pose refinement without ground truth).
 //
 // Design: the target of each crop is sorted once by x (rank by counting, fp64 keys, index
-// tie-break); a query scans only the x-slab [px - r, px + r] found by binary search, so a
-// 0.2 cm radius on a 10-20 cm object touches a few dozen candidates instead of the whole
-// target. Per iteration two launches: match (grid = source blocks x crops: nearest target,
+// tie-break; SoA x / y / z / index) with a 1024-bucket x table; a query scans only the x-slab
+// [px - r, px + r], starting one bucket before its lower edge and loading candidates 8 at a
+// time (independent loads, so the scan is not a chain of memory latencies), so a 0.2 cm radius
+// on a 10-20 cm object touches ~100 candidates instead of the whole target. Per iteration two launches: match (grid = source blocks x crops: nearest target,
 // pair test, block partial sums of count, sum d^2, the matched source and target points and
 // their products, shifted by the crop's first target point against cancellation) and update
 // (one wave per crop: partials in block order, the convergence test, Horn's quaternion fit of
@@ -40,40 +41,48 @@ constexpr int kNPart = 17;  // count, sum d^2, sum p (3), sum q (3), sum p q^T (
 struct IcpState {  // per crop, in the work buffer
   double T[16];
   double fit, rmse, prev_fit, prev_rmse;
+  double xmin, inv_w;  // x-bucket table of the sorted target: bucket k starts at xmin + k / inv_w
   int iter, active, converged, pad;
 };
 
+constexpr int kNBuckets = 1024;
+
 struct IcpWork {
   IcpState* st;
-  double* sx;     // [B][ntgt_max] sorted x
-  double* sp;     // [B][ntgt_max][3] points in x order
+  double* sx;     // [B][ntgt_max] target x, y, z in x order (SoA)
+  double* sy;
+  double* sz;
   int32_t* sidx;  // [B][ntgt_max] original index
+  int32_t* tbl;   // [B][kNBuckets + 1] first sorted index of each x bucket
   double* part;   // [B][nblk][kNPart]
 };
 
 __host__ __device__ inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
-__host__ __device__ inline IcpWork carve(void* w, int B, int nsrc_max, int ntgt_max) {
+__host__ __device__ inline IcpWork carve(void* w, int B, int ntgt_max) {
   char* p = static_cast<char*>(w);
-  const int64_t nblk = (nsrc_max + kIThreads - 1) / kIThreads;
   IcpWork o;
   o.st = reinterpret_cast<IcpState*>(p);
   p += al256((int64_t)B * sizeof(IcpState));
   o.sx = reinterpret_cast<double*>(p);
   p += al256((int64_t)B * ntgt_max * 8);
-  o.sp = reinterpret_cast<double*>(p);
-  p += al256((int64_t)B * ntgt_max * 24);
+  o.sy = reinterpret_cast<double*>(p);
+  p += al256((int64_t)B * ntgt_max * 8);
+  o.sz = reinterpret_cast<double*>(p);
+  p += al256((int64_t)B * ntgt_max * 8);
   o.sidx = reinterpret_cast<int32_t*>(p);
   p += al256((int64_t)B * ntgt_max * 4);
+  o.tbl = reinterpret_cast<int32_t*>(p);
+  p += al256((int64_t)B * (kNBuckets + 1) * 4);
   o.part = reinterpret_cast<double*>(p);
-  (void)nblk;
   return o;
 }
 
 inline int64_t work_bytes_for(int B, int nsrc_max, int ntgt_max) {
   const int64_t nblk = (nsrc_max + kIThreads - 1) / kIThreads;
-  return al256((int64_t)B * sizeof(IcpState)) + al256((int64_t)B * ntgt_max * 8) + al256((int64_t)B * ntgt_max * 24) +
-         al256((int64_t)B * ntgt_max * 4) + al256((int64_t)B * (nblk > 0 ? nblk : 1) * kNPart * 8);
+  return al256((int64_t)B * sizeof(IcpState)) + 3 * al256((int64_t)B * ntgt_max * 8) +
+         al256((int64_t)B * ntgt_max * 4) + al256((int64_t)B * (kNBuckets + 1) * 4) +
+         al256((int64_t)B * (nblk > 0 ? nblk : 1) * kNPart * 8);
 }
 
 // grid (B): T <- T_init, counters reset.
@@ -92,8 +101,8 @@ __global__ void icp_init_kernel(const double* __restrict__ T_init, IcpState* __r
 // crop's x values staged through LDS; scatter into the sorted arrays.
 __global__ __launch_bounds__(kIThreads) void icp_sort_kernel(const double* __restrict__ tgt,
                                                              const int64_t* __restrict__ tgt_off, int ntgt_max,
-                                                             double* __restrict__ sx, double* __restrict__ sp,
-                                                             int32_t* __restrict__ sidx) {
+                                                             double* __restrict__ sx, double* __restrict__ sy,
+                                                             double* __restrict__ sz, int32_t* __restrict__ sidx) {
   constexpr int kTile = 2048;
   __shared__ double xs[kTile];
   const int b = blockIdx.y;
@@ -120,10 +129,39 @@ __global__ __launch_bounds__(kIThreads) void icp_sort_kernel(const double* __res
   if (!own) return;
   const int64_t o = (int64_t)b * ntgt_max + rank;
   sx[o] = xi;
-  sp[3 * o] = xi;
-  sp[3 * o + 1] = T[3 * i + 1];
-  sp[3 * o + 2] = T[3 * i + 2];
+  sy[o] = T[3 * i + 1];
+  sz[o] = T[3 * i + 2];
   sidx[o] = i;
+}
+
+// grid (B), block 1024: the x-bucket table of the sorted target: tbl[k] = first sorted index
+// with x >= xmin + k w (w = (xmax - xmin) / kNBuckets), by binary search per bucket. A query's
+// slab scan starts at the bucket BEFORE its lower edge's bucket, so a rounding of the bucket
+// index can only start the scan early (points left of the slab are never pairs: d^2 >= dx^2 > r^2).
+__global__ __launch_bounds__(1024) void icp_bucket_kernel(const int64_t* __restrict__ tgt_off, int ntgt_max,
+                                                          const double* __restrict__ sx, IcpState* __restrict__ st,
+                                                          int32_t* __restrict__ tbl) {
+  const int b = blockIdx.x;
+  const int nt = (int)(tgt_off[b + 1] - tgt_off[b]);
+  const double* X = sx + (int64_t)b * ntgt_max;
+  int32_t* Tb = tbl + (int64_t)b * (kNBuckets + 1);
+  const double xmin = nt > 0 ? X[0] : 0.0, xmax = nt > 0 ? X[nt - 1] : 0.0;
+  const double w = (xmax - xmin) / kNBuckets;
+  const double inv_w = w > 0.0 ? 1.0 / w : 0.0;
+  if (threadIdx.x == 0) {
+    st[b].xmin = xmin;
+    st[b].inv_w = inv_w;
+  }
+  for (int k = threadIdx.x; k <= kNBuckets; k += blockDim.x) {
+    const double edge = xmin + (double)k * w;
+    int lo = 0, hi = nt;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (X[mid] < edge) lo = mid + 1;
+      else hi = mid;
+    }
+    Tb[k] = (k == 0) ? 0 : lo;
+  }
 }
 
 __device__ __forceinline__ void block_sum(double v[kNPart], double* __restrict__ out) {
@@ -152,8 +190,8 @@ __device__ __forceinline__ void block_sum(double v[kNPart], double* __restrict__
 __global__ __launch_bounds__(kIThreads) void icp_match_kernel(
     const double* __restrict__ src, const int64_t* __restrict__ src_off, const double* __restrict__ tgt,
     const int64_t* __restrict__ tgt_off, double r, int ntgt_max, int nblk, const IcpState* __restrict__ st,
-    const double* __restrict__ sx, const double* __restrict__ sp, const int32_t* __restrict__ sidx,
-    double* __restrict__ part) {
+    const double* __restrict__ sx, const double* __restrict__ sy, const double* __restrict__ sz,
+    const int32_t* __restrict__ sidx, const int32_t* __restrict__ tbl, double* __restrict__ part) {
   const int b = blockIdx.y;
   if (!st[b].active) return;  // block-uniform
   const int64_t s0 = src_off[b];
@@ -171,35 +209,46 @@ __global__ __launch_bounds__(kIThreads) void icp_match_kernel(
     const double px = ((M[0] * x + M[1] * y) + M[2] * z) + M[3];
     const double py = ((M[4] * x + M[5] * y) + M[6] * z) + M[7];
     const double pz = ((M[8] * x + M[9] * y) + M[10] * z) + M[11];
-    const double* X = sx + (int64_t)b * ntgt_max;
-    const double* Pp = sp + 3 * (int64_t)b * ntgt_max;
-    const int32_t* I = sidx + (int64_t)b * ntgt_max;
-    // first k with X[k] >= px - r
+    const int64_t tb = (int64_t)b * ntgt_max;
+    const double* X = sx + tb;
+    const double* Y = sy + tb;
+    const double* Z = sz + tb;
+    const int32_t* I = sidx + tb;
     const double lo_x = px - r, hi_x = px + r;
-    int lo = 0, hi = nt;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (X[mid] < lo_x) lo = mid + 1;
-      else hi = mid;
-    }
+    // scan start: the bucket before the slab's lower edge (see icp_bucket_kernel)
+    const double kb = (lo_x - st[b].xmin) * st[b].inv_w;
+    int k0 = 0;
+    if (kb >= 1.0) k0 = tbl[(int64_t)b * (kNBuckets + 1) + (kb >= (double)kNBuckets ? kNBuckets : (int)kb) - 1];
     double best = INFINITY;
     int bi = INT32_MAX, bk = -1;
-    for (int k = lo; k < nt; ++k) {
-      const double qx = Pp[3 * k];
-      if (qx > hi_x) break;
-      const double dx = px - qx, dy = py - Pp[3 * k + 1], dz = pz - Pp[3 * k + 2];
-      const double d2 = (dx * dx + dy * dy) + dz * dz;
-      const int id = I[k];
-      if (d2 < best || (d2 == best && id < bi)) {
-        best = d2;
-        bi = id;
-        bk = k;
+    // candidates in batches of 8 independent loads (no load waits on the previous candidate)
+    for (int k = k0; k < nt; k += 8) {
+      double qx[8], qy[8], qz[8];
+      int id[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool in = k + j < nt;
+        const int kk = in ? k + j : k;
+        qx[j] = in ? X[kk] : INFINITY;
+        qy[j] = Y[kk];
+        qz[j] = Z[kk];
+        id[j] = I[kk];
       }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const double dx = px - qx[j], dy = py - qy[j], dz = pz - qz[j];
+        const double d2 = (dx * dx + dy * dy) + dz * dz;
+        const bool take = d2 < best || (d2 == best && id[j] < bi);
+        best = take ? d2 : best;
+        bi = take ? id[j] : bi;
+        bk = take ? k + j : bk;
+      }
+      if (qx[7] > hi_x) break;
     }
     if (bk >= 0 && best < r * r) {
       const double* c = tgt + 3 * t0;  // shift: the crop's first target point
       const double ax = px - c[0], ay = py - c[1], az = pz - c[2];
-      const double bx = Pp[3 * bk] - c[0], by = Pp[3 * bk + 1] - c[1], bz = Pp[3 * bk + 2] - c[2];
+      const double bx = X[bk] - c[0], by = Y[bk] - c[1], bz = Z[bk] - c[2];
       acc[0] = 1.0;
       acc[1] = best;
       acc[2] = ax; acc[3] = ay; acc[4] = az;
@@ -322,14 +371,16 @@ extern "C" int pk_icp_init(const double* tgt, const int64_t* tgt_off, const doub
   PK_REQUIRE(tgt && tgt_off && T_init && work);
   PK_REQUIRE(work_bytes >= work_bytes_for(B, nsrc_max, ntgt_max));
   hipStream_t s = pk::as_stream(stream);
-  const IcpWork w = carve(work, B, nsrc_max, ntgt_max);
+  const IcpWork w = carve(work, B, ntgt_max);
   hipLaunchKernelGGL(icp_init_kernel, dim3(B), dim3(64), 0, s, T_init, w.st);
   PK_CHECK_LAUNCH();
   if (ntgt_max > 0) {
     hipLaunchKernelGGL(icp_sort_kernel, dim3((ntgt_max + kIThreads - 1) / kIThreads, B), dim3(kIThreads), 0, s, tgt,
-                       tgt_off, ntgt_max, w.sx, w.sp, w.sidx);
+                       tgt_off, ntgt_max, w.sx, w.sy, w.sz, w.sidx);
     PK_CHECK_LAUNCH();
   }
+  hipLaunchKernelGGL(icp_bucket_kernel, dim3(B), dim3(1024), 0, s, tgt_off, ntgt_max, w.sx, w.st, w.tbl);
+  PK_CHECK_LAUNCH();
   return PK_OK;
 }
 
@@ -342,11 +393,11 @@ extern "C" int pk_icp_iterate(const double* src, const int64_t* src_off, const d
   PK_REQUIRE(src && src_off && tgt && tgt_off && work);
   PK_REQUIRE(work_bytes >= work_bytes_for(B, nsrc_max, ntgt_max));
   hipStream_t s = pk::as_stream(stream);
-  const IcpWork w = carve(work, B, nsrc_max, ntgt_max);
+  const IcpWork w = carve(work, B, ntgt_max);
   const int nblk = nsrc_max > 0 ? (nsrc_max + kIThreads - 1) / kIThreads : 1;
   for (int k = 0; k < steps; ++k) {
     hipLaunchKernelGGL(icp_match_kernel, dim3(nblk, B), dim3(kIThreads), 0, s, src, src_off, tgt, tgt_off, max_dist,
-                       ntgt_max, nblk, w.st, w.sx, w.sp, w.sidx, w.part);
+                       ntgt_max, nblk, w.st, w.sx, w.sy, w.sz, w.sidx, w.tbl, w.part);
     PK_CHECK_LAUNCH();
     hipLaunchKernelGGL(icp_update_kernel, dim3(B), dim3(64), 0, s, src_off, tgt, tgt_off, nblk, max_iter,
                        rel_fitness, rel_rmse, w.st, w.part);
@@ -363,7 +414,7 @@ extern "C" int pk_icp_result(const void* work, int B, double* T, double* stats, 
   PK_REQUIRE(B >= 0);
   if (B == 0) return PK_OK;
   PK_REQUIRE(work && T && stats);
-  const IcpWork w = carve(const_cast<void*>(work), B, 0, 0);
+  const IcpWork w = carve(const_cast<void*>(work), B, 0);
   hipLaunchKernelGGL(icp_result_kernel, dim3(B), dim3(64), 0, pk::as_stream(stream), w.st, T, stats);
   PK_CHECK_LAUNCH();
   return PK_OK;
