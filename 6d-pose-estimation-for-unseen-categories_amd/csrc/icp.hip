@@ -19,7 +19,8 @@
 // The reference aligns the CAD to the GT-posed CAD (its target); the host mirror also offers
 // the observed crop as the target (pose refinement without ground truth).
 //
-// Design: the target of each crop is sorted once by x (rank by counting, fp64 keys, index
+// Design: the source queries are visited in x order under T_init (so the 64 slabs of a wave
+// overlap and their candidate loads share cache lines) and the target of each crop is sorted once by x (rank by counting, fp64 keys, index
 // tie-break; SoA x / y / z / index) with a 1024-bucket x table; a query scans only the x-slab
 // [px - r, px + r], starting one bucket before its lower edge and loading candidates 8 at a
 // time (independent loads, so the scan is not a chain of memory latencies), so a 0.2 cm radius
@@ -54,12 +55,13 @@ struct IcpWork {
   double* sz;
   int32_t* sidx;  // [B][ntgt_max] original index
   int32_t* tbl;   // [B][kNBuckets + 1] first sorted index of each x bucket
+  int32_t* perm;  // [B][nsrc_max] source points in x order under T_init (query order)
   double* part;   // [B][nblk][kNPart]
 };
 
 __host__ __device__ inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
-__host__ __device__ inline IcpWork carve(void* w, int B, int ntgt_max) {
+__host__ __device__ inline IcpWork carve(void* w, int B, int nsrc_max, int ntgt_max) {
   char* p = static_cast<char*>(w);
   IcpWork o;
   o.st = reinterpret_cast<IcpState*>(p);
@@ -74,6 +76,8 @@ __host__ __device__ inline IcpWork carve(void* w, int B, int ntgt_max) {
   p += al256((int64_t)B * ntgt_max * 4);
   o.tbl = reinterpret_cast<int32_t*>(p);
   p += al256((int64_t)B * (kNBuckets + 1) * 4);
+  o.perm = reinterpret_cast<int32_t*>(p);
+  p += al256((int64_t)B * nsrc_max * 4);
   o.part = reinterpret_cast<double*>(p);
   return o;
 }
@@ -82,7 +86,7 @@ inline int64_t work_bytes_for(int B, int nsrc_max, int ntgt_max) {
   const int64_t nblk = (nsrc_max + kIThreads - 1) / kIThreads;
   return al256((int64_t)B * sizeof(IcpState)) + 3 * al256((int64_t)B * ntgt_max * 8) +
          al256((int64_t)B * ntgt_max * 4) + al256((int64_t)B * (kNBuckets + 1) * 4) +
-         al256((int64_t)B * (nblk > 0 ? nblk : 1) * kNPart * 8);
+         al256((int64_t)B * nsrc_max * 4) + al256((int64_t)B * (nblk > 0 ? nblk : 1) * kNPart * 8);
 }
 
 // grid (B): T <- T_init, counters reset.
@@ -97,40 +101,55 @@ __global__ void icp_init_kernel(const double* __restrict__ T_init, IcpState* __r
   }
 }
 
-// grid (ceil(ntgt_max / 256), B): each point's rank in (x, index) order by counting over the
-// crop's x values staged through LDS; scatter into the sorted arrays.
-__global__ __launch_bounds__(kIThreads) void icp_sort_kernel(const double* __restrict__ tgt,
-                                                             const int64_t* __restrict__ tgt_off, int ntgt_max,
+__device__ __forceinline__ uint64_t ordered_bits(double x) {  // monotone map double -> uint64
+  const uint64_t u = (uint64_t)__double_as_longlong(x);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+// grid (ceil(nmax / 256), B): each point's rank in (x, index) order by counting over the crop's
+// keys staged through LDS (x as order-preserving uint64 bits: integer compares; index tie-break);
+// scatter. With M (4x4 row-major per crop, the initial poses) the key is the x of M p — the
+// source query order; sx / sy / sz may then be NULL and only the permutation is written.
+__global__ __launch_bounds__(kIThreads) void icp_sort_kernel(const double* __restrict__ pts,
+                                                             const int64_t* __restrict__ off, int nmax,
+                                                             const double* __restrict__ M,
                                                              double* __restrict__ sx, double* __restrict__ sy,
                                                              double* __restrict__ sz, int32_t* __restrict__ sidx) {
-  constexpr int kTile = 2048;
-  __shared__ double xs[kTile];
+  constexpr int kTile = 4096;
+  __shared__ uint64_t ks[kTile];
   const int b = blockIdx.y;
-  const int64_t t0 = tgt_off[b];
-  const int nt = (int)(tgt_off[b + 1] - t0);
-  if ((int)blockIdx.x * kIThreads >= nt) return;  // block-uniform
-  const double* T = tgt + 3 * t0;
+  const int64_t p0 = off[b];
+  const int n = (int)(off[b + 1] - p0);
+  if ((int)blockIdx.x * kIThreads >= n) return;  // block-uniform
+  const double* P = pts + 3 * p0;
+  const double* Mb = M ? M + 16 * b : nullptr;
+  auto key_x = [&](int j) {
+    const double* q = P + 3 * j;
+    return Mb ? ((Mb[0] * q[0] + Mb[1] * q[1]) + Mb[2] * q[2]) + Mb[3] : q[0];
+  };
   const int i = blockIdx.x * kIThreads + threadIdx.x;
-  const bool own = i < nt;
-  const double xi = own ? T[3 * i] : 0.0;
+  const bool own = i < n;
+  const uint64_t ki = own ? ordered_bits(key_x(i)) : 0ull;
   int rank = 0;
-  for (int j0 = 0; j0 < nt; j0 += kTile) {
-    const int jn = min(kTile, nt - j0);
+  for (int j0 = 0; j0 < n; j0 += kTile) {
+    const int jn = min(kTile, n - j0);
     __syncthreads();
-    for (int j = threadIdx.x; j < jn; j += kIThreads) xs[j] = T[3 * (j0 + j)];
+    for (int j = threadIdx.x; j < jn; j += kIThreads) ks[j] = ordered_bits(key_x(j0 + j));
     __syncthreads();
     if (own) {
-      for (int j = 0; j < jn; ++j) {
-        const double xj = xs[j];
-        rank += (xj < xi) || (xj == xi && j0 + j < i);
-      }
+      const int lim = min(jn, i - j0);  // keys before i: ties count (index tie-break)
+      int j = 0;
+#pragma unroll 8
+      for (; j < jn; ++j) rank += (ks[j] < ki) || (ks[j] == ki && j < lim);
     }
   }
   if (!own) return;
-  const int64_t o = (int64_t)b * ntgt_max + rank;
-  sx[o] = xi;
-  sy[o] = T[3 * i + 1];
-  sz[o] = T[3 * i + 2];
+  const int64_t o = (int64_t)b * nmax + rank;
+  if (sx) {
+    sx[o] = P[3 * i];
+    sy[o] = P[3 * i + 1];
+    sz[o] = P[3 * i + 2];
+  }
   sidx[o] = i;
 }
 
@@ -191,7 +210,8 @@ __global__ __launch_bounds__(kIThreads) void icp_match_kernel(
     const double* __restrict__ src, const int64_t* __restrict__ src_off, const double* __restrict__ tgt,
     const int64_t* __restrict__ tgt_off, double r, int ntgt_max, int nblk, const IcpState* __restrict__ st,
     const double* __restrict__ sx, const double* __restrict__ sy, const double* __restrict__ sz,
-    const int32_t* __restrict__ sidx, const int32_t* __restrict__ tbl, double* __restrict__ part) {
+    const int32_t* __restrict__ sidx, const int32_t* __restrict__ tbl, const int32_t* __restrict__ perm,
+    int nsrc_max, double* __restrict__ part) {
   const int b = blockIdx.y;
   if (!st[b].active) return;  // block-uniform
   const int64_t s0 = src_off[b];
@@ -204,7 +224,7 @@ __global__ __launch_bounds__(kIThreads) void icp_match_kernel(
   for (int k = 0; k < kNPart; ++k) acc[k] = 0.0;
   if (i < ns && nt > 0) {
     const double* M = st[b].T;
-    const double* s = src + 3 * (s0 + i);
+    const double* s = src + 3 * (s0 + perm[(int64_t)b * nsrc_max + i]);  // x-ordered queries: a wave's slabs overlap
     const double x = s[0], y = s[1], z = s[2];
     const double px = ((M[0] * x + M[1] * y) + M[2] * z) + M[3];
     const double py = ((M[4] * x + M[5] * y) + M[6] * z) + M[7];
@@ -364,19 +384,25 @@ extern "C" int64_t pk_icp_work_size(int B, int nsrc_max, int ntgt_max) {
   return work_bytes_for(B, nsrc_max, ntgt_max);
 }
 
-extern "C" int pk_icp_init(const double* tgt, const int64_t* tgt_off, const double* T_init, int B, int nsrc_max,
-                           int ntgt_max, void* work, int64_t work_bytes, void* stream) {
+extern "C" int pk_icp_init(const double* src, const int64_t* src_off, const double* tgt, const int64_t* tgt_off,
+                           const double* T_init, int B, int nsrc_max, int ntgt_max, void* work, int64_t work_bytes,
+                           void* stream) {
   PK_REQUIRE(B >= 0 && nsrc_max >= 0 && ntgt_max >= 0);
   if (B == 0) return PK_OK;
-  PK_REQUIRE(tgt && tgt_off && T_init && work);
+  PK_REQUIRE(src && src_off && tgt && tgt_off && T_init && work);
   PK_REQUIRE(work_bytes >= work_bytes_for(B, nsrc_max, ntgt_max));
   hipStream_t s = pk::as_stream(stream);
-  const IcpWork w = carve(work, B, ntgt_max);
+  const IcpWork w = carve(work, B, nsrc_max, ntgt_max);
   hipLaunchKernelGGL(icp_init_kernel, dim3(B), dim3(64), 0, s, T_init, w.st);
   PK_CHECK_LAUNCH();
   if (ntgt_max > 0) {
     hipLaunchKernelGGL(icp_sort_kernel, dim3((ntgt_max + kIThreads - 1) / kIThreads, B), dim3(kIThreads), 0, s, tgt,
-                       tgt_off, ntgt_max, w.sx, w.sy, w.sz, w.sidx);
+                       tgt_off, ntgt_max, nullptr, w.sx, w.sy, w.sz, w.sidx);
+    PK_CHECK_LAUNCH();
+  }
+  if (nsrc_max > 0) {
+    hipLaunchKernelGGL(icp_sort_kernel, dim3((nsrc_max + kIThreads - 1) / kIThreads, B), dim3(kIThreads), 0, s, src,
+                       src_off, nsrc_max, T_init, nullptr, nullptr, nullptr, w.perm);
     PK_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(icp_bucket_kernel, dim3(B), dim3(1024), 0, s, tgt_off, ntgt_max, w.sx, w.st, w.tbl);
@@ -393,11 +419,11 @@ extern "C" int pk_icp_iterate(const double* src, const int64_t* src_off, const d
   PK_REQUIRE(src && src_off && tgt && tgt_off && work);
   PK_REQUIRE(work_bytes >= work_bytes_for(B, nsrc_max, ntgt_max));
   hipStream_t s = pk::as_stream(stream);
-  const IcpWork w = carve(work, B, ntgt_max);
+  const IcpWork w = carve(work, B, nsrc_max, ntgt_max);
   const int nblk = nsrc_max > 0 ? (nsrc_max + kIThreads - 1) / kIThreads : 1;
   for (int k = 0; k < steps; ++k) {
     hipLaunchKernelGGL(icp_match_kernel, dim3(nblk, B), dim3(kIThreads), 0, s, src, src_off, tgt, tgt_off, max_dist,
-                       ntgt_max, nblk, w.st, w.sx, w.sy, w.sz, w.sidx, w.tbl, w.part);
+                       ntgt_max, nblk, w.st, w.sx, w.sy, w.sz, w.sidx, w.tbl, w.perm, nsrc_max, w.part);
     PK_CHECK_LAUNCH();
     hipLaunchKernelGGL(icp_update_kernel, dim3(B), dim3(64), 0, s, src_off, tgt, tgt_off, nblk, max_iter,
                        rel_fitness, rel_rmse, w.st, w.part);
@@ -414,7 +440,7 @@ extern "C" int pk_icp_result(const void* work, int B, double* T, double* stats, 
   PK_REQUIRE(B >= 0);
   if (B == 0) return PK_OK;
   PK_REQUIRE(work && T && stats);
-  const IcpWork w = carve(const_cast<void*>(work), B, 0);
+  const IcpWork w = carve(const_cast<void*>(work), B, 0, 0);
   hipLaunchKernelGGL(icp_result_kernel, dim3(B), dim3(64), 0, pk::as_stream(stream), w.st, T, stats);
   PK_CHECK_LAUNCH();
   return PK_OK;
@@ -428,7 +454,7 @@ extern "C" int pk_icp(const double* src, const int64_t* src_off, const double* t
                       int nsrc_max, int ntgt_max, int poll, void* work, int64_t work_bytes, int32_t* dev_count,
                       double* T, double* stats, void* stream) {
   PK_REQUIRE(poll > 0 && dev_count);
-  int rc = pk_icp_init(tgt, tgt_off, T_init, B, nsrc_max, ntgt_max, work, work_bytes, stream);
+  int rc = pk_icp_init(src, src_off, tgt, tgt_off, T_init, B, nsrc_max, ntgt_max, work, work_bytes, stream);
   if (rc) return rc;
   if (B == 0) return PK_OK;
   hipStream_t s = pk::as_stream(stream);

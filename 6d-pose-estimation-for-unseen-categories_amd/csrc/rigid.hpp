@@ -9,7 +9,7 @@ namespace pk_rigid {
 
 // Jacobi eigen-decomposition of a symmetric 4x4 (a, in place) -> eigenvector of the
 // largest eigenvalue in q.
-__device__ inline void top_eigvec4(double a[4][4], double q[4]) {
+__host__ __device__ inline void top_eigvec4(double a[4][4], double q[4]) {
   double v[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
   for (int sweep = 0; sweep < 12; ++sweep) {
     double off = 0.0;
@@ -62,7 +62,7 @@ __device__ inline void top_eigvec4(double a[4][4], double q[4]) {
 }
 
 // 3 x 3 determinant of rows (a, b, c)
-__device__ __forceinline__ double det3(double a0, double a1, double a2, double b0, double b1, double b2, double c0,
+__host__ __device__ __forceinline__ double det3(double a0, double a1, double a2, double b0, double b1, double b2, double c0,
                                        double c1, double c2) {
   return a0 * (b1 * c2 - b2 * c1) - a1 * (b0 * c2 - b2 * c0) + a2 * (b0 * c1 - b1 * c0);
 }
@@ -73,7 +73,7 @@ __device__ __forceinline__ double det3(double a0, double a1, double a2, double b
 // from above), then the eigenvector as the largest column of adj(N - l I). Returns false when
 // that column is tiny relative to the scale (a near-multiple top eigenvalue: 4 draws with a
 // repeated or collinear correspondence), where the caller falls back to Jacobi.
-__device__ inline bool top_eigvec4_qcp(const double N[4][4], const double S[3][3], double q[4]) {
+__host__ __device__ inline bool top_eigvec4_qcp(const double N[4][4], const double S[3][3], double q[4]) {
   double f2 = 0.0;
 #pragma unroll
   for (int r = 0; r < 3; ++r)
@@ -146,7 +146,7 @@ __device__ inline bool top_eigvec4_qcp(const double N[4][4], const double S[3][3
 
 // R (row-major) and t with d ≈ R s + t from the centred cross-covariance S (any positive
 // scale) and the two centroids.
-__device__ inline void rigid_from_cov(const double S[3][3], const double ms[3], const double md[3], double R[9],
+__host__ __device__ inline void rigid_from_cov(const double S[3][3], const double ms[3], const double md[3], double R[9],
                                       double t[3]) {
   const double Sxx = S[0][0], Sxy = S[0][1], Sxz = S[0][2];
   const double Syx = S[1][0], Syy = S[1][1], Syz = S[1][2];

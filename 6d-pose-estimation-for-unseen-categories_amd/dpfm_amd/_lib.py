@@ -85,10 +85,12 @@ SIGNATURES = {
     "pk_sample_rgb": [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],
     "pk_sample_features": [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],
     "pk_icp_work_size": [_I, _I, _I],
-    "pk_icp_init": [_P, _P, _P, _I, _I, _I, _P, _I64, _P],
+    "pk_icp_init": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I64, _P],
     "pk_icp_iterate": [_P, _P, _P, _P, _D, _I, _D, _D, _I, _I, _I, _I, _P, _I64, _P, _P],
     "pk_icp_result": [_P, _I, _P, _P, _P],
     "pk_icp": [_P, _P, _P, _P, _P, _D, _I, _D, _D, _I, _I, _I, _I, _P, _I64, _P, _P, _P, _P],
+    "pk_teaser_graph": [_P, _P, _P, _I, _I, _D, _P, _P, _P],
+    "pk_teaser_solve": [_P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P],  # host pointers
 }
 
 RESTYPES = {"pk_cgt_lstsq_work_size": _I64, "pk_linear_wgrad_grouped_work": _I64, "pk_ransac_work_size": _I64,
@@ -102,6 +104,13 @@ class WgradCall(ctypes.Structure):
     _fields_ = [("x", _P), ("dy", _P), ("dw", _P), ("db", _P), ("R", _I64), ("I", ctypes.c_int32),
                 ("O", ctypes.c_int32), ("N", ctypes.c_int32), ("layout", ctypes.c_int32),
                 ("accumulate", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class TeaserParams(ctypes.Structure):
+    """pk_teaser_params (include/posekern.h); defaults = scripts/test_teaser.py:357-364."""
+    _fields_ = [("noise_bound", _D), ("cbar2", _D), ("rotation_gnc_factor", _D), ("rotation_cost_threshold", _D),
+                ("kcore_heuristic_threshold", _D), ("rotation_max_iterations", ctypes.c_int32),
+                ("pad", ctypes.c_int32), ("max_clique_nodes", _I64)]
 
 
 class PoseKernError(RuntimeError):

@@ -1024,7 +1024,8 @@ def icp(src: torch.Tensor, src_off: torch.Tensor, tgt: torch.Tensor, tgt_off: to
     work = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
     cnt = torch.zeros((1,), dtype=torch.int32, device=dev)
     s = _lib.stream(dev)
-    call("pk_icp_init", ptr(tgt), ptr(tgt_off), ptr(T0), B, int(nsrc_max), int(ntgt_max), ptr(work), nbytes, s)
+    call("pk_icp_init", ptr(src), ptr(src_off), ptr(tgt), ptr(tgt_off), ptr(T0), B, int(nsrc_max), int(ntgt_max),
+         ptr(work), nbytes, s)
     done = 0
     while B and done <= max_iter:
         steps = min(int(poll), max_iter + 1 - done)
@@ -1038,6 +1039,57 @@ def icp(src: torch.Tensor, src_off: torch.Tensor, tgt: torch.Tensor, tgt_off: to
     stats = torch.empty((B, 4), dtype=torch.float64, device=dev)
     call("pk_icp_result", ptr(work), B, ptr(T), ptr(stats), s)
     return T, stats
+
+
+def teaser_graph(src: torch.Tensor, dst: torch.Tensor, off: torch.Tensor, nmax: int, beta: float):
+    """pk_teaser_graph: the pairwise-consistency bitsets of every crop's matched point pairs ->
+    (adj uint64 as int64 [B, nmax, ceil(nmax/64)], deg int32 [B, nmax]) on the device."""
+    B = off.numel() - 1
+    W = (int(nmax) + 63) // 64
+    adj = torch.empty((B, max(int(nmax), 1), max(W, 1)), dtype=torch.int64, device=src.device)
+    deg = torch.empty((B, max(int(nmax), 1)), dtype=torch.int32, device=src.device)
+    call("pk_teaser_graph", ptr(src), ptr(dst), ptr(off), B, int(nmax), float(beta), ptr(adj), ptr(deg),
+         _lib.stream(src.device), work=("valu64", B * int(nmax) * int(nmax) * 20))
+    return adj, deg
+
+
+def teaser_solve_host(src: np.ndarray, dst: np.ndarray, off: np.ndarray, nmax: int, adj: np.ndarray, deg: np.ndarray,
+                      params, threads: int = 8):
+    """pk_teaser_solve on host arrays (max clique / GNC-TLS / adaptive voting are native host
+    code): (T f64 [B,4,4], clique int32 [B, nmax], clique_size int32 [B], info int32 [B, 4])."""
+    import ctypes
+    B = off.shape[0] - 1
+    c = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    src = np.ascontiguousarray(src, dtype=np.float64)
+    dst = np.ascontiguousarray(dst, dtype=np.float64)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    adj = np.ascontiguousarray(adj)
+    deg = np.ascontiguousarray(deg, dtype=np.int32)
+    T = np.zeros((B, 4, 4))
+    clique = np.zeros((B, max(int(nmax), 1)), dtype=np.int32)
+    size = np.zeros(B, dtype=np.int32)
+    info = np.zeros((B, 4), dtype=np.int32)
+    status = _lib.lib().pk_teaser_solve(c(src), c(dst), c(off), B, int(nmax), c(adj), c(deg), ctypes.byref(params),
+                                        int(threads), c(T), c(clique), c(size), c(info))
+    if status != 0:
+        raise _lib.PoseKernError(f"pk_teaser_solve failed: {_lib._ERRORS.get(status, status)}")
+    return T, clique, size, info
+
+
+def teaser(src: torch.Tensor, dst: torch.Tensor, off: torch.Tensor, nmax: Optional[int] = None,
+           noise_bound: float = 0.05, cbar2: float = 1.0, rotation_gnc_factor: float = 1.4,
+           rotation_max_iterations: int = 100, rotation_cost_threshold: float = 1e-12,
+           kcore_heuristic_threshold: float = 0.5, max_clique_nodes: int = 2_000_000, threads: int = 8):
+    """Batched TEASER++ (pk_teaser_graph on the device, one download of the bitsets, then
+    pk_teaser_solve on host threads). src / dst f64 [T,3] matched pairs packed by off [B+1]."""
+    B = off.numel() - 1
+    if nmax is None:
+        nmax = int((off[1:] - off[:-1]).max()) if B else 0
+    p = _lib.TeaserParams(noise_bound, cbar2, rotation_gnc_factor, rotation_cost_threshold, kcore_heuristic_threshold,
+                          int(rotation_max_iterations), 0, int(max_clique_nodes))
+    adj, deg = teaser_graph(src, dst, off, nmax, 2.0 * noise_bound * math.sqrt(cbar2))
+    return teaser_solve_host(src.cpu().numpy(), dst.cpu().numpy(), off.cpu().numpy(), nmax,
+                             adj.cpu().numpy(), deg.cpu().numpy(), p, threads)
 
 
 def pose_metrics(cad: torch.Tensor, off: torch.Tensor, nmax: int, T_est: torch.Tensor, T_gt: torch.Tensor):

@@ -54,9 +54,11 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="graph mode without overlapping crop formation of the next batch")
     ap.add_argument("--probe-steps", type=int, default=2, help="eager steps after timing for the kernel breakdown")
-    ap.add_argument("--mode", choices=("train", "infer", "corr4096", "icp"), default="train",
+    ap.add_argument("--mode", choices=("train", "infer", "corr4096", "icp", "teaser"), default="train",
                     help="train: the headline fwd+bwd step (default); infer: configs[1]/[3] inference; "
-                         "corr4096: configs[4] feature distance + RANSAC; icp: the (f4) ICP refinement")
+                         "corr4096: configs[4] feature distance + RANSAC; icp: the (f4) ICP refinement; "
+                         "teaser: the (f2) TEASER++ solver")
+    ap.add_argument("--teaser-n", type=int, default=2000, help="teaser: correspondences per crop")
     ap.add_argument("--icp-target", choices=("gt_cad", "crop"), default="gt_cad",
                     help="icp: the reference's target (CAD under T_gt) or the observed crop")
     ap.add_argument("--hypotheses", type=int, default=1024, help="RANSAC hypotheses per crop (infer/corr4096)")
@@ -251,6 +253,7 @@ TRAIN_METRIC = "RGB-D crops/sec (fwd+bwd), 1024 pts, at 1/2/4/8 MI355X; pose err
 INFER_METRIC = ("RGB-D crops/sec (inference: crop formation + DPFM fwd + spatial-filter solver + IR + "
                 "RANSAC 1024 hyp + pose metrics)")
 CORR_METRIC = "4096-pt dense correspondence solves/sec (4096^2 feature distance + 1024-hypothesis RANSAC)"
+TEASER_METRIC = "TEASER++ solves/sec (pairwise-consistency graph + max clique + GNC-TLS + adaptive voting)"
 ICP_METRIC = "ICP refinements/sec (point-to-point after RANSAC, ~5000-vertex CAD, threshold 0.2 cm, <= 2000 iterations)"
 CROP_FAMS = {"pk_backproject", "pk_sor", "pk_fps_npoint", "pk_fps", "pk_gather_transform", "pk_collate_pad",
              "pk_ball_query_mask", "pk_ball_query_pairs", "pk_sample_rgb", "pk_erode_mask"}
@@ -443,6 +446,72 @@ def build_icp(args, dev, rank, world):
     return one_step, one_step, ICP_METRIC, B, config
 
 
+def teaser_workload(B: int, n: int, rank: int):
+    """(f2) per rank: B crops of n correspondences (CAD points in cm, ~10 cm objects), 40 %
+    planted inliers under a random pose with 0.01 cm noise, the rest random points around the
+    object (the spatial-filter output the reference hands TEASER++, test_teaser.py:366-425)."""
+    from dpfm_amd.dataset.synthetic import random_rotation
+    rng = np.random.default_rng(4242 + rank)
+    A, Bm = [], []
+    for _ in range(B):
+        R = random_rotation(rng)
+        t = rng.normal(size=3) * 10 + np.array([0, 0, 90.0])
+        a = rng.normal(size=(n, 3)) * 5
+        b = a @ R.T + t + rng.normal(size=(n, 3)) * 0.01
+        out = rng.random(n) >= 0.4
+        b[out] = rng.normal(size=(int(out.sum()), 3)) * 5 + t
+        A.append(a)
+        Bm.append(b)
+    return A, Bm
+
+
+def build_teaser(args, dev, rank, world):
+    """(f2): TEASER++ for B crops per rank, no collective. One step = device graph + one
+    download of the bitsets + the host clique / GNC-TLS / voting on 16 threads."""
+    from dpfm_amd import ops
+    B, n = args.batch, args.teaser_n
+    A, Bm = teaser_workload(B, n, rank)
+    a = torch.from_numpy(np.concatenate(A)).to(dev)
+    b = torch.from_numpy(np.concatenate(Bm)).to(dev)
+    off = torch.arange(0, (B + 1) * n, n, dtype=torch.int64, device=dev)
+
+    def one_step():
+        T, clique, size, info = ops.teaser(a, b, off, n, threads=16)
+        return {"info": info, "size": size}
+    config = {"workload": f"(f2) TEASER++: B={B} crops/GPU x {n} correspondences (40 % inliers), noise_bound 0.05, "
+                          "cbar2 1, no scaling, GNC-TLS 1.4 / 100 / 1e-12, max clique (k-core heuristic 0.5)",
+              "execution": "eager: device graph, host solve on 16 threads", "global_batch": B * world,
+              "correspondences": n, "precision": "fp64", "parallelism": f"shard{world}"}
+    return one_step, one_step, TEASER_METRIC, B, config
+
+
+def cpu_teaser_baseline(n_crops: int, n: int) -> dict:
+    """The same solve with the consistency graph built on the host (numpy, the oracle's
+    vectorized restatement) instead of the device; the clique / GNC / voting stage is the same
+    native host code on 16 threads."""
+    from oracle import dpfm_oracle as O
+    from dpfm_amd import _lib, ops
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
+    A, Bm = teaser_workload(n_crops, n, 0)
+    W = (n + 63) // 64
+    p = _lib.TeaserParams(0.05, 1.0, 1.4, 1e-12, 0.5, 100, 0, 2_000_000)
+    t0 = time.perf_counter()
+    adj = np.zeros((n_crops, n, W), np.uint64)
+    deg = np.zeros((n_crops, n), np.int32)
+    for k in range(n_crops):
+        g = O.teaser_graph(A[k], Bm[k], 0.1)
+        full = np.zeros((n, W * 64), bool)
+        full[:, :n] = g
+        adj[k] = np.packbits(full, axis=1, bitorder="little").view(np.uint64)
+        deg[k] = g.sum(1)
+    off = np.arange(0, (n_crops + 1) * n, n, dtype=np.int64)
+    ops.teaser_solve_host(np.concatenate(A), np.concatenate(Bm), off, n, adj, deg, p, threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(n_crops / dt, 4), "unit": "solves/s", "cores": threads, "kind": "port",
+            "sample": f"{n_crops} crops x {n} correspondences: numpy consistency graph + the native host solve",
+            "seconds": round(dt, 3)}
+
+
 def cpu_icp_baseline(n_crops: int, target: str) -> dict:
     """The same ICP loop on the host the way Open3D runs it: a KD-tree nearest-neighbour query
     per evaluation (scipy cKDTree, C++, `workers` threads, distance_upper_bound = threshold)
@@ -480,7 +549,8 @@ def main():
     args = parse()
     world, rank, dev = setup_dist()
     from dpfm_amd import _lib
-    build = {"train": build_train, "infer": build_infer, "corr4096": build_corr, "icp": build_icp}[args.mode]
+    build = {"train": build_train, "infer": build_infer, "corr4096": build_corr, "icp": build_icp,
+             "teaser": build_teaser}[args.mode]
     one_step, probe_step, metric, units, config = build(args, dev, rank, world)
 
     for _ in range(args.warmup):
@@ -511,6 +581,11 @@ def main():
                  "pair_overflow": bool(log["pair_overflow"])}
     elif args.mode == "infer":
         extra = {"mean_ir": round(float(log["ir"].mean()), 5), "mean_corr": round(float(log["n_corr"].float().mean()), 1)}
+    elif args.mode == "teaser":
+        info = log["info"]
+        extra = {"teaser": {"valid": int(info[:, 0].sum()), "kcore_heuristic": int((info[:, 1] == 2).sum()),
+                            "exact": int((info[:, 1] == 1).sum()), "mean_clique": round(float(log["size"].mean()), 1),
+                            "mean_rotation_inliers": round(float(info[:, 2].mean()), 1)}}
     elif args.mode == "icp":
         st = log["stats"].cpu().numpy()
         extra = {"icp": {"mean_fitness": round(float(st[:, 0].mean()), 5), "mean_rmse": round(float(st[:, 1].mean()), 6),
@@ -551,7 +626,7 @@ def main():
         out = {
             "metric": metric,
             "value": round(units * world / elapsed * args.steps, 3),
-            "unit": {"corr4096": "solves/s", "icp": "refinements/s"}.get(args.mode, "crops/s"),
+            "unit": {"corr4096": "solves/s", "icp": "refinements/s", "teaser": "solves/s"}.get(args.mode, "crops/s"),
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(total_ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -585,6 +660,8 @@ def main():
                 out["cpu_baseline"] = cpu_ransac_baseline(args.hypotheses)
             elif args.mode == "icp":
                 out["cpu_baseline"] = cpu_icp_baseline(32, args.icp_target)
+            elif args.mode == "teaser":
+                out["cpu_baseline"] = cpu_teaser_baseline(8, args.teaser_n)
             elif args.mode == "infer":
                 out["cpu_baseline"] = cpu_infer_baseline(max(1, args.cpu_crops // 3), args.points, args.points,
                                                          args.hypotheses)

@@ -457,7 +457,8 @@ int pk_sample_features(const float* fmap, int F, int C, int H, int W, const doub
  * a pair iff d^2 < max_dist^2; fitness = pairs / |src|, rmse = sqrt(sum d^2 / pairs) (0 without
  * pairs). Update: Umeyama (no scaling) of the pairs (identity without pairs), T <- U T. Stop
  * when |dfitness| < rel_fitness and |drmse| < rel_rmse, or after max_iter updates.
- *   pk_icp_init       sorts each crop's target by x (slab search) and loads T_init;
+ *   pk_icp_init       sorts each crop's target by x (slab search), orders the source queries by x
+ *                     under T_init, and loads T_init;
  *   pk_icp_iterate    enqueues `steps` evaluations (converged crops return at once) and, if
  *                     active_count != NULL, writes the number of crops still iterating (int32,
  *                     device) — a host loop polls it; capture-safe (no host synchronisation);
@@ -466,8 +467,8 @@ int pk_sample_features(const float* fmap, int F, int C, int H, int W, const doub
  *                     evaluations (one 4-byte read and a stream synchronisation each).
  * work: pk_icp_work_size(B, nsrc_max, ntgt_max) bytes, kept between the calls of one run. */
 int64_t pk_icp_work_size(int B, int nsrc_max, int ntgt_max);
-int pk_icp_init(const double* tgt, const int64_t* tgt_off, const double* T_init, int B, int nsrc_max, int ntgt_max,
-                void* work, int64_t work_bytes, void* stream);
+int pk_icp_init(const double* src, const int64_t* src_off, const double* tgt, const int64_t* tgt_off,
+                const double* T_init, int B, int nsrc_max, int ntgt_max, void* work, int64_t work_bytes, void* stream);
 int pk_icp_iterate(const double* src, const int64_t* src_off, const double* tgt, const int64_t* tgt_off,
                    double max_dist, int max_iter, double rel_fitness, double rel_rmse, int B, int nsrc_max,
                    int ntgt_max, int steps, void* work, int64_t work_bytes, int32_t* active_count, void* stream);
@@ -475,6 +476,37 @@ int pk_icp_result(const void* work, int B, double* T, double* stats, void* strea
 int pk_icp(const double* src, const int64_t* src_off, const double* tgt, const int64_t* tgt_off, const double* T_init,
            double max_dist, int max_iter, double rel_fitness, double rel_rmse, int B, int nsrc_max, int ntgt_max,
            int poll, void* work, int64_t work_bytes, int32_t* dev_count, double* T, double* stats, void* stream);
+
+/* (f2) TEASER++ robust registration, the alternative pose solver (scripts/test_teaser.py:
+ * 327-331, 362-435: RobustRegistrationSolver, cbar2 1, noise_bound 0.05, no scaling, GNC-TLS
+ * rotation with gnc factor 1.4 / 100 iterations / cost threshold 1e-12; PMC_EXACT max clique with
+ * the 0.5 k-core heuristic; CHAIN rotation TIMs). Restated from the public TEASER++ algorithm
+ * (parity unpinned: teaserpp_python is absent).
+ *   pk_teaser_graph (device): src / dst f64 [T,3] — the matched points (CAD side, crop side), packed
+ *     by off [B+1] (device); adj uint64 [B][nmax][ceil(nmax/64)] (bit j of row i: pair (i, j)
+ *     consistent: ||src_j - src_i| - |dst_j - dst_i|| <= beta, beta = 2 noise sqrt(cbar2));
+ *     deg int32 [B][nmax] row degrees. Rows >= n_b are zero.
+ *   pk_teaser_solve (HOST pointers only, blocking, `threads` host threads over crops): max clique
+ *     (or the max k-core when its core number exceeds kcore_heuristic_threshold * n), GNC-TLS
+ *     rotation over the chain TIMs of the sorted clique, adaptive-voting translation over the
+ *     clique. T f64 [B,4,4] (identity when invalid), clique int32 [B][nmax] (sorted, clique_size
+ *     [B] entries valid), info int32 [B][4] = (valid, clique mode: 1 exact / 0 node budget hit /
+ *     2 k-core heuristic, rotation inliers, translation inliers). */
+typedef struct pk_teaser_params {
+  double noise_bound;                /* 0.05 */
+  double cbar2;                      /* 1 */
+  double rotation_gnc_factor;        /* 1.4 */
+  double rotation_cost_threshold;    /* 1e-12 */
+  double kcore_heuristic_threshold;  /* 0.5 */
+  int32_t rotation_max_iterations;   /* 100 */
+  int32_t pad;
+  int64_t max_clique_nodes;          /* branch-and-bound node budget */
+} pk_teaser_params;
+int pk_teaser_graph(const double* src, const double* dst, const int64_t* off, int B, int nmax, double beta,
+                    uint64_t* adj, int32_t* deg, void* stream);
+int pk_teaser_solve(const double* src, const double* dst, const int64_t* off, int B, int nmax, const uint64_t* adj,
+                    const int32_t* deg, const pk_teaser_params* params, int threads, double* T, int32_t* clique,
+                    int32_t* clique_size, int32_t* info);
 
 #ifdef __cplusplus
 }

@@ -382,6 +382,145 @@ def registration_icp(source: np.ndarray, target: np.ndarray, max_dist: float, in
     return T, fit, rmse, it, conv
 
 
+# ---------------------------------------------------------------------------- (f2) TEASER++
+# scripts/test_teaser.py:327-331, 362-435 -> teaserpp_python RobustRegistrationSolver (absent:
+# restated from the published TEASER++ algorithm, parity unpinned), estimate_scaling = False.
+
+
+def teaser_graph(src: np.ndarray, dst: np.ndarray, beta: float) -> np.ndarray:
+    """ScaleInliersSelector over all pairs: edge (i, j) iff ||a_j - a_i| - |b_j - b_i|| <= beta."""
+    def norms(x):
+        d = x[None, :, :] - x[:, None, :]
+        return np.sqrt((d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2])
+    e = np.abs(norms(src) - norms(dst)) <= beta
+    np.fill_diagonal(e, False)
+    return e
+
+
+def core_numbers(adj: np.ndarray) -> np.ndarray:
+    """k-core numbers by repeated minimum-degree peeling (pmc compute_cores)."""
+    n = adj.shape[0]
+    deg = adj.sum(1).astype(np.int64)
+    alive = np.ones(n, bool)
+    core = np.zeros(n, np.int64)
+    k = 0
+    for _ in range(n):
+        cand = np.where(alive)[0]
+        v = cand[np.argmin(deg[cand])]
+        k = max(k, int(deg[v]))
+        core[v] = k
+        alive[v] = False
+        deg[adj[v] & alive] -= 1
+    return core
+
+
+def max_clique_size(adj: np.ndarray) -> int:
+    """Bron-Kerbosch with pivoting (exact; small graphs only)."""
+    n = adj.shape[0]
+    nb = [set(np.flatnonzero(adj[v])) for v in range(n)]
+    best = [0]
+
+    def bk(R, P, X):
+        if not P and not X:
+            best[0] = max(best[0], R)
+            return
+        if R + len(P) <= best[0]:
+            return
+        u = max(P | X, key=lambda w: len(P & nb[w]))
+        for v in list(P - nb[u]):
+            bk(R + 1, P & nb[v], X & nb[v])
+            P = P - {v}
+            X = X | {v}
+    bk(0, set(range(n)), set())
+    return best[0]
+
+
+def svd_rot(X: np.ndarray, Y: np.ndarray, w: np.ndarray) -> np.ndarray:
+    """teaser::utils::svdRot(X[3,m], Y[3,m], W): R = V U^T of H = X W Y^T, det-fixed."""
+    H = (X * w[None, :]) @ Y.T
+    U, _, Vt = np.linalg.svd(H)
+    V = Vt.T
+    if np.linalg.det(U) * np.linalg.det(V) < 0:
+        V[:, 2] *= -1
+    return V @ U.T
+
+
+def gnc_tls_rotation(s: np.ndarray, d: np.ndarray, noise_bound: float, gnc_factor: float = 1.4,
+                     max_iterations: int = 100, cost_threshold: float = 1e-12):
+    """GNCTLSRotationSolver::solveForRotation on TIMs s, d [m, 3] -> (R, weights)."""
+    m = s.shape[0]
+    nb2 = noise_bound ** 2
+    if nb2 < 1e-16:
+        nb2 = 1e-2
+    w = np.ones(m)
+    mu, prev = 1.0, math.inf
+    R = np.eye(3)
+    for it in range(max_iterations):
+        R = svd_rot(s.T, d.T, w)
+        q = d - s @ R.T
+        r2 = (q * q).sum(1)
+        if it == 0:
+            mu = 1.0 / (2.0 * r2.max() / nb2 - 1.0)
+            if mu <= 0:
+                break
+        th1, th2 = (mu + 1) / mu * nb2, mu / (mu + 1) * nb2
+        cost = float((w * r2).sum())
+        w = np.where(r2 >= th1, 0.0, np.where(r2 <= th2, 1.0, np.sqrt(nb2 * mu * (mu + 1) / np.maximum(r2, 1e-300)) - mu))
+        diff = abs(cost - prev)
+        mu *= gnc_factor
+        prev = cost
+        if diff < cost_threshold:
+            break
+    return R, w
+
+
+def scalar_tls(X: np.ndarray, rng: float):
+    """ScalarTLSEstimator::estimate (adaptive voting) -> (estimate, inlier mask)."""
+    N = X.shape[0]
+    h = []
+    for i in range(N):
+        h.append((X[i] - rng, i + 1))
+        h.append((X[i] + rng, -i - 1))
+    h.sort(key=lambda p: p[0])  # stable
+    w = 1.0 / (rng * rng)
+    rsum, dxw, dw, sx, sx2, card = rng * N, 0.0, 0.0, 0.0, 0.0, 0
+    best, est = math.inf, 0.0
+    for val, sgn in h:
+        i = abs(sgn) - 1
+        e = 1 if sgn > 0 else -1
+        card += e
+        dw += e * w
+        dxw += e * w * X[i]
+        rsum -= e * rng
+        sx += e * X[i]
+        sx2 += e * X[i] * X[i]
+        xh = dxw / dw
+        cost = (card * xh * xh + sx2 - 2 * sx * xh) + rsum
+        if cost < best:
+            best, est = cost, xh
+    return est, np.abs(X - est) <= rng
+
+
+def teaser_from_clique(src: np.ndarray, dst: np.ndarray, clique, noise_bound=0.05, cbar2=1.0, gnc_factor=1.4,
+                       max_iterations=100, cost_threshold=1e-12):
+    """Steps 3-4 of RobustRegistrationSolver::solve given the sorted clique: chain TIMs, GNC-TLS
+    (noise bound 2 noise), adaptive-voting translation over the clique -> (T, rot_inl, trans_inl)."""
+    C = np.asarray(clique)
+    m = C.size
+    leaf = np.roll(C, -1)
+    s, d = src[leaf] - src[C], dst[leaf] - dst[C]
+    R, w = gnc_tls_rotation(s, d, 2 * noise_bound, gnc_factor, max_iterations, cost_threshold)
+    raw = dst[C] - src[C] @ R.T
+    t = np.zeros(3)
+    inl = np.ones(m, bool)
+    for r in range(3):
+        t[r], ii = scalar_tls(raw[:, r], noise_bound * math.sqrt(cbar2))
+        inl &= ii
+    T = np.eye(4)
+    T[:3, :3], T[:3, 3] = R, t
+    return T, int((w >= 0.5).sum()), int(inl.sum())
+
+
 def ransac_evaluate(src: np.ndarray, dst: np.ndarray, corres: np.ndarray, T: np.ndarray, max_dist: float):
     """Open3D EvaluateRANSACBasedOnCorrespondence: fitness, inlier_rmse."""
     s = src[corres[:, 0]]
