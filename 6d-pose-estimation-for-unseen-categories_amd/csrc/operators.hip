@@ -1,0 +1,493 @@
+// (f1) Spectral operator construction on the device: the CPU cache-fill of
+// dataset/object.py:214, 246 (upstream diffusion-net geometry.compute_operators with
+// robust_laplacian.point_cloud_laplacian for crops, potpourri3d cotan_laplacian + vertex areas for
+// the CAD mesh, and scipy eigsh(L + eps I, k = 64, M = diag(mass), sigma = eps)).
+//
+//   pk_knn             exact k nearest neighbours per point (fp64 ((dx dx + dy dy) + dz dz), ties
+//                      to the lower index), crop points staged through LDS in tiles; a sorted
+//                      register list per query (k <= 32), insertion by an unrolled compare-swap
+//                      chain, entered only when the candidate beats the current k-th.
+//   pk_pc_local_tri    robust_laplacian's local triangulation: per point, the PCA normal of the
+//                      point and its neighbours (Jacobi on the 3x3 covariance), the neighbours in
+//                      the tangent plane, and the Delaunay triangles incident to the point = the
+//                      finite vertices of its 2-D Voronoi cell: neighbour j is a Voronoi neighbour
+//                      iff its bisector keeps a non-empty segment under the other half-planes,
+//                      and the segment's CCW end names the next neighbour l -> triangle (i, j, l).
+//                      O(k^2) per point, one thread per point, no sorting.
+//   pk_cotan_dense     cotan Laplacian (cot = dot / (|cross| + denom_eps), weight cot / 2 per
+//                      edge) and lumped mass (area / 3 per corner) of a triangle list into a dense
+//                      fp64 [nmax, nmax] matrix per crop (fp64 atomics: the summation order of a
+//                      shared entry is not fixed), times `scale` (1/3 for the point-cloud soup).
+//   pk_sym_scale       A = D^-1/2 (L + eps I) D^-1/2 with D = diag(mass) — the generalised
+//                      problem L v = lambda M v as a standard symmetric one (v = D^-1/2 w).
+//   pk_dgemm_cheb      out = alpha (A Y) + beta Y + gamma X for a dense symmetric A [n, n] and
+//                      blocks X, Y [n, m]: one step of the Chebyshev-filtered subspace iteration
+//                      (the three-term recurrence fused into the product's epilogue); fp64, LDS
+//                      tiles of A and Y, 4 x 4 register micro-tiles.
+//   pk_dgemm_tn        G = X^T Y [m, m] (Gram / Rayleigh quotient matrices), partial sums over
+//                      row slabs in a fixed order.
+//
+// Deviations from robust_laplacian (parity unpinned): no tufted cover / intrinsic Delaunay flips
+// and no mollification of the soup; the tangent basis and the normal's sign are this build's
+// (they do not change the triangulation).
+#include "common.hpp"
+
+namespace {
+
+constexpr int kKnnThreads = 256;
+constexpr int kKnnTile = 1024;
+constexpr int kKmax = 32;
+
+// grid (ceil(nmax / 256), B)
+__global__ __launch_bounds__(kKnnThreads) void knn_kernel(const double* __restrict__ pts,
+                                                          const int64_t* __restrict__ off, int k, int omit_self,
+                                                          int32_t* __restrict__ idx, double* __restrict__ d2out) {
+  __shared__ double sx[kKnnTile], sy[kKnnTile], sz[kKnnTile];
+  const int b = blockIdx.y;
+  const int64_t p0 = off[b];
+  const int n = (int)(off[b + 1] - p0);
+  if ((int)blockIdx.x * kKnnThreads >= n) return;
+  const double* P = pts + 3 * p0;
+  const int i = blockIdx.x * kKnnThreads + threadIdx.x;
+  const bool own = i < n;
+  const double qx = own ? P[3 * i] : 0.0, qy = own ? P[3 * i + 1] : 0.0, qz = own ? P[3 * i + 2] : 0.0;
+  double bd[kKmax];
+  int bi[kKmax];
+#pragma unroll
+  for (int p = 0; p < kKmax; ++p) {
+    bd[p] = INFINITY;
+    bi[p] = INT32_MAX;
+  }
+  double worst = INFINITY;  // bd[k - 1]
+  for (int j0 = 0; j0 < n; j0 += kKnnTile) {
+    const int jn = min(kKnnTile, n - j0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < jn; j += kKnnThreads) {
+      sx[j] = P[3 * (j0 + j)];
+      sy[j] = P[3 * (j0 + j) + 1];
+      sz[j] = P[3 * (j0 + j) + 2];
+    }
+    __syncthreads();
+    if (!own) continue;
+    for (int j = 0; j < jn; ++j) {
+      const double dx = qx - sx[j], dy = qy - sy[j], dz = qz - sz[j];
+      const double d = (dx * dx + dy * dy) + dz * dz;
+      const int jj = j0 + j;
+      if (d < worst && !(omit_self && jj == i)) {
+        // insert (d, jj): candidates arrive in index order, so strict < keeps ties index-ordered
+        double cd = d;
+        int ci = jj;
+#pragma unroll
+        for (int p = 0; p < kKmax; ++p) {
+          const bool sw = cd < bd[p];
+          const double td = bd[p];
+          const int ti = bi[p];
+          bd[p] = sw ? cd : td;
+          bi[p] = sw ? ci : ti;
+          cd = sw ? td : cd;
+          ci = sw ? ti : ci;
+        }
+        double w = bd[0];
+#pragma unroll
+        for (int p = 1; p < kKmax; ++p) w = (p == k - 1) ? bd[p] : w;
+        worst = w;
+      }
+    }
+  }
+  if (!own) return;
+  int32_t* o = idx + (p0 + i) * k;
+  double* od = d2out ? d2out + (p0 + i) * k : nullptr;
+#pragma unroll
+  for (int p = 0; p < kKmax; ++p)
+    if (p < k) {
+      o[p] = bi[p] == INT32_MAX ? -1 : bi[p];
+      if (od) od[p] = bd[p];
+    }
+}
+
+// smallest-eigenvalue eigenvector of a symmetric 3x3 (cyclic Jacobi)
+__device__ void min_eigvec3(double a[3][3], double v[3]) {
+  double V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+  for (int sweep = 0; sweep < 20; ++sweep) {
+    const double off = a[0][1] * a[0][1] + a[0][2] * a[0][2] + a[1][2] * a[1][2];
+    if (off < 1e-30 * (a[0][0] * a[0][0] + a[1][1] * a[1][1] + a[2][2] * a[2][2]) + 1e-300) break;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int q = p + 1; q < 3; ++q) {
+        const double apq = a[p][q];
+        if (apq == 0.0) continue;
+        const double th = (a[q][q] - a[p][p]) / (2.0 * apq);
+        const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const double arp = a[r][p], arq = a[r][q];
+          a[r][p] = c * arp - s * arq;
+          a[r][q] = s * arp + c * arq;
+        }
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const double apr = a[p][r], aqr = a[q][r];
+          a[p][r] = c * apr - s * aqr;
+          a[q][r] = s * apr + c * aqr;
+        }
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const double vrp = V[r][p], vrq = V[r][q];
+          V[r][p] = c * vrp - s * vrq;
+          V[r][q] = s * vrp + c * vrq;
+        }
+      }
+  }
+  int m = 0;
+  double best = a[0][0];
+  if (a[1][1] < best) {
+    best = a[1][1];
+    m = 1;
+  }
+  if (a[2][2] < best) m = 2;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) v[r] = m == 0 ? V[r][0] : (m == 1 ? V[r][1] : V[r][2]);
+}
+
+// grid (ceil(nmax / 128), B), block 128; LDS holds each thread's projected neighbours.
+constexpr int kTriThreads = 128;
+__global__ __launch_bounds__(kTriThreads) void pc_local_tri_kernel(const double* __restrict__ pts,
+                                                                   const int64_t* __restrict__ off,
+                                                                   const int32_t* __restrict__ knn, int k,
+                                                                   int32_t* __restrict__ tri,
+                                                                   int32_t* __restrict__ ntri,
+                                                                   double* __restrict__ normals) {
+  __shared__ double qs[kTriThreads][kKmax][2];
+  const int b = blockIdx.y;
+  const int64_t p0 = off[b];
+  const int n = (int)(off[b + 1] - p0);
+  const int i = blockIdx.x * kTriThreads + threadIdx.x;
+  if (i >= n) return;
+  const double* P = pts + 3 * p0;
+  const int32_t* nb = knn + (p0 + i) * k;
+  // PCA normal of the point and its neighbours
+  double mx = P[3 * i], my = P[3 * i + 1], mz = P[3 * i + 2];
+  for (int j = 0; j < k; ++j) {
+    const int q = nb[j] < 0 ? i : nb[j];
+    mx += P[3 * q];
+    my += P[3 * q + 1];
+    mz += P[3 * q + 2];
+  }
+  const double inv = 1.0 / (double)(k + 1);
+  mx *= inv;
+  my *= inv;
+  mz *= inv;
+  double C[3][3] = {};
+  for (int j = -1; j < k; ++j) {
+    const int q = (j < 0 || nb[j] < 0) ? i : nb[j];
+    const double d[3] = {P[3 * q] - mx, P[3 * q + 1] - my, P[3 * q + 2] - mz};
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) C[r][c] += d[r] * d[c];
+  }
+  double nrm[3];
+  min_eigvec3(C, nrm);
+  const double nn = sqrt(nrm[0] * nrm[0] + nrm[1] * nrm[1] + nrm[2] * nrm[2]);
+#pragma unroll
+  for (int r = 0; r < 3; ++r) nrm[r] /= nn;
+  if (normals) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) normals[3 * (p0 + i) + r] = nrm[r];
+  }
+  // tangent basis: e1 = n x (axis of the smallest |n_c|), e2 = n x e1
+  const double an0 = fabs(nrm[0]), an1 = fabs(nrm[1]), an2 = fabs(nrm[2]);
+  const int ax = (an0 <= an1 && an0 <= an2) ? 0 : (an1 <= an2 ? 1 : 2);
+  const double ea[3] = {ax == 0 ? 1.0 : 0.0, ax == 1 ? 1.0 : 0.0, ax == 2 ? 1.0 : 0.0};
+  double e1[3] = {nrm[1] * ea[2] - nrm[2] * ea[1], nrm[2] * ea[0] - nrm[0] * ea[2], nrm[0] * ea[1] - nrm[1] * ea[0]};
+  const double n1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+#pragma unroll
+  for (int r = 0; r < 3; ++r) e1[r] /= n1;
+  const double e2[3] = {nrm[1] * e1[2] - nrm[2] * e1[1], nrm[2] * e1[0] - nrm[0] * e1[2], nrm[0] * e1[1] - nrm[1] * e1[0]};
+  for (int j = 0; j < k; ++j) {
+    const int q = nb[j] < 0 ? i : nb[j];
+    const double d[3] = {P[3 * q] - P[3 * i], P[3 * q + 1] - P[3 * i + 1], P[3 * q + 2] - P[3 * i + 2]};
+    qs[threadIdx.x][j][0] = (d[0] * e1[0] + d[1] * e1[1]) + d[2] * e1[2];
+    qs[threadIdx.x][j][1] = (d[0] * e2[0] + d[1] * e2[1]) + d[2] * e2[2];
+  }
+  int cnt = 0;
+  int32_t* out = tri + (p0 + i) * 2 * k;
+  for (int j = 0; j < k; ++j) {
+    const double qjx = qs[threadIdx.x][j][0], qjy = qs[threadIdx.x][j][1];
+    const double nj = qjx * qjx + qjy * qjy;
+    if (!(nj > 0.0) || nb[j] < 0) continue;
+    // bisector of j: x = q_j / 2 + t u, u = (-q_j.y, q_j.x); half-plane of l: x . q_l <= |q_l|^2 / 2
+    const double mxj = 0.5 * qjx, myj = 0.5 * qjy, ux = -qjy, uy = qjx;
+    double tlo = -INFINITY, thi = INFINITY;
+    int hi_l = -1;
+    bool feasible = true;
+    for (int l = 0; l < k; ++l) {
+      if (l == j || nb[l] < 0) continue;
+      const double qlx = qs[threadIdx.x][l][0], qly = qs[threadIdx.x][l][1];
+      const double nl = qlx * qlx + qly * qly;
+      if (!(nl > 0.0)) continue;
+      const double s = ux * qlx + uy * qly;
+      const double r = 0.5 * nl - (mxj * qlx + myj * qly);
+      if (s > 0.0) {
+        const double t = r / s;
+        if (t < thi) {
+          thi = t;
+          hi_l = l;
+        }
+      } else if (s < 0.0) {
+        const double t = r / s;
+        if (t > tlo) tlo = t;
+      } else if (r < 0.0) {
+        feasible = false;
+      }
+    }
+    if (feasible && tlo < thi && hi_l >= 0) {
+      out[2 * cnt] = nb[j];
+      out[2 * cnt + 1] = nb[hi_l];
+      ++cnt;
+    }
+  }
+  ntri[p0 + i] = cnt;
+}
+
+// grid (ceil(nmax / 128), B): triangles (i, tri[i][2c], tri[i][2c + 1]) of each point i (soup), or
+// with faces != NULL: grid (ceil(fmax / 128), B), faces int32 [F,3] packed by foff, local indices.
+__global__ __launch_bounds__(128) void cotan_dense_kernel(const double* __restrict__ pts,
+                                                          const int64_t* __restrict__ off,
+                                                          const int32_t* __restrict__ tri,
+                                                          const int32_t* __restrict__ ntri, int k,
+                                                          const int32_t* __restrict__ faces,
+                                                          const int64_t* __restrict__ foff, int nmax, double scale,
+                                                          double denom_eps, double* __restrict__ L,
+                                                          double* __restrict__ mass) {
+  const int b = blockIdx.y;
+  const int64_t p0 = off[b];
+  const double* P = pts + 3 * p0;
+  double* Lb = L + (int64_t)b * nmax * nmax;
+  double* Mb = mass + (int64_t)b * nmax;
+  const int t = blockIdx.x * 128 + threadIdx.x;
+  int cnt = 0, a0 = 0;
+  const int32_t* list = nullptr;
+  if (faces) {
+    const int64_t f0 = foff[b];
+    const int nf = (int)(foff[b + 1] - f0);
+    if (t >= nf) return;
+    cnt = 1;
+    list = faces + 3 * (f0 + t);
+  } else {
+    const int n = (int)(off[b + 1] - p0);
+    if (t >= n) return;
+    cnt = ntri[p0 + t];
+    a0 = t;
+    list = tri + (p0 + t) * 2 * k;
+  }
+  for (int c = 0; c < cnt; ++c) {
+    int v[3];
+    if (faces) {
+      v[0] = list[0];
+      v[1] = list[1];
+      v[2] = list[2];
+    } else {
+      v[0] = a0;
+      v[1] = list[2 * c];
+      v[2] = list[2 * c + 1];
+    }
+    double area2 = 0.0;
+#pragma unroll
+    for (int corner = 0; corner < 3; ++corner) {
+      const int o = v[corner], u = v[(corner + 1) % 3], w = v[(corner + 2) % 3];
+      const double eu[3] = {P[3 * u] - P[3 * o], P[3 * u + 1] - P[3 * o + 1], P[3 * u + 2] - P[3 * o + 2]};
+      const double ev[3] = {P[3 * w] - P[3 * o], P[3 * w + 1] - P[3 * o + 1], P[3 * w + 2] - P[3 * o + 2]};
+      const double cx = eu[1] * ev[2] - eu[2] * ev[1], cy = eu[2] * ev[0] - eu[0] * ev[2],
+                   cz = eu[0] * ev[1] - eu[1] * ev[0];
+      const double cr = sqrt((cx * cx + cy * cy) + cz * cz);
+      if (corner == 0) area2 = cr;
+      const double wgt = scale * 0.5 * ((eu[0] * ev[0] + eu[1] * ev[1]) + eu[2] * ev[2]) / (cr + denom_eps);
+      atomicAdd(&Lb[(int64_t)u * nmax + w], -wgt);
+      atomicAdd(&Lb[(int64_t)w * nmax + u], -wgt);
+      atomicAdd(&Lb[(int64_t)u * nmax + u], wgt);
+      atomicAdd(&Lb[(int64_t)w * nmax + w], wgt);
+    }
+    const double m = scale * 0.5 * area2 / 3.0;
+    atomicAdd(&Mb[v[0]], m);
+    atomicAdd(&Mb[v[1]], m);
+    atomicAdd(&Mb[v[2]], m);
+  }
+}
+
+// grid (ceil(nmax / 16), ceil(nmax / 16), B), block 16 x 16: A = D^-1/2 (L + eps I) D^-1/2 in place;
+// rows / columns beyond n_b become the identity (so padding decouples with eigenvalue 1 / ...).
+__global__ void sym_scale_kernel(const int64_t* __restrict__ off, int nmax, double eps,
+                                 const double* __restrict__ mass, double pad_diag, double* __restrict__ A) {
+  const int b = blockIdx.z;
+  const int n = (int)(off[b + 1] - off[b]);
+  const int r = blockIdx.y * 16 + threadIdx.y, c = blockIdx.x * 16 + threadIdx.x;
+  if (r >= nmax || c >= nmax) return;
+  double* a = A + ((int64_t)b * nmax + r) * nmax + c;
+  if (r >= n || c >= n) {
+    *a = (r == c) ? pad_diag : 0.0;
+    return;
+  }
+  const double* m = mass + (int64_t)b * nmax;
+  const double v = *a + (r == c ? eps : 0.0);
+  *a = v / (sqrt(m[r]) * sqrt(m[c]));
+}
+
+// out = alpha (A Y) + beta Y + gamma X; A [B][n][n], X / Y / out [B][n][m] row-major.
+// block 256 = 16 x 16 threads computes a 64 x 64 output tile (4 x 4 per thread); K tiles of 16.
+constexpr int kGT = 64, kGK = 16;
+__global__ __launch_bounds__(256) void dgemm_cheb_kernel(const double* __restrict__ A, const double* __restrict__ Y,
+                                                         const double* __restrict__ X, int n, int m, double alpha,
+                                                         double beta, double gamma, double* __restrict__ out) {
+  __shared__ double As[kGK][kGT + 1];  // As[k][row]
+  __shared__ double Ys[kGK][kGT + 1];  // Ys[k][col]
+  const int b = blockIdx.z;
+  const double* Ab = A + (int64_t)b * n * n;
+  const double* Yb = Y + (int64_t)b * n * m;
+  const int r0 = blockIdx.y * kGT, c0 = blockIdx.x * kGT;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  double acc[4][4] = {};
+  for (int k0 = 0; k0 < n; k0 += kGK) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < kGT * kGK; e += 256) {
+      const int rr = e / kGK, kk = e % kGK;  // A tile: rows r0 + rr, cols k0 + kk (coalesced along kk)
+      const int gr = r0 + rr, gk = k0 + kk;
+      As[kk][rr] = (gr < n && gk < n) ? Ab[(int64_t)gr * n + gk] : 0.0;
+      const int kk2 = e / kGT, cc = e % kGT;  // Y tile: rows k0 + kk2, cols c0 + cc
+      const int gk2 = k0 + kk2, gc = c0 + cc;
+      Ys[kk2][cc] = (gk2 < n && gc < m) ? Yb[(int64_t)gk2 * m + gc] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < kGK; ++kk) {
+      double a[4], y[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty + 16 * i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[j] = Ys[kk][tx + 16 * j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], y[j], acc[i][j]);
+    }
+  }
+  const double* Xb = X ? X + (int64_t)b * n * m : nullptr;
+  double* ob = out + (int64_t)b * n * m;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + ty + 16 * i;
+    if (r >= n) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + tx + 16 * j;
+      if (c >= m) continue;
+      const int64_t o = (int64_t)r * m + c;
+      double v = alpha * acc[i][j] + beta * Yb[o];
+      if (Xb) v += gamma * Xb[o];
+      ob[o] = v;
+    }
+  }
+}
+
+// G = X^T Y: X, Y [B][n][m]; block (16 x 16) computes a 16 x 16 tile of G over all rows in order.
+__global__ __launch_bounds__(256) void dgemm_tn_kernel(const double* __restrict__ X, const double* __restrict__ Y,
+                                                       int n, int m, double* __restrict__ G) {
+  __shared__ double xs[64][17], ys[64][17];
+  const int b = blockIdx.z;
+  const double* Xb = X + (int64_t)b * n * m;
+  const double* Yb = Y + (int64_t)b * n * m;
+  const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  double acc = 0.0;
+  for (int r0 = 0; r0 < n; r0 += 64) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < 64 * 16; e += 256) {
+      const int rr = e / 16, cc = e % 16;
+      const int r = r0 + rr;
+      xs[rr][cc] = (r < n && i0 + cc < m) ? Xb[(int64_t)r * m + i0 + cc] : 0.0;
+      ys[rr][cc] = (r < n && j0 + cc < m) ? Yb[(int64_t)r * m + j0 + cc] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int rr = 0; rr < 64; ++rr) acc = fma(xs[rr][ty], ys[rr][tx], acc);
+  }
+  if (i0 + ty < m && j0 + tx < m) G[((int64_t)b * m + i0 + ty) * m + j0 + tx] = acc;
+}
+
+}  // namespace
+
+extern "C" int pk_knn(const double* pts, const int64_t* off, int B, int nmax, int k, int omit_self, int32_t* idx,
+                      double* d2, void* stream) {
+  PK_REQUIRE(B >= 0 && nmax >= 0 && k >= 1 && k <= kKmax);
+  if (B == 0 || nmax == 0) return PK_OK;
+  PK_REQUIRE(pts && off && idx);
+  hipLaunchKernelGGL(knn_kernel, dim3((nmax + kKnnThreads - 1) / kKnnThreads, B), dim3(kKnnThreads), 0,
+                     pk::as_stream(stream), pts, off, k, omit_self, idx, d2);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_pc_local_tri(const double* pts, const int64_t* off, int B, int nmax, const int32_t* knn, int k,
+                               int32_t* tri, int32_t* ntri, double* normals, void* stream) {
+  PK_REQUIRE(B >= 0 && nmax >= 0 && k >= 2 && k <= kKmax);
+  if (B == 0 || nmax == 0) return PK_OK;
+  PK_REQUIRE(pts && off && knn && tri && ntri);
+  hipLaunchKernelGGL(pc_local_tri_kernel, dim3((nmax + kTriThreads - 1) / kTriThreads, B), dim3(kTriThreads), 0,
+                     pk::as_stream(stream), pts, off, knn, k, tri, ntri, normals);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_cotan_dense(const double* pts, const int64_t* off, int B, int nmax, const int32_t* tri,
+                              const int32_t* ntri, int k, const int32_t* faces, const int64_t* foff, int fmax,
+                              double scale, double denom_eps, double* L, double* mass, void* stream) {
+  PK_REQUIRE(B >= 0 && nmax >= 0);
+  if (B == 0 || nmax == 0) return PK_OK;
+  PK_REQUIRE(pts && off && L && mass);
+  PK_REQUIRE(faces ? (foff != nullptr && fmax >= 0) : (tri != nullptr && ntri != nullptr && k >= 1));
+  hipStream_t s = pk::as_stream(stream);
+  hipError_t e = pk::zero_async(L, (size_t)B * nmax * nmax * sizeof(double), s);
+  if (e == hipSuccess) e = pk::zero_async(mass, (size_t)B * nmax * sizeof(double), s);
+  if (e != hipSuccess) return (int)e;
+  const int items = faces ? fmax : nmax;
+  if (items > 0) {
+    hipLaunchKernelGGL(cotan_dense_kernel, dim3((items + 127) / 128, B), dim3(128), 0, s, pts, off, tri, ntri, k,
+                       faces, foff, nmax, scale, denom_eps, L, mass);
+    PK_CHECK_LAUNCH();
+  }
+  return PK_OK;
+}
+
+extern "C" int pk_sym_scale(const int64_t* off, int B, int nmax, double eps, const double* mass, double pad_diag,
+                            double* A, void* stream) {
+  PK_REQUIRE(B >= 0 && nmax >= 0);
+  if (B == 0 || nmax == 0) return PK_OK;
+  PK_REQUIRE(off && mass && A);
+  hipLaunchKernelGGL(sym_scale_kernel, dim3((nmax + 15) / 16, (nmax + 15) / 16, B), dim3(16, 16), 0,
+                     pk::as_stream(stream), off, nmax, eps, mass, pad_diag, A);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_dgemm_cheb(const double* A, const double* Y, const double* X, int B, int n, int m, double alpha,
+                             double beta, double gamma, double* out, void* stream) {
+  PK_REQUIRE(B >= 0 && n >= 0 && m >= 0);
+  if (B == 0 || n == 0 || m == 0) return PK_OK;
+  PK_REQUIRE(A && Y && out && out != Y && out != X);
+  hipLaunchKernelGGL(dgemm_cheb_kernel, dim3((m + kGT - 1) / kGT, (n + kGT - 1) / kGT, B), dim3(256), 0,
+                     pk::as_stream(stream), A, Y, X, n, m, alpha, beta, gamma, out);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_dgemm_tn(const double* X, const double* Y, int B, int n, int m, double* G, void* stream) {
+  PK_REQUIRE(B >= 0 && n >= 0 && m >= 0);
+  if (B == 0 || m == 0) return PK_OK;
+  PK_REQUIRE(X && Y && G);
+  hipLaunchKernelGGL(dgemm_tn_kernel, dim3((m + 15) / 16, (m + 15) / 16, B), dim3(256), 0, pk::as_stream(stream), X,
+                     Y, n, m, G);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}

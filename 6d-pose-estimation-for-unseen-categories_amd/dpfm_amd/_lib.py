@@ -90,6 +90,12 @@ SIGNATURES = {
     "pk_icp_result": [_P, _I, _P, _P, _P],
     "pk_icp": [_P, _P, _P, _P, _P, _D, _I, _D, _D, _I, _I, _I, _I, _P, _I64, _P, _P, _P, _P],
     "pk_teaser_graph": [_P, _P, _P, _I, _I, _D, _P, _P, _P],
+    "pk_knn": [_P, _P, _I, _I, _I, _I, _P, _P, _P],
+    "pk_pc_local_tri": [_P, _P, _I, _I, _P, _I, _P, _P, _P, _P],
+    "pk_cotan_dense": [_P, _P, _I, _I, _P, _P, _I, _P, _P, _I, _D, _D, _P, _P, _P],
+    "pk_sym_scale": [_P, _I, _I, _D, _P, _D, _P, _P],
+    "pk_dgemm_cheb": [_P, _P, _P, _I, _I, _I, _D, _D, _D, _P, _P],
+    "pk_dgemm_tn": [_P, _P, _I, _I, _I, _P, _P],
     "pk_teaser_solve": [_P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P],  # host pointers
 }
 

@@ -1,0 +1,141 @@
+"""Spectral operators on the device — the (f1) row of SURVEY.md §8(f).
+
+The reference computes the operators on the CPU when it fills its cache:
+  CAD:  dataset/object.py:214 geometry.get_operators(verts, faces, normals, k_eig=64)
+        -> potpourri3d cotan_laplacian(denom_eps=1e-10) + vertex_areas (+ 1e-8 * mean)
+  crop: dataset/object.py:246 geometry.get_operators(verts, faces=[], k_eig=64)
+        -> robust_laplacian.point_cloud_laplacian(verts) (30 neighbours, local Delaunay fans)
+  both: scipy eigsh(L + 1e-8 I, k=64, M=diag(mass), sigma=1e-8), evals clipped at 0
+(upstream diffusion-net geometry.compute_operators).
+
+Here every step runs in hand-written kernels (csrc/operators.hip): kNN, the local fans, the
+cotan assembly, and a Chebyshev-filtered subspace iteration for the 64 smallest eigenpairs of
+A = M^-1/2 (L + eps I) M^-1/2 whose block products are pk_dgemm_cheb / pk_dgemm_tn; only the
+m x m Rayleigh-Ritz / Cholesky problems (m = k + 32) are solved on the host. Dense fp64
+operators: N <= ~5000 per shape (200 MB for the CAD), well inside HBM.
+
+Returns what compute_operators returns that the model reads (mass, L, evals, evecs); frames and
+gradX / gradY feed only gradient features, which this model configuration does not use
+(models/dpfm.py:22-30, with_gradient_features=False), and are None. Parity unpinned."""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import ops
+
+
+@dataclass
+class SpectralOperators:
+    mass: torch.Tensor     # f64 [B, nmax]
+    L: torch.Tensor        # f64 [B, nmax, nmax] dense cotan Laplacian
+    evals: torch.Tensor    # f64 [B, k]
+    evecs: torch.Tensor    # f64 [B, nmax, k], M-orthonormal
+    normals: Optional[torch.Tensor]  # f64 [T, 3] (point clouds)
+    iterations: int
+    residual: torch.Tensor  # f64 [B] max eigen-residual / spectral bound over the k pairs
+    frames = None
+    gradX = None
+    gradY = None
+
+
+def _pack(verts: Sequence[np.ndarray], device):
+    off = np.concatenate([[0], np.cumsum([v.shape[0] for v in verts])]).astype(np.int64)
+    pts = torch.as_tensor(np.concatenate([np.asarray(v, dtype=np.float64) for v in verts]), device=device)
+    return pts, torch.as_tensor(off, device=device), int(max(v.shape[0] for v in verts))
+
+
+def cheb_filter(A, X, degree: int, a: float, b: float, a0: float = 0.0):
+    """Scaled Chebyshev filter (Zhou & Saad) damping [a, b], amplifying below a."""
+    e, c = (b - a) / 2.0, (b + a) / 2.0
+    sigma = e / (a0 - c)
+    tau = 2.0 / sigma
+    Y = ops.dgemm_cheb(A, X, None, sigma / e, -c * sigma / e, 0.0)
+    for _ in range(2, degree + 1):
+        s2 = 1.0 / (tau - sigma)
+        Y, X = ops.dgemm_cheb(A, Y, X, 2.0 * s2 / e, -2.0 * s2 * c / e, -sigma * s2), Y
+        sigma = s2
+    return Y
+
+
+def _orth(X):
+    """Cholesky QR (twice): X <- X R^-1 with R^T R = X^T X (R from the m x m Gram, on the host)."""
+    for _ in range(2):
+        G = ops.dgemm_tn(X, X).cpu().numpy()
+        G = 0.5 * (G + np.swapaxes(G, 1, 2))
+        Rinv = np.stack([np.linalg.inv(np.linalg.cholesky(g).T) for g in G])
+        X = torch.bmm(X, torch.as_tensor(Rinv, device=X.device))
+    return X
+
+
+def subspace_eigs(A: torch.Tensor, counts: Sequence[int], k: int, extra: int = 64, degree: int = 24,
+                  tol: float = 1e-8, max_iter: int = 300, seed: int = 0):
+    """k smallest eigenpairs of each symmetric A[b] (padding rows / columns of crop b beyond
+    counts[b] hold a large diagonal): Chebyshev-filtered subspace iteration with Rayleigh-Ritz.
+    Converged when every wanted residual |A x - theta x| <= tol * theta_k (ARPACK's relative
+    criterion at the k-th Ritz value; the operators are stored in fp32 downstream)."""
+    B, N, _ = A.shape
+    m = min(k + extra, min(counts))
+    if m < k:
+        raise ValueError(f"a shape has fewer points ({min(counts)}) than eigenpairs requested ({k})")
+    upper = float(A.abs().sum(-1).amax())  # Gershgorin bound over the batch
+    rng = np.random.default_rng(seed)
+    X0 = rng.standard_normal((B, N, m))
+    for b, n in enumerate(counts):
+        X0[b, n:] = 0.0
+    X = _orth(torch.as_tensor(X0, device=A.device))
+    cut = 0.05 * upper
+    theta = None
+    it = 0
+    res = None
+    for it in range(1, max_iter + 1):
+        X = _orth(cheb_filter(A, X, degree, cut, upper))
+        AX = ops.dgemm_cheb(A, X, None, 1.0, 0.0, 0.0)
+        H = ops.dgemm_tn(X, AX).cpu().numpy()
+        H = 0.5 * (H + np.swapaxes(H, 1, 2))
+        th, W = np.linalg.eigh(H)
+        Wt = torch.as_tensor(W, device=A.device)
+        X = torch.bmm(X, Wt)
+        AX = torch.bmm(AX, Wt)
+        theta = torch.as_tensor(th, device=A.device)
+        R = AX[:, :, :k] - X[:, :, :k] * theta[:, None, :k]
+        res = R.norm(dim=1).amax(-1) / theta[:, k - 1].abs().clamp(min=1e-300)
+        if float(res.max()) < tol:
+            break
+        cut = float(th[:, m - 1].min())
+    return theta[:, :k], X[:, :, :k], it, res
+
+
+def get_operators(verts: Sequence[np.ndarray], faces: Optional[Sequence[np.ndarray]] = None, k_eig: int = 64,
+                  n_neighbors: int = 30, eps: float = 1e-8, device=None, **eig_kw) -> SpectralOperators:
+    """Operators of a batch of shapes: triangle meshes when `faces` is given (the CAD path), point
+    clouds otherwise (the crop path)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    pts, off, nmax = _pack(verts, dev)
+    counts = [int(v.shape[0]) for v in verts]
+    normals = None
+    if faces is None:
+        idx, _ = ops.knn(pts, off, nmax, n_neighbors, omit_self=True)
+        tri, ntri, normals = ops.pc_local_tri(pts, off, nmax, idx)
+        L, mass = ops.cotan_dense(pts, off, nmax, tri=tri, ntri=ntri, scale=1.0 / 3.0, denom_eps=0.0)
+    else:
+        fo = np.concatenate([[0], np.cumsum([f.shape[0] for f in faces])]).astype(np.int64)
+        fc = torch.as_tensor(np.concatenate([np.asarray(f, dtype=np.int32) for f in faces]), device=dev)
+        L, mass = ops.cotan_dense(pts, off, nmax, faces=fc, foff=torch.as_tensor(fo, device=dev),
+                                  fmax=int(max(f.shape[0] for f in faces)), scale=1.0, denom_eps=1e-10)
+        for b, n in enumerate(counts):  # vertex_areas + eps * mean (compute_operators)
+            mass[b, :n] += eps * mass[b, :n].mean()
+    for b, n in enumerate(counts):
+        mass[b, n:] = 1.0
+    upper = float(L.abs().sum(-1).amax() / mass.amin())
+    A = ops.sym_scale(L, off, mass, eps, pad_diag=upper)
+    evals, W, iters, res = subspace_eigs(A, counts, k_eig, **eig_kw)
+    evecs = W / mass.sqrt()[:, :, None]
+    for b, n in enumerate(counts):
+        evecs[b, n:] = 0.0
+        mass[b, n:] = 0.0
+    return SpectralOperators(mass=mass, L=L, evals=evals.clamp(min=0.0), evecs=evecs, normals=normals,
+                             iterations=iters, residual=res)

@@ -1092,6 +1092,67 @@ def teaser(src: torch.Tensor, dst: torch.Tensor, off: torch.Tensor, nmax: Option
                              adj.cpu().numpy(), deg.cpu().numpy(), p, threads)
 
 
+def knn(pts: torch.Tensor, off: torch.Tensor, nmax: int, k: int, omit_self: bool = True):
+    """pk_knn: (idx int32 [T, k] local to each crop, d2 f64 [T, k]) exact nearest neighbours."""
+    T = pts.shape[0]
+    idx = torch.empty((max(T, 1), k), dtype=torch.int32, device=pts.device)
+    d2 = torch.empty((max(T, 1), k), dtype=torch.float64, device=pts.device)
+    B = off.numel() - 1
+    call("pk_knn", ptr(pts), ptr(off), B, int(nmax), int(k), int(omit_self), ptr(idx), ptr(d2),
+         _lib.stream(pts.device), work=("valu64", B * int(nmax) * int(nmax) * 9))
+    return idx[:T], d2[:T]
+
+
+def pc_local_tri(pts: torch.Tensor, off: torch.Tensor, nmax: int, knn_idx: torch.Tensor):
+    """pk_pc_local_tri: (tri int32 [T, k, 2], ntri int32 [T], normals f64 [T, 3])."""
+    T, k = knn_idx.shape
+    tri = torch.empty((max(T, 1), k, 2), dtype=torch.int32, device=pts.device)
+    ntri = torch.empty((max(T, 1),), dtype=torch.int32, device=pts.device)
+    nrm = torch.empty((max(T, 1), 3), dtype=torch.float64, device=pts.device)
+    call("pk_pc_local_tri", ptr(pts), ptr(off), off.numel() - 1, int(nmax), ptr(knn_idx.contiguous()), int(k), ptr(tri),
+         ptr(ntri), ptr(nrm), _lib.stream(pts.device))
+    return tri[:T], ntri[:T], nrm[:T]
+
+
+def cotan_dense(pts: torch.Tensor, off: torch.Tensor, nmax: int, tri=None, ntri=None, faces=None, foff=None,
+                fmax: int = 0, scale: float = 1.0, denom_eps: float = 1e-10):
+    """pk_cotan_dense: dense cotan Laplacian f64 [B, nmax, nmax] and lumped mass f64 [B, nmax] of a
+    triangle soup (tri / ntri of pc_local_tri) or of mesh faces (int32 [F, 3] packed by foff)."""
+    B = off.numel() - 1
+    L = torch.empty((B, nmax, nmax), dtype=torch.float64, device=pts.device)
+    mass = torch.empty((B, nmax), dtype=torch.float64, device=pts.device)
+    k = int(tri.shape[1]) if tri is not None else 0
+    call("pk_cotan_dense", ptr(pts), ptr(off), B, int(nmax), ptr(tri), ptr(ntri), k, ptr(faces), ptr(foff), int(fmax),
+         float(scale), float(denom_eps), ptr(L), ptr(mass), _lib.stream(pts.device))
+    return L, mass
+
+
+def sym_scale(L: torch.Tensor, off: torch.Tensor, mass: torch.Tensor, eps: float, pad_diag: float) -> torch.Tensor:
+    """pk_sym_scale on a copy of L: D^-1/2 (L + eps I) D^-1/2, padding rows / columns -> pad_diag I."""
+    A = L.clone()
+    B, n, _ = L.shape
+    call("pk_sym_scale", ptr(off), B, int(n), float(eps), ptr(mass), float(pad_diag), ptr(A), _lib.stream(L.device))
+    return A
+
+
+def dgemm_cheb(A: torch.Tensor, Y: torch.Tensor, X: Optional[torch.Tensor], alpha: float, beta: float,
+               gamma: float) -> torch.Tensor:
+    """pk_dgemm_cheb: alpha (A Y) + beta Y + gamma X, batched, fp64."""
+    B, n, m = Y.shape
+    out = torch.empty_like(Y)
+    call("pk_dgemm_cheb", ptr(A), ptr(Y), ptr(X), B, int(n), int(m), float(alpha), float(beta), float(gamma),
+         ptr(out), _lib.stream(Y.device), work=("valu64", 2 * B * n * n * m))
+    return out
+
+
+def dgemm_tn(X: torch.Tensor, Y: torch.Tensor) -> torch.Tensor:
+    """pk_dgemm_tn: X^T Y per crop, fp64 [B, m, m]."""
+    B, n, m = X.shape
+    G = torch.empty((B, m, m), dtype=torch.float64, device=X.device)
+    call("pk_dgemm_tn", ptr(X), ptr(Y), B, int(n), int(m), ptr(G), _lib.stream(X.device))
+    return G
+
+
 def pose_metrics(cad: torch.Tensor, off: torch.Tensor, nmax: int, T_est: torch.Tensor, T_gt: torch.Tensor):
     """pk_pose_metrics -> f64 [B, 7] (ADD, xyz-direction means x3, ADD-S 1-D means x3)."""
     B = off.numel() - 1

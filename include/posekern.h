@@ -508,6 +508,36 @@ int pk_teaser_solve(const double* src, const double* dst, const int64_t* off, in
                     const int32_t* deg, const pk_teaser_params* params, int threads, double* T, int32_t* clique,
                     int32_t* clique_size, int32_t* info);
 
+/* (f1) Spectral operators on the device (dataset/object.py:214, 246 -> upstream diffusion-net
+ * geometry.compute_operators: robust_laplacian.point_cloud_laplacian for crops, potpourri3d
+ * cotan_laplacian + vertex areas for the CAD mesh, scipy eigsh(L + eps I, 64, M, sigma = eps)).
+ * Parity unpinned (those packages are absent); see csrc/operators.hip for the deviations.
+ *   pk_knn           pts f64 [T,3] packed by off; idx int32 [T,k] (crop-local, ties to the lower
+ *                    index; -1 when the crop has fewer points), d2 f64 [T,k] (may be NULL); k <= 32.
+ *   pk_pc_local_tri  per point the Delaunay triangles of its tangent-plane neighbourhood incident to
+ *                    it: tri int32 [T,k,2] (the other two corners, crop-local), ntri int32 [T],
+ *                    normals f64 [T,3] (PCA; may be NULL).
+ *   pk_cotan_dense   dense cotan Laplacian L f64 [B,nmax,nmax] (off-diagonal -sum cot/2, diagonal
+ *                    = minus the row sum) and lumped mass f64 [B,nmax] (area / 3 per corner) of the
+ *                    soup (tri / ntri / k) or of mesh faces (int32 [F,3] crop-local, packed by foff
+ *                    [B+1], fmax >= every crop's face count); everything times `scale`.
+ *   pk_sym_scale     A = D^-1/2 (L + eps I) D^-1/2 in place (D = diag(mass)); rows / columns past n_b
+ *                    become pad_diag * I.
+ *   pk_dgemm_cheb    out = alpha A Y + beta Y + gamma X (X may be NULL), A [B,n,n], X / Y / out [B,n,m].
+ *   pk_dgemm_tn      G [B,m,m] = X^T Y. */
+int pk_knn(const double* pts, const int64_t* off, int B, int nmax, int k, int omit_self, int32_t* idx, double* d2,
+           void* stream);
+int pk_pc_local_tri(const double* pts, const int64_t* off, int B, int nmax, const int32_t* knn, int k, int32_t* tri,
+                    int32_t* ntri, double* normals, void* stream);
+int pk_cotan_dense(const double* pts, const int64_t* off, int B, int nmax, const int32_t* tri, const int32_t* ntri,
+                   int k, const int32_t* faces, const int64_t* foff, int fmax, double scale, double denom_eps,
+                   double* L, double* mass, void* stream);
+int pk_sym_scale(const int64_t* off, int B, int nmax, double eps, const double* mass, double pad_diag, double* A,
+                 void* stream);
+int pk_dgemm_cheb(const double* A, const double* Y, const double* X, int B, int n, int m, double alpha, double beta,
+                  double gamma, double* out, void* stream);
+int pk_dgemm_tn(const double* X, const double* Y, int B, int n, int m, double* G, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

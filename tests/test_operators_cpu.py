@@ -1,0 +1,94 @@
+"""(f1) Spectral operators, CPU side:
+  * the oracle's local fans (scipy Delaunay per neighbourhood) against the half-plane Voronoi rule
+    the device kernel uses (restated here in numpy) — pins the kernel's algorithm on the CPU;
+  * the Chebyshev-filtered subspace iteration of dpfm_amd.geometry (its block products swapped for
+    torch-CPU ones; the kernels themselves are tested in test_operators_gpu.py) against scipy eigsh
+    on the oracle's point-cloud Laplacian: eigenvalues, M-orthonormality, residuals.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import operators_oracle as OO
+
+
+def voronoi_fans(pts, nbrs):
+    out = set()
+    for i in range(pts.shape[0]):
+        nb = nbrs[i]
+        n = OO.pca_normal(pts, i, nb)
+        e1, e2 = OO.tangent_basis(n)
+        d = pts[nb] - pts[i]
+        q = np.stack([d @ e1, d @ e2], 1)
+        for j in range(len(nb)):
+            u = np.array([-q[j, 1], q[j, 0]])
+            mj = 0.5 * q[j]
+            tlo, thi, hl = -np.inf, np.inf, -1
+            ok = True
+            for l in range(len(nb)):
+                if l == j:
+                    continue
+                s = u @ q[l]
+                r = 0.5 * (q[l] @ q[l]) - mj @ q[l]
+                if s > 0 and r / s < thi:
+                    thi, hl = r / s, l
+                elif s < 0 and r / s > tlo:
+                    tlo = r / s
+                elif s == 0 and r < 0:
+                    ok = False
+            if ok and tlo < thi and hl >= 0:
+                out.add((i, int(nb[j]), int(nb[hl])))
+    return out
+
+
+def ellipsoid(rng, n, axes=(5.0, 4.0, 3.0)):
+    u = rng.normal(size=(n, 3))
+    return u / np.linalg.norm(u, axis=1, keepdims=True) * np.asarray(axes)
+
+
+def test_local_fans_voronoi_rule_matches_delaunay():
+    rng = np.random.default_rng(0)
+    pts = ellipsoid(rng, 300)
+    idx, _ = OO.knn(pts, 30)
+    ref = {(i, j, l) for (i, j, l) in OO.local_triangles(pts, idx)}
+    got = voronoi_fans(pts, idx)
+    canon = lambda S: {(i, min(j, l), max(j, l)) for (i, j, l) in S}  # noqa: E731
+    assert canon(got) == canon(ref)
+
+
+def test_subspace_iteration_matches_eigsh(monkeypatch):
+    from dpfm_amd import geometry, ops
+
+    def cheb(A, Y, X, alpha, beta, gamma):
+        out = alpha * torch.bmm(A, Y) + beta * Y
+        return out + gamma * X if X is not None else out
+
+    monkeypatch.setattr(ops, "dgemm_cheb", cheb)
+    monkeypatch.setattr(ops, "dgemm_tn", lambda X, Y: torch.bmm(X.transpose(1, 2), Y))
+    rng = np.random.default_rng(1)
+    shapes = [ellipsoid(rng, 350), ellipsoid(rng, 300, (6.0, 3.0, 2.0))]
+    nmax, k, eps = 350, 24, 1e-8
+    Ls, Ms = [], []
+    for p in shapes:
+        idx, _ = OO.knn(p, 30)
+        L, M = OO.cotan_laplacian(p, OO.local_triangles(p, idx), scale=1.0 / 3.0, denom_eps=0.0)
+        Ls.append(L)
+        Ms.append(M)
+    A = np.zeros((2, nmax, nmax))
+    upper = max(np.abs(L).sum(1).max() / M.min() for L, M in zip(Ls, Ms))
+    for b, (L, M) in enumerate(zip(Ls, Ms)):
+        n = L.shape[0]
+        s = 1.0 / np.sqrt(M)
+        A[b, :n, :n] = (L + eps * np.eye(n)) * s[:, None] * s[None, :]
+        A[b, n:, n:] = np.eye(nmax - n) * upper
+    ev, W, it, res = geometry.subspace_eigs(torch.as_tensor(A), [350, 300], k, tol=1e-9)
+    print("iterations", it, "residual", res)
+    assert float(res.max()) < 1e-9 and it < 100
+    for b, (L, M) in enumerate(zip(Ls, Ms)):
+        n = L.shape[0]
+        ref, V = OO.eigsh_operators(L, M, k, eps)
+        np.testing.assert_allclose(ev[b].numpy(), np.sort(ref), rtol=1e-8, atol=1e-10)
+        evecs = W[b, :n].numpy() / np.sqrt(M)[:, None]
+        np.testing.assert_allclose(evecs.T @ (M[:, None] * evecs), np.eye(k), atol=1e-8)
+        r = (L + eps * np.eye(n)) @ evecs - (M[:, None] * evecs) * ev[b].numpy()[None, :]
+        assert np.abs(r).max() < 1e-7
