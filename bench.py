@@ -54,10 +54,11 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="graph mode without overlapping crop formation of the next batch")
     ap.add_argument("--probe-steps", type=int, default=2, help="eager steps after timing for the kernel breakdown")
-    ap.add_argument("--mode", choices=("train", "infer", "corr4096", "icp", "teaser"), default="train",
+    ap.add_argument("--mode", choices=("train", "infer", "corr4096", "icp", "teaser", "operators"), default="train",
                     help="train: the headline fwd+bwd step (default); infer: configs[1]/[3] inference; "
                          "corr4096: configs[4] feature distance + RANSAC; icp: the (f4) ICP refinement; "
-                         "teaser: the (f2) TEASER++ solver")
+                         "teaser: the (f2) TEASER++ solver; operators: the (f1) spectral operators")
+    ap.add_argument("--op-points", type=int, default=2000, help="operators: points per crop")
     ap.add_argument("--teaser-n", type=int, default=2000, help="teaser: correspondences per crop")
     ap.add_argument("--icp-target", choices=("gt_cad", "crop"), default="gt_cad",
                     help="icp: the reference's target (CAD under T_gt) or the observed crop")
@@ -253,6 +254,7 @@ TRAIN_METRIC = "RGB-D crops/sec (fwd+bwd), 1024 pts, at 1/2/4/8 MI355X; pose err
 INFER_METRIC = ("RGB-D crops/sec (inference: crop formation + DPFM fwd + spatial-filter solver + IR + "
                 "RANSAC 1024 hyp + pose metrics)")
 CORR_METRIC = "4096-pt dense correspondence solves/sec (4096^2 feature distance + 1024-hypothesis RANSAC)"
+OPS_METRIC = "crop spectral operators/sec (kNN-30 fans + cotan Laplacian + mass + 64 eigenpairs)"
 TEASER_METRIC = "TEASER++ solves/sec (pairwise-consistency graph + max clique + GNC-TLS + adaptive voting)"
 ICP_METRIC = "ICP refinements/sec (point-to-point after RANSAC, ~5000-vertex CAD, threshold 0.2 cm, <= 2000 iterations)"
 CROP_FAMS = {"pk_backproject", "pk_sor", "pk_fps_npoint", "pk_fps", "pk_gather_transform", "pk_collate_pad",
@@ -446,6 +448,56 @@ def build_icp(args, dev, rank, world):
     return one_step, one_step, ICP_METRIC, B, config
 
 
+def ops_workload(B: int, n: int, rank: int):
+    """(f1) per rank: B crop-like point clouds of n points: the camera-facing half of an ellipsoid
+    (semi-axes 4-8 cm) with 0.02 cm noise — the shape of an eroded, outlier-filtered depth crop."""
+    rng = np.random.default_rng(99 + rank)
+    out = []
+    for _ in range(B):
+        ax = rng.uniform(4, 8, size=3)
+        u = rng.normal(size=(4 * n, 3))
+        u = u[u[:, 2] < 0][:n]
+        out.append(u / np.linalg.norm(u, axis=1, keepdims=True) * ax + rng.normal(size=(n, 3)) * 0.02)
+    return out
+
+
+def build_operators(args, dev, rank, world):
+    """(f1): get_operators for B crops per rank (the reference's pc_LBO cache fill,
+    dataset/object.py:246), no collective."""
+    from dpfm_amd import geometry
+    B, n = args.batch, args.op_points
+    shapes = ops_workload(B, n, rank)
+    state = {}
+
+    def one_step():
+        op = geometry.get_operators(shapes, k_eig=64, device=dev)
+        state["it"] = op.iterations
+        return {"iterations": op.iterations, "residual": float(op.residual.max())}
+    config = {"workload": f"(f1) spectral operators: B={B} crop point clouds/GPU x {n} points, kNN 30, local Delaunay "
+                          "fans, cotan Laplacian / 3, lumped mass, 64 smallest eigenpairs of L v = lambda M v "
+                          "(Chebyshev-filtered subspace iteration, m = 128, degree 24, tol 1e-8)",
+              "execution": "eager; host Rayleigh-Ritz per iteration", "global_batch": B * world, "points_per_crop": n,
+              "precision": "fp64", "parallelism": f"shard{world}"}
+    return one_step, one_step, OPS_METRIC, B, config
+
+
+def cpu_ops_baseline(n_crops: int, n: int) -> dict:
+    """oracle/operators_oracle.py on the host: numpy kNN, scipy (Qhull) Delaunay per neighbourhood,
+    the cotan assembly and scipy eigsh(sigma = eps) — the same steps as compute_operators."""
+    from oracle import operators_oracle as OO
+    shapes = ops_workload(n_crops, n, 0)
+    t0 = time.perf_counter()
+    for s in shapes:
+        idx, _ = OO.knn(s, 30)
+        L, M = OO.cotan_laplacian(s, OO.local_triangles(s, idx), scale=1.0 / 3.0, denom_eps=0.0)
+        OO.eigsh_operators(L, M, 64)
+    dt = time.perf_counter() - t0
+    return {"value": round(n_crops / dt, 4), "unit": "operator sets/s", "cores": 1, "kind": "port",
+            "sample": f"{n_crops} crops x {n} points: numpy kNN, per-point scipy Delaunay fans (Python loop), "
+                      "cotan assembly (Python loop), scipy eigsh shift-invert",
+            "seconds": round(dt, 3)}
+
+
 def teaser_workload(B: int, n: int, rank: int):
     """(f2) per rank: B crops of n correspondences (CAD points in cm, ~10 cm objects), 40 %
     planted inliers under a random pose with 0.01 cm noise, the rest random points around the
@@ -550,7 +602,7 @@ def main():
     world, rank, dev = setup_dist()
     from dpfm_amd import _lib
     build = {"train": build_train, "infer": build_infer, "corr4096": build_corr, "icp": build_icp,
-             "teaser": build_teaser}[args.mode]
+             "teaser": build_teaser, "operators": build_operators}[args.mode]
     one_step, probe_step, metric, units, config = build(args, dev, rank, world)
 
     for _ in range(args.warmup):
@@ -581,6 +633,8 @@ def main():
                  "pair_overflow": bool(log["pair_overflow"])}
     elif args.mode == "infer":
         extra = {"mean_ir": round(float(log["ir"].mean()), 5), "mean_corr": round(float(log["n_corr"].float().mean()), 1)}
+    elif args.mode == "operators":
+        extra = {"operators": log}
     elif args.mode == "teaser":
         info = log["info"]
         extra = {"teaser": {"valid": int(info[:, 0].sum()), "kcore_heuristic": int((info[:, 1] == 2).sum()),
@@ -626,7 +680,8 @@ def main():
         out = {
             "metric": metric,
             "value": round(units * world / elapsed * args.steps, 3),
-            "unit": {"corr4096": "solves/s", "icp": "refinements/s", "teaser": "solves/s"}.get(args.mode, "crops/s"),
+            "unit": {"corr4096": "solves/s", "icp": "refinements/s", "teaser": "solves/s",
+                     "operators": "operator sets/s"}.get(args.mode, "crops/s"),
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(total_ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -662,6 +717,8 @@ def main():
                 out["cpu_baseline"] = cpu_icp_baseline(32, args.icp_target)
             elif args.mode == "teaser":
                 out["cpu_baseline"] = cpu_teaser_baseline(8, args.teaser_n)
+            elif args.mode == "operators":
+                out["cpu_baseline"] = cpu_ops_baseline(2, args.op_points)
             elif args.mode == "infer":
                 out["cpu_baseline"] = cpu_infer_baseline(max(1, args.cpu_crops // 3), args.points, args.points,
                                                          args.hypotheses)
