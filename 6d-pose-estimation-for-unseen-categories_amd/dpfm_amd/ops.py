@@ -999,10 +999,16 @@ def ransac(src: torch.Tensor, src_off: torch.Tensor, dst: torch.Tensor, dst_off:
     work = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
     T = torch.empty((B, 4, 4), dtype=torch.float64, device=dev)
     stats = torch.empty((B, 3), dtype=torch.float64, device=dev)
-    # fp64 VALU work: ~30 flops per (hypothesis, correspondence) residual + ~6000 per 4-point fit
+    # fp64 VALU work: ~30 flops per (hypothesis, correspondence) residual + ~6000 per 4-point fit,
+    # over the TRUE correspondence counts (nmax is only a capacity): when a probe is timing the
+    # launch, the total count is snapshotted on the device and read after the timed region
+    wk = None
+    if _lib._probe is not None:
+        tot = (cor_off[-1] - cor_off[0]).clone()
+        wk = lambda: ("valu64", int(H) * (30 * int(tot.item()) + 6000 * B))  # noqa: E731
     call("pk_ransac", ptr(src), ptr(src_off), ptr(dst), ptr(dst_off), ptr(corres),
          ptr(cor_off), ptr(hyps), ptr(hyp_off), ctypes_u64(seed), int(H), float(max_dist), B, nmax, ptr(work),
-         nbytes, ptr(T), ptr(stats), _lib.stream(dev), work=("valu64", B * int(H) * (30 * nmax + 6000)))
+         nbytes, ptr(T), ptr(stats), _lib.stream(dev), work=wk)
     return T, stats
 
 

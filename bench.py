@@ -88,7 +88,7 @@ class KernelProbe:
         out = {}
         for k, lst in self.ev.items():
             ms = [s.elapsed_time(e) for s, e, _ in lst]
-            works = [w for _, _, w in lst]
+            works = [w() if callable(w) else w for _, _, w in lst]  # deferred: read after the timed region
             known = all(w is not None for w in works)
             out[k] = dict(avg_ms=float(np.mean(ms)), launches=len(ms), total_ms=float(np.sum(ms)),
                           bound=works[0][0] if known else None,
