@@ -153,6 +153,63 @@ __global__ __launch_bounds__(kIThreads) void icp_sort_kernel(const double* __res
   sidx[o] = i;
 }
 
+// grid (B), block 1024, dynamic LDS P x 12 B (P = the power of two >= nmax, <= 8192): the same
+// (x key, index) order as icp_sort_kernel by an in-LDS bitonic sort — log2(P)(log2(P)+1)/2 passes of
+// P/2 compare-exchanges instead of n^2 / 256 key comparisons per thread.
+__global__ __launch_bounds__(1024) void icp_bitonic_kernel(const double* __restrict__ pts,
+                                                           const int64_t* __restrict__ off, int nmax, int P,
+                                                           const double* __restrict__ M, double* __restrict__ sx,
+                                                           double* __restrict__ sy, double* __restrict__ sz,
+                                                           int32_t* __restrict__ sidx) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  uint64_t* key = lds;
+  int32_t* val = reinterpret_cast<int32_t*>(lds + P);
+  const int b = blockIdx.x;
+  const int64_t p0 = off[b];
+  const int n = (int)(off[b + 1] - p0);
+  const double* Pt = pts + 3 * p0;
+  const double* Mb = M ? M + 16 * b : nullptr;
+  for (int t = threadIdx.x; t < P; t += blockDim.x) {
+    if (t < n) {
+      const double* q = Pt + 3 * t;
+      key[t] = ordered_bits(Mb ? ((Mb[0] * q[0] + Mb[1] * q[1]) + Mb[2] * q[2]) + Mb[3] : q[0]);
+    } else {
+      key[t] = ~0ull;
+    }
+    val[t] = t;
+  }
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = threadIdx.x; t < P; t += blockDim.x) {
+        const int u = t ^ j;
+        if (u > t) {
+          const uint64_t ka = key[t], kb = key[u];
+          const int va = val[t], vb = val[u];
+          const bool b_less = kb < ka || (kb == ka && vb < va);
+          if (b_less == ((t & k) == 0)) {
+            key[t] = kb;
+            key[u] = ka;
+            val[t] = vb;
+            val[u] = va;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    const int i = val[t];
+    const int64_t o = (int64_t)b * nmax + t;
+    if (sx) {
+      sx[o] = Pt[3 * i];
+      sy[o] = Pt[3 * i + 1];
+      sz[o] = Pt[3 * i + 2];
+    }
+    sidx[o] = i;
+  }
+}
+
 // grid (B), block 1024: the x-bucket table of the sorted target: tbl[k] = first sorted index
 // with x >= xmin + k w (w = (xmax - xmin) / kNBuckets), by binary search per bucket. A query's
 // slab scan starts at the bucket BEFORE its lower edge's bucket, so a rounding of the bucket
@@ -395,16 +452,26 @@ extern "C" int pk_icp_init(const double* src, const int64_t* src_off, const doub
   const IcpWork w = carve(work, B, nsrc_max, ntgt_max);
   hipLaunchKernelGGL(icp_init_kernel, dim3(B), dim3(64), 0, s, T_init, w.st);
   PK_CHECK_LAUNCH();
-  if (ntgt_max > 0) {
-    hipLaunchKernelGGL(icp_sort_kernel, dim3((ntgt_max + kIThreads - 1) / kIThreads, B), dim3(kIThreads), 0, s, tgt,
-                       tgt_off, ntgt_max, nullptr, w.sx, w.sy, w.sz, w.sidx);
+  // x order of the targets (and of the source queries under T_init): bitonic in LDS up to 8192
+  // points per crop, rank counting beyond
+  auto sort = [&](const double* p, const int64_t* o, int nm, const double* M, double* x, double* y, double* z,
+                  int32_t* idx) -> int {
+    if (nm <= 0) return PK_OK;
+    int P = 1;
+    while (P < nm) P <<= 1;
+    if (P <= 8192) {
+      hipLaunchKernelGGL(icp_bitonic_kernel, dim3(B), dim3(1024), (size_t)P * 12, s, p, o, nm, P, M, x, y, z, idx);
+    } else {
+      hipLaunchKernelGGL(icp_sort_kernel, dim3((nm + kIThreads - 1) / kIThreads, B), dim3(kIThreads), 0, s, p, o, nm, M,
+                         x, y, z, idx);
+    }
     PK_CHECK_LAUNCH();
-  }
-  if (nsrc_max > 0) {
-    hipLaunchKernelGGL(icp_sort_kernel, dim3((nsrc_max + kIThreads - 1) / kIThreads, B), dim3(kIThreads), 0, s, src,
-                       src_off, nsrc_max, T_init, nullptr, nullptr, nullptr, w.perm);
-    PK_CHECK_LAUNCH();
-  }
+    return PK_OK;
+  };
+  int rc = sort(tgt, tgt_off, ntgt_max, nullptr, w.sx, w.sy, w.sz, w.sidx);
+  if (rc) return rc;
+  rc = sort(src, src_off, nsrc_max, T_init, nullptr, nullptr, nullptr, w.perm);
+  if (rc) return rc;
   hipLaunchKernelGGL(icp_bucket_kernel, dim3(B), dim3(1024), 0, s, tgt_off, ntgt_max, w.sx, w.st, w.tbl);
   PK_CHECK_LAUNCH();
   return PK_OK;
