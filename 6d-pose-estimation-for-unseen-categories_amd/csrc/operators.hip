@@ -416,6 +416,181 @@ __global__ __launch_bounds__(256) void dgemm_tn_kernel(const double* __restrict_
   if (i0 + ty < m && j0 + tx < m) G[((int64_t)b * m + i0 + ty) * m + j0 + tx] = acc;
 }
 
+// ---- dense fp64 Cholesky (blocked, lower, in place) and triangular solves for the shift-invert
+// subspace iteration: A + tau I = L L^T once per shape, then every iteration X <- L^-T L^-1 X.
+
+constexpr int kNB = 64;  // block size
+
+// grid (B), block 256: unblocked Cholesky of the kNB x kNB diagonal block at (k0, k0) in LDS;
+// a non-positive or NaN pivot sets fail[b].
+__global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, int n, int k0, int nb,
+                                                        int* __restrict__ fail) {
+  __shared__ double a[kNB][kNB + 1];
+  const int b = blockIdx.x;
+  double* Ab = A + (int64_t)b * n * n;
+  for (int e = threadIdx.x; e < nb * nb; e += 256) {
+    const int r = e / nb, c = e % nb;
+    a[r][c] = Ab[(int64_t)(k0 + r) * n + k0 + c];
+  }
+  __syncthreads();
+  for (int j = 0; j < nb; ++j) {
+    const double d = a[j][j];
+    if (!(d > 0.0)) {
+      if (threadIdx.x == 0) fail[b] = 1;
+      return;  // block-uniform (every thread read the same d)
+    }
+    const double s = sqrt(d);
+    __syncthreads();
+    if (threadIdx.x == 0) a[j][j] = s;
+    for (int i = j + 1 + threadIdx.x; i < nb; i += 256) a[i][j] /= s;
+    __syncthreads();
+    const int m = nb - j - 1;
+    for (int e = threadIdx.x; e < m * m; e += 256) {
+      const int i = j + 1 + e / m, c = j + 1 + e % m;
+      if (c <= i) a[i][c] -= a[i][j] * a[c][j];
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < nb * nb; e += 256) {
+    const int r = e / nb, c = e % nb;
+    if (c <= r) Ab[(int64_t)(k0 + r) * n + k0 + c] = a[r][c];
+  }
+}
+
+// grid (ceil(rows / 16), B), block 1024 = 16 waves, one wave per panel row i >= k0 + nb:
+// L_i = A_i L_kk^-T by forward substitution over the block's columns (lane = column).
+__global__ __launch_bounds__(1024) void chol_panel_kernel(double* __restrict__ A, int n, int k0, int nb) {
+  __shared__ double l[kNB][kNB + 1];
+  const int b = blockIdx.y;
+  double* Ab = A + (int64_t)b * n * n;
+  for (int e = threadIdx.x; e < nb * nb; e += 1024) {
+    const int r = e / nb, c = e % nb;
+    l[r][c] = c <= r ? Ab[(int64_t)(k0 + r) * n + k0 + c] : 0.0;
+  }
+  __syncthreads();
+  const int i = k0 + nb + blockIdx.x * 16 + pk::wave_id();
+  if (i >= n) return;
+  const int lane = pk::lane_id();
+  double* row = Ab + (int64_t)i * n + k0;
+  double v = lane < nb ? row[lane] : 0.0;
+  for (int j = 0; j < nb; ++j) {
+    const double xj = __shfl(v, j) / l[j][j];  // x_j (final once the earlier columns are removed)
+    if (lane == j) v = xj;
+    else if (lane > j) v -= xj * l[lane][j];
+  }
+  if (lane < nb) row[lane] = v;
+}
+
+// C (rows r0.., cols c0.., ld n) -= op(P) op(Q) with K = kk: generic batched fp64 update
+//   mode 0: C[i][j] -= sum_l A[ra + i][ka + l] * A[rb + j][ka + l]     (trailing update L21 L21^T; lower tiles)
+//   mode 1: C[i][j] -= sum_l A[ra + i][ka + l] * X[rb + l][j]          (forward solve update, X [n][m])
+//   mode 2: C[i][j] -= sum_l A[ka + l][ra + i] * X[rb + l][j]          (backward solve update, A transposed)
+// block 256 = 16 x 16 threads, 64 x 64 tile, K tiles of 16.
+template <int MODE>
+__global__ __launch_bounds__(256) void dgemm_sub_kernel(const double* __restrict__ A, const double* __restrict__ X,
+                                                        double* __restrict__ C, int n, int ldc, int rows, int cols,
+                                                        int kk, int ra, int rb, int ka, int r0, int c0) {
+  __shared__ double Ps[kGK][kGT + 1];
+  __shared__ double Qs[kGK][kGT + 1];
+  const int b = blockIdx.z;
+  const int ti = blockIdx.y, tj = blockIdx.x;
+  if (MODE == 0 && tj > ti) return;  // symmetric trailing matrix: lower tiles only (block-uniform)
+  const double* Ab = A + (int64_t)b * n * n;
+  const double* Xb = X ? X + (int64_t)b * n * ldc : nullptr;
+  double* Cb = C + (int64_t)b * n * ldc;
+  const int i0 = ti * kGT, j0 = tj * kGT;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  double acc[4][4] = {};
+  for (int l0 = 0; l0 < kk; l0 += kGK) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < kGT * kGK; e += 256) {
+      if (MODE == 2) {  // P[i][l] = A[ka + l][ra + i]: coalesced along i
+        const int ll = e / kGT, ii = e % kGT;
+        const int gi = i0 + ii, gl = l0 + ll;
+        Ps[ll][ii] = (gi < rows && gl < kk) ? Ab[(int64_t)(ka + gl) * n + ra + gi] : 0.0;
+      } else {  // P[i][l] = A[ra + i][ka + l]: coalesced along l
+        const int ii = e / kGK, ll = e % kGK;
+        const int gi = i0 + ii, gl = l0 + ll;
+        Ps[ll][ii] = (gi < rows && gl < kk) ? Ab[(int64_t)(ra + gi) * n + ka + gl] : 0.0;
+      }
+      if (MODE == 0) {  // Q[l][j] = A[rb + j][ka + l]
+        const int jj = e / kGK, ll = e % kGK;
+        const int gj = j0 + jj, gl = l0 + ll;
+        Qs[ll][jj] = (gj < cols && gl < kk) ? Ab[(int64_t)(rb + gj) * n + ka + gl] : 0.0;
+      } else {  // Q[l][j] = X[rb + l][j]
+        const int ll = e / kGT, jj = e % kGT;
+        const int gj = j0 + jj, gl = l0 + ll;
+        Qs[ll][jj] = (gj < cols && gl < kk) ? Xb[(int64_t)(rb + gl) * ldc + gj] : 0.0;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int l = 0; l < kGK; ++l) {
+      double p[4], q[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) p[i] = Ps[l][ty + 16 * i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) q[j] = Qs[l][tx + 16 * j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fma(p[i], q[j], acc[i][j]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gi = i0 + ty + 16 * i;
+    if (gi >= rows) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int gj = j0 + tx + 16 * j;
+      if (gj >= cols || (MODE == 0 && gj > gi)) continue;
+      Cb[(int64_t)(r0 + gi) * ldc + c0 + gj] -= acc[i][j];
+    }
+  }
+}
+
+// grid (ceil(m / 64), B), block 64: one right-hand-side column per thread; the diagonal block
+// L_kk staged in LDS; forward (Y_k = L_kk^-1 Y_k) or backward (X_k = L_kk^-T X_k) substitution
+// in place on rows [k0, k0 + nb) of X [n][m].
+template <bool FWD>
+__global__ __launch_bounds__(64) void trsv_block_kernel(const double* __restrict__ A, double* __restrict__ X, int n,
+                                                        int m, int k0, int nb) {
+  __shared__ double l[kNB][kNB + 1];
+  __shared__ double xs[kNB][64 + 1];
+  const int b = blockIdx.y;
+  const double* Ab = A + (int64_t)b * n * n;
+  double* Xb = X + (int64_t)b * n * m;
+  for (int e = threadIdx.x; e < nb * nb; e += 64) {
+    const int r = e / nb, c = e % nb;
+    l[r][c] = c <= r ? Ab[(int64_t)(k0 + r) * n + k0 + c] : 0.0;
+  }
+  const int col = blockIdx.x * 64 + threadIdx.x;
+  for (int r = 0; r < nb; ++r) xs[r][threadIdx.x] = col < m ? Xb[(int64_t)(k0 + r) * m + col] : 0.0;
+  __syncthreads();
+  if (col >= m) return;
+  if (FWD) {
+    for (int j = 0; j < nb; ++j) {
+      double v = xs[j][threadIdx.x];
+      for (int q = 0; q < j; ++q) v -= l[j][q] * xs[q][threadIdx.x];
+      xs[j][threadIdx.x] = v / l[j][j];
+    }
+  } else {
+    for (int j = nb - 1; j >= 0; --j) {
+      double v = xs[j][threadIdx.x];
+      for (int q = j + 1; q < nb; ++q) v -= l[q][j] * xs[q][threadIdx.x];
+      xs[j][threadIdx.x] = v / l[j][j];
+    }
+  }
+  for (int r = 0; r < nb; ++r) Xb[(int64_t)(k0 + r) * m + col] = xs[r][threadIdx.x];
+}
+
+// grid (ceil(n / 256), B): A += tau I on the first n_b diagonal entries (the shift of shift-invert)
+__global__ void add_diag_kernel(double* __restrict__ A, int n, double tau) {
+  const int b = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) A[((int64_t)b * n + i) * n + i] += tau;
+}
+
 }  // namespace
 
 extern "C" int pk_knn(const double* pts, const int64_t* off, int B, int nmax, int k, int omit_self, int32_t* idx,
@@ -489,5 +664,69 @@ extern "C" int pk_dgemm_tn(const double* X, const double* Y, int B, int n, int m
   hipLaunchKernelGGL(dgemm_tn_kernel, dim3((m + 15) / 16, (m + 15) / 16, B), dim3(256), 0, pk::as_stream(stream), X,
                      Y, n, m, G);
   PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+// Cholesky A + tau I = L L^T in place (lower triangle; the strict upper triangle is left as it
+// was), blocked by 64: per block column the diagonal factor (one workgroup), the panel solve (a
+// wave per row) and the symmetric trailing update (lower 64 x 64 tiles). fail int32 [B] (device,
+// zeroed here): 1 where a pivot was not positive (retry with a larger tau).
+extern "C" int pk_dpotrf(double* A, int B, int n, double tau, int32_t* fail, void* stream) {
+  PK_REQUIRE(B >= 0 && n >= 0);
+  if (B == 0 || n == 0) return PK_OK;
+  PK_REQUIRE(A && fail);
+  hipStream_t s = pk::as_stream(stream);
+  hipError_t e = pk::zero_async(fail, (size_t)B * sizeof(int32_t), s);
+  if (e != hipSuccess) return (int)e;
+  if (tau != 0.0) {
+    hipLaunchKernelGGL(add_diag_kernel, dim3((n + 255) / 256, B), dim3(256), 0, s, A, n, tau);
+    PK_CHECK_LAUNCH();
+  }
+  for (int k0 = 0; k0 < n; k0 += kNB) {
+    const int nb = min(kNB, n - k0);
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(B), dim3(256), 0, s, A, n, k0, nb, fail);
+    PK_CHECK_LAUNCH();
+    const int rest = n - k0 - nb;
+    if (rest <= 0) break;
+    hipLaunchKernelGGL(chol_panel_kernel, dim3((rest + 15) / 16, B), dim3(1024), 0, s, A, n, k0, nb);
+    PK_CHECK_LAUNCH();
+    const int t = (rest + kGT - 1) / kGT;
+    hipLaunchKernelGGL(dgemm_sub_kernel<0>, dim3(t, t, B), dim3(256), 0, s, A, nullptr, A, n, n, rest, rest, nb,
+                       k0 + nb, k0 + nb, k0, k0 + nb, k0 + nb);
+    PK_CHECK_LAUNCH();
+  }
+  return PK_OK;
+}
+
+// X [B][n][m] <- (L L^T)^-1 X in place with L from pk_dpotrf: blocked forward then backward
+// substitution (diagonal blocks one RHS column per thread, off-diagonal updates as GEMMs).
+extern "C" int pk_dpotrs(const double* L, double* X, int B, int n, int m, void* stream) {
+  PK_REQUIRE(B >= 0 && n >= 0 && m >= 0);
+  if (B == 0 || n == 0 || m == 0) return PK_OK;
+  PK_REQUIRE(L && X);
+  hipStream_t s = pk::as_stream(stream);
+  const int cb = (m + 63) / 64, ct = (m + kGT - 1) / kGT;
+  for (int k0 = 0; k0 < n; k0 += kNB) {  // L Y = X
+    const int nb = min(kNB, n - k0);
+    hipLaunchKernelGGL(trsv_block_kernel<true>, dim3(cb, B), dim3(64), 0, s, L, X, n, m, k0, nb);
+    PK_CHECK_LAUNCH();
+    const int rest = n - k0 - nb;
+    if (rest > 0) {  // X[k0 + nb:] -= L[k0 + nb:, k0:k0 + nb] Y_k
+      hipLaunchKernelGGL(dgemm_sub_kernel<1>, dim3(ct, (rest + kGT - 1) / kGT, B), dim3(256), 0, s, L, X, X, n, m,
+                         rest, m, nb, k0 + nb, k0, k0, k0 + nb, 0);
+      PK_CHECK_LAUNCH();
+    }
+  }
+  const int last = ((n - 1) / kNB) * kNB;
+  for (int k0 = last; k0 >= 0; k0 -= kNB) {  // L^T X = Y
+    const int nb = min(kNB, n - k0);
+    hipLaunchKernelGGL(trsv_block_kernel<false>, dim3(cb, B), dim3(64), 0, s, L, X, n, m, k0, nb);
+    PK_CHECK_LAUNCH();
+    if (k0 > 0) {  // X[:k0] -= L[k0:k0 + nb, :k0]^T X_k
+      hipLaunchKernelGGL(dgemm_sub_kernel<2>, dim3(ct, (k0 + kGT - 1) / kGT, B), dim3(256), 0, s, L, X, X, n, m, k0,
+                         m, nb, 0, k0, k0, 0, 0);
+      PK_CHECK_LAUNCH();
+    }
+  }
   return PK_OK;
 }

@@ -96,6 +96,8 @@ SIGNATURES = {
     "pk_sym_scale": [_P, _I, _I, _D, _P, _D, _P, _P],
     "pk_dgemm_cheb": [_P, _P, _P, _I, _I, _I, _D, _D, _D, _P, _P],
     "pk_dgemm_tn": [_P, _P, _I, _I, _I, _P, _P],
+    "pk_dpotrf": [_P, _I, _I, _D, _P, _P],
+    "pk_dpotrs": [_P, _P, _I, _I, _I, _P],
     "pk_teaser_solve": [_P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P],  # host pointers
 }
 

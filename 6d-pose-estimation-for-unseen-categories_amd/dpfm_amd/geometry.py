@@ -9,9 +9,12 @@ The reference computes the operators on the CPU when it fills its cache:
 (upstream diffusion-net geometry.compute_operators).
 
 Here every step runs in hand-written kernels (csrc/operators.hip): kNN, the local fans, the
-cotan assembly, and a Chebyshev-filtered subspace iteration for the 64 smallest eigenpairs of
-A = M^-1/2 (L + eps I) M^-1/2 whose block products are pk_dgemm_cheb / pk_dgemm_tn; only the
-m x m Rayleigh-Ritz / Cholesky problems (m = k + 32) are solved on the host. Dense fp64
+cotan assembly, and a shift-invert subspace iteration (eigsh's sigma mode) for the 64 smallest
+eigenpairs of A = M^-1/2 (L + eps I) M^-1/2: a blocked fp64 Cholesky of A + tau I (pk_dpotrf),
+blocked triangular solves (pk_dpotrs) and the block products pk_dgemm_cheb / pk_dgemm_tn; only the
+m x m Rayleigh-Ritz / Cholesky-QR problems (m = 2k) are solved on the host. (A Chebyshev-filtered
+variant, cheb_filter, converges too slowly on crop Laplacians: their spectral bound reaches ~1e4
+against lambda_64 ~ 3, because of tiny-mass points.) Dense fp64
 operators: N <= ~5000 per shape (200 MB for the CAD), well inside HBM.
 
 Returns what compute_operators returns that the model reads (mass, L, evals, evecs); frames and
@@ -71,28 +74,36 @@ def _orth(X):
     return X
 
 
-def subspace_eigs(A: torch.Tensor, counts: Sequence[int], k: int, extra: int = 64, degree: int = 24,
-                  tol: float = 1e-8, max_iter: int = 300, seed: int = 0):
+def subspace_eigs(A: torch.Tensor, counts: Sequence[int], k: int, extra: int = 64, tol: float = 1e-8,
+                  max_iter: int = 200, seed: int = 0, tau_rel: float = 1e-6):
     """k smallest eigenpairs of each symmetric A[b] (padding rows / columns of crop b beyond
-    counts[b] hold a large diagonal): Chebyshev-filtered subspace iteration with Rayleigh-Ritz.
-    Converged when every wanted residual |A x - theta x| <= tol * theta_k (ARPACK's relative
-    criterion at the k-th Ritz value; the operators are stored in fp32 downstream)."""
+    counts[b] hold a large diagonal) by shift-invert subspace iteration — eigsh's sigma mode:
+    A + tau I = L L^T once (pk_dpotrf; tau escalated x10 when a pivot fails, as compute_operators
+    escalates eps), then X <- (L L^T)^-1 X (pk_dpotrs), Cholesky-QR and a Rayleigh-Ritz step with
+    A itself per iteration. Converged when every wanted residual |A x - theta x| <= tol * theta_k
+    (ARPACK's relative criterion at the k-th Ritz value; the operators are stored in fp32
+    downstream). The rate per iteration is (lambda_k + tau) / (lambda_m + tau), m = k + extra."""
     B, N, _ = A.shape
     m = min(k + extra, min(counts))
     if m < k:
         raise ValueError(f"a shape has fewer points ({min(counts)}) than eigenpairs requested ({k})")
     upper = float(A.abs().sum(-1).amax())  # Gershgorin bound over the batch
+    tau = tau_rel * upper
+    for _ in range(6):
+        Lf = A.clone()
+        if not bool(ops.dpotrf(Lf, tau).any()):
+            break
+        tau *= 10.0
+    else:
+        raise RuntimeError("failed to compute eigendecomp (shifted Cholesky kept failing)")
     rng = np.random.default_rng(seed)
     X0 = rng.standard_normal((B, N, m))
     for b, n in enumerate(counts):
         X0[b, n:] = 0.0
     X = _orth(torch.as_tensor(X0, device=A.device))
-    cut = 0.05 * upper
-    theta = None
-    it = 0
-    res = None
+    theta, res, it = None, None, 0
     for it in range(1, max_iter + 1):
-        X = _orth(cheb_filter(A, X, degree, cut, upper))
+        X = _orth(ops.dpotrs(Lf, X.contiguous()))
         AX = ops.dgemm_cheb(A, X, None, 1.0, 0.0, 0.0)
         H = ops.dgemm_tn(X, AX).cpu().numpy()
         H = 0.5 * (H + np.swapaxes(H, 1, 2))
@@ -105,7 +116,6 @@ def subspace_eigs(A: torch.Tensor, counts: Sequence[int], k: int, extra: int = 6
         res = R.norm(dim=1).amax(-1) / theta[:, k - 1].abs().clamp(min=1e-300)
         if float(res.max()) < tol:
             break
-        cut = float(th[:, m - 1].min())
     return theta[:, :k], X[:, :, :k], it, res
 
 

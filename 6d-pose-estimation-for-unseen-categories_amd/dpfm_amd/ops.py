@@ -1159,6 +1159,23 @@ def dgemm_tn(X: torch.Tensor, Y: torch.Tensor) -> torch.Tensor:
     return G
 
 
+def dpotrf(A: torch.Tensor, tau: float = 0.0):
+    """pk_dpotrf in place on A [B, n, n] (fp64): lower Cholesky of A + tau I; returns the int32 [B]
+    failure flags (device)."""
+    B, n, _ = A.shape
+    fail = torch.empty((max(B, 1),), dtype=torch.int32, device=A.device)
+    call("pk_dpotrf", ptr(A), B, int(n), float(tau), ptr(fail), _lib.stream(A.device),
+         work=("valu64", B * n ** 3 // 3))
+    return fail[:B]
+
+
+def dpotrs(L: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
+    """pk_dpotrs: X <- (L L^T)^-1 X in place (X [B, n, m] fp64, contiguous)."""
+    B, n, m = X.shape
+    call("pk_dpotrs", ptr(L), ptr(X), B, int(n), int(m), _lib.stream(X.device), work=("valu64", 2 * B * n * n * m))
+    return X
+
+
 def pose_metrics(cad: torch.Tensor, off: torch.Tensor, nmax: int, T_est: torch.Tensor, T_gt: torch.Tensor):
     """pk_pose_metrics -> f64 [B, 7] (ADD, xyz-direction means x3, ADD-S 1-D means x3)."""
     B = off.numel() - 1

@@ -537,6 +537,11 @@ int pk_sym_scale(const int64_t* off, int B, int nmax, double eps, const double* 
 int pk_dgemm_cheb(const double* A, const double* Y, const double* X, int B, int n, int m, double alpha, double beta,
                   double gamma, double* out, void* stream);
 int pk_dgemm_tn(const double* X, const double* Y, int B, int n, int m, double* G, void* stream);
+/* Shift-invert support: pk_dpotrf factors A[b] + tau I = L L^T in place (lower triangle, blocked by
+ * 64; fail int32 [B] = 1 where a pivot was not positive); pk_dpotrs solves X <- (L L^T)^-1 X in
+ * place for X [B,n,m]. */
+int pk_dpotrf(double* A, int B, int n, double tau, int32_t* fail, void* stream);
+int pk_dpotrs(const double* L, double* X, int B, int n, int m, void* stream);
 
 #ifdef __cplusplus
 }

@@ -63,8 +63,15 @@ def test_subspace_iteration_matches_eigsh(monkeypatch):
         out = alpha * torch.bmm(A, Y) + beta * Y
         return out + gamma * X if X is not None else out
 
+    def potrf(A, tau=0.0):
+        L = torch.linalg.cholesky(A + tau * torch.eye(A.shape[-1], dtype=A.dtype))
+        A.copy_(L)
+        return torch.zeros(A.shape[0], dtype=torch.int32)
+
     monkeypatch.setattr(ops, "dgemm_cheb", cheb)
     monkeypatch.setattr(ops, "dgemm_tn", lambda X, Y: torch.bmm(X.transpose(1, 2), Y))
+    monkeypatch.setattr(ops, "dpotrf", potrf)
+    monkeypatch.setattr(ops, "dpotrs", lambda L, X: X.copy_(torch.cholesky_solve(X, L)))
     rng = np.random.default_rng(1)
     shapes = [ellipsoid(rng, 350), ellipsoid(rng, 300, (6.0, 3.0, 2.0))]
     nmax, k, eps = 350, 24, 1e-8
@@ -83,7 +90,7 @@ def test_subspace_iteration_matches_eigsh(monkeypatch):
         A[b, n:, n:] = np.eye(nmax - n) * upper
     ev, W, it, res = geometry.subspace_eigs(torch.as_tensor(A), [350, 300], k, tol=1e-9)
     print("iterations", it, "residual", res)
-    assert float(res.max()) < 1e-9 and it < 100
+    assert float(res.max()) < 1e-9 and it < 60
     for b, (L, M) in enumerate(zip(Ls, Ms)):
         n = L.shape[0]
         ref, V = OO.eigsh_operators(L, M, k, eps)

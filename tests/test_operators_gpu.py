@@ -140,3 +140,26 @@ def test_get_operators_matches_eigsh(device, kind):
         np.testing.assert_allclose(E.T @ (Mr[:, None] * E), np.eye(k), atol=1e-7)
         r = (Lr + eps * np.eye(n)) @ E - (Mr[:, None] * E) * ev[b][None, :]
         assert np.abs(r).max() < 1e-6 * max(1.0, ev[b].max())
+
+
+@pytest.mark.parametrize("n", [64, 150, 333])
+def test_dpotrf_dpotrs(device, n):
+    """Blocked Cholesky (64-blocks, ragged last block) and the blocked triangular solves against
+    torch fp64; a non-SPD matrix sets the failure flag."""
+    from dpfm_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(n)
+    M = torch.randn(2, n, n, dtype=torch.float64, generator=g)
+    A = (M @ M.transpose(1, 2) / n + 0.1 * torch.eye(n, dtype=torch.float64)).to(device)
+    Lf = A.clone()
+    fail = ops.dpotrf(Lf, 0.05)
+    assert not bool(fail.any())
+    ref = torch.linalg.cholesky(A.cpu() + 0.05 * torch.eye(n, dtype=torch.float64))
+    got = torch.tril(Lf.cpu())
+    assert (got - ref).abs().max() < 1e-12 * ref.abs().max()
+    X = torch.randn(2, n, 70, dtype=torch.float64, generator=g)
+    Y = ops.dpotrs(Lf, X.to(device).contiguous()).cpu()
+    Yr = torch.cholesky_solve(X, ref)
+    assert (Y - Yr).abs().max() < 1e-10 * Yr.abs().max()
+    bad = A.clone()
+    bad[1] -= 10.0 * torch.eye(n, dtype=torch.float64, device=device)
+    assert ops.dpotrf(bad, 0.0).cpu().tolist() == [0, 1]
