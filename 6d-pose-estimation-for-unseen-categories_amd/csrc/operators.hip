@@ -550,39 +550,47 @@ __global__ __launch_bounds__(256) void dgemm_sub_kernel(const double* __restrict
   }
 }
 
-// grid (ceil(m / 64), B), block 64: one right-hand-side column per thread; the diagonal block
-// L_kk staged in LDS; forward (Y_k = L_kk^-1 Y_k) or backward (X_k = L_kk^-T X_k) substitution
-// in place on rows [k0, k0 + nb) of X [n][m].
+// grid (ceil(m / 64), B), block 64: one right-hand-side column per thread, held in registers
+// (fully unrolled, 246 VGPRs); the diagonal block L_kk staged in LDS (identity-padded past nb, so a
+// ragged last block needs no branches); substitution in place on rows [k0, k0 + nb) of X [n][m].
+// After x_j is known every remaining row takes one independent FMA, so the 2016 FMAs do not form
+// one dependent chain.
 template <bool FWD>
 __global__ __launch_bounds__(64) void trsv_block_kernel(const double* __restrict__ A, double* __restrict__ X, int n,
                                                         int m, int k0, int nb) {
+  // One loop for both sweeps: the backward sweep L^T x = y runs as written; the forward sweep
+  // L y = b is the same loop on the index-reversed problem (i -> 63 - i turns the lower solve
+  // into the upper one): l[a][c] = L[63 - c][63 - a], x'[i] = x[63 - i].
   __shared__ double l[kNB][kNB + 1];
-  __shared__ double xs[kNB][64 + 1];
   const int b = blockIdx.y;
   const double* Ab = A + (int64_t)b * n * n;
   double* Xb = X + (int64_t)b * n * m;
-  for (int e = threadIdx.x; e < nb * nb; e += 64) {
-    const int r = e / nb, c = e % nb;
-    l[r][c] = c <= r ? Ab[(int64_t)(k0 + r) * n + k0 + c] : 0.0;
+  for (int e = threadIdx.x; e < kNB * kNB; e += 64) {
+    const int r = e / kNB, c = e % kNB;
+    const double v = (r < nb && c < nb) ? (c <= r ? Ab[(int64_t)(k0 + r) * n + k0 + c] : 0.0) : (r == c ? 1.0 : 0.0);
+    if (FWD) l[kNB - 1 - c][kNB - 1 - r] = v;
+    else l[r][c] = v;
   }
-  const int col = blockIdx.x * 64 + threadIdx.x;
-  for (int r = 0; r < nb; ++r) xs[r][threadIdx.x] = col < m ? Xb[(int64_t)(k0 + r) * m + col] : 0.0;
   __syncthreads();
+  const int col = blockIdx.x * 64 + threadIdx.x;
   if (col >= m) return;
-  if (FWD) {
-    for (int j = 0; j < nb; ++j) {
-      double v = xs[j][threadIdx.x];
-      for (int q = 0; q < j; ++q) v -= l[j][q] * xs[q][threadIdx.x];
-      xs[j][threadIdx.x] = v / l[j][j];
-    }
-  } else {
-    for (int j = nb - 1; j >= 0; --j) {
-      double v = xs[j][threadIdx.x];
-      for (int q = j + 1; q < nb; ++q) v -= l[q][j] * xs[q][threadIdx.x];
-      xs[j][threadIdx.x] = v / l[j][j];
-    }
+  double x[kNB];
+#pragma unroll
+  for (int i = 0; i < kNB; ++i) {
+    const int r = FWD ? kNB - 1 - i : i;
+    x[i] = r < nb ? Xb[(int64_t)(k0 + r) * m + col] : 0.0;
   }
-  for (int r = 0; r < nb; ++r) Xb[(int64_t)(k0 + r) * m + col] = xs[r][threadIdx.x];
+#pragma unroll
+  for (int j = kNB - 1; j >= 0; --j) {
+    x[j] /= l[j][j];
+#pragma unroll
+    for (int q = 0; q < j; ++q) x[q] = fma(-l[j][q], x[j], x[q]);
+  }
+#pragma unroll
+  for (int i = 0; i < kNB; ++i) {
+    const int r = FWD ? kNB - 1 - i : i;
+    if (r < nb) Xb[(int64_t)(k0 + r) * m + col] = x[i];
+  }
 }
 
 // grid (ceil(n / 256), B): A += tau I on the first n_b diagonal entries (the shift of shift-invert)

@@ -71,7 +71,7 @@ def test_subspace_iteration_matches_eigsh(monkeypatch):
     monkeypatch.setattr(ops, "dgemm_cheb", cheb)
     monkeypatch.setattr(ops, "dgemm_tn", lambda X, Y: torch.bmm(X.transpose(1, 2), Y))
     monkeypatch.setattr(ops, "dpotrf", potrf)
-    monkeypatch.setattr(ops, "dpotrs", lambda L, X: X.copy_(torch.cholesky_solve(X, L)))
+    monkeypatch.setattr(ops, "dpotrs", lambda L, X: X.copy_(torch.cholesky_solve(X, torch.tril(L))))
     rng = np.random.default_rng(1)
     shapes = [ellipsoid(rng, 350), ellipsoid(rng, 300, (6.0, 3.0, 2.0))]
     nmax, k, eps = 350, 24, 1e-8
