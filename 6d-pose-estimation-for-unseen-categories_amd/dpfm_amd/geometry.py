@@ -12,7 +12,7 @@ Here every step runs in hand-written kernels (csrc/operators.hip): kNN, the loca
 cotan assembly, and a shift-invert subspace iteration (eigsh's sigma mode) for the 64 smallest
 eigenpairs of A = M^-1/2 (L + eps I) M^-1/2: a blocked fp64 Cholesky of A + tau I (pk_dpotrf),
 blocked triangular solves (pk_dpotrs) and the block products pk_dgemm_cheb / pk_dgemm_tn; only the
-m x m Rayleigh-Ritz / Cholesky-QR problems (m = 2k) are solved on the host. (A Chebyshev-filtered
+m x m Rayleigh-Ritz / Cholesky-QR problems (m = 2k) use torch.linalg on the device. (A Chebyshev-filtered
 variant, cheb_filter, converges too slowly on crop Laplacians: their spectral bound reaches ~1e4
 against lambda_64 ~ 3, because of tiny-mass points.) Dense fp64
 operators: N <= ~5000 per shape (200 MB for the CAD), well inside HBM.
@@ -65,12 +65,12 @@ def cheb_filter(A, X, degree: int, a: float, b: float, a0: float = 0.0):
 
 
 def _orth(X):
-    """Cholesky QR (twice): X <- X R^-1 with R^T R = X^T X (R from the m x m Gram, on the host)."""
+    """Cholesky QR (twice): X <- X R^-1 with R^T R = X^T X (the m x m Gram from pk_dgemm_tn; the
+    m x m Cholesky and triangular solve stay on the device, no host round trip)."""
     for _ in range(2):
-        G = ops.dgemm_tn(X, X).cpu().numpy()
-        G = 0.5 * (G + np.swapaxes(G, 1, 2))
-        Rinv = np.stack([np.linalg.inv(np.linalg.cholesky(g).T) for g in G])
-        X = torch.bmm(X, torch.as_tensor(Rinv, device=X.device))
+        G = ops.dgemm_tn(X, X)
+        R = torch.linalg.cholesky(0.5 * (G + G.transpose(1, 2)), upper=True)
+        X = torch.linalg.solve_triangular(R, X, upper=True, left=False)
     return X
 
 
@@ -112,13 +112,10 @@ def subspace_eigs(A: torch.Tensor, counts: Sequence[int], k: int, extra: int = 6
     for it in range(1, max_iter + 1):
         X = _orth(ops.dgemm_cheb(Ainv, X, None, 1.0, 0.0, 0.0))
         AX = ops.dgemm_cheb(A, X, None, 1.0, 0.0, 0.0)
-        H = ops.dgemm_tn(X, AX).cpu().numpy()
-        H = 0.5 * (H + np.swapaxes(H, 1, 2))
-        th, W = np.linalg.eigh(H)
-        Wt = torch.as_tensor(W, device=A.device)
+        H = ops.dgemm_tn(X, AX)
+        theta, Wt = torch.linalg.eigh(0.5 * (H + H.transpose(1, 2)))  # m x m Rayleigh-Ritz, on the device
         X = torch.bmm(X, Wt)
         AX = torch.bmm(AX, Wt)
-        theta = torch.as_tensor(th, device=A.device)
         R = AX[:, :, :k] - X[:, :, :k] * theta[:, None, :k]
         res = R.norm(dim=1).amax(-1) / theta[:, k - 1].abs().clamp(min=1e-300)
         if float(res.max()) < tol:
