@@ -19,6 +19,11 @@ run() {  # name timeout cmd...
 }
 for step in "$@"; do
   case $step in
+    icp) run icp 200 python bench.py --mode icp ;;
+    teaser) run teaser 200 python bench.py --mode teaser --steps 5 --warmup 1 ;;
+    ops) run ops 300 python bench.py --mode operators --batch 8 --steps 3 --warmup 1 ;;
+    infer) run infer 300 python bench.py --mode infer ;;
+    corr) run corr 300 python bench.py --mode corr4096 ;;
     tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
@@ -40,18 +45,11 @@ for step in "$@"; do
     fdpmc) run fdpmc1 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$out/fdpmc1" -o run -- python tools/fd_bench.py 2
            python tools/mfma_util.py "$out/fdpmc1" fd_main_kernel fd_prep_kernel > "$out/mfma_util.json" 2>&1
            run fdpmc2 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$out/fdpmc2" -o run -- python tools/fd_bench.py 2 ;;
-    diag) run diag 300 python tools/diag_model.py ;;
     tprof) run tprof 300 python tools/torch_prof.py "$tag" ;;
-    rdiag) run rdiag 300 python tools/replay_diag.py default ;;
     rdiag2) run rdiag2 300 python tools/replay_diag2.py ;;
     rdiag3) run rdiag3 300 python tools/replay_diag3.py ;;
-    gdump) run gdump 300 python tools/graph_dump.py "$tag" ;;
     mprobe) run mprobe 300 python tools/memset_graph_probe.py ;;
     mprobe_nopc) DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run mprobe_nopc 300 python tools/memset_graph_probe.py ;;
-    gtrace) run gtrace 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d "$out/gtrace" -o run -- python tools/graph_dump.py "$tag" ;;
-    rdiag_rocblas) run rdiag_rocblas 300 python tools/replay_diag.py cublas ;;
-    gdiag) run gdiag 300 python tools/graph_diag.py ;;
-    gdiag_rocblas) run gdiag_rocblas 300 python tools/graph_diag.py cublas ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
