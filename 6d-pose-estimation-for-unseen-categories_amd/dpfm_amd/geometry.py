@@ -70,7 +70,7 @@ def _orth(X):
     for _ in range(2):
         G = ops.dgemm_tn(X, X)
         R = torch.linalg.cholesky(0.5 * (G + G.transpose(1, 2)), upper=True)
-        X = torch.linalg.solve_triangular(R, X, upper=True, left=False)
+        X = torch.linalg.solve_triangular(R, X, upper=True, left=False).contiguous()
     return X
 
 
