@@ -63,6 +63,111 @@ __global__ __launch_bounds__(256) void rigid_score_kernel(const int64_t* __restr
   if (jj < n) score[(int64_t)b * ldl + jj] = acc / (float)n;
 }
 
+// Symmetric scoring: the pair term |‖CAD_i − CAD_j‖ − ‖PC_i − PC_j‖| is the same for (i, j) and
+// (j, i), so each unordered pair is evaluated once (two sqrt per pair instead of four). Grid
+// (T (T + 1) / 2, B) over 64 x 64 tile pairs I <= J of the current list (T = ceil(nmax / 64));
+// block 256 = 16 x 16 threads, 4 x 4 pairs each. A block writes, for every list entry x of tile
+// I, the sum over tile J (part[b][J][x]) and, when I != J, for every entry of tile J the sum over
+// tile I (part[b][I][x]): each (tile, entry) slot is written exactly once, and rigid_reduce_kernel
+// adds the slots in tile order (deterministic).
+constexpr int kRT = 64;
+__global__ __launch_bounds__(256) void rigid_pair_kernel(const int64_t* __restrict__ list, int ldl,
+                                                         const int32_t* __restrict__ nlist,
+                                                         const int64_t* __restrict__ cand, int ldc,
+                                                         const float* __restrict__ cad, int ldcad,
+                                                         const float* __restrict__ pc, int ldpc, int T,
+                                                         float* __restrict__ part) {
+  __shared__ float si[kRT][7], sj[kRT][7];
+  __shared__ float red[16][kRT + 1];
+  const int b = blockIdx.y;
+  const int n = nlist[b];
+  const int t = blockIdx.x;
+  int J = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
+  while ((J + 1) * (J + 2) / 2 <= t) ++J;
+  while (J * (J + 1) / 2 > t) --J;
+  const int I = t - J * (J + 1) / 2;
+  if (J * kRT >= n) return;  // block-uniform: tile outside this round's list
+  const int64_t* L = list + (int64_t)b * ldl;
+  const int64_t* Cd = cand + (int64_t)b * ldc * 2;
+  const float* CA = cad + (int64_t)b * ldcad * 3;
+  const float* PCb = pc + (int64_t)b * ldpc * 3;
+  const int tid = threadIdx.x;
+  if (tid < 2 * kRT) {
+    const int e = tid & (kRT - 1);
+    const int x = (tid < kRT ? I : J) * kRT + e;
+    float (*dst)[7] = tid < kRT ? si : sj;
+    if (x < n) {
+      const int64_t k = L[x];
+      const int64_t c = Cd[2 * k], q = Cd[2 * k + 1];
+      dst[e][0] = CA[3 * c]; dst[e][1] = CA[3 * c + 1]; dst[e][2] = CA[3 * c + 2];
+      dst[e][3] = PCb[3 * q]; dst[e][4] = PCb[3 * q + 1]; dst[e][5] = PCb[3 * q + 2];
+      dst[e][6] = 1.f;
+    } else {
+      dst[e][0] = dst[e][1] = dst[e][2] = dst[e][3] = dst[e][4] = dst[e][5] = 0.f;
+      dst[e][6] = 0.f;
+    }
+  }
+  __syncthreads();
+  const int tx = tid & 15, ty = tid >> 4;
+  float ra[4] = {0.f, 0.f, 0.f, 0.f}, ca[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = ty * 4 + r;
+    const float ax = si[i][0], ay = si[i][1], az = si[i][2], px = si[i][3], py = si[i][4], pz = si[i][5];
+    const float vi = si[i][6];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int j = tx * 4 + c;
+      const float dx = sj[j][0] - ax, dy = sj[j][1] - ay, dz = sj[j][2] - az;
+      const float ex = sj[j][3] - px, ey = sj[j][4] - py, ez = sj[j][5] - pz;
+      const float a = __builtin_amdgcn_sqrtf((dx * dx + dy * dy) + dz * dz);
+      const float bb = __builtin_amdgcn_sqrtf((ex * ex + ey * ey) + ez * ez);
+      const float v = fabsf(a - bb) * (vi * sj[j][6]);  // invalid entries contribute 0
+      ra[r] += v;
+      ca[c] += v;
+    }
+  }
+  float* P = part + (int64_t)b * T * ldl;
+  // row sums of tile I over tile J: reduce over tx in order
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[tx][ty * 4 + r] = ra[r];
+  __syncthreads();
+  if (tid < kRT) {
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc += red[q][tid];
+    const int x = I * kRT + tid;
+    if (x < n) P[(int64_t)J * ldl + x] = acc;
+  }
+  if (I == J) return;  // block-uniform; the diagonal tile's row sums already cover both orders
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < 4; ++c) red[ty][tx * 4 + c] = ca[c];
+  __syncthreads();
+  if (tid < kRT) {
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc += red[q][tid];
+    const int x = J * kRT + tid;
+    if (x < n) P[(int64_t)I * ldl + x] = acc;
+  }
+}
+
+// grid (ceil(nmax / 256), B): score[x] = (sum over tiles in order of part[b][tile][x]) / n.
+__global__ __launch_bounds__(256) void rigid_reduce_kernel(const int32_t* __restrict__ nlist, int ldl,
+                                                           const float* __restrict__ part, int T,
+                                                           float* __restrict__ score) {
+  const int b = blockIdx.y;
+  const int n = nlist[b];
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  if (x >= n) return;
+  const int nt = (n + kRT - 1) / kRT;
+  const float* P = part + (int64_t)b * T * ldl + x;
+  float acc = 0.f;
+  for (int q = 0; q < nt; ++q) acc += P[(int64_t)q * ldl];
+  score[(int64_t)b * ldl + x] = acc / (float)n;
+}
+
 // One block per crop: ordered compaction of list entries whose score < tau * diam.
 // round 3 (fallback > 0): if nothing passes tau, use the fallback threshold.
 // thr f32 [B, 4]: tau * diam_cad for tau = 0.3, 0.15, 0.055, 0.065, evaluated in double and
@@ -439,10 +544,15 @@ __global__ __launch_bounds__(64) void cgt_solve_kernel(const double* __restrict_
 
 }  // namespace
 
+extern "C" int64_t pk_rigidity_filter_work_size(int B, int nmax, int ldc) {
+  if (B <= 0 || nmax <= 0) return 0;
+  return (int64_t)B * ((nmax + kRT - 1) / kRT) * ldc * (int64_t)sizeof(float);
+}
+
 extern "C" int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* ncand, const float* cad,
                                   int ldcad, const float* pc, int ldpc, const float* thr4, int B, int nmax,
                                   int64_t* list_a, int64_t* list_b, int32_t* n_a, int32_t* n_b, float* score,
-                                  void* stream) {
+                                  float* partial, void* stream) {
   PK_REQUIRE(B >= 0 && nmax >= 0 && ldc >= nmax);
   if (B == 0) return PK_OK;
   PK_REQUIRE(cand && ncand && cad && pc && thr4 && list_a && list_b && n_a && n_b && score);
@@ -455,9 +565,17 @@ extern "C" int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* n
   int64_t* lout = list_b;
   int32_t* nout = n_b;
   int32_t* nspare = n_a;
+  const int T = (nmax + kRT - 1) / kRT;
   for (int r = 0; r < 3; ++r) {
-    hipLaunchKernelGGL(rigid_score_kernel, g, dim3(256), 0, s, lin, ldc, nin, cand, ldc, cad, ldcad, pc, ldpc,
-                       score);
+    if (partial && T > 0) {  // symmetric pair tiles + ordered reduction
+      hipLaunchKernelGGL(rigid_pair_kernel, dim3(T * (T + 1) / 2, B), dim3(256), 0, s, lin, ldc, nin, cand, ldc, cad,
+                         ldcad, pc, ldpc, T, partial);
+      PK_CHECK_LAUNCH();
+      hipLaunchKernelGGL(rigid_reduce_kernel, g, dim3(256), 0, s, nin, ldc, partial, T, score);
+    } else {
+      hipLaunchKernelGGL(rigid_score_kernel, g, dim3(256), 0, s, lin, ldc, nin, cand, ldc, cad, ldcad, pc, ldpc,
+                         score);
+    }
     PK_CHECK_LAUNCH();
     hipLaunchKernelGGL(rigid_compact_kernel, dim3(B), dim3(1024), 0, s, lin, ldc, nin, score, thr4, r, lout,
                        nout);

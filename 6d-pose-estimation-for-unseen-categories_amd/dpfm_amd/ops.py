@@ -953,11 +953,13 @@ def rigidity_filter(cand: torch.Tensor, ncand: torch.Tensor, cad: torch.Tensor, 
     na = torch.empty((B,), dtype=torch.int32, device=dev)
     nb = torch.empty((B,), dtype=torch.int32, device=dev)
     score = torch.empty((B, L), dtype=torch.float32, device=dev)
-    # f32 VALU work of the first (largest) round: per candidate pair two 3-D distances and
-    # |a - b| accumulated, ~20 flops (the later rounds run on its survivors)
+    nbytes = int(_lib.lib().pk_rigidity_filter_work_size(B, L, L))
+    part = torch.empty((max(nbytes // 4, 1),), dtype=torch.float32, device=dev)
+    # f32 VALU work of the first (largest) round: per UNORDERED candidate pair (the term is
+    # symmetric) two 3-D distances and |a - b|, ~20 flops (later rounds run on its survivors)
     call("pk_rigidity_filter", ptr(cand.contiguous()), L, ptr(ncand), ptr(cad.contiguous()), cad.shape[1],
          ptr(pc.contiguous()), pc.shape[1], ptr(thr4), B, L, ptr(la), ptr(lb), ptr(na), ptr(nb), ptr(score),
-         _lib.stream(dev), work=("valu32", 20 * B * L * L))
+         ptr(part), _lib.stream(dev), work=("valu32", 10 * B * L * L))
     return lb, nb
 
 

@@ -341,11 +341,15 @@ int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, const float
  * on device with the 0.055 -> 0.065 fallback.
  *   cand int64 [B,ldc,2] (cad idx, pc idx), ncand int32 [B]; cad f32 [B,ldcad,3],
  *   pc f32 [B,ldpc,3]; thr4 f32 [B,4] = diam * (0.3, 0.15, 0.055, 0.065)
- *   list_a/list_b int64 [B,ldc], n_a/n_b int32 [B], score f32 [B,ldc] scratch.
+ *   list_a/list_b int64 [B,ldc], n_a/n_b int32 [B], score f32 [B,ldc] scratch;
+ *   partial f32 scratch of pk_rigidity_filter_work_size(B, nmax, ldc) bytes, or NULL: with it each
+ *   unordered candidate pair is evaluated once (64 x 64 tile pairs, per-tile partial sums added in
+ *   tile order); without it every candidate sums over all others itself.
  * Result: survivors' candidate rows in list_b[b, :n_b[b]] (input order). */
+int64_t pk_rigidity_filter_work_size(int B, int nmax, int ldc);
 int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* ncand, const float* cad, int ldcad,
                        const float* pc, int ldpc, const float* thr4, int B, int nmax, int64_t* list_a,
-                       int64_t* list_b, int32_t* n_a, int32_t* n_b, float* score, void* stream);
+                       int64_t* list_b, int32_t* n_a, int32_t* n_b, float* score, float* partial, void* stream);
 
 /* H12 inlier ratio (utils/utils.py:81-105) per crop: mean(||cad[c] - pc_aligned[p]|| < thr),
  * 0 when there are no correspondences.
