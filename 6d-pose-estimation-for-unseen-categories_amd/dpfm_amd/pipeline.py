@@ -594,6 +594,60 @@ class GraphedInfer:
         return self.out
 
 
+class PipelinedInfer:
+    """Crop formation of batch i+1 overlapped with inference on batch i (the inference twin of
+    PipelinedTrainer): graph C_k forms crops into buffer k on a side stream, graph I_k runs
+    InferStep on buffer k on the main stream; events order C_k after I_k's previous use of the
+    buffer and I_k after C_k. Crop formation (FPS, SOR: one workgroup per crop, latency-bound)
+    then hides under the model, the correspondence head and RANSAC (wide kernels). Each call
+    returns the static outputs of the graph it replayed (overwritten two calls later)."""
+
+    def __init__(self, crop_formation: CropFormation, infer: InferStep, fb: FrameBatch, op: Operators,
+                 warmup: int = 2):
+        self.main = torch.cuda.current_stream()
+        self.side = torch.cuda.Stream()
+        tmp = torch.cuda.Stream()
+        tmp.wait_stream(self.main)
+        with torch.cuda.stream(tmp):
+            for _ in range(warmup):
+                infer(fb, op, crop_formation(fb))
+        self.main.wait_stream(tmp)
+        torch.cuda.synchronize()
+        self.crop_graphs, self.crops, self.infer_graphs, self.outs = [], [], [], []
+        for k in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.crops.append(crop_formation(fb))
+            self.crop_graphs.append(g)
+        for k in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.outs.append(infer(fb, op, self.crops[k]))
+            self.infer_graphs.append(g)
+        self.formed = [torch.cuda.Event(), torch.cuda.Event()]
+        self.consumed = [torch.cuda.Event(), torch.cuda.Event()]
+        for k in range(2):
+            self.consumed[k].record(self.main)
+        self.i = 0
+        self._form(0)
+
+    def _form(self, k):
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(self.consumed[k])
+            self.crop_graphs[k].replay()
+            self.formed[k].record(self.side)
+
+    def __call__(self) -> dict:
+        k = self.i & 1
+        self._form(k ^ 1)  # the next batch's crops, concurrently
+        with torch.cuda.stream(self.main):
+            self.main.wait_event(self.formed[k])
+            self.infer_graphs[k].replay()
+            self.consumed[k].record(self.main)
+        self.i += 1
+        return self.outs[k]
+
+
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     """Rank-contiguous partition of n crops (configs[3]: 256 crops over 8 GPUs): rank r takes
     [r*n//world, (r+1)*n//world)."""

@@ -316,19 +316,25 @@ def build_infer(args, dev, rank, world):
     own shard of the batch, no collective on the data path): one inference pass per iteration."""
     from dpfm_amd.dataset.object import CropFormation
     from dpfm_amd.models.dpfm import DPFMNet
-    from dpfm_amd.pipeline import GraphedInfer, InferStep, make_frame_batch
+    from dpfm_amd.pipeline import GraphedInfer, InferStep, PipelinedInfer, make_frame_batch
     B, N = args.batch, args.points
     torch.manual_seed(1234)
     model = DPFMNet().to(dev).eval()
     fb, op = make_frame_batch(B, N, N, seed=1000 * rank, device=dev)
     crops_of = CropFormation(n1=N, npoint=N, seed=0, base=rank * B)
     infer = InferStep(model, hypotheses=args.hypotheses, seed=0)
-    one_step = (lambda: infer(fb, op, crops_of(fb))) if args.eager else GraphedInfer(crops_of, infer, fb, op)
+    if args.eager:
+        one_step = lambda: infer(fb, op, crops_of(fb))  # noqa: E731
+    elif args.no_overlap:
+        one_step = GraphedInfer(crops_of, infer, fb, op)
+    else:  # crop formation of the next batch on a second stream, as in training
+        one_step = PipelinedInfer(crops_of, infer, fb, op)
     name = "configs[3] shard" if N == 2048 else "configs[1]"
     config = {"workload": f"{name}: B={B} synthetic 640x480 RGB-D crops/GPU, {N} pts, inference (eval.py + "
                           f"test_RANSAC.py: top-5 + 3-round rigidity filter + IR + RANSAC {args.hypotheses} "
                           "hypotheses + ADD metrics), batch-sharded across ranks (weak scaling)",
-              "execution": "eager" if args.eager else "hip-graph",
+              "execution": "eager" if args.eager else ("hip-graph" if args.no_overlap else
+                                                       "hip-graph, crop formation overlapped"),
               "global_batch": B * world, "points_per_crop": N, "cad_points": N, "hypotheses": args.hypotheses,
               "precision": "model fp32 (f32 MFMA); crop geometry / RANSAC fp64", "parallelism": f"shard{world}"}
     probe = lambda: infer(fb, op, crops_of(fb))  # noqa: E731
@@ -667,7 +673,7 @@ def main():
         # dominant kernel family on the critical path: in the pipelined training execution crop
         # formation runs on a second stream under the training step, so the training kernels
         # bound the step; the crop-formation families are reported beside it
-        overlapped = args.mode == "train" and not args.no_overlap and not args.eager
+        overlapped = args.mode in ("train", "infer") and not args.no_overlap and not args.eager
         main_k = {k: v for k, v in kern.items() if not (overlapped and k in CROP_FAMS)} or kern
         dom = max(main_k.items(), key=lambda kv: kv[1]["total_ms"]) if main_k else None
         crop_k = {k: v for k, v in kern.items() if k in CROP_FAMS}
@@ -690,7 +696,7 @@ def main():
             "config": config,
             "roofline": roof,
             "roofline_crop_formation": (dict(roofline_for(dom_crop[0], dom_crop[1]),
-                                             stream="side (overlapped with the training step)")
+                                             stream="side (overlapped with the main step)")
                                         if dom_crop is not None and overlapped else
                                         (roofline_for(dom_crop[0], dom_crop[1]) if dom_crop else None)),
             "roofline_mfma_kernels": {k: {"achieved": v["achieved"], "frac": v["frac"], "unit": v["unit"]}

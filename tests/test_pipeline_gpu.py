@@ -225,3 +225,24 @@ def test_fused_clip_rmsprop_matches_torch(device, scale):
             sqa, sqb = sa.opt.state[p]["square_avg"], sb.opt.state[q]["square_avg"]
             assert (sqa - sqb).abs().max().item() <= 2e-6 * float(sqb.abs().max()) + 1e-30, (it, n)
         assert float(sa.opt.state[next(ma.parameters())]["step"]) == it + 1
+
+
+def test_pipelined_infer_matches_graphed(device):
+    """PipelinedInfer (crop formation of the next batch on a side stream, two ping-pong buffers)
+    returns, call after call, exactly what the single-stream GraphedInfer returns on the same
+    resident frames."""
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import GraphedInfer, InferStep, PipelinedInfer, make_frame_batch
+    torch.manual_seed(0)
+    F, N = 4, 512
+    fb, op = make_frame_batch(F, N, N, seed=71, device=device)
+    model = DPFMNet().to(device).eval()
+    g = GraphedInfer(CropFormation(n1=N, npoint=N, seed=3), InferStep(model, hypotheses=256), fb, op)
+    ref = {k: v.clone() for k, v in g().items() if torch.is_tensor(v)}
+    p = PipelinedInfer(CropFormation(n1=N, npoint=N, seed=3), InferStep(model, hypotheses=256), fb, op)
+    for _ in range(4):
+        out = p()
+        torch.cuda.synchronize()
+        for key in ("T", "ir", "n_corr", "metrics", "p_pred"):
+            assert torch.equal(out[key], ref[key]), key
