@@ -153,50 +153,135 @@ __global__ __launch_bounds__(kIThreads) void icp_sort_kernel(const double* __res
   sidx[o] = i;
 }
 
-// grid (B), block 1024, dynamic LDS P x 12 B (P = the power of two >= nmax, <= 8192): the same
-// (x key, index) order as icp_sort_kernel by an in-LDS bitonic sort — log2(P)(log2(P)+1)/2 passes of
-// P/2 compare-exchanges instead of n^2 / 256 key comparisons per thread.
-__global__ __launch_bounds__(1024) void icp_bitonic_kernel(const double* __restrict__ pts,
-                                                           const int64_t* __restrict__ off, int nmax, int P,
-                                                           const double* __restrict__ M, double* __restrict__ sx,
-                                                           double* __restrict__ sy, double* __restrict__ sz,
-                                                           int32_t* __restrict__ sidx) {
+// grid (B), block 1024, dynamic LDS P x 12 B + 16 KiB (P = the power of two >= nmax, <= 8192): the
+// same (x key, index) order as icp_sort_kernel by a bucket sort: keys binned into 2048 x-buckets
+// (monotone in x: floor((x - xmin) * NB / (xmax - xmin))), histogram + scan + scatter in LDS, then
+// every bucket insertion-sorted by (key, index) by one thread — a few keys per bucket, so ~10
+// LDS passes instead of bitonic's log2(P)(log2(P)+1)/2 = 91 block-wide passes. The scatter order
+// inside a bucket does not matter (the insertion sort fixes it), so the result is deterministic.
+// A bucket above 64 keys (heavily repeated x) sends the whole crop through a block bitonic sort.
+constexpr int kSortBuckets = 2048;
+__global__ __launch_bounds__(1024) void icp_bucket_sort_kernel(const double* __restrict__ pts,
+                                                               const int64_t* __restrict__ off, int nmax, int P,
+                                                               const double* __restrict__ M, double* __restrict__ sx,
+                                                               double* __restrict__ sy, double* __restrict__ sz,
+                                                               int32_t* __restrict__ sidx) {
   extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-  uint64_t* key = lds;
-  int32_t* val = reinterpret_cast<int32_t*>(lds + P);
+  uint64_t* key = lds;                                       // [P] keys in bucket order
+  int32_t* val = reinterpret_cast<int32_t*>(lds + P);        // [P]
+  int32_t* cnt = val + P;                                    // [kSortBuckets]
+  int32_t* fill = cnt + kSortBuckets;                        // [kSortBuckets]
+  __shared__ double rmin[16], rmax[16];
+  __shared__ int maxcnt;
   const int b = blockIdx.x;
   const int64_t p0 = off[b];
   const int n = (int)(off[b + 1] - p0);
   const double* Pt = pts + 3 * p0;
   const double* Mb = M ? M + 16 * b : nullptr;
-  for (int t = threadIdx.x; t < P; t += blockDim.x) {
-    if (t < n) {
-      const double* q = Pt + 3 * t;
-      key[t] = ordered_bits(Mb ? ((Mb[0] * q[0] + Mb[1] * q[1]) + Mb[2] * q[2]) + Mb[3] : q[0]);
-    } else {
-      key[t] = ~0ull;
+  auto key_x = [&](int t) {  // recomputed per pass (keeps LDS at 12 B per key: P <= 8192 fits)
+    const double* q = Pt + 3 * t;
+    return Mb ? ((Mb[0] * q[0] + Mb[1] * q[1]) + Mb[2] * q[2]) + Mb[3] : q[0];
+  };
+  double lo = INFINITY, hi = -INFINITY;
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    const double x = key_x(t);
+    lo = fmin(lo, x);
+    hi = fmax(hi, x);
+  }
+  for (int t = threadIdx.x; t < kSortBuckets; t += blockDim.x) cnt[t] = fill[t] = 0;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o));
+    hi = fmax(hi, __shfl_xor(hi, o));
+  }
+  if (pk::lane_id() == 0) {
+    rmin[pk::wave_id()] = lo;
+    rmax[pk::wave_id()] = hi;
+  }
+  if (threadIdx.x == 0) maxcnt = 0;
+  __syncthreads();
+  lo = rmin[0];
+  hi = rmax[0];
+  for (int w = 1; w < 16; ++w) {
+    lo = fmin(lo, rmin[w]);
+    hi = fmax(hi, rmax[w]);
+  }
+  const double scale = hi > lo ? (double)kSortBuckets / (hi - lo) : 0.0;
+  auto bucket_of = [&](double x) {
+    const int k = (int)((x - lo) * scale);
+    return k < 0 ? 0 : (k >= kSortBuckets ? kSortBuckets - 1 : k);
+  };
+  for (int t = threadIdx.x; t < n; t += blockDim.x) atomicAdd(&cnt[bucket_of(key_x(t))], 1);
+  __syncthreads();
+  if (threadIdx.x < 64) {  // exclusive scan of the bucket counts by one wave (32 per lane)
+    constexpr int per = kSortBuckets / 64;
+    int local = 0, mx = 0;
+    for (int q = 0; q < per; ++q) {
+      const int c = cnt[threadIdx.x * per + q];
+      local += c;
+      mx = max(mx, c);
     }
-    val[t] = t;
+    const int incl = pk::wave_inclusive_scan_i32(local);
+    int run = incl - local;
+    for (int q = 0; q < per; ++q) {
+      const int c = cnt[threadIdx.x * per + q];
+      fill[threadIdx.x * per + q] = run;  // bucket start
+      run += c;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+    if (threadIdx.x == 0) maxcnt = mx;
   }
   __syncthreads();
-  for (int k = 2; k <= P; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = threadIdx.x; t < P; t += blockDim.x) {
-        const int u = t ^ j;
-        if (u > t) {
-          const uint64_t ka = key[t], kb = key[u];
-          const int va = val[t], vb = val[u];
-          const bool b_less = kb < ka || (kb == ka && vb < va);
-          if (b_less == ((t & k) == 0)) {
-            key[t] = kb;
-            key[u] = ka;
-            val[t] = vb;
-            val[u] = va;
+  if (maxcnt > 64) {  // skewed: bitonic over (key, index) in place of the bucket pass
+    for (int t = threadIdx.x; t < P; t += blockDim.x) {
+      key[t] = t < n ? ordered_bits(key_x(t)) : ~0ull;
+      val[t] = t;
+    }
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int t = threadIdx.x; t < P; t += blockDim.x) {
+          const int u = t ^ j;
+          if (u > t) {
+            const uint64_t ka = key[t], kb = key[u];
+            const int va = val[t], vb = val[u];
+            const bool b_less = kb < ka || (kb == ka && vb < va);
+            if (b_less == ((t & k) == 0)) {
+              key[t] = kb;
+              key[u] = ka;
+              val[t] = vb;
+              val[u] = va;
+            }
           }
         }
+        __syncthreads();
       }
-      __syncthreads();
     }
+  } else {
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {  // scatter (in-bucket order arbitrary)
+      const double x = key_x(t);
+      const int pos = atomicAdd(&fill[bucket_of(x)], 1);
+      key[pos] = ordered_bits(x);
+      val[pos] = t;
+    }
+    __syncthreads();
+    for (int bk = threadIdx.x; bk < kSortBuckets; bk += blockDim.x) {  // insertion sort per bucket
+      const int e = fill[bk], s0 = e - cnt[bk];
+      for (int i = s0 + 1; i < e; ++i) {
+        const uint64_t kk = key[i];
+        const int vv = val[i];
+        int j = i - 1;
+        while (j >= s0 && (key[j] > kk || (key[j] == kk && val[j] > vv))) {
+          key[j + 1] = key[j];
+          val[j + 1] = val[j];
+          --j;
+        }
+        key[j + 1] = kk;
+        val[j + 1] = vv;
+      }
+    }
+    __syncthreads();
   }
   for (int t = threadIdx.x; t < n; t += blockDim.x) {
     const int i = val[t];
@@ -452,15 +537,16 @@ extern "C" int pk_icp_init(const double* src, const int64_t* src_off, const doub
   const IcpWork w = carve(work, B, nsrc_max, ntgt_max);
   hipLaunchKernelGGL(icp_init_kernel, dim3(B), dim3(64), 0, s, T_init, w.st);
   PK_CHECK_LAUNCH();
-  // x order of the targets (and of the source queries under T_init): bitonic in LDS up to 8192
-  // points per crop, rank counting beyond
+  // x order of the targets (and of the source queries under T_init): bucket sort in LDS up to
+  // 8192 points per crop, rank counting beyond
   auto sort = [&](const double* p, const int64_t* o, int nm, const double* M, double* x, double* y, double* z,
                   int32_t* idx) -> int {
     if (nm <= 0) return PK_OK;
     int P = 1;
     while (P < nm) P <<= 1;
     if (P <= 8192) {
-      hipLaunchKernelGGL(icp_bitonic_kernel, dim3(B), dim3(1024), (size_t)P * 12, s, p, o, nm, P, M, x, y, z, idx);
+      hipLaunchKernelGGL(icp_bucket_sort_kernel, dim3(B), dim3(1024), (size_t)P * 12 + kSortBuckets * 8, s, p, o, nm, P,
+                         M, x, y, z, idx);
     } else {
       hipLaunchKernelGGL(icp_sort_kernel, dim3((nm + kIThreads - 1) / kIThreads, B), dim3(kIThreads), 0, s, p, o, nm, M,
                          x, y, z, idx);
