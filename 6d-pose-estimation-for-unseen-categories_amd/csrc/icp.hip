@@ -37,6 +37,7 @@
 namespace {
 
 constexpr int kIThreads = 256;
+constexpr int kWin = 1536;  // LDS candidate window of a match block (28 B per target point)
 constexpr int kNPart = 17;  // count, sum d^2, sum p (3), sum q (3), sum p q^T (9)
 
 struct IcpState {  // per crop, in the work buffer
@@ -364,25 +365,87 @@ __global__ __launch_bounds__(kIThreads) void icp_match_kernel(
   double acc[kNPart];
 #pragma unroll
   for (int k = 0; k < kNPart; ++k) acc[k] = 0.0;
-  if (i < ns && nt > 0) {
+  const bool own = i < ns && nt > 0;
+  int k0 = 0, k1 = 0;
+  double qpx = 0.0, qpy = 0.0, qpz = 0.0, qlo = 0.0, qhi = 0.0;
+  if (own) {
     const double* M = st[b].T;
     const double* s = src + 3 * (s0 + perm[(int64_t)b * nsrc_max + i]);  // x-ordered queries: a wave's slabs overlap
     const double x = s[0], y = s[1], z = s[2];
     const double px = ((M[0] * x + M[1] * y) + M[2] * z) + M[3];
     const double py = ((M[4] * x + M[5] * y) + M[6] * z) + M[7];
     const double pz = ((M[8] * x + M[9] * y) + M[10] * z) + M[11];
-    const int64_t tb = (int64_t)b * ntgt_max;
-    const double* X = sx + tb;
-    const double* Y = sy + tb;
-    const double* Z = sz + tb;
-    const int32_t* I = sidx + tb;
     const double lo_x = px - r, hi_x = px + r;
     // scan start: the bucket before the slab's lower edge (see icp_bucket_kernel)
     const double kb = (lo_x - st[b].xmin) * st[b].inv_w;
-    int k0 = 0;
+    k0 = 0;
     if (kb >= 1.0) k0 = tbl[(int64_t)b * (kNBuckets + 1) + (kb >= (double)kNBuckets ? kNBuckets : (int)kb) - 1];
-    double best = INFINITY;
-    int bi = INT32_MAX, bk = -1;
+    // scan end bound: the start of the bucket two past the slab's upper edge (every later
+    // point has x > hi_x even after rounding of the bucket index)
+    const double kh = (hi_x - st[b].xmin) * st[b].inv_w;
+    k1 = nt;
+    if (kh < (double)(kNBuckets - 2) && kh >= -1.0) k1 = tbl[(int64_t)b * (kNBuckets + 1) + (int)kh + 2];
+    if (kh < -1.0) k1 = k0;
+    qpx = px;
+    qpy = py;
+    qpz = pz;
+    qlo = lo_x;
+    qhi = hi_x;
+  }
+  // the block's candidate window [min k0, max k1): staged in LDS when it fits (x-ordered queries
+  // make the 256 slabs of a block overlap: a few hundred target points instead of 256 x ~100
+  // scattered L2 gathers), scanned from global memory otherwise (block-uniform choice)
+  __shared__ int wlo[kIThreads / 64], whi[kIThreads / 64];
+  __shared__ double wxs[kWin], wys[kWin], wzs[kWin];
+  __shared__ int wid[kWin];
+  int lo = own ? k0 : INT32_MAX, hi = own ? k1 : 0;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    lo = min(lo, __shfl_xor(lo, o));
+    hi = max(hi, __shfl_xor(hi, o));
+  }
+  if (pk::lane_id() == 0) {
+    wlo[pk::wave_id()] = lo;
+    whi[pk::wave_id()] = hi;
+  }
+  __syncthreads();
+  lo = wlo[0];
+  hi = whi[0];
+#pragma unroll
+  for (int w = 1; w < kIThreads / 64; ++w) {
+    lo = min(lo, wlo[w]);
+    hi = max(hi, whi[w]);
+  }
+  const int64_t tb = (int64_t)b * ntgt_max;
+  const double* X = sx + tb;
+  const double* Y = sy + tb;
+  const double* Z = sz + tb;
+  const int32_t* I = sidx + tb;
+  double best = INFINITY;
+  int bi = INT32_MAX, bk = -1;
+  if (hi > lo && hi - lo <= kWin) {
+    for (int j = threadIdx.x; j < hi - lo; j += kIThreads) {
+      wxs[j] = X[lo + j];
+      wys[j] = Y[lo + j];
+      wzs[j] = Z[lo + j];
+      wid[j] = I[lo + j];
+    }
+    __syncthreads();
+    if (own) {
+      for (int k = k0; k < k1; ++k) {
+        const double qx = wxs[k - lo];
+        if (qx > qhi) break;
+        const double dx = qpx - qx, dy = qpy - wys[k - lo], dz = qpz - wzs[k - lo];
+        const double d2 = (dx * dx + dy * dy) + dz * dz;
+        const int id = wid[k - lo];
+        if (d2 < best || (d2 == best && id < bi)) {
+          best = d2;
+          bi = id;
+          bk = k;
+        }
+      }
+    }
+  } else if (own) {
     // candidates in batches of 8 independent loads (no load waits on the previous candidate)
     for (int k = k0; k < nt; k += 8) {
       double qx[8], qy[8], qz[8];
@@ -398,15 +461,18 @@ __global__ __launch_bounds__(kIThreads) void icp_match_kernel(
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const double dx = px - qx[j], dy = py - qy[j], dz = pz - qz[j];
+        const double dx = qpx - qx[j], dy = qpy - qy[j], dz = qpz - qz[j];
         const double d2 = (dx * dx + dy * dy) + dz * dz;
         const bool take = d2 < best || (d2 == best && id[j] < bi);
         best = take ? d2 : best;
         bi = take ? id[j] : bi;
         bk = take ? k + j : bk;
       }
-      if (qx[7] > hi_x) break;
+      if (qx[7] > qhi) break;
     }
+  }
+  if (own) {
+    const double px = qpx, py = qpy, pz = qpz;
     if (bk >= 0 && best < r * r) {
       const double* c = tgt + 3 * t0;  // shift: the crop's first target point
       const double ax = px - c[0], ay = py - c[1], az = pz - c[2];
