@@ -804,6 +804,14 @@ def roofline_for(name: str, k: dict) -> dict:
     base = {"kernel": name, "avg_ms": round(k["avg_ms"], 4), "launches_per_step_probe": k["launches"],
             "work_per_launch": None if k["work"] is None else k["work"] / k["launches"]}
     traffic = pmc_traffic(name)
+    layer_pmc = None
+    if name in ("pk_linear_fwd", "pk_linear_ex"):
+        # the counters cannot split the two entry points (same kernels): report the combined
+        # per-kernel-launch bytes beside the roofline instead of as this family's traffic
+        v = pmc_traffic("pk_linear_fwd+ex")
+        layer_pmc = None if v is None else {"family": "pk_linear_fwd+ex", "bytes_per_kernel_launch": v,
+                                             "note": "PMC FETCH+WRITE per per-point-layer kernel launch of both "
+                                                     "entry points (profiles/pmc_traffic.json)"}
     if k["work"] is None:
         return dict(base, bound="hbm", achieved=None, peak=HBM_PEAK_GBS, unit="GB/s", frac=None, traffic=traffic)
     sec = k["total_ms"] * 1e-3
@@ -832,6 +840,8 @@ def roofline_for(name: str, k: dict) -> dict:
     if name == "pk_fps":
         r["note"] = ("sequential npoint-step argmax, one workgroup per crop: latency-bound; the HBM "
                      "fraction is reported for completeness, not as its limiter")
+    if layer_pmc is not None:
+        r["pmc_layer_kernels"] = layer_pmc
     return r
 
 

@@ -28,10 +28,9 @@ FAMILIES = {
     "pk_linear_wgrad": ["wgrad_v2_kernel", "wgrad_partial_kernel", "wgrad_reduce_kernel"],
     "pk_feat_dist_topk": ["fd_prep_kernel", "fd_main_kernel"],
     "pk_cgt_lstsq": ["cgt_count_kernel", "cgt_partial_kernel", "cgt_reduce_kernel", "cgt_solve_kernel"],
-    "pk_linear_fwd": ["linear_fwd_rows_kernel", "linear_fwd_cf_kernel", "linear_fwd_kernel", "linear_thin_kernel"],
-    # pk_linear_ex (epilogue / placement variant) launches the same kernels as pk_linear_fwd, so
-    # the two families share one per-launch average
-    "pk_linear_ex": ["linear_fwd_rows_kernel", "linear_fwd_cf_kernel", "linear_fwd_kernel", "linear_thin_kernel"],
+    # pk_linear_fwd and pk_linear_ex (its epilogue / placement variant) launch the same kernels: the
+    # counters cannot tell them apart, so they form one family, per KERNEL launch
+    "pk_linear_fwd+ex": ["linear_fwd_rows_kernel", "linear_fwd_cf_kernel", "linear_fwd_kernel", "linear_thin_kernel"],
     "pk_linear_wgrad_grouped": ["wgrad_grouped_kernel", "wgrad_grouped_reduce_kernel"],
     "pk_nce_loss": ["nce_pass_kernel<false>", "nce_pass_kernel<true>", "zero_fill_kernel"],
     "pk_clip_rmsprop": ["grad_sumsq_kernel", "clip_rmsprop_kernel"],
@@ -42,7 +41,7 @@ FAMILIES = {
     "pk_l2_normalize_bwd": ["l2norm_bwd_kernel"],
 }
 # families whose launches are ONE of several kernels (every dispatch is a family launch)
-ANY_LEAD = {"pk_linear_fwd", "pk_linear_ex"}
+ANY_LEAD = {"pk_linear_fwd+ex"}
 # (the first kernel of each family is counted once per family launch)
 
 
