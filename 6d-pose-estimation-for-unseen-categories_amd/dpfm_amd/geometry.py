@@ -64,10 +64,12 @@ def cheb_filter(A, X, degree: int, a: float, b: float, a0: float = 0.0):
     return Y
 
 
-def _orth(X):
-    """Cholesky QR (twice): X <- X R^-1 with R^T R = X^T X (the m x m Gram from pk_dgemm_tn; the
-    m x m Cholesky and triangular solve stay on the device, no host round trip)."""
-    for _ in range(2):
+def _orth(X, passes: int = 2):
+    """Cholesky QR: X <- X R^-1 with R^T R = X^T X (the m x m Gram from pk_dgemm_tn; the m x m
+    Cholesky and triangular solve stay on the device, no host round trip). One pass suffices after
+    an inverse application to an orthonormal block (its condition number is at most the subspace's
+    eigenvalue spread, ~1e2-1e3, so CholQR loses ~kappa^2 u ~ 1e-10); two for the random start."""
+    for _ in range(passes):
         G = ops.dgemm_tn(X, X)
         R = torch.linalg.cholesky(0.5 * (G + G.transpose(1, 2)), upper=True)
         X = torch.linalg.solve_triangular(R, X, upper=True, left=False).contiguous()
@@ -75,13 +77,14 @@ def _orth(X):
 
 
 def subspace_eigs(A: torch.Tensor, counts: Sequence[int], k: int, extra: int = 64, tol: float = 1e-8,
-                  max_iter: int = 200, seed: int = 0, tau_rel: float = 1e-6):
+                  max_iter: int = 200, seed: int = 0, tau_rel: float = 1e-6, rr_every: int = 3):
     """k smallest eigenpairs of each symmetric A[b] (padding rows / columns of crop b beyond
     counts[b] hold a large diagonal) by shift-invert subspace iteration — eigsh's sigma mode:
     A + tau I = L L^T once (pk_dpotrf; tau escalated x10 when a pivot fails, as compute_operators
     escalates eps), (A + tau I)^-1 = L^-T L^-1 I once (pk_dpotrs with N right-hand sides), then per
-    iteration X <- (A + tau I)^-1 X (pk_dgemm_cheb), Cholesky-QR and a Rayleigh-Ritz step with A
-    itself. Converged when every wanted residual |A x - theta x| <= tol * theta_k
+    iteration X <- (A + tau I)^-1 X (pk_dgemm_cheb) and one Cholesky-QR pass; every rr_every
+    iterations a Rayleigh-Ritz step with A itself (subspace iteration converges without it; it
+    extracts the eigenpairs and tests convergence, and its m x m eigensolve is the costly part). Converged when every wanted residual |A x - theta x| <= tol * theta_k
     (ARPACK's relative criterion at the k-th Ritz value; the operators are stored in fp32
     downstream). The rate per iteration is (lambda_k + tau) / (lambda_m + tau), m = k + extra."""
     B, N, _ = A.shape
@@ -110,7 +113,9 @@ def subspace_eigs(A: torch.Tensor, counts: Sequence[int], k: int, extra: int = 6
     X = _orth(torch.as_tensor(X0, device=A.device))
     theta, res, it = None, None, 0
     for it in range(1, max_iter + 1):
-        X = _orth(ops.dgemm_cheb(Ainv, X, None, 1.0, 0.0, 0.0))
+        X = _orth(ops.dgemm_cheb(Ainv, X, None, 1.0, 0.0, 0.0), passes=1)
+        if it % rr_every and it != max_iter:  # Rayleigh-Ritz (and the convergence test) every rr_every
+            continue
         AX = ops.dgemm_cheb(A, X, None, 1.0, 0.0, 0.0)
         H = ops.dgemm_tn(X, AX)
         theta, Wt = torch.linalg.eigh(0.5 * (H + H.transpose(1, 2)))  # m x m Rayleigh-Ritz, on the device
