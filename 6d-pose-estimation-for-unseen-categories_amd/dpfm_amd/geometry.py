@@ -17,9 +17,11 @@ variant, cheb_filter, converges too slowly on crop Laplacians: their spectral bo
 against lambda_64 ~ 3, because of tiny-mass points.) Dense fp64
 operators: N <= ~5000 per shape (200 MB for the CAD), well inside HBM.
 
-Returns what compute_operators returns that the model reads (mass, L, evals, evecs); frames and
-gradX / gradY feed only gradient features, which this model configuration does not use
-(models/dpfm.py:22-30, with_gradient_features=False), and are None. Parity unpinned."""
+Returns what compute_operators returns that the model reads (mass, L, evals, evecs) plus the
+tangent frames (build_tangent_frames from the PCA normals of the crop's 30-neighbourhoods, or the
+mesh's area-weighted vertex normals); gradX / gradY feed only gradient features, which this model
+configuration does not use (models/dpfm.py:22-30, with_gradient_features=False), and are None.
+Parity unpinned."""
 from __future__ import annotations
 
 from dataclasses import dataclass
@@ -40,9 +42,34 @@ class SpectralOperators:
     normals: Optional[torch.Tensor]  # f64 [T, 3] (point clouds)
     iterations: int
     residual: torch.Tensor  # f64 [B] max eigen-residual / spectral bound over the k pairs
-    frames = None
+    frames: Optional[torch.Tensor] = None  # f64 [T, 3, 3] (basisX, basisY, normal) per point
     gradX = None
     gradY = None
+
+
+def tangent_frames(normals: torch.Tensor) -> torch.Tensor:
+    """diffusion-net build_tangent_frames: basisX = the x axis (the y axis where |n . x| >= 0.9)
+    projected to the tangent plane and normalized, basisY = n x basisX; [T, 3, 3] rows (X, Y, n)."""
+    n = normals
+    ex = torch.zeros_like(n)
+    ex[:, 0] = 1.0
+    ey = torch.zeros_like(n)
+    ey[:, 1] = 1.0
+    cand = torch.where((n[:, 0].abs() < 0.9)[:, None], ex, ey)
+    bx = cand - (cand * n).sum(-1, keepdim=True) * n
+    bx = bx / bx.norm(dim=-1, keepdim=True)
+    by = torch.cross(n, bx, dim=-1)
+    return torch.stack((bx, by, n), dim=-2)
+
+
+def mesh_vertex_normals(pts: torch.Tensor, faces: torch.Tensor) -> torch.Tensor:
+    """diffusion-net mesh_vertex_normals: area-weighted face normals summed per vertex, normalized."""
+    a, b, c = pts[faces[:, 0]], pts[faces[:, 1]], pts[faces[:, 2]]
+    fn = torch.cross(b - a, c - a, dim=-1)
+    vn = torch.zeros_like(pts)
+    for k in range(3):
+        vn.index_add_(0, faces[:, k].long(), fn)
+    return vn / vn.norm(dim=-1, keepdim=True).clamp(min=1e-300)
 
 
 def _pack(verts: Sequence[np.ndarray], device):
@@ -156,5 +183,9 @@ def get_operators(verts: Sequence[np.ndarray], faces: Optional[Sequence[np.ndarr
     for b, n in enumerate(counts):
         evecs[b, n:] = 0.0
         mass[b, n:] = 0.0
+    if normals is None:  # mesh: vertex normals from the faces (crop-local indices -> packed rows)
+        fl = torch.cat([torch.as_tensor(np.asarray(f, dtype=np.int64), device=dev) + int(o)
+                        for f, o in zip(faces, off[:-1].cpu().tolist())])
+        normals = mesh_vertex_normals(pts, fl)
     return SpectralOperators(mass=mass, L=L, evals=evals.clamp(min=0.0), evecs=evecs, normals=normals,
-                             iterations=iters, residual=res)
+                             iterations=iters, residual=res, frames=tangent_frames(normals))

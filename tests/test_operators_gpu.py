@@ -131,6 +131,9 @@ def test_get_operators_matches_eigsh(device, kind):
             Lr, Mr = OO.cotan_laplacian(v, [tuple(x) for x in f], scale=1.0, denom_eps=1e-10)
             refs.append((Lr, Mr + eps * Mr.mean()))
     ev, V, M = op.evals.cpu().numpy(), op.evecs.cpu().numpy(), op.mass.cpu().numpy()
+    Fr = op.frames.cpu().numpy()  # orthonormal right-handed frames, third row = the normal
+    np.testing.assert_allclose(np.einsum("tij,tkj->tik", Fr, Fr), np.broadcast_to(np.eye(3), Fr.shape), atol=1e-12)
+    np.testing.assert_allclose(np.linalg.det(Fr), 1.0, atol=1e-12)
     for b, (s, (Lr, Mr)) in enumerate(zip(shapes, refs)):
         n = s.shape[0]
         np.testing.assert_allclose(M[b, :n], Mr, rtol=1e-12)
