@@ -1178,6 +1178,29 @@ def dpotrs(L: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
     return X
 
 
+def icp_fixed(src: torch.Tensor, src_off: torch.Tensor, tgt: torch.Tensor, tgt_off: torch.Tensor,
+              T_init: torch.Tensor, max_dist: float, evaluations: int, nsrc_max: int, ntgt_max: int,
+              rel_fitness: float = 1e-6, rel_rmse: float = 1e-6):
+    """ICP with a fixed number of enqueued evaluations and no host read (HIP-graph capturable):
+    max_iteration = evaluations - 1, so every crop stops by the last one (converged crops return
+    early in each launch). Same results as `icp` with that max_iteration."""
+    B = src_off.numel() - 1
+    dev = src.device
+    T0 = T_init.to(dtype=torch.float64).reshape(B, 16).contiguous()
+    nbytes = int(_lib.lib().pk_icp_work_size(B, int(nsrc_max), int(ntgt_max)))
+    work = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+    s = _lib.stream(dev)
+    call("pk_icp_init", ptr(src), ptr(src_off), ptr(tgt), ptr(tgt_off), ptr(T0), B, int(nsrc_max), int(ntgt_max),
+         ptr(work), nbytes, s)
+    call("pk_icp_iterate", ptr(src), ptr(src_off), ptr(tgt), ptr(tgt_off), float(max_dist), int(evaluations) - 1,
+         float(rel_fitness), float(rel_rmse), B, int(nsrc_max), int(ntgt_max), int(evaluations), ptr(work), nbytes,
+         None, s, work=("hbm", int(evaluations) * int(src.shape[0]) * 48))
+    T = torch.empty((B, 4, 4), dtype=torch.float64, device=dev)
+    stats = torch.empty((B, 4), dtype=torch.float64, device=dev)
+    call("pk_icp_result", ptr(work), B, ptr(T), ptr(stats), s)
+    return T, stats
+
+
 def pose_metrics(cad: torch.Tensor, off: torch.Tensor, nmax: int, T_est: torch.Tensor, T_gt: torch.Tensor):
     """pk_pose_metrics -> f64 [B, 7] (ADD, xyz-direction means x3, ADD-S 1-D means x3)."""
     B = off.numel() - 1

@@ -528,8 +528,14 @@ class PipelinedTrainer:
 class InferStep:
     """eval.py inference + test_RANSAC.py pose fit for a batch of crops."""
 
-    def __init__(self, model: DPFMNet, hypotheses: int = 1024, seed: int = 0, max_dist: float = 0.05):
+    def __init__(self, model: DPFMNet, hypotheses: int = 1024, seed: int = 0, max_dist: float = 0.05,
+                 icp_evaluations: int = 0, icp_threshold: float = 0.2):
+        """icp_evaluations > 0 refines each RANSAC pose by point-to-point ICP of the CAD against the
+        observed crop (test_RANSAC.py:436-446 runs ICP after RANSAC, against the GT-posed CAD; the
+        crop is the target available without ground truth), with that many evaluations enqueued
+        (capturable: no host read) and the metrics also reported for the refined pose."""
         self.model, self.H, self.seed, self.max_dist = model, hypotheses, seed, max_dist
+        self.icp_evaluations, self.icp_threshold = icp_evaluations, icp_threshold
 
     @torch.no_grad()
     def __call__(self, fb: FrameBatch, op: Operators, crops: Crops):
@@ -566,8 +572,13 @@ class InferStep:
         T_gt[:, :3, 3] = fb.t
         T_gt[:, 3, 3] = 1.0
         metrics = ops.pose_metrics(fb.cad64, fb.cad_off, V1, T, T_gt)
-        return dict(C=C_pred, cand=cand, p_pred=p_pred, n_corr=nsurv, ir=ir, T=T, ransac=stats, metrics=metrics,
-                    corres=corres, cor_off=cor_off)
+        out = dict(C=C_pred, cand=cand, p_pred=p_pred, n_corr=nsurv, ir=ir, T=T, ransac=stats, metrics=metrics,
+                   corres=corres, cor_off=cor_off)
+        if self.icp_evaluations > 0:
+            T_icp, icp_stats = ops.icp_fixed(fb.cad64, fb.cad_off, crops.pc64, crops.off, T, self.icp_threshold,
+                                             self.icp_evaluations, V1, V2)
+            out.update(T_icp=T_icp, icp=icp_stats, metrics_icp=ops.pose_metrics(fb.cad64, fb.cad_off, V1, T_icp, T_gt))
+        return out
 
 
 class GraphedInfer:

@@ -59,6 +59,8 @@ def parse():
                          "corr4096: configs[4] feature distance + RANSAC; icp: the (f4) ICP refinement; "
                          "teaser: the (f2) TEASER++ solver; operators: the (f1) spectral operators")
     ap.add_argument("--op-points", type=int, default=2000, help="operators: points per crop")
+    ap.add_argument("--icp-evals", type=int, default=0,
+                    help="infer: refine every RANSAC pose by ICP against the crop (evaluations enqueued)")
     ap.add_argument("--teaser-n", type=int, default=2000, help="teaser: correspondences per crop")
     ap.add_argument("--icp-target", choices=("gt_cad", "crop"), default="gt_cad",
                     help="icp: the reference's target (CAD under T_gt) or the observed crop")
@@ -336,7 +338,7 @@ def build_infer(args, dev, rank, world):
     model = DPFMNet().to(dev).eval()
     fb, op = make_frame_batch(B, N, N, seed=1000 * rank, device=dev)
     crops_of = CropFormation(n1=N, npoint=N, seed=0, base=rank * B)
-    infer = InferStep(model, hypotheses=args.hypotheses, seed=0)
+    infer = InferStep(model, hypotheses=args.hypotheses, seed=0, icp_evaluations=args.icp_evals)
     if args.eager:
         one_step = lambda: infer(fb, op, crops_of(fb))  # noqa: E731
     elif args.no_overlap:
@@ -346,7 +348,9 @@ def build_infer(args, dev, rank, world):
     name = "configs[3] shard" if N == 2048 else "configs[1]"
     config = {"workload": f"{name}: B={B} synthetic 640x480 RGB-D crops/GPU, {N} pts, inference (eval.py + "
                           f"test_RANSAC.py: top-5 + 3-round rigidity filter + IR + RANSAC {args.hypotheses} "
-                          "hypotheses + ADD metrics), batch-sharded across ranks (weak scaling)",
+                          "hypotheses + ADD metrics" + (f" + ICP to the crop ({args.icp_evals} evaluations)"
+                                                         if args.icp_evals else "") +
+                          "), batch-sharded across ranks (weak scaling)",
               "execution": "eager" if args.eager else ("hip-graph" if args.no_overlap else
                                                        "hip-graph, crop formation overlapped"),
               "global_batch": B * world, "points_per_crop": N, "cad_points": N, "hypotheses": args.hypotheses,

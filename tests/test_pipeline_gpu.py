@@ -246,3 +246,24 @@ def test_pipelined_infer_matches_graphed(device):
         torch.cuda.synchronize()
         for key in ("T", "ir", "n_corr", "metrics", "p_pred"):
             assert torch.equal(out[key], ref[key]), key
+
+
+def test_infer_step_with_icp_matches_standalone_icp(device):
+    """InferStep(icp_evaluations=E) refines the RANSAC poses against the crops exactly as the
+    host-polled ops.icp with max_iteration E - 1 does, and stays HIP-graph capturable."""
+    from dpfm_amd import ops
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import GraphedInfer, InferStep, make_frame_batch
+    torch.manual_seed(0)
+    F, N, E = 4, 512, 12
+    fb, op = make_frame_batch(F, N, N, seed=72, device=device)
+    model = DPFMNet().to(device).eval()
+    crops = CropFormation(n1=N, npoint=N, seed=2)(fb)
+    out = InferStep(model, hypotheses=256, icp_evaluations=E)(fb, op, crops)
+    T, st = ops.icp(fb.cad64, fb.cad_off, crops.pc64, crops.off, out["T"], 0.2, E - 1, nsrc_max=N, ntgt_max=N)
+    assert torch.equal(out["T_icp"], T) and torch.equal(out["icp"], st)
+    g = GraphedInfer(CropFormation(n1=N, npoint=N, seed=2), InferStep(model, hypotheses=256, icp_evaluations=E), fb, op)
+    o2 = g()
+    torch.cuda.synchronize()
+    assert torch.equal(o2["T_icp"], out["T_icp"]) and torch.isfinite(o2["metrics_icp"]).all()
