@@ -704,7 +704,7 @@ __device__ __forceinline__ void lr_stage(const float* __restrict__ w, int Cout, 
   }
 }
 
-template <int Q, int TO>  // Cin = 16 Q, Cout <= 16 TO
+template <int Q, int TO, bool GEN>  // Cin = 16 Q, Cout <= 16 TO; GEN: mask / add / split / cf epilogue
 __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __restrict__ x, int64_t sx,
                                                               const float* __restrict__ w,
                                                               const float* __restrict__ bias, int64_t R, int Cin,
@@ -751,8 +751,9 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
     // TO x 4 outputs are issued before the first use, not one dependent load per store
     // (workgroup-uniform branches around unconditional loads at clamped indices: no per-load
     // exec-mask branch, so no wait per load)
+    // (the plain instantiation drops the epilogue operands: 8 TO fewer VGPRs, more waves)
     float mk[TO][4], ad[TO][4];
-    if (e.mask != nullptr) {
+    if (GEN && e.mask != nullptr) {
 #pragma unroll
       for (int t = 0; t < TO; ++t)
 #pragma unroll
@@ -768,7 +769,7 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
 #pragma unroll
         for (int r = 0; r < 4; ++r) mk[t][r] = 1.f;
     }
-    if (e.add != nullptr) {
+    if (GEN && e.add != nullptr) {
 #pragma unroll
       for (int t = 0; t < TO; ++t)
 #pragma unroll
@@ -795,10 +796,10 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
           float v = lin_act(e.relu, acc[t][r] + bv[t]);
           v = mk[t][r] <= 0.f ? 0.f : v;  // relu_mask
           v += ad[t][r];  // 0 without add / past add_cols
-          if (e.store_cf) {
+          if (GEN && e.store_cf) {
             const int64_t b = pr / e.N, n = pr - b * e.N;
             e.y[b * e.sy + (int64_t)o * e.N + n] = v;
-          } else if (o >= e.split) {
+          } else if (GEN && o >= e.split) {
             e.y2[pr * e.sy2 + (o - e.split)] = v;
           } else {
             e.y[pr * e.sy + o] = v;
@@ -1129,15 +1130,21 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
     const int64_t tiles = (R + 15) / 16;
     const unsigned blocks = (unsigned)std::min<int64_t>((tiles + 3) / 4, (int64_t)kRowsMaxBlocks);
     const int TO = Cout <= 16 ? 1 : Cout <= 32 ? 2 : Cout <= 64 ? 4 : 8;
-    auto pick = [&](auto q) {
+    auto pick = [&](auto q, auto gen) {
       constexpr int Q = decltype(q)::value;
-      return TO == 1 ? linear_fwd_rows_kernel<Q, 1>
-             : TO == 2 ? linear_fwd_rows_kernel<Q, 2>
-             : TO == 4 ? linear_fwd_rows_kernel<Q, 4> : linear_fwd_rows_kernel<Q, 8>;
+      constexpr bool G = decltype(gen)::value;
+      return TO == 1 ? linear_fwd_rows_kernel<Q, 1, G>
+             : TO == 2 ? linear_fwd_rows_kernel<Q, 2, G>
+             : TO == 4 ? linear_fwd_rows_kernel<Q, 4, G> : linear_fwd_rows_kernel<Q, 8, G>;
     };
-    auto kern = Cin == 16 ? pick(std::integral_constant<int, 1>{})
-                : Cin == 32 ? pick(std::integral_constant<int, 2>{})
-                : Cin == 64 ? pick(std::integral_constant<int, 4>{}) : pick(std::integral_constant<int, 8>{});
+    auto pickq = [&](auto gen) {
+      return Cin == 16 ? pick(std::integral_constant<int, 1>{}, gen)
+             : Cin == 32 ? pick(std::integral_constant<int, 2>{}, gen)
+             : Cin == 64 ? pick(std::integral_constant<int, 4>{}, gen) : pick(std::integral_constant<int, 8>{}, gen);
+    };
+    // plain: no mask, no residual add, one contiguous output (split == Cout)
+    const bool plain = e.mask == nullptr && e.add == nullptr && e.y2 == nullptr && !e.store_cf && e.split >= Cout;
+    auto kern = plain ? pickq(std::integral_constant<bool, false>{}) : pickq(std::integral_constant<bool, true>{});
     const size_t lds = sizeof(float) * (size_t)(16 * TO) * (Cin + 4);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, st, x, sx, w, bias, R, Cin, Cout, transw, e);
     PK_CHECK_LAUNCH();
