@@ -720,6 +720,7 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
   lr_stage<Q, TO>(w, Cout, transw, Ws);
   __syncthreads();
   if (tile >= T) return;
+  constexpr int TH = TO < 4 ? TO : 4, NH = TO / TH;
   float bv[TO];
 #pragma unroll
   for (int t = 0; t < TO; ++t) {
@@ -729,71 +730,75 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
   for (;;) {
     const int64_t tn = tile + stride;
     if (tn < T) lr_load<Q>(x, sx, tn * 16 + m, R, g, nxt);
-    f32x4 acc[TO];
+    // outputs in groups of TH = 4 column tiles (Cout = 128 runs two passes over the same
+    // operands): acc / wv / epilogue operands stay at TH tiles, so TO = 8 keeps 4 waves per SIMD
 #pragma unroll
-    for (int t = 0; t < TO; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int hh = 0; hh < NH; ++hh) {
+    __builtin_amdgcn_sched_barrier(0);  // one output group's registers live at a time
+    f32x4 acc[TH];
+#pragma unroll
+    for (int t = 0; t < TH; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       {
-        f32x4 wv[TO];
+        f32x4 wv[TH];
 #pragma unroll
-        for (int t = 0; t < TO; ++t)
-          wv[t] = *reinterpret_cast<const f32x4*>(&Ws[(t * 16 + m) * ST + 16 * q + 4 * g]);
+        for (int t = 0; t < TH; ++t)
+          wv[t] = *reinterpret_cast<const f32x4*>(&Ws[((hh * TH + t) * 16 + m) * ST + 16 * q + 4 * g]);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int t = 0; t < TO; ++t)
+          for (int t = 0; t < TH; ++t)
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[q][i], wv[t][i], acc[t], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);  // keep the weight reads per chunk (no hoisting of all Q x TO)
+        __builtin_amdgcn_sched_barrier(0);  // keep the weight reads per chunk (no hoisting of all Q x TH)
       }
     }
     // D[point 4 g + r][out t * 16 + m]; the epilogue's operand loads (mask, add) for all
-    // TO x 4 outputs are issued before the first use, not one dependent load per store
+    // TH x 4 outputs are issued before the first use, not one dependent load per store
     // (workgroup-uniform branches around unconditional loads at clamped indices: no per-load
     // exec-mask branch, so no wait per load)
-    // (the plain instantiation drops the epilogue operands: 8 TO fewer VGPRs, more waves)
-    float mk[TO][4], ad[TO][4];
+    float mk[TH][4], ad[TH][4];
     if (GEN && e.mask != nullptr) {
 #pragma unroll
-      for (int t = 0; t < TO; ++t)
+      for (int t = 0; t < TH; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t pr = tile * 16 + 4 * g + r;
-          const int o = t * 16 + m;
+          const int o = (hh * TH + t) * 16 + m;
           const float v = e.mask[(pr < R && o < Cout) ? pr * Cout + o : 0];
           mk[t][r] = v;
         }
     } else {
 #pragma unroll
-      for (int t = 0; t < TO; ++t)
+      for (int t = 0; t < TH; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) mk[t][r] = 1.f;
     }
-    if (GEN && e.add != nullptr) {
+    if (GEN && e.add != nullptr && hh * TH * 16 < e.add_cols) {
 #pragma unroll
-      for (int t = 0; t < TO; ++t)
+      for (int t = 0; t < TH; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t pr = tile * 16 + 4 * g + r;
-          const int o = t * 16 + m;
+          const int o = (hh * TH + t) * 16 + m;
           const bool ok = pr < R && o < e.add_cols;
           const float v = e.add[ok ? pr * e.sa + o : 0];
           ad[t][r] = ok ? v : 0.f;
         }
     } else {
 #pragma unroll
-      for (int t = 0; t < TO; ++t)
+      for (int t = 0; t < TH; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) ad[t][r] = 0.f;
     }
 #pragma unroll
-    for (int t = 0; t < TO; ++t) {
-      const int o = t * 16 + m;
+    for (int t = 0; t < TH; ++t) {
+      const int o = (hh * TH + t) * 16 + m;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t pr = tile * 16 + 4 * g + r;
         if (pr < R && o < Cout) {
-          float v = lin_act(e.relu, acc[t][r] + bv[t]);
+          float v = lin_act(e.relu, acc[t][r] + bv[hh * TH + t]);
           v = mk[t][r] <= 0.f ? 0.f : v;  // relu_mask
           v += ad[t][r];  // 0 without add / past add_cols
           if (GEN && e.store_cf) {
@@ -806,6 +811,7 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
           }
         }
       }
+    }
     }
     if (tn >= T) break;
     tile = tn;
