@@ -735,26 +735,9 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
 #pragma unroll
     for (int hh = 0; hh < NH; ++hh) {
     __builtin_amdgcn_sched_barrier(0);  // one output group's registers live at a time
-    f32x4 acc[TH];
-#pragma unroll
-    for (int t = 0; t < TH; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      {
-        f32x4 wv[TH];
-#pragma unroll
-        for (int t = 0; t < TH; ++t)
-          wv[t] = *reinterpret_cast<const f32x4*>(&Ws[((hh * TH + t) * 16 + m) * ST + 16 * q + 4 * g]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int t = 0; t < TH; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[q][i], wv[t][i], acc[t], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);  // keep the weight reads per chunk (no hoisting of all Q x TH)
-      }
-    }
     // D[point 4 g + r][out t * 16 + m]; the epilogue's operand loads (mask, add) for all
-    // TH x 4 outputs are issued before the first use, not one dependent load per store
+    // TH x 4 outputs are issued before this group's MFMAs (their latency hides behind them),
+    // not one dependent load per store
     // (workgroup-uniform branches around unconditional loads at clamped indices: no per-load
     // exec-mask branch, so no wait per load)
     float mk[TH][4], ad[TH][4];
@@ -790,6 +773,24 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
       for (int t = 0; t < TH; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) ad[t][r] = 0.f;
+    }
+    f32x4 acc[TH];
+#pragma unroll
+    for (int t = 0; t < TH; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      {
+        f32x4 wv[TH];
+#pragma unroll
+        for (int t = 0; t < TH; ++t)
+          wv[t] = *reinterpret_cast<const f32x4*>(&Ws[((hh * TH + t) * 16 + m) * ST + 16 * q + 4 * g]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int t = 0; t < TH; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[q][i], wv[t][i], acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);  // keep the weight reads per chunk (no hoisting of all Q x TH)
+      }
     }
 #pragma unroll
     for (int t = 0; t < TH; ++t) {
