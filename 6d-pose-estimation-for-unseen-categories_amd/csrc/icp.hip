@@ -90,15 +90,21 @@ inline int64_t work_bytes_for(int B, int nsrc_max, int ntgt_max) {
          al256((int64_t)B * nsrc_max * 4) + al256((int64_t)B * (nblk > 0 ? nblk : 1) * kNPart * 8);
 }
 
-// grid (B): T <- T_init, counters reset.
-__global__ void icp_init_kernel(const double* __restrict__ T_init, IcpState* __restrict__ st) {
+// grid (B): T <- T_init, counters reset. A crop whose source or target exceeds the capacity
+// (nsrc_max / ntgt_max, the work buffer's per-crop rows) never runs: inactive, converged = -1
+// (the result's overflow flag), T = T_init.
+__global__ void icp_init_kernel(const double* __restrict__ T_init, const int64_t* __restrict__ src_off,
+                                const int64_t* __restrict__ tgt_off, int nsrc_max, int ntgt_max,
+                                IcpState* __restrict__ st) {
   const int b = blockIdx.x;
   if (threadIdx.x < 16) st[b].T[threadIdx.x] = T_init[16 * b + threadIdx.x];
   if (threadIdx.x == 0) {
+    const bool over = src_off[b + 1] - src_off[b] > nsrc_max || tgt_off[b + 1] - tgt_off[b] > ntgt_max;
     st[b].fit = st[b].rmse = st[b].prev_fit = st[b].prev_rmse = 0.0;
+    st[b].xmin = st[b].inv_w = 0.0;
     st[b].iter = 0;
-    st[b].active = 1;
-    st[b].converged = 0;
+    st[b].active = over ? 0 : 1;
+    st[b].converged = over ? -1 : 0;
   }
 }
 
@@ -121,7 +127,7 @@ __global__ __launch_bounds__(kIThreads) void icp_sort_kernel(const double* __res
   const int b = blockIdx.y;
   const int64_t p0 = off[b];
   const int n = (int)(off[b + 1] - p0);
-  if ((int)blockIdx.x * kIThreads >= n) return;  // block-uniform
+  if ((int)blockIdx.x * kIThreads >= n || n > nmax) return;  // block-uniform (over capacity: skipped, see init)
   const double* P = pts + 3 * p0;
   const double* Mb = M ? M + 16 * b : nullptr;
   auto key_x = [&](int j) {
@@ -177,6 +183,7 @@ __global__ __launch_bounds__(1024) void icp_bucket_sort_kernel(const double* __r
   const int b = blockIdx.x;
   const int64_t p0 = off[b];
   const int n = (int)(off[b + 1] - p0);
+  if (n > nmax) return;  // over capacity: skipped (see icp_init_kernel)
   const double* Pt = pts + 3 * p0;
   const double* Mb = M ? M + 16 * b : nullptr;
   auto key_x = [&](int t) {  // recomputed per pass (keeps LDS at 12 B per key: P <= 8192 fits)
@@ -305,6 +312,7 @@ __global__ __launch_bounds__(1024) void icp_bucket_kernel(const int64_t* __restr
                                                           int32_t* __restrict__ tbl) {
   const int b = blockIdx.x;
   const int nt = (int)(tgt_off[b + 1] - tgt_off[b]);
+  if (nt > ntgt_max) return;  // over capacity: the crop stays inactive (icp_init_kernel)
   const double* X = sx + (int64_t)b * ntgt_max;
   int32_t* Tb = tbl + (int64_t)b * (kNBuckets + 1);
   const double xmin = nt > 0 ? X[0] : 0.0, xmax = nt > 0 ? X[nt - 1] : 0.0;
@@ -601,7 +609,7 @@ extern "C" int pk_icp_init(const double* src, const int64_t* src_off, const doub
   PK_REQUIRE(work_bytes >= work_bytes_for(B, nsrc_max, ntgt_max));
   hipStream_t s = pk::as_stream(stream);
   const IcpWork w = carve(work, B, nsrc_max, ntgt_max);
-  hipLaunchKernelGGL(icp_init_kernel, dim3(B), dim3(64), 0, s, T_init, w.st);
+  hipLaunchKernelGGL(icp_init_kernel, dim3(B), dim3(64), 0, s, T_init, src_off, tgt_off, nsrc_max, ntgt_max, w.st);
   PK_CHECK_LAUNCH();
   // x order of the targets (and of the source queries under T_init): bucket sort in LDS up to
   // 8192 points per crop, rank counting beyond

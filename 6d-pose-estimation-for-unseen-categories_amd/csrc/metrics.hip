@@ -9,6 +9,7 @@
 //                 1-D data, reported as sqrt(d*d))
 //  Outputs per crop: out[b] = {ADD, mean xyz[0..2], mean adds[0..2]} (means in fp64; the
 //  reference's np.mean uses pairwise summation, so results agree to rounding).
+//  A crop with more points than the capacity nmax is not evaluated: its outputs are NaN.
 #include "common.hpp"
 
 namespace {
@@ -31,7 +32,7 @@ __global__ __launch_bounds__(256) void pm_point_kernel(const double* __restrict_
   const int64_t o = off[b];
   const int n = (int)(off[b + 1] - o);
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || n > nmax) return;
   const double* p = cad + 3 * (o + i);
   const double x = p[0], y = p[1], z = p[2];
   const double* te = Te + 16 * b;
@@ -56,7 +57,7 @@ __global__ __launch_bounds__(256) void pm_adds_kernel(const int64_t* __restrict_
   const int b = blockIdx.z, r = blockIdx.y;
   const int n = (int)(off[b + 1] - off[b]);
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (blockIdx.x * 256 >= n) return;
+  if (blockIdx.x * 256 >= n || n > nmax) return;
   const double ei = i < n ? e[((int64_t)b * 3 + r) * nmax + i] : 0.0;
   double best = __builtin_huge_val();
   for (int t0 = 0; t0 < n; t0 += 1024) {
@@ -78,6 +79,10 @@ __global__ __launch_bounds__(256) void pm_mean_kernel(const int64_t* __restrict_
   __shared__ double ws[4];
   const int b = blockIdx.y, q = blockIdx.x;
   const int n = (int)(off[b + 1] - off[b]);
+  if (n > nmax) {  // over capacity: not evaluated
+    if (threadIdx.x == 0) out[b * 7 + q] = __builtin_nan("");
+    return;
+  }
   double s = 0.0;
   for (int i = threadIdx.x; i < n; i += 256) s += per[((int64_t)b * 7 + q) * nmax + i];
   s = pk::wave_sum_f64(s);

@@ -21,8 +21,11 @@
 //     written over the distances (the A operand of the next product, same register layout);
 //   dQ[16 x 32] = R[16 x 512] . O[512 x 32]  (k-slot g of step (t, v) = partner 16 t + 4 g + v);
 //   dq_a = q_a sum_o r - (R O)_a  (torch's _euclidean_dist_backward), then F.normalize's
-//   backward, added into g_own[b, idx(a)] (global f32 atomics: a CAD point can sit in several
-//   pairs, as torch's gather-backward scatter_add).
+//   backward, written as slot a's gradient row dx[a] (scratch [B, S, 32]).
+// A CAD / crop point can sit in several pairs (torch's gather backward scatter_adds them); a
+// third launch (nce_scatter_kernel, one block per crop and side) zero-fills g and adds each
+// point's slot rows in ascending slot order: the gradients are deterministic (the float
+// atomics of round 2 made the graphed and eager steps differ in the last bits).
 // Column pass: the same per key column o -> g2;  block (0, b) also writes
 //   loss[b] = sum_a term[a] / max(n_valid, 1) in a fixed order (deterministic).
 // prenorm: f1 / f2 are already F.normalize'd (the overlap head's l2-normalize writes a rows
@@ -82,7 +85,7 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
     const FeatView f1, const FeatView f2, int64_t N1, int64_t N2,
     const int64_t* __restrict__ pairs, int cap, const int64_t* __restrict__ rows,
     const uint8_t* __restrict__ valid, int S, float inv_t, int prenorm, float* __restrict__ lse,
-    float* __restrict__ term, float* __restrict__ loss, float* __restrict__ g_own) {
+    float* __restrict__ term, float* __restrict__ loss, float* __restrict__ dx_own) {
   __shared__ __attribute__((aligned(16))) float Os[kMaxS * kLd];  // the other side's normalized vectors
   __shared__ __attribute__((aligned(16))) float on_s[kMaxS];      // their |u|^2 (+inf: invalid slot)
   __shared__ __attribute__((aligned(16))) float lse_s[kMaxS];     // COLS: the softmax rows' lse
@@ -164,7 +167,7 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
     t = pk::wave_sum_f32(t);
     if (lane == 0) loss[b] = t * sc;
   }
-  if (COLS && g_own == nullptr) return;
+  if (COLS && dx_own == nullptr) return;
   const int a0 = blockIdx.x * kTile + w * kRowsPerWave;  // wave-uniform; no barrier below
   if (a0 >= S) return;
   const int r = lane & 15, g = lane >> 4;
@@ -246,7 +249,7 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
       lse[(int64_t)b * S + a] = ok ? lse_a : 0.f;
       term[(int64_t)b * S + a] = ok ? lse_a - ldg : 0.f;
     }
-    if (g_own == nullptr) return;
+    if (dx_own == nullptr) return;
   }
   // (R O)[row 4 g + v][channel 16 h + r]
   fx4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -276,12 +279,68 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
 #pragma unroll
     for (int off = 1; off < 16; off <<= 1) vdv += __shfl_xor(vdv, off);  // the row's 16 lanes
     if (!okw) continue;
-    const int64_t base = ((int64_t)b * N_own + widx_s[trw]) * kC + r;
+    const int64_t base = ((int64_t)b * S + a0 + rw) * kC + r;  // slot row (the scatter sums them)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const float dx = prenorm ? dv[h] : nw > 1e-12f ? (dv[h] - vc[h] * vdv) / nw : dv[h] / 1e-12f;
-      atomicAdd(g_own + base + 16 * h, dx);
+      dx_own[base + 16 * h] = dx;
     }
+  }
+}
+
+// g[b, idx] = sum of the slot rows dx[b, a] with idx(a) = idx, in ascending slot order (0 for
+// points in no valid slot). One 512-thread block per (crop, side): the (idx, slot) keys of the
+// crop's slots are sorted in LDS (bitonic, 512 keys), so every point's slots form one ascending
+// run; work item (sorted position, channel) at a run's head sums the run (128-B coalesced rows).
+constexpr int kScT = 512;
+__global__ __launch_bounds__(kScT) void nce_scatter_kernel(const int64_t* __restrict__ pairs, int cap,
+                                                           const int64_t* __restrict__ rows,
+                                                           const uint8_t* __restrict__ valid, int S, int64_t N1,
+                                                           int64_t N2, const float* __restrict__ dxr,
+                                                           float* __restrict__ g1, float* __restrict__ g2) {
+  __shared__ int64_t key[kMaxS];
+  const int b = blockIdx.x, side = blockIdx.y, B = gridDim.x;
+  const int t = threadIdx.x;
+  const int64_t N = side ? N2 : N1;
+  float* __restrict__ g = (side ? g2 : g1) + (int64_t)b * N * kC;
+  const float* __restrict__ dx = dxr + ((int64_t)side * B + b) * S * kC;
+  constexpr int64_t kNone = 0x7fffffffffffffffLL;
+  if (t < kMaxS) {
+    int64_t k = kNone;
+    if (t < S && valid[(int64_t)b * S + t] != 0) {
+      const int64_t r = rows[(int64_t)b * S + t];
+      k = (pairs[((int64_t)b * cap + r) * 2 + side] << 9) | t;
+    }
+    key[t] = k;
+  }
+  float4* gz = reinterpret_cast<float4*>(g);  // N * 32 floats, 16-B aligned (torch allocation, N * 128 B rows)
+  for (int64_t e = t; e < N * (kC / 4); e += kScT) gz[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  for (int k = 2; k <= kMaxS; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (t < kMaxS / 2) {
+        const int i = (t / j) * 2 * j + (t % j), ixj = i + j;
+        const int64_t x = key[i], y = key[ixj];
+        if ((x > y) == ((i & k) == 0)) {
+          key[i] = y;
+          key[ixj] = x;
+        }
+      }
+      __syncthreads();
+    }
+  const int c = t & (kC - 1);
+  for (int p = t / kC; p < kMaxS; p += kScT / kC) {
+    const int64_t k = key[p];
+    if (k == kNone) break;  // sentinels sort last
+    const int64_t idx = k >> 9;
+    if (p > 0 && (key[p - 1] >> 9) == idx) continue;  // not the head of its run
+    float s = dx[(k & 511) * kC + c];
+    for (int q = p + 1; q < kMaxS; ++q) {
+      const int64_t kq = key[q];
+      if (kq == kNone || (kq >> 9) != idx) break;
+      s += dx[(kq & 511) * kC + c];
+    }
+    g[idx * kC + c] = s;
   }
 }
 
@@ -291,28 +350,34 @@ extern "C" int pk_nce_loss(const float* f1, const int64_t* st1, const float* f2,
                            int64_t N1, int64_t N2, int C,
                            const int64_t* pairs, int cap, const int64_t* rows, const uint8_t* valid, int S,
                            float nce_t, int prenorm, float* lse, float* term, float* loss, float* g1, float* g2,
-                           void* stream) {
+                           float* dx_rows, void* stream) {
   PK_REQUIRE(B >= 0 && C == kC && S >= 0 && S <= kMaxS && cap >= 0 && nce_t > 0.f);
   PK_REQUIRE((g1 == nullptr) == (g2 == nullptr));
+  PK_REQUIRE(g1 == nullptr || dx_rows != nullptr);
   if (B == 0) return PK_OK;
   PK_REQUIRE(loss != nullptr);
   hipStream_t s = pk::as_stream(stream);
-  if (g1) {
-    hipError_t e = pk::zero_async(g1, sizeof(float) * (size_t)B * N1 * kC, s);
-    if (e == hipSuccess) e = pk::zero_async(g2, sizeof(float) * (size_t)B * N2 * kC, s);
-    if (e != hipSuccess) return (int)e;
+  if (S == 0) {
+    hipError_t e = pk::zero_async(loss, sizeof(float) * B, s);
+    if (g1 && e == hipSuccess) e = pk::zero_async(g1, sizeof(float) * (size_t)B * N1 * kC, s);
+    if (g1 && e == hipSuccess) e = pk::zero_async(g2, sizeof(float) * (size_t)B * N2 * kC, s);
+    return e == hipSuccess ? PK_OK : (int)e;
   }
-  if (S == 0) return pk::zero_async(loss, sizeof(float) * B, s) == hipSuccess ? PK_OK : PK_ERR_ARG;
   PK_REQUIRE(f1 && f2 && pairs && rows && valid && lse && term && cap > 0);
   const float inv_t = 1.f / nce_t;
   const dim3 grid((S + kTile - 1) / kTile, B);
   const FeatView v1{f1, st1 ? st1[0] : N1 * kC, st1 ? st1[1] : kC, st1 ? st1[2] : 1};
   const FeatView v2{f2, st2 ? st2[0] : N2 * kC, st2 ? st2[1] : kC, st2 ? st2[2] : 1};
   hipLaunchKernelGGL(nce_pass_kernel<false>, grid, dim3(64 * kWaves), 0, s, v1, v2, N1, N2, pairs, cap, rows, valid,
-                     S, inv_t, prenorm, lse, term, loss, g1);
+                     S, inv_t, prenorm, lse, term, loss, g1 ? dx_rows : nullptr);
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(nce_pass_kernel<true>, grid, dim3(64 * kWaves), 0, s, v1, v2, N1, N2, pairs, cap, rows, valid,
-                     S, inv_t, prenorm, lse, term, loss, g2);
+                     S, inv_t, prenorm, lse, term, loss, g2 ? dx_rows + (size_t)B * S * kC : nullptr);
   PK_CHECK_LAUNCH();
+  if (g1) {
+    hipLaunchKernelGGL(nce_scatter_kernel, dim3(B, 2), dim3(kScT), 0, s, pairs, cap, rows, valid, S, N1, N2, dx_rows,
+                       g1, g2);
+    PK_CHECK_LAUNCH();
+  }
   return PK_OK;
 }

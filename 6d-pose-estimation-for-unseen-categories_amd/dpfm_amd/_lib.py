@@ -58,7 +58,7 @@ SIGNATURES = {
     "pk_linear_wgrad": [_P, _P, _I, _I64, _I, _I, _I, _P, _P, _P, _I, _P],
     "pk_linear_wgrad_grouped_work": [_P, _I],
     "pk_linear_wgrad_grouped": [_P, _I, _P, _I64, _P],
-    "pk_nce_loss": [_P, _P, _P, _P, _I, _I64, _I64, _I, _P, _I, _P, _P, _I, _F, _I, _P, _P, _P, _P, _P, _P],
+    "pk_nce_loss": [_P, _P, _P, _P, _I, _I64, _I64, _I, _P, _I, _P, _P, _I, _F, _I, _P, _P, _P, _P, _P, _P, _P],
     "pk_affine_cat": [_P, _I64, _P, _I64, _F, _F, _P, _P],
     "pk_loss_head": [_P, _P, _I, _I, _P, _P, _F, _F, _F, _P, _P, _P, _P],
     "pk_loss_scale": [_P, _P, _P, _P, _I, _P, _P],

@@ -809,9 +809,10 @@ class _NCELoss(torch.autograd.Function):
         loss = torch.empty((B,), dtype=torch.float32, device=dev)
         g1 = torch.empty((B, N1, C), dtype=torch.float32, device=dev) if want else None
         g2 = torch.empty((B, N2, C), dtype=torch.float32, device=dev) if want else None
+        dxr = torch.empty((2, B, max(S, 1), C), dtype=torch.float32, device=dev) if want else None
         call("pk_nce_loss", ctypes.c_void_p(f1c.data_ptr()), st(f1c), ctypes.c_void_p(f2c.data_ptr()), st(f2c), B, int(N1), int(N2), int(C), ptr(pairs), int(pairs.shape[1]),
              ptr(rows), ptr(valid), int(S), float(nce_t), 0, ptr(lse), ptr(term), ptr(loss), ptr(g1), ptr(g2),
-             _lib.stream(dev), work=None)
+             ptr(dxr), _lib.stream(dev), work=None)
         ctx.save_for_backward(g1, g2)
         return loss
 
@@ -866,9 +867,10 @@ def _nce_raw(f1, f2, pairs, rows, valid, nce_t, want, prenorm=False):
     loss = torch.empty((B,), dtype=torch.float32, device=dev)
     g1 = torch.empty((B, N1, C), dtype=torch.float32, device=dev) if want else None
     g2 = torch.empty((B, N2, C), dtype=torch.float32, device=dev) if want else None
+    dxr = torch.empty((2, B, max(S, 1), C), dtype=torch.float32, device=dev) if want else None
     call("pk_nce_loss", ctypes.c_void_p(f1c.data_ptr()), st(f1c), ctypes.c_void_p(f2c.data_ptr()), st(f2c), B,
          int(N1), int(N2), int(C), ptr(pairs), int(pairs.shape[1]), ptr(rows), ptr(valid), int(S), float(nce_t),
-         int(prenorm), ptr(lse), ptr(term), ptr(loss), ptr(g1), ptr(g2), _lib.stream(dev), work=None)
+         int(prenorm), ptr(lse), ptr(term), ptr(loss), ptr(g1), ptr(g2), ptr(dxr), _lib.stream(dev), work=None)
     return loss, g1, g2
 
 

@@ -571,13 +571,17 @@ class InferStep:
         T_gt[:, :3, :3] = fb.R.view(B, 3, 3)
         T_gt[:, :3, 3] = fb.t
         T_gt[:, 3, 3] = 1.0
-        metrics = ops.pose_metrics(fb.cad64, fb.cad_off, V1, T, T_gt)
+        # capacities of the packed point sets the pose stages read: the frame batch's CADs (fb.n1max, the
+        # largest; the operator rows V1 may be a decimated CAD) and the crops (crops.ld)
+        n1cap = max(int(fb.n1max or 0), V1)
+        metrics = ops.pose_metrics(fb.cad64, fb.cad_off, n1cap, T, T_gt)
         out = dict(C=C_pred, cand=cand, p_pred=p_pred, n_corr=nsurv, ir=ir, T=T, ransac=stats, metrics=metrics,
                    corres=corres, cor_off=cor_off)
         if self.icp_evaluations > 0:
             T_icp, icp_stats = ops.icp_fixed(fb.cad64, fb.cad_off, crops.pc64, crops.off, T, self.icp_threshold,
-                                             self.icp_evaluations, V1, V2)
-            out.update(T_icp=T_icp, icp=icp_stats, metrics_icp=ops.pose_metrics(fb.cad64, fb.cad_off, V1, T_icp, T_gt))
+                                             self.icp_evaluations, n1cap, max(int(crops.ld), V2))
+            out.update(T_icp=T_icp, icp=icp_stats,
+                       metrics_icp=ops.pose_metrics(fb.cad64, fb.cad_off, n1cap, T_icp, T_gt))
         return out
 
 

@@ -3,11 +3,11 @@
 One step = one training iteration of the reference (scripts/train.py:88-124) for a batch
 of B synthetic 640x480 RGB-D frames, with the dataset's crop formation on the device:
   back-projection + erosion -> SOR kNN-20 -> FPS to 1024 -> align transform -> ball
-  query (P, overlaps) -> RGB at the crop points -> DPFMNet fwd -> C_gt + DPFMLoss ->
+  query (P, overlaps) -> DPFMNet fwd -> C_gt + DPFMLoss ->
   naive point map + inlier ratio -> backward -> grad all-reduce (N > 1) -> clip -> RMSprop.
 Inputs (frames, CAD models, cached spectral operators) are resident in HBM before timing.
 
-  python bench.py [--gpus N --steps K --warmup W --batch B]
+  python bench.py [--gpus N --steps K --warmup W --batch B]   (N > 1: spawns N ranks itself)
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 Rank 0 prints one JSON line (contract in the task statement / DESIGN.md §Measurement).
 """
@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--points", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-crops", type=int, default=30, help="bounded CPU-baseline sample (crops)")
+    ap.add_argument("--pose-crops", type=int, default=8,
+                    help="train: crops of the post-timing pose-vs-reference check (0: skip)")
     ap.add_argument("--no-roofline-probe", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP graph: launch every kernel from Python")
     ap.add_argument("--train-only", action="store_true",
@@ -266,6 +268,70 @@ def cpu_infer_baseline(n_crops: int, n1: int, n2: int, H: int) -> dict:
             "rates": [round(r, 4) for r in rates], "seconds": round(dt, 2)}
 
 
+def cpu_pose_check(model, fb, op, crops, out: dict, n_sample: int, H: int, seed: int) -> dict:
+    """The metric's "pose err vs ref": the device pose path (InferStep: DPFMNet forward ->
+    top-5 -> rigidity filter -> RANSAC, already run, `out`) against the reference CPU path
+    restated by oracle/ on the SAME crops and weights, for a bounded sample of crops:
+      end_to_end   torch-CPU fp32 DPFMNet -> spacial_filtering_fmap2pointmap -> C RANSAC (the
+                   same hash-drawn hypotheses) -> T_ref, compared with the device T;
+      same_corr    the C RANSAC on the device's own survivors (isolates the pose stage).
+    ADD (test_RANSAC.py:162-173) of both poses vs T_gt. North-star tolerance: 1e-4."""
+    import ctypes
+    from oracle import dpfm_oracle as O
+    from oracle import dpfm_model_oracle as M
+    from dpfm_amd.pipeline import model_batch
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "liboracle.so"))
+    P = ctypes.c_void_p
+    lib.oc_ransac.argtypes = [P, P, P, ctypes.c_int, P, ctypes.c_uint64, ctypes.c_int64, ctypes.c_double, P, P]
+    cp = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    ref = M.DPFMNet().eval()
+    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
+    mb = model_batch(op, crops)
+    B = int(crops.off.numel() - 1)
+    n = min(n_sample, B)
+    keys = ("xyz", "mass", "evals", "evecs")
+    cpu = {k: {kk: vv[:n].cpu() for kk, vv in v.items() if kk in keys} for k, v in mb.items()}
+    T_dev = out["T"].cpu().numpy()
+    p_pred, ncorr = out["p_pred"].cpu().numpy(), out["n_corr"].cpu().numpy()
+    cad64, cad_off = fb.cad64.cpu().numpy(), fb.cad_off.cpu().numpy()
+    pc64, off = crops.pc64.cpu().numpy(), crops.off.cpu().numpy()
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        C_ref = ref(cpu)[0]
+    e2e, same, within, add_dev, add_ref = [], [], 0, [], []
+    for b in range(n):
+        cad_b = np.ascontiguousarray(cad64[cad_off[b]:cad_off[b + 1]])
+        pc_b = np.ascontiguousarray(pc64[off[b]:off[b + 1]])
+        ex, ey = cpu["shape1"]["evecs"][b, :, :30], cpu["shape2"]["evecs"][b, :, :30]
+        with torch.no_grad():
+            corr = O.spacial_filtering_fmap2pointmap(C_ref[b], ex, ey, cpu["shape1"]["xyz"][b], cpu["shape2"]["xyz"][b],
+                                                     fb.diam[b])
+        T_ref = np.zeros(16)
+        st = np.zeros(3)
+        cor = np.ascontiguousarray(corr.t().numpy().astype(np.int32))
+        lib.oc_ransac(cp(cad_b), cp(pc_b), cp(cor), int(cor.shape[0]), None, seed, H, 0.05, cp(T_ref), cp(st))
+        T_s = np.zeros(16)
+        cs = np.ascontiguousarray(p_pred[b, :ncorr[b]].astype(np.int32))
+        lib.oc_ransac(cp(cad_b), cp(pc_b), cp(cs), int(ncorr[b]), None, seed, H, 0.05, cp(T_s), cp(st))
+        d = float(np.abs(T_dev[b] - T_ref.reshape(4, 4)).max())
+        e2e.append(d)
+        within += d <= 1e-4
+        same.append(float(np.abs(T_dev[b] - T_s.reshape(4, 4)).max()))
+        T_gt = np.eye(4)
+        T_gt[:3, :3] = fb.R[b].cpu().numpy().reshape(3, 3)
+        T_gt[:3, 3] = fb.t[b].cpu().numpy()
+        add_dev.append(O.add(T_dev[b], T_gt, cad_b, fb.diam[b])[0])
+        add_ref.append(O.add(T_ref.reshape(4, 4), T_gt, cad_b, fb.diam[b])[0])
+    return {"crops": n, "hypotheses": H, "tolerance": 1e-4,
+            "end_to_end_max_abs_dT": round(max(e2e), 12), "end_to_end_crops_within_tol": int(within),
+            "same_corr_max_abs_dT": round(max(same), 15),
+            "mean_add_device": round(float(np.mean(add_dev)), 6), "mean_add_ref": round(float(np.mean(add_ref)), 6),
+            "seconds": round(time.perf_counter() - t0, 2),
+            "note": "device InferStep vs oracle/ (torch-CPU fp32 model, spacial filtering, C RANSAC on the same "
+                    "hypothesis draws) on the same crops and weights; same_corr runs the oracle RANSAC on the "
+                    "device's survivors; ADD in cm vs the synthetic T_gt (random-init weights: ADD is large)"}
+
+
 TRAIN_METRIC = "RGB-D crops/sec (fwd+bwd), 1024 pts, at 1/2/4/8 MI355X; pose err vs ref"
 INFER_METRIC = ("RGB-D crops/sec (inference: crop formation + DPFM fwd + spatial-filter solver + IR + "
                 "RANSAC 1024 hyp + pose metrics)")
@@ -277,8 +343,28 @@ CROP_FAMS = {"pk_backproject", "pk_sor", "pk_fps_npoint", "pk_fps", "pk_gather_t
              "pk_ball_query_mask", "pk_ball_query_pairs", "pk_sample_rgb", "pk_erode_mask"}
 
 
-def setup_dist():
+def launcher_cmd(argv, env) -> list | None:
+    """`python bench.py --gpus N` (N > 1) outside a torch.distributed launcher: the command that
+    starts N ranks (one process per GPU) as a CHILD process, or None when this process is
+    already a rank (WORLD_SIZE set) or N == 1. The parent never touches the GPU; it waits for
+    the child and exits with its code (no exec from a process that initialised HIP)."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    known, _ = ap.parse_known_args(argv)
+    if "WORLD_SIZE" in env or known.gpus <= 1:
+        return None
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={known.gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def setup_dist(gpus: int = 0):
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if gpus and world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}; launch with --nproc-per-node {gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knob: PK_BENCH_BACKEND=gloo with more ranks than GPUs shares the cards
@@ -293,6 +379,9 @@ def setup_dist():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     return world, rank, dev
+
+
+POSE_CHECK = {}  # mode -> the post-timing pose-vs-reference check (cpu_baseline leg)
 
 
 def build_train(args, dev, rank, world):
@@ -324,6 +413,14 @@ def build_train(args, dev, rank, world):
               "precision": "model fp32 (f32 MFMA); crop geometry / C_gt normal equations fp64",
               "parallelism": f"dp{world}"}
     probe = lambda: step(op, crops_of(fb))  # noqa: E731
+
+    def pose_check(n_sample):  # the metric's "pose err vs ref" on the trained weights (after timing)
+        from dpfm_amd.pipeline import InferStep
+        crops = crops_of(fb)
+        out = InferStep(model, hypotheses=1024, seed=5)(fb, op, crops)
+        torch.cuda.synchronize()
+        return cpu_pose_check(model, fb, op, crops, out, n_sample, 1024, 5)
+    POSE_CHECK["fn"] = pose_check
     return one_step, probe, TRAIN_METRIC, B, config
 
 
@@ -622,8 +719,14 @@ def cpu_icp_baseline(n_crops: int, target: str) -> dict:
 
 
 def main():
+    cmd = launcher_cmd(sys.argv[1:], os.environ)
+    if cmd is not None:  # --gpus N > 1 without a launcher: N ranks as a child job
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        sys.exit(subprocess.call(cmd, env=env))
     args = parse()
-    world, rank, dev = setup_dist()
+    world, rank, dev = setup_dist(args.gpus)
     from dpfm_amd import _lib
     build = {"train": build_train, "infer": build_infer, "corr4096": build_corr, "icp": build_icp,
              "teaser": build_teaser, "operators": build_operators}[args.mode]
@@ -735,6 +838,8 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             if args.mode == "train":
                 out["cpu_baseline"] = cpu_baseline(args.cpu_crops, args.points, args.points)
+                if "fn" in POSE_CHECK and args.pose_crops > 0:
+                    out["pose_err"] = POSE_CHECK["fn"](args.pose_crops)
             elif args.mode == "corr4096":
                 out["cpu_baseline"] = cpu_ransac_baseline(args.hypotheses)
             elif args.mode == "icp":

@@ -383,14 +383,15 @@ int pk_nce_select(const int64_t* count, int B, int64_t cap, int num, uint64_t se
  * strides st1 / st2 = HOST int64[3] {batch, point, channel} (NULL: contiguous rows), so a
  * channels-first [B, C, N] storage is read in place;
  * S <= 512. lse / term f32 [B, S] scratch. g1 / g2 (both or neither) f32 [B, N1|N2, C]
- * receive d loss[b] / d f1[b], f2[b] (zero-filled, then accumulated with f32 atomics,
- * as torch's gather backward).  * prenorm = 1: f1 / f2 are already F.normalize'd; g1 / g2 are then the gradients with
+ * receive d loss[b] / d f1[b], f2[b]: the passes write each slot's gradient row into
+ * dx_rows (f32 [2, B, S, C] scratch, required with g1 / g2), and a third launch sums a
+ * point's slot rows in ascending slot order (torch's gather backward, deterministic).  * prenorm = 1: f1 / f2 are already F.normalize'd; g1 / g2 are then the gradients with
  * respect to the normalized features (no normalize backward).
  */
 int pk_nce_loss(const float* f1, const int64_t* st1, const float* f2, const int64_t* st2, int B, int64_t N1,
                 int64_t N2, int C, const int64_t* pairs,
                 int cap, const int64_t* rows, const uint8_t* valid, int S, float nce_t, int prenorm, float* lse,
-                float* term, float* loss, float* g1, float* g2, void* stream);
+                float* term, float* loss, float* g1, float* g2, float* dx_rows, void* stream);
 
 /* H15 DPFMLoss scalar head (utils/loss.py:44-99, FrobeniusLoss :8-15), one launch:
  *   fmap = w_fmap * mean_b clamp(sum (C12_b - Cgt_b)^2, -1, 1000); nce = sum_b nce[b] w_nce / B;
@@ -428,7 +429,8 @@ int pk_ransac(const double* src, const int64_t* src_off, const double* dst, cons
  *   cad f64 [T,3] packed / off (model points in the object frame), T_est / T_gt f64
  *   [B,4,4] row-major; work f64 [13 * B * nmax] scratch
  *   out f64 [B,7] = {ADD (add), mean per-row |.| x3 (compute_add_score's xyz-direction
- *   distances), mean per-row 1-D nearest-GT distance x3 (compute_adds_score)} */
+ *   distances), mean per-row 1-D nearest-GT distance x3 (compute_adds_score)}; a crop with more
+ *   than nmax points (the scratch capacity) is not evaluated: its row is NaN */
 int pk_pose_metrics(const double* cad, const int64_t* off, int B, int nmax, const double* T_est,
                     const double* T_gt, double* work, double* out, void* stream);
 
@@ -456,7 +458,8 @@ int pk_sample_features(const float* fmap, int F, int C, int H, int W, const doub
  * ICPConvergenceCriteria(max_iteration 2000), relative fitness / rmse 1e-6)), batched.
  *   src f64 [Ts,3] packed by src_off [B+1] (the CAD), tgt f64 [Tt,3] packed by tgt_off [B+1]
  *   (the reference's GT-posed CAD, or the observed crop); T_init f64 [B,4,4] row-major;
- *   nsrc_max / ntgt_max >= every crop's sizes (host bounds: grid and scratch sizing).
+ *   nsrc_max / ntgt_max: per-crop capacities (grid and scratch sizing); a crop whose source or
+ *   target is larger is not refined (T = T_init, stats converged = -1: capacity exceeded).
  * Per evaluation every source point T s takes its nearest target point (ties: lowest index);
  * a pair iff d^2 < max_dist^2; fitness = pairs / |src|, rmse = sqrt(sum d^2 / pairs) (0 without
  * pairs). Update: Umeyama (no scaling) of the pairs (identity without pairs), T <- U T. Stop

@@ -151,3 +151,30 @@ def test_pk_icp_blocking_entry_matches_polled(device):
     assert rc == 0
     torch.cuda.synchronize()
     assert torch.equal(Ta, Tb) and torch.equal(sa, sb)
+
+
+def test_icp_and_metrics_capacity_overflow(device, coracle):
+    """A crop whose source or target exceeds the capacities the caller sized the scratch for
+    (nsrc_max / ntgt_max) is not refined and flagged (converged = -1, T = T_init) instead of
+    writing past its rows; the other crops are refined as the oracle does. pk_pose_metrics
+    reports NaN for a crop above its capacity."""
+    from dpfm_amd import ops
+    rng = np.random.default_rng(77)
+    srcs = [rng.normal(size=(n, 3)) * 3 for n in (300, 700, 300)]
+    tgts = [s + rng.normal(size=s.shape) * 0.01 for s in srcs]
+    tgts[2] = np.concatenate([tgts[2], rng.normal(size=(500, 3)) * 3])   # 800 target points
+    T0s = [_perturb(rng, np.eye(4), 2.0, 0.02, s.mean(0)) for s in srcs]
+    s, so = _pack(srcs, device)
+    t, to = _pack(tgts, device)
+    T0 = torch.from_numpy(np.stack(T0s)).to(device)
+    T, st = ops.icp(s, so, t, to, T0, 0.2, 50, nsrc_max=400, ntgt_max=400)
+    T, st = T.cpu().numpy(), st.cpu().numpy()
+    assert st[1, 3] == -1 and st[2, 3] == -1 and st[1, 2] == 0 and st[2, 2] == 0
+    np.testing.assert_array_equal(T[1], T0s[1])
+    np.testing.assert_array_equal(T[2], T0s[2])
+    To, sto = _oracle(coracle, srcs[0], tgts[0], T0s[0], 0.2, 50)
+    assert st[0, 2] == sto[2] and st[0, 3] == sto[3] and st[0, 0] == sto[0]
+    np.testing.assert_allclose(T[0], To, atol=1e-9)
+    m = ops.pose_metrics(s, so, 400, T0, T0).cpu().numpy()
+    assert np.isnan(m[1]).all() and not np.isnan(m[0]).any() and not np.isnan(m[2]).any()
+    assert (m[0] == 0).all()

@@ -32,7 +32,7 @@ FAMILIES = {
     # counters cannot tell them apart, so they form one family, per KERNEL launch
     "pk_linear_fwd+ex": ["linear_fwd_rows_kernel", "linear_fwd_cf_kernel", "linear_fwd_kernel", "linear_thin_kernel"],
     "pk_linear_wgrad_grouped": ["wgrad_grouped_kernel", "wgrad_grouped_reduce_kernel"],
-    "pk_nce_loss": ["nce_pass_kernel<false>", "nce_pass_kernel<true>", "zero_fill_kernel"],
+    "pk_nce_loss": ["nce_pass_kernel<false>", "nce_pass_kernel<true>", "nce_scatter_kernel"],
     "pk_clip_rmsprop": ["grad_sumsq_kernel", "clip_rmsprop_kernel"],
     "pk_instnorm_relu_fwd": ["instnorm_relu_fwd"],
     "pk_instnorm_relu_bwd": ["instnorm_relu_bwd"],
