@@ -91,9 +91,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
                                                        float* __restrict__ lse) {
   __shared__ float Ks[kD * kSR];
   __shared__ float Vs[kT * kSC];
-  const int h = blockIdx.y, b = blockIdx.z;
+  const int3 lb = pk::xcd_block3();  // a (crop, head)'s query blocks share one XCD's L2 (K / V)
+  const int h = lb.y, b = lb.z;
   const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
-  const int qi = blockIdx.x * kT + pk::wave_id() * 16 + c;
+  const int qi = lb.x * kT + pk::wave_id() * 16 + c;
   const float* qb = q + ((int64_t)b * kD * H + h) * N;
   const float* kb = k + ((int64_t)b * kD * H + h) * M;
   const float* vb = v + ((int64_t)b * kD * H + h) * M;
@@ -189,9 +190,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
   __shared__ float Ks[kD * kSR];
   __shared__ float Vs[kD * kSR];
   __shared__ float KT[kT * kSC];
-  const int h = blockIdx.y, b = blockIdx.z;
+  const int3 lb = pk::xcd_block3();  // a (crop, head)'s query blocks share one XCD's L2 (K / V)
+  const int h = lb.y, b = lb.z;
   const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
-  const int qi = blockIdx.x * kT + pk::wave_id() * 16 + c;
+  const int qi = lb.x * kT + pk::wave_id() * 16 + c;
   const int64_t qoff = ((int64_t)b * kD * H + h) * N;
   const float* kb = k + ((int64_t)b * kD * H + h) * M;
   const float* vb = v + ((int64_t)b * kD * H + h) * M;
@@ -270,9 +272,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
   __shared__ __attribute__((aligned(16))) float Ls[kT];
   __shared__ __attribute__((aligned(16))) float Is[kT];
   __shared__ __attribute__((aligned(16))) float Ds[kT];
-  const int h = blockIdx.y, b = blockIdx.z;
+  const int3 xb = pk::xcd_block3();  // a (crop, head)'s key blocks share one XCD's L2 (Q / dO)
+  const int h = xb.y, b = xb.z;
   const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
-  const int kj = blockIdx.x * kT + pk::wave_id() * 16 + c;
+  const int kj = xb.x * kT + pk::wave_id() * 16 + c;
   const int64_t koff = ((int64_t)b * kD * H + h) * M;
   const float* qb = q + ((int64_t)b * kD * H + h) * N;
   const float* gb = dout + ((int64_t)b * kD * H + h) * N;

@@ -28,6 +28,20 @@ namespace pk {
 constexpr int kWave = 64;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+// XCD-aware block renumbering for a 3-D grid: hardware block L = x + X (y + Y z) runs on XCD
+// L % 8 (round-robin dispatch, MI355X_MICROARCH.md); each XCD gets a contiguous range of
+// logical blocks (bijective for any grid size), so the x-blocks of one (y, z) — e.g. the
+// query blocks of one (crop, head), which share their K / V — sit in one XCD's L2.
+// Returns the logical (x, y, z).
+__device__ __forceinline__ int3 xcd_block3() {
+  const int X = gridDim.x, Y = gridDim.y;
+  const int G = X * Y * gridDim.z;
+  const int L = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
+  const int q8 = G >> 3, r8 = G & 7, x8 = L & 7;
+  const int lg = x8 * q8 + (x8 < r8 ? x8 : r8) + (L >> 3);
+  return make_int3(lg % X, (lg / X) % Y, lg / (X * Y));
+}
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {

@@ -399,8 +399,11 @@ __global__ __launch_bounds__(256) void cgt_reduce_kernel(const double* __restric
   }
 }
 
-// Minimum-norm least squares for a rank-deficient (or empty) pair list, the solution
-// torch.linalg.lstsq's CPU driver (LAPACK gelsy: complete orthogonal factorization) returns:
+// Minimum-norm least squares for a rank-deficient (or empty) pair list. This is a deliberate
+// deviation: the reference calls C_from_sparse_P on evecs already on the GPU (train.py:92,101),
+// where torch.linalg.lstsq uses the 'gels' driver (QR, no rank handling: garbage or NaN for a
+// rank-deficient system), so parity with the reference is unpinned for such crops. We return
+// what torch's CPU driver (LAPACK gelsy: complete orthogonal factorization) returns:
 // X = V diag(w) V^T H with G = V diag(lambda) V^T (cyclic Jacobi, fp64) and w_i = 1/lambda_i
 // for lambda_i > rcond^2 lambda_max (sigma_i > rcond sigma_max of A), else 0; rcond =
 // eps_f32 * max(P, 30), torch's default for f32 inputs. One wave; lane k < 30 owns index k.

@@ -368,6 +368,119 @@ __global__ __launch_bounds__(NT) void fps_lane_kernel(
   }
 }
 
+// Flat variant (the production path up to 8192 points). Thread t owns the PPT CONSECUTIVE
+// points t PPT .. t PPT + PPT - 1 (so lane order = index order), their running distances and
+// their box; the lane's running maximum bd and its first argmax bk are kept exactly. Per
+// iteration a lane updates its points only when the centroid can lower one of them (box
+// distance lb with lb (1 - 2^-19) < bd, the exactness argument of fps_pruned_kernel), a wave
+// whose lanes all skip reuses its cached best, and the block argmax is ONE LDS atomic per wave:
+// ds_max_u64 of key = (distance bits << 32) | ~index (max distance, then lowest index, torch.max's
+// tie rule) into a triple-buffered word, one barrier, one broadcast read. Round 2's kernels spent
+// ~0.7 us per iteration in per-bucket / per-wave reductions and a 16-slot second stage.
+template <int NT, int PPT>
+__global__ __launch_bounds__(NT) void fps_flat_kernel(
+    const float* __restrict__ xyz, const int64_t* __restrict__ offsets,
+    const int32_t* __restrict__ start, const int32_t* __restrict__ npoint,
+    int64_t* __restrict__ out, int out_stride) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);  // [3] (4 words reserved)
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = pk::lane_id();
+  const int64_t base = offsets[b];
+  const int n = (int)(offsets[b + 1] - base);
+  const int np = npoint[b];
+  const float* __restrict__ p = xyz + base * 3;
+  float* sx = reinterpret_cast<float*>(smem + 4 * sizeof(unsigned long long));
+  const int n_pad = (n + 3) & ~3;
+  float* sy = sx + n_pad;
+  float* sz = sy + n_pad;
+
+  const float inf = __builtin_huge_valf();
+  float px[PPT], py[PPT], pz[PPT], pd[PPT];
+  float bx0 = inf, bx1 = -inf, by0 = inf, by1 = -inf, bz0 = inf, bz1 = -inf;
+  const int i0 = tid * PPT;
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const bool ok = i0 + k < n;
+    px[k] = ok ? p[3 * (i0 + k) + 0] : 0.f;
+    py[k] = ok ? p[3 * (i0 + k) + 1] : 0.f;
+    pz[k] = ok ? p[3 * (i0 + k) + 2] : 0.f;
+    pd[k] = ok ? 1e10f : -1.f;  // empty slot: min(-1, d >= 0) keeps it at -1, never selected
+    if (ok) {
+      sx[i0 + k] = px[k];
+      sy[i0 + k] = py[k];
+      sz[i0 + k] = pz[k];
+      bx0 = fminf(bx0, px[k]); bx1 = fmaxf(bx1, px[k]);
+      by0 = fminf(by0, py[k]); by1 = fmaxf(by1, py[k]);
+      bz0 = fminf(bz0, pz[k]); bz1 = fmaxf(bz1, pz[k]);
+    }
+  }
+  if (tid < 3) keys[tid] = 0ull;
+  if (n <= 0 || np <= 0) return;  // block-uniform
+  const bool lval = i0 < n;
+  float bd = lval ? 1e10f : -1.f;  // the lane's max running distance, first reached at k = bk
+  int bk = 0;
+  __syncthreads();
+  int far = start[b];
+  float cx = sx[far], cy = sy[far], cz = sz[far];
+  unsigned long long wkey = 0ull;  // the wave's best (cached while its lanes skip)
+  int64_t* __restrict__ o = out + (int64_t)b * out_stride;
+  for (int i = 0; i < np; ++i) {
+    if (tid == 0) o[i] = far;
+    const float ddx = fmaxf(fmaxf(bx0 - cx, cx - bx1), 0.f);
+    const float ddy = fmaxf(fmaxf(by0 - cy, cy - by1), 0.f);
+    const float ddz = fmaxf(fmaxf(bz0 - cz, cz - bz1), 0.f);
+    const float lb = (ddx * ddx + ddy * ddy) + ddz * ddz;
+    const bool need = lval && !(lb * 0.99999809f >= bd);
+    if (__ballot(need)) {  // wave-uniform
+      if (need) {
+#pragma unroll
+        for (int k = 0; k < PPT; ++k) {
+          const float dx = px[k] - cx;
+          const float dy = py[k] - cy;
+          const float dz = pz[k] - cz;
+          const float d = (dx * dx + dy * dy) + dz * dz;  // no contraction (TU flag)
+          pd[k] = fminf(pd[k], d);
+        }
+        float m = pd[0];
+#pragma unroll
+        for (int k = 1; k < PPT; ++k) m = fmaxf(m, pd[k]);
+        int kk = PPT - 1;
+#pragma unroll
+        for (int k = PPT - 2; k >= 0; --k) kk = pd[k] == m ? k : kk;  // first k at the max
+        bd = m;
+        bk = kk;
+      }
+      const bool valid = bd >= 0.f;
+      const uint32_t bits = valid ? pk::f32_bits(bd) : 0u;
+      const uint32_t wbits = pk::wave_max_u32_s(bits);
+      const uint64_t at = __ballot(valid && bits == wbits);
+      const uint32_t widx = pk::readlane((uint32_t)(i0 + bk), __ffsll((unsigned long long)at) - 1);
+      wkey = ((unsigned long long)wbits << 32) | (unsigned long long)(0xffffffffu - widx);
+    }
+    if (lane == 0 && wkey != 0ull) atomicMax(&keys[i % 3], wkey);
+    if (tid == 0) keys[(i + 1) % 3] = 0ull;  // last read after barrier i - 2: every wave is past it
+    __syncthreads();
+    const unsigned long long key = keys[i % 3];
+    far = (int)(0xffffffffu - (uint32_t)(key & 0xffffffffull));
+    cx = sx[far];
+    cy = sy[far];
+    cz = sz[far];
+  }
+}
+
+template <int NT, int PPT>
+int launch_fps_flat(const float* xyz, const int64_t* offsets, const int32_t* start, const int32_t* npoint,
+                    int64_t* out, int out_stride, int B, int nmax, hipStream_t s) {
+  const int n_pad = (nmax + 3) & ~3;
+  const size_t lds = 4 * sizeof(unsigned long long) + 3 * (size_t)n_pad * sizeof(float);
+  hipLaunchKernelGGL((fps_flat_kernel<NT, PPT>), dim3(B), dim3(NT), lds, s, xyz, offsets, start, npoint, out,
+                     out_stride);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
 template <int NT, int PPT>
 int launch_fps_lane(const float* xyz, const int64_t* offsets, const int32_t* start, const int32_t* npoint,
                     int64_t* out, int out_stride, int B, hipStream_t s) {
@@ -419,6 +532,12 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
   if (B == 0) return PK_OK;
   PK_REQUIRE(xyz && offsets && start && npoint && out);
   hipStream_t s = pk::as_stream(stream);
+#ifndef PK_FPS_ROUND2  // flat kernel (one LDS atomic per wave per iteration) up to 8192 points
+  if (nmax <= 1024) return launch_fps_flat<1024, 1>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
+  if (nmax <= 2048) return launch_fps_flat<1024, 2>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
+  if (nmax <= 4096) return launch_fps_flat<1024, 4>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
+  if (nmax <= 8192) return launch_fps_flat<1024, 8>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
+#endif
 #define PK_FPS(NT, PPT) return launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s)
   // 1024-thread workgroups above 4096 points: measured 0.712 us per FPS step against 0.78
   // (512 threads) and 1.09 (256) on the bench's crops (n <= 6588, profiles/r02_kbench_fps.txt)
@@ -440,7 +559,7 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
 }
 
 // Development hook (not part of include/posekern.h): force the block size / points
-// per thread, per-lane buckets (pruned = 3), pruned (1) or plain (0), for tools/kbench.py's sweeps.
+// per thread, flat (pruned = 4), per-lane buckets (3), pruned (1) or plain (0), for tools/kbench.py's sweeps.
 extern "C" int pkdev_fps_cfg(const float* xyz, const int64_t* offsets, int B, int nmax,
                              const int32_t* start, const int32_t* npoint, int64_t* out,
                              int out_stride, int nt, int pruned, void* stream) {
@@ -448,7 +567,8 @@ extern "C" int pkdev_fps_cfg(const float* xyz, const int64_t* offsets, int B, in
   const int ppt = (nmax + nt - 1) / nt;
 #define PK_FPS(NT, PPT)                                                                          \
   if (nt == NT && ppt <= PPT)                                                                    \
-    return pruned == 3 ? launch_fps_lane<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, s) \
+    return pruned == 4 ? launch_fps_flat<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s) \
+           : pruned == 3 ? launch_fps_lane<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, s) \
            : pruned ? launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s) \
                   : launch_fps_plain<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
   PK_FPS(256, 4) PK_FPS(256, 8) PK_FPS(256, 16) PK_FPS(256, 32)

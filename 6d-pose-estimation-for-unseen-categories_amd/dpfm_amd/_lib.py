@@ -100,6 +100,10 @@ SIGNATURES = {
     "pk_dpotrf": [_P, _I, _I, _D, _P, _P],
     "pk_dpotrs": [_P, _P, _I, _I, _I, _P],
     "pk_teaser_solve": [_P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P],  # host pointers
+    "pk_device_cu_count": [_P],
+    "pk_stream_create_cu_mask": [_P, _I, _P],
+    "pk_stream_get_cu_mask": [_P, _I, _P],
+    "pk_stream_destroy": [_P],
 }
 
 RESTYPES = {"pk_cgt_lstsq_work_size": _I64, "pk_linear_wgrad_grouped_work": _I64, "pk_ransac_work_size": _I64,

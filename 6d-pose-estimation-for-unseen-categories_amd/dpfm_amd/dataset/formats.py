@@ -28,6 +28,7 @@ caches and datasets hold, write what its scripts read, without executing anythin
 """
 from __future__ import annotations
 
+import functools
 import json
 import os
 from dataclasses import dataclass, field
@@ -181,6 +182,7 @@ class BopScenes:
         self.root, self.mode, self.color = Path(root), mode, color
         self.render_data_name = self.root.name
         self.frames = []
+        scanned = 0  # the reference counts every scanned depth path, kept or dropped (scene.py:86-110)
         for depth_path in sorted((self.root / mode).rglob("*/depth/*.png")):
             scene = depth_path.parents[1]
             stem = depth_path.stem
@@ -191,7 +193,8 @@ class BopScenes:
                 rec["color"] = (scene / "rgb" / stem).with_suffix(".jpg")
             if all(p.exists() for k, p in rec.items() if k != "seg") and all(p.exists() for p in seg):
                 self.frames.append(rec)
-            if num_samples > 0 and len(self.frames) == num_samples:
+            scanned += 1
+            if scanned == num_samples:
                 break
         self._json = {}
 
@@ -247,8 +250,16 @@ def load_mapping_list(path) -> np.ndarray:
 
 
 def load_models_info(models_dir) -> dict:
+    return dict(_models_info(str(Path(models_dir).resolve())))
+
+
+@functools.lru_cache(maxsize=16)
+def _models_info(models_dir: str) -> dict:
     with open(Path(models_dir) / "models_info.json") as f:
         return json.load(f)
+
+
+_CAD_CACHE: dict = {}  # (models_dir, obj_id) -> vertices * 0.1: a PLY is parsed once per process
 
 
 def object_frame(scenes: BopScenes, i: int, j: int, models_dir, cad_cache: Optional[dict] = None) -> dict:
@@ -261,16 +272,22 @@ def object_frame(scenes: BopScenes, i: int, j: int, models_dir, cad_cache: Optio
     gt = sc["scene_gt"][j]
     oid = int(gt["obj_id"])
     models_dir = Path(models_dir)
-    cad_cache = {} if cad_cache is None else cad_cache
-    if oid not in cad_cache:
-        cad_cache[oid] = read_ply(models_dir / f"obj_{oid:06d}.ply").vertices * 0.1
-    info = load_models_info(models_dir)
+    if cad_cache is None:  # module-level cache keyed by the models directory
+        key = (str(models_dir.resolve()), oid)
+        if key not in _CAD_CACHE:
+            _CAD_CACHE[key] = read_ply(models_dir / f"obj_{oid:06d}.ply").vertices * 0.1
+        cad = _CAD_CACHE[key]
+    else:
+        if oid not in cad_cache:
+            cad_cache[oid] = read_ply(models_dir / f"obj_{oid:06d}.ply").vertices * 0.1
+        cad = cad_cache[oid]
+    info = _models_info(str(models_dir.resolve()))
     return {"depth": sc["depth"], "mask": sc["seg"][j], "K": np.asarray(sc["camera"]["cam_K"], np.float64).reshape(3, 3),
             "depth_scale": float(sc["camera"]["depth_scale"]),
             "R_m2c": np.asarray(gt["cam_R_m2c"], np.float64).reshape(3, 3),
             "t_m2c": np.asarray(gt["cam_t_m2c"], np.float64) * 0.1, "obj_id": oid,
             "visib_fract": float(sc["scene_info"][j]["visib_fract"]),
-            "cad": cad_cache[oid], "diam_cad": float(info[str(oid)]["diameter"]) * 0.1,
+            "cad": cad, "diam_cad": float(info[str(oid)]["diameter"]) * 0.1,
             "rgb": sc.get("color")}
 
 

@@ -107,3 +107,20 @@ def lbo_operators(n: int, k: int, seed: int, area: float = 300.0):
     evals = np.sort(rng.uniform(0.0, 2.0, size=k))
     evals[0] = 0.0
     return mass.astype(np.float32), evals.astype(np.float32), evecs.astype(np.float32)
+
+
+def ragged_frames(F: int, seed: int, n1: int = 5000) -> list:
+    """Frames at the reference's real sizes (tests/golden/real_crops.npz): objects of
+    1.5-7 cm semi-axes at 70-100 cm give masks of a few hundred to ~10k pixels, so the sample
+    policy (object.py:145-148) yields crops of ~200-2000 points; CADs of n1 +- 3 vertices (the
+    reference's decimated CADs have 4996-5002). Dicts with the fields pipeline.frame_batch reads."""
+    rng = np.random.default_rng(seed + 7_000_003)
+    out = []
+    for f in range(F):
+        top = float(rng.uniform(1.5, 7.0))
+        fr = make_frame(seed + f, axes_range=(0.75 * top, top))
+        n = n1 + int(rng.integers(-4, 3))
+        out.append(dict(depth=fr.depth, mask=fr.mask, rgb=fr.rgb, K=fr.K, depth_scale=fr.depth_scale,
+                        R_m2c=fr.R_m2c, t_m2c=fr.t_m2c, cad=cad_points(fr, n, seed + f), diam_cad=fr.diam_cad))
+    return out
+

@@ -13,12 +13,24 @@ def _one(x: torch.Tensor) -> torch.Tensor:
 
 
 def nn_query(feat_x, feat_y, dim=-2):
-    """argmin_i ||feat_x[i] - feat_y[j]|| for every j (naive.py:23-34); feat_x [V1, 30],
-    feat_y [V2, 30] on the device."""
+    """argmin_i ||feat_x[i] - feat_y[j]|| for every j (naive.py:23-34); feat_x [V1, C],
+    feat_y [V2, C] on the device. C <= 30 runs on the feature-distance kernel (zero columns
+    appended up to its 30-wide contraction leave every distance unchanged); wider features
+    take torch.cdist + argmin on the device, the reference's own formula."""
     if dim not in (-2, 0):
         raise ValueError("nn_query reduces over the first (V1) dimension")
+    if feat_x.dim() != 2 or feat_y.dim() != 2 or feat_x.shape[1] != feat_y.shape[1]:
+        raise ValueError("nn_query takes feat_x [V1, C] and feat_y [V2, C]")
+    if not feat_x.is_cuda:
+        raise ops._lib.PoseKernError("nn_query runs on HIP devices only (no CPU fallback)")
     V1, V2 = feat_x.shape[0], feat_y.shape[0]
+    C = feat_x.shape[1]
     dev = feat_x.device
+    if C > 30:
+        return torch.cdist(feat_x.float(), feat_y.float()).argmin(dim=0)
+    if C < 30:
+        feat_x = torch.nn.functional.pad(feat_x.float(), (0, 30 - C))
+        feat_y = torch.nn.functional.pad(feat_y.float(), (0, 30 - C))
     eye = torch.eye(30, dtype=torch.float32, device=dev)[None]
     n1 = torch.tensor([V1], dtype=torch.int32, device=dev)
     n2 = torch.tensor([V2], dtype=torch.int32, device=dev)

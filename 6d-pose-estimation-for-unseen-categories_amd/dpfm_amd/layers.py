@@ -21,9 +21,12 @@ from . import ops
 _SIDE = None  # the active GroupedWgrad (TrainStep's backward), or None
 FOLD_RELU = True  # fold a producer layer's ReLU backward into the consumer's input gradient
 # input gradients whose producer ReLU mask a consumer already applied: (dx storage pointer,
-# mask storage pointer). Keyed by storage, not by tensor object: autograd hands the producer a
-# transposed view of the consumer's dx for channels-first layers (a new Python object)
-_MASKED = set()
+# mask storage pointer) -> dx's version counter when the mask was applied. Keyed by storage, not
+# by tensor object: autograd hands the producer a transposed view of the consumer's dx for
+# channels-first layers (a new Python object, same storage and version counter). The version
+# check rejects a dx that autograd has since accumulated another consumer's gradient into (in
+# place, same pointer) and a stale entry whose address the caching allocator has reused.
+_MASKED = {}
 
 
 class GroupedWgrad:
@@ -129,7 +132,7 @@ class _PointwiseFn(torch.autograd.Function):
         w2 = weight.view(weight.shape[0], -1)
         cf = ctx.cf
         dy = dy.contiguous()
-        if ctx.relu and (dy.data_ptr(), y.data_ptr()) not in _MASKED:
+        if ctx.relu and _MASKED.get((dy.data_ptr(), y.data_ptr())) != dy._version:
             # the fused ReLU's backward (aten's ReluBackward: threshold_backward on the output),
             # unless the consuming layer already applied it in its input-gradient epilogue
             dy = torch.ops.aten.threshold_backward(dy, y, 0.0)
@@ -148,13 +151,13 @@ class _PointwiseFn(torch.autograd.Function):
                 ops.linear_ex(dy, w2, None, 0, dy.numel() // Cout, 0, Cout, Cin, y=dx, transw=True,
                               mask=x if ctx.in_relu else None, pre=y, pre_out=dz)
             if ctx.in_relu:
-                _MASKED.add((dx.data_ptr(), x.data_ptr()))
+                _MASKED[(dx.data_ptr(), x.data_ptr())] = dx._version
             dy = dz
         elif ctx.needs_input_grad[0]:
             # dy W (rows) / W^T dy (cf); with in_relu the producer's ReLU backward is folded in
             dx = ops.linear_fwd(dy, w2, None, channels_first=cf, transw=True, mask=x if ctx.in_relu else None)
             if ctx.in_relu:
-                _MASKED.add((dx.data_ptr(), x.data_ptr()))
+                _MASKED[(dx.data_ptr(), x.data_ptr())] = dx._version
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             if _side_owns(ctx.param, ctx.bias):
                 _SIDE.launch(x, dy, ctx.param, ctx.bias, channels_first=cf)

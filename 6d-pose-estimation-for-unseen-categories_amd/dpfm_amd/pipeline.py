@@ -20,7 +20,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import ops
+from . import _lib, ops
 from .dataset.object import CropFormation, Crops, FrameBatch
 from .dataset.synthetic import cad_points, lbo_operators, make_frame
 from .models.dpfm import DPFMNet
@@ -420,6 +420,43 @@ class GraphedTrainStep:
         return self.log
 
 
+_MASKED_STREAMS = {}
+
+
+def cu_split_streams(side_cus: int, device=None):
+    """(main, side) torch streams over disjoint CU sets (pk_stream_create_cu_mask): `side_cus` CUs
+    spread evenly over the device's CU index range for crop formation, the rest for the training
+    (or inference) step, so the two never share a CU. Cached per (device, side_cus); the HIP
+    streams live for the process."""
+    import ctypes
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    key = (str(dev), int(side_cus))
+    if key in _MASKED_STREAMS:
+        return _MASKED_STREAMS[key]
+    n = ctypes.c_int(0)
+    with torch.cuda.device(dev):
+        _lib.call("pk_device_cu_count", ctypes.byref(n))
+        ncu = int(n.value)
+        if not 0 < side_cus < ncu:
+            raise ValueError(f"side_cus must be in (0, {ncu})")
+        words = (ncu + 31) // 32
+        side_set = {min(ncu - 1, int((i + 0.5) * ncu / side_cus)) for i in range(side_cus)}
+        masks = []
+        for sel in (lambda c: c not in side_set, lambda c: c in side_set):
+            m = (ctypes.c_uint32 * words)()
+            for c in range(ncu):
+                if sel(c):
+                    m[c // 32] |= 1 << (c % 32)
+            masks.append(m)
+        out = []
+        for m in masks:
+            h = ctypes.c_void_p()
+            _lib.call("pk_stream_create_cu_mask", m, words, ctypes.byref(h))
+            out.append(torch.cuda.ExternalStream(h.value, device=dev))
+    _MASKED_STREAMS[key] = tuple(out)
+    return _MASKED_STREAMS[key]
+
+
 class PipelinedTrainer:
     """Crop formation of batch i+1 overlapped with the training step on batch i.
 
@@ -442,6 +479,10 @@ class PipelinedTrainer:
         # crop-formation stream priority (development knob PK_SIDE_PRIORITY: torch's stream
         # priorities, lower number = higher priority; default 0, the main stream's)
         self.side = torch.cuda.Stream(priority=int(os.environ.get("PK_SIDE_PRIORITY", "0")))
+        side_cus = int(os.environ.get("PK_SIDE_CUS", "0"))
+        if side_cus > 0:  # disjoint CU sets for the two streams (cu_split_streams)
+            self.main, self.side = cu_split_streams(side_cus)
+            self.main.wait_stream(torch.cuda.current_stream())
         side = torch.cuda.Stream()
         side.wait_stream(self.main)
         with torch.cuda.stream(side):  # warm-up outside capture
@@ -621,6 +662,10 @@ class PipelinedInfer:
                  warmup: int = 2):
         self.main = torch.cuda.current_stream()
         self.side = torch.cuda.Stream()
+        side_cus = int(os.environ.get("PK_SIDE_CUS", "0"))
+        if side_cus > 0:  # disjoint CU sets for the two streams (cu_split_streams)
+            self.main, self.side = cu_split_streams(side_cus)
+            self.main.wait_stream(torch.cuda.current_stream())
         tmp = torch.cuda.Stream()
         tmp.wait_stream(self.main)
         with torch.cuda.stream(tmp):

@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="crops per GPU (configs[1]: 32)")
     ap.add_argument("--points", type=int, default=1024)
+    ap.add_argument("--ragged", action="store_true",
+                    help="train / infer at the reference's real sizes: ragged crops of ~200-2000 points (the "
+                         "object.py:145-148 sample policy), ~5000-vertex CADs, collate padding to 2000")
+    ap.add_argument("--cad-points", type=int, default=5000, help="--ragged: CAD vertices")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-crops", type=int, default=30, help="bounded CPU-baseline sample (crops)")
     ap.add_argument("--pose-crops", type=int, default=8,
@@ -56,7 +60,8 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="graph mode without overlapping crop formation of the next batch")
     ap.add_argument("--probe-steps", type=int, default=2, help="eager steps after timing for the kernel breakdown")
-    ap.add_argument("--mode", choices=("train", "infer", "corr4096", "icp", "teaser", "operators"), default="train",
+    ap.add_argument("--mode", choices=("train", "infer", "corr4096", "icp", "teaser", "operators", "ransac_ref"),
+                    default="train",
                     help="train: the headline fwd+bwd step (default); infer: configs[1]/[3] inference; "
                          "corr4096: configs[4] feature distance + RANSAC; icp: the (f4) ICP refinement; "
                          "teaser: the (f2) TEASER++ solver; operators: the (f1) spectral operators")
@@ -67,6 +72,7 @@ def parse():
     ap.add_argument("--icp-target", choices=("gt_cad", "crop"), default="gt_cad",
                     help="icp: the reference's target (CAD under T_gt) or the observed crop")
     ap.add_argument("--hypotheses", type=int, default=1024, help="RANSAC hypotheses per crop (infer/corr4096)")
+    ap.add_argument("--ransac-crops", type=int, default=1, help="ransac_ref: crops per step")
     ap.add_argument("--fd-precision", choices=("fp32", "bf16", "bf16x3"), default="fp32",
                     help="corr4096: feature-distance contraction precision (fp32 = the parity path)")
     return ap.parse_args()
@@ -384,6 +390,26 @@ def setup_dist(gpus: int = 0):
 POSE_CHECK = {}  # mode -> the post-timing pose-vs-reference check (cpu_baseline leg)
 
 
+def ragged_setup(B: int, n1: int, rank: int, dev):
+    """The reference's real sizes: frames whose masks give ~200-2000-point crops under
+    the sample policy (CropFormation(npoint=0), padded to the policy maximum 2000 so the step is
+    graph-capturable), CADs of ~n1 vertices, and the cached-operator stand-ins of those sizes
+    (operators_for reads the crop sizes once, at setup: the reference computes them offline)."""
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.dataset.synthetic import ragged_frames
+    from dpfm_amd.pipeline import frame_batch, operators_for
+    frames = ragged_frames(B, 1000 * rank + 77, n1=n1)
+    fb = frame_batch(frames, dev)
+    crops_of = CropFormation(npoint=0, seed=rank, pad="fixed", base=rank * B)
+    c0 = crops_of(fb)
+    counts = c0.n2.cpu().tolist()
+    op = operators_for([f["cad"] for f in frames], counts, fb.diam, 1000 * rank, dev, ld2=c0.ld)
+    cads = [len(f["cad"]) for f in frames]
+    sizes = {"crop_min": int(min(counts)), "crop_max": int(max(counts)), "crop_mean": round(float(np.mean(counts)), 1),
+             "cad_min": min(cads), "cad_max": max(cads), "cad_mean": round(float(np.mean(cads)), 1)}
+    return fb, op, crops_of, sizes
+
+
 def build_train(args, dev, rank, world):
     """configs[1] shape (configs[2] semantics for N > 1): one training step per iteration."""
     from dpfm_amd.dataset.object import CropFormation
@@ -392,8 +418,11 @@ def build_train(args, dev, rank, world):
     B, N = args.batch, args.points
     torch.manual_seed(1234)  # identical initial weights on every rank (DDP broadcast semantics)
     model = DPFMNet().to(dev)
-    fb, op = make_frame_batch(B, N, N, seed=1000 * rank, device=dev)
-    crops_of = CropFormation(n1=N, npoint=N, seed=rank)
+    if args.ragged:
+        fb, op, crops_of, sizes = ragged_setup(B, args.cad_points, rank, dev)
+    else:
+        fb, op = make_frame_batch(B, N, N, seed=1000 * rank, device=dev)
+        crops_of = CropFormation(n1=N, npoint=N, seed=rank)
     step = TrainStep(model, seed=rank, capturable=not args.eager)
     if args.eager:
         one_step = lambda: step(op, crops_of(fb))  # noqa: E731
@@ -412,6 +441,11 @@ def build_train(args, dev, rank, world):
               "global_batch": B * world, "points_per_crop": N, "cad_points": N,
               "precision": "model fp32 (f32 MFMA); crop geometry / C_gt normal equations fp64",
               "parallelism": f"dp{world}"}
+    if args.ragged:
+        config.update(workload=f"reference sizes: B={B} synthetic 640x480 RGB-D frames/GPU, ragged crops "
+                               f"{sizes['crop_min']}-{sizes['crop_max']} pts (sample policy, collate padding to 2000), "
+                               f"CADs {sizes['cad_min']}-{sizes['cad_max']} vertices, training step fwd+bwd",
+                      points_per_crop=sizes["crop_mean"], cad_points=sizes["cad_mean"])
     probe = lambda: step(op, crops_of(fb))  # noqa: E731
 
     def pose_check(n_sample):  # the metric's "pose err vs ref" on the trained weights (after timing)
@@ -433,8 +467,11 @@ def build_infer(args, dev, rank, world):
     B, N = args.batch, args.points
     torch.manual_seed(1234)
     model = DPFMNet().to(dev).eval()
-    fb, op = make_frame_batch(B, N, N, seed=1000 * rank, device=dev)
-    crops_of = CropFormation(n1=N, npoint=N, seed=0, base=rank * B)
+    if args.ragged:
+        fb, op, crops_of, sizes = ragged_setup(B, args.cad_points, rank, dev)
+    else:
+        fb, op = make_frame_batch(B, N, N, seed=1000 * rank, device=dev)
+        crops_of = CropFormation(n1=N, npoint=N, seed=0, base=rank * B)
     infer = InferStep(model, hypotheses=args.hypotheses, seed=0, icp_evaluations=args.icp_evals)
     if args.eager:
         one_step = lambda: infer(fb, op, crops_of(fb))  # noqa: E731
@@ -452,6 +489,12 @@ def build_infer(args, dev, rank, world):
                                                        "hip-graph, crop formation overlapped"),
               "global_batch": B * world, "points_per_crop": N, "cad_points": N, "hypotheses": args.hypotheses,
               "precision": "model fp32 (f32 MFMA); crop geometry / RANSAC fp64", "parallelism": f"shard{world}"}
+    if args.ragged:
+        config.update(workload=f"reference sizes: B={B} synthetic 640x480 RGB-D frames/GPU, ragged crops "
+                               f"{sizes['crop_min']}-{sizes['crop_max']} pts (collate padding to 2000), CADs "
+                               f"{sizes['cad_min']}-{sizes['cad_max']} vertices, inference + RANSAC "
+                               f"{args.hypotheses} hypotheses", points_per_crop=sizes["crop_mean"],
+                      cad_points=sizes["cad_mean"])
     probe = lambda: infer(fb, op, crops_of(fb))  # noqa: E731
     return one_step, probe, INFER_METRIC, B, config
 
@@ -539,6 +582,66 @@ def icp_workload(B: int, rank: int, target: str):
         tgts.append(np.ascontiguousarray(tgt))
         T0s.append(D @ Tg)
     return srcs, tgts, T0s
+
+
+RANSAC_REF_METRIC = ("reference pose-stage solves/sec (test_RANSAC.py:288-310: 4x10^6 RANSAC hypotheses per "
+                     "crop over ~760 correspondences, ~5000-vertex CAD)")
+
+
+def build_ransac_ref(args, dev, rank, world):
+    """The reference's own pose workload (test_RANSAC.py:308, call at :400): per crop 4 x 10^6
+    hypotheses (RANSACConvergenceCriteria(4000000, 80000): confidence clamps to 1, so every
+    hypothesis runs) over the spatially filtered correspondences (n ~ 450-770 on its real crops)
+    with a ~5000-vertex CAD. Synthetic: n = 760 correspondences, 40 % inliers, B = --batch crops
+    per step (default 1 here: one crop's solve per step)."""
+    from dpfm_amd import ops
+    from dpfm_amd.dataset.synthetic import random_rotation
+    H = args.hypotheses if args.hypotheses != 1024 else 4_000_000
+    B, V1, n = max(1, args.ransac_crops), args.cad_points, 760
+    rng = np.random.default_rng(7000 + rank)
+    cads, pcs, cors = [], [], []
+    for b in range(B):
+        cad = rng.normal(size=(V1, 3)) * 6
+        R = random_rotation(rng)
+        gen = rng.integers(0, V1, n)
+        pc = (cad[gen] + rng.normal(size=(n, 3)) * 0.01) @ R.T + np.array([2.0, -1.0, 90.0])
+        src = rng.integers(0, V1, n)
+        good = rng.random(n) < 0.4
+        src[good] = gen[good]
+        cads.append(cad)
+        pcs.append(pc)
+        cors.append(np.stack([src, np.arange(n)], 1))
+    cad_t = torch.from_numpy(np.concatenate(cads)).to(dev)
+    pc_t = torch.from_numpy(np.concatenate(pcs)).to(dev)
+    cad_off = ops.packed_offsets([V1] * B, dev)
+    pc_off = ops.packed_offsets([n] * B, dev)
+    corres = torch.from_numpy(np.concatenate(cors).astype(np.int32)).to(dev)
+    cor_off = ops.packed_offsets([n] * B, dev)
+
+    def solve():
+        T, st = ops.ransac(cad_t, cad_off, pc_t, pc_off, corres, cor_off, H, seed=0, nmax=n)
+        return {"T": T, "stats": st}
+
+    one_step = solve
+    if not args.eager:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            solve()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = solve()
+
+        def one_step():
+            g.replay()
+            return out
+    config = {"workload": f"reference pose stage: {B} crop(s) x {H} RANSAC hypotheses x {n} correspondences "
+                          f"(40 % inliers), {V1}-vertex CAD, fp64 Umeyama/Horn fit + scoring",
+              "execution": "eager" if args.eager else "hip-graph", "global_batch": B * world, "hypotheses": H,
+              "correspondences": n, "cad_points": V1, "precision": "fp64", "parallelism": f"shard{world}"}
+    return one_step, solve, RANSAC_REF_METRIC, B, config
 
 
 def build_icp(args, dev, rank, world):
@@ -729,6 +832,7 @@ def main():
     world, rank, dev = setup_dist(args.gpus)
     from dpfm_amd import _lib
     build = {"train": build_train, "infer": build_infer, "corr4096": build_corr, "icp": build_icp,
+             "ransac_ref": build_ransac_ref,
              "teaser": build_teaser, "operators": build_operators}[args.mode]
     one_step, probe_step, metric, units, config = build(args, dev, rank, world)
 
@@ -808,7 +912,7 @@ def main():
             "metric": metric,
             "value": round(units * world / elapsed * args.steps, 3),
             "unit": {"corr4096": "solves/s", "icp": "refinements/s", "teaser": "solves/s",
-                     "operators": "operator sets/s"}.get(args.mode, "crops/s"),
+                     "operators": "operator sets/s", "ransac_ref": "solves/s"}.get(args.mode, "crops/s"),
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(total_ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -825,9 +929,11 @@ def main():
             "kernels": kernels,
         }
         out.update(extra)
-        if "pk_ransac" in kern and args.mode in ("infer", "corr4096"):
+        if "pk_ransac" in kern and args.mode in ("infer", "corr4096", "ransac_ref"):
             rk = kern["pk_ransac"]
             crops_per_launch = 1 if args.mode == "corr4096" else units
+            if args.mode == "ransac_ref":
+                args.hypotheses = config["hypotheses"]
             r64 = roofline_for("pk_ransac", rk)
             out["ransac"] = {"hypotheses_per_s": round(args.hypotheses * crops_per_launch / (rk["avg_ms"] * 1e-3), 1),
                              "ms_per_launch": round(rk["avg_ms"], 4), "hypotheses_per_launch":
@@ -835,13 +941,16 @@ def main():
                              "valu64_frac": r64["frac"]}
         if args.mode == "train" and not args.no_roofline_probe and world == 1:
             out["roofline_ball_query"] = ball_query_roofline(dev)
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and not args.ragged:
             if args.mode == "train":
                 out["cpu_baseline"] = cpu_baseline(args.cpu_crops, args.points, args.points)
                 if "fn" in POSE_CHECK and args.pose_crops > 0:
                     out["pose_err"] = POSE_CHECK["fn"](args.pose_crops)
             elif args.mode == "corr4096":
                 out["cpu_baseline"] = cpu_ransac_baseline(args.hypotheses)
+            elif args.mode == "ransac_ref":
+                out["cpu_baseline"] = cpu_ransac_baseline(config["hypotheses"], V=args.cad_points, n=760,
+                                                          sample_h=200_000)
             elif args.mode == "icp":
                 out["cpu_baseline"] = cpu_icp_baseline(32, args.icp_target)
             elif args.mode == "teaser":
@@ -857,7 +966,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_ransac_baseline(H: int, V: int = 4096, sample_h: int = 0) -> dict:
+def cpu_ransac_baseline(H: int, V: int = 4096, sample_h: int = 0, n: int = 0) -> dict:
     """configs[4]'s pose stage on the host: the C/OpenMP restatement of Open3D 0.17's
     RegistrationRANSACBasedOnCorrespondence loop (oracle/c/oracle.c oc_ransac_o3d: per
     hypothesis a 4-point Umeyama, the WHOLE source cloud transformed as Open3D's loop does, the
@@ -876,18 +985,19 @@ def cpu_ransac_baseline(H: int, V: int = 4096, sample_h: int = 0) -> dict:
     cad = np.ascontiguousarray(rng.normal(size=(V, 3)) * 6)
     R = random_rotation(rng)
     pc = np.ascontiguousarray((cad[rng.permutation(V)] + rng.normal(size=(V, 3)) * 0.02) @ R.T + np.array([2.0, -1.0, 90.0]))
-    corres = np.ascontiguousarray(np.stack([rng.integers(0, V, V), np.arange(V)], 1).astype(np.int32))
+    n = n or V
+    corres = np.ascontiguousarray(np.stack([rng.integers(0, V, n), np.arange(n)], 1).astype(np.int32))
     T, st = np.zeros(16), np.zeros(3)
     cp = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
     h = sample_h or H
-    lib.oc_ransac_o3d(cp(cad), V, cp(pc), cp(corres), V, None, 0, 64, 0.05, cp(T), cp(st))  # warm-up
+    lib.oc_ransac_o3d(cp(cad), V, cp(pc), cp(corres), n, None, 0, 64, 0.05, cp(T), cp(st))  # warm-up
     t0 = time.perf_counter()
-    lib.oc_ransac_o3d(cp(cad), V, cp(pc), cp(corres), V, None, 0, h, 0.05, cp(T), cp(st))
+    lib.oc_ransac_o3d(cp(cad), V, cp(pc), cp(corres), n, None, 0, h, 0.05, cp(T), cp(st))
     dt = time.perf_counter() - t0
     import platform
     return {"value": round(1.0 / (dt * H / h), 4), "unit": "solves/s (RANSAC stage only, H = %d)" % H,
             "cores": threads, "kind": "port",
-            "sample": f"{h} hypotheses x {V} correspondences, {V}-vertex source transformed per hypothesis "
+            "sample": f"{h} hypotheses x {n} correspondences, {V}-vertex source transformed per hypothesis "
                       f"(Open3D's loop), C/OpenMP on {platform.processor() or 'host'}",
             "seconds": round(dt, 3),
             "reference_4e6_hypotheses_s_extrapolated": round(dt * 4e6 / h, 1)}

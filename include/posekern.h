@@ -550,6 +550,18 @@ int pk_dgemm_tn(const double* X, const double* Y, int B, int n, int m, double* G
 int pk_dpotrf(double* A, int B, int n, double tau, int32_t* fail, void* stream);
 int pk_dpotrs(const double* L, double* X, int B, int n, int m, void* stream);
 
+/* Runtime helpers of the pipelined executors (host only; no reference counterpart: the reference
+ * overlaps crop formation with training through DataLoader worker PROCESSES, train.py /
+ * dataset/object.py:117-274; here the overlap is two HIP streams on one device).
+ *   pk_device_cu_count        the current device's CU count
+ *   pk_stream_create_cu_mask  a stream restricted to the CUs of mask (bit i of word i/32 = CU i;
+ *                             hipExtStreamCreateWithCUMask), released by pk_stream_destroy
+ *   pk_stream_get_cu_mask     the mask a stream runs with */
+int pk_device_cu_count(int* out);
+int pk_stream_create_cu_mask(const uint32_t* mask, int words, void** stream);
+int pk_stream_get_cu_mask(void* stream, int words, uint32_t* mask);
+int pk_stream_destroy(void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -220,7 +220,7 @@ def nce_loss(f1, f2, pairs, selected, t=0.07):
     q = f1[pairs[selected][:, 0]]
     kk = f2[pairs[selected][:, 1]]
     logits = -torch.cdist(q, kk) / t
-    return F.cross_entropy(logits, torch.arange(selected.shape[0]))
+    return F.cross_entropy(logits, torch.arange(selected.shape[0], device=logits.device))
 
 
 def dpfm_loss(C, C_gt, pairs, sel, f1, f2, o12, o21, g12, g21, w_fmap=1.0, w_acc=1.0, w_nce=1.0, t=0.07):

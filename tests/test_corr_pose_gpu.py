@@ -230,3 +230,16 @@ def test_cgt_rank_deficient_and_empty(device):
         scale = max(float(exp.abs().max()), 1e-30)
         torch.testing.assert_close(got[b], exp, rtol=1e-3, atol=1e-4 * scale)
     assert torch.equal(got[2], torch.zeros(30, 30))
+
+
+@pytest.mark.parametrize("C", [8, 30, 45])
+def test_naive_nn_query_any_width(device, C):
+    """naive.py:23-34 nn_query for any feature width (the reference takes [V, C]): argmin of
+    torch.cdist, exact except near-ties within 1e-5 of the largest distance."""
+    from dpfm_amd.fmap2pointmap_solvers.naive import nn_query
+    g = torch.Generator().manual_seed(C)
+    fx, fy = torch.randn(700, C, generator=g), torch.randn(500, C, generator=g)
+    got = nn_query(fx.to(device), fy.to(device)).cpu()
+    d = torch.cdist(fx.double(), fy.double())
+    picked = d.gather(0, got[None])[0]
+    assert (picked - d.min(0).values).abs().max().item() <= 1e-5 * d.max().item()

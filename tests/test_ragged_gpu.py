@@ -260,3 +260,38 @@ def test_infer_step_on_real_crops(device):
     assert (ncorr >= 0).all() and (ncorr <= 5 * np.asarray(n2)).all()
     ir = res["ir"].cpu().numpy()
     assert ((ir >= 0) & (ir <= 1)).all()
+
+
+def test_cgt_real_crops_full_rank(device):
+    """C_from_sparse_P (utils/utils.py:67-79) on the pair lists of the reference's own crops
+    (find_positives on tests/golden/real_crops.npz: 5000-vertex CADs, 200-2000-point crops) with
+    operator stand-ins of the true sizes: full-rank systems, where the reference's GPU `gels` and
+    the CPU drivers agree, so this is the pinned case of pk_cgt_lstsq (the rank-deficient
+    min-norm path is a documented deviation). fp32 device result within 1e-4 of the fp64 oracle's
+    scale."""
+    from dpfm_amd import ops
+    from dpfm_amd.pipeline import lbo_padded
+    crops = _real()
+    B = len(crops)
+    n1 = [c["cad"].shape[0] for c in crops]
+    n2 = [c["pc"].shape[0] for c in crops]
+    plist = []
+    for c in crops:
+        align = O.transform(c["pc"], c["R"], c["t"], inv=True)
+        plist.append(torch.from_numpy(O.find_positives(c["cad"], align, r=c["diam"] * 0.05)))
+    cap = max(p.shape[0] for p in plist)
+    pairs = torch.zeros((B, cap, 2), dtype=torch.int64)
+    for b, p in enumerate(plist):
+        pairs[b, :p.shape[0]] = p
+    e1 = torch.zeros((B, max(n1), 64))
+    e2 = torch.zeros((B, max(n2), 64))
+    for b in range(B):
+        e1[b, :n1[b]] = torch.from_numpy(lbo_padded(n1[b], 2 * b)[2])
+        e2[b, :n2[b]] = torch.from_numpy(lbo_padded(n2[b], 2 * b + 1)[2])
+    got = ops.cgt_lstsq(pairs.to(device), torch.tensor([p.shape[0] for p in plist], device=device), e1.to(device),
+                        e2.to(device)).cpu().double()
+    for b, p in enumerate(plist):
+        assert len(set(p[:, 1].tolist())) >= 30  # full rank: at least 30 distinct crop rows
+        exp = M.C_from_sparse_P(p, e1[b, :n1[b], :30].double(), e2[b, :n2[b], :30].double())
+        scale = float(exp.abs().max())
+        assert (got[b] - exp).abs().max().item() <= 1e-4 * scale, (b, (got[b] - exp).abs().max().item(), scale)
