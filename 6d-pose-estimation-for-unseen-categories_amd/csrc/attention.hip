@@ -87,7 +87,7 @@ __device__ __forceinline__ void store_tile(const Tile& t, float* __restrict__ dr
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__ q,
                                                        const float* __restrict__ k,
                                                        const float* __restrict__ v, int H, int N,
-                                                       int M, float* __restrict__ out,
+                                                       int M, int64_t sbk, int64_t sbv, float* __restrict__ out,
                                                        float* __restrict__ lse) {
   __shared__ float Ks[kD * kSR];
   __shared__ float Vs[kT * kSC];
@@ -96,8 +96,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
   const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
   const int qi = lb.x * kT + pk::wave_id() * 16 + c;
   const float* qb = q + ((int64_t)b * kD * H + h) * N;
-  const float* kb = k + ((int64_t)b * kD * H + h) * M;
-  const float* vb = v + ((int64_t)b * kD * H + h) * M;
+  const float* kb = k + (int64_t)b * sbk + (int64_t)h * M;
+  const float* vb = v + (int64_t)b * sbv + (int64_t)h * M;
   float qr[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) qr[s] = qi < N ? qb[(int64_t)(4 * s + g) * H * N + qi] * kScale : 0.f;
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
     const float* __restrict__ o, const float* __restrict__ dout, const float* __restrict__ lse,
-    int H, int N, int M, float* __restrict__ delta, float* __restrict__ dq) {
+    int H, int N, int M, int64_t sbk, int64_t sbv, float* __restrict__ delta, float* __restrict__ dq) {
   __shared__ float Ks[kD * kSR];
   __shared__ float Vs[kD * kSR];
   __shared__ float KT[kT * kSC];
@@ -195,8 +195,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
   const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
   const int qi = lb.x * kT + pk::wave_id() * 16 + c;
   const int64_t qoff = ((int64_t)b * kD * H + h) * N;
-  const float* kb = k + ((int64_t)b * kD * H + h) * M;
-  const float* vb = v + ((int64_t)b * kD * H + h) * M;
+  const float* kb = k + (int64_t)b * sbk + (int64_t)h * M;
+  const float* vb = v + (int64_t)b * sbv + (int64_t)h * M;
   float qr[4], dor[4];
   float dl = 0.f;
 #pragma unroll
@@ -264,7 +264,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
     const float* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
-    int H, int N, int M, float* __restrict__ dk, float* __restrict__ dv) {
+    int H, int N, int M, int64_t sbk, int64_t sbv, int64_t sbdk, int64_t sbdv, float* __restrict__ dk,
+    float* __restrict__ dv) {
   __shared__ float Qs[kD * kSR];
   __shared__ float Os[kD * kSR];  // dO as [d][q]
   __shared__ float QT[kT * kSC];
@@ -276,7 +277,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
   const int h = xb.y, b = xb.z;
   const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
   const int kj = xb.x * kT + pk::wave_id() * 16 + c;
-  const int64_t koff = ((int64_t)b * kD * H + h) * M;
   const float* qb = q + ((int64_t)b * kD * H + h) * N;
   const float* gb = dout + ((int64_t)b * kD * H + h) * N;
   const float2* lb = reinterpret_cast<const float2*>(lse) + ((int64_t)b * H + h) * N;
@@ -284,9 +284,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
   float kr[4], vr[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int64_t a = koff + (int64_t)(4 * s + g) * H * M + kj;
-    kr[s] = kj < M ? k[a] * kScale : 0.f;
-    vr[s] = kj < M ? v[a] : 0.f;
+    const int64_t a = (int64_t)h * M + (int64_t)(4 * s + g) * H * M + kj;
+    kr[s] = kj < M ? k[(int64_t)b * sbk + a] * kScale : 0.f;
+    vr[s] = kj < M ? v[(int64_t)b * sbv + a] : 0.f;
   }
   // two independent chains (even / odd 16-query sub-tiles; accuracy, see the forward): four
   // would cost this kernel its third wave per SIMD
@@ -348,9 +348,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
   if (kj < M) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t a = koff + (int64_t)(4 * g + r) * H * M + kj;
-      dk[a] = dks[r] * kScale;
-      dv[a] = dvs[r];
+      const int64_t a = (int64_t)h * M + (int64_t)(4 * g + r) * H * M + kj;
+      dk[(int64_t)b * sbdk + a] = dks[r] * kScale;
+      dv[(int64_t)b * sbdv + a] = dvs[r];
     }
   }
 }
@@ -358,28 +358,33 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
 }  // namespace
 
 extern "C" int pk_attention_fwd(const float* q, const float* k, const float* v, int B, int D, int H,
-                                int N, int M, float* out, float* lse, void* stream) {
-  PK_REQUIRE(B >= 0 && H > 0 && N >= 0 && M >= 0 && D == kD);
+                                int N, int M, int64_t sbk, int64_t sbv, float* out, float* lse, void* stream) {
+  PK_REQUIRE(B >= 0 && H > 0 && N >= 0 && M >= 0 && D == kD && sbk >= 0 && sbv >= 0);
   if (B == 0 || N == 0) return PK_OK;
   PK_REQUIRE(M > 0 && q && k && v && out && lse);
+  const int64_t dense = (int64_t)kD * H * M;
   hipLaunchKernelGGL(attn_fwd_kernel, dim3((N + kT - 1) / kT, H, B), dim3(256), 0, pk::as_stream(stream),
-                     q, k, v, H, N, M, out, lse);
+                     q, k, v, H, N, M, sbk ? sbk : dense, sbv ? sbv : dense, out, lse);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
 
 extern "C" int pk_attention_bwd(const float* q, const float* k, const float* v, const float* out,
                                 const float* dout, const float* lse, int B, int D, int H, int N,
-                                int M, float* delta, float* dq, float* dk, float* dv, void* stream) {
-  PK_REQUIRE(B >= 0 && H > 0 && N >= 0 && M >= 0 && D == kD);
+                                int M, int64_t sbk, int64_t sbv, float* delta, float* dq, float* dk, float* dv,
+                                int64_t sbdk, int64_t sbdv, void* stream) {
+  PK_REQUIRE(B >= 0 && H > 0 && N >= 0 && M >= 0 && D == kD && sbk >= 0 && sbv >= 0 && sbdk >= 0 && sbdv >= 0);
   if (B == 0 || N == 0 || M == 0) return PK_OK;
   PK_REQUIRE(q && k && v && out && dout && lse && delta && dq && dk && dv);
   hipStream_t s = pk::as_stream(stream);
+  const int64_t dense = (int64_t)kD * H * M;
+  sbk = sbk ? sbk : dense;
+  sbv = sbv ? sbv : dense;
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((N + kT - 1) / kT, H, B), dim3(256), 0, s, q, k, v, out, dout,
-                     lse, H, N, M, delta, dq);
+                     lse, H, N, M, sbk, sbv, delta, dq);
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(attn_bwd_dkv_kernel, dim3((M + kT - 1) / kT, H, B), dim3(256), 0, s, q, k, v, dout, lse,
-                     delta, H, N, M, dk, dv);
+                     delta, H, N, M, sbk, sbv, sbdk ? sbdk : dense, sbdv ? sbdv : dense, dk, dv);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -14,6 +14,7 @@
 #include "common.hpp"
 #include "../../include/posekern.h"
 
+#include <cstdlib>
 #include <vector>
 
 namespace {
@@ -172,7 +173,7 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 
 template <int LAYOUT>
 __device__ __forceinline__ void load8(const float* __restrict__ p, int C, int c, int N, int64_t rb, int64_t r1,
-                                      int h, float (&v)[8]) {
+                                      int h, float (&v)[8], int64_t sb) {
   if (LAYOUT == 0) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -180,10 +181,10 @@ __device__ __forceinline__ void load8(const float* __restrict__ p, int C, int c,
       v[s] = (c < C && r < r1) ? p[r * C + c] : 0.f;
     }
   } else {
-    if (c < C) {
+    if (c < C) {  // batch stride sb (0: dense C N)
       const int64_t b = rb / N;
       const int64_t n = rb - b * N + 8 * h;
-      const float4* q = reinterpret_cast<const float4*>(p + (b * C + c) * N + n);
+      const float4* q = reinterpret_cast<const float4*>(p + b * (sb ? sb : (int64_t)C * N) + (int64_t)c * N + n);
       const float4 u = q[0], w = q[1];
       v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
       v[4] = w.x; v[5] = w.y; v[6] = w.z; v[7] = w.w;
@@ -203,14 +204,14 @@ struct WgradBatch {
 template <int LAYOUT, int J>
 __device__ __forceinline__ void wgrad_load(WgradBatch<J>& B, const float* __restrict__ x, const float* __restrict__ dy,
                                            int I, int O, int N, int Ti, int T, int tw, int WT, int m, int h,
-                                           int64_t rb, int64_t r1) {
+                                           int64_t rb, int64_t r1, int64_t sbx, int64_t sbdy) {
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int t = tw + WT * j;
     if (t < T) {
       const int to = t / Ti, ti = t - to * Ti;
-      load8<LAYOUT>(dy, O, to * 32 + m, N, rb, r1, h, B.a[j]);
-      load8<LAYOUT>(x, I, ti * 32 + m, N, rb, r1, h, B.b[j]);
+      load8<LAYOUT>(dy, O, to * 32 + m, N, rb, r1, h, B.a[j], sbdy);
+      load8<LAYOUT>(x, I, ti * 32 + m, N, rb, r1, h, B.b[j], sbx);
     }
   }
 }
@@ -243,7 +244,7 @@ template <int LAYOUT, int J>
 __device__ __forceinline__ void wgrad_v2_body(const float* __restrict__ x, const float* __restrict__ dy, int64_t R,
                                               int I, int O, int N, int SL, float* __restrict__ part,
                                               float* __restrict__ partb, int s, float (*comb)[16 * 64],
-                                              float (*combb)[64]) {
+                                              float (*combb)[64], int64_t sbx, int64_t sbdy) {
   const int lane = pk::lane_id(), w = pk::wave_id();
   const int m = lane & 31, h = lane >> 5;
   const int To = (O + 31) >> 5, Ti = (I + 31) >> 5, T = To * Ti;
@@ -265,13 +266,14 @@ __device__ __forceinline__ void wgrad_v2_body(const float* __restrict__ x, const
   if (active) {
     WgradBatch<J> b0, b1;
     int q = g;
-    if (q < nb) wgrad_load<LAYOUT, J>(b0, x, dy, I, O, N, Ti, T, tw, WT, m, h, r0 + 16ll * q, r1);
+    if (q < nb) wgrad_load<LAYOUT, J>(b0, x, dy, I, O, N, Ti, T, tw, WT, m, h, r0 + 16ll * q, r1, sbx, sbdy);
     for (; q < nb; q += 2 * WR) {
       const bool has1 = q + WR < nb;
-      if (has1) wgrad_load<LAYOUT, J>(b1, x, dy, I, O, N, Ti, T, tw, WT, m, h, r0 + 16ll * (q + WR), r1);
+      if (has1) wgrad_load<LAYOUT, J>(b1, x, dy, I, O, N, Ti, T, tw, WT, m, h, r0 + 16ll * (q + WR), r1, sbx, sbdy);
       wgrad_mma<J>(b0, acc, bs, Ti, T, tw, WT);
       if (has1) {
-        if (q + 2 * WR < nb) wgrad_load<LAYOUT, J>(b0, x, dy, I, O, N, Ti, T, tw, WT, m, h, r0 + 16ll * (q + 2 * WR), r1);
+        if (q + 2 * WR < nb)
+          wgrad_load<LAYOUT, J>(b0, x, dy, I, O, N, Ti, T, tw, WT, m, h, r0 + 16ll * (q + 2 * WR), r1, sbx, sbdy);
         wgrad_mma<J>(b1, acc, bs, Ti, T, tw, WT);
       }
     }
@@ -321,7 +323,7 @@ __global__ __launch_bounds__(64 * kV2Waves) void wgrad_v2_kernel(const float* __
                                                                  float* __restrict__ partb) {
   __shared__ float comb[kV2Waves][16 * 64];
   __shared__ float combb[kV2Waves][64];
-  wgrad_v2_body<LAYOUT, J>(x, dy, R, I, O, N, SL, part, partb, blockIdx.x, comb, combb);
+  wgrad_v2_body<LAYOUT, J>(x, dy, R, I, O, N, SL, part, partb, blockIdx.x, comb, combb, 0, 0);
 }
 
 // ---------------------------------------------------------------------------------
@@ -340,6 +342,7 @@ struct WgradProblem {
   float* part;   // S * O * I weight partials, then S * O bias partials
   int64_t R;
   int I, O, N, layout, SL, S, blk0, pad;
+  int64_t sbx, sbdy;  // channels-first batch strides (0: dense)
 };
 struct WgradProblems {
   int G;
@@ -355,8 +358,8 @@ __global__ __launch_bounds__(64 * kV2Waves) void wgrad_grouped_kernel(const Wgra
   const WgradProblem& P = tab.p[g];
   const int s = b - P.blk0;
   float* partb = P.part + (int64_t)P.S * P.O * P.I;
-  if (P.layout == 0) wgrad_v2_body<0, 1>(P.x, P.dy, P.R, P.I, P.O, P.N, P.SL, P.part, partb, s, comb, combb);
-  else wgrad_v2_body<1, 1>(P.x, P.dy, P.R, P.I, P.O, P.N, P.SL, P.part, partb, s, comb, combb);
+  if (P.layout == 0) wgrad_v2_body<0, 1>(P.x, P.dy, P.R, P.I, P.O, P.N, P.SL, P.part, partb, s, comb, combb, 0, 0);
+  else wgrad_v2_body<1, 1>(P.x, P.dy, P.R, P.I, P.O, P.N, P.SL, P.part, partb, s, comb, combb, P.sbx, P.sbdy);
 }
 
 struct WgradOut {
@@ -515,6 +518,7 @@ constexpr int kLfMaxC = 128;
 #define PK_ROWS_BLOCKS 4096
 #endif
 constexpr int kRowsMaxBlocks = PK_ROWS_BLOCKS;
+constexpr int kRowsPersistCUs = 256;  // persistent rows grid: 2 blocks per CU of MI355X
 
 // ReLU backward folded into an input-gradient epilogue: mask = the forward output of the layer
 // whose gradient this is (aten threshold_backward(grad, mask, 0): mask <= 0 -> 0)
@@ -542,6 +546,11 @@ struct LinEpi {
   int N;
   const float* pre;  // thin kernels: input x scaled by pre (1 - pre) first (sigmoid backward)
   float* pre_out;    // ... and that scaled input written here (same indexing as x)
+  const float* add2;  // channels-first kernels: a second added operand (every output), batch stride sa2
+  int64_t sa2;
+  const float* w2;    // stacked weight rows >= wsplit (lr_stage), and bias entries >= wsplit from bias2
+  const float* bias2;
+  int wsplit;
 };
 
 __device__ __forceinline__ float lin_act(int act, float v) {
@@ -672,8 +681,13 @@ __device__ __forceinline__ void lr_load(const float* __restrict__ x, int64_t sx,
 
 // Weight staging shared by the MFMA per-point kernels: Ws[o][k] (o < 16 TO, zero rows past
 // Cout; row stride 16 Q + 4), from W [Cout, 16 Q] or, with transw, from W^T's [16 Q, Cout].
+// w2 / wsplit: stored weight rows >= wsplit come from w2 (row - wsplit) — two layers' weights
+// stacked without a concatenation kernel (transw = 0: rows = outputs; transw = 1: rows = the
+// stored [Cin, Cout] tensor's rows); w2 == nullptr: every row from w.
 template <int Q, int TO>
-__device__ __forceinline__ void lr_stage(const float* __restrict__ w, int Cout, int transw, float* Ws) {
+__device__ __forceinline__ void lr_stage(const float* w, int Cout, int transw, float* Ws, const float* w2,
+                                         int wsplit) {  // callers without a second weight pass w2 = w
+                                                        // (arithmetic on a null w2 crashed clang-22's inliner)
   constexpr int CI = 16 * Q, ST = CI + 4;
   if (!transw) {  // W [Cout, CI] rows: float4 reads, all issued before the LDS writes
     constexpr int NV = TO * 16 * CI / 4, PER = (NV + 255) / 256;
@@ -681,7 +695,8 @@ __device__ __forceinline__ void lr_stage(const float* __restrict__ w, int Cout, 
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int e = threadIdx.x + 256 * i, o = e / (CI / 4);
-      v[i] = (e < NV && o < Cout) ? *reinterpret_cast<const f32x4*>(w + 4 * (int64_t)e) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* src = o < wsplit ? w + 4 * (int64_t)e : w2 + 4 * (int64_t)(e - wsplit * (CI / 4));
+      v[i] = (e < NV && o < Cout) ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -694,7 +709,8 @@ __device__ __forceinline__ void lr_stage(const float* __restrict__ w, int Cout, 
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int e = threadIdx.x + 256 * i, k = e / (TO * 16), o = e - k * (TO * 16);
-      v[i] = (e < NE && o < Cout) ? w[(int64_t)k * Cout + o] : 0.f;
+      const float* src = k < wsplit ? w + (int64_t)k * Cout + o : w2 + (int64_t)(k - wsplit) * Cout + o;
+      v[i] = (e < NE && o < Cout) ? *src : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -704,7 +720,10 @@ __device__ __forceinline__ void lr_stage(const float* __restrict__ w, int Cout, 
   }
 }
 
-template <int Q, int TO, bool GEN>  // Cin = 16 Q, Cout <= 16 TO; GEN: mask / add / split / cf epilogue
+// VAR (development variants, pkdev_linear_rows_var): 0 production; 1 no MFMAs (acc = operand sums:
+// the load / store floor); 2 no stores unless the result is NaN (the load + MFMA floor); 3 no
+// scheduling barriers (the compiler may hoist every weight read)
+template <int Q, int TO, bool GEN, int VAR = 0>  // Cin = 16 Q, Cout <= 16 TO; GEN: mask / add / split / cf epilogue
 __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __restrict__ x, int64_t sx,
                                                               const float* __restrict__ w,
                                                               const float* __restrict__ bias, int64_t R, int Cin,
@@ -717,7 +736,7 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
   // the first tile's operands are in flight while the weight is staged
   f32x4 cur[Q], nxt[Q];
   lr_load<Q>(x, sx, tile < T ? tile * 16 + m : R, R, g, cur);
-  lr_stage<Q, TO>(w, Cout, transw, Ws);
+  lr_stage<Q, TO>(w, Cout, transw, Ws, w, 1 << 30);
   __syncthreads();
   if (tile >= T) return;
   constexpr int TH = TO < 4 ? TO : 4, NH = TO / TH;
@@ -734,7 +753,7 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
     // operands): acc / wv / epilogue operands stay at TH tiles, so TO = 8 keeps 4 waves per SIMD
 #pragma unroll
     for (int hh = 0; hh < NH; ++hh) {
-    __builtin_amdgcn_sched_barrier(0);  // one output group's registers live at a time
+    if (VAR != 3) __builtin_amdgcn_sched_barrier(0);  // one output group's registers live at a time
     // D[point 4 g + r][out t * 16 + m]; the epilogue's operand loads (mask, add) for all
     // TH x 4 outputs are issued before this group's MFMAs (their latency hides behind them),
     // not one dependent load per store
@@ -787,9 +806,11 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int t = 0; t < TH; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[q][i], wv[t][i], acc[t], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);  // keep the weight reads per chunk (no hoisting of all Q x TH)
+          for (int t = 0; t < TH; ++t) {
+            if (VAR == 1) acc[t][i] += cur[q][i] + wv[t][i];
+            else acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[q][i], wv[t][i], acc[t], 0, 0, 0);
+          }
+        if (VAR != 3) __builtin_amdgcn_sched_barrier(0);  // keep the weight reads per chunk (no hoisting of all Q x TH)
       }
     }
 #pragma unroll
@@ -798,7 +819,7 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t pr = tile * 16 + 4 * g + r;
-        if (pr < R && o < Cout) {
+        if (pr < R && o < Cout && (VAR != 2 || acc[t][r] != acc[t][r])) {
           float v = lin_act(e.relu, acc[t][r] + bv[hh * TH + t]);
           v = mk[t][r] <= 0.f ? 0.f : v;  // relu_mask
           v += ad[t][r];  // 0 without add / past add_cols
@@ -818,6 +839,143 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
     tile = tn;
 #pragma unroll
     for (int q = 0; q < Q; ++q) cur[q] = nxt[q];
+  }
+}
+
+// Rows layout, LDS-staged full-line variant (the production rows path). Round 3's PMC passes
+// (profiles/r03_lin_pmc_summary.txt) and the no-MFMA / no-store variants (r03_lin_var.txt) showed
+// linear_fwd_rows_kernel bound by its memory access shapes, not the MFMA: fragment-shaped x loads
+// (16 rows x 64 B per instruction) and 4-B scalar stores. Here:
+//   * each wave stages its 16-row x tile with LANE-LINEAR 16-B loads (64 lanes cover whole 128-B
+//     lines of consecutive rows) into a wave-private LDS tile (XOR-swizzled 16-B chunks: the
+//     fragment reads are conflict-free), the next tile's loads in flight (registers) while the
+//     current tile's MFMAs run;
+//   * the MFMA operands are swapped (A = weight, B = points): D holds 4 CONSECUTIVE outputs of one
+//     point per lane, so the results, the mask and the residual move as 16-B vectors;
+//   * tiles are walked grid-stride by a persistent grid (2 blocks of 4 waves per CU).
+// Same epilogue semantics as linear_fwd_rows_kernel (LinEpi); Cout % 4 == 0 for the vector paths.
+template <int Q, int TO, bool GEN>
+__global__ __launch_bounds__(256, 2) void linear_rows_lds_kernel(const float* __restrict__ x, int64_t sx,
+                                                                 const float* __restrict__ w,
+                                                                 const float* __restrict__ bias, int64_t R, int Cin,
+                                                                 int Cout, int transw, LinEpi e) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int CI = 16 * Q, ST = CI + 4;
+  constexpr int CH = CI / 4;               // 16-B chunks per point row
+  constexpr int SWZ = CH >= 16 ? 15 : CH - 1;
+  constexpr int PF = CH / 4;               // 16-B loads per lane per tile (16 rows x CH chunks / 64 lanes)
+  float* Ws = lds;                                           // [16 TO][ST]
+  const int wave = pk::wave_id(), lane = pk::lane_id(), m = lane & 15, g = lane >> 4;
+  f32x4* Xs = reinterpret_cast<f32x4*>(lds + 16 * TO * ST) + wave * (16 * CH);  // this wave's [16][CH] tile
+  const int64_t T = (R + 15) >> 4, stride = (int64_t)gridDim.x * 4;
+  int64_t tile = (int64_t)blockIdx.x * 4 + wave;
+  f32x4 pf[PF];
+  auto load_tile = [&](int64_t tt) {  // lane-linear: flat chunk f = lane + 64 j -> (row f / CH, chunk f % CH)
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int f = lane + 64 * j, row = f / CH, c = f - row * CH;
+      const int64_t r = tt * 16 + row;
+      pf[j] = r < R ? *reinterpret_cast<const f32x4*>(x + r * sx + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto write_tile = [&]() {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int f = lane + 64 * j, row = f / CH, c = f - row * CH;
+      Xs[row * CH + (c ^ (row & SWZ))] = pf[j];
+    }
+  };
+  if (tile < T) load_tile(tile);
+  lr_stage<Q, TO>(w, Cout, transw, Ws, w, 1 << 30);
+  __syncthreads();
+  if (tile >= T) return;
+  write_tile();
+  int64_t tn = tile + stride;
+  if (tn < T) load_tile(tn);
+  constexpr int TH = TO < 4 ? TO : 4, NH = TO / TH;
+  const bool vec = (Cout & 3) == 0;
+  for (;;) {
+#pragma unroll
+    for (int hh = 0; hh < NH; ++hh) {
+      f32x4 acc[TH];
+#pragma unroll
+      for (int t = 0; t < TH; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const f32x4 xf = Xs[m * CH + ((4 * q + g) ^ (m & SWZ))];  // B: x[point m][16 q + 4 g + i]
+        f32x4 wv[TH];
+#pragma unroll
+        for (int t = 0; t < TH; ++t)
+          wv[t] = *reinterpret_cast<const f32x4*>(&Ws[((hh * TH + t) * 16 + m) * ST + 16 * q + 4 * g]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int t = 0; t < TH; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[t][i], xf[i], acc[t], 0, 0, 0);
+      }
+      // D[out (hh TH + t) 16 + 4 g + r][point m]: lane (m, g) holds 4 consecutive outputs of point m
+      const int64_t pr = tile * 16 + m;
+      if (pr < R) {
+#pragma unroll
+        for (int t = 0; t < TH; ++t) {
+          const int o0 = (hh * TH + t) * 16 + 4 * g;
+          if (o0 >= Cout) continue;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int o = o0 + r;
+            const float bo = (bias != nullptr && o < Cout) ? bias[o] : 0.f;
+            v[r] = lin_act(e.relu, acc[t][r] + bo);
+          }
+          if (GEN && e.mask != nullptr) {
+            if (vec) {
+              const f32x4 mk = *reinterpret_cast<const f32x4*>(e.mask + pr * Cout + o0);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = mk[r] <= 0.f ? 0.f : v[r];
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (o0 + r < Cout && e.mask[pr * Cout + o0 + r] <= 0.f) v[r] = 0.f;
+            }
+          }
+          if (GEN && e.add != nullptr && o0 < e.add_cols) {
+            if (o0 + 3 < e.add_cols && ((e.sa & 3) == 0)) {
+              const f32x4 ad = *reinterpret_cast<const f32x4*>(e.add + pr * e.sa + o0);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] += ad[r];
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (o0 + r < e.add_cols) v[r] += e.add[pr * e.sa + o0 + r];
+            }
+          }
+          if (GEN && e.store_cf) {
+            const int64_t b = pr / e.N, n = pr - b * e.N;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (o0 + r < Cout) e.y[b * e.sy + (int64_t)(o0 + r) * e.N + n] = v[r];
+          } else if (GEN && o0 >= e.split) {
+            float* dst = e.y2 + pr * e.sy2 + (o0 - e.split);
+            if (vec && (e.sy2 & 3) == 0) *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
+            else
+#pragma unroll
+              for (int r = 0; r < 4; ++r) if (o0 + r < Cout) dst[r] = v[r];
+          } else {
+            float* dst = e.y + pr * e.sy + o0;
+            if (vec && (e.sy & 3) == 0 && o0 + 3 < (GEN ? e.split : Cout)) *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
+            else
+#pragma unroll
+              for (int r = 0; r < 4; ++r) if (o0 + r < Cout) dst[r] = v[r];
+          }
+        }
+      }
+    }
+    if (tn >= T) break;
+    tile = tn;
+    // this wave's fragment reads of the finished tile precede these writes (in-order LDS per wave)
+    __builtin_amdgcn_sched_barrier(0);
+    write_tile();
+    tn = tile + stride;
+    if (tn < T) load_tile(tn);
   }
 }
 
@@ -856,7 +1014,7 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
 #pragma unroll
       for (int i = 0; i < 4; ++i) xv[q][i] = *reinterpret_cast<const V*>(xb + (int64_t)(16 * q + 4 * g + i) * N);
   }
-  lr_stage<Q, TO>(w, Cout, transw, Ws);
+  lr_stage<Q, TO>(w, Cout, transw, Ws, e.w2 ? e.w2 : w, e.w2 ? e.wsplit : (1 << 30));
   __syncthreads();
   if (tile >= T) return;
   f32x4 acc[TO][SUB];
@@ -896,7 +1054,8 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
       const int o = t * 16 + 4 * g + r;
       bo4[t][r] = 0.f;
       if (bias != nullptr) {
-        const float b = bias[o < Cout ? o : 0];
+        const int oc = o < Cout ? o : 0;
+        const float b = (e.bias2 != nullptr && oc >= e.wsplit) ? e.bias2[oc - e.wsplit] : bias[oc];
         bo4[t][r] = o < Cout ? b : 0.f;
       }
     }
@@ -918,6 +1077,16 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
         av[t][r] = *reinterpret_cast<const V*>(e.add + bb * e.sa + (int64_t)(o < e.add_cols ? o : 0) * N + pn);
       }
   }
+  V a2v[TO][4];
+  if (e.add2 != nullptr) {
+#pragma unroll
+    for (int t = 0; t < TO; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = t * 16 + 4 * g + r;
+        a2v[t][r] = *reinterpret_cast<const V*>(e.add2 + bb * e.sa2 + (int64_t)(o < Cout ? o : 0) * N + pn);
+      }
+  }
 #pragma unroll
   for (int t = 0; t < TO; ++t)
 #pragma unroll
@@ -937,6 +1106,9 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
           }
           if (has_add) {
             if constexpr (SUB == 1) z += av[t][r]; else z += av[t][r][u];
+          }
+          if (e.add2 != nullptr) {  // (z + add) + add2: the order of autograd's two accumulations
+            if constexpr (SUB == 1) z += a2v[t][r]; else z += a2v[t][r][u];
           }
           if constexpr (SUB == 1) v = z; else v[u] = z;
         }
@@ -1107,6 +1279,17 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
   e.N = N;
   e.pre = a->pre;
   e.pre_out = a->pre_out;
+  e.add2 = a->add2;
+  e.sa2 = a->lda2 ? a->lda2 : (int64_t)Cout * N;
+  e.w2 = a->w2;
+  e.bias2 = a->bias2;
+  e.wsplit = a->w2 ? a->wsplit : (1 << 30);
+  // stacked weights and the second add operand: channels-first MFMA kernel only
+  PK_REQUIRE((a->w2 == nullptr && a->add2 == nullptr && a->bias2 == nullptr) ||
+             (layout == 1 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128) && N % 16 == 0 &&
+              Cin > 4 && Cout > 4 && !a->store_cf && a->y2 == nullptr));
+  PK_REQUIRE(a->w2 == nullptr || (a->wsplit > 0 && a->wsplit < (a->transw ? Cin : Cout)));
+  PK_REQUIRE(a->bias2 == nullptr || (a->w2 != nullptr && !a->transw));
   const float* x = a->x;
   const float* w = a->w;
   const float* bias = a->bias;
@@ -1151,6 +1334,29 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
     };
     // plain: no mask, no residual add, one contiguous output (split == Cout)
     const bool plain = e.mask == nullptr && e.add == nullptr && e.y2 == nullptr && !e.store_cf && e.split >= Cout;
+    // development switch (read once): PK_ROWS_LDS=1 takes the LDS-staged full-line kernel; measured
+    // within +-15 % of the fragment-load kernel shape by shape (profiles/r03_lin_bench_lds_vs_r2.txt),
+    // so round 2's kernel stays the default
+    static const bool rows_lds = getenv("PK_ROWS_LDS") != nullptr;
+    if (rows_lds && Cin >= 32) {  // LDS-staged full-line kernel (linear_rows_lds_kernel)
+      auto pickl = [&](auto q, auto gen) {
+        constexpr int Qv = decltype(q)::value;
+        constexpr bool G = decltype(gen)::value;
+        return TO == 1 ? linear_rows_lds_kernel<Qv, 1, G>
+               : TO == 2 ? linear_rows_lds_kernel<Qv, 2, G>
+               : TO == 4 ? linear_rows_lds_kernel<Qv, 4, G> : linear_rows_lds_kernel<Qv, 8, G>;
+      };
+      auto pickql = [&](auto gen) {
+        return Cin == 32 ? pickl(std::integral_constant<int, 2>{}, gen)
+               : Cin == 64 ? pickl(std::integral_constant<int, 4>{}, gen) : pickl(std::integral_constant<int, 8>{}, gen);
+      };
+      auto kl = plain ? pickql(std::integral_constant<bool, false>{}) : pickql(std::integral_constant<bool, true>{});
+      const size_t ldsl = sizeof(float) * ((size_t)(16 * TO) * (Cin + 4) + 4 * (size_t)16 * Cin);
+      const unsigned bl = (unsigned)std::min<int64_t>((tiles + 3) / 4, (int64_t)(2 * kRowsPersistCUs));
+      hipLaunchKernelGGL(kl, dim3(bl), dim3(256), ldsl, st, x, sx, w, bias, R, Cin, Cout, transw, e);
+      PK_CHECK_LAUNCH();
+      return PK_OK;
+    }
     auto kern = plain ? pickq(std::integral_constant<bool, false>{}) : pickq(std::integral_constant<bool, true>{});
     const size_t lds = sizeof(float) * (size_t)(16 * TO) * (Cin + 4);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, st, x, sx, w, bias, R, Cin, Cout, transw, e);
@@ -1164,7 +1370,7 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
     sub = std::min(sub, 256 / Cin);
     while (N % (16 * sub)) sub >>= 1;
     // vector loads / stores of SUB points need SUB-aligned batch strides
-    while (sub > 1 && ((sx % sub) || (e.sy % sub) || (e.add && (e.sa % sub)))) sub >>= 1;
+    while (sub > 1 && ((sx % sub) || (e.sy % sub) || (e.add && (e.sa % sub)) || (e.add2 && (e.sa2 % sub)))) sub >>= 1;
     const int TO = Cout <= 16 ? 1 : Cout <= 32 ? 2 : Cout <= 64 ? 4 : 8;
     auto pick = [&](auto q, auto u) {
       constexpr int Q = decltype(q)::value, U = decltype(u)::value;
@@ -1197,6 +1403,99 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
   else
     hipLaunchKernelGGL(linear_fwd_kernel<1>, dim3(blocks), dim3(256), lds, st, x, w, bias, R, N, Cin, Cout, transw,
                        e.relu, e.mask, e.y);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+// Weight-stationary rows kernel (development, pkdev_linear_rows_var var = 4 / 5): the wave's
+// whole weight fragment lives in VGPRs (lane (m, g): W[16 t + m][16 q + 4 g + i], TO x Q float4s),
+// copied once from the block's LDS stage, so the MFMA loop reads no LDS; tiles of 16 rows are
+// walked grid-stride with the next tile's operands in flight. WPS = minimum waves per SIMD.
+template <int Q, int TO, int WPS>
+__global__ __launch_bounds__(256, WPS) void linear_ws_rows_kernel(const float* __restrict__ x, int64_t sx,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ bias, int64_t R,
+                                                                  int Cout, float* __restrict__ y, int64_t sy) {
+  extern __shared__ float Ws[];
+  constexpr int CI = 16 * Q, ST = CI + 4;
+  const int lane = pk::lane_id(), m = lane & 15, g = lane >> 4;
+  const int64_t T = (R + 15) >> 4, stride = (int64_t)gridDim.x * 4;
+  int64_t tile = (int64_t)blockIdx.x * 4 + pk::wave_id();
+  f32x4 cur[Q], nxt[Q];
+  lr_load<Q>(x, sx, tile < T ? tile * 16 + m : R, R, g, cur);
+  lr_stage<Q, TO>(w, Cout, 0, Ws, w, 1 << 30);
+  __syncthreads();
+  if (tile >= T) return;
+  f32x4 wf[TO][Q];
+#pragma unroll
+  for (int t = 0; t < TO; ++t)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) wf[t][q] = *reinterpret_cast<const f32x4*>(&Ws[(t * 16 + m) * ST + 16 * q + 4 * g]);
+  float bv[TO];
+#pragma unroll
+  for (int t = 0; t < TO; ++t) {
+    const int o = t * 16 + m;
+    bv[t] = (bias != nullptr && o < Cout) ? bias[o] : 0.f;
+  }
+  for (;;) {
+    const int64_t tn = tile + stride;
+    if (tn < T) lr_load<Q>(x, sx, tn * 16 + m, R, g, nxt);
+    f32x4 acc[TO];
+#pragma unroll
+    for (int t = 0; t < TO; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < TO; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[q][i], wf[t][q][i], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < TO; ++t) {
+      const int o = t * 16 + m;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t pr = tile * 16 + 4 * g + r;
+        if (pr < R && o < Cout) y[pr * sy + o] = fmaxf(acc[t][r] + bv[t], 0.f);
+      }
+    }
+    if (tn >= T) break;
+    tile = tn;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) cur[q] = nxt[q];
+  }
+}
+
+// Development hook (not in include/posekern.h): the plain rows kernel (no epilogue operands) of
+// y = x W^T + b with Cin = 16 Q in {64, 128}, Cout = 64, in variant `var` (see the kernel), at
+// `blocks` workgroups (0: the production grid), for tools/lin_var.py.
+extern "C" int pkdev_linear_rows_var(const float* x, const float* w, const float* bias, int64_t R, int Cin,
+                                     float* y, int var, int blocks, void* stream) {
+  if (!(Cin == 64 || Cin == 128) || R <= 0 || var < 0 || var > 5) return PK_ERR_ARG;
+  LinEpi e{};
+  e.y = y;
+  e.sy = 64;
+  e.split = 64;
+  const int64_t tiles = (R + 15) / 16;
+  const unsigned nb = blocks > 0 ? (unsigned)blocks : (unsigned)std::min<int64_t>((tiles + 3) / 4, (int64_t)kRowsMaxBlocks);
+  const size_t lds = sizeof(float) * (size_t)64 * (Cin + 4);
+  hipStream_t st = pk::as_stream(stream);
+#define PK_VAR(QQ, V) hipLaunchKernelGGL((linear_fwd_rows_kernel<QQ, 4, false, V>), dim3(nb), dim3(256), lds, st, x, \
+                                         (int64_t)Cin, w, bias, R, Cin, 64, 0, e)
+#define PK_WS(QQ, W) hipLaunchKernelGGL((linear_ws_rows_kernel<QQ, 4, W>), dim3(nb), dim3(256), lds, st, x, (int64_t)Cin, \
+                                        w, bias, R, 64, y, (int64_t)64)
+  if (var >= 4) {  // weight-stationary: 2 (var 4) or 1 (var 5) waves per SIMD at least
+    if (Cin == 64) {
+      if (var == 4) PK_WS(4, 2); else PK_WS(4, 1);
+    } else {
+      if (var == 4) PK_WS(8, 2); else PK_WS(8, 1);
+    }
+  } else if (Cin == 64) {
+    if (var == 0) PK_VAR(4, 0); else if (var == 1) PK_VAR(4, 1); else if (var == 2) PK_VAR(4, 2); else PK_VAR(4, 3);
+  } else {
+    if (var == 0) PK_VAR(8, 0); else if (var == 1) PK_VAR(8, 1); else if (var == 2) PK_VAR(8, 2); else PK_VAR(8, 3);
+  }
+#undef PK_VAR
+#undef PK_WS
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
@@ -1244,6 +1543,8 @@ extern "C" int pk_linear_wgrad_grouped(const pk_wgrad_call* calls, int n, float*
     PK_REQUIRE(k.dw && k.R >= 0 && k.I > 0 && k.O > 0 && k.I <= kMaxC && k.O <= kMaxC);
     PK_REQUIRE(((k.O + 31) / 32) * ((k.I + 31) / 32) <= kV2Waves);  // one 32x32 tile per wave
     PK_REQUIRE(k.layout == 0 || (k.layout == 1 && k.N > 0 && k.N % 16 == 0));
+    PK_REQUIRE((k.sx == 0 && k.sdy == 0) || (k.layout == 1 && k.sx >= 0 && k.sdy >= 0 && k.sx % 4 == 0 &&
+                                               k.sdy % 4 == 0));
     PK_REQUIRE(k.R == 0 || (k.x && k.dy));
     if (k.accumulate) {
       int f = -1;
@@ -1280,7 +1581,8 @@ extern "C" int pk_linear_wgrad_grouped(const pk_wgrad_call* calls, int n, float*
     const pk_wgrad_call& k = calls[c];
     if (S[c] == 0) continue;
     WgradProblem& P = tp.p[tp.G++];
-    P = WgradProblem{k.x, k.dy, work + off[c], k.R, k.I, k.O, k.N, k.layout, (int)SLv[c], (int)S[c], blocks, 0};
+    P = WgradProblem{k.x, k.dy, work + off[c], k.R, k.I, k.O, k.N, k.layout, (int)SLv[c], (int)S[c], blocks, 0,
+                     k.sx, k.sdy};
     blocks += (int)S[c];
     if (tp.G == kGroupMax) {
       const int rc = flush_p();

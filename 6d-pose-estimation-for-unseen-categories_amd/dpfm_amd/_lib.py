@@ -30,7 +30,9 @@ class LinearArgs(ctypes.Structure):
                 ("R", _I64), ("Cin", ctypes.c_int32), ("Cout", ctypes.c_int32), ("transw", ctypes.c_int32),
                 ("act", ctypes.c_int32), ("mask", _P), ("ldx", _I64), ("y", _P), ("ldy", _I64), ("y2", _P),
                 ("ldy2", _I64), ("split", ctypes.c_int32), ("store_cf", ctypes.c_int32), ("add", _P), ("lda", _I64),
-                ("add_cols", ctypes.c_int32), ("pad", ctypes.c_int32), ("pre", _P), ("pre_out", _P)]
+                ("add_cols", ctypes.c_int32), ("pad", ctypes.c_int32), ("pre", _P), ("pre_out", _P),
+                ("w2", _P), ("bias2", _P), ("wsplit", ctypes.c_int32), ("pad2", ctypes.c_int32), ("add2", _P),
+                ("lda2", _I64)]
 
 
 # name -> argtypes, mirroring include/posekern.h one for one.
@@ -53,8 +55,8 @@ SIGNATURES = {
     "pk_fmap_head_bwd": [_P, _P, _P, _P, _P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "pk_fmap_solve": [_P, _P, _P, _F, _I, _I, _P, _P],
     "pk_fmap_solve_backward": [_P, _P, _P, _F, _I, _I, _P, _P, _P, _P],
-    "pk_attention_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P],
-    "pk_attention_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "pk_attention_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I64, _I64, _P, _P, _P],
+    "pk_attention_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _P],
     "pk_linear_wgrad": [_P, _P, _I, _I64, _I, _I, _I, _P, _P, _P, _I, _P],
     "pk_linear_wgrad_grouped_work": [_P, _I],
     "pk_linear_wgrad_grouped": [_P, _I, _P, _I64, _P],
@@ -117,7 +119,7 @@ class WgradCall(ctypes.Structure):
     """pk_wgrad_call (include/posekern.h)."""
     _fields_ = [("x", _P), ("dy", _P), ("dw", _P), ("db", _P), ("R", _I64), ("I", ctypes.c_int32),
                 ("O", ctypes.c_int32), ("N", ctypes.c_int32), ("layout", ctypes.c_int32),
-                ("accumulate", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("accumulate", ctypes.c_int32), ("pad", ctypes.c_int32), ("sx", _I64), ("sdy", _I64)]
 
 
 class TeaserParams(ctypes.Structure):

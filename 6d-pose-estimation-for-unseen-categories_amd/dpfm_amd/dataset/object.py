@@ -157,6 +157,9 @@ class Crops:
     kept: torch.Tensor       # int64 [F] points after outlier removal
     pair_cap: int = 0
     overflow_flag: Optional[torch.Tensor] = None  # 0-d bool formed with the crops (see overflow)
+    # f32 [F, k, k] ground-truth functional map (utils/utils.py:67-79) when the producer formed it
+    # beside the crops (PipelinedTrainer: on the crop-formation stream); None: the step solves it
+    C_gt: Optional[torch.Tensor] = None
 
     def overflow(self) -> torch.Tensor:
         """0-d bool on the device: some crop had more ball-query pairs than pair_cap (its P

@@ -167,6 +167,53 @@ class _PointwiseFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, None
 
 
+class _PointwiseResidualFn(torch.autograd.Function):
+    """y = W x + b + res for a channels-first [B, C, N] layer (the residual add of
+    modeling/dpfm.py:101-103, desc = desc + layer(...), folded into the layer's epilogue:
+    pk_linear_ex `add`). Backward: dres = dy, the input gradient and the grouped weight
+    gradients as _PointwiseFn's."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, res, in_relu):
+        w2 = weight.view(weight.shape[0], -1)
+        Cout, Cin = w2.shape
+        Bn, _, N = x.shape
+        y = torch.empty((Bn, Cout, N), dtype=x.dtype, device=x.device)
+        ops.linear_ex(x, w2, bias, 1, Bn * N, N, Cin, Cout, y=y, add=res, add_cols=Cout)
+        ctx.param, ctx.bias, ctx.has_bias = weight, bias, bias is not None
+        ctx.in_relu = FOLD_RELU and in_relu
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        w2 = weight.view(weight.shape[0], -1)
+        dy = dy.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = ops.linear_fwd(dy, w2, None, channels_first=True, transw=True, mask=x if ctx.in_relu else None)
+            if ctx.in_relu:
+                _MASKED[(dx.data_ptr(), x.data_ptr())] = dx._version
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            if _side_owns(ctx.param, ctx.bias):
+                _SIDE.launch(x, dy, ctx.param, ctx.bias, channels_first=True)
+            else:
+                dw, db = ops.linear_wgrad(x, dy, channels_first=True, want_bias=ctx.has_bias)
+                dw = dw.view(weight.shape)
+        return dx, dw, db, dy if ctx.needs_input_grad[3] else None, None
+
+
+def pointwise_residual(layer: "Conv1d", x: torch.Tensor, res: torch.Tensor) -> torch.Tensor:
+    """res + layer(x) for a Conv1d(k=1) layer on channels-first [B, C, N] tensors in one launch
+    (falls back to the two-step form for other storage orders)."""
+    if (x.is_cuda and x.dim() == 3 and x.is_contiguous() and res.is_contiguous() and res.shape[1] == layer.out_channels
+            and res.shape[0] == x.shape[0] and res.shape[2] == x.shape[2] and res.dtype == x.dtype
+            and x.shape[2] % 16 == 0 and layer.in_channels in (16, 32, 64, 128)):  # the cf MFMA kernel's range
+        return _PointwiseResidualFn.apply(x, layer.weight, layer.bias, res, getattr(x, "_pk_relu_out", False))
+    return res + layer(x)
+
+
 def _pointwise(x, weight, bias, sem_cf: bool, out_cf: Optional[bool] = None, relu: bool = False,
                sigmoid: bool = False):
     """Apply the layer to x of semantic layout sem_cf (False: [..., C]; True: [B, C, N]).

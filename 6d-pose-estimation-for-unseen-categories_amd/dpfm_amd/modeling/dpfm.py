@@ -17,7 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ..layers import Conv1d, Linear
+from ..layers import Conv1d, Linear, pointwise_residual
 from ..dpfm_utils import get_mask_batched
 
 
@@ -31,6 +31,9 @@ class InstanceNormReLU(nn.InstanceNorm1d):
         if self.affine or self.track_running_stats:
             raise ValueError("the reference's InstanceNorm1d is affine=False, track_running_stats=False")
         return ops.instnorm_relu(x, self.eps)
+
+
+FUSED_ATTN_PROP = True  # AttentionalPropagation + residual as one fused node (attnprop.py)
 
 
 def MLP(channels: list, do_bn=True):
@@ -81,6 +84,19 @@ class AttentionalPropagation(nn.Module):
         message = self.attn(x, source, source)
         return self.mlp(torch.cat([x, message], dim=1))
 
+    def forward_residual(self, x, source):
+        """x + forward(x, source) (modeling/dpfm.py:101-103's residual update): one fused autograd
+        node (attnprop.attn_prop_residual) where the shapes allow, else the module path with the
+        add folded into the MLP's last layer (layers.pointwise_residual)."""
+        if FUSED_ATTN_PROP:
+            from ..attnprop import attn_prop_residual
+            y = attn_prop_residual(self, x, source)
+            if y is not None:
+                return y
+        message = self.attn(x, source, source)
+        h = self.mlp[:-1](torch.cat([x, message], dim=1))
+        return pointwise_residual(self.mlp[-1], h, x)
+
 
 class CrossAttentionRefinementNet(nn.Module):
     def __init__(self, n_in=128, num_head=4, gnn_dim=512, overlap_feat_dim=32, n_layers=2,
@@ -109,8 +125,8 @@ class CrossAttentionRefinementNet(nn.Module):
     def forward(self, coords0, coords1, features_x, features_y, batch=None):
         desc0, desc1 = self.first_lin(features_x).transpose(1, 2), self.first_lin(features_y).transpose(1, 2)
         for layer in self.layers:
-            desc0 = desc0 + layer(desc0, desc1)
-            desc1 = desc1 + layer(desc1, desc0)
+            desc0 = layer.forward_residual(desc0, desc1)
+            desc1 = layer.forward_residual(desc1, desc0)  # with the updated desc0 (:101-103)
         ax = self.last_lin(desc0.transpose(1, 2))
         ay = self.last_lin(desc1.transpose(1, 2))
         if ax.shape[-1] == self.n_in:  # "normal" attention: the whole width (no slice, whose

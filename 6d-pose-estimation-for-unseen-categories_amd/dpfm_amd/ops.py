@@ -388,8 +388,8 @@ class _Attention(torch.autograd.Function):
         M = k.shape[3]
         out = torch.empty_like(q)
         lse = torch.empty((B, H, N, 2), dtype=torch.float32, device=q.device)  # (row max, 1/sum)
-        call("pk_attention_fwd", ptr(q), ptr(k), ptr(v), B, D, H, N, M, ptr(out), ptr(lse), _lib.stream(q.device),
-             work=("mfma", 2 * 2 * N * M * D * B * H))  # S = Q K^T, O = P V
+        call("pk_attention_fwd", ptr(q), ptr(k), ptr(v), B, D, H, N, M, 0, 0, ptr(out), ptr(lse),
+             _lib.stream(q.device), work=("mfma", 2 * 2 * N * M * D * B * H))  # S = Q K^T, O = P V
         ctx.save_for_backward(q, k, v, out, lse)
         return out
 
@@ -401,8 +401,8 @@ class _Attention(torch.autograd.Function):
         M = k.shape[3]
         delta = torch.empty((B, H, N), dtype=torch.float32, device=q.device)
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-        call("pk_attention_bwd", ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse), B, D, H, N, M, ptr(delta),
-             ptr(dq), ptr(dk), ptr(dv), _lib.stream(q.device),
+        call("pk_attention_bwd", ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse), B, D, H, N, M, 0, 0,
+             ptr(delta), ptr(dq), ptr(dk), ptr(dv), 0, 0, _lib.stream(q.device),
              work=("mfma", 7 * 2 * N * M * D * B * H))  # S, dP, dQ | S, dP, dV, dK
         return dq, dk, dv
 
@@ -461,7 +461,15 @@ def linear_wgrad_grouped(calls) -> None:
     flops = 0
     keep = []
     for k, (x, dy, cf, dw, db, acc) in enumerate(calls):
-        x, dy = x.contiguous(), dy.contiguous()
+        sx = sdy = 0
+        if cf and x.dim() == 3 and x.stride(2) == 1 and x.stride(1) == x.shape[2] and x.stride(0) % 4 == 0:
+            sx = x.stride(0)  # a channel slice of a wider channels-first buffer: read in place
+        else:
+            x = x.contiguous()
+        if cf and dy.dim() == 3 and dy.stride(2) == 1 and dy.stride(1) == dy.shape[2] and dy.stride(0) % 4 == 0:
+            sdy = dy.stride(0)
+        else:
+            dy = dy.contiguous()
         keep += [x, dy]
         if cf:
             Bn, I, N = x.shape
@@ -471,8 +479,8 @@ def linear_wgrad_grouped(calls) -> None:
             R, N, layout = x.numel() // I, 0, 0
         if dw.numel() != O * I or not dw.is_contiguous() or (db is not None and (db.numel() != O or not db.is_contiguous())):
             raise _lib.PoseKernError("linear_wgrad_grouped: output buffers must be contiguous [O, I] / [O]")
-        arr[k] = _lib.WgradCall(ptr(x).value, ptr(dy).value, ptr(dw).value, ptr(db).value if db is not None else None,
-                                int(R), I, O, int(N), layout, int(bool(acc)), 0)
+        arr[k] = _lib.WgradCall(_dp(x), _dp(dy), ptr(dw).value, ptr(db).value if db is not None else None,
+                                int(R), I, O, int(N), layout, int(bool(acc)), 0, int(sx), int(sdy))
         flops += 2 * int(R) * I * O
     n_work = _lib.lib().pk_linear_wgrad_grouped_work(arr, len(calls))
     if n_work < 0:
@@ -697,7 +705,8 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], c
         raise _lib.PoseKernError("linear_fwd: mask must be contiguous and shaped like the output")
     call("pk_linear_fwd", ptr(x), ptr(w), ptr(bias), layout, int(R), int(N), int(Cin), int(Cout), int(transw),
          int(relu), ptr(mask), ptr(y), _lib.stream(x.device),
-         work=("hbm", 4 * int(R) * (Cin + Cout) + 4 * Cin * Cout, 2 * int(R) * Cin * Cout))
+         work=("hbm", 4 * int(R) * (Cin + Cout + (Cout if mask is not None else 0)) + 4 * Cin * Cout,
+               2 * int(R) * Cin * Cout))
     return y
 
 
@@ -715,7 +724,9 @@ def linear_ex(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], la
               relu: bool = False, mask: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None,
               split: int = 0, ldy2: int = 0, store_cf: bool = False, add: Optional[torch.Tensor] = None,
               lda: int = 0, add_cols: int = 0, act: Optional[int] = None, pre: Optional[torch.Tensor] = None,
-              pre_out: Optional[torch.Tensor] = None) -> None:
+              pre_out: Optional[torch.Tensor] = None, w2: Optional[torch.Tensor] = None,
+              bias2: Optional[torch.Tensor] = None, wsplit: int = 0, add2: Optional[torch.Tensor] = None,
+              lda2: int = 0) -> None:
     """pk_linear_ex: a per-point layer writing into caller-placed (strided) outputs with a
     residual / accumulation epilogue. x, y, y2, add are the first elements of their (possibly
     strided) operands; strides as in include/posekern.h (0 = contiguous)."""
@@ -724,10 +735,22 @@ def linear_ex(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], la
                         mask=_dp(mask),
                         ldx=int(ldx), y=_dp(y), ldy=int(ldy), y2=_dp(y2), ldy2=int(ldy2), split=int(split),
                         store_cf=int(store_cf), add=_dp(add), lda=int(lda), add_cols=int(add_cols), pre=_dp(pre),
-                        pre_out=_dp(pre_out))
+                        pre_out=_dp(pre_out), w2=_dp(w2.contiguous()) if w2 is not None else None, bias2=_dp(bias2),
+                        wsplit=int(wsplit), add2=_dp(add2), lda2=int(lda2))
     import ctypes
-    call("pk_linear_ex", ctypes.addressof(a), _lib.stream(x.device),
-         work=("hbm", 4 * int(R) * (Cin + Cout) + 4 * Cin * Cout, 2 * int(R) * Cin * Cout))
+    # algorithmic bytes: the input rows, the output rows, the weight, and every epilogue /
+    # prologue operand the fused launch must move (the ReLU-backward mask, the residual rows, the
+    # sigmoid-backward input and its scaled copy) — each crosses HBM exactly once
+    byts = 4 * int(R) * (Cin + Cout) + 4 * Cin * Cout
+    if mask is not None:
+        byts += 4 * int(R) * Cout
+    if add is not None:
+        byts += 4 * int(R) * (int(add_cols) or Cout)
+    if pre is not None:
+        byts += 4 * int(R) * Cin * (2 if pre_out is not None else 1)
+    if add2 is not None:
+        byts += 4 * int(R) * Cout
+    call("pk_linear_ex", ctypes.addressof(a), _lib.stream(x.device), work=("hbm", byts, 2 * int(R) * Cin * Cout))
 
 
 def spectral_raw(x: torch.Tensor, ld_in: int, mass, evals, evecs, t, clamp_t: bool, mode: int, out: torch.Tensor,

@@ -294,14 +294,23 @@ class TrainStep:
             g.copy_(self.flat[o:o + n].view_as(g))
             o += n
 
+    @staticmethod
+    @torch.no_grad()
+    def ground_truth(op: Operators, crops: Crops) -> torch.Tensor:
+        """C_gt of the crops (utils/utils.py:67-79): reads only P and the two bases, so a
+        producer may form it with the crops (Crops.C_gt) off the step's critical path."""
+        return ops.cgt_lstsq(crops.pairs, crops.npairs, op.cad_evecs, op.pc_evecs)
+
     def forward_backward(self, op: Operators, crops: Crops) -> dict:
         self.model.train()
         batch = model_batch(op, crops)
         main = torch.cuda.current_stream() if self.overlap else None
         if self.overlap:  # C_gt needs only the crops: beside the model forward
             self.aux.wait_stream(main)
-        with torch.no_grad(), _on(self.aux):
-            C_gt = ops.cgt_lstsq(crops.pairs, crops.npairs, op.cad_evecs, op.pc_evecs)
+        C_gt = crops.C_gt
+        if C_gt is None:
+            with torch.no_grad(), _on(self.aux):
+                C_gt = self.ground_truth(op, crops)
         C_pred, o12, o21, f1, f2, _, _ = self.model(batch)
         if self.overlap:
             main.wait_stream(self.aux)
@@ -495,7 +504,12 @@ class PipelinedTrainer:
         for k in range(2):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self.crops.append(crop_formation(fb))
+                c = crop_formation(fb)
+                # C_gt depends only on the crops and the bases: solve it on the crop-formation
+                # stream too (PK_CGT_SIDE=0 keeps it in the training graph)
+                if os.environ.get("PK_CGT_SIDE", "1") == "1":
+                    c.C_gt = TrainStep.ground_truth(op, c)
+                self.crops.append(c)
             self.crop_graphs.append(g)
         for k in range(2):
             step.opt.zero_grad(set_to_none=True)  # each training graph owns its gradients
@@ -677,7 +691,12 @@ class PipelinedInfer:
         for k in range(2):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self.crops.append(crop_formation(fb))
+                c = crop_formation(fb)
+                # C_gt depends only on the crops and the bases: solve it on the crop-formation
+                # stream too (PK_CGT_SIDE=0 keeps it in the training graph)
+                if os.environ.get("PK_CGT_SIDE", "1") == "1":
+                    c.C_gt = TrainStep.ground_truth(op, c)
+                self.crops.append(c)
             self.crop_graphs.append(g)
         for k in range(2):
             g = torch.cuda.CUDAGraph()

@@ -154,12 +154,16 @@ int pk_fmap_solve_backward(const float* AAt, const float* BAt, const float* D, f
  *   q f32 [B, D, H, N], k / v f32 [B, D, H, M] (heads interleaved as the reference's
  *   view(B, dim, heads, N) of a [B, D*H, N] projection), out f32 [B, D, H, N],
  *   lse f32 [B, H, N, 2]: per query the row max m and 1 / sum of exp(s - m) (for the backward).
- * Backward: dout like out; delta f32 [B, H, N] scratch; dq like q, dk / dv like k. */
+ * Backward: dout like out; delta f32 [B, H, N] scratch; dq like q, dk / dv like k.
+ * sbk / sbv (sbdk / sbdv): batch strides in elements of k / v (dk / dv); 0 = dense D H M. A
+ * batch stride of 2 D H M reads (writes) the key and value halves of one [B, 2 D H, M] buffer:
+ * the stacked key / value projection (one launch for modeling/dpfm.py:63-67's proj[1], proj[2]). */
 int pk_attention_fwd(const float* q, const float* k, const float* v, int B, int D, int H, int N,
-                     int M, float* out, float* lse, void* stream);
+                     int M, int64_t sbk, int64_t sbv, float* out, float* lse, void* stream);
 int pk_attention_bwd(const float* q, const float* k, const float* v, const float* out,
                      const float* dout, const float* lse, int B, int D, int H, int N, int M,
-                     float* delta, float* dq, float* dk, float* dv, void* stream);
+                     int64_t sbk, int64_t sbv, float* delta, float* dq, float* dk, float* dv, int64_t sbdk,
+                     int64_t sbdv, void* stream);
 
 /* Weight/bias gradients of the per-point layers of H7/H8 (DiffusionNet Linear layers,
  * models/dpfm.py:22-30; refinement Conv1d(k=1), modeling/dpfm.py:16-26,45-54,82-95):
@@ -188,6 +192,9 @@ typedef struct pk_wgrad_call {
   float* db;
   int64_t R;
   int32_t I, O, N, layout, accumulate, pad;
+  int64_t sx, sdy; /* layout 1: batch strides of x / dy in elements (0: dense I N / O N), so a
+                    * channel slice of a wider buffer (the stacked key / value gradients) is read
+                    * in place */
 } pk_wgrad_call;
 int64_t pk_linear_wgrad_grouped_work(const pk_wgrad_call* calls, int n);
 int pk_linear_wgrad_grouped(const pk_wgrad_call* calls, int n, float* work, int64_t work_elems, void* stream);
@@ -319,6 +326,19 @@ typedef struct pk_linear_args {
   int32_t add_cols, pad;
   const float* pre;
   float* pre_out;
+  /* channels-first MFMA kernel only (layout 1, Cin in {16, 32, 64, 128}, N % 16 == 0):
+   *   w2 / wsplit: stored weight rows >= wsplit are read from w2 (row - wsplit): two layers'
+   *     weights stacked with no concatenation (transw = 0: rows = outputs, e.g. the key and value
+   *     projections of modeling/dpfm.py:63-67 as one 32 -> 64 launch; transw = 1: rows of the stored
+   *     [Cin, Cout] weight, e.g. their input gradients summed in one 64 -> 32 launch); bias2: bias
+   *     entries >= wsplit (transw = 0);
+   *   add2 / lda2: a second added operand over every output, after add (gradient accumulation of
+   *     an input used three times). NULL / 0: unused. */
+  const float* w2;
+  const float* bias2;
+  int32_t wsplit, pad2;
+  const float* add2;
+  int64_t lda2;
 } pk_linear_args;
 int pk_linear_ex(const pk_linear_args* a, void* stream);
 

@@ -600,3 +600,35 @@ def test_fused_fmap_head_matches_module_path(device, N1, N2, monkeypatch):
     g0 = torch.cat([g.reshape(-1) for g in res["0"][1].values()])
     g1 = torch.cat([res["1"][1][k].reshape(-1) for k in res["0"][1]])
     assert (g1 - g0).norm().item() <= 1e-3 * g0.norm().item()
+
+
+def test_fused_attn_prop_matches_module_path(device, monkeypatch):
+    """attnprop._AttnPropFn (one autograd node per AttentionalPropagation call + residual:
+    stacked key/value projection, attention on the stacked buffer, merge into the
+    concatenation, the input gradients of desc summed in one epilogue) vs the module path
+    (modeling/dpfm.py:45-82, 101-103): refinement outputs and every parameter gradient within
+    fp32 rounding (1e-5 of each tensor's scale; the summation orders differ)."""
+    from dpfm_amd.modeling import dpfm as MD
+    torch.manual_seed(3)
+    net = MD.CrossAttentionRefinementNet(n_in=32, num_head=2, gnn_dim=32, n_layers=1, cross_sampling_ratio=1).to(device)
+    g = torch.Generator().manual_seed(4)
+    fx = torch.randn(4, 512, 32, generator=g).to(device)
+    fy = torch.randn(4, 384, 32, generator=g).to(device)
+
+    def run(fused):
+        monkeypatch.setattr(MD, "FUSED_ATTN_PROP", fused)
+        net.zero_grad()
+        a, b = fx.clone().requires_grad_(True), fy.clone().requires_grad_(True)
+        rx, ry, ox, oy = net(None, None, a, b)
+        (rx.square().sum() + 0.5 * ry.square().sum() + ox.sum() + 2 * oy.sum()).backward()
+        return [t.detach().clone() for t in (rx, ry, ox, oy, a.grad, b.grad)] + \
+               [p.grad.detach().clone() for p in net.parameters()]
+
+    ref, got = run(False), run(True)
+    names = ["rx", "ry", "ox", "oy", "dfx", "dfy"] + [n for n, _ in net.named_parameters()]
+    # floor for parameters whose true gradient vanishes by invariance (biases in front of the
+    # InstanceNorm: merge / mlp.0 biases): their values are rounding noise of the global scale
+    floor = 1e-6 * float(torch.cat([r.reshape(-1) for r in ref[6:]]).norm())
+    for n, r, o in zip(names, ref, got):
+        scale = max(float(r.abs().max()), 1e-30)
+        assert (o - r).abs().max().item() <= 1e-5 * scale + floor, (n, (o - r).abs().max().item(), scale, floor)
