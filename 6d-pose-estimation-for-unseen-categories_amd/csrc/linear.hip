@@ -162,8 +162,9 @@ __global__ __launch_bounds__(64 * kRedGroups) void wgrad_reduce_kernel(const flo
 // Lane l supplies A[l & 31][l >> 5] and B[l >> 5][l & 31], i.e. one value of row
 // r(step, h = l >> 5) at channel (l & 31). Rows are taken in batches of 16 (8 k-steps):
 //   layout 0 ([R, C]): r = rb + 2 s + h       (32 lanes read 128 contiguous bytes)
-//   layout 1 ([Bn, C, N], N % 16 == 0): r = rb + 8 h + s  (a lane's 8 rows are 8
-//            consecutive n of one channel: two 16-byte loads)
+//   layout 1 ([Bn, C, N]): r = rb + 8 h + s  (a lane's 8 rows are 8 consecutive n of one
+//            channel: two 16-byte loads when N % 16 == 0, else 8 scalar loads with the tail
+//            rows past the slice end read as 0)
 // Both operands use the same r(s, h), so the contraction is the same sum over rows.
 // Workgroup = one row slice; its 4 waves split the 32x32 output tiles (T = To * Ti <= 16)
 // and, when there are fewer than 4 tiles, the slice's batches; wave row groups are
@@ -179,6 +180,14 @@ __device__ __forceinline__ void load8(const float* __restrict__ p, int C, int c,
     for (int s = 0; s < 8; ++s) {
       const int64_t r = rb + 2 * s + h;
       v[s] = (c < C && r < r1) ? p[r * C + c] : 0.f;
+    }
+  } else if (N & 15) {  // ragged items (N % 16 != 0): a 16-row batch may straddle two items
+    const int64_t cs = sb ? sb : (int64_t)C * N;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int64_t r = rb + 8 * h + s;
+      const int64_t b = r / N;
+      v[s] = (c < C && r < r1) ? p[b * cs + (int64_t)c * N + (r - b * N)] : 0.f;
     }
   } else {
     if (c < C) {  // batch stride sb (0: dense C N)
@@ -465,9 +474,9 @@ extern "C" int pk_linear_wgrad(const float* x, const float* dy, int layout, int6
   PK_REQUIRE(x && dy && work);
   float* part = work;
   // direct-load kernel: slices of >= 128 rows (so S never exceeds the documented work
-  // size), ~320 slices for the large calls; channels-first needs N % 16 == 0
-  int S2 = S;
-  if (layout == 0 || N % 16 == 0) {
+  // size), ~320 slices for the large calls
+  int S2;
+  {
     int64_t SL = (R + 319) / 320;
     SL = (SL + 15) / 16 * 16;
     if (SL < kSlice) SL = kSlice;
@@ -486,9 +495,6 @@ extern "C" int pk_linear_wgrad(const float* x, const float* dy, int layout, int6
       else PK_WGRAD_V2(1, 2);
     }
 #undef PK_WGRAD_V2
-  } else {
-    float* partb = work + (int64_t)S * O * I;
-    hipLaunchKernelGGL(wgrad_partial_kernel, dim3(S), dim3(256), 0, s, x, dy, layout, R, I, O, N, part, partb);
   }
   PK_CHECK_LAUNCH();
   const int total = O * I + O;
@@ -979,8 +985,10 @@ __global__ __launch_bounds__(256, 2) void linear_rows_lds_kernel(const float* __
   }
 }
 
-// Channels-first layout (1) [Bn, C, N] with Cin in {16, 32, 64, 128} and N % (16 SUB) == 0:
-// one wave computes 16 SUB consecutive points of one item x all outputs. A = weight
+// Channels-first layout (1) [Bn, C, N] with Cin in {16, 32, 64, 128}: one wave computes 16 SUB
+// consecutive points of one item x all outputs; tpc tiles per item (SUB > 1 needs N % (16 SUB)
+// == 0; with SUB = 1 an item's last tile may be ragged: its columns past N compute on a clamped
+// point and are not stored — the MFMA columns are independent points). A = weight
 // (Ws[o][k] chunks, ds_read_b128), B = points: lane (j, g) loads its SUB consecutive points
 // as one vector per channel row k = 16 q + 4 g + i, and element u of that
 // vector is column j of point sub-tile u (sub-tile u holds points SUB j + u), so loads and
@@ -994,21 +1002,22 @@ template <int Q, int TO, int SUB>
 __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restrict__ x, int64_t sx,
                                                             const float* __restrict__ w,
                                                             const float* __restrict__ bias, int64_t R, int N, int Cout,
-                                                            int transw, LinEpi e) {
+                                                            int transw, LinEpi e, int64_t tpc) {
   using V = typename LcVec<SUB>::T;
   extern __shared__ float Ws[];
   constexpr int CI = 16 * Q, ST = CI + 4, P = 16 * SUB;
   const int lane = pk::lane_id(), m = lane & 15, g = lane >> 4;
-  const int64_t T = R / P;
+  const int64_t T = (R / N) * tpc;
   const int64_t tile = (int64_t)blockIdx.x * 4 + pk::wave_id();
   // the tile's operands are in flight while the weight is staged
   V xv[Q][4];
   int64_t bb = 0, n0 = 0;
+  bool live = true;  // this lane's point column exists (only a SUB = 1 ragged tail has dead ones)
   if (tile < T) {
-    const int64_t p0 = tile * P;
-    bb = p0 / N;
-    n0 = p0 - bb * N;
-    const float* xb = x + bb * sx + n0 + SUB * m;
+    bb = tile / tpc;
+    n0 = (tile - bb * tpc) * P;
+    if (SUB == 1) live = n0 + m < N;
+    const float* xb = x + bb * sx + n0 + (live ? SUB * m : 0);
 #pragma unroll
     for (int q = 0; q < Q; ++q)
 #pragma unroll
@@ -1040,7 +1049,7 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
     __builtin_amdgcn_sched_barrier(0);
   }
   // D[out t * 16 + 4 g + r][column m of sub-tile u] = point n0 + SUB m + u
-  const int64_t pn = n0 + SUB * m;
+  const int64_t pn = n0 + (live ? SUB * m : 0);
   float* yb = e.y + bb * e.sy + pn;
   const int64_t mb = bb * Cout * (int64_t)N + pn;  // contiguous index (mask)
   // epilogue operands (mask, add) of all TO x 4 output rows loaded before the first use:
@@ -1092,7 +1101,7 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int o = t * 16 + 4 * g + r;
-      if (o < Cout) {
+      if (o < Cout && live) {
         const float bo = bo4[t][r];
         const bool has_add = e.add != nullptr && o < e.add_cols;
         V v;
@@ -1286,7 +1295,7 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
   e.wsplit = a->w2 ? a->wsplit : (1 << 30);
   // stacked weights and the second add operand: channels-first MFMA kernel only
   PK_REQUIRE((a->w2 == nullptr && a->add2 == nullptr && a->bias2 == nullptr) ||
-             (layout == 1 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128) && N % 16 == 0 &&
+             (layout == 1 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128) &&
               Cin > 4 && Cout > 4 && !a->store_cf && a->y2 == nullptr));
   PK_REQUIRE(a->w2 == nullptr || (a->wsplit > 0 && a->wsplit < (a->transw ? Cin : Cout)));
   PK_REQUIRE(a->bias2 == nullptr || (a->w2 != nullptr && !a->transw));
@@ -1363,12 +1372,12 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
     PK_CHECK_LAUNCH();
     return PK_OK;
   }
-  if (layout == 1 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128) && N % 16 == 0) {
+  if (layout == 1 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128) && N > 0) {
     PK_REQUIRE(e.y2 == nullptr && !e.store_cf);
     // points per wave: 16 SUB, as many as keep >= 1024 waves and <= 64 operand VGPRs
     int sub = R >= 131072 ? 4 : R >= 32768 ? 2 : 1;
     sub = std::min(sub, 256 / Cin);
-    while (N % (16 * sub)) sub >>= 1;
+    while (sub > 1 && N % (16 * sub)) sub >>= 1;  // N % 16 != 0: SUB = 1 with ragged item tails
     // vector loads / stores of SUB points need SUB-aligned batch strides
     while (sub > 1 && ((sx % sub) || (e.sy % sub) || (e.add && (e.sa % sub)) || (e.add2 && (e.sa2 % sub)))) sub >>= 1;
     const int TO = Cout <= 16 ? 1 : Cout <= 32 ? 2 : Cout <= 64 ? 4 : 8;
@@ -1385,10 +1394,11 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
     };
     auto kern = sub == 4 ? pickq(std::integral_constant<int, 4>{})
                 : sub == 2 ? pickq(std::integral_constant<int, 2>{}) : pickq(std::integral_constant<int, 1>{});
-    const int64_t tiles = R / (16 * sub);
+    const int64_t tpc = (N + 16 * sub - 1) / (16 * sub);
+    const int64_t tiles = (R / N) * tpc;
     const size_t lds = sizeof(float) * (size_t)(16 * TO) * (Cin + 4);
     hipLaunchKernelGGL(kern, dim3((unsigned)((tiles + 3) / 4)), dim3(256), lds, st, x, sx, w, bias, R, N, Cout,
-                       transw, e);
+                       transw, e, tpc);
     PK_CHECK_LAUNCH();
     return PK_OK;
   }
@@ -1542,7 +1552,7 @@ extern "C" int pk_linear_wgrad_grouped(const pk_wgrad_call* calls, int n, float*
     const pk_wgrad_call& k = calls[c];
     PK_REQUIRE(k.dw && k.R >= 0 && k.I > 0 && k.O > 0 && k.I <= kMaxC && k.O <= kMaxC);
     PK_REQUIRE(((k.O + 31) / 32) * ((k.I + 31) / 32) <= kV2Waves);  // one 32x32 tile per wave
-    PK_REQUIRE(k.layout == 0 || (k.layout == 1 && k.N > 0 && k.N % 16 == 0));
+    PK_REQUIRE(k.layout == 0 || (k.layout == 1 && k.N > 0));
     PK_REQUIRE((k.sx == 0 && k.sdy == 0) || (k.layout == 1 && k.sx >= 0 && k.sdy >= 0 && k.sx % 4 == 0 &&
                                                k.sdy % 4 == 0));
     PK_REQUIRE(k.R == 0 || (k.x && k.dy));

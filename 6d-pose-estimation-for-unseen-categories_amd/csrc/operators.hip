@@ -27,9 +27,11 @@
 //   pk_dgemm_tn        G = X^T Y [m, m] (Gram / Rayleigh quotient matrices), partial sums over
 //                      row slabs in a fixed order.
 //
-// Deviations from robust_laplacian (parity unpinned): no tufted cover / intrinsic Delaunay flips
-// and no mollification of the soup; the tangent basis and the normal's sign are this build's
-// (they do not change the triangulation).
+// robust_laplacian's remaining stages — mollification, the tufted cover and its intrinsic
+// Delaunay flips — run on the host (csrc/tufted.cpp, pk_tufted_laplacian) on the fans built here;
+// pk_cotan_dense's soup operator is that Laplacian before any flip (geometry.py robust=False).
+// Parity unpinned (robust_laplacian is absent); the tangent basis and the normal's sign are this
+// build's (they do not change the triangulation).
 #include "common.hpp"
 
 namespace {

@@ -162,18 +162,72 @@ def get_operators(verts: Sequence[np.ndarray], faces: Optional[Sequence[np.ndarr
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     pts, off, nmax = _pack(verts, dev)
     counts = [int(v.shape[0]) for v in verts]
-    normals = None
     if faces is None:
-        idx, _ = ops.knn(pts, off, nmax, n_neighbors, omit_self=True)
-        tri, ntri, normals = ops.pc_local_tri(pts, off, nmax, idx)
-        L, mass = ops.cotan_dense(pts, off, nmax, tri=tri, ntri=ntri, scale=1.0 / 3.0, denom_eps=0.0)
+        return point_cloud_operators(pts, off, counts, k_eig=k_eig, n_neighbors=n_neighbors, eps=eps, **eig_kw)
+    fo = np.concatenate([[0], np.cumsum([f.shape[0] for f in faces])]).astype(np.int64)
+    fc = torch.as_tensor(np.concatenate([np.asarray(f, dtype=np.int32) for f in faces]), device=dev)
+    L, mass = ops.cotan_dense(pts, off, nmax, faces=fc, foff=torch.as_tensor(fo, device=dev),
+                              fmax=int(max(f.shape[0] for f in faces)), scale=1.0, denom_eps=1e-10)
+    for b, n in enumerate(counts):  # vertex_areas + eps * mean (compute_operators)
+        mass[b, :n] += eps * mass[b, :n].mean()
+    return _spectral(pts, off, counts, L, mass, None, k_eig, eps, faces=faces, **eig_kw)
+
+
+def point_cloud_operators(pts: torch.Tensor, off: torch.Tensor, counts: Sequence[int], k_eig: int = 64,
+                          n_neighbors: int = 30, eps: float = 1e-8, robust: bool = True,
+                          mollify_factor: float = 1e-5, **eig_kw) -> SpectralOperators:
+    """The crop path (dataset/object.py:246 get_operators(verts=pcd_depth, faces=[])) on packed
+    device points: f64 [T, 3] rows off[b]..off[b+1] per cloud (e.g. Crops.pc64 / Crops.off as
+    CropFormation leaves them). kNN, the local fans and the eigensolver run on the device;
+    robust=True (robust_laplacian.point_cloud_laplacian) lifts each cloud's fan soup to its
+    mollified tufted cover and flips it to intrinsic Delaunay on the host (pk_tufted_laplacian,
+    one thread per cloud), the result scattered back into the dense device L; robust=False keeps
+    the soup's own cotan Laplacian (pk_cotan_dense, the same operator before any flip)."""
+    pts = pts.to(torch.float64).contiguous()
+    off = off.to(device=pts.device, dtype=torch.int64).contiguous()
+    counts = [int(c) for c in counts]
+    nmax = max(counts)
+    idx, _ = ops.knn(pts, off, nmax, n_neighbors, omit_self=True)
+    tri, ntri, normals = ops.pc_local_tri(pts, off, nmax, idx)
+    if robust:
+        L, mass = tufted_dense(pts, off, counts, nmax, tri, ntri, mollify_factor)
     else:
-        fo = np.concatenate([[0], np.cumsum([f.shape[0] for f in faces])]).astype(np.int64)
-        fc = torch.as_tensor(np.concatenate([np.asarray(f, dtype=np.int32) for f in faces]), device=dev)
-        L, mass = ops.cotan_dense(pts, off, nmax, faces=fc, foff=torch.as_tensor(fo, device=dev),
-                                  fmax=int(max(f.shape[0] for f in faces)), scale=1.0, denom_eps=1e-10)
-        for b, n in enumerate(counts):  # vertex_areas + eps * mean (compute_operators)
-            mass[b, :n] += eps * mass[b, :n].mean()
+        L, mass = ops.cotan_dense(pts, off, nmax, tri=tri, ntri=ntri, scale=1.0 / 3.0, denom_eps=0.0)
+    return _spectral(pts, off, counts, L, mass, normals, k_eig, eps, **eig_kw)
+
+
+def tufted_dense(pts, off, counts, nmax, tri, ntri, mollify_factor=1e-5):
+    """Dense device (L f64 [B, nmax, nmax], mass f64 [B, nmax]) of the clouds' tufted-cover
+    Laplacians (pk_tufted_laplacian per cloud on host threads; the distinct pairs scattered with
+    index_put_ — no duplicate indices, so the result is deterministic)."""
+    from concurrent.futures import ThreadPoolExecutor
+    dev = pts.device
+    B = len(counts)
+    o = off.cpu().numpy()
+    P, T, NT = pts.cpu().numpy(), tri.cpu().numpy(), ntri.cpu().numpy()
+
+    def one(b):
+        a, e = int(o[b]), int(o[b + 1])
+        return ops.tufted_laplacian(P[a:e], ops.soup_triangles(T[a:e], NT[a:e]), mollify_factor)
+    with ThreadPoolExecutor(max_workers=max(1, min(B, 16))) as ex:
+        res = list(ex.map(one, range(B)))
+    L = torch.zeros((B, nmax, nmax), dtype=torch.float64, device=dev)
+    mass = torch.zeros((B, nmax), dtype=torch.float64, device=dev)
+    for b, (i, j, w, m, _) in enumerate(res):
+        n = counts[b]
+        diag = np.bincount(i, weights=w, minlength=n) + np.bincount(j, weights=w, minlength=n)
+        it, jt = torch.as_tensor(i.astype(np.int64), device=dev), torch.as_tensor(j.astype(np.int64), device=dev)
+        wt = torch.as_tensor(-w, device=dev)
+        L[b].index_put_((it, jt), wt)
+        L[b].index_put_((jt, it), wt)
+        L[b, :n, :n].diagonal().copy_(torch.as_tensor(diag, device=dev))
+        mass[b, :n] = torch.as_tensor(m, device=dev)
+    return L, mass
+
+
+def _spectral(pts, off, counts, L, mass, normals, k_eig, eps, faces=None, **eig_kw) -> SpectralOperators:
+    """eigsh(L + eps I, k, M = diag(mass), sigma) for the assembled operators, then the frames."""
+    dev = L.device
     for b, n in enumerate(counts):
         mass[b, n:] = 1.0
     upper = float(L.abs().sum(-1).amax() / mass.amin())

@@ -74,7 +74,7 @@ class GroupedWgrad:
     def _groupable(c) -> bool:
         x, dy, cf, dw, _, _ = c
         O, I = dw.shape
-        return ((O + 31) // 32) * ((I + 31) // 32) <= 8 and (not cf or x.shape[-1] % 16 == 0)
+        return ((O + 31) // 32) * ((I + 31) // 32) <= 8
 
     def end(self, run: bool = True):
         global _SIDE
@@ -209,7 +209,7 @@ def pointwise_residual(layer: "Conv1d", x: torch.Tensor, res: torch.Tensor) -> t
     (falls back to the two-step form for other storage orders)."""
     if (x.is_cuda and x.dim() == 3 and x.is_contiguous() and res.is_contiguous() and res.shape[1] == layer.out_channels
             and res.shape[0] == x.shape[0] and res.shape[2] == x.shape[2] and res.dtype == x.dtype
-            and x.shape[2] % 16 == 0 and layer.in_channels in (16, 32, 64, 128)):  # the cf MFMA kernel's range
+            and layer.in_channels in (16, 32, 64, 128)):  # the cf MFMA kernel's range
         return _PointwiseResidualFn.apply(x, layer.weight, layer.bias, res, getattr(x, "_pk_relu_out", False))
     return res + layer(x)
 

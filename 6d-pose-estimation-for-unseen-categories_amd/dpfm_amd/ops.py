@@ -6,6 +6,7 @@ concatenated and `offsets[b] .. offsets[b+1]` delimits crop b (int64, on device)
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import Optional, Sequence
 
@@ -1145,6 +1146,34 @@ def pc_local_tri(pts: torch.Tensor, off: torch.Tensor, nmax: int, knn_idx: torch
     call("pk_pc_local_tri", ptr(pts), ptr(off), off.numel() - 1, int(nmax), ptr(knn_idx.contiguous()), int(k), ptr(tri),
          ptr(ntri), ptr(nrm), _lib.stream(pts.device))
     return tri[:T], ntri[:T], nrm[:T]
+
+
+def soup_triangles(tri: np.ndarray, ntri: np.ndarray) -> np.ndarray:
+    """The (center, u, v) soup of one cloud from pc_local_tri's fans (host arrays tri [n, k, 2],
+    ntri [n], cloud-local): int32 [sum ntri, 3], point-major, each fan in its stored order."""
+    n, k = tri.shape[0], tri.shape[1]
+    keep = np.arange(k)[None, :] < ntri[:, None]
+    centers = np.broadcast_to(np.arange(n, dtype=np.int32)[:, None], (n, k))[keep]
+    return np.ascontiguousarray(np.concatenate([centers[:, None], tri[keep]], axis=1).astype(np.int32))
+
+
+def tufted_laplacian(pts: np.ndarray, tris: np.ndarray, mollify_factor: float = 1e-5):
+    """pk_tufted_laplacian (host): robust_laplacian's mollified tufted-cover intrinsic Delaunay
+    Laplacian of one cloud's soup. Returns (i, j, w, mass, nflips): the distinct pairs i < j with
+    L_ij = L_ji = -w (L_ii = the sum of the row's w) and the lumped mass, as numpy arrays."""
+    pts = np.ascontiguousarray(pts, dtype=np.float64)
+    tris = np.ascontiguousarray(tris, dtype=np.int32)
+    n, nt = pts.shape[0], tris.shape[0]
+    cap = max(3 * nt, 1)
+    ii, jj = np.empty(cap, np.int32), np.empty(cap, np.int32)
+    ww, mass = np.empty(cap, np.float64), np.empty(max(n, 1), np.float64)
+    nnz, nfl = ctypes.c_int64(0), ctypes.c_int64(0)
+    call("pk_tufted_laplacian", pts.ctypes.data, n, tris.ctypes.data, nt, float(mollify_factor), cap,
+         ii.ctypes.data, jj.ctypes.data, ww.ctypes.data, ctypes.byref(nnz), mass.ctypes.data, ctypes.byref(nfl))
+    m = int(nnz.value)
+    if m > cap:
+        raise _lib.PoseKernError("pk_tufted_laplacian: pair capacity exceeded")
+    return ii[:m], jj[:m], ww[:m], mass[:n], int(nfl.value)
 
 
 def cotan_dense(pts: torch.Tensor, off: torch.Tensor, nmax: int, tri=None, ntri=None, faces=None, foff=None,

@@ -47,6 +47,7 @@ class Operators:
     ir_thr: torch.Tensor     # f32 [F] 0.1 * diam (train.py:115)
     rig_thr: torch.Tensor    # f32 [F, 4] spatial-filter thresholds
     cad_n: Optional[torch.Tensor] = None  # int32 [F] CAD vertices per crop (rows of cad_* not padding)
+    pc_spectral: Optional[object] = None  # geometry.SpectralOperators the pc_* fields came from (f1 path)
 
 
 def pad_rows(arrs, ld: Optional[int] = None) -> np.ndarray:
@@ -72,6 +73,28 @@ def crop_operators(op: Operators, crops: Crops, seed: int) -> Operators:
     pe = torch.as_tensor(np.stack([o[1] for o in ops_p]), device=dev)
     return Operators(cad_mass=op.cad_mass, cad_evals=op.cad_evals, cad_evecs=op.cad_evecs, cad_xyz=op.cad_xyz,
                      pc_mass=pm, pc_evals=pe, pc_evecs=pv, ir_thr=op.ir_thr, rig_thr=op.rig_thr, cad_n=op.cad_n)
+
+
+def device_crop_operators(op: Operators, crops: Crops, k_eig: int = 64, **eig_kw) -> Operators:
+    """The (f1) new-crop path: the crops' spectral operators computed on the device from the formed
+    crop points themselves (dataset/object.py:246 get_operators(verts=torch.Tensor(pcd_depth),
+    faces=[], k_eig=64): the reference rounds the crop to f32 first, so does this), zero-padded to
+    crops.ld as collate pads them; the CAD part of `op` is kept (the reference caches it per
+    object). Chains crop formation -> operators -> DPFMNet -> pose without the offline cache.
+    Reads the crop sizes (host sync: the eigensolver's subspace width depends on them)."""
+    from . import geometry
+    counts = crops.n2.cpu().tolist()
+    pts = crops.pc64.float().double()
+    so = geometry.point_cloud_operators(pts, crops.off, counts, k_eig=k_eig, **eig_kw)
+    F, ld, nm = len(counts), crops.ld, so.evecs.shape[1]
+    dev = crops.pc32.device
+    pv = torch.zeros(F, ld, k_eig, dtype=torch.float32, device=dev)
+    pv[:, :nm] = so.evecs.float()
+    pm = torch.zeros(F, ld, dtype=torch.float32, device=dev)
+    pm[:, :nm] = so.mass.float()
+    return Operators(cad_mass=op.cad_mass, cad_evals=op.cad_evals, cad_evecs=op.cad_evecs, cad_xyz=op.cad_xyz,
+                     pc_mass=pm, pc_evals=so.evals.float().contiguous(), pc_evecs=pv, ir_thr=op.ir_thr,
+                     rig_thr=op.rig_thr, cad_n=op.cad_n, pc_spectral=so)
 
 
 def make_frame_batch(F: int, n1: int, n2: int, seed: int, device) -> tuple[FrameBatch, Operators]:

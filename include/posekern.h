@@ -569,6 +569,18 @@ int pk_dgemm_tn(const double* X, const double* Y, int B, int n, int m, double* G
  * place for X [B,n,m]. */
 int pk_dpotrf(double* A, int B, int n, double tau, int32_t* fail, void* stream);
 int pk_dpotrs(const double* L, double* X, int B, int n, int m, void* stream);
+/* (f1) robust_laplacian.point_cloud_laplacian's intrinsic stage (replaces the third-party call at
+ * the end of diffusion-net compute_operators, reached from dataset/object.py:246), HOST code, one
+ * cloud per call: the soup tri int32 [ntri,3] (cloud-local; pk_pc_local_tri's fans as (center,
+ * u, v) triples) over pts f64 [n,3] is mollified (mollify_factor x mean edge length), lifted to
+ * its tufted cover, flipped to intrinsic Delaunay, and its cotan Laplacian / lumped mass scaled
+ * by 1/6 (cover x soup multiplicity) returned as the distinct off-diagonal pairs i < j with the
+ * weight w_ij (L = sum_ij w_ij (e_i - e_j)(e_i - e_j)^T; ii/jj int32 [cap], ww f64 [cap], sorted
+ * by (i, j); nnz = their count — when nnz > cap nothing is written, call again with cap >= nnz;
+ * 3 ntri always suffices) and mass f64 [n]; nflips (may be NULL) = the flips performed. */
+int pk_tufted_laplacian(const double* pts, int64_t n, const int32_t* tri, int64_t ntri, double mollify_factor,
+                        int64_t cap, int32_t* ii, int32_t* jj, double* ww, int64_t* nnz, double* mass,
+                        int64_t* nflips);
 
 /* Runtime helpers of the pipelined executors (host only; no reference counterpart: the reference
  * overlaps crop formation with training through DataLoader worker PROCESSES, train.py /

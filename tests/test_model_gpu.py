@@ -113,6 +113,7 @@ def test_linear_wgrad_grouped(device):
         ((64, 1024), 128, 64, False, None), ((64, 1024), 64, 64, False, None), ((3, 700), 3, 64, False, None),
         ((32, 1024), 32, 32, True, None), ((32, 1024), 64, 32, True, None), ((32, 1024), 32, 32, True, 3),
         ((0,), 16, 8, False, None), ((5, 33), 64, 32, False, None), ((2, 1024), 64, 64, True, 1 << 30),
+        ((3, 5002), 64, 32, True, None), ((2, 300), 64, 32, True, 9),  # ragged items (N % 16 != 0)
     ]
     specs = specs + [((7, 48), 32, 32, False, None)] * 30
     calls, exp = [], {}
@@ -229,7 +230,10 @@ def test_dpfmnet_matches_oracle(device, N1, N2):
                                                           ((5000, 32, 1), False, False), ((777, 16, 100), False, True),
                                                           ((32, 32, 1024, 1), True, False), ((32, 1, 1024, 32), True, True),
                                                           ((3, 2, 100, 7), True, False), ((10, 33, 3), False, True),
-                                                          ((2, 40, 64, 3), True, True), ((65536, 3, 64), False, False)])
+                                                          ((2, 40, 64, 3), True, True), ((65536, 3, 64), False, False),
+                                                          # ragged channels-first items (N % 16 != 0: tiles end per item)
+                                                          ((2, 64, 5002, 32), True, True), ((3, 128, 203, 64), True, False),
+                                                          ((2, 16, 7, 20), True, False)])
 def test_linear_fwd(device, shape, channels_first, transw):
     """pk_linear_fwd (per-point layer forward, bias fused; transw = the input gradient dy W)
     vs fp64: |err| <= 1e-5 * sum_k |x||w| + 1e-6 |b|."""
@@ -602,7 +606,8 @@ def test_fused_fmap_head_matches_module_path(device, N1, N2, monkeypatch):
     assert (g1 - g0).norm().item() <= 1e-3 * g0.norm().item()
 
 
-def test_fused_attn_prop_matches_module_path(device, monkeypatch):
+@pytest.mark.parametrize("N1,N2", [(512, 384), (300, 203)])  # (300, 203): ragged channels-first tiles
+def test_fused_attn_prop_matches_module_path(device, monkeypatch, N1, N2):
     """attnprop._AttnPropFn (one autograd node per AttentionalPropagation call + residual:
     stacked key/value projection, attention on the stacked buffer, merge into the
     concatenation, the input gradients of desc summed in one epilogue) vs the module path
@@ -612,8 +617,8 @@ def test_fused_attn_prop_matches_module_path(device, monkeypatch):
     torch.manual_seed(3)
     net = MD.CrossAttentionRefinementNet(n_in=32, num_head=2, gnn_dim=32, n_layers=1, cross_sampling_ratio=1).to(device)
     g = torch.Generator().manual_seed(4)
-    fx = torch.randn(4, 512, 32, generator=g).to(device)
-    fy = torch.randn(4, 384, 32, generator=g).to(device)
+    fx = torch.randn(4, N1, 32, generator=g).to(device)
+    fy = torch.randn(4, N2, 32, generator=g).to(device)
 
     def run(fused):
         monkeypatch.setattr(MD, "FUSED_ATTN_PROP", fused)

@@ -6,8 +6,11 @@ numpy / scipy restatement (oracle/operators_oracle.py):
   * pk_cotan_dense: the soup (1/3-scaled) and mesh-face Laplacians / masses within 1e-12 relative
     (fp64 atomics: the summation order of a shared entry is not fixed);
   * pk_dgemm_cheb / pk_dgemm_tn against torch fp64;
-  * get_operators (point clouds and a mesh) against scipy eigsh(L + eps I, k, M, sigma = eps):
-    eigenvalues, M-orthonormality, residuals.
+  * get_operators (point clouds — robust_laplacian's tufted-cover intrinsic Delaunay Laplacian —
+    and a mesh) against scipy eigsh(L + eps I, k, M, sigma = eps) on the oracle's operator:
+    eigenvalues, M-orthonormality, residuals;
+  * the new-crop chain (crop formation -> device operators at 2000 points, k = 64 -> DPFMNet ->
+    InferStep) against the same oracle per crop and the oracle model on the chained operators.
 """
 import numpy as np
 import pytest
@@ -110,18 +113,24 @@ def test_dgemm_kernels(device):
     assert (G - torch.bmm(X.transpose(1, 2), Y)).abs().max() < 1e-12 * G.abs().max()
 
 
-@pytest.mark.parametrize("kind", ["cloud", "mesh"])
+@pytest.mark.parametrize("kind", ["cloud", "cloud-soup", "mesh"])
 def test_get_operators_matches_eigsh(device, kind):
     from dpfm_amd import geometry
     rng = np.random.default_rng(3)
     k, eps = 32, 1e-8
-    if kind == "cloud":
-        shapes = [ellipsoid(rng, 500), ellipsoid(rng, 420, (6.0, 3.0, 2.0))]
-        op = geometry.get_operators(shapes, k_eig=k, device=device, tol=1e-10)
+    if kind.startswith("cloud"):
+        robust = kind == "cloud"
+        shapes = [ellipsoid(rng, 500) + 0.01 * rng.normal(size=(500, 3)), ellipsoid(rng, 420, (6.0, 3.0, 2.0))]
+        op = geometry.get_operators(shapes, k_eig=k, device=device, tol=1e-10, robust=robust)
         refs = []
-        for s in shapes:
+        for b, s in enumerate(shapes):
             ki, _ = OO.knn(s, 30)
-            refs.append(OO.cotan_laplacian(s, OO.local_triangles(s, ki), scale=1.0 / 3.0, denom_eps=0.0))
+            tris = OO.local_triangles(s, ki)
+            Lr, Mr = (OO.tufted_laplacian(s, tris)[:2] if robust
+                      else OO.cotan_laplacian(s, tris, scale=1.0 / 3.0, denom_eps=0.0))
+            n = s.shape[0]
+            assert np.abs(op.L[b, :n, :n].cpu().numpy() - Lr).max() <= 1e-10 * np.abs(Lr).max()
+            refs.append((Lr, Mr))
     else:
         meshes = [_hull_mesh(rng, 500, (5, 4, 3)), _hull_mesh(rng, 400, (2, 3, 4))]
         shapes = [m[0] for m in meshes]
@@ -166,3 +175,58 @@ def test_dpotrf_dpotrs(device, n):
     bad = A.clone()
     bad[1] -= 10.0 * torch.eye(n, dtype=torch.float64, device=device)
     assert ops.dpotrf(bad, 0.0).cpu().tolist() == [0, 1]
+
+
+def test_new_crop_chain_2000_k64(device):
+    """(f1) chained: CropFormation (2 frames, 2000-point crops) -> pipeline.device_crop_operators
+    (kNN, local fans, cotan soup, shift-invert eigensolver, k = 64, on the device) -> InferStep.
+    Operators per crop vs the oracle's scipy eigsh on the oracle's own tufted-cover Laplacian of the
+    same f32-rounded crop points (dataset/object.py:246): L to 1e-10, mass to 1e-12, eigenvalues to 1e-7,
+    M-orthonormality and residuals as above; the chain's f32 fields are the f64 result rounded.
+    Then the model on the chained operators: C vs the oracle DPFMNet in fp64 within 3x the fp32
+    reference's error (as test_configs_gpu's chain test), poses finite."""
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import InferStep, device_crop_operators, make_frame_batch, model_batch
+    from oracle import dpfm_model_oracle as M
+    B, N, k, eps = 2, 2000, 64, 1e-8
+    fb, op = make_frame_batch(B, 1024, N, seed=41, device=device)
+    crops = CropFormation(n1=1024, npoint=N, seed=3)(fb)
+    op2 = device_crop_operators(op, crops, k_eig=k, tol=1e-10)
+    so = op2.pc_spectral
+    counts = crops.n2.cpu().tolist()
+    assert min(counts) == N
+    off = crops.off.cpu().numpy()
+    pts = crops.pc64.float().double().cpu().numpy()
+    ev, V, Mm = so.evals.cpu().numpy(), so.evecs.cpu().numpy(), so.mass.cpu().numpy()
+    assert torch.equal(op2.pc_evecs[:, :N].cpu(), so.evecs.float().cpu())
+    assert torch.equal(op2.pc_mass[:, :N].cpu(), so.mass.float().cpu())
+    for b in range(B):
+        s = pts[off[b]:off[b + 1]]
+        ki, _ = OO.knn(s, 30)
+        Lr, Mr, _ = OO.tufted_laplacian(s, OO.local_triangles(s, ki))
+        np.testing.assert_allclose(Mm[b, :N], Mr, rtol=1e-12)
+        Lg = so.L[b, :N, :N].cpu().numpy()
+        assert np.abs(Lg - Lr).max() <= 1e-10 * np.abs(Lr).max()
+        er, _ = OO.eigsh_operators(Lr, Mr, k, eps)
+        np.testing.assert_allclose(ev[b], np.sort(er), rtol=1e-7, atol=1e-9)
+        E = V[b, :N]
+        np.testing.assert_allclose(E.T @ (Mr[:, None] * E), np.eye(k), atol=1e-7)
+        r = (Lr + eps * np.eye(N)) @ E - (Mr[:, None] * E) * ev[b][None, :]
+        assert np.abs(r).max() < 1e-6 * max(1.0, ev[b].max())
+    torch.manual_seed(2)
+    ref = M.DPFMNet()
+    mine = DPFMNet().to(device)
+    mine.load_state_dict(ref.state_dict())
+    out = InferStep(mine, hypotheses=256, seed=1)(fb, op2, crops)
+    torch.cuda.synchronize()
+    mb = model_batch(op2, crops)
+    cpu = {kk: {a: v.cpu() for a, v in d.items() if a in ("xyz", "mass", "evals", "evecs")} for kk, d in mb.items()}
+    with torch.no_grad():
+        C32 = ref(cpu)[0]
+        truth = M.DPFMNet().double()
+        truth.load_state_dict(ref.state_dict())
+        C64 = truth({kk: {a: v.double() for a, v in d.items()} for kk, d in cpu.items()})[0]
+    e_ref = (C32.double() - C64).abs().max().item()
+    assert (out["C"].cpu().double() - C64).abs().max().item() <= 3 * e_ref + 1e-6 * (1 + C64.abs().max().item())
+    assert torch.isfinite(out["T"]).all()
