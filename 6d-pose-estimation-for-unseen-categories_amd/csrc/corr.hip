@@ -153,15 +153,212 @@ __global__ __launch_bounds__(256) void rigid_pair_kernel(const int64_t* __restri
   }
 }
 
-// grid (ceil(nmax / 256), B): score[x] = (sum over tiles in order of part[b][tile][x]) / n.
+// ---- Round 3 production path: packed coordinates, 128 x 128 pair tiles, packed-f32 arithmetic.
+// Round 2's rigid_pair_kernel spent most of a block on its prologue: every entry of both tiles
+// was a dependent gather list -> cand -> cad / pc (three global loads in a chain) for only 16
+// pairs per thread. Here the coordinates of the current list live in a packed array (one
+// 32-B record per entry: {cad_x, pc_x, cad_y, pc_y, cad_z, pc_z, valid, 0}); the first round's is
+// gathered once (rigid_gather_kernel) and each compaction carries the survivors' records
+// along (rigid_compact_pts_kernel), so a pair block loads its two tiles with plain 16-B loads.
+// The pair term pairs the CAD and crop halves as float2 lanes: the differences, squares and
+// sums are v_pk_add_f32 / v_pk_mul_f32 (two separately rounded values per instruction, the
+// reference's ((dx^2 + dy^2) + dz^2) order, -ffp-contract=off), two v_sqrt_f32, and |a - b|
+// of two pairs at once; 8 x 8 pairs per thread.
+constexpr int kRT2 = 128;
+typedef float rf2 __attribute__((ext_vector_type(2)));
+
+struct __attribute__((aligned(16))) RigidRec {
+  rf2 x, y;  // {cad_x, pc_x}, {cad_y, pc_y}
+  rf2 z, v;  // {cad_z, pc_z}, {valid, 0}
+};
+
+// grid (ceil(nmax/256), B): list[i] = i and the packed record of candidate i (round 1).
+__global__ __launch_bounds__(256) void rigid_gather_kernel(const int64_t* __restrict__ cand, int ldc,
+                                                           const int32_t* __restrict__ ncand,
+                                                           const float* __restrict__ cad, int ldcad,
+                                                           const float* __restrict__ pc, int ldpc,
+                                                           int64_t* __restrict__ list, RigidRec* __restrict__ pts) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= ncand[b]) return;
+  const int64_t c = cand[((int64_t)b * ldc + i) * 2], p = cand[((int64_t)b * ldc + i) * 2 + 1];
+  const float* CA = cad + ((int64_t)b * ldcad + c) * 3;
+  const float* PC = pc + ((int64_t)b * ldpc + p) * 3;
+  RigidRec r;
+  r.x = rf2{CA[0], PC[0]};
+  r.y = rf2{CA[1], PC[1]};
+  r.z = rf2{CA[2], PC[2]};
+  r.v = rf2{1.f, 0.f};
+  pts[(int64_t)b * ldc + i] = r;
+  list[(int64_t)b * ldc + i] = i;
+}
+
+// 8 x 8 pairs of one thread: rows i = ty + 16 r, columns j = tx + 16 c. ra[r]: this thread's
+// row sums (over its 8 columns, as float2 halves), ca[k]: its column sums for columns 2k, 2k+1.
+template <bool EDGE>
+__device__ __forceinline__ void rigid_tile_pairs(const RigidRec* __restrict__ si, const RigidRec* __restrict__ sj,
+                                                 int tx, int ty, rf2 (&ra)[8], rf2 (&ca)[4]) {
+  RigidRec cj[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) cj[c] = sj[tx + 16 * c];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const RigidRec ci = si[ty + 16 * r];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float a[2], bb[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const RigidRec& q = cj[2 * k + h];
+        const rf2 dx = q.x - ci.x, dy = q.y - ci.y, dz = q.z - ci.z;
+        const rf2 s = (dx * dx + dy * dy) + dz * dz;  // {|CAD_i - CAD_j|^2, |PC_i - PC_j|^2}
+        a[h] = __builtin_amdgcn_sqrtf(s.x);
+        bb[h] = __builtin_amdgcn_sqrtf(s.y);
+      }
+      rf2 v = rf2{a[0], a[1]} - rf2{bb[0], bb[1]};
+      v = rf2{fabsf(v.x), fabsf(v.y)};
+      if (EDGE) v = v * (rf2{cj[2 * k].v.x, cj[2 * k + 1].v.x} * ci.v.x);  // invalid entries contribute 0
+      ra[r] += v;
+      ca[k] += v;
+    }
+  }
+}
+
+// Grid (T (T + 1) / 2, B) over 128 x 128 tile pairs I <= J (T = ceil(nmax / 128)), XCD-aware
+// (a crop's tile pairs share one XCD's L2); block 256 = 16 x 16 threads. As rigid_pair_kernel:
+// part[b][J][x] = sum over tile J of entry x of tile I, and for I != J part[b][I][y] for the
+// entries y of tile J; every slot written once, summed in tile order by rigid_reduce_kernel.
+// Fixed-order reductions (16-lane butterflies, then the 4 waves' column partials in wave order).
+__global__ __launch_bounds__(256) void rigid_pair2_kernel(const int32_t* __restrict__ nlist, int ldl,
+                                                          const RigidRec* __restrict__ pts, int T,
+                                                          float* __restrict__ part) {
+  __shared__ RigidRec si[kRT2], sj[kRT2];
+  __shared__ float red[4][kRT2];
+  const int3 lb = pk::xcd_block3();
+  const int b = lb.y;
+  const int n = nlist[b];
+  const int t = lb.x;
+  int J = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
+  while ((J + 1) * (J + 2) / 2 <= t) ++J;
+  while (J * (J + 1) / 2 > t) --J;
+  const int I = t - J * (J + 1) / 2;
+  if (J * kRT2 >= n) return;  // block-uniform: tile outside this round's list
+  const RigidRec* P0 = pts + (int64_t)b * ldl;
+  const int tid = threadIdx.x;
+  {
+    const int e = tid & (kRT2 - 1);
+    const int x = (tid < kRT2 ? I : J) * kRT2 + e;
+    RigidRec* dst = tid < kRT2 ? si : sj;
+    RigidRec r;
+    if (x < n) r = P0[x];
+    else r.x = r.y = r.z = r.v = rf2{0.f, 0.f};
+    dst[e] = r;
+  }
+  __syncthreads();
+  const int tx = tid & 15, ty = tid >> 4;
+  rf2 ra[8], ca[4];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) ra[r] = rf2{0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ca[k] = rf2{0.f, 0.f};
+  if ((J + 1) * kRT2 > n) rigid_tile_pairs<true>(si, sj, tx, ty, ra, ca);
+  else rigid_tile_pairs<false>(si, sj, tx, ty, ra, ca);
+  float* P = part + (int64_t)b * T * ldl;
+  // row sums of tile I over tile J: butterfly over the 16 tx lanes (lane tx = 0 keeps a fixed order)
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    float v = ra[r].x + ra[r].y;
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    const int x = I * kRT2 + ty + 16 * r;
+    if (tx == 0 && x < n) P[(int64_t)J * ldl + x] = v;
+  }
+  if (I == J) return;  // block-uniform; the diagonal tile's row sums already cover both orders
+  // column sums of tile J over tile I: the wave's 4 ty rows by butterfly, then the 4 waves in order
+  const int w = pk::wave_id();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v = h ? ca[k].y : ca[k].x;
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if ((tid & 63) < 16) red[w][tx + 16 * (2 * k + h)] = v;
+    }
+  }
+  __syncthreads();
+  if (tid < kRT2) {
+    const float v = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+    const int x = J * kRT2 + tid;
+    if (x < n) P[(int64_t)I * ldl + x] = v;
+  }
+}
+
+// One block per crop: rigid_compact_kernel's ordered compaction, carrying the survivors' packed
+// records into the next round's array.
+__global__ __launch_bounds__(1024) void rigid_compact_pts_kernel(const int64_t* __restrict__ list_in, int ldl,
+                                                                 const int32_t* __restrict__ nin,
+                                                                 const float* __restrict__ score,
+                                                                 const float* __restrict__ thr4, int round,
+                                                                 const RigidRec* __restrict__ pts_in,
+                                                                 int64_t* __restrict__ list_out,
+                                                                 RigidRec* __restrict__ pts_out,
+                                                                 int32_t* __restrict__ nout) {
+  __shared__ int ws[16];
+  __shared__ int carry;
+  __shared__ float thr_s;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int n = nin[b];
+  const float* S = score + (int64_t)b * ldl;
+  if (tid == 0) {
+    carry = 0;
+    thr_s = thr4[b * 4 + round];
+  }
+  __syncthreads();
+  if (round == 2) {
+    int c = 0;
+    for (int i = tid; i < n; i += 1024) c += S[i] < thr_s ? 1 : 0;
+    c = pk::wave_sum_i32_s(c);
+    if (pk::lane_id() == 0) ws[pk::wave_id()] = c;
+    __syncthreads();
+    if (tid == 0) {
+      int tot = 0;
+      for (int w = 0; w < 16; ++w) tot += ws[w];
+      if (tot == 0) thr_s = thr4[b * 4 + 3];
+    }
+    __syncthreads();
+  }
+  const float thr = thr_s;
+  for (int base = 0; base < n; base += 1024) {
+    const int i = base + tid;
+    const bool keep = i < n && S[i] < thr;
+    const uint64_t bal = __ballot(keep);
+    if (pk::lane_id() == 0) ws[pk::wave_id()] = __popcll(bal);
+    __syncthreads();
+    int pre = carry;
+    for (int w = 0; w < pk::wave_id(); ++w) pre += ws[w];
+    if (keep) {
+      const int64_t o = (int64_t)b * ldl + pre + __popcll(bal & ((1ull << pk::lane_id()) - 1ull));
+      list_out[o] = list_in[(int64_t)b * ldl + i];
+      if (pts_out != nullptr) pts_out[o] = pts_in[(int64_t)b * ldl + i];
+    }
+    __syncthreads();
+    if (tid == 1023) carry = pre + __popcll(bal);
+    __syncthreads();
+  }
+  if (tid == 0) nout[b] = carry;
+}
+
+// grid (ceil(nmax / 256), B): score[x] = (sum over tiles in order of part[b][tile][x]) / n,
+// tiles of `rt` entries.
 __global__ __launch_bounds__(256) void rigid_reduce_kernel(const int32_t* __restrict__ nlist, int ldl,
-                                                           const float* __restrict__ part, int T,
+                                                           const float* __restrict__ part, int T, int rt,
                                                            float* __restrict__ score) {
   const int b = blockIdx.y;
   const int n = nlist[b];
   const int x = blockIdx.x * 256 + threadIdx.x;
   if (x >= n) return;
-  const int nt = (n + kRT - 1) / kRT;
+  const int nt = (n + rt - 1) / rt;
   const float* P = part + (int64_t)b * T * ldl + x;
   float acc = 0.f;
   for (int q = 0; q < nt; ++q) acc += P[(int64_t)q * ldl];
@@ -547,9 +744,26 @@ __global__ __launch_bounds__(64) void cgt_solve_kernel(const double* __restrict_
 
 }  // namespace
 
+// scratch: the tile partials [B][T][ldc] f32 (T = ceil(nmax / 128)), then two packed-record
+// arrays [B][ldc] (the current and the next round's list), 16-B aligned
+static int64_t rigid_part_bytes(int B, int nmax, int ldc) {
+  const int64_t b = (int64_t)B * ((nmax + kRT2 - 1) / kRT2) * ldc * (int64_t)sizeof(float);
+  return (b + 255) & ~(int64_t)255;
+}
+
+static int g_rigid_variant = 0;  // 1: round 2's 64-tile gather path (pkdev_rigidity_variant, A/B timing)
+
 extern "C" int64_t pk_rigidity_filter_work_size(int B, int nmax, int ldc) {
   if (B <= 0 || nmax <= 0) return 0;
-  return (int64_t)B * ((nmax + kRT - 1) / kRT) * ldc * (int64_t)sizeof(float);
+  const int64_t v2 = rigid_part_bytes(B, nmax, ldc) + 2 * (int64_t)B * ldc * (int64_t)sizeof(RigidRec);
+  const int64_t v1 = (int64_t)B * ((nmax + kRT - 1) / kRT) * ldc * (int64_t)sizeof(float);
+  return v2 > v1 ? v2 : v1;
+}
+
+extern "C" int pkdev_rigidity_variant(int v) {
+  const int old = g_rigid_variant;
+  if (v >= 0) g_rigid_variant = v;
+  return old;
 }
 
 extern "C" int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* ncand, const float* cad,
@@ -561,7 +775,17 @@ extern "C" int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* n
   PK_REQUIRE(cand && ncand && cad && pc && thr4 && list_a && list_b && n_a && n_b && score);
   hipStream_t s = pk::as_stream(stream);
   const dim3 g((nmax + 255) / 256, B);
-  hipLaunchKernelGGL(iota_kernel, g, dim3(256), 0, s, list_a, ldc, ncand);
+  const int T2 = (nmax + kRT2 - 1) / kRT2;
+  const bool packed = partial != nullptr && T2 > 0 && g_rigid_variant == 0;
+  RigidRec* pa = nullptr;
+  RigidRec* pb = nullptr;
+  if (packed) {
+    pa = reinterpret_cast<RigidRec*>(reinterpret_cast<char*>(partial) + rigid_part_bytes(B, nmax, ldc));
+    pb = pa + (int64_t)B * ldc;
+    hipLaunchKernelGGL(rigid_gather_kernel, g, dim3(256), 0, s, cand, ldc, ncand, cad, ldcad, pc, ldpc, list_a, pa);
+  } else {
+    hipLaunchKernelGGL(iota_kernel, g, dim3(256), 0, s, list_a, ldc, ncand);
+  }
   PK_CHECK_LAUNCH();
   const int32_t* nin = ncand;
   int64_t* lin = list_a;
@@ -570,19 +794,32 @@ extern "C" int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* n
   int32_t* nspare = n_a;
   const int T = (nmax + kRT - 1) / kRT;
   for (int r = 0; r < 3; ++r) {
-    if (partial && T > 0) {  // symmetric pair tiles + ordered reduction
+    if (packed) {
+      hipLaunchKernelGGL(rigid_pair2_kernel, dim3(T2 * (T2 + 1) / 2, B), dim3(256), 0, s, nin, ldc, pa, T2, partial);
+      PK_CHECK_LAUNCH();
+      hipLaunchKernelGGL(rigid_reduce_kernel, g, dim3(256), 0, s, nin, ldc, partial, T2, kRT2, score);
+      PK_CHECK_LAUNCH();
+      hipLaunchKernelGGL(rigid_compact_pts_kernel, dim3(B), dim3(1024), 0, s, lin, ldc, nin, score, thr4, r, pa, lout,
+                         r < 2 ? pb : nullptr, nout);
+      PK_CHECK_LAUNCH();
+      RigidRec* tp = pa;
+      pa = pb;
+      pb = tp;
+    } else if (partial && T > 0) {  // round 2: symmetric 64-tiles with gathers, ordered reduction
       hipLaunchKernelGGL(rigid_pair_kernel, dim3(T * (T + 1) / 2, B), dim3(256), 0, s, lin, ldc, nin, cand, ldc, cad,
                          ldcad, pc, ldpc, T, partial);
       PK_CHECK_LAUNCH();
-      hipLaunchKernelGGL(rigid_reduce_kernel, g, dim3(256), 0, s, nin, ldc, partial, T, score);
+      hipLaunchKernelGGL(rigid_reduce_kernel, g, dim3(256), 0, s, nin, ldc, partial, T, kRT, score);
     } else {
       hipLaunchKernelGGL(rigid_score_kernel, g, dim3(256), 0, s, lin, ldc, nin, cand, ldc, cad, ldcad, pc, ldpc,
                          score);
     }
     PK_CHECK_LAUNCH();
-    hipLaunchKernelGGL(rigid_compact_kernel, dim3(B), dim3(1024), 0, s, lin, ldc, nin, score, thr4, r, lout,
-                       nout);
-    PK_CHECK_LAUNCH();
+    if (!packed) {
+      hipLaunchKernelGGL(rigid_compact_kernel, dim3(B), dim3(1024), 0, s, lin, ldc, nin, score, thr4, r, lout,
+                         nout);
+      PK_CHECK_LAUNCH();
+    }
     nin = nout;
     int64_t* t = lin;
     lin = lout;

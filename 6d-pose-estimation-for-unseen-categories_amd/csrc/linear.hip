@@ -1144,6 +1144,16 @@ __global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restric
   __shared__ float Ws[kThinMaxW];  // Ws[o * Cin + k]
   __shared__ float bs[kLfMaxC];
   const int Cin = CINT > 0 ? CINT : Cin_;
+  // rows layout, compile-time Cin, no prologue (first_lin 3 -> 64): the point's inputs are in
+  // flight while the weight is staged (one memory latency instead of two before the stores)
+  float xe[CINT > 0 ? CINT : 1];
+  if (LAYOUT == 0 && CINT > 0) {
+    const int G = (Cout + 3) >> 2;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t r = t < R * G ? t / G : 0;
+#pragma unroll
+    for (int k = 0; k < (CINT > 0 ? CINT : 1); ++k) xe[k] = (t < R * G && e.pre == nullptr) ? x[r * sx + k] : 0.f;
+  }
   for (int e = threadIdx.x; e < Cout * Cin; e += 256) {
     const int o = e / Cin, k = e - o * Cin;
     Ws[e] = transw ? w[(int64_t)k * Cout + o] : w[e];
@@ -1182,7 +1192,7 @@ __global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restric
     }
 #pragma unroll 4
     for (int k = k0; k < Cin; ++k) {
-      float xv = x[r * sx + k];
+      float xv = (CINT > 0 && e.pre == nullptr) ? xe[CINT > 0 ? k : 0] : x[r * sx + k];
       if (e.pre) {
         const float s = e.pre[r * sx + k];
         xv = xv * (s * (1.f - s));

@@ -35,6 +35,14 @@ class LinearArgs(ctypes.Structure):
                 ("lda2", _I64)]
 
 
+class OverlapHeadArgs(ctypes.Structure):
+    """pk_overlap_head_args (include/posekern.h)."""
+    _fields_ = [("x", _P * 2), ("strides", (_I64 * 3) * 2), ("N", ctypes.c_int32 * 2), ("B", ctypes.c_int32),
+                ("pad", ctypes.c_int32), ("w0", _P), ("b0", _P), ("w1", _P), ("b1", _P), ("n", _P * 2),
+                ("nrm", _P * 2), ("nrows", _P * 2), ("h", _P * 2), ("s", _P * 2), ("ds", _P * 2), ("dnr", _P * 2),
+                ("g", _P * 2), ("dh", _P * 2), ("dx", _P * 2)]
+
+
 # name -> argtypes, mirroring include/posekern.h one for one.
 SIGNATURES = {
     "pk_fps": [_P, _P, _I, _I, _P, _P, _P, _I, _P],
@@ -70,6 +78,8 @@ SIGNATURES = {
     "pk_wbce": [_P, _P, _I, _P, _P, _I, _I, _P, _P, _P, _P],
     "pk_l2_normalize_fwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P],
     "pk_l2_normalize_bwd": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "pk_overlap_head_fwd": [_P, _P],
+    "pk_overlap_head_bwd": [_P, _P],
     "pk_mlp3_fwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P],
     "pk_resolvent_mask": [_P, _I, _P, _I, _I, _I, _F, _P, _P],
     "pk_linear_fwd": [_P, _P, _P, _I, _I64, _I, _I, _I, _I, _I, _P, _P, _P],

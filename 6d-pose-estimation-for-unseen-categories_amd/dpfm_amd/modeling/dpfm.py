@@ -34,6 +34,7 @@ class InstanceNormReLU(nn.InstanceNorm1d):
 
 
 FUSED_ATTN_PROP = True  # AttentionalPropagation + residual as one fused node (attnprop.py)
+FUSED_OVERLAP_HEAD = True  # OverlapPredictorNet for both shapes as one fused node (ops.overlap_head)
 
 
 def MLP(channels: list, do_bn=True):
@@ -152,7 +153,22 @@ class OverlapPredictorNet(nn.Module):
         self.overlap_score_net[0].relu_out = True
         self.overlap_score_net[2].sigmoid_out = True
 
+    def _fusable(self, fx, fy) -> bool:
+        l0, l2 = self.overlap_score_net[0], self.overlap_score_net[2]
+        return (FUSED_OVERLAP_HEAD and fx.is_cuda and fx.dim() == 3 and fy.dim() == 3 and fx.shape[-1] == 32
+                and fy.shape[-1] == 32 and fx.shape[0] == fy.shape[0] and fx.dtype == torch.float32
+                and fy.dtype == torch.float32 and tuple(l0.weight.shape) == (32, 32) and tuple(l2.weight.shape) == (1, 32)
+                and l0.bias is not None and l2.bias is not None and l0.relu_out and l2.sigmoid_out)
+
     def forward(self, overlap_feat_x, overlap_feat_y):
+        if self._fusable(overlap_feat_x, overlap_feat_y):
+            # the whole head for both shapes in one launch per direction (ops.overlap_head); the
+            # rows copies of the normalized features go to the loss's NCE term as below
+            l0, l2 = self.overlap_score_net[0], self.overlap_score_net[2]
+            sx, sy, rx, ry = ops.overlap_head(overlap_feat_x, overlap_feat_y, l0.weight, l0.bias, l2.weight, l2.bias)
+            if rx is not None:
+                overlap_feat_x._pk_nrows, overlap_feat_y._pk_nrows = rx, ry
+            return sx.squeeze(0), sy.squeeze(0)  # [B, N] = the reference's [B, N, 1].squeeze(2).squeeze(0)
         # F.normalize(., p=2, dim=-1) (modeling/dpfm.py:140-141), fused, storage order kept; a rows
         # copy of the normalized features is attached to the input for the loss's NCE term
         # (the same normalization, utils/loss.py:23-24), which then reads whole rows

@@ -665,6 +665,107 @@ def l2_normalize(x: torch.Tensor) -> torch.Tensor:
     return _L2Normalize.apply(x)
 
 
+def _ovh_args(fx, fy, w0, b0, w1, b1):
+    import ctypes
+    a = _lib.OverlapHeadArgs()
+    for s, f in enumerate((fx, fy)):
+        a.x[s] = f.data_ptr()
+        for j in range(3):
+            a.strides[s][j] = f.stride(j)
+        a.N[s] = f.shape[1]
+    a.B = fx.shape[0]
+    a.w0, a.b0, a.w1, a.b1 = w0.data_ptr(), b0.data_ptr(), w1.data_ptr(), b1.data_ptr()
+    return a, ctypes
+
+
+class _OverlapHeadFn(torch.autograd.Function):
+    """OverlapPredictorNet (modeling/dpfm.py:125-145) for both shapes as one autograd node:
+    F.normalize -> Linear(32, 32) + ReLU -> Linear(32, 1) + Sigmoid in one launch per direction
+    (pk_overlap_head_fwd / _bwd, bit-identical to the per-layer path). Outputs the two score maps
+    and the rows copies of the normalized features (the NCE term's input, utils/loss.py:23-24);
+    the weight gradients go to the grouped launch (layers.GroupedWgrad) or are computed here."""
+
+    @staticmethod
+    def forward(ctx, fx, fy, w0, b0, w1, b1):
+        B = fx.shape[0]
+        dev = fx.device
+        a, ctypes = _ovh_args(fx, fy, w0, b0, w1, b1)
+        want = any(ctx.needs_input_grad)  # (grad mode is off inside forward)
+        outs = []
+        for s, f in enumerate((fx, fy)):
+            N = f.shape[1]
+            n = torch.empty_strided(f.shape, f.stride(), dtype=torch.float32, device=dev)
+            nrm = torch.empty((B * N,), dtype=torch.float32, device=dev)
+            nrows = torch.empty((B, N, 32), dtype=torch.float32, device=dev) if want else None
+            h = torch.empty((B, N, 32), dtype=torch.float32, device=dev) if want else None
+            sc = torch.empty((B, N), dtype=torch.float32, device=dev)
+            a.n[s], a.nrm[s] = n.data_ptr(), nrm.data_ptr()
+            a.nrows[s] = nrows.data_ptr() if nrows is not None else None
+            a.h[s] = h.data_ptr() if h is not None else None
+            a.s[s] = sc.data_ptr()
+            outs.append((n, nrm, nrows, h, sc))
+        call("pk_overlap_head_fwd", ctypes.addressof(a), _lib.stream(dev),
+             work=("hbm", 4 * B * (fx.shape[1] + fy.shape[1]) * (32 + 32 + (64 if want else 0) + 2)))
+        ctx.params = (w0, b0, w1, b1)
+        ctx.shapes = (tuple(fx.shape), tuple(fx.stride()), tuple(fy.shape), tuple(fy.stride()))
+        (nx, nrx, rx, hx, sx), (ny, nry, ry, hy, sy) = outs
+        ctx.save_for_backward(nx, nrx, rx, hx, sx, ny, nry, ry, hy, sy)
+        return sx, sy, rx, ry
+
+    @staticmethod
+    def backward(ctx, dsx, dsy, drx, dry):
+        from . import layers
+        nx, nrx, rx, hx, sx, ny, nry, ry, hy, sy = ctx.saved_tensors
+        w0, b0, w1, b1 = ctx.params
+        dev = nx.device
+        a, ctypes = _ovh_args(nx, ny, w0, b0, w1, b1)
+        B = nx.shape[0]
+        res = []
+        for s, (n, nrm, rows, h, sc, ds, dr) in enumerate(((nx, nrx, rx, hx, sx, dsx, drx),
+                                                           (ny, nry, ry, hy, sy, dsy, dry))):
+            N = n.shape[1]
+            ds = torch.zeros((B, N), dtype=torch.float32, device=dev) if ds is None else ds.contiguous()
+            dr = dr.contiguous() if dr is not None else None
+            g = torch.empty((B, N, 1), dtype=torch.float32, device=dev)
+            dh = torch.empty((B, N, 32), dtype=torch.float32, device=dev)
+            dx = torch.empty_strided(n.shape, n.stride(), dtype=torch.float32, device=dev)
+            a.n[s], a.nrm[s], a.h[s], a.s[s] = n.data_ptr(), nrm.data_ptr(), h.data_ptr(), sc.data_ptr()
+            a.ds[s], a.dnr[s] = ds.data_ptr(), (dr.data_ptr() if dr is not None else None)
+            a.g[s], a.dh[s], a.dx[s] = g.data_ptr(), dh.data_ptr(), dx.data_ptr()
+            res.append((rows, h, g, dh, dx, ds, dr))
+        call("pk_overlap_head_bwd", ctypes.addressof(a), _lib.stream(dev),
+             work=("hbm", 4 * B * (nx.shape[1] + ny.shape[1]) * (32 * 5 + 4)))
+        gw0 = gb0 = gw1 = gb1 = None
+        side0 = layers._side_owns(w0, b0)
+        side1 = layers._side_owns(w1, b1)
+        for rows, h, g, dh, _, _, _ in res:
+            if side1:
+                layers._SIDE.launch(h, g, w1, b1, channels_first=False)
+            else:
+                dw, db = linear_wgrad(h, g, channels_first=False, want_bias=True)
+                gw1 = dw.view(w1.shape) if gw1 is None else gw1 + dw.view(w1.shape)
+                gb1 = db if gb1 is None else gb1 + db
+            if side0:
+                layers._SIDE.launch(rows, dh, w0, b0, channels_first=False)
+            else:
+                dw, db = linear_wgrad(rows, dh, channels_first=False, want_bias=True)
+                gw0 = dw.view(w0.shape) if gw0 is None else gw0 + dw.view(w0.shape)
+                gb0 = db if gb0 is None else gb0 + db
+        return res[0][4], res[1][4], gw0, gb0, gw1, gb1
+
+
+def overlap_head(fx: torch.Tensor, fy: torch.Tensor, w0, b0, w1, b1):
+    """(s_x [B, N1], s_y [B, N2], nrows_x, nrows_y) of OverlapPredictorNet's score net applied to
+    F.normalize(f, dim=-1) of both shapes, f32 [B, N, 32] in rows or channels-first storage."""
+    if (fx.dim() != 3 or fy.dim() != 3 or fx.shape[-1] != 32 or fy.shape[-1] != 32 or fx.shape[0] != fy.shape[0]
+            or fx.dtype != torch.float32 or fy.dtype != torch.float32):
+        raise _lib.PoseKernError("overlap_head takes f32 [B, N, 32] features of both shapes")
+    fx, _ = _l2_layout(fx)
+    fy, _ = _l2_layout(fy)
+    w0, b0, w1, b1 = (t.contiguous() for t in (w0, b0, w1, b1))
+    return _OverlapHeadFn.apply(fx, fy, w0, b0, w1, b1)
+
+
 def mlp3_fwd(x_in: torch.Tensor, x_diff: torch.Tensor, w1, b1, w2, b2, w3, b3):
     """pk_mlp3_fwd: (cat, h1, h2, y) of the DiffusionNet block MLP with its residual."""
     x_in, x_diff = x_in.contiguous(), x_diff.contiguous()

@@ -244,6 +244,43 @@ int pk_l2_normalize_fwd(const float* x, const int64_t* strides, int B, int N, in
 int pk_l2_normalize_bwd(const float* y, const float* dy, const float* nrm, const int64_t* strides, int B, int N,
                         int C, float* dx, const float* dy_rows, void* stream);
 
+/* H8 overlap head, fused (modeling/dpfm.py:125-145 OverlapPredictorNet: F.normalize(x, dim=-1)
+ * -> Linear(32, 32) -> ReLU -> Linear(32, 1) -> Sigmoid), both shapes in one launch per
+ * direction. Replaces pk_l2_normalize_fwd + two pk_linear_ex launches per shape (forward) and
+ * the sigmoid-backward thin layer + the 32 -> 32 input gradient + pk_l2_normalize_bwd
+ * (backward) with the same arithmetic in the same order (bit-identical outputs).
+ * Per shape s (0: CAD, 1: crop): x[s] f32 [B, N[s], 32] at element strides[s] {batch, point,
+ * channel} (rows or channels-first storage); w0 [32, 32], b0 [32], w1 [1, 32], b1 [1].
+ * Forward writes n[s] (the normalized features, x's storage), nrm[s] [B N] (||x||),
+ * s[s] [B N] (the scores); nrows[s] / h[s] (may be NULL): the normalized features and the
+ * hidden ReLU output as rows [B N, 32] (the NCE term's input and the weight gradients' input).
+ * Backward reads n, nrm, h, s and ds[s] [B N] (d loss / d score), dnr[s] (may be NULL: a
+ * second gradient on the rows copy of n, the NCE term's), writes g[s] [B N] (d loss / d the
+ * last layer's pre-activation), dh[s] [B N, 32] (d loss / d the first layer's
+ * pre-activation, ReLU applied) and dx[s] (x's storage). */
+typedef struct pk_overlap_head_args {
+  const float* x[2];
+  int64_t strides[2][3];
+  int32_t N[2];
+  int32_t B, pad;
+  const float* w0;
+  const float* b0;
+  const float* w1;
+  const float* b1;
+  float* n[2];
+  float* nrm[2];
+  float* nrows[2];
+  float* h[2];
+  float* s[2];
+  const float* ds[2];
+  const float* dnr[2];
+  float* g[2];
+  float* dh[2];
+  float* dx[2];
+} pk_overlap_head_args;
+int pk_overlap_head_fwd(const pk_overlap_head_args* a, void* stream);
+int pk_overlap_head_bwd(const pk_overlap_head_args* a, void* stream);
+
 /* H7 DiffusionNet block MLP forward, fused (upstream DiffusionNetBlock.forward at
  * models/dpfm.py:22-30: mlp(cat[x_in, x_diffuse]) + x_in, MiniMLP 128 -> 64 -> ReLU -> 64 ->
  * ReLU -> 64). x_in / x_diff f32 [R, C], C = 64; W1 [64, 128], W2 / W3 [64, 64], biases

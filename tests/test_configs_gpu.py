@@ -113,6 +113,45 @@ def test_rigidity_filter_configs(device, V2):
     assert 0.2 * V2 < kept < 5 * V2
 
 
+def test_rigidity_filter_ragged_batch(device):
+    """Crops with different candidate counts in one launch (empty, single, tile-edge ±1 of the
+    128-entry pair tiles, and a 2-tile-plus crop): each crop's survivors vs the oracle; the
+    round-2 gather path (pkdev_rigidity_variant(1)) on the same batch agrees."""
+    import ctypes
+    from dpfm_amd import _lib, ops
+    sizes = [0, 1, 127, 129, 640, 1000]
+    scenes = [_rigid_scene(max((s + 4) // 5, 1), 7 + i) for i, s in enumerate(sizes)]
+    Lc = max(sizes)
+    cand = np.zeros((len(sizes), Lc, 2), dtype=np.int64)
+    cads, pcs = [], []
+    for i, (s, sc) in enumerate(zip(sizes, scenes)):
+        cand[i, :s] = sc[2][:s]
+        cads.append(np.pad(sc[0], ((0, 600 - sc[0].shape[0]), (0, 0))))
+        pcs.append(np.pad(sc[1], ((0, 600 - sc[1].shape[0]), (0, 0))))
+    dcand = torch.from_numpy(cand).to(device)
+    ncand = torch.tensor(sizes, dtype=torch.int32, device=device)
+    dcad = torch.from_numpy(np.stack(cads)).to(device)
+    dpc = torch.from_numpy(np.stack(pcs)).to(device)
+    thr = ops.rigidity_thresholds([sc[3] for sc in scenes], device)
+    rows, n = ops.rigidity_filter(dcand, ncand, dcad, dpc, thr)
+    rows, n = rows.cpu().numpy(), n.cpu().numpy()
+    assert n[0] == 0
+    for i, (s, sc) in enumerate(zip(sizes, scenes)):
+        if s == 0:
+            continue
+        _rigidity_parity(sc[0], sc[1], sc[2][:s], rows[i], int(n[i]), sc[3])
+    L = _lib.lib()
+    L.pkdev_rigidity_variant.argtypes = [ctypes.c_int]
+    L.pkdev_rigidity_variant(1)
+    try:
+        rows1, n1 = ops.rigidity_filter(dcand, ncand, dcad, dpc, thr)
+    finally:
+        L.pkdev_rigidity_variant(0)
+    rows1, n1 = rows1.cpu().numpy(), n1.cpu().numpy()
+    for i in range(len(sizes)):
+        assert abs(int(n1[i]) - int(n[i])) <= max(2, int(n[i]) // 100), (i, n1[i], n[i])
+
+
 def test_ransac_configs4(device, coracle):
     """configs[4]'s pose stage: 1024 hypotheses over n = 4096 correspondences (4096-vertex CAD)
     vs the C oracle on the same hash-drawn hypotheses: same best hypothesis and fitness, pose

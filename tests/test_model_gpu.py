@@ -531,6 +531,51 @@ def test_fused_encoder_matches_module_path(device, B, N, monkeypatch):
         assert (g1 - g0).abs().max().item() <= 2e-5 * scale, (k, (g1 - g0).abs().max().item(), scale)
 
 
+@pytest.mark.parametrize("cf,N1,N2", [(True, 1024, 1024), (True, 300, 203), (False, 257, 130)])
+def test_fused_overlap_head_matches_layer_path(device, cf, N1, N2, monkeypatch):
+    """OverlapPredictorNet (modeling/dpfm.py:125-145) for both shapes in one launch per direction
+    (ops.overlap_head) against the per-layer path (l2 normalize, 32 -> 32 MFMA layer, thin
+    32 -> 1 sigmoid layer) on the same weights and inputs, channels-first and rows storage, ragged
+    N: scores, the NCE rows copies and the feature gradients (with an NCE-like rows gradient
+    added) bit-identical — same operations in the same order; weight gradients within 1e-5 of
+    their scale (the weight-gradient reduction reads rows instead of channels-first operands)."""
+    from dpfm_amd.modeling import dpfm as mdp
+    torch.manual_seed(5)
+    head = mdp.OverlapPredictorNet(32).to(device)
+    B = 3
+    g = torch.Generator().manual_seed(9)
+
+    def feats(N):
+        t = torch.randn(B, 32, N, generator=g) if cf else torch.randn(B, N, 32, generator=g)
+        if cf:  # a few zero points (the clamped norm branch)
+            t[0, :, :3] = 0.0
+        else:
+            t[0, :3, :] = 0.0
+        t = t.to(device)
+        return t.transpose(1, 2) if cf else t
+
+    fx0, fy0 = feats(N1), feats(N2)
+    ws = (torch.randn(B, N1, generator=g).to(device), torch.randn(B, N2, generator=g).to(device))
+    wr = (torch.randn(B, N1, 32, generator=g).to(device), torch.randn(B, N2, 32, generator=g).to(device))
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(mdp, "FUSED_OVERLAP_HEAD", fused)
+        head.zero_grad(set_to_none=True)
+        fx, fy = fx0.detach().clone().requires_grad_(True), fy0.detach().clone().requires_grad_(True)
+        sx, sy = head(fx, fy)
+        rx, ry = fx._pk_nrows, fy._pk_nrows
+        loss = (sx * ws[0]).sum() + (sy * ws[1]).sum() + (rx * wr[0]).sum() + (ry * wr[1]).sum()
+        loss.backward()
+        res[fused] = ([t.detach().clone() for t in (sx, sy, rx, ry, fx.grad, fy.grad)],
+                      {k: p.grad.detach().clone() for k, p in head.named_parameters()})
+    for a, b in zip(res[True][0], res[False][0]):
+        assert a.shape == b.shape and torch.equal(a, b), (a - b).abs().max().item()
+    for k, g0 in res[False][1].items():
+        g1 = res[True][1][k]
+        scale = float(g0.abs().max()) + 1e-30
+        assert (g1 - g0).abs().max().item() <= 1e-5 * scale, (k, (g1 - g0).abs().max().item(), scale)
+
+
 def test_nce_on_prenormalized_rows_matches_raw(device):
     """The NCE term fed the overlap head's F.normalize'd rows copy (ops.l2_normalize_two,
     pk_nce_loss prenorm = 1, its gradient joining the l2-normalize backward) against the term
