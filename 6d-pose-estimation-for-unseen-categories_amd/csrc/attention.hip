@@ -68,7 +68,8 @@ __device__ __forceinline__ Tile load_tile(const float* __restrict__ src, int HL,
   for (int j = 0; j < 4; ++j) {
     const int e = threadIdx.x + 256 * j;
     const int d = e >> 6, r = e & 63;
-    t.x[j] = r0 + r < L ? src[(int64_t)d * HL + r0 + r] : 0.f;
+    const float v = src[(int64_t)d * HL + (r0 + r < L ? r0 + r : 0)];  // unconditional (no branch + wait)
+    t.x[j] = r0 + r < L ? v : 0.f;
   }
   return t;
 }
@@ -100,7 +101,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
   const float* vb = v + (int64_t)b * sbv + (int64_t)h * M;
   float qr[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) qr[s] = qi < N ? qb[(int64_t)(4 * s + g) * H * N + qi] * kScale : 0.f;
+  for (int s = 0; s < 4; ++s) {  // unconditional load at a clamped query
+    const float qv = qb[(int64_t)(4 * s + g) * H * N + (qi < N ? qi : 0)];
+    qr[s] = qi < N ? qv * kScale : 0.f;
+  }
   // one accumulator per 16-key sub-tile: four independent MFMA chains (a serial chain over
   // M ~ 5000 keys of a real CAD measured 4-5x torch's gradient error; split, it is within 1.5x)
   f32x4 acc[4];
@@ -201,14 +205,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
   float dl = 0.f;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int64_t a = qoff + (int64_t)(4 * s + g) * H * N + qi;
-    qr[s] = qi < N ? q[a] * kScale : 0.f;
-    dor[s] = qi < N ? dout[a] : 0.f;
-    dl = fmaf(dor[s], qi < N ? o[a] : 0.f, dl);
+    // unconditional loads at a clamped query (a conditional load is a branch + a wait each)
+    const int64_t a = qoff + (int64_t)(4 * s + g) * H * N + (qi < N ? qi : 0);
+    const float qv = q[a], dv0 = dout[a], ov = o[a];
+    qr[s] = qi < N ? qv * kScale : 0.f;
+    dor[s] = qi < N ? dv0 : 0.f;
+    dl = fmaf(dor[s], qi < N ? ov : 0.f, dl);
   }
   dl = grp_sum(dl);  // delta = sum_d dO * O for query qi
-  const float2 ms = qi < N ? reinterpret_cast<const float2*>(lse)[((int64_t)b * H + h) * N + qi]
-                           : make_float2(__builtin_huge_valf(), 0.f);
+  const float2 msl = reinterpret_cast<const float2*>(lse)[((int64_t)b * H + h) * N + (qi < N ? qi : 0)];
+  const float2 ms = qi < N ? msl : make_float2(__builtin_huge_valf(), 0.f);
   if (qi < N && g == 0) delta[((int64_t)b * H + h) * N + qi] = dl;
   f32x4 acc[4];  // independent chains per 16-key sub-tile (accuracy, see the forward)
 #pragma unroll
@@ -284,10 +290,25 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
   float kr[4], vr[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int64_t a = (int64_t)h * M + (int64_t)(4 * s + g) * H * M + kj;
-    kr[s] = kj < M ? k[(int64_t)b * sbk + a] * kScale : 0.f;
-    vr[s] = kj < M ? v[(int64_t)b * sbv + a] : 0.f;
+    const int64_t a = (int64_t)h * M + (int64_t)(4 * s + g) * H * M + (kj < M ? kj : 0);
+    const float kv = k[(int64_t)b * sbk + a], vv = v[(int64_t)b * sbv + a];  // unconditional
+    kr[s] = kj < M ? kv * kScale : 0.f;
+    vr[s] = kj < M ? vv : 0.f;
   }
+  // the per-query (m, 1 / sum) and delta of a 64-query tile, one query per thread < kT, loaded a
+  // tile ahead like Q / dO (a load issued between the loop's barriers exposed a full memory
+  // latency per tile)
+  auto load_md = [&](int q0, float2& msv, float& dv) {
+    const int qq = q0 + (int)threadIdx.x;
+    const int qc = qq < N ? qq : 0;
+    const float2 m2 = lb[qc];
+    const float d1 = db[qc];
+    msv = qq < N ? m2 : make_float2(__builtin_huge_valf(), 0.f);  // exp2(-inf) = 0
+    dv = qq < N ? d1 : 0.f;
+  };
+  float2 msn = make_float2(0.f, 0.f);
+  float dn = 0.f;
+  if (threadIdx.x < kT) load_md(0, msn, dn);
   // two independent chains (even / odd 16-query sub-tiles; accuracy, see the forward): four
   // would cost this kernel its third wave per SIMD
   f32x4 dka[2], dva[2];
@@ -299,16 +320,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
     store_tile(qt, Qs, QT);
     store_tile(gt, Os, OT);
     if (threadIdx.x < kT) {
-      const int qq = q0 + threadIdx.x;
-      const float2 ms = qq < N ? lb[qq] : make_float2(__builtin_huge_valf(), 0.f);  // exp2(-inf) = 0
-      Ls[threadIdx.x] = ms.x;
-      Is[threadIdx.x] = ms.y;
-      Ds[threadIdx.x] = qq < N ? db[qq] : 0.f;
+      Ls[threadIdx.x] = msn.x;
+      Is[threadIdx.x] = msn.y;
+      Ds[threadIdx.x] = dn;
     }
     __syncthreads();
     if (q0 + kT < N) {
       qt = load_tile(qb, H * N, N, q0 + kT);
       gt = load_tile(gb, H * N, N, q0 + kT);
+      if (threadIdx.x < kT) load_md(q0 + kT, msn, dn);
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {

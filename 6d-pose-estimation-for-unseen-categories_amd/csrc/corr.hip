@@ -264,12 +264,15 @@ __global__ __launch_bounds__(256) void rigid_pair2_kernel(const int32_t* __restr
   if ((J + 1) * kRT2 > n) rigid_tile_pairs<true>(si, sj, tx, ty, ra, ca);
   else rigid_tile_pairs<false>(si, sj, tx, ty, ra, ca);
   float* P = part + (int64_t)b * T * ldl;
-  // row sums of tile I over tile J: butterfly over the 16 tx lanes (lane tx = 0 keeps a fixed order)
+  // row sums of tile I over tile J: the 16 tx lanes are one DPP row (quad_perm / half-mirror /
+  // mirror adds: VALU only, no LDS round trips); lane tx = 0's association order is fixed
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     float v = ra[r].x + ra[r].y;
-#pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    v += __int_as_float((int)PK_DPP(__float_as_int(v), 0xB1));
+    v += __int_as_float((int)PK_DPP(__float_as_int(v), 0x4E));
+    v += __int_as_float((int)PK_DPP(__float_as_int(v), 0x141));
+    v += __int_as_float((int)PK_DPP(__float_as_int(v), 0x140));
     const int x = I * kRT2 + ty + 16 * r;
     if (tx == 0 && x < n) P[(int64_t)J * ldl + x] = v;
   }
@@ -684,7 +687,10 @@ __global__ __launch_bounds__(64) void cgt_solve_kernel(const double* __restrict_
   const bool row_ok = r < kF;
   double a[kF];
 #pragma unroll
-  for (int c = 0; c < kF; ++c) a[c] = row_ok ? GH[(int64_t)b * 2 * kFF + r * 2 * kF + h * kF + c] : 0.0;
+  for (int c = 0; c < kF; ++c) {  // unconditional at a clamped row (no branch + wait per load)
+    const double v = GH[(int64_t)b * 2 * kFF + (row_ok ? r : 0) * 2 * kF + h * kF + c];
+    a[c] = row_ok ? v : 0.0;
+  }
   bool used = !row_ok;
   int var = -1;
   double pmin = __builtin_inf(), pmax = 0.0;

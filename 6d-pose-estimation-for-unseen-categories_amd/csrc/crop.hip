@@ -193,7 +193,10 @@ __device__ __forceinline__ int sor_gather(const int32_t* __restrict__ row, int u
                                           double (&s)[kSorBatch]) {
   int j[kSorBatch];
 #pragma unroll
-  for (int t = 0; t < kSorBatch; ++t) j[t] = uu + t <= u1 ? row[uu + t] : -1;
+  for (int t = 0; t < kSorBatch; ++t) {  // unconditional at a clamped pixel (no branch + wait per load)
+    const int32_t v = row[uu + t <= u1 ? uu + t : uu];
+    j[t] = uu + t <= u1 ? v : -1;
+  }
   double c[kSorBatch][3];
 #pragma unroll
   for (int t = 0; t < kSorBatch; ++t) {
@@ -393,10 +396,18 @@ struct SeqShared {
 template <class F>
 __device__ double seq_sum_exact(F term, int n, SeqShared& sh) {
   const int tid = threadIdx.x, lane = pk::lane_id(), w = pk::wave_id();
-  if (tid == 0) {
+  if (tid == 0) {  // the first terms one by one, 16 loads in flight at a time (same order)
     double s = 0.0;
     const int m = min(n, kSeqWarm);
-    for (int k = 0; k < m; ++k) s = s + term(k);
+    int k = 0;
+    for (; k + 16 <= m; k += 16) {
+      double tv[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) tv[i] = term(k + i);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s = s + tv[i];
+    }
+    for (; k < m; ++k) s = s + term(k);
     sh.s = s;
     sh.k = m;
   }
@@ -414,13 +425,16 @@ __device__ double seq_sum_exact(F term, int n, SeqShared& sh) {
     int64_t mv[kSeqPer];
     bool bad[kSeqPer];
     int64_t tot = 0;
+    double tv[kSeqPer];  // the chunk's terms, unconditionally at clamped indices (k < n is valid)
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) tv[i] = term(j0 + i < n ? j0 + i : k);
 #pragma unroll
     for (int i = 0; i < kSeqPer; ++i) {
       const int j = j0 + i;
       mv[i] = 0;
       bad[i] = false;
       if (j < n) {
-        const double t = term(j);
+        const double t = tv[i];
         const double r = ldexp(t, 53 - e);
         if (s == 0.0) {  // 0 + t: exact, but the binade is unknown; zeros leave s at 0
           bad[i] = t != 0.0;

@@ -1,0 +1,96 @@
+// Development probes (not in include/posekern.h): memory-stream shapes of the per-point layer
+// kernels without their arithmetic, to separate what bounds linear_fwd_rows_kernel (20 us for a
+// 128 -> 64 layer over 65,536 rows = 50 MB, 2.5 TB/s, while a torch copy of that size reaches
+// 6 TB/s). y[r][o] = x[r][o] + x[r][64 + o] for o < 64 (x [R, 128], y [R, 64]):
+//   mode 0  lane-linear 16-B loads and stores, one thread per (row, 4 outputs), many blocks
+//   mode 1  the rows kernel's access shapes: one wave per 16-row tile, fragment loads (lane
+//           (m, g) reads float4 16 q + 4 g of row m: 16 rows x 64 B per instruction), 4-B stores
+//           in MFMA D layout (row 4 g + r, column 16 t + m), one tile per wave
+//   mode 2  mode 1 plus the layer kernels' weight staging (64 x 132 floats into LDS from an L2-
+//           resident weight, one barrier) before the tile is consumed
+//   mode 3  mode 1 with 16-B stores (a lane owns 4 consecutive outputs of one row)
+#include "common.hpp"
+
+namespace {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+__global__ __launch_bounds__(256) void probe_linear_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                           int64_t R) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (row, quad)
+  if (t >= R * 16) return;
+  const int64_t r = t >> 4;
+  const int q = (int)(t & 15);
+  const float4 a = *reinterpret_cast<const float4*>(x + r * 128 + 4 * q);
+  const float4 b = *reinterpret_cast<const float4*>(x + r * 128 + 64 + 4 * q);
+  *reinterpret_cast<float4*>(y + r * 64 + 4 * q) = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void probe_tile_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                         float* __restrict__ y, int64_t R) {
+  extern __shared__ float Ws[];
+  const int lane = pk::lane_id(), m = lane & 15, g = lane >> 4;
+  const int64_t tile = (int64_t)blockIdx.x * 4 + pk::wave_id();
+  const int64_t T = (R + 15) >> 4;
+  f32x4 v[8];
+  const int64_t row = tile * 16 + m;
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    v[q] = (tile < T && row < R) ? *reinterpret_cast<const f32x4*>(x + row * 128 + 16 * q + 4 * g)
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+  if (MODE == 2) {  // 64 x 128 weight, float4 reads, row stride 132 in LDS
+    f32x4 s[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      s[i] = *reinterpret_cast<const f32x4*>(w + 4 * (int64_t)e);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = threadIdx.x + 256 * i, o = e >> 5, k4 = e & 31;
+      *reinterpret_cast<f32x4*>(&Ws[o * 132 + 4 * k4]) = s[i];
+    }
+    __syncthreads();
+  }
+  if (tile >= T) return;
+  // lane (m, g) holds x[row m][16 q + 4 g + i]; the probe's output: column c = 16 t + m (t < 4) of row
+  // 4 g + r gets a value built from the lane's registers (no cross-lane exchange: same traffic)
+  float wsum = MODE == 2 ? Ws[m * 132 + g] : 0.f;
+  if (MODE == 3) {
+    const int64_t pr = tile * 16 + m;
+    if (pr < R) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const f32x4 a = v[2 * t], b = v[2 * t + 1];
+        *reinterpret_cast<f32x4*>(y + pr * 64 + 16 * t + 4 * g) = f32x4{a[0] + b[0], a[1] + b[1], a[2] + b[2], a[3] + b[3]};
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t pr = tile * 16 + 4 * g + r;
+      if (pr < R) y[pr * 64 + 16 * t + m] = v[2 * t][r] + v[2 * t + 1][r] + wsum;
+    }
+}
+
+}  // namespace
+
+extern "C" int pkdev_probe_linear(const float* x, const float* w, float* y, int64_t R, int mode, void* stream) {
+  if (R <= 0 || mode < 0 || mode > 3) return PK_ERR_ARG;
+  hipStream_t s = pk::as_stream(stream);
+  if (mode == 0) {
+    hipLaunchKernelGGL(probe_linear_kernel, dim3((unsigned)((R * 16 + 255) / 256)), dim3(256), 0, s, x, y, R);
+  } else {
+    const unsigned nb = (unsigned)(((R + 15) / 16 + 3) / 4);
+    const size_t lds = mode == 2 ? sizeof(float) * 64 * 132 : 0;
+    if (mode == 1) hipLaunchKernelGGL(probe_tile_kernel<1>, dim3(nb), dim3(256), lds, s, x, w, y, R);
+    else if (mode == 2) hipLaunchKernelGGL(probe_tile_kernel<2>, dim3(nb), dim3(256), lds, s, x, w, y, R);
+    else hipLaunchKernelGGL(probe_tile_kernel<3>, dim3(nb), dim3(256), lds, s, x, w, y, R);
+  }
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}

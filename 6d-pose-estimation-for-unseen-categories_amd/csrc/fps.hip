@@ -23,6 +23,8 @@
 // repeats, leaving the next centroid in a scalar register.
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int kFpsMaxLds = 13312;  // points whose SoA copy fits in LDS (156 KiB)
@@ -153,14 +155,23 @@ __global__ __launch_bounds__(NT) void fps_pruned_kernel(
   float bx0 = 0.f, bx1 = 0.f, by0 = 0.f, by1 = 0.f, bz0 = 0.f, bz1 = 0.f;
   uint32_t bmb = 0u, bmi = 0xffffffffu;
   bool bval = false;
+  // every point's coordinates first, unconditionally at a clamped index (a conditional load is a
+  // branch + a wait: PPT serial memory round trips before the first iteration)
+  if (n > 0) {  // block-uniform (an empty crop's base may be the end of the buffer)
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const int idx = tid + k * NT;
+      const int ic = idx < n ? idx : 0;
+      px[k] = p[3 * ic + 0];
+      py[k] = p[3 * ic + 1];
+      pz[k] = p[3 * ic + 2];
+    }
+  }
 #pragma unroll
   for (int k = 0; k < PPT; ++k) {
     const int idx = tid + k * NT;
     const bool ok = idx < n;
     if (ok) {
-      px[k] = p[3 * idx + 0];
-      py[k] = p[3 * idx + 1];
-      pz[k] = p[3 * idx + 2];
       pd[k] = 1e10f;
       sx[idx] = px[k];
       sy[idx] = py[k];
@@ -274,12 +285,21 @@ __global__ __launch_bounds__(NT) void fps_lane_kernel(
   const float inf = __builtin_huge_valf();
   float bx0 = inf, bx1 = -inf, by0 = inf, by1 = -inf, bz0 = inf, bz1 = -inf;
   const int i0 = tid * PPT;
+  if (n > 0) {  // unconditional loads at a clamped index (block-uniform guard: empty crop)
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const int ic = i0 + k < n ? i0 + k : 0;
+      px[k] = p[3 * ic + 0];
+      py[k] = p[3 * ic + 1];
+      pz[k] = p[3 * ic + 2];
+    }
+  }
 #pragma unroll
   for (int k = 0; k < PPT; ++k) {
     const bool ok = i0 + k < n;
-    px[k] = ok ? p[3 * (i0 + k) + 0] : 0.f;
-    py[k] = ok ? p[3 * (i0 + k) + 1] : 0.f;
-    pz[k] = ok ? p[3 * (i0 + k) + 2] : 0.f;
+    px[k] = ok ? px[k] : 0.f;
+    py[k] = ok ? py[k] : 0.f;
+    pz[k] = ok ? pz[k] : 0.f;
     pd[k] = ok ? 1e10f : -1.f;  // empty slot: min(-1, d >= 0) keeps it at -1, never selected
     if (ok) {
       bx0 = fminf(bx0, px[k]); bx1 = fmaxf(bx1, px[k]);
@@ -400,12 +420,21 @@ __global__ __launch_bounds__(NT) void fps_flat_kernel(
   float px[PPT], py[PPT], pz[PPT], pd[PPT];
   float bx0 = inf, bx1 = -inf, by0 = inf, by1 = -inf, bz0 = inf, bz1 = -inf;
   const int i0 = tid * PPT;
+  if (n > 0) {  // unconditional loads at a clamped index (block-uniform guard: empty crop)
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const int ic = i0 + k < n ? i0 + k : 0;
+      px[k] = p[3 * ic + 0];
+      py[k] = p[3 * ic + 1];
+      pz[k] = p[3 * ic + 2];
+    }
+  }
 #pragma unroll
   for (int k = 0; k < PPT; ++k) {
     const bool ok = i0 + k < n;
-    px[k] = ok ? p[3 * (i0 + k) + 0] : 0.f;
-    py[k] = ok ? p[3 * (i0 + k) + 1] : 0.f;
-    pz[k] = ok ? p[3 * (i0 + k) + 2] : 0.f;
+    px[k] = ok ? px[k] : 0.f;
+    py[k] = ok ? py[k] : 0.f;
+    pz[k] = ok ? pz[k] : 0.f;
     pd[k] = ok ? 1e10f : -1.f;  // empty slot: min(-1, d >= 0) keeps it at -1, never selected
     if (ok) {
       sx[i0 + k] = px[k];
@@ -539,6 +568,13 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
   if (nmax <= 8192) return launch_fps_flat<1024, 8>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
 #endif
 #define PK_FPS(NT, PPT) return launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s)
+  // development knob (read once): PK_FPS_NT=256 / 512 runs the pruned kernel with fewer waves per
+  // crop above 4096 points (less of each CU held while crop formation overlaps the step)
+  static const int fps_nt = getenv("PK_FPS_NT") ? atoi(getenv("PK_FPS_NT")) : 1024;
+  if (nmax > 4096 && nmax <= 8192 && fps_nt == 512) PK_FPS(512, 16);
+  if (nmax > 4096 && nmax <= 13312 && fps_nt == 512) PK_FPS(512, 26);
+  if (nmax > 4096 && nmax <= 8192 && fps_nt == 256) PK_FPS(256, 32);
+  if (nmax > 4096 && nmax <= 13312 && fps_nt == 256) PK_FPS(256, 52);
   // 1024-thread workgroups above 4096 points: measured 0.712 us per FPS step against 0.78
   // (512 threads) and 1.09 (256) on the bench's crops (n <= 6588, profiles/r02_kbench_fps.txt)
   if (nmax <= 1024) PK_FPS(256, 4);

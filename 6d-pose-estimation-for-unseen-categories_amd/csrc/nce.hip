@@ -66,11 +66,16 @@ __device__ __forceinline__ const float* nce_row_ptr(const FeatView& f, const int
 
 // one feature row into dst[0..31]: x / max(||x||, 1e-12) (F.normalize, sequential fmaf norm),
 // or as is under prenorm; returns the pre-normalization norm (1 under prenorm)
-__device__ __forceinline__ float stage_row(const float* p, int64_t sc, bool ok, int prenorm, float* dst) {
+__device__ __forceinline__ float stage_row(const float* p, int64_t sc, bool ok, int prenorm, float* dst,
+                                           const float* safe) {
   float x[kC];
   float ss = 0.f;
+  const float* q = ok ? p : safe;  // unconditional loads at a valid address (no branch + wait per load)
 #pragma unroll
-  for (int c = 0; c < kC; ++c) x[c] = ok ? p[c * sc] : 0.f;
+  for (int c = 0; c < kC; ++c) {
+    const float v = q[c * sc];
+    x[c] = ok ? v : 0.f;
+  }
 #pragma unroll
   for (int c = 0; c < kC; ++c) ss = fmaf(x[c], x[c], ss);
   const float nrm = prenorm ? 1.f : sqrtf(ss);
@@ -129,7 +134,7 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
       const bool ok = o < S && vb[o] != 0;
       int64_t idx = 0;
       const float* p = ok ? nce_row_ptr(f_oth, pairs, cap, rows, S, b, o, 1 - side_own, &idx) : nullptr;
-      stage_row(p, f_oth.sc, ok, prenorm, &Os[o * kLd]);
+      stage_row(p, f_oth.sc, ok, prenorm, &Os[o * kLd], f_oth.base);
     }
   }
   // this block's own rows (all their dependent index / feature loads in parallel)
@@ -139,7 +144,7 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
     int64_t idx = 0;
     const float* p = ok ? nce_row_ptr(f_own, pairs, cap, rows, S, b, a, side_own, &idx) : nullptr;
     float* dst = &Ws[threadIdx.x * kLd];
-    const float nrm = stage_row(p, f_own.sc, ok, prenorm, dst);
+    const float nrm = stage_row(p, f_own.sc, ok, prenorm, dst, f_own.base);
     float vn = 0.f;
 #pragma unroll
     for (int c = 0; c < kC; ++c) vn = fmaf(dst[c], dst[c], vn);

@@ -14,17 +14,19 @@
 namespace {
 
 constexpr int kRows = 64;     // rows of Phi reduced per block in pass 1
-constexpr int kSub = 32;      // rows staged in LDS per step
 constexpr int kKC = 64;       // K == C == 64 (C_width, k_eig) — checked on the host
 
 // pass 1: part[b, s] = sum_{rows in chunk s} Phi[r, :]^T (w_r * x[r, :]), w = mass or 1.
-// grid (S, B), block 256 = 16 x 16 threads, each owning a 4 x 4 output micro-tile.
+// grid (S, B), block 256 = 16 x 16 threads, each owning a 4 x 4 output micro-tile. The chunk's 64
+// rows of Phi and x (and its masses) are loaded in one go, unconditionally at clamped rows (a
+// conditional load compiled to a branch and a wait per load: serial memory round trips), then
+// summed in row order (the same fmaf chain as before).
 __global__ __launch_bounds__(256) void spec_reduce_kernel(const float* __restrict__ x, int ldx,
                                                           const float* __restrict__ mass,
                                                           const float* __restrict__ evecs, int N, int S,
                                                           float* __restrict__ part) {
-  __shared__ float4 sphi[kSub][kKC / 4 + 1];
-  __shared__ float4 sx[kSub][kKC / 4 + 1];
+  __shared__ float4 sphi[kRows][kKC / 4 + 1];
+  __shared__ float4 sx[kRows][kKC / 4 + 1];
   const int s = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int ty = tid >> 4, tx = tid & 15;
   const float* __restrict__ phi = evecs + (int64_t)b * N * kKC;
@@ -33,35 +35,40 @@ __global__ __launch_bounds__(256) void spec_reduce_kernel(const float* __restric
   float acc[4][4] = {};
   const int r_begin = s * kRows;
   const int r_end = min(N, r_begin + kRows);
-  for (int r0 = r_begin; r0 < r_end; r0 += kSub) {
-    __syncthreads();
-    for (int e = tid; e < kSub * (kKC / 4); e += 256) {
-      const int rr = e / (kKC / 4), q = e % (kKC / 4);
-      const int r = r0 + rr;
-      float4 pv = make_float4(0.f, 0.f, 0.f, 0.f), xv = pv;
-      if (r < r_end) {
-        pv = reinterpret_cast<const float4*>(phi + (int64_t)r * kKC)[q];
-        xv = reinterpret_cast<const float4*>(xb + (int64_t)r * ldx)[q];
-        if (mb) {
-          const float w = mb[r];
-          xv.x *= w; xv.y *= w; xv.z *= w; xv.w *= w;
-        }
-      }
-      sphi[rr][q] = pv;
-      sx[rr][q] = xv;
+  constexpr int PER = kRows * (kKC / 4) / 256;  // float4s per thread per operand
+  float4 pv[PER], xv[PER];
+  float wv[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int e = tid + 256 * j, rr = e / (kKC / 4), q = e % (kKC / 4);
+    const int r = r_begin + rr < r_end ? r_begin + rr : r_begin;
+    pv[j] = reinterpret_cast<const float4*>(phi + (int64_t)r * kKC)[q];
+    xv[j] = reinterpret_cast<const float4*>(xb + (int64_t)r * ldx)[q];
+    wv[j] = mb ? mb[r] : 1.f;
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int e = tid + 256 * j, rr = e / (kKC / 4), q = e % (kKC / 4);
+    const bool ok = r_begin + rr < r_end;
+    float4 a = xv[j];
+    if (mb) {
+      const float w = wv[j];
+      a.x *= w; a.y *= w; a.z *= w; a.w *= w;
     }
-    __syncthreads();
+    sphi[rr][q] = ok ? pv[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    sx[rr][q] = ok ? a : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
 #pragma unroll 4
-    for (int rr = 0; rr < kSub; ++rr) {
-      const float4 p = sphi[rr][ty];
-      const float4 v = sx[rr][tx];
-      const float pk[4] = {p.x, p.y, p.z, p.w};
-      const float vc[4] = {v.x, v.y, v.z, v.w};
+  for (int rr = 0; rr < kRows; ++rr) {
+    const float4 p = sphi[rr][ty];
+    const float4 v = sx[rr][tx];
+    const float pk[4] = {p.x, p.y, p.z, p.w};
+    const float vc[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(pk[i], vc[j], acc[i][j]);
-    }
+      for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(pk[i], vc[j], acc[i][j]);
   }
   float* __restrict__ o = part + ((int64_t)b * S + s) * kKC * kKC;
 #pragma unroll
@@ -92,7 +99,19 @@ __global__ __launch_bounds__(1024) void spec_combine_kernel(float* __restrict__ 
   // fp32 sum over ~80 slabs dominated the error of the diffusion-time gradient, a
   // cancellation-prone contraction of two such sums
   double v[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int s = 0; s < S; ++s) {
+  int s = 0;
+  for (; s + 4 <= S; s += 4) {  // 4 slabs' loads issued together, added in slab order
+    float ld[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ld[u][i] = pb[(int64_t)(s + u) * kKC * kKC + i * kKC];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] += (double)ld[u][i];
+  }
+  for (; s < S; ++s) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] += (double)pb[(int64_t)s * kKC * kKC + i * kKC];
   }
@@ -140,18 +159,42 @@ __global__ __launch_bounds__(256) void spec_expand_kernel(const float* __restric
     gt[tid] = a;
   }
   const float* __restrict__ cb = coef + (int64_t)b * kKC * kKC;
-  for (int e = tid; e < kKC * kKC / 4; e += 256) scoef[e / 16][e % 16] = reinterpret_cast<const float4*>(cb)[e];
+  {
+    float4 cvv[kKC * kKC / 4 / 256];
+#pragma unroll
+    for (int j = 0; j < kKC * kKC / 4 / 256; ++j) cvv[j] = reinterpret_cast<const float4*>(cb)[tid + 256 * j];
+#pragma unroll
+    for (int j = 0; j < kKC * kKC / 4 / 256; ++j) scoef[(tid + 256 * j) / 16][(tid + 256 * j) % 16] = cvv[j];
+  }
   const int r0 = tile * 64;
   const float* __restrict__ phi = evecs + (int64_t)b * N * kKC;
-  for (int e = tid; e < 64 * kKC / 4; e += 256) {
-    const int rr = e / 16, q = e % 16;
-    const int r = r0 + rr;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r < N) v = reinterpret_cast<const float4*>(phi + (int64_t)r * kKC)[q];
-    sphi[rr][4 * q + 0] = v.x;
-    sphi[rr][4 * q + 1] = v.y;
-    sphi[rr][4 * q + 2] = v.z;
-    sphi[rr][4 * q + 3] = v.w;
+  {
+    float4 pvv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // unconditional at clamped rows, then selected
+      const int e = tid + 256 * j, rr = e / 16, q = e % 16;
+      const int r = r0 + rr < N ? r0 + rr : r0;
+      pvv[j] = reinterpret_cast<const float4*>(phi + (int64_t)r * kKC)[q];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = tid + 256 * j, rr = e / 16, q = e % 16;
+      const float4 v = r0 + rr < N ? pvv[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      sphi[rr][4 * q + 0] = v.x;
+      sphi[rr][4 * q + 1] = v.y;
+      sphi[rr][4 * q + 2] = v.z;
+      sphi[rr][4 * q + 3] = v.w;
+    }
+  }
+  // the epilogue's operands (mass, the accumulated output) in flight during the products
+  float wr[4];
+  float4 old[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + ty * 4 + i < N ? r0 + ty * 4 + i : r0;
+    wr[i] = mass ? mass[(int64_t)b * N + r] : 1.f;
+    old[i] = accumulate ? reinterpret_cast<const float4*>(y + ((int64_t)b * N + r) * ldy)[tx]
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
   float acc[4][4] = {};
@@ -170,12 +213,11 @@ __global__ __launch_bounds__(256) void spec_expand_kernel(const float* __restric
   for (int i = 0; i < 4; ++i) {
     const int r = r0 + ty * 4 + i;
     if (r >= N) continue;
-    float w = 1.f;
-    if (mass) w = mass[(int64_t)b * N + r];
+    const float w = wr[i];
     float4* yp = reinterpret_cast<float4*>(y + ((int64_t)b * N + r) * ldy) + tx;
     float4 v = make_float4(acc[i][0] * w, acc[i][1] * w, acc[i][2] * w, acc[i][3] * w);
     if (accumulate) {
-      const float4 o = *yp;
+      const float4 o = old[i];
       v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
     }
     *yp = v;

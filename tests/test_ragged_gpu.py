@@ -295,3 +295,36 @@ def test_cgt_real_crops_full_rank(device):
         exp = M.C_from_sparse_P(p, e1[b, :n1[b], :30].double(), e2[b, :n2[b], :30].double())
         scale = float(exp.abs().max())
         assert (got[b] - exp).abs().max().item() <= 1e-4 * scale, (b, (got[b] - exp).abs().max().item(), scale)
+
+
+def test_cgt_real_crops_full_rank(device):
+    """C_from_sparse_P (utils/utils.py:67-79) on the reference's own pair structure: the ball-query
+    positives of its real crops (object.py:174-177, r = 0.05 diam) with operators of the true
+    sizes. Every crop matches >= 30 distinct crop rows, so the normal equations are full rank and
+    pk_cgt_lstsq takes its Gauss-Jordan path; C_gt agrees with the torch lstsq restatement
+    (fp32 tolerance of the 30 x 30 solve). The rank-deficient / empty cases, where the device
+    returns the minimum-norm solution, are test_corr_pose_gpu.py::test_cgt_rank_deficient_and_empty."""
+    from dpfm_amd import ops
+    from dpfm_amd.pipeline import lbo_padded
+    crops = _real()
+    B = len(crops)
+    Ps = [O.find_positives(c["cad"], O.transform(c["pc"], c["R"], c["t"], inv=True), r=c["diam"] * 0.05)
+          for c in crops]
+    L = max(P.shape[0] for P in Ps)
+    V1 = max(c["cad"].shape[0] for c in crops)
+    V2 = max(c["pc"].shape[0] for c in crops)
+    pairs = np.zeros((B, L, 2), dtype=np.int64)
+    e1 = np.zeros((B, V1, 64), dtype=np.float32)
+    e2 = np.zeros((B, V2, 64), dtype=np.float32)
+    for b, (c, P) in enumerate(zip(crops, Ps)):
+        assert np.unique(P[:, 1]).shape[0] >= 30, b  # full rank: >= 30 distinct crop rows
+        pairs[b, :P.shape[0]] = P
+        e1[b, :c["cad"].shape[0]] = lbo_padded(c["cad"].shape[0], 2 * b)[2]
+        e2[b, :c["pc"].shape[0]] = lbo_padded(c["pc"].shape[0], 2 * b + 1)[2]
+    got = ops.cgt_lstsq(torch.from_numpy(pairs).to(device),
+                        torch.tensor([P.shape[0] for P in Ps], dtype=torch.int64, device=device),
+                        torch.from_numpy(e1).to(device), torch.from_numpy(e2).to(device)).cpu()
+    for b, P in enumerate(Ps):
+        exp = M.C_from_sparse_P(torch.from_numpy(P), torch.from_numpy(e1[b, :, :30]), torch.from_numpy(e2[b, :, :30]))
+        scale = max(float(exp.abs().max()), 1e-30)
+        torch.testing.assert_close(got[b], exp, rtol=1e-3, atol=1e-4 * scale)

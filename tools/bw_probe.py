@@ -44,7 +44,7 @@ for mb in (4, 8, 17, 33, 67, 134, 268, 1074):
         k[0] += 1
 
     def sm():
-        torch.sum(src[k[0] % len(src)], out=out)
+        torch.sum(src[k[0] % len(src)], dim=(0,), out=out)
         k[0] += 1
     tc, ts = timed(cp), timed(sm)
     print(f"{mb:5d} MB: copy {tc:8.2f} us {2 * n * 4 / tc / 1e3:6.0f} GB/s   sum {ts:8.2f} us {n * 4 / ts / 1e3:6.0f} GB/s",
