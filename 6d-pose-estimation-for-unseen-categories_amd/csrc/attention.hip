@@ -68,8 +68,7 @@ __device__ __forceinline__ Tile load_tile(const float* __restrict__ src, int HL,
   for (int j = 0; j < 4; ++j) {
     const int e = threadIdx.x + 256 * j;
     const int d = e >> 6, r = e & 63;
-    const float v = src[(int64_t)d * HL + (r0 + r < L ? r0 + r : 0)];  // unconditional (no branch + wait)
-    t.x[j] = r0 + r < L ? v : 0.f;
+    t.x[j] = r0 + r < L ? src[(int64_t)d * HL + r0 + r] : 0.f;
   }
   return t;
 }
@@ -101,10 +100,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
   const float* vb = v + (int64_t)b * sbv + (int64_t)h * M;
   float qr[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {  // unconditional load at a clamped query
-    const float qv = qb[(int64_t)(4 * s + g) * H * N + (qi < N ? qi : 0)];
-    qr[s] = qi < N ? qv * kScale : 0.f;
-  }
+  for (int s = 0; s < 4; ++s) qr[s] = qi < N ? qb[(int64_t)(4 * s + g) * H * N + qi] * kScale : 0.f;
   // one accumulator per 16-key sub-tile: four independent MFMA chains (a serial chain over
   // M ~ 5000 keys of a real CAD measured 4-5x torch's gradient error; split, it is within 1.5x)
   f32x4 acc[4];
@@ -205,16 +201,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
   float dl = 0.f;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    // unconditional loads at a clamped query (a conditional load is a branch + a wait each)
-    const int64_t a = qoff + (int64_t)(4 * s + g) * H * N + (qi < N ? qi : 0);
-    const float qv = q[a], dv0 = dout[a], ov = o[a];
-    qr[s] = qi < N ? qv * kScale : 0.f;
-    dor[s] = qi < N ? dv0 : 0.f;
-    dl = fmaf(dor[s], qi < N ? ov : 0.f, dl);
+    const int64_t a = qoff + (int64_t)(4 * s + g) * H * N + qi;
+    qr[s] = qi < N ? q[a] * kScale : 0.f;
+    dor[s] = qi < N ? dout[a] : 0.f;
+    dl = fmaf(dor[s], qi < N ? o[a] : 0.f, dl);
   }
   dl = grp_sum(dl);  // delta = sum_d dO * O for query qi
-  const float2 msl = reinterpret_cast<const float2*>(lse)[((int64_t)b * H + h) * N + (qi < N ? qi : 0)];
-  const float2 ms = qi < N ? msl : make_float2(__builtin_huge_valf(), 0.f);
+  const float2 ms = qi < N ? reinterpret_cast<const float2*>(lse)[((int64_t)b * H + h) * N + qi]
+                           : make_float2(__builtin_huge_valf(), 0.f);
   if (qi < N && g == 0) delta[((int64_t)b * H + h) * N + qi] = dl;
   f32x4 acc[4];  // independent chains per 16-key sub-tile (accuracy, see the forward)
 #pragma unroll

@@ -394,18 +394,16 @@ __global__ __launch_bounds__(64 * kWaves) void fd_main_kernel(
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
       const int e = threadIdx.x + 64 * kWaves * v;
-      const bool in = e < cn * TB / 16;
-      const float4 ld = src[in ? e : 0];  // unconditional at a clamped index (no branch + wait per load)
-      // past the row part: padding rows (+inf |x|^2 slot in mode 0: lane group 2, k = 30)
-      const int q = e % (TB / 16);
-      const bool inf_slot = MODE == 0 && (q & 1) && (q >> 5) == 2;
-      stage[v] = in ? ld : make_float4(0.f, 0.f, 0.f, inf_slot ? __builtin_huge_valf() : 0.f);
+      if (e < cn * TB / 16) {
+        stage[v] = src[e];
+      } else {  // past the row part: padding rows (+inf |x|^2 slot in mode 0: lane group 2, k = 30)
+        const int q = e % (TB / 16);
+        const bool inf_slot = MODE == 0 && (q & 1) && (q >> 5) == 2;
+        stage[v] = make_float4(0.f, 0.f, 0.f, inf_slot ? __builtin_huge_valf() : 0.f);
+      }
     }
     if (MODE != 0 && threadIdx.x < kCH * 16)
-    {
-      const float nv = nAt[(int64_t)c0 * 16 + (threadIdx.x < cn * 16 ? threadIdx.x : 0)];
-      nst = threadIdx.x < cn * 16 ? nv : __builtin_huge_valf();
-    }
+      nst = threadIdx.x < cn * 16 ? nAt[(int64_t)c0 * 16 + threadIdx.x] : __builtin_huge_valf();
   };
   auto lstore = [&](int buf) {
     float4* dst = reinterpret_cast<float4*>(&ring[buf][0][0]);

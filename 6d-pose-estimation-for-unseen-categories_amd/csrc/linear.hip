@@ -175,40 +175,29 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 template <int LAYOUT>
 __device__ __forceinline__ void load8(const float* __restrict__ p, int C, int c, int N, int64_t rb, int64_t r1,
                                       int h, float (&v)[8], int64_t sb) {
-  // every load is unconditional at a clamped (valid) address and masked afterwards: a
-  // conditional load compiles to an exec-mask branch with a vmcnt wait per load, which
-  // serialises the batch's memory round trips
-  const bool cok = c < C;
-  const int cc = cok ? c : 0;
   if (LAYOUT == 0) {
-    float t[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int64_t r = rb + 2 * s + h;
-      t[s] = p[(r < r1 ? r : rb) * C + cc];
+      v[s] = (c < C && r < r1) ? p[r * C + c] : 0.f;
     }
-#pragma unroll
-    for (int s = 0; s < 8; ++s) v[s] = (cok && rb + 2 * s + h < r1) ? t[s] : 0.f;
   } else if (N & 15) {  // ragged items (N % 16 != 0): a 16-row batch may straddle two items
     const int64_t cs = sb ? sb : (int64_t)C * N;
-    float t[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const int64_t r0 = rb + 8 * h + s;
-      const int64_t r = r0 < r1 ? r0 : rb;
+      const int64_t r = rb + 8 * h + s;
       const int64_t b = r / N;
-      t[s] = p[b * cs + (int64_t)cc * N + (r - b * N)];
+      v[s] = (c < C && r < r1) ? p[b * cs + (int64_t)c * N + (r - b * N)] : 0.f;
     }
-#pragma unroll
-    for (int s = 0; s < 8; ++s) v[s] = (cok && rb + 8 * h + s < r1) ? t[s] : 0.f;
-  } else {  // batch stride sb (0: dense C N)
-    const int64_t b = rb / N;
-    const int64_t n = rb - b * N + 8 * h;
-    const float4* q = reinterpret_cast<const float4*>(p + b * (sb ? sb : (int64_t)C * N) + (int64_t)cc * N + n);
-    const float4 u = q[0], w = q[1];
-    v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
-    v[4] = w.x; v[5] = w.y; v[6] = w.z; v[7] = w.w;
-    if (!cok) {
+  } else {
+    if (c < C) {  // batch stride sb (0: dense C N)
+      const int64_t b = rb / N;
+      const int64_t n = rb - b * N + 8 * h;
+      const float4* q = reinterpret_cast<const float4*>(p + b * (sb ? sb : (int64_t)C * N) + (int64_t)c * N + n);
+      const float4 u = q[0], w = q[1];
+      v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
+      v[4] = w.x; v[5] = w.y; v[6] = w.z; v[7] = w.w;
+    } else {
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = 0.f;
     }
@@ -692,11 +681,8 @@ template <int Q>
 __device__ __forceinline__ void lr_load(const float* __restrict__ x, int64_t sx, int64_t row, int64_t R, int g,
                                         f32x4 (&xa)[Q]) {
 #pragma unroll
-  for (int q = 0; q < Q; ++q) {  // unconditional loads at a clamped row, then a select: a
-    // conditional load compiled to a branch and a vmcnt(0) per pair of loads (4 serial round trips)
-    const f32x4 v = *reinterpret_cast<const f32x4*>(x + (row < R ? row : 0) * sx + 16 * q + 4 * g);
-    xa[q] = row < R ? v : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+  for (int q = 0; q < Q; ++q)
+    xa[q] = row < R ? *reinterpret_cast<const f32x4*>(x + row * sx + 16 * q + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
 // Weight staging shared by the MFMA per-point kernels: Ws[o][k] (o < 16 TO, zero rows past
@@ -715,10 +701,8 @@ __device__ __forceinline__ void lr_stage(const float* w, int Cout, int transw, f
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int e = threadIdx.x + 256 * i, o = e / (CI / 4);
-      const bool ok = e < NV && o < Cout;
-      const float* src = !ok ? w : o < wsplit ? w + 4 * (int64_t)e : w2 + 4 * (int64_t)(e - wsplit * (CI / 4));
-      const f32x4 ld = *reinterpret_cast<const f32x4*>(src);  // unconditional (clamped address)
-      v[i] = ok ? ld : f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* src = o < wsplit ? w + 4 * (int64_t)e : w2 + 4 * (int64_t)(e - wsplit * (CI / 4));
+      v[i] = (e < NV && o < Cout) ? *reinterpret_cast<const f32x4*>(src) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -731,10 +715,8 @@ __device__ __forceinline__ void lr_stage(const float* w, int Cout, int transw, f
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int e = threadIdx.x + 256 * i, k = e / (TO * 16), o = e - k * (TO * 16);
-      const bool ok = e < NE && o < Cout;
-      const float* src = !ok ? w : k < wsplit ? w + (int64_t)k * Cout + o : w2 + (int64_t)(k - wsplit) * Cout + o;
-      const float ld = *src;  // unconditional (clamped address)
-      v[i] = ok ? ld : 0.f;
+      const float* src = k < wsplit ? w + (int64_t)k * Cout + o : w2 + (int64_t)(k - wsplit) * Cout + o;
+      v[i] = (e < NE && o < Cout) ? *src : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -768,8 +750,7 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
 #pragma unroll
   for (int t = 0; t < TO; ++t) {
     const int o = t * 16 + m;
-    const float bl = bias != nullptr ? bias[o < Cout ? o : 0] : 0.f;  // uniform pointer test, clamped index
-    bv[t] = o < Cout ? bl : 0.f;
+    bv[t] = (bias != nullptr && o < Cout) ? bias[o] : 0.f;
   }
   for (;;) {
     const int64_t tn = tile + stride;
@@ -900,8 +881,7 @@ __global__ __launch_bounds__(256, 2) void linear_rows_lds_kernel(const float* __
     for (int j = 0; j < PF; ++j) {
       const int f = lane + 64 * j, row = f / CH, c = f - row * CH;
       const int64_t r = tt * 16 + row;
-      const f32x4 ld = *reinterpret_cast<const f32x4*>(x + (r < R ? r : 0) * sx + 4 * c);
-      pf[j] = r < R ? ld : f32x4{0.f, 0.f, 0.f, 0.f};
+      pf[j] = r < R ? *reinterpret_cast<const f32x4*>(x + r * sx + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
   auto write_tile = [&]() {
@@ -1475,8 +1455,7 @@ __global__ __launch_bounds__(256, WPS) void linear_ws_rows_kernel(const float* _
 #pragma unroll
   for (int t = 0; t < TO; ++t) {
     const int o = t * 16 + m;
-    const float bl = bias != nullptr ? bias[o < Cout ? o : 0] : 0.f;  // uniform pointer test, clamped index
-    bv[t] = o < Cout ? bl : 0.f;
+    bv[t] = (bias != nullptr && o < Cout) ? bias[o] : 0.f;
   }
   for (;;) {
     const int64_t tn = tile + stride;

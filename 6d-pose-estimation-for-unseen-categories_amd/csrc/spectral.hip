@@ -14,19 +14,17 @@
 namespace {
 
 constexpr int kRows = 64;     // rows of Phi reduced per block in pass 1
+constexpr int kSub = 32;      // rows staged in LDS per step
 constexpr int kKC = 64;       // K == C == 64 (C_width, k_eig) — checked on the host
 
 // pass 1: part[b, s] = sum_{rows in chunk s} Phi[r, :]^T (w_r * x[r, :]), w = mass or 1.
-// grid (S, B), block 256 = 16 x 16 threads, each owning a 4 x 4 output micro-tile. The chunk's 64
-// rows of Phi and x (and its masses) are loaded in one go, unconditionally at clamped rows (a
-// conditional load compiled to a branch and a wait per load: serial memory round trips), then
-// summed in row order (the same fmaf chain as before).
+// grid (S, B), block 256 = 16 x 16 threads, each owning a 4 x 4 output micro-tile.
 __global__ __launch_bounds__(256) void spec_reduce_kernel(const float* __restrict__ x, int ldx,
                                                           const float* __restrict__ mass,
                                                           const float* __restrict__ evecs, int N, int S,
                                                           float* __restrict__ part) {
-  __shared__ float4 sphi[kRows][kKC / 4 + 1];
-  __shared__ float4 sx[kRows][kKC / 4 + 1];
+  __shared__ float4 sphi[kSub][kKC / 4 + 1];
+  __shared__ float4 sx[kSub][kKC / 4 + 1];
   const int s = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int ty = tid >> 4, tx = tid & 15;
   const float* __restrict__ phi = evecs + (int64_t)b * N * kKC;
@@ -35,40 +33,35 @@ __global__ __launch_bounds__(256) void spec_reduce_kernel(const float* __restric
   float acc[4][4] = {};
   const int r_begin = s * kRows;
   const int r_end = min(N, r_begin + kRows);
-  constexpr int PER = kRows * (kKC / 4) / 256;  // float4s per thread per operand
-  float4 pv[PER], xv[PER];
-  float wv[PER];
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int e = tid + 256 * j, rr = e / (kKC / 4), q = e % (kKC / 4);
-    const int r = r_begin + rr < r_end ? r_begin + rr : r_begin;
-    pv[j] = reinterpret_cast<const float4*>(phi + (int64_t)r * kKC)[q];
-    xv[j] = reinterpret_cast<const float4*>(xb + (int64_t)r * ldx)[q];
-    wv[j] = mb ? mb[r] : 1.f;
-  }
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int e = tid + 256 * j, rr = e / (kKC / 4), q = e % (kKC / 4);
-    const bool ok = r_begin + rr < r_end;
-    float4 a = xv[j];
-    if (mb) {
-      const float w = wv[j];
-      a.x *= w; a.y *= w; a.z *= w; a.w *= w;
+  for (int r0 = r_begin; r0 < r_end; r0 += kSub) {
+    __syncthreads();
+    for (int e = tid; e < kSub * (kKC / 4); e += 256) {
+      const int rr = e / (kKC / 4), q = e % (kKC / 4);
+      const int r = r0 + rr;
+      float4 pv = make_float4(0.f, 0.f, 0.f, 0.f), xv = pv;
+      if (r < r_end) {
+        pv = reinterpret_cast<const float4*>(phi + (int64_t)r * kKC)[q];
+        xv = reinterpret_cast<const float4*>(xb + (int64_t)r * ldx)[q];
+        if (mb) {
+          const float w = mb[r];
+          xv.x *= w; xv.y *= w; xv.z *= w; xv.w *= w;
+        }
+      }
+      sphi[rr][q] = pv;
+      sx[rr][q] = xv;
     }
-    sphi[rr][q] = ok ? pv[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-    sx[rr][q] = ok ? a : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  __syncthreads();
+    __syncthreads();
 #pragma unroll 4
-  for (int rr = 0; rr < kRows; ++rr) {
-    const float4 p = sphi[rr][ty];
-    const float4 v = sx[rr][tx];
-    const float pk[4] = {p.x, p.y, p.z, p.w};
-    const float vc[4] = {v.x, v.y, v.z, v.w};
+    for (int rr = 0; rr < kSub; ++rr) {
+      const float4 p = sphi[rr][ty];
+      const float4 v = sx[rr][tx];
+      const float pk[4] = {p.x, p.y, p.z, p.w};
+      const float vc[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(pk[i], vc[j], acc[i][j]);
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(pk[i], vc[j], acc[i][j]);
+    }
   }
   float* __restrict__ o = part + ((int64_t)b * S + s) * kKC * kKC;
 #pragma unroll

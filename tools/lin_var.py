@@ -14,13 +14,13 @@ L.pkdev_linear_rows_var.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_v
                                     ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
 dev = torch.device("cuda:0")
 R = 65536
-names = {0: "production", 1: "no-MFMA", 2: "no-store", 3: "no-sched-barrier"}
+names = {0: "production", 1: "no-MFMA", 2: "no-store", 3: "no-sched-barrier", 4: "weight-stat. 2w/SIMD", 5: "weight-stat. 1w/SIMD"}
 for cin in (128, 64):
     x = torch.randn(R, cin, device=dev)
     w = torch.randn(64, cin, device=dev)
     b = torch.randn(64, device=dev)
     y = torch.empty(R, 64, device=dev)
-    for var in (0, 1, 2, 3):
+    for var in (0, 2, 4, 5):
         for blocks in (0, 256, 512):
             f = lambda: L.pkdev_linear_rows_var(x.data_ptr(), w.data_ptr(), b.data_ptr(), R, cin, y.data_ptr(),  # noqa
                                                 var, blocks, torch.cuda.current_stream().cuda_stream)
