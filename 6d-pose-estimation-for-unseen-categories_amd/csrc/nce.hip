@@ -310,37 +310,54 @@ __global__ __launch_bounds__(kScT) void nce_scatter_kernel(const int64_t* __rest
   float* __restrict__ g = (side ? g2 : g1) + (int64_t)b * N * kC;
   const float* __restrict__ dx = dxr + ((int64_t)side * B + b) * S * kC;
   constexpr int64_t kNone = 0x7fffffffffffffffLL;
-  if (t < kMaxS) {
-    int64_t k = kNone;
-    if (t < S && valid[(int64_t)b * S + t] != 0) {
-      const int64_t r = rows[(int64_t)b * S + t];
-      k = (pairs[((int64_t)b * cap + r) * 2 + side] << 9) | t;
-    }
-    key[t] = k;
+  static_assert(kScT == kMaxS, "one key per thread");
+  int64_t kk = kNone;
+  if (t < S && valid[(int64_t)b * S + t] != 0) {
+    const int64_t r = rows[(int64_t)b * S + t];
+    kk = (pairs[((int64_t)b * cap + r) * 2 + side] << 9) | t;
   }
   float4* gz = reinterpret_cast<float4*>(g);  // N * 32 floats, 16-B aligned (torch allocation, N * 128 B rows)
   for (int64_t e = t; e < N * (kC / 4); e += kScT) gz[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-  __syncthreads();
+  // bitonic sort, one key per thread: partners within a wave (j < 64) by lane shuffles, only the
+  // 6 wider stages through LDS (12 barriers instead of 45)
   for (int k = 2; k <= kMaxS; k <<= 1)
     for (int j = k >> 1; j > 0; j >>= 1) {
-      if (t < kMaxS / 2) {
-        const int i = (t / j) * 2 * j + (t % j), ixj = i + j;
-        const int64_t x = key[i], y = key[ixj];
-        if ((x > y) == ((i & k) == 0)) {
-          key[i] = y;
-          key[ixj] = x;
-        }
+      int64_t other;
+      if (j >= 64) {
+        key[t] = kk;
+        __syncthreads();
+        other = key[t ^ j];
+        __syncthreads();
+      } else {
+        const uint32_t lo = (uint32_t)(uint64_t)kk, hi = (uint32_t)((uint64_t)kk >> 32);
+        const uint32_t olo = (uint32_t)__shfl_xor((int)lo, j), ohi = (uint32_t)__shfl_xor((int)hi, j);
+        other = (int64_t)(((uint64_t)ohi << 32) | olo);
       }
-      __syncthreads();
+      const bool up = (t & k) == 0, lower = (t & j) == 0;
+      kk = (lower == up) ? (kk < other ? kk : other) : (kk > other ? kk : other);
     }
+  key[t] = kk;
+  __syncthreads();
+  // every sorted position's first row value is loaded up front (one load per position, all in
+  // flight together; a run's further rows — points in several slots, rare — are added after);
+  // round 2's loop issued one dependent load per position: 32 serial memory round trips
   const int c = t & (kC - 1);
-  for (int p = t / kC; p < kMaxS; p += kScT / kC) {
+  constexpr int kPer = kMaxS / (kScT / kC);
+  float v[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int64_t k = key[t / kC + (kScT / kC) * i];
+    v[i] = dx[(k == kNone ? 0 : (k & 511)) * kC + c];  // slot 0's row stands in for a sentinel
+  }
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int p = t / kC + (kScT / kC) * i;
     const int64_t k = key[p];
     if (k == kNone) break;  // sentinels sort last
     const int64_t idx = k >> 9;
     if (p > 0 && (key[p - 1] >> 9) == idx) continue;  // not the head of its run
-    float s = dx[(k & 511) * kC + c];
-    for (int q = p + 1; q < kMaxS; ++q) {
+    float s = v[i];
+    for (int q = p + 1; q < kMaxS; ++q) {  // the run's further slots, ascending
       const int64_t kq = key[q];
       if (kq == kNone || (kq >> 9) != idx) break;
       s += dx[(kq & 511) * kC + c];

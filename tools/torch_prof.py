@@ -29,7 +29,7 @@ step = TrainStep(model, seed=0)
 for _ in range(3):
     step(op, crops_of(fb))
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True, with_stack=True) as prof:
     for _ in range(2):
         step(op, crops_of(fb))
     torch.cuda.synchronize()
@@ -47,4 +47,12 @@ with open(os.path.join(out, "torch_prof_glue.txt"), "w") as f:
             rows.append((dev_us, e.count, e.key, str(e.input_shapes)[:150]))
     for r in sorted(rows, reverse=True)[:60]:
         f.write(f"{r[0]/2:9.1f} us/step {r[1]/2:5.1f}/step  {r[2]:32s} {r[3]}\n")
+with open(os.path.join(out, "torch_prof_stacks.txt"), "w") as f:
+    for e in prof.key_averages(group_by_stack_n=6):
+        dev_us = getattr(e, "self_device_time_total", None) or getattr(e, "self_cuda_time_total", 0)
+        if e.key in ("aten::copy_", "aten::add", "aten::add_", "aten::fill_", "aten::cat", "aten::zero_",
+                     "aten::mul", "aten::sub", "aten::contiguous") and dev_us > 0:
+            f.write(f"{dev_us / 2:9.1f} us/step {e.count / 2:5.1f}/step {e.key}\n")
+            for fr in (e.stack or [])[:6]:
+                f.write(f"      {fr}\n")
 print("ok", out)
