@@ -74,14 +74,24 @@ __global__ __launch_bounds__(256) void fmap_solve_kernel(const float* __restrict
   const int lane = pk::lane_id();
   const float* __restrict__ Ab = AAt + (int64_t)b * kN * kN;
   double row[kN + NRHS];
-  const double reg = lane < kN ? (double)lambda * (double)D[((int64_t)b * kN + i) * kN + lane] : 0.0;
+  // every operand load issued before the first use, unconditionally at a clamped lane (round 2's
+  // per-element conditional loads were each waited for: 30+ serial memory round trips)
+  const bool lv = lane < kN;
+  const int lc = lv ? lane : 0;
+  float af[kN];
+#pragma unroll
+  for (int j = 0; j < kN; ++j) af[j] = Ab[lc * kN + j];
+  const float dv = D[((int64_t)b * kN + i) * kN + lc];
+  const float bv = BAt[((int64_t)b * kN + i) * kN + lc];
+  const float gv = BWD ? G[((int64_t)b * kN + i) * kN + lc] : 0.f;
+  const double reg = lv ? (double)lambda * (double)dv : 0.0;
 #pragma unroll
   for (int j = 0; j < kN; ++j) {
-    const double a = lane < kN ? (double)Ab[lane * kN + j] : 0.0;
+    const double a = lv ? (double)af[j] : 0.0;
     row[j] = j == lane ? a + reg : a;  // static index: no scratch
   }
-  row[kN] = lane < kN ? (double)BAt[((int64_t)b * kN + i) * kN + lane] : 0.0;
-  if (BWD) row[kN + 1] = lane < kN ? (double)G[((int64_t)b * kN + i) * kN + lane] : 0.0;
+  row[kN] = lv ? (double)bv : 0.0;
+  if (BWD) row[kN + 1] = lv ? (double)gv : 0.0;
   int var;
   gj_solve<NRHS>(row, lane, var);
   // lane with var == k holds x_k (row[kN]) and w_k (row[kN+1])

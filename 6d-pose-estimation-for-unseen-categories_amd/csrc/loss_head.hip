@@ -35,23 +35,42 @@ __global__ __launch_bounds__(kLossThreads) void loss_head_kernel(const float* __
                                                                  const float* __restrict__ wb, float w_fmap,
                                                                  float w_acc, float w_nce, float* __restrict__ loss,
                                                                  float* __restrict__ logs, float* __restrict__ dC) {
-  __shared__ float fb[1024];
+  __shared__ float fb[1024], snce[1024], swb[1024];
   const int lane = pk::lane_id(), w = pk::wave_id();
   constexpr int NW = kLossThreads / pk::kWave;
+  constexpr int kPer = 16;  // K * K <= 1024 elements per crop: 16 per lane, loaded together
   const float scale = 2.f * (w_fmap / (float)B);  // d mean_b / d f_b * d f_b / d (a - b), per unit gradient
+  // the per-crop scalars of the other terms into LDS by many threads (thread 0 then reads LDS,
+  // not 3 B dependent global loads)
+  for (int b = threadIdx.x; b < B; b += kLossThreads) {
+    snce[b] = nce[b];
+    swb[b] = wb[b] + wb[B + b];
+  }
   for (int b = w; b < B; b += NW) {
     const float* a = C12 + (int64_t)b * KK;
     const float* g = Cgt + (int64_t)b * KK;
-    float s = 0.f;
-    for (int e = lane; e < KK; e += pk::kWave) {
-      const float d = a[e] - g[e];
-      s = fmaf(d, d, s);
+    // all of the lane's elements in flight at once (round 2's loop waited for each pair of loads)
+    float d[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = lane + pk::kWave * i;
+      const int ec = e < KK ? e : 0;
+      const float av = a[ec], gv = g[ec];
+      d[i] = e < KK ? av - gv : 0.f;
     }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i)
+      if (lane + pk::kWave * i < KK) s = fmaf(d[i], d[i], s);  // the same per-lane order as before
     s = pk::wave_sum_f32(s);  // butterfly: every lane holds the same sum
     if (lane == 0) fb[b] = s;
     const bool pass = s >= -1.f && s <= 1000.f;  // clamp's gradient mask (inclusive bounds)
     float* o = dC + (int64_t)b * KK;
-    for (int e = lane; e < KK; e += pk::kWave) o[e] = pass ? scale * (a[e] - g[e]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = lane + pk::kWave * i;
+      if (e < KK) o[e] = pass ? scale * d[i] : 0.f;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -59,8 +78,8 @@ __global__ __launch_bounds__(kLossThreads) void loss_head_kernel(const float* __
     const float m = (float)B;
     for (int b = 0; b < B; ++b) {
       fm += fminf(fmaxf(fb[b], -1.f), 1000.f);
-      nl += nce[b] * w_nce / m;
-      al += (wb[b] + wb[B + b]) * w_acc / m;
+      nl += snce[b] * w_nce / m;
+      al += swb[b] * w_acc / m;
     }
     const float fmap_loss = fm / m * w_fmap;
     loss[0] = (fmap_loss + al) + nl;
@@ -87,7 +106,7 @@ __global__ __launch_bounds__(256) void loss_scale_kernel(ScaleTable t, const flo
 extern "C" int pk_loss_head(const float* C12, const float* Cgt, int B, int K, const float* nce, const float* wb,
                             float w_fmap, float w_acc, float w_nce, float* loss, float* logs, float* dC,
                             void* stream) {
-  PK_REQUIRE(B >= 1 && B <= 1024 && K >= 1);
+  PK_REQUIRE(B >= 1 && B <= 1024 && K >= 1 && K * K <= 1024);
   PK_REQUIRE(C12 && Cgt && nce && wb && loss && logs && dC);
   hipLaunchKernelGGL(loss_head_kernel, dim3(1), dim3(kLossThreads), 0, pk::as_stream(stream), C12, Cgt, B, K * K,
                      nce, wb, w_fmap, w_acc, w_nce, loss, logs, dC);
