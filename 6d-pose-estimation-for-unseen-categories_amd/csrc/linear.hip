@@ -273,25 +273,18 @@ __device__ __forceinline__ void wgrad_v2_body(const float* __restrict__ x, const
   const int64_t r1 = r0 + SL < R ? r0 + SL : R;
   const int nb = (int)((r1 - r0 + 15) / 16);
   if (active) {
-    // three register buffers: two batches' loads in flight while a third batch's MFMAs run
-    // (round 2 kept one batch ahead: ~4 KB per wave in flight, below what hides HBM latency);
-    // batches are still accumulated in order, so the sums are unchanged
-    WgradBatch<J> b0, b1, b2;
+    WgradBatch<J> b0, b1;
     int q = g;
-    auto ld = [&](WgradBatch<J>& bb, int qq) {
-      wgrad_load<LAYOUT, J>(bb, x, dy, I, O, N, Ti, T, tw, WT, m, h, r0 + 16ll * qq, r1, sbx, sbdy);
-    };
-    if (q < nb) ld(b0, q);
-    if (q + WR < nb) ld(b1, q + WR);
-    for (; q < nb; q += 3 * WR) {
-      if (q + 2 * WR < nb) ld(b2, q + 2 * WR);
+    if (q < nb) wgrad_load<LAYOUT, J>(b0, x, dy, I, O, N, Ti, T, tw, WT, m, h, r0 + 16ll * q, r1, sbx, sbdy);
+    for (; q < nb; q += 2 * WR) {
+      const bool has1 = q + WR < nb;
+      if (has1) wgrad_load<LAYOUT, J>(b1, x, dy, I, O, N, Ti, T, tw, WT, m, h, r0 + 16ll * (q + WR), r1, sbx, sbdy);
       wgrad_mma<J>(b0, acc, bs, Ti, T, tw, WT);
-      if (q + WR >= nb) break;
-      if (q + 3 * WR < nb) ld(b0, q + 3 * WR);
-      wgrad_mma<J>(b1, acc, bs, Ti, T, tw, WT);
-      if (q + 2 * WR >= nb) break;
-      if (q + 4 * WR < nb) ld(b1, q + 4 * WR);
-      wgrad_mma<J>(b2, acc, bs, Ti, T, tw, WT);
+      if (has1) {
+        if (q + 2 * WR < nb)
+          wgrad_load<LAYOUT, J>(b0, x, dy, I, O, N, Ti, T, tw, WT, m, h, r0 + 16ll * (q + 2 * WR), r1, sbx, sbdy);
+        wgrad_mma<J>(b1, acc, bs, Ti, T, tw, WT);
+      }
     }
   }
   // combine row groups (only when WT < 8, i.e. one tile per wave) in group order
