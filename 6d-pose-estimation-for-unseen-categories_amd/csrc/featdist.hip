@@ -22,13 +22,17 @@
 // chain over k in order; y side: y) and its squared norm, and writes the operand straight
 // into MFMA operand-tile order (16-row tiles, lane l = 16 g + c holding row c's k values of
 // its group g), so pass 2 moves whole tiles with 16-byte loads and no transposes.
-// Pass 2 (main): a block = 4 waves x CW column tiles (B operands in registers); the crop's
-// row tiles (or the block's share of them, RS row splits) stream through a two-stage LDS
-// ring shared by the 4 waves (one barrier per chunk of CH tiles): every A tile read from L2
-// feeds 4 CW column tiles. Epilogue per 16 x 16 tile: running argmin / sorted top-5 per
-// column (ties: lowest row). With RS > 1 the row parts write partial lists that pass 3
-// merges (same tie rule), so one 4096-point crop (configs[4]) still spreads over the chip.
+// Pass 2 (main, fd_main_direct_kernel): a block = 4 waves over 4 column tiles and the block's
+// row tiles; each wave takes 2 column tiles (B operands in registers) and half the rows, and
+// streams its rows' fragments from L2 into registers one chunk ahead of the MFMAs (every A
+// fragment feeds two accumulation chains). Epilogue per 16 x 16 tile: running argmin / sorted
+// top-5 per column (ties: lowest row); the two row halves merge through LDS at the end. With
+// RS > 1 the blocks' row parts write partial lists that pass 3 merges (same tie rule), so one
+// 4096-point crop (configs[4]) still spreads over the chip. fd_main_kernel (development knob
+// PK_FD_DIRECT=0) is the earlier pass: one column tile per wave, rows staged through an LDS
+// ring shared by the block's 4 waves (measured slower: DESIGN.md §5).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -71,17 +75,35 @@ __global__ __launch_bounds__(256) void fd_prep_kernel(const float* __restrict__ 
   const int T = xside ? T1 : T2;
   const int tile = blockIdx.x * 4 + w;
   if (tile >= T) return;
-  const int nval = xside ? n1[b] : n2[b];
   const int r = tile * 16 + c16;
-  const bool valid = r < nval;
-  const float* rowp = xside ? ex + ((int64_t)b * V1max + (valid ? r : 0)) * ldx
-                            : ey + ((int64_t)b * V2max + (valid ? r : 0)) * ldy;
+  // every operand load is issued before the first wait: the row at a clamped index (its
+  // validity against n applied by select afterwards), the C entries (both sides: C is tiny),
+  // and n itself — a load addressed through n, or behind the x-side branch, would add a round
+  // trip each
+  const float* rowp = xside ? ex + ((int64_t)b * V1max + min(r, V1max - 1)) * ldx
+                            : ey + ((int64_t)b * V2max + min(r, V2max - 1)) * ldy;
   // this lane's 8 row values at k = 4 s + g (the f32 MFMA operand layout), 0 past k = 29
   float xv[8];
+  float cvs[2][8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) xv[s] = rowp[min(4 * s + g, kF - 1)];
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      cvs[n][s] = C[((int64_t)b * kF + min(16 * n + c16, kF - 1)) * kF + min(4 * s + g, kF - 1)];
+  const int nval = xside ? n1[b] : n2[b];
+  const bool valid = r < nval;
+  // the empty asm pins the loads above this point (else the compiler sinks them under the
+  // select / the x-side branch, behind a wait of their own)
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) asm volatile("" : "+v"(cvs[n][s]));
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    const int k = 4 * s + g;
-    xv[s] = (valid && k < kF) ? rowp[k] : 0.f;
+    asm volatile("" : "+v"(xv[s]));
+    xv[s] = (valid && 4 * s + g < kF) ? xv[s] : 0.f;
   }
   float (*Ew)[kK + 1] = E[w];
   if (xside) {
@@ -91,11 +113,8 @@ __global__ __launch_bounds__(256) void fd_prep_kernel(const float* __restrict__ 
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       const int cc = 16 * n + c16;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const int k = 4 * s + g;
-        const float cv = (cc < kF && k < kF) ? C[((int64_t)b * kF + cc) * kF + k] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s], cv, acc, 0, 0, 0);
-      }
+      for (int s = 0; s < 8; ++s)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[s], (cc < kF && 4 * s + g < kF) ? cvs[n][s] : 0.f, acc, 0, 0, 0);
 #pragma unroll
       for (int q = 0; q < 4; ++q) Ew[4 * g + q][cc] = acc[q];
     }
@@ -287,15 +306,17 @@ struct Top1x4 {
 };
 
 // kCH row tiles of one LDS chunk against this wave's column tile
+// (all kCH fragments are read from LDS before the first MFMA: one LDS latency per chunk instead
+// of one per tile, and kCH independent accumulation chains for the MFMA pipe)
 template <int MODE>
 __device__ __forceinline__ void chunk_dist(const char* rb, const float* nb, const BOp<MODE>& bo, int lane,
                                            float (&d)[kCH][4]) {
+  Frag<MODE> f[kCH];
 #pragma unroll
-  for (int t = 0; t < kCH; ++t) {
-    Frag<MODE> f;
-    read_frag<MODE>(rb + tile_bytes(MODE) * t, nb + t * 16, lane, f);
-    tile_dist<MODE>(f, bo, d[t]);
-  }
+  for (int t = 0; t < kCH; ++t) read_frag<MODE>(rb + tile_bytes(MODE) * t, nb + t * 16, lane, f[t]);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int t = 0; t < kCH; ++t) tile_dist<MODE>(f[t], bo, d[t]);
 }
 
 // the selection over one chunk's distances (tiles c0 .. c0 + kCH - 1)
@@ -389,27 +410,33 @@ __global__ __launch_bounds__(64 * kWaves) void fd_main_kernel(
   constexpr int VPT = kCH * TB / 16 / (64 * kWaves);  // float4s per thread per chunk
   float4 stage[VPT];
   float nst = 0.f;  // one norm per thread (threads < kCH * 16)
+  // (unconditional loads at a clamped element: a guarded load would put an
+  // exec-mask branch and a wait for it inside the MFMA loop)
+  // exec-mask branch and a wait for it inside the MFMA loop); the padding select happens at the
+  // LDS store, after the chunk's MFMAs, so nothing reads the loaded registers early
+  int lim = 0;
   auto gload = [&](int c0, int cn) {
     const float4* src = reinterpret_cast<const float4*>(At + (int64_t)c0 * TB);
+    lim = cn * TB / 16;
 #pragma unroll
-    for (int v = 0; v < VPT; ++v) {
-      const int e = threadIdx.x + 64 * kWaves * v;
-      if (e < cn * TB / 16) {
-        stage[v] = src[e];
-      } else {  // past the row part: padding rows (+inf |x|^2 slot in mode 0: lane group 2, k = 30)
-        const int q = e % (TB / 16);
-        const bool inf_slot = MODE == 0 && (q & 1) && (q >> 5) == 2;
-        stage[v] = make_float4(0.f, 0.f, 0.f, inf_slot ? __builtin_huge_valf() : 0.f);
-      }
-    }
-    if (MODE != 0 && threadIdx.x < kCH * 16)
-      nst = threadIdx.x < cn * 16 ? nAt[(int64_t)c0 * 16 + threadIdx.x] : __builtin_huge_valf();
+    for (int v = 0; v < VPT; ++v) stage[v] = src[min((int)threadIdx.x + 64 * kWaves * v, lim - 1)];
+    if (MODE != 0 && threadIdx.x < kCH * 16) nst = nAt[(int64_t)c0 * 16 + min((int)threadIdx.x, cn * 16 - 1)];
   };
   auto lstore = [&](int buf) {
     float4* dst = reinterpret_cast<float4*>(&ring[buf][0][0]);
 #pragma unroll
-    for (int v = 0; v < VPT; ++v) dst[threadIdx.x + 64 * kWaves * v] = stage[v];
-    if (MODE != 0 && threadIdx.x < kCH * 16) (&nring[buf][0][0])[threadIdx.x] = nst;
+    for (int v = 0; v < VPT; ++v) {
+      const int e = threadIdx.x + 64 * kWaves * v;
+      // past the row part: padding rows (+inf |x|^2 slot in mode 0: lane group 2, k = 30)
+      const int q = e % (TB / 16);
+      const bool inf_slot = MODE == 0 && (q & 1) && (q >> 5) == 2;
+      const bool in = e < lim;
+      const float4 x = stage[v];
+      dst[e] = make_float4(in ? x.x : 0.f, in ? x.y : 0.f, in ? x.z : 0.f,
+                           in ? x.w : (inf_slot ? __builtin_huge_valf() : 0.f));
+    }
+    if (MODE != 0 && threadIdx.x < kCH * 16)
+      (&nring[buf][0][0])[threadIdx.x] = (int)threadIdx.x < lim / (TB / 16) * 16 ? nst : __builtin_huge_valf();
   };
   const int nch = (te - tb + kCH - 1) / kCH;
   if (nch > 0) {
@@ -417,6 +444,10 @@ __global__ __launch_bounds__(64 * kWaves) void fd_main_kernel(
     lstore(0);
   }
   __syncthreads();
+  // vmcnt(0) on every path into the loop (the column operand's loads included): otherwise the
+  // wait counter pass keeps them pending at the loop header and waits for the next chunk's
+  // loads inside the MFMA loop
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   // software pipeline: the selection over chunk ci - 1 (registers) runs beside the MFMAs of
   // chunk ci; dp starts as +inf (never selected)
   float dp[kCH][4];
@@ -469,6 +500,187 @@ __global__ __launch_bounds__(64 * kWaves) void fd_main_kernel(
     for (int q = 0; q < TOPK; ++q) {
       part_v[o + q] = best.v[q];
       part_i[o + q] = best.i[q];
+    }
+  }
+}
+
+// The main pass without LDS staging (the default; PK_FD_DIRECT=0 selects the LDS-ring pass
+// above). Block = 4 waves = 2 column pairs x 2 row halves: wave (wc, wr) takes column tiles
+// 4 cg + 2 wc and 4 cg + 2 wc + 1 and half wr of the block's row tiles, reading the rows' MFMA
+// fragments straight from L2 into registers one chunk of CHD tiles ahead of the MFMAs (two
+// register buffers: the next chunk's loads are in flight during this chunk's 16 * CHD MFMAs).
+// Every A fragment feeds both column tiles (two independent accumulation chains per row tile,
+// half the L2 traffic per MFMA of a one-column wave); no barrier until the end, where the
+// second row half hands its lists through LDS to the first, which merges them (ties: lower
+// row) and writes the block's columns.
+template <int TOPK, int MODE>
+__global__ __launch_bounds__(64 * kWaves) void fd_main_direct_kernel(
+    const char* __restrict__ A, const char* __restrict__ Bq, const float* __restrict__ nA,
+    const float* __restrict__ nB, const int32_t* __restrict__ n1, const int32_t* __restrict__ n2, int T1, int T2,
+    int V2max, int NCG, int RS, int64_t* __restrict__ out_idx, float* __restrict__ out_dist,
+    float* __restrict__ part_v, int32_t* __restrict__ part_i) {
+  constexpr int TB = tile_bytes(MODE);
+  constexpr int CHD = MODE == 2 ? 2 : 4;
+  __shared__ float hv[2][2][16][TOPK];  // second row half's lists: [wc][column tile][column][k]
+  __shared__ int hi_[2][2][16][TOPK];
+  const int per = NCG * RS;
+  const int B = (int)(gridDim.x / per);
+  int b, k;
+  {  // all blocks of crop b on XCD b % 8 (hardware block L lands on XCD L % 8) when B % 8 == 0
+    const int L = blockIdx.x;
+    if ((B & 7) == 0) {
+      const int x8 = L & 7, q = L >> 3;
+      b = x8 + 8 * (q / per);
+      k = q - (q / per) * per;
+    } else {
+      b = L / per;
+      k = L - b * per;
+    }
+  }
+  const int cg = k % NCG, rs = k / NCG;
+  const int lane = pk::lane_id(), w = pk::wave_id();
+  const int g = lane >> 4, c16 = lane & 15;
+  // (readfirstlane: the wave-uniform values in scalar registers, so the chunk loop is a scalar
+  // loop and not an exec-masked one whose wait counts the compiler cannot track)
+  const int wc = __builtin_amdgcn_readfirstlane(w & 1), wr = __builtin_amdgcn_readfirstlane(w >> 1);
+  const int ct0 = cg * kWaves + 2 * wc;  // this wave's column tiles ct0, ct0 + 1
+  const int N1 = n1[b], N2 = n2[b];
+  const int nt = (N1 + 15) >> 4;
+  const int tb0 = (nt * rs) / RS, te0 = (nt * (rs + 1)) / RS;      // the block's row part
+  const int tb = tb0 + ((te0 - tb0) * wr) / 2, te = tb0 + ((te0 - tb0) * (wr + 1)) / 2;  // this wave's half
+  BOp<MODE> bo[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {  // (a column tile past T2 reads tile T2 - 1; its lists are not written)
+    const char* bt = Bq + ((int64_t)b * T2 + min(ct0 + c, T2 - 1)) * TB;
+    if constexpr (MODE == 0) {
+      const float4* p = reinterpret_cast<const float4*>(bt + lane * 32);
+      const float4 u = p[0], v = p[1];
+      bo[c].b[0] = u.x; bo[c].b[1] = u.y; bo[c].b[2] = u.z; bo[c].b[3] = u.w;
+      bo[c].b[4] = v.x; bo[c].b[5] = v.y; bo[c].b[6] = v.z; bo[c].b[7] = v.w;
+    } else {
+      bo[c].hi = *reinterpret_cast<const bf16x8*>(bt + lane * 16);
+      if constexpr (MODE == 2) bo[c].lo = *reinterpret_cast<const bf16x8*>(bt + 1024 + lane * 16);
+      bo[c].n = nB[((int64_t)b * T2 + min(ct0 + c, T2 - 1)) * 16 + c16];
+    }
+  }
+  const char* At = A + (int64_t)b * T1 * TB;
+  const float* nAt = MODE != 0 ? nA + (int64_t)b * T1 * 16 : nullptr;
+  TopK<TOPK> best[2];
+  Top1x4 b4[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    best[c].init();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      b4[c].k[r] = 0x7f800000;  // +inf: never replaced by an equal key
+      b4[c].t[r] = 0x7fffffff;
+    }
+  }
+  // tiles past te are loaded at te - 1 (unconditional loads: no branch, no early wait) and
+  // their distances masked to +inf before the selection
+  auto load = [&](Frag<MODE> (&f)[CHD], int c0) {
+#pragma unroll
+    for (int t = 0; t < CHD; ++t) {
+      const int tt = min(c0 + t, te - 1);
+      read_frag<MODE>(At + (int64_t)tt * TB, nAt ? nAt + (int64_t)tt * 16 : nullptr, lane, f[t]);
+    }
+  };
+  auto compute = [&](const Frag<MODE> (&f)[CHD], int c0) {
+#pragma unroll
+    for (int t = 0; t < CHD; ++t) {
+      float d[2][4];
+      tile_dist<MODE>(f[t], bo[0], d[0]);
+      tile_dist<MODE>(f[t], bo[1], d[1]);
+      const bool in = c0 + t < te;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        if constexpr (TOPK == 1) {
+          constexpr int kClamp = 0x0da24260;  // bits of 1e-30f: clamp_min(1e-30) (cdist mm path)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = in ? max(__float_as_int(d[c][r]), kClamp) : 0x7f800000;
+            const int m = (key - b4[c].k[r]) >> 31;  // -1 iff key < best
+            b4[c].t[r] = (m & (c0 + t)) | (~m & b4[c].t[r]);
+            b4[c].k[r] = min(key, b4[c].k[r]);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) d[c][r] = in ? d[c][r] : __builtin_huge_valf();
+          epilogue<TOPK>(d[c], (c0 + t) * 16 + 4 * g, best[c]);
+        }
+      }
+    }
+  };
+  const int nch = __builtin_amdgcn_readfirstlane(te > tb ? (te - tb + CHD - 1) / CHD : 0);
+  if (nch > 0) {
+    // (sched_barrier: the scheduler would otherwise sink each load next to its first use)
+    Frag<MODE> fa[CHD], fb[CHD];
+    load(fa, tb);
+    // (no early exit: every iteration issues both loads, so a chunk's loads are always in
+    // flight across the previous chunk's MFMAs, the back edge included)
+    for (int ci = 0; ci < nch; ci += 2) {
+      const int c0 = tb + ci * CHD;
+      load(fb, c0 + CHD);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(fa, c0);
+      load(fa, c0 + 2 * CHD);
+      __builtin_amdgcn_sched_barrier(0);
+      if (ci + 1 < nch) compute(fb, c0 + CHD);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    if constexpr (TOPK == 1) {  // the 4 row offsets: smallest value, ties lowest row
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = b4[c].t[r] == 0x7fffffff ? 0x7fffffff : b4[c].t[r] * 16 + 4 * g + r;
+        const float v = __int_as_float(b4[c].k[r]);
+        const bool take = v < best[c].v[0] || (v == best[c].v[0] && row < best[c].i[0]);
+        best[c].v[0] = take ? v : best[c].v[0];
+        best[c].i[0] = take ? row : best[c].i[0];
+      }
+    }
+    lanegroup_merge<TOPK>(best[c]);
+  }
+  // the second row half's lists to the first (ties: lower row — the merge's index rule)
+  if (wr == 1 && g == 0) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int q = 0; q < TOPK; ++q) {
+        hv[wc][c][c16][q] = best[c].v[q];
+        hi_[wc][c][c16][q] = best[c].i[q];
+      }
+  }
+  __syncthreads();
+  if (wr == 1 || g != 0) return;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    float ov[TOPK];
+    int oi[TOPK];
+#pragma unroll
+    for (int q = 0; q < TOPK; ++q) {
+      ov[q] = hv[wc][c][c16][q];
+      oi[q] = hi_[wc][c][c16][q];
+    }
+    best[c].merge(ov, oi);
+    const int ct = ct0 + c;
+    const int j = ct * 16 + c16;
+    if (ct >= T2 || j >= N2) continue;
+    if (RS == 1) {
+      const int64_t o = ((int64_t)b * V2max + j) * TOPK;
+#pragma unroll
+      for (int q = 0; q < TOPK; ++q) {
+        out_idx[o + q] = best[c].i[q] == 0x7fffffff ? -1 : best[c].i[q];
+        if (out_dist) out_dist[o + q] = sqrtf(best[c].v[q]);
+      }
+    } else {
+      const int64_t o = (((int64_t)b * RS + rs) * V2max + j) * TOPK;
+#pragma unroll
+      for (int q = 0; q < TOPK; ++q) {
+        part_v[o + q] = best[c].v[q];
+        part_i[o + q] = best[c].i[q];
+      }
     }
   }
 }
@@ -558,15 +770,25 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
   int32_t* pi = p.RS > 1 ? reinterpret_cast<int32_t*>(reinterpret_cast<char*>(pv) + p.pv_bytes) : nullptr;
   const dim3 pg((std::max(p.T1, p.T2) + 3) / 4, B, 2);
 #define PK_FD_PREP(M)                                                                                              \
-  hipLaunchKernelGGL(fd_prep_kernel<M>, pg, dim3(256), 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, n2, V1max, V2max, \
+  hipLaunchKernelGGL((fd_prep_kernel<M>), pg, dim3(256), 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, n2, V1max, V2max, \
                      p.T1, p.T2, A, Bq, nA, nB)
   if (mode == 0) PK_FD_PREP(0); else if (mode == 1) PK_FD_PREP(1); else PK_FD_PREP(2);
 #undef PK_FD_PREP
   PK_CHECK_LAUNCH();
   const dim3 grid((unsigned)((int64_t)B * p.NCG * p.RS)), block(64 * kWaves);
-#define PK_FD_MAIN(K, M)                                                                                        \
-  hipLaunchKernelGGL((fd_main_kernel<K, M>), grid, block, 0, s, A, Bq, nA, nB, n1, n2, p.T1, p.T2, V2max, p.NCG, \
-                     p.RS, out_idx, out_dist, pv, pi)
+  static const int direct = [] {  // development knob PK_FD_DIRECT: 0 = LDS-ring main pass
+    const char* e = std::getenv("PK_FD_DIRECT");
+    return e ? std::atoi(e) : 1;
+  }();
+#define PK_FD_MAIN(K, M)                                                                                          \
+  do {                                                                                                            \
+    if (direct)                                                                                                   \
+      hipLaunchKernelGGL((fd_main_direct_kernel<K, M>), grid, block, 0, s, A, Bq, nA, nB, n1, n2, p.T1, p.T2,     \
+                         V2max, p.NCG, p.RS, out_idx, out_dist, pv, pi);                                          \
+    else                                                                                                          \
+      hipLaunchKernelGGL((fd_main_kernel<K, M>), grid, block, 0, s, A, Bq, nA, nB, n1, n2, p.T1, p.T2, V2max,     \
+                         p.NCG, p.RS, out_idx, out_dist, pv, pi);                                                 \
+  } while (0)
   if (topk == 1) {
     if (mode == 0) PK_FD_MAIN(1, 0); else if (mode == 1) PK_FD_MAIN(1, 1); else PK_FD_MAIN(1, 2);
   } else {
