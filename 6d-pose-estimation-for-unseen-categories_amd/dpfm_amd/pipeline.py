@@ -324,7 +324,21 @@ class TrainStep:
         producer may form it with the crops (Crops.C_gt) off the step's critical path."""
         return ops.cgt_lstsq(crops.pairs, crops.npairs, op.cad_evecs, op.pc_evecs)
 
-    def forward_backward(self, op: Operators, crops: Crops) -> dict:
+    @staticmethod
+    @torch.no_grad()
+    def inlier_ratio_of(op: Operators, crops: Crops, C_pred: torch.Tensor) -> torch.Tensor:
+        """train.py:109-116: the naive point map of C_pred and its mean inlier ratio over the
+        crops (naive_p2p_batched without materialising its arange row: the IR kernel reads the
+        map as [B, V2] CAD indices of crop points 0..n2-1)."""
+        B_, V2_ = op.pc_evecs.shape[0], op.pc_evecs.shape[1]
+        n1 = _counts(op.cad_n, B_, op.cad_evecs.shape[1], C_pred.device)
+        npred = _counts(crops.n2, B_, V2_, C_pred.device)
+        p_map, _ = ops.feat_dist_topk(op.cad_evecs, C_pred.detach(), op.pc_evecs, n1, npred, 1)
+        return ops.inlier_ratio(p_map[..., 0], npred, op.cad_xyz, crops.align32, op.ir_thr, layout=2).mean()
+
+    def forward_backward(self, op: Operators, crops: Crops, ir: bool = True) -> dict:
+        """ir=False leaves the naive point map + IR out of the step (PipelinedTrainer computes it
+        beside the next steps from the C_pred this step leaves in `self.last_C_pred`)."""
         self.model.train()
         batch = model_batch(op, crops)
         main = torch.cuda.current_stream() if self.overlap else None
@@ -335,6 +349,7 @@ class TrainStep:
             with torch.no_grad(), _on(self.aux):
                 C_gt = self.ground_truth(op, crops)
         C_pred, o12, o21, f1, f2, _, _ = self.model(batch)
+        self.last_C_pred = C_pred.detach()
         if self.overlap:
             main.wait_stream(self.aux)
             C_gt.record_stream(main)
@@ -343,13 +358,7 @@ class TrainStep:
         if self.overlap:  # the point map + IR read only C_pred: beside the backward
             self.aux.wait_stream(main)
         with torch.no_grad(), _on(self.aux):  # train.py:109-116 (naive solver + IR per crop)
-            # naive point map (naive_p2p_batched without materialising its arange row: the IR
-            # kernel reads the map as [B, V2] CAD indices of crop points 0..n2-1)
-            B_, V2_ = op.pc_evecs.shape[0], op.pc_evecs.shape[1]
-            n1 = _counts(op.cad_n, B_, op.cad_evecs.shape[1], C_pred.device)
-            npred = _counts(crops.n2, B_, V2_, C_pred.device)
-            p_map, _ = ops.feat_dist_topk(op.cad_evecs, C_pred.detach(), op.pc_evecs, n1, npred, 1)
-            ir = ops.inlier_ratio(p_map[..., 0], npred, op.cad_xyz, crops.align32, op.ir_thr, layout=2).mean()
+            ir = self.inlier_ratio_of(op, crops, C_pred) if ir else None
             # P truncated at the pair capacity would train on partial labels: flag it (device
             # bool, formed with the crops on the crop-formation stream)
             log["pair_overflow"] = crops.overflow()
@@ -368,10 +377,11 @@ class TrainStep:
         finally:
             if self.side is not None:
                 self.side.end(run=ok)
-        if self.overlap:
+        if self.overlap and ir is not None:
             main.wait_stream(self.aux)
             ir.record_stream(main)
-        log["IR"] = ir
+        if ir is not None:
+            log["IR"] = ir
         return log
 
     def _fused_state(self):
@@ -498,7 +508,13 @@ class PipelinedTrainer:
     crop buffers ping-pong: graph C_k forms crops into buffer k on the side stream, graph
     T_k trains on buffer k on the main stream; events order C_k after T_k of the previous
     use and T_k after C_k. Every piece is a HIP graph replay. With several ranks each
-    T_k is split around the eager RCCL all-reduce, as in GraphedTrainStep."""
+    T_k is split around the eager RCCL all-reduce, as in GraphedTrainStep.
+
+    The step's naive point map + IR (a logged metric; nothing trains on it) leaves the training
+    graphs (development knob PK_DEFER_IR=0 keeps it there): graph I_k computes the IR of
+    buffer k's batch from the C_pred that T_k left, on the crop-formation stream right before
+    C_k overwrites the buffer. The IR of step i is therefore ready once the next call has
+    enqueued I_k (or after flush()); the log's "IR" tensor is filled in place."""
 
     def __init__(self, crop_formation: CropFormation, step: TrainStep, fb: FrameBatch, op: Operators,
                  warmup: int = 3):
@@ -534,14 +550,21 @@ class PipelinedTrainer:
                     c.C_gt = TrainStep.ground_truth(op, c)
                 self.crops.append(c)
             self.crop_graphs.append(g)
+        self.defer_ir = os.environ.get("PK_DEFER_IR", "1") == "1"
+        self.ir_graphs, self._trained = [], [False, False]
         for k in range(2):
             step.opt.zero_grad(set_to_none=True)  # each training graph owns its gradients
             ga = torch.cuda.CUDAGraph()
             ga.register_generator_state(step.gen)
             with torch.cuda.graph(ga):
-                self.logs.append(step.forward_backward(op, self.crops[k]))
+                self.logs.append(step.forward_backward(op, self.crops[k], ir=not self.defer_ir))
                 if not self.split:
                     step.apply(allreduce=False, reset=False)
+            if self.defer_ir:  # I_k: reads buffer k's crops and T_k's C_pred (both graph-static)
+                gi = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gi):
+                    self.logs[k]["IR"] = TrainStep.inlier_ratio_of(op, self.crops[k], step.last_C_pred)
+                self.ir_graphs.append(gi)
             self.grads.append([p.grad for p in step.params])
             gb = None
             if self.split:
@@ -571,8 +594,23 @@ class PipelinedTrainer:
     def _form(self, k):
         with torch.cuda.stream(self.side):
             self.side.wait_event(self.consumed[k])
+            if self.defer_ir and self._trained[k]:  # the IR of the batch T_k last trained on
+                self.ir_graphs[k].replay()
             self.crop_graphs[k].replay()
             self.formed[k].record(self.side)
+
+    def flush(self):
+        """Compute the IR still pending for the last step (its buffer's I_k), so every log
+        returned so far holds its IR once the device reaches this point."""
+        if not self.defer_ir or self.i == 0:
+            return
+        k = (self.i - 1) & 1
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(self.consumed[k])
+            self.ir_graphs[k].replay()
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        torch.cuda.current_stream().wait_event(ev)
 
     def _worker_loop(self):
         torch.cuda.set_device(self.main.device)
@@ -599,6 +637,7 @@ class PipelinedTrainer:
                 self.step.allreduce_grads(self.grads[k])
                 self.train_b[k].replay()
             self.consumed[k].record(self.main)
+        self._trained[k] = True
         self.i += 1
         return self.logs[k]
 

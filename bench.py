@@ -858,6 +858,9 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if hasattr(one_step, "flush"):  # PipelinedTrainer: the last step's IR (computed beside the next step)
+        one_step.flush()
+        torch.cuda.synchronize()
     extra = {}
     if args.mode == "train":
         extra = {"loss": round(float(log["loss"]), 5), "ir": round(float(log["IR"]), 5),

@@ -184,8 +184,10 @@ def test_pipelined_trainer_matches_eager(device):
         eager.load_state_from(ps)
         le = eager(op, cf(fb))
         lp = pipe()
+        pipe.flush()  # the step's IR, computed beside the training stream (PipelinedTrainer doc)
         torch.cuda.synchronize()
         assert torch.equal(le["loss"], lp["loss"]), (le["loss"], lp["loss"])
+        assert torch.equal(le["IR"], lp["IR"]), (le["IR"], lp["IR"])
         diff = [n for (n, a), b in zip(m_eager.named_parameters(), m_pipe.parameters()) if not torch.equal(a, b)]
         assert not diff, diff
 
