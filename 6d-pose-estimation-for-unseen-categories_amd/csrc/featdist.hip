@@ -53,7 +53,7 @@ __host__ __device__ constexpr int tile_bytes(int mode) { return mode == 0 ? 2048
 
 __device__ __forceinline__ __bf16 to_bf16(float v) { return (__bf16)v; }
 
-// grid (ceil(max(T1, T2) / 4), B, 2), block 256: wave = one 16-row tile of one side (z = 0:
+// grid (ceil(max(T1, T2) / 8), B, 2), block 512: wave = one 16-row tile of one side (z = 0:
 // x side, 1: y side). Lane (g, c) = (lane >> 4, lane & 15).
 //   x side: emb = x C^T on the f32 MFMA ([16 x 32] x [32 x 32], two 16 x 16 output tiles,
 //           K = 30 zero-padded; an f32 MFMA accumulates as the fmaf chain over k in order),
@@ -61,19 +61,21 @@ __device__ __forceinline__ __bf16 to_bf16(float v) { return (__bf16)v; }
 //   y side: y itself.
 // The squared norm of a row is its lane group's 8 values summed per lane, then across the 4
 // lanes of the row (fixed order). Rows >= n (and the tile padding) are written as zeros.
+constexpr int kPrepWaves = 8;  // one 16-row tile per wave, 8 waves per block
+
 template <int MODE>
-__global__ __launch_bounds__(256) void fd_prep_kernel(const float* __restrict__ ex, int ldx,
+__global__ __launch_bounds__(64 * kPrepWaves) void fd_prep_kernel(const float* __restrict__ ex, int ldx,
                                                       const float* __restrict__ C, const float* __restrict__ ey,
                                                       int ldy, const int32_t* __restrict__ n1,
                                                       const int32_t* __restrict__ n2, int V1max, int V2max, int T1,
                                                       int T2, char* __restrict__ A, char* __restrict__ Bq,
                                                       float* __restrict__ nA, float* __restrict__ nB) {
-  __shared__ float E[4][16][kK + 1];  // per wave: the tile's rows (emb or y), k padded to 32
+  __shared__ float E[kPrepWaves][16][kK + 1];  // per wave: the tile's rows (emb or y), k padded to 32
   const int b = blockIdx.y;
   const bool xside = blockIdx.z == 0;
   const int w = pk::wave_id(), lane = pk::lane_id(), g = lane >> 4, c16 = lane & 15;
   const int T = xside ? T1 : T2;
-  const int tile = blockIdx.x * 4 + w;
+  const int tile = blockIdx.x * kPrepWaves + w;
   if (tile >= T) return;
   const int r = tile * 16 + c16;
   // every operand load is issued before the first wait: the row at a clamped index (its
@@ -768,9 +770,9 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
   float* nB = mode ? reinterpret_cast<float*>(Bq + p.b_bytes + p.na_bytes) : nullptr;
   float* pv = p.RS > 1 ? reinterpret_cast<float*>(Bq + p.b_bytes + p.na_bytes + p.nb_bytes) : nullptr;
   int32_t* pi = p.RS > 1 ? reinterpret_cast<int32_t*>(reinterpret_cast<char*>(pv) + p.pv_bytes) : nullptr;
-  const dim3 pg((std::max(p.T1, p.T2) + 3) / 4, B, 2);
+  const dim3 pg((std::max(p.T1, p.T2) + kPrepWaves - 1) / kPrepWaves, B, 2);
 #define PK_FD_PREP(M)                                                                                              \
-  hipLaunchKernelGGL((fd_prep_kernel<M>), pg, dim3(256), 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, n2, V1max, V2max, \
+  hipLaunchKernelGGL((fd_prep_kernel<M>), pg, dim3(64 * kPrepWaves), 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, n2, V1max, V2max, \
                      p.T1, p.T2, A, Bq, nA, nB)
   if (mode == 0) PK_FD_PREP(0); else if (mode == 1) PK_FD_PREP(1); else PK_FD_PREP(2);
 #undef PK_FD_PREP
