@@ -8,7 +8,7 @@ attention, the merge, a concatenation, the MLP (two layers + InstanceNorm/ReLU) 
 add forward; backward adds the slices' copies and the gradient accumulations of desc and src.
 This node issues (forward) q, the stacked key/value projection (one 32 -> 64 launch reading
 `src` once, pk_linear_ex w2), the attention on the stacked buffer (batch strides), the merge
-written straight into the concatenation buffer, a copy of desc beside it, mlp.0,
+written straight into the concatenation buffer, a copy of desc beside it (pk_copy_rows), mlp.0,
 InstanceNorm+ReLU and mlp.3 with the residual in its epilogue; backward: mlp.3^T, the norm
 backward, mlp.0^T, the merge^T reading its slice in place, the attention backward writing dk / dv
 into one stacked buffer, Pq^T with BOTH other contributions to d desc (the residual and the
@@ -52,7 +52,8 @@ class _AttnPropFn(torch.autograd.Function):
         call("pk_attention_fwd", ptr(q), ptr(kv), vptr, B, D, heads, N, M, 2 * C * M, 2 * C * M, ptr(a), ptr(lse),
              _lib.stream(dev), work=("mfma", 2 * 2 * N * M * D * B * heads))
         hc = torch.empty((B, 2 * C, N), dtype=torch.float32, device=dev)  # cat(desc, message)
-        hc[:, :C].copy_(x)
+        call("pk_copy_rows", ptr(hc), 2 * C * N, ptr(x), C * N, B, C * N, _lib.stream(dev),
+             work=("hbm", 8 * B * C * N))
         ops.linear_ex(a, f(wm), bm, 1, B * N, N, C, C, y=hc[:, C:], ldy=2 * C * N)
         h1 = torch.empty((B, 2 * C, N), dtype=torch.float32, device=dev)
         ops.linear_ex(hc, f(w0), b0, 1, B * N, N, 2 * C, 2 * C, y=h1)

@@ -619,6 +619,12 @@ int pk_tufted_laplacian(const double* pts, int64_t n, const int32_t* tri, int64_
                         int64_t cap, int32_t* ii, int32_t* jj, double* ww, int64_t* nnz, double* mass,
                         int64_t* nflips);
 
+/* pk_copy_rows: rows blocks of n floats from src (block stride ld_src floats) to dst (ld_dst):
+ * the x half of torch.cat([x, message], dim=1) (modeling/dpfm.py:67) in the fused
+ * AttentionalPropagation node's [B, 2C, N] buffer (rows = B, n = C N, ld_dst = 2 C N). */
+int pk_copy_rows(float* dst, int64_t ld_dst, const float* src, int64_t ld_src, int64_t rows, int64_t n,
+                 void* stream);
+
 /* Runtime helpers of the pipelined executors (host only; no reference counterpart: the reference
  * overlaps crop formation with training through DataLoader worker PROCESSES, train.py /
  * dataset/object.py:117-274; here the overlap is two HIP streams on one device).

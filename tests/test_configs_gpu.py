@@ -61,6 +61,38 @@ def test_feat_dist_argmin_top5_configs(device, B, V):
     assert ties <= max(2, B * V // 1000), ties
 
 
+def test_feat_dist_ragged_edges(device):
+    """The feature-distance passes on a ragged batch whose per-crop sizes straddle the 16-row
+    tile, the 4-tile register chunk and the two row halves of a block (n1, n2 in 1 .. 301):
+    argmin / top-5 vs cdist on each crop's valid block (near-ties counted as above); with fewer
+    than 5 valid rows the top-5 list holds them in order, then -1."""
+    from dpfm_amd import ops
+    sizes = [(1, 1), (1, 301), (301, 1), (15, 16), (16, 17), (17, 15), (64, 65), (65, 129), (129, 64),
+             (200, 200), (5, 300), (300, 5)]
+    B, V1, V2 = len(sizes), 320, 320
+    g = torch.Generator().manual_seed(11)
+    ex = torch.stack([_spectral(V1, 300 + b) for b in range(B)])
+    ey = torch.stack([_spectral(V2, 400 + b) for b in range(B)])
+    C = torch.eye(30)[None] + 0.3 * torch.randn(B, 30, 30, generator=g)
+    n1 = torch.tensor([a for a, _ in sizes], dtype=torch.int32, device=device)
+    n2 = torch.tensor([c for _, c in sizes], dtype=torch.int32, device=device)
+    i1, _ = ops.feat_dist_topk(ex.to(device), C.to(device), ey.to(device), n1, n2, 1)
+    i5, _ = ops.feat_dist_topk(ex.to(device), C.to(device), ey.to(device), n1, n2, 5)
+    i1, i5 = i1.cpu().numpy(), i5.cpu().numpy()
+    ties = 0
+    for b, (a, c) in enumerate(sizes):
+        dist = torch.cdist(ex[b, :a, :30] @ C[b].t(), ey[b, :c, :30]).numpy().astype(np.float64)
+        ties += check_topk(dist, i1[b, :c], 1)
+        if a >= 5:
+            ties += check_topk(dist, i5[b, :c], 5)
+        else:  # fewer than 5 rows: the valid ones in order, then -1
+            assert (i5[b, :c, a:] == -1).all()
+            srt = np.argsort(dist, axis=0, kind="stable")[:a].T
+            picked = np.take_along_axis(dist, i5[b, :c, :a].T, axis=0)
+            assert np.allclose(picked, np.take_along_axis(dist, srt.T, axis=0), rtol=1e-5, atol=1e-6)
+    assert ties <= 3, ties
+
+
 def _rigid_scene(V2, seed):
     from dpfm_amd.dataset.synthetic import random_rotation
     rng = np.random.default_rng(seed)
