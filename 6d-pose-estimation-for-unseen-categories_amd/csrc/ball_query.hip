@@ -546,6 +546,7 @@ extern "C" int pk_ball_query_mask(const double* cad, const int64_t* cad_off, con
   return PK_OK;
 }
 
+#ifdef PK_DEVBUILD
 // Development hook (not in include/posekern.h): the previous fp32-screen kernel, for A/B timing.
 extern "C" int pkdev_ball_query_mask_v1(const double* cad, const int64_t* cad_off, const double* pc,
                                         const int64_t* pc_off, const double* thr2, int B, int n1max,
@@ -558,7 +559,9 @@ extern "C" int pkdev_ball_query_mask_v1(const double* cad, const int64_t* cad_of
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
+#endif  // PK_DEVBUILD
 
+#ifdef PK_DEVBUILD
 // Development hook (not in include/posekern.h): the all-fp64 mask kernel, for A/B timing.
 extern "C" int pkdev_ball_query_mask64(const double* cad, const int64_t* cad_off, const double* pc,
                                        const int64_t* pc_off, const double* thr2, int B, int n1max,
@@ -573,6 +576,7 @@ extern "C" int pkdev_ball_query_mask64(const double* cad, const int64_t* cad_off
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
+#endif  // PK_DEVBUILD
 
 extern "C" int pk_ball_query_pairs(const double* cad, const int64_t* cad_off, const double* pc,
                                    const int64_t* pc_off, const double* thr2, int B, int n1max,

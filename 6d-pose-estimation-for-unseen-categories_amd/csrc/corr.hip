@@ -757,7 +757,11 @@ static int64_t rigid_part_bytes(int B, int nmax, int ldc) {
   return (b + 255) & ~(int64_t)255;
 }
 
+#ifdef PK_DEVBUILD
 static int g_rigid_variant = 0;  // 1: round 2's 64-tile gather path (pkdev_rigidity_variant, A/B timing)
+#else
+constexpr int g_rigid_variant = 0;
+#endif
 
 extern "C" int64_t pk_rigidity_filter_work_size(int B, int nmax, int ldc) {
   if (B <= 0 || nmax <= 0) return 0;
@@ -766,11 +770,13 @@ extern "C" int64_t pk_rigidity_filter_work_size(int B, int nmax, int ldc) {
   return v2 > v1 ? v2 : v1;
 }
 
+#ifdef PK_DEVBUILD
 extern "C" int pkdev_rigidity_variant(int v) {
   const int old = g_rigid_variant;
   if (v >= 0) g_rigid_variant = v;
   return old;
 }
+#endif  // PK_DEVBUILD
 
 extern "C" int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* ncand, const float* cad,
                                   int ldcad, const float* pc, int ldpc, const float* thr4, int B, int nmax,

@@ -914,9 +914,11 @@ extern "C" int pk_sample_rgb(const uint8_t* img, int F, int H, int W, int C, con
   return PK_OK;
 }
 
+#ifdef PK_DEVBUILD
 extern "C" int pkdev_seq_sum(const double* v, int n, double* out, void* stream) {
   PK_REQUIRE(n >= 0 && out && (n == 0 || v));
   hipLaunchKernelGGL(seq_sum_dev_kernel, dim3(1), dim3(kStatThreads), 0, pk::as_stream(stream), v, n, out);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
+#endif  // PK_DEVBUILD

@@ -778,6 +778,7 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
 #undef PK_FD_PREP
   PK_CHECK_LAUNCH();
   const dim3 grid((unsigned)((int64_t)B * p.NCG * p.RS)), block(64 * kWaves);
+#ifdef PK_DEVBUILD
   static const int direct = [] {  // development knob PK_FD_DIRECT: 0 = LDS-ring main pass
     const char* e = std::getenv("PK_FD_DIRECT");
     return e ? std::atoi(e) : 1;
@@ -791,6 +792,11 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
       hipLaunchKernelGGL((fd_main_kernel<K, M>), grid, block, 0, s, A, Bq, nA, nB, n1, n2, p.T1, p.T2, V2max,     \
                          p.NCG, p.RS, out_idx, out_dist, pv, pi);                                                 \
   } while (0)
+#else
+#define PK_FD_MAIN(K, M)                                                                                          \
+  hipLaunchKernelGGL((fd_main_direct_kernel<K, M>), grid, block, 0, s, A, Bq, nA, nB, n1, n2, p.T1, p.T2, V2max,  \
+                     p.NCG, p.RS, out_idx, out_dist, pv, pi)
+#endif
   if (topk == 1) {
     if (mode == 0) PK_FD_MAIN(1, 0); else if (mode == 1) PK_FD_MAIN(1, 1); else PK_FD_MAIN(1, 2);
   } else {

@@ -571,6 +571,7 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
   if (nmax <= kFpsMaxLds) return launch_fps_flat<1024, 13>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
 #endif
 #define PK_FPS(NT, PPT) return launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s)
+#ifdef PK_DEVBUILD
   // development knob (read once): PK_FPS_NT=256 / 512 runs the pruned kernel with fewer waves per
   // crop above 4096 points (less of each CU held while crop formation overlaps the step)
   static const int fps_nt = getenv("PK_FPS_NT") ? atoi(getenv("PK_FPS_NT")) : 1024;
@@ -578,6 +579,7 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
   if (nmax > 4096 && nmax <= 13312 && fps_nt == 512) PK_FPS(512, 26);
   if (nmax > 4096 && nmax <= 8192 && fps_nt == 256) PK_FPS(256, 32);
   if (nmax > 4096 && nmax <= 13312 && fps_nt == 256) PK_FPS(256, 52);
+#endif
   // 1024-thread workgroups above 4096 points: measured 0.712 us per FPS step against 0.78
   // (512 threads) and 1.09 (256) on the bench's crops (n <= 6588, profiles/r02_kbench_fps.txt)
   if (nmax <= 1024) PK_FPS(256, 4);
@@ -597,6 +599,7 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
   return PK_ERR_ARG;  // > 32768 points per crop
 }
 
+#ifdef PK_DEVBUILD
 // Development hook (not part of include/posekern.h): force the block size / points
 // per thread, flat (pruned = 4), per-lane buckets (3), pruned (1) or plain (0), for tools/kbench.py's sweeps.
 extern "C" int pkdev_fps_cfg(const float* xyz, const int64_t* offsets, int B, int nmax,
@@ -616,3 +619,4 @@ extern "C" int pkdev_fps_cfg(const float* xyz, const int64_t* offsets, int B, in
 #undef PK_FPS
   return PK_ERR_ARG;
 }
+#endif  // PK_DEVBUILD

@@ -440,6 +440,7 @@ inline int64_t grouped_slice_rows(int64_t R) {
 
 }  // namespace
 
+#ifdef PK_DEVBUILD
 // Development hook (not in include/posekern.h): the LDS-staged slice kernel, for A/B timing.
 extern "C" int pkdev_linear_wgrad_v1(const float* x, const float* dy, int layout, int64_t R, int I, int O, int N,
                                      float* work, float* dw, float* db, void* stream) {
@@ -456,6 +457,7 @@ extern "C" int pkdev_linear_wgrad_v1(const float* x, const float* dy, int layout
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
+#endif  // PK_DEVBUILD
 
 extern "C" int pk_linear_wgrad(const float* x, const float* dy, int layout, int64_t R, int I, int O, int N,
                                float* work, float* dw, float* db, int accumulate, void* stream) {
@@ -1356,7 +1358,11 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
     // development switch (read once): PK_ROWS_LDS=1 takes the LDS-staged full-line kernel; measured
     // within +-15 % of the fragment-load kernel shape by shape (profiles/r03_lin_bench_lds_vs_r2.txt),
     // so round 2's kernel stays the default
+#ifdef PK_DEVBUILD
     static const bool rows_lds = getenv("PK_ROWS_LDS") != nullptr;
+#else
+    constexpr bool rows_lds = false;
+#endif
     if (rows_lds && Cin >= 32) {  // LDS-staged full-line kernel (linear_rows_lds_kernel)
       auto pickl = [&](auto q, auto gen) {
         constexpr int Qv = decltype(q)::value;
@@ -1485,6 +1491,7 @@ __global__ __launch_bounds__(256, WPS) void linear_ws_rows_kernel(const float* _
   }
 }
 
+#ifdef PK_DEVBUILD
 // Development hook (not in include/posekern.h): the plain rows kernel (no epilogue operands) of
 // y = x W^T + b with Cin = 16 Q in {64, 128}, Cout = 64, in variant `var` (see the kernel), at
 // `blocks` workgroups (0: the production grid), for tools/lin_var.py.
@@ -1519,6 +1526,7 @@ extern "C" int pkdev_linear_rows_var(const float* x, const float* w, const float
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
+#endif  // PK_DEVBUILD
 
 extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, int layout, int64_t R, int N,
                              int Cin, int Cout, int transw, int relu, const float* mask, float* y, void* stream) {

@@ -14,6 +14,9 @@ import torch  # noqa: F401  (loads torch's HIP runtime first so the library bind
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libposekern.so")
+# the same sources built with -DPK_DEVBUILD (development pkdev_* entry points, PK_* environment
+# switches): loaded only by tests / tools that exercise a development hook, never by dpfm_amd
+DEV_LIB_PATH = os.path.join(_HERE, "lib", "libposekern_dev.so")
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -125,6 +128,7 @@ RESTYPES = {"pk_cgt_lstsq_work_size": _I64, "pk_linear_wgrad_grouped_work": _I64
             "pk_rigidity_filter_work_size": _I64}  # everything else returns an int status
 
 _lib: Optional[ctypes.CDLL] = None
+_dev_lib: Optional[ctypes.CDLL] = None
 
 
 class WgradCall(ctypes.Structure):
@@ -159,6 +163,32 @@ def lib() -> ctypes.CDLL:
             fn.restype = RESTYPES.get(name, ctypes.c_int)
         _lib = l
     return _lib
+
+
+def dev_lib() -> ctypes.CDLL:
+    """libposekern_dev.so (pkdev_* hooks; the pk_* entry points bound as in lib()). Its kernels
+    are its own copies: device buffers are shared, library state is not."""
+    global _dev_lib
+    if _dev_lib is None:
+        if not os.path.exists(DEV_LIB_PATH):
+            raise PoseKernError(f"libposekern_dev.so not found at {DEV_LIB_PATH}: `make -C "
+                                "6d-pose-estimation-for-unseen-categories_amd`")
+        l = ctypes.CDLL(DEV_LIB_PATH, mode=ctypes.RTLD_LOCAL)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(l, name)
+            fn.argtypes = argtypes
+            fn.restype = RESTYPES.get(name, ctypes.c_int)
+        _dev_lib = l
+    return _dev_lib
+
+
+def use_dev_lib() -> None:
+    """Route every dpfm_amd call of this process through libposekern_dev.so (tools/ only: the
+    A/B and probe scripts toggle pkdev_* variants of the kernels ops.* launches)."""
+    global _lib
+    if _lib is not None and _lib is not dev_lib():
+        raise PoseKernError("use_dev_lib() must run before the first library call")
+    _lib = dev_lib()
 
 
 _ERRORS = {1000: "invalid argument", 1001: "output capacity exceeded"}

@@ -125,7 +125,7 @@ def attn_prop_residual(layer, x: torch.Tensor, src: torch.Tensor) -> torch.Tenso
     ok = (x.is_cuda and x.dim() == 3 and src.dim() == 3 and x.is_contiguous() and src.is_contiguous()
           and x.dtype == torch.float32 and src.dtype == torch.float32 and C in (16, 32, 64)
           and attn.dim == 16 and C == attn.dim * attn.num_heads and len(mlp) == 4
-          and x.shape[0] == src.shape[0]
+          and x.shape[0] == src.shape[0] and src.shape[1] == C
           and mlp[0].out_channels == 2 * C and mlp[3].out_channels == C)
     if not ok:
         return None

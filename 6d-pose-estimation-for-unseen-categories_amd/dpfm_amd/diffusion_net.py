@@ -11,13 +11,15 @@ per direction (ops.spectral_diffusion); the per-point MLPs are GEMMs.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.nn as nn
 
 from . import ops
 from .layers import Linear
+
+# The whole configured DiffusionNet as one autograd node (_EncoderFn); False runs the per-module
+# path (the parity tests compare the two)
+FUSED_ENCODER = True
 
 
 class LearnedTimeDiffusion(nn.Module):
@@ -103,7 +105,7 @@ class DiffusionNetBlock(nn.Module):
     # The fused block forward (pk_mlp3_fwd) is opt-in: on MI355X it measured no faster than the
     # per-layer kernels it replaces (46 us vs 20 + 12 + 12 us of layer launches plus the concat
     # and the residual add: one 8-wave block per CU, 103 KB of LDS), DESIGN.md §3
-    fused_mlp = os.environ.get("PK_FUSED_BLOCK_MLP", "0") == "1"
+    fused_mlp = False
 
     def _fusable(self, x_in) -> bool:
         lins = [m for m in self.mlp if isinstance(m, Linear)]
@@ -268,7 +270,7 @@ class DiffusionNet(nn.Module):
         if appended:
             x_in, mass, evals, evecs = x_in[None], mass[None], evals[None], evecs[None]
         ps = self._fused_params(x_in) if evecs is not None and evecs.shape[-1] == 64 else None
-        if ps is not None and os.environ.get("PK_FUSED_ENCODER", "1") == "1":
+        if ps is not None and FUSED_ENCODER:
             x = _EncoderFn.apply(x_in.contiguous(), mass.contiguous(), evals.contiguous(), evecs.contiguous(),
                                  len(self.blocks), *ps)
             return x[0] if appended else x

@@ -8,14 +8,16 @@ ref_feat1, ref_feat2). state_dict keys equal weights/weights.pt.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.nn as nn
 
 from .. import ops
 from ..diffusion_net import DiffusionNet
 from ..modeling.dpfm import CrossAttentionRefinementNet, RegularizedFMNet
+
+# models/dpfm.py:66-72 + RegularizedFMNet as the fused two-launch head (ops.fmap_head); False runs
+# the per-module path (the parity tests compare the two)
+FUSED_FMAP_HEAD = True
 
 DEFAULT_CFG = {  # config/dpfm_orig.yaml
     "fmap": {"n_fmap": 30, "k_eig": 64, "n_feat": 32, "C_in": 3, "lambda_": 100, "resolvant_gamma": 0.5,
@@ -80,7 +82,7 @@ class DPFMNet(nn.Module):
 
         k = self.n_fmap
         if (evecs1.dim() == 3 and evecs1.is_cuda and k == 30 and use_feat1.shape[-1] == 32
-                and os.environ.get("PK_FUSED_FMAP_HEAD", "1") == "1"):
+                and FUSED_FMAP_HEAD):
             # models/dpfm.py:66-72 + RegularizedFMNet (modeling/dpfm.py:154-195) fused: the
             # projections, AAt / BAt, the resolvent mask and the solve in two launches
             C_pred = ops.fmap_head(use_feat1, use_feat2, evecs1, evecs2, mass1, mass2, evals1, evals2,

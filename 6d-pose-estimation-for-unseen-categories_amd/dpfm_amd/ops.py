@@ -463,11 +463,13 @@ def linear_wgrad_grouped(calls) -> None:
     keep = []
     for k, (x, dy, cf, dw, db, acc) in enumerate(calls):
         sx = sdy = 0
-        if cf and x.dim() == 3 and x.stride(2) == 1 and x.stride(1) == x.shape[2] and x.stride(0) % 4 == 0:
+        if (cf and x.dim() == 3 and x.stride(2) == 1 and x.stride(1) == x.shape[2] and x.stride(0) % 4 == 0
+                and x.stride(0) >= x.shape[1] * x.shape[2]):  # (stride 0 = an expanded batch: copy)
             sx = x.stride(0)  # a channel slice of a wider channels-first buffer: read in place
         else:
             x = x.contiguous()
-        if cf and dy.dim() == 3 and dy.stride(2) == 1 and dy.stride(1) == dy.shape[2] and dy.stride(0) % 4 == 0:
+        if (cf and dy.dim() == 3 and dy.stride(2) == 1 and dy.stride(1) == dy.shape[2] and dy.stride(0) % 4 == 0
+                and dy.stride(0) >= dy.shape[1] * dy.shape[2]):
             sdy = dy.stride(0)
         else:
             dy = dy.contiguous()

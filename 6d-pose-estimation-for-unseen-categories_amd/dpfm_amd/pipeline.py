@@ -12,7 +12,6 @@ Nothing here synchronises with the host; callers decide when to read results.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -26,12 +25,6 @@ from .dataset.synthetic import cad_points, lbo_operators, make_frame
 from .models.dpfm import DPFMNet
 from .layers import Conv1d, GroupedWgrad, Linear
 from .utils.loss import DPFMLoss
-
-
-def _on(stream):
-    """torch.cuda.stream(stream), or a no-op context for None."""
-    import contextlib
-    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
 
 
 @dataclass
@@ -232,7 +225,7 @@ class TrainStep:
 
     def __init__(self, model: DPFMNet, lr: float = 5e-4, max_norm: float = 5.0, nce_num_pairs: int = 512,
                  group: Optional[dist.ProcessGroup] = None, seed: int = 0, capturable: bool = False,
-                 overlap: bool = True, grouped: bool = True, fused_opt: bool = True):
+                 grouped: bool = True, fused_opt: bool = True):
         self.model = model
         self.params = [p for p in model.parameters()]
         # config/dpfm_orig.gin:62-63; capturable keeps the step count on the device
@@ -257,12 +250,8 @@ class TrainStep:
         self.fused_opt = fused_opt and dev.type == "cuda" and len(self.params) <= 96
         # grouped=True (HIP devices): the per-point layers' weight gradients are recorded during
         # backward and computed in one grouped launch pair at its end (layers.GroupedWgrad).
-        # overlap=True (development knob PK_STEP_OVERLAP=aux): C_gt and the naive point map +
-        # IR on an auxiliary stream beside the model. Off by default: a HIP graph with a
-        # forked stream replayed ~1 ms/step slower than the serial one on MI355X.
-        mode = os.environ.get("PK_STEP_OVERLAP", "none")
-        self.overlap = overlap and dev.type == "cuda" and mode == "aux"
-        self.aux = torch.cuda.Stream(dev) if self.overlap else None
+        # The step stays on one stream: forking C_gt / the IR onto an auxiliary stream inside
+        # the captured graph replayed ~1 ms/step slower on MI355X.
         self.side = None
         if grouped and dev.type == "cuda":
             lin = [p for m in model.modules() if isinstance(m, (Linear, Conv1d)) for p in m.parameters(recurse=False)]
@@ -341,23 +330,14 @@ class TrainStep:
         beside the next steps from the C_pred this step leaves in `self.last_C_pred`)."""
         self.model.train()
         batch = model_batch(op, crops)
-        main = torch.cuda.current_stream() if self.overlap else None
-        if self.overlap:  # C_gt needs only the crops: beside the model forward
-            self.aux.wait_stream(main)
         C_gt = crops.C_gt
         if C_gt is None:
-            with torch.no_grad(), _on(self.aux):
-                C_gt = self.ground_truth(op, crops)
+            C_gt = self.ground_truth(op, crops)
         C_pred, o12, o21, f1, f2, _, _ = self.model(batch)
         self.last_C_pred = C_pred.detach()
-        if self.overlap:
-            main.wait_stream(self.aux)
-            C_gt.record_stream(main)
         loss, log = self.crit.forward_batched(C_pred, C_gt, crops.pairs, crops.npairs, f1, f2, o12, o21,
                                               crops.overlap_12, crops.overlap_21, generator=self.gen)
-        if self.overlap:  # the point map + IR read only C_pred: beside the backward
-            self.aux.wait_stream(main)
-        with torch.no_grad(), _on(self.aux):  # train.py:109-116 (naive solver + IR per crop)
+        with torch.no_grad():  # train.py:109-116 (naive solver + IR per crop)
             ir = self.inlier_ratio_of(op, crops, C_pred) if ir else None
             # P truncated at the pair capacity would train on partial labels: flag it (device
             # bool, formed with the crops on the crop-formation stream)
@@ -377,9 +357,6 @@ class TrainStep:
         finally:
             if self.side is not None:
                 self.side.end(run=ok)
-        if self.overlap and ir is not None:
-            main.wait_stream(self.aux)
-            ir.record_stream(main)
         if ir is not None:
             log["IR"] = ir
         return log
@@ -511,23 +488,21 @@ class PipelinedTrainer:
     T_k is split around the eager RCCL all-reduce, as in GraphedTrainStep.
 
     The step's naive point map + IR (a logged metric; nothing trains on it) leaves the training
-    graphs (development knob PK_DEFER_IR=0 keeps it there): graph I_k computes the IR of
-    buffer k's batch from the C_pred that T_k left, on the crop-formation stream right before
-    C_k overwrites the buffer. The IR of step i is therefore ready once the next call has
-    enqueued I_k (or after flush()); the log's "IR" tensor is filled in place."""
+    graphs (defer_ir=False keeps it there): graph I_k computes the IR of buffer k's batch from
+    the C_pred that T_k left, on the crop-formation stream right before C_k overwrites the
+    buffer. The log's "IR" tensor is filled in place by that side-stream graph, so a reader must
+    be ordered after it: call wait_ir() (the current stream then waits for every IR enqueued so
+    far: the logs of all calls but the last) or flush() (also computes the last call's IR)
+    before reading log["IR"] on the device or the host.
+
+    cgt_side=True solves C_gt with the crops on the crop-formation stream; side_cus > 0 puts the
+    two streams on disjoint CU sets (cu_split_streams; measured no faster)."""
 
     def __init__(self, crop_formation: CropFormation, step: TrainStep, fb: FrameBatch, op: Operators,
-                 warmup: int = 3):
+                 warmup: int = 3, defer_ir: bool = True, cgt_side: bool = True, side_cus: int = 0):
         self.step, self.split = step, step.world > 1
-        # development knob PK_MAIN_PRIORITY: run the training graphs on a stream of that priority
-        mp = os.environ.get("PK_MAIN_PRIORITY")
-        self.main = torch.cuda.Stream(priority=int(mp)) if mp else torch.cuda.current_stream()
-        if mp:
-            self.main.wait_stream(torch.cuda.current_stream())
-        # crop-formation stream priority (development knob PK_SIDE_PRIORITY: torch's stream
-        # priorities, lower number = higher priority; default 0, the main stream's)
-        self.side = torch.cuda.Stream(priority=int(os.environ.get("PK_SIDE_PRIORITY", "0")))
-        side_cus = int(os.environ.get("PK_SIDE_CUS", "0"))
+        self.main = torch.cuda.current_stream()
+        self.side = torch.cuda.Stream()
         if side_cus > 0:  # disjoint CU sets for the two streams (cu_split_streams)
             self.main, self.side = cu_split_streams(side_cus)
             self.main.wait_stream(torch.cuda.current_stream())
@@ -545,13 +520,14 @@ class PipelinedTrainer:
             with torch.cuda.graph(g):
                 c = crop_formation(fb)
                 # C_gt depends only on the crops and the bases: solve it on the crop-formation
-                # stream too (PK_CGT_SIDE=0 keeps it in the training graph)
-                if os.environ.get("PK_CGT_SIDE", "1") == "1":
+                # stream too (cgt_side=False keeps it in the training graph)
+                if cgt_side:
                     c.C_gt = TrainStep.ground_truth(op, c)
                 self.crops.append(c)
             self.crop_graphs.append(g)
-        self.defer_ir = os.environ.get("PK_DEFER_IR", "1") == "1"
+        self.defer_ir = defer_ir
         self.ir_graphs, self._trained = [], [False, False]
+        self.ir_done, self._ir_enqueued = [torch.cuda.Event(), torch.cuda.Event()], [False, False]
         for k in range(2):
             step.opt.zero_grad(set_to_none=True)  # each training graph owns its gradients
             ga = torch.cuda.CUDAGraph()
@@ -579,57 +555,46 @@ class PipelinedTrainer:
             self.consumed[k].record(self.main)
         self.i = 0
         self._form(0)
-        # development knob PK_PIPE_THREAD=1: launch the crop graphs from a worker thread (graph
-        # launches block the host; the training stream should not wait behind them)
-        self._jobs = None
-        if os.environ.get("PK_PIPE_THREAD", "0") == "1":
-            import queue
-            import threading
-            self._jobs = queue.Queue()
-            self._queued = [threading.Event(), threading.Event()]
-            self._queued[0].set()
-            self._worker = threading.Thread(target=self._worker_loop, daemon=True)
-            self._worker.start()
+
+    def _replay_ir(self, k):
+        """I_k on the side stream (after T_k released buffer k), then its completion event."""
+        self.ir_graphs[k].replay()
+        self.ir_done[k].record(self.side)
+        self._ir_enqueued[k] = True
 
     def _form(self, k):
         with torch.cuda.stream(self.side):
             self.side.wait_event(self.consumed[k])
             if self.defer_ir and self._trained[k]:  # the IR of the batch T_k last trained on
-                self.ir_graphs[k].replay()
+                self._replay_ir(k)
+                self._trained[k] = False
             self.crop_graphs[k].replay()
             self.formed[k].record(self.side)
 
+    def wait_ir(self, stream=None):
+        """Order `stream` (default: the current stream) after every I_k enqueued so far, so the
+        "IR" of every log returned before the last call is safe to read on it."""
+        s = stream if stream is not None else torch.cuda.current_stream()
+        for k in range(2):
+            if self._ir_enqueued[k]:
+                s.wait_event(self.ir_done[k])
+
     def flush(self):
-        """Compute the IR still pending for the last step (its buffer's I_k), so every log
-        returned so far holds its IR once the device reaches this point."""
+        """Compute the IR still pending for the last step (its buffer's I_k) and order the
+        current stream after it: every log returned so far then holds its IR."""
         if not self.defer_ir or self.i == 0:
             return
         k = (self.i - 1) & 1
-        with torch.cuda.stream(self.side):
-            self.side.wait_event(self.consumed[k])
-            self.ir_graphs[k].replay()
-            ev = torch.cuda.Event()
-            ev.record(self.side)
-        torch.cuda.current_stream().wait_event(ev)
-
-    def _worker_loop(self):
-        torch.cuda.set_device(self.main.device)
-        while True:
-            k = self._jobs.get()
-            if k is None:
-                return
-            self._form(k)
-            self._queued[k].set()
+        if self._trained[k]:
+            with torch.cuda.stream(self.side):
+                self.side.wait_event(self.consumed[k])
+                self._replay_ir(k)
+            self._trained[k] = False
+        self.wait_ir()
 
     def __call__(self) -> dict:
         k = self.i & 1
-        if self._jobs is not None:  # crop graphs launched from a second host thread
-            self._queued[k].wait()             # C_k enqueued (host side) before T_k waits on it
-            self._queued[k].clear()
-            self._queued[k ^ 1].clear()
-            self._jobs.put(k ^ 1)
-        else:
-            self._form(k ^ 1)                  # next batch's crops, concurrently
+        self._form(k ^ 1)                      # next batch's crops, concurrently
         with torch.cuda.stream(self.main):
             self.main.wait_event(self.formed[k])
             self.train_a[k].replay()
@@ -735,10 +700,9 @@ class PipelinedInfer:
     returns the static outputs of the graph it replayed (overwritten two calls later)."""
 
     def __init__(self, crop_formation: CropFormation, infer: InferStep, fb: FrameBatch, op: Operators,
-                 warmup: int = 2):
+                 warmup: int = 2, side_cus: int = 0):
         self.main = torch.cuda.current_stream()
         self.side = torch.cuda.Stream()
-        side_cus = int(os.environ.get("PK_SIDE_CUS", "0"))
         if side_cus > 0:  # disjoint CU sets for the two streams (cu_split_streams)
             self.main, self.side = cu_split_streams(side_cus)
             self.main.wait_stream(torch.cuda.current_stream())
@@ -752,13 +716,8 @@ class PipelinedInfer:
         self.crop_graphs, self.crops, self.infer_graphs, self.outs = [], [], [], []
         for k in range(2):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                c = crop_formation(fb)
-                # C_gt depends only on the crops and the bases: solve it on the crop-formation
-                # stream too (PK_CGT_SIDE=0 keeps it in the training graph)
-                if os.environ.get("PK_CGT_SIDE", "1") == "1":
-                    c.C_gt = TrainStep.ground_truth(op, c)
-                self.crops.append(c)
+            with torch.cuda.graph(g):  # (InferStep reads no C_gt: none is solved here)
+                self.crops.append(crop_formation(fb))
             self.crop_graphs.append(g)
         for k in range(2):
             g = torch.cuda.CUDAGraph()

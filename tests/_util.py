@@ -87,3 +87,116 @@ def model_parity(M, DPFMNet, batch, device, diffusion_times=True):
 
     check(lambda o: o[1].sum() + o[2].sum() + o[3].square().sum() + o[4].square().sum(), "overlap+features")
     check(lambda o: o[0].sum(), "fmap")
+
+
+def check_topk(dist: np.ndarray, got: np.ndarray, k: int, rel: float = 1e-5) -> int:
+    """dist [V1, V2] (fp64 copy of the oracle's cdist), got [V2, k] row indices. Every column's
+    k picks must be distinct and their distances the k smallest of the column in ascending
+    order, up to near-ties |d_a - d_b| <= rel * max(d). Returns the number of columns that
+    differ from the oracle's stable sort only by such ties."""
+    tol = rel * max(float(dist.max()), 1e-12)
+    srt = np.sort(dist, axis=0)[:k]                      # [k, V2] the k smallest per column
+    picked = np.take_along_axis(dist, got.T, axis=0)     # [k, V2] distances of the picks
+    assert (np.abs(picked - srt) <= tol).all(), float(np.abs(picked - srt).max())
+    for j in range(got.shape[0]):
+        assert len(set(got[j].tolist())) == k, j
+    exp = np.argsort(dist, axis=0, kind="stable")[:k].T
+    return int((exp != got).any(1).sum())
+
+
+def rigidity_parity(cad, pc, cand, rows, n, diam, got=None):
+    """survivors equal the oracle's on the same candidates, except candidates whose oracle score
+    lies within 1e-5 (relative) of its round's threshold. `got`: the device's survivor pairs
+    (default cand[rows[:n]])."""
+    import torch
+    from oracle import dpfm_oracle as O
+    cad = cad.numpy() if torch.is_tensor(cad) else cad
+    pc = pc.numpy() if torch.is_tensor(pc) else pc
+    p = torch.from_numpy(cand).t()
+    exp, scores = O.spacial_filtering(torch.from_numpy(cad), torch.from_numpy(pc), p, diam, return_scores=True)
+    if got is None:
+        got = cand[rows[:n]]
+    a, b = set(map(tuple, got.tolist())), set(map(tuple, exp.t().tolist()))
+    near = 0
+    for s, tau in zip(scores, (0.3, 0.15, 0.055)):
+        thr = float(np.float32(tau * diam))
+        near += int((np.abs(s.numpy() - thr) <= 1e-5 * thr).sum())
+    if near == 0:
+        assert a == b and np.array_equal(got, exp.t().numpy())  # same survivors, same order
+    else:
+        assert len(a ^ b) <= 4 * near + max(2, len(b) // 1000), (len(a ^ b), near)
+    return len(b)
+
+
+def train_step_parity(M, op, crops, device, model_seed, step_seed):
+    """One TrainStep.forward_backward (fused encoder, NCE on the device draw, grouped weight
+    gradients) vs the reference training step restated by the oracle (utils/utils.py:67-79
+    C_gt, utils/loss.py DPFMLoss, autograd) evaluated in fp64 (the truth), with the same
+    weights, crops and NCE pair draw. Yardstick (model_parity's): the same oracle in fp32 on
+    the CPU and on the GPU; the HIP step's loss and every parameter gradient must be within
+    3x the larger of their errors (gradient floor 1e-6 x the global gradient norm for the
+    invariance-zero parameters); C_gt within 1e-4 of its scale."""
+    import torch
+    from dpfm_amd import ops
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import TrainStep, model_batch
+    B = crops.npairs.shape[0]
+    torch.manual_seed(model_seed)
+    ref = M.DPFMNet()
+    with torch.no_grad():
+        ref.feature_extractor.block_0.diffusion.diffusion_time.uniform_(-0.001, 12)
+        ref.feature_extractor.block_1.diffusion.diffusion_time.uniform_(-0.001, 12)
+    truth = M.DPFMNet().double()
+    truth.load_state_dict(ref.state_dict())
+    gref = M.DPFMNet().to(device)
+    gref.load_state_dict(ref.state_dict())
+    mine = DPFMNet().to(device)
+    mine.load_state_dict(ref.state_dict(), strict=True)
+    step = TrainStep(mine, seed=step_seed)
+    # the step's NCE draw, reproduced from its generator seed and device counter (not advanced)
+    cap = crops.pairs.shape[1]
+    rows, valid = ops.nce_select(crops.npairs, cap, 512, int(step.gen.initial_seed()), step.nce_counter().clone())
+    C_gt_dev = ops.cgt_lstsq(crops.pairs, crops.npairs, op.cad_evecs, op.pc_evecs)
+    log = step.forward_backward(op, crops)
+    torch.cuda.synchronize()
+    npairs = crops.npairs.cpu()
+    assert int(npairs.max()) <= cap
+    pairs = crops.pairs.cpu()
+    plist = [pairs[b, :int(npairs[b])] for b in range(B)]
+    sel = [rows[b][valid[b]].cpu() for b in range(B)]
+    g12, g21 = crops.overlap_12.cpu(), crops.overlap_21.cpu()
+    mb = model_batch(op, crops)
+    keys = ("xyz", "mass", "evals", "evecs")
+    cpu = {k: {kk: vv.cpu() for kk, vv in v.items() if kk in keys} for k, v in mb.items()}
+    cpu64 = {k: {kk: vv.double() for kk, vv in v.items()} for k, v in cpu.items()}
+    gpu = {k: {kk: vv.to(device) for kk, vv in v.items()} for k, v in cpu.items()}
+
+    def oracle_step(model, batch, dt):
+        model.zero_grad()
+        ex, ey = batch["shape1"]["evecs"], batch["shape2"]["evecs"]
+        C_gt = torch.stack([M.C_from_sparse_P(plist[b].to(ex.device), ex[b, :, :30], ey[b, :, :30]) for b in range(B)])
+        C, o12, o21, f1, f2, _, _ = model(batch)
+        dv = ex.device
+        loss = M.dpfm_loss(C, C_gt, [p.to(dv) for p in plist], [s.to(dv) for s in sel], f1, f2, o12, o21,
+                           g12.to(dv), g21.to(dv))
+        loss.backward()
+        grads = [torch.zeros(p.shape, dtype=torch.float64) if p.grad is None else p.grad.detach().cpu().double()
+                 for p in model.parameters()]
+        return float(loss), C_gt.detach().cpu().double(), grads
+
+    l64, cg64, gr64 = oracle_step(truth, cpu64, torch.float64)
+    l32, _, gr32 = oracle_step(ref, cpu, torch.float32)
+    lg, _, grg = oracle_step(gref, gpu, torch.float32)
+    # C_gt
+    cgd = C_gt_dev.cpu().double()
+    assert (cgd - cg64).abs().max().item() <= 1e-4 * cg64.abs().max().item(), (cgd - cg64).abs().max().item()
+    # loss
+    ld = float(log["loss"])
+    e = [abs(l32 - l64), abs(lg - l64), abs(ld - l64)]
+    assert e[2] <= 3 * max(e[0], e[1]) + 1e-6 * abs(l64), (e, l64)
+    # every parameter gradient
+    floor = 1e-6 * torch.cat([g.reshape(-1) for g in gr64]).norm().item()
+    mine_g = [p.grad.detach().cpu().double() for p in mine.parameters()]
+    for (name, _), t, a, b, d in zip(truth.named_parameters(), gr64, gr32, grg, mine_g):
+        ee = [(a - t).norm().item(), (b - t).norm().item(), (d - t).norm().item()]
+        assert ee[2] <= 3 * max(ee[0], ee[1]) + floor, (name, ee, floor, t.norm().item())

@@ -14,6 +14,8 @@ Nothing here imports or runs reference code; it reads PNG / JSON / PLY / TXT dat
                  reference's printed metrics (ADD ICP, Add Score ICP thres (xyz direction),
                  Add-S Score ICP, Error [cm], Error [deg], diameter from models_info.json)
   p_pred.npy     sample-data/sample_P_pred/p_i0.npy (RANSAC correspondence shape/order)
+  real_crops.npz 7 published crops + the 5 decimated CADs (see real_crops)
+  icp_pin.npz    512 published crops: T_gt, printed T_pred, the reference's ICP output (see icp_pin)
 """
 import glob
 import json
@@ -109,8 +111,10 @@ def main():
     out["n"] = np.int64(len(rows))
     np.savez_compressed(f"{OUT}/pose_metrics.npz", **out)
     np.save(f"{OUT}/p_pred.npy", np.load(f"{REF}/sample-data/sample_P_pred/p_i0.npy"))
-    real_crops(info)
-    print(f"wrote lm_frame.npz, pose_metrics.npz ({len(rows)} crops), p_pred.npy, real_crops.npz")
+    cads = real_crops(info)
+    n_icp = icp_pin(cads)
+    print(f"wrote lm_frame.npz, pose_metrics.npz ({len(rows)} crops), p_pred.npy, real_crops.npz, "
+          f"icp_pin.npz ({n_icp} crops)")
 
 
 # Real crops of the published PBR/RANSAC results, chosen to span the reference's crop sizes:
@@ -147,6 +151,50 @@ def real_crops(info):
         out[f"cad_{oid}"] = cad
     out["n"] = np.int64(len(REAL_CROPS))
     np.savez_compressed(f"{OUT}/real_crops.npz", **out)
+    return cads
+
+
+TREES = ("results_on_pbr", "results_on_real")
+SOLVERS = ("RANSAC", "TEASER")
+
+
+def icp_pin(cads, per_dir=128):
+    """icp_pin.npz: the reference's own Open3D ICP outputs (f4 / Umeyama pin).
+
+    test_RANSAC.py:424-446 (test_teaser.py:469-483 likewise) refines the solver's T_est with
+    registration_icp(source = CAD, target = transform(CAD, T_gt), r = 0.2, init = T_est,
+    PointToPoint, max_iteration = 2000) and stores, per crop, cad_i.ply, cad_i_pose_gt.ply
+    (= the target), cad_i_pose_est.ply (= CAD under the ICP result) and the txt with T_pred
+    printed to 9 digits. Per crop this keeps: the object id (CAD = real_crops.npz cad_<id>,
+    checked identical here), T_gt and T_icp fitted at full precision from the plys (checked
+    against the printed matrices), T_pred as printed (the ICP init). per_dir crops are taken
+    evenly strided from each of the four result directories (sorted file order)."""
+    rows = {k: [] for k in ("obj_id", "tree", "solver", "index", "T_gt", "T_pred", "T_icp", "target_dev")}
+    for ti, tree in enumerate(TREES):
+        for si, solver in enumerate(SOLVERS):
+            base = f"{REF}/{tree}/results_poses_{solver}"
+            files = sorted(glob.glob(f"{base}/results/*.txt"))
+            pick = np.unique(np.linspace(0, len(files) - 1, per_dir).round().astype(int))
+            for k in pick:
+                name = os.path.basename(files[k])[:-4]
+                i = name.split("_")[-1]
+                d = f"{base}/ply/{name}"
+                r = parse_result_txt(files[k])
+                cad = read_ply_xyz(f"{d}/cad_{i}.ply")
+                assert np.array_equal(cad, cads[r["obj_id"]]), name
+                tgt = read_ply_xyz(f"{d}/cad_{i}_pose_gt.ply")
+                T_gt = fit_rigid(cad, tgt)
+                T_icp = fit_rigid(cad, read_ply_xyz(f"{d}/cad_{i}_pose_est.ply"))
+                assert np.allclose(T_gt, r["T_gt"], atol=1e-6), name
+                assert np.allclose(T_icp, r["T_icp"], atol=1e-6), name
+                # the test rebuilds the target as transform(CAD, T_gt) (test_RANSAC.py:154-160)
+                dev = np.abs(cad @ T_gt[:3, :3].T + T_gt[:3, 3] - tgt).max()
+                for key, v in (("obj_id", r["obj_id"]), ("tree", ti), ("solver", si), ("index", int(i)),
+                               ("T_gt", T_gt), ("T_pred", r["T_pred"]), ("T_icp", T_icp), ("target_dev", dev)):
+                    rows[key].append(v)
+    out = {k: np.asarray(v) for k, v in rows.items()}
+    np.savez_compressed(f"{OUT}/icp_pin.npz", **out)
+    return len(rows["obj_id"])
 
 
 if __name__ == "__main__":

@@ -40,3 +40,18 @@ def test_no_cpu_fallback():
     off = torch.tensor([0, 10])
     with pytest.raises(_lib.PoseKernError):
         ops.fps_packed(x, off, 10, torch.zeros(1, dtype=torch.int32), torch.ones(1, dtype=torch.int32), 1)
+
+
+def test_product_library_has_no_development_hooks():
+    """The product libposekern.so exports no pkdev_* hook and reads no environment switch
+    (those live in libposekern_dev.so, built from the same sources with -DPK_DEVBUILD); the dev
+    library exports the hooks the tests / tools use."""
+    import subprocess
+    from dpfm_amd import _lib
+    nm = lambda p: subprocess.run(["nm", "-D", p], capture_output=True, text=True, check=True).stdout  # noqa: E731
+    prod = nm(_lib.LIB_PATH)
+    assert "pkdev_" not in prod
+    assert not re.search(r"\bU getenv\b", prod)
+    dev = nm(_lib.DEV_LIB_PATH)
+    for hook in ("pkdev_seq_sum", "pkdev_rigidity_variant", "pkdev_probe_linear", "pkdev_fps_cfg"):
+        assert hook in dev, hook

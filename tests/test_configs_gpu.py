@@ -15,6 +15,7 @@ import torch
 
 from oracle import dpfm_oracle as O
 from oracle import dpfm_model_oracle as M
+from _util import check_topk, rigidity_parity as _rigidity_parity, train_step_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -22,21 +23,6 @@ pytestmark = pytest.mark.gpu
 def _spectral(V, seed):
     from dpfm_amd.dataset.synthetic import lbo_operators
     return torch.from_numpy(lbo_operators(V, 64, seed)[2])
-
-
-def check_topk(dist: np.ndarray, got: np.ndarray, k: int, rel: float = 1e-5) -> int:
-    """dist [V1, V2] (fp64 copy of the oracle's cdist), got [V2, k] row indices. Every column's
-    k picks must be distinct and their distances the k smallest of the column in ascending
-    order, up to near-ties |d_a - d_b| <= rel * max(d). Returns the number of columns that
-    differ from the oracle's stable sort only by such ties."""
-    tol = rel * max(float(dist.max()), 1e-12)
-    srt = np.sort(dist, axis=0)[:k]                      # [k, V2] the k smallest per column
-    picked = np.take_along_axis(dist, got.T, axis=0)     # [k, V2] distances of the picks
-    assert (np.abs(picked - srt) <= tol).all(), float(np.abs(picked - srt).max())
-    for j in range(got.shape[0]):
-        assert len(set(got[j].tolist())) == k, j
-    exp = np.argsort(dist, axis=0, kind="stable")[:k].T
-    return int((exp != got).any(1).sum())
 
 
 @pytest.mark.parametrize("B,V", [(8, 2048), (1, 4096)])
@@ -110,28 +96,6 @@ def _rigid_scene(V2, seed):
     return cad, pc, cand.reshape(-1, 2), 2.0 * 5 * 2.5
 
 
-def _rigidity_parity(cad, pc, cand, rows, n, diam, got=None):
-    """survivors equal the oracle's on the same candidates, except candidates whose oracle score
-    lies within 1e-5 (relative) of its round's threshold. `got`: the device's survivor pairs
-    (default cand[rows[:n]])."""
-    cad = cad.numpy() if torch.is_tensor(cad) else cad
-    pc = pc.numpy() if torch.is_tensor(pc) else pc
-    p = torch.from_numpy(cand).t()
-    exp, scores = O.spacial_filtering(torch.from_numpy(cad), torch.from_numpy(pc), p, diam, return_scores=True)
-    if got is None:
-        got = cand[rows[:n]]
-    a, b = set(map(tuple, got.tolist())), set(map(tuple, exp.t().tolist()))
-    near = 0
-    for s, tau in zip(scores, (0.3, 0.15, 0.055)):
-        thr = float(np.float32(tau * diam))
-        near += int((np.abs(s.numpy() - thr) <= 1e-5 * thr).sum())
-    if near == 0:
-        assert a == b and np.array_equal(got, exp.t().numpy())  # same survivors, same order
-    else:
-        assert len(a ^ b) <= 4 * near + max(2, len(b) // 1000), (len(a ^ b), near)
-    return len(b)
-
-
 @pytest.mark.parametrize("V2", [1024, 2048])
 def test_rigidity_filter_configs(device, V2):
     """spacial_filtering.py:42-75 at n = 5 V2 = 5120 (configs[1]) and 10240 (configs[3])."""
@@ -147,10 +111,8 @@ def test_rigidity_filter_configs(device, V2):
 
 def test_rigidity_filter_ragged_batch(device):
     """Crops with different candidate counts in one launch (empty, single, tile-edge ±1 of the
-    128-entry pair tiles, and a 2-tile-plus crop): each crop's survivors vs the oracle; the
-    round-2 gather path (pkdev_rigidity_variant(1)) on the same batch agrees."""
-    import ctypes
-    from dpfm_amd import _lib, ops
+    128-entry pair tiles, and a 2-tile-plus crop): each crop's survivors vs the oracle."""
+    from dpfm_amd import ops
     sizes = [0, 1, 127, 129, 640, 1000]
     scenes = [_rigid_scene(max((s + 4) // 5, 1), 7 + i) for i, s in enumerate(sizes)]
     Lc = max(sizes)
@@ -172,16 +134,6 @@ def test_rigidity_filter_ragged_batch(device):
         if s == 0:
             continue
         _rigidity_parity(sc[0], sc[1], sc[2][:s], rows[i], int(n[i]), sc[3])
-    L = _lib.lib()
-    L.pkdev_rigidity_variant.argtypes = [ctypes.c_int]
-    L.pkdev_rigidity_variant(1)
-    try:
-        rows1, n1 = ops.rigidity_filter(dcand, ncand, dcad, dpc, thr)
-    finally:
-        L.pkdev_rigidity_variant(0)
-    rows1, n1 = rows1.cpu().numpy(), n1.cpu().numpy()
-    for i in range(len(sizes)):
-        assert abs(int(n1[i]) - int(n[i])) <= max(2, int(n[i]) // 100), (i, n1[i], n[i])
 
 
 def test_ransac_configs4(device, coracle):
@@ -290,76 +242,14 @@ def test_train_step_configs2_vs_oracle(device):
     TrainStep.forward_backward (fused encoder, NCE on the device draw, grouped weight
     gradients) vs the reference training step restated by the oracle (utils/utils.py:67-79
     C_gt, utils/loss.py DPFMLoss, autograd) evaluated in fp64 (the truth), with the same
-    weights, crops and NCE pair draw. Yardstick (_util.model_parity's): the same oracle in fp32
-    on the CPU and on the GPU; the HIP step's loss and every parameter gradient must be within
-    3x the larger of their errors (gradient floor 1e-6 x the global gradient norm for the
-    invariance-zero parameters); C_gt within 1e-4 of its scale."""
-    from dpfm_amd import ops
+    weights, crops and NCE pair draw; bars in _util.train_step_parity."""
     from dpfm_amd.dataset.object import CropFormation
-    from dpfm_amd.models.dpfm import DPFMNet
-    from dpfm_amd.pipeline import TrainStep, make_frame_batch, model_batch
+    from dpfm_amd.pipeline import make_frame_batch
     B, N = 32, 1024
     fb, op = make_frame_batch(B, N, N, seed=600, device=device)
     crops = CropFormation(n1=N, npoint=N, seed=4)(fb)
-    torch.manual_seed(21)
-    ref = M.DPFMNet()
-    with torch.no_grad():
-        ref.feature_extractor.block_0.diffusion.diffusion_time.uniform_(-0.001, 12)
-        ref.feature_extractor.block_1.diffusion.diffusion_time.uniform_(-0.001, 12)
-    truth = M.DPFMNet().double()
-    truth.load_state_dict(ref.state_dict())
-    gref = M.DPFMNet().to(device)
-    gref.load_state_dict(ref.state_dict())
-    mine = DPFMNet().to(device)
-    mine.load_state_dict(ref.state_dict(), strict=True)
-    step = TrainStep(mine, seed=13)
-    # the step's NCE draw, reproduced from its generator seed and device counter (not advanced)
-    cap = crops.pairs.shape[1]
-    rows, valid = ops.nce_select(crops.npairs, cap, 512, int(step.gen.initial_seed()), step.nce_counter().clone())
-    C_gt_dev = ops.cgt_lstsq(crops.pairs, crops.npairs, op.cad_evecs, op.pc_evecs)
-    log = step.forward_backward(op, crops)
-    torch.cuda.synchronize()
-    npairs = crops.npairs.cpu()
-    assert int(npairs.min()) > 0 and int(npairs.max()) <= cap
-    pairs = crops.pairs.cpu()
-    plist = [pairs[b, :int(npairs[b])] for b in range(B)]
-    sel = [rows[b][valid[b]].cpu() for b in range(B)]
-    g12, g21 = crops.overlap_12.cpu(), crops.overlap_21.cpu()
-    mb = model_batch(op, crops)
-    keys = ("xyz", "mass", "evals", "evecs")
-    cpu = {k: {kk: vv.cpu() for kk, vv in v.items() if kk in keys} for k, v in mb.items()}
-    cpu64 = {k: {kk: vv.double() for kk, vv in v.items()} for k, v in cpu.items()}
-    gpu = {k: {kk: vv.to(device) for kk, vv in v.items()} for k, v in cpu.items()}
-
-    def oracle_step(model, batch, dt):
-        model.zero_grad()
-        ex, ey = batch["shape1"]["evecs"], batch["shape2"]["evecs"]
-        C_gt = torch.stack([M.C_from_sparse_P(plist[b].to(ex.device), ex[b, :, :30], ey[b, :, :30]) for b in range(B)])
-        C, o12, o21, f1, f2, _, _ = model(batch)
-        dv = ex.device
-        loss = M.dpfm_loss(C, C_gt, [p.to(dv) for p in plist], [s.to(dv) for s in sel], f1, f2, o12, o21,
-                           g12.to(dv), g21.to(dv))
-        loss.backward()
-        grads = [torch.zeros(p.shape, dtype=torch.float64) if p.grad is None else p.grad.detach().cpu().double()
-                 for p in model.parameters()]
-        return float(loss), C_gt.detach().cpu().double(), grads
-
-    l64, cg64, gr64 = oracle_step(truth, cpu64, torch.float64)
-    l32, _, gr32 = oracle_step(ref, cpu, torch.float32)
-    lg, _, grg = oracle_step(gref, gpu, torch.float32)
-    # C_gt
-    cgd = C_gt_dev.cpu().double()
-    assert (cgd - cg64).abs().max().item() <= 1e-4 * cg64.abs().max().item(), (cgd - cg64).abs().max().item()
-    # loss
-    ld = float(log["loss"])
-    e = [abs(l32 - l64), abs(lg - l64), abs(ld - l64)]
-    assert e[2] <= 3 * max(e[0], e[1]) + 1e-6 * abs(l64), (e, l64)
-    # every parameter gradient
-    floor = 1e-6 * torch.cat([g.reshape(-1) for g in gr64]).norm().item()
-    mine_g = [p.grad.detach().cpu().double() for p in mine.parameters()]
-    for (name, _), t, a, b, d in zip(truth.named_parameters(), gr64, gr32, grg, mine_g):
-        ee = [(a - t).norm().item(), (b - t).norm().item(), (d - t).norm().item()]
-        assert ee[2] <= 3 * max(ee[0], ee[1]) + floor, (name, ee, floor, t.norm().item())
+    assert int(crops.npairs.min()) > 0
+    train_step_parity(M, op, crops, device, model_seed=21, step_seed=13)
 
 
 @pytest.mark.parametrize("precision", ["bf16", "bf16x3"])

@@ -170,7 +170,7 @@ def test_sor_ordered_sum_exact(device):
         v = np.ascontiguousarray(v, dtype=np.float64)
         t = torch.from_numpy(v).to(device)
         out = torch.empty(1, dtype=torch.float64, device=device)
-        assert _lib.lib().pkdev_seq_sum(_lib.ptr(t), int(v.size), _lib.ptr(out), _lib.stream(device)) == 0
+        assert _lib.dev_lib().pkdev_seq_sum(_lib.ptr(t), int(v.size), _lib.ptr(out), _lib.stream(device)) == 0
         got = float(out.cpu()[0])
         exp = _seq_sum(v)
         assert got == exp, (i, got, exp, got - exp)

@@ -434,7 +434,7 @@ def test_block_mlp_fused_matches_layers(device):
     from dpfm_amd.diffusion_net import DiffusionNetBlock
     torch.manual_seed(2)
     blk = DiffusionNetBlock(C_width=64, mlp_hidden_dims=[64, 64], dropout=False).to(device)
-    blk.fused_mlp = True  # opt-in path (PK_FUSED_BLOCK_MLP=1)
+    blk.fused_mlp = True  # opt-in path (DiffusionNetBlock.fused_mlp)
     assert blk._fusable(torch.zeros(1, device=device))
     g = torch.Generator().manual_seed(9)
     B, N = 4, 700
@@ -479,8 +479,9 @@ def test_relu_backward_folded_into_dgrad(device, monkeypatch):
     """The fused ReLU's backward folded into the next layer's input-gradient epilogue
     (pk_linear_fwd mask) gives the same DiffusionNet input and parameter gradients, bit for
     bit, as applying aten threshold_backward separately."""
-    monkeypatch.setenv("PK_FUSED_ENCODER", "0")  # the per-module path is the one that folds
+    from dpfm_amd import diffusion_net as DN
     from dpfm_amd import layers
+    monkeypatch.setattr(DN, "FUSED_ENCODER", False)  # the per-module path is the one that folds
     from dpfm_amd.diffusion_net import DiffusionNet
     torch.manual_seed(6)
     net = DiffusionNet(C_in=3, C_out=32, C_width=64, N_block=2, dropout=False,
@@ -505,10 +506,11 @@ def test_relu_backward_folded_into_dgrad(device, monkeypatch):
 def test_fused_encoder_matches_module_path(device, B, N, monkeypatch):
     """The DiffusionNet encoder as one autograd node (_EncoderFn: concatenation-free blocks,
     residual adds and split input gradients in the layer epilogues, diffusion backward
-    accumulated in place) against the per-module path (PK_FUSED_ENCODER=0) on the same
+    accumulated in place) against the per-module path (FUSED_ENCODER = False) on the same
     weights: forward bit-identical (same kernels and per-element arithmetic), gradients of
     every parameter within 2e-5 of their scale (only the order of the residual / diffusion
     gradient sums differs)."""
+    from dpfm_amd import diffusion_net as DN
     from dpfm_amd.models.dpfm import DPFMNet
     torch.manual_seed(11)
     net = DPFMNet().feature_extractor.to(device)
@@ -517,7 +519,7 @@ def test_fused_encoder_matches_module_path(device, B, N, monkeypatch):
     g = torch.randn(B, N, 32, device=device)
     res = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("PK_FUSED_ENCODER", mode)
+        monkeypatch.setattr(DN, "FUSED_ENCODER", mode == "1")
         net.zero_grad(set_to_none=True)
         for blk in net.blocks:  # above the clamp: both paths see the same diffusion times
             blk.diffusion.diffusion_time.data.copy_(torch.linspace(0.01, 2.0, 64, device=device))
@@ -627,13 +629,14 @@ def test_fused_fmap_head_matches_module_path(device, N1, N2, monkeypatch):
     1e-3 in norm (f32 summation order of the projections differs, and the lambda = 100
     regularized solve amplifies it; test_dpfmnet_matches_oracle holds the fused path to the
     fp64 oracle with the 3x fp32 yardstick, parameter by parameter)."""
+    from dpfm_amd.models import dpfm as MD
     from dpfm_amd.models.dpfm import DPFMNet
     torch.manual_seed(21)
     net = DPFMNet().to(device)
     b = _to(_inputs(2, N1, N2, seed=5), device)
     res = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("PK_FUSED_FMAP_HEAD", mode)
+        monkeypatch.setattr(MD, "FUSED_FMAP_HEAD", mode == "1")
         net.zero_grad(set_to_none=True)
         C = net(b)[0]
         g = torch.linspace(-1, 1, C.numel(), device=device).view_as(C)

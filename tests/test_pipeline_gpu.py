@@ -192,6 +192,32 @@ def test_pipelined_trainer_matches_eager(device):
         assert not diff, diff
 
 
+def test_pipelined_trainer_deferred_ir_readers(device):
+    """The deferred IR is written by a side-stream graph: wait_ir() orders the reader after
+    every I_k enqueued so far (the logs of all calls but the last), flush() computes the last
+    one (test_pipelined_trainer_matches_eager checks the values against the eager step)."""
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import PipelinedTrainer, TrainStep, make_frame_batch
+    F, N = 4, 512
+    fb, op = make_frame_batch(F, N, N, seed=92, device=device)
+    cf = CropFormation(n1=N, npoint=N, seed=3)
+    torch.manual_seed(1)
+    ps = TrainStep(DPFMNet().to(device), seed=8, capturable=True)
+    pipe = PipelinedTrainer(cf, ps, fb, op, warmup=1)
+    logs = [pipe() for _ in range(3)]
+    pipe.wait_ir()
+    early = [logs[0]["IR"].clone(), logs[1]["IR"].clone()]  # calls 0 and 1 (I_0, I_1 enqueued)
+    pipe.flush()
+    last = logs[2]["IR"].clone()
+    torch.cuda.synchronize()
+    for ir in early + [last]:
+        assert 0.0 <= float(ir) <= 1.0
+    # call 1's IR read after wait_ir() is final (nothing writes buffer 1's slot again before call 3)
+    assert torch.equal(early[1], logs[1]["IR"])
+    assert torch.equal(last, logs[2]["IR"])
+
+
 @pytest.mark.parametrize("scale", [10.0, 1e-3])
 def test_fused_clip_rmsprop_matches_torch(device, scale):
     """pk_clip_rmsprop (TrainStep.apply's clip_grad_norm_(5.0) + RMSprop(5e-4) in one launch)

@@ -108,15 +108,19 @@ def test_pair_capacity_overflow_is_flagged(device):
 
 
 def test_train_step_on_ragged_crops(device):
-    """A training step over ragged crops (eager): finite loss, no pair overflow, IR in [0, 1],
-    parameters updated."""
+    """A training step over ragged crops (LM masks + synthetic frames: 0- to 2000-point crops,
+    collate padding): finite loss, no pair overflow, IR in [0, 1], parameters updated; and the
+    same step's forward_backward vs the oracle's training step in fp64 (C_gt, loss, every
+    parameter gradient; bars of _util.train_step_parity) on the padded ragged batch."""
     from dpfm_amd.dataset.object import CropFormation
     from dpfm_amd.models.dpfm import DPFMNet
     from dpfm_amd.pipeline import TrainStep, frame_batch, operators_for
+    from _util import train_step_parity
     frames = [f for f in _frames() if f["mask"].any()][:6]
     fb = frame_batch(frames, device)
     crops = CropFormation(npoint=0, seed=5, pad="batch")(fb)
     op = operators_for([f["cad"] for f in frames], crops.n2.cpu().tolist(), fb.diam, 0, device, ld2=crops.ld)
+    assert crops.ld >= 1999 and min(crops.n2.cpu().tolist()) < 1024
     torch.manual_seed(0)
     model = DPFMNet().to(device)
     step = TrainStep(model)
@@ -126,6 +130,7 @@ def test_train_step_on_ragged_crops(device):
     assert np.isfinite(float(log["loss"])) and not bool(log["pair_overflow"])
     assert 0.0 <= float(log["IR"]) <= 1.0
     assert any(not torch.equal(a, p) for a, p in zip(before, model.parameters()))
+    train_step_parity(M, op, crops, device, model_seed=17, step_seed=29)
 
 
 # ----------------------------------------------------------------------------- real crops
@@ -226,13 +231,15 @@ def test_dpfmnet_real_crops_matches_oracle(device):
     model_parity(M, DPFMNet, batch, device)
 
 
-def test_infer_step_on_real_crops(device):
-    """Inference (eval.py + test_RANSAC.py) on real crops: the spatial-filter solver on the
-    non-padding rows, RANSAC in the camera frame, finite poses and metrics."""
+def test_infer_step_on_real_crops(device, coracle):
+    """Inference (eval.py + test_RANSAC.py) on the reference's real crops (200-2000 points,
+    ~5000-vertex CADs): the spatial-filter solver on the non-padding rows, RANSAC in the camera
+    frame, checked stage by stage against the oracle chain (below)."""
     from dpfm_amd import ops
     from dpfm_amd.dataset.object import Crops, FrameBatch
     from dpfm_amd.models.dpfm import DPFMNet
-    from dpfm_amd.pipeline import InferStep, operators_for
+    from dpfm_amd.pipeline import InferStep, model_batch, operators_for
+    from _util import check_topk, cp, rigidity_parity
     crops_np = _real()
     B = len(crops_np)
     n2 = [c["pc"].shape[0] for c in crops_np]
@@ -253,13 +260,59 @@ def test_infer_step_on_real_crops(device):
     crops = Crops(pc64=pc64, pc32=pc32, align64=al.to(device), align32=al32, off=pc_off, n2=n2t, ld=ld, npoint=None,
                   pairs=None, npairs=None, overlap_12=None, overlap_21=None, rgb=None, kept=None)
     torch.manual_seed(1)
-    res = InferStep(DPFMNet().to(device), hypotheses=256)(fb, op, crops)
+    ref = M.DPFMNet()
+    mine = DPFMNet().to(device)
+    mine.load_state_dict(ref.state_dict())
+    H = 256
+    res = InferStep(mine, hypotheses=H, seed=3)(fb, op, crops)
     torch.cuda.synchronize()
     assert torch.isfinite(res["T"]).all() and torch.isfinite(res["metrics"]).all()
     ncorr = res["n_corr"].cpu().numpy()
     assert (ncorr >= 0).all() and (ncorr <= 5 * np.asarray(n2)).all()
     ir = res["ir"].cpu().numpy()
     assert ((ir >= 0) & (ir <= 1)).all()
+    # stage by stage vs the oracle chain (each stage's oracle on the device's previous-stage
+    # output, as test_configs_gpu.py::test_infer_step_configs1_vs_oracle_chain): the model's C on
+    # the padded 5002 x 2000 batch, then for two crops (200 and ~1000 points; the CPU oracle's
+    # rigidity rounds are O(n^2) at n = 5 n2) top-5 on the valid rows, rigidity survivors, IR,
+    # RANSAC (C oracle, same draws) and ADD.
+    mb = model_batch(op, crops)
+    cpu = {k: {kk: vv.cpu() for kk, vv in v.items() if kk in ("xyz", "mass", "evals", "evecs")} for k, v in mb.items()}
+    with torch.no_grad():
+        C32 = ref(cpu)[0]
+        truth = M.DPFMNet().double()
+        truth.load_state_dict(ref.state_dict())
+        C64 = truth({k: {kk: vv.double() for kk, vv in v.items()} for k, v in cpu.items()})[0]
+    Cg = res["C"].cpu().double()
+    e_ref = (C32.double() - C64).abs().max().item()
+    assert (Cg - C64).abs().max().item() <= 3 * e_ref + 1e-6 * (1 + C64.abs().max().item())
+    cand = res["cand"].cpu().numpy()
+    p_pred = res["p_pred"].cpu().numpy()
+    T = res["T"].cpu().numpy()
+    st = res["ransac"].cpu().numpy()
+    ex, ey = cpu["shape1"]["evecs"], cpu["shape2"]["evecs"]
+    cadx, pcx, al32c = cpu["shape1"]["xyz"], cpu["shape2"]["xyz"], crops.align32.cpu()
+    order = np.argsort(n2)
+    ties = 0
+    for b in (int(order[0]), int(order[len(order) // 2])):
+        n1b, n2b = cads[b].shape[0], n2[b]
+        dist = torch.cdist(ex[b, :n1b, :30] @ res["C"][b].cpu().t(), ey[b, :n2b, :30]).numpy().astype(np.float64)
+        ties += check_topk(dist, cand[b, :5 * n2b, 0].reshape(n2b, 5), 5)
+        surv = p_pred[b, :ncorr[b]]
+        rigidity_parity(cadx[b, :n1b], pcx[b, :n2b], cand[b, :5 * n2b], None, 0, crops_np[b]["diam"], got=surv)
+        exp_ir = O.compute_inlier_ratio(torch.from_numpy(surv), cadx[b], al32c[b], np.float32(0.1 * crops_np[b]["diam"]))
+        assert float(ir[b]) == float(exp_ir), b
+        cor = np.ascontiguousarray(surv.astype(np.int32))
+        T_c, st_c = np.zeros(16), np.zeros(3)
+        coracle.oc_ransac(cp(np.ascontiguousarray(cads[b])), cp(np.ascontiguousarray(crops_np[b]["pc"])), cp(cor),
+                          int(ncorr[b]), None, 3, H, 0.05, cp(T_c), cp(st_c))
+        assert int(st[b, 2]) == int(st_c[2]) and st[b, 0] == st_c[0], b
+        np.testing.assert_allclose(T[b], T_c.reshape(4, 4), atol=1e-4)
+        T_gt = np.eye(4)
+        T_gt[:3, :3], T_gt[:3, 3] = crops_np[b]["R"], crops_np[b]["t"]
+        e_add, _ = O.add(T[b], T_gt, cads[b], crops_np[b]["diam"])
+        np.testing.assert_allclose(res["metrics"][b, 0].item(), e_add, rtol=1e-9)
+    assert ties <= max(2, (n2[int(order[0])] + n2[int(order[len(order) // 2])]) // 200), ties
 
 
 def test_cgt_real_crops_full_rank(device):
@@ -297,7 +350,7 @@ def test_cgt_real_crops_full_rank(device):
         assert (got[b] - exp).abs().max().item() <= 1e-4 * scale, (b, (got[b] - exp).abs().max().item(), scale)
 
 
-def test_cgt_real_crops_full_rank(device):
+def test_cgt_real_crops_full_rank_fp32_oracle(device):
     """C_from_sparse_P (utils/utils.py:67-79) on the reference's own pair structure: the ball-query
     positives of its real crops (object.py:174-177, r = 0.05 diam) with operators of the true
     sizes. Every crop matches >= 30 distinct crop rows, so the normal equations are full rank and

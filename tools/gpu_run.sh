@@ -25,6 +25,7 @@ for step in "$@"; do
     infer) run infer 300 python bench.py --mode infer ;;
     corr) run corr 300 python bench.py --mode corr4096 ;;
     tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    testsall) run testsall 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     benchq) run benchq 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;

@@ -22,6 +22,7 @@ def timeit(fn, iters=20, warm=3):
 
 rng = np.random.default_rng(0)
 from dpfm_amd import _lib  # noqa: E402
+_lib.use_dev_lib()  # pkdev_* hooks: libposekern_dev.so (Makefile)
 from dpfm_amd.pipeline import make_frame_batch  # noqa: E402
 
 L = _lib.lib()

@@ -8,6 +8,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "6d-pose-estimation-for-unseen-categories_amd")]
 import torch  # noqa: E402
 from dpfm_amd import _lib, ops  # noqa: E402
+_lib.use_dev_lib()  # pkdev_* hooks: libposekern_dev.so (Makefile)
 
 L = _lib.lib()
 L.pkdev_probe_linear.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,

@@ -12,6 +12,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "6d-pose-estimation-for-unseen-categori
 import torch  # noqa: E402
 
 from dpfm_amd import _lib, ops  # noqa: E402
+_lib.use_dev_lib()  # pkdev_* hooks: libposekern_dev.so (Makefile)
 from dpfm_amd.pipeline import make_frame_batch  # noqa: E402
 
 dev = torch.device("cuda:0")

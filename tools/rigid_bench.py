@@ -10,6 +10,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "6d-pose-estimation-for-unseen-categori
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from dpfm_amd import _lib, ops  # noqa: E402
+_lib.use_dev_lib()  # pkdev_* hooks: libposekern_dev.so (Makefile)
 from test_configs_gpu import _rigid_scene  # noqa: E402
 
 L = _lib.lib()
