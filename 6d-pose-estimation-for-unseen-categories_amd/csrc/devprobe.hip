@@ -77,7 +77,58 @@ __global__ __launch_bounds__(256) void probe_tile_kernel(const float* __restrict
     }
 }
 
+// Clock probe for MFMA-bound kernels: every wave runs `iters` x CH independent accumulation
+// chains of 8 v_mfma_f32_16x16x4f32 on operands derived from its lane (non-trivial bits), as
+// the feature-distance pass does per tile; one store per lane at the end. Also stamps
+// s_memtime / s_memrealtime around the loop (wave 0 of block 0) into stamp[0..3].
+template <int CH>
+__global__ __launch_bounds__(512, 2) void probe_mfma_kernel(const float* __restrict__ seed, int iters,
+                                                            float* __restrict__ out, long long* __restrict__ stamp) {
+  const int lane = threadIdx.x & 63;
+  float a[8], b[CH][8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    a[s] = seed[(lane * 8 + s) & 1023];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) b[c][s] = seed[(lane * 8 + s + 77 * c + 512) & 1023];
+  }
+  f32x4 acc[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool stamper = blockIdx.x == 0 && threadIdx.x == 0;
+  long long t0 = 0, r0 = 0;
+  if (stamper) {
+    t0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int s = 0; s < 8; ++s) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[c][s], acc[c], 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) a[s] = acc[s & (CH - 1)][s & 3];  // next operands depend on this step
+  }
+  if (stamper) {
+    const long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    stamp[0] = t0; stamp[1] = t1; stamp[2] = r0; stamp[3] = r1;
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) sum += acc[c][0] + acc[c][1] + acc[c][2] + acc[c][3];
+  out[(int64_t)blockIdx.x * blockDim.x + threadIdx.x] = sum;
+}
+
 }  // namespace
+
+extern "C" int pkdev_probe_mfma(const float* seed, int blocks, int iters, float* out, long long* stamp,
+                                void* stream) {
+  if (blocks <= 0 || iters <= 0) return PK_ERR_ARG;
+  hipLaunchKernelGGL(probe_mfma_kernel<4>, dim3(blocks), dim3(512), 0, pk::as_stream(stream), seed, iters, out,
+                     stamp);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
 
 extern "C" int pkdev_probe_linear(const float* x, const float* w, float* y, int64_t R, int mode, void* stream) {
   if (R <= 0 || mode < 0 || mode > 3) return PK_ERR_ARG;

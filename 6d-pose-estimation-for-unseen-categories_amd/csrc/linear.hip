@@ -987,6 +987,159 @@ __global__ __launch_bounds__(256, 2) void linear_rows_lds_kernel(const float* __
   }
 }
 
+// Rows layout, LDS-DMA pipeline (the production rows path since round 4 for Cin in {32, 64, 128}):
+// round 3 found the per-point layers bound by serialisation, not bytes — every wave resident from
+// the start, all loads in one burst, then all MFMAs, then the stores (DESIGN.md §5 'Per-point
+// layers'). Here a block is 4 waves, one per SIMD, walking 16-point tiles grid-stride through a
+// ring of D LDS slots per wave filled by global_load_lds_dwordx4 (no VGPR cost, so D - 1 tiles
+// are in flight while the MFMAs of the current tile run):
+//   * slot = the tile's x rows (16 x Cin), then, with GEN, its mask rows and residual rows
+//     (16 x 16 TO each), every 16-B chunk XOR-swizzled on the SOURCE address (the LDS image of a
+//     glds is lane-linear) so the fragment reads are conflict-free;
+//   * the weight sits in VGPRs (A operand: lane (g, m) of output tile t at step (q, i) holds
+//     W[16 t + m][16 q + 4 g + i]), so D[out][point]: a lane ends with 4 CONSECUTIVE outputs of one
+//     point — bias, mask, residual and the store move as 16-B vectors;
+//   * the contraction order (k = 16 q + 4 g + i at step (q, i)) and the epilogue are those of
+//     linear_fwd_rows_kernel: results are bit-identical to it;
+//   * counted waits: every tile issues the same G glds (tiles past the end are loaded again at a
+//     clamped index), so "tile k landed" is s_waitcnt vmcnt((D - 1) G): vector-memory ops retire
+//     in issue order and at least the next D - 1 tiles' glds are younger (the stores in between
+//     are left out of the count, which only makes the wait more conservative).
+// MASK / ADD (GEN epilogues): the ReLU-backward mask rows (shaped like the output) and the
+// residual rows (row stride sa, columns < add_cols) ride in the slot; SPLIT: outputs >= split
+// (a multiple of 16) go to y2. Cout % 16 == 0, act 0 / 1, no channels-first store (host checks).
+__device__ __forceinline__ void vm_wait(int n) {  // s_waitcnt vmcnt(n), expcnt / lgkmcnt untouched
+  switch (n) {
+#define PK_VMW(N) case N: __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8)); break;
+    PK_VMW(0) PK_VMW(1) PK_VMW(2) PK_VMW(3) PK_VMW(4) PK_VMW(5) PK_VMW(6) PK_VMW(7) PK_VMW(8) PK_VMW(9)
+    PK_VMW(10) PK_VMW(11) PK_VMW(12) PK_VMW(13) PK_VMW(14) PK_VMW(15) PK_VMW(16) PK_VMW(17) PK_VMW(18)
+    PK_VMW(19) PK_VMW(20) PK_VMW(21) PK_VMW(22) PK_VMW(23) PK_VMW(24) PK_VMW(25) PK_VMW(26) PK_VMW(27)
+    PK_VMW(28) PK_VMW(29) PK_VMW(30) PK_VMW(31) PK_VMW(32) PK_VMW(33) PK_VMW(34) PK_VMW(35) PK_VMW(36)
+    PK_VMW(37) PK_VMW(38) PK_VMW(39) PK_VMW(40) PK_VMW(41) PK_VMW(42) PK_VMW(43) PK_VMW(44) PK_VMW(45)
+    PK_VMW(46) PK_VMW(47) PK_VMW(48) PK_VMW(49) PK_VMW(50) PK_VMW(51) PK_VMW(52) PK_VMW(53) PK_VMW(54)
+    PK_VMW(55) PK_VMW(56) PK_VMW(57) PK_VMW(58) PK_VMW(59) PK_VMW(60) PK_VMW(61) PK_VMW(62)
+#undef PK_VMW
+    default: __builtin_amdgcn_s_waitcnt((63 & 15) | ((63 >> 4) << 14) | (7 << 4) | (15 << 8)); break;
+  }
+}
+
+// 16 rows x CW floats (row stride ld, columns >= cols_ok read at column 0 of the row: valid
+// memory, masked at use) into an LDS region of 16 x CW floats, chunk (row, c) at position
+// row * CW / 4 + (c ^ (row & (CW / 4 - 1) & 15)): CW / 16 glds per wave
+template <int CW>
+__device__ __forceinline__ void glds_rows(const float* __restrict__ src, int64_t ld, int64_t row0, int64_t R,
+                                          int cols_ok, float* lds_dst, int lane) {
+  constexpr int CPR = CW / 4, NI = CW / 16;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int p = j * 64 + lane;
+    const int row = p / CPR, cl = p % CPR;
+    const int c = cl ^ (row & (CPR - 1) & 15);
+    const int64_t gr = min(row0 + row, R - 1);
+    const int col = 4 * c < cols_ok ? 4 * c : 0;
+    __builtin_amdgcn_global_load_lds(src + gr * ld + col, (__attribute__((address_space(3))) void*)(lds_dst + j * 256),
+                                     16, 0, 0);
+  }
+}
+
+template <int CW>
+__device__ __forceinline__ f32x4 lds_chunk(const float* region, int row, int c) {
+  constexpr int CPR = CW / 4;
+  return *reinterpret_cast<const f32x4*>(region + 4 * (row * CPR + (c ^ (row & (CPR - 1) & 15))));
+}
+
+template <int Q, int TO, bool MASK, bool ADD, bool SPLIT>
+__global__ __launch_bounds__(256, 1) void linear_glds_rows_kernel(const float* __restrict__ x, int64_t sx,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ bias, int64_t R, int Cin,
+                                                                  int Cout, int transw, LinEpi e) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int CI = 16 * Q, CO = 16 * TO;
+  constexpr int SLOT = 16 * CI + (MASK ? 16 * CO : 0) + (ADD ? 16 * CO : 0);  // floats
+  constexpr int G = Q + (MASK ? TO : 0) + (ADD ? TO : 0);  // glds per tile
+  constexpr int D = 3 * 4 * SLOT * 4 <= 159 * 1024 ? 3 : 2;  // ring depth within the CU's LDS
+  const int lane = pk::lane_id(), wv = pk::wave_id(), m = lane & 15, g = lane >> 4;
+  // weight -> VGPRs through the (not yet used) ring: Ws[o][k], row stride CI + 4
+  lr_stage<Q, TO>(w, Cout, transw, lds, w, 1 << 30);
+  __syncthreads();
+  f32x4 wf[TO][Q];
+#pragma unroll
+  for (int t = 0; t < TO; ++t)
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      wf[t][q] = *reinterpret_cast<const f32x4*>(&lds[(t * 16 + m) * (CI + 4) + 16 * q + 4 * g]);
+  f32x4 bv[TO];  // bias of outputs 16 t + 4 g + r
+#pragma unroll
+  for (int t = 0; t < TO; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = 16 * t + 4 * g + r;
+      bv[t][r] = (bias != nullptr && o < Cout) ? bias[o] : 0.f;
+    }
+  __syncthreads();  // every wave holds its weight: the ring may now overwrite the stage
+  float* ring = lds + (int64_t)wv * D * SLOT;
+  const int64_t T = (R + 15) >> 4, stride = (int64_t)gridDim.x * 4;
+  const int64_t t0 = (int64_t)blockIdx.x * 4 + wv;
+  if (t0 >= T) return;
+  const int64_t nt = (T - 1 - t0) / stride + 1;  // tiles of this wave
+  auto issue = [&](int64_t k) {  // glds of this wave's k-th tile (clamped: constant op count)
+    const int64_t tile = t0 + min(k, nt - 1) * stride;
+    float* s = ring + (k % D) * SLOT;
+    glds_rows<CI>(x, sx, tile * 16, R, CI, s, lane);
+    if constexpr (MASK) glds_rows<CO>(e.mask, Cout, tile * 16, R, Cout, s + 16 * CI, lane);
+    if constexpr (ADD) glds_rows<CO>(e.add, e.sa, tile * 16, R, e.add_cols, s + 16 * CI + (MASK ? 16 * CO : 0), lane);
+  };
+#pragma unroll
+  for (int k = 0; k < D - 1; ++k) issue(k);
+  for (int64_t k = 0; k < nt; ++k) {
+    issue(k + D - 1);
+    // tile k landed: at least the (D - 1) G glds of tiles k+1 .. k+D-1 are younger than its own
+    // (vector-memory ops retire in issue order); the stores issued in between are not counted,
+    // so the wait also drains the oldest of them — conservative whatever the stores' exec masks
+    vm_wait((D - 1) * G);
+    const float* s = ring + (k % D) * SLOT;
+    const int64_t tile = t0 + k * stride;
+    f32x4 acc[TO];
+#pragma unroll
+    for (int t = 0; t < TO; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const f32x4 xv = lds_chunk<CI>(s, m, 4 * q + g);  // point m, features 16 q + 4 g .. + 3
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < TO; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[t][q][i], xv[i], acc[t], 0, 0, 0);
+    }
+    // D[out 16 t + 4 g + r][point m]
+    const int64_t pr = tile * 16 + m;
+#pragma unroll
+    for (int t = 0; t < TO; ++t) {
+      f32x4 mk = {1.f, 1.f, 1.f, 1.f}, ad = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (MASK) mk = lds_chunk<CO>(s + 16 * CI, m, 4 * t + g);
+      if constexpr (ADD) {
+        if (16 * t + 4 * g < e.add_cols) ad = lds_chunk<CO>(s + 16 * CI + (MASK ? 16 * CO : 0), m, 4 * t + g);
+      }
+      f32x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = 16 * t + 4 * g + r;
+        float u = acc[t][r] + bv[t][r];
+        u = e.relu ? fmaxf(u, 0.f) : u;  // (act 0 / 1 only here: the host routes sigmoid elsewhere)
+        u = mk[r] <= 0.f ? 0.f : u;      // relu_mask
+        v[r] = ADD ? u + (o < e.add_cols ? ad[r] : 0.f) : u;
+      }
+      const int o0 = 16 * t + 4 * g;
+      if (pr < R) {
+        if (SPLIT && 16 * t >= e.split)  // (split % 16 == 0: wave-uniform per output tile)
+          *reinterpret_cast<f32x4*>(&e.y2[pr * e.sy2 + (o0 - e.split)]) = v;
+        else
+          *reinterpret_cast<f32x4*>(&e.y[pr * e.sy + o0]) = v;
+      }
+    }
+  }
+  vm_wait(0);
+}
+
 // Channels-first layout (1) [Bn, C, N] with Cin in {16, 32, 64, 128}: one wave computes 16 SUB
 // consecutive points of one item x all outputs; tpc tiles per item (SUB > 1 needs N % (16 SUB)
 // == 0; with SUB = 1 an item's last tile may be ragged: its columns past N compute on a clamped
@@ -1355,6 +1508,51 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
     };
     // plain: no mask, no residual add, one contiguous output (split == Cout)
     const bool plain = e.mask == nullptr && e.add == nullptr && e.y2 == nullptr && !e.store_cf && e.split >= Cout;
+#ifdef PK_DEVBUILD
+    static const bool glds_on = getenv("PK_ROWS_GLDS") == nullptr || atoi(getenv("PK_ROWS_GLDS")) != 0;
+#else
+    constexpr bool glds_on = true;
+#endif
+    auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    const bool glds_ok = glds_on && Cin >= 32 && Cout >= 32 && Cout % 16 == 0 && TO * (Cin / 16) <= 32 &&
+                         e.relu <= 1 && !e.store_cf && al16(x) && al16(e.y) && e.sy % 4 == 0 &&
+                         (e.y2 == nullptr || (al16(e.y2) && e.sy2 % 4 == 0 && split % 16 == 0)) &&
+                         (e.mask == nullptr || al16(e.mask)) && (e.add == nullptr || (al16(e.add) && e.sa % 4 == 0));
+    if (glds_ok) {
+      const bool MK = e.mask != nullptr, AD = e.add != nullptr, SP = e.y2 != nullptr;
+      const int slot = 16 * Cin + (MK ? 16 * Cout : 0) + (AD ? 16 * Cout : 0);
+      const int D = 3 * 4 * slot * 4 <= 159 * 1024 ? 3 : 2;  // (the kernel's own constexpr D)
+      const size_t ldsg = std::max((size_t)D * 4 * slot, (size_t)(16 * TO) * (Cin + 4)) * sizeof(float);
+      const unsigned bg = (unsigned)std::min<int64_t>((tiles + 3) / 4, (int64_t)kRowsPersistCUs);
+      auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(bg), dim3(256), ldsg, st, x, sx, w, bias, R, Cin, Cout, transw, e);
+      };
+      auto pe = [&](auto q, auto to) {
+        constexpr int Qv = decltype(q)::value, TOv = decltype(to)::value;
+        if (SP) {
+          if (MK && AD) launch(linear_glds_rows_kernel<Qv, TOv, true, true, true>);
+          else if (MK) launch(linear_glds_rows_kernel<Qv, TOv, true, false, true>);
+          else if (AD) launch(linear_glds_rows_kernel<Qv, TOv, false, true, true>);
+          else launch(linear_glds_rows_kernel<Qv, TOv, false, false, true>);
+        } else {
+          if (MK && AD) launch(linear_glds_rows_kernel<Qv, TOv, true, true, false>);
+          else if (MK) launch(linear_glds_rows_kernel<Qv, TOv, true, false, false>);
+          else if (AD) launch(linear_glds_rows_kernel<Qv, TOv, false, true, false>);
+          else launch(linear_glds_rows_kernel<Qv, TOv, false, false, false>);
+        }
+      };
+      using I2 = std::integral_constant<int, 2>;
+      using I4 = std::integral_constant<int, 4>;
+      using I8 = std::integral_constant<int, 8>;
+      auto pt = [&](auto q) {  // TO x Q <= 32 (the weight's VGPRs)
+        if (TO == 2) pe(q, I2{});
+        else if (TO == 4) pe(q, I4{});
+        else if constexpr (decltype(q)::value <= 4) pe(q, I8{});
+      };
+      if (Cin == 32) pt(I2{}); else if (Cin == 64) pt(I4{}); else pt(I8{});
+      PK_CHECK_LAUNCH();
+      return PK_OK;
+    }
     // development switch (read once): PK_ROWS_LDS=1 takes the LDS-staged full-line kernel; measured
     // within +-15 % of the fragment-load kernel shape by shape (profiles/r03_lin_bench_lds_vs_r2.txt),
     // so round 2's kernel stays the default

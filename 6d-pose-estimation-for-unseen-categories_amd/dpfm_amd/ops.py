@@ -807,10 +807,10 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], c
     # at or below the f32 MFMA ridge (157.3 TFLOP/s / 8 TB/s = 19.7): HBM-bound (flops beside)
     if mask is not None and (mask.shape != y.shape or not mask.is_contiguous()):
         raise _lib.PoseKernError("linear_fwd: mask must be contiguous and shaped like the output")
-    call("pk_linear_fwd", ptr(x), ptr(w), ptr(bias), layout, int(R), int(N), int(Cin), int(Cout), int(transw),
-         int(relu), ptr(mask), ptr(y), _lib.stream(x.device),
-         work=("hbm", 4 * int(R) * (Cin + Cout + (Cout if mask is not None else 0)) + 4 * Cin * Cout,
-               2 * int(R) * Cin * Cout))
+    # through pk_linear_ex (pk_linear_fwd's own body): every per-point layer launch of the step is
+    # then one entry point, so the bench's per-entry timing and the PMC pass's per-kernel bytes
+    # describe the same launches
+    linear_ex(x, w, bias, layout, int(R), int(N), int(Cin), int(Cout), y, transw=transw, relu=relu, mask=mask)
     return y
 
 
@@ -880,12 +880,37 @@ def spectral_raw(x: torch.Tensor, ld_in: int, mass, evals, evecs, t, clamp_t: bo
 FD_MODES = {"fp32": 0, "bf16": 1, "bf16x3": 2}
 
 
+_FD_WORK = {}
+_FD_CAPTURED = []
+
+
+def _fd_work(dev: torch.device, nbytes: int) -> torch.Tensor:
+    """pk_feat_dist_topk's scratch. Its leading arrival words must be zero before the first call and
+    every call leaves them zero (posekern.h), and a buffer must not serve two streams at once, so:
+    eager calls reuse one persistent buffer per (device, stream), zero-filled once when created or
+    grown; a call inside a HIP-graph capture gets a buffer of its own whose zero fill is captured
+    with it (graphs may share a capture stream; every replay then starts from zero words), kept
+    alive for the graph's lifetime."""
+    if torch.cuda.is_current_stream_capturing():
+        buf = torch.zeros((max(nbytes, 256),), dtype=torch.uint8, device=dev)
+        _FD_CAPTURED.append(buf)
+        return buf
+    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
+    buf = _FD_WORK.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.zeros((max(nbytes, 256),), dtype=torch.uint8, device=dev)
+        _FD_WORK[key] = buf
+    return buf
+
+
 def feat_dist_topk(evecs_x: torch.Tensor, C: torch.Tensor, evecs_y: torch.Tensor, n1: torch.Tensor,
-                   n2: torch.Tensor, topk: int, want_dist: bool = False, precision: str = "fp32"):
+                   n2: torch.Tensor, topk: int, want_dist: bool = False, precision: str = "fp32",
+                   work: Optional[torch.Tensor] = None):
     """Nearest CAD rows of every crop point in the spectral embedding (pk_feat_dist_topk).
     evecs_x [B,V1,K>=30], C [B,30,30], evecs_y [B,V2,K>=30], n1/n2 int32 [B].
     precision: "fp32" (the parity path: torch.cdist's augmented contraction on the f32 MFMA),
-    "bf16" or "bf16x3" (opt-in: bf16 MFMA cross term, f32 norms)."""
+    "bf16" or "bf16x3" (opt-in: bf16 MFMA cross term, f32 norms). work: optional caller scratch
+    (uint8, zero-initialised before its first use, see _fd_work); default: a per-stream buffer."""
     B, V1, ldx = evecs_x.shape
     _, V2, ldy = evecs_y.shape
     dev = evecs_x.device
@@ -893,7 +918,10 @@ def feat_dist_topk(evecs_x: torch.Tensor, C: torch.Tensor, evecs_y: torch.Tensor
     nbytes = int(_lib.lib().pk_feat_dist_work_size(B, V1, V2, int(topk), mode))
     if nbytes < 0:
         raise _lib.PoseKernError("feat_dist_topk: invalid shape / topk / precision")
-    work = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+    if work is None:
+        work = _fd_work(dev, nbytes)
+    elif work.numel() < nbytes:
+        raise _lib.PoseKernError(f"feat_dist_topk: work holds {work.numel()} bytes, {nbytes} needed")
     idx = torch.empty((B, V2, topk), dtype=torch.int64, device=dev)
     dist = torch.empty((B, V2, topk), dtype=torch.float32, device=dev) if want_dist else None
     call("pk_feat_dist_topk", ptr(evecs_x.contiguous()), ldx, ptr(C.contiguous()), ptr(evecs_y.contiguous()), ldy,

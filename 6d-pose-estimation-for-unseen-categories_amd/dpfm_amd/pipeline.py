@@ -283,14 +283,16 @@ class TrainStep:
             self.opt.state[p] = sp
         self.nce_counter().copy_(other.nce_counter())
 
-    def allreduce_grads(self, grads=None):
+    def allreduce_grads(self, grads=None, force: bool = False):
         """DDP's gradient averaging in one bucket (49,281 f32 = 197 KB: latency-bound).
-        `grads` defaults to the parameters' .grad tensors."""
-        if self.world <= 1:
+        `grads` defaults to the parameters' .grad tensors. With one rank nothing runs unless
+        `force` (the collective path on an initialised group of size 1: tests/_rccl_worker.py)."""
+        if self.world <= 1 and not force:
             return
         if self.flat_grads:  # the gradients ARE views of flat: one collective, one scale
             dist.all_reduce(self.flat, group=self.group)
-            self.flat.div_(self.world)
+            if self.world > 1:
+                self.flat.div_(self.world)
             return
         grads = grads if grads is not None else [p.grad for p in self.params]
         o = 0
@@ -299,7 +301,8 @@ class TrainStep:
             self.flat[o:o + n].copy_(g.reshape(-1))
             o += n
         dist.all_reduce(self.flat, group=self.group)
-        self.flat.div_(self.world)
+        if self.world > 1:
+            self.flat.div_(self.world)
         o = 0
         for g in grads:
             n = g.numel()

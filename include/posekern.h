@@ -386,10 +386,14 @@ int pk_linear_ex(const pk_linear_args* a, void* stream);
  *   evecs_y f32 [B,V2max,ldy]; n1/n2 int32 [B] valid rows
  *   mode 0: fp32 MFMA on torch.cdist's augmented K = 32 operands (the parity path);
  *   mode 1: bf16 MFMA cross term + f32 norms; mode 2: bf16x3 (hi/lo split, three bf16 MFMAs)
- *   work: scratch of pk_feat_dist_work_size(B, V1max, V2max, topk, mode) bytes
+ *   work: scratch of pk_feat_dist_work_size(B, V1max, V2max, topk, mode) bytes. Its first
+ *     pk_feat_dist_counter_bytes(...) bytes are arrival words of the single-launch mode-0 pass
+ *     (row parts combined in the launch): they must be zero before the first call that uses the
+ *     buffer, and every call leaves them zero (keep one buffer per stream; zero it once).
  *   out_idx int64 [B,V2max,topk] ascending distance (ties: lower index); out_dist f32
  *   [B,V2max,topk] Euclidean distances (may be NULL). Fused selection epilogue. */
 int64_t pk_feat_dist_work_size(int B, int V1max, int V2max, int topk, int mode);
+int64_t pk_feat_dist_counter_bytes(int B, int V1max, int V2max, int topk, int mode);
 int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, const float* evecs_y, int ldy,
                       const int32_t* n1, const int32_t* n2, int B, int V1max, int V2max, int topk, int mode,
                       void* work, int64_t work_bytes, int64_t* out_idx, float* out_dist, void* stream);

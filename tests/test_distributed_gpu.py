@@ -42,3 +42,15 @@ def test_sharded_inference_equals_single_rank():
     """configs[3] sharding: 2 ranks x 2 crops give bit-identical poses, IR, correspondence
     counts, metrics and C to one process over the 4 crops."""
     _launch("_dist_infer_worker.py", "sharded-infer ok")
+
+
+@pytest.mark.timeout(240)
+def test_rccl_flat_allreduce_world1():
+    """RCCL (backend "nccl") initialised and used by the training step's gradient collective,
+    world size 1 (one GPU per rank; see tests/_rccl_worker.py)."""
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_rccl_worker.py")], env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=220)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert "rccl ok" in r.stdout

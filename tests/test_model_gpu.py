@@ -264,6 +264,60 @@ def test_linear_fwd(device, shape, channels_first, transw):
     assert (y - exp).abs().le(1e-5 * bound + 1e-6 * (0 if b is None else b.abs().max().item()) + 1e-30).all()
 
 
+@pytest.mark.parametrize("R,I,O,epi", [(65536, 128, 64, "relu"), (65536, 64, 64, "add"), (65536, 64, 128, "split_add"),
+                                        (65536, 64, 64, "mask"), (40000, 128, 32, "mask_add"), (4099, 32, 128, "split"),
+                                        (17, 64, 64, "mask_add"), (300000, 64, 64, "relu"), (65536, 64, 32, "plain")])
+def test_linear_ex_rows_epilogues(device, R, I, O, epi):
+    """pk_linear_ex on the rows layout (the LDS-DMA pipeline for Cin, Cout in {32, 64, 128}) with the
+    step's epilogues vs fp64: ReLU; the ReLU-backward mask; a residual added to the first add_cols
+    outputs from a wider row-strided buffer; outputs >= split to a second strided tensor; R with a
+    partial last tile and many tiles per wave. Bound |err| <= 1e-5 sum_k |x||w| (+ |b|, |add|
+    rounding)."""
+    from dpfm_amd import ops
+    g = torch.Generator().manual_seed(R + I + O)
+    ldx = I + 16
+    xs = torch.randn(R, ldx, generator=g)
+    x = xs[:, :I]
+    w = torch.randn(O, I, generator=g) * 0.2
+    b = torch.randn(O, generator=g)
+    dev = device
+    xd, wd = x.double(), w.double()
+    exp = xd @ wd.t() + b.double()
+    bound = xd.abs() @ wd.abs().t() * 1e-5 + 1e-6 * b.abs().max().item()
+    relu = epi in ("relu",)
+    if relu:
+        exp = exp.clamp_min(0)
+    mask = None
+    if "mask" in epi:
+        mask = torch.randn(R, O, generator=g)
+        exp = torch.where(mask.double() <= 0, torch.zeros_like(exp), exp)
+    add = None
+    add_cols = 0
+    lda = 0
+    if "add" in epi:
+        add_cols = O // 2
+        lda = O + 8
+        add = torch.randn(R, lda, generator=g)
+        exp[:, :add_cols] += add[:, :add_cols].double()
+        bound[:, :add_cols] += 1e-6 * add[:, :add_cols].abs().double()
+    split = O // 2 if "split" in epi else 0
+    ldy = O + 4 if not split else split + 4
+    y = torch.full((R, ldy), float("nan"), device=dev)
+    y2 = torch.full((R, O - split + 12), float("nan"), device=dev) if split else None
+    xg = xs.to(dev)
+    ops.linear_ex(xg, w.to(dev), b.to(dev), 0, R, 0, I, O, y, ldx=ldx, ldy=ldy, relu=relu,
+                  mask=None if mask is None else mask.to(dev), add=None if add is None else add.to(dev), lda=lda,
+                  add_cols=add_cols, y2=y2, split=split, ldy2=0 if y2 is None else y2.shape[1])
+    got = y.cpu().double()
+    if split:
+        full = torch.cat([got[:, :split], y2.cpu().double()[:, :O - split]], 1)
+        assert torch.isnan(got[:, split:]).all() and torch.isnan(y2.cpu()[:, O - split:]).all()
+    else:
+        full = got[:, :O]
+        assert torch.isnan(got[:, O:]).all()  # nothing written past the row's outputs
+    assert (full - exp).abs().le(bound + 1e-30).all(), float(((full - exp).abs() - bound).max())
+
+
 def test_dpfm_loss_matches_oracle(device):
     """H15 DPFMLoss (Frobenius + fused NCE kernel pk_nce_loss + weighted BCE, batched over
     crops) vs the reference loss restated in fp64 on the CPU (utils/loss.py:8-99), on the

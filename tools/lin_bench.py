@@ -4,7 +4,10 @@ import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "6d-pose-estimation-for-unseen-categories_amd")]
 import torch
-from dpfm_amd import ops
+from dpfm_amd import _lib, ops
+
+if os.environ.get("PK_DEV") == "1":  # libposekern_dev.so (its PK_* switches, e.g. PK_ROWS_GLDS=0)
+    _lib.use_dev_lib()
 
 dev = torch.device("cuda:0")
 shapes = [  # (lead, Cin, Cout, cf, transw)  lead = rows (cl) or (B, N) (cf)

@@ -2,7 +2,13 @@
 MI355X_MICROARCH.md's rocprofv3 section requires) into per-kernel-family HBM traffic per
 launch.
 
-  python tools/pmc_summary.py <fetch_dir> <write_dir> <out.json>
+  python tools/pmc_summary.py <fetch_dir> <write_dir> <out.json> [bench.json]
+
+With bench.json (the JSON line of the same `bench.py --eager --warmup 0` command the passes
+profiled), a family listed in PER_ENTRY is reported per ENTRY-POINT call: its kernels' bytes
+over every dispatch / the calls the bench's probe counted for that entry point (one entry call
+may launch several kernels). pk_linear_ex is such a family: every per-point layer launch of the
+step goes through it (ops.linear_fwd included), so its bytes match bench.py's roofline unit.
 
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE is in KiB and on gfx950
 reports half the bytes of 16-B-per-lane coalesced reads, so it is doubled; WRITE_SIZE
@@ -42,6 +48,12 @@ FAMILIES = {
 }
 # families whose launches are ONE of several kernels (every dispatch is a family launch)
 ANY_LEAD = {"pk_linear_fwd+ex"}
+# entry point -> its kernels, normalised per entry call with the bench's call count
+PER_ENTRY = {"pk_linear_ex": FAMILIES["pk_linear_fwd+ex"],
+             "pk_feat_dist_topk": ["fd_wide_kernel", "fd_prep_kernel", "fd_main_direct_kernel", "fd_merge_kernel",
+                                   "fd_fused_kernel", "fd_rows_kernel", "fd_cols_kernel"],
+             "pk_linear_wgrad_grouped": FAMILIES["pk_linear_wgrad_grouped"],
+             "pk_attention_fwd": FAMILIES["pk_attention_fwd"], "pk_attention_bwd": FAMILIES["pk_attention_bwd"]}
 # (the first kernel of each family is counted once per family launch)
 
 
@@ -86,6 +98,21 @@ def main():
         write_b = wb * 1024 / nw
         res[fam] = {"fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
                     "traffic_bytes_per_launch": fetch_b + write_b, "launches": nf}
+    if len(sys.argv) > 4:
+        bench = json.loads(open(sys.argv[4]).read().strip().splitlines()[-1])
+        calls = {k: v["launches"] for k, v in bench.get("kernels", {}).items()}
+        for ent, names in PER_ENTRY.items():
+            n = calls.get(ent)
+            if not n:
+                continue
+            fb = sum(s for k, (_, s) in read(fetch_dir, "FETCH_SIZE", 0, PROBE_GRID - 1).items()
+                     if any(nm in k for nm in names))
+            wb = sum(s for k, (_, s) in read(write_dir, "WRITE_SIZE", 0, PROBE_GRID - 1).items()
+                     if any(nm in k for nm in names))
+            fetch_b, write_b = 2.0 * fb * 1024 / n, wb * 1024 / n
+            res[ent] = {"fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
+                        "traffic_bytes_per_launch": fetch_b + write_b, "launches": n,
+                        "per": "entry-point call (bench probe count)"}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
