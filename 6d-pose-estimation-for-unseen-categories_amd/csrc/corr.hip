@@ -153,17 +153,15 @@ __global__ __launch_bounds__(256) void rigid_pair_kernel(const int64_t* __restri
   }
 }
 
-// ---- Round 3 production path: packed coordinates, 128 x 128 pair tiles, packed-f32 arithmetic.
+// ---- Packed coordinates, 128 x 128 pair tiles (rounds 2 and 3 of the filter).
 // Round 2's rigid_pair_kernel spent most of a block on its prologue: every entry of both tiles
 // was a dependent gather list -> cand -> cad / pc (three global loads in a chain) for only 16
 // pairs per thread. Here the coordinates of the current list live in a packed array (one
 // 32-B record per entry: {cad_x, pc_x, cad_y, pc_y, cad_z, pc_z, valid, 0}); the first round's is
 // gathered once (rigid_gather_kernel) and each compaction carries the survivors' records
 // along (rigid_compact_pts_kernel), so a pair block loads its two tiles with plain 16-B loads.
-// The pair term pairs the CAD and crop halves as float2 lanes: the differences, squares and
-// sums are v_pk_add_f32 / v_pk_mul_f32 (two separately rounded values per instruction, the
-// reference's ((dx^2 + dy^2) + dz^2) order, -ffp-contract=off), two v_sqrt_f32, and |a - b|
-// of two pairs at once; 8 x 8 pairs per thread.
+// The pair term is two rigid_dist (FMA sums of squares, v_sqrt_f32) and |a - b| folded into the
+// row and column sums as a source modifier; 8 x 8 pairs per thread.
 constexpr int kRT2 = 128;
 typedef float rf2 __attribute__((ext_vector_type(2)));
 
@@ -193,11 +191,21 @@ __global__ __launch_bounds__(256) void rigid_gather_kernel(const int64_t* __rest
   list[(int64_t)b * ldc + i] = i;
 }
 
+// One side of the pair term: the distance ||p - q|| with the squares summed as
+// (dx^2 + dy^2) + dz^2 in two fused multiply-adds (dx dx, then + dy dy, then + dz dz: each
+// partial sum rounded once; the reference's unfused form rounds the squares too, a <= 1-ulp
+// difference per term, below the f32 error of the n-term mean it feeds).
+__device__ __forceinline__ float rigid_dist(float px, float py, float pz, float qx, float qy, float qz) {
+  const float dx = qx - px, dy = qy - py, dz = qz - pz;
+  return __builtin_amdgcn_sqrtf(__builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx)));
+}
+
 // 8 x 8 pairs of one thread: rows i = ty + 16 r, columns j = tx + 16 c. ra[r]: this thread's
-// row sums (over its 8 columns, as float2 halves), ca[k]: its column sums for columns 2k, 2k+1.
+// row sums (over its 8 columns), ca[c]: its column sums. Scalar VALU: on MI355X a v_pk_*_f32
+// costs the issue of two scalar ops (measured: round 3's packed form ran at the scalar rate).
 template <bool EDGE>
 __device__ __forceinline__ void rigid_tile_pairs(const RigidRec* __restrict__ si, const RigidRec* __restrict__ sj,
-                                                 int tx, int ty, rf2 (&ra)[8], rf2 (&ca)[4]) {
+                                                 int tx, int ty, float (&ra)[8], float (&ca)[8]) {
   RigidRec cj[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) cj[c] = sj[tx + 16 * c];
@@ -205,21 +213,14 @@ __device__ __forceinline__ void rigid_tile_pairs(const RigidRec* __restrict__ si
   for (int r = 0; r < 8; ++r) {
     const RigidRec ci = si[ty + 16 * r];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float a[2], bb[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const RigidRec& q = cj[2 * k + h];
-        const rf2 dx = q.x - ci.x, dy = q.y - ci.y, dz = q.z - ci.z;
-        const rf2 s = (dx * dx + dy * dy) + dz * dz;  // {|CAD_i - CAD_j|^2, |PC_i - PC_j|^2}
-        a[h] = __builtin_amdgcn_sqrtf(s.x);
-        bb[h] = __builtin_amdgcn_sqrtf(s.y);
-      }
-      rf2 v = rf2{a[0], a[1]} - rf2{bb[0], bb[1]};
-      v = rf2{fabsf(v.x), fabsf(v.y)};
-      if (EDGE) v = v * (rf2{cj[2 * k].v.x, cj[2 * k + 1].v.x} * ci.v.x);  // invalid entries contribute 0
+    for (int c = 0; c < 8; ++c) {
+      const RigidRec& q = cj[c];
+      const float a = rigid_dist(ci.x.x, ci.y.x, ci.z.x, q.x.x, q.y.x, q.z.x);
+      const float bb = rigid_dist(ci.x.y, ci.y.y, ci.z.y, q.x.y, q.y.y, q.z.y);
+      float v = fabsf(a - bb);
+      if (EDGE) v = v * (q.v.x * ci.v.x);  // invalid entries contribute 0
       ra[r] += v;
-      ca[k] += v;
+      ca[c] += v;
     }
   }
 }
@@ -256,11 +257,9 @@ __global__ __launch_bounds__(256) void rigid_pair2_kernel(const int32_t* __restr
   }
   __syncthreads();
   const int tx = tid & 15, ty = tid >> 4;
-  rf2 ra[8], ca[4];
+  float ra[8], ca[8];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) ra[r] = rf2{0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) ca[k] = rf2{0.f, 0.f};
+  for (int r = 0; r < 8; ++r) ra[r] = ca[r] = 0.f;
   if ((J + 1) * kRT2 > n) rigid_tile_pairs<true>(si, sj, tx, ty, ra, ca);
   else rigid_tile_pairs<false>(si, sj, tx, ty, ra, ca);
   float* P = part + (int64_t)b * T * ldl;
@@ -268,7 +267,7 @@ __global__ __launch_bounds__(256) void rigid_pair2_kernel(const int32_t* __restr
   // mirror adds: VALU only, no LDS round trips); lane tx = 0's association order is fixed
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
-    float v = ra[r].x + ra[r].y;
+    float v = ra[r];
     v += __int_as_float((int)PK_DPP(__float_as_int(v), 0xB1));
     v += __int_as_float((int)PK_DPP(__float_as_int(v), 0x4E));
     v += __int_as_float((int)PK_DPP(__float_as_int(v), 0x141));
@@ -280,20 +279,154 @@ __global__ __launch_bounds__(256) void rigid_pair2_kernel(const int32_t* __restr
   // column sums of tile J over tile I: the wave's 4 ty rows by butterfly, then the 4 waves in order
   const int w = pk::wave_id();
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float v = h ? ca[k].y : ca[k].x;
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      if ((tid & 63) < 16) red[w][tx + 16 * (2 * k + h)] = v;
-    }
+  for (int c = 0; c < 8; ++c) {
+    float v = ca[c];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if ((tid & 63) < 16) red[w][tx + 16 * c] = v;
   }
   __syncthreads();
   if (tid < kRT2) {
     const float v = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
     const int x = J * kRT2 + tid;
     if (x < n) P[(int64_t)I * ldl + x] = v;
+  }
+}
+
+// ---- Round 1 (round-4 path): the candidates of nn_query come in groups of K = 5 that share one
+// crop point (spacial_filtering.py:36-38: p2p = stack([idx, idx_p]).reshape(2, -1), crop point
+// p repeated for its 5 nearest CAD points), so the crop half of the pair term,
+// ||PC[p_i] - PC[p_j]||, is the same for all 25 pairs of two groups. Tiles of 32 groups
+// (160 entries); thread (tx, ty) of 16 x 16 owns row groups ty, ty + 16 and column groups tx,
+// tx + 16: per group pair one crop distance, then 25 CAD distances. The pair value |a - b| is
+// bit-identical to rigid_pair2_kernel's (same rigid_dist); only the association of the sums
+// differs (fixed).
+// A tile pair whose groups do not share their crop coordinates (a caller passing another
+// candidate order) takes the general form of the same loop (both sqrt per pair), so any
+// candidate list is scored correctly. Partials as rigid_pair2_kernel, tiles of kRG entries.
+constexpr int kGK = 5;              // candidates per crop point (nn_query's K)
+constexpr int kGT = 32;             // groups per tile
+constexpr int kRG = kGK * kGT;      // entries per tile
+
+template <bool SHARED, bool EDGE>
+__device__ __forceinline__ void rigid_group_pairs(const RigidRec* __restrict__ si, const RigidRec* __restrict__ sj,
+                                                  int tx, int ty, float (&ra)[2][kGK], float (&ca)[2][kGK]) {
+  RigidRec cj[2][kGK];  // column entries (Q0 = tx, l) and (Q1 = tx + 16, l)
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int l = 0; l < kGK; ++l) cj[h][l] = sj[kGK * (tx + 16 * h) + l];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int P = ty + 16 * r;
+    float bq[2] = {0.f, 0.f};
+    if (SHARED) {  // one crop distance per (P, Q0) / (P, Q1)
+      const RigidRec p = si[kGK * P];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) bq[h] = rigid_dist(p.x.y, p.y.y, p.z.y, cj[h][0].x.y, cj[h][0].y.y, cj[h][0].z.y);
+    }
+#pragma unroll
+    for (int k = 0; k < kGK; ++k) {
+      const RigidRec ci = si[kGK * P + k];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int l = 0; l < kGK; ++l) {
+          const RigidRec& q = cj[h][l];
+          const float a = rigid_dist(ci.x.x, ci.y.x, ci.z.x, q.x.x, q.y.x, q.z.x);
+          const float b = SHARED ? bq[h] : rigid_dist(ci.x.y, ci.y.y, ci.z.y, q.x.y, q.y.y, q.z.y);
+          float v = fabsf(a - b);
+          if (EDGE) v = v * (q.v.x * ci.v.x);  // invalid entries contribute 0
+          ra[r][k] += v;
+          ca[h][l] += v;
+        }
+    }
+  }
+}
+
+// Grid (T (T + 1) / 2, B) over kRG x kRG tile pairs I <= J (T = ceil(nmax / kRG)), XCD-aware;
+// block 256. Writes part[b][J][x] (x in tile I) and, for I != J, part[b][I][y] (y in tile J).
+__global__ __launch_bounds__(256) void rigid_group_kernel(const int32_t* __restrict__ nlist, int ldl,
+                                                          const RigidRec* __restrict__ pts, int T,
+                                                          float* __restrict__ part) {
+  __shared__ RigidRec si[kRG], sj[kRG];
+  __shared__ float red[4][kRG];
+  const int3 lb = pk::xcd_block3();
+  const int b = lb.y;
+  const int n = nlist[b];
+  const int t = lb.x;
+  int J = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
+  while ((J + 1) * (J + 2) / 2 <= t) ++J;
+  while (J * (J + 1) / 2 > t) --J;
+  const int I = t - J * (J + 1) / 2;
+  if (J * kRG >= n) return;  // block-uniform: tile outside the list
+  const RigidRec* P0 = pts + (int64_t)b * ldl;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 2 * kRG; e += 256) {
+    const int loc = e < kRG ? e : e - kRG;
+    const int x = (e < kRG ? I : J) * kRG + loc;
+    RigidRec r;
+    if (x < n) r = P0[x];
+    else r.x = r.y = r.z = r.v = rf2{0.f, 0.f};
+    (e < kRG ? si : sj)[loc] = r;
+  }
+  __syncthreads();
+  // do the valid members of every group carry their group's crop coordinates (bitwise)?
+  int split = 0;
+  if (tid < 2 * kGT) {
+    const RigidRec* g = (tid < kGT ? si : sj) + kGK * (tid & (kGT - 1));
+    for (int k = 1; k < kGK; ++k)
+      if (g[k].v.x != 0.f && (__float_as_uint(g[k].x.y) != __float_as_uint(g[0].x.y) ||
+                              __float_as_uint(g[k].y.y) != __float_as_uint(g[0].y.y) ||
+                              __float_as_uint(g[k].z.y) != __float_as_uint(g[0].z.y)))
+        split = 1;
+  }
+  const bool shared = !__syncthreads_or(split);
+  const bool edge = (J + 1) * kRG > n;
+  const int tx = tid & 15, ty = tid >> 4;
+  float ra[2][kGK], ca[2][kGK];
+#pragma unroll
+  for (int l = 0; l < kGK; ++l) ra[0][l] = ra[1][l] = ca[0][l] = ca[1][l] = 0.f;
+  if (shared) {
+    if (edge) rigid_group_pairs<true, true>(si, sj, tx, ty, ra, ca);
+    else rigid_group_pairs<true, false>(si, sj, tx, ty, ra, ca);
+  } else {
+    if (edge) rigid_group_pairs<false, true>(si, sj, tx, ty, ra, ca);
+    else rigid_group_pairs<false, false>(si, sj, tx, ty, ra, ca);
+  }
+  float* Pp = part + (int64_t)b * T * ldl;
+  // row sums of tile I over tile J: the 16 tx lanes of a DPP row, fixed association
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+#pragma unroll
+    for (int k = 0; k < kGK; ++k) {
+      float v = ra[r][k];
+      v += __int_as_float((int)PK_DPP(__float_as_int(v), 0xB1));
+      v += __int_as_float((int)PK_DPP(__float_as_int(v), 0x4E));
+      v += __int_as_float((int)PK_DPP(__float_as_int(v), 0x141));
+      v += __int_as_float((int)PK_DPP(__float_as_int(v), 0x140));
+      const int x = I * kRG + kGK * (ty + 16 * r) + k;
+      if (tx == 0 && x < n) Pp[(int64_t)J * ldl + x] = v;
+    }
+  }
+  if (I == J) return;  // block-uniform; the diagonal tile's row sums cover both orders
+  // column sums of tile J over tile I: the wave's 4 ty rows by butterfly, then the 4 waves in order
+  const int w = pk::wave_id();
+#pragma unroll
+  for (int l = 0; l < kGK; ++l) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v = ca[h][l];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if ((tid & 63) < 16) red[w][kGK * (tx + 16 * h) + l] = v;
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < kRG; e += 256) {
+    const float v = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+    const int x = J * kRG + e;
+    if (x < n) Pp[(int64_t)I * ldl + x] = v;
   }
 }
 
@@ -758,7 +891,8 @@ static int64_t rigid_part_bytes(int B, int nmax, int ldc) {
 }
 
 #ifdef PK_DEVBUILD
-static int g_rigid_variant = 0;  // 1: round 2's 64-tile gather path (pkdev_rigidity_variant, A/B timing)
+static int g_rigid_variant = 0;  // pkdev_rigidity_variant (A/B timing): 1 round 2's 64-tile gather path,
+                                 // 2 round 3's ungrouped first round
 #else
 constexpr int g_rigid_variant = 0;
 #endif
@@ -788,7 +922,8 @@ extern "C" int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* n
   hipStream_t s = pk::as_stream(stream);
   const dim3 g((nmax + 255) / 256, B);
   const int T2 = (nmax + kRT2 - 1) / kRT2;
-  const bool packed = partial != nullptr && T2 > 0 && g_rigid_variant == 0;
+  const int T1 = (nmax + kRG - 1) / kRG;  // <= T2: the grouped round's partial rows fit
+  const bool packed = partial != nullptr && T2 > 0 && g_rigid_variant != 1;
   RigidRec* pa = nullptr;
   RigidRec* pb = nullptr;
   if (packed) {
@@ -806,10 +941,16 @@ extern "C" int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* n
   int32_t* nspare = n_a;
   const int T = (nmax + kRT - 1) / kRT;
   for (int r = 0; r < 3; ++r) {
-    if (packed) {
+    if (packed && r == 0 && g_rigid_variant != 2) {  // grouped first round (T1 <= T2 partial rows)
+      hipLaunchKernelGGL(rigid_group_kernel, dim3(T1 * (T1 + 1) / 2, B), dim3(256), 0, s, nin, ldc, pa, T1, partial);
+      PK_CHECK_LAUNCH();
+      hipLaunchKernelGGL(rigid_reduce_kernel, g, dim3(256), 0, s, nin, ldc, partial, T1, kRG, score);
+    } else if (packed) {
       hipLaunchKernelGGL(rigid_pair2_kernel, dim3(T2 * (T2 + 1) / 2, B), dim3(256), 0, s, nin, ldc, pa, T2, partial);
       PK_CHECK_LAUNCH();
       hipLaunchKernelGGL(rigid_reduce_kernel, g, dim3(256), 0, s, nin, ldc, partial, T2, kRT2, score);
+    }
+    if (packed) {
       PK_CHECK_LAUNCH();
       hipLaunchKernelGGL(rigid_compact_pts_kernel, dim3(B), dim3(1024), 0, s, lin, ldc, nin, score, thr4, r, pa, lout,
                          r < 2 ? pb : nullptr, nout);

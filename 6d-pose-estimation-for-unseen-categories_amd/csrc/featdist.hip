@@ -1414,6 +1414,15 @@ __global__ __launch_bounds__(256, 2) void fd_wide_kernel(
       for (int r = 0; r < 4; ++r) {
         const int c = 4 * grp + cc;
         const int key = max(__float_as_int(acc[cc][r]), kClamp);
+        if constexpr (VAR == 5) {  // (development variant: the value only, no row index)
+          bk[c][r] = min(key, bk[c][r]);
+          continue;
+        }
+        if constexpr (VAR == 6) {  // (development variant: the compiler's compare + select)
+          bt[c][r] = key < bk[c][r] ? tt : bt[c][r];
+          bk[c][r] = min(key, bk[c][r]);
+          continue;
+        }
         int dif = key - bk[c][r];
         // (the empty asm hides the difference's range: the compiler would rewrite the sign mask
         // as a v_cmp + v_cndmask pair through VCC, with hazard s_nops, a serial chain per distance)
@@ -1441,8 +1450,14 @@ __global__ __launch_bounds__(256, 2) void fd_wide_kernel(
     const bool more = ch + 1 < nchunk;
     if (more) xload(c0 + kWideChunk + 2 * w, xv);
     const int ntile = min(kWideChunk, te - c0);
+    f32x4 n0 = cb[lane], n1 = cb[64 + lane];  // the next tile's A fragment, one tile ahead
     for (int t = 0; t < ntile; ++t) {
-      const f32x4 a0 = cb[t * 128 + lane], a1 = cb[t * 128 + 64 + lane];
+      const f32x4 a0 = n0, a1 = n1;
+      {
+        const int tn = min(t + 1, ntile - 1);
+        n0 = cb[tn * 128 + lane];
+        n1 = cb[tn * 128 + 64 + lane];
+      }
       const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
 #pragma unroll
       for (int grp = 0; grp < CT / 4; ++grp) {
@@ -1469,10 +1484,12 @@ __global__ __launch_bounds__(256, 2) void fd_wide_kernel(
         } else if (prev_grp >= 0) {
           sel(acc[(CT / 4 - 1) & 1], CT / 4 - 1, prev_t);
         }
+        if constexpr (VAR != 4) {  // (VAR 4, development variant: the compiler's own schedule)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // 5 VALU
+          for (int i = 0; i < 16; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // 5 VALU
+          }
         }
       }
       prev_grp = CT / 4 - 1;
@@ -1715,13 +1732,15 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
     auto* part = static_cast<unsigned long long*>(work);
     const dim3 wgrid((unsigned)((int64_t)B * wp.NCG * wp.RS));
 #ifdef PK_DEVBUILD
-    static const int wvar = [] {  // development knob PK_FD_VAR: 1 no selection, 2 no MFMAs, 3 neither
+    static const int wvar = [] {  // development knob PK_FD_VAR: 1 no selection, 2 no MFMAs, 3 neither,
+      // 4 no sched_group_barrier, 5 value-only selection, 6 compare + select
       const char* e = std::getenv("PK_FD_VAR");
       return e ? std::atoi(e) : 0;
     }();
 #define PK_FDW(V) hipLaunchKernelGGL((fd_wide_kernel<kWideCT, V>), wgrid, dim3(256), 0, s, evecs_x, ldx, C, evecs_y, \
                                      ldy, n1, n2, V1max, V2max, wp.NCG, wp.RS, out_idx, out_dist, part, arrivals)
-    if (wvar == 1) PK_FDW(1); else if (wvar == 2) PK_FDW(2); else if (wvar == 3) PK_FDW(3); else PK_FDW(0);
+    if (wvar == 1) PK_FDW(1); else if (wvar == 2) PK_FDW(2); else if (wvar == 3) PK_FDW(3);
+    else if (wvar == 4) PK_FDW(4); else if (wvar == 5) PK_FDW(5); else if (wvar == 6) PK_FDW(6); else PK_FDW(0);
 #undef PK_FDW
 #else
     hipLaunchKernelGGL(fd_wide_kernel<kWideCT>, wgrid, dim3(256), 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, n2, V1max,

@@ -1140,6 +1140,239 @@ __global__ __launch_bounds__(256, 1) void linear_glds_rows_kernel(const float* _
   vm_wait(0);
 }
 
+// ---- Weight gradients on the LDS-DMA pipeline (round 4, the grouped path's default) ----
+// Round 3's wgrad_v2_body gave each of 8 waves one 32 x 32 output tile and had every wave load
+// its own columns of x and dy straight into VGPRs: each row was fetched by To + Ti waves and
+// only two 16-row batches were in flight per wave (0.20 ms/step at 0.2 of the f32 MFMA rate and
+// 0.3 of HBM). Here a block is 4 waves, one per SIMD, over one slice of one problem's rows; wave
+// w walks the slice's 16-row tiles w, w + 4, ... through a ring of D LDS slots filled by
+// global_load_lds_dwordx4 (x rows, then dy rows: each byte fetched once, D - 1 tiles in flight
+// at no VGPR cost), and holds the WHOLE [O, I] gradient as TO x TI 16 x 16 accumulators
+// (v_mfma_f32_16x16x4f32: A[o][k] = dY[row k][o], B[k][i] = X[row k][i]). The 4 waves' sums are
+// added through LDS in wave order and written as the block's partial; the grouped reduction sums
+// the partials in block order (deterministic, as before).
+//   layout 0 ([R, C]): the slot holds glds_rows images (row-major, 16-B chunks XOR-swizzled per
+//     row); k-step q, lane (g, m) takes row 4 q + g and the TO (TI) CONSECUTIVE channels
+//     TO m .. TO m + TO - 1 of dy (x) in one vector read: accumulator tile t holds o = TO m' + t.
+//     The last tile of a problem may be ragged: its clamped rows get dy = 0.
+//   layout 1 ([Bn, C, N], N % 16 == 0, batch stride 4-aligned): the slot holds per channel the
+//     tile's 16 rows, 16-B chunk j of channel c at position j ^ ((c >> 2) & 3) (XOR on the
+//     SOURCE address: conflict-free reads); lane (g, m) reads rows 4 g .. 4 g + 3 of channel
+//     m + 16 t as one vector, i.e. k-step q takes row 4 g + q (any bijection works: A and B use
+//     the same one). Tile t holds o = m' + 16 t.
+// Bias: db[o] = the sum of the dy values the lanes feed the MFMAs (fixed order).
+constexpr int kWgBlocks = 256;   // target blocks per grouped launch (one per CU: LDS-bound)
+constexpr int kWgLdsBytes = 4 * 3 * 16 * (128 + 64) * 4;  // 3 slots per wave of the largest (I + O = 192)
+// ring depth: as many slots as the LDS holds, <= 8 (bytes in flight per CU = 4 (D - 1) slots:
+// the thin problems are HBM-bound and need the depth, the wide ones have the MFMA work)
+constexpr int wg_depth(int slot_floats) {
+  return kWgLdsBytes / (4 * slot_floats * 4) < 8 ? kWgLdsBytes / (4 * slot_floats * 4) : 8;
+}
+
+// NV consecutive floats NV m .. NV m + NV - 1 of row `row` of a glds_rows<CW> image (chunks
+// XOR-swizzled per row; NV = 1, 2, 4 or 8)
+template <int CW, int NV>
+__device__ __forceinline__ void lds_rowvec(const float* region, int row, int m, float (&v)[NV]) {
+  constexpr int CPR = CW / 4;
+  const int sw = row & (CPR - 1) & 15;
+  if constexpr (NV >= 4) {
+#pragma unroll
+    for (int h = 0; h < NV / 4; ++h) {
+      const int c = (NV / 4) * m + h;
+      const f32x4 u = *reinterpret_cast<const f32x4*>(region + 4 * (row * CPR + (c ^ sw)));
+      v[4 * h] = u[0]; v[4 * h + 1] = u[1]; v[4 * h + 2] = u[2]; v[4 * h + 3] = u[3];
+    }
+  } else {
+    const int c = (NV * m) >> 2, off = (NV * m) & 3;
+    const float* p = region + 4 * (row * CPR + (c ^ sw)) + off;
+    if constexpr (NV == 2) {
+      const float2 u = *reinterpret_cast<const float2*>(p);
+      v[0] = u.x; v[1] = u.y;
+    } else {
+      v[0] = p[0];
+    }
+  }
+}
+
+// 16 rows [row0, row0 + 16) of a channels-first operand (item b = row0 / N) into a [C][16] LDS image
+template <int C>
+__device__ __forceinline__ void glds_cf(const float* __restrict__ src, int64_t sb, int N, int64_t row0, float* lds_dst,
+                                        int lane) {
+  const int64_t b = row0 / N, n0 = row0 - b * N;
+#pragma unroll
+  for (int j = 0; j < C / 16; ++j) {
+    const int p = j * 64 + lane;
+    const int c = p >> 2, pos = p & 3;
+    const int ch = pos ^ ((c >> 2) & 3);
+    __builtin_amdgcn_global_load_lds(src + b * sb + (int64_t)c * N + n0 + 4 * ch,
+                                     (__attribute__((address_space(3))) void*)(lds_dst + j * 256), 16, 0, 0);
+  }
+}
+
+template <int LAYOUT, int TI, int TO>
+__device__ __forceinline__ void wgrad_glds_body(const WgradProblem& P, int s, float* lds) {
+  constexpr int I = 16 * TI, O = 16 * TO;
+  constexpr int SLOT = 16 * (I + O);        // floats
+  constexpr int G = I / 16 + O / 16;        // glds per tile
+  constexpr int kWgD = wg_depth(SLOT);
+  const int lane = pk::lane_id(), wv = pk::wave_id(), m = lane & 15, g = lane >> 4;
+  const int64_t r0 = (int64_t)s * P.SL;
+  const int64_t r1 = r0 + P.SL < P.R ? r0 + P.SL : P.R;
+  const int64_t ntile = (r1 - r0 + 15) >> 4;
+  const int64_t nt = ntile > wv ? (ntile - 1 - wv) / 4 + 1 : 0;  // tiles of this wave
+  const int64_t sbx = P.sbx ? P.sbx : (int64_t)I * P.N, sbdy = P.sbdy ? P.sbdy : (int64_t)O * P.N;
+  float* ring = lds + wv * kWgD * SLOT;
+  auto issue = [&](int64_t k) {  // glds of the wave's k-th tile (clamped: constant op count)
+    const int64_t kk = k < nt ? k : nt - 1;
+    const int64_t row0 = r0 + 16 * (wv + 4 * kk);
+    float* sl = ring + (k % kWgD) * SLOT;
+    if constexpr (LAYOUT == 0) {
+      glds_rows<I>(P.x, I, row0, P.R, I, sl, lane);
+      glds_rows<O>(P.dy, O, row0, P.R, O, sl + 16 * I, lane);
+    } else {
+      glds_cf<I>(P.x, sbx, P.N, row0, sl, lane);
+      glds_cf<O>(P.dy, sbdy, P.N, row0, sl + 16 * I, lane);
+    }
+  };
+  f32x4 acc[TO][TI];
+  float bs[TO];
+#pragma unroll
+  for (int t = 0; t < TO; ++t) {
+    bs[t] = 0.f;
+#pragma unroll
+    for (int u = 0; u < TI; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (nt > 0) {
+#pragma unroll
+    for (int k = 0; k < kWgD - 1; ++k) issue(k);
+    for (int64_t k = 0; k < nt; ++k) {
+      issue(k + kWgD - 1);
+      vm_wait((kWgD - 1) * G);  // tile k landed (glds retire in issue order)
+      const float* sx = ring + (k % kWgD) * SLOT;
+      const float* sd = sx + 16 * I;
+      if constexpr (LAYOUT == 0) {
+        const int64_t row0 = r0 + 16 * (wv + 4 * k);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = 4 * q + g;
+          float a[TO], b[TI];
+          lds_rowvec<O, TO>(sd, row, m, a);
+          lds_rowvec<I, TI>(sx, row, m, b);
+          const bool ok = row0 + row < P.R;  // clamped rows of a ragged last tile: dy = 0
+#pragma unroll
+          for (int t = 0; t < TO; ++t) {
+            a[t] = ok ? a[t] : 0.f;
+            bs[t] += a[t];
+          }
+#pragma unroll
+          for (int t = 0; t < TO; ++t)
+#pragma unroll
+            for (int u = 0; u < TI; ++u) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[u], acc[t][u], 0, 0, 0);
+        }
+      } else {
+        f32x4 a[TO], b[TI];
+#pragma unroll
+        for (int t = 0; t < TO; ++t) {
+          const int c = m + 16 * t;
+          a[t] = *reinterpret_cast<const f32x4*>(sd + 16 * c + 4 * (g ^ ((c >> 2) & 3)));
+          bs[t] += (a[t][0] + a[t][1]) + (a[t][2] + a[t][3]);
+        }
+#pragma unroll
+        for (int u = 0; u < TI; ++u) {
+          const int c = m + 16 * u;
+          b[u] = *reinterpret_cast<const f32x4*>(sx + 16 * c + 4 * (g ^ ((c >> 2) & 3)));
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int t = 0; t < TO; ++t)
+#pragma unroll
+            for (int u = 0; u < TI; ++u)
+              acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][q], b[u][q], acc[t][u], 0, 0, 0);
+      }
+    }
+  }
+  vm_wait(0);
+  // bias: the four row groups g of a channel, fixed order
+#pragma unroll
+  for (int t = 0; t < TO; ++t) {
+    bs[t] += __shfl_xor(bs[t], 16);
+    bs[t] += __shfl_xor(bs[t], 32);
+  }
+  __syncthreads();  // every wave is done with its ring: the LDS now holds waves 1..3's sums
+  constexpr int NA = TO * TI * 4;
+  if (wv > 0) {
+    float* dst = lds + (wv - 1) * (NA + TO) * 64;
+#pragma unroll
+    for (int t = 0; t < TO; ++t)
+#pragma unroll
+      for (int u = 0; u < TI; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[((t * TI + u) * 4 + r) * 64 + lane] = acc[t][u][r];
+#pragma unroll
+    for (int t = 0; t < TO; ++t) dst[(NA + t) * 64 + lane] = bs[t];
+  }
+  __syncthreads();
+  if (wv != 0) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    const float* src = lds + w * (NA + TO) * 64;
+#pragma unroll
+    for (int t = 0; t < TO; ++t) {
+#pragma unroll
+      for (int u = 0; u < TI; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[t][u][r] += src[((t * TI + u) * 4 + r) * 64 + lane];
+      bs[t] += src[(NA + t) * 64 + lane];
+    }
+  }
+  float* ps = P.part + (int64_t)s * O * I;
+  float* pb = P.part + (int64_t)P.S * O * I + (int64_t)s * O;
+#pragma unroll
+  for (int t = 0; t < TO; ++t) {
+#pragma unroll
+    for (int u = 0; u < TI; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ol = 4 * g + r;
+        const int o = LAYOUT == 0 ? TO * ol + t : ol + 16 * t;
+        const int i = LAYOUT == 0 ? TI * m + u : m + 16 * u;
+        ps[o * I + i] = acc[t][u][r];
+      }
+    if (g == 0) pb[LAYOUT == 0 ? TO * m + t : m + 16 * t] = bs[t];
+  }
+}
+
+// Shapes on the pipeline: I, O in {16, 32, 64, 128}, O I <= 8192 (the acc of one wave).
+__host__ __device__ constexpr int wg_shape_id(int I, int O) {
+  return (I == 16 || I == 32 || I == 64 || I == 128) && (O == 16 || O == 32 || O == 64 || O == 128) && I * O <= 8192
+             ? (I == 16 ? 0 : I == 32 ? 1 : I == 64 ? 2 : 3) * 4 + (O == 16 ? 0 : O == 32 ? 1 : O == 64 ? 2 : 3)
+             : -1;
+}
+
+template <int LAYOUT>
+__device__ __forceinline__ void wgrad_glds_dispatch(const WgradProblem& P, int s, float* lds) {
+  switch (wg_shape_id(P.I, P.O)) {
+#define PK_WG(I_, O_) case wg_shape_id(I_, O_): wgrad_glds_body<LAYOUT, I_ / 16, O_ / 16>(P, s, lds); break;
+    PK_WG(16, 16) PK_WG(16, 32) PK_WG(16, 64) PK_WG(16, 128)
+    PK_WG(32, 16) PK_WG(32, 32) PK_WG(32, 64) PK_WG(32, 128)
+    PK_WG(64, 16) PK_WG(64, 32) PK_WG(64, 64) PK_WG(64, 128)
+    PK_WG(128, 16) PK_WG(128, 32) PK_WG(128, 64)
+#undef PK_WG
+    default: break;
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void wgrad_glds_grouped_kernel(const WgradProblems tab) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int b = blockIdx.x;
+  int g = 0;
+  while (g + 1 < tab.G && b >= tab.p[g + 1].blk0) ++g;  // block-uniform scan
+  const WgradProblem& P = tab.p[g];
+  if (P.layout == 0) wgrad_glds_dispatch<0>(P, b - P.blk0, lds);
+  else wgrad_glds_dispatch<1>(P, b - P.blk0, lds);
+}
+
 // Channels-first layout (1) [Bn, C, N] with Cin in {16, 32, 64, 128}: one wave computes 16 SUB
 // consecutive points of one item x all outputs; tpc tiles per item (SUB > 1 needs N % (16 SUB)
 // == 0; with SUB = 1 an item's last tile may be ragged: its columns past N compute on a clamped
@@ -1746,15 +1979,58 @@ extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, 
   return pk_linear_ex(&a, stream);
 }
 
-extern "C" int64_t pk_linear_wgrad_grouped_work(const pk_wgrad_call* calls, int n) {
-  if (n < 0 || (n > 0 && calls == nullptr)) return -1;
-  int64_t tot = 0;
+// Slicing of a grouped call list. Pipeline problems (wgrad_glds_grouped_kernel: shape on
+// wg_shape_id, channels-first only with N % 16 == 0, 16-B aligned operands) get blocks in
+// proportion to their cost (wg_cost), about kWgBlocks in all (slices of whole 16-row tiles, >= 64
+// rows); the others keep round 3's wgrad_v2 slicing. S[c] partials of call c, SL[c] rows each.
+static bool wg_on_pipeline(const pk_wgrad_call& k) {
+#ifdef PK_DEVBUILD
+  static const bool on = getenv("PK_WG_GLDS") == nullptr || atoi(getenv("PK_WG_GLDS")) != 0;
+  if (!on) return false;
+#endif
+  return k.R > 0 && wg_shape_id(k.I, k.O) >= 0 && (k.layout == 0 || k.N % 16 == 0) &&
+         ((reinterpret_cast<uintptr_t>(k.x) | reinterpret_cast<uintptr_t>(k.dy)) & 15) == 0;
+}
+
+// a problem's time at the chip's rates, in HBM bytes: max(its bytes, its flops / (157.3 TF /
+// 8 TB/s)) — the thin layers are byte-bound, the 128 x 64 ones flop-bound
+static double wg_cost(const pk_wgrad_call& k) {
+  const double bytes = 4.0 * (double)k.R * (k.I + k.O), flops = 2.0 * (double)k.R * k.I * k.O;
+  return bytes > flops / 19.66 ? bytes : flops / 19.66;
+}
+
+static void wg_plan(const pk_wgrad_call* calls, int n, std::vector<int64_t>& S, std::vector<int64_t>& SL,
+                    std::vector<char>& glds) {
+  S.assign(n, 0);
+  SL.assign(n, 0);
+  glds.assign(n, 0);
+  double wtot = 0.0;
+  for (int c = 0; c < n; ++c)
+    if (wg_on_pipeline(calls[c])) wtot += wg_cost(calls[c]);
   for (int c = 0; c < n; ++c) {
     const pk_wgrad_call& k = calls[c];
     if (k.R <= 0) continue;
-    const int64_t S = (k.R + grouped_slice_rows(k.R) - 1) / grouped_slice_rows(k.R);
-    tot += S * ((int64_t)k.O * k.I + k.O);
+    if (wg_on_pipeline(k)) {
+      glds[c] = 1;
+      const double share = wg_cost(k) / wtot * kWgBlocks;
+      int64_t nb = (int64_t)(share + 0.5);
+      const int64_t cap = (k.R + 63) / 64;
+      nb = nb < 1 ? 1 : nb > cap ? cap : nb;
+      SL[c] = ((k.R + nb - 1) / nb + 15) / 16 * 16;
+    } else {
+      SL[c] = grouped_slice_rows(k.R);
+    }
+    S[c] = (k.R + SL[c] - 1) / SL[c];
   }
+}
+
+extern "C" int64_t pk_linear_wgrad_grouped_work(const pk_wgrad_call* calls, int n) {
+  if (n < 0 || (n > 0 && calls == nullptr)) return -1;
+  std::vector<int64_t> S, SL;
+  std::vector<char> glds;
+  wg_plan(calls, n, S, SL, glds);
+  int64_t tot = 0;
+  for (int c = 0; c < n; ++c) tot += S[c] * ((int64_t)calls[c].O * calls[c].I + calls[c].O);
   return tot;
 }
 
@@ -1782,15 +2058,40 @@ extern "C" int pk_linear_wgrad_grouped(const pk_wgrad_call* calls, int n, float*
   }
   const int64_t need = pk_linear_wgrad_grouped_work(calls, n);
   PK_REQUIRE(need <= work_elems && (need == 0 || work != nullptr));
-  std::vector<int64_t> S(n, 0), SLv(n, 0), off(n, 0);
+  std::vector<int64_t> S, SLv, off(n, 0);
+  std::vector<char> glds;
+  wg_plan(calls, n, S, SLv, glds);
   int64_t o = 0;
   for (int c = 0; c < n; ++c) {
-    const pk_wgrad_call& k = calls[c];
-    if (k.R <= 0) continue;
-    SLv[c] = grouped_slice_rows(k.R);
-    S[c] = (k.R + SLv[c] - 1) / SLv[c];
     off[c] = o;
-    o += S[c] * ((int64_t)k.O * k.I + k.O);
+    o += S[c] * ((int64_t)calls[c].O * calls[c].I + calls[c].O);
+  }
+  // pipeline partials: chunks of <= kGroupMax problems
+  {
+    WgradProblems tp{};
+    int blocks = 0;
+    auto flush = [&]() -> int {
+      if (tp.G == 0) return PK_OK;
+      hipLaunchKernelGGL(wgrad_glds_grouped_kernel, dim3(blocks), dim3(256), kWgLdsBytes, st, tp);
+      PK_CHECK_LAUNCH();
+      tp.G = 0;
+      blocks = 0;
+      return PK_OK;
+    };
+    for (int c = 0; c < n; ++c) {
+      const pk_wgrad_call& k = calls[c];
+      if (S[c] == 0 || !glds[c]) continue;
+      WgradProblem& P = tp.p[tp.G++];
+      P = WgradProblem{k.x, k.dy, work + off[c], k.R, k.I, k.O, k.N, k.layout, (int)SLv[c], (int)S[c], blocks, 0,
+                       k.sx, k.sdy};
+      blocks += (int)S[c];
+      if (tp.G == kGroupMax) {
+        const int rc = flush();
+        if (rc != PK_OK) return rc;
+      }
+    }
+    const int rc = flush();
+    if (rc != PK_OK) return rc;
   }
   // partials: chunks of <= kGroupMax problems
   WgradProblems tp{};
@@ -1805,7 +2106,7 @@ extern "C" int pk_linear_wgrad_grouped(const pk_wgrad_call* calls, int n, float*
   };
   for (int c = 0; c < n; ++c) {
     const pk_wgrad_call& k = calls[c];
-    if (S[c] == 0) continue;
+    if (S[c] == 0 || glds[c]) continue;
     WgradProblem& P = tp.p[tp.G++];
     P = WgradProblem{k.x, k.dy, work + off[c], k.R, k.I, k.O, k.N, k.layout, (int)SLv[c], (int)S[c], blocks, 0,
                      k.sx, k.sdy};

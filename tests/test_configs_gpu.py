@@ -111,9 +111,10 @@ def test_rigidity_filter_configs(device, V2):
 
 def test_rigidity_filter_ragged_batch(device):
     """Crops with different candidate counts in one launch (empty, single, tile-edge ±1 of the
-    128-entry pair tiles, and a 2-tile-plus crop): each crop's survivors vs the oracle."""
+    128-entry pair tiles and of the first round's 160-entry group tiles, partial last groups,
+    and a multi-tile crop): each crop's survivors vs the oracle."""
     from dpfm_amd import ops
-    sizes = [0, 1, 127, 129, 640, 1000]
+    sizes = [0, 1, 127, 129, 159, 161, 322, 640, 1000]
     scenes = [_rigid_scene(max((s + 4) // 5, 1), 7 + i) for i, s in enumerate(sizes)]
     Lc = max(sizes)
     cand = np.zeros((len(sizes), Lc, 2), dtype=np.int64)
@@ -134,6 +135,26 @@ def test_rigidity_filter_ragged_batch(device):
         if s == 0:
             continue
         _rigidity_parity(sc[0], sc[1], sc[2][:s], rows[i], int(n[i]), sc[3])
+
+
+@pytest.mark.parametrize("order", ["shuffled", "one_split_group"])
+def test_rigidity_filter_candidate_orders(device, order):
+    """The first round shares one crop distance per pair of 5-candidate groups (nn_query's
+    pc-major order, spacial_filtering.py:36-38); candidate lists in another order take the
+    general pair form tile by tile. Shuffled: every tile general; one split group: one group's
+    members point at two crop points, so only the tile pairs touching it are general."""
+    from dpfm_amd import ops
+    cad, pc, cand, diam = _rigid_scene(400, 23)
+    cand = cand.copy()
+    if order == "shuffled":
+        cand = cand[np.random.default_rng(5).permutation(cand.shape[0])]
+    else:
+        cand[5 * 37 + 2, 1] = (cand[5 * 37 + 2, 1] + 1) % 400
+    thr = ops.rigidity_thresholds([diam], device)
+    rows, n = ops.rigidity_filter(torch.from_numpy(cand)[None].to(device),
+                                  torch.tensor([cand.shape[0]], dtype=torch.int32, device=device),
+                                  torch.from_numpy(cad)[None].to(device), torch.from_numpy(pc)[None].to(device), thr)
+    _rigidity_parity(cad, pc, cand, rows[0].cpu().numpy(), int(n[0]), diam)
 
 
 def test_ransac_configs4(device, coracle):

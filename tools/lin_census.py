@@ -12,6 +12,9 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from dpfm_amd import _lib, ops  # noqa: E402
 
+if os.environ.get("PK_DEV") == "1":  # libposekern_dev.so (its PK_* switches, e.g. PK_WG_GLDS=0)
+    _lib.use_dev_lib()
+
 sys.argv = ["bench.py"]
 args = bench.parse()
 dev = torch.device("cuda:0")
@@ -39,6 +42,17 @@ def rec(x, w, bias, layout, R, N, Cin, Cout, y, **kw):
 
 ops.linear_ex = rec
 times = []
+wcalls = []
+orig_w = ops.linear_wgrad_grouped
+
+
+def rec_w(cl):
+    wcalls.append([("cf", tuple(x.shape), dy.shape[1]) if cf else ("cl", x.numel() // x.shape[-1], x.shape[-1],
+                   dy.shape[-1]) for (x, dy, cf, dw, db, acc) in cl])
+    return orig_w(cl)
+
+
+ops.linear_wgrad_grouped = rec_w
 
 
 def hook(name, fn, work=None):
@@ -48,12 +62,17 @@ def hook(name, fn, work=None):
     e.record()
     if name == "pk_linear_ex":
         times.append((s, e, work))
+    if name == "pk_linear_wgrad_grouped":
+        wtimes.append((s, e, work))
     return r
 
 
+wtimes = []
 for rep in range(2):
     calls.clear()
     times.clear()
+    wcalls.clear()
+    wtimes.clear()
     _lib.set_probe(hook)
     torch.cuda.synchronize()
     torch.cuda._sleep(int(2.5e8))
@@ -72,3 +91,9 @@ print(f"{len(calls)} pk_linear_ex calls, {tot:.1f} us per step")
 for k, (n, us, byts) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
     print(f"{str(k):60s} n={n:2d} {us / n:6.1f} us/call {us:7.1f} us total  {byts / n / 1e6:6.2f} MB/call "
           f"{byts / (us * 1e-6) / 1e9:6.0f} GB/s")
+
+for cl, (s, e, w) in zip(wcalls, wtimes):
+    rows = collections.Counter(map(tuple, cl))
+    print(f"pk_linear_wgrad_grouped: {len(cl)} calls, {s.elapsed_time(e) * 1e3:.1f} us, {w[1] / 1e9:.2f} GFLOP")
+    for k, n in sorted(rows.items(), key=lambda kv: str(kv[0])):
+        print(f"   {str(k):50s} x{n}")
