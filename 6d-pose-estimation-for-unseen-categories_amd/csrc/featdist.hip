@@ -1278,6 +1278,11 @@ __global__ __launch_bounds__(64 * NW, 2) void fd_cols_kernel(
 // handed-off byte is stored and loaded sc1, cdna_hip_programming.md §6 Guideline 16), keeps the
 // smallest (value, then row) and resets the ticket (zero before the first launch on the buffer,
 // zero after every launch).
+__device__ __forceinline__ int med3i(int a, int b, int c) {  // v_med3_i32: the median of three
+  int d;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
 constexpr int kWideCT = 8;
 constexpr int kWideChunk = 8;
 
@@ -1306,6 +1311,10 @@ __global__ __launch_bounds__(256, 2) void fd_wide_kernel(
     }
   }
   const int cg = k % NCG, rs = k / NCG;
+  if constexpr (VAR == 7) {  // (development variant: an AGPR operand in the kernel, so the
+    float z = 0.f;           // MFMAs are selected in their AGPR-accumulator form)
+    asm volatile("; agpr %0" ::"a"(z));
+  }
   const int lane = pk::lane_id(), w = __builtin_amdgcn_readfirstlane(pk::wave_id());
   const int g = lane >> 4, c16 = lane & 15;
   const int N1 = n1[b], N2 = n2[b];
@@ -1413,23 +1422,35 @@ __global__ __launch_bounds__(256, 2) void fd_wide_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int c = 4 * grp + cc;
+        if constexpr (VAR == 9) {  // (development variant: value only, one v_med3_i32)
+          bk[c][r] = med3i(__float_as_int(acc[cc][r]), kClamp, bk[c][r]);
+          continue;
+        }
+        if constexpr (VAR == 8) {  // (development variant: clamp + min in one v_med3_i32)
+          const int nb = med3i(__float_as_int(acc[cc][r]), kClamp, bk[c][r]);  // bk >= kClamp
+          bt[c][r] = nb < bk[c][r] ? tt : bt[c][r];
+          bk[c][r] = nb;
+          continue;
+        }
         const int key = max(__float_as_int(acc[cc][r]), kClamp);
         if constexpr (VAR == 5) {  // (development variant: the value only, no row index)
           bk[c][r] = min(key, bk[c][r]);
           continue;
         }
-        if constexpr (VAR == 6) {  // (development variant: the compiler's compare + select)
-          bt[c][r] = key < bk[c][r] ? tt : bt[c][r];
+        if constexpr (VAR == 6) {  // (development variant: round 4's integer select; the asm
+          int dif = key - bk[c][r];  // hides the difference's range, else LLVM rewrites it as
+          asm volatile("" : "+v"(dif));  // the compare + select below)
+          int m = dif >> 31;  // -1 iff key < best (both keys in [kClamp, 0x7f800000])
+          asm volatile("" : "+v"(m));
+          bt[c][r] = (m & tt) | (~m & bt[c][r]);
           bk[c][r] = min(key, bk[c][r]);
           continue;
         }
-        int dif = key - bk[c][r];
-        // (the empty asm hides the difference's range: the compiler would rewrite the sign mask
-        // as a v_cmp + v_cndmask pair through VCC, with hazard s_nops, a serial chain per distance)
-        asm volatile("" : "+v"(dif));
-        int m = dif >> 31;  // -1 iff key < best (both keys in [kClamp, 0x7f800000])
-        asm volatile("" : "+v"(m));  // (and the mask's: else select(dif < 0, ...) again)
-        bt[c][r] = (m & tt) | (~m & bt[c][r]);
+        // compare + select (v_cmp into an SGPR pair, v_cndmask): 5 % faster than the integer
+        // select (VAR 6) — on gfx950 the f32 MFMAs never co-execute with VALU work
+        // (SQ_VALU_MFMA_COEXEC_CYCLES = 0 on this kernel), so every selection instruction adds
+        // to the MFMA time; see DESIGN.md §5 'Feature distance'
+        bt[c][r] = key < bk[c][r] ? tt : bt[c][r];
         bk[c][r] = min(key, bk[c][r]);
       }
   };
@@ -1733,14 +1754,15 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
     const dim3 wgrid((unsigned)((int64_t)B * wp.NCG * wp.RS));
 #ifdef PK_DEVBUILD
     static const int wvar = [] {  // development knob PK_FD_VAR: 1 no selection, 2 no MFMAs, 3 neither,
-      // 4 no sched_group_barrier, 5 value-only selection, 6 compare + select
+      // 4 no sched_group_barrier, 5 value-only selection, 6 integer select, 7 AGPR accumulators,
+      // 8 med3 + compare + select, 9 value-only med3
       const char* e = std::getenv("PK_FD_VAR");
       return e ? std::atoi(e) : 0;
     }();
 #define PK_FDW(V) hipLaunchKernelGGL((fd_wide_kernel<kWideCT, V>), wgrid, dim3(256), 0, s, evecs_x, ldx, C, evecs_y, \
                                      ldy, n1, n2, V1max, V2max, wp.NCG, wp.RS, out_idx, out_dist, part, arrivals)
     if (wvar == 1) PK_FDW(1); else if (wvar == 2) PK_FDW(2); else if (wvar == 3) PK_FDW(3);
-    else if (wvar == 4) PK_FDW(4); else if (wvar == 5) PK_FDW(5); else if (wvar == 6) PK_FDW(6); else PK_FDW(0);
+    else if (wvar == 4) PK_FDW(4); else if (wvar == 5) PK_FDW(5); else if (wvar == 6) PK_FDW(6); else if (wvar == 7) PK_FDW(7); else if (wvar == 8) PK_FDW(8); else if (wvar == 9) PK_FDW(9); else PK_FDW(0);
 #undef PK_FDW
 #else
     hipLaunchKernelGGL(fd_wide_kernel<kWideCT>, wgrid, dim3(256), 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, n2, V1max,

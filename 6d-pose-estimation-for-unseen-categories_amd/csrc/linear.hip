@@ -1048,6 +1048,45 @@ __device__ __forceinline__ f32x4 lds_chunk(const float* region, int row, int c) 
   return *reinterpret_cast<const f32x4*>(region + 4 * (row * CPR + (c ^ (row & (CPR - 1) & 15))));
 }
 
+// Per-lane float offsets of the 16-B chunks of a glds_rows<CW> image within one 16-row block (row
+// stride ld, columns >= cols_ok at column 0), computed once: a tile whose 16 rows are all in range
+// is then issued from a scalar base (glds_issue16) without per-lane 64-bit address arithmetic,
+// which on gfx950 would be VALU work serialised with the f32 MFMAs.
+template <int CW>
+__device__ __forceinline__ void glds_rows_off(int64_t ld, int cols_ok, int lane, int (&off)[CW / 16]) {
+  constexpr int CPR = CW / 4;
+#pragma unroll
+  for (int j = 0; j < CW / 16; ++j) {
+    const int p = j * 64 + lane;
+    const int row = p / CPR, cl = p % CPR;
+    const int c = cl ^ (row & (CPR - 1) & 15);
+    off[j] = (int)(row * ld) + (4 * c < cols_ok ? 4 * c : 0);
+  }
+}
+
+// the same for a glds_cf<C> image: chunk (c, pos) holds floats 4 (pos ^ ((c >> 2) & 3)) .. + 3
+// of channel c (channel stride N)
+template <int C>
+__device__ __forceinline__ void glds_cf_off(int N, int lane, int (&off)[C / 16]) {
+#pragma unroll
+  for (int j = 0; j < C / 16; ++j) {
+    const int p = j * 64 + lane;
+    const int c = p >> 2, pos = p & 3;
+    off[j] = c * N + 4 * (pos ^ ((c >> 2) & 3));
+  }
+}
+
+template <int NI, int BYTES>
+__device__ __forceinline__ void glds_issue(const float* base, const int* off, float* lds_dst) {  // off[NI]
+  static_assert(BYTES == 16 || BYTES == 4, "glds piece");
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    auto* d = (__attribute__((address_space(3))) void*)(lds_dst + j * BYTES * 16);
+    if constexpr (BYTES == 16) __builtin_amdgcn_global_load_lds(base + off[j], d, 16, 0, 0);
+    else __builtin_amdgcn_global_load_lds(base + off[j], d, 4, 0, 0);
+  }
+}
+
 template <int Q, int TO, bool MASK, bool ADD, bool SPLIT>
 __global__ __launch_bounds__(256, 1) void linear_glds_rows_kernel(const float* __restrict__ x, int64_t sx,
                                                                   const float* __restrict__ w,
@@ -1082,12 +1121,24 @@ __global__ __launch_bounds__(256, 1) void linear_glds_rows_kernel(const float* _
   const int64_t t0 = (int64_t)blockIdx.x * 4 + wv;
   if (t0 >= T) return;
   const int64_t nt = (T - 1 - t0) / stride + 1;  // tiles of this wave
+  // lane offsets of the glds chunks, computed once (a full tile is then issued from a scalar base)
+  int offx[Q], offm[MASK ? TO : 1], offa[ADD ? TO : 1];
+  glds_rows_off<CI>(sx, CI, lane, offx);
+  if constexpr (MASK) glds_rows_off<CO>(Cout, Cout, lane, offm);
+  if constexpr (ADD) glds_rows_off<CO>(e.sa, e.add_cols, lane, offa);
   auto issue = [&](int64_t k) {  // glds of this wave's k-th tile (clamped: constant op count)
     const int64_t tile = t0 + min(k, nt - 1) * stride;
     float* s = ring + (k % D) * SLOT;
-    glds_rows<CI>(x, sx, tile * 16, R, CI, s, lane);
-    if constexpr (MASK) glds_rows<CO>(e.mask, Cout, tile * 16, R, Cout, s + 16 * CI, lane);
-    if constexpr (ADD) glds_rows<CO>(e.add, e.sa, tile * 16, R, e.add_cols, s + 16 * CI + (MASK ? 16 * CO : 0), lane);
+    const int64_t r0 = tile * 16;
+    if (r0 + 16 <= R) {  // (wave-uniform) every row in range
+      glds_issue<Q, 16>(x + r0 * sx, offx, s);
+      if constexpr (MASK) glds_issue<TO, 16>(e.mask + r0 * Cout, offm, s + 16 * CI);
+      if constexpr (ADD) glds_issue<TO, 16>(e.add + r0 * e.sa, offa, s + 16 * CI + (MASK ? 16 * CO : 0));
+    } else {
+      glds_rows<CI>(x, sx, r0, R, CI, s, lane);
+      if constexpr (MASK) glds_rows<CO>(e.mask, Cout, r0, R, Cout, s + 16 * CI, lane);
+      if constexpr (ADD) glds_rows<CO>(e.add, e.sa, r0, R, e.add_cols, s + 16 * CI + (MASK ? 16 * CO : 0), lane);
+    }
   };
 #pragma unroll
   for (int k = 0; k < D - 1; ++k) issue(k);
@@ -1209,11 +1260,30 @@ __device__ __forceinline__ void glds_cf(const float* __restrict__ src, int64_t s
   }
 }
 
-template <int LAYOUT, int TI, int TO>
+// Rows [row0, row0 + 16) of a thin rows-layout operand (C < 16 channels: 16 C contiguous
+// floats) by 4-byte glds, lane p taking float p (indices clamped to the tensor: a ragged last
+// tile reads valid memory, its rows past R are masked at use): ceil(16 C / 64) instructions.
+template <int C>
+__device__ __forceinline__ void glds_thin(const float* __restrict__ src, int64_t row0, int64_t R, float* lds_dst,
+                                          int lane) {
+#pragma unroll
+  for (int j = 0; j < (16 * C + 63) / 64; ++j) {
+    const int64_t idx = min(row0 * C + j * 64 + lane, R * C - 1);
+    __builtin_amdgcn_global_load_lds(src + idx, (__attribute__((address_space(3))) void*)(lds_dst + j * 64), 4, 0,
+                                     0);
+  }
+}
+
+// XT / DT > 0: x (dy) is a thin rows-layout operand of XT (DT) < 16 channels (TI = 1 / TO = 1):
+// the input layer 3 -> 64 and the 32 -> 1 heads; lanes m >= XT (DT) feed zeros.
+template <int LAYOUT, int TI, int TO, int XT = 0, int DT = 0>
 __device__ __forceinline__ void wgrad_glds_body(const WgradProblem& P, int s, float* lds) {
+  static_assert((XT == 0 || (TI == 1 && LAYOUT == 0)) && (DT == 0 || (TO == 1 && LAYOUT == 0)), "thin operands");
   constexpr int I = 16 * TI, O = 16 * TO;
-  constexpr int SLOT = 16 * (I + O);        // floats
-  constexpr int G = I / 16 + O / 16;        // glds per tile
+  constexpr int XS = XT ? 64 * ((16 * XT + 63) / 64) : 16 * I;  // slot floats of the x rows
+  constexpr int DS = DT ? 64 * ((16 * DT + 63) / 64) : 16 * O;  // and of the dy rows
+  constexpr int SLOT = XS + DS;
+  constexpr int G = (XT ? (16 * XT + 63) / 64 : I / 16) + (DT ? (16 * DT + 63) / 64 : O / 16);  // glds per tile
   constexpr int kWgD = wg_depth(SLOT);
   const int lane = pk::lane_id(), wv = pk::wave_id(), m = lane & 15, g = lane >> 4;
   const int64_t r0 = (int64_t)s * P.SL;
@@ -1222,16 +1292,61 @@ __device__ __forceinline__ void wgrad_glds_body(const WgradProblem& P, int s, fl
   const int64_t nt = ntile > wv ? (ntile - 1 - wv) / 4 + 1 : 0;  // tiles of this wave
   const int64_t sbx = P.sbx ? P.sbx : (int64_t)I * P.N, sbdy = P.sbdy ? P.sbdy : (int64_t)O * P.N;
   float* ring = lds + wv * kWgD * SLOT;
-  auto issue = [&](int64_t k) {  // glds of the wave's k-th tile (clamped: constant op count)
-    const int64_t kk = k < nt ? k : nt - 1;
-    const int64_t row0 = r0 + 16 * (wv + 4 * kk);
-    float* sl = ring + (k % kWgD) * SLOT;
-    if constexpr (LAYOUT == 0) {
-      glds_rows<I>(P.x, I, row0, P.R, I, sl, lane);
-      glds_rows<O>(P.dy, O, row0, P.R, O, sl + 16 * I, lane);
+  constexpr int NX = XT ? (16 * XT + 63) / 64 : I / 16, ND = DT ? (16 * DT + 63) / 64 : O / 16;
+  int offx[NX], offd[ND];  // lane offsets of the glds chunks (4-B pieces for a thin operand)
+  if constexpr (LAYOUT == 0) {
+    if constexpr (XT > 0) {
+#pragma unroll
+      for (int j = 0; j < NX; ++j) offx[j] = j * 64 + lane;
     } else {
-      glds_cf<I>(P.x, sbx, P.N, row0, sl, lane);
-      glds_cf<O>(P.dy, sbdy, P.N, row0, sl + 16 * I, lane);
+      glds_rows_off<I>(I, I, lane, offx);
+    }
+    if constexpr (DT > 0) {
+#pragma unroll
+      for (int j = 0; j < ND; ++j) offd[j] = j * 64 + lane;
+    } else {
+      glds_rows_off<O>(O, O, lane, offd);
+    }
+  } else {
+    glds_cf_off<I>(P.N, lane, offx);
+    glds_cf_off<O>(P.N, lane, offd);
+  }
+  // channels-first issue cursor: item cb, first point cn of the next tile to issue (tiles of a
+  // wave step by 64 rows; N % 16 == 0, so a 16-row tile never straddles two items)
+  int64_t cb = 0, cn = 0, lb = 0, ln = 0, lrow = 0;
+  if constexpr (LAYOUT == 1) {
+    const int64_t rs = r0 + 16 * wv;
+    cb = rs / P.N;
+    cn = rs - cb * P.N;
+  }
+  auto issue = [&](int64_t k) {  // glds of the wave's k-th tile (clamped: constant op count)
+    float* sl = ring + (k % kWgD) * SLOT;
+    if (k < nt) {
+      lrow = r0 + 16 * (wv + 4 * k);
+      if constexpr (LAYOUT == 1) {
+        lb = cb;
+        ln = cn;
+        cn += 64;
+        while (cn >= P.N) {
+          cn -= P.N;
+          ++cb;
+        }
+      }
+    }
+    const int64_t row0 = lrow;
+    if constexpr (LAYOUT == 0) {
+      if (row0 + 16 <= P.R) {  // (wave-uniform) all rows in range: scalar base + lane offsets
+        glds_issue<NX, XT ? 4 : 16>(P.x + row0 * (XT ? XT : I), offx, sl);
+        glds_issue<ND, DT ? 4 : 16>(P.dy + row0 * (DT ? DT : O), offd, sl + XS);
+      } else {
+        if constexpr (XT > 0) glds_thin<XT>(P.x, row0, P.R, sl, lane);
+        else glds_rows<I>(P.x, I, row0, P.R, I, sl, lane);
+        if constexpr (DT > 0) glds_thin<DT>(P.dy, row0, P.R, sl + XS, lane);
+        else glds_rows<O>(P.dy, O, row0, P.R, O, sl + XS, lane);
+      }
+    } else {
+      glds_issue<NX, 16>(P.x + lb * sbx + ln, offx, sl);
+      glds_issue<ND, 16>(P.dy + lb * sbdy + ln, offd, sl + XS);
     }
   };
   f32x4 acc[TO][TI];
@@ -1249,21 +1364,24 @@ __device__ __forceinline__ void wgrad_glds_body(const WgradProblem& P, int s, fl
       issue(k + kWgD - 1);
       vm_wait((kWgD - 1) * G);  // tile k landed (glds retire in issue order)
       const float* sx = ring + (k % kWgD) * SLOT;
-      const float* sd = sx + 16 * I;
+      const float* sd = sx + XS;
       if constexpr (LAYOUT == 0) {
         const int64_t row0 = r0 + 16 * (wv + 4 * k);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int row = 4 * q + g;
           float a[TO], b[TI];
-          lds_rowvec<O, TO>(sd, row, m, a);
-          lds_rowvec<I, TI>(sx, row, m, b);
-          const bool ok = row0 + row < P.R;  // clamped rows of a ragged last tile: dy = 0
+          if constexpr (DT > 0) a[0] = m < DT ? sd[row * DT + m] : 0.f;
+          else lds_rowvec<O, TO>(sd, row, m, a);
+          if constexpr (XT > 0) b[0] = m < XT ? sx[row * XT + m] : 0.f;
+          else lds_rowvec<I, TI>(sx, row, m, b);
+          if (row0 + 16 > P.R) {  // (wave-uniform) clamped rows of a ragged last tile: dy = 0
+            const bool ok = row0 + row < P.R;
 #pragma unroll
-          for (int t = 0; t < TO; ++t) {
-            a[t] = ok ? a[t] : 0.f;
-            bs[t] += a[t];
+            for (int t = 0; t < TO; ++t) a[t] = ok ? a[t] : 0.f;
           }
+#pragma unroll
+          for (int t = 0; t < TO; ++t) bs[t] += a[t];
 #pragma unroll
           for (int t = 0; t < TO; ++t)
 #pragma unroll
@@ -1326,8 +1444,8 @@ __device__ __forceinline__ void wgrad_glds_body(const WgradProblem& P, int s, fl
       bs[t] += src[(NA + t) * 64 + lane];
     }
   }
-  float* ps = P.part + (int64_t)s * O * I;
-  float* pb = P.part + (int64_t)P.S * O * I + (int64_t)s * O;
+  float* ps = P.part + (int64_t)s * P.O * P.I;
+  float* pb = P.part + (int64_t)P.S * P.O * P.I + (int64_t)s * P.O;
 #pragma unroll
   for (int t = 0; t < TO; ++t) {
 #pragma unroll
@@ -1337,28 +1455,39 @@ __device__ __forceinline__ void wgrad_glds_body(const WgradProblem& P, int s, fl
         const int ol = 4 * g + r;
         const int o = LAYOUT == 0 ? TO * ol + t : ol + 16 * t;
         const int i = LAYOUT == 0 ? TI * m + u : m + 16 * u;
-        ps[o * I + i] = acc[t][u][r];
+        if ((XT == 0 || i < XT) && (DT == 0 || o < DT)) ps[o * P.I + i] = acc[t][u][r];
       }
-    if (g == 0) pb[LAYOUT == 0 ? TO * m + t : m + 16 * t] = bs[t];
+    const int ob = LAYOUT == 0 ? TO * m + t : m + 16 * t;
+    if (g == 0 && (DT == 0 || ob < DT)) pb[ob] = bs[t];
   }
 }
 
-// Shapes on the pipeline: I, O in {16, 32, 64, 128}, O I <= 8192 (the acc of one wave).
-__host__ __device__ constexpr int wg_shape_id(int I, int O) {
+// Shapes on the pipeline: I, O in {16, 32, 64, 128}, O I <= 8192 (the acc of one wave), and the
+// thin rows-layout shapes below.
+// Thin rows-layout shapes (the step's 3 -> 64 input layer and 32 -> 1 heads): ids 16, 17.
+__host__ __device__ constexpr int wg_shape_id(int I, int O, int layout = 0) {
   return (I == 16 || I == 32 || I == 64 || I == 128) && (O == 16 || O == 32 || O == 64 || O == 128) && I * O <= 8192
              ? (I == 16 ? 0 : I == 32 ? 1 : I == 64 ? 2 : 3) * 4 + (O == 16 ? 0 : O == 32 ? 1 : O == 64 ? 2 : 3)
-             : -1;
+         : layout == 0 && I == 3 && O == 64 ? 16
+         : layout == 0 && I == 32 && O == 1 ? 17
+                                            : -1;
 }
 
 template <int LAYOUT>
 __device__ __forceinline__ void wgrad_glds_dispatch(const WgradProblem& P, int s, float* lds) {
-  switch (wg_shape_id(P.I, P.O)) {
+  switch (wg_shape_id(P.I, P.O, LAYOUT)) {
 #define PK_WG(I_, O_) case wg_shape_id(I_, O_): wgrad_glds_body<LAYOUT, I_ / 16, O_ / 16>(P, s, lds); break;
     PK_WG(16, 16) PK_WG(16, 32) PK_WG(16, 64) PK_WG(16, 128)
     PK_WG(32, 16) PK_WG(32, 32) PK_WG(32, 64) PK_WG(32, 128)
     PK_WG(64, 16) PK_WG(64, 32) PK_WG(64, 64) PK_WG(64, 128)
     PK_WG(128, 16) PK_WG(128, 32) PK_WG(128, 64)
 #undef PK_WG
+    case 16:
+      if constexpr (LAYOUT == 0) wgrad_glds_body<0, 1, 4, 3, 0>(P, s, lds);
+      break;
+    case 17:
+      if constexpr (LAYOUT == 0) wgrad_glds_body<0, 2, 1, 0, 1>(P, s, lds);
+      break;
     default: break;
   }
 }
@@ -1988,7 +2117,7 @@ static bool wg_on_pipeline(const pk_wgrad_call& k) {
   static const bool on = getenv("PK_WG_GLDS") == nullptr || atoi(getenv("PK_WG_GLDS")) != 0;
   if (!on) return false;
 #endif
-  return k.R > 0 && wg_shape_id(k.I, k.O) >= 0 && (k.layout == 0 || k.N % 16 == 0) &&
+  return k.R > 0 && wg_shape_id(k.I, k.O, k.layout) >= 0 && (k.layout == 0 || k.N % 16 == 0) &&
          ((reinterpret_cast<uintptr_t>(k.x) | reinterpret_cast<uintptr_t>(k.dy)) & 15) == 0;
 }
 

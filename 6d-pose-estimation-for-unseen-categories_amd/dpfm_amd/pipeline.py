@@ -624,6 +624,12 @@ class InferStep:
 
     @torch.no_grad()
     def __call__(self, fb: FrameBatch, op: Operators, crops: Crops):
+        return self.pose_stage(fb, op, crops, self.model_stage(fb, op, crops))
+
+    @torch.no_grad()
+    def model_stage(self, fb: FrameBatch, op: Operators, crops: Crops) -> dict:
+        """DPFMNet forward and the naive solver's top-5 candidates (eval.py:80-87,
+        spacial_filtering.py:32-38): the MFMA-bound first half of the step."""
         self.model.eval()
         C_pred, o12, o21, f1, f2, _, _ = self.model(model_batch(op, crops))
         B, V1, _ = op.cad_evecs.shape
@@ -635,7 +641,16 @@ class InferStep:
         top, _ = ops.feat_dist_topk(op.cad_evecs, C_pred, op.pc_evecs, n1, n2, 5)      # spacial_filtering.py:32-38
         cand = torch.stack([top.reshape(B, -1),
                             torch.arange(V2, device=dev)[None, :, None].expand(B, V2, 5).reshape(B, -1)], -1)
-        ncand = 5 * n2
+        return dict(C=C_pred, cand=cand, ncand=5 * n2)
+
+    @torch.no_grad()
+    def pose_stage(self, fb: FrameBatch, op: Operators, crops: Crops, m: dict) -> dict:
+        """Rigidity filter, IR, RANSAC and the pose metrics (spacial_filtering.py:42-75,
+        eval.py:89, test_RANSAC.py): the VALU-bound second half of the step."""
+        C_pred, cand, ncand = m["C"], m["cand"], m["ncand"]
+        B, V1, _ = op.cad_evecs.shape
+        V2 = op.pc_evecs.shape[1]
+        dev = C_pred.device
         rows, nsurv = ops.rigidity_filter(cand, ncand, op.cad_xyz, crops.pc32, op.rig_thr)  # :42-75
         p_pred = torch.gather(cand, 1, rows[..., None].expand(-1, -1, 2))                  # [B, L, 2]
         ir = ops.inlier_ratio(p_pred, nsurv, op.cad_xyz, crops.align32, op.ir_thr, layout=0)  # eval.py:89
@@ -700,15 +715,25 @@ class PipelinedInfer:
     InferStep on buffer k on the main stream; events order C_k after I_k's previous use of the
     buffer and I_k after C_k. Crop formation (FPS, SOR: one workgroup per crop, latency-bound)
     then hides under the model, the correspondence head and RANSAC (wide kernels). Each call
-    returns the static outputs of the graph it replayed (overwritten two calls later)."""
+    returns the static outputs of the graph it replayed (overwritten two calls later).
+
+    stages=3 also splits InferStep at the candidates: M_k (model forward + top-5, MFMA-bound,
+    many small launches) of batch i runs on the main stream while P_k (rigidity filter, IR,
+    RANSAC, metrics: VALU-bound wide launches) of batch i-1 runs on a third stream, with three
+    crop buffers (formation i+1, model i, pose i-1 in flight at once). Call i then returns the
+    outputs of batch i-1 (None on the first call; flush() runs the last pending pose stage)."""
 
     def __init__(self, crop_formation: CropFormation, infer: InferStep, fb: FrameBatch, op: Operators,
-                 warmup: int = 2, side_cus: int = 0):
+                 warmup: int = 2, side_cus: int = 0, stages: int = 2):
+        if stages not in (2, 3):
+            raise ValueError("PipelinedInfer: stages must be 2 or 3")
+        self.stages = stages
         self.main = torch.cuda.current_stream()
         self.side = torch.cuda.Stream()
         if side_cus > 0:  # disjoint CU sets for the two streams (cu_split_streams)
             self.main, self.side = cu_split_streams(side_cus)
             self.main.wait_stream(torch.cuda.current_stream())
+        self.post = torch.cuda.Stream() if stages == 3 else self.main
         tmp = torch.cuda.Stream()
         tmp.wait_stream(self.main)
         with torch.cuda.stream(tmp):
@@ -716,22 +741,35 @@ class PipelinedInfer:
                 infer(fb, op, crop_formation(fb))
         self.main.wait_stream(tmp)
         torch.cuda.synchronize()
+        nb = 2 if stages == 2 else 3
+        self.nb = nb
         self.crop_graphs, self.crops, self.infer_graphs, self.outs = [], [], [], []
-        for k in range(2):
+        self.pose_graphs, self.mids = [], []
+        for k in range(nb):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):  # (InferStep reads no C_gt: none is solved here)
                 self.crops.append(crop_formation(fb))
             self.crop_graphs.append(g)
-        for k in range(2):
+        for k in range(nb):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self.outs.append(infer(fb, op, self.crops[k]))
+                if stages == 2:
+                    self.outs.append(infer(fb, op, self.crops[k]))
+                else:
+                    self.mids.append(infer.model_stage(fb, op, self.crops[k]))
             self.infer_graphs.append(g)
-        self.formed = [torch.cuda.Event(), torch.cuda.Event()]
-        self.consumed = [torch.cuda.Event(), torch.cuda.Event()]
-        for k in range(2):
+            if stages == 3:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self.outs.append(infer.pose_stage(fb, op, self.crops[k], self.mids[k]))
+                self.pose_graphs.append(g)
+        self.formed = [torch.cuda.Event() for _ in range(nb)]
+        self.modeled = [torch.cuda.Event() for _ in range(nb)]
+        self.consumed = [torch.cuda.Event() for _ in range(nb)]  # buffer k's last reader done
+        for k in range(nb):
             self.consumed[k].record(self.main)
         self.i = 0
+        self._pending = None  # stages=3: the buffer whose pose stage is still to run
         self._form(0)
 
     def _form(self, k):
@@ -740,15 +778,41 @@ class PipelinedInfer:
             self.crop_graphs[k].replay()
             self.formed[k].record(self.side)
 
-    def __call__(self) -> dict:
-        k = self.i & 1
-        self._form(k ^ 1)  # the next batch's crops, concurrently
+    def _pose(self, k):
+        with torch.cuda.stream(self.post):
+            self.post.wait_event(self.modeled[k])
+            self.pose_graphs[k].replay()
+            self.consumed[k].record(self.post)
+        return self.outs[k]
+
+    def __call__(self):
+        if self.stages == 2:
+            k = self.i & 1
+            self._form(k ^ 1)  # the next batch's crops, concurrently
+            with torch.cuda.stream(self.main):
+                self.main.wait_event(self.formed[k])
+                self.infer_graphs[k].replay()
+                self.consumed[k].record(self.main)
+            self.i += 1
+            return self.outs[k]
+        k = self.i % 3
+        self._form((self.i + 1) % 3)  # batch i+1 (its buffer's pose stage, batch i-2, is ordered before)
         with torch.cuda.stream(self.main):
             self.main.wait_event(self.formed[k])
             self.infer_graphs[k].replay()
-            self.consumed[k].record(self.main)
+            self.modeled[k].record(self.main)
+        out = self._pose(self._pending) if self._pending is not None else None  # batch i-1
+        self._pending = k
         self.i += 1
-        return self.outs[k]
+        return out
+
+    def flush(self):
+        """stages=3: run the pose stage still pending (the last call's batch) and return its outputs."""
+        if self.stages == 2 or self._pending is None:
+            return None
+        out = self._pose(self._pending)
+        self._pending = None
+        return out
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:

@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--eager", action="store_true", help="no HIP graph: launch every kernel from Python")
     ap.add_argument("--train-only", action="store_true",
                     help="diagnostic: crops formed once, outside the timed graph (not a headline number)")
+    ap.add_argument("--infer-stages", type=int, choices=(2, 3), default=2,
+                    help="infer: 3 = also overlap the pose stage of batch i-1 with the model of batch i")
     ap.add_argument("--no-overlap", action="store_true",
                     help="graph mode without overlapping crop formation of the next batch")
     ap.add_argument("--probe-steps", type=int, default=2, help="eager steps after timing for the kernel breakdown")
@@ -437,7 +439,9 @@ def build_train(args, dev, rank, world):
                           "fwd+bwd (configs[2] semantics, DDP over RCCL when N>1)",
               "execution": "eager" if args.eager else ("hip-graph, training only (diagnostic)" if args.train_only else
                                                        "hip-graph" if args.no_overlap else
-                                                       "hip-graph, crop formation overlapped"),
+                                                       "hip-graph, crop formation overlapped" +
+                                                       (", pose stage of the previous batch overlapped"
+                                                        if args.infer_stages == 3 else "")),
               "global_batch": B * world, "points_per_crop": N, "cad_points": N,
               "precision": "model fp32 (f32 MFMA); crop geometry / C_gt normal equations fp64",
               "parallelism": f"dp{world}"}
@@ -478,7 +482,7 @@ def build_infer(args, dev, rank, world):
     elif args.no_overlap:
         one_step = GraphedInfer(crops_of, infer, fb, op)
     else:  # crop formation of the next batch on a second stream, as in training
-        one_step = PipelinedInfer(crops_of, infer, fb, op)
+        one_step = PipelinedInfer(crops_of, infer, fb, op, stages=args.infer_stages)
     name = "configs[3] shard" if N == 2048 else "configs[1]"
     config = {"workload": f"{name}: B={B} synthetic 640x480 RGB-D crops/GPU, {N} pts, inference (eval.py + "
                           f"test_RANSAC.py: top-5 + 3-round rigidity filter + IR + RANSAC {args.hypotheses} "
@@ -486,7 +490,9 @@ def build_infer(args, dev, rank, world):
                                                          if args.icp_evals else "") +
                           "), batch-sharded across ranks (weak scaling)",
               "execution": "eager" if args.eager else ("hip-graph" if args.no_overlap else
-                                                       "hip-graph, crop formation overlapped"),
+                                                       "hip-graph, crop formation overlapped" +
+                                                       (", pose stage of the previous batch overlapped"
+                                                        if args.infer_stages == 3 else "")),
               "global_batch": B * world, "points_per_crop": N, "cad_points": N, "hypotheses": args.hypotheses,
               "precision": "model fp32 (f32 MFMA); crop geometry / RANSAC fp64", "parallelism": f"shard{world}"}
     if args.ragged:

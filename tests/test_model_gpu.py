@@ -106,7 +106,8 @@ def test_linear_wgrad(device, shape, channels_first):
 def test_linear_wgrad_grouped(device):
     """pk_linear_wgrad_grouped (every layer of a backward in two launches) vs fp64 per call:
     both layouts, a shared layer fed by two calls (accumulate), an empty call, a layer
-    whose only call is empty (zero gradient), and > 32 calls (several table chunks)."""
+    whose only call is empty (zero gradient), thin operands and ragged last tiles on the LDS-DMA
+    pipeline, and > 32 calls (several table chunks)."""
     from dpfm_amd import ops
     g = torch.Generator().manual_seed(11)
     specs = [  # (lead shape, I, O, channels_first, shared-with index or None)
@@ -114,6 +115,8 @@ def test_linear_wgrad_grouped(device):
         ((32, 1024), 32, 32, True, None), ((32, 1024), 64, 32, True, None), ((32, 1024), 32, 32, True, 3),
         ((0,), 16, 8, False, None), ((5, 33), 64, 32, False, None), ((2, 1024), 64, 64, True, 1 << 30),
         ((3, 5002), 64, 32, True, None), ((2, 300), 64, 32, True, 9),  # ragged items (N % 16 != 0)
+        ((65536,), 3, 64, False, None), ((4, 1001), 32, 1, False, None),  # thin operands (3 -> 64, 32 -> 1)
+        ((2, 32768), 128, 64, False, None),
     ]
     specs = specs + [((7, 48), 32, 32, False, None)] * 30
     calls, exp = [], {}

@@ -271,6 +271,28 @@ def test_pipelined_infer_matches_graphed(device):
             assert torch.equal(out[key], ref[key]), key
 
 
+def test_three_stage_pipelined_infer_matches_graphed(device):
+    """PipelinedInfer(stages=3): crop formation (side stream), model + top-5 (main) and rigidity /
+    IR / RANSAC / metrics (third stream) of three consecutive batches in flight; every batch's
+    outputs equal the single-stream GraphedInfer's, one call late, and flush() returns the last."""
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import GraphedInfer, InferStep, PipelinedInfer, make_frame_batch
+    torch.manual_seed(0)
+    F, N = 4, 512
+    fb, op = make_frame_batch(F, N, N, seed=71, device=device)
+    model = DPFMNet().to(device).eval()
+    g = GraphedInfer(CropFormation(n1=N, npoint=N, seed=3), InferStep(model, hypotheses=256), fb, op)
+    ref = {k: v.clone() for k, v in g().items() if torch.is_tensor(v)}
+    p = PipelinedInfer(CropFormation(n1=N, npoint=N, seed=3), InferStep(model, hypotheses=256), fb, op, stages=3)
+    assert p() is None
+    outs = [p() for _ in range(5)] + [p.flush()]
+    torch.cuda.synchronize()
+    for out in outs[-3:]:  # (the static outputs of the three pose graphs)
+        for key in ("T", "ir", "n_corr", "metrics", "p_pred", "C"):
+            assert torch.equal(out[key], ref[key]), key
+
+
 def test_infer_step_with_icp_matches_standalone_icp(device):
     """InferStep(icp_evaluations=E) refines the RANSAC poses against the crops exactly as the
     host-polled ops.icp with max_iteration E - 1 does, and stays HIP-graph capturable."""
