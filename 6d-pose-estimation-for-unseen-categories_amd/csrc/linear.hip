@@ -1212,7 +1212,7 @@ __global__ __launch_bounds__(256, 1) void linear_glds_rows_kernel(const float* _
 //     m + 16 t as one vector, i.e. k-step q takes row 4 g + q (any bijection works: A and B use
 //     the same one). Tile t holds o = m' + 16 t.
 // Bias: db[o] = the sum of the dy values the lanes feed the MFMAs (fixed order).
-constexpr int kWgBlocks = 256;   // target blocks per grouped launch (one per CU: LDS-bound)
+constexpr int kWgBlocks = 1024;  // blocks per grouped launch: 4 x the CU count (MI355X: 256; wg_budget)
 constexpr int kWgLdsBytes = 4 * 3 * 16 * (128 + 64) * 4;  // 3 slots per wave of the largest (I + O = 192)
 // ring depth: as many slots as the LDS holds, <= 8 (bytes in flight per CU = 4 (D - 1) slots:
 // the thin problems are HBM-bound and need the depth, the wide ones have the MFMA work)
@@ -1335,15 +1335,15 @@ __device__ __forceinline__ void wgrad_glds_body(const WgradProblem& P, int s, fl
     }
     const int64_t row0 = lrow;
     if constexpr (LAYOUT == 0) {
-      if (row0 + 16 <= P.R) {  // (wave-uniform) all rows in range: scalar base + lane offsets
-        glds_issue<NX, XT ? 4 : 16>(P.x + row0 * (XT ? XT : I), offx, sl);
-        glds_issue<ND, DT ? 4 : 16>(P.dy + row0 * (DT ? DT : O), offd, sl + XS);
-      } else {
-        if constexpr (XT > 0) glds_thin<XT>(P.x, row0, P.R, sl, lane);
-        else glds_rows<I>(P.x, I, row0, P.R, I, sl, lane);
-        if constexpr (DT > 0) glds_thin<DT>(P.dy, row0, P.R, sl + XS, lane);
-        else glds_rows<O>(P.dy, O, row0, P.R, O, sl + XS, lane);
-      }
+      // thin operands: every lane of the 4-B glds loads one float, 64 per instruction, past the
+      // tile's 16 C: always clamped to the tensor (glds_thin), whatever the tile
+      const bool full = row0 + 16 <= P.R;  // (wave-uniform) all rows in range
+      if constexpr (XT > 0) glds_thin<XT>(P.x, row0, P.R, sl, lane);
+      else if (full) glds_issue<NX, 16>(P.x + row0 * I, offx, sl);
+      else glds_rows<I>(P.x, I, row0, P.R, I, sl, lane);
+      if constexpr (DT > 0) glds_thin<DT>(P.dy, row0, P.R, sl + XS, lane);
+      else if (full) glds_issue<ND, 16>(P.dy + row0 * O, offd, sl + XS);
+      else glds_rows<O>(P.dy, O, row0, P.R, O, sl + XS, lane);
     } else {
       glds_issue<NX, 16>(P.x + lb * sbx + ln, offx, sl);
       glds_issue<ND, 16>(P.dy + lb * sbdy + ln, offd, sl + XS);
@@ -2128,24 +2128,81 @@ static double wg_cost(const pk_wgrad_call& k) {
   return bytes > flops / 19.66 ? bytes : flops / 19.66;
 }
 
+// Blocks: one resident per CU (each holds 144 KB of LDS), so the launch runs in rounds of
+// blocks; 4 x the CU count in equal-cost slices keeps the last round's idle CUs to a quarter of a
+// block time (measured, tools/wg_bench.py under rocprofv3: 256 blocks 248 us, 512 140 us, 1024
+// 136 us — one block per CU is NOT one round: a few CUs take a second block). Shares of the
+// budget by cost, floored (>= 1 block, >= 64 rows each), leftovers to the largest remainders.
+static int wg_budget() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = kWgBlocks / 4;
+    n *= 4;
+#ifdef PK_DEVBUILD
+    if (const char* e = getenv("PK_WG_BUDGET")) n = atoi(e) > 0 ? atoi(e) : n;  // (development knob)
+#endif
+    return n;
+  }();
+  return cus;
+}
+
 static void wg_plan(const pk_wgrad_call* calls, int n, std::vector<int64_t>& S, std::vector<int64_t>& SL,
                     std::vector<char>& glds) {
   S.assign(n, 0);
   SL.assign(n, 0);
   glds.assign(n, 0);
   double wtot = 0.0;
+  int ne = 0;
   for (int c = 0; c < n; ++c)
-    if (wg_on_pipeline(calls[c])) wtot += wg_cost(calls[c]);
+    if (wg_on_pipeline(calls[c])) {
+      wtot += wg_cost(calls[c]);
+      ++ne;
+    }
+  std::vector<int64_t> nb(n, 0);
+  std::vector<double> want(n, 0.0);
+  if (ne > 0) {
+    const int budget = wg_budget() > ne ? wg_budget() : ne;
+    int64_t tot = 0;
+    for (int c = 0; c < n; ++c) {
+      if (!wg_on_pipeline(calls[c])) continue;
+      const int64_t cap = (calls[c].R + 63) / 64;
+      want[c] = wg_cost(calls[c]) / wtot * budget;
+      int64_t v = (int64_t)want[c];
+      nb[c] = v < 1 ? 1 : v > cap ? cap : v;
+      tot += nb[c];
+    }
+    while (tot > budget) {  // (only from the >= 1 floors) take from the largest
+      int best = -1;
+      for (int c = 0; c < n; ++c)
+        if (nb[c] > 1 && (best < 0 || nb[c] > nb[best])) best = c;
+      if (best < 0) break;
+      --nb[best];
+      --tot;
+    }
+    while (tot < budget) {  // leftover CUs to the largest remainders (below their row cap)
+      int best = -1;
+      double rem = -1e300;
+      for (int c = 0; c < n; ++c) {
+        if (!wg_on_pipeline(calls[c]) || nb[c] >= (calls[c].R + 63) / 64) continue;
+        const double r = want[c] - (double)nb[c];
+        if (r > rem) {
+          rem = r;
+          best = c;
+        }
+      }
+      if (best < 0) break;
+      ++nb[best];
+      ++tot;
+    }
+  }
   for (int c = 0; c < n; ++c) {
     const pk_wgrad_call& k = calls[c];
     if (k.R <= 0) continue;
     if (wg_on_pipeline(k)) {
       glds[c] = 1;
-      const double share = wg_cost(k) / wtot * kWgBlocks;
-      int64_t nb = (int64_t)(share + 0.5);
-      const int64_t cap = (k.R + 63) / 64;
-      nb = nb < 1 ? 1 : nb > cap ? cap : nb;
-      SL[c] = ((k.R + nb - 1) / nb + 15) / 16 * 16;
+      SL[c] = ((k.R + nb[c] - 1) / nb[c] + 15) / 16 * 16;
     } else {
       SL[c] = grouped_slice_rows(k.R);
     }

@@ -135,7 +135,9 @@ def train_step_parity(M, op, crops, device, model_seed, step_seed):
     weights, crops and NCE pair draw. Yardstick (model_parity's): the same oracle in fp32 on
     the CPU and on the GPU; the HIP step's loss and every parameter gradient must be within
     3x the larger of their errors (gradient floor 1e-6 x the global gradient norm for the
-    invariance-zero parameters); C_gt within 1e-4 of its scale."""
+    invariance-zero parameters), the oracle's loss taking the step's C_gt; C_gt itself per crop
+    within 1e-4 of its scale where the pair system is well conditioned, else a least-squares
+    solution at least as good as the fp64 oracle's."""
     import torch
     from dpfm_amd import ops
     from dpfm_amd.models.dpfm import DPFMNet
@@ -171,10 +173,17 @@ def train_step_parity(M, op, crops, device, model_seed, step_seed):
     cpu64 = {k: {kk: vv.double() for kk, vv in v.items()} for k, v in cpu.items()}
     gpu = {k: {kk: vv.to(device) for kk, vv in v.items()} for k, v in cpu.items()}
 
+    cgd = C_gt_dev.cpu().double()
+
     def oracle_step(model, batch, dt):
         model.zero_grad()
         ex, ey = batch["shape1"]["evecs"], batch["shape2"]["evecs"]
         C_gt = torch.stack([M.C_from_sparse_P(plist[b].to(ex.device), ex[b, :, :30], ey[b, :, :30]) for b in range(B)])
+        if dt == torch.float64:
+            C_gt_of[0] = C_gt.detach().cpu().double()
+        # the step's own C_gt (checked against this one below, rank-aware): the loss and
+        # gradients are then compared on the same target
+        C_gt = cgd.to(device=ex.device, dtype=C_gt.dtype)
         C, o12, o21, f1, f2, _, _ = model(batch)
         dv = ex.device
         loss = M.dpfm_loss(C, C_gt, [p.to(dv) for p in plist], [s.to(dv) for s in sel], f1, f2, o12, o21,
@@ -184,12 +193,27 @@ def train_step_parity(M, op, crops, device, model_seed, step_seed):
                  for p in model.parameters()]
         return float(loss), C_gt.detach().cpu().double(), grads
 
-    l64, cg64, gr64 = oracle_step(truth, cpu64, torch.float64)
+    C_gt_of = [None]
+    l64, _, gr64 = oracle_step(truth, cpu64, torch.float64)
     l32, _, gr32 = oracle_step(ref, cpu, torch.float32)
     lg, _, grg = oracle_step(gref, gpu, torch.float32)
-    # C_gt
-    cgd = C_gt_dev.cpu().double()
-    assert (cgd - cg64).abs().max().item() <= 1e-4 * cg64.abs().max().item(), (cgd - cg64).abs().max().item()
+    # C_gt per crop: within 1e-4 of its scale where the pair system is well conditioned (>= 30
+    # pairs, sigma_min / sigma_max >= 1e-5); otherwise (few or degenerate pairs: the reference's
+    # CUDA gels has no defined answer, both sides give a least-squares solution) the device's
+    # residual no larger than the fp64 oracle's + 1e-4 of the right-hand side
+    cg64 = C_gt_of[0]
+    ex64, ey64 = cpu64["shape1"]["evecs"], cpu64["shape2"]["evecs"]
+    for b in range(B):
+        p = plist[b]
+        a1, a2 = ex64[b][p[:, 0], :30], ey64[b][p[:, 1], :30]
+        sv = torch.linalg.svdvals(a2) if p.shape[0] else torch.zeros(1, dtype=torch.float64)
+        if p.shape[0] >= 30 and float(sv[-1]) >= 1e-5 * float(sv[0]):
+            err = (cgd[b] - cg64[b]).abs().max().item()
+            assert err <= 1e-4 * max(cg64[b].abs().max().item(), 1e-30), (b, err)
+        else:
+            rd = (a2 @ cgd[b] - a1).norm().item()
+            ro = (a2 @ cg64[b] - a1).norm().item()
+            assert rd <= ro + 1e-4 * max(a1.norm().item(), 1e-30), (b, rd, ro)
     # loss
     ld = float(log["loss"])
     e = [abs(l32 - l64), abs(lg - l64), abs(ld - l64)]

@@ -32,12 +32,13 @@ FAMILIES = {
     "pk_attention_fwd": ["attn_fwd_kernel"],
     "pk_attention_bwd": ["attn_bwd_dq_kernel", "attn_bwd_dkv_kernel"],
     "pk_linear_wgrad": ["wgrad_v2_kernel", "wgrad_partial_kernel", "wgrad_reduce_kernel"],
-    "pk_feat_dist_topk": ["fd_prep_kernel", "fd_main_kernel"],
+    "pk_feat_dist_topk": ["fd_wide_kernel", "fd_prep_kernel", "fd_main_direct_kernel", "fd_main_kernel"],
     "pk_cgt_lstsq": ["cgt_count_kernel", "cgt_partial_kernel", "cgt_reduce_kernel", "cgt_solve_kernel"],
     # pk_linear_fwd and pk_linear_ex (its epilogue / placement variant) launch the same kernels: the
     # counters cannot tell them apart, so they form one family, per KERNEL launch
-    "pk_linear_fwd+ex": ["linear_fwd_rows_kernel", "linear_fwd_cf_kernel", "linear_fwd_kernel", "linear_thin_kernel"],
-    "pk_linear_wgrad_grouped": ["wgrad_grouped_kernel", "wgrad_grouped_reduce_kernel"],
+    "pk_linear_fwd+ex": ["linear_glds_rows_kernel", "linear_fwd_rows_kernel", "linear_fwd_cf_kernel", "linear_fwd_kernel",
+                         "linear_thin_kernel"],
+    "pk_linear_wgrad_grouped": ["wgrad_glds_grouped_kernel", "wgrad_grouped_kernel", "wgrad_grouped_reduce_kernel"],
     "pk_nce_loss": ["nce_pass_kernel<false>", "nce_pass_kernel<true>", "nce_scatter_kernel"],
     "pk_clip_rmsprop": ["grad_sumsq_kernel", "clip_rmsprop_kernel"],
     "pk_instnorm_relu_fwd": ["instnorm_relu_fwd"],
