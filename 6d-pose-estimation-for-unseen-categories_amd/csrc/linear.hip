@@ -2128,11 +2128,11 @@ static double wg_cost(const pk_wgrad_call& k) {
   return bytes > flops / 19.66 ? bytes : flops / 19.66;
 }
 
-// Blocks: one resident per CU (each holds 144 KB of LDS), so the launch runs in rounds of
-// blocks; 4 x the CU count in equal-cost slices keeps the last round's idle CUs to a quarter of a
-// block time (measured, tools/wg_bench.py under rocprofv3: 256 blocks 248 us, 512 140 us, 1024
-// 136 us — one block per CU is NOT one round: a few CUs take a second block). Shares of the
-// budget by cost, floored (>= 1 block, >= 64 rows each), leftovers to the largest remainders.
+// Blocks: one resident per CU (each holds 144 KB of LDS), so the launch runs in rounds; 4 x the
+// CU count lets the dispatcher balance what the cost model misses (measured, tools/wg_bench.py
+// under rocprofv3, whole step's call list: 240 / 248 / 252 / 256 blocks 243-248 us — one round,
+// bound by its slowest slice — 496 135 us, 1024 136 us, 2048 155 us). Shares of the budget by
+// cost, floored (>= 1 block, >= 64 rows each), leftovers to the largest remainders.
 static int wg_budget() {
   static const int cus = [] {
     int dev = 0, n = 0;

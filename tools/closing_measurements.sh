@@ -1,9 +1,9 @@
 #!/bin/bash
-# round-4 closing measurements: the headline train bench (with CPU baseline), inference at
+# Closing measurements of a round: the headline train bench (with CPU baseline), inference at
 # configs[1] and at the configs[3] shard, (f1) operators, the step kernel trace, and the PMC
 # traffic passes. Each step under its own limit; the first failure ends the script.
 export TMPDIR=/tmp
-O=gpurun_out/r04close
+O=gpurun_out/${TAG:-close}
 mkdir -p $O
 step() { local name=$1 to=$2; shift 2; timeout -k 10 $to "$@" > $O/$name.out 2> $O/$name.err || { echo "$name failed"; tail -20 $O/$name.err; exit 1; }; tail -c 400 $O/$name.out; echo; }
 step train 600 python3 -u bench.py
@@ -12,5 +12,5 @@ step infer2048 300 python3 -u bench.py --mode infer --points 2048 --no-cpu-basel
 step ops 400 python3 -u bench.py --mode operators --batch 8 --steps 3 --warmup 1
 step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline-probe
 find $O/prof -type f ! -name "*stats.csv" -delete
-TAG=r04close/pmc bash tools/pmc_step.sh > $O/pmc.out 2>&1 || { tail -20 $O/pmc.out; exit 1; }
+TAG=${TAG:-close}/pmc bash tools/pmc_step.sh > $O/pmc.out 2>&1 || { tail -20 $O/pmc.out; exit 1; }
 tail -5 $O/pmc.out

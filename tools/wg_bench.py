@@ -63,6 +63,9 @@ def line(name, us, nb, fl):
             f"of HBM)  {fl / 1e9:5.2f} GFLOP -> {fl / us / 1e6:6.1f} TF/s ({fl / us / 1e6 / 157.3:.3f} of f32 MFMA)")
 
 
+if os.environ.get("WG_ONLY"):  # one shape group alone (its index in spec), e.g. under rocprofv3
+    name, calls, nbytes, flops = groups[int(os.environ["WG_ONLY"])]
+    print(f"group {name}")
 print(f"device: {torch.cuda.get_device_properties(0).multi_processor_count} CUs; "
       f"PK_WG_BUDGET={os.environ.get('PK_WG_BUDGET', '-')} PK_WG_GLDS={os.environ.get('PK_WG_GLDS', '-')}")
 print("wgrad grouped " + line(f"({len(calls)} calls)", timed(calls), nbytes, flops))
