@@ -161,8 +161,9 @@ __global__ __launch_bounds__(256) void rigid_pair_kernel(const int64_t* __restri
 // gathered once (rigid_gather_kernel) and each compaction carries the survivors' records
 // along (rigid_compact_pts_kernel), so a pair block loads its two tiles with plain 16-B loads.
 // The pair term is two rigid_dist (FMA sums of squares, v_sqrt_f32) and |a - b| folded into the
-// row and column sums as a source modifier; 8 x 8 pairs per thread.
-constexpr int kRT2 = 128;
+// row and column sums as a source modifier; kPS x kPS (16 x 16) pairs per thread.
+constexpr int kRT2 = 256;            // entries per tile (rounds 2, 3)
+constexpr int kPS = kRT2 / 16;       // entries per thread per side
 typedef float rf2 __attribute__((ext_vector_type(2)));
 
 struct __attribute__((aligned(16))) RigidRec {
@@ -200,32 +201,38 @@ __device__ __forceinline__ float rigid_dist(float px, float py, float pz, float 
   return __builtin_amdgcn_sqrtf(__builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx)));
 }
 
-// 8 x 8 pairs of one thread: rows i = ty + 16 r, columns j = tx + 16 c. ra[r]: this thread's
-// row sums (over its 8 columns), ca[c]: its column sums. Scalar VALU: on MI355X a v_pk_*_f32
+// kPS x kPS pairs of one thread: rows i = ty + 16 r, columns j = tx + 16 c. ra[r]: this thread's
+// row sums (over its kPS columns), ca[c]: its column sums. Scalar VALU: on MI355X a v_pk_*_f32
 // costs the issue of two scalar ops (measured: round 3's packed form ran at the scalar rate).
 template <bool EDGE>
 __device__ __forceinline__ void rigid_tile_pairs(const RigidRec* __restrict__ si, const RigidRec* __restrict__ sj,
-                                                 int tx, int ty, float (&ra)[8], float (&ca)[8]) {
-  RigidRec cj[8];
+                                                 int tx, int ty, float (&ra)[kPS], float (&ca)[kPS]) {
+  float ax[kPS], ay[kPS], az[kPS], px[kPS], py[kPS], pz[kPS], cv[kPS];  // column entries
 #pragma unroll
-  for (int c = 0; c < 8; ++c) cj[c] = sj[tx + 16 * c];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
+  for (int c = 0; c < kPS; ++c) {
+    const RigidRec q = sj[tx + 16 * c];
+    ax[c] = q.x.x; ay[c] = q.y.x; az[c] = q.z.x;
+    px[c] = q.x.y; py[c] = q.y.y; pz[c] = q.z.y;
+    cv[c] = q.v.x;
+  }
+#pragma unroll 2
+  for (int r = 0; r < kPS; ++r) {
     const RigidRec ci = si[ty + 16 * r];
+    float rs = 0.f;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const RigidRec& q = cj[c];
-      const float a = rigid_dist(ci.x.x, ci.y.x, ci.z.x, q.x.x, q.y.x, q.z.x);
-      const float bb = rigid_dist(ci.x.y, ci.y.y, ci.z.y, q.x.y, q.y.y, q.z.y);
+    for (int c = 0; c < kPS; ++c) {
+      const float a = rigid_dist(ci.x.x, ci.y.x, ci.z.x, ax[c], ay[c], az[c]);
+      const float bb = rigid_dist(ci.x.y, ci.y.y, ci.z.y, px[c], py[c], pz[c]);
       float v = fabsf(a - bb);
-      if (EDGE) v = v * (q.v.x * ci.v.x);  // invalid entries contribute 0
-      ra[r] += v;
+      if (EDGE) v = v * (cv[c] * ci.v.x);  // invalid entries contribute 0
+      rs += v;
       ca[c] += v;
     }
+    ra[r] = rs;
   }
 }
 
-// Grid (T (T + 1) / 2, B) over 128 x 128 tile pairs I <= J (T = ceil(nmax / 128)), XCD-aware
+// Grid (T (T + 1) / 2, B) over kRT2 x kRT2 tile pairs I <= J (T = ceil(nmax / kRT2)), XCD-aware
 // (a crop's tile pairs share one XCD's L2); block 256 = 16 x 16 threads. As rigid_pair_kernel:
 // part[b][J][x] = sum over tile J of entry x of tile I, and for I != J part[b][I][y] for the
 // entries y of tile J; every slot written once, summed in tile order by rigid_reduce_kernel.
@@ -246,27 +253,26 @@ __global__ __launch_bounds__(256) void rigid_pair2_kernel(const int32_t* __restr
   if (J * kRT2 >= n) return;  // block-uniform: tile outside this round's list
   const RigidRec* P0 = pts + (int64_t)b * ldl;
   const int tid = threadIdx.x;
-  {
-    const int e = tid & (kRT2 - 1);
-    const int x = (tid < kRT2 ? I : J) * kRT2 + e;
-    RigidRec* dst = tid < kRT2 ? si : sj;
+  for (int e2 = tid; e2 < 2 * kRT2; e2 += 256) {
+    const int e = e2 & (kRT2 - 1);
+    const int x = (e2 < kRT2 ? I : J) * kRT2 + e;
     RigidRec r;
     if (x < n) r = P0[x];
     else r.x = r.y = r.z = r.v = rf2{0.f, 0.f};
-    dst[e] = r;
+    (e2 < kRT2 ? si : sj)[e] = r;
   }
   __syncthreads();
   const int tx = tid & 15, ty = tid >> 4;
-  float ra[8], ca[8];
+  float ra[kPS], ca[kPS];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) ra[r] = ca[r] = 0.f;
+  for (int r = 0; r < kPS; ++r) ra[r] = ca[r] = 0.f;
   if ((J + 1) * kRT2 > n) rigid_tile_pairs<true>(si, sj, tx, ty, ra, ca);
   else rigid_tile_pairs<false>(si, sj, tx, ty, ra, ca);
   float* P = part + (int64_t)b * T * ldl;
   // row sums of tile I over tile J: the 16 tx lanes are one DPP row (quad_perm / half-mirror /
   // mirror adds: VALU only, no LDS round trips); lane tx = 0's association order is fixed
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
+  for (int r = 0; r < kPS; ++r) {
     float v = ra[r];
     v += __int_as_float((int)PK_DPP(__float_as_int(v), 0xB1));
     v += __int_as_float((int)PK_DPP(__float_as_int(v), 0x4E));
@@ -279,16 +285,16 @@ __global__ __launch_bounds__(256) void rigid_pair2_kernel(const int32_t* __restr
   // column sums of tile J over tile I: the wave's 4 ty rows by butterfly, then the 4 waves in order
   const int w = pk::wave_id();
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
+  for (int c = 0; c < kPS; ++c) {
     float v = ca[c];
     v += __shfl_xor(v, 16);
     v += __shfl_xor(v, 32);
     if ((tid & 63) < 16) red[w][tx + 16 * c] = v;
   }
   __syncthreads();
-  if (tid < kRT2) {
-    const float v = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
-    const int x = J * kRT2 + tid;
+  for (int e = tid; e < kRT2; e += 256) {
+    const float v = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+    const int x = J * kRT2 + e;
     if (x < n) P[(int64_t)I * ldl + x] = v;
   }
 }
@@ -296,47 +302,69 @@ __global__ __launch_bounds__(256) void rigid_pair2_kernel(const int32_t* __restr
 // ---- Round 1 (round-4 path): the candidates of nn_query come in groups of K = 5 that share one
 // crop point (spacial_filtering.py:36-38: p2p = stack([idx, idx_p]).reshape(2, -1), crop point
 // p repeated for its 5 nearest CAD points), so the crop half of the pair term,
-// ||PC[p_i] - PC[p_j]||, is the same for all 25 pairs of two groups. Tiles of 32 groups
-// (160 entries); thread (tx, ty) of 16 x 16 owns row groups ty, ty + 16 and column groups tx,
-// tx + 16: per group pair one crop distance, then 25 CAD distances. The pair value |a - b| is
+// ||PC[p_i] - PC[p_j]||, is the same for all 25 pairs of two groups. Tiles of 64 groups
+// (320 entries); thread (tx, ty) of 16 x 16 owns row groups ty + 16 r and column groups tx + 16 h
+// (r, h < 4): per group pair one crop distance, then 25 CAD distances. The pair value |a - b| is
 // bit-identical to rigid_pair2_kernel's (same rigid_dist); only the association of the sums
 // differs (fixed).
 // A tile pair whose groups do not share their crop coordinates (a caller passing another
 // candidate order) takes the general form of the same loop (both sqrt per pair), so any
 // candidate list is scored correctly. Partials as rigid_pair2_kernel, tiles of kRG entries.
 constexpr int kGK = 5;              // candidates per crop point (nn_query's K)
-constexpr int kGT = 32;             // groups per tile
+constexpr int kGT = 64;             // groups per tile
+constexpr int kGS = kGT / 16;       // groups per thread per side (thread (tx, ty) of 16 x 16)
 constexpr int kRG = kGK * kGT;      // entries per tile
 
+// Thread (tx, ty): row groups ty + 16 r and column groups tx + 16 h (r, h < kGS): kGS^2 group
+// pairs = 25 kGS^2 pairs (400), so the per-thread prologue and the row / column reductions stay
+// a few % of the pair work (12.7 VALU per pair with 100 pairs per thread).
 template <bool SHARED, bool EDGE>
 __device__ __forceinline__ void rigid_group_pairs(const RigidRec* __restrict__ si, const RigidRec* __restrict__ sj,
-                                                  int tx, int ty, float (&ra)[2][kGK], float (&ca)[2][kGK]) {
-  RigidRec cj[2][kGK];  // column entries (Q0 = tx, l) and (Q1 = tx + 16, l)
+                                                  int tx, int ty, float (&ra)[kGS][kGK], float (&ca)[kGS][kGK]) {
+  float cx[kGS][kGK], cy[kGS][kGK], cz[kGS][kGK], cv[kGS][kGK];  // column entries' CAD point, validity
+  float qx[kGS], qy[kGS], qz[kGS];                                 // column groups' crop point
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < kGS; ++h) {
 #pragma unroll
-    for (int l = 0; l < kGK; ++l) cj[h][l] = sj[kGK * (tx + 16 * h) + l];
+    for (int l = 0; l < kGK; ++l) {
+      const RigidRec q = sj[kGK * (tx + 16 * h) + l];
+      cx[h][l] = q.x.x;
+      cy[h][l] = q.y.x;
+      cz[h][l] = q.z.x;
+      cv[h][l] = q.v.x;
+      if (l == 0) {
+        qx[h] = q.x.y;
+        qy[h] = q.y.y;
+        qz[h] = q.z.y;
+      }
+    }
+  }
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
+  for (int r = 0; r < kGS; ++r) {
     const int P = ty + 16 * r;
-    float bq[2] = {0.f, 0.f};
-    if (SHARED) {  // one crop distance per (P, Q0) / (P, Q1)
+    float bq[kGS];
+    if (SHARED) {  // one crop distance per (P, Q_h)
       const RigidRec p = si[kGK * P];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) bq[h] = rigid_dist(p.x.y, p.y.y, p.z.y, cj[h][0].x.y, cj[h][0].y.y, cj[h][0].z.y);
+      for (int h = 0; h < kGS; ++h) bq[h] = rigid_dist(p.x.y, p.y.y, p.z.y, qx[h], qy[h], qz[h]);
     }
 #pragma unroll
     for (int k = 0; k < kGK; ++k) {
       const RigidRec ci = si[kGK * P + k];
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+      for (int h = 0; h < kGS; ++h)
 #pragma unroll
         for (int l = 0; l < kGK; ++l) {
-          const RigidRec& q = cj[h][l];
-          const float a = rigid_dist(ci.x.x, ci.y.x, ci.z.x, q.x.x, q.y.x, q.z.x);
-          const float b = SHARED ? bq[h] : rigid_dist(ci.x.y, ci.y.y, ci.z.y, q.x.y, q.y.y, q.z.y);
+          const float a = rigid_dist(ci.x.x, ci.y.x, ci.z.x, cx[h][l], cy[h][l], cz[h][l]);
+          float b;
+          if (SHARED) {
+            b = bq[h];
+          } else {  // (general candidate order: the column entry's own crop point, from LDS)
+            const RigidRec q = sj[kGK * (tx + 16 * h) + l];
+            b = rigid_dist(ci.x.y, ci.y.y, ci.z.y, q.x.y, q.y.y, q.z.y);
+          }
           float v = fabsf(a - b);
-          if (EDGE) v = v * (q.v.x * ci.v.x);  // invalid entries contribute 0
+          if (EDGE) v = v * (cv[h][l] * ci.v.x);  // invalid entries contribute 0
           ra[r][k] += v;
           ca[h][l] += v;
         }
@@ -384,9 +412,11 @@ __global__ __launch_bounds__(256) void rigid_group_kernel(const int32_t* __restr
   const bool shared = !__syncthreads_or(split);
   const bool edge = (J + 1) * kRG > n;
   const int tx = tid & 15, ty = tid >> 4;
-  float ra[2][kGK], ca[2][kGK];
+  float ra[kGS][kGK], ca[kGS][kGK];
 #pragma unroll
-  for (int l = 0; l < kGK; ++l) ra[0][l] = ra[1][l] = ca[0][l] = ca[1][l] = 0.f;
+  for (int r = 0; r < kGS; ++r)
+#pragma unroll
+    for (int l = 0; l < kGK; ++l) ra[r][l] = ca[r][l] = 0.f;
   if (shared) {
     if (edge) rigid_group_pairs<true, true>(si, sj, tx, ty, ra, ca);
     else rigid_group_pairs<true, false>(si, sj, tx, ty, ra, ca);
@@ -397,7 +427,7 @@ __global__ __launch_bounds__(256) void rigid_group_kernel(const int32_t* __restr
   float* Pp = part + (int64_t)b * T * ldl;
   // row sums of tile I over tile J: the 16 tx lanes of a DPP row, fixed association
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
+  for (int r = 0; r < kGS; ++r) {
 #pragma unroll
     for (int k = 0; k < kGK; ++k) {
       float v = ra[r][k];
@@ -415,7 +445,7 @@ __global__ __launch_bounds__(256) void rigid_group_kernel(const int32_t* __restr
 #pragma unroll
   for (int l = 0; l < kGK; ++l) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < kGS; ++h) {
       float v = ca[h][l];
       v += __shfl_xor(v, 16);
       v += __shfl_xor(v, 32);

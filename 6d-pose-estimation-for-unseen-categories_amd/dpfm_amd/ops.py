@@ -884,22 +884,27 @@ _FD_WORK = {}
 _FD_CAPTURED = []
 
 
-def _fd_work(dev: torch.device, nbytes: int) -> torch.Tensor:
-    """pk_feat_dist_topk's scratch. Its leading arrival words must be zero before the first call and
-    every call leaves them zero (posekern.h), and a buffer must not serve two streams at once, so:
-    eager calls reuse one persistent buffer per (device, stream), zero-filled once when created or
-    grown; a call inside a HIP-graph capture gets a buffer of its own whose zero fill is captured
-    with it (graphs may share a capture stream; every replay then starts from zero words), kept
-    alive for the graph's lifetime."""
+def _fd_work(dev: torch.device, nbytes: int, ctr_bytes: int) -> torch.Tensor:
+    """pk_feat_dist_topk's scratch: [ctr_bytes of arrival words][path scratch]. The arrival words
+    must be zero before a call and every call leaves them zero (posekern.h), and a buffer must not
+    serve two streams at once, so: eager calls reuse one persistent buffer per (device, stream),
+    zero-filled when created or grown, and its leading ctr_bytes re-zeroed whenever the counter
+    size differs from the buffer's previous call (the previous layout's scratch — or a bf16 /
+    top-5 call's, which has no counter prefix — may lie where the new words are); a call inside
+    a HIP-graph capture gets a buffer of its own whose zero fill is captured with it (graphs may
+    share a capture stream; every replay then starts from zero words), kept alive for the graph's
+    lifetime."""
     if torch.cuda.is_current_stream_capturing():
         buf = torch.zeros((max(nbytes, 256),), dtype=torch.uint8, device=dev)
         _FD_CAPTURED.append(buf)
         return buf
     key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
-    buf = _FD_WORK.get(key)
+    buf, last = _FD_WORK.get(key, (None, 0))
     if buf is None or buf.numel() < nbytes:
         buf = torch.zeros((max(nbytes, 256),), dtype=torch.uint8, device=dev)
-        _FD_WORK[key] = buf
+    elif ctr_bytes > 0 and ctr_bytes != last:
+        buf[:ctr_bytes].zero_()
+    _FD_WORK[key] = (buf, ctr_bytes)
     return buf
 
 
@@ -910,7 +915,8 @@ def feat_dist_topk(evecs_x: torch.Tensor, C: torch.Tensor, evecs_y: torch.Tensor
     evecs_x [B,V1,K>=30], C [B,30,30], evecs_y [B,V2,K>=30], n1/n2 int32 [B].
     precision: "fp32" (the parity path: torch.cdist's augmented contraction on the f32 MFMA),
     "bf16" or "bf16x3" (opt-in: bf16 MFMA cross term, f32 norms). work: optional caller scratch
-    (uint8, zero-initialised before its first use, see _fd_work); default: a per-stream buffer."""
+    (uint8; its leading pk_feat_dist_counter_bytes zero before the call, see _fd_work); default: a
+    per-stream buffer."""
     B, V1, ldx = evecs_x.shape
     _, V2, ldy = evecs_y.shape
     dev = evecs_x.device
@@ -919,7 +925,7 @@ def feat_dist_topk(evecs_x: torch.Tensor, C: torch.Tensor, evecs_y: torch.Tensor
     if nbytes < 0:
         raise _lib.PoseKernError("feat_dist_topk: invalid shape / topk / precision")
     if work is None:
-        work = _fd_work(dev, nbytes)
+        work = _fd_work(dev, nbytes, int(_lib.lib().pk_feat_dist_counter_bytes(B, V1, V2, int(topk), mode)))
     elif work.numel() < nbytes:
         raise _lib.PoseKernError(f"feat_dist_topk: work holds {work.numel()} bytes, {nbytes} needed")
     idx = torch.empty((B, V2, topk), dtype=torch.int64, device=dev)

@@ -388,8 +388,10 @@ int pk_linear_ex(const pk_linear_args* a, void* stream);
  *   mode 1: bf16 MFMA cross term + f32 norms; mode 2: bf16x3 (hi/lo split, three bf16 MFMAs)
  *   work: scratch of pk_feat_dist_work_size(B, V1max, V2max, topk, mode) bytes. Its first
  *     pk_feat_dist_counter_bytes(...) bytes are arrival words of the single-launch mode-0 pass
- *     (row parts combined in the launch): they must be zero before the first call that uses the
- *     buffer, and every call leaves them zero (keep one buffer per stream; zero it once).
+ *     (row parts combined in the launch): they must be zero before a call, and every call
+ *     leaves them zero. The remaining bytes are the call's scratch, so after a call of another
+ *     layout (another counter size, or a mode 1/2 or topk 5 call) re-zero the prefix; keep one
+ *     buffer per stream.
  *   out_idx int64 [B,V2max,topk] ascending distance (ties: lower index); out_dist f32
  *   [B,V2max,topk] Euclidean distances (may be NULL). Fused selection epilogue. */
 int64_t pk_feat_dist_work_size(int B, int V1max, int V2max, int topk, int mode);

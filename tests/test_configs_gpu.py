@@ -47,6 +47,33 @@ def test_feat_dist_argmin_top5_configs(device, B, V):
     assert ties <= max(2, B * V // 1000), ties
 
 
+def test_feat_dist_scratch_reuse_across_layouts(device):
+    """The default per-stream scratch of pk_feat_dist_topk serves calls of different layouts in
+    turn (top-1 fp32 with its arrival-word prefix, bf16 and top-5 scratch without / with another
+    prefix): every top-1 fp32 result equals the same call on a fresh zeroed buffer, so no call
+    inherits another's bytes as arrival words (ops._fd_work re-zeroes the prefix on a change)."""
+    from dpfm_amd import _lib, ops
+    g = torch.Generator().manual_seed(77)
+
+    def inputs(B, V):
+        ex = torch.randn(B, V, 32, generator=g).to(device)
+        ey = torch.randn(B, V, 32, generator=g).to(device)
+        C = torch.randn(B, 30, 30, generator=g).to(device)
+        n = torch.full((B,), V, dtype=torch.int32, device=device)
+        return ex, C, ey, n
+
+    seq = [(2, 300, 1, "fp32"), (4, 512, 1, "bf16"), (32, 1024, 1, "fp32"), (3, 700, 5, "fp32"),
+           (8, 2048, 1, "fp32"), (2, 300, 1, "fp32"), (4, 4096, 1, "bf16x3"), (32, 1024, 1, "fp32")]
+    for B, V, k, prec in seq:
+        ex, C, ey, n = inputs(B, V)
+        got, _ = ops.feat_dist_topk(ex, C, ey, n, n, k, precision=prec)
+        mode = ops.FD_MODES[prec]
+        nb = int(_lib.lib().pk_feat_dist_work_size(B, V, V, k, mode))
+        ref, _ = ops.feat_dist_topk(ex, C, ey, n, n, k, precision=prec,
+                                    work=torch.zeros(nb, dtype=torch.uint8, device=device))
+        assert torch.equal(got, ref), (B, V, k, prec)
+
+
 def test_feat_dist_ragged_edges(device):
     """The feature-distance passes on a ragged batch whose per-crop sizes straddle the 16-row
     tile, the 4-tile register chunk and the two row halves of a block (n1, n2 in 1 .. 301):
@@ -111,10 +138,10 @@ def test_rigidity_filter_configs(device, V2):
 
 def test_rigidity_filter_ragged_batch(device):
     """Crops with different candidate counts in one launch (empty, single, tile-edge ±1 of the
-    128-entry pair tiles and of the first round's 160-entry group tiles, partial last groups,
-    and a multi-tile crop): each crop's survivors vs the oracle."""
+    256-entry pair tiles and of the first round's 320-entry group tiles, partial last groups,
+    and multi-tile crops): each crop's survivors vs the oracle."""
     from dpfm_amd import ops
-    sizes = [0, 1, 127, 129, 159, 161, 322, 640, 1000]
+    sizes = [0, 1, 127, 255, 257, 319, 321, 642, 1000]
     scenes = [_rigid_scene(max((s + 4) // 5, 1), 7 + i) for i, s in enumerate(sizes)]
     Lc = max(sizes)
     cand = np.zeros((len(sizes), Lc, 2), dtype=np.int64)
