@@ -350,7 +350,7 @@ struct WgradProblem {
   const float* dy;
   float* part;   // S * O * I weight partials, then S * O bias partials
   int64_t R;
-  int I, O, N, layout, SL, S, blk0, pad;
+  int I, O, N, layout, SL, S, blk0, pad;  // pad: the pipeline kernel's development variant (0)
   int64_t sbx, sbdy;  // channels-first batch strides (0: dense)
 };
 struct WgradProblems {
@@ -1363,6 +1363,7 @@ __device__ __forceinline__ void wgrad_glds_body(const WgradProblem& P, int s, fl
     for (int64_t k = 0; k < nt; ++k) {
       issue(k + kWgD - 1);
       vm_wait((kWgD - 1) * G);  // tile k landed (glds retire in issue order)
+      if (P.pad == 2) continue;  // (development variant: the glds stream alone)
       const float* sx = ring + (k % kWgD) * SLOT;
       const float* sd = sx + XS;
       if constexpr (LAYOUT == 0) {
@@ -1382,6 +1383,10 @@ __device__ __forceinline__ void wgrad_glds_body(const WgradProblem& P, int s, fl
           }
 #pragma unroll
           for (int t = 0; t < TO; ++t) bs[t] += a[t];
+          if (P.pad == 1) {  // (development variant: the operand stream without the MFMAs)
+            acc[0][0][0] += b[0];
+            continue;
+          }
 #pragma unroll
           for (int t = 0; t < TO; ++t)
 #pragma unroll
@@ -1399,6 +1404,10 @@ __device__ __forceinline__ void wgrad_glds_body(const WgradProblem& P, int s, fl
         for (int u = 0; u < TI; ++u) {
           const int c = m + 16 * u;
           b[u] = *reinterpret_cast<const f32x4*>(sx + 16 * c + 4 * (g ^ ((c >> 2) & 3)));
+        }
+        if (P.pad == 1) {  // (development variant: the operand stream without the MFMAs)
+          acc[0][0] += b[0];
+          continue;
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -2112,6 +2121,16 @@ extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, 
 // wg_shape_id, channels-first only with N % 16 == 0, 16-B aligned operands) get blocks in
 // proportion to their cost (wg_cost), about kWgBlocks in all (slices of whole 16-row tiles, >= 64
 // rows); the others keep round 3's wgrad_v2 slicing. S[c] partials of call c, SL[c] rows each.
+// development variants of the pipeline kernel (limiter study): 1 no MFMAs, 2 no LDS reads either
+static int wg_variant() {
+#ifdef PK_DEVBUILD
+  static const int v = getenv("PK_WG_VAR") ? atoi(getenv("PK_WG_VAR")) : 0;
+  return v;
+#else
+  return 0;
+#endif
+}
+
 static bool wg_on_pipeline(const pk_wgrad_call& k) {
 #ifdef PK_DEVBUILD
   static const bool on = getenv("PK_WG_GLDS") == nullptr || atoi(getenv("PK_WG_GLDS")) != 0;
@@ -2268,8 +2287,8 @@ extern "C" int pk_linear_wgrad_grouped(const pk_wgrad_call* calls, int n, float*
       const pk_wgrad_call& k = calls[c];
       if (S[c] == 0 || !glds[c]) continue;
       WgradProblem& P = tp.p[tp.G++];
-      P = WgradProblem{k.x, k.dy, work + off[c], k.R, k.I, k.O, k.N, k.layout, (int)SLv[c], (int)S[c], blocks, 0,
-                       k.sx, k.sdy};
+      P = WgradProblem{k.x, k.dy, work + off[c], k.R, k.I, k.O, k.N, k.layout, (int)SLv[c], (int)S[c], blocks,
+                       wg_variant(), k.sx, k.sdy};
       blocks += (int)S[c];
       if (tp.G == kGroupMax) {
         const int rc = flush();
