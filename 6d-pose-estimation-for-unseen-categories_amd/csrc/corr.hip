@@ -232,16 +232,60 @@ __device__ __forceinline__ void rigid_tile_pairs(const RigidRec* __restrict__ si
   }
 }
 
+// The same kPS x kPS pairs with the crop half from a table: the survivors of a round keep
+// nn_query's order, so a tile's entries come in runs that share one crop point (what is left of
+// each group of 5). tab[u * RJ + w] = rigid_dist(run u of tile I, run w of tile J) is computed
+// once per run pair from the runs' own (bitwise-equal) coordinates, so the looked-up value is
+// bit-identical to rigid_tile_pairs' second rigid_dist; si[].v.y carries u * RJ, sj[].v.y w.
+template <bool EDGE>
+__device__ __forceinline__ void rigid_tile_pairs_tab(const RigidRec* __restrict__ si, const RigidRec* __restrict__ sj,
+                                                     const float* __restrict__ tab, int tx, int ty, float (&ra)[kPS],
+                                                     float (&ca)[kPS]) {
+  float ax[kPS], ay[kPS], az[kPS], cv[kPS];
+  int cj[kPS];
+#pragma unroll
+  for (int c = 0; c < kPS; ++c) {
+    const RigidRec q = sj[tx + 16 * c];
+    ax[c] = q.x.x; ay[c] = q.y.x; az[c] = q.z.x;
+    cv[c] = q.v.x;
+    cj[c] = __float_as_int(q.v.y);
+  }
+#pragma unroll 2
+  for (int r = 0; r < kPS; ++r) {
+    const RigidRec ci = si[ty + 16 * r];
+    const float* __restrict__ trow = tab + __float_as_int(ci.v.y);
+    float rs = 0.f;
+#pragma unroll
+    for (int c = 0; c < kPS; ++c) {
+      const float a = rigid_dist(ci.x.x, ci.y.x, ci.z.x, ax[c], ay[c], az[c]);
+      float v = fabsf(a - trow[cj[c]]);
+      if (EDGE) v = v * (cv[c] * ci.v.x);
+      rs += v;
+      ca[c] += v;
+    }
+    ra[r] = rs;
+  }
+}
+
+constexpr int kTab = 8192;  // run-pair table entries (32 KB of LDS)
+
 // Grid (T (T + 1) / 2, B) over kRT2 x kRT2 tile pairs I <= J (T = ceil(nmax / kRT2)), XCD-aware
 // (a crop's tile pairs share one XCD's L2); block 256 = 16 x 16 threads. As rigid_pair_kernel:
 // part[b][J][x] = sum over tile J of entry x of tile I, and for I != J part[b][I][y] for the
 // entries y of tile J; every slot written once, summed in tile order by rigid_reduce_kernel.
 // Fixed-order reductions (16-lane butterflies, then the 4 waves' column partials in wave order).
+// When the two tiles' crop-point runs give at most kTab run pairs (and use_tab), the crop
+// distances come from the run-pair table (rigid_tile_pairs_tab): one crop sqrt per run pair
+// instead of per entry pair; otherwise (a general candidate order, sparse survivors) both
+// distances per pair. Either way the pair values, and so the partial sums, are the same bits.
 __global__ __launch_bounds__(256) void rigid_pair2_kernel(const int32_t* __restrict__ nlist, int ldl,
                                                           const RigidRec* __restrict__ pts, int T,
-                                                          float* __restrict__ part) {
+                                                          float* __restrict__ part, int use_tab) {
   __shared__ RigidRec si[kRT2], sj[kRT2];
   __shared__ float red[4][kRT2];
+  __shared__ float tab[kTab];
+  __shared__ float rq[2][3][kRT2];  // the runs' crop points (tile I, tile J)
+  __shared__ int rcnt[2][4];        // runs starting in each wave's 64 entries
   const int3 lb = pk::xcd_block3();
   const int b = lb.y;
   const int n = nlist[b];
@@ -262,12 +306,75 @@ __global__ __launch_bounds__(256) void rigid_pair2_kernel(const int32_t* __restr
     (e2 < kRT2 ? si : sj)[e] = r;
   }
   __syncthreads();
+  bool tbl = false;
+  if (use_tab) {  // block-uniform
+    // runs of bitwise-equal crop points; entry tid of each tile (kRT2 == blockDim)
+    const int w = pk::wave_id(), lane = pk::lane_id();
+    bool head[2];
+    int loc[2];
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+      const RigidRec* s = sd ? sj : si;
+      const RigidRec c = s[tid];
+      bool h = tid == 0;
+      if (tid > 0) {
+        const RigidRec p = s[tid - 1];
+        h = __float_as_uint(c.x.y) != __float_as_uint(p.x.y) || __float_as_uint(c.y.y) != __float_as_uint(p.y.y) ||
+            __float_as_uint(c.z.y) != __float_as_uint(p.z.y);
+      }
+      const uint64_t bal = __ballot(h);
+      loc[sd] = __popcll(bal & ((1ull << lane) - 1ull));  // heads before this entry in its wave
+      if (lane == 0) rcnt[sd][w] = __popcll(bal);
+      head[sd] = h;
+    }
+    __syncthreads();
+    int rid[2], R[2];
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+      int off = 0, tot = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        off += q < w ? rcnt[sd][q] : 0;
+        tot += rcnt[sd][q];
+      }
+      rid[sd] = off + loc[sd] + (head[sd] ? 0 : -1);  // run of this entry
+      R[sd] = tot;
+      if (head[sd]) {
+        const RigidRec c = (sd ? sj : si)[tid];
+        rq[sd][0][rid[sd]] = c.x.y;
+        rq[sd][1][rid[sd]] = c.y.y;
+        rq[sd][2][rid[sd]] = c.z.y;
+      }
+    }
+    tbl = R[0] * R[1] <= kTab;
+    if (tbl) {
+      si[tid].v.y = __int_as_float(rid[0] * R[1]);
+      sj[tid].v.y = __int_as_float(rid[1]);
+    }
+    __syncthreads();
+    if (tbl) {
+      const int RJ = R[1], per = kRT2 / RJ;
+      const int cj = tid % RJ, r0 = tid / RJ;
+      if (r0 < per) {
+        const float qx = rq[1][0][cj], qy = rq[1][1][cj], qz = rq[1][2][cj];
+        for (int u = r0; u < R[0]; u += per)
+          tab[u * RJ + cj] = rigid_dist(rq[0][0][u], rq[0][1][u], rq[0][2][u], qx, qy, qz);
+      }
+      __syncthreads();
+    }
+  }
   const int tx = tid & 15, ty = tid >> 4;
   float ra[kPS], ca[kPS];
 #pragma unroll
   for (int r = 0; r < kPS; ++r) ra[r] = ca[r] = 0.f;
-  if ((J + 1) * kRT2 > n) rigid_tile_pairs<true>(si, sj, tx, ty, ra, ca);
-  else rigid_tile_pairs<false>(si, sj, tx, ty, ra, ca);
+  const bool edge = (J + 1) * kRT2 > n;
+  if (tbl) {
+    if (edge) rigid_tile_pairs_tab<true>(si, sj, tab, tx, ty, ra, ca);
+    else rigid_tile_pairs_tab<false>(si, sj, tab, tx, ty, ra, ca);
+  } else {
+    if (edge) rigid_tile_pairs<true>(si, sj, tx, ty, ra, ca);
+    else rigid_tile_pairs<false>(si, sj, tx, ty, ra, ca);
+  }
   float* P = part + (int64_t)b * T * ldl;
   // row sums of tile I over tile J: the 16 tx lanes are one DPP row (quad_perm / half-mirror /
   // mirror adds: VALU only, no LDS round trips); lane tx = 0's association order is fixed
@@ -922,7 +1029,7 @@ static int64_t rigid_part_bytes(int B, int nmax, int ldc) {
 
 #ifdef PK_DEVBUILD
 static int g_rigid_variant = 0;  // pkdev_rigidity_variant (A/B timing): 1 round 2's 64-tile gather path,
-                                 // 2 round 3's ungrouped first round
+                                 // 2 round 3's ungrouped first round, 3 no run-pair crop tables
 #else
 constexpr int g_rigid_variant = 0;
 #endif
@@ -976,7 +1083,8 @@ extern "C" int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* n
       PK_CHECK_LAUNCH();
       hipLaunchKernelGGL(rigid_reduce_kernel, g, dim3(256), 0, s, nin, ldc, partial, T1, kRG, score);
     } else if (packed) {
-      hipLaunchKernelGGL(rigid_pair2_kernel, dim3(T2 * (T2 + 1) / 2, B), dim3(256), 0, s, nin, ldc, pa, T2, partial);
+      hipLaunchKernelGGL(rigid_pair2_kernel, dim3(T2 * (T2 + 1) / 2, B), dim3(256), 0, s, nin, ldc, pa, T2, partial,
+                         (int)(g_rigid_variant != 3));
       PK_CHECK_LAUNCH();
       hipLaunchKernelGGL(rigid_reduce_kernel, g, dim3(256), 0, s, nin, ldc, partial, T2, kRT2, score);
     }

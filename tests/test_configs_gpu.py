@@ -164,6 +164,66 @@ def test_rigidity_filter_ragged_batch(device):
         _rigidity_parity(sc[0], sc[1], sc[2][:s], rows[i], int(n[i]), sc[3])
 
 
+def _rigid_dev(dl, variant, cand, ncand, cad, pc, thr):
+    """pk_rigidity_filter of the dev library under pkdev_rigidity_variant(variant): (survivor
+    rows, counts, the last round's scores)."""
+    from dpfm_amd import _lib
+    B, L, _ = cand.shape
+    dev = cand.device
+    la, lb = (torch.zeros((B, L), dtype=torch.int64, device=dev) for _ in range(2))
+    na, nb = (torch.empty((B,), dtype=torch.int32, device=dev) for _ in range(2))
+    score = torch.zeros((B, L), dtype=torch.float32, device=dev)
+    part = torch.empty((max(int(dl.pk_rigidity_filter_work_size(B, L, L)) // 4, 1),), dtype=torch.float32,
+                       device=dev)
+    old = dl.pkdev_rigidity_variant(variant)
+    try:
+        rc = dl.pk_rigidity_filter(_lib.ptr(cand), L, _lib.ptr(ncand), _lib.ptr(cad), cad.shape[1], _lib.ptr(pc),
+                                   pc.shape[1], _lib.ptr(thr), B, L, _lib.ptr(la), _lib.ptr(lb), _lib.ptr(na),
+                                   _lib.ptr(nb), _lib.ptr(score), _lib.ptr(part), _lib.stream(dev))
+        torch.cuda.synchronize()
+    finally:
+        dl.pkdev_rigidity_variant(old)
+    assert rc == 0
+    return lb.cpu(), nb.cpu(), score.cpu()
+
+
+@pytest.mark.parametrize("case", ["configs3", "ragged", "split_group"])
+def test_rigidity_run_tables_bit_identical(device, case):
+    """Rounds 2 / 3 look the crop distance up in a run-pair table when a tile pair's crop-point
+    runs are few (rigid_pair2_kernel): the pair values, scores and survivors must be the same bits
+    as with both distances per pair (pkdev_rigidity_variant 3), on the configs[3] size, a ragged
+    batch and a list with a split group."""
+    import ctypes
+    from dpfm_amd import _lib, ops
+    dl = _lib.dev_lib()
+    dl.pkdev_rigidity_variant.argtypes = [ctypes.c_int]
+    if case == "configs3":
+        scenes = [_rigid_scene(2048, 300 + b) for b in range(2)]
+        sizes = [s[2].shape[0] for s in scenes]
+    else:
+        sizes = [1, 257, 642, 1000, 1500] if case == "ragged" else [2000]
+        scenes = [_rigid_scene(max((s + 4) // 5, 1), 40 + i) for i, s in enumerate(sizes)]
+    Lc, V1 = max(sizes), max(sc[0].shape[0] for sc in scenes)
+    V2 = max(sc[1].shape[0] for sc in scenes)
+    cand = np.zeros((len(sizes), Lc, 2), dtype=np.int64)
+    for i, (s, sc) in enumerate(zip(sizes, scenes)):
+        cand[i, :s] = sc[2][:s]
+    if case == "split_group":
+        cand[0, 5 * 37 + 2, 1] = (cand[0, 5 * 37 + 2, 1] + 1) % 400
+    dcand = torch.from_numpy(cand).to(device)
+    ncand = torch.tensor(sizes, dtype=torch.int32, device=device)
+    dcad = torch.from_numpy(np.stack([np.pad(sc[0], ((0, V1 - sc[0].shape[0]), (0, 0))) for sc in scenes])).to(device)
+    dpc = torch.from_numpy(np.stack([np.pad(sc[1], ((0, V2 - sc[1].shape[0]), (0, 0))) for sc in scenes])).to(device)
+    thr = ops.rigidity_thresholds([sc[3] for sc in scenes], device)
+    r0, n0, s0 = _rigid_dev(dl, 0, dcand, ncand, dcad, dpc, thr)
+    r3, n3, s3 = _rigid_dev(dl, 3, dcand, ncand, dcad, dpc, thr)
+    assert torch.equal(n0, n3)
+    assert torch.equal(r0, r3)
+    for b in range(len(sizes)):  # the last round's scores over its input list (the round-2 survivors)
+        assert torch.equal(s0[b].view(torch.int32), s3[b].view(torch.int32)), b
+    assert int(n0.sum()) > 0
+
+
 @pytest.mark.parametrize("order", ["shuffled", "one_split_group"])
 def test_rigidity_filter_candidate_orders(device, order):
     """The first round shares one crop distance per pair of 5-candidate groups (nn_query's

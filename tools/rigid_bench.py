@@ -1,7 +1,8 @@
 """pk_rigidity_filter A/B timing (pkdev_rigidity_variant): 0 the production path (grouped first
-round), 2 round 3's path (ungrouped 128-tile first round), 1 round 2's 64-tile gather path;
-B crops x n = 5 V2 candidates, eager back-to-back launches.
-python tools/rigid_bench.py [V2 ...]"""
+round, run-pair crop tables in rounds 2 / 3), 3 without the tables, 2 round 3's path (ungrouped
+first round), 1 round 2's 64-tile gather path; B crops x n = 5 V2 candidates, eager back-to-back
+launches; every variant's survivors compared with variant 0's.
+RIGID_VARS=3,2,0 python tools/rigid_bench.py [V2 ...]"""
 import ctypes
 import os
 import sys
@@ -27,7 +28,8 @@ for V2 in [int(a) for a in sys.argv[1:]] or [1024, 2048]:
     ncand = torch.full((B,), cand.shape[1], dtype=torch.int32, device=dev)
     thr = ops.rigidity_thresholds([s[3] for s in scenes], dev)
     res = {}
-    for var in (2, 0):
+    variants = [int(v) for v in os.environ.get("RIGID_VARS", "3,2,0").split(",")]
+    for var in variants:
         L.pkdev_rigidity_variant(var)
         for _ in range(3):
             rows, n = ops.rigidity_filter(cand, ncand, cad, pc, thr)
@@ -45,7 +47,8 @@ for V2 in [int(a) for a in sys.argv[1:]] or [1024, 2048]:
         flop = 10.0 * B * nl * nl  # the bench's accounting: ~20 flop per unordered pair of round 1
         print(f"V2={V2} n={nl} variant={var}: {ms * 1e3:8.1f} us per filter (3 rounds), "
               f"{flop / ms / 1e9:6.1f} TFLOP/s = {flop / ms / 1e9 / 157.3:.3f} of f32 VALU; survivors {int(n.sum())}")
-    same = torch.equal(res[0][1], res[2][1]) and all(
-        torch.equal(res[0][0][b, :res[0][1][b]], res[2][0][b, :res[2][1][b]]) for b in range(B))
-    print(f"V2={V2}: variants give identical survivors: {same}")
+    for var in variants:
+        same = torch.equal(res[0][1], res[var][1]) and all(
+            torch.equal(res[0][0][b, :res[0][1][b]], res[var][0][b, :res[var][1][b]]) for b in range(B))
+        print(f"V2={V2}: variant {var} survivors identical to variant 0's: {same}")
     L.pkdev_rigidity_variant(0)
