@@ -217,6 +217,221 @@ __global__ __launch_bounds__(256) void spec_expand_kernel(const float* __restric
   }
 }
 
+// ---- Round 4: passes 1 and 3 on the f32 MFMA (v_mfma_f32_16x16x4_f32). The scalar-FMA forms
+// above ran at 0.8-1.2 TB/s (0.10-0.15 of HBM) on these 8-17 MB passes; the products are 2 N K C
+// flops per crop, small next to the bytes, so the MFMA forms are bound by the row streams.
+// Lane map as in attention.hip: A[i = l & 15][k = l >> 4], B[k = l >> 4][j = l & 15],
+// D[4 (l >> 4) + rr][l & 15]. Every lane loads whole float4s of a row, and the matrix indices are
+// permuted to match (documented per kernel), so no operand goes through LDS shuffles.
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// pass 1: part[b, s] (64 x 64) over the 64 rows of slab s; grid (S, B), block 256 = 4 waves.
+// Wave w contracts the 16 rows r0 + 16 w + 4 q + g (K-steps q < 4, g = l >> 4); lane
+// (u = l & 15, g) loads the float4s Phi[r][4u .. 4u+3] and w_r x[r][4u .. 4u+3] once. Tile
+// (kt, ct) holds the output rows k = 4 i + kt (A = component kt of the Phi float4 of lane (i, g))
+// and columns c = 4 j + ct (B = component ct of the x float4 of lane (j, g)): register rr of
+// tile (kt, ct) in lane (j, g) is the wave's part[4 (4 g + rr) + kt][4 j + ct]. The four waves'
+// 64 x 64 partials meet in LDS and are added in wave order.
+__global__ __launch_bounds__(256) void spec_reduce_mfma_kernel(const float* __restrict__ x, int ldx,
+                                                               const float* __restrict__ mass,
+                                                               const float* __restrict__ evecs, int N, int S,
+                                                               float* __restrict__ part) {
+  __shared__ float4 red[4][kKC * kKC / 4];  // [wave][k][c / 4]
+  const int s = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63, u = l & 15, g = l >> 4;
+  const float* __restrict__ phi = evecs + (int64_t)b * N * kKC;
+  const float* __restrict__ xb = x + (int64_t)b * N * ldx;
+  const float* __restrict__ mb = mass ? mass + (int64_t)b * N : nullptr;
+  const int rw = s * kRows + 16 * w;
+  float4 pv[4], xv[4];
+  float wv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = rw + 4 * q + g;
+    const int rc = r < N ? r : N - 1;  // clamped, then zeroed
+    pv[q] = reinterpret_cast<const float4*>(phi + (int64_t)rc * kKC)[u];
+    xv[q] = reinterpret_cast<const float4*>(xb + (int64_t)rc * ldx)[u];
+    wv[q] = mb ? mb[rc] : 1.f;
+  }
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) acc[kt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const bool ok = rw + 4 * q + g < N;
+    const float wr = ok ? wv[q] : 0.f;
+    const float a[4] = {pv[q].x, pv[q].y, pv[q].z, pv[q].w};
+    const float xs[4] = {mb ? xv[q].x * wr : (ok ? xv[q].x : 0.f), mb ? xv[q].y * wr : (ok ? xv[q].y : 0.f),
+                         mb ? xv[q].z * wr : (ok ? xv[q].z : 0.f), mb ? xv[q].w * wr : (ok ? xv[q].w : 0.f)};
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) acc[kt][ct] = mfma4(a[kt], xs[ct], acc[kt][ct]);
+  }
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+      red[w][(4 * (4 * g + rr) + kt) * (kKC / 4) + u] =
+          make_float4(acc[kt][0][rr], acc[kt][1][rr], acc[kt][2][rr], acc[kt][3][rr]);
+  __syncthreads();
+  float4* __restrict__ o = reinterpret_cast<float4*>(part + ((int64_t)b * S + s) * kKC * kKC);
+#pragma unroll
+  for (int j = 0; j < kKC * kKC / 4 / 256; ++j) {
+    const int e = tid + 256 * j;
+    const float4 v0 = red[0][e], v1 = red[1][e], v2 = red[2][e], v3 = red[3][e];
+    o[e] = make_float4(((v0.x + v1.x) + v2.x) + v3.x, ((v0.y + v1.y) + v2.y) + v3.y, ((v0.z + v1.z) + v2.z) + v3.z,
+                       ((v0.w + v1.w) + v2.w) + v3.w);
+  }
+}
+
+// pass 2 for the MFMA passes: spec_combine_kernel's sums over 4 x as many blocks (grid (B, 4),
+// block 1024: thread (k = 16 y + (tid >> 6), c = tid & 63) sums its one coefficient over the S
+// slabs in slab order, fp64, 8 slabs' loads in flight). gt (backward): block y's partial over its
+// 16 rows k goes to row 16 y of its crop's slab 0 (read by this block only, consumed before the
+// barrier); spec_expand_mfma_kernel adds the 4 per crop, then the crops, in order.
+__global__ __launch_bounds__(1024) void spec_combine4_kernel(float* __restrict__ part, int S,
+                                                             const float* __restrict__ evals,
+                                                             float* __restrict__ t, int clamp_t, int write_t,
+                                                             float* __restrict__ raw, float* __restrict__ scaled,
+                                                             const float* __restrict__ saved, int want_gt) {
+  __shared__ double gsum[16][kKC];
+  const int b = blockIdx.x, y = blockIdx.y, tid = threadIdx.x;
+  const int c = tid & 63, k = 16 * y + (tid >> 6);
+  const float* pb = part + (int64_t)b * S * kKC * kKC + k * kKC + c;
+  const float tc = clamp_t ? fmaxf(t[c], 1e-8f) : t[c];
+  double v = 0.0;
+  int s = 0;
+  for (; s + 8 <= S; s += 8) {
+    float ld[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ld[q] = pb[(int64_t)(s + q) * kKC * kKC];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v += (double)ld[q];
+  }
+  for (; s < S; ++s) v += (double)pb[(int64_t)s * kKC * kKC];
+  const float lam = evals[b * kKC + k];
+  const float E = expf(-lam * tc);
+  const int64_t o = (int64_t)b * kKC * kKC + k * kKC + c;
+  const float vf = (float)v;
+  if (raw) raw[o] = vf;
+  scaled[o] = E * vf;
+  if (write_t && b == 0 && y == 0 && tid < kKC) t[c] = tc;
+  if (want_gt) {
+    gsum[tid >> 6][c] = -(double)lam * (double)E * ((double)saved[o] * v);
+    __syncthreads();
+    if (tid < kKC) {
+      double a = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) a += gsum[q][c];
+      part[(int64_t)b * S * kKC * kKC + (16 * y) * kKC + c] = (float)a;
+    }
+  }
+}
+
+// pass 3: y[r, :] = Phi[r, :] · coef (· mass[r]) (+ y). grid (ceil(N / 64), B), block 256: wave w
+// owns the 16 rows r0 + 16 w + (0..15), all 64 columns (4 tiles). Lane (i = l & 15, g = l >> 4)
+// loads Phi[r][16 t + 4 g .. +3] (t < 4), so K-step (t, e) pairs A[i][g] = Phi[r][16 t + 4 g + e]
+// with B[g][j] = coef[16 t + 4 g + e][4 j + ct] (one ds_read_b128 of the LDS copy of coef gives
+// all 4 tiles); D register rr of tile ct in lane (j, g) is y[r0 + 16 w + 4 g + rr][4 j + ct].
+__global__ __launch_bounds__(256) void spec_expand_mfma_kernel(const float* __restrict__ evecs,
+                                                               const float* __restrict__ coef,
+                                                               const float* __restrict__ mass, int N,
+                                                               float* __restrict__ y, int ldy, int accumulate,
+                                                               const float* __restrict__ gtb, int64_t gt_stride,
+                                                               float* __restrict__ gt) {
+  __shared__ float4 scoef[kKC * kKC / 4];  // [k][c / 4]
+  const int tile = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63, u = l & 15, g = l >> 4;
+  const float* __restrict__ cb = coef + (int64_t)b * kKC * kKC;
+  {
+    float4 cv[kKC * kKC / 4 / 256];
+#pragma unroll
+    for (int j = 0; j < kKC * kKC / 4 / 256; ++j) cv[j] = reinterpret_cast<const float4*>(cb)[tid + 256 * j];
+#pragma unroll
+    for (int j = 0; j < kKC * kKC / 4 / 256; ++j) scoef[tid + 256 * j] = cv[j];
+  }
+  const int rw = tile * 64 + 16 * w;  // this wave's first row
+  const float* __restrict__ phi = evecs + (int64_t)b * N * kKC;
+  float4 pv[4];
+  {
+    const int r = rw + u < N ? rw + u : N - 1;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) pv[t] = reinterpret_cast<const float4*>(phi + (int64_t)r * kKC)[4 * t + g];
+  }
+  // the epilogue's operands in flight during the products
+  float wr[4];
+  float4 old[4];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int r = rw + 4 * g + rr < N ? rw + 4 * g + rr : N - 1;
+    wr[rr] = mass ? mass[(int64_t)b * N + r] : 1.f;
+    old[rr] = accumulate ? reinterpret_cast<const float4*>(y + ((int64_t)b * N + r) * ldy)[u]
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+  f32x4 acc[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float pa[4] = {pv[t].x, pv[t].y, pv[t].z, pv[t].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float4 bv = scoef[(16 * t + 4 * g + e) * (kKC / 4) + u];
+      acc[0] = mfma4(pa[e], bv.x, acc[0]);
+      acc[1] = mfma4(pa[e], bv.y, acc[1]);
+      acc[2] = mfma4(pa[e], bv.z, acc[2]);
+      acc[3] = mfma4(pa[e], bv.w, acc[3]);
+    }
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int r = rw + 4 * g + rr;
+    if (r >= N) continue;
+    const float m = wr[rr];
+    float4 v = make_float4(acc[0][rr] * m, acc[1][rr] * m, acc[2][rr] * m, acc[3][rr] * m);
+    if (accumulate) {
+      const float4 o = old[rr];
+      v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+    }
+    reinterpret_cast<float4*>(y + ((int64_t)b * N + r) * ldy)[u] = v;
+  }
+  // after this block's rows: one block sums dL/dt, off the other blocks' critical path
+  if (gt && tile == 0 && b == 0 && tid < kKC) {  // spec_combine4_kernel's 4 partials per crop
+    float a = 0.f;
+    const int nq = (int)gridDim.y;
+    for (int q0 = 0; q0 < nq; q0 += 8) {  // 8 crops' 32 loads in flight, added in crop order
+      float v[8][4];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float* gq = gtb + (int64_t)(q0 + q < nq ? q0 + q : q0) * gt_stride + tid;
+#pragma unroll
+        for (int y = 0; y < 4; ++y) v[q][y] = gq[16 * kKC * y];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q0 + q < nq) a += ((v[q][0] + v[q][1]) + v[q][2]) + v[q][3];
+    }
+    gt[tid] = a;
+  }
+}
+
+#ifdef PK_DEVBUILD
+static bool spec_scalar() {  // PK_SPEC_SCALAR=1: round 1's scalar-FMA passes 1 and 3 (A/B)
+  static const bool v = getenv("PK_SPEC_SCALAR") != nullptr && atoi(getenv("PK_SPEC_SCALAR")) != 0;
+  return v;
+}
+#else
+constexpr bool spec_scalar() { return false; }
+#endif
+
 }  // namespace
 
 // mode 0 (forward): in = x, out = y, raw = spec (saved for backward), reduce weights = mass.
@@ -233,15 +448,28 @@ extern "C" int pk_spectral_diffusion(const float* in, int ld_in, const float* ma
   PK_REQUIRE(mode == 0 || (saved && gt));
   hipStream_t s = pk::as_stream(stream);
   const int S = (N + kRows - 1) / kRows;
-  hipLaunchKernelGGL(spec_reduce_kernel, dim3(S, B), dim3(256), 0, s, in, ld_in, mode == 0 ? mass : nullptr,
-                     evecs, N, S, work);
+  if (spec_scalar())
+    hipLaunchKernelGGL(spec_reduce_kernel, dim3(S, B), dim3(256), 0, s, in, ld_in, mode == 0 ? mass : nullptr,
+                       evecs, N, S, work);
+  else
+    hipLaunchKernelGGL(spec_reduce_mfma_kernel, dim3(S, B), dim3(256), 0, s, in, ld_in,
+                       mode == 0 ? mass : nullptr, evecs, N, S, work);
   PK_CHECK_LAUNCH();
-  hipLaunchKernelGGL(spec_combine_kernel, dim3(B), dim3(1024), 0, s, work, S, evals, t, clamp_t,
-                     (int)(clamp_t && mode == 0), raw, scaled, mode == 1 ? saved : nullptr, (int)(mode == 1));
+  if (spec_scalar())
+    hipLaunchKernelGGL(spec_combine_kernel, dim3(B), dim3(1024), 0, s, work, S, evals, t, clamp_t,
+                       (int)(clamp_t && mode == 0), raw, scaled, mode == 1 ? saved : nullptr, (int)(mode == 1));
+  else
+    hipLaunchKernelGGL(spec_combine4_kernel, dim3(B, 4), dim3(1024), 0, s, work, S, evals, t, clamp_t,
+                       (int)(clamp_t && mode == 0), raw, scaled, mode == 1 ? saved : nullptr, (int)(mode == 1));
   PK_CHECK_LAUNCH();
-  hipLaunchKernelGGL(spec_expand_kernel, dim3((N + 63) / 64, B), dim3(256), 0, s, evecs, scaled,
-                     mode == 1 ? mass : nullptr, N, out, ld_out, accumulate, work, (int64_t)S * kKC * kKC,
-                     mode == 1 ? gt : nullptr);
+  if (spec_scalar())
+    hipLaunchKernelGGL(spec_expand_kernel, dim3((N + 63) / 64, B), dim3(256), 0, s, evecs, scaled,
+                       mode == 1 ? mass : nullptr, N, out, ld_out, accumulate, work, (int64_t)S * kKC * kKC,
+                       mode == 1 ? gt : nullptr);
+  else
+    hipLaunchKernelGGL(spec_expand_mfma_kernel, dim3((N + 63) / 64, B), dim3(256), 0, s, evecs, scaled,
+                       mode == 1 ? mass : nullptr, N, out, ld_out, accumulate, work, (int64_t)S * kKC * kKC,
+                       mode == 1 ? gt : nullptr);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
