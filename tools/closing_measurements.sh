@@ -1,7 +1,8 @@
 #!/bin/bash
 # Closing measurements of a round: the headline train bench (with CPU baseline), inference at
 # configs[1] and at the configs[3] shard, (f1) operators, the step kernel trace, and the PMC
-# traffic passes. Each step under its own limit; the first failure ends the script.
+# traffic passes (SKIP_OPS / SKIP_PMC: leave those two out). Each step under its own limit; the first
+# failure ends the script.
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-close}
 mkdir -p $O
@@ -9,8 +10,9 @@ step() { local name=$1 to=$2; shift 2; timeout -k 10 $to "$@" > $O/$name.out 2> 
 step train 600 python3 -u bench.py
 step infer 300 python3 -u bench.py --mode infer
 step infer2048 300 python3 -u bench.py --mode infer --points 2048 --no-cpu-baseline
-step ops 400 python3 -u bench.py --mode operators --batch 8 --steps 3 --warmup 1
+[ -n "$SKIP_OPS" ] || step ops 400 python3 -u bench.py --mode operators --batch 8 --steps 3 --warmup 1
 step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline-probe
 find $O/prof -type f ! -name "*stats.csv" -delete
+[ -n "$SKIP_PMC" ] && exit 0
 TAG=${TAG:-close}/pmc bash tools/pmc_step.sh > $O/pmc.out 2>&1 || { tail -20 $O/pmc.out; exit 1; }
 tail -5 $O/pmc.out
