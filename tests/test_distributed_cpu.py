@@ -148,7 +148,9 @@ def _gather_worker(rank, world, port, q):
     local = {"T": idx.double()[:, None, None].expand(-1, 4, 4).contiguous(), "ir": idx.float() / 10,
              "n_corr": idx.int(), "metrics": idx.double()[:, None].expand(-1, 7).contiguous()}
     out = gather_results(local, world=world)
-    q.put((rank, {k: v.clone() for k, v in out.items()}))
+    # numpy copies: a torch tensor in a queue is a shared-memory handle the parent fetches from this
+    # process, which may already have exited (ConnectionResetError)
+    q.put((rank, {k: v.numpy().copy() for k, v in out.items()}))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -168,7 +170,7 @@ def test_sharded_inference_gather_cpu():
     for p in procs:
         p.join(timeout=60)
     for r in range(2):
-        out = res[r]
+        out = {k: torch.from_numpy(v) for k, v in res[r].items()}
         assert torch.equal(out["n_corr"], torch.arange(7).int())
         assert torch.equal(out["T"][:, 0, 0], torch.arange(7).double())
         assert torch.equal(out["ir"], torch.arange(7).float() / 10)
