@@ -701,12 +701,13 @@ __global__ __launch_bounds__(256) void ir_kernel(const int64_t* __restrict__ pai
                                                  int col_cad, int col_pc, const int32_t* __restrict__ npairs,
                                                  const float* __restrict__ cad, int ldcad,
                                                  const float* __restrict__ pcal, int ldpc,
-                                                 const float* __restrict__ thr, float* __restrict__ ir) {
+                                                 const float* __restrict__ thr, float* __restrict__ ir,
+                                                 int32_t* __restrict__ status) {
   __shared__ int ws[4];
   const int b = blockIdx.x;
   const int n = npairs[b];
   const float t = thr[b];
-  int c = 0;
+  int c = 0, bad = 0;
   for (int k = threadIdx.x; k < n; k += 256) {
     const int64_t* pr = pairs + (int64_t)b * ldp * 2;
     int64_t ci, pi;
@@ -717,12 +718,19 @@ __global__ __launch_bounds__(256) void ir_kernel(const int64_t* __restrict__ pai
       ci = pr[col_cad * (pair_stride == 1 ? ldp : 1) + k * (pair_stride == 1 ? 1 : 2)];
       pi = pr[col_pc * (pair_stride == 1 ? ldp : 1) + k * (pair_stride == 1 ? 1 : 2)];
     }
+    // an index outside its array is not read: the pair counts as an outlier and status[b] = 1
+    if (ci < 0 || ci >= ldcad || pi < 0 || pi >= ldpc) {
+      bad = 1;
+      continue;
+    }
     const float* a = cad + ((int64_t)b * ldcad + ci) * 3;
     const float* p = pcal + ((int64_t)b * ldpc + pi) * 3;
     const float dx = a[0] - p[0], dy = a[1] - p[1], dz = a[2] - p[2];
     const float d = __fsqrt_rn((dx * dx + dy * dy) + dz * dz);
     c += d < t ? 1 : 0;
   }
+  bad = __syncthreads_or(bad);
+  if (status && threadIdx.x == 0) status[b] = bad;
   c = pk::wave_sum_i32_s(c);
   if (pk::lane_id() == 0) ws[pk::wave_id()] = c;
   __syncthreads();
@@ -1125,7 +1133,7 @@ extern "C" int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* n
 
 extern "C" int pk_inlier_ratio(const int64_t* pairs, int ldp, int layout, const int32_t* npairs, const float* cad,
                                int ldcad, const float* pc_aligned, int ldpc, const float* thr, int B, float* ir,
-                               void* stream) {
+                               int32_t* status, void* stream) {
   PK_REQUIRE(B >= 0 && layout >= 0 && layout <= 2);
   if (B == 0) return PK_OK;
   PK_REQUIRE(pairs && npairs && cad && pc_aligned && thr && ir);
@@ -1133,7 +1141,7 @@ extern "C" int pk_inlier_ratio(const int64_t* pairs, int ldp, int layout, const 
   // layout 2: [B, ldp] CAD index of crop point k (a point map; pc index = k)
   hipLaunchKernelGGL(ir_kernel, dim3(B), dim3(256), 0, pk::as_stream(stream), pairs, ldp,
                      layout == 2 ? 0 : layout == 1 ? 1 : 2, 0, 1,
-                     npairs, cad, ldcad, pc_aligned, ldpc, thr, ir);
+                     npairs, cad, ldcad, pc_aligned, ldpc, thr, ir, status);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -628,14 +628,28 @@ __global__ __launch_bounds__(256) void gather_transform_kernel(
     const double* __restrict__ pcd, const int64_t* __restrict__ off, const int64_t* __restrict__ idx,
     int idx_stride, const int32_t* __restrict__ npoint, const int64_t* __restrict__ out_off,
     const double* __restrict__ R, const double* __restrict__ t, double* __restrict__ sel64,
-    double* __restrict__ align64, float* __restrict__ sel32) {
+    double* __restrict__ align64, float* __restrict__ sel32, int32_t* __restrict__ status) {
   const int b = blockIdx.y;
   const int j = blockIdx.x * 256 + threadIdx.x;
   const int np = npoint[b];
   const int cnt = np < 0 ? -np : np;
+  const int64_t nb = off[b + 1] - off[b];
+  if (status && blockIdx.x == 0) {  // the crop's index check (written for every crop: no init needed)
+    int bad = 0;
+    if (np >= 0)
+      for (int k = threadIdx.x; k < cnt; k += 256) {
+        const int64_t i = idx[(int64_t)b * idx_stride + k];
+        bad |= (i < 0 || i >= nb) ? 1 : 0;
+      }
+    bad = __syncthreads_or(bad);
+    if (threadIdx.x == 0) status[b] = bad;
+  }
   if (j >= cnt) return;
-  const int64_t src = off[b] + (np < 0 ? j : idx[(int64_t)b * idx_stride + j]);
-  const double x = pcd[3 * src], y = pcd[3 * src + 1], z = pcd[3 * src + 2];
+  const int64_t i = np < 0 ? j : idx[(int64_t)b * idx_stride + j];
+  const bool inr = i >= 0 && i < nb;  // an out-of-range index is not read: its outputs are NaN
+  const int64_t src = off[b] + (inr ? i : 0);
+  const double nan = __builtin_nan("");
+  const double x = inr ? pcd[3 * src] : nan, y = inr ? pcd[3 * src + 1] : nan, z = inr ? pcd[3 * src + 2] : nan;
   const double* Rb = R + 9 * b;  // row-major R_m2c
   const double* tb = t + 3 * b;
   const int64_t w = out_off[b] + j;
@@ -786,13 +800,14 @@ extern "C" int pk_fps_npoint(const int64_t* off, int B, int fixed, int limit, ui
 extern "C" int pk_gather_transform(const double* pcd, const int64_t* off, int B, const int64_t* idx,
                                    int idx_stride, const int32_t* npoint, int npmax,
                                    const int64_t* out_off, const double* R, const double* t,
-                                   double* sel64, double* align64, float* sel32, void* stream) {
+                                   double* sel64, double* align64, float* sel32, int32_t* status,
+                                   void* stream) {
   PK_REQUIRE(B >= 0 && npmax >= 0);
-  if (B == 0 || npmax == 0) return PK_OK;
+  if (B == 0) return PK_OK;
   PK_REQUIRE(pcd && off && npoint && out_off && R && t);
-  hipLaunchKernelGGL(gather_transform_kernel, dim3((npmax + 255) / 256, B), dim3(256), 0,
+  hipLaunchKernelGGL(gather_transform_kernel, dim3(std::max(1, (npmax + 255) / 256), B), dim3(256), 0,
                      pk::as_stream(stream), pcd, off, idx, idx_stride, npoint, out_off, R, t, sel64,
-                     align64, sel32);
+                     align64, sel32, status);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -307,205 +307,6 @@ struct Top1x4 {
   int t[4];
 };
 
-// kCH row tiles of one LDS chunk against this wave's column tile
-// (all kCH fragments are read from LDS before the first MFMA: one LDS latency per chunk instead
-// of one per tile, and kCH independent accumulation chains for the MFMA pipe)
-template <int MODE>
-__device__ __forceinline__ void chunk_dist(const char* rb, const float* nb, const BOp<MODE>& bo, int lane,
-                                           float (&d)[kCH][4]) {
-  Frag<MODE> f[kCH];
-#pragma unroll
-  for (int t = 0; t < kCH; ++t) read_frag<MODE>(rb + tile_bytes(MODE) * t, nb + t * 16, lane, f[t]);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int t = 0; t < kCH; ++t) tile_dist<MODE>(f[t], bo, d[t]);
-}
-
-// the selection over one chunk's distances (tiles c0 .. c0 + kCH - 1)
-template <int TOPK>
-__device__ __forceinline__ void chunk_select(const float (&d)[kCH][4], int c0, int g, TopK<TOPK>& best, Top1x4& b4) {
-  if constexpr (TOPK == 1) {
-    constexpr int kClamp = 0x0da24260;  // bits of 1e-30f: clamp_min(1e-30) (cdist mm path)
-#pragma unroll
-    for (int t = 0; t < kCH; ++t) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = max(__float_as_int(d[t][r]), kClamp);
-        const int m = (key - b4.k[r]) >> 31;  // -1 iff key < best (both in [kClamp, 0x7fffffff])
-        b4.t[r] = (m & (c0 + t)) | (~m & b4.t[r]);
-        b4.k[r] = min(key, b4.k[r]);
-      }
-    }
-  } else {
-#pragma unroll
-    for (int t = 0; t < kCH; ++t) epilogue<TOPK>(d[t], (c0 + t) * 16 + 4 * g, best);
-  }
-}
-
-// grid (B * NCG * RS) (1-D, XCD-aware), block 256. Block = (crop b, column group cg: wave w
-// takes column tile 4 cg + w, row split rs: row tiles [tb, te) of the crop's valid ones).
-template <int TOPK, int MODE>
-__global__ __launch_bounds__(64 * kWaves) void fd_main_kernel(
-    const char* __restrict__ A, const char* __restrict__ Bq, const float* __restrict__ nA,
-    const float* __restrict__ nB, const int32_t* __restrict__ n1, const int32_t* __restrict__ n2, int T1, int T2,
-    int V2max, int NCG, int RS, int64_t* __restrict__ out_idx, float* __restrict__ out_dist,
-    float* __restrict__ part_v, int32_t* __restrict__ part_i) {
-  constexpr int TB = tile_bytes(MODE);
-  __shared__ __attribute__((aligned(16))) char ring[2][kCH][TB];
-  __shared__ __attribute__((aligned(16))) float nring[2][kCH][16];
-  const int per = NCG * RS;
-  const int B = (int)(gridDim.x / per);
-  int b, k;
-  {  // all blocks of crop b on XCD b % 8 (hardware block L lands on XCD L % 8) when B % 8 == 0
-    const int L = blockIdx.x;
-    if ((B & 7) == 0) {
-      const int x8 = L & 7, q = L >> 3;
-      b = x8 + 8 * (q / per);
-      k = q - (q / per) * per;
-    } else {
-      b = L / per;
-      k = L - b * per;
-    }
-  }
-  const int cg = k % NCG, rs = k / NCG;
-  const int lane = pk::lane_id(), w = pk::wave_id();
-  const int g = lane >> 4, c16 = lane & 15;
-  const int ct = cg * kWaves + w;  // this wave's column tile
-  const int N1 = n1[b], N2 = n2[b];
-  const int nt = (N1 + 15) >> 4;
-  const int tb = (nt * rs) / RS, te = (nt * (rs + 1)) / RS;
-  const bool col_ok = ct < T2 && ct * 16 < N2;
-  BOp<MODE> bo;
-  if (col_ok) {
-    const char* bt = Bq + ((int64_t)b * T2 + ct) * TB;
-    if constexpr (MODE == 0) {
-      const float4* p = reinterpret_cast<const float4*>(bt + lane * 32);
-      const float4 u = p[0], v = p[1];
-      bo.b[0] = u.x; bo.b[1] = u.y; bo.b[2] = u.z; bo.b[3] = u.w;
-      bo.b[4] = v.x; bo.b[5] = v.y; bo.b[6] = v.z; bo.b[7] = v.w;
-    } else {
-      bo.hi = *reinterpret_cast<const bf16x8*>(bt + lane * 16);
-      if constexpr (MODE == 2) bo.lo = *reinterpret_cast<const bf16x8*>(bt + 1024 + lane * 16);
-      bo.n = nB[((int64_t)b * T2 + ct) * 16 + c16];
-    }
-  } else {
-    if constexpr (MODE == 0) {
-#pragma unroll
-      for (int s = 0; s < 8; ++s) bo.b[s] = 0.f;
-    } else {
-      bo.hi = bf16x8{};
-      if constexpr (MODE == 2) bo.lo = bf16x8{};
-      bo.n = 0.f;
-    }
-  }
-  TopK<TOPK> best;
-  best.init();
-  Top1x4 b4;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    b4.k[r] = 0x7f800000;  // +inf: never replaced by an equal key
-    b4.t[r] = 0x7fffffff;
-  }
-  const char* At = A + (int64_t)b * T1 * TB;
-  const float* nAt = MODE != 0 ? nA + (int64_t)b * T1 * 16 : nullptr;
-  // staging: a chunk of kCH tiles = kCH * TB bytes, 16 B per thread per step
-  constexpr int VPT = kCH * TB / 16 / (64 * kWaves);  // float4s per thread per chunk
-  float4 stage[VPT];
-  float nst = 0.f;  // one norm per thread (threads < kCH * 16)
-  // (unconditional loads at a clamped element: a guarded load would put an
-  // exec-mask branch and a wait for it inside the MFMA loop)
-  // exec-mask branch and a wait for it inside the MFMA loop); the padding select happens at the
-  // LDS store, after the chunk's MFMAs, so nothing reads the loaded registers early
-  int lim = 0;
-  auto gload = [&](int c0, int cn) {
-    const float4* src = reinterpret_cast<const float4*>(At + (int64_t)c0 * TB);
-    lim = cn * TB / 16;
-#pragma unroll
-    for (int v = 0; v < VPT; ++v) stage[v] = src[min((int)threadIdx.x + 64 * kWaves * v, lim - 1)];
-    if (MODE != 0 && threadIdx.x < kCH * 16) nst = nAt[(int64_t)c0 * 16 + min((int)threadIdx.x, cn * 16 - 1)];
-  };
-  auto lstore = [&](int buf) {
-    float4* dst = reinterpret_cast<float4*>(&ring[buf][0][0]);
-#pragma unroll
-    for (int v = 0; v < VPT; ++v) {
-      const int e = threadIdx.x + 64 * kWaves * v;
-      // past the row part: padding rows (+inf |x|^2 slot in mode 0: lane group 2, k = 30)
-      const int q = e % (TB / 16);
-      const bool inf_slot = MODE == 0 && (q & 1) && (q >> 5) == 2;
-      const bool in = e < lim;
-      const float4 x = stage[v];
-      dst[e] = make_float4(in ? x.x : 0.f, in ? x.y : 0.f, in ? x.z : 0.f,
-                           in ? x.w : (inf_slot ? __builtin_huge_valf() : 0.f));
-    }
-    if (MODE != 0 && threadIdx.x < kCH * 16)
-      (&nring[buf][0][0])[threadIdx.x] = (int)threadIdx.x < lim / (TB / 16) * 16 ? nst : __builtin_huge_valf();
-  };
-  const int nch = (te - tb + kCH - 1) / kCH;
-  if (nch > 0) {
-    gload(tb, min(kCH, te - tb));
-    lstore(0);
-  }
-  __syncthreads();
-  // vmcnt(0) on every path into the loop (the column operand's loads included): otherwise the
-  // wait counter pass keeps them pending at the loop header and waits for the next chunk's
-  // loads inside the MFMA loop
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-  // software pipeline: the selection over chunk ci - 1 (registers) runs beside the MFMAs of
-  // chunk ci; dp starts as +inf (never selected)
-  float dp[kCH][4];
-#pragma unroll
-  for (int t = 0; t < kCH; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dp[t][r] = __builtin_huge_valf();
-  int cp = 0;
-  for (int ci = 0; ci < nch; ++ci) {
-    const int c0 = tb + ci * kCH;
-    if (ci + 1 < nch) gload(c0 + kCH, min(kCH, te - c0 - kCH));
-    if (col_ok) {
-      float d[kCH][4];
-      chunk_dist<MODE>(&ring[ci & 1][0][0], &nring[ci & 1][0][0], bo, lane, d);
-      chunk_select<TOPK>(dp, cp, g, best, b4);
-#pragma unroll
-      for (int t = 0; t < kCH; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dp[t][r] = d[t][r];
-      cp = c0;
-    }
-    if (ci + 1 < nch) lstore((ci + 1) & 1);
-    __syncthreads();
-  }
-  if (!col_ok) return;
-  chunk_select<TOPK>(dp, cp, g, best, b4);
-  if constexpr (TOPK == 1) {  // the 4 row offsets: smallest value, ties lowest row
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = b4.t[r] == 0x7fffffff ? 0x7fffffff : b4.t[r] * 16 + 4 * g + r;
-      const float v = __int_as_float(b4.k[r]);
-      const bool take = v < best.v[0] || (v == best.v[0] && row < best.i[0]);
-      best.v[0] = take ? v : best.v[0];
-      best.i[0] = take ? row : best.i[0];
-    }
-  }
-  lanegroup_merge<TOPK>(best);
-  const int j = ct * 16 + c16;
-  if (g != 0 || j >= N2) return;
-  if (RS == 1) {
-    const int64_t o = ((int64_t)b * V2max + j) * TOPK;
-#pragma unroll
-    for (int q = 0; q < TOPK; ++q) {
-      out_idx[o + q] = best.i[q] == 0x7fffffff ? -1 : best.i[q];
-      if (out_dist) out_dist[o + q] = sqrtf(best.v[q]);
-    }
-  } else {
-    const int64_t o = (((int64_t)b * RS + rs) * V2max + j) * TOPK;
-#pragma unroll
-    for (int q = 0; q < TOPK; ++q) {
-      part_v[o + q] = best.v[q];
-      part_i[o + q] = best.i[q];
-    }
-  }
-}
-
 // The main pass without LDS staging (the default; PK_FD_DIRECT=0 selects the LDS-ring pass
 // above). Block = 4 waves = 2 column pairs x 2 row halves: wave (wc, wr) takes column tiles
 // 4 cg + 2 wc and 4 cg + 2 wc + 1 and half wr of the block's row tiles, reading the rows' MFMA
@@ -687,40 +488,48 @@ __global__ __launch_bounds__(64 * kWaves) void fd_main_direct_kernel(
   }
 }
 
-// The fused fp32 pass (mode 0, the default since round 4): prep and main in ONE launch, no
-// operand round trip through HBM. Block = NW waves = (crop b, column group cg, row part rs);
-// wave w owns column tiles CT * (NW cg + w) + c, c < CT (their B operands, the y side, stay in
-// registers for the whole launch) and every wave streams the block's row part.
-//
-// Contraction-slot order. The MFMA sums over its 32 k-slots in a fixed order; which feature
-// sits in which slot is free as long as the A (row) and B (column) operands agree. Here slot
-// (step s = 4 n + q, lane group g) holds feature k = 16 n + 4 g + q, so:
-//   * a lane's 8 y values are two contiguous float4 of its row (two 16-B loads per column tile);
-//   * the row embedding emb = x C^T computed on the MFMA as D' = C x^T (M = emb feature, N = x
-//     row) comes out of the accumulators already in A-operand order: lane (g, c) of output tile
-//     n holds emb[row c][16 n + 4 g + q], q = 0..3 (no transposition, no LDS round trip for it);
-//   * the emb contraction over x's features uses the same order (two float4 x loads per row).
-// Slots k = 30, 31 (lane group 3, steps 6 and 7; features >= 30 are zero) carry the augmented
-// terms of torch.cdist's mm path: A [-2 emb, |emb|^2, 1] . B [y, 1, |y|^2] (padding rows: an
-// +inf |x|^2 slot, never selected). The squared norms are fmaf chains over a lane's 8 slots,
-// then the 4 lane groups summed in the order 0, 1, 2, 3.
-//
-// Row loop: chunks of NW row tiles; wave w computes the emb tile of chunk row tile w (16 f32
-// MFMAs, C read from LDS in operand order) and stores it into a double-buffered LDS chunk in
-// operand order; one barrier per chunk; then every wave runs its CT column tiles against the
-// chunk's NW row tiles (CT independent accumulation chains per A fragment), the selection of
-// each tile software-pipelined behind the next tile's MFMAs. The x rows of the next chunk are
-// loaded at the top of the chunk (registers) and consumed after its MFMAs. With RS > 1 every
-// block writes its columns' partial lists and fd_merge_kernel combines them in row-part order.
-template <int TOPK, int CT, int NW, int VAR = 0>
-__global__ __launch_bounds__(64 * NW, 2) void fd_fused_kernel(
+// Top-1 fp32 (round 5, the default argmin of the training step's naive point map and the IR):
+// ONE launch, no state across calls, no scratch unless the grid needs row parts.
+// Block = (crop b, column group of kTop1CT = 8 column tiles = 128 columns, row part rs); its 4
+// waves share the block's 8 column tiles (B operands in registers) and split the row part's
+// tiles, so every column's argmin over the row part is finished inside the block (the waves'
+// results meet in LDS) — no ticket, no arrival words, nothing a previous call can leave behind.
+// Each wave forms its own rows' emb = x C^T operands on the MFMA (16 per row tile, C in
+// registers): the emb D layout is the main contraction's A operand in the permuted slot order
+// (lane (point c, group g) holds features 16 n + 4 g + q), so no LDS and no barrier sit in the
+// main loop. Selection per distance: compare, select the tile, min (the running (key, tile) of
+// each (column tile, row offset r) per lane; key = the distance's bits as a signed int, ties keep
+// the earlier tile, then the lower r / lane group / wave = the lower row). torch.cdist's
+// clamp_min(1e-30) is not applied per distance: a column whose best key is <= bits(1e-30)
+// (a zero, tiny or negative expansion) is rescanned for its first row at or below the clamp
+// (wave-uniform, rare: coincident features). With RS > 1 (small batches) the row parts' keys go
+// to scratch and fd_top1_merge_kernel takes the minimum (stateless: every key is rewritten).
+constexpr int kTop1CT = 8;
+constexpr int kTop1Waves = 8;  // two per SIMD: one wave's dependency stalls are the other's MFMA time
+#ifdef PK_DEVBUILD
+__device__ unsigned long long g_fd_stamps[4096 * 8];  // (development: VAR 13 phase stamps per block)
+#define FD_STAMP(i, v)                                                  \
+  do {                                                                  \
+    if constexpr (VAR == 13) {                                          \
+      if (threadIdx.x == 0) g_fd_stamps[blockIdx.x * 8 + (i)] = (v);    \
+    }                                                                   \
+  } while (0)
+#else
+#define FD_STAMP(i, v) \
+  do {                 \
+  } while (0)
+#endif
+constexpr int kClampBits = 0x0da24260;  // bits of 1e-30f: clamp_min(1e-30) (cdist mm path)
+
+template <int VAR = 0>
+__global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top1_kernel(
     const float* __restrict__ ex, int ldx, const float* __restrict__ C, const float* __restrict__ ey, int ldy,
     const int32_t* __restrict__ n1, const int32_t* __restrict__ n2, int V1max, int V2max, int NCG, int RS,
-    int64_t* __restrict__ out_idx, float* __restrict__ out_dist, float* __restrict__ part_v,
-    int32_t* __restrict__ part_i, int32_t* __restrict__ arrivals) {
-  __shared__ __attribute__((aligned(16))) f32x4 chunk[2][NW][2][64];  // A tiles in operand order
-  __shared__ int last_arrival;
-  __shared__ __attribute__((aligned(16))) f32x4 cop[2][2][64];        // C in emb-MFMA A order [n][h][lane]
+    int64_t* __restrict__ out_idx, float* __restrict__ out_dist, unsigned long long* __restrict__ part) {
+  __shared__ f32x4 sB[kTop1CT][2][64];      // the column operands in B order (16 KB)
+  __shared__ f32x4 sC[2][2][64];            // -2 C in the emb MFMA's A order (4 KB)
+  __shared__ float sPart[4][kTop1CT * 16];  // per lane group partial |y|^2
+  __shared__ unsigned long long wkeys[kTop1Waves][kTop1CT * 16];
   const int per = NCG * RS;
   const int B = (int)(gridDim.x / per);
   int b, k;
@@ -736,846 +545,271 @@ __global__ __launch_bounds__(64 * NW, 2) void fd_fused_kernel(
     }
   }
   const int cg = k % NCG, rs = k / NCG;
-  const int lane = pk::lane_id(), w = __builtin_amdgcn_readfirstlane(pk::wave_id());
-  const int g = lane >> 4, c16 = lane & 15;
+  FD_STAMP(0, __builtin_amdgcn_s_memtime());
+  FD_STAMP(5, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4));
+  FD_STAMP(6, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20));
   const int N1 = n1[b], N2 = n2[b];
+  const int j0 = cg * kTop1CT * 16;
+  if (j0 >= N2) return;  // (block-uniform)
+  const int tid = threadIdx.x, lane = pk::lane_id(), w = __builtin_amdgcn_readfirstlane(pk::wave_id());
+  const int g = lane >> 4, c16 = lane & 15;
   const int nt = (N1 + 15) >> 4;
-  const int tb = (nt * rs) / RS, te = (nt * (rs + 1)) / RS;  // the block's row tiles
-  const float* Cb = C + (int64_t)b * kF * kF;
-  // C in the emb MFMA's A order: lane (g, m) of output tile n, step s = 4 h + q holds
-  // C[16 n + m][16 h + 4 g + q] (zero past row / feature 29); 4 KB, staged once per block
-  if (threadIdx.x < 256) {
-    const int n = threadIdx.x >> 7, h = (threadIdx.x >> 6) & 1, l = threadIdx.x & 63;
-    const int m = l & 15, gg = l >> 4, row = 16 * n + m;
-    float v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int f = 16 * h + 4 * gg + q;
-      v[q] = (row < kF && f < kF) ? Cb[row * kF + f] : 0.f;
-    }
-    cop[n][h][l] = f32x4{v[0], v[1], v[2], v[3]};
-  }
-  // column operands (y side): lane (g, c) of column tile ct holds y[16 ct + c][16 n + 4 g + q]
-  // at step 4 n + q; slot k = 30 -> 1, k = 31 -> |y|^2
-  float bo[CT][8];
-#pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    const int ct = CT * (NW * cg + w) + c;
-    const int j = ct * 16 + c16;
-    const float* yr = ey + ((int64_t)b * V2max + min(j, V2max - 1)) * ldy;
-    const float4 y0 = *reinterpret_cast<const float4*>(yr + 4 * g);
-    const float4 y1 = *reinterpret_cast<const float4*>(yr + 16 + 4 * g);
-    const bool ok = j < N2;
-    float v[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
-    float part = 0.f;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const bool in = ok && (s < 6 || g < 3);  // feature 16 (s >> 2) + 4 g + (s & 3) < 30
-      v[s] = in ? v[s] : 0.f;
-      part = fmaf(v[s], v[s], part);
-    }
-    const float p1 = __shfl_xor(part, 16), p2 = __shfl_xor(part, 32), p3 = __shfl_xor(part, 48);
-    const float mine[4] = {part, p1, p2, p3};
-    float nrm = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) nrm += mine[q ^ g];
-    if (g == 3) {
-      v[6] = 1.f;
-      v[7] = nrm;
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s) bo[c][s] = v[s];
-  }
-  // x rows of row tile `tt` (features 16 h + 4 g .. + 3 of row 16 tt + c16), unmasked loads at
-  // a clamped row; the feature / row masks apply at use
+  const int Q = RS * kTop1Waves, qw = rs * kTop1Waves + w;
+  const int tb = (int)((int64_t)nt * qw / Q), te = (int)((int64_t)nt * (qw + 1) / Q);  // this wave's row tiles
   const float* xb = ex + (int64_t)b * V1max * ldx;
-  auto xload = [&](int tt, float4 (&xv)[2]) {
-    const int row = min(tt * 16 + c16, V1max - 1);
-    const float* xr = xb + (int64_t)row * ldx;
+  auto xload = [&](int t, float4 (&xv)[2]) {  // row t*16 + c16; a padding row reads row 0 (finite)
+    const int r0 = t * 16 + c16;
+    const float* xr = xb + (int64_t)(r0 < N1 ? r0 : 0) * ldx;
     xv[0] = *reinterpret_cast<const float4*>(xr + 4 * g);
     xv[1] = *reinterpret_cast<const float4*>(xr + 16 + 4 * g);
   };
-  // emb tile of row tile tt -> A operand [-2 emb, |emb|^2, 1] into LDS chunk slot (buf, w)
-  auto emb_tile = [&](int tt, const float4 (&xv)[2], int buf) {
-    const int row = tt * 16 + c16;
-    const bool rok = row < N1;
-    float xs[8] = {xv[0].x, xv[0].y, xv[0].z, xv[0].w, xv[1].x, xv[1].y, xv[1].z, xv[1].w};
+  float4 xc[2];
+  if (tb < te) xload(tb, xc);
+  {  // staging: -2 C in A order (threads 0..255), the 128 columns' [y, 1, |y|^2] in B order
+    if (tid < 256) {
+      const float* Cb = C + (int64_t)b * kF * kF;
+      const int n = tid >> 7, h = (tid >> 6) & 1, l = tid & 63;
+      const int row = 16 * n + (l & 15), gg = l >> 4;
+      float v[4];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) xs[s] = (rok && (s < 6 || g < 3)) ? xs[s] : 0.f;
-    float e[8];
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const f32x4 c0 = cop[n][0][lane], c1 = cop[n][1][lane];
-      const float cv[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(cv[s], xs[s], acc, 0, 0, 0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) e[4 * n + q] = acc[q];  // emb[row c16][16 n + 4 g + q]
-    }
-    float part = 0.f;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) part = fmaf(e[s], e[s], part);
-    const float p1 = __shfl_xor(part, 16), p2 = __shfl_xor(part, 32), p3 = __shfl_xor(part, 48);
-    const float mine[4] = {part, p1, p2, p3};
-    float nrm = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) nrm += mine[q ^ g];
-    float o[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) o[s] = -2.f * e[s];
-    if (g == 3) {
-      o[6] = rok ? nrm : __builtin_huge_valf();  // padding row: +inf |x|^2 slot
-      o[7] = 1.f;
-    }
-    chunk[buf][w][0][lane] = f32x4{o[0], o[1], o[2], o[3]};
-    chunk[buf][w][1][lane] = f32x4{o[4], o[5], o[6], o[7]};
-  };
-  TopK<TOPK> best[CT];
-  Top1x4 b4[CT];
-#pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    best[c].init();
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      b4[c].k[r] = 0x7f800000;  // +inf: never replaced by an equal key
-      b4[c].t[r] = 0x7fffffff;
-    }
-  }
-  // selection of one tile's distances (tile index tt, masked to +inf past the part)
-  auto select = [&](const float (&d)[CT][4], int tt, bool in) {
-#pragma unroll
-    for (int c = 0; c < CT; ++c) {
-      if constexpr (TOPK == 1) {
-        constexpr int kClamp = 0x0da24260;  // bits of 1e-30f: clamp_min(1e-30) (cdist mm path)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = in ? max(__float_as_int(d[c][r]), kClamp) : 0x7f800000;
-          const int m = (key - b4[c].k[r]) >> 31;  // -1 iff key < best
-          b4[c].t[r] = (m & tt) | (~m & b4[c].t[r]);
-          b4[c].k[r] = min(key, b4[c].k[r]);
-        }
-      } else {
-        float dd[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dd[r] = in ? d[c][r] : __builtin_huge_valf();
-        epilogue<TOPK>(dd, tt * 16 + 4 * g, best[c]);
+      for (int q = 0; q < 4; ++q) {
+        const int f = 16 * h + 4 * gg + q;
+        v[q] = (row < kF && f < kF) ? -2.f * Cb[row * kF + f] : 0.f;
       }
+      sC[n][h][l] = f32x4{v[0], v[1], v[2], v[3]};
     }
-  };
-  const int nchunk = te > tb ? (te - tb + NW - 1) / NW : 0;
-  float4 xv[2];
-  if (nchunk > 0) {
-    xload(min(tb + w, te - 1), xv);
-    __syncthreads();  // cop staged
-    emb_tile(tb + w, xv, 0);
-  }
-  __syncthreads();
-  float dprev[CT][4];
-  int tprev = -1;
-  for (int ch = 0; ch < nchunk; ++ch) {
-    const int c0 = tb + ch * NW;
-    const int buf = ch & 1;
-    const bool more = ch + 1 < nchunk;
-    if (more) xload(min(c0 + NW + w, te - 1), xv);
-    const int ntile = min(NW, te - c0);
-    for (int t = 0; t < ntile; ++t) {
-      const f32x4 a0 = chunk[buf][t][0][lane], a1 = chunk[buf][t][1][lane];
-      const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-      float d[CT][4];
+    const int jj = tid & (kTop1CT * 16 - 1), gy = tid >> 7;  // column jj of the block, lane group gy
+    const int j = j0 + jj;
+    const float* yr = ey + ((int64_t)b * V2max + min(j, V2max - 1)) * ldy;
+    const float4 y0 = *reinterpret_cast<const float4*>(yr + 4 * gy);
+    const float4 y1 = *reinterpret_cast<const float4*>(yr + 16 + 4 * gy);
+    const bool ok = j < N2;
+    float v[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+    float part_ = 0.f;
 #pragma unroll
-      for (int c = 0; c < CT; ++c) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (VAR == 2 || VAR == 3) {  // (development variants: no main-loop MFMAs)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[r] = av[r] + av[4 + r] * bo[c][r];
-        } else {
-#pragma unroll
-          for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bo[c][s], acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) d[c][r] = acc[r];
-      }
-      if constexpr (VAR == 1 || VAR == 3) {  // (development variants: no selection, one VALU op)
-        if (tprev >= 0) b4[0].k[0] ^= __float_as_int(dprev[0][0] + dprev[CT - 1][3]);
-      } else {
-        if (tprev >= 0) select(dprev, tprev, true);  // the previous tile, beside these MFMAs
-      }
-#pragma unroll
-      for (int c = 0; c < CT; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dprev[c][r] = d[c][r];
-      tprev = c0 + t;
+    for (int s = 0; s < 8; ++s) {
+      v[s] = (ok && (s < 6 || gy < 3)) ? v[s] : 0.f;
+      part_ = fmaf(v[s], v[s], part_);
     }
-    if (more) emb_tile(c0 + NW + w, xv, buf ^ 1);
+    sPart[gy][jj] = part_;
+    __syncthreads();
+    if (gy == 3) {  // |y|^2: the lane groups' partials in the order 0, 1, 2, 3
+      float nrm = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nrm += sPart[q][jj];
+      v[6] = 1.f;
+      v[7] = nrm;
+    }
+    const int c = jj >> 4, l = gy * 16 + (jj & 15);
+    sB[c][0][l] = f32x4{v[0], v[1], v[2], v[3]};
+    sB[c][1][l] = f32x4{v[4], v[5], v[6], v[7]};
     __syncthreads();
   }
-  if (tprev >= 0) select(dprev, tprev, true);
-#pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    if constexpr (TOPK == 1) {  // the 4 row offsets: smallest value, ties lowest row
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = b4[c].t[r] == 0x7fffffff ? 0x7fffffff : b4[c].t[r] * 16 + 4 * g + r;
-        const float v = __int_as_float(b4[c].k[r]);
-        const bool take = v < best[c].v[0] || (v == best[c].v[0] && row < best[c].i[0]);
-        best[c].v[0] = take ? v : best[c].v[0];
-        best[c].i[0] = take ? row : best[c].i[0];
-      }
-    }
-    lanegroup_merge<TOPK>(best[c]);
-  }
-  if (g == 0) {
-#pragma unroll
-    for (int c = 0; c < CT; ++c) {
-      const int j = (CT * (NW * cg + w) + c) * 16 + c16;
-      if (j >= N2) continue;
-      if (RS == 1) {
-        const int64_t o = ((int64_t)b * V2max + j) * TOPK;
-#pragma unroll
-        for (int q = 0; q < TOPK; ++q) {
-          out_idx[o + q] = best[c].i[q] == 0x7fffffff ? -1 : best[c].i[q];
-          if (out_dist) out_dist[o + q] = sqrtf(best[c].v[q]);
-        }
-      } else {
-        const int64_t o = (((int64_t)b * RS + rs) * V2max + j) * TOPK;
-#pragma unroll
-        for (int q = 0; q < TOPK; ++q) {
-          part_v[o + q] = best[c].v[q];
-          part_i[o + q] = best[c].i[q];
-        }
-      }
-    }
-  }
-  if (RS == 1) return;
-  // in-launch combine of the RS row parts (cdna_hip_programming.md §6 Guideline 16, counter
-  // form): every wave drains its partial stores, one agent-scope release, one relaxed ticket per
-  // block on arrivals[b][cg]; the block that draws RS - 1 acquires, merges the RS lists of each of
-  // its columns in row-part order (ties: lower row) and resets the ticket to 0 (the word is zero
-  // before the first launch on this buffer and after every launch)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int old = __hip_atomic_fetch_add(arrivals + (int64_t)b * NCG + cg, 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    last_arrival = old == RS - 1;
-    if (old == RS - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(arrivals + (int64_t)b * NCG + cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  if (!last_arrival) return;
-  for (int jj = threadIdx.x; jj < NW * CT * 16; jj += 64 * NW) {
-    const int j = CT * NW * 16 * cg + jj;
-    if (j >= N2) continue;
-    TopK<TOPK> m;
-    m.init();
-    for (int r = 0; r < RS; ++r) {
-      const int64_t o = (((int64_t)b * RS + r) * V2max + j) * TOPK;
-      float ov[TOPK];
-      int oi[TOPK];
-#pragma unroll
-      for (int q = 0; q < TOPK; ++q) {
-        ov[q] = part_v[o + q];
-        oi[q] = part_i[o + q];
-      }
-      m.merge(ov, oi);
-    }
-    const int64_t o = ((int64_t)b * V2max + j) * TOPK;
-#pragma unroll
-    for (int q = 0; q < TOPK; ++q) {
-      out_idx[o + q] = m.i[q] == 0x7fffffff ? -1 : m.i[q];
-      if (out_dist) out_dist[o + q] = sqrtf(m.v[q]);
-    }
-  }
-}
-
-// The fp32 parity path since round 4: fd_rows_kernel + fd_cols_kernel.
-//
-// Contraction-slot order. The MFMA sums over its 32 k-slots in a fixed order; which feature
-// sits in which slot is free as long as the A (row) and B (column) operands agree. Here slot
-// (step s = 4 n + q, lane group g) holds feature k = 16 n + 4 g + q, so:
-//   * a lane's 8 y values are two contiguous float4 of its row (two 16-B loads per column tile);
-//   * the row embedding emb = x C^T computed on the MFMA as D' = C x^T (M = emb feature, N = x
-//     row) comes out of the accumulators already in A-operand order: lane (g, c) of output tile
-//     n holds emb[row c][16 n + 4 g + q], q = 0..3 (no transposition through LDS);
-//   * the emb contraction over x's features uses the same order (two float4 x loads per row).
-// Slots k = 30, 31 (lane group 3, steps 6 and 7; features >= 30 are zero) carry the augmented
-// terms of torch.cdist's mm path: A [-2 emb, |emb|^2, 1] . B [y, 1, |y|^2] (padding rows: an
-// +inf |x|^2 slot, never selected). The squared norms are fmaf chains over a lane's 8 slots,
-// then the 4 lane groups summed in the order 0, 1, 2, 3.
-//
-// fd_rows_kernel: grid (ceil(T1 / 4), B), 4 waves, one 16-row tile per wave: x rows (two 16-B
-// loads per lane), C from L2 in the emb MFMA's A order, 16 f32 MFMAs, norms, and the tile's A
-// operand stored as two lane-contiguous 1 KB halves (slots 0-3, 4-7).
-__global__ __launch_bounds__(256) void fd_rows_kernel(const float* __restrict__ ex, int ldx,
-                                                     const float* __restrict__ C, const int32_t* __restrict__ n1,
-                                                     int V1max, int T1, f32x4* __restrict__ A) {
-  const int b = blockIdx.y;
-  const int lane = pk::lane_id(), g = lane >> 4, c16 = lane & 15;
-  const int tt = blockIdx.x * 4 + pk::wave_id();
-  if (tt >= T1) return;
-  const int row = tt * 16 + c16;
-  const float* xr = ex + ((int64_t)b * V1max + min(row, V1max - 1)) * ldx;
-  const float4 x0 = *reinterpret_cast<const float4*>(xr + 4 * g);
-  const float4 x1 = *reinterpret_cast<const float4*>(xr + 16 + 4 * g);
-  // C operand: lane (g, m) of output tile n at step s = 4 h + q holds C[16 n + m][16 h + 4 g + q]
-  const float* Cb = C + (int64_t)b * kF * kF;
-  float cv[2][8];
+  float cv[2][8], bo[kTop1CT][8];
 #pragma unroll
   for (int n = 0; n < 2; ++n)
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int r = 16 * n + c16, f = 16 * (s >> 2) + 4 * g + (s & 3);
-      cv[n][s] = Cb[min(r, kF - 1) * kF + min(f, kF - 1)];
-    }
-  const bool rok = row < n1[b];
-  float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 t4 = sC[n][h][lane];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) xs[s] = (rok && (s < 6 || g < 3)) ? xs[s] : 0.f;  // feature < 30
-  float e[8];
-#pragma unroll
-  for (int n = 0; n < 2; ++n) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int r = 16 * n + c16;
-      const bool cok = r < kF && (s < 6 || g < 3);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(cok ? cv[n][s] : 0.f, xs[s], acc, 0, 0, 0);
+      for (int q = 0; q < 4; ++q) cv[n][4 * h + q] = t4[q];
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) e[4 * n + q] = acc[q];  // emb[row c16][16 n + 4 g + q]
-  }
-  float part = 0.f;
+  for (int c = 0; c < kTop1CT; ++c)
 #pragma unroll
-  for (int s = 0; s < 8; ++s) part = fmaf(e[s], e[s], part);
-  const float p1 = __shfl_xor(part, 16), p2 = __shfl_xor(part, 32), p3 = __shfl_xor(part, 48);
-  const float mine[4] = {part, p1, p2, p3};
-  float nrm = 0.f;
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 t4 = sB[c][h][lane];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) nrm += mine[q ^ g];  // lane groups 0, 1, 2, 3 in that order
-  float o[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) o[s] = -2.f * e[s];
-  if (g == 3) {
-    o[6] = rok ? nrm : __builtin_huge_valf();  // padding row: +inf |x|^2 slot
-    o[7] = 1.f;
-  }
-  f32x4* At = A + ((int64_t)b * T1 + tt) * 128;
-  At[lane] = f32x4{o[0], o[1], o[2], o[3]};
-  At[64 + lane] = f32x4{o[4], o[5], o[6], o[7]};
-}
-
-// fd_cols_kernel: grid B * NCG * RS (1-D, XCD-aware), NW waves. Block = (crop b, column group
-// cg of CT column tiles, row part rs); every wave holds the group's CT column operands (the y
-// side, two 16-B loads per lane and tile, norms in-wave) in registers and takes 1/NW of the row
-// part's tiles, streaming their A operands from L2 two tiles ahead (two 16-B loads per lane and
-// tile); per tile CT independent accumulation chains of 8 MFMAs, the selection of each tile
-// software-pipelined behind the next tile's MFMAs. The NW waves' lists merge through LDS in wave
-// (= row) order; with RS > 1 the block writes partial lists that fd_merge_kernel combines.
-template <int TOPK, int CT, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void fd_cols_kernel(
-    const f32x4* __restrict__ A, const float* __restrict__ ey, int ldy, const int32_t* __restrict__ n1,
-    const int32_t* __restrict__ n2, int V2max, int T1, int NCG, int RS, int64_t* __restrict__ out_idx,
-    float* __restrict__ out_dist, float* __restrict__ part_v, int32_t* __restrict__ part_i) {
-  __shared__ float mv[NW][CT][16][TOPK];
-  __shared__ int mi[NW][CT][16][TOPK];
-  const int per = NCG * RS;
-  const int B = (int)(gridDim.x / per);
-  int b, k;
-  {  // all blocks of crop b on XCD b % 8 (hardware block L lands on XCD L % 8) when B % 8 == 0
-    const int L = blockIdx.x;
-    if ((B & 7) == 0) {
-      const int x8 = L & 7, q = L >> 3;
-      b = x8 + 8 * (q / per);
-      k = q - (q / per) * per;
-    } else {
-      b = L / per;
-      k = L - b * per;
+      for (int q = 0; q < 4; ++q) bo[c][4 * h + q] = t4[q];
     }
-  }
-  const int cg = k % NCG, rs = k / NCG;
-  const int lane = pk::lane_id(), w = __builtin_amdgcn_readfirstlane(pk::wave_id());
-  const int g = lane >> 4, c16 = lane & 15;
-  const int N1 = n1[b], N2 = n2[b];
-  const int nt = (N1 + 15) >> 4;
-  const int tb0 = (nt * rs) / RS, te0 = (nt * (rs + 1)) / RS;  // the block's row part
-  const int nb = te0 - tb0;
-  const int tb = __builtin_amdgcn_readfirstlane(tb0 + (nb * w) / NW);
-  const int te = __builtin_amdgcn_readfirstlane(tb0 + (nb * (w + 1)) / NW);  // this wave's tiles
-  // column operands: lane (g, c) of column tile ct holds y[16 ct + c][16 n + 4 g + q] at step
-  // 4 n + q; slot k = 30 -> 1, k = 31 -> |y|^2
-  float bo[CT][8];
+  // A operand [-2 emb, |emb|^2, 1] of row tile t: -2 emb straight from the MFMA with -2 C (exact
+  // power-of-two scaling), |emb|^2 = (sum of the squares of -2 emb) / 4 (exact); padding rows:
+  // |emb|^2 = +inf, never selected. Split into the MFMAs and the norm so that the loop below can
+  // issue tile t + 1's emb MFMAs among tile t's.
+  auto emb_mfma = [&](const float4 (&xv)[2], f32x4 (&e)[2]) {
+    const float xs[8] = {xv[0].x, xv[0].y, xv[0].z, xv[0].w, xv[1].x, xv[1].y, xv[1].z, xv[1].w};
 #pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    const int j = (cg * CT + c) * 16 + c16;
-    const float* yr = ey + ((int64_t)b * V2max + min(j, V2max - 1)) * ldy;
-    const float4 y0 = *reinterpret_cast<const float4*>(yr + 4 * g);
-    const float4 y1 = *reinterpret_cast<const float4*>(yr + 16 + 4 * g);
-    const bool ok = j < N2;
-    float v[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
-    float part = 0.f;
+    for (int n = 0; n < 2; ++n) e[n] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      v[s] = (ok && (s < 6 || g < 3)) ? v[s] : 0.f;
-      part = fmaf(v[s], v[s], part);
-    }
-    const float p1 = __shfl_xor(part, 16), p2 = __shfl_xor(part, 32), p3 = __shfl_xor(part, 48);
-    const float mine[4] = {part, p1, p2, p3};
-    float nrm = 0.f;
+    for (int s = 0; s < 8; ++s)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) nrm += mine[q ^ g];
-    if (g == 3) {
-      v[6] = 1.f;
-      v[7] = nrm;
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s) bo[c][s] = v[s];
-  }
-  TopK<TOPK> best[CT];
-  Top1x4 b4[CT];
-#pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    best[c].init();
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      b4[c].k[r] = 0x7f800000;  // +inf: never replaced by an equal key
-      b4[c].t[r] = 0x7fffffff;
-    }
-  }
-  auto select = [&](const float (&d)[CT][4], int tt) {
-#pragma unroll
-    for (int c = 0; c < CT; ++c) {
-      if constexpr (TOPK == 1) {
-        constexpr int kClamp = 0x0da24260;  // bits of 1e-30f: clamp_min(1e-30) (cdist mm path)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = max(__float_as_int(d[c][r]), kClamp);
-          const int m = (key - b4[c].k[r]) >> 31;  // -1 iff key < best
-          b4[c].t[r] = (m & tt) | (~m & b4[c].t[r]);
-          b4[c].k[r] = min(key, b4[c].k[r]);
-        }
-      } else {
-        epilogue<TOPK>(d[c], tt * 16 + 4 * g, best[c]);
-      }
-    }
+      for (int n = 0; n < 2; ++n) e[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(cv[n][s], xs[s], e[n], 0, 0, 0);
   };
-  const f32x4* Ab = A + (int64_t)b * T1 * 128;
-  if (te > tb) {
-    // A fragments two tiles ahead (unconditional loads at a clamped tile: no branch in the loop)
-    f32x4 a0[3], a1[3];
+  auto emb_norm = [&](int t, const f32x4 (&e)[2], float (&a)[8]) {
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const f32x4* at = Ab + (int64_t)min(tb + p, te - 1) * 128;
-      a0[p] = at[lane];
-      a1[p] = at[64 + lane];
-    }
-    float dprev[CT][4];
-    for (int t = tb; t < te; ++t) {
-      {
-        const f32x4* at = Ab + (int64_t)min(t + 2, te - 1) * 128;
-        a0[2] = at[lane];
-        a1[2] = at[64 + lane];
-      }
-      const float av[8] = {a0[0][0], a0[0][1], a0[0][2], a0[0][3], a1[0][0], a1[0][1], a1[0][2], a1[0][3]};
-      float d[CT][4];
+    for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int c = 0; c < CT; ++c) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bo[c][s], acc, 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) d[c][r] = acc[r];
-      }
-      if (t > tb) select(dprev, t - 1);  // the previous tile, beside these MFMAs
-#pragma unroll
-      for (int c = 0; c < CT; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dprev[c][r] = d[c][r];
-      a0[0] = a0[1]; a1[0] = a1[1];
-      a0[1] = a0[2]; a1[1] = a1[2];
-    }
-    select(dprev, te - 1);
-  }
-#pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    if constexpr (TOPK == 1) {  // the 4 row offsets: smallest value, ties lowest row
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = b4[c].t[r] == 0x7fffffff ? 0x7fffffff : b4[c].t[r] * 16 + 4 * g + r;
-        const float v = __int_as_float(b4[c].k[r]);
-        const bool take = v < best[c].v[0] || (v == best[c].v[0] && row < best[c].i[0]);
-        best[c].v[0] = take ? v : best[c].v[0];
-        best[c].i[0] = take ? row : best[c].i[0];
-      }
-    }
-    lanegroup_merge<TOPK>(best[c]);
-    if (g == 0) {
-#pragma unroll
-      for (int q = 0; q < TOPK; ++q) {
-        mv[w][c][c16][q] = best[c].v[q];
-        mi[w][c][c16][q] = best[c].i[q];
-      }
-    }
-  }
-  __syncthreads();
-  // wave c < CT merges column tile c's NW lists in wave order (row order; ties: lower row)
-  if (w >= CT || g != 0) return;
-  const int c = w;
-  TopK<TOPK> m;
-#pragma unroll
-  for (int q = 0; q < TOPK; ++q) {
-    m.v[q] = mv[0][c][c16][q];
-    m.i[q] = mi[0][c][c16][q];
-  }
-#pragma unroll
-  for (int ww = 1; ww < NW; ++ww) {
-    float ov[TOPK];
-    int oi[TOPK];
-#pragma unroll
-    for (int q = 0; q < TOPK; ++q) {
-      ov[q] = mv[ww][c][c16][q];
-      oi[q] = mi[ww][c][c16][q];
-    }
-    m.merge(ov, oi);
-  }
-  const int j = (cg * CT + c) * 16 + c16;
-  if (j >= N2) return;
-  if (RS == 1) {
-    const int64_t o = ((int64_t)b * V2max + j) * TOPK;
-#pragma unroll
-    for (int q = 0; q < TOPK; ++q) {
-      out_idx[o + q] = m.i[q] == 0x7fffffff ? -1 : m.i[q];
-      if (out_dist) out_dist[o + q] = sqrtf(m.v[q]);
-    }
-  } else {
-    const int64_t o = (((int64_t)b * RS + rs) * V2max + j) * TOPK;
-#pragma unroll
-    for (int q = 0; q < TOPK; ++q) {
-      part_v[o + q] = m.v[q];
-      part_i[o + q] = m.i[q];
-    }
-  }
-}
-
-// fd_wide_kernel (mode 0, top-1: the naive solver's argmin, the training step's and the IR's
-// feature-distance pass): ONE launch, one wave per SIMD. Block = 4 waves = one CU = (crop b,
-// column group cg of 4 x CT column tiles, row part rs); wave w holds column tiles
-// CT (4 cg + w) + c, c < CT, in registers (their y operands, CT x 8 VGPRs) and every wave
-// streams the block's row part from a double-buffered LDS chunk of 8 row tiles, which the four
-// waves fill with the rows' emb operands (two tiles each, computed on the MFMA from x in the
-// permuted slot order above: no transposition), one barrier per chunk. Per row tile a wave runs
-// 4 groups of 4 column tiles x 8 MFMAs (4 independent accumulation chains); the selection of
-// each group's 16 distances is interleaved into the next group's MFMAs at compile time (one
-// wave per SIMD issues in order: the VALU selection fills the MFMA issue gaps). Row parts
-// (RS > 1) combine in the launch: each block stores its columns' (distance bits, row) keys as
-// 8-byte write-through stores, drains, and takes a ticket on arrivals[b][cg]; the block that
-// draws RS - 1 reads the RS keys of each column with write-through loads (no fence: every
-// handed-off byte is stored and loaded sc1, cdna_hip_programming.md §6 Guideline 16), keeps the
-// smallest (value, then row) and resets the ticket (zero before the first launch on the buffer,
-// zero after every launch).
-__device__ __forceinline__ int med3i(int a, int b, int c) {  // v_med3_i32: the median of three
-  int d;
-  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-  return d;
-}
-constexpr int kWideCT = 8;
-constexpr int kWideChunk = 8;
-
-template <int CT, int VAR = 0>
-__global__ __launch_bounds__(256, 2) void fd_wide_kernel(
-    const float* __restrict__ ex, int ldx, const float* __restrict__ C, const float* __restrict__ ey, int ldy,
-    const int32_t* __restrict__ n1, const int32_t* __restrict__ n2, int V1max, int V2max, int NCG, int RS,
-    int64_t* __restrict__ out_idx, float* __restrict__ out_dist, unsigned long long* part,
-    int32_t* arrivals) {
-  __shared__ __attribute__((aligned(16))) f32x4 lds[2 * kWideChunk * 128 + 4 * 64 + 4];
-  f32x4* chunk = lds;                            // [2][kWideChunk][2][64]: A tiles in operand order
-  f32x4* cop = lds + 2 * kWideChunk * 128;       // [2][2][64]: C in the emb MFMA's A order
-  int* flag = reinterpret_cast<int*>(lds + 2 * kWideChunk * 128 + 4 * 64);
-  const int per = NCG * RS;
-  const int B = (int)(gridDim.x / per);
-  int b, k;
-  {  // all blocks of crop b on XCD b % 8 (hardware block L lands on XCD L % 8) when B % 8 == 0
-    const int L = blockIdx.x;
-    if ((B & 7) == 0) {
-      const int x8 = L & 7, q = L >> 3;
-      b = x8 + 8 * (q / per);
-      k = q - (q / per) * per;
-    } else {
-      b = L / per;
-      k = L - b * per;
-    }
-  }
-  const int cg = k % NCG, rs = k / NCG;
-  if constexpr (VAR == 7) {  // (development variant: an AGPR operand in the kernel, so the
-    float z = 0.f;           // MFMAs are selected in their AGPR-accumulator form)
-    asm volatile("; agpr %0" ::"a"(z));
-  }
-  const int lane = pk::lane_id(), w = __builtin_amdgcn_readfirstlane(pk::wave_id());
-  const int g = lane >> 4, c16 = lane & 15;
-  const int N1 = n1[b], N2 = n2[b];
-  const int nt = (N1 + 15) >> 4;
-  const int tb = (nt * rs) / RS, te = (nt * (rs + 1)) / RS;  // the block's row tiles
-  {  // C operand, staged once: thread (n, h, l) holds C[16 n + m][16 h + 4 gg + q], q = 0..3
-    const float* Cb = C + (int64_t)b * kF * kF;
-    const int n = threadIdx.x >> 7, h = (threadIdx.x >> 6) & 1, l = threadIdx.x & 63;
-    const int m = l & 15, gg = l >> 4, row = 16 * n + m;
-    float v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int f = 16 * h + 4 * gg + q;
-      v[q] = (row < kF && f < kF) ? Cb[min(row, kF - 1) * kF + min(f, kF - 1)] : 0.f;
-    }
-    cop[threadIdx.x] = f32x4{v[0], v[1], v[2], v[3]};
-  }
-  // column operands
-  float bo[CT][8];
-#pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    const int j = (CT * (4 * cg + w) + c) * 16 + c16;
-    const float* yr = ey + ((int64_t)b * V2max + min(j, V2max - 1)) * ldy;
-    const float4 y0 = *reinterpret_cast<const float4*>(yr + 4 * g);
-    const float4 y1 = *reinterpret_cast<const float4*>(yr + 16 + 4 * g);
-    const bool ok = j < N2;
-    float v[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+      for (int q = 0; q < 4; ++q) a[4 * n + q] = e[n][q];
     float part_ = 0.f;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      v[s] = (ok && (s < 6 || g < 3)) ? v[s] : 0.f;
-      part_ = fmaf(v[s], v[s], part_);
-    }
+    for (int s = 0; s < 8; ++s) part_ = fmaf(a[s], a[s], part_);
     const float p1 = __shfl_xor(part_, 16), p2 = __shfl_xor(part_, 32), p3 = __shfl_xor(part_, 48);
-    const float mine[4] = {part_, p1, p2, p3};
-    float nrm = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) nrm += mine[q ^ g];
-    if (g == 3) {
-      v[6] = 1.f;
-      v[7] = nrm;
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s) bo[c][s] = v[s];
-  }
-  // x rows of two row tiles (this wave's emb share of a chunk), unmasked at a clamped row
-  const float* xb = ex + (int64_t)b * V1max * ldx;
-  auto xload = [&](int t0, float4 (&xv)[2][2]) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int row = min((t0 + u) * 16 + c16, V1max - 1);
-      const float* xr = xb + (int64_t)row * ldx;
-      xv[u][0] = *reinterpret_cast<const float4*>(xr + 4 * g);
-      xv[u][1] = *reinterpret_cast<const float4*>(xr + 16 + 4 * g);
-    }
+    // lane group 3: p3 = group 0, p2 = group 1, p1 = group 2, own = group 3
+    const float nrm = 0.25f * (((p3 + p2) + p1) + part_);
+    const bool g3 = g == 3;
+    a[6] = g3 ? (t * 16 + c16 < N1 ? nrm : __builtin_huge_valf()) : a[6];
+    a[7] = g3 ? 1.f : a[7];
   };
-  auto emb_tile = [&](int tt, const float4 (&xv)[2], f32x4* dst) {
-    const int row = tt * 16 + c16;
-    const bool rok = row < N1;
-    float xs[8] = {xv[0].x, xv[0].y, xv[0].z, xv[0].w, xv[1].x, xv[1].y, xv[1].z, xv[1].w};
-#pragma unroll
-    for (int s = 0; s < 8; ++s) xs[s] = (rok && (s < 6 || g < 3)) ? xs[s] : 0.f;
-    float e[8];
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const f32x4 c0 = cop[(2 * n) * 64 + lane], c1 = cop[(2 * n + 1) * 64 + lane];
-      const float cv[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(cv[s], xs[s], acc, 0, 0, 0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) e[4 * n + q] = acc[q];
-    }
-    float part_ = 0.f;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) part_ = fmaf(e[s], e[s], part_);
-    const float p1 = __shfl_xor(part_, 16), p2 = __shfl_xor(part_, 32), p3 = __shfl_xor(part_, 48);
-    const float mine[4] = {part_, p1, p2, p3};
-    float nrm = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) nrm += mine[q ^ g];
-    float o[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) o[s] = -2.f * e[s];
-    if (g == 3) {
-      o[6] = rok ? nrm : __builtin_huge_valf();
-      o[7] = 1.f;
-    }
-    dst[lane] = f32x4{o[0], o[1], o[2], o[3]};
-    dst[64 + lane] = f32x4{o[4], o[5], o[6], o[7]};
+  auto emb = [&](int t, const float4 (&xv)[2], float (&a)[8]) {
+    f32x4 e[2];
+    emb_mfma(xv, e);
+    emb_norm(t, e, a);
   };
-  // running (key, tile) per column tile and row offset r (Top1x4's scheme)
-  int bk[CT][4], bt[CT][4];
+  FD_STAMP(1, __builtin_amdgcn_s_memtime());
+  int bk[kTop1CT][4], bt[kTop1CT][4];
 #pragma unroll
-  for (int c = 0; c < CT; ++c)
+  for (int c = 0; c < kTop1CT; ++c)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       bk[c][r] = 0x7f800000;
-      bt[c][r] = 0x7fffffff;
+      bt[c][r] = -1;
     }
-  constexpr int kClamp = 0x0da24260;  // bits of 1e-30f: clamp_min(1e-30) (cdist mm path)
-  auto sel = [&](const f32x4 (&acc)[4], int grp, int tt) {
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = 4 * grp + cc;
-        if constexpr (VAR == 9) {  // (development variant: value only, one v_med3_i32)
-          bk[c][r] = med3i(__float_as_int(acc[cc][r]), kClamp, bk[c][r]);
-          continue;
-        }
-        if constexpr (VAR == 8) {  // (development variant: clamp + min in one v_med3_i32)
-          const int nb = med3i(__float_as_int(acc[cc][r]), kClamp, bk[c][r]);  // bk >= kClamp
-          bt[c][r] = nb < bk[c][r] ? tt : bt[c][r];
-          bk[c][r] = nb;
-          continue;
-        }
-        const int key = max(__float_as_int(acc[cc][r]), kClamp);
-        if constexpr (VAR == 5) {  // (development variant: the value only, no row index)
-          bk[c][r] = min(key, bk[c][r]);
-          continue;
-        }
-        if constexpr (VAR == 6) {  // (development variant: round 4's integer select; the asm
-          int dif = key - bk[c][r];  // hides the difference's range, else LLVM rewrites it as
-          asm volatile("" : "+v"(dif));  // the compare + select below)
-          int m = dif >> 31;  // -1 iff key < best (both keys in [kClamp, 0x7f800000])
-          asm volatile("" : "+v"(m));
-          bt[c][r] = (m & tt) | (~m & bt[c][r]);
-          bk[c][r] = min(key, bk[c][r]);
-          continue;
-        }
-        // compare + select (v_cmp into an SGPR pair, v_cndmask): 5 % faster than the integer
-        // select (VAR 6) — on gfx950 the f32 MFMAs never co-execute with VALU work
-        // (SQ_VALU_MFMA_COEXEC_CYCLES = 0 on this kernel), so every selection instruction adds
-        // to the MFMA time; see DESIGN.md §5 'Feature distance'
-        bt[c][r] = key < bk[c][r] ? tt : bt[c][r];
-        bk[c][r] = min(key, bk[c][r]);
-      }
-  };
-  const int nchunk = te > tb ? (te - tb + kWideChunk - 1) / kWideChunk : 0;
-  float4 xv[2][2];
-  if (nchunk > 0) xload(tb + 2 * w, xv);
-  __syncthreads();  // cop staged
-  if (nchunk > 0) {
-    emb_tile(tb + 2 * w, xv[0], chunk + (2 * w) * 128);
-    emb_tile(tb + 2 * w + 1, xv[1], chunk + (2 * w + 1) * 128);
-  }
-  __syncthreads();
-  f32x4 acc[2][4];  // [group parity: group g accumulates into acc[g & 1]][column tile of the group]
-  int prev_grp = -1, prev_t = 0;
-  for (int ch = 0; ch < nchunk; ++ch) {
-    const int c0 = tb + ch * kWideChunk;
-    const f32x4* cb = chunk + (ch & 1) * kWideChunk * 128;
-    const bool more = ch + 1 < nchunk;
-    if (more) xload(c0 + kWideChunk + 2 * w, xv);
-    const int ntile = min(kWideChunk, te - c0);
-    f32x4 n0 = cb[lane], n1 = cb[64 + lane];  // the next tile's A fragment, one tile ahead
-    for (int t = 0; t < ntile; ++t) {
-      const f32x4 a0 = n0, a1 = n1;
-      {
-        const int tn = min(t + 1, ntile - 1);
-        n0 = cb[tn * 128 + lane];
-        n1 = cb[tn * 128 + 64 + lane];
-      }
-      const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-#pragma unroll
-      for (int grp = 0; grp < CT / 4; ++grp) {
-        f32x4 (&cur)[4] = acc[grp & 1];
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) cur[cc] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (VAR == 2 || VAR == 3) {  // (development variants: no MFMAs)
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) cur[cc][r] = av[r] + bo[4 * grp + cc][r];
-        } else {
-#pragma unroll
-          for (int s = 0; s < 8; ++s)
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc)
-              cur[cc] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bo[4 * grp + cc][s], cur[cc], 0, 0, 0);
-        }
-        // the previous group's selection, interleaved into this group's MFMAs
-        if constexpr (VAR == 1 || VAR == 3) {  // (development variants: no selection)
-          bk[grp][0] ^= __float_as_int(acc[(grp + 1) & 1][0][0]);
-        } else if (grp > 0) {
-          sel(acc[(grp - 1) & 1], grp - 1, c0 + t);
-        } else if (prev_grp >= 0) {
-          sel(acc[(CT / 4 - 1) & 1], CT / 4 - 1, prev_t);
-        }
-        if constexpr (VAR != 4) {  // (VAR 4, development variant: the compiler's own schedule)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // 5 VALU
-          }
-        }
-      }
-      prev_grp = CT / 4 - 1;
-      prev_t = c0 + t;
-    }
-    if (more) {
-      f32x4* nb = chunk + ((ch + 1) & 1) * kWideChunk * 128;
-      emb_tile(c0 + kWideChunk + 2 * w, xv[0], nb + (2 * w) * 128);
-      emb_tile(c0 + kWideChunk + 2 * w + 1, xv[1], nb + (2 * w + 1) * 128);
-    }
-    __syncthreads();
-  }
-  if (prev_grp >= 0) sel(acc[(CT / 4 - 1) & 1], CT / 4 - 1, prev_t);
-  // per column tile: the 4 row offsets (smallest value, ties lowest row), then the lane groups
-#pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    unsigned long long best = ~0ull;
+  auto sel = [&](const f32x4& acc, int c, int t) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const unsigned row = bt[c][r] == 0x7fffffff ? 0x7fffffffu : (unsigned)(bt[c][r] * 16 + 4 * g + r);
-      const unsigned long long key = ((unsigned long long)(unsigned)bk[c][r] << 32) | row;
-      best = key < best ? key : best;
+      const int key = __float_as_int(acc[r]);
+      const bool lt = key < bk[c][r];
+      bt[c][r] = lt ? t : bt[c][r];
+      bk[c][r] = lt ? key : bk[c][r];
     }
+  };
+  // software pipeline: tile t's 8 column tiles in pairs (two accumulation chains each), the
+  // selection of pair p - 1 behind pair p's MFMAs, tile t + 1's emb MFMAs behind the last pair,
+  // the last pair's selection and tile t + 1's norm behind those; no branch in the body (the
+  // x loads past the wave's last tile re-read its last tile, their emb is never used)
+  float a[8];
+  float4 xn[2];
+  if (tb < te) {
+    emb(tb, xc, a);
+    xload(min(tb + 1, te - 1), xn);
+  }
+  for (int t = tb; t < te; ++t) {
+    f32x4 acc[kTop1CT];
 #pragma unroll
-    for (int off = 16; off <= 32; off <<= 1) {
-      const unsigned long long o = ((unsigned long long)(unsigned)__shfl_xor((int)(best >> 32), off) << 32) |
-                                   (unsigned)__shfl_xor((int)(best & 0xffffffffu), off);
-      best = o < best ? o : best;
+    for (int p = 0; p < kTop1CT / 2; ++p) {
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bo[2 * p][s], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bo[2 * p + 1][s], a1, 0, 0, 0);
+      }
+      acc[2 * p] = a0;
+      acc[2 * p + 1] = a1;
+      if (p > 0) {
+        sel(acc[2 * p - 2], 2 * p - 2, t);
+        sel(acc[2 * p - 1], 2 * p - 1, t);
+      }
     }
-    const int j = (CT * (4 * cg + w) + c) * 16 + c16;
-    if (g != 0 || j >= N2) continue;
-    if (RS == 1) {
-      const unsigned row = (unsigned)(best & 0xffffffffu);
-      out_idx[(int64_t)b * V2max + j] = row >= 0x7fffffffu ? -1 : (int64_t)row;
-      if (out_dist) out_dist[(int64_t)b * V2max + j] = sqrtf(__int_as_float((int)(best >> 32)));
-    } else {
-      __hip_atomic_store(part + ((int64_t)b * RS + rs) * V2max + j, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    f32x4 e[2];
+    emb_mfma(xn, e);
+    xload(min(t + 2, te - 1), xn);
+    sel(acc[kTop1CT - 2], kTop1CT - 2, t);
+    sel(acc[kTop1CT - 1], kTop1CT - 1, t);
+    emb_norm(t + 1, e, a);
+  }
+  FD_STAMP(2, __builtin_amdgcn_s_memtime());
+  // per column tile: the lane's best (key, row) over its 4 row offsets
+  unsigned long long best[kTop1CT];
+  unsigned clampmask = 0;
+#pragma unroll
+  for (int c = 0; c < kTop1CT; ++c) {
+    best[c] = ~0ull;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      clampmask |= (bk[c][r] <= kClampBits ? 1u : 0u) << c;
+      const unsigned row = bt[c][r] < 0 ? 0x7fffffffu : (unsigned)(bt[c][r] * 16 + 4 * g + r);
+      const unsigned long long key = ((unsigned long long)(unsigned)bk[c][r] << 32) | row;
+      best[c] = key < best[c] ? key : best[c];
     }
   }
-  if (RS == 1) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through keys
+  // a column with a distance at or below torch.cdist's clamp: its first such row (rare)
+  if (__builtin_amdgcn_ballot_w64(clampmask != 0)) {
+    for (int c = 0; c < kTop1CT; ++c) {
+      if (!__builtin_amdgcn_ballot_w64((clampmask >> c) & 1)) continue;  // (wave-uniform)
+      unsigned frow = 0x7fffffffu;
+      for (int t = tb; t < te; ++t) {
+        float4 xv[2];
+        xload(t, xv);
+        float a[8];
+        emb(t, xv, a);
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bo[c][s], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (frow == 0x7fffffffu && __float_as_int(acc[r]) <= kClampBits) frow = (unsigned)(t * 16 + 4 * g + r);
+      }
+      if (frow != 0x7fffffffu) best[c] = ((unsigned long long)(unsigned)kClampBits << 32) | frow;
+    }
+  }
+  // the 4 lane groups of each column (rows 4 g + r of every tile), then the waves through LDS
+#pragma unroll
+  for (int off = 16; off <= 32; off <<= 1)
+#pragma unroll
+    for (int c = 0; c < kTop1CT; ++c) {
+      const unsigned long long o = ((unsigned long long)(unsigned)__shfl_xor((int)(best[c] >> 32), off) << 32) |
+                                   (unsigned)__shfl_xor((int)(best[c] & 0xffffffffu), off);
+      best[c] = o < best[c] ? o : best[c];
+    }
+  if (g == 0) {
+#pragma unroll
+    for (int c = 0; c < kTop1CT; ++c) wkeys[w][c * 16 + c16] = best[c];
+  }
+  FD_STAMP(3, __builtin_amdgcn_s_memtime());
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(arrivals + (int64_t)b * NCG + cg, 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == RS - 1;
-    if (last) __hip_atomic_store(arrivals + (int64_t)b * NCG + cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (orders the loads after the ticket)
-  for (int jj = threadIdx.x; jj < 4 * CT * 16; jj += 256) {
-    const int j = CT * 4 * 16 * cg + jj;
-    if (j >= N2) continue;
-    unsigned long long best = ~0ull;
-    for (int r = 0; r < RS; ++r) {
-      const unsigned long long key =
-          __hip_atomic_load(part + ((int64_t)b * RS + r) * V2max + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      best = key < best ? key : best;
+  if (tid < kTop1CT * 16) {
+    const int jj = tid, j = j0 + jj;
+    if (j < N2) {
+      unsigned long long bb = wkeys[0][jj];
+#pragma unroll
+      for (int v = 1; v < kTop1Waves; ++v) bb = wkeys[v][jj] < bb ? wkeys[v][jj] : bb;  // ties: lower wave = lower row
+      if (RS == 1) {
+        const unsigned row = (unsigned)(bb & 0xffffffffu);
+        out_idx[(int64_t)b * V2max + j] = row >= 0x7fffffffu ? -1 : (int64_t)row;
+        if (out_dist) out_dist[(int64_t)b * V2max + j] = sqrtf(__int_as_float((int)(bb >> 32)));
+      } else {
+        part[((int64_t)b * RS + rs) * V2max + j] = bb;
+      }
     }
-    const unsigned row = (unsigned)(best & 0xffffffffu);
-    out_idx[(int64_t)b * V2max + j] = row >= 0x7fffffffu ? -1 : (int64_t)row;
-    if (out_dist) out_dist[(int64_t)b * V2max + j] = sqrtf(__int_as_float((int)(best >> 32)));
   }
+  FD_STAMP(4, __builtin_amdgcn_s_memtime());
+}
+
+// RS > 1: grid (ceil(V2max / 256), B): the smallest of each column's RS row-part keys (value,
+// then row: the first index), written as the index and the clamped distance
+__global__ __launch_bounds__(256) void fd_top1_merge_kernel(const unsigned long long* __restrict__ part,
+                                                            const int32_t* __restrict__ n2, int V2max, int RS,
+                                                            int64_t* __restrict__ out_idx, float* __restrict__ out_dist) {
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n2[b]) return;
+  unsigned long long best = ~0ull;
+  for (int r = 0; r < RS; ++r) {
+    const unsigned long long key = part[((int64_t)b * RS + r) * V2max + j];
+    best = key < best ? key : best;
+  }
+  const unsigned row = (unsigned)(best & 0xffffffffu);
+  out_idx[(int64_t)b * V2max + j] = row >= 0x7fffffffu ? -1 : (int64_t)row;
+  if (out_dist) out_dist[(int64_t)b * V2max + j] = sqrtf(__int_as_float((int)(best >> 32)));
+}
+
+struct Top1Plan {
+  int NCG, RS;
+  int64_t part_bytes;
+};
+
+inline int64_t al256_(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+inline Top1Plan top1_plan(int B, int V1max, int V2max) {
+  Top1Plan p{};
+  const int T1 = (V1max + 15) / 16, T2 = (V2max + 15) / 16;
+  p.NCG = std::max(1, (T2 + kTop1CT - 1) / kTop1CT);
+  const int64_t blocks = (int64_t)B * p.NCG;
+  // row parts only when the batch leaves the chip short of blocks (each wave keeps >= 2 row tiles)
+  const int rs = blocks >= 192 ? 1 : (int)((256 + blocks - 1) / blocks);
+  p.RS = std::max(1, std::min(rs, T1 / (2 * kTop1Waves)));
+  p.part_bytes = p.RS > 1 ? al256_((int64_t)B * p.RS * V2max * 8) : 0;
+  return p;
 }
 
 // pass 3 (RS > 1): grid (ceil(V2max / 256), B): merge the RS partial lists of each column in
@@ -1635,92 +869,16 @@ inline FdPlan fd_plan(int B, int V1max, int V2max, int topk, int mode) {
   return p;
 }
 
-// the fused fp32 pass: NW = 8 waves per block, CT column tiles per wave (4 for the argmin, 2 for
-// the top-5 lists), row parts RS so that the grid holds >= 512 blocks (two per CU)
-constexpr int kFusedNW = 8;
-inline int fused_ct(int topk) { return topk == 1 ? 4 : 2; }
-
-struct FusedPlan {
-  int NCG, RS;
-  int64_t ctr_bytes, pv_bytes;
-};
-
-inline FusedPlan fused_plan(int B, int V1max, int V2max, int topk) {
-  FusedPlan p{};
-  const int T1 = (V1max + 15) / 16, T2 = (V2max + 15) / 16;
-  p.NCG = std::max(1, (T2 + kFusedNW * fused_ct(topk) - 1) / (kFusedNW * fused_ct(topk)));
-  const int64_t blocks = (int64_t)B * p.NCG;
-  const int rs = blocks >= 512 ? 1 : (int)((512 + blocks - 1) / blocks);
-  p.RS = std::max(1, std::min(rs, T1));
-  p.pv_bytes = p.RS > 1 ? al256((int64_t)B * p.RS * V2max * topk * 4) : 0;
-  p.ctr_bytes = al256((int64_t)B * std::max(T2, 1) * 4);  // (>= B x NCG of every one-launch plan)
-  return p;
-}
-
-struct WidePlan {
-  int NCG, RS;
-  int64_t part_bytes;
-};
-
-inline WidePlan wide_plan(int B, int V1max, int V2max) {
-  WidePlan p{};
-  const int T1 = (V1max + 15) / 16, T2 = (V2max + 15) / 16;
-  p.NCG = std::max(1, (T2 + 4 * kWideCT - 1) / (4 * kWideCT));
-  const int64_t blocks = (int64_t)B * p.NCG;
-#ifdef PK_DEVBUILD
-  static const int target = [] {  // development knob PK_FD_BLOCKS: grid target (256 = 1 per CU)
-    const char* e = std::getenv("PK_FD_BLOCKS");
-    return e ? std::atoi(e) : 256;
-  }();
-#else
-  constexpr int target = 256;
-#endif
-  const int rs = blocks >= target ? 1 : (int)((target + blocks - 1) / blocks);
-  p.RS = std::max(1, std::min(rs, T1));
-  p.part_bytes = p.RS > 1 ? al256((int64_t)B * p.RS * V2max * 8) : 0;
-  return p;
-}
-
-// the split fp32 path: CT column tiles per block (one column group), NW waves splitting the rows
-constexpr int kColsNW = 8;
-inline int cols_ct(int topk) { return topk == 1 ? 4 : 2; }
-
-struct ColsPlan {
-  int T1, NCG, RS;
-  int64_t a_bytes, pv_bytes;
-};
-
-inline ColsPlan cols_plan(int B, int V1max, int V2max, int topk) {
-  ColsPlan p{};
-  p.T1 = (V1max + 15) / 16;
-  const int T2 = (V2max + 15) / 16;
-  p.NCG = std::max(1, (T2 + cols_ct(topk) - 1) / cols_ct(topk));
-  const int64_t blocks = (int64_t)B * p.NCG;
-  const int rs = blocks >= 512 ? 1 : (int)((512 + blocks - 1) / blocks);
-  p.RS = std::max(1, std::min(rs, p.T1 / kColsNW));
-  p.a_bytes = al256((int64_t)B * p.T1 * 2048);
-  p.pv_bytes = p.RS > 1 ? al256((int64_t)B * p.RS * V2max * topk * 4) : 0;
-  return p;
-}
-
 }  // namespace
 
 extern "C" int64_t pk_feat_dist_work_size(int B, int V1max, int V2max, int topk, int mode) {
   if (B < 0 || V1max < 0 || V2max < 0 || !(topk == 1 || topk == 5) || mode < 0 || mode > 2) return -1;
   const FdPlan p = fd_plan(B, V1max, V2max, topk, mode);
   const int64_t two_pass = p.a_bytes + p.b_bytes + p.na_bytes + p.nb_bytes + p.pv_bytes + p.pi_bytes;
-  if (mode != 0) return two_pass;
-  // mode 0: the fused pass's arrival words lead the buffer (pk_feat_dist_counter_bytes), then the
-  // larger of its partial lists and the fallback paths' scratch (unaligned operand rows)
-  const FusedPlan f = fused_plan(B, V1max, V2max, topk);
-  const ColsPlan c = cols_plan(B, V1max, V2max, topk);
-  const WidePlan wp = wide_plan(B, V1max, V2max);
-  return f.ctr_bytes + std::max(std::max(std::max(two_pass, 2 * f.pv_bytes), c.a_bytes + 2 * c.pv_bytes), wp.part_bytes);
-}
-
-extern "C" int64_t pk_feat_dist_counter_bytes(int B, int V1max, int V2max, int topk, int mode) {
-  if (B < 0 || V1max < 0 || V2max < 0 || !(topk == 1 || topk == 5) || mode < 0 || mode > 2) return -1;
-  return mode == 0 ? fused_plan(B, V1max, V2max, topk).ctr_bytes : 0;
+  if (mode != 0 || topk != 1) return two_pass;
+  // mode 0 top-1: the one-launch pass's row-part keys, or the two-pass fallback's scratch
+  // (unaligned operand rows); neither keeps anything across calls
+  return std::max(two_pass, top1_plan(B, V1max, V2max).part_bytes);
 }
 
 extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, const float* evecs_y, int ldy,
@@ -1730,96 +888,35 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
   PK_REQUIRE(B >= 0 && V1max >= 0 && V2max >= 0 && ldx >= kF && ldy >= kF && (topk == 1 || topk == 5));
   PK_REQUIRE(mode >= 0 && mode <= 2);
   if (B == 0 || V2max == 0) return PK_OK;
-  PK_REQUIRE(evecs_x && C && evecs_y && n1 && n2 && work && out_idx);
-  PK_REQUIRE(work_bytes >= pk_feat_dist_work_size(B, V1max, V2max, topk, mode));
+  PK_REQUIRE(evecs_x && C && evecs_y && n1 && n2 && out_idx);
+  const int64_t need = pk_feat_dist_work_size(B, V1max, V2max, topk, mode);
+  PK_REQUIRE(work_bytes >= need && (work || need == 0));
   hipStream_t s = pk::as_stream(stream);
   const bool aligned = (ldx % 4) == 0 && (ldy % 4) == 0 && (reinterpret_cast<uintptr_t>(evecs_x) & 15) == 0 &&
                        (reinterpret_cast<uintptr_t>(evecs_y) & 15) == 0;
-#ifdef PK_DEVBUILD
-  static const int path = [] {  // development knob PK_FD_PATH: 0 default (top-1: one launch, top-5: two
-                                //   passes), 1 rows + cols, 2 two-pass, 3 fused 8-wave pass
-    const char* e = std::getenv("PK_FD_PATH");
-    return e ? std::atoi(e) : 0;
-  }();
-#else
-  constexpr int path = 0;
-#endif
-  // mode 0 work layout: [arrival words][scratch of the path taken]
-  const int64_t ctr_bytes = mode == 0 ? fused_plan(B, V1max, V2max, topk).ctr_bytes : 0;
-  int32_t* arrivals = static_cast<int32_t*>(work);
-  work = static_cast<char*>(work) + ctr_bytes;
-  if (mode == 0 && aligned && V1max > 0 && topk == 1 && path == 0) {  // one wave per SIMD, one launch
-    const WidePlan wp = wide_plan(B, V1max, V2max);
+  if (mode == 0 && aligned && V1max > 0 && topk == 1) {  // one launch (+ a merge launch when RS > 1)
+    const Top1Plan tp = top1_plan(B, V1max, V2max);
     auto* part = static_cast<unsigned long long*>(work);
-    const dim3 wgrid((unsigned)((int64_t)B * wp.NCG * wp.RS));
+    const dim3 grid((unsigned)((int64_t)B * tp.NCG * tp.RS));
 #ifdef PK_DEVBUILD
-    static const int wvar = [] {  // development knob PK_FD_VAR: 1 no selection, 2 no MFMAs, 3 neither,
-      // 4 no sched_group_barrier, 5 value-only selection, 6 integer select, 7 AGPR accumulators,
-      // 8 med3 + compare + select, 9 value-only med3
+    static const int tvar = [] {  // development knob PK_FD_VAR: limiter variants of fd_top1_kernel
       const char* e = std::getenv("PK_FD_VAR");
       return e ? std::atoi(e) : 0;
     }();
-#define PK_FDW(V) hipLaunchKernelGGL((fd_wide_kernel<kWideCT, V>), wgrid, dim3(256), 0, s, evecs_x, ldx, C, evecs_y, \
-                                     ldy, n1, n2, V1max, V2max, wp.NCG, wp.RS, out_idx, out_dist, part, arrivals)
-    if (wvar == 1) PK_FDW(1); else if (wvar == 2) PK_FDW(2); else if (wvar == 3) PK_FDW(3);
-    else if (wvar == 4) PK_FDW(4); else if (wvar == 5) PK_FDW(5); else if (wvar == 6) PK_FDW(6); else if (wvar == 7) PK_FDW(7); else if (wvar == 8) PK_FDW(8); else if (wvar == 9) PK_FDW(9); else PK_FDW(0);
-#undef PK_FDW
+#define PK_FDT(V) hipLaunchKernelGGL((fd_top1_kernel<V>), grid, dim3(64 * kTop1Waves), 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, \
+                                     n2, V1max, V2max, tp.NCG, tp.RS, out_idx, out_dist, part)
+    if (tvar == 1) PK_FDT(1); else if (tvar == 13) PK_FDT(13); else PK_FDT(0);
+#undef PK_FDT
 #else
-    hipLaunchKernelGGL(fd_wide_kernel<kWideCT>, wgrid, dim3(256), 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, n2, V1max,
-                       V2max, wp.NCG, wp.RS, out_idx, out_dist, part, arrivals);
+    hipLaunchKernelGGL(fd_top1_kernel<0>, grid, dim3(64 * kTop1Waves), 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, n2, V1max, V2max,
+                       tp.NCG, tp.RS, out_idx, out_dist, part);
 #endif
     PK_CHECK_LAUNCH();
-    return PK_OK;
-  }
-  if (mode == 0 && aligned && V1max > 0 && path == 1) {  // rows + cols
-    const ColsPlan c = cols_plan(B, V1max, V2max, topk);
-    f32x4* A = static_cast<f32x4*>(work);
-    float* pv = c.RS > 1 ? reinterpret_cast<float*>(static_cast<char*>(work) + c.a_bytes) : nullptr;
-    int32_t* pi = c.RS > 1 ? reinterpret_cast<int32_t*>(static_cast<char*>(work) + c.a_bytes + c.pv_bytes) : nullptr;
-    hipLaunchKernelGGL(fd_rows_kernel, dim3((c.T1 + 3) / 4, B), dim3(256), 0, s, evecs_x, ldx, C, n1, V1max, c.T1, A);
-    PK_CHECK_LAUNCH();
-    const dim3 grid((unsigned)((int64_t)B * c.NCG * c.RS)), block(64 * kColsNW);
-    if (topk == 1)
-      hipLaunchKernelGGL((fd_cols_kernel<1, 4, kColsNW>), grid, block, 0, s, A, evecs_y, ldy, n1, n2, V2max, c.T1, c.NCG,
-                         c.RS, out_idx, out_dist, pv, pi);
-    else
-      hipLaunchKernelGGL((fd_cols_kernel<5, 2, kColsNW>), grid, block, 0, s, A, evecs_y, ldy, n1, n2, V2max, c.T1, c.NCG,
-                         c.RS, out_idx, out_dist, pv, pi);
-    PK_CHECK_LAUNCH();
-    if (c.RS > 1) {
-      const dim3 mg((V2max + 255) / 256, B);
-      if (topk == 1)
-        hipLaunchKernelGGL(fd_merge_kernel<1>, mg, dim3(256), 0, s, pv, pi, n2, V2max, c.RS, out_idx, out_dist);
-      else
-        hipLaunchKernelGGL(fd_merge_kernel<5>, mg, dim3(256), 0, s, pv, pi, n2, V2max, c.RS, out_idx, out_dist);
+    if (tp.RS > 1) {
+      hipLaunchKernelGGL(fd_top1_merge_kernel, dim3((V2max + 255) / 256, B), dim3(256), 0, s, part, n2, V2max, tp.RS,
+                         out_idx, out_dist);
       PK_CHECK_LAUNCH();
     }
-    return PK_OK;
-  }
-  if (mode == 0 && aligned && V1max > 0 && path == 3) {  // the fused pass
-    const FusedPlan f = fused_plan(B, V1max, V2max, topk);
-    float* pv = f.RS > 1 ? static_cast<float*>(work) : nullptr;
-    int32_t* pi = f.RS > 1 ? reinterpret_cast<int32_t*>(static_cast<char*>(work) + f.pv_bytes) : nullptr;
-    const dim3 grid((unsigned)((int64_t)B * f.NCG * f.RS)), block(64 * kFusedNW);
-#ifdef PK_DEVBUILD
-    static const int var = [] {  // development knob PK_FD_VAR (limiter study): 1 no selection, 2 no
-      const char* e = std::getenv("PK_FD_VAR");  // main-loop MFMAs, 3 neither
-      return e ? std::atoi(e) : 0;
-    }();
-    if (topk == 1 && var >= 1 && var <= 3) {
-#define PK_FDV(V) hipLaunchKernelGGL((fd_fused_kernel<1, 4, kFusedNW, V>), grid, block, 0, s, evecs_x, ldx, C, evecs_y, \
-                                     ldy, n1, n2, V1max, V2max, f.NCG, f.RS, out_idx, out_dist, pv, pi, arrivals)
-      if (var == 1) PK_FDV(1); else if (var == 2) PK_FDV(2); else PK_FDV(3);
-#undef PK_FDV
-    } else
-#endif
-    if (topk == 1)
-      hipLaunchKernelGGL((fd_fused_kernel<1, 4, kFusedNW>), grid, block, 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, n2,
-                         V1max, V2max, f.NCG, f.RS, out_idx, out_dist, pv, pi, arrivals);
-    else
-      hipLaunchKernelGGL((fd_fused_kernel<5, 2, kFusedNW>), grid, block, 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, n2,
-                         V1max, V2max, f.NCG, f.RS, out_idx, out_dist, pv, pi, arrivals);
-    PK_CHECK_LAUNCH();
     return PK_OK;
   }
   const FdPlan p = fd_plan(B, V1max, V2max, topk, mode);
@@ -1838,25 +935,9 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
 #undef PK_FD_PREP
   PK_CHECK_LAUNCH();
   const dim3 grid((unsigned)((int64_t)B * p.NCG * p.RS)), block(64 * kWaves);
-#ifdef PK_DEVBUILD
-  static const int direct = [] {  // development knob PK_FD_DIRECT: 0 = LDS-ring main pass
-    const char* e = std::getenv("PK_FD_DIRECT");
-    return e ? std::atoi(e) : 1;
-  }();
-#define PK_FD_MAIN(K, M)                                                                                          \
-  do {                                                                                                            \
-    if (direct)                                                                                                   \
-      hipLaunchKernelGGL((fd_main_direct_kernel<K, M>), grid, block, 0, s, A, Bq, nA, nB, n1, n2, p.T1, p.T2,     \
-                         V2max, p.NCG, p.RS, out_idx, out_dist, pv, pi);                                          \
-    else                                                                                                          \
-      hipLaunchKernelGGL((fd_main_kernel<K, M>), grid, block, 0, s, A, Bq, nA, nB, n1, n2, p.T1, p.T2, V2max,     \
-                         p.NCG, p.RS, out_idx, out_dist, pv, pi);                                                 \
-  } while (0)
-#else
 #define PK_FD_MAIN(K, M)                                                                                          \
   hipLaunchKernelGGL((fd_main_direct_kernel<K, M>), grid, block, 0, s, A, Bq, nA, nB, n1, n2, p.T1, p.T2, V2max,  \
                      p.NCG, p.RS, out_idx, out_dist, pv, pi)
-#endif
   if (topk == 1) {
     if (mode == 0) PK_FD_MAIN(1, 0); else if (mode == 1) PK_FD_MAIN(1, 1); else PK_FD_MAIN(1, 2);
   } else {
@@ -1874,3 +955,11 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
   }
   return PK_OK;
 }
+
+#ifdef PK_DEVBUILD
+// development: the VAR 13 phase stamps of the last fd_top1_kernel launch (8 per block)
+extern "C" int pkdev_fd_stamps(unsigned long long* host, int n) {
+  if (n > 4096 * 8) n = 4096 * 8;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fd_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -48,12 +48,16 @@ __device__ __forceinline__ bool better(int g1, double r1, int64_t h1, int g2, do
 }
 
 __device__ __forceinline__ void load_hyp(const double* __restrict__ src, const double* __restrict__ dst,
-                                         const int32_t* __restrict__ cr, int n, uint64_t seed, int64_t h,
+                                         int64_t ns, int64_t nd, const int32_t* __restrict__ cr, int n, uint64_t seed,
+                                         int64_t h,
                                          const int32_t* __restrict__ hyps, double s4[4][3], double d4[4][3]) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = hyps ? hyps[4 * h + j] : hyp_index(seed, h, j, n);
-    const int64_t si = cr[2 * c], di = cr[2 * c + 1];
+    // out-of-range rows are read at 0 (no fault) and reported by ransac_final_kernel
+    const int cc = (c >= 0 && c < n) ? c : 0;
+    const int64_t si0 = cr[2 * cc], di0 = cr[2 * cc + 1];
+    const int64_t si = (si0 >= 0 && si0 < ns) ? si0 : 0, di = (di0 >= 0 && di0 < nd) ? di0 : 0;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       s4[j][k] = src[3 * si + k];
@@ -114,8 +118,8 @@ __global__ __launch_bounds__(kRThreads) void ransac_fit_kernel(
   const int n = (int)(cor_off[b + 1] - c0);
   if (h >= H || n < 4) return;
   double s4[4][3], d4[4][3], R[9], t[3];
-  load_hyp(src + 3 * src_off[b], dst + 3 * dst_off[b], corres + 2 * c0, n, seed, h,
-           hyps ? hyps + 4 * hyp_off[b] : nullptr, s4, d4);
+  load_hyp(src + 3 * src_off[b], dst + 3 * dst_off[b], src_off[b + 1] - src_off[b], dst_off[b + 1] - dst_off[b],
+           corres + 2 * c0, n, seed, h, hyps ? hyps + 4 * hyp_off[b] : nullptr, s4, d4);
   rigid_fit4(s4, d4, R, t);
   double* o = RT + (int64_t)b * 12 * H + h;
 #pragma unroll
@@ -146,6 +150,7 @@ __global__ __launch_bounds__(kRThreads) void ransac_score_kernel(
   const int32_t* cr = corres + 2 * c0;
   const double* S = src + 3 * src_off[b];
   const double* Dp = dst + 3 * dst_off[b];
+  const int64_t ns = src_off[b + 1] - src_off[b], nd = dst_off[b + 1] - dst_off[b];
   double R[9], t[3];
   if (act) {
     const double* r = RT + (int64_t)b * 12 * H + h;
@@ -160,7 +165,8 @@ __global__ __launch_bounds__(kRThreads) void ransac_score_kernel(
     const int tn = min(tile_len, e1 - t0);
     __syncthreads();
     for (int e = threadIdx.x; e < tn; e += kRThreads) {
-      const int64_t si = cr[2 * (t0 + e)], di = cr[2 * (t0 + e) + 1];
+      const int64_t si0 = cr[2 * (t0 + e)], di0 = cr[2 * (t0 + e) + 1];
+      const int64_t si = (si0 >= 0 && si0 < ns) ? si0 : 0, di = (di0 >= 0 && di0 < nd) ? di0 : 0;
       sp[6 * e + 0] = S[3 * si];
       sp[6 * e + 1] = S[3 * si + 1];
       sp[6 * e + 2] = S[3 * si + 2];
@@ -249,16 +255,40 @@ __global__ __launch_bounds__(kRThreads) void ransac_reduce_kernel(const int64_t*
 }
 
 // grid (B), block 256: best over blocks; the winner's stored pose -> T (4x4 row-major), stats.
+// The index check of every crop (status[b] = 1 when a correspondence row lies outside its crop's
+// source / target points, or a caller-given hypothesis row outside [0, n): those reads went to
+// row 0 instead of faulting) — written for every crop, so status needs no initialisation.
 __global__ __launch_bounds__(256) void ransac_final_kernel(const int64_t* __restrict__ cor_off, int64_t H, int nblk,
                                                            const double* __restrict__ RT,
                                                            const int* __restrict__ bgood,
                                                            const double* __restrict__ brmse,
                                                            const int64_t* __restrict__ bh, double* __restrict__ T,
-                                                           double* __restrict__ stats) {
+                                                           double* __restrict__ stats, const int32_t* __restrict__ corres,
+                                                           const int64_t* __restrict__ src_off,
+                                                           const int64_t* __restrict__ dst_off,
+                                                           const int32_t* __restrict__ hyps,
+                                                           const int64_t* __restrict__ hyp_off,
+                                                           int32_t* __restrict__ status) {
   __shared__ int sg[4];
   __shared__ double sr[4];
   __shared__ int64_t shh[4];
   const int b = blockIdx.x;
+  if (status) {
+    const int64_t c0 = cor_off[b], nc = cor_off[b + 1] - c0;
+    const int64_t ns = src_off[b + 1] - src_off[b], nd = dst_off[b + 1] - dst_off[b];
+    int bad = 0;
+    for (int64_t e = threadIdx.x; e < nc; e += 256) {
+      const int64_t si = corres[2 * (c0 + e)], di = corres[2 * (c0 + e) + 1];
+      bad |= (si < 0 || si >= ns || di < 0 || di >= nd) ? 1 : 0;
+    }
+    if (hyps && nc >= 4)
+      for (int64_t e = threadIdx.x; e < 4 * H; e += 256) {
+        const int c = hyps[4 * hyp_off[b] + e];
+        bad |= (c < 0 || c >= nc) ? 1 : 0;
+      }
+    bad = __syncthreads_or(bad);
+    if (threadIdx.x == 0) status[b] = bad;
+  }
   int good = -1;
   double rmse = 0.0;
   int64_t hh = INT64_MAX;
@@ -323,7 +353,7 @@ extern "C" int64_t pk_ransac_work_size(int B, int64_t H, int nmax) {
 extern "C" int pk_ransac(const double* src, const int64_t* src_off, const double* dst, const int64_t* dst_off,
                          const int32_t* corres, const int64_t* cor_off, const int32_t* hyps, const int64_t* hyp_off,
                          uint64_t seed, int64_t H, double max_dist, int B, int nmax, void* work, int64_t work_bytes,
-                         double* T, double* stats, void* stream) {
+                         double* T, double* stats, int32_t* status, void* stream) {
   PK_REQUIRE(B >= 0 && H >= 0 && max_dist > 0.0 && nmax >= 0);
   if (B == 0) return PK_OK;
   PK_REQUIRE(src && src_off && dst && dst_off && corres && cor_off && work && T && stats);
@@ -346,7 +376,7 @@ extern "C" int pk_ransac(const double* src, const int64_t* src_off, const double
     PK_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(ransac_final_kernel, dim3(B), dim3(256), 0, s, cor_off, H, nhb, w.RT, w.bgood, w.brmse, w.bh,
-                     T, stats);
+                     T, stats, corres, src_off, dst_off, hyps, hyp_off, status);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

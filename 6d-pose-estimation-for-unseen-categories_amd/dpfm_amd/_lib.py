@@ -54,7 +54,7 @@ SIGNATURES = {
     "pk_backproject": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P],
     "pk_sor": [_P, _P, _I, _I, _I, _D, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "pk_fps_npoint": [_P, _I, _I, _I, _U64, _I64, _P, _P, _P, _P],
-    "pk_gather_transform": [_P, _P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P],
+    "pk_gather_transform": [_P, _P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "pk_collate_pad": [_P, _I, _I, _P, _I, _I, _P, _P, _P],
     "pk_segment_scan": [_P, _I, _I, _P, _P, _P],
     "pk_offsets_from_counts": [_P, _I, _P, _P],
@@ -87,16 +87,15 @@ SIGNATURES = {
     "pk_resolvent_mask": [_P, _I, _P, _I, _I, _I, _F, _P, _P],
     "pk_linear_fwd": [_P, _P, _P, _I, _I64, _I, _I, _I, _I, _I, _P, _P, _P],
     "pk_feat_dist_work_size": [_I, _I, _I, _I, _I],
-    "pk_feat_dist_counter_bytes": [_I, _I, _I, _I, _I],
     "pk_feat_dist_topk": [_P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I64, _P, _P, _P],
     "pk_rigidity_filter_work_size": [_I, _I, _I],
     "pk_rigidity_filter": [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P],
-    "pk_inlier_ratio": [_P, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P],
+    "pk_inlier_ratio": [_P, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P, _P],
     "pk_cgt_lstsq_work_size": [_I, _I, _I],
     "pk_nce_select": [_P, _I, _I64, _I, ctypes.c_uint64, _P, _P, _P, _P],
     "pk_cgt_lstsq": [_P, _I, _P, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P],
     "pk_ransac_work_size": [_I, _I64, _I],
-    "pk_ransac": [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _I64, _D, _I, _I, _P, _I64, _P, _P, _P],
+    "pk_ransac": [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _I64, _D, _I, _I, _P, _I64, _P, _P, _P, _P],
     "pk_pose_metrics": [_P, _P, _I, _I, _P, _P, _P, _P, _P],
     "pk_erode_mask": [_P, _I, _I, _I, _P, _P],
     "pk_sample_rgb": [_P, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],
@@ -125,7 +124,7 @@ SIGNATURES = {
 }
 
 RESTYPES = {"pk_cgt_lstsq_work_size": _I64, "pk_linear_wgrad_grouped_work": _I64, "pk_ransac_work_size": _I64,
-            "pk_feat_dist_work_size": _I64, "pk_feat_dist_counter_bytes": _I64, "pk_fmap_head_work_len": _I64, "pk_icp_work_size": _I64,
+            "pk_feat_dist_work_size": _I64, "pk_fmap_head_work_len": _I64, "pk_icp_work_size": _I64,
             "pk_rigidity_filter_work_size": _I64}  # everything else returns an int status
 
 _lib: Optional[ctypes.CDLL] = None

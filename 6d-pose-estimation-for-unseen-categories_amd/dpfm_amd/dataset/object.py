@@ -160,6 +160,9 @@ class Crops:
     # f32 [F, k, k] ground-truth functional map (utils/utils.py:67-79) when the producer formed it
     # beside the crops (PipelinedTrainer: on the crop-formation stream); None: the step solves it
     C_gt: Optional[torch.Tensor] = None
+    # int32 [F] per crop 1 when an FPS index fell outside its crop (pk_gather_transform's check;
+    # those points are NaN): checked by check(), never read on the step's path
+    index_status: Optional[torch.Tensor] = None
 
     def overflow(self) -> torch.Tensor:
         """0-d bool on the device: some crop had more ball-query pairs than pair_cap (its P
@@ -170,8 +173,10 @@ class Crops:
         return (self.npairs > self.pair_cap).any()
 
     def check(self) -> None:
-        """Host-synchronising: raise if a pair list overflowed its capacity."""
+        """Host-synchronising: raise if a pair list overflowed its capacity or an FPS index was
+        out of range."""
         ops.check_capacity(self.npairs, self.pair_cap, "ball-query pairs (CropFormation pair_cap)")
+        ops.check_index_status(self.index_status, "CropFormation (FPS indices)")
 
 
 class CropFormation:
@@ -215,8 +220,9 @@ class CropFormation:
         else:
             ld = npmax
         idx = ops.fps_packed(so["xyz32"], so["off"], fb.max_pixels, pol["start"], pol["npoint"], npmax)
+        st = torch.empty((F_,), dtype=torch.int32, device=fb.depth.device)
         g = ops.gather_transform(so["xyz64"], so["off"], idx, pol["npoint"], npmax, pol["off"], fb.R, fb.t,
-                                 F_ * npmax, want_sel32=False)
+                                 F_ * npmax, want_sel32=False, status=st)
         pc32, n2 = ops.collate_pad(g["sel64"], pol["off"], ld)       # PC["xyz"]: f32(pcd), padded
         align32, _ = ops.collate_pad(g["align"], pol["off"], ld)     # Obj["align_pc"]
         n1max = fb.n1max or self.n1
@@ -226,4 +232,4 @@ class CropFormation:
         return Crops(pc64=g["sel64"], pc32=pc32, align64=g["align"], align32=align32, off=pol["off"], n2=n2, ld=ld,
                      npoint=pol["npoint"], pairs=bq["pairs"], npairs=bq["count"], overlap_12=bq["overlap_12"],
                      overlap_21=bq["overlap_21"], rgb=rgb, kept=so["kept"], pair_cap=self.pair_cap,
-                     overflow_flag=(bq["count"] > self.pair_cap).any())
+                     overflow_flag=(bq["count"] > self.pair_cap).any(), index_status=st)

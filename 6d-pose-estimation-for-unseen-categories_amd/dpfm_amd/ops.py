@@ -93,6 +93,29 @@ def ball_query(cad: torch.Tensor, cad_off: torch.Tensor, pc: torch.Tensor, pc_of
                 thr2=thr2)
 
 
+def check_index_status(status: Optional[torch.Tensor], what: str) -> None:
+    """Host-synchronising check of an index consumer's per-crop status (pk_inlier_ratio,
+    pk_gather_transform, pk_ransac: 1 = an index outside its array was met; the kernel did not
+    read through it). Raises PoseKernError naming the crops."""
+    if status is None or status.numel() == 0:
+        return
+    bad = torch.nonzero(status).flatten()
+    if bad.numel():
+        raise _lib.PoseKernError(f"{what}: out-of-range index in crop(s) {bad[:8].tolist()}"
+                                 f"{' ...' if bad.numel() > 8 else ''}")
+
+
+def _index_status(B: int, dev, status: Optional[torch.Tensor], check: Optional[bool]):
+    """(status buffer to pass, whether to check it after the call): a caller-given buffer is
+    written and left to the caller; otherwise a temporary one is checked right after the call
+    (host sync) unless a HIP graph is being captured (no check, nothing to hold it)."""
+    if status is not None:
+        return status, bool(check)
+    if torch.cuda.is_current_stream_capturing():
+        return None, False
+    return torch.empty((B,), dtype=torch.int32, device=dev), check is None or bool(check)
+
+
 def check_capacity(count: torch.Tensor, cap: int, what: str = "pairs") -> None:
     """Host-synchronising overflow check for capacity/count outputs."""
     m = int(count.max().item()) if count.numel() else 0
@@ -197,16 +220,23 @@ def collate_pad(src: torch.Tensor, off: torch.Tensor, ld: int) -> tuple[torch.Te
 
 def gather_transform(pcd: torch.Tensor, off: torch.Tensor, idx: Optional[torch.Tensor], npoint: torch.Tensor,
                      npmax: int, out_off: torch.Tensor, R: torch.Tensor, t: torch.Tensor, total_cap: int,
-                     want_sel64: bool = True, want_align: bool = True, want_sel32: bool = True) -> dict:
+                     want_sel64: bool = True, want_align: bool = True, want_sel32: bool = True,
+                     status: Optional[torch.Tensor] = None, check: Optional[bool] = None) -> dict:
+    """pcd[idx] + transform (pk_gather_transform). status int32 [B] (optional): per crop 1 when
+    an FPS index lies outside its crop (that point's outputs are NaN); without it the call checks
+    a temporary one (host sync) unless capturing. Returns dict(sel64, align, sel32, status)."""
     B = off.numel() - 1
     dev = pcd.device
+    st, chk = _index_status(B, dev, status, check)
     sel64 = torch.empty((total_cap, 3), dtype=torch.float64, device=dev) if want_sel64 else None
     align = torch.empty((total_cap, 3), dtype=torch.float64, device=dev) if want_align else None
     sel32 = torch.empty((total_cap, 3), dtype=torch.float32, device=dev) if want_sel32 else None
     idx_stride = idx.shape[1] if idx is not None else 0
     call("pk_gather_transform", ptr(pcd), ptr(off), B, ptr(idx), int(idx_stride), ptr(npoint), int(npmax),
-         ptr(out_off), ptr(R), ptr(t), ptr(sel64), ptr(align), ptr(sel32), _lib.stream(dev))
-    return dict(sel64=sel64, align=align, sel32=sel32)
+         ptr(out_off), ptr(R), ptr(t), ptr(sel64), ptr(align), ptr(sel32), ptr(st), _lib.stream(dev))
+    if chk:
+        check_index_status(st, "gather_transform (FPS indices)")
+    return dict(sel64=sel64, align=align, sel32=sel32, status=st)
 
 
 # ------------------------------------------------------------------------------ H7 spectral diffusion
@@ -880,34 +910,6 @@ def spectral_raw(x: torch.Tensor, ld_in: int, mass, evals, evecs, t, clamp_t: bo
 FD_MODES = {"fp32": 0, "bf16": 1, "bf16x3": 2}
 
 
-_FD_WORK = {}
-_FD_CAPTURED = []
-
-
-def _fd_work(dev: torch.device, nbytes: int, ctr_bytes: int) -> torch.Tensor:
-    """pk_feat_dist_topk's scratch: [ctr_bytes of arrival words][path scratch]. The arrival words
-    must be zero before a call and every call leaves them zero (posekern.h), and a buffer must not
-    serve two streams at once, so: eager calls reuse one persistent buffer per (device, stream),
-    zero-filled when created or grown, and its leading ctr_bytes re-zeroed whenever the counter
-    size differs from the buffer's previous call (the previous layout's scratch — or a bf16 /
-    top-5 call's, which has no counter prefix — may lie where the new words are); a call inside
-    a HIP-graph capture gets a buffer of its own whose zero fill is captured with it (graphs may
-    share a capture stream; every replay then starts from zero words), kept alive for the graph's
-    lifetime."""
-    if torch.cuda.is_current_stream_capturing():
-        buf = torch.zeros((max(nbytes, 256),), dtype=torch.uint8, device=dev)
-        _FD_CAPTURED.append(buf)
-        return buf
-    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
-    buf, last = _FD_WORK.get(key, (None, 0))
-    if buf is None or buf.numel() < nbytes:
-        buf = torch.zeros((max(nbytes, 256),), dtype=torch.uint8, device=dev)
-    elif ctr_bytes > 0 and ctr_bytes != last:
-        buf[:ctr_bytes].zero_()
-    _FD_WORK[key] = (buf, ctr_bytes)
-    return buf
-
-
 def feat_dist_topk(evecs_x: torch.Tensor, C: torch.Tensor, evecs_y: torch.Tensor, n1: torch.Tensor,
                    n2: torch.Tensor, topk: int, want_dist: bool = False, precision: str = "fp32",
                    work: Optional[torch.Tensor] = None):
@@ -915,8 +917,8 @@ def feat_dist_topk(evecs_x: torch.Tensor, C: torch.Tensor, evecs_y: torch.Tensor
     evecs_x [B,V1,K>=30], C [B,30,30], evecs_y [B,V2,K>=30], n1/n2 int32 [B].
     precision: "fp32" (the parity path: torch.cdist's augmented contraction on the f32 MFMA),
     "bf16" or "bf16x3" (opt-in: bf16 MFMA cross term, f32 norms). work: optional caller scratch
-    (uint8; its leading pk_feat_dist_counter_bytes zero before the call, see _fd_work); default: a
-    per-stream buffer."""
+    (uint8, any contents: the library keeps nothing in it across calls); default: a temporary
+    from torch's allocator (none for the one-launch fp32 argmin at full-chip batch sizes)."""
     B, V1, ldx = evecs_x.shape
     _, V2, ldy = evecs_y.shape
     dev = evecs_x.device
@@ -925,7 +927,7 @@ def feat_dist_topk(evecs_x: torch.Tensor, C: torch.Tensor, evecs_y: torch.Tensor
     if nbytes < 0:
         raise _lib.PoseKernError("feat_dist_topk: invalid shape / topk / precision")
     if work is None:
-        work = _fd_work(dev, nbytes, int(_lib.lib().pk_feat_dist_counter_bytes(B, V1, V2, int(topk), mode)))
+        work = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
     elif work.numel() < nbytes:
         raise _lib.PoseKernError(f"feat_dist_topk: work holds {work.numel()} bytes, {nbytes} needed")
     idx = torch.empty((B, V2, topk), dtype=torch.int64, device=dev)
@@ -1127,13 +1129,20 @@ def rigidity_filter(cand: torch.Tensor, ncand: torch.Tensor, cad: torch.Tensor, 
 
 
 def inlier_ratio(pairs: torch.Tensor, npairs: torch.Tensor, cad: torch.Tensor, pc_aligned: torch.Tensor,
-                 thr: torch.Tensor, layout: int = 0) -> torch.Tensor:
+                 thr: torch.Tensor, layout: int = 0, status: Optional[torch.Tensor] = None,
+                 check: Optional[bool] = None) -> torch.Tensor:
+    """Per-crop inlier ratio (pk_inlier_ratio). status int32 [B] (optional): per crop 1 when a
+    correspondence index lies outside cad / pc_aligned (the pair counts as an outlier, nothing is
+    read through it); without it the call checks a temporary one (host sync) unless capturing."""
     B = cad.shape[0]
     ldp = pairs.shape[1] if layout in (0, 2) else pairs.shape[2]
     ir = torch.empty((B,), dtype=torch.float32, device=cad.device)
+    st, chk = _index_status(B, cad.device, status, check)
     call("pk_inlier_ratio", ptr(pairs.contiguous()), ldp, int(layout), ptr(npairs), ptr(cad.contiguous()),
-         cad.shape[1], ptr(pc_aligned.contiguous()), pc_aligned.shape[1], ptr(thr), B, ptr(ir),
+         cad.shape[1], ptr(pc_aligned.contiguous()), pc_aligned.shape[1], ptr(thr), B, ptr(ir), ptr(st),
          _lib.stream(cad.device))
+    if chk:
+        check_index_status(st, "inlier_ratio (correspondence indices)")
     return ir
 
 
@@ -1151,11 +1160,15 @@ def cgt_lstsq(pairs: torch.Tensor, npairs: torch.Tensor, evecs1: torch.Tensor, e
 def ransac(src: torch.Tensor, src_off: torch.Tensor, dst: torch.Tensor, dst_off: torch.Tensor,
            corres: torch.Tensor, cor_off: torch.Tensor, H: int, seed: int = 0, max_dist: float = 0.05,
            hyps: Optional[torch.Tensor] = None, hyp_off: Optional[torch.Tensor] = None,
-           nmax: Optional[int] = None):
+           nmax: Optional[int] = None, status: Optional[torch.Tensor] = None, check: Optional[bool] = None):
     """Batched RANSAC pose fit (pk_ransac). nmax bounds the correspondences per crop (default:
-    all rows of `corres`). Returns (T f64 [B,4,4], stats f64 [B,3] = fitness, rmse, best h)."""
+    all rows of `corres`). status int32 [B] (optional): per crop 1 when a correspondence or
+    hypothesis row is out of range (read as row 0 instead); without it the call checks a
+    temporary one (host sync) unless capturing. Returns (T f64 [B,4,4], stats f64 [B,3] =
+    fitness, rmse, best h)."""
     B = cor_off.numel() - 1
     dev = src.device
+    st, chk = _index_status(B, dev, status, check)
     corres = corres.to(torch.int32).contiguous()
     if corres.numel() == 0:  # every crop below ransac_n: keep a valid pointer, kernel returns identity
         corres = torch.zeros((1, 2), dtype=torch.int32, device=dev)
@@ -1173,7 +1186,9 @@ def ransac(src: torch.Tensor, src_off: torch.Tensor, dst: torch.Tensor, dst_off:
         wk = lambda: ("valu64", int(H) * (30 * int(tot.item()) + 6000 * B))  # noqa: E731
     call("pk_ransac", ptr(src), ptr(src_off), ptr(dst), ptr(dst_off), ptr(corres),
          ptr(cor_off), ptr(hyps), ptr(hyp_off), ctypes_u64(seed), int(H), float(max_dist), B, nmax, ptr(work),
-         nbytes, ptr(T), ptr(stats), _lib.stream(dev), work=wk)
+         nbytes, ptr(T), ptr(stats), ptr(st), _lib.stream(dev), work=wk)
+    if chk:
+        check_index_status(st, "ransac (correspondence / hypothesis rows)")
     return T, stats
 
 

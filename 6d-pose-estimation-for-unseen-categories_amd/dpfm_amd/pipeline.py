@@ -318,7 +318,8 @@ class TrainStep:
 
     @staticmethod
     @torch.no_grad()
-    def inlier_ratio_of(op: Operators, crops: Crops, C_pred: torch.Tensor) -> torch.Tensor:
+    def inlier_ratio_of(op: Operators, crops: Crops, C_pred: torch.Tensor,
+                        status: Optional[torch.Tensor] = None) -> torch.Tensor:
         """train.py:109-116: the naive point map of C_pred and its mean inlier ratio over the
         crops (naive_p2p_batched without materialising its arange row: the IR kernel reads the
         map as [B, V2] CAD indices of crop points 0..n2-1)."""
@@ -326,7 +327,9 @@ class TrainStep:
         n1 = _counts(op.cad_n, B_, op.cad_evecs.shape[1], C_pred.device)
         npred = _counts(crops.n2, B_, V2_, C_pred.device)
         p_map, _ = ops.feat_dist_topk(op.cad_evecs, C_pred.detach(), op.pc_evecs, n1, npred, 1)
-        return ops.inlier_ratio(p_map[..., 0], npred, op.cad_xyz, crops.align32, op.ir_thr, layout=2).mean()
+        # status (int32 [B], optional): per crop 1 when a point-map index was out of range
+        ir = ops.inlier_ratio(p_map[..., 0], npred, op.cad_xyz, crops.align32, op.ir_thr, layout=2, status=status)
+        return ir.mean()
 
     def forward_backward(self, op: Operators, crops: Crops, ir: bool = True) -> dict:
         """ir=False leaves the naive point map + IR out of the step (PipelinedTrainer computes it
@@ -341,7 +344,10 @@ class TrainStep:
         loss, log = self.crit.forward_batched(C_pred, C_gt, crops.pairs, crops.npairs, f1, f2, o12, o21,
                                               crops.overlap_12, crops.overlap_21, generator=self.gen)
         with torch.no_grad():  # train.py:109-116 (naive solver + IR per crop)
-            ir = self.inlier_ratio_of(op, crops, C_pred) if ir else None
+            st = torch.empty((C_pred.shape[0],), dtype=torch.int32, device=C_pred.device) if ir else None
+            ir = self.inlier_ratio_of(op, crops, C_pred, status=st) if ir else None
+            if st is not None:
+                log["ir_index_status"] = st  # device int32 [B] (ops.check_index_status)
             # P truncated at the pair capacity would train on partial labels: flag it (device
             # bool, formed with the crops on the crop-formation stream)
             log["pair_overflow"] = crops.overflow()
@@ -542,7 +548,9 @@ class PipelinedTrainer:
             if self.defer_ir:  # I_k: reads buffer k's crops and T_k's C_pred (both graph-static)
                 gi = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gi):
-                    self.logs[k]["IR"] = TrainStep.inlier_ratio_of(op, self.crops[k], step.last_C_pred)
+                    st = torch.empty((step.last_C_pred.shape[0],), dtype=torch.int32, device=step.last_C_pred.device)
+                    self.logs[k]["IR"] = TrainStep.inlier_ratio_of(op, self.crops[k], step.last_C_pred, status=st)
+                    self.logs[k]["ir_index_status"] = st
                 self.ir_graphs.append(gi)
             self.grads.append([p.grad for p in step.params])
             gb = None
@@ -653,7 +661,9 @@ class InferStep:
         dev = C_pred.device
         rows, nsurv = ops.rigidity_filter(cand, ncand, op.cad_xyz, crops.pc32, op.rig_thr)  # :42-75
         p_pred = torch.gather(cand, 1, rows[..., None].expand(-1, -1, 2))                  # [B, L, 2]
-        ir = ops.inlier_ratio(p_pred, nsurv, op.cad_xyz, crops.align32, op.ir_thr, layout=0)  # eval.py:89
+        st_ir = torch.empty((B,), dtype=torch.int32, device=dev)
+        st_rs = torch.empty((B,), dtype=torch.int32, device=dev)
+        ir = ops.inlier_ratio(p_pred, nsurv, op.cad_xyz, crops.align32, op.ir_thr, layout=0, status=st_ir)  # eval.py:89
         # RANSAC on (CAD, crop in camera frame) with the surviving correspondences
         cor_off = torch.zeros(B + 1, dtype=torch.int64, device=dev)
         cor_off[1:] = torch.cumsum(nsurv.to(torch.int64), 0)
@@ -666,7 +676,7 @@ class InferStep:
         corres = torch.zeros((B * L + 1, 2), dtype=torch.int32, device=dev)
         corres.index_copy_(0, pos, p_pred.reshape(-1, 2).to(torch.int32))
         T, stats = ops.ransac(fb.cad64, fb.cad_off, crops.pc64, crops.off, corres, cor_off, self.H, seed=self.seed,
-                              max_dist=self.max_dist, nmax=L)
+                              max_dist=self.max_dist, nmax=L, status=st_rs)
         T_gt = torch.zeros((B, 4, 4), dtype=torch.float64, device=dev)
         T_gt[:, :3, :3] = fb.R.view(B, 3, 3)
         T_gt[:, :3, 3] = fb.t
@@ -675,8 +685,9 @@ class InferStep:
         # largest; the operator rows V1 may be a decimated CAD) and the crops (crops.ld)
         n1cap = max(int(fb.n1max or 0), V1)
         metrics = ops.pose_metrics(fb.cad64, fb.cad_off, n1cap, T, T_gt)
+        # per crop 1: an index consumer (IR, RANSAC) met an out-of-range index (ops.check_index_status)
         out = dict(C=C_pred, cand=cand, p_pred=p_pred, n_corr=nsurv, ir=ir, T=T, ransac=stats, metrics=metrics,
-                   corres=corres, cor_off=cor_off)
+                   corres=corres, cor_off=cor_off, index_status=st_ir | st_rs)
         if self.icp_evaluations > 0:
             T_icp, icp_stats = ops.icp_fixed(fb.cad64, fb.cad_off, crops.pc64, crops.off, T, self.icp_threshold,
                                              self.icp_evaluations, n1cap, max(int(crops.ld), V2))

@@ -340,6 +340,65 @@ def cpu_pose_check(model, fb, op, crops, out: dict, n_sample: int, H: int, seed:
                     "device's survivors; ADD in cm vs the synthetic T_gt (random-init weights: ADD is large)"}
 
 
+def pose_real_check(dev, H: int = 1024, seed: int = 7, inlier_frac: float = 0.4, noise_cm: float = 0.005) -> dict:
+    """The metric's "pose err vs ref" on correspondences with real inliers: the 7 published
+    crops of tests/golden/real_crops.npz (the reference's own camera-frame crops pc_i.ply,
+    their decimated CADs and full-precision T_gt). Per crop the target cloud is the real crop
+    plus planted points: a fraction `inlier_frac` of the correspondences are CAD vertices i
+    paired with T_gt CAD[i] + N(0, noise_cm) (inside test_RANSAC.py's 0.05 cm threshold), the
+    rest (>= 60 %) pair every real crop point with a random CAD vertex (outliers). Device
+    pk_ransac (batched over the 7 crops) vs the oracle's C RANSAC (Open3D semantics restated,
+    oracle/c/oracle.c) on the same hash-drawn hypotheses: fitness, rotation / translation error
+    vs T_gt and max |dT| between the two (north-star tolerance 1e-4)."""
+    import ctypes
+    from dpfm_amd import ops
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "liboracle.so"))
+    P = ctypes.c_void_p
+    lib.oc_ransac.argtypes = [P, P, P, ctypes.c_int, P, ctypes.c_uint64, ctypes.c_int64, ctypes.c_double, P, P]
+    cp = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    G = np.load(os.path.join(ROOT, "tests", "golden", "real_crops.npz"))
+    rng = np.random.default_rng(seed)
+    cads, pcs, cors, Tg = [], [], [], []
+    for k in range(int(G["n"])):
+        cad = np.ascontiguousarray(G[f"cad_{int(G[f'{k}_obj_id'])}"], dtype=np.float64)
+        pc = np.asarray(G[f"{k}_pc"], dtype=np.float64)
+        T = np.asarray(G[f"{k}_T_gt"], dtype=np.float64)
+        n_out = pc.shape[0]
+        n_in = int(round(n_out * inlier_frac / (1.0 - inlier_frac)))
+        ci = rng.integers(0, cad.shape[0], n_in)
+        planted = cad[ci] @ T[:3, :3].T + T[:3, 3] + rng.normal(size=(n_in, 3)) * noise_cm
+        tgt = np.ascontiguousarray(np.concatenate([planted, pc]))
+        cor = np.concatenate([np.stack([ci, np.arange(n_in)], 1),
+                              np.stack([rng.integers(0, cad.shape[0], n_out), n_in + np.arange(n_out)], 1)])
+        cor = np.ascontiguousarray(cor[rng.permutation(cor.shape[0])].astype(np.int32))
+        cads.append(cad), pcs.append(tgt), cors.append(cor), Tg.append(T)
+    off = lambda a: torch.tensor(np.concatenate([[0], np.cumsum([x.shape[0] for x in a])]), dtype=torch.int64,  # noqa
+                                 device=dev)
+    Td, st = ops.ransac(torch.from_numpy(np.concatenate(cads)).to(dev), off(cads),
+                        torch.from_numpy(np.concatenate(pcs)).to(dev), off(pcs),
+                        torch.from_numpy(np.concatenate(cors)).to(dev), off(cors), H, seed=seed, max_dist=0.05)
+    Td, st = Td.cpu().numpy(), st.cpu().numpy()
+    dT, fit, rot, tra, fit_ref = [], [], [], [], []
+    for k in range(len(cads)):
+        T_ref, s_ref = np.zeros(16), np.zeros(3)
+        lib.oc_ransac(cp(cads[k]), cp(pcs[k]), cp(cors[k]), int(cors[k].shape[0]), None, seed, H, 0.05, cp(T_ref),
+                      cp(s_ref))
+        dT.append(float(np.abs(Td[k] - T_ref.reshape(4, 4)).max()))
+        fit.append(float(st[k, 0]))
+        fit_ref.append(float(s_ref[0]))
+        Rr = Td[k][:3, :3] @ Tg[k][:3, :3].T
+        rot.append(float(np.degrees(np.arccos(np.clip((np.trace(Rr) - 1) / 2, -1, 1)))))
+        tra.append(float(np.linalg.norm(Td[k][:3, 3] - Tg[k][:3, 3])))
+    return {"crops": len(cads), "hypotheses": H, "tolerance": 1e-4, "max_abs_dT_vs_oracle": round(max(dT), 15),
+            "crops_within_tol": int(sum(d <= 1e-4 for d in dT)), "fitness_min": round(min(fit), 4),
+            "fitness_mean": round(float(np.mean(fit)), 4), "fitness_equal_to_oracle": fit == fit_ref,
+            "rot_err_deg_max": round(max(rot), 5), "trans_err_cm_max": round(max(tra), 5),
+            "inlier_fraction_planted": inlier_frac,
+            "note": "the reference's 7 published real crops (tests/golden/real_crops.npz) + planted inliers "
+                    f"(N(0, {noise_cm} cm) around T_gt CAD[i]); outliers: every real crop point paired with a "
+                    "random CAD vertex; device pk_ransac vs the C oracle on the same hypothesis draws"}
+
+
 TRAIN_METRIC = "RGB-D crops/sec (fwd+bwd), 1024 pts, at 1/2/4/8 MI355X; pose err vs ref"
 INFER_METRIC = ("RGB-D crops/sec (inference: crop formation + DPFM fwd + spatial-filter solver + IR + "
                 "RANSAC 1024 hyp + pose metrics)")
@@ -953,8 +1012,10 @@ def main():
         if not args.no_cpu_baseline and world == 1 and not args.ragged:
             if args.mode == "train":
                 out["cpu_baseline"] = cpu_baseline(args.cpu_crops, args.points, args.points)
-                if "fn" in POSE_CHECK and args.pose_crops > 0:
-                    out["pose_err"] = POSE_CHECK["fn"](args.pose_crops)
+                if args.pose_crops > 0:
+                    out["pose_err"] = pose_real_check(dev, H=args.hypotheses)
+                    if "fn" in POSE_CHECK:  # the model path on the synthetic batch (random-init weights)
+                        out["pose_err"]["model_path"] = POSE_CHECK["fn"](args.pose_crops)
             elif args.mode == "corr4096":
                 out["cpu_baseline"] = cpu_ransac_baseline(args.hypotheses)
             elif args.mode == "ransac_ref":

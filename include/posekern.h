@@ -103,11 +103,13 @@ int pk_fps_npoint(const int64_t* off, int B, int fixed, int limit, uint64_t seed
 /* H4 pcd[idx0] (dataset/object.py:148) + transform(pcd, R, t, inv=True) (:174, :304-309).
  *   pcd f64 [T,3] packed / off; idx int64 [B, idx_stride] FPS output (unused when
  *   npoint[b] < 0); R f64 [B,9] row-major R_m2c, t f64 [B,3] (cm)
- *   sel64 f64 / align64 f64 / sel32 f32 [sum npoint, 3] packed by out_off (any NULL) */
+ *   sel64 f64 / align64 f64 / sel32 f32 [sum npoint, 3] packed by out_off (any NULL)
+ *   status int32 [B] or NULL: 1 when an index of crop b lies outside [0, off[b+1] - off[b])
+ *   (that point is not read: its outputs are NaN), else 0; written for every crop. */
 int pk_gather_transform(const double* pcd, const int64_t* off, int B, const int64_t* idx,
                         int idx_stride, const int32_t* npoint, int npmax, const int64_t* out_off,
                         const double* R, const double* t, double* sel64, double* align64,
-                        float* sel32, void* stream);
+                        float* sel32, int32_t* status, void* stream);
 
 /* H6 collate (dataset/helpers.py:22-50: torch.Tensor(x) then pad_sequence(batch_first=True))
  * of one packed per-crop field: src [T, C] f64 (src_f64 = 1) or f32, packed by off [B+1];
@@ -386,16 +388,13 @@ int pk_linear_ex(const pk_linear_args* a, void* stream);
  *   evecs_y f32 [B,V2max,ldy]; n1/n2 int32 [B] valid rows
  *   mode 0: fp32 MFMA on torch.cdist's augmented K = 32 operands (the parity path);
  *   mode 1: bf16 MFMA cross term + f32 norms; mode 2: bf16x3 (hi/lo split, three bf16 MFMAs)
- *   work: scratch of pk_feat_dist_work_size(B, V1max, V2max, topk, mode) bytes. Its first
- *     pk_feat_dist_counter_bytes(...) bytes are arrival words of the single-launch mode-0 pass
- *     (row parts combined in the launch): they must be zero before a call, and every call
- *     leaves them zero. The remaining bytes are the call's scratch, so after a call of another
- *     layout (another counter size, or a mode 1/2 or topk 5 call) re-zero the prefix; keep one
- *     buffer per stream.
+ *   work: scratch of pk_feat_dist_work_size(B, V1max, V2max, topk, mode) bytes (may be 0 and
+ *     NULL), any contents: nothing in it is read before this call writes it, and nothing is kept
+ *     across calls (round 5: the mode-0 top-1 pass finishes every column inside one workgroup,
+ *     or writes row-part keys that a second launch merges — no arrival words, no zeroing contract).
  *   out_idx int64 [B,V2max,topk] ascending distance (ties: lower index); out_dist f32
  *   [B,V2max,topk] Euclidean distances (may be NULL). Fused selection epilogue. */
 int64_t pk_feat_dist_work_size(int B, int V1max, int V2max, int topk, int mode);
-int64_t pk_feat_dist_counter_bytes(int B, int V1max, int V2max, int topk, int mode);
 int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, const float* evecs_y, int ldy,
                       const int32_t* n1, const int32_t* n2, int B, int V1max, int V2max, int topk, int mode,
                       void* work, int64_t work_bytes, int64_t* out_idx, float* out_dist, void* stream);
@@ -418,10 +417,12 @@ int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* ncand, const
  * 0 when there are no correspondences.
  *   pairs int64: layout 0 [B,ldp,2] (cad, pc), layout 1 [B,2,ldp], or layout 2 [B,ldp] the CAD
  *   index of crop point k (a point map: pc index = k); npairs int32 [B]
- *   cad f32 [B,ldcad,3], pc_aligned f32 [B,ldpc,3], thr f32 [B] -> ir f32 [B] */
+ *   cad f32 [B,ldcad,3], pc_aligned f32 [B,ldpc,3], thr f32 [B] -> ir f32 [B]
+ *   status int32 [B] or NULL: 1 when a CAD index of crop b lies outside [0, ldcad) or a crop index
+ *   outside [0, ldpc) (such a pair is not read and counts as an outlier), else 0; every crop written */
 int pk_inlier_ratio(const int64_t* pairs, int ldp, int layout, const int32_t* npairs, const float* cad,
                     int ldcad, const float* pc_aligned, int ldpc, const float* thr, int B, float* ir,
-                    void* stream);
+                    int32_t* status, void* stream);
 
 /* H15 C_gt (utils/utils.py:67-79 C_from_sparse_P): least squares
  * evecs2[P[:,1], :30] X = evecs1[P[:,0], :30] per crop (fp64 normal equations: G from the
@@ -481,12 +482,15 @@ int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs, const flo
  *   work: scratch of pk_ransac_work_size(B, H, nmax) bytes (fitted poses, per-chunk scores)
  *   T f64 [B,4,4] row-major best pose, stats f64 [B,3] (fitness, inlier rmse, best h).
  * Best = (fitness desc, rmse asc, index asc). A crop's error sum is taken per chunk in
- * correspondence order, then over chunks in order. */
+ * correspondence order, then over chunks in order.
+ *   status int32 [B] or NULL: 1 when a correspondence row of crop b lies outside its source /
+ *   target points or a given hypothesis row outside [0, n_b) (read as row 0 instead of faulting),
+ *   else 0; written for every crop. */
 int64_t pk_ransac_work_size(int B, int64_t H, int nmax);
 int pk_ransac(const double* src, const int64_t* src_off, const double* dst, const int64_t* dst_off,
               const int32_t* corres, const int64_t* cor_off, const int32_t* hyps, const int64_t* hyp_off,
               uint64_t seed, int64_t H, double max_dist, int B, int nmax, void* work, int64_t work_bytes,
-              double* T, double* stats, void* stream);
+              double* T, double* stats, int32_t* status, void* stream);
 
 /* H14 pose metrics of scripts/test_RANSAC.py:77-81, 154-238 for B crops:
  *   cad f64 [T,3] packed / off (model points in the object frame), T_est / T_gt f64

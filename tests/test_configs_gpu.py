@@ -47,11 +47,12 @@ def test_feat_dist_argmin_top5_configs(device, B, V):
     assert ties <= max(2, B * V // 1000), ties
 
 
-def test_feat_dist_scratch_reuse_across_layouts(device):
-    """The default per-stream scratch of pk_feat_dist_topk serves calls of different layouts in
-    turn (top-1 fp32 with its arrival-word prefix, bf16 and top-5 scratch without / with another
-    prefix): every top-1 fp32 result equals the same call on a fresh zeroed buffer, so no call
-    inherits another's bytes as arrival words (ops._fd_work re-zeroes the prefix on a change)."""
+def test_feat_dist_scratch_contents_do_not_matter(device):
+    """pk_feat_dist_topk keeps nothing in its scratch across calls (posekern.h): every call of a
+    sequence of layouts (top-1 fp32 with and without row parts, bf16 / bf16x3, top-5) gives the
+    same result on a zeroed buffer, on one filled with 0xFF and on one of random bytes, each call
+    interleaved with the others on the same garbage buffers (the round-4 abort: stale arrival
+    words from another layout left a column group unmerged)."""
     from dpfm_amd import _lib, ops
     g = torch.Generator().manual_seed(77)
 
@@ -63,15 +64,64 @@ def test_feat_dist_scratch_reuse_across_layouts(device):
         return ex, C, ey, n
 
     seq = [(2, 300, 1, "fp32"), (4, 512, 1, "bf16"), (32, 1024, 1, "fp32"), (3, 700, 5, "fp32"),
-           (8, 2048, 1, "fp32"), (2, 300, 1, "fp32"), (4, 4096, 1, "bf16x3"), (32, 1024, 1, "fp32")]
-    for B, V, k, prec in seq:
-        ex, C, ey, n = inputs(B, V)
-        got, _ = ops.feat_dist_topk(ex, C, ey, n, n, k, precision=prec)
-        mode = ops.FD_MODES[prec]
-        nb = int(_lib.lib().pk_feat_dist_work_size(B, V, V, k, mode))
+           (8, 2048, 1, "fp32"), (1, 4096, 1, "fp32"), (4, 4096, 1, "bf16x3"), (32, 1024, 1, "fp32")]
+    cases = [(inputs(B, V), B, V, k, prec) for B, V, k, prec in seq]
+    nmax = max(int(_lib.lib().pk_feat_dist_work_size(B, V, V, k, ops.FD_MODES[p])) for _, B, V, k, p in cases)
+    ff = torch.full((nmax + 4096,), 0xFF, dtype=torch.uint8, device=device)
+    rnd = torch.randint(0, 256, (nmax + 4096,), dtype=torch.uint8, generator=g).to(device)
+    refs = []
+    for (ex, C, ey, n), B, V, k, prec in cases:
+        nb = int(_lib.lib().pk_feat_dist_work_size(B, V, V, k, ops.FD_MODES[prec]))
         ref, _ = ops.feat_dist_topk(ex, C, ey, n, n, k, precision=prec,
-                                    work=torch.zeros(nb, dtype=torch.uint8, device=device))
-        assert torch.equal(got, ref), (B, V, k, prec)
+                                    work=torch.zeros(max(nb, 1), dtype=torch.uint8, device=device))
+        refs.append(ref)
+    for rep in range(2):
+        for ((ex, C, ey, n), B, V, k, prec), ref in zip(cases, refs):
+            for buf in (ff, rnd):
+                got, _ = ops.feat_dist_topk(ex, C, ey, n, n, k, precision=prec, work=buf)
+                assert torch.equal(got, ref), (B, V, k, prec, rep)
+            got, _ = ops.feat_dist_topk(ex, C, ey, n, n, k, precision=prec)  # default temporary
+            assert torch.equal(got, ref), (B, V, k, prec, rep)
+    assert (refs[0] >= 0).all() and (refs[0] < 300).all()
+
+
+def test_feat_dist_clamp_and_duplicate_rows(device):
+    """torch.cdist's clamp_min(1e-30) tie rule on the one-launch argmin: with C = I and crop
+    features equal to CAD rows, the matching distances are rounding noise around 0 (some at or
+    below the clamp, which the kernel resolves by its rescan), and every such CAD row is
+    duplicated at a later row: the argmin must be the first copy, clamped or not. Batches with
+    and without row parts (RS > 1)."""
+    from dpfm_amd import ops
+    for B, V in [(32, 512), (2, 600)]:
+        g = torch.Generator().manual_seed(B)
+        ex = torch.randn(B, V, 32, generator=g)
+        ey = torch.randn(B, V, 32, generator=g)
+        C = torch.eye(30).repeat(B, 1, 1)
+        expect = {}
+        for b in range(B):
+            src = torch.randperm(V // 2, generator=g)[:40]
+            dup = V // 2 + torch.randperm(V // 2, generator=g)[:40]
+            cols = torch.randperm(V, generator=g)[:40]
+            ex[b, dup] = ex[b, src]
+            ey[b, cols] = ex[b, src]
+            for j, i in zip(cols.tolist(), src.tolist()):
+                expect[(b, j)] = i
+        n = torch.full((B,), V, dtype=torch.int32, device=device)
+        idx, dist = ops.feat_dist_topk(ex.to(device), C.to(device), ey.to(device), n, n, 1, want_dist=True)
+        idx, dist = idx[..., 0].cpu(), dist[..., 0].cpu()
+        clamped = 0
+        for (b, j), i in expect.items():
+            assert idx[b, j].item() == i, (B, V, b, j, idx[b, j].item(), i)
+            clamped += int(abs(dist[b, j].item() - 1e-15) < 1e-18)
+        assert clamped > 0  # the rescan ran
+        # the other columns still match cdist (near-ties counted)
+        i1 = idx.numpy()
+        ties = 0
+        for b in range(B):
+            d = torch.cdist(ex[b, :, :30], ey[b, :, :30]).numpy().astype(np.float64)
+            keep = np.array([(b, j) not in expect for j in range(V)])
+            ties += check_topk(d[:, keep], i1[b, keep][:, None], 1)
+        assert ties <= 4, ties
 
 
 def test_feat_dist_ragged_edges(device):
