@@ -489,21 +489,31 @@ __global__ __launch_bounds__(64 * kWaves) void fd_main_direct_kernel(
 }
 
 // Top-1 fp32 (round 5, the default argmin of the training step's naive point map and the IR):
-// ONE launch, no state across calls, no scratch unless the grid needs row parts.
-// Block = (crop b, column group of kTop1CT = 8 column tiles = 128 columns, row part rs); its 4
-// waves share the block's 8 column tiles (B operands in registers) and split the row part's
-// tiles, so every column's argmin over the row part is finished inside the block (the waves'
-// results meet in LDS) — no ticket, no arrival words, nothing a previous call can leave behind.
-// Each wave forms its own rows' emb = x C^T operands on the MFMA (16 per row tile, C in
-// registers): the emb D layout is the main contraction's A operand in the permuted slot order
-// (lane (point c, group g) holds features 16 n + 4 g + q), so no LDS and no barrier sit in the
-// main loop. Selection per distance: compare, select the tile, min (the running (key, tile) of
-// each (column tile, row offset r) per lane; key = the distance's bits as a signed int, ties keep
-// the earlier tile, then the lower r / lane group / wave = the lower row). torch.cdist's
-// clamp_min(1e-30) is not applied per distance: a column whose best key is <= bits(1e-30)
-// (a zero, tiny or negative expansion) is rescanned for its first row at or below the clamp
-// (wave-uniform, rare: coincident features). With RS > 1 (small batches) the row parts' keys go
-// to scratch and fd_top1_merge_kernel takes the minimum (stateless: every key is rewritten).
+// nothing kept across calls (no arrival words, no zeroing contract on `work`).
+//
+// Pass 1, fd_top1_prep_kernel (one wave per 16-row tile of x): the row operand
+// A = [-2 emb, |emb|^2, 1] with emb = x C^T, computed once per tile on the f32 MFMA and stored in
+// the main contraction's A-operand order (2 KB per tile) — rather than by every column group that
+// reads the tile (each tile feeds 8 blocks at configs[1]: 16 of every 80 MFMAs were emb MFMAs).
+// Contraction-slot order: slot (step s = 4 n + q, lane group g) holds feature 16 n + 4 g + q, so
+// the emb MFMA's D layout (C x^T: lane (point c, group g) holds features 16 n + 4 g + q) IS the
+// A-operand layout, and a lane's y values are two contiguous float4 of its row. Slots 30, 31
+// carry torch.cdist's augmented terms [-2 emb, |emb|^2, 1] . [y, 1, |y|^2]; padding rows get an
+// +inf |emb|^2 slot (never selected).
+// Pass 2, fd_top1_kernel: block = (crop b, column group of kTop1CT = 8 column tiles = 128
+// columns, row part rs); its 8 waves (two per SIMD) share the group's B operands (staged once per
+// block through LDS, then in registers) and split the row part's tiles, streaming their A tiles
+// from L2 two tiles ahead; so every column's argmin over the row part is finished inside the
+// block (the waves' results meet in LDS). Per tile: 8 column tiles in pairs of accumulation
+// chains, the selection of a pair behind the next pair's MFMAs. Selection per distance: compare
+// into a lane mask, select the tile, min (the running (key, tile) of each (column tile, row offset
+// r) per lane; key = the distance's bits as a signed int; ties keep the earlier tile, then the
+// lower r / lane group / wave = the lower row). torch.cdist's clamp_min(1e-30) is not applied per
+// distance: a column whose best key is <= bits(1e-30) (a zero, tiny or negative expansion) is
+// rescanned for its first row at or below the clamp (wave-uniform, rare: coincident features).
+// With RS > 1 (small batches) the row parts' keys go to scratch and fd_top1_merge_kernel takes
+// the minimum. The development variant PK_FD_VAR=20 forms the emb operands inside the main pass
+// instead (one launch; the round-5 first form, A/B).
 constexpr int kTop1CT = 8;
 constexpr int kTop1Waves = 8;  // two per SIMD: one wave's dependency stalls are the other's MFMA time
 #ifdef PK_DEVBUILD
@@ -521,13 +531,109 @@ __device__ unsigned long long g_fd_stamps[4096 * 8];  // (development: VAR 13 ph
 #endif
 constexpr int kClampBits = 0x0da24260;  // bits of 1e-30f: clamp_min(1e-30) (cdist mm path)
 
-template <int VAR = 0>
+// -2 C in the emb MFMA's A order: lane (m, gg) holds -2 C[16 n + m][16 h + 4 gg + q] at s = 4 h + q
+__device__ __forceinline__ void top1_cv(const float* __restrict__ Cb, int c16, int g, float (&cv)[2][8]) {
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) {
+      const int row = 16 * n + c16, f = 16 * (s8 >> 2) + 4 * g + (s8 & 3);
+      const float cval = Cb[min(row, kF - 1) * kF + min(f, kF - 1)];  // (unconditional load)
+      cv[n][s8] = (row < kF && f < kF) ? -2.f * cval : 0.f;
+    }
+}
+
+// x row t*16 + c16 of a crop (a padding row reads row 0: finite, its distance is +inf anyway)
+__device__ __forceinline__ void top1_xload(const float* __restrict__ xb, int ldx, int N1, int t, int c16, int g,
+                                           float4 (&xv)[2]) {
+  const int r0 = t * 16 + c16;
+  const float* xr = xb + (int64_t)(r0 < N1 ? r0 : 0) * ldx;
+  xv[0] = *reinterpret_cast<const float4*>(xr + 4 * g);
+  xv[1] = *reinterpret_cast<const float4*>(xr + 16 + 4 * g);
+}
+
+// -2 emb of a tile on the MFMA with -2 C (exact power-of-two scaling of emb)
+__device__ __forceinline__ void top1_emb_mfma(const float (&cv)[2][8], const float4 (&xv)[2], f32x4 (&e)[2]) {
+  const float xs[8] = {xv[0].x, xv[0].y, xv[0].z, xv[0].w, xv[1].x, xv[1].y, xv[1].z, xv[1].w};
+#pragma unroll
+  for (int n = 0; n < 2; ++n) e[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) e[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(cv[n][s], xs[s], e[n], 0, 0, 0);
+}
+
+// the A operand [-2 emb, |emb|^2, 1]: |emb|^2 = (the sum of squares of -2 emb) / 4 (exact), the
+// lane groups' partials added in the order 0, 1, 2, 3; every lane gets them by row swaps (VALU,
+// no LDS round trip): the 16-swap pairs rows (0,1) / (2,3), the 32-swaps then rows 0-1 with 2-3
+__device__ __forceinline__ void top1_emb_norm(int t, int N1, int c16, int g, const f32x4 (&e)[2], float (&a)[8]) {
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[4 * n + q] = e[n][q];
+  float part_ = 0.f;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) part_ = fmaf(a[s], a[s], part_);
+  const auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(part_), __float_as_uint(part_), false, false);
+  const auto e32 = __builtin_amdgcn_permlane32_swap(s16[0], s16[0], false, false);  // {p0, p2}
+  const auto o32 = __builtin_amdgcn_permlane32_swap(s16[1], s16[1], false, false);  // {p1, p3}
+  const float nrm = 0.25f * (((__uint_as_float(e32[0]) + __uint_as_float(o32[0])) + __uint_as_float(e32[1])) +
+                             __uint_as_float(o32[1]));
+  const bool g3 = g == 3;
+  a[6] = g3 ? (t * 16 + c16 < N1 ? nrm : __builtin_huge_valf()) : a[6];
+  a[7] = g3 ? 1.f : a[7];
+}
+
+// pass 1: grid (ceil(T1 / 8), B), 8 waves: wave = one 16-row tile of crop b's x side, its A tile
+// [-2 emb, |emb|^2, 1]; -2 C staged once per block in LDS with a 32-float row pitch so each lane
+// reads its 16 C values as four 16-B loads. Tiles at or past a crop's valid rows are skipped
+// (pass 2 never reads them).
+__global__ __launch_bounds__(512) void fd_top1_prep_kernel(const float* __restrict__ ex, int ldx,
+                                                          const float* __restrict__ C,
+                                                          const int32_t* __restrict__ n1, int V1max, int T1,
+                                                          f32x4* __restrict__ Atile) {
+  __shared__ __attribute__((aligned(16))) float sc[kK * 32];
+  const int lane = pk::lane_id(), w = __builtin_amdgcn_readfirstlane(pk::wave_id());
+  const int g = lane >> 4, c16 = lane & 15;
+  const int b = blockIdx.y, t = blockIdx.x * 8 + w;
+  const int N1 = n1[b];
+  const bool act = t < T1 && t * 16 < N1;
+  float4 xv[2];
+  if (act) top1_xload(ex + (int64_t)b * V1max * ldx, ldx, N1, t, c16, g, xv);
+  const float* Cb = C + (int64_t)b * kF * kF;
+  for (int e = threadIdx.x; e < kK * 32; e += 512) {  // -2 C, zero-padded to 32 x 32
+    const int row = e >> 5, f = e & 31;
+    const float cval = Cb[min(row, kF - 1) * kF + min(f, kF - 1)];
+    sc[e] = (row < kF && f < kF) ? -2.f * cval : 0.f;
+  }
+  __syncthreads();
+  if (!act) return;
+  float cv[2][8];
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 v4 = *reinterpret_cast<const f32x4*>(sc + (16 * n + c16) * 32 + 16 * h + 4 * g);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cv[n][4 * h + q] = v4[q];
+    }
+  f32x4 e[2];
+  top1_emb_mfma(cv, xv, e);
+  float a[8];
+  top1_emb_norm(t, N1, c16, g, e, a);
+  f32x4* dst = Atile + ((int64_t)b * T1 + t) * 128;
+  dst[lane] = f32x4{a[0], a[1], a[2], a[3]};
+  dst[64 + lane] = f32x4{a[4], a[5], a[6], a[7]};
+}
+
+// pass 2 (EMB: form the emb operands in this pass instead of reading pass 1's tiles)
+template <int VAR = 0, bool EMB = false>
 __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top1_kernel(
-    const float* __restrict__ ex, int ldx, const float* __restrict__ C, const float* __restrict__ ey, int ldy,
-    const int32_t* __restrict__ n1, const int32_t* __restrict__ n2, int V1max, int V2max, int NCG, int RS,
-    int64_t* __restrict__ out_idx, float* __restrict__ out_dist, unsigned long long* __restrict__ part) {
+    const float* __restrict__ ex, int ldx, const float* __restrict__ C, const f32x4* __restrict__ Atile, int T1,
+    const float* __restrict__ ey, int ldy, const int32_t* __restrict__ n1, const int32_t* __restrict__ n2, int V1max,
+    int V2max, int NCG, int RS, int64_t* __restrict__ out_idx, float* __restrict__ out_dist,
+    unsigned long long* __restrict__ part) {
   __shared__ f32x4 sB[kTop1CT][2][64];      // the column operands in B order (16 KB)
-  __shared__ f32x4 sC[2][2][64];            // -2 C in the emb MFMA's A order (4 KB)
   __shared__ float sPart[4][kTop1CT * 16];  // per lane group partial |y|^2
   __shared__ unsigned long long wkeys[kTop1Waves][kTop1CT * 16];
   const int per = NCG * RS;
@@ -557,27 +663,37 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top1_kernel(
   const int Q = RS * kTop1Waves, qw = rs * kTop1Waves + w;
   const int tb = (int)((int64_t)nt * qw / Q), te = (int)((int64_t)nt * (qw + 1) / Q);  // this wave's row tiles
   const float* xb = ex + (int64_t)b * V1max * ldx;
-  auto xload = [&](int t, float4 (&xv)[2]) {  // row t*16 + c16; a padding row reads row 0 (finite)
-    const int r0 = t * 16 + c16;
-    const float* xr = xb + (int64_t)(r0 < N1 ? r0 : 0) * ldx;
-    xv[0] = *reinterpret_cast<const float4*>(xr + 4 * g);
-    xv[1] = *reinterpret_cast<const float4*>(xr + 16 + 4 * g);
-  };
-  float4 xc[2];
-  if (tb < te) xload(tb, xc);
-  {  // staging: -2 C in A order (threads 0..255), the 128 columns' [y, 1, |y|^2] in B order
-    if (tid < 256) {
-      const float* Cb = C + (int64_t)b * kF * kF;
-      const int n = tid >> 7, h = (tid >> 6) & 1, l = tid & 63;
-      const int row = 16 * n + (l & 15), gg = l >> 4;
-      float v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int f = 16 * h + 4 * gg + q;
-        v[q] = (row < kF && f < kF) ? -2.f * Cb[row * kF + f] : 0.f;
-      }
-      sC[n][h][l] = f32x4{v[0], v[1], v[2], v[3]};
+  const f32x4* Ab = Atile + (int64_t)b * T1 * 128;
+  // the operand of tile t: pass 1's A tile (two 16-B loads per lane), or x rows to embed here
+  auto opload = [&](int t, float4 (&xv)[2]) {
+    if constexpr (EMB) {
+      top1_xload(xb, ldx, N1, t, c16, g, xv);
+    } else {
+      const f32x4 u0 = Ab[(int64_t)t * 128 + lane], u1 = Ab[(int64_t)t * 128 + 64 + lane];
+      xv[0] = make_float4(u0[0], u0[1], u0[2], u0[3]);
+      xv[1] = make_float4(u1[0], u1[1], u1[2], u1[3]);
     }
+  };
+  float cv[2][8];
+  if constexpr (EMB) top1_cv(C + (int64_t)b * kF * kF, c16, g, cv);
+  auto emb = [&](int t, const float4 (&xv)[2], float (&a)[8]) {
+    if constexpr (EMB) {
+      f32x4 e[2];
+      top1_emb_mfma(cv, xv, e);
+      top1_emb_norm(t, N1, c16, g, e, a);
+    } else {
+      a[0] = xv[0].x, a[1] = xv[0].y, a[2] = xv[0].z, a[3] = xv[0].w;
+      a[4] = xv[1].x, a[5] = xv[1].y, a[6] = xv[1].z, a[7] = xv[1].w;
+    }
+  };
+  float4 xc[2], xn[2];
+  float a[8];
+  if (tb < te) {
+    opload(tb, xc);
+    opload(min(tb + 1, te - 1), xn);
+  }
+  float bo[kTop1CT][8];
+  {  // staging: the block's 128 columns' [y, 1, |y|^2] in B order, through LDS
     const int jj = tid & (kTop1CT * 16 - 1), gy = tid >> 7;  // column jj of the block, lane group gy
     const int j = j0 + jj;
     const float* yr = ey + ((int64_t)b * V2max + min(j, V2max - 1)) * ldy;
@@ -587,11 +703,12 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top1_kernel(
     float v[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
     float part_ = 0.f;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      v[s] = (ok && (s < 6 || gy < 3)) ? v[s] : 0.f;
-      part_ = fmaf(v[s], v[s], part_);
+    for (int s8 = 0; s8 < 8; ++s8) {
+      v[s8] = (ok && (s8 < 6 || gy < 3)) ? v[s8] : 0.f;
+      part_ = fmaf(v[s8], v[s8], part_);
     }
     sPart[gy][jj] = part_;
+    if (tb < te) emb(tb, xc, a);  // (the first tile's operand while the partials meet)
     __syncthreads();
     if (gy == 3) {  // |y|^2: the lane groups' partials in the order 0, 1, 2, 3
       float nrm = 0.f;
@@ -604,57 +721,15 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top1_kernel(
     sB[c][0][l] = f32x4{v[0], v[1], v[2], v[3]};
     sB[c][1][l] = f32x4{v[4], v[5], v[6], v[7]};
     __syncthreads();
+#pragma unroll
+    for (int c2 = 0; c2 < kTop1CT; ++c2)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 t4 = sB[c2][h][lane];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bo[c2][4 * h + q] = t4[q];
+      }
   }
-  float cv[2][8], bo[kTop1CT][8];
-#pragma unroll
-  for (int n = 0; n < 2; ++n)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x4 t4 = sC[n][h][lane];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) cv[n][4 * h + q] = t4[q];
-    }
-#pragma unroll
-  for (int c = 0; c < kTop1CT; ++c)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x4 t4 = sB[c][h][lane];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bo[c][4 * h + q] = t4[q];
-    }
-  // A operand [-2 emb, |emb|^2, 1] of row tile t: -2 emb straight from the MFMA with -2 C (exact
-  // power-of-two scaling), |emb|^2 = (sum of the squares of -2 emb) / 4 (exact); padding rows:
-  // |emb|^2 = +inf, never selected. Split into the MFMAs and the norm so that the loop below can
-  // issue tile t + 1's emb MFMAs among tile t's.
-  auto emb_mfma = [&](const float4 (&xv)[2], f32x4 (&e)[2]) {
-    const float xs[8] = {xv[0].x, xv[0].y, xv[0].z, xv[0].w, xv[1].x, xv[1].y, xv[1].z, xv[1].w};
-#pragma unroll
-    for (int n = 0; n < 2; ++n) e[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-#pragma unroll
-      for (int n = 0; n < 2; ++n) e[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(cv[n][s], xs[s], e[n], 0, 0, 0);
-  };
-  auto emb_norm = [&](int t, const f32x4 (&e)[2], float (&a)[8]) {
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a[4 * n + q] = e[n][q];
-    float part_ = 0.f;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) part_ = fmaf(a[s], a[s], part_);
-    const float p1 = __shfl_xor(part_, 16), p2 = __shfl_xor(part_, 32), p3 = __shfl_xor(part_, 48);
-    // lane group 3: p3 = group 0, p2 = group 1, p1 = group 2, own = group 3
-    const float nrm = 0.25f * (((p3 + p2) + p1) + part_);
-    const bool g3 = g == 3;
-    a[6] = g3 ? (t * 16 + c16 < N1 ? nrm : __builtin_huge_valf()) : a[6];
-    a[7] = g3 ? 1.f : a[7];
-  };
-  auto emb = [&](int t, const float4 (&xv)[2], float (&a)[8]) {
-    f32x4 e[2];
-    emb_mfma(xv, e);
-    emb_norm(t, e, a);
-  };
   FD_STAMP(1, __builtin_amdgcn_s_memtime());
   int bk[kTop1CT][4], bt[kTop1CT][4];
 #pragma unroll
@@ -662,27 +737,34 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top1_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       bk[c][r] = 0x7f800000;
-      bt[c][r] = -1;
+      bt[c][r] = 0x07ffffff;  // no row yet: its row index (16 bt + 4 g + r) >= 0x7ffffff0
     }
+  // per distance: compare into a lane mask, select the tile, min. Four compares into four SGPR
+  // pairs before their selects (no VCC write -> read hazard wait states between them)
   auto sel = [&](const f32x4& acc, int c, int t) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int key = __float_as_int(acc[r]);
-      const bool lt = key < bk[c][r];
-      bt[c][r] = lt ? t : bt[c][r];
-      bk[c][r] = lt ? key : bk[c][r];
-    }
+    unsigned long long m0, m1, m2, m3;
+    asm("v_cmp_lt_i32_e64 %[m0], %[k0], %[b0]\n\t"
+        "v_cmp_lt_i32_e64 %[m1], %[k1], %[b1]\n\t"
+        "v_cmp_lt_i32_e64 %[m2], %[k2], %[b2]\n\t"
+        "v_cmp_lt_i32_e64 %[m3], %[k3], %[b3]\n\t"
+        "v_min_i32_e32 %[b0], %[k0], %[b0]\n\t"
+        "v_min_i32_e32 %[b1], %[k1], %[b1]\n\t"
+        "v_min_i32_e32 %[b2], %[k2], %[b2]\n\t"
+        "v_min_i32_e32 %[b3], %[k3], %[b3]\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[tv], %[m0]\n\t"
+        "v_cndmask_b32_e64 %[t1], %[t1], %[tv], %[m1]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t2], %[tv], %[m2]\n\t"
+        "v_cndmask_b32_e64 %[t3], %[t3], %[tv], %[m3]"
+        : [b0] "+v"(bk[c][0]), [b1] "+v"(bk[c][1]), [b2] "+v"(bk[c][2]), [b3] "+v"(bk[c][3]),
+          [t0] "+v"(bt[c][0]), [t1] "+v"(bt[c][1]), [t2] "+v"(bt[c][2]), [t3] "+v"(bt[c][3]),
+          [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3)
+        : [k0] "v"(__float_as_int(acc[0])), [k1] "v"(__float_as_int(acc[1])), [k2] "v"(__float_as_int(acc[2])),
+          [k3] "v"(__float_as_int(acc[3])), [tv] "v"(t));
   };
   // software pipeline: tile t's 8 column tiles in pairs (two accumulation chains each), the
-  // selection of pair p - 1 behind pair p's MFMAs, tile t + 1's emb MFMAs behind the last pair,
-  // the last pair's selection and tile t + 1's norm behind those; no branch in the body (the
-  // x loads past the wave's last tile re-read its last tile, their emb is never used)
-  float a[8];
-  float4 xn[2];
-  if (tb < te) {
-    emb(tb, xc, a);
-    xload(min(tb + 1, te - 1), xn);
-  }
+  // selection of pair p - 1 behind pair p's MFMAs, tile t + 1's operand (loaded two tiles ahead;
+  // with EMB its emb MFMAs) behind the last pair; no branch in the body (loads past the wave's
+  // last tile re-read its last tile, never used)
   for (int t = tb; t < te; ++t) {
     f32x4 acc[kTop1CT];
 #pragma unroll
@@ -700,60 +782,82 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top1_kernel(
         sel(acc[2 * p - 1], 2 * p - 1, t);
       }
     }
-    f32x4 e[2];
-    emb_mfma(xn, e);
-    xload(min(t + 2, te - 1), xn);
-    sel(acc[kTop1CT - 2], kTop1CT - 2, t);
-    sel(acc[kTop1CT - 1], kTop1CT - 1, t);
-    emb_norm(t + 1, e, a);
-  }
-  FD_STAMP(2, __builtin_amdgcn_s_memtime());
-  // per column tile: the lane's best (key, row) over its 4 row offsets
-  unsigned long long best[kTop1CT];
-  unsigned clampmask = 0;
-#pragma unroll
-  for (int c = 0; c < kTop1CT; ++c) {
-    best[c] = ~0ull;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      clampmask |= (bk[c][r] <= kClampBits ? 1u : 0u) << c;
-      const unsigned row = bt[c][r] < 0 ? 0x7fffffffu : (unsigned)(bt[c][r] * 16 + 4 * g + r);
-      const unsigned long long key = ((unsigned long long)(unsigned)bk[c][r] << 32) | row;
-      best[c] = key < best[c] ? key : best[c];
+    if constexpr (EMB) {
+      f32x4 e[2];
+      top1_emb_mfma(cv, xn, e);
+      opload(min(t + 2, te - 1), xn);
+      sel(acc[kTop1CT - 2], kTop1CT - 2, t);
+      sel(acc[kTop1CT - 1], kTop1CT - 1, t);
+      top1_emb_norm(t + 1, N1, c16, g, e, a);
+    } else {
+      emb(t + 1, xn, a);
+      opload(min(t + 2, te - 1), xn);
+      sel(acc[kTop1CT - 2], kTop1CT - 2, t);
+      sel(acc[kTop1CT - 1], kTop1CT - 1, t);
     }
   }
+  FD_STAMP(2, __builtin_amdgcn_s_memtime());
+  // per column tile: the lane's best (value, row) over its 4 row offsets: the smallest key, then
+  // the lowest row holding it
+  int bv[kTop1CT];
+  unsigned br[kTop1CT];
+  int vmin = 0x7fffffff;
+#pragma unroll
+  for (int c = 0; c < kTop1CT; ++c) {
+    bv[c] = min(min(bk[c][0], bk[c][1]), min(bk[c][2], bk[c][3]));
+    br[c] = 0xffffffffu;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const unsigned row = (unsigned)(bt[c][r] * 16 + 4 * g + r);
+      br[c] = bk[c][r] == bv[c] ? min(br[c], row) : br[c];
+    }
+    vmin = min(vmin, bv[c]);
+  }
   // a column with a distance at or below torch.cdist's clamp: its first such row (rare)
-  if (__builtin_amdgcn_ballot_w64(clampmask != 0)) {
+  if (__builtin_amdgcn_ballot_w64(vmin <= kClampBits)) {
     for (int c = 0; c < kTop1CT; ++c) {
-      if (!__builtin_amdgcn_ballot_w64((clampmask >> c) & 1)) continue;  // (wave-uniform)
+      if (!__builtin_amdgcn_ballot_w64(bv[c] <= kClampBits)) continue;  // (wave-uniform)
       unsigned frow = 0x7fffffffu;
       for (int t = tb; t < te; ++t) {
         float4 xv[2];
-        xload(t, xv);
-        float a[8];
-        emb(t, xv, a);
+        opload(t, xv);
+        float at[8];
+        emb(t, xv, at);
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bo[c][s], acc, 0, 0, 0);
+        for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s], bo[c][s], acc, 0, 0, 0);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (frow == 0x7fffffffu && __float_as_int(acc[r]) <= kClampBits) frow = (unsigned)(t * 16 + 4 * g + r);
       }
-      if (frow != 0x7fffffffu) best[c] = ((unsigned long long)(unsigned)kClampBits << 32) | frow;
+      if (frow != 0x7fffffffu) {
+        bv[c] = kClampBits;
+        br[c] = frow;
+      }
     }
   }
-  // the 4 lane groups of each column (rows 4 g + r of every tile), then the waves through LDS
+  // the 4 lane groups of each column (rows 4 g + r of every tile) by row swaps, then the waves
+  // through LDS. Keys (value bits, row) compare as one unsigned 64-bit number: the values are
+  // positive here (a clamped column holds the clamp's bits)
+  auto xg = [&](int c, bool by32) {
+    const auto sv = by32 ? __builtin_amdgcn_permlane32_swap((unsigned)bv[c], (unsigned)bv[c], false, false)
+                         : __builtin_amdgcn_permlane16_swap((unsigned)bv[c], (unsigned)bv[c], false, false);
+    const auto sr = by32 ? __builtin_amdgcn_permlane32_swap(br[c], br[c], false, false)
+                         : __builtin_amdgcn_permlane16_swap(br[c], br[c], false, false);
+    const unsigned long long k0 = ((unsigned long long)sv[0] << 32) | sr[0];
+    const unsigned long long k1 = ((unsigned long long)sv[1] << 32) | sr[1];
+    const unsigned long long kk = k0 < k1 ? k0 : k1;
+    bv[c] = (int)(kk >> 32);
+    br[c] = (unsigned)kk;
+  };
 #pragma unroll
-  for (int off = 16; off <= 32; off <<= 1)
+  for (int c = 0; c < kTop1CT; ++c) xg(c, false);
 #pragma unroll
-    for (int c = 0; c < kTop1CT; ++c) {
-      const unsigned long long o = ((unsigned long long)(unsigned)__shfl_xor((int)(best[c] >> 32), off) << 32) |
-                                   (unsigned)__shfl_xor((int)(best[c] & 0xffffffffu), off);
-      best[c] = o < best[c] ? o : best[c];
-    }
+  for (int c = 0; c < kTop1CT; ++c) xg(c, true);
   if (g == 0) {
 #pragma unroll
-    for (int c = 0; c < kTop1CT; ++c) wkeys[w][c * 16 + c16] = best[c];
+    for (int c = 0; c < kTop1CT; ++c)
+      wkeys[w][c * 16 + c16] = ((unsigned long long)(unsigned)bv[c] << 32) | br[c];
   }
   FD_STAMP(3, __builtin_amdgcn_s_memtime());
   __syncthreads();
@@ -765,7 +869,7 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top1_kernel(
       for (int v = 1; v < kTop1Waves; ++v) bb = wkeys[v][jj] < bb ? wkeys[v][jj] : bb;  // ties: lower wave = lower row
       if (RS == 1) {
         const unsigned row = (unsigned)(bb & 0xffffffffu);
-        out_idx[(int64_t)b * V2max + j] = row >= 0x7fffffffu ? -1 : (int64_t)row;
+        out_idx[(int64_t)b * V2max + j] = row >= 0x7ffffff0u ? -1 : (int64_t)row;
         if (out_dist) out_dist[(int64_t)b * V2max + j] = sqrtf(__int_as_float((int)(bb >> 32)));
       } else {
         part[((int64_t)b * RS + rs) * V2max + j] = bb;
@@ -789,13 +893,13 @@ __global__ __launch_bounds__(256) void fd_top1_merge_kernel(const unsigned long 
     best = key < best ? key : best;
   }
   const unsigned row = (unsigned)(best & 0xffffffffu);
-  out_idx[(int64_t)b * V2max + j] = row >= 0x7fffffffu ? -1 : (int64_t)row;
+  out_idx[(int64_t)b * V2max + j] = row >= 0x7ffffff0u ? -1 : (int64_t)row;
   if (out_dist) out_dist[(int64_t)b * V2max + j] = sqrtf(__int_as_float((int)(best >> 32)));
 }
 
 struct Top1Plan {
-  int NCG, RS;
-  int64_t part_bytes;
+  int T1, T2, NCG, RS;
+  int64_t a_bytes, b_bytes, part_bytes;
 };
 
 inline int64_t al256_(int64_t x) { return (x + 255) & ~(int64_t)255; }
@@ -808,6 +912,10 @@ inline Top1Plan top1_plan(int B, int V1max, int V2max) {
   // row parts only when the batch leaves the chip short of blocks (each wave keeps >= 2 row tiles)
   const int rs = blocks >= 192 ? 1 : (int)((256 + blocks - 1) / blocks);
   p.RS = std::max(1, std::min(rs, T1 / (2 * kTop1Waves)));
+  p.T1 = T1;
+  p.T2 = T2;
+  p.a_bytes = al256_((int64_t)B * T1 * 2048);
+  p.b_bytes = al256_((int64_t)B * T2 * 2048);
   p.part_bytes = p.RS > 1 ? al256_((int64_t)B * p.RS * V2max * 8) : 0;
   return p;
 }
@@ -878,7 +986,8 @@ extern "C" int64_t pk_feat_dist_work_size(int B, int V1max, int V2max, int topk,
   if (mode != 0 || topk != 1) return two_pass;
   // mode 0 top-1: the one-launch pass's row-part keys, or the two-pass fallback's scratch
   // (unaligned operand rows); neither keeps anything across calls
-  return std::max(two_pass, top1_plan(B, V1max, V2max).part_bytes);
+  const Top1Plan tp = top1_plan(B, V1max, V2max);
+  return std::max(two_pass, tp.a_bytes + tp.part_bytes);
 }
 
 extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, const float* evecs_y, int ldy,
@@ -894,23 +1003,33 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
   hipStream_t s = pk::as_stream(stream);
   const bool aligned = (ldx % 4) == 0 && (ldy % 4) == 0 && (reinterpret_cast<uintptr_t>(evecs_x) & 15) == 0 &&
                        (reinterpret_cast<uintptr_t>(evecs_y) & 15) == 0;
-  if (mode == 0 && aligned && V1max > 0 && topk == 1) {  // one launch (+ a merge launch when RS > 1)
+  if (mode == 0 && aligned && V1max > 0 && topk == 1) {  // two launches (+ a merge launch when RS > 1)
     const Top1Plan tp = top1_plan(B, V1max, V2max);
-    auto* part = static_cast<unsigned long long*>(work);
+    auto* At = static_cast<f32x4*>(work);
+    auto* part = reinterpret_cast<unsigned long long*>(static_cast<char*>(work) + tp.a_bytes);
     const dim3 grid((unsigned)((int64_t)B * tp.NCG * tp.RS));
 #ifdef PK_DEVBUILD
-    static const int tvar = [] {  // development knob PK_FD_VAR: limiter variants of fd_top1_kernel
+    static const int tvar = [] {  // development knob PK_FD_VAR: 13 phase stamps, 20 emb in the main pass
       const char* e = std::getenv("PK_FD_VAR");
       return e ? std::atoi(e) : 0;
     }();
-#define PK_FDT(V) hipLaunchKernelGGL((fd_top1_kernel<V>), grid, dim3(64 * kTop1Waves), 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, \
-                                     n2, V1max, V2max, tp.NCG, tp.RS, out_idx, out_dist, part)
-    if (tvar == 1) PK_FDT(1); else if (tvar == 13) PK_FDT(13); else PK_FDT(0);
-#undef PK_FDT
 #else
-    hipLaunchKernelGGL(fd_top1_kernel<0>, grid, dim3(64 * kTop1Waves), 0, s, evecs_x, ldx, C, evecs_y, ldy, n1, n2, V1max, V2max,
-                       tp.NCG, tp.RS, out_idx, out_dist, part);
+    constexpr int tvar = 0;
 #endif
+    if (tvar != 20) {
+      hipLaunchKernelGGL(fd_top1_prep_kernel, dim3((unsigned)((tp.T1 + 7) / 8), B), dim3(512), 0, s, evecs_x, ldx, C,
+                         n1, V1max, tp.T1, At);
+      PK_CHECK_LAUNCH();
+    }
+#define PK_FDT(V, E)                                                                                              \
+  hipLaunchKernelGGL((fd_top1_kernel<V, E>), grid, dim3(64 * kTop1Waves), 0, s, evecs_x, ldx, C, At, tp.T1, evecs_y, \
+                     ldy, n1, n2, V1max, V2max, tp.NCG, tp.RS, out_idx, out_dist, part)
+#ifdef PK_DEVBUILD
+    if (tvar == 13) PK_FDT(13, false); else if (tvar == 20) PK_FDT(0, true); else PK_FDT(0, false);
+#else
+    PK_FDT(0, false);
+#endif
+#undef PK_FDT
     PK_CHECK_LAUNCH();
     if (tp.RS > 1) {
       hipLaunchKernelGGL(fd_top1_merge_kernel, dim3((V2max + 255) / 256, B), dim3(256), 0, s, part, n2, V2max, tp.RS,
