@@ -229,13 +229,17 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// pass 1: part[b, s] (64 x 64) over the 64 rows of slab s; grid (S, B), block 256 = 4 waves.
-// Wave w contracts the 16 rows r0 + 16 w + 4 q + g (K-steps q < 4, g = l >> 4); lane
-// (u = l & 15, g) loads the float4s Phi[r][4u .. 4u+3] and w_r x[r][4u .. 4u+3] once. Tile
-// (kt, ct) holds the output rows k = 4 i + kt (A = component kt of the Phi float4 of lane (i, g))
-// and columns c = 4 j + ct (B = component ct of the x float4 of lane (j, g)): register rr of
-// tile (kt, ct) in lane (j, g) is the wave's part[4 (4 g + rr) + kt][4 j + ct]. The four waves'
-// 64 x 64 partials meet in LDS and are added in wave order.
+// pass 1: part[b, s] (64 x 64) over the kCPB x 64 rows of slab s; grid (S, B), block 256 = 4 waves.
+// Per 64-row chunk, wave w contracts the 16 rows r0 + 16 w + 4 q + g (K-steps q < 4, g = l >> 4);
+// lane (u = l & 15, g) loads the float4s Phi[r][4u .. 4u+3] and w_r x[r][4u .. 4u+3] once, the
+// next chunk's loads in flight during this chunk's MFMAs. Tile (kt, ct) holds the output rows
+// k = 4 i + kt (A = component kt of the Phi float4 of lane (i, g)) and columns c = 4 j + ct (B =
+// component ct of the x float4 of lane (j, g)): register rr of tile (kt, ct) in lane (j, g) is the
+// wave's part[4 (4 g + rr) + kt][4 j + ct], accumulated over the block's chunks in order. The four
+// waves' 64 x 64 partials meet in LDS and are added in wave order. Round 5: kCPB = 4 chunks per
+// block (was 1): the partial slabs written and re-read by the combine drop 4x (they were 0.5 B per
+// input byte, the round-4 PMC excess of 1.8x the algorithmic bytes).
+constexpr int kCPB = 4;
 __global__ __launch_bounds__(256) void spec_reduce_mfma_kernel(const float* __restrict__ x, int ldx,
                                                                const float* __restrict__ mass,
                                                                const float* __restrict__ evecs, int N, int S,
@@ -246,33 +250,47 @@ __global__ __launch_bounds__(256) void spec_reduce_mfma_kernel(const float* __re
   const float* __restrict__ phi = evecs + (int64_t)b * N * kKC;
   const float* __restrict__ xb = x + (int64_t)b * N * ldx;
   const float* __restrict__ mb = mass ? mass + (int64_t)b * N : nullptr;
-  const int rw = s * kRows + 16 * w;
+  const int r0 = s * kCPB * kRows;
+  const int nch = min(kCPB, (N - r0 + kRows - 1) / kRows);  // chunks of this block (>= 1)
   float4 pv[4], xv[4];
   float wv[4];
+  auto load = [&](int ch) {
+    const int rw = r0 + ch * kRows + 16 * w;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = rw + 4 * q + g;
-    const int rc = r < N ? r : N - 1;  // clamped, then zeroed
-    pv[q] = reinterpret_cast<const float4*>(phi + (int64_t)rc * kKC)[u];
-    xv[q] = reinterpret_cast<const float4*>(xb + (int64_t)rc * ldx)[u];
-    wv[q] = mb ? mb[rc] : 1.f;
-  }
+    for (int q = 0; q < 4; ++q) {
+      const int r = rw + 4 * q + g;
+      const int rc = r < N ? r : N - 1;  // clamped, then zeroed
+      pv[q] = reinterpret_cast<const float4*>(phi + (int64_t)rc * kKC)[u];
+      xv[q] = reinterpret_cast<const float4*>(xb + (int64_t)rc * ldx)[u];
+      wv[q] = mb ? mb[rc] : 1.f;
+    }
+  };
   f32x4 acc[4][4];
 #pragma unroll
   for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) acc[kt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  for (int ch = 0; ch < nch; ++ch) {
+    const int rw = r0 + ch * kRows + 16 * w;
+    float a[4][4], xs[4][4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const bool ok = rw + 4 * q + g < N;
-    const float wr = ok ? wv[q] : 0.f;
-    const float a[4] = {pv[q].x, pv[q].y, pv[q].z, pv[q].w};
-    const float xs[4] = {mb ? xv[q].x * wr : (ok ? xv[q].x : 0.f), mb ? xv[q].y * wr : (ok ? xv[q].y : 0.f),
-                         mb ? xv[q].z * wr : (ok ? xv[q].z : 0.f), mb ? xv[q].w * wr : (ok ? xv[q].w : 0.f)};
+    for (int q = 0; q < 4; ++q) {
+      const bool ok = rw + 4 * q + g < N;
+      const float wr = ok ? wv[q] : 0.f;
+      a[q][0] = pv[q].x, a[q][1] = pv[q].y, a[q][2] = pv[q].z, a[q][3] = pv[q].w;
+      xs[q][0] = mb ? xv[q].x * wr : (ok ? xv[q].x : 0.f);
+      xs[q][1] = mb ? xv[q].y * wr : (ok ? xv[q].y : 0.f);
+      xs[q][2] = mb ? xv[q].z * wr : (ok ? xv[q].z : 0.f);
+      xs[q][3] = mb ? xv[q].w * wr : (ok ? xv[q].w : 0.f);
+    }
+    if (ch + 1 < nch) load(ch + 1);
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) acc[kt][ct] = mfma4(a[kt], xs[ct], acc[kt][ct]);
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[kt][ct] = mfma4(a[q][kt], xs[q][ct], acc[kt][ct]);
   }
 #pragma unroll
   for (int kt = 0; kt < 4; ++kt)
@@ -347,7 +365,10 @@ __global__ __launch_bounds__(256) void spec_expand_mfma_kernel(const float* __re
                                                                const float* __restrict__ gtb, int64_t gt_stride,
                                                                float* __restrict__ gt) {
   __shared__ float4 scoef[kKC * kKC / 4];  // [k][c / 4]
-  const int tile = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  // a crop's row blocks on one XCD: its 16 KB of coefficients come from HBM once per crop, not
+  // once per XCD (the round-5 PMC pass counted the re-fetches at ~15 MB per launch)
+  const int3 lb = pk::xcd_block3();
+  const int tile = lb.x, b = lb.y, tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63, u = l & 15, g = l >> 4;
   const float* __restrict__ cb = coef + (int64_t)b * kKC * kKC;
   {
@@ -447,7 +468,8 @@ extern "C" int pk_spectral_diffusion(const float* in, int ld_in, const float* ma
   PK_REQUIRE(in && evecs && evals && t && work && scaled && out);
   PK_REQUIRE(mode == 0 || (saved && gt));
   hipStream_t s = pk::as_stream(stream);
-  const int S = (N + kRows - 1) / kRows;
+  // slabs per crop: 64 rows each for the scalar passes, kCPB x 64 for the MFMA reduce
+  const int S = spec_scalar() ? (N + kRows - 1) / kRows : (N + kCPB * kRows - 1) / (kCPB * kRows);
   if (spec_scalar())
     hipLaunchKernelGGL(spec_reduce_kernel, dim3(S, B), dim3(256), 0, s, in, ld_in, mode == 0 ? mass : nullptr,
                        evecs, N, S, work);

@@ -103,7 +103,7 @@ class _AttnPropFn(torch.autograd.Function):
         call("pk_attention_bwd", ptr(q), ptr(kv), ctypes.c_void_p(kv.data_ptr() + off), ptr(a), ptr(da), ptr(lse),
              B, D, heads, N, M, 2 * C * M, 2 * C * M, ptr(delta), ptr(dq), ptr(dkv),
              ctypes.c_void_p(dkv.data_ptr() + off), 2 * C * M, 2 * C * M, _lib.stream(dev),
-             work=("mfma", 7 * 2 * N * M * D * B * heads))
+             work=("mfma", 5 * 2 * N * M * D * B * heads))  # algorithmic: S, dP, dV, dK, dQ (7 executed)
         # d desc = Pq^T dq + dout (residual) + dhc[:, :C] (concatenation), one launch
         dx = torch.empty((B, C, N), dtype=torch.float32, device=dev)
         ops.linear_ex(dq, f(wq), None, 1, B * N, N, C, C, y=dx, transw=True, add=dout, add_cols=C,

@@ -434,7 +434,7 @@ class _Attention(torch.autograd.Function):
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         call("pk_attention_bwd", ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse), B, D, H, N, M, 0, 0,
              ptr(delta), ptr(dq), ptr(dk), ptr(dv), 0, 0, _lib.stream(q.device),
-             work=("mfma", 7 * 2 * N * M * D * B * H))  # S, dP, dQ | S, dP, dV, dK
+             work=("mfma", 5 * 2 * N * M * D * B * H))  # algorithmic S, dP, dV, dK, dQ (executed: S, dP, dQ | S, dP, dV, dK)
         return dq, dk, dv
 
 

@@ -546,11 +546,17 @@ class PipelinedTrainer:
                 if not self.split:
                     step.apply(allreduce=False, reset=False)
             if self.defer_ir:  # I_k: reads buffer k's crops and T_k's C_pred (both graph-static)
+                # its results go to buffers allocated outside the capture, each written by one
+                # kernel: a graph-pool output could share memory with the graph's own scratch
+                # (the feature distance's), which holds other bytes during a replay
+                dev_ = step.last_C_pred.device
+                ir_out = torch.zeros((), dtype=torch.float32, device=dev_)
+                st = torch.zeros((step.last_C_pred.shape[0],), dtype=torch.int32, device=dev_)
                 gi = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gi):
-                    st = torch.empty((step.last_C_pred.shape[0],), dtype=torch.int32, device=step.last_C_pred.device)
-                    self.logs[k]["IR"] = TrainStep.inlier_ratio_of(op, self.crops[k], step.last_C_pred, status=st)
-                    self.logs[k]["ir_index_status"] = st
+                    ir_out.copy_(TrainStep.inlier_ratio_of(op, self.crops[k], step.last_C_pred, status=st))
+                self.logs[k]["IR"] = ir_out
+                self.logs[k]["ir_index_status"] = st
                 self.ir_graphs.append(gi)
             self.grads.append([p.grad for p in step.params])
             gb = None
@@ -789,6 +795,25 @@ class PipelinedInfer:
             self.crop_graphs[k].replay()
             self.formed[k].record(self.side)
 
+    def _enter(self) -> torch.cuda.Stream:
+        """The caller's stream; every stream that replays a graph writing returned outputs waits
+        for it first, so the caller's reads of earlier outputs (enqueued before this call) finish
+        before a replay overwrites them."""
+        cur = torch.cuda.current_stream()
+        for st in (self.main, self.post):
+            if st != cur:
+                st.wait_stream(cur)
+        return cur
+
+    @staticmethod
+    def _hand_out(cur: torch.cuda.Stream, producer: torch.cuda.Stream, out):
+        """Order the caller's stream after the graph that wrote `out` (no host sync)."""
+        if out is not None and producer != cur:
+            ev = torch.cuda.Event()
+            ev.record(producer)
+            cur.wait_event(ev)
+        return out
+
     def _pose(self, k):
         with torch.cuda.stream(self.post):
             self.post.wait_event(self.modeled[k])
@@ -797,6 +822,7 @@ class PipelinedInfer:
         return self.outs[k]
 
     def __call__(self):
+        cur = self._enter()
         if self.stages == 2:
             k = self.i & 1
             self._form(k ^ 1)  # the next batch's crops, concurrently
@@ -805,7 +831,7 @@ class PipelinedInfer:
                 self.infer_graphs[k].replay()
                 self.consumed[k].record(self.main)
             self.i += 1
-            return self.outs[k]
+            return self._hand_out(cur, self.main, self.outs[k])
         k = self.i % 3
         self._form((self.i + 1) % 3)  # batch i+1 (its buffer's pose stage, batch i-2, is ordered before)
         with torch.cuda.stream(self.main):
@@ -815,15 +841,16 @@ class PipelinedInfer:
         out = self._pose(self._pending) if self._pending is not None else None  # batch i-1
         self._pending = k
         self.i += 1
-        return out
+        return self._hand_out(cur, self.post, out)
 
     def flush(self):
         """stages=3: run the pose stage still pending (the last call's batch) and return its outputs."""
         if self.stages == 2 or self._pending is None:
             return None
+        cur = self._enter()
         out = self._pose(self._pending)
         self._pending = None
-        return out
+        return self._hand_out(cur, self.post, out)
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:

@@ -142,6 +142,37 @@ def ball_query_roofline(dev, probe_launches: int = 10) -> dict:
             "ms_per_launch": round(ms, 4), "bytes_per_launch": byts}
 
 
+def feat_dist_roofline(dev, launches: int = 20) -> dict:
+    """The north-star MFMA gate kernel: pk_feat_dist_topk (fp32 argmin, the naive solver's and the
+    IR's feature distance, fmap2pointmap_solvers/naive.py:20,33) at configs[1] (32 crops of
+    1024 x 1024, K = 32: 2.147 GFLOP per call), `launches` back-to-back calls between two HIP
+    events on the launch stream (its prep + main passes included), spectral-basis operands."""
+    from dpfm_amd import ops
+    from dpfm_amd.dataset.synthetic import lbo_operators
+    B, V = 32, 1024
+    ex = torch.stack([torch.from_numpy(lbo_operators(V, 64, 10 + b)[2]) for b in range(B)]).to(dev)
+    ey = torch.stack([torch.from_numpy(lbo_operators(V, 64, 50 + b)[2]) for b in range(B)]).to(dev)
+    C = (torch.eye(30)[None] + 0.3 * torch.randn(B, 30, 30, generator=torch.Generator().manual_seed(B))).to(dev)
+    n = torch.full((B,), V, dtype=torch.int32, device=dev)
+    wk = torch.empty(1 << 24, dtype=torch.uint8, device=dev)
+    f = lambda: ops.feat_dist_topk(ex, C, ey, n, n, 1, work=wk)  # noqa: E731
+    for _ in range(3):
+        f()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(launches):
+        f()
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / launches
+    flops = 2.0 * B * V * V * 32
+    ach = flops / (ms * 1e-3) / 1e12
+    return {"kernel": "pk_feat_dist_topk (configs[1]: 32 x 1024 x 1024, fp32 top-1, prep + main)", "bound": "mfma",
+            "achieved": round(ach, 2), "peak": F32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / F32_MFMA_TFLOPS, 4),
+            "ms_per_launch": round(ms, 4), "flops_per_launch": flops, "launches": launches}
+
+
 def cpu_baseline(n_crops: int, n1: int, n2: int) -> dict:
     """The oracle (reference CPU path restated: numpy / torch-CPU) on the same synthetic
     inputs: crop formation + DPFM fwd+bwd + loss + naive IR + RMSprop, per crop."""
@@ -1009,6 +1040,7 @@ def main():
                              "valu64_frac": r64["frac"]}
         if args.mode == "train" and not args.no_roofline_probe and world == 1:
             out["roofline_ball_query"] = ball_query_roofline(dev)
+            out["roofline_feat_dist"] = feat_dist_roofline(dev)
         if not args.no_cpu_baseline and world == 1 and not args.ragged:
             if args.mode == "train":
                 out["cpu_baseline"] = cpu_baseline(args.cpu_crops, args.points, args.points)

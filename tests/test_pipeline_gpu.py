@@ -293,6 +293,41 @@ def test_three_stage_pipelined_infer_matches_graphed(device):
             assert torch.equal(out[key], ref[key]), key
 
 
+def test_pipelined_infer_outputs_ordered_on_caller_stream(device):
+    """PipelinedInfer hands its outputs to the caller's current stream: copies taken
+    on that stream right after each call, with no device synchronisation in between, equal the
+    single-stream graph's outputs — for stages=3 (pose graphs on a private stream) and from a
+    caller stream other than the pipeline's main stream."""
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import GraphedInfer, InferStep, PipelinedInfer, make_frame_batch
+    torch.manual_seed(0)
+    F, N = 4, 512
+    fb, op = make_frame_batch(F, N, N, seed=73, device=device)
+    model = DPFMNet().to(device).eval()
+    g = GraphedInfer(CropFormation(n1=N, npoint=N, seed=4), InferStep(model, hypotheses=256), fb, op)
+    ref = {k: v.clone() for k, v in g().items() if torch.is_tensor(v)}
+    torch.cuda.synchronize()
+    for stages in (3, 2):
+        p = PipelinedInfer(CropFormation(n1=N, npoint=N, seed=4), InferStep(model, hypotheses=256), fb, op,
+                           stages=stages)
+        caller = torch.cuda.Stream()
+        copies = []
+        with torch.cuda.stream(caller):
+            for _ in range(6):
+                out = p()
+                if out is not None:
+                    copies.append({k: out[k].clone() for k in ("T", "ir", "metrics", "C")})
+            if stages == 3:
+                out = p.flush()
+                copies.append({k: out[k].clone() for k in ("T", "ir", "metrics", "C")})
+        torch.cuda.synchronize()
+        assert len(copies) == 6
+        for c in copies:
+            for key, v in c.items():
+                assert torch.equal(v, ref[key]), (stages, key)
+
+
 def test_infer_step_with_icp_matches_standalone_icp(device):
     """InferStep(icp_evaluations=E) refines the RANSAC poses against the crops exactly as the
     host-polled ops.icp with max_iteration E - 1 does, and stays HIP-graph capturable."""
