@@ -20,12 +20,15 @@
 // with keys 4g + r (g = l >> 4) of query l & 15, which is directly the B operand of the
 // next contraction over keys when step r pairs key 4g + r with A's lane group g.
 //
-// Kernels (one workgroup = 4 waves x 16 rows = 64 rows of one (crop, head)):
-//   attn_fwd_kernel     queries; streams 64-key tiles of K, V through LDS; writes out
-//                       and (m, 1 / sum) per query (saved for the backward)
-//   attn_bwd_dq_kernel  queries; delta = rowsum(dO * O) then dQ = 0.25 dS K
-//   attn_bwd_dkv_kernel keys; streams 64-query tiles of Q, dO; dV = P^T dO,
-//                       dK = 0.25 dS^T Q with dS = P (dP - delta), dP = dO V^T
+// Kernels:
+//   attn_fwd_kernel            one workgroup = 4 waves x 16 queries = 64 queries of one (crop,
+//                              head); streams 64-key tiles of K, V through LDS; writes out and
+//                              (m, 1 / sum) per query (saved for the backward)
+//   attn_bwd_kernel            one workgroup = 8 waves x 32 keys = 256 keys of one (crop, head);
+//                              streams 64-query tiles of Q, dO, O; delta = rowsum(dO * O),
+//                              dV = P^T dO, dK = 0.25 dS^T Q, and a dQ = 0.25 dS K partial per key
+//                              block (dS = P (dP - delta), dP = dO V^T): each contraction once
+//   attn_bwd_dq_reduce_kernel  the dQ partials added in key-block order
 #include "common.hpp"
 
 namespace {
@@ -183,189 +186,211 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
   }
 }
 
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
+// One-pass backward (round 5): one workgroup of 8 waves per (crop, head, 256-key block); wave w
+// owns keys kb0 + 32 w .. + 31 (two 16-key sub-tiles) with K, V (and K^T for dQ) in registers and
+// walks every 64-query tile of the crop, staged once per block in LDS. Per 16 x 16 (query, key)
+// sub-tile it forms S and dP (8 MFMAs), P and dS in registers, dV^T += dO^T P and dK^T += Q^T dS
+// (8 MFMAs; P and dS in the S D-layout are directly the B operands), and dQ^T += K^T dS^T
+// (4 MFMAs) after moving dS through a wave-private LDS tile (the one transposition the two
+// contractions need: 4 ds_write_b32 + 1 ds_read_b128 per sub-tile). That is the 5 algorithmic
+// contractions once each — the two-kernel form recomputed S and dP in both (7).
+// dQ: the 8 waves' 32-key partials of a 64-query tile are added in wave order through LDS; the
+// block's 256-key sum is written to partial slot p = key block (slot 0 is dq itself, the others
+// the caller's work buffer) and attn_bwd_dq_reduce_kernel adds the slots in slot order and scales
+// (deterministic; a single key block writes dq scaled, no reduce launch).
+// delta = rowsum(dO * O) is formed per query as the tile is staged (fmaf over d in order, the
+// four lanes' partial sums of a query added as (p0 + p1) + (p2 + p3)).
+constexpr int kKB = 256;   // keys per block
+constexpr int kSA = 20;    // [q][p(d)] stride
+constexpr int kSQ = 68;    // [d][q] stride
+constexpr int kSTs = 36;   // dS transpose tile [q][32 keys] stride
+constexpr int kSRq = 20;   // dQ partial [q][d] stride
+
+__global__ __launch_bounds__(512, 1) void attn_bwd_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
-    const float* __restrict__ o, const float* __restrict__ dout, const float* __restrict__ lse,
-    int H, int N, int M, int64_t sbk, int64_t sbv, float* __restrict__ delta, float* __restrict__ dq) {
-  __shared__ float Ks[kD * kSR];
-  __shared__ float Vs[kD * kSR];
-  __shared__ float KT[kT * kSC];
-  const int3 lb = pk::xcd_block3();  // a (crop, head)'s query blocks share one XCD's L2 (K / V)
-  const int h = lb.y, b = lb.z;
-  const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
-  const int qi = lb.x * kT + pk::wave_id() * 16 + c;
+    const float* __restrict__ o, const float* __restrict__ dout, const float* __restrict__ lse, int H, int N,
+    int M, int64_t sbk, int64_t sbv, int64_t sbdk, int64_t sbdv, float* __restrict__ dq,
+    float* __restrict__ part, float* __restrict__ dk, float* __restrict__ dv) {
+  __shared__ __attribute__((aligned(16))) float QA[kT * kSA];   // Q  [q][p(d)], p(4 s + g) = 4 g + s
+  __shared__ __attribute__((aligned(16))) float GA[kT * kSA];   // dO [q][p(d)]
+  __shared__ __attribute__((aligned(16))) float QT[kD * kSQ];   // Q  [d][q]
+  __shared__ __attribute__((aligned(16))) float GT[kD * kSQ];   // dO [d][q]
+  __shared__ __attribute__((aligned(16))) float MI[3 * kT];     // m, 1 / sum, delta per query
+  __shared__ __attribute__((aligned(16))) float TS[8 * 16 * kSTs];    // per-wave dS transpose
+  __shared__ __attribute__((aligned(16))) float RQ[8 * kT * kSRq];    // per-wave dQ partials
+  const int3 xb = pk::xcd_block3();  // a (crop, head)'s key blocks share one XCD's L2 (Q / dO / O)
+  const int kblk = xb.x, h = xb.y, b = xb.z;
+  const int wave = pk::wave_id(), lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
+  const int HN = H * N;
   const int64_t qoff = ((int64_t)b * kD * H + h) * N;
-  const float* kb = k + (int64_t)b * sbk + (int64_t)h * M;
-  const float* vb = v + (int64_t)b * sbv + (int64_t)h * M;
-  float qr[4], dor[4];
-  float dl = 0.f;
+  const float2* lb = reinterpret_cast<const float2*>(lse) + ((int64_t)b * H + h) * N;
+  // this wave's keys: kk(t) = kb0 + 16 t + c (S / dP operands), kk(t, r) = kb0 + 16 t + 4 g + r (K^T)
+  const int kb0 = kblk * kKB + 32 * wave;
+  const float* kbp = k + (int64_t)b * sbk + (int64_t)h * M;
+  const float* vbp = v + (int64_t)b * sbv + (int64_t)h * M;
+  float kr[2][4], vr[2][4], kt[2][4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int64_t a = qoff + (int64_t)(4 * s + g) * H * N + qi;
-    qr[s] = qi < N ? q[a] * kScale : 0.f;
-    dor[s] = qi < N ? dout[a] : 0.f;
-    dl = fmaf(dor[s], qi < N ? o[a] : 0.f, dl);
-  }
-  dl = grp_sum(dl);  // delta = sum_d dO * O for query qi
-  const float2 ms = qi < N ? reinterpret_cast<const float2*>(lse)[((int64_t)b * H + h) * N + qi]
-                           : make_float2(__builtin_huge_valf(), 0.f);
-  if (qi < N && g == 0) delta[((int64_t)b * H + h) * N + qi] = dl;
-  f32x4 acc[4];  // independent chains per 16-key sub-tile (accuracy, see the forward)
+  for (int t = 0; t < 2; ++t) {
+    const int kj = kb0 + 16 * t + c;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  Tile kt = load_tile(kb, H * M, M, 0), vt = load_tile(vb, H * M, M, 0);
-  for (int k0 = 0; k0 < M; k0 += kT) {
-    __syncthreads();
-    store_tile(kt, Ks, KT);
-    store_tile(vt, Vs, nullptr);
-    __syncthreads();
-    if (k0 + kT < M) {
-      kt = load_tile(kb, H * M, M, k0 + kT);
-      vt = load_tile(vb, H * M, M, k0 + kT);
+    for (int s = 0; s < 4; ++s) {
+      const int64_t a = (int64_t)(4 * s + g) * H * M + (kj < M ? kj : 0);
+      const float kv = kbp[a], vv = vbp[a];  // unconditional at a clamped key
+      kr[t][s] = kj < M ? kv * kScale : 0.f;
+      vr[t][s] = kj < M ? vv : 0.f;
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        st = mfma(Ks[(4 * s + g) * kSR + 16 * t + c], qr[s], st);
-        dp = mfma(Vs[(4 * s + g) * kSR + 16 * t + c], dor[s], dp);
-      }
-      // packed pairs (v_pk_*: the same per-element rounding as the scalar ops)
-      float pr[4], dsr[4];
-#pragma unroll
-      for (int r = 0; r < 4; r += 2) {
-        f32x2 d = {st[r], st[r + 1]};
-        d = (d - f32x2{ms.x, ms.x}) * f32x2{kLog2e, kLog2e};
-        f32x2 pp = f32x2{exp2_(d.x), exp2_(d.y)} * f32x2{ms.y, ms.y};
-        const f32x2 ds = pp * (f32x2{dp[r], dp[r + 1]} - f32x2{dl, dl});
-        pr[r] = pp.x;
-        pr[r + 1] = pp.y;
-        dsr[r] = ds.x;
-        dsr[r + 1] = ds.y;
-      }
-      if (k0 + kT > M) {  // workgroup-uniform: keys past M (ragged last tile) carry no weight
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (k0 + 16 * t + 4 * g + r >= M) dsr[r] = 0.f;
-      }
-      (void)pr;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[t] = mfma(KT[(16 * t + 4 * g + r) * kSC + c], dsr[r], acc[t]);
+    for (int r = 0; r < 4; ++r) {
+      const int kj2 = kb0 + 16 * t + 4 * g + r;
+      const float kv = kbp[(int64_t)c * H * M + (kj2 < M ? kj2 : 0)];
+      kt[t][r] = kj2 < M ? kv : 0.f;
     }
   }
-  const f32x4 accs = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-  if (qi < N) {
+  const bool ragged_keys = kb0 + 32 > M;  // wave-uniform
+  // staging: waves 0-3 carry dO and O (and form delta), waves 4-7 Q and (m, 1 / sum); thread ->
+  // (query sq = (tid & 255) >> 2, channels 4 sp .. 4 sp + 3)
+  const int sq = (threadIdx.x & 255) >> 2, sp = threadIdx.x & 3;
+  const bool stage_g = threadIdx.x < 256;
+  float pf[8];
+  float2 pm = make_float2(0.f, 0.f);
+  auto issue = [&](int q0) {
+    const int qq = q0 + sq, qc = qq < N ? qq : 0;
+    const float* src0 = stage_g ? dout : q;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dq[qoff + (int64_t)(4 * g + r) * H * N + qi] = accs[r] * kScale;
+    for (int i = 0; i < 4; ++i) pf[i] = src0[qoff + (int64_t)(4 * sp + i) * HN + qc];
+    if (stage_g) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pf[4 + i] = o[qoff + (int64_t)(4 * sp + i) * HN + qc];
+    } else if (sp == 0) {
+      pm = lb[qc];
+    }
+  };
+  auto stage = [&](int q0) {
+    const bool ok = q0 + sq < N;
+    float* A = stage_g ? GA : QA;
+    float* T = stage_g ? GT : QT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x = ok ? pf[i] : 0.f;
+      const int d = 4 * sp + i;
+      A[sq * kSA + 4 * (d & 3) + (d >> 2)] = x;
+      T[d * kSQ + sq] = x;
+    }
+    if (stage_g) {
+      float dl = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dl = fmaf(ok ? pf[i] : 0.f, ok ? pf[4 + i] : 0.f, dl);
+      const float d1 = dl + __shfl_xor(dl, 1);
+      const float d2 = d1 + __shfl_xor(d1, 2);
+      if (sp == 0) MI[2 * kT + sq] = d2;
+    } else if (sp == 0) {
+      MI[sq] = ok ? pm.x : __builtin_huge_valf();  // exp2(-inf) * 0 = 0: padding queries carry no weight
+      MI[kT + sq] = ok ? pm.y : 0.f;
+    }
+  };
+  f32x4 dka[2][2], dva[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) dka[t][e] = dva[t][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float* ts = TS + wave * 16 * kSTs;
+  float* rq = RQ + wave * kT * kSRq;
+  const int P = gridDim.x;
+  float* dst = kblk == 0 ? dq : part + (int64_t)(kblk - 1) * ((int64_t)gridDim.z * kD * HN);
+  const float osc = P == 1 ? kScale : 1.f;  // one key block: dq final here
+  issue(0);
+  stage(0);
+  for (int q0 = 0; q0 < N; q0 += kT) {
+    __syncthreads();  // tile q0 staged; RQ free
+    if (q0 + kT < N) issue(q0 + kT);
+    f32x4 dqa[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4 qa = *reinterpret_cast<const f32x4*>(&QA[(16 * u + c) * kSA + 4 * g]);
+      const f32x4 ga = *reinterpret_cast<const f32x4*>(&GA[(16 * u + c) * kSA + 4 * g]);
+      const f32x4 qtv = *reinterpret_cast<const f32x4*>(&QT[c * kSQ + 16 * u + 4 * g]);
+      const f32x4 gtv = *reinterpret_cast<const f32x4*>(&GT[c * kSQ + 16 * u + 4 * g]);
+      const f32x4 L4 = *reinterpret_cast<const f32x4*>(&MI[16 * u + 4 * g]);
+      const f32x4 I4 = *reinterpret_cast<const f32x4*>(&MI[kT + 16 * u + 4 * g]);
+      const f32x4 D4 = *reinterpret_cast<const f32x4*>(&MI[2 * kT + 16 * u + 4 * g]);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          st = mfma(qa[s], kr[t][s], st);  // S[q 16u + 4g + r][key 16t + c]
+          dp = mfma(ga[s], vr[t][s], dp);  // dP
+        }
+        float pr[4], dsr[4];
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          const f32x2 Lp = {L4[r], L4[r + 1]}, Ip = {I4[r], I4[r + 1]}, Dp = {D4[r], D4[r + 1]};
+          f32x2 d = (f32x2{st[r], st[r + 1]} - Lp) * f32x2{kLog2e, kLog2e};
+          const f32x2 pp = f32x2{exp2_(d.x), exp2_(d.y)} * Ip;
+          const f32x2 ds = pp * (f32x2{dp[r], dp[r + 1]} - Dp);
+          pr[r] = pp.x;
+          pr[r + 1] = pp.y;
+          dsr[r] = ds.x;
+          dsr[r + 1] = ds.y;
+        }
+        if (ragged_keys && kb0 + 16 * t + c >= M) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dsr[r] = 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dva[t][u & 1] = mfma(gtv[r], pr[r], dva[t][u & 1]);   // dV^T[d][key] += dO^T[d][q] P[q][key]
+          dka[t][u & 1] = mfma(qtv[r], dsr[r], dka[t][u & 1]);  // dK^T[d][key] += Q^T[d][q] dS[q][key]
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ts[(4 * g + r) * kSTs + 16 * t + c] = dsr[r];
+      }
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f32x4 dsT = *reinterpret_cast<const f32x4*>(&ts[c * kSTs + 16 * t + 4 * g]);  // dS[q c][key 16t + 4g + r]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc = mfma(kt[t][r], dsT[r], acc);  // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+      }
+      dqa[u] = acc;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) *reinterpret_cast<f32x4*>(&rq[(16 * u + c) * kSRq + 4 * g]) = dqa[u];
+    __syncthreads();  // every wave's partial in RQ; QA .. MI no longer read
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + 512 * i, d = e >> 6, qq = e & 63;
+      float sum = RQ[qq * kSRq + d];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) sum += RQ[w * kT * kSRq + qq * kSRq + d];
+      if (q0 + qq < N) dst[qoff + (int64_t)d * HN + q0 + qq] = sum * osc;
+    }
+    if (q0 + kT < N) stage(q0 + kT);
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int kj = kb0 + 16 * t + c;
+    if (kj < M) {
+      const f32x4 dks = dka[t][0] + dka[t][1], dvs = dva[t][0] + dva[t][1];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t a = (int64_t)h * M + (int64_t)(4 * g + r) * H * M + kj;
+        dk[(int64_t)b * sbdk + a] = dks[r] * kScale;
+        dv[(int64_t)b * sbdv + a] = dvs[r];
+      }
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
-    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
-    const float* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
-    int H, int N, int M, int64_t sbk, int64_t sbv, int64_t sbdk, int64_t sbdv, float* __restrict__ dk,
-    float* __restrict__ dv) {
-  __shared__ float Qs[kD * kSR];
-  __shared__ float Os[kD * kSR];  // dO as [d][q]
-  __shared__ float QT[kT * kSC];
-  __shared__ float OT[kT * kSC];  // dO as [q][d]
-  __shared__ __attribute__((aligned(16))) float Ls[kT];
-  __shared__ __attribute__((aligned(16))) float Is[kT];
-  __shared__ __attribute__((aligned(16))) float Ds[kT];
-  const int3 xb = pk::xcd_block3();  // a (crop, head)'s key blocks share one XCD's L2 (Q / dO)
-  const int h = xb.y, b = xb.z;
-  const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
-  const int kj = xb.x * kT + pk::wave_id() * 16 + c;
-  const float* qb = q + ((int64_t)b * kD * H + h) * N;
-  const float* gb = dout + ((int64_t)b * kD * H + h) * N;
-  const float2* lb = reinterpret_cast<const float2*>(lse) + ((int64_t)b * H + h) * N;
-  const float* db = delta + ((int64_t)b * H + h) * N;
-  float kr[4], vr[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int64_t a = (int64_t)h * M + (int64_t)(4 * s + g) * H * M + (kj < M ? kj : 0);
-    const float kv = k[(int64_t)b * sbk + a], vv = v[(int64_t)b * sbv + a];  // unconditional
-    kr[s] = kj < M ? kv * kScale : 0.f;
-    vr[s] = kj < M ? vv : 0.f;
-  }
-  // the per-query (m, 1 / sum) and delta of a 64-query tile, one query per thread < kT, loaded a
-  // tile ahead like Q / dO (a load issued between the loop's barriers exposed a full memory
-  // latency per tile)
-  auto load_md = [&](int q0, float2& msv, float& dv) {
-    const int qq = q0 + (int)threadIdx.x;
-    const int qc = qq < N ? qq : 0;
-    const float2 m2 = lb[qc];
-    const float d1 = db[qc];
-    msv = qq < N ? m2 : make_float2(__builtin_huge_valf(), 0.f);  // exp2(-inf) = 0
-    dv = qq < N ? d1 : 0.f;
-  };
-  float2 msn = make_float2(0.f, 0.f);
-  float dn = 0.f;
-  if (threadIdx.x < kT) load_md(0, msn, dn);
-  // two independent chains (even / odd 16-query sub-tiles; accuracy, see the forward): four
-  // would cost this kernel its third wave per SIMD
-  f32x4 dka[2], dva[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) dka[t] = dva[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  Tile qt = load_tile(qb, H * N, N, 0), gt = load_tile(gb, H * N, N, 0);
-  for (int q0 = 0; q0 < N; q0 += kT) {
-    __syncthreads();
-    store_tile(qt, Qs, QT);
-    store_tile(gt, Os, OT);
-    if (threadIdx.x < kT) {
-      Ls[threadIdx.x] = msn.x;
-      Is[threadIdx.x] = msn.y;
-      Ds[threadIdx.x] = dn;
-    }
-    __syncthreads();
-    if (q0 + kT < N) {
-      qt = load_tile(qb, H * N, N, q0 + kT);
-      gt = load_tile(gb, H * N, N, q0 + kT);
-      if (threadIdx.x < kT) load_md(q0 + kT, msn, dn);
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        st = mfma(Qs[(4 * s + g) * kSR + 16 * t + c], kr[s], st);  // S[q][key]
-        dp = mfma(Os[(4 * s + g) * kSR + 16 * t + c], vr[s], dp);  // dP[q][key]
-      }
-      // per-query (m, 1 / sum, delta) of queries 16 t + 4 g .. + 3 as 16-B LDS reads; packed pairs
-      const float4 L4 = *reinterpret_cast<const float4*>(&Ls[16 * t + 4 * g]);
-      const float4 I4 = *reinterpret_cast<const float4*>(&Is[16 * t + 4 * g]);
-      const float4 D4 = *reinterpret_cast<const float4*>(&Ds[16 * t + 4 * g]);
-      float pr[4], dsr[4];
-#pragma unroll
-      for (int r = 0; r < 4; r += 2) {
-        const f32x2 Lp = r == 0 ? f32x2{L4.x, L4.y} : f32x2{L4.z, L4.w};
-        const f32x2 Ip = r == 0 ? f32x2{I4.x, I4.y} : f32x2{I4.z, I4.w};
-        const f32x2 Dp = r == 0 ? f32x2{D4.x, D4.y} : f32x2{D4.z, D4.w};
-        f32x2 d = (f32x2{st[r], st[r + 1]} - Lp) * f32x2{kLog2e, kLog2e};
-        const f32x2 pp = f32x2{exp2_(d.x), exp2_(d.y)} * Ip;
-        const f32x2 ds = pp * (f32x2{dp[r], dp[r + 1]} - Dp);
-        pr[r] = pp.x;
-        pr[r + 1] = pp.y;
-        dsr[r] = ds.x;
-        dsr[r + 1] = ds.y;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qq = 16 * t + 4 * g + r;
-        dva[t & 1] = mfma(OT[qq * kSC + c], pr[r], dva[t & 1]);   // dV^T[d][key] += dO^T[d][q] P[q][key]
-        dka[t & 1] = mfma(QT[qq * kSC + c], dsr[r], dka[t & 1]);  // dK^T[d][key] += Q^T[d][q] dS[q][key]
-      }
-    }
-  }
-  const f32x4 dks = dka[0] + dka[1], dvs = dva[0] + dva[1];
-  if (kj < M) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t a = (int64_t)h * M + (int64_t)(4 * g + r) * H * M + kj;
-      dk[(int64_t)b * sbdk + a] = dks[r] * kScale;
-      dv[(int64_t)b * sbdv + a] = dvs[r];
-    }
+// dq = 0.25 (slot 0 + slot 1 + ... + slot P - 1), slots added in order; slot 0 is dq itself
+template <typename V>
+__global__ __launch_bounds__(256) void attn_bwd_dq_reduce_kernel(float* __restrict__ dq,
+                                                                 const float* __restrict__ part, int64_t n, int P) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    V s = reinterpret_cast<const V*>(dq)[i];
+    for (int p = 1; p < P; ++p) s += reinterpret_cast<const V*>(part)[(int64_t)(p - 1) * n + i];
+    reinterpret_cast<V*>(dq)[i] = s * kScale;
   }
 }
 
@@ -383,22 +408,36 @@ extern "C" int pk_attention_fwd(const float* q, const float* k, const float* v, 
   return PK_OK;
 }
 
+extern "C" int64_t pk_attention_bwd_work_size(int B, int D, int H, int N, int M) {
+  if (B <= 0 || H <= 0 || N <= 0 || M <= 0 || D != kD) return 0;
+  const int64_t P = (M + kKB - 1) / kKB;
+  return (P - 1) * (int64_t)B * kD * H * N * (int64_t)sizeof(float);
+}
+
 extern "C" int pk_attention_bwd(const float* q, const float* k, const float* v, const float* out,
                                 const float* dout, const float* lse, int B, int D, int H, int N,
-                                int M, int64_t sbk, int64_t sbv, float* delta, float* dq, float* dk, float* dv,
+                                int M, int64_t sbk, int64_t sbv, float* work, float* dq, float* dk, float* dv,
                                 int64_t sbdk, int64_t sbdv, void* stream) {
   PK_REQUIRE(B >= 0 && H > 0 && N >= 0 && M >= 0 && D == kD && sbk >= 0 && sbv >= 0 && sbdk >= 0 && sbdv >= 0);
   if (B == 0 || N == 0 || M == 0) return PK_OK;
-  PK_REQUIRE(q && k && v && out && dout && lse && delta && dq && dk && dv);
+  const int P = (M + kKB - 1) / kKB;
+  PK_REQUIRE(q && k && v && out && dout && lse && dq && dk && dv && (work || P == 1));
+  PK_REQUIRE((int64_t)P * B * H <= (int64_t)INT32_MAX && (int64_t)H * N <= (int64_t)INT32_MAX);
   hipStream_t s = pk::as_stream(stream);
   const int64_t dense = (int64_t)kD * H * M;
-  sbk = sbk ? sbk : dense;
-  sbv = sbv ? sbv : dense;
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((N + kT - 1) / kT, H, B), dim3(256), 0, s, q, k, v, out, dout,
-                     lse, H, N, M, sbk, sbv, delta, dq);
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(P, H, B), dim3(512), 0, s, q, k, v, out, dout, lse, H, N, M,
+                     sbk ? sbk : dense, sbv ? sbv : dense, sbdk ? sbdk : dense, sbdv ? sbdv : dense, dq, work, dk, dv);
   PK_CHECK_LAUNCH();
-  hipLaunchKernelGGL(attn_bwd_dkv_kernel, dim3((M + kT - 1) / kT, H, B), dim3(256), 0, s, q, k, v, dout, lse,
-                     delta, H, N, M, sbk, sbv, sbdk ? sbdk : dense, sbdv ? sbdv : dense, dk, dv);
-  PK_CHECK_LAUNCH();
+  if (P > 1) {
+    const int64_t n = (int64_t)B * kD * H * N;
+    if (n % 4 == 0 && (reinterpret_cast<uintptr_t>(dq) & 15) == 0 && (reinterpret_cast<uintptr_t>(work) & 15) == 0) {
+      const unsigned g = (unsigned)std::min<int64_t>((n / 4 + 255) / 256, 2048);
+      hipLaunchKernelGGL(attn_bwd_dq_reduce_kernel<f32x4>, dim3(g), dim3(256), 0, s, dq, work, n / 4, P);
+    } else {
+      const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 2048);
+      hipLaunchKernelGGL(attn_bwd_dq_reduce_kernel<float>, dim3(g), dim3(256), 0, s, dq, work, n, P);
+    }
+    PK_CHECK_LAUNCH();
+  }
   return PK_OK;
 }

@@ -728,10 +728,7 @@ __device__ __forceinline__ void lr_stage(const float* w, int Cout, int transw, f
   }
 }
 
-// VAR (development variants, pkdev_linear_rows_var): 0 production; 1 no MFMAs (acc = operand sums:
-// the load / store floor); 2 no stores unless the result is NaN (the load + MFMA floor); 3 no
-// scheduling barriers (the compiler may hoist every weight read)
-template <int Q, int TO, bool GEN, int VAR = 0>  // Cin = 16 Q, Cout <= 16 TO; GEN: mask / add / split / cf epilogue
+template <int Q, int TO, bool GEN>  // Cin = 16 Q, Cout <= 16 TO; GEN: mask / add / split / cf epilogue
 __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __restrict__ x, int64_t sx,
                                                               const float* __restrict__ w,
                                                               const float* __restrict__ bias, int64_t R, int Cin,
@@ -761,7 +758,7 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
     // operands): acc / wv / epilogue operands stay at TH tiles, so TO = 8 keeps 4 waves per SIMD
 #pragma unroll
     for (int hh = 0; hh < NH; ++hh) {
-    if (VAR != 3) __builtin_amdgcn_sched_barrier(0);  // one output group's registers live at a time
+    __builtin_amdgcn_sched_barrier(0);  // one output group's registers live at a time
     // D[point 4 g + r][out t * 16 + m]; the epilogue's operand loads (mask, add) for all
     // TH x 4 outputs are issued before this group's MFMAs (their latency hides behind them),
     // not one dependent load per store
@@ -815,10 +812,9 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int t = 0; t < TH; ++t) {
-            if (VAR == 1) acc[t][i] += cur[q][i] + wv[t][i];
-            else acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[q][i], wv[t][i], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[q][i], wv[t][i], acc[t], 0, 0, 0);
           }
-        if (VAR != 3) __builtin_amdgcn_sched_barrier(0);  // keep the weight reads per chunk (no hoisting of all Q x TH)
+        __builtin_amdgcn_sched_barrier(0);  // keep the weight reads per chunk (no hoisting of all Q x TH)
       }
     }
 #pragma unroll
@@ -827,7 +823,7 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t pr = tile * 16 + 4 * g + r;
-        if (pr < R && o < Cout && (VAR != 2 || acc[t][r] != acc[t][r])) {
+        if (pr < R && o < Cout) {
           float v = lin_act(e.relu, acc[t][r] + bv[hh * TH + t]);
           v = mk[t][r] <= 0.f ? 0.f : v;  // relu_mask
           v += ad[t][r];  // 0 without add / past add_cols
@@ -847,143 +843,6 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
     tile = tn;
 #pragma unroll
     for (int q = 0; q < Q; ++q) cur[q] = nxt[q];
-  }
-}
-
-// Rows layout, LDS-staged full-line variant (the production rows path). Round 3's PMC passes
-// (profiles/r03_lin_pmc_summary.txt) and the no-MFMA / no-store variants (r03_lin_var.txt) showed
-// linear_fwd_rows_kernel bound by its memory access shapes, not the MFMA: fragment-shaped x loads
-// (16 rows x 64 B per instruction) and 4-B scalar stores. Here:
-//   * each wave stages its 16-row x tile with LANE-LINEAR 16-B loads (64 lanes cover whole 128-B
-//     lines of consecutive rows) into a wave-private LDS tile (XOR-swizzled 16-B chunks: the
-//     fragment reads are conflict-free), the next tile's loads in flight (registers) while the
-//     current tile's MFMAs run;
-//   * the MFMA operands are swapped (A = weight, B = points): D holds 4 CONSECUTIVE outputs of one
-//     point per lane, so the results, the mask and the residual move as 16-B vectors;
-//   * tiles are walked grid-stride by a persistent grid (2 blocks of 4 waves per CU).
-// Same epilogue semantics as linear_fwd_rows_kernel (LinEpi); Cout % 4 == 0 for the vector paths.
-template <int Q, int TO, bool GEN>
-__global__ __launch_bounds__(256, 2) void linear_rows_lds_kernel(const float* __restrict__ x, int64_t sx,
-                                                                 const float* __restrict__ w,
-                                                                 const float* __restrict__ bias, int64_t R, int Cin,
-                                                                 int Cout, int transw, LinEpi e) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int CI = 16 * Q, ST = CI + 4;
-  constexpr int CH = CI / 4;               // 16-B chunks per point row
-  constexpr int SWZ = CH >= 16 ? 15 : CH - 1;
-  constexpr int PF = CH / 4;               // 16-B loads per lane per tile (16 rows x CH chunks / 64 lanes)
-  float* Ws = lds;                                           // [16 TO][ST]
-  const int wave = pk::wave_id(), lane = pk::lane_id(), m = lane & 15, g = lane >> 4;
-  f32x4* Xs = reinterpret_cast<f32x4*>(lds + 16 * TO * ST) + wave * (16 * CH);  // this wave's [16][CH] tile
-  const int64_t T = (R + 15) >> 4, stride = (int64_t)gridDim.x * 4;
-  int64_t tile = (int64_t)blockIdx.x * 4 + wave;
-  f32x4 pf[PF];
-  auto load_tile = [&](int64_t tt) {  // lane-linear: flat chunk f = lane + 64 j -> (row f / CH, chunk f % CH)
-#pragma unroll
-    for (int j = 0; j < PF; ++j) {
-      const int f = lane + 64 * j, row = f / CH, c = f - row * CH;
-      const int64_t r = tt * 16 + row;
-      pf[j] = r < R ? *reinterpret_cast<const f32x4*>(x + r * sx + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-  auto write_tile = [&]() {
-#pragma unroll
-    for (int j = 0; j < PF; ++j) {
-      const int f = lane + 64 * j, row = f / CH, c = f - row * CH;
-      Xs[row * CH + (c ^ (row & SWZ))] = pf[j];
-    }
-  };
-  if (tile < T) load_tile(tile);
-  lr_stage<Q, TO>(w, Cout, transw, Ws, w, 1 << 30);
-  __syncthreads();
-  if (tile >= T) return;
-  write_tile();
-  int64_t tn = tile + stride;
-  if (tn < T) load_tile(tn);
-  constexpr int TH = TO < 4 ? TO : 4, NH = TO / TH;
-  const bool vec = (Cout & 3) == 0;
-  for (;;) {
-#pragma unroll
-    for (int hh = 0; hh < NH; ++hh) {
-      f32x4 acc[TH];
-#pragma unroll
-      for (int t = 0; t < TH; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const f32x4 xf = Xs[m * CH + ((4 * q + g) ^ (m & SWZ))];  // B: x[point m][16 q + 4 g + i]
-        f32x4 wv[TH];
-#pragma unroll
-        for (int t = 0; t < TH; ++t)
-          wv[t] = *reinterpret_cast<const f32x4*>(&Ws[((hh * TH + t) * 16 + m) * ST + 16 * q + 4 * g]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int t = 0; t < TH; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[t][i], xf[i], acc[t], 0, 0, 0);
-      }
-      // D[out (hh TH + t) 16 + 4 g + r][point m]: lane (m, g) holds 4 consecutive outputs of point m
-      const int64_t pr = tile * 16 + m;
-      if (pr < R) {
-#pragma unroll
-        for (int t = 0; t < TH; ++t) {
-          const int o0 = (hh * TH + t) * 16 + 4 * g;
-          if (o0 >= Cout) continue;
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int o = o0 + r;
-            const float bo = (bias != nullptr && o < Cout) ? bias[o] : 0.f;
-            v[r] = lin_act(e.relu, acc[t][r] + bo);
-          }
-          if (GEN && e.mask != nullptr) {
-            if (vec) {
-              const f32x4 mk = *reinterpret_cast<const f32x4*>(e.mask + pr * Cout + o0);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] = mk[r] <= 0.f ? 0.f : v[r];
-            } else {
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                if (o0 + r < Cout && e.mask[pr * Cout + o0 + r] <= 0.f) v[r] = 0.f;
-            }
-          }
-          if (GEN && e.add != nullptr && o0 < e.add_cols) {
-            if (o0 + 3 < e.add_cols && ((e.sa & 3) == 0)) {
-              const f32x4 ad = *reinterpret_cast<const f32x4*>(e.add + pr * e.sa + o0);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] += ad[r];
-            } else {
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                if (o0 + r < e.add_cols) v[r] += e.add[pr * e.sa + o0 + r];
-            }
-          }
-          if (GEN && e.store_cf) {
-            const int64_t b = pr / e.N, n = pr - b * e.N;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (o0 + r < Cout) e.y[b * e.sy + (int64_t)(o0 + r) * e.N + n] = v[r];
-          } else if (GEN && o0 >= e.split) {
-            float* dst = e.y2 + pr * e.sy2 + (o0 - e.split);
-            if (vec && (e.sy2 & 3) == 0) *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
-            else
-#pragma unroll
-              for (int r = 0; r < 4; ++r) if (o0 + r < Cout) dst[r] = v[r];
-          } else {
-            float* dst = e.y + pr * e.sy + o0;
-            if (vec && (e.sy & 3) == 0 && o0 + 3 < (GEN ? e.split : Cout)) *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
-            else
-#pragma unroll
-              for (int r = 0; r < 4; ++r) if (o0 + r < Cout) dst[r] = v[r];
-          }
-        }
-      }
-    }
-    if (tn >= T) break;
-    tile = tn;
-    // this wave's fragment reads of the finished tile precede these writes (in-order LDS per wave)
-    __builtin_amdgcn_sched_barrier(0);
-    write_tile();
-    tn = tile + stride;
-    if (tn < T) load_tile(tn);
   }
 }
 
@@ -1924,33 +1783,6 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
       PK_CHECK_LAUNCH();
       return PK_OK;
     }
-    // development switch (read once): PK_ROWS_LDS=1 takes the LDS-staged full-line kernel; measured
-    // within +-15 % of the fragment-load kernel shape by shape (profiles/r03_lin_bench_lds_vs_r2.txt),
-    // so round 2's kernel stays the default
-#ifdef PK_DEVBUILD
-    static const bool rows_lds = getenv("PK_ROWS_LDS") != nullptr;
-#else
-    constexpr bool rows_lds = false;
-#endif
-    if (rows_lds && Cin >= 32) {  // LDS-staged full-line kernel (linear_rows_lds_kernel)
-      auto pickl = [&](auto q, auto gen) {
-        constexpr int Qv = decltype(q)::value;
-        constexpr bool G = decltype(gen)::value;
-        return TO == 1 ? linear_rows_lds_kernel<Qv, 1, G>
-               : TO == 2 ? linear_rows_lds_kernel<Qv, 2, G>
-               : TO == 4 ? linear_rows_lds_kernel<Qv, 4, G> : linear_rows_lds_kernel<Qv, 8, G>;
-      };
-      auto pickql = [&](auto gen) {
-        return Cin == 32 ? pickl(std::integral_constant<int, 2>{}, gen)
-               : Cin == 64 ? pickl(std::integral_constant<int, 4>{}, gen) : pickl(std::integral_constant<int, 8>{}, gen);
-      };
-      auto kl = plain ? pickql(std::integral_constant<bool, false>{}) : pickql(std::integral_constant<bool, true>{});
-      const size_t ldsl = sizeof(float) * ((size_t)(16 * TO) * (Cin + 4) + 4 * (size_t)16 * Cin);
-      const unsigned bl = (unsigned)std::min<int64_t>((tiles + 3) / 4, (int64_t)(2 * kRowsPersistCUs));
-      hipLaunchKernelGGL(kl, dim3(bl), dim3(256), ldsl, st, x, sx, w, bias, R, Cin, Cout, transw, e);
-      PK_CHECK_LAUNCH();
-      return PK_OK;
-    }
     auto kern = plain ? pickq(std::integral_constant<bool, false>{}) : pickq(std::integral_constant<bool, true>{});
     const size_t lds = sizeof(float) * (size_t)(16 * TO) * (Cin + 4);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, st, x, sx, w, bias, R, Cin, Cout, transw, e);
@@ -2001,101 +1833,6 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
-
-// Weight-stationary rows kernel (development, pkdev_linear_rows_var var = 4 / 5): the wave's
-// whole weight fragment lives in VGPRs (lane (m, g): W[16 t + m][16 q + 4 g + i], TO x Q float4s),
-// copied once from the block's LDS stage, so the MFMA loop reads no LDS; tiles of 16 rows are
-// walked grid-stride with the next tile's operands in flight. WPS = minimum waves per SIMD.
-template <int Q, int TO, int WPS>
-__global__ __launch_bounds__(256, WPS) void linear_ws_rows_kernel(const float* __restrict__ x, int64_t sx,
-                                                                  const float* __restrict__ w,
-                                                                  const float* __restrict__ bias, int64_t R,
-                                                                  int Cout, float* __restrict__ y, int64_t sy) {
-  extern __shared__ float Ws[];
-  constexpr int CI = 16 * Q, ST = CI + 4;
-  const int lane = pk::lane_id(), m = lane & 15, g = lane >> 4;
-  const int64_t T = (R + 15) >> 4, stride = (int64_t)gridDim.x * 4;
-  int64_t tile = (int64_t)blockIdx.x * 4 + pk::wave_id();
-  f32x4 cur[Q], nxt[Q];
-  lr_load<Q>(x, sx, tile < T ? tile * 16 + m : R, R, g, cur);
-  lr_stage<Q, TO>(w, Cout, 0, Ws, w, 1 << 30);
-  __syncthreads();
-  if (tile >= T) return;
-  f32x4 wf[TO][Q];
-#pragma unroll
-  for (int t = 0; t < TO; ++t)
-#pragma unroll
-    for (int q = 0; q < Q; ++q) wf[t][q] = *reinterpret_cast<const f32x4*>(&Ws[(t * 16 + m) * ST + 16 * q + 4 * g]);
-  float bv[TO];
-#pragma unroll
-  for (int t = 0; t < TO; ++t) {
-    const int o = t * 16 + m;
-    bv[t] = (bias != nullptr && o < Cout) ? bias[o] : 0.f;
-  }
-  for (;;) {
-    const int64_t tn = tile + stride;
-    if (tn < T) lr_load<Q>(x, sx, tn * 16 + m, R, g, nxt);
-    f32x4 acc[TO];
-#pragma unroll
-    for (int t = 0; t < TO; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < Q; ++q)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int t = 0; t < TO; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[q][i], wf[t][q][i], acc[t], 0, 0, 0);
-#pragma unroll
-    for (int t = 0; t < TO; ++t) {
-      const int o = t * 16 + m;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t pr = tile * 16 + 4 * g + r;
-        if (pr < R && o < Cout) y[pr * sy + o] = fmaxf(acc[t][r] + bv[t], 0.f);
-      }
-    }
-    if (tn >= T) break;
-    tile = tn;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) cur[q] = nxt[q];
-  }
-}
-
-#ifdef PK_DEVBUILD
-// Development hook (not in include/posekern.h): the plain rows kernel (no epilogue operands) of
-// y = x W^T + b with Cin = 16 Q in {64, 128}, Cout = 64, in variant `var` (see the kernel), at
-// `blocks` workgroups (0: the production grid), for tools/lin_var.py.
-extern "C" int pkdev_linear_rows_var(const float* x, const float* w, const float* bias, int64_t R, int Cin,
-                                     float* y, int var, int blocks, void* stream) {
-  if (!(Cin == 64 || Cin == 128) || R <= 0 || var < 0 || var > 5) return PK_ERR_ARG;
-  LinEpi e{};
-  e.y = y;
-  e.sy = 64;
-  e.split = 64;
-  const int64_t tiles = (R + 15) / 16;
-  const unsigned nb = blocks > 0 ? (unsigned)blocks : (unsigned)std::min<int64_t>((tiles + 3) / 4, (int64_t)kRowsMaxBlocks);
-  const size_t lds = sizeof(float) * (size_t)64 * (Cin + 4);
-  hipStream_t st = pk::as_stream(stream);
-#define PK_VAR(QQ, V) hipLaunchKernelGGL((linear_fwd_rows_kernel<QQ, 4, false, V>), dim3(nb), dim3(256), lds, st, x, \
-                                         (int64_t)Cin, w, bias, R, Cin, 64, 0, e)
-#define PK_WS(QQ, W) hipLaunchKernelGGL((linear_ws_rows_kernel<QQ, 4, W>), dim3(nb), dim3(256), lds, st, x, (int64_t)Cin, \
-                                        w, bias, R, 64, y, (int64_t)64)
-  if (var >= 4) {  // weight-stationary: 2 (var 4) or 1 (var 5) waves per SIMD at least
-    if (Cin == 64) {
-      if (var == 4) PK_WS(4, 2); else PK_WS(4, 1);
-    } else {
-      if (var == 4) PK_WS(8, 2); else PK_WS(8, 1);
-    }
-  } else if (Cin == 64) {
-    if (var == 0) PK_VAR(4, 0); else if (var == 1) PK_VAR(4, 1); else if (var == 2) PK_VAR(4, 2); else PK_VAR(4, 3);
-  } else {
-    if (var == 0) PK_VAR(8, 0); else if (var == 1) PK_VAR(8, 1); else if (var == 2) PK_VAR(8, 2); else PK_VAR(8, 3);
-  }
-#undef PK_VAR
-#undef PK_WS
-  PK_CHECK_LAUNCH();
-  return PK_OK;
-}
-#endif  // PK_DEVBUILD
 
 extern "C" int pk_linear_fwd(const float* x, const float* w, const float* bias, int layout, int64_t R, int N,
                              int Cin, int Cout, int transw, int relu, const float* mask, float* y, void* stream) {

@@ -87,6 +87,7 @@ SIGNATURES = {
     "pk_resolvent_mask": [_P, _I, _P, _I, _I, _I, _F, _P, _P],
     "pk_linear_fwd": [_P, _P, _P, _I, _I64, _I, _I, _I, _I, _I, _P, _P, _P],
     "pk_feat_dist_work_size": [_I, _I, _I, _I, _I],
+    "pk_attention_bwd_work_size": [_I, _I, _I, _I, _I],
     "pk_feat_dist_topk": [_P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I64, _P, _P, _P],
     "pk_rigidity_filter_work_size": [_I, _I, _I],
     "pk_rigidity_filter": [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P],
@@ -125,7 +126,7 @@ SIGNATURES = {
 
 RESTYPES = {"pk_cgt_lstsq_work_size": _I64, "pk_linear_wgrad_grouped_work": _I64, "pk_ransac_work_size": _I64,
             "pk_feat_dist_work_size": _I64, "pk_fmap_head_work_len": _I64, "pk_icp_work_size": _I64,
-            "pk_rigidity_filter_work_size": _I64}  # everything else returns an int status
+            "pk_rigidity_filter_work_size": _I64, "pk_attention_bwd_work_size": _I64}  # everything else returns an int status
 
 _lib: Optional[ctypes.CDLL] = None
 _dev_lib: Optional[ctypes.CDLL] = None

@@ -97,13 +97,13 @@ class _AttnPropFn(torch.autograd.Function):
         # attention backward: dk / dv into one stacked buffer
         dq = torch.empty((B, C, N), dtype=torch.float32, device=dev)
         dkv = torch.empty((B, 2 * C, M), dtype=torch.float32, device=dev)
-        delta = torch.empty((B, heads, N), dtype=torch.float32, device=dev)
+        work = ops.attention_bwd_work(B, D, heads, N, M, dev)
         import ctypes
         off = 4 * C * M
         call("pk_attention_bwd", ptr(q), ptr(kv), ctypes.c_void_p(kv.data_ptr() + off), ptr(a), ptr(da), ptr(lse),
-             B, D, heads, N, M, 2 * C * M, 2 * C * M, ptr(delta), ptr(dq), ptr(dkv),
+             B, D, heads, N, M, 2 * C * M, 2 * C * M, ptr(work), ptr(dq), ptr(dkv),
              ctypes.c_void_p(dkv.data_ptr() + off), 2 * C * M, 2 * C * M, _lib.stream(dev),
-             work=("mfma", 5 * 2 * N * M * D * B * heads))  # algorithmic: S, dP, dV, dK, dQ (7 executed)
+             work=("mfma", 5 * 2 * N * M * D * B * heads))  # S, dP, dV, dK, dQ: each contraction once
         # d desc = Pq^T dq + dout (residual) + dhc[:, :C] (concatenation), one launch
         dx = torch.empty((B, C, N), dtype=torch.float32, device=dev)
         ops.linear_ex(dq, f(wq), None, 1, B * N, N, C, C, y=dx, transw=True, add=dout, add_cols=C,

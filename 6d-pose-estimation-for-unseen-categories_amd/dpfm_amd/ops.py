@@ -430,12 +430,18 @@ class _Attention(torch.autograd.Function):
         dout = dout.contiguous()
         B, D, H, N = q.shape
         M = k.shape[3]
-        delta = torch.empty((B, H, N), dtype=torch.float32, device=q.device)
+        work = attention_bwd_work(B, D, H, N, M, q.device)
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         call("pk_attention_bwd", ptr(q), ptr(k), ptr(v), ptr(out), ptr(dout), ptr(lse), B, D, H, N, M, 0, 0,
-             ptr(delta), ptr(dq), ptr(dk), ptr(dv), 0, 0, _lib.stream(q.device),
-             work=("mfma", 5 * 2 * N * M * D * B * H))  # algorithmic S, dP, dV, dK, dQ (executed: S, dP, dQ | S, dP, dV, dK)
+             ptr(work), ptr(dq), ptr(dk), ptr(dv), 0, 0, _lib.stream(q.device),
+             work=("mfma", 5 * 2 * N * M * D * B * H))  # S, dP, dV, dK, dQ: each contraction once
         return dq, dk, dv
+
+
+def attention_bwd_work(B: int, D: int, H: int, N: int, M: int, device) -> Optional[torch.Tensor]:
+    """Scratch of pk_attention_bwd (the dQ partials of key blocks 1 ..; None when one block covers M)."""
+    nbytes = int(_lib.lib().pk_attention_bwd_work_size(B, D, H, N, M))
+    return torch.empty((nbytes // 4,), dtype=torch.float32, device=device) if nbytes > 0 else None
 
 
 def attention(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor) -> torch.Tensor:

@@ -156,15 +156,19 @@ int pk_fmap_solve_backward(const float* AAt, const float* BAt, const float* D, f
  *   q f32 [B, D, H, N], k / v f32 [B, D, H, M] (heads interleaved as the reference's
  *   view(B, dim, heads, N) of a [B, D*H, N] projection), out f32 [B, D, H, N],
  *   lse f32 [B, H, N, 2]: per query the row max m and 1 / sum of exp(s - m) (for the backward).
- * Backward: dout like out; delta f32 [B, H, N] scratch; dq like q, dk / dv like k.
+ * Backward: dout like out; dq like q, dk / dv like k; work: pk_attention_bwd_work_size bytes of
+ * scratch (any contents, nothing kept across calls; NULL when that size is 0, i.e. M <= 256). One
+ * pass over (query tile, 256-key block) forms S, dP, dV, dK and a dQ partial per key block; the
+ * partials (slot 0 in dq, the others in work) are added in key-block order by a second launch.
  * sbk / sbv (sbdk / sbdv): batch strides in elements of k / v (dk / dv); 0 = dense D H M. A
  * batch stride of 2 D H M reads (writes) the key and value halves of one [B, 2 D H, M] buffer:
  * the stacked key / value projection (one launch for modeling/dpfm.py:63-67's proj[1], proj[2]). */
 int pk_attention_fwd(const float* q, const float* k, const float* v, int B, int D, int H, int N,
                      int M, int64_t sbk, int64_t sbv, float* out, float* lse, void* stream);
+int64_t pk_attention_bwd_work_size(int B, int D, int H, int N, int M);
 int pk_attention_bwd(const float* q, const float* k, const float* v, const float* out,
                      const float* dout, const float* lse, int B, int D, int H, int N, int M,
-                     int64_t sbk, int64_t sbv, float* delta, float* dq, float* dk, float* dv, int64_t sbdk,
+                     int64_t sbk, int64_t sbv, float* work, float* dq, float* dk, float* dv, int64_t sbdk,
                      int64_t sbdv, void* stream);
 
 /* Weight/bias gradients of the per-point layers of H7/H8 (DiffusionNet Linear layers,

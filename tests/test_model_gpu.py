@@ -148,7 +148,7 @@ def test_linear_wgrad_grouped(device):
         assert (db - eb).abs().le(1e-5 * bw.max() + 1e-30).all(), k
 
 
-@pytest.mark.parametrize("N,M", [(300, 200), (1024, 1024), (64, 1), (17, 130)])
+@pytest.mark.parametrize("N,M", [(300, 200), (1024, 1024), (64, 1), (17, 130), (77, 600), (5, 513), (130, 257)])
 def test_attention_fwd_bwd(device, N, M):
     """H8 fused attention vs modeling/dpfm.py:29-37 evaluated in fp64 (truth) and fp32:
     out and dq/dk/dv within 3x the fp32 reference's own error + 1e-6 of scale."""
@@ -174,6 +174,33 @@ def test_attention_fwd_bwd(device, N, M):
     for name, t, r, d in zip(["out", "dq", "dk", "dv"], *res):
         e_ref, e_mine = (r - t).abs().max().item(), (d - t).abs().max().item()
         assert e_mine <= 3 * e_ref + 1e-6 * (1 + scale), (name, e_mine, e_ref)
+
+
+def test_attention_bwd_deterministic_any_scratch(device):
+    """The one-pass backward's dQ partials (one per 256-key block, slot 0 = dq) are added in
+    slot order: two calls agree bit for bit, whatever the work buffer held before."""
+    import ctypes
+    from dpfm_amd import _lib, ops
+    g = torch.Generator().manual_seed(11)
+    B, D, H, N, M = 2, 16, 2, 333, 1100
+    q, k, v, go = (torch.randn(B, D, H, n, generator=g).to(device) for n in (N, M, M, N))
+    out = torch.empty_like(q)
+    lse = torch.empty((B, H, N, 2), device=device)
+    P = _lib.ptr
+    _lib.call("pk_attention_fwd", P(q), P(k), P(v), B, D, H, N, M, 0, 0, P(out), P(lse), _lib.stream(device))
+    res = []
+    for fill in (0.0, float("nan"), 1e30):
+        work = ops.attention_bwd_work(B, D, H, N, M, device)
+        assert work is not None and work.numel() == 4 * B * D * H * N  # 5 key blocks: 4 extra slots
+        work.fill_(fill)
+        dq, dk, dv = torch.full_like(q, fill), torch.empty_like(k), torch.empty_like(v)
+        _lib.call("pk_attention_bwd", P(q), P(k), P(v), P(out), P(go), P(lse), B, D, H, N, M, 0, 0, P(work),
+                  P(dq), P(dk), P(dv), 0, 0, _lib.stream(device))
+        res.append((dq.cpu(), dk.cpu(), dv.cpu()))
+    for r in res[1:]:
+        for a, b in zip(res[0], r):
+            assert torch.equal(a, b)
+    assert ops.attention_bwd_work(B, D, H, N, 256, device) is None  # one key block: no scratch
 
 
 @pytest.mark.parametrize("N1,N2", [(256, 256), (300, 200)])

@@ -9,7 +9,7 @@ timeout -s KILL 90 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- pyth
 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o run -- python tools/attn_pmc.py 10 > $OUT/sq.log 2>&1
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python tools/attn_pmc.py 10 > $OUT/fetch.log 2>&1
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python tools/attn_pmc.py 10 > $OUT/write.log 2>&1
-for kn in attn_fwd attn_bwd_dq attn_bwd_dkv; do
+for kn in attn_fwd attn_bwd_kernel attn_bwd_dq_reduce; do
   for p in sq fetch write; do python tools/pmc_pick.py $OUT/$p $kn "$kn/$p" >> $OUT/summary.txt; done
 done
 cat $OUT/timing.txt $OUT/summary.txt

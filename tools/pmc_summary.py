@@ -30,7 +30,7 @@ FAMILIES = {
     "pk_backproject": ["bp_count_kernel", "bp_write_kernel"],
     "pk_spectral_diffusion": ["spec_reduce_kernel", "spec_combine_kernel", "spec_expand_kernel"],
     "pk_attention_fwd": ["attn_fwd_kernel"],
-    "pk_attention_bwd": ["attn_bwd_dq_kernel", "attn_bwd_dkv_kernel"],
+    "pk_attention_bwd": ["attn_bwd_kernel", "attn_bwd_dq_reduce_kernel"],
     "pk_linear_wgrad": ["wgrad_v2_kernel", "wgrad_partial_kernel", "wgrad_reduce_kernel"],
     "pk_feat_dist_topk": ["fd_wide_kernel", "fd_prep_kernel", "fd_main_direct_kernel", "fd_main_kernel"],
     "pk_cgt_lstsq": ["cgt_count_kernel", "cgt_partial_kernel", "cgt_reduce_kernel", "cgt_solve_kernel"],
