@@ -16,8 +16,9 @@ from dpfm_amd.dataset.object import CropFormation  # noqa: E402
 from dpfm_amd.models.dpfm import DPFMNet  # noqa: E402
 from dpfm_amd.pipeline import TrainStep, make_frame_batch  # noqa: E402
 
-WATCH = ("copy_", "add", "add_", "cat", "fill_", "zero_", "mean", "sum", "clone", "contiguous", "mul", "sub",
-         "where", "any", "gt", "lt", "ne", "eq", "index", "stack", "neg", "div")
+WATCH = ("copy_", "add", "add_", "cat", "fill_", "zero_", "zeros", "zeros_like", "new_zeros", "mean", "sum", "clone",
+         "contiguous", "mul", "sub", "where", "any", "gt", "lt", "ne", "eq", "index", "stack", "neg", "div",
+         "slice_backward", "select_backward", "threshold_backward", "split_backward", "_to_copy", "fill")
 log = collections.Counter()
 
 
@@ -26,6 +27,7 @@ class Mode(TorchDispatchMode):
         name = func.__name__.split(".")[0]
         if name in WATCH:
             t = [a for a in args if isinstance(a, torch.Tensor)]
+            t += [x for a in args if isinstance(a, (list, tuple)) for x in a if isinstance(x, torch.Tensor)]
             if t and t[0].is_cuda:
                 fr = [f for f in traceback.extract_stack() if "dpfm_amd" in f.filename]
                 where = f"{os.path.basename(fr[-1].filename)}:{fr[-1].lineno} {fr[-1].name}" if fr else "engine"
