@@ -820,6 +820,23 @@ __global__ __launch_bounds__(256) void linear_fwd_rows_kernel(const float* __res
 #pragma unroll
     for (int t = 0; t < TH; ++t) {
       const int o = (hh * TH + t) * 16 + m;
+      const int64_t p0 = tile * 16 + 4 * g;
+      if (GEN && e.store_cf && ((e.N | e.sy) & 3) == 0 && (reinterpret_cast<uintptr_t>(e.y) & 15) == 0 && p0 + 3 < R) {
+        // channels-first store: the lane's 4 consecutive points of channel o (one item, as
+        // N % 4 == 0) as one 16-B store
+        if (o < Cout) {
+          f32x4 v4;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = lin_act(e.relu, acc[t][r] + bv[hh * TH + t]);
+            v = mk[t][r] <= 0.f ? 0.f : v;
+            v4[r] = v + ad[t][r];
+          }
+          const int64_t b = p0 / e.N, n = p0 - b * e.N;
+          *reinterpret_cast<f32x4*>(e.y + b * e.sy + (int64_t)o * e.N + n) = v4;
+        }
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t pr = tile * 16 + 4 * g + r;

@@ -117,6 +117,7 @@ SIGNATURES = {
     "pk_dpotrs": [_P, _P, _I, _I, _I, _P],
     "pk_tufted_laplacian": [_P, _I64, _P, _I64, _D, _I64, _P, _P, _P, _P, _P, _P],
     "pk_teaser_solve": [_P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P],  # host pointers
+    "pk_transpose_cf_rows": [_P, _P, _I, _I, _I, _I, _I64, _P, _P],
     "pk_copy_rows": [_P, _I64, _P, _I64, _I64, _I64, _P],
     "pk_device_cu_count": [_P],
     "pk_stream_create_cu_mask": [_P, _I, _P],

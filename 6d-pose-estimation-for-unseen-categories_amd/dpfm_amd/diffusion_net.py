@@ -213,9 +213,13 @@ class _EncoderFn(torch.autograd.Function):
             dD = torch.empty_like(dy)
             # dcat = d1 W1: columns 0..63 (+ the residual's dy) -> dX, 64..127 -> dD
             ops.linear_ex(d1, w1, None, 0, R, 0, 64, 128, y=dX, transw=True, y2=dD, split=64, add=dy, add_cols=64)
-            gt = torch.empty((64,), dtype=torch.float32, device=dev)
+            # dL/dt straight into t's persistent .grad when the grouped weight gradient owns it (no
+            # autograd accumulation launch)
+            from . import layers
+            gbuf = layers._SIDE.direct(t) if layers._SIDE is not None else None
+            gt = gbuf if gbuf is not None else torch.empty((64,), dtype=torch.float32, device=dev)
             ops.spectral_raw(dD, 64, mass, evals, evecs, t, True, 1, dX, 64, saved=raws[i], gt=gt, accumulate=True)
-            grads[k] = gt
+            grads[k] = None if gbuf is not None else gt
             dy = dX
         grads[0], grads[1] = _wgrad(fcat, dy, w0, b0)
         dfcat = None

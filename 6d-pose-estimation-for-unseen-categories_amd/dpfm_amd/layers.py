@@ -61,6 +61,15 @@ class GroupedWgrad:
     def owns(self, p) -> bool:
         return id(p) in self.bufs
 
+    def direct(self, p):
+        """p's persistent .grad buffer for a kernel that writes p's whole gradient itself (e.g. the
+        diffusion-time gradient of pk_spectral_diffusion's backward), on p's first use in this
+        backward; None otherwise (the caller then returns the gradient to autograd)."""
+        if id(p) not in self.bufs or id(p) in self.seen:
+            return None
+        self.seen.add(id(p))
+        return self.bufs[id(p)]
+
     def launch(self, x, dy, weight, bias, channels_first: bool):
         acc = id(weight) in self.seen
         self.seen.add(id(weight))
@@ -202,6 +211,59 @@ class _PointwiseResidualFn(torch.autograd.Function):
                 dw, db = ops.linear_wgrad(x, dy, channels_first=True, want_bias=ctx.has_bias)
                 dw = dw.view(weight.shape)
         return dx, dw, db, dy if ctx.needs_input_grad[3] else None, None
+
+
+class _LinearPairCfFn(torch.autograd.Function):
+    """The refinement's first_lin on both shapes at once (modeling/dpfm.py:98, desc =
+    first_lin(x).transpose(1, 2) for x = features_x, features_y) from the encoder's concatenated
+    rows-layout features [2B, N, Cin]: one launch writing channels-first [2B, Cout, N]
+    (pk_linear_ex store_cf), returned as the two shapes' desc [B0, Cout, N] and [2B - B0, Cout, N]
+    — no transpose copies and no concatenation of the two features' gradients. Backward: the two
+    channels-first gradients into one rows-layout dy (pk_transpose_cf_rows), the features'
+    gradient in one launch, the weight gradient recorded once for both shapes."""
+
+    @staticmethod
+    def forward(ctx, feat, weight, bias, B0):
+        B2, N, Cin = feat.shape
+        w2 = weight.view(weight.shape[0], -1)
+        Cout = w2.shape[0]
+        y = torch.empty((B2, Cout, N), dtype=feat.dtype, device=feat.device)
+        ops.linear_ex(feat, w2, bias, 0, B2 * N, N, Cin, Cout, y=y, store_cf=True)
+        ctx.B0, ctx.param, ctx.bias, ctx.has_bias = B0, weight, bias, bias is not None
+        ctx.save_for_backward(feat, weight)
+        return y[:B0], y[B0:]
+
+    @staticmethod
+    def backward(ctx, g0, g1):
+        feat, weight = ctx.saved_tensors
+        w2 = weight.view(weight.shape[0], -1)
+        B2, N, Cin = feat.shape
+        Cout = w2.shape[0]
+        g0, g1 = g0.contiguous(), g1.contiguous()
+        dyr = torch.empty((B2, N, Cout), dtype=feat.dtype, device=feat.device)
+        ops._lib.call("pk_transpose_cf_rows", ops._lib.ptr(g0), ops._lib.ptr(g1), ctx.B0, B2, Cout, N, Cout * N,
+                      ops._lib.ptr(dyr), ops._lib.stream(feat.device), work=("hbm", 8 * B2 * N * Cout))
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = ops.linear_fwd(dyr, w2, None, channels_first=False, transw=True)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            if _side_owns(ctx.param, ctx.bias):
+                _SIDE.launch(feat, dyr, ctx.param, ctx.bias, channels_first=False)
+            else:
+                dw, db = ops.linear_wgrad(feat, dyr, channels_first=False, want_bias=ctx.has_bias)
+                dw = dw.view(weight.shape)
+        return dx, dw, db, None
+
+
+def linear_pair_cf(layer: "Linear", feat: torch.Tensor, B0: int):
+    """(desc0, desc1) = layer(feat[:B0]).transpose(1, 2), layer(feat[B0:]).transpose(1, 2) as two
+    contiguous channels-first tensors (_LinearPairCfFn), or None outside its shapes."""
+    Cin, Cout = layer.in_features, layer.out_features
+    if not (feat.is_cuda and feat.dim() == 3 and feat.is_contiguous() and feat.dtype == torch.float32
+            and feat.shape[-1] == Cin and 0 < B0 < feat.shape[0] and Cin in (16, 32, 64, 128)
+            and Cout % 16 == 0 and Cout <= 128 and not layer.relu_out and not layer.sigmoid_out):
+        return None
+    return _LinearPairCfFn.apply(feat, layer.weight, layer.bias, B0)
 
 
 def pointwise_residual(layer: "Conv1d", x: torch.Tensor, res: torch.Tensor) -> torch.Tensor:

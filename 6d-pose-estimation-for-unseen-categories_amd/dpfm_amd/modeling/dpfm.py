@@ -123,11 +123,27 @@ class CrossAttentionRefinementNet(nn.Module):
         self.last_lin = Linear(gnn_dim + additional_dim, n_in + additional_dim)
         self.overlap_predictor = OverlapPredictorNet(overlap_feat_dim=overlap_feat_dim)
 
-    def forward(self, coords0, coords1, features_x, features_y, batch=None):
-        desc0, desc1 = self.first_lin(features_x).transpose(1, 2), self.first_lin(features_y).transpose(1, 2)
+    def forward(self, coords0, coords1, features_x, features_y, batch=None, features_xy=None):
+        """features_xy (optional): the encoder's [2B, N, C] output of which features_x / features_y
+        are the two halves; first_lin then runs once on it (layers.linear_pair_cf)."""
+        pair = None
+        if features_xy is not None and FUSED_ATTN_PROP:
+            from ..layers import linear_pair_cf
+            pair = linear_pair_cf(self.first_lin, features_xy, features_x.shape[0])
+        if pair is not None:
+            desc0, desc1 = pair
+        else:
+            desc0, desc1 = self.first_lin(features_x).transpose(1, 2), self.first_lin(features_y).transpose(1, 2)
         for layer in self.layers:
-            desc0 = layer.forward_residual(desc0, desc1)
-            desc1 = layer.forward_residual(desc1, desc0)  # with the updated desc0 (:101-103)
+            pair = None
+            if FUSED_ATTN_PROP:  # both calls of the layer as one node (attnprop.attn_prop_pair)
+                from ..attnprop import attn_prop_pair
+                pair = attn_prop_pair(layer, desc0, desc1)
+            if pair is not None:
+                desc0, desc1 = pair
+            else:
+                desc0 = layer.forward_residual(desc0, desc1)
+                desc1 = layer.forward_residual(desc1, desc0)  # with the updated desc0 (:101-103)
         ax = self.last_lin(desc0.transpose(1, 2))
         ay = self.last_lin(desc1.transpose(1, 2))
         if ax.shape[-1] == self.n_in:  # "normal" attention: the whole width (no slice, whose

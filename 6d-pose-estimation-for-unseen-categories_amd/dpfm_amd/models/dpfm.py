@@ -71,13 +71,16 @@ class DPFMNet(nn.Module):
                 fcat = torch.cat(((verts1 - 110) / 50, (verts2 - 110) / 50), 0)
             feat = self.feature_extractor(fcat, _cat0(mass1, mass2),
                                           evals=_cat0(evals1, evals2), evecs=_cat0(evecs1, evecs2))
-            feat1, feat2 = torch.chunk(feat, 2, 0)  # backward: one concat (slices: two zero-fills + copies)
+            feat1, feat2 = torch.chunk(feat, 2, 0)  # (the refiner's first_lin reads feat whole)
+            fused_cat = True
         else:
+            fused_cat = False
             features1, features2 = (verts1 - 110) / 50, (verts2 - 110) / 50  # models/dpfm.py:53
             feat1 = self.feature_extractor(features1, mass1, evals=evals1, evecs=evecs1)
             feat2 = self.feature_extractor(features2, mass2, evals=evals2, evecs=evecs2)
 
-        ref_feat1, ref_feat2, overlap_score12, overlap_score21 = self.feat_refiner(verts1, verts2, feat1, feat2, batch)
+        ref_feat1, ref_feat2, overlap_score12, overlap_score21 = self.feat_refiner(
+            verts1, verts2, feat1, feat2, batch, features_xy=feat if fused_cat else None)
         use_feat1, use_feat2 = (ref_feat1, ref_feat2) if self.robust else (feat1, feat2)
 
         k = self.n_fmap

@@ -24,6 +24,7 @@ from .dataset.object import CropFormation, Crops, FrameBatch
 from .dataset.synthetic import cad_points, lbo_operators, make_frame
 from .models.dpfm import DPFMNet
 from .layers import Conv1d, GroupedWgrad, Linear
+from .diffusion_net import LearnedTimeDiffusion
 from .utils.loss import DPFMLoss
 
 
@@ -255,6 +256,8 @@ class TrainStep:
         self.side = None
         if grouped and dev.type == "cuda":
             lin = [p for m in model.modules() if isinstance(m, (Linear, Conv1d)) for p in m.parameters(recurse=False)]
+            # gradients the kernels write whole into .grad (GroupedWgrad.direct): the diffusion times
+            lin += [m.diffusion_time for m in model.modules() if isinstance(m, LearnedTimeDiffusion)]
             self.side = GroupedWgrad(lin, bufs={id(p): v for p, v in zip(self.params, self.gviews)}
                                      if self.flat_grads else None)
 

@@ -639,6 +639,13 @@ int pk_tufted_laplacian(const double* pts, int64_t n, const int32_t* tri, int64_
 int pk_copy_rows(float* dst, int64_t ld_dst, const float* src, int64_t ld_src, int64_t rows, int64_t n,
                  void* stream);
 
+/* pk_transpose_cf_rows: channels-first items [C, N] (item b at src0 + b sb for b < B0, else at
+ * src1 + (b - B0) sb) into one rows-layout buffer dst [B, N, C]; C in {16, 32, 64, 128}. The
+ * refinement's first_lin backward (modeling/dpfm.py:98, desc = first_lin(x).transpose(1, 2)): the
+ * two shapes' channels-first gradients of desc as the rows-layout dy of the layer. */
+int pk_transpose_cf_rows(const float* src0, const float* src1, int B0, int B, int C, int N, int64_t sb,
+                         float* dst, void* stream);
+
 /* Runtime helpers of the pipelined executors (host only; no reference counterpart: the reference
  * overlaps crop formation with training through DataLoader worker PROCESSES, train.py /
  * dataset/object.py:117-274; here the overlap is two HIP streams on one device).

@@ -738,16 +738,23 @@ def test_fused_fmap_head_matches_module_path(device, N1, N2, monkeypatch):
     assert (g1 - g0).norm().item() <= 1e-3 * g0.norm().item()
 
 
-@pytest.mark.parametrize("N1,N2", [(512, 384), (300, 203)])  # (300, 203): ragged channels-first tiles
-def test_fused_attn_prop_matches_module_path(device, monkeypatch, N1, N2):
-    """attnprop._AttnPropFn (one autograd node per AttentionalPropagation call + residual:
-    stacked key/value projection, attention on the stacked buffer, merge into the
-    concatenation, the input gradients of desc summed in one epilogue) vs the module path
-    (modeling/dpfm.py:45-82, 101-103): refinement outputs and every parameter gradient within
-    fp32 rounding (1e-5 of each tensor's scale; the summation orders differ)."""
+@pytest.mark.parametrize("N1,N2,layers,pair", [(512, 384, 1, True), (300, 203, 1, True), (300, 203, 2, True),
+                                                (512, 384, 2, False)])  # (300, 203): ragged channels-first tiles
+def test_fused_attn_prop_matches_module_path(device, monkeypatch, N1, N2, layers, pair):
+    """attnprop._AttnPropPairFn (both calls of a refinement layer as one autograd node: the two
+    gradients that meet at desc0' and at desc1 summed in launch epilogues) and _AttnPropFn (one
+    node per AttentionalPropagation call + residual: stacked key/value projection, attention on
+    the stacked buffer, merge into the concatenation, the input gradients of desc summed in one
+    epilogue) vs the module path (modeling/dpfm.py:45-82, 101-103): refinement outputs and every
+    parameter gradient within fp32 rounding (1e-5 of each tensor's scale; the summation orders
+    differ)."""
+    from dpfm_amd import attnprop
     from dpfm_amd.modeling import dpfm as MD
+    if not pair:
+        monkeypatch.setattr(attnprop, "attn_prop_pair", lambda *a: None)
     torch.manual_seed(3)
-    net = MD.CrossAttentionRefinementNet(n_in=32, num_head=2, gnn_dim=32, n_layers=1, cross_sampling_ratio=1).to(device)
+    net = MD.CrossAttentionRefinementNet(n_in=32, num_head=2, gnn_dim=32, n_layers=layers,
+                                         cross_sampling_ratio=1).to(device)
     g = torch.Generator().manual_seed(4)
     fx = torch.randn(4, N1, 32, generator=g).to(device)
     fy = torch.randn(4, N2, 32, generator=g).to(device)
@@ -769,3 +776,28 @@ def test_fused_attn_prop_matches_module_path(device, monkeypatch, N1, N2):
     for n, r, o in zip(names, ref, got):
         scale = max(float(r.abs().max()), 1e-30)
         assert (o - r).abs().max().item() <= 1e-5 * scale + floor, (n, (o - r).abs().max().item(), scale, floor)
+
+def test_first_lin_pair_matches_per_shape(device):
+    """layers._LinearPairCfFn (the refinement's first_lin once over the encoder's concatenated
+    [2B, N, C] features, channels-first output, the two gradients transposed into one rows dy by
+    pk_transpose_cf_rows) vs first_lin per shape (modeling/dpfm.py:98): refinement outputs, the
+    features' gradient and every parameter gradient within fp32 rounding."""
+    from dpfm_amd.modeling import dpfm as MD
+    torch.manual_seed(5)
+    net = MD.CrossAttentionRefinementNet(n_in=32, num_head=2, gnn_dim=32, n_layers=2, cross_sampling_ratio=1).to(device)
+    g = torch.Generator().manual_seed(6)
+    feat = torch.randn(6, 300, 32, generator=g).to(device)
+
+    def run(pair):
+        net.zero_grad()
+        f = feat.clone().requires_grad_(True)
+        fx, fy = torch.chunk(f, 2, 0)
+        rx, ry, ox, oy = net(None, None, fx, fy, features_xy=f if pair else None)
+        (rx.square().sum() + 0.5 * ry.square().sum() + ox.sum() + 2 * oy.sum()).backward()
+        return [t.detach().clone() for t in (rx, ry, ox, oy, f.grad)] + [p.grad.detach().clone() for p in net.parameters()]
+
+    ref, got = run(False), run(True)
+    floor = 1e-6 * float(torch.cat([r.reshape(-1) for r in ref[5:]]).norm())
+    for i, (r, o) in enumerate(zip(ref, got)):
+        scale = max(float(r.abs().max()), 1e-30)
+        assert (o - r).abs().max().item() <= 1e-5 * scale + floor, (i, (o - r).abs().max().item(), scale)
