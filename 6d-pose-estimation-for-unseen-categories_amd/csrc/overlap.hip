@@ -40,6 +40,7 @@ struct OvhShape {
   float* g;
   float* dh;
   float* dx;
+  const float* dadd;
 };
 struct OvhArgs {
   OvhShape sh[2];
@@ -227,8 +228,16 @@ __global__ __launch_bounds__(256) void ovh_bwd_kernel(const OvhArgs a, const flo
   for (int c = 0; c < kC; ++c) yd += nv[c] * dn[c];
   const bool clamped = !(nr > 1e-12f);
   if (ok) {
+    // dadd: another consumer's gradient of x (x's storage), added to this one (the sum autograd
+    // would form where the two consumers meet)
+    float ad[kC];
 #pragma unroll
-    for (int c = 0; c < kC; ++c) S.dx[off + c * S.sc] = clamped ? dn[c] / 1e-12f : (dn[c] - nv[c] * yd) / nr;
+    for (int c = 0; c < kC; ++c) ad[c] = S.dadd != nullptr ? S.dadd[off + c * S.sc] : 0.f;
+#pragma unroll
+    for (int c = 0; c < kC; ++c) {
+      const float v = clamped ? dn[c] / 1e-12f : (dn[c] - nv[c] * yd) / nr;
+      S.dx[off + c * S.sc] = S.dadd != nullptr ? v + ad[c] : v;
+    }
   }
 }
 
@@ -251,6 +260,7 @@ OvhArgs ovh_args(const pk_overlap_head_args* a) {
     S.g = a->g[s];
     S.dh = a->dh[s];
     S.dx = a->dx[s];
+    S.dadd = a->dadd[s];
   }
   k.B = a->B;
   return k;

@@ -43,7 +43,7 @@ class OverlapHeadArgs(ctypes.Structure):
     _fields_ = [("x", _P * 2), ("strides", (_I64 * 3) * 2), ("N", ctypes.c_int32 * 2), ("B", ctypes.c_int32),
                 ("pad", ctypes.c_int32), ("w0", _P), ("b0", _P), ("w1", _P), ("b1", _P), ("n", _P * 2),
                 ("nrm", _P * 2), ("nrows", _P * 2), ("h", _P * 2), ("s", _P * 2), ("ds", _P * 2), ("dnr", _P * 2),
-                ("g", _P * 2), ("dh", _P * 2), ("dx", _P * 2)]
+                ("g", _P * 2), ("dh", _P * 2), ("dx", _P * 2), ("dadd", _P * 2)]
 
 
 # name -> argtypes, mirroring include/posekern.h one for one.

@@ -144,6 +144,22 @@ class CrossAttentionRefinementNet(nn.Module):
             else:
                 desc0 = layer.forward_residual(desc0, desc1)
                 desc1 = layer.forward_residual(desc1, desc0)  # with the updated desc0 (:101-103)
+        op = self.overlap_predictor
+        ll = self.last_lin
+        if (FUSED_ATTN_PROP and self.attention_type == "normal" and ll.out_features == self.n_in
+                and not ll.relu_out and not ll.sigmoid_out and desc0.is_contiguous() and desc1.is_contiguous()
+                and desc0.dim() == 3 and ll.in_features == desc0.shape[1] == desc1.shape[1]
+                and ll.in_features in (16, 32, 64, 128)
+                and op._fusable(desc0.transpose(1, 2)[..., :self.n_in], desc1.transpose(1, 2)[..., :self.n_in])):
+            # last_lin + the overlap head as one node: the refined features' two consumers (the
+            # overlap head here, the fmap head downstream) meet in one launch's epilogue
+            l0, l2 = op.overlap_score_net[0], op.overlap_score_net[2]
+            y0, y1, sx, sy, rx, ry = ops.lastlin_overlap_head(desc0, desc1, ll.weight, ll.bias, l0.weight, l0.bias,
+                                                              l2.weight, l2.bias)
+            ref_x, ref_y = y0.transpose(1, 2), y1.transpose(1, 2)
+            if rx is not None:
+                ref_x._pk_nrows, ref_y._pk_nrows = rx, ry
+            return ref_x, ref_y, sx.squeeze(0), sy.squeeze(0)
         ax = self.last_lin(desc0.transpose(1, 2))
         ay = self.last_lin(desc1.transpose(1, 2))
         if ax.shape[-1] == self.n_in:  # "normal" attention: the whole width (no slice, whose

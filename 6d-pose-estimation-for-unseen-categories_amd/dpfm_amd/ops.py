@@ -716,6 +716,78 @@ def _ovh_args(fx, fy, w0, b0, w1, b1):
     return a, ctypes
 
 
+def _ovh_forward(fx, fy, w0, b0, w1, b1, want: bool):
+    """pk_overlap_head_fwd on both shapes: ((s_x, s_y, nrows_x, nrows_y), the saved tensors)."""
+    B = fx.shape[0]
+    dev = fx.device
+    a, ctypes = _ovh_args(fx, fy, w0, b0, w1, b1)
+    outs = []
+    for s, f in enumerate((fx, fy)):
+        N = f.shape[1]
+        n = torch.empty_strided(f.shape, f.stride(), dtype=torch.float32, device=dev)
+        nrm = torch.empty((B * N,), dtype=torch.float32, device=dev)
+        nrows = torch.empty((B, N, 32), dtype=torch.float32, device=dev) if want else None
+        h = torch.empty((B, N, 32), dtype=torch.float32, device=dev) if want else None
+        sc = torch.empty((B, N), dtype=torch.float32, device=dev)
+        a.n[s], a.nrm[s] = n.data_ptr(), nrm.data_ptr()
+        a.nrows[s] = nrows.data_ptr() if nrows is not None else None
+        a.h[s] = h.data_ptr() if h is not None else None
+        a.s[s] = sc.data_ptr()
+        outs.append((n, nrm, nrows, h, sc))
+    call("pk_overlap_head_fwd", ctypes.addressof(a), _lib.stream(dev),
+         work=("hbm", 4 * B * (fx.shape[1] + fy.shape[1]) * (32 + 32 + (64 if want else 0) + 2)))
+    (nx, nrx, rx, hx, sx), (ny, nry, ry, hy, sy) = outs
+    return (sx, sy, rx, ry), (nx, nrx, rx, hx, sx, ny, nry, ry, hy, sy)
+
+
+def _ovh_backward(saved, params, dsx, dsy, drx, dry, dadd=(None, None)):
+    """pk_overlap_head_bwd on both shapes: (d f_x, d f_y (+ dadd, another consumer's gradient of
+    the features, added in the launch), the four weight gradients (None where the grouped launch
+    takes them))."""
+    from . import layers
+    nx, nrx, rx, hx, sx, ny, nry, ry, hy, sy = saved
+    w0, b0, w1, b1 = params
+    dev = nx.device
+    a, ctypes = _ovh_args(nx, ny, w0, b0, w1, b1)
+    B = nx.shape[0]
+    res = []
+    for s, (n, nrm, rows, h, sc, ds, dr, da) in enumerate(((nx, nrx, rx, hx, sx, dsx, drx, dadd[0]),
+                                                           (ny, nry, ry, hy, sy, dsy, dry, dadd[1]))):
+        N = n.shape[1]
+        ds = torch.zeros((B, N), dtype=torch.float32, device=dev) if ds is None else ds.contiguous()
+        dr = dr.contiguous() if dr is not None else None
+        g = torch.empty((B, N, 1), dtype=torch.float32, device=dev)
+        dh = torch.empty((B, N, 32), dtype=torch.float32, device=dev)
+        dx = torch.empty_strided(n.shape, n.stride(), dtype=torch.float32, device=dev)
+        if da is not None and da.stride() != n.stride():
+            da = torch.empty_strided(n.shape, n.stride(), dtype=torch.float32, device=dev).copy_(da)
+        a.n[s], a.nrm[s], a.h[s], a.s[s] = n.data_ptr(), nrm.data_ptr(), h.data_ptr(), sc.data_ptr()
+        a.ds[s], a.dnr[s] = ds.data_ptr(), (dr.data_ptr() if dr is not None else None)
+        a.g[s], a.dh[s], a.dx[s] = g.data_ptr(), dh.data_ptr(), dx.data_ptr()
+        a.dadd[s] = da.data_ptr() if da is not None else None
+        res.append((rows, h, g, dh, dx, ds, dr, da))
+    call("pk_overlap_head_bwd", ctypes.addressof(a), _lib.stream(dev),
+         work=("hbm", 4 * B * (nx.shape[1] + ny.shape[1]) * (32 * 5 + 4) +
+               sum(4 * d.numel() for d in dadd if d is not None)))
+    gw0 = gb0 = gw1 = gb1 = None
+    side0 = layers._side_owns(w0, b0)
+    side1 = layers._side_owns(w1, b1)
+    for rows, h, g, dh, _, _, _, _ in res:
+        if side1:
+            layers._SIDE.launch(h, g, w1, b1, channels_first=False)
+        else:
+            dw, db = linear_wgrad(h, g, channels_first=False, want_bias=True)
+            gw1 = dw.view(w1.shape) if gw1 is None else gw1 + dw.view(w1.shape)
+            gb1 = db if gb1 is None else gb1 + db
+        if side0:
+            layers._SIDE.launch(rows, dh, w0, b0, channels_first=False)
+        else:
+            dw, db = linear_wgrad(rows, dh, channels_first=False, want_bias=True)
+            gw0 = dw.view(w0.shape) if gw0 is None else gw0 + dw.view(w0.shape)
+            gb0 = db if gb0 is None else gb0 + db
+    return res[0][4], res[1][4], gw0, gb0, gw1, gb1
+
+
 class _OverlapHeadFn(torch.autograd.Function):
     """OverlapPredictorNet (modeling/dpfm.py:125-145) for both shapes as one autograd node:
     F.normalize -> Linear(32, 32) + ReLU -> Linear(32, 1) + Sigmoid in one launch per direction
@@ -725,71 +797,73 @@ class _OverlapHeadFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, fx, fy, w0, b0, w1, b1):
-        B = fx.shape[0]
-        dev = fx.device
-        a, ctypes = _ovh_args(fx, fy, w0, b0, w1, b1)
-        want = any(ctx.needs_input_grad)  # (grad mode is off inside forward)
-        outs = []
-        for s, f in enumerate((fx, fy)):
-            N = f.shape[1]
-            n = torch.empty_strided(f.shape, f.stride(), dtype=torch.float32, device=dev)
-            nrm = torch.empty((B * N,), dtype=torch.float32, device=dev)
-            nrows = torch.empty((B, N, 32), dtype=torch.float32, device=dev) if want else None
-            h = torch.empty((B, N, 32), dtype=torch.float32, device=dev) if want else None
-            sc = torch.empty((B, N), dtype=torch.float32, device=dev)
-            a.n[s], a.nrm[s] = n.data_ptr(), nrm.data_ptr()
-            a.nrows[s] = nrows.data_ptr() if nrows is not None else None
-            a.h[s] = h.data_ptr() if h is not None else None
-            a.s[s] = sc.data_ptr()
-            outs.append((n, nrm, nrows, h, sc))
-        call("pk_overlap_head_fwd", ctypes.addressof(a), _lib.stream(dev),
-             work=("hbm", 4 * B * (fx.shape[1] + fy.shape[1]) * (32 + 32 + (64 if want else 0) + 2)))
+        outs, saved = _ovh_forward(fx, fy, w0, b0, w1, b1, any(ctx.needs_input_grad))
         ctx.params = (w0, b0, w1, b1)
-        ctx.shapes = (tuple(fx.shape), tuple(fx.stride()), tuple(fy.shape), tuple(fy.stride()))
-        (nx, nrx, rx, hx, sx), (ny, nry, ry, hy, sy) = outs
-        ctx.save_for_backward(nx, nrx, rx, hx, sx, ny, nry, ry, hy, sy)
-        return sx, sy, rx, ry
+        ctx.save_for_backward(*saved)
+        return outs
 
     @staticmethod
     def backward(ctx, dsx, dsy, drx, dry):
+        return _ovh_backward(ctx.saved_tensors, ctx.params, dsx, dsy, drx, dry)
+
+
+class _LastLinOverlapFn(torch.autograd.Function):
+    """The refinement's last_lin on both shapes (modeling/dpfm.py:111-112, desc.transpose(1, 2)
+    read in place: channels-first in and out) and the overlap head on its outputs (:125-145) as
+    one node, so the two consumers of the refined features — the overlap head and the fmap head
+    (models/dpfm.py:80-90) — meet inside it: the fmap head's gradient enters
+    pk_overlap_head_bwd's dadd and the features' total gradient leaves that launch (no autograd
+    accumulation kernel), then last_lin's input gradient and grouped weight gradient."""
+
+    @staticmethod
+    def forward(ctx, d0, d1, wl, bl, w0, b0, w1, b1):
+        w2 = wl.view(wl.shape[0], -1)
+        Co, Ci = w2.shape
+        ys = []
+        for d in (d0, d1):
+            B, _, N = d.shape
+            y = torch.empty((B, Co, N), dtype=torch.float32, device=d.device)
+            linear_ex(d, w2, bl, 1, B * N, N, Ci, Co, y=y)
+            ys.append(y)
+        fx, fy = ys[0].transpose(1, 2), ys[1].transpose(1, 2)
+        want = any(ctx.needs_input_grad)
+        (sx, sy, rx, ry), saved = _ovh_forward(fx, fy, w0, b0, w1, b1, want)
+        ctx.params = (w0, b0, w1, b1)
+        ctx.lin = (wl, bl)
+        ctx.save_for_backward(d0, d1, wl, *saved)
+        return ys[0], ys[1], sx, sy, rx, ry
+
+    @staticmethod
+    def backward(ctx, gy0, gy1, dsx, dsy, drx, dry):
         from . import layers
-        nx, nrx, rx, hx, sx, ny, nry, ry, hy, sy = ctx.saved_tensors
-        w0, b0, w1, b1 = ctx.params
-        dev = nx.device
-        a, ctypes = _ovh_args(nx, ny, w0, b0, w1, b1)
-        B = nx.shape[0]
-        res = []
-        for s, (n, nrm, rows, h, sc, ds, dr) in enumerate(((nx, nrx, rx, hx, sx, dsx, drx),
-                                                           (ny, nry, ry, hy, sy, dsy, dry))):
-            N = n.shape[1]
-            ds = torch.zeros((B, N), dtype=torch.float32, device=dev) if ds is None else ds.contiguous()
-            dr = dr.contiguous() if dr is not None else None
-            g = torch.empty((B, N, 1), dtype=torch.float32, device=dev)
-            dh = torch.empty((B, N, 32), dtype=torch.float32, device=dev)
-            dx = torch.empty_strided(n.shape, n.stride(), dtype=torch.float32, device=dev)
-            a.n[s], a.nrm[s], a.h[s], a.s[s] = n.data_ptr(), nrm.data_ptr(), h.data_ptr(), sc.data_ptr()
-            a.ds[s], a.dnr[s] = ds.data_ptr(), (dr.data_ptr() if dr is not None else None)
-            a.g[s], a.dh[s], a.dx[s] = g.data_ptr(), dh.data_ptr(), dx.data_ptr()
-            res.append((rows, h, g, dh, dx, ds, dr))
-        call("pk_overlap_head_bwd", ctypes.addressof(a), _lib.stream(dev),
-             work=("hbm", 4 * B * (nx.shape[1] + ny.shape[1]) * (32 * 5 + 4)))
-        gw0 = gb0 = gw1 = gb1 = None
-        side0 = layers._side_owns(w0, b0)
-        side1 = layers._side_owns(w1, b1)
-        for rows, h, g, dh, _, _, _ in res:
-            if side1:
-                layers._SIDE.launch(h, g, w1, b1, channels_first=False)
+        sv = ctx.saved_tensors
+        d0, d1, wl = sv[:3]
+        wl_p, bl = ctx.lin
+        w2 = wl.view(wl.shape[0], -1)
+        Co, Ci = w2.shape
+        dadd = tuple(None if g is None else g.transpose(1, 2) for g in (gy0, gy1))
+        dfx, dfy, gw0, gb0, gw1, gb1 = _ovh_backward(sv[3:], ctx.params, dsx, dsy, drx, dry, dadd=dadd)
+        dd, gwl, gbl = [None, None], None, None
+        # shape 1 first: the order autograd ran the two last_lin calls' backward in
+        for s, (d, df) in reversed(list(enumerate(((d0, dfx), (d1, dfy))))):
+            B, _, N = d.shape
+            dy = df.transpose(1, 2)  # [B, Co, N] contiguous (the channels-first storage of y)
+            if ctx.needs_input_grad[s]:
+                dd[s] = torch.empty_like(d)
+                linear_ex(dy, w2, None, 1, B * N, N, Co, Ci, y=dd[s], transw=True)
+            if layers._side_owns(wl_p, bl):
+                layers._SIDE.launch(d, dy, wl_p, bl, channels_first=True)
             else:
-                dw, db = linear_wgrad(h, g, channels_first=False, want_bias=True)
-                gw1 = dw.view(w1.shape) if gw1 is None else gw1 + dw.view(w1.shape)
-                gb1 = db if gb1 is None else gb1 + db
-            if side0:
-                layers._SIDE.launch(rows, dh, w0, b0, channels_first=False)
-            else:
-                dw, db = linear_wgrad(rows, dh, channels_first=False, want_bias=True)
-                gw0 = dw.view(w0.shape) if gw0 is None else gw0 + dw.view(w0.shape)
-                gb0 = db if gb0 is None else gb0 + db
-        return res[0][4], res[1][4], gw0, gb0, gw1, gb1
+                dw, db = linear_wgrad(d, dy, channels_first=True, want_bias=bl is not None)
+                gwl = dw.view(wl.shape) if gwl is None else gwl + dw.view(wl.shape)
+                gbl = db if gbl is None else (gbl + db if db is not None else gbl)
+        return dd[0], dd[1], gwl, gbl, gw0, gb0, gw1, gb1
+
+
+def lastlin_overlap_head(d0: torch.Tensor, d1: torch.Tensor, wl, bl, w0, b0, w1, b1):
+    """(y0, y1 [B, 32, N] channels-first last_lin outputs, s_x, s_y, nrows_x, nrows_y): the
+    refinement's last_lin + overlap head node (_LastLinOverlapFn)."""
+    return _LastLinOverlapFn.apply(d0, d1, wl, bl, w0.contiguous(), b0.contiguous(), w1.contiguous(), b1.contiguous())
 
 
 def overlap_head(fx: torch.Tensor, fy: torch.Tensor, w0, b0, w1, b1):

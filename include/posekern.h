@@ -263,7 +263,9 @@ int pk_l2_normalize_bwd(const float* y, const float* dy, const float* nrm, const
  * Backward reads n, nrm, h, s and ds[s] [B N] (d loss / d score), dnr[s] (may be NULL: a
  * second gradient on the rows copy of n, the NCE term's), writes g[s] [B N] (d loss / d the
  * last layer's pre-activation), dh[s] [B N, 32] (d loss / d the first layer's
- * pre-activation, ReLU applied) and dx[s] (x's storage). */
+ * pre-activation, ReLU applied) and dx[s] (x's storage); dadd[s] (may be NULL; x's storage): a
+ * gradient of x from another consumer, added to dx[s] (the features' second consumer, the fmap
+ * head, models/dpfm.py:80-90). */
 typedef struct pk_overlap_head_args {
   const float* x[2];
   int64_t strides[2][3];
@@ -283,6 +285,7 @@ typedef struct pk_overlap_head_args {
   float* g[2];
   float* dh[2];
   float* dx[2];
+  const float* dadd[2];
 } pk_overlap_head_args;
 int pk_overlap_head_fwd(const pk_overlap_head_args* a, void* stream);
 int pk_overlap_head_bwd(const pk_overlap_head_args* a, void* stream);
