@@ -468,8 +468,15 @@ __global__ __launch_bounds__(256) void bq_pairs_kernel(
     const double* __restrict__ thr2v, int n1max, int n2max, int ld,
     const uint8_t* __restrict__ mask, const int32_t* __restrict__ rowcount,
     const int64_t* __restrict__ rowoff, int64_t* __restrict__ pairs, int64_t cap,
-    int8_t* __restrict__ ov12, int8_t* __restrict__ ov21) {
+    int8_t* __restrict__ ov12, int8_t* __restrict__ ov21, const int64_t* __restrict__ count, int B,
+    int32_t* __restrict__ over) {
   const int b = blockIdx.y;
+  if (over != nullptr && blockIdx.x == 0 && b == 0) {  // the pass-1 totals are final: any above cap?
+    int o = 0;
+    for (int k = threadIdx.x; k < B; k += 256) o |= count[k] > cap;
+    o = __syncthreads_or(o);
+    if (threadIdx.x == 0) over[0] = o;
+  }
   const int i = blockIdx.x * 4 + pk::wave_id();
   const int64_t c0 = cad_off[b], p0 = pc_off[b];
   const int n1 = (int)(cad_off[b + 1] - c0);
@@ -583,7 +590,7 @@ extern "C" int pk_ball_query_pairs(const double* cad, const int64_t* cad_off, co
                                    int n2max, const uint8_t* mask, int ld,
                                    const int32_t* rowcount, int64_t* rowoff, int64_t* pairs,
                                    int64_t cap, int64_t* count, int8_t* ov12, int8_t* ov21,
-                                   void* stream) {
+                                   int32_t* over, void* stream) {
   PK_REQUIRE(B >= 0 && n1max >= 0 && n2max >= 0 && cap >= 0);
   if (B == 0) return PK_OK;
   PK_REQUIRE(cad && cad_off && pc && pc_off && thr2 && rowcount && rowoff && count);
@@ -596,13 +603,14 @@ extern "C" int pk_ball_query_pairs(const double* cad, const int64_t* cad_off, co
   }
   if (n1max == 0) {
     hipError_t e = pk::zero_async(count, sizeof(int64_t) * B, s);
+    if (e == hipSuccess && over != nullptr) e = pk::zero_async(over, sizeof(int32_t), s);
     return e == hipSuccess ? PK_OK : (int)e;
   }
   hipLaunchKernelGGL(bq_scan_kernel, dim3(B), dim3(1024), 0, s, rowcount, n1max, rowoff, count);
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(bq_pairs_kernel, dim3((n1max + 3) / 4, B), dim3(256), 0, s, cad, cad_off, pc,
                      pc_off, thr2, n1max, n2max, ld, mask, rowcount, rowoff, pairs, cap, ov12,
-                     ov21);
+                     ov21, count, B, over);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

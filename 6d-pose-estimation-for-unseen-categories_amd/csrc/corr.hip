@@ -1146,6 +1146,27 @@ extern "C" int pk_inlier_ratio(const int64_t* pairs, int ldp, int layout, const 
   return PK_OK;
 }
 
+// mean of n floats: 256 lane sums over a stride, then one wave adds them in a fixed tree order
+__global__ __launch_bounds__(256) void mean_f32_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+  __shared__ float part[256];
+  float a = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 256) a += x[i];
+  part[threadIdx.x] = a;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = part[0] / (float)n;
+}
+
+extern "C" int pk_mean_f32(const float* x, int64_t n, float* out, void* stream) {
+  PK_REQUIRE(n >= 1 && x && out);
+  hipLaunchKernelGGL(mean_f32_kernel, dim3(1), dim3(256), 0, pk::as_stream(stream), x, n, out);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
 extern "C" int64_t pk_cgt_lstsq_work_size(int ldp, int V2max, int B) {
   const int64_t SH = ldp > 0 ? (ldp + kCgtRows - 1) / kCgtRows : 0;
   const int64_t SG = (V2max + kCgtRows - 1) / kCgtRows;

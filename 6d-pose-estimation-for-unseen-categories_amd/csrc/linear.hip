@@ -1401,16 +1401,14 @@ template <> struct LcVec<2> { using T = __attribute__((ext_vector_type(2))) floa
 template <> struct LcVec<4> { using T = f32x4; };
 
 template <int Q, int TO, int SUB>
-__global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restrict__ x, int64_t sx,
-                                                            const float* __restrict__ w,
-                                                            const float* __restrict__ bias, int64_t R, int N, int Cout,
-                                                            int transw, LinEpi e, int64_t tpc) {
+__device__ __forceinline__ void linear_cf_body(const float* __restrict__ x, int64_t sx, const float* __restrict__ w,
+                                               const float* __restrict__ bias, int64_t R, int N, int Cout, int transw,
+                                               const LinEpi& e, int64_t tpc, int64_t blk, float* Ws) {
   using V = typename LcVec<SUB>::T;
-  extern __shared__ float Ws[];
   constexpr int CI = 16 * Q, ST = CI + 4, P = 16 * SUB;
   const int lane = pk::lane_id(), m = lane & 15, g = lane >> 4;
   const int64_t T = (R / N) * tpc;
-  const int64_t tile = (int64_t)blockIdx.x * 4 + pk::wave_id();
+  const int64_t tile = blk * 4 + pk::wave_id();
   // the tile's operands are in flight while the weight is staged
   V xv[Q][4];
   int64_t bb = 0, n0 = 0;
@@ -1526,6 +1524,40 @@ __global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restr
         *reinterpret_cast<V*>(yb + (int64_t)o * N) = v;
       }
     }
+}
+
+template <int Q, int TO, int SUB>
+__global__ __launch_bounds__(256) void linear_fwd_cf_kernel(const float* __restrict__ x, int64_t sx,
+                                                            const float* __restrict__ w,
+                                                            const float* __restrict__ bias, int64_t R, int N, int Cout,
+                                                            int transw, LinEpi e, int64_t tpc) {
+  extern __shared__ float Ws[];
+  linear_cf_body<Q, TO, SUB>(x, sx, w, bias, R, N, Cout, transw, e, tpc, blockIdx.x, Ws);
+}
+
+// Two independent channels-first layers in one launch (pk_linear_ex2): blocks [0, nb0) run
+// problem 0, the rest problem 1 — the pair shares one launch's ramp and tail (the refinement's
+// q / stacked k-v projections, Pq^T / [Pk; Pv]^T, the two shapes' last_lin).
+struct CfProb {
+  const float* x;
+  int64_t sx;
+  const float* w;
+  const float* bias;
+  int64_t R;
+  int N, Cout, transw, pad;
+  int64_t tpc;
+  LinEpi e;
+};
+
+template <int Q0, int TO0, int Q1, int TO1, int SUB>
+__global__ __launch_bounds__(256) void linear_cf_pair_kernel(const CfProb p0, const CfProb p1, int nb0) {
+  extern __shared__ float Ws[];
+  if ((int)blockIdx.x < nb0)
+    linear_cf_body<Q0, TO0, SUB>(p0.x, p0.sx, p0.w, p0.bias, p0.R, p0.N, p0.Cout, p0.transw, p0.e, p0.tpc,
+                                 blockIdx.x, Ws);
+  else
+    linear_cf_body<Q1, TO1, SUB>(p1.x, p1.sx, p1.w, p1.bias, p1.R, p1.N, p1.Cout, p1.transw, p1.e, p1.tpc,
+                                 (int64_t)blockIdx.x - nb0, Ws);
 }
 
 // Thin layers (Cin <= 4 or Cout <= 4: DiffusionNet's first_lin 3 -> 64, the overlap head's
@@ -1668,6 +1700,123 @@ __global__ __launch_bounds__(256) void linear_thin_kernel(const float* __restric
 }
 
 }  // namespace
+
+// argument checks and the epilogue record of one pk_linear_ex call (PK_OK or an error status)
+static int lin_setup(const pk_linear_args* a, LinEpi& e, int64_t& sx_out) {
+  PK_REQUIRE(a != nullptr);
+  const int layout = a->layout, Cin = a->Cin, Cout = a->Cout, N = a->N;
+  const int64_t R = a->R;
+  PK_REQUIRE((layout == 0 || layout == 1) && R >= 0 && Cin > 0 && Cout > 0 && Cin <= kLfMaxC && Cout <= kLfMaxC);
+  PK_REQUIRE(layout == 0 || (N > 0 && R % N == 0));
+  PK_REQUIRE(a->act >= 0 && a->act <= 2);
+  if (R == 0) return PK_OK;
+  PK_REQUIRE(a->x && a->w && a->y);
+  const int split = a->y2 ? a->split : Cout;
+  PK_REQUIRE(split >= 1 && split <= Cout && (a->y2 == nullptr || (layout == 0 && !a->store_cf && split < Cout)));
+  PK_REQUIRE(a->store_cf == 0 || (layout == 0 && N > 0 && R % N == 0));
+  PK_REQUIRE(a->add == nullptr || (a->add_cols >= 1 && a->add_cols <= Cout));
+  sx_out = a->ldx ? a->ldx : (layout == 0 ? Cin : (int64_t)Cin * N);
+  e = LinEpi{};
+  e.y = a->y;
+  e.sy = a->ldy ? a->ldy : (layout == 0 && !a->store_cf ? split : (int64_t)Cout * N);
+  e.y2 = a->y2;
+  e.sy2 = a->ldy2 ? a->ldy2 : Cout - split;
+  e.split = split;
+  e.add = a->add;
+  e.sa = a->lda ? a->lda : (layout == 0 ? (int64_t)(a->add_cols > 0 ? a->add_cols : Cout) : (int64_t)Cout * N);
+  e.add_cols = a->add ? a->add_cols : 0;
+  e.mask = a->mask;
+  e.relu = a->act;
+  e.store_cf = a->store_cf;
+  e.N = N;
+  e.pre = a->pre;
+  e.pre_out = a->pre_out;
+  e.add2 = a->add2;
+  e.sa2 = a->lda2 ? a->lda2 : (int64_t)Cout * N;
+  e.w2 = a->w2;
+  e.bias2 = a->bias2;
+  e.wsplit = a->w2 ? a->wsplit : (1 << 30);
+  PK_REQUIRE((a->w2 == nullptr && a->add2 == nullptr && a->bias2 == nullptr) ||
+             (layout == 1 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128) &&
+              Cin > 4 && Cout > 4 && !a->store_cf && a->y2 == nullptr));
+  PK_REQUIRE(a->w2 == nullptr || (a->wsplit > 0 && a->wsplit < (a->transw ? Cin : Cout)));
+  PK_REQUIRE(a->bias2 == nullptr || (a->w2 != nullptr && !a->transw));
+  PK_REQUIRE((e.pre == nullptr && e.relu != 2) || ((Cin <= 4 || Cout <= 4) && Cin * Cout <= kThinMaxW));
+  return PK_OK;
+}
+
+// points per wave of the channels-first kernel: 16 SUB, as many as keep >= 1024 waves and <= 64
+// operand VGPRs; SUB-aligned items and strides for the vector loads / stores
+static int cf_sub(int64_t R, int N, int Cin, int64_t sx, const LinEpi& e) {
+  int sub = R >= 131072 ? 4 : R >= 32768 ? 2 : 1;
+  sub = std::min(sub, 256 / Cin);
+  while (sub > 1 && N % (16 * sub)) sub >>= 1;  // N % 16 != 0: SUB = 1 with ragged item tails
+  while (sub > 1 && ((sx % sub) || (e.sy % sub) || (e.add && (e.sa % sub)) || (e.add2 && (e.sa2 % sub)))) sub >>= 1;
+  return sub;
+}
+
+extern "C" int pk_linear_ex2(const pk_linear_args* a0, const pk_linear_args* a1, void* stream) {
+  PK_REQUIRE(a0 != nullptr && a1 != nullptr);
+  LinEpi e0, e1;
+  int64_t sx0 = 0, sx1 = 0;
+  int rc = lin_setup(a0, e0, sx0);
+  if (rc != PK_OK) return rc;
+  rc = lin_setup(a1, e1, sx1);
+  if (rc != PK_OK) return rc;
+  auto cf_ok = [](const pk_linear_args* a) {
+    return a->layout == 1 && a->R > 0 && (a->Cin == 32 || a->Cin == 64) && (a->Cout == 32 || a->Cout == 64) &&
+           a->y2 == nullptr && !a->store_cf && a->pre == nullptr && a->act <= 1;
+  };
+  const int sub0 = cf_ok(a0) ? cf_sub(a0->R, a0->N, a0->Cin, sx0, e0) : 0;
+  const int sub1 = cf_ok(a1) ? cf_sub(a1->R, a1->N, a1->Cin, sx1, e1) : 0;
+  if (sub0 == 0 || sub0 != sub1 || sub0 == 4) {  // not a pair this kernel takes: two launches
+    rc = pk_linear_ex(a0, stream);
+    return rc != PK_OK ? rc : pk_linear_ex(a1, stream);
+  }
+  auto prob = [](const pk_linear_args* a, const LinEpi& e, int64_t sx, int sub) {
+    CfProb p{};
+    p.x = a->x;
+    p.sx = sx;
+    p.w = a->w;
+    p.bias = a->bias;
+    p.R = a->R;
+    p.N = a->N;
+    p.Cout = a->Cout;
+    p.transw = a->transw;
+    p.tpc = (a->N + 16 * sub - 1) / (16 * sub);
+    p.e = e;
+    return p;
+  };
+  const CfProb p0 = prob(a0, e0, sx0, sub0), p1 = prob(a1, e1, sx1, sub1);
+  const int64_t nb0 = ((a0->R / a0->N) * p0.tpc + 3) / 4, nb1 = ((a1->R / a1->N) * p1.tpc + 3) / 4;
+  PK_REQUIRE(nb0 + nb1 <= (int64_t)INT32_MAX);
+  const int TO0 = a0->Cout / 16, TO1 = a1->Cout / 16;
+  const size_t lds = sizeof(float) * std::max((size_t)(16 * TO0) * (a0->Cin + 4), (size_t)(16 * TO1) * (a1->Cin + 4));
+  hipStream_t st = pk::as_stream(stream);
+  const dim3 grid((unsigned)(nb0 + nb1));
+#define PK_CFP(Q0, T0, Q1, T1, S) \
+  hipLaunchKernelGGL((linear_cf_pair_kernel<Q0, T0, Q1, T1, S>), grid, dim3(256), lds, st, p0, p1, (int)nb0)
+#define PK_CFP_S(Q0, T0, Q1, T1) \
+  do { if (sub0 == 2) PK_CFP(Q0, T0, Q1, T1, 2); else PK_CFP(Q0, T0, Q1, T1, 1); } while (0)
+#define PK_CFP_1(Q0, T0)                                                    \
+  do {                                                                      \
+    const int q1 = a1->Cin / 16;                                            \
+    if (q1 == 2 && TO1 == 2) PK_CFP_S(Q0, T0, 2, 2);                        \
+    else if (q1 == 2) PK_CFP_S(Q0, T0, 2, 4);                               \
+    else if (TO1 == 2) PK_CFP_S(Q0, T0, 4, 2);                              \
+    else PK_CFP_S(Q0, T0, 4, 4);                                            \
+  } while (0)
+  const int q0 = a0->Cin / 16;
+  if (q0 == 2 && TO0 == 2) PK_CFP_1(2, 2);
+  else if (q0 == 2) PK_CFP_1(2, 4);
+  else if (TO0 == 2) PK_CFP_1(4, 2);
+  else PK_CFP_1(4, 4);
+#undef PK_CFP_1
+#undef PK_CFP_S
+#undef PK_CFP
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
 
 extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
   PK_REQUIRE(a != nullptr);

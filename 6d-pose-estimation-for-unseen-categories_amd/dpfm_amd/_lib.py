@@ -50,7 +50,7 @@ class OverlapHeadArgs(ctypes.Structure):
 SIGNATURES = {
     "pk_fps": [_P, _P, _I, _I, _P, _P, _P, _I, _P],
     "pk_ball_query_mask": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P],
-    "pk_ball_query_pairs": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _I64, _P, _P, _P, _P],
+    "pk_ball_query_pairs": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _I64, _P, _P, _P, _P, _P],
     "pk_backproject": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P],
     "pk_sor": [_P, _P, _I, _I, _I, _D, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "pk_fps_npoint": [_P, _I, _I, _I, _U64, _I64, _P, _P, _P, _P],
@@ -60,6 +60,7 @@ SIGNATURES = {
     "pk_offsets_from_counts": [_P, _I, _P, _P],
     "pk_spectral_diffusion": [_P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _P],
     "pk_linear_ex": [_P, _P],
+    "pk_linear_ex2": [_P, _P, _P],
     "pk_fmap_head_work_len": [_I, _I, _I],
     "pk_fmap_head_fwd": [_P, _I, _P, _P, _P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _I, _F, _P, _P, _P, _P,
                          _P, _P, _I64, _P],
@@ -118,6 +119,7 @@ SIGNATURES = {
     "pk_tufted_laplacian": [_P, _I64, _P, _I64, _D, _I64, _P, _P, _P, _P, _P, _P],
     "pk_teaser_solve": [_P, _P, _P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P],  # host pointers
     "pk_transpose_cf_rows": [_P, _P, _I, _I, _I, _I, _I64, _P, _P],
+    "pk_mean_f32": [_P, _I64, _P, _P],
     "pk_copy_rows": [_P, _I64, _P, _I64, _I64, _I64, _P],
     "pk_device_cu_count": [_P],
     "pk_stream_create_cu_mask": [_P, _I, _P],

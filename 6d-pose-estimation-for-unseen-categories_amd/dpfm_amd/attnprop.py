@@ -42,9 +42,10 @@ def _prop_fwd(x, src, P, heads, eps):
     dev = x.device
     f = lambda w: w.view(w.shape[0], -1)  # noqa: E731  Conv1d [O, I, 1] -> [O, I]
     q = torch.empty((B, C, N), dtype=torch.float32, device=dev)
-    ops.linear_ex(x, f(wq), bq, 1, B * N, N, C, C, y=q)
     kv = torch.empty((B, 2 * C, M), dtype=torch.float32, device=dev)
-    ops.linear_ex(src, f(wk), bk, 1, B * M, M, C, 2 * C, y=kv, w2=f(wv), bias2=bv, wsplit=C)
+    # the query and the stacked key / value projections: independent, one launch (pk_linear_ex2)
+    ops.linear_ex2((x, f(wq), bq, 1, B * N, N, C, C, q), {},
+                   (src, f(wk), bk, 1, B * M, M, C, 2 * C, kv), dict(w2=f(wv), bias2=bv, wsplit=C))
     a = torch.empty((B, C, N), dtype=torch.float32, device=dev)
     lse = torch.empty((B, heads, N, 2), dtype=torch.float32, device=dev)
     import ctypes
@@ -102,18 +103,18 @@ def _prop_bwd(saved, P, heads, dout, dsrc_add=None):
          B, D, heads, N, M, 2 * C * M, 2 * C * M, ptr(work), ptr(dq), ptr(dkv),
          ctypes.c_void_p(dkv.data_ptr() + off), 2 * C * M, 2 * C * M, _lib.stream(dev),
          work=("mfma", 5 * 2 * N * M * D * B * heads))  # S, dP, dV, dK, dQ: each contraction once
-    # d desc = Pq^T dq + dout (residual) + dhc[:, :C] (concatenation), one launch
+    # d desc = Pq^T dq + dout (residual) + dhc[:, :C] (concatenation) and d src = Pk^T dk + Pv^T dv
+    # (+ the source's other gradient; the stacked weight's transpose, 64 -> 32): independent, one
+    # launch (pk_linear_ex2)
     dx = torch.empty((B, C, N), dtype=torch.float32, device=dev)
-    ops.linear_ex(dq, f(wq), None, 1, B * N, N, C, C, y=dx, transw=True, add=dout, add_cols=C,
-                  add2=dhc[:, :C], lda2=2 * C * N)
-    g_wq, g_bq = _wgrad(x, dq, wq, bq)
-    # d src = Pk^T dk + Pv^T dv (+ the source's other gradient): the stacked weight's transpose,
-    # one 64 -> 32 launch
     dsrc = torch.empty((B, C, M), dtype=torch.float32, device=dev)
     if dsrc_add is not None:
         dsrc_add = dsrc_add.contiguous()
-    ops.linear_ex(dkv, f(wk), None, 1, B * M, M, 2 * C, C, y=dsrc, transw=True, w2=f(wv), wsplit=C,
-                  add=dsrc_add, add_cols=C if dsrc_add is not None else 0)
+    ops.linear_ex2((dq, f(wq), None, 1, B * N, N, C, C, dx),
+                   dict(transw=True, add=dout, add_cols=C, add2=dhc[:, :C], lda2=2 * C * N),
+                   (dkv, f(wk), None, 1, B * M, M, 2 * C, C, dsrc),
+                   dict(transw=True, w2=f(wv), wsplit=C, add=dsrc_add, add_cols=C if dsrc_add is not None else 0))
+    g_wq, g_bq = _wgrad(x, dq, wq, bq)
     g_wk, g_bk = _wgrad(src, dkv[:, :C], wk, bk)
     g_wv, g_bv = _wgrad(src, dkv[:, C:], wv, bv)
     return dx, dsrc, [g_wq, g_bq, g_wk, g_bk, g_wv, g_bv, g_wm, g_bm, g_w0, g_b0, g_w3, g_b3]

@@ -156,7 +156,7 @@ class Crops:
     rgb: Optional[torch.Tensor]  # f32 [*, C] colour at each packed crop point (H16) or None
     kept: torch.Tensor       # int64 [F] points after outlier removal
     pair_cap: int = 0
-    overflow_flag: Optional[torch.Tensor] = None  # 0-d bool formed with the crops (see overflow)
+    overflow_flag: Optional[torch.Tensor] = None  # 0-d int32 formed with the crops (see overflow)
     # f32 [F, k, k] ground-truth functional map (utils/utils.py:67-79) when the producer formed it
     # beside the crops (PipelinedTrainer: on the crop-formation stream); None: the step solves it
     C_gt: Optional[torch.Tensor] = None
@@ -165,8 +165,8 @@ class Crops:
     index_status: Optional[torch.Tensor] = None
 
     def overflow(self) -> torch.Tensor:
-        """0-d bool on the device: some crop had more ball-query pairs than pair_cap (its P
-        was truncated). No host sync; `check()` raises on it. CropFormation forms it on its
+        """0-d flag on the device (nonzero: some crop had more ball-query pairs than pair_cap, its
+        P was truncated; pk_ball_query_pairs forms it). No host sync; `check()` raises on it. CropFormation forms it on its
         own stream, so the training step only reads it."""
         if self.overflow_flag is not None:
             return self.overflow_flag
@@ -232,4 +232,4 @@ class CropFormation:
         return Crops(pc64=g["sel64"], pc32=pc32, align64=g["align"], align32=align32, off=pol["off"], n2=n2, ld=ld,
                      npoint=pol["npoint"], pairs=bq["pairs"], npairs=bq["count"], overlap_12=bq["overlap_12"],
                      overlap_21=bq["overlap_21"], rgb=rgb, kept=so["kept"], pair_cap=self.pair_cap,
-                     overflow_flag=(bq["count"] > self.pair_cap).any(), index_status=st)
+                     overflow_flag=bq["overflow"], index_status=st)

@@ -86,11 +86,12 @@ def ball_query(cad: torch.Tensor, cad_off: torch.Tensor, pc: torch.Tensor, pc_of
     count = torch.empty((B,), dtype=torch.int64, device=dev)
     ov12 = torch.empty((B, n1max), dtype=torch.int8, device=dev)
     ov21 = torch.empty((B, n2max), dtype=torch.int8, device=dev)
+    over = torch.empty((1,), dtype=torch.int32, device=dev)
     call("pk_ball_query_pairs", ptr(cad), ptr(cad_off), ptr(pc), ptr(pc_off), ptr(thr2), B, int(n1max),
          int(n2max), ptr(mask), int(ld), ptr(rowcount), ptr(rowoff), ptr(pairs), int(cap), ptr(count),
-         ptr(ov12), ptr(ov21), s)
+         ptr(ov12), ptr(ov21), ptr(over), s)
     return dict(mask=mask, rowcount=rowcount, pairs=pairs, count=count, overlap_12=ov12, overlap_21=ov21,
-                thr2=thr2)
+                thr2=thr2, overflow=over[0])
 
 
 def check_index_status(status: Optional[torch.Tensor], what: str) -> None:
@@ -819,12 +820,9 @@ class _LastLinOverlapFn(torch.autograd.Function):
     def forward(ctx, d0, d1, wl, bl, w0, b0, w1, b1):
         w2 = wl.view(wl.shape[0], -1)
         Co, Ci = w2.shape
-        ys = []
-        for d in (d0, d1):
-            B, _, N = d.shape
-            y = torch.empty((B, Co, N), dtype=torch.float32, device=d.device)
-            linear_ex(d, w2, bl, 1, B * N, N, Ci, Co, y=y)
-            ys.append(y)
+        ys = [torch.empty((d.shape[0], Co, d.shape[2]), dtype=torch.float32, device=d.device) for d in (d0, d1)]
+        linear_ex2(*[a for d, y in zip((d0, d1), ys)
+                     for a in ((d, w2, bl, 1, d.shape[0] * d.shape[2], d.shape[2], Ci, Co, y), {})])
         fx, fy = ys[0].transpose(1, 2), ys[1].transpose(1, 2)
         want = any(ctx.needs_input_grad)
         (sx, sy, rx, ry), saved = _ovh_forward(fx, fy, w0, b0, w1, b1, want)
@@ -843,14 +841,12 @@ class _LastLinOverlapFn(torch.autograd.Function):
         Co, Ci = w2.shape
         dadd = tuple(None if g is None else g.transpose(1, 2) for g in (gy0, gy1))
         dfx, dfy, gw0, gb0, gw1, gb1 = _ovh_backward(sv[3:], ctx.params, dsx, dsy, drx, dry, dadd=dadd)
-        dd, gwl, gbl = [None, None], None, None
-        # shape 1 first: the order autograd ran the two last_lin calls' backward in
-        for s, (d, df) in reversed(list(enumerate(((d0, dfx), (d1, dfy))))):
-            B, _, N = d.shape
-            dy = df.transpose(1, 2)  # [B, Co, N] contiguous (the channels-first storage of y)
-            if ctx.needs_input_grad[s]:
-                dd[s] = torch.empty_like(d)
-                linear_ex(dy, w2, None, 1, B * N, N, Co, Ci, y=dd[s], transw=True)
+        dd, gwl, gbl = [torch.empty_like(d0), torch.empty_like(d1)], None, None
+        dys = [df.transpose(1, 2) for df in (dfx, dfy)]  # [B, Co, N] contiguous (y's storage)
+        linear_ex2(*[a for d, dy, o in zip((d0, d1), dys, dd)
+                     for a in ((dy, w2, None, 1, d.shape[0] * d.shape[2], d.shape[2], Co, Ci, o), dict(transw=True))])
+        # weight gradients: shape 1 first, the order autograd ran the two last_lin calls' backward in
+        for s, (d, dy) in reversed(list(enumerate(zip((d0, d1), dys)))):
             if layers._side_owns(wl_p, bl):
                 layers._SIDE.launch(d, dy, wl_p, bl, channels_first=True)
             else:
@@ -933,25 +929,24 @@ def _dp(t: Optional[torch.Tensor]) -> Optional[int]:
     return t.data_ptr()
 
 
-def linear_ex(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], layout: int, R: int, N: int,
-              Cin: int, Cout: int, y: torch.Tensor, ldx: int = 0, ldy: int = 0, transw: bool = False,
-              relu: bool = False, mask: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None,
-              split: int = 0, ldy2: int = 0, store_cf: bool = False, add: Optional[torch.Tensor] = None,
-              lda: int = 0, add_cols: int = 0, act: Optional[int] = None, pre: Optional[torch.Tensor] = None,
-              pre_out: Optional[torch.Tensor] = None, w2: Optional[torch.Tensor] = None,
-              bias2: Optional[torch.Tensor] = None, wsplit: int = 0, add2: Optional[torch.Tensor] = None,
-              lda2: int = 0) -> None:
-    """pk_linear_ex: a per-point layer writing into caller-placed (strided) outputs with a
-    residual / accumulation epilogue. x, y, y2, add are the first elements of their (possibly
-    strided) operands; strides as in include/posekern.h (0 = contiguous)."""
-    a = _lib.LinearArgs(x=_dp(x), w=_dp(w.contiguous()), bias=_dp(bias), layout=int(layout), N=int(N), R=int(R),
+def _linear_args(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], layout: int, R: int, N: int,
+                 Cin: int, Cout: int, y: torch.Tensor, ldx: int = 0, ldy: int = 0, transw: bool = False,
+                 relu: bool = False, mask: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None,
+                 split: int = 0, ldy2: int = 0, store_cf: bool = False, add: Optional[torch.Tensor] = None,
+                 lda: int = 0, add_cols: int = 0, act: Optional[int] = None, pre: Optional[torch.Tensor] = None,
+                 pre_out: Optional[torch.Tensor] = None, w2: Optional[torch.Tensor] = None,
+                 bias2: Optional[torch.Tensor] = None, wsplit: int = 0, add2: Optional[torch.Tensor] = None,
+                 lda2: int = 0):
+    """(pk_linear_args, algorithmic bytes, flops) of one per-point layer call."""
+    w = w.contiguous()
+    w2c = w2.contiguous() if w2 is not None else None
+    a = _lib.LinearArgs(x=_dp(x), w=_dp(w), bias=_dp(bias), layout=int(layout), N=int(N), R=int(R),
                         Cin=int(Cin), Cout=int(Cout), transw=int(transw), act=int(relu) if act is None else int(act),
                         mask=_dp(mask),
                         ldx=int(ldx), y=_dp(y), ldy=int(ldy), y2=_dp(y2), ldy2=int(ldy2), split=int(split),
                         store_cf=int(store_cf), add=_dp(add), lda=int(lda), add_cols=int(add_cols), pre=_dp(pre),
-                        pre_out=_dp(pre_out), w2=_dp(w2.contiguous()) if w2 is not None else None, bias2=_dp(bias2),
+                        pre_out=_dp(pre_out), w2=_dp(w2c), bias2=_dp(bias2),
                         wsplit=int(wsplit), add2=_dp(add2), lda2=int(lda2))
-    import ctypes
     # algorithmic bytes: the input rows, the output rows, the weight, and every epilogue /
     # prologue operand the fused launch must move (the ReLU-backward mask, the residual rows, the
     # sigmoid-backward input and its scaled copy) — each crosses HBM exactly once
@@ -964,7 +959,27 @@ def linear_ex(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], la
         byts += 4 * int(R) * Cin * (2 if pre_out is not None else 1)
     if add2 is not None:
         byts += 4 * int(R) * Cout
-    call("pk_linear_ex", ctypes.addressof(a), _lib.stream(x.device), work=("hbm", byts, 2 * int(R) * Cin * Cout))
+    return a, (w, w2c), byts, 2 * int(R) * Cin * Cout
+
+
+def linear_ex(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], layout: int, R: int, N: int,
+              Cin: int, Cout: int, y: torch.Tensor, **kw) -> None:
+    """pk_linear_ex: a per-point layer writing into caller-placed (strided) outputs with a
+    residual / accumulation epilogue. x, y, y2, add are the first elements of their (possibly
+    strided) operands; strides as in include/posekern.h (0 = contiguous)."""
+    import ctypes
+    a, keep, byts, flops = _linear_args(x, w, bias, layout, R, N, Cin, Cout, y, **kw)
+    call("pk_linear_ex", ctypes.addressof(a), _lib.stream(x.device), work=("hbm", byts, flops))
+
+
+def linear_ex2(args0: tuple, kw0: dict, args1: tuple, kw1: dict) -> None:
+    """pk_linear_ex2: two independent linear_ex calls (positional args, keyword args each), one
+    launch when both are channels-first 32/64-channel layers."""
+    import ctypes
+    a0, k0, b0, f0 = _linear_args(*args0, **kw0)
+    a1, k1, b1, f1 = _linear_args(*args1, **kw1)
+    call("pk_linear_ex2", ctypes.addressof(a0), ctypes.addressof(a1), _lib.stream(args0[0].device),
+         work=("hbm", b0 + b1, f0 + f1))
 
 
 def spectral_raw(x: torch.Tensor, ld_in: int, mass, evals, evecs, t, clamp_t: bool, mode: int, out: torch.Tensor,
@@ -1224,6 +1239,16 @@ def inlier_ratio(pairs: torch.Tensor, npairs: torch.Tensor, cad: torch.Tensor, p
     if chk:
         check_index_status(st, "inlier_ratio (correspondence indices)")
     return ir
+
+
+def mean_f32(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """0-d mean of a float32 device tensor (pk_mean_f32: fixed summation order), into `out` when
+    given (a 0-d / 1-element float32 device tensor)."""
+    x = x.contiguous()
+    if out is None:
+        out = torch.empty((), dtype=torch.float32, device=x.device)
+    call("pk_mean_f32", ptr(x), x.numel(), ptr(out), _lib.stream(x.device))
+    return out
 
 
 def cgt_lstsq(pairs: torch.Tensor, npairs: torch.Tensor, evecs1: torch.Tensor, evecs2: torch.Tensor) -> torch.Tensor:

@@ -322,7 +322,7 @@ class TrainStep:
     @staticmethod
     @torch.no_grad()
     def inlier_ratio_of(op: Operators, crops: Crops, C_pred: torch.Tensor,
-                        status: Optional[torch.Tensor] = None) -> torch.Tensor:
+                        status: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """train.py:109-116: the naive point map of C_pred and its mean inlier ratio over the
         crops (naive_p2p_batched without materialising its arange row: the IR kernel reads the
         map as [B, V2] CAD indices of crop points 0..n2-1)."""
@@ -332,7 +332,7 @@ class TrainStep:
         p_map, _ = ops.feat_dist_topk(op.cad_evecs, C_pred.detach(), op.pc_evecs, n1, npred, 1)
         # status (int32 [B], optional): per crop 1 when a point-map index was out of range
         ir = ops.inlier_ratio(p_map[..., 0], npred, op.cad_xyz, crops.align32, op.ir_thr, layout=2, status=status)
-        return ir.mean()
+        return ops.mean_f32(ir, out=out)
 
     def forward_backward(self, op: Operators, crops: Crops, ir: bool = True) -> dict:
         """ir=False leaves the naive point map + IR out of the step (PipelinedTrainer computes it
@@ -557,7 +557,7 @@ class PipelinedTrainer:
                 st = torch.zeros((step.last_C_pred.shape[0],), dtype=torch.int32, device=dev_)
                 gi = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gi):
-                    ir_out.copy_(TrainStep.inlier_ratio_of(op, self.crops[k], step.last_C_pred, status=st))
+                    TrainStep.inlier_ratio_of(op, self.crops[k], step.last_C_pred, status=st, out=ir_out)
                 self.logs[k]["IR"] = ir_out
                 self.logs[k]["ir_index_status"] = st
                 self.ir_graphs.append(gi)

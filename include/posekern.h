@@ -51,12 +51,13 @@ int pk_ball_query_mask(const double* cad, const int64_t* cad_off, const double* 
  *   mask from pass 1 or NULL (distances recomputed), rowcount from pass 1
  *   rowoff int64 [B, n1max] scratch (exclusive scan of rowcount)
  *   pairs int64 [B, cap, 2] (i, j) in row-major order, count int64 [B] true totals
- *   ov12 int8 [B, n1max], ov21 int8 [B, n2max] (either may be NULL) */
+ *   ov12 int8 [B, n1max], ov21 int8 [B, n2max] (either may be NULL)
+ *   over int32 [1] or NULL: 1 when some crop's count exceeds cap (its pair list was truncated) */
 int pk_ball_query_pairs(const double* cad, const int64_t* cad_off, const double* pc,
                         const int64_t* pc_off, const double* thr2, int B, int n1max, int n2max,
                         const uint8_t* mask, int ld, const int32_t* rowcount, int64_t* rowoff,
                         int64_t* pairs, int64_t cap, int64_t* count, int8_t* ov12, int8_t* ov21,
-                        void* stream);
+                        int32_t* over, void* stream);
 
 /* H1 crop formation. Replaces dataset/object.py:73-88 dpt_2_pcld (with the plus-shaped
  * erode_seg_mask of :52-71 and `seg == 255` of :137) for F frames at once.
@@ -387,6 +388,11 @@ typedef struct pk_linear_args {
   int64_t lda2;
 } pk_linear_args;
 int pk_linear_ex(const pk_linear_args* a, void* stream);
+/* Two independent pk_linear_ex calls; when both are channels-first layers with Cin, Cout in
+ * {32, 64} and the same points-per-wave choice they share one launch (the refinement's q and
+ * stacked k / v projections, Pq^T and [Pk; Pv]^T, both shapes' last_lin: modeling/dpfm.py:50-54,
+ * 111-112), otherwise they run as two. Same arguments and results as two pk_linear_ex calls. */
+int pk_linear_ex2(const pk_linear_args* a0, const pk_linear_args* a1, void* stream);
 
 /* H10 / H11 correspondence head. Replaces fmap2pointmap_solvers/naive.py:20-34
  * (topk = 1: dist.argmin(dim=-2)) and spacial_filtering.py:19-38 (topk = 5: the first 5
@@ -430,6 +436,9 @@ int pk_rigidity_filter(const int64_t* cand, int ldc, const int32_t* ncand, const
 int pk_inlier_ratio(const int64_t* pairs, int ldp, int layout, const int32_t* npairs, const float* cad,
                     int ldcad, const float* pc_aligned, int ldpc, const float* thr, int B, float* ir,
                     int32_t* status, void* stream);
+/* The batch's mean inlier ratio (train.py:116 `IR.mean()` over the crops' ratios): out f32 [1] =
+ * (sum of x[0..n)) / n, the sum in a fixed order (deterministic). */
+int pk_mean_f32(const float* x, int64_t n, float* out, void* stream);
 
 /* H15 C_gt (utils/utils.py:67-79 C_from_sparse_P): least squares
  * evecs2[P[:,1], :30] X = evecs1[P[:,0], :30] per crop (fp64 normal equations: G from the

@@ -80,6 +80,7 @@ def test_ball_query_bitexact(device, with_mask):
     cap = 200000
     res = ops.ball_query(cad, coff, pc, poff, rs, n1max, n2max, cap, with_mask=with_mask)
     ops.check_capacity(res["count"], cap)
+    assert int(res["overflow"]) == 0  # the kernel's flag: no crop above cap
     count = res["count"].cpu().numpy()
     pairs = res["pairs"].cpu().numpy()
     o12 = res["overlap_12"].cpu().numpy()
@@ -110,6 +111,7 @@ def test_ball_query_capacity_overflow_reported(device):
     pc, poff = _packed([p], np.float64, device)
     res = ops.ball_query(cad, coff, pc, poff, [1.0], 64, 64, 100)
     assert int(res["count"][0]) == 64 * 64
+    assert int(res["overflow"]) == 1  # pk_ball_query_pairs' device flag (Crops.overflow)
     with pytest.raises(_lib.PoseKernError):
         ops.check_capacity(res["count"], 100)
     exp = O.find_positives(c, p, 1.0)[:100]

@@ -801,3 +801,38 @@ def test_first_lin_pair_matches_per_shape(device):
     for i, (r, o) in enumerate(zip(ref, got)):
         scale = max(float(r.abs().max()), 1e-30)
         assert (o - r).abs().max().item() <= 1e-5 * scale + floor, (i, (o - r).abs().max().item(), scale)
+
+
+@pytest.mark.parametrize("N", [1024, 300])  # 300: ragged channels-first tiles (SUB = 1)
+def test_linear_ex2_pair_matches_two_calls(device, N):
+    """pk_linear_ex2 (two independent channels-first layers in one launch) writes exactly what
+    two pk_linear_ex calls write, for every Cin / Cout pair it takes and the epilogues the
+    refinement uses (bias, stacked weight + bias2, transposed weight, add, add2)."""
+    from dpfm_amd import ops
+    g = torch.Generator().manual_seed(8)
+    B = 32 if N == 1024 else 4  # 32 x 1024: 32 points per wave (SUB = 2)
+
+    def r(*s):
+        return torch.randn(*s, generator=g).to(device)
+
+    for ci0, co0, ci1, co1 in [(32, 32, 32, 64), (32, 32, 64, 32), (64, 64, 32, 32), (64, 32, 64, 64)]:
+        x0, x1 = r(B, ci0, N), r(B, ci1, N)
+        w0, w1, b0, b1 = r(co0, ci0), r(co1 // 2, ci1), r(co0), r(co1 // 2)
+        w1b, b1b = r(co1 - co1 // 2, ci1), r(co1 - co1 // 2)
+        add0, add20 = r(B, co0, N), r(B, co0, N)
+        kw0 = dict(add=add0, add_cols=co0, add2=add20)
+        kw1 = dict(w2=w1b, bias2=b1b, wsplit=co1 // 2)
+        outs = []
+        for pair in (False, True):
+            y0, y1 = torch.full((B, co0, N), 7.0, device=device), torch.full((B, co1, N), 7.0, device=device)
+            a0 = (x0, w0, b0, 1, B * N, N, ci0, co0, y0)
+            a1 = (x1, w1, b1, 1, B * N, N, ci1, co1, y1)
+            if pair:
+                ops.linear_ex2(a0, kw0, a1, kw1)
+            else:
+                ops.linear_ex(*a0, **kw0)
+                ops.linear_ex(*a1, **kw1)
+            outs.append((y0.cpu(), y1.cpu()))
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), (ci0, co0, ci1, co1)
+        ref0 = torch.einsum("oi,bin->bon", w0.cpu(), x0.cpu()) + b0.cpu()[None, :, None] + add0.cpu() + add20.cpu()
+        assert (outs[1][0] - ref0).abs().max().item() <= 1e-4 * ref0.abs().max().item()
