@@ -10,6 +10,7 @@ step() { local name=$1 to=$2; shift 2; timeout -k 10 $to "$@" > $O/$name.out 2> 
 step train 600 python3 -u bench.py
 step infer 300 python3 -u bench.py --mode infer
 step infer2048 300 python3 -u bench.py --mode infer --points 2048 --no-cpu-baseline
+step ragged 600 python3 -u bench.py --ragged --no-cpu-baseline
 [ -n "$SKIP_OPS" ] || step ops 400 python3 -u bench.py --mode operators --batch 8 --steps 3 --warmup 1
 step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline-probe
 find $O/prof -type f ! -name "*stats.csv" -delete

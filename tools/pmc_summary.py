@@ -28,16 +28,18 @@ FAMILIES = {
     "pk_sor": ["sor_knn_kernel", "sor_stats_kernel", "sor_count_kernel", "sor_write_kernel"],
     "pk_ball_query_mask": ["bq_mask_stream_kernel", "bq_mask_f32_kernel"],
     "pk_backproject": ["bp_count_kernel", "bp_write_kernel"],
-    "pk_spectral_diffusion": ["spec_reduce_kernel", "spec_combine_kernel", "spec_expand_kernel"],
+    "pk_spectral_diffusion": ["spec_reduce_mfma_kernel", "spec_combine4_kernel", "spec_expand_mfma_kernel",
+                              "spec_reduce_kernel", "spec_combine_kernel", "spec_expand_kernel"],
     "pk_attention_fwd": ["attn_fwd_kernel"],
     "pk_attention_bwd": ["attn_bwd_kernel", "attn_bwd_dq_reduce_kernel"],
     "pk_linear_wgrad": ["wgrad_v2_kernel", "wgrad_partial_kernel", "wgrad_reduce_kernel"],
-    "pk_feat_dist_topk": ["fd_wide_kernel", "fd_prep_kernel", "fd_main_direct_kernel", "fd_main_kernel"],
+    "pk_feat_dist_topk": ["fd_top1_prep_kernel", "fd_top1_kernel", "fd_top1_merge_kernel", "fd_prep_kernel",
+                          "fd_main_direct_kernel", "fd_merge_kernel"],
     "pk_cgt_lstsq": ["cgt_count_kernel", "cgt_partial_kernel", "cgt_reduce_kernel", "cgt_solve_kernel"],
     # pk_linear_fwd and pk_linear_ex (its epilogue / placement variant) launch the same kernels: the
     # counters cannot tell them apart, so they form one family, per KERNEL launch
     "pk_linear_fwd+ex": ["linear_glds_rows_kernel", "linear_fwd_rows_kernel", "linear_fwd_cf_kernel", "linear_fwd_kernel",
-                         "linear_thin_kernel"],
+                         "linear_thin_kernel", "linear_cf_pair_kernel"],
     "pk_linear_wgrad_grouped": ["wgrad_glds_grouped_kernel", "wgrad_grouped_kernel", "wgrad_grouped_reduce_kernel"],
     "pk_nce_loss": ["nce_pass_kernel<false>", "nce_pass_kernel<true>", "nce_scatter_kernel"],
     "pk_clip_rmsprop": ["grad_sumsq_kernel", "clip_rmsprop_kernel"],
@@ -51,8 +53,7 @@ FAMILIES = {
 ANY_LEAD = {"pk_linear_fwd+ex"}
 # entry point -> its kernels, normalised per entry call with the bench's call count
 PER_ENTRY = {"pk_linear_ex": FAMILIES["pk_linear_fwd+ex"],
-             "pk_feat_dist_topk": ["fd_wide_kernel", "fd_prep_kernel", "fd_main_direct_kernel", "fd_merge_kernel",
-                                   "fd_fused_kernel", "fd_rows_kernel", "fd_cols_kernel"],
+             "pk_feat_dist_topk": FAMILIES["pk_feat_dist_topk"],
              "pk_linear_wgrad_grouped": FAMILIES["pk_linear_wgrad_grouped"],
              "pk_attention_fwd": FAMILIES["pk_attention_fwd"], "pk_attention_bwd": FAMILIES["pk_attention_bwd"]}
 # (the first kernel of each family is counted once per family launch)
