@@ -29,6 +29,8 @@
 //                              dV = P^T dO, dK = 0.25 dS^T Q, and a dQ = 0.25 dS K partial per key
 //                              block (dS = P (dP - delta), dP = dO V^T): each contraction once
 //   attn_bwd_dq_reduce_kernel  the dQ partials added in key-block order
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace {
@@ -37,8 +39,6 @@ using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f32x2 = __attribute__((ext_vector_type(2))) float;
 constexpr int kD = 16;       // head dim
 constexpr int kT = 64;       // rows per tile / per workgroup
-constexpr int kSR = 80;      // LDS stride of [d][row] arrays (bank-conflict-free MFMA reads)
-constexpr int kSC = 20;      // LDS stride of [row][d] arrays
 constexpr float kScale = 0.25f;  // 1 / sqrt(dim) for the gradients
 
 __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
@@ -59,75 +59,88 @@ constexpr float kLog2e = 1.4426950408889634f;
 
 __device__ __forceinline__ float exp2_(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// A 64-row tile of a [D, H, L] slab (row index contiguous), 4 elements per thread:
-// element e = tid + 256 j -> (d = e >> 6, row = e & 63); rows >= L read as 0.
-struct Tile {
-  float x[4];
-};
+constexpr int kKB = 256;   // keys per block (backward)
+constexpr int kSA = 20;    // [row][p(d)] stride
+constexpr int kSQ = 68;    // [d][row] stride
+constexpr int kSTs = 36;   // dS transpose tile [q][32 keys] stride
+constexpr int kSRq = 20;   // dQ partial [q][d] stride
+constexpr int kOA = 0, kOG = kT * kSA, kOQT = 2 * kT * kSA, kOGT = kOQT + kD * kSQ, kOMI = kOGT + kD * kSQ;
+constexpr int kTileF = kOMI + 3 * kT;  // floats per query-tile buffer
+// LDS banking (MI355X_MICROARCH.md §LDS): a ds_read_b128 is served in four 16-lane groups, each
+// holding every c = l & 15 once and lane groups g, g ^ 1 split as c in [4, 12) vs the rest. Rows
+// c of a stride with an odd count of 16-B chunks fall on 16 distinct chunk slots, so a read of
+// (row c, chunk g) is conflict-free once the chunk index is XORed with swz(c) = [4 <= c < 12]:
+// the group then reads one chunk column. Every [row][.] / [d][.] tile below stores chunk j of row
+// r at j ^ swz(r & 15).
+__device__ __forceinline__ int swz(int c) { return ((c + 4) >> 3) & 1; }
 
-__device__ __forceinline__ Tile load_tile(const float* __restrict__ src, int HL, int L, int r0) {
-  Tile t;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int e = threadIdx.x + 256 * j;
-    const int d = e >> 6, r = e & 63;
-    t.x[j] = r0 + r < L ? src[(int64_t)d * HL + r0 + r] : 0.f;
-  }
-  return t;
-}
-
-// into LDS as [d][row] (stride kSR) and/or [row][d] (stride kSC)
-__device__ __forceinline__ void store_tile(const Tile& t, float* __restrict__ dr, float* __restrict__ rd) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int e = threadIdx.x + 256 * j;
-    const int d = e >> 6, r = e & 63;
-    if (dr) dr[d * kSR + r] = t.x[j];
-    if (rd) rd[r * kSC + d] = t.x[j];
-  }
-}
-
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__ q,
+// Forward: one workgroup = 8 waves x 16 queries = 128 queries of one (crop, head); 64-key tiles of
+// K and V staged once per block in LDS, double-buffered with one barrier per tile (the next tile's
+// global loads in flight during this one), K as [key][p(d)] and V as [d][key] so each MFMA operand
+// quad is one conflict-free ds_read_b128 (8 per lane per tile).
+constexpr int kFQ = 128;                            // queries per forward block
+constexpr int kFKV = kT * kSA + kD * kSQ;           // floats per K / V tile buffer
+__global__ __launch_bounds__(512) void attn_fwd_kernel(const float* __restrict__ q,
                                                        const float* __restrict__ k,
                                                        const float* __restrict__ v, int H, int N,
                                                        int M, int64_t sbk, int64_t sbv, float* __restrict__ out,
                                                        float* __restrict__ lse) {
-  __shared__ float Ks[kD * kSR];
-  __shared__ float Vs[kT * kSC];
+  __shared__ __attribute__((aligned(16))) float KV[2 * kFKV];
   const int3 lb = pk::xcd_block3();  // a (crop, head)'s query blocks share one XCD's L2 (K / V)
   const int h = lb.y, b = lb.z;
   const int lane = pk::lane_id(), g = lane >> 4, c = lane & 15;
-  const int qi = lb.x * kT + pk::wave_id() * 16 + c;
+  const int qi = lb.x * kFQ + pk::wave_id() * 16 + c;
   const float* qb = q + ((int64_t)b * kD * H + h) * N;
   const float* kb = k + (int64_t)b * sbk + (int64_t)h * M;
   const float* vb = v + (int64_t)b * sbv + (int64_t)h * M;
+  const int HM = H * M;
   float qr[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) qr[s] = qi < N ? qb[(int64_t)(4 * s + g) * H * N + qi] * kScale : 0.f;
+  // staging: threads 0-255 carry K, 256-511 V; thread -> (key sk = (tid & 255) >> 2, d 4 sp .. + 3)
+  const int sk = (threadIdx.x & 255) >> 2, sp = threadIdx.x & 3;
+  const bool stage_k = threadIdx.x < 256;
+  const float* src = stage_k ? kb : vb;
+  float pf[4];
+  auto issue = [&](int k0) {
+    const int kk = k0 + sk, kc = kk < M ? kk : 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pf[i] = src[(int64_t)(4 * sp + i) * HM + kc];
+  };
+  auto stage = [&](int k0, float* buf) {
+    const bool ok = k0 + sk < M;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x = ok ? pf[i] : 0.f;
+      const int d = 4 * sp + i;
+      if (stage_k) buf[sk * kSA + 4 * (i ^ swz(sk & 15)) + sp] = x;  // K [key][p(d)], p(d) = 4 i + sp
+      else buf[kT * kSA + d * kSQ + 4 * ((sk >> 2) ^ swz(d)) + (sk & 3)] = x;  // V [d][key]
+    }
+  };
   // one accumulator per 16-key sub-tile: four independent MFMA chains (a serial chain over
   // M ~ 5000 keys of a real CAD measured 4-5x torch's gradient error; split, it is within 1.5x)
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -__builtin_huge_valf(), l = 0.f;
-  Tile kt = load_tile(kb, H * M, M, 0), vt = load_tile(vb, H * M, M, 0);
-  for (int k0 = 0; k0 < M; k0 += kT) {
-    __syncthreads();
-    store_tile(kt, Ks, nullptr);
-    store_tile(vt, nullptr, Vs);
-    __syncthreads();
-    if (k0 + kT < M) {  // next tile in flight during this one
-      kt = load_tile(kb, H * M, M, k0 + kT);
-      vt = load_tile(vb, H * M, M, k0 + kT);
-    }
+  issue(0);
+  stage(0, KV);
+  if (kT < M) issue(kT);
+  const int gs = 4 * (g ^ swz(c));
+  // one 64-key tile; RAG: the ragged last tile (keys past M masked to -inf) — a separate
+  // instantiation, so the full tiles carry no masking code (a uniform branch the compiler would
+  // otherwise if-convert into every tile)
+  auto tile = [&](const float* buf, int k0, auto rag) {
+    constexpr bool RAG = decltype(rag)::value;
     f32x4 st[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
+      const f32x4 ka = *reinterpret_cast<const f32x4*>(&buf[(16 * t + c) * kSA + gs]);  // K[16t + c][4s + g]
       st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) st[t] = mfma(Ks[(4 * s + g) * kSR + 16 * t + c], qr[s], st[t]);
+      for (int s = 0; s < 4; ++s) st[t] = mfma(ka[s], qr[s], st[t]);  // S^T[key 16t + 4g + r][q c]
     }
-    if (k0 + kT > M) {  // workgroup-uniform: only a ragged last tile has keys past M
+    if constexpr (RAG) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -143,9 +156,18 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
     const float mn = fmaxf(m, mt);
     const float alpha = m == -__builtin_huge_valf() ? 0.f : exp2_((m - mn) * kLog2e);
     m = mn;
+    l *= alpha;
+    const f32x2 al2 = {alpha, alpha};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x2 a0 = {acc[t][0], acc[t][1]}, a1 = {acc[t][2], acc[t][3]};
+      a0 *= al2;
+      a1 *= al2;
+      acc[t] = f32x4{a0.x, a0.y, a1.x, a1.y};
+    }
     // (s - m) log2 e on packed f32 pairs (v_pk_add_f32 / v_pk_mul_f32: the same per-element
     // rounding), row sums in two pair lanes
-    const f32x2 mn2 = {mn, mn}, l2e = {kLog2e, kLog2e};
+    const f32x2 mn2 = {m, m}, l2e = {kLog2e, kLog2e};
     f32x2 ps2 = {0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -158,19 +180,31 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
         st[t][r + 1] = p.y;
         ps2 += p;
       }
-    l = l * alpha + (ps2.x + ps2.y);
-    const f32x2 al2 = {alpha, alpha};
+    l += ps2.x + ps2.y;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      f32x2 a0 = {acc[t][0], acc[t][1]}, a1 = {acc[t][2], acc[t][3]};
-      a0 *= al2;
-      a1 *= al2;
-      acc[t] = f32x4{a0.x, a0.y, a1.x, a1.y};
+      const f32x4 va = *reinterpret_cast<const f32x4*>(&buf[kT * kSA + c * kSQ + 16 * t + gs]);  // V[16t + 4g + r][c]
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[t] = mfma(va[r], st[t][r], acc[t]);
     }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[t] = mfma(Vs[(16 * t + 4 * g + r) * kSC + c], st[t][r], acc[t]);
+  };
+  auto sync_stage = [&](int j) {
+    const int k0 = j * kT;
+    __syncthreads();  // tile j staged; the buffer of tile j - 1 free
+    if (k0 + kT < M) {
+      stage(k0 + kT, KV + ((j + 1) & 1) * kFKV);
+      if (k0 + 2 * kT < M) issue(k0 + 2 * kT);
+    }
+  };
+  const int nfull = M / kT;
+  int j = 0;
+  for (; j < nfull; ++j) {
+    sync_stage(j);
+    tile(KV + (j & 1) * kFKV, j * kT, std::false_type{});
+  }
+  if (j * kT < M) {  // the ragged last tile
+    sync_stage(j);
+    tile(KV + (j & 1) * kFKV, j * kT, std::true_type{});
   }
   l = grp_sum(l);
   const f32x4 accs = (acc[0] + acc[1]) + (acc[2] + acc[3]);
@@ -200,20 +234,6 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__
 // (deterministic; a single key block writes dq scaled, no reduce launch).
 // delta = rowsum(dO * O) is formed per query as the tile is staged (fmaf over d in order, the
 // four lanes' partial sums of a query added as (p0 + p1) + (p2 + p3)).
-constexpr int kKB = 256;   // keys per block
-constexpr int kSA = 20;    // [q][p(d)] stride
-constexpr int kSQ = 68;    // [d][q] stride
-constexpr int kSTs = 36;   // dS transpose tile [q][32 keys] stride
-constexpr int kSRq = 20;   // dQ partial [q][d] stride
-constexpr int kOA = 0, kOG = kT * kSA, kOQT = 2 * kT * kSA, kOGT = kOQT + kD * kSQ, kOMI = kOGT + kD * kSQ;
-constexpr int kTileF = kOMI + 3 * kT;  // floats per query-tile buffer
-// LDS banking (MI355X_MICROARCH.md §LDS): a ds_read_b128 is served in four 16-lane groups, each
-// holding every c = l & 15 once and lane groups g, g ^ 1 split as c in [4, 12) vs the rest. Rows
-// c of a stride with an odd count of 16-B chunks fall on 16 distinct chunk slots, so a read of
-// (row c, chunk g) is conflict-free once the chunk index is XORed with swz(c) = [4 <= c < 12]:
-// the group then reads one chunk column. Every [q][.] / [d][.] tile below stores chunk j of row
-// r at j ^ swz(r & 15).
-__device__ __forceinline__ int swz(int c) { return ((c + 4) >> 3) & 1; }
 
 __global__ __launch_bounds__(512, 1) void attn_bwd_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
@@ -436,7 +456,7 @@ extern "C" int pk_attention_fwd(const float* q, const float* k, const float* v, 
   if (B == 0 || N == 0) return PK_OK;
   PK_REQUIRE(M > 0 && q && k && v && out && lse);
   const int64_t dense = (int64_t)kD * H * M;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((N + kT - 1) / kT, H, B), dim3(256), 0, pk::as_stream(stream),
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3((N + kFQ - 1) / kFQ, H, B), dim3(512), 0, pk::as_stream(stream),
                      q, k, v, H, N, M, sbk ? sbk : dense, sbv ? sbv : dense, out, lse);
   PK_CHECK_LAUNCH();
   return PK_OK;
