@@ -511,13 +511,22 @@ class PipelinedTrainer:
     two streams on disjoint CU sets (cu_split_streams; measured no faster)."""
 
     def __init__(self, crop_formation: CropFormation, step: TrainStep, fb: FrameBatch, op: Operators,
-                 warmup: int = 3, defer_ir: bool = True, cgt_side: bool = True, side_cus: int = 0):
+                 warmup: int = 3, defer_ir: bool = True, cgt_side: bool = True, side_cus: int = 0,
+                 main_priority: int = 0):
         self.step, self.split = step, step.world > 1
         self.main = torch.cuda.current_stream()
         self.side = torch.cuda.Stream()
+        self.own_main = False
         if side_cus > 0:  # disjoint CU sets for the two streams (cu_split_streams)
             self.main, self.side = cu_split_streams(side_cus)
             self.main.wait_stream(torch.cuda.current_stream())
+            self.own_main = True
+        elif main_priority == 1:  # the training stream at the highest queue priority, crop formation below
+            self.main = torch.cuda.Stream(priority=torch.cuda.Stream.priority_range()[1])
+            self.main.wait_stream(torch.cuda.current_stream())
+            self.own_main = True
+        elif main_priority == -1:  # crop formation at the highest queue priority
+            self.side = torch.cuda.Stream(priority=torch.cuda.Stream.priority_range()[1])
         side = torch.cuda.Stream()
         side.wait_stream(self.main)
         with torch.cuda.stream(side):  # warm-up outside capture
@@ -622,6 +631,8 @@ class PipelinedTrainer:
                 self.step.allreduce_grads(self.grads[k])
                 self.train_b[k].replay()
             self.consumed[k].record(self.main)
+        if self.own_main:  # the caller's stream reads the step's outputs after it
+            torch.cuda.current_stream().wait_stream(self.main)
         self._trained[k] = True
         self.i += 1
         return self.logs[k]
