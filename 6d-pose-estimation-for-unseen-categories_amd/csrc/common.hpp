@@ -7,6 +7,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #define PK_OK 0
 #define PK_ERR_ARG 1000      // invalid argument (shape / size / null pointer)
@@ -24,6 +25,31 @@
   } while (0)
 
 namespace pk {
+
+// Wave priority of the crop-formation kernels that run beside the training step on the second
+// stream (FPS, SOR): s_setprio(1..3) raises their waves' issue priority over the training
+// kernels' waves sharing a SIMD; 0: unchanged. The product library uses PK_SIDE_PRIO_DEFAULT;
+// the development library reads PK_SIDE_PRIO (tools/prio_ab.py).
+#ifndef PK_SIDE_PRIO_DEFAULT
+#define PK_SIDE_PRIO_DEFAULT 0
+#endif
+inline int side_prio() {
+#ifdef PK_DEVBUILD
+  static const int v = [] {
+    const char* e = std::getenv("PK_SIDE_PRIO");
+    const int x = e ? std::atoi(e) : PK_SIDE_PRIO_DEFAULT;
+    return x < 0 ? 0 : x > 3 ? 3 : x;
+  }();
+  return v;
+#else
+  return PK_SIDE_PRIO_DEFAULT;
+#endif
+}
+__device__ __forceinline__ void set_wave_prio(int prio) {
+  if (prio == 1) __builtin_amdgcn_s_setprio(1);
+  else if (prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (prio == 3) __builtin_amdgcn_s_setprio(3);
+}
 
 constexpr int kWave = 64;
 

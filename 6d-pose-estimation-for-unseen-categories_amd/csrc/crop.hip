@@ -223,7 +223,8 @@ __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const
                                                                  const int32_t* __restrict__ pix,
                                                                  const int32_t* __restrict__ idxmap, int H, int W,
                                                                  const double* __restrict__ Kmat, int tiles, int B,
-                                                                 double* __restrict__ avg) {
+                                                                 double* __restrict__ avg, int prio) {
+  pk::set_wave_prio(prio);
   __shared__ float4 tile[kSorTile];
   {
   const int item = blockIdx.x;
@@ -489,7 +490,9 @@ __device__ double seq_sum_exact(F term, int n, SeqShared& sh) {
 
 __global__ __launch_bounds__(kStatThreads) void sor_stats_kernel(const double* __restrict__ avg,
                                                                  const int64_t* __restrict__ off,
-                                                                 double std_ratio, double* __restrict__ thr) {
+                                                                 double std_ratio, double* __restrict__ thr,
+                                                                 int prio) {
+  pk::set_wave_prio(prio);
   __shared__ SeqShared sh;
   const int b = blockIdx.x;
   const int64_t base = off[b];
@@ -745,10 +748,10 @@ extern "C" int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, in
     const int tiles = (nmax + kSorThreads - 1) / kSorThreads;
     hipLaunchKernelGGL(sor_knn_kernel, dim3((unsigned)((int64_t)tiles * B)),
                        dim3(kSorThreads), 0, s, xyz, off, knn, pix, idxmap, H, W,
-                       pix != nullptr ? K : nullptr, tiles, B, avg);
+                       pix != nullptr ? K : nullptr, tiles, B, avg, pk::side_prio());
     PK_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(sor_stats_kernel, dim3(B), dim3(kStatThreads), 0, s, avg, off, std_ratio, thr);
+  hipLaunchKernelGGL(sor_stats_kernel, dim3(B), dim3(kStatThreads), 0, s, avg, off, std_ratio, thr, pk::side_prio());
   PK_CHECK_LAUNCH();
   if (nchunk > 0) {
     hipLaunchKernelGGL(sor_count_kernel, dim3(nchunk, B), dim3(1024), 0, s, avg, off, thr, nchunk, ccount);

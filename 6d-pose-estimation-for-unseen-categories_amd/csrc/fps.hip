@@ -401,7 +401,8 @@ template <int NT, int PPT>
 __global__ __launch_bounds__(NT) void fps_flat_kernel(
     const float* __restrict__ xyz, const int64_t* __restrict__ offsets,
     const int32_t* __restrict__ start, const int32_t* __restrict__ npoint,
-    int64_t* __restrict__ out, int out_stride) {
+    int64_t* __restrict__ out, int out_stride, int prio) {
+  pk::set_wave_prio(prio);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);  // [3] (4 words reserved)
   const int b = blockIdx.x;
@@ -505,7 +506,7 @@ int launch_fps_flat(const float* xyz, const int64_t* offsets, const int32_t* sta
   const int n_pad = (nmax + 3) & ~3;
   const size_t lds = 4 * sizeof(unsigned long long) + 3 * (size_t)n_pad * sizeof(float);
   hipLaunchKernelGGL((fps_flat_kernel<NT, PPT>), dim3(B), dim3(NT), lds, s, xyz, offsets, start, npoint, out,
-                     out_stride);
+                     out_stride, pk::side_prio());
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

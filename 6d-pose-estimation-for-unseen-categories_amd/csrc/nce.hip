@@ -98,6 +98,7 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
   __shared__ float wn_s[kTile];      // their norms (-1: invalid row)
   __shared__ float vn_s[kTile];      // their |v|^2
   __shared__ int64_t widx_s[kTile];  // their feature indices
+  __shared__ int64_t ooff_s[kMaxS];  // the other side's row offsets (-1: invalid slot)
   __shared__ int nv_s[kWaves];
   const int b = blockIdx.y;
   const int lane = pk::lane_id(), w = pk::wave_id();
@@ -108,49 +109,81 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
   const int64_t N_own = COLS ? N2 : N1;
   const int side_own = COLS ? 1 : 0;
 
-  // number of valid slots (identical in every block of the crop)
+  // Staging in three round trips instead of one dependent chain per row: (1) every slot's
+  // valid flag / row / pair index, all loads unconditional at clamped addresses (an invalid slot's
+  // row may hold anything) and the own rows' features alongside; (2) every other-side feature
+  // row, all of a thread's loads in flight together (the round-4 loop waited for each row's
+  // three dependent loads in turn: 16 serial chains per thread, most of the pass).
+  constexpr int kOPer = kMaxS / (64 * kWaves);  // other-side slots per thread
   int nv = 0;
-  for (int o = threadIdx.x; o < S; o += 64 * kWaves) nv += vb[o] ? 1 : 0;
-  nv = pk::wave_sum_i32(nv);
-  if (lane == 0) nv_s[w] = nv;
-  // stage the other side (slots >= S and invalid slots: zeros)
-  const bool vec = prenorm && f_oth.sc == 1 && (((uintptr_t)f_oth.base) & 15) == 0 && (f_oth.sn & 3) == 0 &&
-                   (f_oth.sb & 3) == 0;
-  if (vec) {  // normalized rows storage: 8 lanes per row, 16 B each
-    for (int e = threadIdx.x; e < kMaxS * 8; e += 64 * kWaves) {
-      const int o = e >> 3, q = e & 7;
-      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (o < S && vb[o] != 0) {
-        int64_t idx;
-        const float* p = nce_row_ptr(f_oth, pairs, cap, rows, S, b, o, 1 - side_own, &idx);
-        x = *reinterpret_cast<const float4*>(p + 4 * q);
-      }
-      float2* d2 = reinterpret_cast<float2*>(&Os[o * kLd + 4 * q]);  // 8-B aligned (kLd even)
-      d2[0] = make_float2(x.x, x.y);
-      d2[1] = make_float2(x.z, x.w);
+  {
+    int64_t rr[kOPer];
+    bool okv[kOPer];
+#pragma unroll
+    for (int i = 0; i < kOPer; ++i) {
+      const int o = threadIdx.x + i * 64 * kWaves;
+      const int oc = o < S ? o : S - 1;
+      okv[i] = o < S && vb[oc] != 0;
+      rr[i] = rows[(int64_t)b * S + oc];
     }
-  } else {
-    for (int o = threadIdx.x; o < kMaxS; o += 64 * kWaves) {
-      const bool ok = o < S && vb[o] != 0;
-      int64_t idx = 0;
-      const float* p = ok ? nce_row_ptr(f_oth, pairs, cap, rows, S, b, o, 1 - side_own, &idx) : nullptr;
-      stage_row(p, f_oth.sc, ok, prenorm, &Os[o * kLd], f_oth.base);
+#pragma unroll
+    for (int i = 0; i < kOPer; ++i) {
+      const int64_t r = rr[i] < 0 ? 0 : rr[i] >= cap ? cap - 1 : rr[i];
+      rr[i] = pairs[((int64_t)b * cap + r) * 2 + (1 - side_own)];
+    }
+#pragma unroll
+    for (int i = 0; i < kOPer; ++i) {
+      const int o = threadIdx.x + i * 64 * kWaves;
+      ooff_s[o] = okv[i] ? (int64_t)b * f_oth.sb + rr[i] * f_oth.sn : -1;
+      nv += okv[i] ? 1 : 0;
     }
   }
-  // this block's own rows (all their dependent index / feature loads in parallel)
+  nv = pk::wave_sum_i32(nv);
+  if (lane == 0) nv_s[w] = nv;
+  // this block's own rows (their dependent index / feature loads overlap the loads above)
   if (threadIdx.x < kTile) {
     const int a = blockIdx.x * kTile + threadIdx.x;
-    const bool ok = a < S && vb[a] != 0;
-    int64_t idx = 0;
-    const float* p = ok ? nce_row_ptr(f_own, pairs, cap, rows, S, b, a, side_own, &idx) : nullptr;
+    const int ac = a < S ? a : S - 1;
+    const bool ok = a < S && vb[ac] != 0;
+    int64_t r = rows[(int64_t)b * S + ac];
+    r = r < 0 ? 0 : r >= cap ? cap - 1 : r;
+    const int64_t idx = ok ? pairs[((int64_t)b * cap + r) * 2 + side_own] : 0;
+    const float* p = f_own.base + (int64_t)b * f_own.sb + idx * f_own.sn;
     float* dst = &Ws[threadIdx.x * kLd];
-    const float nrm = stage_row(p, f_own.sc, ok, prenorm, dst, f_own.base);
+    const float nrm = stage_row(ok ? p : nullptr, f_own.sc, ok, prenorm, dst, f_own.base);
     float vn = 0.f;
 #pragma unroll
     for (int c = 0; c < kC; ++c) vn = fmaf(dst[c], dst[c], vn);
     wn_s[threadIdx.x] = ok ? nrm : -1.f;
     vn_s[threadIdx.x] = vn;
     widx_s[threadIdx.x] = idx;
+  }
+  __syncthreads();
+  // the other side (slots >= S and invalid slots: zeros)
+  const bool vec = prenorm && f_oth.sc == 1 && (((uintptr_t)f_oth.base) & 15) == 0 && (f_oth.sn & 3) == 0 &&
+                   (f_oth.sb & 3) == 0;
+  if (vec) {  // normalized rows storage: 8 lanes per row, 16 B each, kMaxS * 8 / 256 = 16 loads per thread
+    constexpr int kVPer = kMaxS * 8 / (64 * kWaves);
+    float4 x[kVPer];
+#pragma unroll
+    for (int i = 0; i < kVPer; ++i) {
+      const int e = threadIdx.x + i * 64 * kWaves;
+      const int64_t off = ooff_s[e >> 3];
+      x[i] = *reinterpret_cast<const float4*>(f_oth.base + (off < 0 ? 0 : off) + 4 * (e & 7));
+      if (off < 0) x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < kVPer; ++i) {
+      const int e = threadIdx.x + i * 64 * kWaves;
+      float2* d2 = reinterpret_cast<float2*>(&Os[(e >> 3) * kLd + 4 * (e & 7)]);  // 8-B aligned (kLd even)
+      d2[0] = make_float2(x[i].x, x[i].y);
+      d2[1] = make_float2(x[i].z, x[i].w);
+    }
+  } else {
+    for (int o = threadIdx.x; o < kMaxS; o += 64 * kWaves) {
+      const int64_t off = ooff_s[o];
+      stage_row(off >= 0 ? f_oth.base + off : nullptr, f_oth.sc, off >= 0, prenorm, &Os[o * kLd], f_oth.base);
+    }
   }
   __syncthreads();
   for (int o = threadIdx.x; o < kMaxS; o += 64 * kWaves) {  // |u|^2: the same fmaf chain in both passes
@@ -294,10 +327,14 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
 }
 
 // g[b, idx] = sum of the slot rows dx[b, a] with idx(a) = idx, in ascending slot order (0 for
-// points in no valid slot). One 512-thread block per (crop, side): the (idx, slot) keys of the
-// crop's slots are sorted in LDS (bitonic, 512 keys), so every point's slots form one ascending
-// run; work item (sorted position, channel) at a run's head sums the run (128-B coalesced rows).
+// points in no valid slot). Blocks (crop, side, part): each 512-thread block sorts the (idx, slot)
+// keys of the crop's slots in LDS (bitonic, 512 keys; every part repeats it), so every point's
+// slots form one ascending run, and owns the points [part N / kScP, (part + 1) N / kScP): it zero-fills
+// their rows and, for the sorted positions whose point it owns (one contiguous range), work item
+// (sorted position, channel) at a run's head sums the run (128-B coalesced rows). Round 4 ran one
+// block per (crop, side): 64 blocks on 256 CUs, every block's loads and stores in series.
 constexpr int kScT = 512;
+constexpr int kScP = 4;
 __global__ __launch_bounds__(kScT) void nce_scatter_kernel(const int64_t* __restrict__ pairs, int cap,
                                                            const int64_t* __restrict__ rows,
                                                            const uint8_t* __restrict__ valid, int S, int64_t N1,
@@ -307,6 +344,8 @@ __global__ __launch_bounds__(kScT) void nce_scatter_kernel(const int64_t* __rest
   const int b = blockIdx.x, side = blockIdx.y, B = gridDim.x;
   const int t = threadIdx.x;
   const int64_t N = side ? N2 : N1;
+  const int64_t per = (N + kScP - 1) / kScP;
+  const int64_t lo = blockIdx.z * per, hi = lo + per < N ? lo + per : N;
   float* __restrict__ g = (side ? g2 : g1) + (int64_t)b * N * kC;
   const float* __restrict__ dx = dxr + ((int64_t)side * B + b) * S * kC;
   constexpr int64_t kNone = 0x7fffffffffffffffLL;
@@ -317,7 +356,7 @@ __global__ __launch_bounds__(kScT) void nce_scatter_kernel(const int64_t* __rest
     kk = (pairs[((int64_t)b * cap + r) * 2 + side] << 9) | t;
   }
   float4* gz = reinterpret_cast<float4*>(g);  // N * 32 floats, 16-B aligned (torch allocation, N * 128 B rows)
-  for (int64_t e = t; e < N * (kC / 4); e += kScT) gz[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t e = lo * (kC / 4) + t; e < hi * (kC / 4); e += kScT) gz[e] = make_float4(0.f, 0.f, 0.f, 0.f);
   // bitonic sort, one key per thread: partners within a wave (j < 64) by lane shuffles, only the
   // 6 wider stages through LDS (12 barriers instead of 45)
   for (int k = 2; k <= kMaxS; k <<= 1)
@@ -329,31 +368,34 @@ __global__ __launch_bounds__(kScT) void nce_scatter_kernel(const int64_t* __rest
         other = key[t ^ j];
         __syncthreads();
       } else {
-        const uint32_t lo = (uint32_t)(uint64_t)kk, hi = (uint32_t)((uint64_t)kk >> 32);
-        const uint32_t olo = (uint32_t)__shfl_xor((int)lo, j), ohi = (uint32_t)__shfl_xor((int)hi, j);
+        const uint32_t klo = (uint32_t)(uint64_t)kk, khi = (uint32_t)((uint64_t)kk >> 32);
+        const uint32_t olo = (uint32_t)__shfl_xor((int)klo, j), ohi = (uint32_t)__shfl_xor((int)khi, j);
         other = (int64_t)(((uint64_t)ohi << 32) | olo);
       }
       const bool up = (t & k) == 0, lower = (t & j) == 0;
       kk = (lower == up) ? (kk < other ? kk : other) : (kk > other ? kk : other);
     }
   key[t] = kk;
-  __syncthreads();
-  // every sorted position's first row value is loaded up front (one load per position, all in
-  // flight together; a run's further rows — points in several slots, rare — are added after);
-  // round 2's loop issued one dependent load per position: 32 serial memory round trips
+  // the sorted positions of this part's points: [p0, p1) (sentinels sort last, above every point)
+  const int p0 = __syncthreads_count((kk >> 9) < lo);
+  const int p1 = __syncthreads_count((kk >> 9) < hi);
+  // every owned position's first row value is loaded up front (all in flight together; a run's
+  // further rows — points in several slots, rare — are added after)
   const int c = t & (kC - 1);
-  constexpr int kPer = kMaxS / (kScT / kC);
+  constexpr int kStep = kScT / kC;  // positions per pass of the block
+  constexpr int kPer = kMaxS / kStep;
   float v[kPer];
 #pragma unroll
   for (int i = 0; i < kPer; ++i) {
-    const int64_t k = key[t / kC + (kScT / kC) * i];
-    v[i] = dx[(k == kNone ? 0 : (k & 511)) * kC + c];  // slot 0's row stands in for a sentinel
+    const int p = p0 + t / kC + kStep * i;
+    const int64_t k = key[p < p1 ? p : p0];
+    v[i] = dx[(p < p1 ? (k & 511) : 0) * kC + c];  // slot 0's row stands in past the range
   }
 #pragma unroll
   for (int i = 0; i < kPer; ++i) {
-    const int p = t / kC + (kScT / kC) * i;
+    const int p = p0 + t / kC + kStep * i;
+    if (p >= p1) break;
     const int64_t k = key[p];
-    if (k == kNone) break;  // sentinels sort last
     const int64_t idx = k >> 9;
     if (p > 0 && (key[p - 1] >> 9) == idx) continue;  // not the head of its run
     float s = v[i];
@@ -397,7 +439,7 @@ extern "C" int pk_nce_loss(const float* f1, const int64_t* st1, const float* f2,
                      S, inv_t, prenorm, lse, term, loss, g2 ? dx_rows + (size_t)B * S * kC : nullptr);
   PK_CHECK_LAUNCH();
   if (g1) {
-    hipLaunchKernelGGL(nce_scatter_kernel, dim3(B, 2), dim3(kScT), 0, s, pairs, cap, rows, valid, S, N1, N2, dx_rows,
+    hipLaunchKernelGGL(nce_scatter_kernel, dim3(B, 2, kScP), dim3(kScT), 0, s, pairs, cap, rows, valid, S, N1, N2, dx_rows,
                        g1, g2);
     PK_CHECK_LAUNCH();
   }

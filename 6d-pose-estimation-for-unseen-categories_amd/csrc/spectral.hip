@@ -358,20 +358,73 @@ __global__ __launch_bounds__(1024) void spec_combine4_kernel(float* __restrict__
 // loads Phi[r][16 t + 4 g .. +3] (t < 4), so K-step (t, e) pairs A[i][g] = Phi[r][16 t + 4 g + e]
 // with B[g][j] = coef[16 t + 4 g + e][4 j + ct] (one ds_read_b128 of the LDS copy of coef gives
 // all 4 tiles); D register rr of tile ct in lane (j, g) is y[r0 + 16 w + 4 g + rr][4 j + ct].
+// FUSED (the forward): no combine launch — every block sums its crop's S partial slabs itself
+// (fp64, slab order: spec_combine4_kernel's arithmetic, so raw / scaled are bit-identical),
+// scales by exp(-lambda t) into its LDS copy of the coefficients, and the crop's block 0 writes
+// raw (saved for the backward) and, for crop 0, the clamped diffusion time. The slabs are read
+// from L2 (a crop's row blocks share an XCD), so the partials cross HBM once, when written.
+struct SpecFuse {
+  const float* part;
+  int S, clamp_t, write_t, pad;
+  const float* evals;
+  float* t;
+  float* raw;
+};
+
+template <bool FUSED>
 __global__ __launch_bounds__(256) void spec_expand_mfma_kernel(const float* __restrict__ evecs,
                                                                const float* __restrict__ coef,
                                                                const float* __restrict__ mass, int N,
                                                                float* __restrict__ y, int ldy, int accumulate,
                                                                const float* __restrict__ gtb, int64_t gt_stride,
-                                                               float* __restrict__ gt) {
+                                                               float* __restrict__ gt, SpecFuse fz) {
   __shared__ float4 scoef[kKC * kKC / 4];  // [k][c / 4]
   // a crop's row blocks on one XCD: its 16 KB of coefficients come from HBM once per crop, not
   // once per XCD (the round-5 PMC pass counted the re-fetches at ~15 MB per launch)
   const int3 lb = pk::xcd_block3();
   const int tile = lb.x, b = lb.y, tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63, u = l & 15, g = l >> 4;
-  const float* __restrict__ cb = coef + (int64_t)b * kKC * kKC;
-  {
+  if constexpr (FUSED) {
+    // thread: coefficients (k, 4 c4 .. 4 c4 + 3) for e = tid + 256 j, k = e >> 4, c4 = e & 15
+    constexpr int PER = kKC * kKC / 4 / 256;
+    const float* pb = fz.part + (int64_t)b * fz.S * kKC * kKC;
+    double v[PER][4];
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[j][q] = 0.0;
+    for (int s0 = 0; s0 < fz.S; ++s0) {
+      float4 ld[PER];
+#pragma unroll
+      for (int j = 0; j < PER; ++j) ld[j] = reinterpret_cast<const float4*>(pb + (int64_t)s0 * kKC * kKC)[tid + 256 * j];
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        v[j][0] += (double)ld[j].x;
+        v[j][1] += (double)ld[j].y;
+        v[j][2] += (double)ld[j].z;
+        v[j][3] += (double)ld[j].w;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int e = tid + 256 * j, k = e >> 4, c4 = e & 15;
+      const float lam = fz.evals[b * kKC + k];
+      float o[4], r[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 4 * c4 + q;
+        const float tc = fz.clamp_t ? fmaxf(fz.t[c], 1e-8f) : fz.t[c];
+        const float E = expf(-lam * tc);
+        r[q] = (float)v[j][q];
+        o[q] = E * r[q];
+      }
+      scoef[e] = make_float4(o[0], o[1], o[2], o[3]);
+      if (tile == 0 && fz.raw != nullptr)
+        reinterpret_cast<float4*>(fz.raw + (int64_t)b * kKC * kKC)[e] = make_float4(r[0], r[1], r[2], r[3]);
+    }
+    if (fz.write_t && tile == 0 && b == 0 && tid < kKC) fz.t[tid] = fmaxf(fz.t[tid], 1e-8f);
+  } else {
+    const float* __restrict__ cb = coef + (int64_t)b * kKC * kKC;
     float4 cv[kKC * kKC / 4 / 256];
 #pragma unroll
     for (int j = 0; j < kKC * kKC / 4 / 256; ++j) cv[j] = reinterpret_cast<const float4*>(cb)[tid + 256 * j];
@@ -477,6 +530,13 @@ extern "C" int pk_spectral_diffusion(const float* in, int ld_in, const float* ma
     hipLaunchKernelGGL(spec_reduce_mfma_kernel, dim3(S, B), dim3(256), 0, s, in, ld_in,
                        mode == 0 ? mass : nullptr, evecs, N, S, work);
   PK_CHECK_LAUNCH();
+  if (!spec_scalar() && mode == 0) {  // forward: the combine inside the expand (no third launch)
+    SpecFuse fz{work, S, clamp_t, (int)(clamp_t != 0), 0, evals, t, raw};
+    hipLaunchKernelGGL(spec_expand_mfma_kernel<true>, dim3((N + 63) / 64, B), dim3(256), 0, s, evecs, scaled,
+                       nullptr, N, out, ld_out, accumulate, work, (int64_t)S * kKC * kKC, nullptr, fz);
+    PK_CHECK_LAUNCH();
+    return PK_OK;
+  }
   if (spec_scalar())
     hipLaunchKernelGGL(spec_combine_kernel, dim3(B), dim3(1024), 0, s, work, S, evals, t, clamp_t,
                        (int)(clamp_t && mode == 0), raw, scaled, mode == 1 ? saved : nullptr, (int)(mode == 1));
@@ -489,9 +549,9 @@ extern "C" int pk_spectral_diffusion(const float* in, int ld_in, const float* ma
                        mode == 1 ? mass : nullptr, N, out, ld_out, accumulate, work, (int64_t)S * kKC * kKC,
                        mode == 1 ? gt : nullptr);
   else
-    hipLaunchKernelGGL(spec_expand_mfma_kernel, dim3((N + 63) / 64, B), dim3(256), 0, s, evecs, scaled,
+    hipLaunchKernelGGL(spec_expand_mfma_kernel<false>, dim3((N + 63) / 64, B), dim3(256), 0, s, evecs, scaled,
                        mode == 1 ? mass : nullptr, N, out, ld_out, accumulate, work, (int64_t)S * kKC * kKC,
-                       mode == 1 ? gt : nullptr);
+                       mode == 1 ? gt : nullptr, SpecFuse{});
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

@@ -133,7 +133,8 @@ int pk_offsets_from_counts(const int64_t* counts, int B, int64_t* off, void* str
  *   slice of a wider concatenation buffer), mass [B,N], evecs [B,N,K], evals [B,K], t [C];
  *   clamp_t: use max(t, 1e-8), and in mode 0 write it back into t (the reference's in-place
  *   diffusion_time.clamp_(min=1e-8) before every diffusion);
- *   work f32 [B, ceil(N/64), K, C]; raw (mode 0, may be NULL) / scaled [B,K,C];
+ *   work f32 [B, ceil(N/64), K, C]; raw (mode 0, may be NULL) / scaled [B,K,C] (scratch: mode 0
+ *   forms the coefficients inside the expand pass and leaves it unwritten);
  *   saved = raw of the forward (mode 1); gt [C] (mode 1, summed over crops in crop order);
  *   accumulate: out += result (a gradient summed into an existing one) instead of out = result */
 int pk_spectral_diffusion(const float* in, int ld_in, const float* mass, const float* evecs, const float* evals,
