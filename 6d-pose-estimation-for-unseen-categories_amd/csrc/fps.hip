@@ -27,6 +27,14 @@
 
 namespace {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float vmin_f32(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 constexpr int kFpsMaxLds = 13312;  // points whose SoA copy fits in LDS (156 KiB)
 
 template <int NT, int PPT, bool LDS>
@@ -418,32 +426,36 @@ __global__ __launch_bounds__(NT) void fps_flat_kernel(
   float* sz = sy + n_pad;
 
   const float inf = __builtin_huge_valf();
-  float px[PPT], py[PPT], pz[PPT], pd[PPT];
+  // the lane's points in pairs (packed f32 arithmetic: v_pk_add / v_pk_mul round each element
+  // like the scalar ops); an odd PPT's last pair carries an empty slot (distance -1)
+  constexpr int PH = (PPT + 1) / 2;
+  f32x2 X[PH], Y[PH], Z[PH], D[PH];
   float bx0 = inf, bx1 = -inf, by0 = inf, by1 = -inf, bz0 = inf, bz1 = -inf;
   const int i0 = tid * PPT;
   if (n > 0) {  // unconditional loads at a clamped index (block-uniform guard: empty crop)
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
       const int ic = i0 + k < n ? i0 + k : 0;
-      px[k] = p[3 * ic + 0];
-      py[k] = p[3 * ic + 1];
-      pz[k] = p[3 * ic + 2];
+      X[k >> 1][k & 1] = p[3 * ic + 0];
+      Y[k >> 1][k & 1] = p[3 * ic + 1];
+      Z[k >> 1][k & 1] = p[3 * ic + 2];
     }
   }
 #pragma unroll
-  for (int k = 0; k < PPT; ++k) {
-    const bool ok = i0 + k < n;
-    px[k] = ok ? px[k] : 0.f;
-    py[k] = ok ? py[k] : 0.f;
-    pz[k] = ok ? pz[k] : 0.f;
-    pd[k] = ok ? 1e10f : -1.f;  // empty slot: min(-1, d >= 0) keeps it at -1, never selected
+  for (int k = 0; k < 2 * PH; ++k) {
+    const bool ok = k < PPT && i0 + k < n;
+    const float x = ok ? X[k >> 1][k & 1] : 0.f, y = ok ? Y[k >> 1][k & 1] : 0.f, z = ok ? Z[k >> 1][k & 1] : 0.f;
+    X[k >> 1][k & 1] = x;
+    Y[k >> 1][k & 1] = y;
+    Z[k >> 1][k & 1] = z;
+    D[k >> 1][k & 1] = ok ? 1e10f : -1.f;  // empty slot: min(-1, d >= 0) keeps it at -1, never selected
     if (ok) {
-      sx[i0 + k] = px[k];
-      sy[i0 + k] = py[k];
-      sz[i0 + k] = pz[k];
-      bx0 = fminf(bx0, px[k]); bx1 = fmaxf(bx1, px[k]);
-      by0 = fminf(by0, py[k]); by1 = fmaxf(by1, py[k]);
-      bz0 = fminf(bz0, pz[k]); bz1 = fmaxf(bz1, pz[k]);
+      sx[i0 + k] = x;
+      sy[i0 + k] = y;
+      sz[i0 + k] = z;
+      bx0 = fminf(bx0, x); bx1 = fmaxf(bx1, x);
+      by0 = fminf(by0, y); by1 = fmaxf(by1, y);
+      bz0 = fminf(bz0, z); bz1 = fmaxf(bz1, z);
     }
   }
   if (tid < 3) keys[tid] = 0ull;
@@ -465,20 +477,24 @@ __global__ __launch_bounds__(NT) void fps_flat_kernel(
     const bool need = lval && !(lb * 0.99999809f >= bd);
     if (__ballot(need)) {  // wave-uniform
       if (need) {
+        const f32x2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
 #pragma unroll
-        for (int k = 0; k < PPT; ++k) {
-          const float dx = px[k] - cx;
-          const float dy = py[k] - cy;
-          const float dz = pz[k] - cz;
-          const float d = (dx * dx + dy * dy) + dz * dz;  // no contraction (TU flag)
-          pd[k] = fminf(pd[k], d);
+        for (int j = 0; j < PH; ++j) {
+          const f32x2 dx = X[j] - c2x;
+          const f32x2 dy = Y[j] - c2y;
+          const f32x2 dz = Z[j] - c2z;
+          const f32x2 d = (dx * dx + dy * dy) + dz * dz;  // no contraction (TU flag)
+          // plain v_min_f32: fminf would canonicalise the loop-carried D first (one v_max per point;
+          // both operands are finite here, so the result is fminf's)
+          D[j][0] = vmin_f32(D[j][0], d[0]);
+          D[j][1] = vmin_f32(D[j][1], d[1]);
         }
-        float m = pd[0];
+        float m = D[0][0];
 #pragma unroll
-        for (int k = 1; k < PPT; ++k) m = fmaxf(m, pd[k]);
+        for (int k = 1; k < PPT; ++k) m = fmaxf(m, D[k >> 1][k & 1]);
         int kk = PPT - 1;
 #pragma unroll
-        for (int k = PPT - 2; k >= 0; --k) kk = pd[k] == m ? k : kk;  // first k at the max
+        for (int k = PPT - 2; k >= 0; --k) kk = D[k >> 1][k & 1] == m ? k : kk;  // first k at the max
         bd = m;
         bk = kk;
       }

@@ -10,16 +10,20 @@
 // diagonal, their backwards, scatter-adds); here it is three launches:
 //   zero(g1, g2) -> row pass -> column pass.
 // Each pass is two f32 MFMA contractions (v_mfma_f32_16x16x4f32: exact f32, an fmaf chain
-// over the 32 channels in order, so both passes see bit-identical distances), one wave per
-// 16 own rows (4 waves per block; grid S/64 x B), the other side's S <= 512 normalized
-// vectors staged once per block in LDS:
-//   G^T[512 x 16] = O[512 x 32] . V^T[32 x 16]: lane (row r = lane % 16, group g = lane / 16)
-//     holds its row's distances to partners 16 t + 4 g + v (t < 32, v < 4) in 128 VGPRs;
-//   row pass: max / sum over a row = in-lane over 128, then xor 16, 32 -> lse[a],
+// over the 32 channels in order, so both passes see bit-identical distances), two waves per
+// 16 own rows, each over one half of the partners (8 waves per block = 4 row groups x 2 halves,
+// two waves per SIMD so one's MFMAs run under the other's exp / sqrt; grid S/64 x B), the other
+// side's S <= 512 normalized vectors staged once per block in LDS:
+//   G^T[256 x 16] = O[half x 32] . V^T[32 x 16]: lane (row r = lane % 16, group g = lane / 16)
+//     holds its row's distances to partners 16 t + 4 g + v (t in the half's 16 tiles, v < 4) in
+//     64 VGPRs;
+//   row pass: max / sum over a row = in-lane over 64, then xor 16, 32, then the two halves
+//     through LDS (min exactly; sums half 0 + half 1) -> lse[a],
 //     term[a] = lse[a] - logit[a][a];  column pass: the softmax rows' lse from the row pass;
 //   r[a][o] = dL/dd = -(softmax - [o == a]) / (n_valid t d)  (0 where d == 0 or invalid),
 //     written over the distances (the A operand of the next product, same register layout);
-//   dQ[16 x 32] = R[16 x 512] . O[512 x 32]  (k-slot g of step (t, v) = partner 16 t + 4 g + v);
+//   dQ[16 x 32] = R[16 x 512] . O[512 x 32]  (k-slot g of step (t, v) = partner 16 t + 4 g + v;
+//     per half, half 1's partial added to half 0's through LDS);
 //   dq_a = q_a sum_o r - (R O)_a  (torch's _euclidean_dist_backward), then F.normalize's
 //   backward, written as slot a's gradient row dx[a] (scratch [B, S, 32]).
 // A CAD / crop point can sit in several pairs (torch's gather backward scatter_adds them); a
@@ -46,8 +50,11 @@ constexpr int kC = 32;           // feature width (n_feat, config/dpfm_orig.yaml
 constexpr int kMaxS = 512;       // nce_num_pairs (config/dpfm_orig.gin:58)
 constexpr int kPT = kMaxS / 16;  // partner tiles of 16
 constexpr int kRowsPerWave = 16;
-constexpr int kWaves = 4;  // one block per CU (LDS), one wave per SIMD
-constexpr int kTile = kRowsPerWave * kWaves;  // rows per block
+constexpr int kGroups = 4;  // row groups of 16 per block
+constexpr int kHalves = 2;  // partner halves: wave (group, half) takes partners [256 half, 256 half + 256)
+constexpr int kWaves = kGroups * kHalves;  // one block per CU (LDS), two waves per SIMD
+constexpr int kTile = kRowsPerWave * kGroups;  // rows per block
+constexpr int kHT = kPT / kHalves;  // partner tiles per wave
 constexpr int kLd = kC + 2;  // LDS row stride: the G operand reads (row r, channel 4 s + g) hit distinct banks
 
 struct FeatView {  // f[b, n, c] = base[b * sb + n * sn + c * sc] (rows or channels-first storage)
@@ -100,6 +107,8 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
   __shared__ int64_t widx_s[kTile];  // their feature indices
   __shared__ int64_t ooff_s[kMaxS];  // the other side's row offsets (-1: invalid slot)
   __shared__ int nv_s[kWaves];
+  __shared__ float xst_s[2][kGroups][kHalves][16];       // the row statistics of each half (min d, sum)
+  __shared__ float xacc_s[kGroups][9][64];               // half 1's (R O) partial and row sums
   const int b = blockIdx.y;
   const int lane = pk::lane_id(), w = pk::wave_id();
   const uint8_t* __restrict__ vb = valid + (int64_t)b * S;
@@ -205,27 +214,30 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
     t = pk::wave_sum_f32(t);
     if (lane == 0) loss[b] = t * sc;
   }
-  if (COLS && dx_own == nullptr) return;
-  const int a0 = blockIdx.x * kTile + w * kRowsPerWave;  // wave-uniform; no barrier below
-  if (a0 >= S) return;
+  if (COLS && dx_own == nullptr) return;  // block-uniform
+  // wave (row group rg, partner half hf); every wave runs to the end (the halves meet at
+  // barriers): a row group past S computes on its zero rows (ok = false) and stores nothing
+  const int rg = w % kGroups, hf = w / kGroups;
+  const int a0 = blockIdx.x * kTile + rg * kRowsPerWave;
   const int r = lane & 15, g = lane >> 4;
-  const int tr = w * kRowsPerWave + r;  // the lane's row within the staged tile
+  const int tr = rg * kRowsPerWave + r;  // the lane's row within the staged tile
   const int a = a0 + r;
   const bool ok = a < S && wn_s[tr] >= 0.f;
   const float vn = vn_s[tr];
+  const int t0 = hf * kHT;
 
-  // d[t][v]: distance to partner 16 t + 4 g + v (-1: no logit there)
+  // d[t][v]: distance to partner 16 (t0 + t) + 4 g + v (-1: no logit there)
   float bv[kC / 4];
 #pragma unroll
   for (int s = 0; s < kC / 4; ++s) bv[s] = Ws[tr * kLd + 4 * s + g];
-  float d[kPT][4];
+  float d[kHT][4];
 #pragma unroll
-  for (int t = 0; t < kPT; ++t) {
+  for (int t = 0; t < kHT; ++t) {
     fx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < kC / 4; ++s)
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Os[(16 * t + r) * kLd + 4 * s + g], bv[s], acc, 0, 0, 0);
-    const float4 on = *reinterpret_cast<const float4*>(&on_s[16 * t + 4 * g]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Os[(16 * (t0 + t) + r) * kLd + 4 * s + g], bv[s], acc, 0, 0, 0);
+    const float4 on = *reinterpret_cast<const float4*>(&on_s[16 * (t0 + t) + 4 * g]);
     const float onv[4] = {on.x, on.y, on.z, on.w};
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
@@ -233,43 +245,50 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
       d[t][v] = ok && onv[v] < __builtin_huge_valf() ? __builtin_amdgcn_sqrtf(d2) : -1.f;  // v_sqrt_f32 (1 ulp)
     }
   }
-  // row pass: the row's softmax statistics; max logit = -(min d) / t exactly (monotone rounding)
+  // row pass: the row's softmax statistics over both halves (exchanged through LDS: the min
+  // exactly, the sums as half 0 + half 1); max logit = -(min d) / t exactly (monotone rounding)
   float mx = 0.f, is = 0.f, lse_a = 0.f;
   if (!COLS) {
     float dm = __builtin_huge_valf();
 #pragma unroll
-    for (int t = 0; t < kPT; ++t)
+    for (int t = 0; t < kHT; ++t)
 #pragma unroll
       for (int v = 0; v < 4; ++v)
         if (d[t][v] >= 0.f) dm = fminf(dm, d[t][v]);
     dm = fminf(dm, __shfl_xor(dm, 16));
     dm = fminf(dm, __shfl_xor(dm, 32));
+    if (g == 0) xst_s[0][rg][hf][r] = dm;
+    __syncthreads();
+    dm = fminf(xst_s[0][rg][0][r], xst_s[0][rg][1][r]);
     mx = ok ? -dm * inv_t : 0.f;
     float s = 0.f;
 #pragma unroll
-    for (int t = 0; t < kPT; ++t)
+    for (int t = 0; t < kHT; ++t)
 #pragma unroll
       for (int v = 0; v < 4; ++v) s += d[t][v] >= 0.f ? __expf(-d[t][v] * inv_t - mx) : 0.f;
     s += __shfl_xor(s, 16);
     s += __shfl_xor(s, 32);
+    if (g == 0) xst_s[1][rg][hf][r] = s;
+    __syncthreads();
+    s = xst_s[1][rg][0][r] + xst_s[1][rg][1][r];
     is = __builtin_amdgcn_rcpf(s);
     lse_a = mx + __logf(s);
   }
-  // r = dL/dd over the distances; the row pass also picks the diagonal logit
+  // r = dL/dd over the distances; the row pass also picks the diagonal logit (in half a / 256)
   const float k_r = -sc * inv_t;
   float rs = 0.f, ldg = 0.f;
 #pragma unroll
-  for (int t = 0; t < kPT; ++t) {
+  for (int t = 0; t < kHT; ++t) {
     float lo[4] = {0.f, 0.f, 0.f, 0.f};
     if (COLS) {
-      const float4 l4 = *reinterpret_cast<const float4*>(&lse_s[16 * t + 4 * g]);
+      const float4 l4 = *reinterpret_cast<const float4*>(&lse_s[16 * (t0 + t) + 4 * g]);
       lo[0] = l4.x; lo[1] = l4.y; lo[2] = l4.z; lo[3] = l4.w;
     }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const float dd = d[t][v];
       const float lg = -dd * inv_t;
-      const bool diag = 16 * t + 4 * g + v == a;
+      const bool diag = 16 * (t0 + t) + 4 * g + v == a;
       const float p = dd >= 0.f ? (COLS ? __expf(lg - lo[v]) : __expf(lg - mx) * is) : 0.f;
       if (!COLS && diag) ldg = lg;
       const float gg = p - (diag ? 1.f : 0.f);
@@ -283,28 +302,43 @@ __global__ __launch_bounds__(64 * kWaves) void nce_pass_kernel(
   if (!COLS) {
     ldg += __shfl_xor(ldg, 16);  // one group holds it, the others add zeros
     ldg += __shfl_xor(ldg, 32);
-    if (g == 0 && a < S) {
+    if (hf == ((a0 / (16 * kHT)) & 1) && g == 0 && a < S) {  // the half holding the row's diagonal
       lse[(int64_t)b * S + a] = ok ? lse_a : 0.f;
       term[(int64_t)b * S + a] = ok ? lse_a - ldg : 0.f;
     }
-    if (dx_own == nullptr) return;
+    if (dx_own == nullptr) return;  // block-uniform
   }
-  // (R O)[row 4 g + v][channel 16 h + r]
+  // (R O)[row 4 g + v][channel 16 h + r] over this half's partners
   fx4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-  for (int t = 0; t < kPT; ++t)
+  for (int t = 0; t < kHT; ++t)
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const float* orow = &Os[(16 * t + 4 * g + v) * kLd + r];
+      const float* orow = &Os[(16 * (t0 + t) + 4 * g + v) * kLd + r];
 #pragma unroll
       for (int h = 0; h < 2; ++h) acc2[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(d[t][v], orow[16 * h], acc2[h], 0, 0, 0);
     }
+  // half 1 hands its partial product and row sums to half 0 (added as half 0 + half 1)
+  if (hf == 1) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) xacc_s[rg][4 * h + v][lane] = acc2[h][v];
+    xacc_s[rg][8][lane] = rs;
+  }
+  __syncthreads();
+  if (hf == 1) return;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) acc2[h][v] += xacc_s[rg][4 * h + v][lane];
+  rs += xacc_s[rg][8][lane];
   // dq, then F.normalize backward: (dv - v (v . dv)) / n  (dv / 1e-12 when clamped)
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
     const int rw = 4 * g + v;               // row of this accumulator slot
     const float rs_w = __shfl(rs, rw);      // lane rw holds row rw's sum (group 0)
-    const int trw = w * kRowsPerWave + rw;
+    const int trw = rg * kRowsPerWave + rw;
     const bool okw = a0 + rw < S && wn_s[trw] >= 0.f;
     const float nw = wn_s[trw];
     float vc[2], dv[2];
