@@ -379,12 +379,12 @@ __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const
 // scan gives every term's S before it, and the first term that ties, is >= s, or would reach
 // 2^53 is a break: s = (S + P) U exactly up to it, then that one term is added by the FPU
 // (the true sequential step) and the next round restarts after it. Breaks happen at binade
-// crossings (~log2 n of them: the first 256 terms are added sequentially, where most
+// crossings (~log2 n of them: the first 1024 terms are added sequentially from LDS, where most
 // crossings are) and at exact ties, so a crop takes a handful of rounds instead of n
 // dependent fp64 additions.
 constexpr int kStatThreads = 1024;
 constexpr int kSeqPer = 8;     // terms per thread per round
-constexpr int kSeqWarm = 256;  // first terms added one by one
+constexpr int kSeqWarm = 1024;  // first terms added one by one (one per thread loaded into LDS)
 
 struct SeqShared {
   double s;
@@ -392,23 +392,20 @@ struct SeqShared {
   int brk;
   int64_t part[kStatThreads / 64];
   double s_next;
+  double warm[kSeqWarm];  // the first terms, loaded by all threads at once
 };
 
 template <class F>
 __device__ double seq_sum_exact(F term, int n, SeqShared& sh) {
   const int tid = threadIdx.x, lane = pk::lane_id(), w = pk::wave_id();
-  if (tid == 0) {  // the first terms one by one, 16 loads in flight at a time (same order)
+  // the first terms one by one (same order) from LDS: every thread loads one, so the warm-up
+  // costs one memory round trip (round 4's thread 0 waited for 16 batches of 16 loads)
+  const int m = min(n, kSeqWarm);
+  if (tid < m) sh.warm[tid] = term(tid);
+  __syncthreads();
+  if (tid == 0) {
     double s = 0.0;
-    const int m = min(n, kSeqWarm);
-    int k = 0;
-    for (; k + 16 <= m; k += 16) {
-      double tv[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) tv[i] = term(k + i);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s = s + tv[i];
-    }
-    for (; k < m; ++k) s = s + term(k);
+    for (int k = 0; k < m; ++k) s = s + sh.warm[k];
     sh.s = s;
     sh.k = m;
   }

@@ -29,6 +29,13 @@ namespace {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// row b's entries past npoint[b] (the whole row for an empty crop) are written as 0 by the
+// kernel itself, so the caller's output needs no fill launch
+__device__ __forceinline__ void fps_zero_tail(int64_t* __restrict__ out, int out_stride, int b, int np) {
+  int64_t* __restrict__ o = out + (int64_t)b * out_stride;
+  for (int i = (np > 0 ? np : 0) + (int)threadIdx.x; i < out_stride; i += (int)blockDim.x) o[i] = 0;
+}
+
 __device__ __forceinline__ float vmin_f32(float a, float b) {
   float r;
   asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -78,6 +85,7 @@ __global__ __launch_bounds__(NT) void fps_kernel(
       pd[k] = -1.f;  // empty slot: min(-1, d >= 0) keeps it at -1, never selected
     }
   }
+  fps_zero_tail(out, out_stride, b, np);
   if (n <= 0 || np <= 0) return;
   __syncthreads();
 
@@ -210,6 +218,7 @@ __global__ __launch_bounds__(NT) void fps_pruned_kernel(
       }
     }
   }
+  fps_zero_tail(out, out_stride, b, np);
   if (n <= 0 || np <= 0) return;
   __syncthreads();
 
@@ -316,6 +325,7 @@ __global__ __launch_bounds__(NT) void fps_lane_kernel(
     }
   }
   const bool lval = i0 < n;
+  fps_zero_tail(out, out_stride, b, np);
   if (n <= 0 || np <= 0) return;
 
   // the lane's current maximum running distance, its point and that point's coordinates
@@ -459,6 +469,7 @@ __global__ __launch_bounds__(NT) void fps_flat_kernel(
     }
   }
   if (tid < 3) keys[tid] = 0ull;
+  fps_zero_tail(out, out_stride, b, np);
   if (n <= 0 || np <= 0) return;  // block-uniform
   const bool lval = i0 < n;
   float bd = lval ? 1e10f : -1.f;  // the lane's max running distance, first reached at k = bk

@@ -35,7 +35,7 @@ def fps_packed(xyz: torch.Tensor, offsets: torch.Tensor, nmax: int, start: torch
     """
     assert xyz.dtype == torch.float32 and xyz.dim() == 2 and xyz.shape[1] == 3
     B = offsets.numel() - 1
-    out = torch.zeros((B, out_stride), dtype=torch.int64, device=xyz.device)
+    out = torch.empty((B, out_stride), dtype=torch.int64, device=xyz.device)  # the kernel zero-fills the tails
     call("pk_fps", ptr(xyz), ptr(offsets), B, int(nmax), ptr(start.to(torch.int32).contiguous()),
          ptr(npoint.to(torch.int32).contiguous()), ptr(out), int(out_stride), _lib.stream(xyz.device),
          work=("hbm", 12 * xyz.shape[0] + 8 * B * int(out_stride)))

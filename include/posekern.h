@@ -31,7 +31,8 @@ extern "C" {
  * (the random start becomes the explicit start[b]).
  *   xyz    f32 [T,3] packed crops, off int64 [B+1], nmax = max crop size
  *   start  int32 [B] first centroid, npoint int32 [B] samples per crop
- *   out    int64 [B, out_stride]; row b holds npoint[b] indices local to crop b
+ *   out    int64 [B, out_stride]; row b holds npoint[b] indices local to crop b, then zeros
+ *          (written by the call: out needs no initialisation)
  * Bit-exact: fp32 ((dx²+dy²)+dz²), strict-< update, first-index argmax. */
 int pk_fps(const float* xyz, const int64_t* off, int B, int nmax, const int32_t* start,
            const int32_t* npoint, int64_t* out, int out_stride, void* stream);
