@@ -972,23 +972,24 @@ __global__ __launch_bounds__(64) void cgt_solve_kernel(const double* __restrict_
   bool used = !row_ok;
   int var = -1;
   double pmin = __builtin_inf(), pmax = 0.0;
+  // fully unrolled: G[r][k] is a static register (round 4 selected it with 30 fp64 cndmasks per
+  // step), and the pivot search is two DPP max reductions of the |G[r][k]| bit pattern instead of
+  // five ds_bpermute butterflies of (value, row) pairs
+#pragma unroll
   for (int k = 0; k < kF; ++k) {
-    // pivot: max |G[r][k]| over unused rows (half-0 lanes), lowest row on ties
-    double ak = 0.0;  // a[k] through static indices (no scratch)
-#pragma unroll
-    for (int c = 0; c < kF; ++c) ak = c == k ? a[c] : ak;
-    double key = (h == 0 && !used) ? fabs(ak) : -1.0;
-    int who = r;
-#pragma unroll
-    for (int off = 16; off >= 1; off >>= 1) {
-      const double ok = __shfl_xor(key, off);
-      const int ow = __shfl_xor(who, off);
-      if (ok > key || (ok == key && ow < who)) {
-        key = ok;
-        who = ow;
-      }
-    }
-    const int p = __shfl(who, 0);
+    // pivot: max |G[r][k]| over unused rows (half-0 lanes), lowest row on ties. |x| >= 0 orders
+    // as its bit pattern; candidates carry hi + 1 so no candidate ties an excluded lane's 0 (a
+    // NaN, which the elimination's pmin / pmax check sends to the fallback path, orders last)
+    const double ak = a[k];
+    const double fa = fabs(ak);
+    const bool cand = h == 0 && !used;
+    const uint64_t bits = (uint64_t)__double_as_longlong(fa == fa ? fa : 0.0);
+    const uint32_t khi = cand ? (uint32_t)(bits >> 32) + 1u : 0u;
+    const uint32_t mhi = pk::wave_max_u32_s(khi);
+    const uint32_t klo = (cand && khi == mhi) ? (uint32_t)bits : 0u;
+    const uint32_t mlo = pk::wave_max_u32_s(klo);
+    const uint64_t win = __ballot(cand && khi == mhi && klo == mlo);
+    const int p = win ? __ffsll((unsigned long long)win) - 1 : 0;  // lane = row (half 0)
     const double pivot = __shfl(ak, p);  // G[p][k] from half 0
     pmin = fmin(pmin, fabs(pivot));
     pmax = fmax(pmax, fabs(pivot));

@@ -596,6 +596,9 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
   if (nmax <= 8192) return launch_fps_flat<1024, 8>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
   // up to the LDS bound (3 x 13312 floats + the key words = 156 KiB): the bench's 640x480 crops
   // (8-9k points) ran the pruned kernel at 0.78 us per iteration; the flat one measured 0.53 at 1024 threads
+  // 10 points per lane up to 10,240 (the bench's synthetic frames: up to 9,289 mask pixels): an
+  // updating wave's distance / argmax work scales with the points per lane
+  if (nmax <= 10240) return launch_fps_flat<1024, 10>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
   if (nmax <= kFpsMaxLds) return launch_fps_flat<1024, 13>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
 #endif
 #define PK_FPS(NT, PPT) return launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s)

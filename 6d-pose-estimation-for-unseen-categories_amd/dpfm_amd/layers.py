@@ -25,8 +25,27 @@ FOLD_RELU = True  # fold a producer layer's ReLU backward into the consumer's in
 # by tensor object: autograd hands the producer a transposed view of the consumer's dx for
 # channels-first layers (a new Python object, same storage and version counter). The version
 # check rejects a dx that autograd has since accumulated another consumer's gradient into (in
-# place, same pointer) and a stale entry whose address the caching allocator has reused.
+# place, same pointer). The entry holds dx itself, so its memory cannot be handed to another
+# tensor while the entry exists (an address match is the same storage), and the producer's
+# backward pops it (a stale entry of an earlier backward could otherwise match a new tensor at a
+# reused address with the same version 0 and skip a ReLU backward).
 _MASKED = {}
+
+
+def _masked_put(dx, mask) -> None:
+    """Record that dx already carries the ReLU mask `mask` (an entry whose producer never runs
+    its backward, e.g. one that needs no input gradient, is dropped with the rest past 512)."""
+    if len(_MASKED) > 512:
+        _MASKED.clear()
+    _MASKED[(dx.data_ptr(), mask.data_ptr())] = (dx._version, dx)
+
+
+def _masked_pop(dy, y) -> bool:
+    """True when the consumer of `dy` already applied the ReLU mask `y` (and drops the entry)."""
+    if not _MASKED:
+        return False
+    ent = _MASKED.pop((dy.data_ptr(), y.data_ptr()), None)
+    return ent is not None and ent[0] == dy._version
 
 
 class GroupedWgrad:
@@ -141,7 +160,7 @@ class _PointwiseFn(torch.autograd.Function):
         w2 = weight.view(weight.shape[0], -1)
         cf = ctx.cf
         dy = dy.contiguous()
-        if ctx.relu and _MASKED.get((dy.data_ptr(), y.data_ptr())) != dy._version:
+        if ctx.relu and not _masked_pop(dy, y):
             # the fused ReLU's backward (aten's ReluBackward: threshold_backward on the output),
             # unless the consuming layer already applied it in its input-gradient epilogue
             dy = torch.ops.aten.threshold_backward(dy, y, 0.0)
@@ -160,13 +179,13 @@ class _PointwiseFn(torch.autograd.Function):
                 ops.linear_ex(dy, w2, None, 0, dy.numel() // Cout, 0, Cout, Cin, y=dx, transw=True,
                               mask=x if ctx.in_relu else None, pre=y, pre_out=dz)
             if ctx.in_relu:
-                _MASKED[(dx.data_ptr(), x.data_ptr())] = dx._version
+                _masked_put(dx, x)
             dy = dz
         elif ctx.needs_input_grad[0]:
             # dy W (rows) / W^T dy (cf); with in_relu the producer's ReLU backward is folded in
             dx = ops.linear_fwd(dy, w2, None, channels_first=cf, transw=True, mask=x if ctx.in_relu else None)
             if ctx.in_relu:
-                _MASKED[(dx.data_ptr(), x.data_ptr())] = dx._version
+                _masked_put(dx, x)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             if _side_owns(ctx.param, ctx.bias):
                 _SIDE.launch(x, dy, ctx.param, ctx.bias, channels_first=cf)
@@ -203,7 +222,7 @@ class _PointwiseResidualFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = ops.linear_fwd(dy, w2, None, channels_first=True, transw=True, mask=x if ctx.in_relu else None)
             if ctx.in_relu:
-                _MASKED[(dx.data_ptr(), x.data_ptr())] = dx._version
+                _masked_put(dx, x)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             if _side_owns(ctx.param, ctx.bias):
                 _SIDE.launch(x, dy, ctx.param, ctx.bias, channels_first=True)

@@ -1158,12 +1158,15 @@ class _DPFMLossFn(torch.autograd.Function):
         ctx.save_for_backward(dC, g1, g2, g12, g21)
         ctx.scales = (1.0, w_nce / B, w_nce / B, w_acc / B, w_acc / B)
         ctx.mark_non_differentiable(logs)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for `logs` (a fill launch per step)
         return loss, logs
 
     @staticmethod
     def backward(ctx, gl, _glogs):
         import ctypes
         saved = ctx.saved_tensors
+        if gl is None:  # (not materialised: nothing flows into the loss)
+            return (None,) * 14
         need = ctx.needs_input_grad[:5]
         outs = [torch.empty_like(t) if (n and t is not None) else None for t, n in zip(saved, need)]
         sel = [i for i, o in enumerate(outs) if o is not None]

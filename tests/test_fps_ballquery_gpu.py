@@ -19,6 +19,8 @@ def _packed(arrs, dtype, device):
     ([1, 7, 100, 1024, 2049, 4500, 9000, 13000, 14000, 20000, 26000], False),  # > 13312: per-lane buckets, plain
     ([1, 7, 100, 1024, 2049, 4500, 9000, 13000], False),         # pruned buckets, random order
     ([500, 3000, 8000, 13312], True),                             # pruned, spatially coherent runs
+    ([300, 2649, 5100, 9289], True),                              # 10 points per lane (<= 10,240)
+    ([9, 600, 10240], False),
 ])
 def test_fps_ragged_batch_bitexact(device, coracle, sizes, grid):
     from dpfm_amd import ops
@@ -44,6 +46,7 @@ def test_fps_ragged_batch_bitexact(device, coracle, sizes, grid):
     for b, x in enumerate(crops):
         exp = c_fps(coracle, x, start[b], npoint[b])
         np.testing.assert_array_equal(out[b, :npoint[b]], exp, err_msg=f"crop {b} (n={sizes[b]})")
+        assert (out[b, npoint[b]:] == 0).all(), f"crop {b}: the row's tail is written as zeros"
 
 
 def test_fps_reference_signature(device):
