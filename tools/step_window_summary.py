@@ -60,6 +60,13 @@ def main():
                 prev = short(rs[i - 1]["Kernel_Name"]) if i > 0 else "-"
                 nxt = short(rs[i + 1]["Kernel_Name"]) if i + 1 < len(rs) else "-"
                 ctx[(q, short(r["Kernel_Name"]), prev, nxt)] += 1
+    # one step's launch sequence per queue (the last timed step: between the last two markers)
+    lo2 = int(marks[-2]["End_Timestamp"])
+    for q, rs in sorted(byq.items(), key=lambda kv: -len(kv[1])):
+        seq = [r for r in rs if int(r["Start_Timestamp"]) >= lo2]
+        print(f"\nqueue {q}: {len(seq)} launches in the last step")
+        for r in seq:
+            print(f"  {(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3:8.2f}  {short(r['Kernel_Name'])}")
     if ctx:
         print("\ntorch / runtime kernels in the window (queue, kernel, previous, next):")
         for (q, k, a, b), c in sorted(ctx.items(), key=lambda kv: -kv[1]):
