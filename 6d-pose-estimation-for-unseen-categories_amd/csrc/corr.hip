@@ -786,22 +786,40 @@ __global__ __launch_bounds__(256) void cgt_partial_kernel(const int64_t* __restr
   const int64_t r0 = (int64_t)s * kCgtRows;
   if (r0 >= n) return;  // inactive slice: the reduction skips it
   const int rn = (int)min((int64_t)kCgtRows, n - r0);
-  for (int e = tid; e < kCgtRows * 32; e += 256) {
-    const int r = e >> 5, k = e & 31;
-    double u = 0.0, v = 0.0;
-    if (r < rn && k < kF) {
+  {  // staging: thread (row group rb, column k) takes rows rb + 8 i; every index load, then every
+     // row load, issued before the first use, unconditionally at clamped rows / columns (round 4
+     // waited for each row's pair -> row chain in turn: 8 serial round trips per thread)
+    constexpr int kPer = kCgtRows * 32 / 256;
+    const int k = tid & 31, rb = tid >> 5, kc = k < kF ? k : 0;
+    int64_t ja[kPer], ia[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int r = rb + 8 * i, rc = r < rn ? r : rn - 1;
       if (isH) {
-        const int64_t* P = pairs + ((int64_t)b * ldp + r0 + r) * 2;
-        u = (double)e2[((int64_t)b * V2max + P[1]) * ld2 + k];
-        v = (double)e1[((int64_t)b * V1max + P[0]) * ld1 + k];
+        const int64_t* P = pairs + ((int64_t)b * ldp + r0 + rc) * 2;
+        ia[i] = P[0];
+        ja[i] = P[1];
       } else {
-        const int64_t j = r0 + r;
-        u = (double)e2[((int64_t)b * V2max + j) * ld2 + k];
-        v = u * (double)cnt[(int64_t)b * V2max + j];
+        ja[i] = r0 + rc;
+        ia[i] = 0;
       }
     }
-    U[r][k] = u;
-    V[r][k] = v;
+    float fu[kPer], fv[kPer];
+    int cv[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      fu[i] = e2[((int64_t)b * V2max + ja[i]) * ld2 + kc];
+      if (isH) fv[i] = e1[((int64_t)b * V1max + ia[i]) * ld1 + kc];
+      else cv[i] = cnt[(int64_t)b * V2max + ja[i]];
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int r = rb + 8 * i;
+      const bool ok = r < rn && k < kF;
+      const double u = ok ? (double)fu[i] : 0.0;
+      U[r][k] = u;
+      V[r][k] = ok ? (isH ? (double)fv[i] : u * (double)cv[i]) : 0.0;
+    }
   }
   __syncthreads();
   const int w = pk::wave_id(), lane = pk::lane_id();

@@ -596,30 +596,39 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
-__global__ void npoint_kernel(const int64_t* __restrict__ off, int B, int fixed, int limit,
-                              uint64_t seed, int64_t base, int32_t* __restrict__ npoint, int32_t* __restrict__ start,
-                              int64_t* __restrict__ out_off) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  int64_t acc = 0;
-  for (int b = 0; b < B; ++b) {
-    const int n = (int)(off[b + 1] - off[b]);
-    int np;
-    if (fixed > 0) {
-      // a fixed target acts as the reference's limit without its int(ratio * n) rounding:
-      // FPS to exactly `fixed` when the crop is larger, every point (in order) otherwise
-      np = n > fixed ? fixed : -n;
-    } else if (n > limit) {
-      const double ratio = (double)limit / (double)n;  // object.py:146
-      np = (int)(ratio * (double)n);                   // int(ratio * N) in upstream FPS
-    } else {
-      np = -n;  // no FPS: keep all n points in order (encoded negative)
+// One wave: lane b of each 64-crop chunk computes its crop's policy and start draw (the 64-bit
+// modulo is a long software sequence: round 4's single thread ran the B of them in series, ~13 us),
+// then a wave scan of |npoint| carried across chunks gives the packed offsets.
+__global__ __launch_bounds__(64) void npoint_kernel(const int64_t* __restrict__ off, int B, int fixed, int limit,
+                                                     uint64_t seed, int64_t base, int32_t* __restrict__ npoint,
+                                                     int32_t* __restrict__ start, int64_t* __restrict__ out_off) {
+  const int lane = threadIdx.x;
+  int64_t carry = 0;
+  for (int b0 = 0; b0 < B; b0 += 64) {
+    const int b = b0 + lane;
+    int64_t cnt = 0;
+    if (b < B) {
+      const int n = (int)(off[b + 1] - off[b]);
+      int np;
+      if (fixed > 0) {
+        // a fixed target acts as the reference's limit without its int(ratio * n) rounding:
+        // FPS to exactly `fixed` when the crop is larger, every point (in order) otherwise
+        np = n > fixed ? fixed : -n;
+      } else if (n > limit) {
+        const double ratio = (double)limit / (double)n;  // object.py:146
+        np = (int)(ratio * (double)n);                   // int(ratio * N) in upstream FPS
+      } else {
+        np = -n;  // no FPS: keep all n points in order (encoded negative)
+      }
+      npoint[b] = np;
+      if (start) start[b] = n > 0 ? (int32_t)(splitmix64(seed ^ splitmix64((uint64_t)(base + b))) % (uint64_t)n) : 0;
+      cnt = np < 0 ? -np : np;
     }
-    npoint[b] = np;
-    if (start) start[b] = n > 0 ? (int32_t)(splitmix64(seed ^ splitmix64((uint64_t)(base + b))) % (uint64_t)n) : 0;
-    out_off[b] = acc;
-    acc += np < 0 ? -np : np;
+    const int64_t inc = pk::wave_inclusive_scan_i64(cnt);
+    if (b < B) out_off[b] = carry + inc - cnt;
+    carry += __shfl(inc, 63);
   }
-  out_off[B] = acc;
+  if (lane == 0) out_off[B] = carry;
 }
 
 // pcd[idx] (f64) -> align = pcd @ R + (-t @ R) with left-to-right 3-term dots, plus f32

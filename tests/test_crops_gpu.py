@@ -194,3 +194,39 @@ def test_sor_threshold_bitexact(device):
         ss = _seq_sum(np.where(avg > 0, (avg - mean) * (avg - mean), 0.0))
         exp = mean + 0.3 * math.sqrt(ss / (n - 1))
         assert thr[b] == exp, (b, thr[b], exp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fixed", [0, 1024])
+def test_fps_npoint_many_crops(device, fixed):
+    """pk_fps_npoint over 150 crops (three 64-crop chunks of the one-wave kernel): the policy per
+    crop, the start draw splitmix64(seed ^ splitmix64(base + b)) % n, and the packed offsets as
+    the running sum of |npoint| (the chunk carry)."""
+    from dpfm_amd import ops
+    rng = np.random.default_rng(5)
+    counts = rng.integers(0, 6000, 150)
+    counts[[3, 70, 140]] = 0
+    off = torch.from_numpy(np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)).to(device)
+    seed, base = 11, 1000
+    pol = ops.fps_npoint(off, fixed=fixed, limit=2000, seed=seed, base=base)
+    npoint = pol["npoint"].cpu().numpy()
+    start = pol["start"].cpu().numpy()
+    oo = pol["off"].cpu().numpy()
+    M = (1 << 64) - 1
+
+    def sm(x):
+        x = (x + 0x9E3779B97F4A7C15) & M
+        x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M
+        x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M
+        return x ^ (x >> 31)
+    acc = 0
+    for b, n in enumerate(counts.tolist()):
+        if fixed:
+            exp = fixed if n > fixed else -n
+        else:
+            exp = O.fps_npoint(n) if n > 2000 else -n
+        assert npoint[b] == exp, b
+        assert start[b] == (sm(seed ^ sm(base + b)) % n if n > 0 else 0), b
+        assert oo[b] == acc, b
+        acc += abs(exp)
+    assert oo[150] == acc
