@@ -744,11 +744,13 @@ __global__ __launch_bounds__(256) void ir_kernel(const int64_t* __restrict__ pai
 // Least squares A X = Bm with A = e2[P[:,1], :30], Bm = e1[P[:,0], :30] (utils.py:67-79)
 // via the normal equations G X = H in fp64, G = A^T A, H = A^T Bm:
 //   G = sum_j cnt_j e2[j]^T e2[j]   (cnt_j = pairs with crop index j: V2 rows, not P)
-//   H = sum_p e2[j_p]^T e1[i_p]     (64-pair slices, one partial per slice)
+//   H = sum_p e2[j_p]^T e1[i_p]     (256-pair slices staged as four 64-pair chunks, one partial per slice)
 // fp32 inputs, fp64 products and sums; partials reduced in slice order (deterministic),
 // then one wave per crop runs Gauss-Jordan with partial pivoting, rows in registers.
 constexpr int kF = 30;
-constexpr int kCgtRows = 64;   // pairs (H) or crop rows (G) per partial slice
+constexpr int kCgtRows = 64;   // pairs (H) or crop rows (G) per staged chunk
+constexpr int kCgtChunks = 4;  // chunks per partial slice (round 5: 4 x fewer fp64 partials to write and reduce)
+constexpr int kCgtSlice = kCgtRows * kCgtChunks;
 constexpr int kFF = kF * kF;
 
 // grid (ceil(ldp/256), B): cnt[b, j] += 1 for every pair of crop b (integer atomics).
@@ -783,9 +785,20 @@ __global__ __launch_bounds__(256) void cgt_partial_kernel(const int64_t* __restr
   const bool isH = (int)blockIdx.x < SH;
   const int s = isH ? blockIdx.x : blockIdx.x - SH;
   const int64_t n = isH ? (npairs[b] < ldp ? npairs[b] : ldp) : V2max;
-  const int64_t r0 = (int64_t)s * kCgtRows;
-  if (r0 >= n) return;  // inactive slice: the reduction skips it
+  const int64_t rs0 = (int64_t)s * kCgtSlice;
+  if (rs0 >= n) return;  // inactive slice: the reduction skips it
+  const int w = pk::wave_id(), lane = pk::lane_id();
+  const int kb = lane >> 3, lb = lane & 7;
+  double acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+  for (int ch = 0; ch < kCgtChunks; ++ch) {  // (block-uniform bounds)
+  const int64_t r0 = rs0 + (int64_t)ch * kCgtRows;
+  if (r0 >= n) break;
   const int rn = (int)min((int64_t)kCgtRows, n - r0);
+  if (ch > 0) __syncthreads();  // the previous chunk's rows are consumed
   {  // staging: thread (row group rb, column k) takes rows rb + 8 i; every index load, then every
      // row load, issued before the first use, unconditionally at clamped rows / columns (round 4
      // waited for each row's pair -> row chain in turn: 8 serial round trips per thread)
@@ -822,13 +835,6 @@ __global__ __launch_bounds__(256) void cgt_partial_kernel(const int64_t* __restr
     }
   }
   __syncthreads();
-  const int w = pk::wave_id(), lane = pk::lane_id();
-  const int kb = lane >> 3, lb = lane & 7;
-  double acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
   for (int r = w; r < rn; r += 4) {
     double u[4], v[4];
 #pragma unroll
@@ -841,6 +847,7 @@ __global__ __launch_bounds__(256) void cgt_partial_kernel(const int64_t* __restr
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = fma(u[i], v[j], acc[i][j]);
   }
+  }  // chunks
   __syncthreads();  // staging buffer becomes the combine buffer
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -871,7 +878,7 @@ __global__ __launch_bounds__(256) void cgt_reduce_kernel(const double* __restric
     const int ee = isG ? e : e - kFF;
     const int64_t n = isG ? V2max : (npairs[b] < ldp ? npairs[b] : ldp);
     const int S = isG ? SG : SH;
-    const int active = (int)min((int64_t)S, (n + kCgtRows - 1) / kCgtRows);
+    const int active = (int)min((int64_t)S, (n + kCgtSlice - 1) / kCgtSlice);
     const double* p = (isG ? partG + (int64_t)b * SG * kFF : partH + (int64_t)b * SH * kFF) + ee;
     const int s0 = (active * qtr) / 4, s1 = (active * (qtr + 1)) / 4;
     double a0 = 0.0, a1 = 0.0;
@@ -1187,8 +1194,8 @@ extern "C" int pk_mean_f32(const float* x, int64_t n, float* out, void* stream) 
 }
 
 extern "C" int64_t pk_cgt_lstsq_work_size(int ldp, int V2max, int B) {
-  const int64_t SH = ldp > 0 ? (ldp + kCgtRows - 1) / kCgtRows : 0;
-  const int64_t SG = (V2max + kCgtRows - 1) / kCgtRows;
+  const int64_t SH = ldp > 0 ? (ldp + kCgtSlice - 1) / kCgtSlice : 0;
+  const int64_t SG = (V2max + kCgtSlice - 1) / kCgtSlice;
   return (int64_t)B * ((SH + SG) * kFF + 2 * kFF) + ((int64_t)B * V2max + 1) / 2;
 }
 
@@ -1199,8 +1206,8 @@ extern "C" int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs
   if (B == 0) return PK_OK;
   PK_REQUIRE(pairs && npairs && evecs1 && evecs2 && work && Cgt);
   hipStream_t s = pk::as_stream(stream);
-  const int SH = ldp > 0 ? (ldp + kCgtRows - 1) / kCgtRows : 0;
-  const int SG = (V2max + kCgtRows - 1) / kCgtRows;
+  const int SH = ldp > 0 ? (ldp + kCgtSlice - 1) / kCgtSlice : 0;
+  const int SG = (V2max + kCgtSlice - 1) / kCgtSlice;
   double* partH = work;
   double* partG = partH + (int64_t)B * SH * kFF;
   double* GH = partG + (int64_t)B * SG * kFF;
