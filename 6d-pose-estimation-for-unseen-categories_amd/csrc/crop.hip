@@ -140,6 +140,122 @@ __global__ __launch_bounds__(64) void bp_write_kernel(
   }
 }
 
+// ---- Round 5: one wave per image row, 16 consecutive pixels per lane (64 x 16 = 1024-pixel
+// segments), the erosion of the lane's pixels as bit operations on three rows' is-255 masks.
+// Every mask / depth load of a segment is issued at once (16-B vectors when the rows are
+// 16-B aligned): round 4's kernels walked a row in 64-pixel chunks, five dependent byte loads
+// each, one block per row (15,360 blocks of one wave at 640 x 480 x 32).
+constexpr int kBpPx = 16;
+struct BpRow {  // bit c: pixel u0 + c of the segment
+  uint32_t keep;  // eroded (255 with every in-image 4-neighbour 255)
+  uint32_t valid; // u0 + c < W
+};
+
+__device__ __forceinline__ uint32_t bp_is255_16(const uint8_t* __restrict__ row, int u0, int W, bool vec) {
+  uint32_t m = 0;
+  if (vec && u0 + kBpPx <= W) {
+    const uint4 q = *reinterpret_cast<const uint4*>(row + u0);
+    const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int c = 0; c < kBpPx; ++c) m |= (((w4[c >> 2] >> (8 * (c & 3))) & 0xFFu) == 0xFFu ? 1u : 0u) << c;
+  } else {
+    uint8_t b[kBpPx];
+#pragma unroll
+    for (int c = 0; c < kBpPx; ++c) b[c] = row[u0 + c < W ? u0 + c : 0];  // unconditional, masked below
+#pragma unroll
+    for (int c = 0; c < kBpPx; ++c) m |= (u0 + c < W && b[c] == 255 ? 1u : 0u) << c;
+  }
+  return m;
+}
+
+__device__ __forceinline__ BpRow bp_erode16(const uint8_t* __restrict__ m, int H, int W, int v, int u0, bool vec) {
+  BpRow r;
+  r.valid = u0 >= W ? 0u : (W - u0 >= kBpPx ? 0xFFFFu : ((1u << (W - u0)) - 1u));
+  if (u0 >= W) {
+    r.keep = 0;
+    return r;
+  }
+  const uint8_t* row = m + (int64_t)v * W;
+  const uint32_t c = bp_is255_16(row, u0, W, vec);
+  const uint32_t up = v > 0 ? bp_is255_16(row - W, u0, W, vec) : 0xFFFFu;
+  const uint32_t dn = v + 1 < H ? bp_is255_16(row + W, u0, W, vec) : 0xFFFFu;
+  const uint32_t lb = u0 > 0 ? (row[u0 - 1] == 255 ? 1u : 0u) : 1u;  // left neighbour of pixel 0
+  const int ur = u0 + kBpPx;                                          // right neighbour of pixel 15
+  const uint32_t rb = ur < W ? (row[ur] == 255 ? 1u : 0u) : 1u;
+  // pixel W - 1 (inside the segment) has no right neighbour: its bit of c >> 1 is forced
+  const uint32_t edge = (W - 1 - u0 >= 0 && W - 1 - u0 < kBpPx) ? (1u << (W - 1 - u0)) : 0u;
+  const uint32_t left = (c << 1) | lb, right = (c >> 1) | (rb << (kBpPx - 1)) | edge;
+  r.keep = c & up & dn & left & right & r.valid;
+  return r;
+}
+
+// grid (ceil(H / 4), F), block 256: wave w counts row 4 blockIdx.x + w.
+__global__ __launch_bounds__(256) void bp_count16_kernel(const uint8_t* __restrict__ mask, int H, int W,
+                                                         int32_t* __restrict__ rowcnt) {
+  const int v = blockIdx.x * 4 + pk::wave_id(), f = blockIdx.y, lane = pk::lane_id();
+  if (v >= H) return;
+  const uint8_t* m = mask + (int64_t)f * H * W;
+  const bool vec = (W % 16) == 0 && (((uintptr_t)mask) & 15) == 0;
+  int c = 0;
+  for (int s0 = 0; s0 < W; s0 += 64 * kBpPx) c += __popc(bp_erode16(m, H, W, v, s0 + kBpPx * lane, vec).keep);
+  c = pk::wave_sum_i32_s(c);
+  if (lane == 0) rowcnt[(int64_t)f * H + v] = c;
+}
+
+// grid (ceil(H / 4), F), block 256: wave w writes row 4 blockIdx.x + w in pixel order.
+__global__ __launch_bounds__(256) void bp_write16_kernel(
+    const uint16_t* __restrict__ depth, const uint8_t* __restrict__ mask, int H, int W,
+    const double* __restrict__ K, const float* __restrict__ cam_scale,
+    const int64_t* __restrict__ rowoff, const int64_t* __restrict__ frame_off, double* __restrict__ out,
+    int64_t cap, int32_t* __restrict__ pix, int32_t* __restrict__ idxmap) {
+  const int v = blockIdx.x * 4 + pk::wave_id(), f = blockIdx.y, lane = pk::lane_id();
+  if (v >= H) return;
+  const uint8_t* m = mask + (int64_t)f * H * W;
+  const uint16_t* d = depth + (int64_t)f * H * W + (int64_t)v * W;
+  const bool vec = (W % 16) == 0 && (((uintptr_t)mask) & 15) == 0;
+  const double fx = K[f * 9 + 0], cx = K[f * 9 + 2], fy = K[f * 9 + 4], cy = K[f * 9 + 5];
+  const float cs = cam_scale[f];
+  const int64_t fo = frame_off[f];
+  int64_t o = fo + rowoff[(int64_t)f * H + v];
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (int s0 = 0; s0 < W; s0 += 64 * kBpPx) {
+    const BpRow r = bp_erode16(m, H, W, v, s0 + kBpPx * lane, vec);
+    // the stores go pixel-major (pass j: pixels s0 + 64 j + lane, consecutive lanes writing
+    // consecutive points and index-map entries); each pass takes its keep bits from the lane
+    // that eroded them (lane 4 j + lane / 16, bit lane % 16)
+    uint16_t dz[kBpPx];
+    uint32_t kp = 0;  // bit j: pass j's pixel kept (all shuffles issued before the passes)
+#pragma unroll
+    for (int j = 0; j < kBpPx; ++j) {
+      const int u = s0 + 64 * j + lane;
+      dz[j] = d[u < W ? u : 0];
+      kp |= (u < W ? (((uint32_t)__shfl((int)r.keep, 4 * j + (lane >> 4)) >> (lane & 15)) & 1u) : 0u) << j;
+    }
+#pragma unroll
+    for (int j = 0; j < kBpPx; ++j) {
+      const int u = s0 + 64 * j + lane;
+      const bool keep = (kp >> j) & 1u;
+      const uint64_t bal = __ballot(keep);
+      const int64_t w = o + __popcll(bal & lt);
+      if (idxmap != nullptr && u < W) idxmap[(int64_t)f * H * W + (int64_t)v * W + u] = keep ? (int32_t)(w - fo) : -1;
+      if (keep) {
+        if (pix != nullptr && w < cap) pix[w] = v * W + u;
+        if (w < cap) {
+          const float z32 = (float)dz[j] / cs;  // f32 / f32, correctly rounded
+          const double z = (double)z32;
+          const double X = (((double)u - cx) * z) / fx;
+          const double Y = (((double)v - cy) * z) / fy;
+          out[3 * w + 0] = X * 100.0;
+          out[3 * w + 1] = Y * 100.0;
+          out[3 * w + 2] = z * 100.0;
+        }
+      }
+      o += __popcll(bal);
+      if (s0 + 64 * (j + 1) >= W) break;  // (wave-uniform) past the row
+    }
+  }
+}
+
 // ---------------------------------------------------------------- SOR (H2)
 constexpr int kKnn = 20;
 constexpr int kSorThreads = 256;
@@ -727,13 +843,13 @@ extern "C" int pk_backproject(const uint16_t* depth, const uint8_t* mask, int F,
   if (F == 0) return PK_OK;
   PK_REQUIRE(depth && mask && K && cam_scale && rowcnt && rowoff && count && off && (xyz || cap == 0));
   hipStream_t s = pk::as_stream(stream);
-  hipLaunchKernelGGL(bp_count_kernel, dim3(H, F), dim3(256), 0, s, mask, H, W, rowcnt);
+  hipLaunchKernelGGL(bp_count16_kernel, dim3((H + 3) / 4, F), dim3(256), 0, s, mask, H, W, rowcnt);
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(seg_scan_kernel, dim3(F), dim3(1024), 0, s, rowcnt, H, rowoff, count);
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(offsets_kernel, dim3(1), dim3(64), 0, s, count, F, off);
   PK_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bp_write_kernel, dim3(H, F), dim3(64), 0, s, depth, mask, H, W, K, cam_scale,
+  hipLaunchKernelGGL(bp_write16_kernel, dim3((H + 3) / 4, F), dim3(256), 0, s, depth, mask, H, W, K, cam_scale,
                      rowoff, off, xyz, cap, pix, idxmap);
   PK_CHECK_LAUNCH();
   return PK_OK;

@@ -230,3 +230,45 @@ def test_fps_npoint_many_crops(device, fixed):
         assert oo[b] == acc, b
         acc += abs(exp)
     assert oo[150] == acc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W", [633, 1100])
+def test_backproject_odd_widths_and_index_map(device, W):
+    """pk_backproject at row widths off the 16-pixel vector path (633) and past one 1024-pixel
+    segment (1100): points bit-exact vs the oracle, and pix / idxmap consistent with them."""
+    from dpfm_amd import ops
+    fr = _frames()
+    rng = np.random.default_rng(W)
+    ds, ms = [], []
+    for d, m, k, s_ in fr[:4] + fr[-2:]:
+        dd = np.zeros((d.shape[0], W), d.dtype)
+        mm = np.zeros((m.shape[0], W), m.dtype)
+        c = min(W, d.shape[1])
+        dd[:, :c], mm[:, :c] = d[:, :c], m[:, :c]
+        if W > d.shape[1]:  # the extra columns: a mirrored copy of the frame's right part
+            e = W - d.shape[1]
+            dd[:, c:], mm[:, c:] = d[:, -e:][:, ::-1], m[:, -e:][:, ::-1]
+        mm[rng.random(mm.shape) < 0.002] = 0  # holes: erosion at scattered pixels
+        ds.append(dd)
+        ms.append(mm)
+    sel = fr[:4] + fr[-2:]
+    depth = torch.from_numpy(np.stack([x.astype(np.int16) for x in ds])).to(device)
+    mask = torch.from_numpy(np.stack(ms)).to(device)
+    K = torch.from_numpy(np.stack([f[2].reshape(9) for f in sel])).to(device)
+    cs = torch.tensor([1000.0 / f[3] for f in sel], dtype=torch.float32, device=device)
+    out = ops.backproject(depth, mask, K, cs, cap=400000)
+    off = out["off"].cpu().numpy()
+    xyz = out["xyz"].cpu().numpy()
+    pix = out["pix"].cpu().numpy()
+    idxmap = out["idxmap"].cpu().numpy()
+    H = ds[0].shape[0]
+    for b in range(len(sel)):
+        exp = O.dpt_2_pcld(ds[b], 1000 / sel[b][3], sel[b][2], ms[b] == 255)
+        got = xyz[off[b]:off[b + 1]]
+        assert got.shape == exp.shape, b
+        np.testing.assert_array_equal(got, exp, err_msg=f"frame {b}")
+        p = pix[off[b]:off[b + 1]]
+        im = idxmap[b].reshape(H, W)
+        assert (im.reshape(-1)[p] == np.arange(p.shape[0])).all(), b
+        assert (im >= 0).sum() == p.shape[0], b
