@@ -117,6 +117,12 @@ __device__ __forceinline__ int wave_inclusive_scan_i32(int v) {
   return v;
 }
 
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {  // exact: any order
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
 __device__ __forceinline__ int64_t wave_inclusive_scan_i64(int64_t v) {
   const int lane = lane_id();
 #pragma unroll

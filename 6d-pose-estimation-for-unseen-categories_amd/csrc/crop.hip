@@ -206,8 +206,8 @@ __global__ __launch_bounds__(256) void bp_count16_kernel(const uint8_t* __restri
 __global__ __launch_bounds__(256) void bp_write16_kernel(
     const uint16_t* __restrict__ depth, const uint8_t* __restrict__ mask, int H, int W,
     const double* __restrict__ K, const float* __restrict__ cam_scale,
-    const int64_t* __restrict__ rowoff, const int64_t* __restrict__ frame_off, double* __restrict__ out,
-    int64_t cap, int32_t* __restrict__ pix, int32_t* __restrict__ idxmap) {
+    const int64_t* __restrict__ rowoff, const int64_t* __restrict__ count, int64_t* __restrict__ frame_off,
+    double* __restrict__ out, int64_t cap, int32_t* __restrict__ pix, int32_t* __restrict__ idxmap) {
   const int v = blockIdx.x * 4 + pk::wave_id(), f = blockIdx.y, lane = pk::lane_id();
   if (v >= H) return;
   const uint8_t* m = mask + (int64_t)f * H * W;
@@ -215,7 +215,22 @@ __global__ __launch_bounds__(256) void bp_write16_kernel(
   const bool vec = (W % 16) == 0 && (((uintptr_t)mask) & 15) == 0;
   const double fx = K[f * 9 + 0], cx = K[f * 9 + 2], fy = K[f * 9 + 4], cy = K[f * 9 + 5];
   const float cs = cam_scale[f];
-  const int64_t fo = frame_off[f];
+  // the frame's base = sum of the earlier frames' counts (round 5: no crop-offset launch);
+  // block (0, 0)'s first wave also writes the offsets array for the later stages
+  int64_t fo = 0;
+  for (int q0 = 0; q0 < f; q0 += 64) fo += q0 + lane < f ? count[q0 + lane] : 0;
+  fo = pk::wave_sum_i64(fo);
+  if (blockIdx.x == 0 && f == 0 && pk::wave_id() == 0) {
+    const int F = gridDim.y;
+    int64_t carry = 0;
+    for (int q0 = 0; q0 <= F; q0 += 64) {
+      const int q = q0 + lane;
+      const int64_t cv = q < F ? count[q] : 0;
+      const int64_t inc = pk::wave_inclusive_scan_i64(cv);
+      if (q <= F) frame_off[q] = carry + inc - cv;
+      carry += __shfl(inc, 63);
+    }
+  }
   int64_t o = fo + rowoff[(int64_t)f * H + v];
   const uint64_t lt = (1ull << lane) - 1ull;
   for (int s0 = 0; s0 < W; s0 += 64 * kBpPx) {
@@ -664,31 +679,64 @@ __global__ __launch_bounds__(1024) void sor_count_kernel(const double* __restric
   }
 }
 
-// Ordered write of kept points: f64 copy (packed by out_off) + f32 copy.
+// Ordered write of kept points: f64 copy (packed by out_off) + f32 copy. The offsets come from
+// the chunk counts in the kernel itself (round 5: no per-crop scan and crop-offset launches):
+// block (c, b) sums the chunk counts of the crops before b (the crop's base) and of its crop's
+// chunks before c, in the same barrier as its wave counts; block (0, b) writes kept[b],
+// out_off[b] (and out_off[B] for the last crop), block (c, b) coff[b, c].
 __global__ __launch_bounds__(1024) void sor_write_kernel(
     const double* __restrict__ xyz, const double* __restrict__ avg, const int64_t* __restrict__ off,
-    const double* __restrict__ thr, int nchunk, const int64_t* __restrict__ coff,
-    const int64_t* __restrict__ out_off, double* __restrict__ out64, float* __restrict__ out32,
-    int64_t* __restrict__ kept_idx) {
-  const int b = blockIdx.y;
+    const double* __restrict__ thr, int nchunk, const int32_t* __restrict__ ccount, int B,
+    int64_t* __restrict__ coff, int64_t* __restrict__ kept, int64_t* __restrict__ out_off,
+    double* __restrict__ out64, float* __restrict__ out32, int64_t* __restrict__ kept_idx) {
+  const int b = blockIdx.y, c = blockIdx.x, tid = threadIdx.x;
   const int64_t base = off[b];
   const int n = (int)(off[b + 1] - base);
-  const int i = blockIdx.x * 1024 + threadIdx.x;
+  const int i = c * 1024 + tid;
   const double t = thr[b];
   bool keep = false;
   if (i < n) {
     const double a = avg[base + i];
     keep = a > 0 && a < t;
   }
+  // chunk counts: [0, b nchunk) -> the crop base; [b nchunk, b nchunk + c) -> the chunk base
+  int64_t cb = 0, cc = 0;
+  for (int e = tid; e < b * nchunk + c; e += 1024) {
+    const int64_t v = ccount[e];
+    if (e < b * nchunk) cb += v;
+    else cc += v;
+  }
+  cb = pk::wave_sum_i64(cb);
+  cc = pk::wave_sum_i64(cc);
   const uint64_t bal = __ballot(keep);
   __shared__ int ws[16];
-  if (pk::lane_id() == 0) ws[pk::wave_id()] = __popcll(bal);
+  __shared__ int64_t wb[16], wc[16];
+  if (pk::lane_id() == 0) {
+    ws[pk::wave_id()] = __popcll(bal);
+    wb[pk::wave_id()] = cb;
+    wc[pk::wave_id()] = cc;
+  }
   __syncthreads();
   int pre = 0;
   for (int w = 0; w < pk::wave_id(); ++w) pre += ws[w];
+  int64_t crop0 = 0, chunk0 = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    crop0 += wb[w];
+    chunk0 += wc[w];
+  }
+  if (tid == 0) {
+    if (coff) coff[(int64_t)b * nchunk + c] = chunk0;
+    if (c == 0) {
+      int64_t k = 0;
+      for (int q = 0; q < nchunk; ++q) k += ccount[(int64_t)b * nchunk + q];
+      kept[b] = k;
+      out_off[b] = crop0;
+      if (b == B - 1) out_off[B] = crop0 + k;
+    }
+  }
   if (keep) {
-    const int64_t w = out_off[b] + coff[(int64_t)b * nchunk + blockIdx.x] + pre +
-                      __popcll(bal & ((1ull << pk::lane_id()) - 1ull));
+    const int64_t w = crop0 + chunk0 + pre + __popcll(bal & ((1ull << pk::lane_id()) - 1ull));
     const double* q = xyz + (base + i) * 3;
     if (out64) {
       out64[3 * w] = q[0];
@@ -847,10 +895,8 @@ extern "C" int pk_backproject(const uint16_t* depth, const uint8_t* mask, int F,
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(seg_scan_kernel, dim3(F), dim3(1024), 0, s, rowcnt, H, rowoff, count);
   PK_CHECK_LAUNCH();
-  hipLaunchKernelGGL(offsets_kernel, dim3(1), dim3(64), 0, s, count, F, off);
-  PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(bp_write16_kernel, dim3((H + 3) / 4, F), dim3(256), 0, s, depth, mask, H, W, K, cam_scale,
-                     rowoff, off, xyz, cap, pix, idxmap);
+                     rowoff, count, off, xyz, cap, pix, idxmap);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }
@@ -878,6 +924,14 @@ extern "C" int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, in
   if (nchunk > 0) {
     hipLaunchKernelGGL(sor_count_kernel, dim3(nchunk, B), dim3(1024), 0, s, avg, off, thr, nchunk, ccount);
     PK_CHECK_LAUNCH();
+  }
+  if (nchunk > 0 && (out64 || out32 || kept_idx)) {  // the write forms coff / kept / out_off itself
+    hipLaunchKernelGGL(sor_write_kernel, dim3(nchunk, B), dim3(1024), 0, s, xyz, avg, off, thr, nchunk, ccount,
+                       B, coff, kept, out_off, out64, out32, kept_idx);
+    PK_CHECK_LAUNCH();
+    return PK_OK;
+  }
+  if (nchunk > 0) {
     hipLaunchKernelGGL(seg_scan_kernel, dim3(B), dim3(1024), 0, s, ccount, nchunk, coff, kept);
     PK_CHECK_LAUNCH();
   } else {
@@ -886,11 +940,6 @@ extern "C" int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, in
   }
   hipLaunchKernelGGL(offsets_kernel, dim3(1), dim3(64), 0, s, kept, B, out_off);
   PK_CHECK_LAUNCH();
-  if (nchunk > 0 && (out64 || out32 || kept_idx)) {
-    hipLaunchKernelGGL(sor_write_kernel, dim3(nchunk, B), dim3(1024), 0, s, xyz, avg, off, thr, nchunk,
-                       coff, out_off, out64, out32, kept_idx);
-    PK_CHECK_LAUNCH();
-  }
   return PK_OK;
 }
 
