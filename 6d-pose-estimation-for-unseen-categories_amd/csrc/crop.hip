@@ -801,12 +801,27 @@ __global__ __launch_bounds__(256) void gather_transform_kernel(
     const double* __restrict__ pcd, const int64_t* __restrict__ off, const int64_t* __restrict__ idx,
     int idx_stride, const int32_t* __restrict__ npoint, const int64_t* __restrict__ out_off,
     const double* __restrict__ R, const double* __restrict__ t, double* __restrict__ sel64,
-    double* __restrict__ align64, float* __restrict__ sel32, int32_t* __restrict__ status) {
+    double* __restrict__ align64, float* __restrict__ sel32, int32_t* __restrict__ status, int ld,
+    float* __restrict__ pad_sel, float* __restrict__ pad_align, int32_t* __restrict__ pad_counts) {
   const int b = blockIdx.y;
   const int j = blockIdx.x * 256 + threadIdx.x;
   const int np = npoint[b];
   const int cnt = np < 0 ? -np : np;
   const int64_t nb = off[b + 1] - off[b];
+  // collate's padded f32 copies (pk_gather_transform_pad): rows >= the crop's count are zero
+  if (pad_counts != nullptr && blockIdx.x == 0 && threadIdx.x == 0) pad_counts[b] = cnt < ld ? cnt : ld;
+  if (j >= cnt && j < ld) {
+    if (pad_sel) {
+      pad_sel[((int64_t)b * ld + j) * 3] = 0.f;
+      pad_sel[((int64_t)b * ld + j) * 3 + 1] = 0.f;
+      pad_sel[((int64_t)b * ld + j) * 3 + 2] = 0.f;
+    }
+    if (pad_align) {
+      pad_align[((int64_t)b * ld + j) * 3] = 0.f;
+      pad_align[((int64_t)b * ld + j) * 3 + 1] = 0.f;
+      pad_align[((int64_t)b * ld + j) * 3 + 2] = 0.f;
+    }
+  }
   if (status && blockIdx.x == 0) {  // the crop's index check (written for every crop: no init needed)
     int bad = 0;
     if (np >= 0)
@@ -836,12 +851,20 @@ __global__ __launch_bounds__(256) void gather_transform_kernel(
     sel32[3 * w + 1] = (float)y;
     sel32[3 * w + 2] = (float)z;
   }
-  if (align64) {
+  const bool padr = j < ld;
+  if (pad_sel && padr) {
+    pad_sel[((int64_t)b * ld + j) * 3] = (float)x;
+    pad_sel[((int64_t)b * ld + j) * 3 + 1] = (float)y;
+    pad_sel[((int64_t)b * ld + j) * 3 + 2] = (float)z;
+  }
+  if (align64 || (pad_align && padr)) {
     const double nt0 = -1.0 * tb[0], nt1 = -1.0 * tb[1], nt2 = -1.0 * tb[2];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const double tt = (nt0 * Rb[c] + nt1 * Rb[3 + c]) + nt2 * Rb[6 + c];
-      align64[3 * w + c] = ((x * Rb[c] + y * Rb[3 + c]) + z * Rb[6 + c]) + tt;
+      const double a = ((x * Rb[c] + y * Rb[3 + c]) + z * Rb[6 + c]) + tt;
+      if (align64) align64[3 * w + c] = a;
+      if (pad_align && padr) pad_align[((int64_t)b * ld + j) * 3 + c] = (float)a;
     }
   }
 }
@@ -981,7 +1004,23 @@ extern "C" int pk_gather_transform(const double* pcd, const int64_t* off, int B,
   PK_REQUIRE(pcd && off && npoint && out_off && R && t);
   hipLaunchKernelGGL(gather_transform_kernel, dim3(std::max(1, (npmax + 255) / 256), B), dim3(256), 0,
                      pk::as_stream(stream), pcd, off, idx, idx_stride, npoint, out_off, R, t, sel64,
-                     align64, sel32, status);
+                     align64, sel32, status, 0, nullptr, nullptr, nullptr);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
+
+extern "C" int pk_gather_transform_pad(const double* pcd, const int64_t* off, int B, const int64_t* idx,
+                                       int idx_stride, const int32_t* npoint, int npmax,
+                                       const int64_t* out_off, const double* R, const double* t,
+                                       double* sel64, double* align64, float* sel32, int32_t* status, int ld,
+                                       float* pad_sel32, float* pad_align32, int32_t* counts, void* stream) {
+  PK_REQUIRE(B >= 0 && npmax >= 0 && ld >= 0);
+  if (B == 0) return PK_OK;
+  PK_REQUIRE(pcd && off && npoint && out_off && R && t);
+  const int rows = std::max(npmax, ld);
+  hipLaunchKernelGGL(gather_transform_kernel, dim3(std::max(1, (rows + 255) / 256), B), dim3(256), 0,
+                     pk::as_stream(stream), pcd, off, idx, idx_stride, npoint, out_off, R, t, sel64,
+                     align64, sel32, status, ld, pad_sel32, pad_align32, counts);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

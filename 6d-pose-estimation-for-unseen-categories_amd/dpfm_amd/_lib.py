@@ -55,6 +55,7 @@ SIGNATURES = {
     "pk_sor": [_P, _P, _I, _I, _I, _D, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "pk_fps_npoint": [_P, _I, _I, _I, _U64, _I64, _P, _P, _P, _P],
     "pk_gather_transform": [_P, _P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
+    "pk_gather_transform_pad": [_P, _P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P],
     "pk_collate_pad": [_P, _I, _I, _P, _I, _I, _P, _P, _P],
     "pk_segment_scan": [_P, _I, _I, _P, _P, _P],
     "pk_offsets_from_counts": [_P, _I, _P, _P],

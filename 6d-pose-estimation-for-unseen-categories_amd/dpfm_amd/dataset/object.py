@@ -221,10 +221,10 @@ class CropFormation:
             ld = npmax
         idx = ops.fps_packed(so["xyz32"], so["off"], fb.max_pixels, pol["start"], pol["npoint"], npmax)
         st = torch.empty((F_,), dtype=torch.int32, device=fb.depth.device)
+        # PC["xyz"] = f32(pcd) and Obj["align_pc"], padded as collate does, in the gather's launch
         g = ops.gather_transform(so["xyz64"], so["off"], idx, pol["npoint"], npmax, pol["off"], fb.R, fb.t,
-                                 F_ * npmax, want_sel32=False, status=st)
-        pc32, n2 = ops.collate_pad(g["sel64"], pol["off"], ld)       # PC["xyz"]: f32(pcd), padded
-        align32, _ = ops.collate_pad(g["align"], pol["off"], ld)     # Obj["align_pc"]
+                                 F_ * npmax, want_sel32=False, status=st, pad_ld=ld)
+        pc32, n2, align32 = g["pc32"], g["n2"], g["align32"]
         n1max = fb.n1max or self.n1
         bq = ops.ball_query(fb.cad64, fb.cad_off, g["align"], pol["off"], None, n1max, ld, self.pair_cap,
                             with_mask=self.with_mask, thr2=fb.thr2)

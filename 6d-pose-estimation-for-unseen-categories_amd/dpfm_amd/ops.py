@@ -222,10 +222,13 @@ def collate_pad(src: torch.Tensor, off: torch.Tensor, ld: int) -> tuple[torch.Te
 def gather_transform(pcd: torch.Tensor, off: torch.Tensor, idx: Optional[torch.Tensor], npoint: torch.Tensor,
                      npmax: int, out_off: torch.Tensor, R: torch.Tensor, t: torch.Tensor, total_cap: int,
                      want_sel64: bool = True, want_align: bool = True, want_sel32: bool = True,
-                     status: Optional[torch.Tensor] = None, check: Optional[bool] = None) -> dict:
+                     status: Optional[torch.Tensor] = None, check: Optional[bool] = None,
+                     pad_ld: Optional[int] = None) -> dict:
     """pcd[idx] + transform (pk_gather_transform). status int32 [B] (optional): per crop 1 when
     an FPS index lies outside its crop (that point's outputs are NaN); without it the call checks
-    a temporary one (host sync) unless capturing. Returns dict(sel64, align, sel32, status)."""
+    a temporary one (host sync) unless capturing. Returns dict(sel64, align, sel32, status); with
+    pad_ld also collate_pad's outputs of sel64 and align at ld = pad_ld in the same launch:
+    pc32 / align32 f32 [B, ld, 3] and n2 int32 [B] (pk_gather_transform_pad)."""
     B = off.numel() - 1
     dev = pcd.device
     st, chk = _index_status(B, dev, status, check)
@@ -233,11 +236,22 @@ def gather_transform(pcd: torch.Tensor, off: torch.Tensor, idx: Optional[torch.T
     align = torch.empty((total_cap, 3), dtype=torch.float64, device=dev) if want_align else None
     sel32 = torch.empty((total_cap, 3), dtype=torch.float32, device=dev) if want_sel32 else None
     idx_stride = idx.shape[1] if idx is not None else 0
-    call("pk_gather_transform", ptr(pcd), ptr(off), B, ptr(idx), int(idx_stride), ptr(npoint), int(npmax),
-         ptr(out_off), ptr(R), ptr(t), ptr(sel64), ptr(align), ptr(sel32), ptr(st), _lib.stream(dev))
+    if pad_ld is None:
+        call("pk_gather_transform", ptr(pcd), ptr(off), B, ptr(idx), int(idx_stride), ptr(npoint), int(npmax),
+             ptr(out_off), ptr(R), ptr(t), ptr(sel64), ptr(align), ptr(sel32), ptr(st), _lib.stream(dev))
+        pads = {}
+    else:  # collate of both fields in the same launch (pk_gather_transform_pad)
+        ld = int(pad_ld)
+        pc32 = torch.empty((B, ld, 3), dtype=torch.float32, device=dev)
+        al32 = torch.empty((B, ld, 3), dtype=torch.float32, device=dev)
+        n2 = torch.empty((B,), dtype=torch.int32, device=dev)
+        call("pk_gather_transform_pad", ptr(pcd), ptr(off), B, ptr(idx), int(idx_stride), ptr(npoint), int(npmax),
+             ptr(out_off), ptr(R), ptr(t), ptr(sel64), ptr(align), ptr(sel32), ptr(st), ld, ptr(pc32), ptr(al32),
+             ptr(n2), _lib.stream(dev))
+        pads = dict(pc32=pc32, align32=al32, n2=n2)
     if chk:
         check_index_status(st, "gather_transform (FPS indices)")
-    return dict(sel64=sel64, align=align, sel32=sel32, status=st)
+    return dict(sel64=sel64, align=align, sel32=sel32, status=st, **pads)
 
 
 # ------------------------------------------------------------------------------ H7 spectral diffusion

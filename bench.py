@@ -448,7 +448,8 @@ CORR_METRIC = "4096-pt dense correspondence solves/sec (4096^2 feature distance 
 OPS_METRIC = "crop spectral operators/sec (kNN-30 fans + cotan Laplacian + mass + 64 eigenpairs)"
 TEASER_METRIC = "TEASER++ solves/sec (pairwise-consistency graph + max clique + GNC-TLS + adaptive voting)"
 ICP_METRIC = "ICP refinements/sec (point-to-point after RANSAC, ~5000-vertex CAD, threshold 0.2 cm, <= 2000 iterations)"
-CROP_FAMS = {"pk_backproject", "pk_sor", "pk_fps_npoint", "pk_fps", "pk_gather_transform", "pk_collate_pad",
+CROP_FAMS = {"pk_backproject", "pk_sor", "pk_fps_npoint", "pk_fps", "pk_gather_transform", "pk_gather_transform_pad",
+             "pk_collate_pad",
              "pk_ball_query_mask", "pk_ball_query_pairs", "pk_sample_rgb", "pk_erode_mask"}
 
 

@@ -113,6 +113,16 @@ int pk_gather_transform(const double* pcd, const int64_t* off, int B, const int6
                         const double* R, const double* t, double* sel64, double* align64,
                         float* sel32, int32_t* status, void* stream);
 
+/* pk_gather_transform plus H6's collate of its two fields in the same launch (the crop-formation
+ * path's pk_collate_pad calls on sel64 and align64, dataset/helpers.py:22-50): pad_sel32 /
+ * pad_align32 f32 [B, ld, 3] (any NULL) = f32(sel64) / f32(align64) of crop b's first
+ * min(count_b, ld) points, zero rows after; counts int32 [B] (or NULL) = min(count_b, ld). */
+int pk_gather_transform_pad(const double* pcd, const int64_t* off, int B, const int64_t* idx,
+                            int idx_stride, const int32_t* npoint, int npmax, const int64_t* out_off,
+                            const double* R, const double* t, double* sel64, double* align64,
+                            float* sel32, int32_t* status, int ld, float* pad_sel32, float* pad_align32,
+                            int32_t* counts, void* stream);
+
 /* H6 collate (dataset/helpers.py:22-50: torch.Tensor(x) then pad_sequence(batch_first=True))
  * of one packed per-crop field: src [T, C] f64 (src_f64 = 1) or f32, packed by off [B+1];
  * dst f32 [B, ld, C] with crop b's first min(n_b, ld) rows cast to f32 and every later row

@@ -272,3 +272,32 @@ def test_backproject_odd_widths_and_index_map(device, W):
         im = idxmap[b].reshape(H, W)
         assert (im.reshape(-1)[p] == np.arange(p.shape[0])).all(), b
         assert (im >= 0).sum() == p.shape[0], b
+
+
+@pytest.mark.gpu
+def test_gather_transform_pad_equals_gather_then_collate(device):
+    """pk_gather_transform_pad's padded f32 fields and counts are exactly pk_collate_pad of the
+    packed gather outputs (ld above and below the largest crop), and its packed outputs equal
+    pk_gather_transform's."""
+    from dpfm_amd import ops
+    from dpfm_amd.dataset.synthetic import random_rotation
+    rng = np.random.default_rng(9)
+    counts = [700, 0, 1500, 1024, 33]
+    clouds = [rng.normal(size=(n, 3)) * 20 + 100 for n in counts]
+    x, off = _packed(clouds, device)
+    pol = ops.fps_npoint(off, fixed=1024, limit=2000, seed=3)
+    npmax = 1024
+    idx = ops.fps_packed(x.to(torch.float32), off, max(counts), pol["start"], pol["npoint"], npmax)
+    R = torch.from_numpy(np.stack([random_rotation(rng) for _ in counts]).reshape(-1, 9)).to(device)
+    t = torch.from_numpy(rng.normal(size=(len(counts), 3)) * 40).to(device)
+    total = int(pol["npoint"].abs().sum())
+    st = torch.empty((len(counts),), dtype=torch.int32, device=device)
+    a = ops.gather_transform(x, off, idx, pol["npoint"], npmax, pol["off"], R, t, total, want_sel32=False, status=st)
+    for ld in (1024, 600, 1100):
+        st2 = torch.empty_like(st)
+        b = ops.gather_transform(x, off, idx, pol["npoint"], npmax, pol["off"], R, t, total, want_sel32=False,
+                                 status=st2, pad_ld=ld)
+        assert torch.equal(a["sel64"], b["sel64"]) and torch.equal(a["align"], b["align"])
+        pc, n2 = ops.collate_pad(a["sel64"], pol["off"], ld)
+        al, _ = ops.collate_pad(a["align"], pol["off"], ld)
+        assert torch.equal(b["pc32"], pc) and torch.equal(b["align32"], al) and torch.equal(b["n2"], n2), ld
