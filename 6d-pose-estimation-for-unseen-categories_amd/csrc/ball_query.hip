@@ -437,11 +437,16 @@ __global__ __launch_bounds__(kBqThreads) void bq_count_kernel(
 // Exclusive scan of row counts per crop. grid (B), block 1024.
 __global__ __launch_bounds__(1024) void bq_scan_kernel(const int32_t* __restrict__ rowcount,
                                                        int n1max, int64_t* __restrict__ rowoff,
-                                                       int64_t* __restrict__ total) {
+                                                       int64_t* __restrict__ total, int8_t* __restrict__ ov21,
+                                                       int n2max) {
   __shared__ int64_t wsum[16];
   __shared__ int64_t carry_s;
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
+  // crop b's ov21 flags cleared here (the pairs kernel after this launch sets them): no
+  // separate zero-fill launch
+  if (ov21 != nullptr)
+    for (int j = tid; j < n2max; j += 1024) ov21[(int64_t)b * n2max + j] = 0;
   if (tid == 0) carry_s = 0;
   __syncthreads();
   for (int base = 0; base < n1max; base += 1024) {
@@ -597,16 +602,13 @@ extern "C" int pk_ball_query_pairs(const double* cad, const int64_t* cad_off, co
   PK_REQUIRE(pairs != nullptr || cap == 0);
   PK_REQUIRE(mask == nullptr || (ld >= n2max && ld % kColsPerLane == 0));
   hipStream_t s = pk::as_stream(stream);
-  if (ov21 != nullptr) {
-    hipError_t e = pk::zero_async(ov21, (size_t)B * n2max, s);
-    if (e != hipSuccess) return (int)e;
-  }
   if (n1max == 0) {
-    hipError_t e = pk::zero_async(count, sizeof(int64_t) * B, s);
+    hipError_t e = ov21 != nullptr ? pk::zero_async(ov21, (size_t)B * n2max, s) : hipSuccess;
+    if (e == hipSuccess) e = pk::zero_async(count, sizeof(int64_t) * B, s);
     if (e == hipSuccess && over != nullptr) e = pk::zero_async(over, sizeof(int32_t), s);
     return e == hipSuccess ? PK_OK : (int)e;
   }
-  hipLaunchKernelGGL(bq_scan_kernel, dim3(B), dim3(1024), 0, s, rowcount, n1max, rowoff, count);
+  hipLaunchKernelGGL(bq_scan_kernel, dim3(B), dim3(1024), 0, s, rowcount, n1max, rowoff, count, ov21, n2max);
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(bq_pairs_kernel, dim3((n1max + 3) / 4, B), dim3(256), 0, s, cad, cad_off, pc,
                      pc_off, thr2, n1max, n2max, ld, mask, rowcount, rowoff, pairs, cap, ov12,
