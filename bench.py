@@ -57,8 +57,9 @@ def parse():
     ap.add_argument("--eager", action="store_true", help="no HIP graph: launch every kernel from Python")
     ap.add_argument("--main-priority", type=int, default=0,
                     help="1: the training stream at the highest HIP queue priority (crop formation below)")
-    ap.add_argument("--cgt-side", action="store_true",
-                    help="solve C_gt with the crops on the crop-formation stream (default: in the training graph)")
+    ap.add_argument("--cgt-side", type=int, choices=(0, 1), default=None,
+                    help="1: solve C_gt with the crops on the crop-formation stream, 0: in the training graph "
+                         "(default: 0 for the configs[1] shape, 1 for --ragged: measured faster for each, DESIGN 5b)")
     ap.add_argument("--ir-main", action="store_true",
                     help="keep the naive point map + IR in the training graph (no deferred I_k graph)")
     ap.add_argument("--train-only", action="store_true",
@@ -537,7 +538,8 @@ def build_train(args, dev, rank, world):
         one_step = GraphedTrainStep(crops_of, step, fb, op, warmup=3)
     else:  # same, with crop formation of the next batch on a second stream
         one_step = PipelinedTrainer(crops_of, step, fb, op, warmup=3, main_priority=args.main_priority,
-                                        cgt_side=args.cgt_side, defer_ir=not args.ir_main)
+                                        cgt_side=bool(args.ragged) if args.cgt_side is None else bool(args.cgt_side),
+                                        defer_ir=not args.ir_main)
     config = {"workload": f"configs[1] shape: B={B} synthetic 640x480 RGB-D crops/GPU, {N} pts, training step "
                           "fwd+bwd (configs[2] semantics, DDP over RCCL when N>1)",
               "execution": "eager" if args.eager else ("hip-graph, training only (diagnostic)" if args.train_only else
