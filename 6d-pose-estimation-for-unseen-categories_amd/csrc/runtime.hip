@@ -35,3 +35,13 @@ extern "C" int pk_stream_destroy(void* stream) {
   const hipError_t e = hipStreamDestroy(static_cast<hipStream_t>(stream));
   return e == hipSuccess ? PK_OK : (int)e;
 }
+
+// pk_build_id: the sha256 the Makefile formed over the sources this library was built from
+// (build/build_id.c, regenerated whenever a source, the header or the Makefile changes).
+extern "C" const char pk_build_id_str[];
+
+extern "C" int pk_build_id(char* out, int cap) {
+  PK_REQUIRE(out != nullptr && cap >= 65);
+  for (int i = 0; i < 65; ++i) out[i] = pk_build_id_str[i];
+  return PK_OK;
+}

@@ -126,6 +126,7 @@ SIGNATURES = {
     "pk_stream_create_cu_mask": [_P, _I, _P],
     "pk_stream_get_cu_mask": [_P, _I, _P],
     "pk_stream_destroy": [_P],
+    "pk_build_id": [_P, _I],  # host buffer
 }
 
 RESTYPES = {"pk_cgt_lstsq_work_size": _I64, "pk_linear_wgrad_grouped_work": _I64, "pk_ransac_work_size": _I64,
@@ -198,6 +199,30 @@ def use_dev_lib() -> None:
 
 _ERRORS = {1000: "invalid argument", 1001: "output capacity exceeded"}
 _probe = None
+
+
+def build_id(l: Optional[ctypes.CDLL] = None) -> str:
+    """The sha256 the library was built from (pk_build_id)."""
+    buf = ctypes.create_string_buffer(65)
+    st = (l or lib()).pk_build_id(buf, 65)
+    if st != 0:
+        raise PoseKernError(f"pk_build_id failed: {st}")
+    return buf.value.decode()
+
+
+def tree_build_id() -> str:
+    """The same hash recomputed from the source tree next to this package (the Makefile's recipe:
+    its sorted ID_SRCS list, contents concatenated)."""
+    import glob
+    import hashlib
+    pkg = os.path.dirname(_HERE)
+    names = sorted([os.path.relpath(f, pkg) for pat in ("*.hip", "*.hpp", "*.cpp")
+                    for f in glob.glob(os.path.join(pkg, "csrc", pat))] + ["../include/posekern.h", "Makefile"])
+    h = hashlib.sha256()
+    for n in names:
+        with open(os.path.join(pkg, n), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
 
 
 def set_probe(hook) -> None:

@@ -60,11 +60,20 @@ class GroupedWgrad:
     stays on one stream: a single-stream HIP graph replays without cross-queue
     dependencies (a forked side stream measured slower on MI355X)."""
 
-    def __init__(self, params, bufs=None):
+    def __init__(self, params, bufs=None, direct_params=()):
+        """params: the per-point layers' weights / biases (gradients from the grouped launch);
+        direct_params: parameters whose gradient a kernel may write whole through direct() (the
+        diffusion times under the fused encoder) and that otherwise get autograd's ordinary
+        accumulation (the non-fused encoder path) — never zeroed by end()."""
         self.params = [p for p in params]
-        # persistent .grad buffers (optionally the caller's, e.g. views of one flat buffer)
+        self.direct_params = [p for p in direct_params]
+        self.direct_ids = {id(p) for p in self.direct_params}
+        self.caller_bufs = bufs is not None
+        # persistent .grad buffers (optionally the caller's, e.g. views of one flat buffer the
+        # caller zeroes before each backward)
         self.bufs = {id(p): (bufs[id(p)] if bufs is not None else
-                             torch.zeros_like(p, memory_format=torch.contiguous_format)) for p in self.params}
+                             torch.zeros_like(p, memory_format=torch.contiguous_format))
+                     for p in self.params + self.direct_params}
         self.seen = set()
         self.calls = []
 
@@ -72,6 +81,12 @@ class GroupedWgrad:
         global _SIDE
         _MASKED.clear()
         for p in self.params:
+            p.grad = self.bufs[id(p)]
+        for p in self.direct_params:
+            # autograd accumulates into .grad when no kernel writes it whole: start it from zero
+            # (a caller's flat buffer is already zeroed; an own buffer holds the last step's value)
+            if not self.caller_bufs:
+                self.bufs[id(p)].zero_()
             p.grad = self.bufs[id(p)]
         self.seen = set()
         self.calls = []
@@ -117,6 +132,7 @@ class GroupedWgrad:
             for p in self.params:  # a layer the forward did not use gets a zero gradient
                 if id(p) not in self.seen:
                     p.grad.zero_()
+            # (direct_params: written by direct(), or accumulated by autograd into the zeroed buffer)
         self.calls = []
 
 
@@ -280,7 +296,8 @@ def linear_pair_cf(layer: "Linear", feat: torch.Tensor, B0: int):
     Cin, Cout = layer.in_features, layer.out_features
     if not (feat.is_cuda and feat.dim() == 3 and feat.is_contiguous() and feat.dtype == torch.float32
             and feat.shape[-1] == Cin and 0 < B0 < feat.shape[0] and Cin in (16, 32, 64, 128)
-            and Cout % 16 == 0 and Cout <= 128 and not layer.relu_out and not layer.sigmoid_out):
+            and Cout in (16, 32, 64, 128) and not layer.relu_out and not layer.sigmoid_out):
+        # (Cout: the widths the backward's pk_transpose_cf_rows instantiates)
         return None
     return _LinearPairCfFn.apply(feat, layer.weight, layer.bias, B0)
 

@@ -256,10 +256,11 @@ class TrainStep:
         self.side = None
         if grouped and dev.type == "cuda":
             lin = [p for m in model.modules() if isinstance(m, (Linear, Conv1d)) for p in m.parameters(recurse=False)]
-            # gradients the kernels write whole into .grad (GroupedWgrad.direct): the diffusion times
-            lin += [m.diffusion_time for m in model.modules() if isinstance(m, LearnedTimeDiffusion)]
+            # gradients the fused encoder's kernels write whole into .grad (GroupedWgrad.direct): the
+            # diffusion times (autograd's accumulation on the non-fused encoder path)
+            dts = [m.diffusion_time for m in model.modules() if isinstance(m, LearnedTimeDiffusion)]
             self.side = GroupedWgrad(lin, bufs={id(p): v for p, v in zip(self.params, self.gviews)}
-                                     if self.flat_grads else None)
+                                     if self.flat_grads else None, direct_params=dts)
 
     def nce_counter(self) -> torch.Tensor:
         """The device step counter keying this step's NCE pair draws (utils/loss.py)."""
@@ -615,6 +616,8 @@ class PipelinedTrainer:
         current stream after it: every log returned so far then holds its IR."""
         if not self.defer_ir or self.i == 0:
             return
+        if self.own_main:  # (as in __call__: the replay after the caller's queued work)
+            self.main.wait_stream(torch.cuda.current_stream())
         k = (self.i - 1) & 1
         if self._trained[k]:
             with torch.cuda.stream(self.side):
@@ -625,6 +628,8 @@ class PipelinedTrainer:
 
     def __call__(self) -> dict:
         k = self.i & 1
+        if self.own_main:  # the step after the caller's queued work (its reads of earlier logs / params)
+            self.main.wait_stream(torch.cuda.current_stream())
         self._form(k ^ 1)                      # next batch's crops, concurrently
         with torch.cuda.stream(self.main):
             self.main.wait_event(self.formed[k])

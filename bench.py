@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="crops per GPU (configs[1]: 32)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="crops over all ranks (per rank = global / N; configs[2]: --gpus 2 --global-batch 32); "
+                         "default: --batch per GPU (weak scaling)")
     ap.add_argument("--points", type=int, default=1024)
     ap.add_argument("--ragged", action="store_true",
                     help="train / infer at the reference's real sizes: ragged crops of ~200-2000 points (the "
@@ -121,8 +124,10 @@ class KernelProbe:
         return out
 
 
-def ball_query_roofline(dev, probe_launches: int = 10) -> dict:
-    """pk_ball_query_mask at configs[3] size (B=256 crops, 2048 x 2048): >= 1 GB per launch."""
+def ball_query_roofline(dev, probe_launches: int = 10, blocks: int = 7) -> dict:
+    """pk_ball_query_mask at configs[3] size (B=256 crops, 2048 x 2048): >= 1 GB per launch.
+    `blocks` timed blocks of `probe_launches` back-to-back launches each: the line reports the
+    median block (achieved / frac) and the min / max over blocks (run-to-run spread)."""
     from dpfm_amd import ops
     from dpfm_amd._lib import call, ptr, stream
     B, N = 256, 2048
@@ -139,17 +144,21 @@ def ball_query_roofline(dev, probe_launches: int = 10) -> dict:
     for _ in range(3):
         f()
     torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(probe_launches):
-        f()
-    e.record()
-    torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / probe_launches
     byts = B * (24 * N + 24 * N + N * N) + B * N * 4  # coords in + mask + row counts
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(blocks)]
+    for s, e in ev:
+        s.record()
+        for _ in range(probe_launches):
+            f()
+        e.record()
+    torch.cuda.synchronize()
+    mss = sorted(s.elapsed_time(e) / probe_launches for s, e in ev)
+    ms = float(np.median(mss))
+    fr = lambda m: round(byts / (m * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)  # noqa: E731
     ach = byts / (ms * 1e-3) / 1e9
     return {"kernel": "pk_ball_query_mask (configs[3]: 256 x 2048 x 2048)", "bound": "hbm", "achieved": round(ach, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "frac_min": fr(mss[-1]), "frac_max": fr(mss[0]), "blocks": blocks, "launches_per_block": probe_launches,
             "traffic": pmc_traffic("pk_ball_query_mask@configs3_probe"),
             "ms_per_launch": round(ms, 4), "bytes_per_launch": byts}
 
@@ -515,6 +524,27 @@ def ragged_setup(B: int, n1: int, rank: int, dev):
     return fb, op, crops_of, sizes
 
 
+def train_workload(B: int, N: int, world: int) -> str:
+    """The training line's workload name: which BASELINE.json config the (per-rank batch, world)
+    pair IS, with the true global batch stated."""
+    shape = f"synthetic 640x480 RGB-D crops, {N} pts, training step fwd+bwd"
+    if world == 1:
+        return f"configs[1] shape: B={B} {shape} on 1 GPU (global batch {B})"
+    if world == 2 and B * world == 32 and N == 1024:
+        return f"configs[2]: global batch 32 = 2 ranks x B=16, {shape}, DDP with RCCL gradient all-reduce"
+    return (f"configs[1] shape per GPU, weak scaling: global batch {B * world} = {world} ranks x B={B}, {shape}, "
+            f"DDP with RCCL gradient all-reduce (configs[2] itself: --gpus 2 --global-batch 32)")
+
+
+def apply_global_batch(args, world: int) -> None:
+    """--global-batch G: G crops over all ranks (G / world per rank; must divide)."""
+    if args.global_batch is None:
+        return
+    if args.global_batch % world:
+        raise SystemExit(f"bench.py: --global-batch {args.global_batch} is not divisible by {world} ranks")
+    args.batch = args.global_batch // world
+
+
 def build_train(args, dev, rank, world):
     """configs[1] shape (configs[2] semantics for N > 1): one training step per iteration."""
     from dpfm_amd.dataset.object import CropFormation
@@ -540,8 +570,7 @@ def build_train(args, dev, rank, world):
         one_step = PipelinedTrainer(crops_of, step, fb, op, warmup=3, main_priority=args.main_priority,
                                         cgt_side=bool(args.ragged) if args.cgt_side is None else bool(args.cgt_side),
                                         defer_ir=not args.ir_main)
-    config = {"workload": f"configs[1] shape: B={B} synthetic 640x480 RGB-D crops/GPU, {N} pts, training step "
-                          "fwd+bwd (configs[2] semantics, DDP over RCCL when N>1)",
+    config = {"workload": train_workload(B, N, world),
               "execution": "eager" if args.eager else ("hip-graph, training only (diagnostic)" if args.train_only else
                                                        "hip-graph" if args.no_overlap else
                                                        "hip-graph, crop formation overlapped" +
@@ -630,10 +659,13 @@ def build_corr(args, dev, rank, world):
     ar = torch.arange(V, dtype=torch.int32, device=dev)
     bf16 = args.fd_precision != "fp32"
 
+    st_idx = torch.zeros((1,), dtype=torch.int32, device=dev)  # persistent: no per-call host check
+
     def solve():
         idx, _ = ops.feat_dist_topk(ex, C, ey, n, n, 1, precision=args.fd_precision)
         corres = torch.stack([idx[0, :, 0].to(torch.int32), ar], 1)
-        return {"T": ops.ransac(cad_t, off, pc_t, off, corres, off, H, seed=0, nmax=V)[0]}
+        return {"T": ops.ransac(cad_t, off, pc_t, off, corres, off, H, seed=0, nmax=V, status=st_idx)[0],
+                "index_status": st_idx}
 
     one_step = solve
     if not args.eager:
@@ -729,9 +761,11 @@ def build_ransac_ref(args, dev, rank, world):
     corres = torch.from_numpy(np.concatenate(cors).astype(np.int32)).to(dev)
     cor_off = ops.packed_offsets([n] * B, dev)
 
+    st_idx = torch.zeros((B,), dtype=torch.int32, device=dev)  # persistent: no per-call host check
+
     def solve():
-        T, st = ops.ransac(cad_t, cad_off, pc_t, pc_off, corres, cor_off, H, seed=0, nmax=n)
-        return {"T": T, "stats": st}
+        T, st = ops.ransac(cad_t, cad_off, pc_t, pc_off, corres, cor_off, H, seed=0, nmax=n, status=st_idx)
+        return {"T": T, "stats": st, "index_status": st_idx}
 
     one_step = solve
     if not args.eager:
@@ -941,6 +975,7 @@ def main():
         sys.exit(subprocess.call(cmd, env=env))
     args = parse()
     world, rank, dev = setup_dist(args.gpus)
+    apply_global_batch(args, world)
     from dpfm_amd import _lib
     build = {"train": build_train, "infer": build_infer, "corr4096": build_corr, "icp": build_icp,
              "ransac_ref": build_ransac_ref,
@@ -973,6 +1008,11 @@ def main():
         one_step.flush()
         torch.cuda.synchronize()
     extra = {}
+    # index consumers' per-crop status (IR / RANSAC met an out-of-range index; 0 expected), read
+    # after timing like pair_overflow
+    ist = log.get("ir_index_status" if args.mode == "train" else "index_status") if isinstance(log, dict) else None
+    if ist is not None:
+        extra["index_status_bad_crops"] = int((ist != 0).sum())
     if args.mode == "train":
         extra = {"loss": round(float(log["loss"]), 5), "ir": round(float(log["IR"]), 5),
                  "pair_overflow": bool(log["pair_overflow"])}

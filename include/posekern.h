@@ -682,6 +682,12 @@ int pk_stream_create_cu_mask(const uint32_t* mask, int words, void** stream);
 int pk_stream_get_cu_mask(void* stream, int words, uint32_t* mask);
 int pk_stream_destroy(void* stream);
 
+/* pk_build_id: the library's build identity (no reference counterpart): writes the 64 hex digits
+ * + NUL of the sha256 over the sources it was built from (the csrc .hip / .hpp / .cpp files, this header and the
+ * Makefile, concatenated in sorted path order) into the HOST buffer out (cap >= 65). A test
+ * recomputes the hash from the tree to prove the loaded binary is built from those sources. */
+int pk_build_id(char* out, int cap);
+
 #ifdef __cplusplus
 }
 #endif

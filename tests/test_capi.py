@@ -55,3 +55,24 @@ def test_product_library_has_no_development_hooks():
     dev = nm(_lib.DEV_LIB_PATH)
     for hook in ("pkdev_seq_sum", "pkdev_rigidity_variant", "pkdev_probe_linear", "pkdev_fps_cfg"):
         assert hook in dev, hook
+
+
+def test_build_id_matches_tree():
+    """pk_build_id of the loaded product and dev libraries equals the sha256 recomputed from this
+    tree's sources (csrc, include/posekern.h, Makefile): the binaries are built from them."""
+    from dpfm_amd import _lib
+    want = _lib.tree_build_id()
+    assert _lib.build_id() == want, "libposekern.so was not built from this tree (run make)"
+    assert _lib.build_id(_lib.dev_lib()) == want, "libposekern_dev.so was not built from this tree (run make)"
+
+
+@pytest.mark.gpu
+def test_build_id_matches_tree_on_device():
+    """The same identity check inside the GPU suite (the box runs the .so pushed from the build
+    container), after one device call through the library, so a green -m gpu run proves the tested
+    binary is built from the snapshot's sources."""
+    import torch
+    from dpfm_amd import _lib, ops
+    x = torch.arange(10, dtype=torch.float32, device="cuda")
+    assert float(ops.mean_f32(x)) == 4.5
+    assert _lib.build_id() == _lib.tree_build_id()

@@ -129,7 +129,43 @@ def test_grouped_wgrad_step_matches_serial(device):
         assert (g2.double() - ref).abs().le(1e-5 * bound + 1e-30).all(), n
         spread = (g0 - g1).abs().max().item()
         assert (g0.double() - g2.double()).abs().le(2e-5 * bound + 4 * spread + 1e-30).all(), (n, spread)
-    assert n_params + n_direct == len(steps[2].side.params)
+    assert n_params == len(steps[2].side.params) and n_direct == len(steps[2].side.direct_params)
+
+
+def test_grouped_wgrad_keeps_diffusion_time_grads_on_module_path(device, monkeypatch):
+    """On the per-module encoder path (FUSED_ENCODER = False) no kernel writes the diffusion-time
+    gradients whole (GroupedWgrad.direct is never called): autograd accumulates them into the
+    grouped step's .grad buffers, which end() must leave alone. Grouped and serial steps agree on
+    them (within fp32 spread) over two consecutive backwards, and they are nonzero."""
+    from dpfm_amd import diffusion_net as DN
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import TrainStep, make_frame_batch
+    monkeypatch.setattr(DN, "FUSED_ENCODER", False)
+    F, N = 2, 256
+    fb, op = make_frame_batch(F, N, N, seed=93, device=device)
+    crops = CropFormation(n1=N, npoint=N)(fb)
+    models = []
+    for _ in range(2):
+        torch.manual_seed(4)
+        models.append(DPFMNet().to(device))
+    serial, grouped = TrainStep(models[0], seed=3, grouped=False), TrainStep(models[1], seed=3, grouped=True)
+    assert grouped.side is not None and len(grouped.side.direct_params) > 0
+    for _ in range(2):  # the second backward must not add onto the first one's values
+        for s in (serial, grouped):
+            s.forward_backward(op, crops)
+        torch.cuda.synchronize()
+        n = 0
+        for (name, p0), p1 in zip(models[0].named_parameters(), models[1].parameters()):
+            if not name.endswith("diffusion_time"):
+                continue
+            g0, g1 = p0.grad, p1.grad
+            assert g1 is not None and float(g1.abs().max()) > 0, name
+            assert (g1 - g0).abs().max().item() <= 1e-5 * g0.abs().max().item(), name
+            n += 1
+        assert n == len(grouped.side.direct_params)
+        for s in (serial, grouped):
+            s.opt.zero_grad(set_to_none=True)
 
 
 def test_graphed_train_step_matches_eager(device):

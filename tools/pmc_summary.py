@@ -59,13 +59,35 @@ PER_ENTRY = {"pk_linear_ex": FAMILIES["pk_linear_fwd+ex"],
 # (the first kernel of each family is counted once per family launch)
 
 
-def read(dirpath, counter, min_grid=0, max_grid=None):
-    """kernel name -> (dispatches, summed counter value), dispatches filtered by grid size."""
+# the last kernel of every eager training step (pk_clip_rmsprop): dispatches after the last one
+# belong to bench.py's roofline probes (the configs[3] ball-query probe, the feature-distance
+# probe's 23 calls), not to a step
+STEP_END = "clip_rmsprop_kernel"
+
+
+def step_window_end(dirpath, counter):
+    """Dispatch_Id of the last step's closing kernel (None: no such kernel, no window)."""
+    end = None
+    for f in glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") == counter and STEP_END in row["Kernel_Name"]:
+                    d = int(row["Dispatch_Id"])
+                    end = d if end is None else max(end, d)
+    return end
+
+
+def read(dirpath, counter, min_grid=0, max_grid=None, in_steps=True):
+    """kernel name -> (dispatches, summed counter value), dispatches filtered by grid size and (in_steps)
+    to the eager steps' window (Dispatch_Id up to the last step's closing kernel)."""
     tot = defaultdict(lambda: [0, 0.0])
+    end = step_window_end(dirpath, counter) if in_steps else None
     for f in glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if row.get("Counter_Name") != counter:
+                    continue
+                if end is not None and int(row["Dispatch_Id"]) > end:
                     continue
                 grid = int(float(row.get("Grid_Size", 0) or 0))
                 if grid < min_grid or (max_grid is not None and grid > max_grid):
@@ -86,7 +108,9 @@ def main():
     res = {}
     for fam, names, lo, hi in [(f, n, 0, PROBE_GRID - 1) for f, n in FAMILIES.items()] + \
             [("pk_ball_query_mask@configs3_probe", FAMILIES["pk_ball_query_mask"], PROBE_GRID, None)]:
-        fetch, write = read(fetch_dir, "FETCH_SIZE", lo, hi), read(write_dir, "WRITE_SIZE", lo, hi)
+        steps = not fam.endswith("_probe")  # the probe entry: the dispatches after the steps
+        fetch = read(fetch_dir, "FETCH_SIZE", lo, hi, in_steps=steps)
+        write = read(write_dir, "WRITE_SIZE", lo, hi, in_steps=steps)
         def summed(tab, names=names, fam=fam):
             lead = names if fam in ANY_LEAD else names[:1]
             n_lead = sum(c for k, (c, _) in tab.items() if any(nm in k for nm in lead))

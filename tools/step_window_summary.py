@@ -67,6 +67,25 @@ def main():
         print(f"\nqueue {q}: {len(seq)} launches in the last step")
         for r in seq:
             print(f"  {(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3:8.2f}  {short(r['Kernel_Name'])}")
+    # head of every training replay: the first main-queue kernel after each clip + RMSprop, its
+    # start against the previous step's end and against the crop-formation stream's last kernel
+    # before it (the formed[k] event the replay waits on), and its duration
+    mq = max(byq.items(), key=lambda kv: len(kv[1]))[0]
+    side = [r for q, rs in byq.items() if q != mq for r in rs]
+    print("\nhead of each training replay (us): start - previous clip_rmsprop end, start - last side-queue "
+          "kernel end before it (negative: the head started before crop formation finished), duration")
+    mains = byq[mq]
+    for i, r in enumerate(mains):
+        if i == 0 or "clip_rmsprop_kernel" not in mains[i - 1]["Kernel_Name"]:
+            continue
+        st, prev_end = int(r["Start_Timestamp"]), int(mains[i - 1]["End_Timestamp"])
+        before = [int(x["End_Timestamp"]) for x in side if int(x["Start_Timestamp"]) < st]
+        last_side = max(before) if before else None
+        dur = int(r["End_Timestamp"]) - st
+        sk = [x for x in side if int(x["End_Timestamp"]) == last_side]
+        print(f"  {short(r['Kernel_Name'])[:40]:40s} gap {(st - prev_end) / 1e3:8.2f}  vs side "
+              f"{(st - last_side) / 1e3 if last_side else float('nan'):8.2f} ({short(sk[0]['Kernel_Name'])[:24] if sk else '-'})"
+              f"  dur {dur / 1e3:8.2f}")
     if ctx:
         print("\ntorch / runtime kernels in the window (queue, kernel, previous, next):")
         for (q, k, a, b), c in sorted(ctx.items(), key=lambda kv: -kv[1]):
