@@ -438,7 +438,7 @@ __global__ __launch_bounds__(kBqThreads) void bq_count_kernel(
 __global__ __launch_bounds__(1024) void bq_scan_kernel(const int32_t* __restrict__ rowcount,
                                                        int n1max, int64_t* __restrict__ rowoff,
                                                        int64_t* __restrict__ total, int8_t* __restrict__ ov21,
-                                                       int n2max) {
+                                                       int32_t* __restrict__ colcount, int n2max) {
   __shared__ int64_t wsum[16];
   __shared__ int64_t carry_s;
   const int b = blockIdx.x;
@@ -447,6 +447,8 @@ __global__ __launch_bounds__(1024) void bq_scan_kernel(const int32_t* __restrict
   // separate zero-fill launch
   if (ov21 != nullptr)
     for (int j = tid; j < n2max; j += 1024) ov21[(int64_t)b * n2max + j] = 0;
+  if (colcount != nullptr)  // (likewise the per-column pair counts the pairs kernel accumulates)
+    for (int j = tid; j < n2max; j += 1024) colcount[(int64_t)b * n2max + j] = 0;
   if (tid == 0) carry_s = 0;
   __syncthreads();
   for (int base = 0; base < n1max; base += 1024) {
@@ -474,7 +476,7 @@ __global__ __launch_bounds__(256) void bq_pairs_kernel(
     const uint8_t* __restrict__ mask, const int32_t* __restrict__ rowcount,
     const int64_t* __restrict__ rowoff, int64_t* __restrict__ pairs, int64_t cap,
     int8_t* __restrict__ ov12, int8_t* __restrict__ ov21, const int64_t* __restrict__ count, int B,
-    int32_t* __restrict__ over) {
+    int32_t* __restrict__ over, int32_t* __restrict__ colcount) {
   const int b = blockIdx.y;
   if (over != nullptr && blockIdx.x == 0 && b == 0) {  // the pass-1 totals are final: any above cap?
     int o = 0;
@@ -526,6 +528,8 @@ __global__ __launch_bounds__(256) void bq_pairs_kernel(
       if (w < cap) {
         pb[2 * w + 0] = i;
         pb[2 * w + 1] = j;
+        // pairs per crop point among the kept list (C_gt's G row weights; integer atomics: exact)
+        if (colcount != nullptr) atomicAdd(&colcount[(int64_t)b * n2max + j], 1);
       }
       if (ov21 != nullptr) ov21[(int64_t)b * n2max + j] = 1;
       ++w;
@@ -595,7 +599,7 @@ extern "C" int pk_ball_query_pairs(const double* cad, const int64_t* cad_off, co
                                    int n2max, const uint8_t* mask, int ld,
                                    const int32_t* rowcount, int64_t* rowoff, int64_t* pairs,
                                    int64_t cap, int64_t* count, int8_t* ov12, int8_t* ov21,
-                                   int32_t* over, void* stream) {
+                                   int32_t* over, int32_t* colcount, void* stream) {
   PK_REQUIRE(B >= 0 && n1max >= 0 && n2max >= 0 && cap >= 0);
   if (B == 0) return PK_OK;
   PK_REQUIRE(cad && cad_off && pc && pc_off && thr2 && rowcount && rowoff && count);
@@ -606,13 +610,14 @@ extern "C" int pk_ball_query_pairs(const double* cad, const int64_t* cad_off, co
     hipError_t e = ov21 != nullptr ? pk::zero_async(ov21, (size_t)B * n2max, s) : hipSuccess;
     if (e == hipSuccess) e = pk::zero_async(count, sizeof(int64_t) * B, s);
     if (e == hipSuccess && over != nullptr) e = pk::zero_async(over, sizeof(int32_t), s);
+    if (e == hipSuccess && colcount != nullptr) e = pk::zero_async(colcount, sizeof(int32_t) * (size_t)B * n2max, s);
     return e == hipSuccess ? PK_OK : (int)e;
   }
-  hipLaunchKernelGGL(bq_scan_kernel, dim3(B), dim3(1024), 0, s, rowcount, n1max, rowoff, count, ov21, n2max);
+  hipLaunchKernelGGL(bq_scan_kernel, dim3(B), dim3(1024), 0, s, rowcount, n1max, rowoff, count, ov21, colcount, n2max);
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(bq_pairs_kernel, dim3((n1max + 3) / 4, B), dim3(256), 0, s, cad, cad_off, pc,
                      pc_off, thr2, n1max, n2max, ld, mask, rowcount, rowoff, pairs, cap, ov12,
-                     ov21, count, B, over);
+                     ov21, count, B, over, colcount);
   PK_CHECK_LAUNCH();
   return PK_OK;
 }

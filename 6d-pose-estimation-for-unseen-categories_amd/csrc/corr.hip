@@ -773,7 +773,7 @@ __global__ __launch_bounds__(256) void cgt_partial_kernel(const int64_t* __restr
                                                           const int64_t* __restrict__ npairs,
                                                           const float* __restrict__ e1, int ld1, int V1max,
                                                           const float* __restrict__ e2, int ld2, int V2max,
-                                                          const int32_t* __restrict__ cnt, int SH,
+                                                          const int32_t* __restrict__ cnt, int ldc, int SH,
                                                           double* __restrict__ partH,
                                                           double* __restrict__ partG) {
   __shared__ double UV[2 * kCgtRows * 32];  // U rows, then V rows; reused for the wave combine
@@ -823,7 +823,7 @@ __global__ __launch_bounds__(256) void cgt_partial_kernel(const int64_t* __restr
     for (int i = 0; i < kPer; ++i) {
       fu[i] = e2[((int64_t)b * V2max + ja[i]) * ld2 + kc];
       if (isH) fv[i] = e1[((int64_t)b * V1max + ia[i]) * ld1 + kc];
-      else cv[i] = cnt[(int64_t)b * V2max + ja[i]];
+      else cv[i] = cnt[(int64_t)b * ldc + (ja[i] < ldc ? ja[i] : ldc - 1)];
     }
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
@@ -831,7 +831,7 @@ __global__ __launch_bounds__(256) void cgt_partial_kernel(const int64_t* __restr
       const bool ok = r < rn && k < kF;
       const double u = ok ? (double)fu[i] : 0.0;
       U[r][k] = u;
-      V[r][k] = ok ? (isH ? (double)fv[i] : u * (double)cv[i]) : 0.0;
+      V[r][k] = ok ? (isH ? (double)fv[i] : (ja[i] < ldc ? u * (double)cv[i] : 0.0)) : 0.0;
     }
   }
   __syncthreads();
@@ -1200,9 +1200,10 @@ extern "C" int64_t pk_cgt_lstsq_work_size(int ldp, int V2max, int B) {
 }
 
 extern "C" int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs, const float* evecs1, int ld1,
-                            int V1max, const float* evecs2, int ld2, int V2max, int B, int K, double* work,
-                            float* Cgt, void* stream) {
+                            int V1max, const float* evecs2, int ld2, int V2max, int B, int K, const int32_t* cnt,
+                            int ldc, double* work, float* Cgt, void* stream) {
   PK_REQUIRE(B >= 0 && K == kF && ld1 >= kF && ld2 >= kF && ldp >= 0 && V2max > 0);
+  PK_REQUIRE(cnt == nullptr || ldc > 0);
   if (B == 0) return PK_OK;
   PK_REQUIRE(pairs && npairs && evecs1 && evecs2 && work && Cgt);
   hipStream_t s = pk::as_stream(stream);
@@ -1211,16 +1212,20 @@ extern "C" int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs
   double* partH = work;
   double* partG = partH + (int64_t)B * SH * kFF;
   double* GH = partG + (int64_t)B * SG * kFF;
-  int32_t* cnt = reinterpret_cast<int32_t*>(GH + (int64_t)B * 2 * kFF);
-  hipError_t e = pk::zero_async(cnt, sizeof(int32_t) * (size_t)B * V2max, s);
-  if (e != hipSuccess) return (int)e;
-  if (ldp > 0) {
-    hipLaunchKernelGGL(cgt_count_kernel, dim3((ldp + 255) / 256, B), dim3(256), 0, s, pairs, ldp, npairs, V2max,
-                       cnt);
-    PK_CHECK_LAUNCH();
+  if (cnt == nullptr) {  // the per-row pair counts: counted here (a fill + an atomic-count launch)
+    int32_t* own = reinterpret_cast<int32_t*>(GH + (int64_t)B * 2 * kFF);
+    hipError_t e = pk::zero_async(own, sizeof(int32_t) * (size_t)B * V2max, s);
+    if (e != hipSuccess) return (int)e;
+    if (ldp > 0) {
+      hipLaunchKernelGGL(cgt_count_kernel, dim3((ldp + 255) / 256, B), dim3(256), 0, s, pairs, ldp, npairs, V2max,
+                         own);
+      PK_CHECK_LAUNCH();
+    }
+    cnt = own;
+    ldc = V2max;
   }
   hipLaunchKernelGGL(cgt_partial_kernel, dim3(SH + SG, B), dim3(256), 0, s, pairs, ldp, npairs, evecs1, ld1,
-                     V1max, evecs2, ld2, V2max, cnt, SH, partH, partG);
+                     V1max, evecs2, ld2, V2max, cnt, ldc, SH, partH, partG);
   PK_CHECK_LAUNCH();
   hipLaunchKernelGGL(cgt_reduce_kernel, dim3((2 * kFF + 63) / 64, B), dim3(256), 0, s, partH, partG, SH, SG,
                      npairs, ldp, V2max, GH);

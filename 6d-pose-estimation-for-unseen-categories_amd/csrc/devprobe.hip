@@ -119,7 +119,70 @@ __global__ __launch_bounds__(512, 2) void probe_mfma_kernel(const float* __restr
   out[(int64_t)blockIdx.x * blockDim.x + threadIdx.x] = sum;
 }
 
+// MFMA / VALU co-issue probe: like probe_mfma_kernel<2> (two accumulation chains of 8
+// v_mfma_f32_16x16x4f32 per step, the feature-distance tile shape), plus NV independent integer
+// VALU ops per 8 MFMAs (v_min_i32 on a state that does not feed the MFMAs, as the selection does).
+// Two waves per SIMD (512-thread blocks, one per CU). Time vs NV tells whether VALU issue hides
+// under the f32 MFMAs of the other wave / the same wave.
+template <int NV>
+__global__ __launch_bounds__(512, 1) void probe_mfma_valu_kernel(const float* __restrict__ seed, int iters,
+                                                                 float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  float a[8], b[2][8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    a[s] = seed[(lane * 8 + s) & 1023];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) b[c][s] = seed[(lane * 8 + s + 77 * c + 512) & 1023];
+  }
+  int z[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) z[k] = __float_as_int(seed[(lane + 9 * k) & 1023]);
+  f32x4 acc[2];
+  for (int it = 0; it < iters; ++it) {
+    acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[1] = acc[0];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[0][s], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[1][s], acc[1], 0, 0, 0);
+#pragma unroll
+      for (int v = 0; v < NV / 4; ++v)  // NV per 8 MFMAs: NV / 8 per MFMA, in pairs
+        asm volatile("v_min_i32_e32 %0, %1, %0" : "+v"(z[(s + v) & 7]) : "v"(z[(s + v + 3) & 7]));
+    }
+    // the selection-like consumer of the finished tile (keeps the MFMAs alive)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      z[r] = min(z[r], __float_as_int(acc[0][r]));
+      z[r + 4] = min(z[r + 4], __float_as_int(acc[1][r]));
+    }
+  }
+  int sum = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sum ^= z[k];
+  out[(int64_t)blockIdx.x * blockDim.x + threadIdx.x] = (float)sum;
+}
+
 }  // namespace
+
+extern "C" int pkdev_probe_mfma_valu(const float* seed, int blocks, int iters, int nv, float* out, void* stream) {
+  if (blocks <= 0 || iters <= 0) return PK_ERR_ARG;
+  hipStream_t s = pk::as_stream(stream);
+#define PK_PMV(N) hipLaunchKernelGGL(probe_mfma_valu_kernel<N>, dim3(blocks), dim3(512), 0, s, seed, iters, out)
+  switch (nv) {
+    case 0: PK_PMV(0); break;
+    case 8: PK_PMV(8); break;
+    case 16: PK_PMV(16); break;
+    case 24: PK_PMV(24); break;
+    case 32: PK_PMV(32); break;
+    case 48: PK_PMV(48); break;
+    case 64: PK_PMV(64); break;
+    default: return PK_ERR_ARG;
+  }
+#undef PK_PMV
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
 
 extern "C" int pkdev_probe_mfma(const float* seed, int blocks, int iters, float* out, long long* stamp,
                                 void* stream) {

@@ -50,7 +50,7 @@ class OverlapHeadArgs(ctypes.Structure):
 SIGNATURES = {
     "pk_fps": [_P, _P, _I, _I, _P, _P, _P, _I, _P],
     "pk_ball_query_mask": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P],
-    "pk_ball_query_pairs": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _I64, _P, _P, _P, _P, _P],
+    "pk_ball_query_pairs": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P],
     "pk_backproject": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P],
     "pk_sor": [_P, _P, _I, _I, _I, _D, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "pk_fps_npoint": [_P, _I, _I, _I, _U64, _I64, _P, _P, _P, _P],
@@ -96,7 +96,7 @@ SIGNATURES = {
     "pk_inlier_ratio": [_P, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P, _P],
     "pk_cgt_lstsq_work_size": [_I, _I, _I],
     "pk_nce_select": [_P, _I, _I64, _I, ctypes.c_uint64, _P, _P, _P, _P],
-    "pk_cgt_lstsq": [_P, _I, _P, _P, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P],
+    "pk_cgt_lstsq": [_P, _I, _P, _P, _I, _I, _P, _I, _I, _I, _I, _P, _I, _P, _P, _P],
     "pk_ransac_work_size": [_I, _I64, _I],
     "pk_ransac": [_P, _P, _P, _P, _P, _P, _P, _P, _U64, _I64, _D, _I, _I, _P, _I64, _P, _P, _P, _P],
     "pk_pose_metrics": [_P, _P, _I, _I, _P, _P, _P, _P, _P],

@@ -163,6 +163,9 @@ class Crops:
     # int32 [F] per crop 1 when an FPS index fell outside its crop (pk_gather_transform's check;
     # those points are NaN): checked by check(), never read on the step's path
     index_status: Optional[torch.Tensor] = None
+    # int32 [F, ld] pairs per crop point among the kept P (pk_ball_query_pairs' colcount): C_gt's
+    # row weights, formed with the crops so the step's C_gt needs no count launches
+    pair_cols: Optional[torch.Tensor] = None
 
     def overflow(self) -> torch.Tensor:
         """0-d flag on the device (nonzero: some crop had more ball-query pairs than pair_cap, its
@@ -232,4 +235,4 @@ class CropFormation:
         return Crops(pc64=g["sel64"], pc32=pc32, align64=g["align"], align32=align32, off=pol["off"], n2=n2, ld=ld,
                      npoint=pol["npoint"], pairs=bq["pairs"], npairs=bq["count"], overlap_12=bq["overlap_12"],
                      overlap_21=bq["overlap_21"], rgb=rgb, kept=so["kept"], pair_cap=self.pair_cap,
-                     overflow_flag=bq["overflow"], index_status=st)
+                     overflow_flag=bq["overflow"], index_status=st, pair_cols=bq["colcount"])

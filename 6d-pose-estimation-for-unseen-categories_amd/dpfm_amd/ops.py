@@ -61,11 +61,12 @@ def ball_threshold(r: float) -> float:
 
 def ball_query(cad: torch.Tensor, cad_off: torch.Tensor, pc: torch.Tensor, pc_off: torch.Tensor,
                radius: Sequence[float] | torch.Tensor, n1max: int, n2max: int, cap: int,
-               with_mask: bool = True, thr2: Optional[torch.Tensor] = None) -> dict:
+               with_mask: bool = True, thr2: Optional[torch.Tensor] = None, colcount: bool = True) -> dict:
     """find_positives for B packed crop pairs (pk_ball_query_mask + pk_ball_query_pairs).
 
     Returns dict(mask uint8 [B,n1max,ld] or None, rowcount int32 [B,n1max], pairs int64
-    [B,cap,2], count int64 [B], overlap_12 int8 [B,n1max], overlap_21 int8 [B,n2max]).
+    [B,cap,2], count int64 [B], overlap_12 int8 [B,n1max], overlap_21 int8 [B,n2max],
+    colcount int32 [B,n2max] or None: pairs per crop point among the kept list, C_gt's row weights).
     count[b] > cap means the pair list of crop b was truncated (check_capacity raises).
     """
     assert cad.dtype == torch.float64 and pc.dtype == torch.float64
@@ -87,11 +88,12 @@ def ball_query(cad: torch.Tensor, cad_off: torch.Tensor, pc: torch.Tensor, pc_of
     ov12 = torch.empty((B, n1max), dtype=torch.int8, device=dev)
     ov21 = torch.empty((B, n2max), dtype=torch.int8, device=dev)
     over = torch.empty((1,), dtype=torch.int32, device=dev)
+    cc = torch.empty((B, n2max), dtype=torch.int32, device=dev) if colcount else None
     call("pk_ball_query_pairs", ptr(cad), ptr(cad_off), ptr(pc), ptr(pc_off), ptr(thr2), B, int(n1max),
          int(n2max), ptr(mask), int(ld), ptr(rowcount), ptr(rowoff), ptr(pairs), int(cap), ptr(count),
-         ptr(ov12), ptr(ov21), ptr(over), s)
+         ptr(ov12), ptr(ov21), ptr(over), ptr(cc), s)
     return dict(mask=mask, rowcount=rowcount, pairs=pairs, count=count, overlap_12=ov12, overlap_21=ov21,
-                thr2=thr2, overflow=over[0])
+                thr2=thr2, overflow=over[0], colcount=cc)
 
 
 def check_index_status(status: Optional[torch.Tensor], what: str) -> None:
@@ -1268,14 +1270,19 @@ def mean_f32(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tenso
     return out
 
 
-def cgt_lstsq(pairs: torch.Tensor, npairs: torch.Tensor, evecs1: torch.Tensor, evecs2: torch.Tensor) -> torch.Tensor:
+def cgt_lstsq(pairs: torch.Tensor, npairs: torch.Tensor, evecs1: torch.Tensor, evecs2: torch.Tensor,
+              cnt: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """C_from_sparse_P for every crop (pk_cgt_lstsq). cnt int32 [B, ldc] (optional): the pairs per
+    crop row among the kept list (ball_query's colcount); without it the call counts them."""
     B, L, _ = pairs.shape
+    if cnt is not None:
+        assert cnt.dtype == torch.int32 and cnt.dim() == 2 and cnt.shape[0] == B and cnt.is_contiguous()
     out = torch.empty((B, 30, 30), dtype=torch.float32, device=pairs.device)
     nwork = _lib.lib().pk_cgt_lstsq_work_size(L, evecs2.shape[1], B)
     work = torch.empty((nwork,), dtype=torch.float64, device=pairs.device)
     call("pk_cgt_lstsq", ptr(pairs.contiguous()), L, ptr(npairs), ptr(evecs1.contiguous()), evecs1.shape[2],
-         evecs1.shape[1], ptr(evecs2.contiguous()), evecs2.shape[2], evecs2.shape[1], B, 30, ptr(work), ptr(out),
-         _lib.stream(pairs.device))
+         evecs1.shape[1], ptr(evecs2.contiguous()), evecs2.shape[2], evecs2.shape[1], B, 30, ptr(cnt),
+         int(cnt.shape[1]) if cnt is not None else 0, ptr(work), ptr(out), _lib.stream(pairs.device))
     return out
 
 

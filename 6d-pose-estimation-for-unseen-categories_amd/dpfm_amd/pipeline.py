@@ -318,7 +318,7 @@ class TrainStep:
     def ground_truth(op: Operators, crops: Crops) -> torch.Tensor:
         """C_gt of the crops (utils/utils.py:67-79): reads only P and the two bases, so a
         producer may form it with the crops (Crops.C_gt) off the step's critical path."""
-        return ops.cgt_lstsq(crops.pairs, crops.npairs, op.cad_evecs, op.pc_evecs)
+        return ops.cgt_lstsq(crops.pairs, crops.npairs, op.cad_evecs, op.pc_evecs, cnt=crops.pair_cols)
 
     @staticmethod
     @torch.no_grad()

@@ -53,12 +53,14 @@ int pk_ball_query_mask(const double* cad, const int64_t* cad_off, const double* 
  *   rowoff int64 [B, n1max] scratch (exclusive scan of rowcount)
  *   pairs int64 [B, cap, 2] (i, j) in row-major order, count int64 [B] true totals
  *   ov12 int8 [B, n1max], ov21 int8 [B, n2max] (either may be NULL)
- *   over int32 [1] or NULL: 1 when some crop's count exceeds cap (its pair list was truncated) */
+ *   over int32 [1] or NULL: 1 when some crop's count exceeds cap (its pair list was truncated)
+ *   colcount int32 [B, n2max] or NULL: per crop point j, the pairs (i, j) among the first cap of
+ *            the list (the row weights of C_gt's normal equations: pk_cgt_lstsq's cnt) */
 int pk_ball_query_pairs(const double* cad, const int64_t* cad_off, const double* pc,
                         const int64_t* pc_off, const double* thr2, int B, int n1max, int n2max,
                         const uint8_t* mask, int ld, const int32_t* rowcount, int64_t* rowoff,
                         int64_t* pairs, int64_t cap, int64_t* count, int8_t* ov12, int8_t* ov21,
-                        int32_t* over, void* stream);
+                        int32_t* over, int32_t* colcount, void* stream);
 
 /* H1 crop formation. Replaces dataset/object.py:73-88 dpt_2_pcld (with the plus-shaped
  * erode_seg_mask of :52-71 and `seg == 255` of :137) for F frames at once.
@@ -456,7 +458,10 @@ int pk_mean_f32(const float* x, int64_t n, float* out, void* stream);
  * evecs2[P[:,1], :30] X = evecs1[P[:,0], :30] per crop (fp64 normal equations: G from the
  * per-row pair counts, H over 64-pair slices; Gauss-Jordan with partial pivoting).
  * pairs int64 [B,ldp,2] (any order), npairs int64 [B]; evecs f32 [B,Vmax,ld]; K must be
- * 30; work f64 [pk_cgt_lstsq_work_size(ldp, V2max, B)]; Cgt f32 [B,30,30]. */
+ * 30; work f64 [pk_cgt_lstsq_work_size(ldp, V2max, B)]; Cgt f32 [B,30,30].
+ * cnt int32 [B, ldc] or NULL: per crop row j the pairs with crop index j among the first
+ * min(npairs, ldp) (pk_ball_query_pairs' colcount, formed with the crops; rows j >= ldc count 0);
+ * NULL: counted here (one fill + one integer-atomic count launch). */
 int64_t pk_cgt_lstsq_work_size(int ldp, int V2max, int B);
 
 /* NCE pair selection (utils/loss.py:27-30: np.random.choice(P, num, replace=False) per
@@ -497,8 +502,8 @@ int pk_loss_head(const float* C12, const float* Cgt, int B, int K, const float* 
 int pk_loss_scale(const float* const* src, float* const* dst, const int64_t* numel, const float* scale, int n,
                   const float* g, void* stream);
 int pk_cgt_lstsq(const int64_t* pairs, int ldp, const int64_t* npairs, const float* evecs1, int ld1,
-                 int V1max, const float* evecs2, int ld2, int V2max, int B, int K, double* work,
-                 float* Cgt, void* stream);
+                 int V1max, const float* evecs2, int ld2, int V2max, int B, int K, const int32_t* cnt,
+                 int ldc, double* work, float* Cgt, void* stream);
 
 /* H13 RANSAC + Umeyama (scripts/test_RANSAC.py:288-310, Open3D 0.17 semantics, ransac_n 4).
  *   src f64 (CAD) / dst f64 (crop, camera frame) packed [T,3] with src_off/dst_off [B+1];

@@ -119,3 +119,29 @@ def test_ball_query_capacity_overflow_reported(device):
         ops.check_capacity(res["count"], 100)
     exp = O.find_positives(c, p, 1.0)[:100]
     np.testing.assert_array_equal(res["pairs"][0].cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("cap", [100, 1 << 16])
+def test_ball_query_colcount_and_cgt_from_it(device, cap):
+    """pk_ball_query_pairs' colcount (pairs per crop point among the kept list, integer atomics)
+    equals a bincount of the kept pairs' crop indices, truncated lists included; pk_cgt_lstsq fed
+    with it returns bit for bit what it returns counting the pairs itself (same fp64 sums)."""
+    from dpfm_amd import ops
+    rng = np.random.default_rng(11)
+    cs = [rng.normal(size=(n, 3)) * 2 for n in (300, 64, 1)]
+    ps = [rng.normal(size=(n, 3)) * 2 for n in (250, 64, 5)]
+    cad, coff = _packed(cs, np.float64, device)
+    pc, poff = _packed(ps, np.float64, device)
+    n1max, n2max = 300, 250
+    res = ops.ball_query(cad, coff, pc, poff, [1.0, 3.0, 0.5], n1max, n2max, cap)
+    cc = res["colcount"].cpu().numpy()
+    for b in range(3):
+        k = min(int(res["count"][b]), cap)
+        exp = np.bincount(res["pairs"][b, :k, 1].cpu().numpy(), minlength=n2max)
+        np.testing.assert_array_equal(cc[b], exp)
+    g = torch.Generator().manual_seed(3)
+    e1 = torch.randn(3, n1max, 32, generator=g).to(device)
+    e2 = torch.randn(3, n2max, 32, generator=g).to(device)
+    a = ops.cgt_lstsq(res["pairs"], res["count"], e1, e2)
+    b_ = ops.cgt_lstsq(res["pairs"], res["count"], e1, e2, cnt=res["colcount"])
+    assert torch.equal(a, b_)

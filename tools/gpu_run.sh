@@ -33,6 +33,12 @@ for step in "$@"; do
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline-probe
           find "$out/prof" -type f ! -name "*stats.csv" -delete ;;
     kbench) run kbench 300 python tools/kbench.py ;;
+    steptrace) run steptrace_bench 400 rocprofv3 --kernel-trace --output-format csv -d "$out/steptrace" -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roofline-probe --probe-steps 0
+               tail -1 "$out/steptrace_bench.log" > "$out/steptrace.json"
+               python tools/step_window_summary.py $(find "$out/steptrace" -name "*kernel_trace.csv" | head -1) "$out/steptrace.json" > "$out/step_window_summary.txt" 2>&1
+               find "$out/steptrace" -type f -delete ;;
+    fdstamps) PK_FD_VAR=13 run fdstamps 200 python tools/fd_stamps.py ;;
+    mvprobe) run mvprobe 200 python tools/mfma_valu_probe.py ;;
     kprof) run kprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kprof" -o run -- python tools/kbench.py
           find "$out/kprof" -type f ! -name "*stats.csv" -delete ;;
     pmcm) run pmcm 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$out/pmcm" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager --probe-steps 1
