@@ -3,7 +3,7 @@ HIP graphs (no host gaps): configs[1] (32 crops of 1024 x 1024) and configs[4] (
 4096 crop), every precision mode. Prints achieved TFLOP/s and, for the bf16 modes, the
 argmin / top-5 agreement with the fp32 path.
 
-  python tools/fd_bench.py [iters] [BxV] [precisions, comma-separated]
+  python tools/fd_bench.py [iters] [BxV] [precisions, comma-separated] [top-k values, comma-separated]
 """
 import os
 import sys
@@ -30,7 +30,8 @@ for B, V in [(32, 1024), (8, 2048), (1, 4096)]:
     C = (torch.eye(30)[None] + 0.3 * torch.randn(B, 30, 30, generator=torch.Generator().manual_seed(B))).to(dev)
     n = torch.full((B,), V, dtype=torch.int32, device=dev)
     ref = {}
-    for topk in ((1,) if only else (1, 5)):
+    topks = tuple(int(x) for x in sys.argv[4].split(",")) if len(sys.argv) > 4 else ((1,) if only else (1, 5))
+    for topk in topks:
         for prec in precs:
             wk = torch.zeros(1 << 24, dtype=torch.uint8, device=dev)  # one zeroed scratch, reused
             f = lambda: ops.feat_dist_topk(ex, C, ey, n, n, topk, precision=prec, work=wk)  # noqa: E731

@@ -34,11 +34,12 @@ for step in "$@"; do
           find "$out/prof" -type f ! -name "*stats.csv" -delete ;;
     kbench) run kbench 300 python tools/kbench.py ;;
     steptrace) run steptrace_bench 400 rocprofv3 --kernel-trace --output-format csv -d "$out/steptrace" -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roofline-probe --probe-steps 0
-               tail -1 "$out/steptrace_bench.log" > "$out/steptrace.json"
+               grep "^{\"metric\"" "$out/steptrace_bench.log" | tail -1 > "$out/steptrace.json"
                python tools/step_window_summary.py $(find "$out/steptrace" -name "*kernel_trace.csv" | head -1) "$out/steptrace.json" > "$out/step_window_summary.txt" 2>&1
                find "$out/steptrace" -type f -delete ;;
     fdstamps) PK_FD_VAR=13 run fdstamps 200 python tools/fd_stamps.py ;;
     mvprobe) run mvprobe 200 python tools/mfma_valu_probe.py ;;
+    pmcstep) TAG=$tag/pmcstep run pmcstep 700 bash tools/pmc_step.sh ;;
     kprof) run kprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kprof" -o run -- python tools/kbench.py
           find "$out/kprof" -type f ! -name "*stats.csv" -delete ;;
     pmcm) run pmcm 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$out/pmcm" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager --probe-steps 1
@@ -49,9 +50,9 @@ for step in "$@"; do
          python tools/pmc_summary.py "$out/pmcf" "$out/pmcw" "$out/pmc_traffic.json" > "$out/pmc_summary.log" 2>&1
          find "$out/pmcf" "$out/pmcw" -type f -name "*.csv" -size +2M -delete ;;
     fdb) run fdb 300 python tools/fd_bench.py ;;
-    fdpmc) run fdpmc1 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$out/fdpmc1" -o run -- python tools/fd_bench.py 2
-           python tools/mfma_util.py "$out/fdpmc1" fd_main_kernel fd_prep_kernel > "$out/mfma_util.json" 2>&1
-           run fdpmc2 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$out/fdpmc2" -o run -- python tools/fd_bench.py 2 ;;
+    fdpmc) run fdpmc1 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$out/fdpmc1" -o run -- python tools/fd_bench.py 5 32x1024 fp32 1,5
+           python tools/mfma_util.py "$out/fdpmc1" fd_top1_kernel fd_top1_prep_kernel fd_top1_merge fd_main_direct_kernel fd_prep_kernel fd_merge_kernel > "$out/mfma_util.json" 2>&1
+           python tools/pmc_pick.py "$out/fdpmc1" fd_ > "$out/fd_pmc_counters.txt" 2>&1 || true ;;
     tprof) run tprof 300 python tools/torch_prof.py "$tag" ;;
     rdiag2) run rdiag2 300 python tools/replay_diag2.py ;;
     rdiag3) run rdiag3 300 python tools/replay_diag3.py ;;

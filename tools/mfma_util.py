@@ -26,6 +26,7 @@ def main():
             names[did], grids[did] = r["Kernel_Name"], r.get("Grid_Size", "")
             per[did][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = collections.defaultdict(list)
+    raw = collections.defaultdict(lambda: collections.defaultdict(list))
     for did, c in per.items():
         n = names[did]
         k = next((k for k in keys if k in n), None)
@@ -34,7 +35,17 @@ def main():
         busy, gui = sum(c["SQ_VALU_MFMA_BUSY_CYCLES"]), max(c["GRBM_GUI_ACTIVE"])
         short = re.split(r"[(<]", n.replace("(anonymous namespace)::", "").replace("void ", ""))[0][-60:]
         out[(short, grids[did])].append(busy / (gui * SIMDS))
-    res = {f"{n} grid={g}": {"mfma_util": round(sum(v) / len(v), 4), "dispatches": len(v)} for (n, g), v in out.items()}
+        for cn, vals in c.items():  # every counter of the pass, summed over its instances
+            raw[(short, grids[did])][cn].append(sum(vals) if cn != "GRBM_GUI_ACTIVE" else max(vals))
+    res = {}
+    for (n, g), v in out.items():
+        r = {"mfma_util": round(sum(v) / len(v), 4), "dispatches": len(v)}
+        cs = {cn: sum(x) / len(x) for cn, x in raw[(n, g)].items()}
+        r["counters_per_dispatch"] = {cn: float(f"{x:.4g}") for cn, x in sorted(cs.items())}
+        if cs.get("SQ_INSTS_MFMA"):
+            r["valu_per_mfma"] = round(cs.get("SQ_INSTS_VALU", 0.0) / cs["SQ_INSTS_MFMA"], 3)
+            r["mfma_busy_per_mfma"] = round(cs["SQ_VALU_MFMA_BUSY_CYCLES"] / cs["SQ_INSTS_MFMA"], 2)
+        res[f"{n} grid={g}"] = r
     print(json.dumps(res, indent=1))
 
 
