@@ -163,7 +163,57 @@ __global__ __launch_bounds__(512, 1) void probe_mfma_valu_kernel(const float* __
   out[(int64_t)blockIdx.x * blockDim.x + threadIdx.x] = (float)sum;
 }
 
+// f32 MFMA accumulation-order probe: one wave per 16 x 16 tile, K = 32 in 8 chained
+// v_mfma_f32_16x16x4f32 (slot (step s, lane group g) = k 4 s + g, the feature-distance layout),
+// D[i][j] = sum_k A[i][k] B[k][j]; beside it each lane forms its 4 outputs (rows 4 g + r, column
+// c) three ways: H1 one fmaf chain over k = 0..31 in order; H2 per instruction the 4 products
+// exact (fp64) summed with the accumulator, one rounding to f32; H3 per instruction an fmaf
+// chain of its 4 products from 0, then added to the accumulator. out [tiles][4][256]: MFMA, H1-H3.
+__global__ __launch_bounds__(64) void probe_mfma_order_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                            float* __restrict__ out) {
+  const int t = blockIdx.x, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+  const float* At = A + (int64_t)t * 16 * 32;  // [16][32]
+  const float* Bt = B + (int64_t)t * 32 * 16;  // [32][16]
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(At[c * 32 + 4 * s + g], Bt[(4 * s + g) * 16 + c], acc, 0, 0, 0);
+  float* o = out + (int64_t)t * 4 * 256;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = 4 * g + r;
+    float h1 = 0.f, h3 = 0.f;
+    double h2d = 0.0;
+    float h2 = 0.f;
+    for (int s = 0; s < 8; ++s) {
+      double p = 0.0;
+      float h3i = 0.f;
+      for (int q = 0; q < 4; ++q) {
+        const int k = 4 * s + q;
+        const float a = At[i * 32 + k], b = Bt[k * 16 + c];
+        h1 = fmaf(a, b, h1);
+        p += (double)a * (double)b;
+        h3i = fmaf(a, b, h3i);
+      }
+      h2 = (float)((double)h2 + p);
+      h3 = h3 + h3i;
+      (void)h2d;
+    }
+    o[0 * 256 + i * 16 + c] = acc[r];
+    o[1 * 256 + i * 16 + c] = h1;
+    o[2 * 256 + i * 16 + c] = h2;
+    o[3 * 256 + i * 16 + c] = h3;
+  }
+}
+
 }  // namespace
+
+extern "C" int pkdev_probe_mfma_order(const float* A, const float* B, int tiles, float* out, void* stream) {
+  if (tiles <= 0) return PK_ERR_ARG;
+  hipLaunchKernelGGL(probe_mfma_order_kernel, dim3(tiles), dim3(64), 0, pk::as_stream(stream), A, B, out);
+  PK_CHECK_LAUNCH();
+  return PK_OK;
+}
 
 extern "C" int pkdev_probe_mfma_valu(const float* seed, int blocks, int iters, int nv, float* out, void* stream) {
   if (blocks <= 0 || iters <= 0) return PK_ERR_ARG;

@@ -39,6 +39,7 @@ for step in "$@"; do
                find "$out/steptrace" -type f -delete ;;
     fdstamps) PK_FD_VAR=13 run fdstamps 200 python tools/fd_stamps.py ;;
     mvprobe) run mvprobe 200 python tools/mfma_valu_probe.py ;;
+    moprobe) run moprobe 200 python tools/mfma_order_probe.py ;;
     pmcstep) TAG=$tag/pmcstep run pmcstep 700 bash tools/pmc_step.sh ;;
     kprof) run kprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kprof" -o run -- python tools/kbench.py
           find "$out/kprof" -type f ! -name "*stats.csv" -delete ;;

@@ -1,6 +1,7 @@
 """MFMA utilisation per kernel from a rocprofv3 --pmc pass holding SQ_VALU_MFMA_BUSY_CYCLES
-and GRBM_GUI_ACTIVE (rocprofv3's own MfmaUtil expression: sum over SIMDs of the MFMA-busy
-cycles / (max over instances of GRBM_GUI_ACTIVE x 1024 SIMDs)).
+and GRBM_GUI_ACTIVE: the MFMA-busy cycles summed over the SIMDs / (the kernel's GPU-busy cycles x
+1024 SIMDs), where the kernel's cycles are GRBM_GUI_ACTIVE / 8 (rocprofv3 reports GRBM_GUI_ACTIVE
+summed over the 8 XCDs: MI355X_MICROARCH.md, DVFS give-back).
 
   python tools/mfma_util.py <pmc dir> [kernel-name substring ...]
 """
@@ -32,11 +33,11 @@ def main():
         k = next((k for k in keys if k in n), None)
         if k is None or "SQ_VALU_MFMA_BUSY_CYCLES" not in c or "GRBM_GUI_ACTIVE" not in c:
             continue
-        busy, gui = sum(c["SQ_VALU_MFMA_BUSY_CYCLES"]), max(c["GRBM_GUI_ACTIVE"])
+        busy, gui = sum(c["SQ_VALU_MFMA_BUSY_CYCLES"]), sum(c["GRBM_GUI_ACTIVE"]) / 8.0
         short = re.split(r"[(<]", n.replace("(anonymous namespace)::", "").replace("void ", ""))[0][-60:]
         out[(short, grids[did])].append(busy / (gui * SIMDS))
         for cn, vals in c.items():  # every counter of the pass, summed over its instances
-            raw[(short, grids[did])][cn].append(sum(vals) if cn != "GRBM_GUI_ACTIVE" else max(vals))
+            raw[(short, grids[did])][cn].append(sum(vals))
     res = {}
     for (n, g), v in out.items():
         r = {"mfma_util": round(sum(v) / len(v), 4), "dispatches": len(v)}
