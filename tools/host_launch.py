@@ -9,8 +9,8 @@ import bench
 
 dev = torch.device("cuda:0")
 torch.cuda.set_device(dev)
-args = types.SimpleNamespace(batch=32, points=1024, eager=False, train_only=False, no_overlap=False, ragged=False,
-                               cad_points=1024, infer_stages=2)
+sys.argv = [sys.argv[0]]
+args = bench.parse()  # the bench's defaults (configs[1] training, crop formation overlapped)
 tr, _, _, _, _ = bench.build_train(args, dev, 0, 1)
 for _ in range(5):
     tr()
