@@ -65,8 +65,9 @@ def main():
     for q, rs in sorted(byq.items(), key=lambda kv: -len(kv[1])):
         seq = [r for r in rs if int(r["Start_Timestamp"]) >= lo2]
         print(f"\nqueue {q}: {len(seq)} launches in the last step")
-        for r in seq:
-            print(f"  {(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3:8.2f}  {short(r['Kernel_Name'])}")
+        for r in seq:  # duration, then start / end relative to the step's start (the last clip_rmsprop end)
+            print(f"  {(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3:8.2f}  {short(r['Kernel_Name']):60s}"
+                  f" @ {(int(r['Start_Timestamp']) - lo2) / 1e3:8.1f} .. {(int(r['End_Timestamp']) - lo2) / 1e3:8.1f}")
     # head of every training replay: the first main-queue kernel after each clip + RMSprop, its
     # start against the previous step's end and against the crop-formation stream's last kernel
     # before it (the formed[k] event the replay waits on), and its duration
