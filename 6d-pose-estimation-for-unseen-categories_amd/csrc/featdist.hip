@@ -897,6 +897,375 @@ __global__ __launch_bounds__(256) void fd_top1_merge_kernel(const unsigned long 
   if (out_dist) out_dist[(int64_t)b * V2max + j] = sqrtf(__int_as_float((int)(best >> 32)));
 }
 
+// ---------------------------------------------------------------------------------------------
+// Top-5 fp32 (round 6): the configured solver's candidates, nn_query's dist.sort(dim=-2)[1].T[:, :5]
+// (spacial_filtering.py:32-38; config/dpfm_orig.gin:71). Pass 1 is fd_top1_prep_kernel. Pass 2,
+// fd_top5_kernel, keeps fd_top1_kernel's layout (block = crop b x 128 columns x row part rs, 8 waves
+// splitting the row tiles, the columns' B operands in registers) and its selection cost: on gfx950
+// the f32 MFMAs and the VALU issue one after the other (tools/mfma_valu_probe.py: every VALU op
+// adds its issue cycles to the MFMA time), so the per-distance work is 4 instructions. Per STREAM =
+// (column tile c, row offset r) of a lane — rows 16 t + 4 g + r of its column over the wave's
+// tiles — the smallest key with its tile (compare, min, select: the top-1 pass's three) and the
+// second smallest key's value (v_med3). The column's five are found among the streams after the
+// loop:
+//   E0/E1  T = the 5th smallest of the column's 32 lane minima (min over r): 32 distinct rows'
+//          distances, so an upper bound of the 5th smallest distance;
+//   E2     every stream whose minimum is <= T appends (key, row, second value, stream) to the
+//          column's candidate list in LDS (16 slots);
+//   E3     one thread per column sorts the candidates by (value, row) and keeps five. A kept stream
+//          other than the fifth whose second value is <= the fifth value may hold more members:
+//          its rows are recomputed exactly (the f32 MFMA accumulates as one fmaf chain over the
+//          contraction slots in order, bit for bit: tools/mfma_order_probe.py) and merged;
+//   slow   a column with more than 16 candidates, or a distance at or below torch.cdist's
+//          clamp_min(1e-30), is recomputed whole by one wave (clamped; ties to the lower row).
+// RS > 1: each row part writes its five to part_v / part_i and fd_merge_kernel<5> merges them.
+constexpr int kT5Slots = 16;
+
+// the exact distance of row `row` (tile t, in-tile i) and block column jj, as the MFMA chain forms it
+__device__ __forceinline__ float t5_exact(const f32x4* __restrict__ Ab, int t, int i, const f32x4 (*sB)[2][64],
+                                          int jj) {
+  float acc = 0.f;
+  const f32x4* At = Ab + (int64_t)t * 128;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)  // step s = 4 h + q, then the lane groups in order
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg)
+        acc = fmaf(At[h * 64 + gg * 16 + i][q], sB[jj >> 4][h][gg * 16 + (jj & 15)][q], acc);
+  return acc;
+}
+
+// insert key (value bits << 32 | row, unsigned order) into an ascending 5-list
+__device__ __forceinline__ void t5_insert(unsigned long long (&best)[5], unsigned long long key) {
+  if (!(key < best[4])) return;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const bool sw = key < best[q];
+    const unsigned long long tv = sw ? best[q] : key;
+    best[q] = sw ? key : best[q];
+    key = tv;
+  }
+}
+
+// value-only compare-exchange and the sorted merges of E1
+__device__ __forceinline__ void ce_i(int& a, int& b) {
+  const int lo = min(a, b), hi = max(a, b);
+  a = lo;
+  b = hi;
+}
+
+template <int VAR = 0>
+__global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
+    const f32x4* __restrict__ Atile, int T1, const float* __restrict__ ey, int ldy, const int32_t* __restrict__ n1,
+    const int32_t* __restrict__ n2, int V2max, int NCG, int RS, int64_t* __restrict__ out_idx,
+    float* __restrict__ out_dist, float* __restrict__ part_v, int32_t* __restrict__ part_i) {
+  constexpr int NC = kTop1CT * 16;  // columns per block
+  __shared__ f32x4 sB[kTop1CT][2][64];
+  __shared__ float sPart[4][NC];
+  __shared__ int sLm[NC][4 * kTop1Waves + 1];
+  __shared__ int sT[NC];
+  __shared__ int sCnt[NC];
+  __shared__ unsigned long long sKey[NC][kT5Slots];
+  __shared__ int sK2[NC][kT5Slots];
+  __shared__ int sStr[NC][kT5Slots];
+  __shared__ int sSlow[NC];
+  __shared__ int sNslow;
+  const int per = NCG * RS;
+  const int B = (int)(gridDim.x / per);
+  int b, k;
+  {  // all blocks of crop b on XCD b % 8 when B % 8 == 0 (as fd_top1_kernel)
+    const int L = blockIdx.x;
+    if ((B & 7) == 0) {
+      const int x8 = L & 7, q = L >> 3;
+      b = x8 + 8 * (q / per);
+      k = q - (q / per) * per;
+    } else {
+      b = L / per;
+      k = L - b * per;
+    }
+  }
+  const int cg = k % NCG, rs = k / NCG;
+  const int N1 = n1[b], N2 = n2[b];
+  const int j0 = cg * NC;
+  if (j0 >= N2) return;  // (block-uniform)
+  const int tid = threadIdx.x, lane = pk::lane_id(), w = __builtin_amdgcn_readfirstlane(pk::wave_id());
+  const int g = lane >> 4, c16 = lane & 15;
+  const int nt = (N1 + 15) >> 4;
+  const int Q = RS * kTop1Waves;
+  const int qw = rs * kTop1Waves + w;
+  const int tb = (int)((int64_t)nt * qw / Q), te = (int)((int64_t)nt * (qw + 1) / Q);  // this wave's row tiles
+  const f32x4* Ab = Atile + (int64_t)b * T1 * 128;
+  auto opload = [&](int t, float4 (&xv)[2]) {
+    const f32x4 u0 = Ab[(int64_t)t * 128 + lane], u1 = Ab[(int64_t)t * 128 + 64 + lane];
+    xv[0] = make_float4(u0[0], u0[1], u0[2], u0[3]);
+    xv[1] = make_float4(u1[0], u1[1], u1[2], u1[3]);
+  };
+  float4 xc[2], xn[2];
+  float a[8];
+  if (tb < te) {
+    opload(tb, xc);
+    opload(min(tb + 1, te - 1), xn);
+  }
+  float bo[kTop1CT][8];
+  {  // staging: the block's 128 columns' [y, 1, |y|^2] in B order, through LDS (as fd_top1_kernel)
+    const int jj = tid & (NC - 1), gy = tid >> 7;
+    const int j = j0 + jj;
+    const float* yr = ey + ((int64_t)b * V2max + min(j, V2max - 1)) * ldy;
+    const float4 y0 = *reinterpret_cast<const float4*>(yr + 4 * gy);
+    const float4 y1 = *reinterpret_cast<const float4*>(yr + 16 + 4 * gy);
+    const bool ok = j < N2;
+    float v[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+    float part_ = 0.f;
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) {
+      v[s8] = (ok && (s8 < 6 || gy < 3)) ? v[s8] : 0.f;
+      part_ = fmaf(v[s8], v[s8], part_);
+    }
+    sPart[gy][jj] = part_;
+    if (tb < te) {
+      a[0] = xc[0].x, a[1] = xc[0].y, a[2] = xc[0].z, a[3] = xc[0].w;
+      a[4] = xc[1].x, a[5] = xc[1].y, a[6] = xc[1].z, a[7] = xc[1].w;
+    }
+    if (tid < NC) sCnt[tid] = 0;
+    if (tid == 0) sNslow = 0;
+    __syncthreads();
+    if (gy == 3) {
+      float nrm = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nrm += sPart[q][jj];
+      v[6] = 1.f;
+      v[7] = nrm;
+    }
+    const int c = jj >> 4, l = gy * 16 + (jj & 15);
+    sB[c][0][l] = f32x4{v[0], v[1], v[2], v[3]};
+    sB[c][1][l] = f32x4{v[4], v[5], v[6], v[7]};
+    __syncthreads();
+#pragma unroll
+    for (int c2 = 0; c2 < kTop1CT; ++c2)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 t4 = sB[c2][h][lane];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bo[c2][4 * h + q] = t4[q];
+      }
+  }
+  int k1[kTop1CT][4], t1[kTop1CT][4], k2[kTop1CT][4];
+#pragma unroll
+  for (int c = 0; c < kTop1CT; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      k1[c][r] = 0x7f800000;  // +inf: never replaced by an equal key (padding rows are +inf)
+      k2[c][r] = 0x7f800000;
+      t1[c][r] = 0x07ffffff;
+    }
+  // per distance: compare (lane mask), second value = med3(key, min, second), min, select the tile
+  auto sel = [&](const f32x4& acc, int c, int t) {
+    unsigned long long m0, m1, m2, m3;
+    asm("v_cmp_lt_i32_e64 %[m0], %[k0], %[b0]\n\t"
+        "v_cmp_lt_i32_e64 %[m1], %[k1], %[b1]\n\t"
+        "v_cmp_lt_i32_e64 %[m2], %[k2], %[b2]\n\t"
+        "v_cmp_lt_i32_e64 %[m3], %[k3], %[b3]\n\t"
+        "v_med3_i32 %[s0], %[k0], %[b0], %[s0]\n\t"
+        "v_med3_i32 %[s1], %[k1], %[b1], %[s1]\n\t"
+        "v_med3_i32 %[s2], %[k2], %[b2], %[s2]\n\t"
+        "v_med3_i32 %[s3], %[k3], %[b3], %[s3]\n\t"
+        "v_min_i32_e32 %[b0], %[k0], %[b0]\n\t"
+        "v_min_i32_e32 %[b1], %[k1], %[b1]\n\t"
+        "v_min_i32_e32 %[b2], %[k2], %[b2]\n\t"
+        "v_min_i32_e32 %[b3], %[k3], %[b3]\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[tv], %[m0]\n\t"
+        "v_cndmask_b32_e64 %[t1], %[t1], %[tv], %[m1]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t2], %[tv], %[m2]\n\t"
+        "v_cndmask_b32_e64 %[t3], %[t3], %[tv], %[m3]"
+        : [b0] "+v"(k1[c][0]), [b1] "+v"(k1[c][1]), [b2] "+v"(k1[c][2]), [b3] "+v"(k1[c][3]),
+          [s0] "+v"(k2[c][0]), [s1] "+v"(k2[c][1]), [s2] "+v"(k2[c][2]), [s3] "+v"(k2[c][3]),
+          [t0] "+v"(t1[c][0]), [t1] "+v"(t1[c][1]), [t2] "+v"(t1[c][2]), [t3] "+v"(t1[c][3]),
+          [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3)
+        : [k0] "v"(__float_as_int(acc[0])), [k1] "v"(__float_as_int(acc[1])), [k2] "v"(__float_as_int(acc[2])),
+          [k3] "v"(__float_as_int(acc[3])), [tv] "v"(t));
+  };
+  for (int t = tb; t < te; ++t) {  // (the top-1 pass's software pipeline)
+    f32x4 acc[kTop1CT];
+#pragma unroll
+    for (int p = 0; p < kTop1CT / 2; ++p) {
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bo[2 * p][s], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bo[2 * p + 1][s], a1, 0, 0, 0);
+      }
+      acc[2 * p] = a0;
+      acc[2 * p + 1] = a1;
+      if (p > 0) {
+        sel(acc[2 * p - 2], 2 * p - 2, t);
+        sel(acc[2 * p - 1], 2 * p - 1, t);
+      }
+    }
+    a[0] = xn[0].x, a[1] = xn[0].y, a[2] = xn[0].z, a[3] = xn[0].w;
+    a[4] = xn[1].x, a[5] = xn[1].y, a[6] = xn[1].z, a[7] = xn[1].w;
+    opload(min(t + 2, te - 1), xn);
+    sel(acc[kTop1CT - 2], kTop1CT - 2, t);
+    sel(acc[kTop1CT - 1], kTop1CT - 1, t);
+  }
+  // E0: the lane minima (over r) of every column, per (wave, lane group)
+#pragma unroll
+  for (int c = 0; c < kTop1CT; ++c)
+    sLm[c * 16 + c16][w * 4 + g] = min(min(k1[c][0], k1[c][1]), min(k1[c][2], k1[c][3]));
+  __syncthreads();
+  {  // E1: T = the 5th smallest of a column's 32 lane minima (4 threads per column, 8 values each)
+    const int col = tid >> 2, qq = tid & 3;
+    int v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = sLm[col][8 * qq + i];
+    // 8-input sorting network (19 compare-exchanges)
+    ce_i(v[0], v[1]); ce_i(v[2], v[3]); ce_i(v[4], v[5]); ce_i(v[6], v[7]);
+    ce_i(v[0], v[2]); ce_i(v[1], v[3]); ce_i(v[4], v[6]); ce_i(v[5], v[7]);
+    ce_i(v[1], v[2]); ce_i(v[5], v[6]); ce_i(v[0], v[4]); ce_i(v[3], v[7]);
+    ce_i(v[1], v[5]); ce_i(v[2], v[6]);
+    ce_i(v[1], v[4]); ce_i(v[3], v[6]);
+    ce_i(v[2], v[4]); ce_i(v[3], v[5]);
+    ce_i(v[3], v[4]);
+#pragma unroll
+    for (int off = 1; off <= 2; off <<= 1) {  // merge with the partner's sorted five: lowest five
+      int o[5];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) o[i] = __shfl_xor(v[i], off);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) v[i] = min(v[i], o[4 - i]);  // a bitonic sequence holding the lowest five
+      // 5-input sorting network (9 compare-exchanges)
+      ce_i(v[0], v[1]); ce_i(v[3], v[4]); ce_i(v[2], v[4]); ce_i(v[2], v[3]); ce_i(v[0], v[3]);
+      ce_i(v[0], v[2]); ce_i(v[1], v[4]); ce_i(v[1], v[3]); ce_i(v[1], v[2]);
+    }
+    if (qq == 0) sT[col] = v[4];
+  }
+  __syncthreads();
+  // E2: the candidate streams of each column (minimum <= T)
+#pragma unroll
+  for (int c = 0; c < kTop1CT; ++c) {
+    const int col = c * 16 + c16;
+    const int T = sT[col];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (k1[c][r] <= T) {
+        const int slot = atomicAdd(&sCnt[col], 1);
+        if (slot < kT5Slots) {
+          const unsigned row = (unsigned)(t1[c][r] * 16 + 4 * g + r);
+          sKey[col][slot] = ((unsigned long long)(unsigned)k1[c][r] << 32) | row;
+          sK2[col][slot] = k2[c][r];
+          sStr[col][slot] = (w << 4) | (g << 2) | r;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // E3: one thread per column
+  unsigned long long best[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) best[q] = ~0ull;
+  bool mine = false;
+  if (tid < NC && j0 + tid < N2) {
+    const int col = tid;
+    const int n = sCnt[col];
+    bool slow = n > kT5Slots;
+    int bsl[5] = {-1, -1, -1, -1, -1};  // candidate slot of each kept entry
+    if (!slow) {
+      for (int i = 0; i < n; ++i) {
+        unsigned long long key = sKey[col][i];
+        const int hi = (int)(key >> 32);
+        if (hi <= kClampBits) slow = true;        // a clamped distance: the slow path orders them
+        if (hi >= 0x7f800000) continue;           // no row (padding)
+        if (!(key < best[4])) continue;
+        int si = i;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+          const bool sw = key < best[q];
+          const unsigned long long tv = sw ? best[q] : key;
+          const int ts = sw ? bsl[q] : si;
+          best[q] = sw ? key : best[q];
+          bsl[q] = sw ? si : bsl[q];
+          key = tv;
+          si = ts;
+        }
+      }
+    }
+    if (!slow) {
+      // kept streams ranked 1..4 whose second value is <= the fifth value: recompute their rows
+      const int S = best[4] == ~0ull ? 0x7f800000 : (int)(best[4] >> 32);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (bsl[q] < 0 || sK2[col][bsl[q]] > S) continue;
+        const int st = sStr[col][bsl[q]];
+        const int sw_ = st >> 4, sg = (st >> 2) & 3, sr = st & 3;
+        const int sqw = rs * kTop1Waves + sw_;
+        const int stb = (int)((int64_t)nt * sqw / Q), ste = (int)((int64_t)nt * (sqw + 1) / Q);
+        const unsigned known = (unsigned)(best[q] & 0xffffffffu);
+        for (int t = stb; t < ste; ++t) {
+          const int i = 4 * sg + sr, row = t * 16 + i;
+          if (row >= N1 || (unsigned)row == known) continue;
+          const float d = t5_exact(Ab, t, i, sB, col);
+          if (__float_as_int(d) <= kClampBits) slow = true;
+          t5_insert(best, ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)row);
+        }
+      }
+    }
+    if (slow) {
+      sSlow[atomicAdd(&sNslow, 1)] = col;
+    } else {
+      mine = true;
+    }
+  }
+  auto emit = [&](int col, const unsigned long long (&bst)[5]) {
+    const int j = j0 + col;
+    if (RS == 1) {
+      const int64_t o = ((int64_t)b * V2max + j) * 5;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const bool none = bst[q] == ~0ull;
+        out_idx[o + q] = none ? -1 : (int64_t)(bst[q] & 0xffffffffu);
+        if (out_dist) out_dist[o + q] = none ? __builtin_huge_valf() : sqrtf(__uint_as_float((unsigned)(bst[q] >> 32)));
+      }
+    } else {
+      const int64_t o = (((int64_t)b * RS + rs) * V2max + j) * 5;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const bool none = bst[q] == ~0ull;
+        part_v[o + q] = none ? __builtin_huge_valf() : __uint_as_float((unsigned)(bst[q] >> 32));
+        part_i[o + q] = none ? 0x7fffffff : (int32_t)(bst[q] & 0xffffffffu);
+      }
+    }
+  };
+  if (mine) emit(tid, best);
+  __syncthreads();
+  // slow path: one wave per column, every row of this row part, clamped distances, lower row first
+  const int nslow = sNslow;
+  const int pt0 = (int)((int64_t)nt * (rs * kTop1Waves) / Q), pt1 = (int)((int64_t)nt * (rs * kTop1Waves + kTop1Waves) / Q);
+  for (int si = w; si < nslow; si += kTop1Waves) {
+    const int col = sSlow[si];
+    unsigned long long bl[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) bl[q] = ~0ull;
+    for (int row = pt0 * 16 + lane; row < min(pt1 * 16, N1); row += 64) {  // rows ascending per lane
+      const float d = t5_exact(Ab, row >> 4, row & 15, sB, col);
+      const unsigned v = __float_as_int(d) <= kClampBits ? (unsigned)kClampBits : __float_as_uint(d);
+      t5_insert(bl, ((unsigned long long)v << 32) | (unsigned)row);
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {  // the wave's lists, merged pairwise (keys are unique)
+      unsigned long long o[5];
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const unsigned lo = __shfl_xor((unsigned)(bl[q] & 0xffffffffu), off);
+        const unsigned hi = __shfl_xor((unsigned)(bl[q] >> 32), off);
+        o[q] = ((unsigned long long)hi << 32) | lo;
+      }
+#pragma unroll
+      for (int q = 0; q < 5; ++q) t5_insert(bl, o[q]);
+    }
+    if (lane == 0) emit(col, bl);
+  }
+}
+
 struct Top1Plan {
   int T1, T2, NCG, RS;
   int64_t a_bytes, b_bytes, part_bytes;
@@ -983,11 +1352,12 @@ extern "C" int64_t pk_feat_dist_work_size(int B, int V1max, int V2max, int topk,
   if (B < 0 || V1max < 0 || V2max < 0 || !(topk == 1 || topk == 5) || mode < 0 || mode > 2) return -1;
   const FdPlan p = fd_plan(B, V1max, V2max, topk, mode);
   const int64_t two_pass = p.a_bytes + p.b_bytes + p.na_bytes + p.nb_bytes + p.pv_bytes + p.pi_bytes;
-  if (mode != 0 || topk != 1) return two_pass;
-  // mode 0 top-1: the one-launch pass's row-part keys, or the two-pass fallback's scratch
-  // (unaligned operand rows); neither keeps anything across calls
+  if (mode != 0) return two_pass;
+  // mode 0: the prep + main pass's operand tiles and row-part keys (top-1) / lists (top-5), or the
+  // two-pass fallback's scratch (unaligned operand rows); none keeps anything across calls
   const Top1Plan tp = top1_plan(B, V1max, V2max);
-  return std::max(two_pass, tp.a_bytes + tp.part_bytes);
+  const int64_t t5parts = tp.RS > 1 ? 2 * al256_((int64_t)B * tp.RS * V2max * 5 * 4) : 0;
+  return std::max(two_pass, tp.a_bytes + (topk == 1 ? tp.part_bytes : t5parts));
 }
 
 extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, const float* evecs_y, int ldy,
@@ -1003,6 +1373,34 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
   hipStream_t s = pk::as_stream(stream);
   const bool aligned = (ldx % 4) == 0 && (ldy % 4) == 0 && (reinterpret_cast<uintptr_t>(evecs_x) & 15) == 0 &&
                        (reinterpret_cast<uintptr_t>(evecs_y) & 15) == 0;
+#ifdef PK_DEVBUILD
+  static const bool old_top5 = [] {  // development knob PK_FD_TOP5_OLD=1: the round-3 two-pass top-5
+    const char* e = std::getenv("PK_FD_TOP5_OLD");
+    return e && std::atoi(e) == 1;
+  }();
+#else
+  constexpr bool old_top5 = false;
+#endif
+  if (mode == 0 && aligned && V1max > 0 && topk == 5 && !old_top5) {  // prep + main (+ merge when RS > 1)
+    const Top1Plan tp = top1_plan(B, V1max, V2max);
+    auto* At = static_cast<f32x4*>(work);
+    float* pv = tp.RS > 1 ? reinterpret_cast<float*>(static_cast<char*>(work) + tp.a_bytes) : nullptr;
+    int32_t* pi = tp.RS > 1 ? reinterpret_cast<int32_t*>(reinterpret_cast<char*>(pv) +
+                                                         al256_((int64_t)B * tp.RS * V2max * 5 * 4))
+                            : nullptr;
+    hipLaunchKernelGGL(fd_top1_prep_kernel, dim3((unsigned)((tp.T1 + 7) / 8), B), dim3(512), 0, s, evecs_x, ldx, C,
+                       n1, V1max, tp.T1, At);
+    PK_CHECK_LAUNCH();
+    hipLaunchKernelGGL((fd_top5_kernel<0>), dim3((unsigned)((int64_t)B * tp.NCG * tp.RS)), dim3(64 * kTop1Waves), 0,
+                       s, At, tp.T1, evecs_y, ldy, n1, n2, V2max, tp.NCG, tp.RS, out_idx, out_dist, pv, pi);
+    PK_CHECK_LAUNCH();
+    if (tp.RS > 1) {
+      hipLaunchKernelGGL(fd_merge_kernel<5>, dim3((V2max + 255) / 256, B), dim3(256), 0, s, pv, pi, n2, V2max, tp.RS,
+                         out_idx, out_dist);
+      PK_CHECK_LAUNCH();
+    }
+    return PK_OK;
+  }
   if (mode == 0 && aligned && V1max > 0 && topk == 1) {  // two launches (+ a merge launch when RS > 1)
     const Top1Plan tp = top1_plan(B, V1max, V2max);
     auto* At = static_cast<f32x4*>(work);

@@ -224,3 +224,69 @@ def train_step_parity(M, op, crops, device, model_seed, step_seed):
     for (name, _), t, a, b, d in zip(truth.named_parameters(), gr64, gr32, grg, mine_g):
         ee = [(a - t).norm().item(), (b - t).norm().item(), (d - t).norm().item()]
         assert ee[2] <= 3 * max(ee[0], ee[1]) + floor, (name, ee, floor, t.norm().item())
+
+
+def fd_emulate(ex, C, ey, n1: int, n2: int):
+    """The fp32 feature-distance pass's distances [n1, n2], emulated on the host: the prep's -2 emb
+    = -2 x C^T and |emb|^2, the columns' [y, 1, |y|^2], and the contraction as ONE fmaf chain over
+    the 32 slots in the MFMA's order (v_mfma_f32_16x16x4f32 accumulates exactly so:
+    tools/mfma_order_probe.py). Slot (s, g) holds feature 16 (s >> 2) + 4 g + (s & 3); slot (6, 3)
+    is |emb|^2 x 1, slot (7, 3) is 1 x |y|^2. fmaf is emulated in float64 (exact product, the sum
+    rounded to f64 and then to f32: a double rounding can differ from fmaf in 1 ulp, rarely)."""
+    ex = np.asarray(ex, np.float32)[:n1, :30]
+    ey = np.asarray(ey, np.float32)[:n2, :30]
+    C = np.asarray(C, np.float32)
+
+    def fma(a, b, c):
+        return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(np.float32)
+
+    order = [(s, g) for s in range(8) for g in range(4)]
+    kid = [16 * (s >> 2) + 4 * g + (s & 3) for s, g in order]
+    m2C = (np.float32(-2.0) * C).astype(np.float32)
+    emb2 = np.zeros((n1, 32), np.float32)  # -2 emb by feature (30, 31: zero)
+    for f in range(30):
+        acc = np.zeros(n1, np.float32)
+        for k in kid:
+            if k < 30:
+                acc = fma(np.full(n1, m2C[f, k], np.float32), ex[:, k], acc)
+        emb2[:, f] = acc
+
+    def norm(v):  # per lane group g: fmaf chain of the squares over s; groups added in order
+        tot = np.zeros(v.shape[0], np.float32)
+        for g in range(4):
+            p = np.zeros(v.shape[0], np.float32)
+            for s in range(8):
+                x = v[:, 16 * (s >> 2) + 4 * g + (s & 3)]
+                p = fma(x, x, p)
+            tot = (tot + p).astype(np.float32)
+        return tot
+
+    nA = (np.float32(0.25) * norm(emb2)).astype(np.float32)
+    yv = np.zeros((n2, 32), np.float32)
+    yv[:, :30] = ey
+    nB = norm(yv)
+    A = np.zeros((n1, 32), np.float32)
+    Bm = np.zeros((n2, 32), np.float32)
+    for idx, (s, g) in enumerate(order):
+        k = kid[idx]
+        A[:, idx] = emb2[:, k] if k < 30 else (nA if k == 30 else 1.0)
+        Bm[:, idx] = yv[:, k] if k < 30 else (1.0 if k == 30 else nB)
+    acc = np.zeros((n1, n2), np.float32)
+    for idx in range(32):
+        acc = fma(A[:, idx, None], Bm[None, :, idx], acc)
+    return acc
+
+
+def fd_expected_topk(d, k):
+    """torch.cdist's clamp_min(1e-30), then the k smallest rows of every column in ascending
+    order, ties to the lower row (the reference's dist.sort order on exact ties: stable), -1 past
+    the rows present. Returns (idx [n2, k] int64, clamped values [n2, k] f32)."""
+    dc = np.maximum(d, np.float32(1e-30))
+    n1, n2 = dc.shape
+    order = np.argsort(dc, axis=0, kind="stable")[:k].T
+    idx = np.full((n2, k), -1, np.int64)
+    val = np.full((n2, k), np.inf, np.float32)
+    m = min(k, n1)
+    idx[:, :m] = order[:, :m]
+    val[:, :m] = np.take_along_axis(dc, order[:, :m].T, axis=0).T
+    return idx, val

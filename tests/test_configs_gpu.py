@@ -458,3 +458,73 @@ def test_feat_dist_bf16_configs4_and_ransac(device, coracle, precision):
     assert res.best_hypothesis == int(st_c[2]) and res.fitness == st_c[0]
     np.testing.assert_allclose(res.transformation, T_c.reshape(4, 4), atol=1e-4)
     assert res.fitness >= 0.5 * agree  # the recovered pose explains the matched points
+
+
+@pytest.mark.parametrize("B,V,ragged", [(4, 1024, False), (32, 256, False), (6, 1024, True)])
+def test_feat_dist_top5_exact_vs_emulated_chain(device, B, V, ragged):
+    """The round-6 top-5 pass (stream minima + candidate lists + exact recomputation) against the
+    host emulation of the same fp32 distances (tests/_util.fd_emulate: the prep's operands and
+    the MFMA's fmaf chain) and their stable order: indices, and distances as the sqrt of the
+    clamped values. Row parts (B = 4: RS = 4 + the merge launch), one part per block (B = 32 x 256),
+    ragged crops with fewer than 5 CAD rows (-1 entries) and empty columns. At most one column per
+    case may differ, by a double rounding of the host's float64 fmaf emulation."""
+    from dpfm_amd import ops
+    from _util import fd_emulate, fd_expected_topk
+    g = torch.Generator().manual_seed(B * 7 + V)
+    ex = torch.stack([_spectral(V, 300 + b) for b in range(B)])
+    ey = torch.stack([_spectral(V, 400 + b) for b in range(B)])
+    C = torch.eye(30)[None] + 0.3 * torch.randn(B, 30, 30, generator=g)
+    if ragged:
+        n1 = [3, 5, 17, 300, 1000, V][:B]
+        n2 = [V, 40, 1, 513, 999, 7][:B]
+    else:
+        n1 = n2 = [V] * B
+    t1 = torch.tensor(n1, dtype=torch.int32, device=device)
+    t2 = torch.tensor(n2, dtype=torch.int32, device=device)
+    idx, dist = ops.feat_dist_topk(ex.to(device), C.to(device), ey.to(device), t1, t2, 5, want_dist=True)
+    i1, d1 = ops.feat_dist_topk(ex.to(device), C.to(device), ey.to(device), t1, t2, 1, want_dist=True)
+    idx, dist, i1, d1 = idx.cpu().numpy(), dist.cpu().numpy(), i1.cpu().numpy(), d1.cpu().numpy()
+    bad = bad1 = 0
+    for b in range(B):
+        d = fd_emulate(ex[b].numpy(), C[b].numpy(), ey[b].numpy(), n1[b], n2[b])
+        ei, ev = fd_expected_topk(d, 5)
+        gi = idx[b, :n2[b]]
+        diff = (gi != ei).any(1)
+        bad += int(diff.sum())
+        ok = ~diff
+        np.testing.assert_array_equal(dist[b, :n2[b]][ok], np.sqrt(ev)[ok])
+        # the top-1 pass on the same operands: the first of the five
+        d1ff = i1[b, :n2[b], 0] != ei[:, 0]
+        bad1 += int(d1ff.sum())
+        np.testing.assert_array_equal(d1[b, :n2[b], 0][~d1ff], np.sqrt(ev[:, 0])[~d1ff])
+    assert bad <= 1 and bad1 <= 1, (bad, bad1)
+
+
+def test_feat_dist_top5_duplicates_and_clamp(device):
+    """Exact ties and torch.cdist's clamp: crop features equal to CAD rows (C = I) give distances at
+    or below 1e-30 (clamped, so tied), and each such CAD row is duplicated at a later row: the five
+    must list the tied rows lowest first, then the rest in order (the slow path of the top-5 pass),
+    with and without row parts."""
+    from dpfm_amd import ops
+    from _util import fd_emulate, fd_expected_topk
+    for B, V in [(2, 1024), (32, 256)]:
+        g = torch.Generator().manual_seed(V)
+        ex = torch.randn(B, V, 32, generator=g)
+        ey = torch.randn(B, V, 32, generator=g)
+        C = torch.eye(30).repeat(B, 1, 1)
+        for b in range(B):
+            src = torch.randperm(V // 2, generator=g)[:20]
+            dup = V // 2 + torch.randperm(V // 2, generator=g)[:20]
+            ex[b, dup] = ex[b, src]
+            ex[b, dup[:10] - 1] = ex[b, src[:10]]  # a third copy for half of them
+            cols = torch.randperm(V, generator=g)[:20]
+            ey[b, cols] = ex[b, src]
+        n = torch.full((B,), V, dtype=torch.int32, device=device)
+        idx, dist = ops.feat_dist_topk(ex.to(device), C.to(device), ey.to(device), n, n, 5, want_dist=True)
+        idx = idx.cpu().numpy()
+        bad = 0
+        for b in range(B):
+            d = fd_emulate(ex[b].numpy(), C[b].numpy(), ey[b].numpy(), V, V)
+            ei, _ = fd_expected_topk(d, 5)
+            bad += int((idx[b] != ei).any(1).sum())
+        assert bad <= 1, (B, V, bad)
