@@ -1191,15 +1191,23 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
     }
     if (!slow) {
       // kept streams ranked 1..4 whose second value is <= the fifth value: recompute their rows
+      // (listed first: the insertions below reorder `best`; the fifth value only falls, so the
+      // list from the first selection covers every stream that can still hold a member)
       const int S = best[4] == ~0ull ? 0x7f800000 : (int)(best[4] >> 32);
+      int todo[4], known_row[4], ntodo = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (bsl[q] < 0 || sK2[col][bsl[q]] > S) continue;
-        const int st = sStr[col][bsl[q]];
+        todo[ntodo] = sStr[col][bsl[q]];
+        known_row[ntodo] = (int)(best[q] & 0xffffffffu);
+        ++ntodo;
+      }
+      for (int q = 0; q < ntodo; ++q) {
+        const int st = todo[q];
         const int sw_ = st >> 4, sg = (st >> 2) & 3, sr = st & 3;
         const int sqw = rs * kTop1Waves + sw_;
         const int stb = (int)((int64_t)nt * sqw / Q), ste = (int)((int64_t)nt * (sqw + 1) / Q);
-        const unsigned known = (unsigned)(best[q] & 0xffffffffu);
+        const unsigned known = (unsigned)known_row[q];
         for (int t = stb; t < ste; ++t) {
           const int i = 4 * sg + sr, row = t * 16 + i;
           if (row >= N1 || (unsigned)row == known) continue;
