@@ -515,8 +515,9 @@ class PipelinedTrainer:
 
     def __init__(self, crop_formation: CropFormation, step: TrainStep, fb: FrameBatch, op: Operators,
                  warmup: int = 3, defer_ir: bool = True, cgt_side: bool = False, side_cus: int = 0,
-                 main_priority: int = 0):
+                 main_priority: int = 0, side_after: bool = False):
         self.step, self.split = step, step.world > 1
+        self.side_after = side_after  # host order per call: the training replay first, then crop formation
         self.main = torch.cuda.current_stream()
         self.side = torch.cuda.Stream()
         self.own_main = False
@@ -630,7 +631,8 @@ class PipelinedTrainer:
         k = self.i & 1
         if self.own_main:  # the step after the caller's queued work (its reads of earlier logs / params)
             self.main.wait_stream(torch.cuda.current_stream())
-        self._form(k ^ 1)                      # next batch's crops, concurrently
+        if not self.side_after:
+            self._form(k ^ 1)                  # next batch's crops, concurrently
         with torch.cuda.stream(self.main):
             self.main.wait_event(self.formed[k])
             self.train_a[k].replay()
@@ -638,6 +640,8 @@ class PipelinedTrainer:
                 self.step.allreduce_grads(self.grads[k])
                 self.train_b[k].replay()
             self.consumed[k].record(self.main)
+        if self.side_after:
+            self._form(k ^ 1)
         if self.own_main:  # the caller's stream reads the step's outputs after it
             torch.cuda.current_stream().wait_stream(self.main)
         self._trained[k] = True

@@ -58,6 +58,8 @@ def parse():
                     help="train: crops of the post-timing pose-vs-reference check (0: skip)")
     ap.add_argument("--no-roofline-probe", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP graph: launch every kernel from Python")
+    ap.add_argument("--side-after", action="store_true",
+                    help="train overlapped: enqueue each training replay before the next crop formation")
     ap.add_argument("--side-cus", type=int, default=0,
                     help="train/infer overlapped: crop formation on this many CUs, the step on the rest (0: shared)")
     ap.add_argument("--main-priority", type=int, default=0,
@@ -570,7 +572,7 @@ def build_train(args, dev, rank, world):
         one_step = GraphedTrainStep(crops_of, step, fb, op, warmup=3)
     else:  # same, with crop formation of the next batch on a second stream
         one_step = PipelinedTrainer(crops_of, step, fb, op, warmup=3, main_priority=args.main_priority,
-                                        side_cus=args.side_cus,
+                                        side_cus=args.side_cus, side_after=args.side_after,
                                         cgt_side=bool(args.ragged) if args.cgt_side is None else bool(args.cgt_side),
                                         defer_ir=not args.ir_main)
     config = {"workload": train_workload(B, N, world),
