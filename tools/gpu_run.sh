@@ -37,6 +37,10 @@ for step in "$@"; do
                grep "^{\"metric\"" "$out/steptrace_bench.log" | tail -1 > "$out/steptrace.json"
                python tools/step_window_summary.py $(find "$out/steptrace" -name "*kernel_trace.csv" | head -1) "$out/steptrace.json" > "$out/step_window_summary.txt" 2>&1
                find "$out/steptrace" -type f -delete ;;
+    steptrace_pc1) DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 run steptrace_pc1_bench 400 rocprofv3 --kernel-trace --output-format csv -d "$out/steptrace_pc1" -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roofline-probe --probe-steps 0
+               grep "^{\"metric\"" "$out/steptrace_pc1_bench.log" | tail -1 > "$out/steptrace_pc1.json"
+               python tools/step_window_summary.py $(find "$out/steptrace_pc1" -name "*kernel_trace.csv" | head -1) "$out/steptrace_pc1.json" > "$out/step_window_summary_pc1.txt" 2>&1
+               find "$out/steptrace_pc1" -type f -delete ;;
     steptrace_to) run steptrace_to_bench 400 rocprofv3 --kernel-trace --output-format csv -d "$out/steptrace_to" -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roofline-probe --probe-steps 0 --train-only
                grep "^{\"metric\"" "$out/steptrace_to_bench.log" | tail -1 > "$out/steptrace_to.json"
                python tools/step_window_summary.py $(find "$out/steptrace_to" -name "*kernel_trace.csv" | head -1) "$out/steptrace_to.json" > "$out/step_window_summary_train_only.txt" 2>&1
