@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <cstdlib>
+#include <cstring>
 
 #define PK_OK 0
 #define PK_ERR_ARG 1000      // invalid argument (shape / size / null pointer)
@@ -33,6 +34,21 @@ namespace pk {
 #ifndef PK_SIDE_PRIO_DEFAULT
 #define PK_SIDE_PRIO_DEFAULT 0
 #endif
+// development diagnostics (libposekern_dev.so only): PK_DIAG_SKIP=<name>[,<name>] skips the named
+// crop-formation launches (fps, sorknn, bpwrite, bqmask) so a bench run measures how much each one's
+// occupancy costs the overlapped step; the product library never skips anything
+inline bool diag_skip(const char* name) {
+#ifdef PK_DEVBUILD
+  static const char* e = std::getenv("PK_DIAG_SKIP");
+  if (e == nullptr) return false;
+  const char* p = std::strstr(e, name);
+  return p != nullptr;
+#else
+  (void)name;
+  return false;
+#endif
+}
+
 inline int side_prio() {
 #ifdef PK_DEVBUILD
   static const int v = [] {

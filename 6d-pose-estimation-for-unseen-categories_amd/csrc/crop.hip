@@ -935,7 +935,7 @@ extern "C" int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, in
   PK_REQUIRE((pix == nullptr) == (idxmap == nullptr) && (pix == nullptr || (H > 0 && W > 0)));
   hipStream_t s = pk::as_stream(stream);
   const int nchunk = (nmax + 1023) / 1024;
-  if (nmax > 0) {
+  if (nmax > 0 && !pk::diag_skip("sorknn")) {
     const int tiles = (nmax + kSorThreads - 1) / kSorThreads;
     hipLaunchKernelGGL(sor_knn_kernel, dim3((unsigned)((int64_t)tiles * B)),
                        dim3(kSorThreads), 0, s, xyz, off, knn, pix, idxmap, H, W,

@@ -979,6 +979,9 @@ def main():
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         sys.exit(subprocess.call(cmd, env=env))
     args = parse()
+    if os.environ.get("PK_DEV") == "1":  # development runs only: libposekern_dev.so and its PK_* knobs
+        from dpfm_amd import _lib as _devl
+        _devl.use_dev_lib()
     world, rank, dev = setup_dist(args.gpus)
     apply_global_batch(args, world)
     from dpfm_amd import _lib
