@@ -315,20 +315,18 @@ constexpr int kSorMaxBox = 1024;
 // grid (tiles x B): workgroup = (crop, 256-query tile), crops interleaved; a persistent grid
 // (fewer workgroups looping over the items) measured slower with no gain in overlap.
 //
-// Round 6: the pixel-window and box passes read LDS, not global memory. The block's 256 queries
-// are consecutive points, i.e. a few consecutive image rows of the crop (points are in row-major
-// pixel order); the block first stages the index map of their pixel bounding box widened by
-// kSorMargin (the largest window, 17 x 17; the typical box), and the fp64 coordinates of the
-// points those pixels hold (a contiguous index range: the rows are consecutive), so every
-// window / box lookup inside that region is two LDS reads instead of two dependent global
-// gathers. Pixels outside it (a wide box) and blocks whose region exceeds the LDS budget read
-// global memory as before. Same candidates, same fp64 distances, same insertions: avg is
-// bit-identical. Measured reason (tools/diag_skip_ab.sh): the latency-bound gather version held
-// the whole chip for ~265 us per step, and the overlapped training step ran 1.80 ms with it
-// against 1.46 ms without it.
+// Round 6: the block's 256 queries are consecutive points, i.e. a few consecutive image rows of
+// the crop (points are in row-major pixel order); the block stages the index map of their pixel
+// bounding box widened by kSorMargin (the largest window, 17 x 17; the typical box) in LDS, so a
+// window / box pixel inside that region costs one global round trip (its point's coordinates)
+// instead of two dependent ones, 4 pixels' loads in flight together. Pixels outside it (a wide
+// box) and blocks whose region exceeds the budget read the global index map. Same candidates,
+// same fp64 distances, same insertions: avg is bit-identical. Why it matters
+// (tools/diag_skip_ab.sh): this latency-bound kernel holds the whole chip for ~265 us per step,
+// and the overlapped training step ran 1.80 ms with it against 1.46 ms without it.
 constexpr int kSorMargin = 8;
 constexpr int kSorStageIdx = 4096;  // staged index-map pixels
-constexpr int kSorStagePts = 2048;  // staged points (fp64 coordinates)
+constexpr int kSorBatch = 4;        // pixels of a window / box row whose coordinate loads are in flight together
 
 __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const double* __restrict__ xyz,
                                                                  const int64_t* __restrict__ off, int knn,
@@ -338,10 +336,8 @@ __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const
                                                                  double* __restrict__ avg, int prio) {
   pk::set_wave_prio(prio);
   __shared__ int sIdx[kSorStageIdx];
-  __shared__ double sP[3][kSorStagePts];  // (also the brute-force pass's float4 tile, after the staged passes)
-  __shared__ int sRed[6];                 // vmin, vmax, umin, umax, pmin, pmax
-  float4* tile = reinterpret_cast<float4*>(&sP[0][0]);
-  static_assert(sizeof(sP) >= kSorTile * sizeof(float4), "the brute-force tile fits in the staging buffer");
+  __shared__ float4 tile[kSorTile];
+  __shared__ int sRed[4];  // vmin, vmax, umin, umax
   {
   const int item = blockIdx.x;
   const int b = item % B, bx = item / B;
@@ -366,8 +362,8 @@ __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const
   bool done = false;
   const bool pixel_path = pix != nullptr && idxmap != nullptr;
   // ---- staging (block-uniform branches)
-  int rv0 = 0, rv1 = -1, ru0 = 0, ru1 = -1, RW = 1, plo = 0, phi = 0;
-  bool st_idx = false, st_pts = false;
+  int rv0 = 0, rv1 = -1, ru0 = 0, ru1 = -1, RW = 1;
+  bool st_idx = false;
   int v = 0, u = 0;
   const int32_t* im = pixel_path ? idxmap + (int64_t)b * H * W : nullptr;
   if (pixel_path) {
@@ -378,7 +374,6 @@ __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const
     }
     if (threadIdx.x == 0) {
       sRed[0] = 0x7fffffff; sRed[1] = -1; sRed[2] = 0x7fffffff; sRed[3] = -1;
-      sRed[4] = 0x7fffffff; sRed[5] = -1;
     }
     __syncthreads();
     if (act) {
@@ -394,54 +389,40 @@ __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const
     const int npx = (rv1 - rv0 + 1) * RW;
     st_idx = npx <= kSorStageIdx;
     if (st_idx) {
-      int lo = 0x7fffffff, hi = -1;
       for (int e = threadIdx.x; e < npx; e += kSorThreads) {
         const int vv = rv0 + e / RW, uu = ru0 + e - (e / RW) * RW;
-        const int j = im[vv * W + uu];
-        sIdx[e] = j;
-        if (j >= 0) {
-          lo = min(lo, j);
-          hi = max(hi, j);
-        }
-      }
-      if (hi >= 0) {
-        atomicMin(&sRed[4], lo);
-        atomicMax(&sRed[5], hi);
-      }
-      __syncthreads();
-      plo = sRed[4];
-      phi = sRed[5] + 1;
-      st_pts = phi > plo && phi - plo <= kSorStagePts;
-      if (st_pts) {
-        for (int e = threadIdx.x; e < phi - plo; e += kSorThreads) {
-          const double* c = p + 3 * (int64_t)(plo + e);
-          sP[0][e] = c[0];
-          sP[1][e] = c[1];
-          sP[2][e] = c[2];
-        }
+        sIdx[e] = im[vv * W + uu];
       }
       __syncthreads();
     }
   }
-  // pixel (vv, uu) -> point index (-1: none); point j -> coordinates
-  auto lookup = [&](int vv, int uu) -> int {
-    if (st_idx && vv >= rv0 && vv <= rv1 && uu >= ru0 && uu <= ru1) return sIdx[(vv - rv0) * RW + (uu - ru0)];
-    return im[vv * W + uu];
-  };
-  auto sdist = [&](int j) -> double {
-    double cx, cy, cz;
-    if (st_pts && j >= plo && j < phi) {
-      cx = sP[0][j - plo];
-      cy = sP[1][j - plo];
-      cz = sP[2][j - plo];
-    } else {
-      const double* c = p + 3 * (int64_t)j;
-      cx = c[0];
-      cy = c[1];
-      cz = c[2];
+  // pixels uu .. min(uu + kSorBatch - 1, uhi) of row vv: every index read (LDS inside the staged
+  // region, else global), then every coordinate load, issued before the first use; bit t of the
+  // result: pixel uu + t holds a point (s[t] its exact squared distance)
+  auto gather = [&](int vv, int uu, int uhi, double (&s)[kSorBatch]) -> int {
+    int j[kSorBatch];
+    const bool inreg = st_idx && vv >= rv0 && vv <= rv1 && uu >= ru0 && min(uu + kSorBatch - 1, uhi) <= ru1;
+#pragma unroll
+    for (int t = 0; t < kSorBatch; ++t) {
+      const int ut = uu + t <= uhi ? uu + t : uu;
+      const int jv = inreg ? sIdx[(vv - rv0) * RW + (ut - ru0)] : im[vv * W + ut];
+      j[t] = uu + t <= uhi ? jv : -1;
     }
-    const double dx = q0 - cx, dy = q1 - cy, dz = q2 - cz;
-    return (dx * dx + dy * dy) + dz * dz;  // nanoflann L2: ((dx²+dy²)+dz²), as sqdist
+    double c[kSorBatch][3];
+#pragma unroll
+    for (int t = 0; t < kSorBatch; ++t) {
+      const double* pj = p + 3 * (int64_t)(j[t] >= 0 ? j[t] : 0);
+      c[t][0] = pj[0];
+      c[t][1] = pj[1];
+      c[t][2] = pj[2];
+    }
+    int m = 0;
+#pragma unroll
+    for (int t = 0; t < kSorBatch; ++t) {
+      s[t] = sqdist(q0, q1, q2, c[t]);
+      m |= (j[t] >= 0 ? 1 : 0) << t;
+    }
+    return m;
   };
   if (act && pixel_path) {
     int found = 0, Rw = -1;
@@ -451,12 +432,13 @@ __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const
       for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
       for (int vv = max(v - R, 0); vv <= min(v + R, H - 1); ++vv) {
         const int uhi = min(u + R, W - 1);
-        for (int uu = max(u - R, 0); uu <= uhi; ++uu) {
-          const int j = lookup(vv, uu);
-          if (j >= 0) {
-            topk_insert(best, sdist(j));
-            ++found;
-          }
+        for (int uu = max(u - R, 0); uu <= uhi; uu += kSorBatch) {
+          double sd[kSorBatch];
+          const int m = gather(vv, uu, uhi, sd);
+#pragma unroll
+          for (int t = 0; t < kSorBatch; ++t)
+            if ((m >> t) & 1) topk_insert(best, sd[t]);
+          found += __builtin_popcount(m);
         }
       }
       if (found >= kk) {
@@ -503,12 +485,12 @@ __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const
         for (int seg = 0; seg < 2; ++seg) {
           const int a = in_w ? (seg == 0 ? u0 : max(u0, u + Rw + 1)) : (seg == 0 ? u0 : 1);
           const int c = in_w ? (seg == 0 ? min(u1, u - Rw - 1) : u1) : (seg == 0 ? u1 : 0);
-          for (int uu = a; uu <= c; ++uu) {
-            const int j = lookup(vv, uu);
-            if (j >= 0) {
-              const double sv = sdist(j);
-              if (sv <= T && sv < best[kKnn - 1]) topk_insert(best, sv);
-            }
+          for (int uu = a; uu <= c; uu += kSorBatch) {
+            double sd[kSorBatch];
+            const int m = gather(vv, uu, c, sd);
+#pragma unroll
+            for (int t = 0; t < kSorBatch; ++t)
+              if (((m >> t) & 1) && sd[t] <= T && sd[t] < best[kKnn - 1]) topk_insert(best, sd[t]);
           }
         }
       }
@@ -518,7 +500,7 @@ __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const
       for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
     }
   }
-  if (__syncthreads_or(act && !done)) {  // (the staged data is dead from here: the tile reuses it)
+  if (__syncthreads_or(act && !done)) {
     const float qx = (float)(q0 - ox), qy = (float)(q1 - oy), qz = (float)(q2 - oz);
     const float qa = fmaxf(fabsf(qx), fmaxf(fabsf(qy), fabsf(qz)));
     const float Tf = T == __builtin_huge_val() ? __builtin_huge_valf() : (float)T;
