@@ -308,25 +308,46 @@ __device__ __forceinline__ double sqdist(double ax, double ay, double az, const 
 // The kept set is a superset of the true knn nearest (ties included), so the sorted
 // top-knn values are exactly those of a full brute-force search.
 constexpr int kSorMaxBox = 1024;
+#ifndef PK_SOR_BATCH
+#define PK_SOR_BATCH 4
+#endif
 #ifndef PK_SOR_MINW
 #define PK_SOR_MINW 4
 #endif
+constexpr int kSorBatch = PK_SOR_BATCH;  // pixels of a window row gathered together (loads in flight at once)
+
+// distances from the query to the points of pixels uu .. min(uu + 7, u1) of an index-map row;
+// bit t of the result: pixel uu + t holds a point (s[t] valid). All index loads, then all
+// coordinate loads, are issued before the first use (memory-level parallelism).
+__device__ __forceinline__ int sor_gather(const int32_t* __restrict__ row, int uu, int u1,
+                                          const double* __restrict__ p, double q0, double q1, double q2,
+                                          double (&s)[kSorBatch]) {
+  int j[kSorBatch];
+#pragma unroll
+  for (int t = 0; t < kSorBatch; ++t) {  // unconditional at a clamped pixel (no branch + wait per load)
+    const int32_t v = row[uu + t <= u1 ? uu + t : uu];
+    j[t] = uu + t <= u1 ? v : -1;
+  }
+  double c[kSorBatch][3];
+#pragma unroll
+  for (int t = 0; t < kSorBatch; ++t) {
+    const double* pj = p + 3 * (j[t] >= 0 ? j[t] : 0);
+    c[t][0] = pj[0];
+    c[t][1] = pj[1];
+    c[t][2] = pj[2];
+  }
+  int m = 0;
+#pragma unroll
+  for (int t = 0; t < kSorBatch; ++t) {
+    s[t] = sqdist(q0, q1, q2, c[t]);
+    m |= (j[t] >= 0 ? 1 : 0) << t;
+  }
+  return m;
+}
+
 
 // grid (tiles x B): workgroup = (crop, 256-query tile), crops interleaved; a persistent grid
 // (fewer workgroups looping over the items) measured slower with no gain in overlap.
-//
-// Round 6: the block's 256 queries are consecutive points, i.e. a few consecutive image rows of
-// the crop (points are in row-major pixel order); the block stages the index map of their pixel
-// bounding box widened by kSorMargin (the largest window, 17 x 17; the typical box) in LDS, so a
-// window / box pixel inside that region costs one global round trip (its point's coordinates)
-// instead of two dependent ones, 4 pixels' loads in flight together. Pixels outside it (a wide
-// box) and blocks whose region exceeds the budget read the global index map. Same candidates,
-// same fp64 distances, same insertions: avg is bit-identical. Why it matters
-// (tools/diag_skip_ab.sh): this latency-bound kernel holds the whole chip for ~265 us per step,
-// and the overlapped training step ran 1.80 ms with it against 1.46 ms without it.
-constexpr int kSorMargin = 8;
-constexpr int kSorStageIdx = 4096;  // staged index-map pixels
-constexpr int kSorBatch = 4;        // pixels of a window / box row whose coordinate loads are in flight together
 
 __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const double* __restrict__ xyz,
                                                                  const int64_t* __restrict__ off, int knn,
@@ -335,9 +356,7 @@ __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const
                                                                  const double* __restrict__ Kmat, int tiles, int B,
                                                                  double* __restrict__ avg, int prio) {
   pk::set_wave_prio(prio);
-  __shared__ int sIdx[kSorStageIdx];
   __shared__ float4 tile[kSorTile];
-  __shared__ int sRed[4];  // vmin, vmax, umin, umax
   {
   const int item = blockIdx.x;
   const int b = item % B, bx = item / B;
@@ -360,84 +379,24 @@ __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const
   for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
   double T = __builtin_huge_val();
   bool done = false;
-  const bool pixel_path = pix != nullptr && idxmap != nullptr;
-  // ---- staging (block-uniform branches)
-  int rv0 = 0, rv1 = -1, ru0 = 0, ru1 = -1, RW = 1;
-  bool st_idx = false;
-  int v = 0, u = 0;
-  const int32_t* im = pixel_path ? idxmap + (int64_t)b * H * W : nullptr;
-  if (pixel_path) {
-    if (act) {
-      const int pp = pix[base + i];
-      v = pp / W;
-      u = pp % W;
-    }
-    if (threadIdx.x == 0) {
-      sRed[0] = 0x7fffffff; sRed[1] = -1; sRed[2] = 0x7fffffff; sRed[3] = -1;
-    }
-    __syncthreads();
-    if (act) {
-      atomicMin(&sRed[0], v); atomicMax(&sRed[1], v);
-      atomicMin(&sRed[2], u); atomicMax(&sRed[3], u);
-    }
-    __syncthreads();
-    rv0 = max(sRed[0] - kSorMargin, 0);
-    rv1 = min(sRed[1] + kSorMargin, H - 1);
-    ru0 = max(sRed[2] - kSorMargin, 0);
-    ru1 = min(sRed[3] + kSorMargin, W - 1);
-    RW = ru1 - ru0 + 1;
-    const int npx = (rv1 - rv0 + 1) * RW;
-    st_idx = npx <= kSorStageIdx;
-    if (st_idx) {
-      for (int e = threadIdx.x; e < npx; e += kSorThreads) {
-        const int vv = rv0 + e / RW, uu = ru0 + e - (e / RW) * RW;
-        sIdx[e] = im[vv * W + uu];
-      }
-      __syncthreads();
-    }
-  }
-  // pixels uu .. min(uu + kSorBatch - 1, uhi) of row vv: every index read (LDS inside the staged
-  // region, else global), then every coordinate load, issued before the first use; bit t of the
-  // result: pixel uu + t holds a point (s[t] its exact squared distance)
-  auto gather = [&](int vv, int uu, int uhi, double (&s)[kSorBatch]) -> int {
-    int j[kSorBatch];
-    const bool inreg = st_idx && vv >= rv0 && vv <= rv1 && uu >= ru0 && min(uu + kSorBatch - 1, uhi) <= ru1;
-#pragma unroll
-    for (int t = 0; t < kSorBatch; ++t) {
-      const int ut = uu + t <= uhi ? uu + t : uu;
-      const int jv = inreg ? sIdx[(vv - rv0) * RW + (ut - ru0)] : im[vv * W + ut];
-      j[t] = uu + t <= uhi ? jv : -1;
-    }
-    double c[kSorBatch][3];
-#pragma unroll
-    for (int t = 0; t < kSorBatch; ++t) {
-      const double* pj = p + 3 * (int64_t)(j[t] >= 0 ? j[t] : 0);
-      c[t][0] = pj[0];
-      c[t][1] = pj[1];
-      c[t][2] = pj[2];
-    }
-    int m = 0;
-#pragma unroll
-    for (int t = 0; t < kSorBatch; ++t) {
-      s[t] = sqdist(q0, q1, q2, c[t]);
-      m |= (j[t] >= 0 ? 1 : 0) << t;
-    }
-    return m;
-  };
-  if (act && pixel_path) {
+  if (act && pix != nullptr && idxmap != nullptr) {
+    const int pp = pix[base + i];
+    const int v = pp / W, u = pp % W;
+    const int32_t* im = idxmap + (int64_t)b * H * W;
     int found = 0, Rw = -1;
     for (int R = 2; R <= 8; R *= 2) {  // 5x5, then 9x9, 17x17 near the mask border
       found = 0;
 #pragma unroll
       for (int k = 0; k < kKnn; ++k) best[k] = __builtin_huge_val();
       for (int vv = max(v - R, 0); vv <= min(v + R, H - 1); ++vv) {
-        const int uhi = min(u + R, W - 1);
-        for (int uu = max(u - R, 0); uu <= uhi; uu += kSorBatch) {
-          double sd[kSorBatch];
-          const int m = gather(vv, uu, uhi, sd);
+        const int32_t* row = im + vv * W;
+        const int u1 = min(u + R, W - 1);
+        for (int uu = max(u - R, 0); uu <= u1; uu += kSorBatch) {
+          double s[kSorBatch];
+          const int m = sor_gather(row, uu, u1, p, q0, q1, q2, s);
 #pragma unroll
           for (int t = 0; t < kSorBatch; ++t)
-            if ((m >> t) & 1) topk_insert(best, sd[t]);
+            if ((m >> t) & 1) topk_insert(best, s[t]);
           found += __builtin_popcount(m);
         }
       }
@@ -481,16 +440,17 @@ __global__ __launch_bounds__(kSorThreads, PK_SOR_MINW) void sor_knn_kernel(const
     }
     if (box) {
       for (int vv = v0; vv <= v1; ++vv) {
+        const int32_t* row = im + vv * W;
         const bool in_w = vv >= v - Rw && vv <= v + Rw;  // this row's window pixels are in best
         for (int seg = 0; seg < 2; ++seg) {
           const int a = in_w ? (seg == 0 ? u0 : max(u0, u + Rw + 1)) : (seg == 0 ? u0 : 1);
           const int c = in_w ? (seg == 0 ? min(u1, u - Rw - 1) : u1) : (seg == 0 ? u1 : 0);
           for (int uu = a; uu <= c; uu += kSorBatch) {
-            double sd[kSorBatch];
-            const int m = gather(vv, uu, c, sd);
+            double s[kSorBatch];
+            const int m = sor_gather(row, uu, c, p, q0, q1, q2, s);
 #pragma unroll
             for (int t = 0; t < kSorBatch; ++t)
-              if (((m >> t) & 1) && sd[t] <= T && sd[t] < best[kKnn - 1]) topk_insert(best, sd[t]);
+              if (((m >> t) & 1) && s[t] <= T && s[t] < best[kKnn - 1]) topk_insert(best, s[t]);
           }
         }
       }
