@@ -915,11 +915,13 @@ __global__ __launch_bounds__(256) void fd_top1_merge_kernel(const unsigned long 
 //   E3     one thread per column sorts the candidates by (value, row) and keeps five. A kept stream
 //          other than the fifth whose second value is <= the fifth value may hold more members:
 //          its rows are recomputed exactly (the f32 MFMA accumulates as one fmaf chain over the
-//          contraction slots in order, bit for bit: tools/mfma_order_probe.py) and merged;
+//          contraction slots in order, bit for bit: tools/mfma_order_probe.py), one row per
+//          thread of the block (a task list in LDS), and merged;
 //   slow   a column with more than 16 candidates, or a distance at or below torch.cdist's
 //          clamp_min(1e-30), is recomputed whole by one wave (clamped; ties to the lower row).
 // RS > 1: each row part writes its five to part_v / part_i and fd_merge_kernel<5> merges them.
 constexpr int kT5Slots = 16;
+constexpr int kT5Tasks = 1536;  // rows recomputed per block (E3b)
 
 // the exact distance of row `row` (tile t, in-tile i) and block column jj, as the MFMA chain forms it
 __device__ __forceinline__ float t5_exact(const f32x4* __restrict__ Ab, int t, int i, const f32x4 (*sB)[2][64],
@@ -970,7 +972,9 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
   __shared__ int sK2[NC][kT5Slots];
   __shared__ int sStr[NC][kT5Slots];
   __shared__ int sSlow[NC];
-  __shared__ int sNslow;
+  __shared__ int sNslow, sNtask;
+  __shared__ int sTask[kT5Tasks];
+  __shared__ unsigned long long sTaskKey[kT5Tasks];
   const int per = NCG * RS;
   const int B = (int)(gridDim.x / per);
   int b, k;
@@ -1028,7 +1032,10 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
       a[4] = xc[1].x, a[5] = xc[1].y, a[6] = xc[1].z, a[7] = xc[1].w;
     }
     if (tid < NC) sCnt[tid] = 0;
-    if (tid == 0) sNslow = 0;
+    if (tid == 0) {
+      sNslow = 0;
+      sNtask = 0;
+    }
     __syncthreads();
     if (gy == 3) {
       float nrm = 0.f;
@@ -1159,15 +1166,17 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
     }
   }
   __syncthreads();
-  // E3: one thread per column
+  // E3: one thread per column selects five among its candidates and lists the rows to recompute
+  // (E3b computes them with every thread of the block, one row each, E3c merges)
   unsigned long long best[5];
 #pragma unroll
   for (int q = 0; q < 5; ++q) best[q] = ~0ull;
-  bool mine = false;
+  bool mine = false, slow = false;
+  int tbase = 0, tcnt = 0;
   if (tid < NC && j0 + tid < N2) {
     const int col = tid;
     const int n = sCnt[col];
-    bool slow = n > kT5Slots;
+    slow = n > kT5Slots;
     int bsl[5] = {-1, -1, -1, -1, -1};  // candidate slot of each kept entry
     if (!slow) {
       for (int i = 0; i < n; ++i) {
@@ -1190,31 +1199,61 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
       }
     }
     if (!slow) {
-      // kept streams ranked 1..4 whose second value is <= the fifth value: recompute their rows
-      // (listed first: the insertions below reorder `best`; the fifth value only falls, so the
-      // list from the first selection covers every stream that can still hold a member)
+      // kept streams ranked 1..4 whose second value is <= the fifth value may hold more members:
+      // their rows (but the kept one) become recompute tasks. (The fifth value only falls as
+      // rows are merged, so the streams listed against the first selection cover every stream
+      // that can still hold a member.)
       const int S = best[4] == ~0ull ? 0x7f800000 : (int)(best[4] >> 32);
-      int todo[4], known_row[4], ntodo = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (bsl[q] < 0 || sK2[col][bsl[q]] > S) continue;
-        todo[ntodo] = sStr[col][bsl[q]];
-        known_row[ntodo] = (int)(best[q] & 0xffffffffu);
-        ++ntodo;
-      }
-      for (int q = 0; q < ntodo; ++q) {
-        const int st = todo[q];
-        const int sw_ = st >> 4, sg = (st >> 2) & 3, sr = st & 3;
-        const int sqw = rs * kTop1Waves + sw_;
+        const int st = sStr[col][bsl[q]];
+        const int sqw = rs * kTop1Waves + (st >> 4);
         const int stb = (int)((int64_t)nt * sqw / Q), ste = (int)((int64_t)nt * (sqw + 1) / Q);
-        const unsigned known = (unsigned)known_row[q];
-        for (int t = stb; t < ste; ++t) {
-          const int i = 4 * sg + sr, row = t * 16 + i;
-          if (row >= N1 || (unsigned)row == known) continue;
-          const float d = t5_exact(Ab, t, i, sB, col);
-          if (__float_as_int(d) <= kClampBits) slow = true;
-          t5_insert(best, ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)row);
+        const int i = ((st >> 2) & 3) * 4 + (st & 3);
+        const int known = (int)(best[q] & 0xffffffffu);
+        for (int t = stb; t < ste; ++t)
+          if (t * 16 + i < N1 && t * 16 + i != known) ++tcnt;
+      }
+      if (tcnt > 0) {
+        tbase = atomicAdd(&sNtask, tcnt);
+        if (tbase + tcnt > kT5Tasks) {
+          slow = true;  // (task list full: the slow path takes the column)
+        } else {
+          int k = tbase;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (bsl[q] < 0 || sK2[col][bsl[q]] > S) continue;
+            const int st = sStr[col][bsl[q]];
+            const int sqw = rs * kTop1Waves + (st >> 4);
+            const int stb = (int)((int64_t)nt * sqw / Q), ste = (int)((int64_t)nt * (sqw + 1) / Q);
+            const int i = ((st >> 2) & 3) * 4 + (st & 3);
+            const int known = (int)(best[q] & 0xffffffffu);
+            for (int t = stb; t < ste; ++t)
+              if (t * 16 + i < N1 && t * 16 + i != known) sTask[k++] = (t << 11) | (col << 4) | i;
+          }
         }
+      }
+    }
+  }
+  __syncthreads();
+  {  // E3b: every listed row's exact distance, one per thread
+    const int ntask = min(sNtask, kT5Tasks);
+    for (int k = tid; k < ntask; k += 64 * kTop1Waves) {
+      const int d = sTask[k], t = d >> 11, col = (d >> 4) & (NC - 1), i = d & 15;
+      const float v = t5_exact(Ab, t, i, sB, col);
+      sTaskKey[k] = ((unsigned long long)__float_as_uint(v) << 32) | (unsigned)(t * 16 + i);
+      if (__float_as_int(v) <= kClampBits) sTaskKey[k] = 0ull;  // a clamped distance: the slow path
+    }
+  }
+  __syncthreads();
+  if (tid < NC && j0 + tid < N2) {  // E3c: merge the recomputed rows
+    const int col = tid;
+    if (!slow) {
+      for (int k = tbase; k < tbase + tcnt; ++k) {
+        const unsigned long long key = sTaskKey[k];
+        if (key == 0ull) slow = true;
+        t5_insert(best, key);
       }
     }
     if (slow) {
