@@ -213,8 +213,11 @@ __global__ __launch_bounds__(kBqThreads) void bq_mask_f32_kernel(
 //   * ambiguity: a lane tracks min_u32(bits(d)); non-negative floats order as their
 //     bits and negative ones sort above them, so one unsigned compare against
 //     bits(W), W = fl(hi'' - lo''), flags any pair in (lo, hi] (rare -> fp64 recheck);
-//   * row counts accumulate two rows per register (16-bit fields) and are reduced
-//     across the wave once per 16 rows;
+//   * the q / d arithmetic runs on packed f32 pairs (v_pk_fma_f32, v_pk_add_f32: two
+//     columns per instruction at the scalar issue rate, each half rounded as the
+//     scalar op) -- the kernel is VALU-issue bound, not store bound, without them;
+//   * a lane keeps one running in-count per row (v_sad_u8 over the byte-summed mask
+//     words, no popcounts); the wave reduces them once, at the end;
 //   * blocks are renumbered so that a crop's row blocks land on one XCD (shared L2
 //     for its column data).
 // The classification is the one bq_mask_f32_kernel proves exact: the
@@ -222,6 +225,7 @@ __global__ __launch_bounds__(kBqThreads) void bq_mask_f32_kernel(
 // of (|a|^2 + |b|^2) by one rounding of (lo - |a|^2), covered by the 2u*thr2 term.
 constexpr int kStageCols = 2048;  // columns converted into LDS per stage (32 KiB)
 using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
 
 __device__ __forceinline__ float next_up(float x) {  // nextafter(x, +inf) for finite x
   const uint32_t b = __float_as_uint(x);
@@ -229,6 +233,7 @@ __device__ __forceinline__ float next_up(float x) {  // nextafter(x, +inf) for f
   return __uint_as_float(x > 0.f ? b + 1u : b - 1u);
 }
 
+template <bool NT>  // NT: nontemporal mask stores (the product choice)
 __global__ __launch_bounds__(kBqThreads) void bq_mask_stream_kernel(
     const double* __restrict__ cad, const int64_t* __restrict__ cad_off,
     const double* __restrict__ pc, const int64_t* __restrict__ pc_off,
@@ -262,7 +267,7 @@ __global__ __launch_bounds__(kBqThreads) void bq_mask_stream_kernel(
   const float R = sqrtf(thr2f) * 1.001f;
   const int ncols = mask != nullptr ? ld : n2;
 
-  uint32_t mine = 0;  // lane r < 16: in-pairs of row row0 + r
+  uint32_t cnt[kRowsPerWave] = {};  // this lane's in-pairs of row row0 + r (<= 16 per chunk)
 
   for (int s0 = 0; s0 < ncols; s0 += kStageCols) {
     const int scols = min(kStageCols, ncols - s0);
@@ -317,33 +322,36 @@ __global__ __launch_bounds__(kBqThreads) void bq_mask_stream_kernel(
 
     for (int ch = 0; ch < scols; ch += kColsPerWave) {
       const int j0 = s0 + ch + lane * kColsPerLane;  // first column of this lane
-      float mx[kColsPerLane], my[kColsPerLane], mz[kColsPerLane], b2[kColsPerLane];
+      // column pairs in packed registers: one v_pk_fma_f32 / v_pk_add_f32 does two
+      // columns at the scalar rate, each lane-half rounded exactly as v_fma_f32 / v_sub_f32
+      f32x2 mx[kColsPerLane / 2], my[kColsPerLane / 2], mz[kColsPerLane / 2], b2[kColsPerLane / 2];
 #pragma unroll
       for (int c = 0; c < kColsPerLane; ++c) {
         const float4 v = scol[ch + (c << 6) + lane];
-        mx[c] = v.x;
-        my[c] = v.y;
-        mz[c] = v.z;
-        b2[c] = v.w;
+        mx[c >> 1][c & 1] = v.x;
+        my[c >> 1][c & 1] = v.y;
+        mz[c >> 1][c & 1] = v.z;
+        b2[c >> 1][c & 1] = v.w;
       }
       const bool store = mask != nullptr && (ch + lane * kColsPerLane) < scols;
-#pragma unroll 1
-      for (int rp = 0; rp < kRowsPerWave; rp += 2) {
-      uint32_t pair_cnt = 0;  // this lane's in-pairs of rows rp (low 16 bits) and rp+1 (high)
+      uint8_t* rowp = store ? mask + ((int64_t)b * n1max + row0) * ld + j0 : nullptr;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int r = rp + h;
+      for (int r = 0; r < kRowsPerWave; ++r) {
         const int i = row0 + r;
         if (i >= n1max) break;  // wave-uniform
         const float4 rv = srow[wave * kRowsPerWave + r];
         const uint32_t Wb = srowW[wave * kRowsPerWave + r];
+        const f32x2 ax2 = {rv.x, rv.x}, ay2 = {rv.y, rv.y}, az2 = {rv.z, rv.z}, lo2 = {rv.w, rv.w};
         float d[kColsPerLane];
         uint32_t mn = 0xffffffffu;
 #pragma unroll
-        for (int c = 0; c < kColsPerLane; ++c) {
-          const float qv = fmaf(rv.x, mx[c], fmaf(rv.y, my[c], fmaf(rv.z, mz[c], b2[c])));
-          d[c] = qv - rv.w;
-          mn = min(mn, __float_as_uint(d[c]));
+        for (int c2 = 0; c2 < kColsPerLane / 2; ++c2) {
+          const f32x2 qv = __builtin_elementwise_fma(
+              ax2, mx[c2], __builtin_elementwise_fma(ay2, my[c2], __builtin_elementwise_fma(az2, mz[c2], b2[c2])));
+          const f32x2 dv = qv - lo2;
+          d[2 * c2] = dv.x;
+          d[2 * c2 + 1] = dv.y;
+          mn = min(min(mn, __float_as_uint(dv.x)), __float_as_uint(dv.y));  // v_min3_u32
         }
         // 0x01 where sign(d) = 1 (in). v_perm_b32 selectors 9 / 11 replicate the sign
         // bit of src1 / src0 into a byte; 12 gives 0x00.
@@ -376,21 +384,29 @@ __global__ __launch_bounds__(kBqThreads) void bq_mask_stream_kernel(
             w[m] = (w[m] & ~clr) | set;
           }
         }
-        pair_cnt += (uint32_t)(__popc(w[0]) + __popc(w[1]) + __popc(w[2]) + __popc(w[3])) << (h * 16);
+        // bytes are 0/1, so the byte-wise sum of the four words has no carries (<= 4 per
+        // byte) and v_sad_u8 against 0 adds its four bytes to the row's running count
+        cnt[r] = __builtin_amdgcn_sad_u8(w[0] + w[1] + w[2] + w[3], 0u, cnt[r]);
         if (store) {
-          u32x4* dst = reinterpret_cast<u32x4*>(mask + ((int64_t)b * n1max + i) * ld + j0);
           const u32x4 val = {w[0], w[1], w[2], w[3]};
-          __builtin_nontemporal_store(val, dst);
+          if constexpr (NT) {
+            __builtin_nontemporal_store(val, reinterpret_cast<u32x4*>(rowp + (int64_t)r * ld));
+          } else {
+            *reinterpret_cast<u32x4*>(rowp + (int64_t)r * ld) = val;
+          }
         }
-      }
-      // both rows' totals at once (16-bit fields: a row holds < 65536 pairs); lane r
-      // keeps row r's running count
-      const uint32_t t = (uint32_t)pk::wave_sum_i32_s((int)pair_cnt);
-      if ((lane >> 1) == (rp >> 1)) mine += (lane & 1) ? (t >> 16) : (t & 0xffffu);
       }
     }
   }
   if (row0 >= n1max) return;
+  // row totals, two rows per reduction (16-bit fields: a row holds < 65536 pairs); lane r
+  // keeps row r's count
+  uint32_t mine = 0;
+#pragma unroll
+  for (int rp = 0; rp < kRowsPerWave; rp += 2) {
+    const uint32_t t = (uint32_t)pk::wave_sum_i32_s((int)(cnt[rp] | (cnt[rp + 1] << 16)));
+    if ((lane >> 1) == (rp >> 1)) mine = (lane & 1) ? (t >> 16) : (t & 0xffffu);
+  }
   if (lane < kRowsPerWave && row0 + lane < n1max) rowcount[(int64_t)b * n1max + row0 + lane] = (int32_t)mine;
 }
 
@@ -551,8 +567,21 @@ extern "C" int pk_ball_query_mask(const double* cad, const int64_t* cad_off, con
   hipStream_t s = pk::as_stream(stream);
   const int nrb = (n1max + kRowsPerBlock - 1) / kRowsPerBlock;
   if (n2max < 65536 && (int64_t)nrb * B < (1ll << 31)) {
-    hipLaunchKernelGGL(bq_mask_stream_kernel, dim3(nrb * B), dim3(kBqThreads), 0, s, cad, cad_off, pc,
-                       pc_off, thr2, n1max, ld, nrb, mask, rowcount);
+#define PK_BQS(NT)                                                                              \
+  hipLaunchKernelGGL((bq_mask_stream_kernel<NT>), dim3(nrb * B), dim3(kBqThreads), 0, s, cad, cad_off, \
+                     pc, pc_off, thr2, n1max, ld, nrb, mask, rowcount)
+#ifdef PK_DEVBUILD
+    // PK_BQ_VAR=1: plain mask stores (A/B only: 0.40 vs 0.56 of HBM peak for nt, profiles/r06_bq_ramp.txt)
+    static const int var = [] { const char* e = std::getenv("PK_BQ_VAR"); return e ? std::atoi(e) : 0; }();
+    if (var == 1) {
+      PK_BQS(false);
+    } else {
+      PK_BQS(true);
+    }
+#else
+    PK_BQS(true);
+#endif
+#undef PK_BQS
   } else {
     dim3 grid(nrb, B);
     hipLaunchKernelGGL(bq_mask_f32_kernel, grid, dim3(kBqThreads), 0, s, cad, cad_off, pc, pc_off,

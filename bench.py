@@ -145,7 +145,9 @@ def ball_query_roofline(dev, probe_launches: int = 10, blocks: int = 7) -> dict:
     rc = torch.empty((B, N), dtype=torch.int32, device=dev)
     f = lambda: call("pk_ball_query_mask", ptr(cad), ptr(off), ptr(pc), ptr(off), ptr(thr), B, N, N, ptr(mask), N,  # noqa
                      ptr(rc), stream(dev))
-    for _ in range(3):
+    # untimed warm-up, ~60 ms of launches: under this write load the clocks ramp for ~25 ms (the
+    # per-block fractions climb 0.48 -> 0.62 over the first 10 blocks, profiles/r06_bq_ramp.txt)
+    for _ in range(25 * probe_launches):
         f()
     torch.cuda.synchronize()
     byts = B * (24 * N + 24 * N + N * N) + B * N * 4  # coords in + mask + row counts
@@ -156,13 +158,15 @@ def ball_query_roofline(dev, probe_launches: int = 10, blocks: int = 7) -> dict:
             f()
         e.record()
     torch.cuda.synchronize()
-    mss = sorted(s.elapsed_time(e) / probe_launches for s, e in ev)
+    seq = [s.elapsed_time(e) / probe_launches for s, e in ev]  # time order
+    mss = sorted(seq)
     ms = float(np.median(mss))
     fr = lambda m: round(byts / (m * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)  # noqa: E731
     ach = byts / (ms * 1e-3) / 1e9
     return {"kernel": "pk_ball_query_mask (configs[3]: 256 x 2048 x 2048)", "bound": "hbm", "achieved": round(ach, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-            "frac_min": fr(mss[-1]), "frac_max": fr(mss[0]), "blocks": blocks, "launches_per_block": probe_launches,
+            "frac_min": fr(mss[-1]), "frac_max": fr(mss[0]), "frac_blocks": [fr(m) for m in seq],
+            "blocks": blocks, "launches_per_block": probe_launches,
             "traffic": pmc_traffic("pk_ball_query_mask@configs3_probe"),
             "ms_per_launch": round(ms, 4), "bytes_per_launch": byts}
 
