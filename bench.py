@@ -174,8 +174,9 @@ def ball_query_roofline(dev, probe_launches: int = 10, blocks: int = 7) -> dict:
 def feat_dist_roofline(dev, launches: int = 20) -> dict:
     """The north-star MFMA gate kernel: pk_feat_dist_topk (fp32 argmin, the naive solver's and the
     IR's feature distance, fmap2pointmap_solvers/naive.py:20,33) at configs[1] (32 crops of
-    1024 x 1024, K = 32: 2.147 GFLOP per call), `launches` back-to-back calls between two HIP
-    events on the launch stream (its prep + main passes included), spectral-basis operands."""
+    1024 x 1024, K = 32: 2.147 GFLOP per call), `launches` back-to-back calls in one HIP graph
+    between two HIP events on the launch stream (its prep + main passes included), spectral-basis
+    operands."""
     from dpfm_amd import ops
     from dpfm_amd.dataset.synthetic import lbo_operators
     B, V = 32, 1024
@@ -188,13 +189,22 @@ def feat_dist_roofline(dev, launches: int = 20) -> dict:
     for _ in range(3):
         f()
     torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(launches):
-        f()
-    e.record()
+    # the calls as the pipeline issues them (HIP graph: no host gaps), timed after ~60 ms of
+    # replays (clock ramp, profiles/r06_bq_ramp.txt); median of 5 timed replays
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        for _ in range(launches):
+            f()
+    for _ in range(100):
+        gr.replay()
     torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / launches
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+    for s, e in evs:
+        s.record()
+        gr.replay()
+        e.record()
+    torch.cuda.synchronize()
+    ms = sorted(s.elapsed_time(e) for s, e in evs)[2] / launches
     flops = 2.0 * B * V * V * 32
     ach = flops / (ms * 1e-3) / 1e12
     return {"kernel": "pk_feat_dist_topk (configs[1]: 32 x 1024 x 1024, fp32 top-1, prep + main)", "bound": "mfma",

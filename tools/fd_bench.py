@@ -21,6 +21,7 @@ from dpfm_amd.dataset.synthetic import lbo_operators  # noqa: E402
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 only = sys.argv[2] if len(sys.argv) > 2 else None  # e.g. "32x1024"
 precs = sys.argv[3].split(",") if len(sys.argv) > 3 else ["fp32", "bf16x3", "bf16"]
+warm = int(os.environ.get("FD_WARM", "100"))  # untimed graph replays before timing
 dev = torch.device("cuda:0")
 for B, V in [(32, 1024), (8, 2048), (1, 4096)]:
     if only and only != f"{B}x{V}":
@@ -42,14 +43,16 @@ for B, V in [(32, 1024), (8, 2048), (1, 4096)]:
             with torch.cuda.graph(gr):
                 for _ in range(iters):
                     f()
-            gr.replay()
+            for _ in range(warm):  # past the clock ramp (profiles/r06_bq_ramp.txt)
+                gr.replay()
             torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            gr.replay()
-            e1.record()
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+            for e0, e1 in evs:
+                e0.record()
+                gr.replay()
+                e1.record()
             torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / iters
+            ms = sorted(e0.elapsed_time(e1) for e0, e1 in evs)[2] / iters  # median of 5 replays
             fl = 2.0 * B * V * V * 32
             peak = 157.3 if prec == "fp32" else 2500.0
             idx = out[0]
