@@ -517,11 +517,11 @@ __global__ __launch_bounds__(64 * kWaves) void fd_main_direct_kernel(
 constexpr int kTop1CT = 8;
 constexpr int kTop1Waves = 8;  // two per SIMD: one wave's dependency stalls are the other's MFMA time
 #ifdef PK_DEVBUILD
-__device__ unsigned long long g_fd_stamps[4096 * 8];  // (development: VAR 13 phase stamps per block)
+__device__ unsigned long long g_fd_stamps[4096 * 16];  // (development: VAR 13 phase stamps per block)
 #define FD_STAMP(i, v)                                                  \
   do {                                                                  \
     if constexpr (VAR == 13) {                                          \
-      if (threadIdx.x == 0) g_fd_stamps[blockIdx.x * 8 + (i)] = (v);    \
+      if (threadIdx.x == 0) g_fd_stamps[blockIdx.x * 16 + (i)] = (v);   \
     }                                                                   \
   } while (0)
 #else
@@ -950,6 +950,45 @@ __device__ __forceinline__ void t5_insert(unsigned long long (&best)[5], unsigne
   }
 }
 
+// any of the four lanes 4c..4c+3 (a column's E3 threads)
+__device__ __forceinline__ bool t5_any4(bool v) {
+  int x = v ? 1 : 0;
+  x |= __shfl_xor(x, 1);
+  x |= __shfl_xor(x, 2);
+  return x != 0;
+}
+
+// the lowest five of this lane's and lane ^ off's ascending 5-lists (unique keys but the ~0
+// padding), ascending, with their slots: the elementwise minimum against the partner's reversed
+// list is a bitonic sequence holding the lowest five, then a 5-input sorting network
+__device__ __forceinline__ void t5_merge_xor(unsigned long long (&bst)[5], int (&bsl)[5], int off) {
+  unsigned long long o[5];
+  int os[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const unsigned lo = __shfl_xor((unsigned)(bst[q] & 0xffffffffu), off);
+    const unsigned hi = __shfl_xor((unsigned)(bst[q] >> 32), off);
+    o[q] = ((unsigned long long)hi << 32) | lo;
+    os[q] = __shfl_xor(bsl[q], off);
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const bool tk = o[4 - q] < bst[q];
+    bst[q] = tk ? o[4 - q] : bst[q];
+    bsl[q] = tk ? os[4 - q] : bsl[q];
+  }
+  auto ce = [&](int x, int y) {
+    const bool sw = bst[y] < bst[x];
+    const unsigned long long kx = bst[x], ky = bst[y];
+    const int sx = bsl[x], sy = bsl[y];
+    bst[x] = sw ? ky : kx;
+    bst[y] = sw ? kx : ky;
+    bsl[x] = sw ? sy : sx;
+    bsl[y] = sw ? sx : sy;
+  };
+  ce(0, 1); ce(3, 4); ce(2, 4); ce(2, 3); ce(0, 3); ce(0, 2); ce(1, 4); ce(1, 3); ce(1, 2);
+}
+
 // value-only compare-exchange and the sorted merges of E1
 __device__ __forceinline__ void ce_i(int& a, int& b) {
   const int lo = min(a, b), hi = max(a, b);
@@ -968,9 +1007,10 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
   __shared__ int sLm[NC][4 * kTop1Waves + 1];
   __shared__ int sT[NC];
   __shared__ int sCnt[NC];
-  __shared__ unsigned long long sKey[NC][kT5Slots];
-  __shared__ int sK2[NC][kT5Slots];
-  __shared__ int sStr[NC][kT5Slots];
+  // candidate lists, rows padded by one entry: a wave's 16 columns at one slot spread over the banks
+  __shared__ unsigned long long sKey[NC][kT5Slots + 1];
+  __shared__ int sK2[NC][kT5Slots + 1];
+  __shared__ int sStr[NC][kT5Slots + 1];
   __shared__ int sSlow[NC];
   __shared__ int sNslow, sNtask;
   __shared__ int sTask[kT5Tasks];
@@ -990,6 +1030,7 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
     }
   }
   const int cg = k % NCG, rs = k / NCG;
+  FD_STAMP(0, __builtin_amdgcn_s_memtime());
   const int N1 = n1[b], N2 = n2[b];
   const int j0 = cg * NC;
   if (j0 >= N2) return;  // (block-uniform)
@@ -1057,6 +1098,7 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
         for (int q = 0; q < 4; ++q) bo[c2][4 * h + q] = t4[q];
       }
   }
+  FD_STAMP(1, __builtin_amdgcn_s_memtime());
   int k1[kTop1CT][4], t1[kTop1CT][4], k2[kTop1CT][4];
 #pragma unroll
   for (int c = 0; c < kTop1CT; ++c)
@@ -1115,6 +1157,7 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
     sel(acc[kTop1CT - 2], kTop1CT - 2, t);
     sel(acc[kTop1CT - 1], kTop1CT - 1, t);
   }
+  FD_STAMP(2, __builtin_amdgcn_s_memtime());
   // E0: the lane minima (over r) of every column, per (wave, lane group)
 #pragma unroll
   for (int c = 0; c < kTop1CT; ++c)
@@ -1147,120 +1190,133 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
     if (qq == 0) sT[col] = v[4];
   }
   __syncthreads();
-  // E2: the candidate streams of each column (minimum <= T)
+  FD_STAMP(3, __builtin_amdgcn_s_memtime());
+  // E2: the candidate streams of each column (minimum <= T). One slot-range reservation per
+  // (lane, column) for all of its candidate streams, the 8 reservations in flight together
+  {
+    int base[kTop1CT];
+    unsigned cm[kTop1CT];
 #pragma unroll
-  for (int c = 0; c < kTop1CT; ++c) {
-    const int col = c * 16 + c16;
-    const int T = sT[col];
+    for (int c = 0; c < kTop1CT; ++c) {
+      const int T = sT[c * 16 + c16];
+      cm[c] = (k1[c][0] <= T ? 1u : 0u) | (k1[c][1] <= T ? 2u : 0u) | (k1[c][2] <= T ? 4u : 0u) |
+              (k1[c][3] <= T ? 8u : 0u);
+      base[c] = cm[c] ? atomicAdd(&sCnt[c * 16 + c16], __popc(cm[c])) : 0;
+    }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (k1[c][r] <= T) {
-        const int slot = atomicAdd(&sCnt[col], 1);
-        if (slot < kT5Slots) {
+    for (int c = 0; c < kTop1CT; ++c) {
+      const int col = c * 16 + c16;
+      int slot = base[c];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (((cm[c] >> r) & 1u) && slot < kT5Slots) {
           const unsigned row = (unsigned)(t1[c][r] * 16 + 4 * g + r);
           sKey[col][slot] = ((unsigned long long)(unsigned)k1[c][r] << 32) | row;
           sK2[col][slot] = k2[c][r];
           sStr[col][slot] = (w << 4) | (g << 2) | r;
         }
+        slot += (cm[c] >> r) & 1u;
       }
     }
   }
   __syncthreads();
-  // E3: one thread per column selects five among its candidates and lists the rows to recompute
-  // (E3b computes them with every thread of the block, one row each, E3c merges)
+  FD_STAMP(4, __builtin_amdgcn_s_memtime());
+  // E3: four threads per column (tid = 4 col + qd, lanes of one wave): each selects five among
+  // candidates qd, qd + 4, ...; two shuffle merges give the four the column's five; thread qd then
+  // lists the recompute rows of kept stream qd (E3b computes them with every thread of the block,
+  // one row each). E3c: thread 0 of the column keeps the five, threads 1-3 collect the recomputed
+  // rows they listed, and the same two merges combine the four lists (all rows distinct: a
+  // stream's rows belong to it alone, and its kept row is not listed).
   unsigned long long best[5];
+  int bsl[5];  // candidate slot of each kept entry
 #pragma unroll
-  for (int q = 0; q < 5; ++q) best[q] = ~0ull;
-  bool mine = false, slow = false;
+  for (int q = 0; q < 5; ++q) {
+    best[q] = ~0ull;
+    bsl[q] = -1;
+  }
+  const int col = tid >> 2, qd = tid & 3;
+  const bool colok = j0 + col < N2;
   int tbase = 0, tcnt = 0;
-  if (tid < NC && j0 + tid < N2) {
-    const int col = tid;
-    const int n = sCnt[col];
-    slow = n > kT5Slots;
-    int bsl[5] = {-1, -1, -1, -1, -1};  // candidate slot of each kept entry
-    if (!slow) {
-      for (int i = 0; i < n; ++i) {
-        unsigned long long key = sKey[col][i];
-        const int hi = (int)(key >> 32);
-        if (hi <= kClampBits) slow = true;        // a clamped distance: the slow path orders them
-        if (hi >= 0x7f800000) continue;           // no row (padding)
-        if (!(key < best[4])) continue;
-        int si = i;
+  const int n = colok ? sCnt[col] : 0;
+  bool slow = n > kT5Slots;
+  if (!slow) {
+    for (int i = qd; i < n; i += 4) {
+      unsigned long long key = sKey[col][i];
+      const int hi = (int)(key >> 32);
+      if (hi <= kClampBits) slow = true;        // a clamped distance: the slow path orders them
+      if (hi >= 0x7f800000) continue;           // no row (padding)
+      if (!(key < best[4])) continue;
+      int si = i;
 #pragma unroll
-        for (int q = 0; q < 5; ++q) {
-          const bool sw = key < best[q];
-          const unsigned long long tv = sw ? best[q] : key;
-          const int ts = sw ? bsl[q] : si;
-          best[q] = sw ? key : best[q];
-          bsl[q] = sw ? si : bsl[q];
-          key = tv;
-          si = ts;
-        }
+      for (int q = 0; q < 5; ++q) {
+        const bool sw = key < best[q];
+        const unsigned long long tv = sw ? best[q] : key;
+        const int ts = sw ? bsl[q] : si;
+        best[q] = sw ? key : best[q];
+        bsl[q] = sw ? si : bsl[q];
+        key = tv;
+        si = ts;
       }
     }
-    if (!slow) {
-      // kept streams ranked 1..4 whose second value is <= the fifth value may hold more members:
-      // their rows (but the kept one) become recompute tasks. (The fifth value only falls as
-      // rows are merged, so the streams listed against the first selection cover every stream
-      // that can still hold a member.)
-      const int S = best[4] == ~0ull ? 0x7f800000 : (int)(best[4] >> 32);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (bsl[q] < 0 || sK2[col][bsl[q]] > S) continue;
-        const int st = sStr[col][bsl[q]];
-        const int sqw = rs * kTop1Waves + (st >> 4);
-        const int stb = (int)((int64_t)nt * sqw / Q), ste = (int)((int64_t)nt * (sqw + 1) / Q);
-        const int i = ((st >> 2) & 3) * 4 + (st & 3);
-        const int known = (int)(best[q] & 0xffffffffu);
-        for (int t = stb; t < ste; ++t)
-          if (t * 16 + i < N1 && t * 16 + i != known) ++tcnt;
-      }
+  }
+  slow = t5_any4(slow);
+  t5_merge_xor(best, bsl, 1);
+  t5_merge_xor(best, bsl, 2);
+  if (!slow && colok) {
+    // kept stream qd (ranks 0..3) whose second value is <= the fifth value may hold more members:
+    // its rows (but the kept one) become recompute tasks. (The fifth value only falls as rows are
+    // merged, so the streams listed against the first selection cover every stream that can still
+    // hold a member.)
+    const int S = best[4] == ~0ull ? 0x7f800000 : (int)(best[4] >> 32);
+    if (bsl[qd] >= 0 && sK2[col][bsl[qd]] <= S) {
+      const int st = sStr[col][bsl[qd]];
+      const int sqw = rs * kTop1Waves + (st >> 4);
+      const int stb = (int)((int64_t)nt * sqw / Q), ste = (int)((int64_t)nt * (sqw + 1) / Q);
+      const int i = ((st >> 2) & 3) * 4 + (st & 3);
+      const int known = (int)(best[qd] & 0xffffffffu);
+      for (int t = stb; t < ste; ++t)
+        if (t * 16 + i < N1 && t * 16 + i != known) ++tcnt;
       if (tcnt > 0) {
         tbase = atomicAdd(&sNtask, tcnt);
         if (tbase + tcnt > kT5Tasks) {
           slow = true;  // (task list full: the slow path takes the column)
+          tcnt = 0;
         } else {
           int k = tbase;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (bsl[q] < 0 || sK2[col][bsl[q]] > S) continue;
-            const int st = sStr[col][bsl[q]];
-            const int sqw = rs * kTop1Waves + (st >> 4);
-            const int stb = (int)((int64_t)nt * sqw / Q), ste = (int)((int64_t)nt * (sqw + 1) / Q);
-            const int i = ((st >> 2) & 3) * 4 + (st & 3);
-            const int known = (int)(best[q] & 0xffffffffu);
-            for (int t = stb; t < ste; ++t)
-              if (t * 16 + i < N1 && t * 16 + i != known) sTask[k++] = (t << 11) | (col << 4) | i;
-          }
+          for (int t = stb; t < ste; ++t)
+            if (t * 16 + i < N1 && t * 16 + i != known) sTask[k++] = (t << 11) | (col << 4) | i;
         }
       }
     }
   }
   __syncthreads();
+  FD_STAMP(5, __builtin_amdgcn_s_memtime());
   {  // E3b: every listed row's exact distance, one per thread
     const int ntask = min(sNtask, kT5Tasks);
     for (int k = tid; k < ntask; k += 64 * kTop1Waves) {
-      const int d = sTask[k], t = d >> 11, col = (d >> 4) & (NC - 1), i = d & 15;
-      const float v = t5_exact(Ab, t, i, sB, col);
+      const int d = sTask[k], t = d >> 11, cc = (d >> 4) & (NC - 1), i = d & 15;
+      const float v = t5_exact(Ab, t, i, sB, cc);
       sTaskKey[k] = ((unsigned long long)__float_as_uint(v) << 32) | (unsigned)(t * 16 + i);
       if (__float_as_int(v) <= kClampBits) sTaskKey[k] = 0ull;  // a clamped distance: the slow path
     }
   }
   __syncthreads();
-  if (tid < NC && j0 + tid < N2) {  // E3c: merge the recomputed rows
-    const int col = tid;
-    if (!slow) {
-      for (int k = tbase; k < tbase + tcnt; ++k) {
-        const unsigned long long key = sTaskKey[k];
-        if (key == 0ull) slow = true;
-        t5_insert(best, key);
-      }
+  FD_STAMP(6, __builtin_amdgcn_s_memtime());
+  {  // E3c: merge the recomputed rows
+    if (qd != 0) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q) best[q] = ~0ull;
     }
-    if (slow) {
-      sSlow[atomicAdd(&sNslow, 1)] = col;
-    } else {
-      mine = true;
+    for (int k = tbase; k < tbase + tcnt; ++k) {
+      const unsigned long long key = sTaskKey[k];
+      if (key == 0ull) slow = true;
+      t5_insert(best, key);
     }
+    FD_STAMP(8, __builtin_amdgcn_s_memtime());
+    slow = t5_any4(slow);
+    t5_merge_xor(best, bsl, 1);
+    t5_merge_xor(best, bsl, 2);
+    FD_STAMP(9, __builtin_amdgcn_s_memtime());
   }
   auto emit = [&](int col, const unsigned long long (&bst)[5]) {
     const int j = j0 + col;
@@ -1282,10 +1338,19 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
       }
     }
   };
-  if (mine) emit(tid, best);
+  if (qd == 0 && colok) {
+    if (slow) {
+      sSlow[atomicAdd(&sNslow, 1)] = col;
+    } else {
+      emit(col, best);
+    }
+  }
   __syncthreads();
   // slow path: one wave per column, every row of this row part, clamped distances, lower row first
   const int nslow = sNslow;
+  FD_STAMP(10, __builtin_amdgcn_s_memtime());
+  FD_STAMP(11, (unsigned long long)nslow);
+  FD_STAMP(12, (unsigned long long)sNtask);
   const int pt0 = (int)((int64_t)nt * (rs * kTop1Waves) / Q), pt1 = (int)((int64_t)nt * (rs * kTop1Waves + kTop1Waves) / Q);
   for (int si = w; si < nslow; si += kTop1Waves) {
     const int col = sSlow[si];
@@ -1311,6 +1376,7 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
     }
     if (lane == 0) emit(col, bl);
   }
+  FD_STAMP(7, __builtin_amdgcn_s_memtime());
 }
 
 struct Top1Plan {
@@ -1438,8 +1504,19 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
     hipLaunchKernelGGL(fd_top1_prep_kernel, dim3((unsigned)((tp.T1 + 7) / 8), B), dim3(512), 0, s, evecs_x, ldx, C,
                        n1, V1max, tp.T1, At);
     PK_CHECK_LAUNCH();
-    hipLaunchKernelGGL((fd_top5_kernel<0>), dim3((unsigned)((int64_t)B * tp.NCG * tp.RS)), dim3(64 * kTop1Waves), 0,
-                       s, At, tp.T1, evecs_y, ldy, n1, n2, V2max, tp.NCG, tp.RS, out_idx, out_dist, pv, pi);
+#define PK_FD5(V)                                                                                                \
+  hipLaunchKernelGGL((fd_top5_kernel<V>), dim3((unsigned)((int64_t)B * tp.NCG * tp.RS)), dim3(64 * kTop1Waves), 0, s, \
+                     At, tp.T1, evecs_y, ldy, n1, n2, V2max, tp.NCG, tp.RS, out_idx, out_dist, pv, pi)
+#ifdef PK_DEVBUILD
+    static const int t5var = [] {  // development knob PK_FD_VAR=13: phase stamps (tools/fd_stamps.py)
+      const char* e = std::getenv("PK_FD_VAR");
+      return e ? std::atoi(e) : 0;
+    }();
+    if (t5var == 13) PK_FD5(13); else PK_FD5(0);
+#else
+    PK_FD5(0);
+#endif
+#undef PK_FD5
     PK_CHECK_LAUNCH();
     if (tp.RS > 1) {
       hipLaunchKernelGGL(fd_merge_kernel<5>, dim3((V2max + 255) / 256, B), dim3(256), 0, s, pv, pi, n2, V2max, tp.RS,
