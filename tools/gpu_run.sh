@@ -63,8 +63,6 @@ for step in "$@"; do
            python tools/mfma_util.py "$out/fdpmc1" fd_top1_kernel fd_top1_prep_kernel fd_top1_merge fd_main_direct_kernel fd_prep_kernel fd_merge_kernel > "$out/mfma_util.json" 2>&1
            python tools/pmc_pick.py "$out/fdpmc1" fd_ > "$out/fd_pmc_counters.txt" 2>&1 || true ;;
     tprof) run tprof 300 python tools/torch_prof.py "$tag" ;;
-    rdiag2) run rdiag2 300 python tools/replay_diag2.py ;;
-    rdiag3) run rdiag3 300 python tools/replay_diag3.py ;;
     mprobe) run mprobe 300 python tools/memset_graph_probe.py ;;
     mprobe_nopc) DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run mprobe_nopc 300 python tools/memset_graph_probe.py ;;
     *) echo "unknown step $step"; exit 2 ;;
