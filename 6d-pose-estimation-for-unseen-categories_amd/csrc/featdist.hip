@@ -584,22 +584,52 @@ __device__ __forceinline__ void top1_emb_norm(int t, int N1, int c16, int g, con
   a[7] = g3 ? 1.f : a[7];
 }
 
-// pass 1: grid (ceil(T1 / 8), B), 8 waves: wave = one 16-row tile of crop b's x side, its A tile
-// [-2 emb, |emb|^2, 1]; -2 C staged once per block in LDS with a 32-float row pitch so each lane
-// reads its 16 C values as four 16-B loads. Tiles at or past a crop's valid rows are skipped
-// (pass 2 never reads them).
+// pass 1: grid NTG * B (NTG = ceil(T1 / 8) tile groups per crop), 8 waves: wave = one 16-row tile
+// of crop b's x side, its A tile [-2 emb, |emb|^2, 1]; -2 C staged once per block in LDS with a
+// 32-float row pitch so each lane reads its 16 C values as four 16-B loads. Tiles at or past a
+// crop's valid rows are skipped (pass 2 never reads them). Blocks are numbered as pass 2's (crop
+// b's blocks on XCD b % 8 when B % 8 == 0), and each also touches its share of crop b's y rows —
+// pass 2's column operands — with loads issued beside its own and consumed at the end, so pass 2's
+// staging finds them warm on the XCD that reads them.
 __global__ __launch_bounds__(512) void fd_top1_prep_kernel(const float* __restrict__ ex, int ldx,
                                                           const float* __restrict__ C,
                                                           const int32_t* __restrict__ n1, int V1max, int T1,
-                                                          f32x4* __restrict__ Atile) {
+                                                          f32x4* __restrict__ Atile, const float* __restrict__ ey,
+                                                          int ldy, const int32_t* __restrict__ n2, int V2max,
+                                                          int NTG) {
   __shared__ __attribute__((aligned(16))) float sc[kK * 32];
   const int lane = pk::lane_id(), w = __builtin_amdgcn_readfirstlane(pk::wave_id());
   const int g = lane >> 4, c16 = lane & 15;
-  const int b = blockIdx.y, t = blockIdx.x * 8 + w;
+  const int B = (int)(gridDim.x / NTG);
+  int b, tg;
+  {
+    const int L = blockIdx.x;
+    if ((B & 7) == 0) {
+      const int x8 = L & 7, q = L >> 3;
+      b = x8 + 8 * (q / NTG);
+      tg = q - (q / NTG) * NTG;
+    } else {
+      b = L / NTG;
+      tg = L - b * NTG;
+    }
+  }
+  const int t = tg * 8 + w;
   const int N1 = n1[b];
   const bool act = t < T1 && t * 16 < N1;
   float4 xv[2];
   if (act) top1_xload(ex + (int64_t)b * V1max * ldx, ldx, N1, t, c16, g, xv);
+  f32x4 yt[4];  // the y touch: rows [r0, r1) of crop b, 8 x 16 B each (up to 256 rows per block)
+  {
+    const int N2 = n2[b];
+    const int r0 = (int)((int64_t)N2 * tg / NTG), r1 = (int)((int64_t)N2 * (tg + 1) / NTG);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = threadIdx.x + 512 * u;
+      yt[u] = e < (r1 - r0) * 8
+                  ? *reinterpret_cast<const f32x4*>(ey + ((int64_t)b * V2max + r0 + (e >> 3)) * ldy + 4 * (e & 7))
+                  : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
   const float* Cb = C + (int64_t)b * kF * kF;
   for (int e = threadIdx.x; e < kK * 32; e += 512) {  // -2 C, zero-padded to 32 x 32
     const int row = e >> 5, f = e & 31;
@@ -607,23 +637,25 @@ __global__ __launch_bounds__(512) void fd_top1_prep_kernel(const float* __restri
     sc[e] = (row < kF && f < kF) ? -2.f * cval : 0.f;
   }
   __syncthreads();
-  if (!act) return;
-  float cv[2][8];
+  if (act) {
+    float cv[2][8];
 #pragma unroll
-  for (int n = 0; n < 2; ++n)
+    for (int n = 0; n < 2; ++n)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x4 v4 = *reinterpret_cast<const f32x4*>(sc + (16 * n + c16) * 32 + 16 * h + 4 * g);
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 v4 = *reinterpret_cast<const f32x4*>(sc + (16 * n + c16) * 32 + 16 * h + 4 * g);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) cv[n][4 * h + q] = v4[q];
-    }
-  f32x4 e[2];
-  top1_emb_mfma(cv, xv, e);
-  float a[8];
-  top1_emb_norm(t, N1, c16, g, e, a);
-  f32x4* dst = Atile + ((int64_t)b * T1 + t) * 128;
-  dst[lane] = f32x4{a[0], a[1], a[2], a[3]};
-  dst[64 + lane] = f32x4{a[4], a[5], a[6], a[7]};
+        for (int q = 0; q < 4; ++q) cv[n][4 * h + q] = v4[q];
+      }
+    f32x4 e[2];
+    top1_emb_mfma(cv, xv, e);
+    float a[8];
+    top1_emb_norm(t, N1, c16, g, e, a);
+    f32x4* dst = Atile + ((int64_t)b * T1 + t) * 128;
+    dst[lane] = f32x4{a[0], a[1], a[2], a[3]};
+    dst[64 + lane] = f32x4{a[4], a[5], a[6], a[7]};
+  }
+  asm volatile("" ::"v"(yt[0]), "v"(yt[1]), "v"(yt[2]), "v"(yt[3]));  // (keeps the touch loads)
 }
 
 // pass 2 (EMB: form the emb operands in this pass instead of reading pass 1's tiles)
@@ -654,10 +686,14 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top1_kernel(
   FD_STAMP(0, __builtin_amdgcn_s_memtime());
   FD_STAMP(5, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4));
   FD_STAMP(6, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20));
-  const int N1 = n1[b], N2 = n2[b];
   const int j0 = cg * kTop1CT * 16;
-  if (j0 >= N2) return;  // (block-uniform)
   const int tid = threadIdx.x, lane = pk::lane_id(), w = __builtin_amdgcn_readfirstlane(pk::wave_id());
+  // the column operands' loads go out beside the crop sizes' (their addresses do not need them)
+  const int sjj = tid & (kTop1CT * 16 - 1), sgy = tid >> 7;  // staging: column sjj, lane group sgy
+  const float* syr = ey + ((int64_t)b * V2max + min(j0 + sjj, V2max - 1)) * ldy;
+  const float4 sy0 = *reinterpret_cast<const float4*>(syr + 4 * sgy);
+  const float4 sy1 = *reinterpret_cast<const float4*>(syr + 16 + 4 * sgy);
+  const int N1 = n1[b], N2 = n2[b];
   const int g = lane >> 4, c16 = lane & 15;
   const int nt = (N1 + 15) >> 4;
   const int Q = RS * kTop1Waves, qw = rs * kTop1Waves + w;
@@ -694,13 +730,10 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top1_kernel(
   }
   float bo[kTop1CT][8];
   {  // staging: the block's 128 columns' [y, 1, |y|^2] in B order, through LDS
-    const int jj = tid & (kTop1CT * 16 - 1), gy = tid >> 7;  // column jj of the block, lane group gy
+    const int jj = sjj, gy = sgy;  // column jj of the block, lane group gy
     const int j = j0 + jj;
-    const float* yr = ey + ((int64_t)b * V2max + min(j, V2max - 1)) * ldy;
-    const float4 y0 = *reinterpret_cast<const float4*>(yr + 4 * gy);
-    const float4 y1 = *reinterpret_cast<const float4*>(yr + 16 + 4 * gy);
     const bool ok = j < N2;
-    float v[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+    float v[8] = {sy0.x, sy0.y, sy0.z, sy0.w, sy1.x, sy1.y, sy1.z, sy1.w};
     float part_ = 0.f;
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) {
@@ -708,6 +741,7 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top1_kernel(
       part_ = fmaf(v[s8], v[s8], part_);
     }
     sPart[gy][jj] = part_;
+    if (j0 >= N2) return;  // (block-uniform; after the loads' consumers, so they are not sunk past it)
     if (tb < te) emb(tb, xc, a);  // (the first tile's operand while the partials meet)
     __syncthreads();
     if (gy == 3) {  // |y|^2: the lane groups' partials in the order 0, 1, 2, 3
@@ -1031,10 +1065,14 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
   }
   const int cg = k % NCG, rs = k / NCG;
   FD_STAMP(0, __builtin_amdgcn_s_memtime());
-  const int N1 = n1[b], N2 = n2[b];
   const int j0 = cg * NC;
-  if (j0 >= N2) return;  // (block-uniform)
   const int tid = threadIdx.x, lane = pk::lane_id(), w = __builtin_amdgcn_readfirstlane(pk::wave_id());
+  // the column operands' loads go out beside the crop sizes' (as fd_top1_kernel)
+  const int sjj = tid & (NC - 1), sgy = tid >> 7;
+  const float* syr = ey + ((int64_t)b * V2max + min(j0 + sjj, V2max - 1)) * ldy;
+  const float4 sy0 = *reinterpret_cast<const float4*>(syr + 4 * sgy);
+  const float4 sy1 = *reinterpret_cast<const float4*>(syr + 16 + 4 * sgy);
+  const int N1 = n1[b], N2 = n2[b];
   const int g = lane >> 4, c16 = lane & 15;
   const int nt = (N1 + 15) >> 4;
   const int Q = RS * kTop1Waves;
@@ -1054,13 +1092,10 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
   }
   float bo[kTop1CT][8];
   {  // staging: the block's 128 columns' [y, 1, |y|^2] in B order, through LDS (as fd_top1_kernel)
-    const int jj = tid & (NC - 1), gy = tid >> 7;
+    const int jj = sjj, gy = sgy;
     const int j = j0 + jj;
-    const float* yr = ey + ((int64_t)b * V2max + min(j, V2max - 1)) * ldy;
-    const float4 y0 = *reinterpret_cast<const float4*>(yr + 4 * gy);
-    const float4 y1 = *reinterpret_cast<const float4*>(yr + 16 + 4 * gy);
     const bool ok = j < N2;
-    float v[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+    float v[8] = {sy0.x, sy0.y, sy0.z, sy0.w, sy1.x, sy1.y, sy1.z, sy1.w};
     float part_ = 0.f;
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) {
@@ -1068,6 +1103,7 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
       part_ = fmaf(v[s8], v[s8], part_);
     }
     sPart[gy][jj] = part_;
+    if (j0 >= N2) return;  // (block-uniform; after the loads' consumers)
     if (tb < te) {
       a[0] = xc[0].x, a[1] = xc[0].y, a[2] = xc[0].z, a[3] = xc[0].w;
       a[4] = xc[1].x, a[5] = xc[1].y, a[6] = xc[1].z, a[7] = xc[1].w;
@@ -1501,8 +1537,8 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
     int32_t* pi = tp.RS > 1 ? reinterpret_cast<int32_t*>(reinterpret_cast<char*>(pv) +
                                                          al256_((int64_t)B * tp.RS * V2max * 5 * 4))
                             : nullptr;
-    hipLaunchKernelGGL(fd_top1_prep_kernel, dim3((unsigned)((tp.T1 + 7) / 8), B), dim3(512), 0, s, evecs_x, ldx, C,
-                       n1, V1max, tp.T1, At);
+    hipLaunchKernelGGL(fd_top1_prep_kernel, dim3((unsigned)(((tp.T1 + 7) / 8) * B)), dim3(512), 0, s, evecs_x, ldx, C,
+                       n1, V1max, tp.T1, At, evecs_y, ldy, n2, V2max, (tp.T1 + 7) / 8);
     PK_CHECK_LAUNCH();
 #define PK_FD5(V)                                                                                                \
   hipLaunchKernelGGL((fd_top5_kernel<V>), dim3((unsigned)((int64_t)B * tp.NCG * tp.RS)), dim3(64 * kTop1Waves), 0, s, \
@@ -1539,8 +1575,8 @@ extern "C" int pk_feat_dist_topk(const float* evecs_x, int ldx, const float* C, 
     constexpr int tvar = 0;
 #endif
     if (tvar != 20) {
-      hipLaunchKernelGGL(fd_top1_prep_kernel, dim3((unsigned)((tp.T1 + 7) / 8), B), dim3(512), 0, s, evecs_x, ldx, C,
-                         n1, V1max, tp.T1, At);
+      hipLaunchKernelGGL(fd_top1_prep_kernel, dim3((unsigned)(((tp.T1 + 7) / 8) * B)), dim3(512), 0, s, evecs_x, ldx,
+                         C, n1, V1max, tp.T1, At, evecs_y, ldy, n2, V2max, (tp.T1 + 7) / 8);
       PK_CHECK_LAUNCH();
     }
 #define PK_FDT(V, E)                                                                                              \
