@@ -47,6 +47,20 @@ def main():
             r["valu_per_mfma"] = round(cs.get("SQ_INSTS_VALU", 0.0) / cs["SQ_INSTS_MFMA"], 3)
             r["mfma_busy_per_mfma"] = round(cs["SQ_VALU_MFMA_BUSY_CYCLES"] / cs["SQ_INSTS_MFMA"], 2)
         res[f"{n} grid={g}"] = r
+    # whole calls: a main pass with the prep dispatch right before it (busy and active cycles summed)
+    order = sorted(per, key=lambda x: int(x))
+    calls = collections.defaultdict(list)
+    for prev, did in zip(order, order[1:]):
+        n, pn = names[did], names[prev]
+        c, pc = per[did], per[prev]
+        if "prep" in pn and "prep" not in n and all(k in x for x in (c, pc)
+                                                    for k in ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE")):
+            busy = sum(c["SQ_VALU_MFMA_BUSY_CYCLES"]) + sum(pc["SQ_VALU_MFMA_BUSY_CYCLES"])
+            gui = (sum(c["GRBM_GUI_ACTIVE"]) + sum(pc["GRBM_GUI_ACTIVE"])) / 8.0
+            short = re.split(r"[(<]", n.replace("(anonymous namespace)::", "").replace("void ", ""))[0][-60:]
+            calls[short].append(busy / (gui * SIMDS))
+    for n, v in calls.items():
+        res[f"whole call: prep + {n}"] = {"mfma_util": round(sum(v) / len(v), 4), "calls": len(v)}
     print(json.dumps(res, indent=1))
 
 
