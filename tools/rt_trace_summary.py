@@ -1,5 +1,5 @@
-"""Merge rocprofv3 kernel and HIP API traces of an overlapped training bench: for the last three
-timed steps, the host's graph launches / event records / waits next to the first and last kernel
+"""Merge rocprofv3 kernel and HIP API traces of an overlapped training bench: for three timed steps
+from the middle of the run, the host's graph launches / event records / waits next to the first and last kernel
 of every graph replay on each queue (times in us from the first of those steps' start = the end of
 the clip + RMSprop launch before it).   python tools/rt_trace_summary.py <trace dir>"""
 import csv
@@ -14,7 +14,8 @@ af = glob.glob(os.path.join(d, "**", "*hip_api_trace.csv"), recursive=True)
 ks = sorted(csv.DictReader(open(kf[0])), key=lambda r: int(r["Start_Timestamp"]))
 api = sorted(csv.DictReader(open(af[0])), key=lambda r: int(r["Start_Timestamp"])) if af else []
 marks = [r for r in ks if "clip_rmsprop_kernel" in r["Kernel_Name"]]
-lo, hi = int(marks[-4]["End_Timestamp"]), int(marks[-1]["End_Timestamp"])
+m = len(marks) // 2  # three steps from the middle of the run (inside the timed loop)
+lo, hi = int(marks[m - 2]["End_Timestamp"]), int(marks[m + 1]["End_Timestamp"])
 ev = []
 for a in api:
     s = int(a["Start_Timestamp"])
