@@ -49,6 +49,19 @@ inline bool diag_skip(const char* name) {
 #endif
 }
 
+// development diagnostic (dev library only): PK_DIAG_TWICE names launches issued twice (the
+// marginal cost of a crop-formation kernel beside the overlapped training step; results unchanged:
+// the repeated kernels are idempotent)
+inline bool diag_twice(const char* name) {
+#ifdef PK_DEVBUILD
+  static const char* e = std::getenv("PK_DIAG_TWICE");
+  return e != nullptr && std::strstr(e, name) != nullptr;
+#else
+  (void)name;
+  return false;
+#endif
+}
+
 inline int side_prio() {
 #ifdef PK_DEVBUILD
   static const int v = [] {

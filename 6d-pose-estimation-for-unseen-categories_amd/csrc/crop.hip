@@ -937,13 +937,17 @@ extern "C" int pk_sor(const double* xyz, const int64_t* off, int B, int nmax, in
   const int nchunk = (nmax + 1023) / 1024;
   if (nmax > 0 && !pk::diag_skip("sorknn")) {
     const int tiles = (nmax + kSorThreads - 1) / kSorThreads;
-    hipLaunchKernelGGL(sor_knn_kernel, dim3((unsigned)((int64_t)tiles * B)),
-                       dim3(kSorThreads), 0, s, xyz, off, knn, pix, idxmap, H, W,
-                       pix != nullptr ? K : nullptr, tiles, B, avg, pk::side_prio());
+    for (int rep = 0; rep < (pk::diag_twice("sorknn") ? 2 : 1); ++rep) {
+      hipLaunchKernelGGL(sor_knn_kernel, dim3((unsigned)((int64_t)tiles * B)),
+                         dim3(kSorThreads), 0, s, xyz, off, knn, pix, idxmap, H, W,
+                         pix != nullptr ? K : nullptr, tiles, B, avg, pk::side_prio());
+      PK_CHECK_LAUNCH();
+    }
+  }
+  for (int rep = 0; rep < (pk::diag_twice("sorstats") ? 2 : 1); ++rep) {
+    hipLaunchKernelGGL(sor_stats_kernel, dim3(B), dim3(kStatThreads), 0, s, avg, off, std_ratio, thr, pk::side_prio());
     PK_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(sor_stats_kernel, dim3(B), dim3(kStatThreads), 0, s, avg, off, std_ratio, thr, pk::side_prio());
-  PK_CHECK_LAUNCH();
   if (nchunk > 0) {
     hipLaunchKernelGGL(sor_count_kernel, dim3(nchunk, B), dim3(1024), 0, s, avg, off, thr, nchunk, ccount);
     PK_CHECK_LAUNCH();

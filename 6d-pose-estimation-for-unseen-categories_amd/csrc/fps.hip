@@ -589,7 +589,16 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
   if (B == 0) return PK_OK;
   PK_REQUIRE(xyz && offsets && start && npoint && out);
   hipStream_t s = pk::as_stream(stream);
-  if (pk::diag_skip("fps")) return PK_OK;  // (development diagnostic only: see common.hpp)
+  if (pk::diag_skip("fps")) return PK_OK;  // (development diagnostics only: see common.hpp)
+  if (pk::diag_twice("fps")) {
+    static thread_local bool inner = false;
+    if (!inner) {
+      inner = true;
+      const int rc = pk_fps(xyz, offsets, B, nmax, start, npoint, out, out_stride, stream);
+      inner = false;
+      if (rc != PK_OK) return rc;
+    }
+  }
 #ifndef PK_FPS_ROUND2  // flat kernel (one LDS atomic per wave per iteration) up to 8192 points
   if (nmax <= 1024) return launch_fps_flat<1024, 1>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
   if (nmax <= 2048) return launch_fps_flat<1024, 2>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
