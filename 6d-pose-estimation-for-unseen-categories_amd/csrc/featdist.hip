@@ -956,6 +956,7 @@ __global__ __launch_bounds__(256) void fd_top1_merge_kernel(const unsigned long 
 // RS > 1: each row part writes its five to part_v / part_i and fd_merge_kernel<5> merges them.
 constexpr int kT5Slots = 16;
 constexpr int kT5Tasks = 1536;  // rows recomputed per block (E3b)
+constexpr int kT5X = 8;         // recomputed rows below a column's fifth key kept for its merge (E3c)
 
 // the exact distance of row `row` (tile t, in-tile i) and block column jj, as the MFMA chain forms it
 __device__ __forceinline__ float t5_exact(const f32x4* __restrict__ Ab, int t, int i, const f32x4 (*sB)[2][64],
@@ -1048,7 +1049,9 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
   __shared__ int sSlow[NC];
   __shared__ int sNslow, sNtask;
   __shared__ int sTask[kT5Tasks];
-  __shared__ unsigned long long sTaskKey[kT5Tasks];
+  __shared__ unsigned long long sFifth[NC];  // each column's fifth key after E3 (~0: fewer than five)
+  __shared__ int sXcnt[NC], sXflag[NC];       // recomputed rows below it; the column takes the slow path
+  __shared__ unsigned long long sX[NC][kT5X];
   const int per = NCG * RS;
   const int B = (int)(gridDim.x / per);
   int b, k;
@@ -1298,6 +1301,11 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
   slow = t5_any4(slow);
   t5_merge_xor(best, bsl, 1);
   t5_merge_xor(best, bsl, 2);
+  if (qd == 0) {  // (before the listing below: a full task list flags the column after it)
+    sFifth[col] = best[4];
+    sXcnt[col] = 0;
+    sXflag[col] = slow ? 1 : 0;
+  }
   if (!slow && colok) {
     // kept stream qd (ranks 0..3) whose second value is <= the fifth value may hold more members:
     // its rows (but the kept one) become recompute tasks. (The fifth value only falls as rows are
@@ -1315,7 +1323,7 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
       if (tcnt > 0) {
         tbase = atomicAdd(&sNtask, tcnt);
         if (tbase + tcnt > kT5Tasks) {
-          slow = true;  // (task list full: the slow path takes the column)
+          sXflag[col] = 1;  // (task list full: the slow path takes the column)
           tcnt = 0;
         } else {
           int k = tbase;
@@ -1327,33 +1335,32 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
   }
   __syncthreads();
   FD_STAMP(5, __builtin_amdgcn_s_memtime());
-  {  // E3b: every listed row's exact distance, one per thread
+  {  // E3b: every listed row's exact distance, one per thread; the few below the column's fifth
+     // key go to its short list (any other can never enter the five)
     const int ntask = min(sNtask, kT5Tasks);
     for (int k = tid; k < ntask; k += 64 * kTop1Waves) {
       const int d = sTask[k], t = d >> 11, cc = (d >> 4) & (NC - 1), i = d & 15;
       const float v = t5_exact(Ab, t, i, sB, cc);
-      sTaskKey[k] = ((unsigned long long)__float_as_uint(v) << 32) | (unsigned)(t * 16 + i);
-      if (__float_as_int(v) <= kClampBits) sTaskKey[k] = 0ull;  // a clamped distance: the slow path
+      const unsigned long long key = ((unsigned long long)__float_as_uint(v) << 32) | (unsigned)(t * 16 + i);
+      if (__float_as_int(v) <= kClampBits) {
+        sXflag[cc] = 1;  // a clamped distance: the slow path
+      } else if (key < sFifth[cc]) {
+        const int slot = atomicAdd(&sXcnt[cc], 1);
+        if (slot < kT5X) sX[cc][slot] = key; else sXflag[cc] = 1;
+      }
     }
   }
   __syncthreads();
   FD_STAMP(6, __builtin_amdgcn_s_memtime());
-  {  // E3c: merge the recomputed rows
-    if (qd != 0) {
-#pragma unroll
-      for (int q = 0; q < 5; ++q) best[q] = ~0ull;
+  if (qd == 0 && colok) {  // E3c: merge the column's short list
+    slow = sXflag[col] != 0;
+    if (!slow) {
+      const int nx = min(sXcnt[col], kT5X);
+      for (int x = 0; x < nx; ++x) t5_insert(best, sX[col][x]);
     }
-    for (int k = tbase; k < tbase + tcnt; ++k) {
-      const unsigned long long key = sTaskKey[k];
-      if (key == 0ull) slow = true;
-      t5_insert(best, key);
-    }
-    FD_STAMP(8, __builtin_amdgcn_s_memtime());
-    slow = t5_any4(slow);
-    t5_merge_xor(best, bsl, 1);
-    t5_merge_xor(best, bsl, 2);
-    FD_STAMP(9, __builtin_amdgcn_s_memtime());
   }
+  FD_STAMP(8, __builtin_amdgcn_s_memtime());
+  FD_STAMP(9, __builtin_amdgcn_s_memtime());
   auto emit = [&](int col, const unsigned long long (&bst)[5]) {
     const int j = j0 + col;
     if (RS == 1) {
