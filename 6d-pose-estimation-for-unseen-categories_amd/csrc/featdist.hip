@@ -1048,6 +1048,7 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
   __shared__ int sStr[NC][kT5Slots + 1];
   __shared__ int sSlow[NC];
   __shared__ int sNslow, sNtask;
+  __shared__ int sTR[kTop1Waves][2];
   __shared__ int sTask[kT5Tasks];
   __shared__ unsigned long long sFifth[NC];  // each column's fifth key after E3 (~0: fewer than five)
   __shared__ int sXcnt[NC], sXflag[NC];       // recomputed rows below it; the column takes the slow path
@@ -1112,6 +1113,10 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
       a[4] = xc[1].x, a[5] = xc[1].y, a[6] = xc[1].z, a[7] = xc[1].w;
     }
     if (tid < NC) sCnt[tid] = 0;
+    if (lane == 0) {  // the waves' row-tile ranges (E3's task listing reads them)
+      sTR[w][0] = tb;
+      sTR[w][1] = te;
+    }
     if (tid == 0) {
       sNslow = 0;
       sNtask = 0;
@@ -1298,9 +1303,11 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
       }
     }
   }
+  FD_STAMP(13, __builtin_amdgcn_s_memtime());
   slow = t5_any4(slow);
   t5_merge_xor(best, bsl, 1);
   t5_merge_xor(best, bsl, 2);
+  FD_STAMP(14, __builtin_amdgcn_s_memtime());
   if (qd == 0) {  // (before the listing below: a full task list flags the column after it)
     sFifth[col] = best[4];
     sXcnt[col] = 0;
@@ -1314,12 +1321,11 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
     const int S = best[4] == ~0ull ? 0x7f800000 : (int)(best[4] >> 32);
     if (bsl[qd] >= 0 && sK2[col][bsl[qd]] <= S) {
       const int st = sStr[col][bsl[qd]];
-      const int sqw = rs * kTop1Waves + (st >> 4);
-      const int stb = (int)((int64_t)nt * sqw / Q), ste = (int)((int64_t)nt * (sqw + 1) / Q);
+      const int stb = sTR[st >> 4][0];
       const int i = ((st >> 2) & 3) * 4 + (st & 3);
-      const int known = (int)(best[qd] & 0xffffffffu);
-      for (int t = stb; t < ste; ++t)
-        if (t * 16 + i < N1 && t * 16 + i != known) ++tcnt;
+      const int stm = min(sTR[st >> 4][1], (N1 - i + 15) >> 4);  // tiles whose row t 16 + i exists
+      const int known = (int)(best[qd] & 0xffffffffu);        // one of them: the kept row
+      tcnt = max(0, stm - stb - 1);
       if (tcnt > 0) {
         tbase = atomicAdd(&sNtask, tcnt);
         if (tbase + tcnt > kT5Tasks) {
@@ -1327,8 +1333,8 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
           tcnt = 0;
         } else {
           int k = tbase;
-          for (int t = stb; t < ste; ++t)
-            if (t * 16 + i < N1 && t * 16 + i != known) sTask[k++] = (t << 11) | (col << 4) | i;
+          for (int t = stb; t < stm; ++t)
+            if (t * 16 + i != known) sTask[k++] = (t << 11) | (col << 4) | i;
         }
       }
     }

@@ -38,9 +38,9 @@ st = np.frombuffer(buf, dtype=np.uint64).reshape(NB, 16).astype(np.int64)
 nb = int((st[:, 0] != 0).sum())
 st = st[:nb]
 if topk == 5:
-    names = ["staging 0-1", "main loop 1-2", "E0+E1 2-3", "E2 3-4", "E3 4-5", "E3b 5-6", "E3c tasks 6-8",
-             "E3c merges 8-9", "emit+sync 9-10", "slow 10-7", "total 0-7"]
-    pairs = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (6, 8), (8, 9), (9, 10), (10, 7), (0, 7)]
+    names = ["staging 0-1", "main loop 1-2", "E0+E1 2-3", "E2 3-4", "E3 scan 4-13", "E3 merges 13-14",
+             "E3 list+sync 14-5", "E3b 5-6", "E3c 6-8", "emit+sync 9-10", "slow 10-7", "total 0-7"]
+    pairs = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 13), (13, 14), (14, 5), (5, 6), (6, 8), (9, 10), (10, 7), (0, 7)]
 else:
     names = ["prologue 0-1", "main loop 1-2", "reductions 2-3", "merge+store 3-4", "total 0-4"]
     pairs = [(0, 1), (1, 2), (2, 3), (3, 4), (0, 4)]
