@@ -1245,7 +1245,7 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
       const int T = sT[c * 16 + c16];
       cm[c] = (k1[c][0] <= T ? 1u : 0u) | (k1[c][1] <= T ? 2u : 0u) | (k1[c][2] <= T ? 4u : 0u) |
               (k1[c][3] <= T ? 8u : 0u);
-      base[c] = cm[c] ? atomicAdd(&sCnt[c * 16 + c16], __popc(cm[c])) : 0;
+      base[c] = atomicAdd(&sCnt[c * 16 + c16], __popc(cm[c]));  // (unconditional: no branch per column)
     }
 #pragma unroll
     for (int c = 0; c < kTop1CT; ++c) {
