@@ -1252,13 +1252,13 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
       const int col = c * 16 + c16;
       int slot = base[c];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (((cm[c] >> r) & 1u) && slot < kT5Slots) {
-          const unsigned row = (unsigned)(t1[c][r] * 16 + 4 * g + r);
-          sKey[col][slot] = ((unsigned long long)(unsigned)k1[c][r] << 32) | row;
-          sK2[col][slot] = k2[c][r];
-          sStr[col][slot] = (w << 4) | (g << 2) | r;
-        }
+      for (int r = 0; r < 4; ++r) {  // branch-free: a stream that is not a candidate writes the pad entry
+        const bool on = ((cm[c] >> r) & 1u) && slot < kT5Slots;
+        const int dst = on ? slot : kT5Slots;
+        const unsigned row = (unsigned)(t1[c][r] * 16 + 4 * g + r);
+        sKey[col][dst] = ((unsigned long long)(unsigned)k1[c][r] << 32) | row;
+        sK2[col][dst] = k2[c][r];
+        sStr[col][dst] = (w << 4) | (g << 2) | r;
         slot += (cm[c] >> r) & 1u;
       }
     }
