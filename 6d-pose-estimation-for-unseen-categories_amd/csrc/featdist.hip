@@ -1048,6 +1048,8 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
   __shared__ int sStr[NC][kT5Slots + 1];
   __shared__ int sSlow[NC];
   __shared__ int sNslow, sNtask;
+  __shared__ unsigned long long sBest[NC][5];  // E3: each column's five (rank order) and their slots
+  __shared__ int sBsl[NC][5];
   __shared__ int sTR[kTop1Waves][2];
   __shared__ int sTask[kT5Tasks];
   __shared__ unsigned long long sFifth[NC];  // each column's fifth key after E3 (~0: fewer than five)
@@ -1265,12 +1267,11 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
   }
   __syncthreads();
   FD_STAMP(4, __builtin_amdgcn_s_memtime());
-  // E3: four threads per column (tid = 4 col + qd, lanes of one wave): each selects five among
-  // candidates qd, qd + 4, ...; two shuffle merges give the four the column's five; thread qd then
-  // lists the recompute rows of kept stream qd (E3b computes them with every thread of the block,
-  // one row each). E3c: thread 0 of the column keeps the five, threads 1-3 collect the recomputed
-  // rows they listed, and the same two merges combine the four lists (all rows distinct: a
-  // stream's rows belong to it alone, and its kept row is not listed).
+  // E3: four threads per column (tid = 4 col + qd, lanes of one wave) rank the column's candidates
+  // qd, qd + 4, ... against all of them; thread qd then lists the recompute rows of kept stream qd
+  // (E3b computes them with every thread of the block, one row each, and keeps those below the
+  // column's fifth key; E3c: thread 0 of the column merges them — all rows distinct: a stream's
+  // rows belong to it alone, and its kept row is not listed).
   unsigned long long best[5];
   int bsl[5];  // candidate slot of each kept entry
 #pragma unroll
@@ -1283,30 +1284,37 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
   int tbase = 0, tcnt = 0;
   const int n = colok ? sCnt[col] : 0;
   bool slow = n > kT5Slots;
+  // each candidate's rank among the column's n by (value, row) (keys are unique: distinct rows);
+  // ranks 0..4 are the five, written in place (the four threads are lanes of one wave: LDS
+  // program order, no barrier)
+  if (qd == 0) {
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      sBest[col][q] = ~0ull;
+      sBsl[col][q] = -1;
+    }
+  }
   if (!slow) {
     for (int i = qd; i < n; i += 4) {
-      unsigned long long key = sKey[col][i];
+      const unsigned long long key = sKey[col][i];
       const int hi = (int)(key >> 32);
       if (hi <= kClampBits) slow = true;        // a clamped distance: the slow path orders them
       if (hi >= 0x7f800000) continue;           // no row (padding)
-      if (!(key < best[4])) continue;
-      int si = i;
-#pragma unroll
-      for (int q = 0; q < 5; ++q) {
-        const bool sw = key < best[q];
-        const unsigned long long tv = sw ? best[q] : key;
-        const int ts = sw ? bsl[q] : si;
-        best[q] = sw ? key : best[q];
-        bsl[q] = sw ? si : bsl[q];
-        key = tv;
-        si = ts;
+      int rank = 0;
+      for (int j = 0; j < n; ++j) rank += sKey[col][j] < key ? 1 : 0;
+      if (rank < 5) {
+        sBest[col][rank] = key;
+        sBsl[col][rank] = i;
       }
     }
   }
   FD_STAMP(13, __builtin_amdgcn_s_memtime());
   slow = t5_any4(slow);
-  t5_merge_xor(best, bsl, 1);
-  t5_merge_xor(best, bsl, 2);
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    best[q] = sBest[col][q];
+    bsl[q] = sBsl[col][q];
+  }
   FD_STAMP(14, __builtin_amdgcn_s_memtime());
   if (qd == 0) {  // (before the listing below: a full task list flags the column after it)
     sFifth[col] = best[4];
