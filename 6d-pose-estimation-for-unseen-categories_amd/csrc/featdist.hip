@@ -1295,13 +1295,17 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
     }
   }
   if (!slow) {
+    unsigned long long kl[kT5Slots];  // the column's list in registers (entries past n: never smaller)
+#pragma unroll
+    for (int j = 0; j < kT5Slots; ++j) kl[j] = j < n ? sKey[col][j] : ~0ull;
     for (int i = qd; i < n; i += 4) {
       const unsigned long long key = sKey[col][i];
       const int hi = (int)(key >> 32);
       if (hi <= kClampBits) slow = true;        // a clamped distance: the slow path orders them
       if (hi >= 0x7f800000) continue;           // no row (padding)
       int rank = 0;
-      for (int j = 0; j < n; ++j) rank += sKey[col][j] < key ? 1 : 0;
+#pragma unroll
+      for (int j = 0; j < kT5Slots; ++j) rank += kl[j] < key ? 1 : 0;
       if (rank < 5) {
         sBest[col][rank] = key;
         sBsl[col][rank] = i;
