@@ -46,6 +46,7 @@ constexpr int kCols = kWaves * kCW * 16;  // columns per block
 constexpr int kCH = 8;   // row tiles per LDS stage
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
 
 // bytes of one 16-row operand tile per mode (f32: 64 lanes x 8 floats; bf16: 64 x 8 bf16;
 // bf16x3: hi then lo)
@@ -1024,6 +1025,11 @@ __device__ __forceinline__ void t5_merge_xor(unsigned long long (&bst)[5], int (
   ce(0, 1); ce(3, 4); ce(2, 4); ce(2, 3); ce(0, 3); ce(0, 2); ce(1, 4); ce(1, 3); ce(1, 2);
 }
 
+// a candidate record's (value, row) key
+__device__ __forceinline__ unsigned long long t5_reckey(const u32x4& r) {
+  return ((unsigned long long)r[1] << 32) | r[0];
+}
+
 // value-only compare-exchange and the sorted merges of E1
 __device__ __forceinline__ void ce_i(int& a, int& b) {
   const int lo = min(a, b), hi = max(a, b);
@@ -1043,9 +1049,8 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
   __shared__ int sT[NC];
   __shared__ int sCnt[NC];
   // candidate lists, rows padded by one entry: a wave's 16 columns at one slot spread over the banks
-  __shared__ unsigned long long sKey[NC][kT5Slots + 1];
-  __shared__ int sK2[NC][kT5Slots + 1];
-  __shared__ int sStr[NC][kT5Slots + 1];
+  __shared__ u32x4 sRec[NC][kT5Slots + 1];  // {row, key bits, second key bits, stream}: the key is the
+                                            // first 8 bytes read as one unsigned 64-bit (value, row)
   __shared__ int sSlow[NC];
   __shared__ int sNslow, sNtask;
   __shared__ unsigned long long sBest[NC][5];  // E3: each column's five (rank order) and their slots
@@ -1258,9 +1263,7 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
         const bool on = ((cm[c] >> r) & 1u) && slot < kT5Slots;
         const int dst = on ? slot : kT5Slots;
         const unsigned row = (unsigned)(t1[c][r] * 16 + 4 * g + r);
-        sKey[col][dst] = ((unsigned long long)(unsigned)k1[c][r] << 32) | row;
-        sK2[col][dst] = k2[c][r];
-        sStr[col][dst] = (w << 4) | (g << 2) | r;
+        sRec[col][dst] = u32x4{row, (unsigned)k1[c][r], (unsigned)k2[c][r], (unsigned)((w << 4) | (g << 2) | r)};
         slot += (cm[c] >> r) & 1u;
       }
     }
@@ -1297,9 +1300,9 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
   if (!slow) {
     unsigned long long kl[kT5Slots];  // the column's list in registers (entries past n: never smaller)
 #pragma unroll
-    for (int j = 0; j < kT5Slots; ++j) kl[j] = j < n ? sKey[col][j] : ~0ull;
+    for (int j = 0; j < kT5Slots; ++j) kl[j] = j < n ? t5_reckey(sRec[col][j]) : ~0ull;
     for (int i = qd; i < n; i += 4) {
-      const unsigned long long key = sKey[col][i];
+      const unsigned long long key = t5_reckey(sRec[col][i]);
       const int hi = (int)(key >> 32);
       if (hi <= kClampBits) slow = true;        // a clamped distance: the slow path orders them
       if (hi >= 0x7f800000) continue;           // no row (padding)
@@ -1331,8 +1334,9 @@ __global__ __launch_bounds__(64 * kTop1Waves, 1) void fd_top5_kernel(
     // merged, so the streams listed against the first selection cover every stream that can still
     // hold a member.)
     const int S = best[4] == ~0ull ? 0x7f800000 : (int)(best[4] >> 32);
-    if (bsl[qd] >= 0 && sK2[col][bsl[qd]] <= S) {
-      const int st = sStr[col][bsl[qd]];
+    const u32x4 rec = bsl[qd] >= 0 ? sRec[col][bsl[qd]] : u32x4{0u, 0u, 0x7fffffffu, 0u};
+    if (bsl[qd] >= 0 && (int)rec[2] <= S) {
+      const int st = (int)rec[3];
       const int stb = sTR[st >> 4][0];
       const int i = ((st >> 2) & 3) * 4 + (st & 3);
       const int stm = min(sTR[st >> 4][1], (N1 - i + 15) >> 4);  // tiles whose row t 16 + i exists
