@@ -945,13 +945,16 @@ __global__ __launch_bounds__(256) void fd_top1_merge_kernel(const unsigned long 
 // loop:
 //   E0/E1  T = the 5th smallest of the column's 32 lane minima (min over r): 32 distinct rows'
 //          distances, so an upper bound of the 5th smallest distance;
-//   E2     every stream whose minimum is <= T appends (key, row, second value, stream) to the
-//          column's candidate list in LDS (16 slots);
-//   E3     one thread per column sorts the candidates by (value, row) and keeps five. A kept stream
-//          other than the fifth whose second value is <= the fifth value may hold more members:
-//          its rows are recomputed exactly (the f32 MFMA accumulates as one fmaf chain over the
-//          contraction slots in order, bit for bit: tools/mfma_order_probe.py), one row per
-//          thread of the block (a task list in LDS), and merged;
+//   E2     every stream whose minimum is <= T writes a 16-byte record (row, key, second value,
+//          stream) into the column's candidate list in LDS (16 slots, one slot-range reservation
+//          per lane and column);
+//   E3     four threads per column rank each candidate by (value, row) against the whole list;
+//          ranks 0..4 are the five. A kept stream other than the fifth whose second value is <= the
+//          fifth value may hold more members: its rows (counted in closed form from the waves'
+//          tile ranges) are recomputed exactly (the f32 MFMA accumulates as one fmaf chain over the
+//          contraction slots in order, bit for bit: tools/mfma_order_probe.py), one row per thread
+//          of the block (a task list in LDS, E3b); the few below the column's fifth key go to a
+//          short per-column list that one thread merges (E3c);
 //   slow   a column with more than 16 candidates, or a distance at or below torch.cdist's
 //          clamp_min(1e-30), is recomputed whole by one wave (clamped; ties to the lower row).
 // RS > 1: each row part writes its five to part_v / part_i and fd_merge_kernel<5> merges them.
