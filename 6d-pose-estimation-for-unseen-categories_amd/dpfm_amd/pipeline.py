@@ -612,13 +612,16 @@ class PipelinedTrainer:
             if self._ir_enqueued[k]:
                 s.wait_event(self.ir_done[k])
 
-    def flush(self):
+    def flush(self, check: bool = True):
         """Compute the IR still pending for the last step (its buffer's I_k) and order the
-        current stream after it: every log returned so far then holds its IR."""
+        current stream after it: every log returned so far then holds its IR. check=True then
+        reads the IR's per-crop index status of both buffers (a host sync: flush() runs outside
+        timed loops) and raises PoseKernError if a point-map index was out of range."""
         if not self.defer_ir or self.i == 0:
             return
-        if self.own_main:  # (as in __call__: the replay after the caller's queued work)
-            self.main.wait_stream(torch.cuda.current_stream())
+        cur = torch.cuda.current_stream()
+        if cur != self.main:  # (as in __call__: the replay after the caller's queued work)
+            self.main.wait_stream(cur)
         k = (self.i - 1) & 1
         if self._trained[k]:
             with torch.cuda.stream(self.side):
@@ -626,11 +629,18 @@ class PipelinedTrainer:
                 self._replay_ir(k)
             self._trained[k] = False
         self.wait_ir()
+        if check:
+            for log in self.logs:
+                ops.check_index_status(log.get("ir_index_status"), "PipelinedTrainer IR (naive point map)")
 
     def __call__(self) -> dict:
         k = self.i & 1
-        if self.own_main:  # the step after the caller's queued work (its reads of earlier logs / params)
-            self.main.wait_stream(torch.cuda.current_stream())
+        # a caller on another stream than the replays' (a private main stream, or a caller that
+        # switched streams since construction): the step after the caller's queued work (its reads
+        # of earlier logs / params), and the caller's stream after the step
+        cur = torch.cuda.current_stream()
+        if cur != self.main:
+            self.main.wait_stream(cur)
         if not self.side_after:
             self._form(k ^ 1)                  # next batch's crops, concurrently
         with torch.cuda.stream(self.main):
@@ -642,8 +652,8 @@ class PipelinedTrainer:
             self.consumed[k].record(self.main)
         if self.side_after:
             self._form(k ^ 1)
-        if self.own_main:  # the caller's stream reads the step's outputs after it
-            torch.cuda.current_stream().wait_stream(self.main)
+        if cur != self.main:  # the caller's stream reads the step's outputs after it
+            cur.wait_stream(self.main)
         self._trained[k] = True
         self.i += 1
         return self.logs[k]

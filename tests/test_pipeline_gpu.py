@@ -230,6 +230,39 @@ def test_pipelined_trainer_matches_eager(device):
         assert not diff, diff
 
 
+def test_pipelined_trainer_private_stream_ordered_with_caller(device):
+    """PipelinedTrainer driven from a caller stream other than its replay stream — its default
+    main stream, or a private one (main_priority=1): every call waits for the caller's
+    queued work and hands the step back to the caller's stream, so copies of the loss taken on the
+    caller stream right after each call, with no device synchronisation, are the step's losses and
+    agree between the two pipelines step for step (same seeds, same crops); flush() checks the
+    IR's index status (clean crops: no error)."""
+    from dpfm_amd.dataset.object import CropFormation
+    from dpfm_amd.models.dpfm import DPFMNet
+    from dpfm_amd.pipeline import PipelinedTrainer, TrainStep, make_frame_batch
+    F, N = 4, 512
+    fb, op = make_frame_batch(F, N, N, seed=93, device=device)
+    torch.manual_seed(2)
+    ma, mb = DPFMNet().to(device), DPFMNet().to(device)
+    mb.load_state_dict(ma.state_dict())
+    losses = []
+    for m, prio in ((ma, 0), (mb, 1)):
+        torch.manual_seed(3)  # (the same global RNG state for both pipelines' warm-up and capture)
+        p = PipelinedTrainer(CropFormation(n1=N, npoint=N, seed=5), TrainStep(m, seed=9, capturable=True), fb, op,
+                             warmup=2, main_priority=prio)
+        caller = torch.cuda.Stream()
+        got = []
+        with torch.cuda.stream(caller):
+            for _ in range(4):
+                got.append(p()["loss"].clone())
+            p.flush()
+        torch.cuda.synchronize()
+        losses.append(got)
+    for a, b in zip(*losses):
+        assert torch.equal(a, b), (a, b)
+    assert all(float(a) > 0.0 for a in losses[0])  # (real losses, not a copy taken before the step)
+
+
 def test_pipelined_trainer_deferred_ir_readers(device):
     """The deferred IR is written by a side-stream graph: wait_ir() orders the reader after
     every I_k enqueued so far (the logs of all calls but the last), flush() computes the last
