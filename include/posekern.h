@@ -418,7 +418,9 @@ int pk_linear_ex2(const pk_linear_args* a0, const pk_linear_args* a1, void* stre
  *   work: scratch of pk_feat_dist_work_size(B, V1max, V2max, topk, mode) bytes (may be 0 and
  *     NULL), any contents: nothing in it is read before this call writes it, and nothing is kept
  *     across calls (round 5: the mode-0 top-1 pass finishes every column inside one workgroup,
- *     or writes row-part keys that a second launch merges — no arrival words, no zeroing contract).
+ *     or writes row-part keys that a second launch merges — no arrival words, no zeroing contract;
+ *     round 6: the mode-0 top-5 pass likewise — exact five per column, recomputing only the rows
+ *     of kept streams that may hold more members; row parts merged by a second launch).
  *   out_idx int64 [B,V2max,topk] ascending distance (ties: lower index); out_dist f32
  *   [B,V2max,topk] Euclidean distances (may be NULL). Fused selection epilogue. */
 int64_t pk_feat_dist_work_size(int B, int V1max, int V2max, int topk, int mode);
