@@ -1747,8 +1747,21 @@ static int lin_setup(const pk_linear_args* a, LinEpi& e, int64_t& sx_out) {
 
 // points per wave of the channels-first kernel: 16 SUB, as many as keep >= 1024 waves and <= 64
 // operand VGPRs; SUB-aligned items and strides for the vector loads / stores
+// development knob PK_CF_SUBMAX (1, 2, 4): cap on the channels-first points-per-lane choice
+static int cf_submax() {
+#ifdef PK_DEVBUILD
+  static const int v = [] { const char* e = std::getenv("PK_CF_SUBMAX"); return e ? std::atoi(e) : 4; }();
+  return v;
+#else
+  return 4;
+#endif
+}
+
 static int cf_sub(int64_t R, int N, int Cin, int64_t sx, const LinEpi& e) {
-  int sub = R >= 131072 ? 4 : R >= 32768 ? 2 : 1;
+  // 16 points per wave below 131,072 rows (round 6: the configs[1] step's 65,536-row layers ran
+  // 11 % faster than with 32 — more waves in flight per CU; tools/cf_sub_ab.sh)
+  int sub = R >= 131072 ? 4 : 1;
+  sub = std::min(sub, cf_submax());
   sub = std::min(sub, 256 / Cin);
   while (sub > 1 && N % (16 * sub)) sub >>= 1;  // N % 16 != 0: SUB = 1 with ragged item tails
   while (sub > 1 && ((sx % sub) || (e.sy % sub) || (e.add && (e.sa % sub)) || (e.add2 && (e.sa2 % sub)))) sub >>= 1;
@@ -1957,8 +1970,9 @@ extern "C" int pk_linear_ex(const pk_linear_args* a, void* stream) {
   }
   if (layout == 1 && (Cin == 16 || Cin == 32 || Cin == 64 || Cin == 128) && N > 0) {
     PK_REQUIRE(e.y2 == nullptr && !e.store_cf);
-    // points per wave: 16 SUB, as many as keep >= 1024 waves and <= 64 operand VGPRs
-    int sub = R >= 131072 ? 4 : R >= 32768 ? 2 : 1;
+    // points per wave: 16 SUB (SUB = 4 from 131,072 rows, else 1: cf_sub), <= 64 operand VGPRs
+    int sub = R >= 131072 ? 4 : 1;  // (as cf_sub)
+    sub = std::min(sub, cf_submax());
     sub = std::min(sub, 256 / Cin);
     while (sub > 1 && N % (16 * sub)) sub >>= 1;  // N % 16 != 0: SUB = 1 with ragged item tails
     // vector loads / stores of SUB points need SUB-aligned batch strides
