@@ -415,12 +415,20 @@ __global__ __launch_bounds__(NT) void fps_lane_kernel(
 // ds_max_u64 of key = (distance bits << 32) | ~index (max distance, then lowest index, torch.max's
 // tie rule) into a triple-buffered word, one barrier, one broadcast read. Round 2's kernels spent
 // ~0.7 us per iteration in per-bucket / per-wave reductions and a 16-slot second stage.
-template <int NT, int PPT>
+#ifdef PK_DEVBUILD
+// (development: per-wave phase cycle sums of the stamped flat kernel, tools/fps_stamps.py)
+__device__ unsigned long long g_fps_stamps[64 * 16 * 8];
+#endif
+
+template <int NT, int PPT, bool STAMP = false>
 __global__ __launch_bounds__(NT) void fps_flat_kernel(
     const float* __restrict__ xyz, const int64_t* __restrict__ offsets,
     const int32_t* __restrict__ start, const int32_t* __restrict__ npoint,
     int64_t* __restrict__ out, int out_stride, int prio) {
   pk::set_wave_prio(prio);
+  // STAMP (dev only): per wave, cycles in read + box test / update + wave reduction / atomic +
+  // barrier, and the number of updating iterations
+  [[maybe_unused]] unsigned long long st_box = 0, st_upd = 0, st_bar = 0, st_nupd = 0, t0 = 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);  // [3] (4 words reserved)
   const int b = blockIdx.x;
@@ -479,6 +487,7 @@ __global__ __launch_bounds__(NT) void fps_flat_kernel(
   float cx = sx[far], cy = sy[far], cz = sz[far];
   unsigned long long wkey = 0ull;  // the wave's best (cached while its lanes skip)
   int64_t* __restrict__ o = out + (int64_t)b * out_stride;
+  if (STAMP) t0 = __builtin_amdgcn_s_memtime();
   for (int i = 0; i < np; ++i) {
     if (tid == 0) o[i] = far;
     const float ddx = fmaxf(fmaxf(bx0 - cx, cx - bx1), 0.f);
@@ -486,7 +495,14 @@ __global__ __launch_bounds__(NT) void fps_flat_kernel(
     const float ddz = fmaxf(fmaxf(bz0 - cz, cz - bz1), 0.f);
     const float lb = (ddx * ddx + ddy * ddy) + ddz * ddz;
     const bool need = lval && !(lb * 0.99999809f >= bd);
-    if (__ballot(need)) {  // wave-uniform
+    const uint64_t needm = __ballot(need);
+    unsigned long long t1 = 0;
+    if (STAMP) {
+      t1 = __builtin_amdgcn_s_memtime();
+      st_box += t1 - t0;
+    }
+    if (needm) {  // wave-uniform
+      if (STAMP) ++st_nupd;
       if (need) {
         const f32x2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
 #pragma unroll
@@ -516,23 +532,42 @@ __global__ __launch_bounds__(NT) void fps_flat_kernel(
       const uint32_t widx = pk::readlane((uint32_t)(i0 + bk), __ffsll((unsigned long long)at) - 1);
       wkey = ((unsigned long long)wbits << 32) | (unsigned long long)(0xffffffffu - widx);
     }
+    unsigned long long t2 = 0;
+    if (STAMP) {
+      t2 = __builtin_amdgcn_s_memtime();
+      st_upd += t2 - t1;
+    }
     if (lane == 0 && wkey != 0ull) atomicMax(&keys[i % 3], wkey);
     if (tid == 0) keys[(i + 1) % 3] = 0ull;  // last read after barrier i - 2: every wave is past it
     __syncthreads();
+    if (STAMP) {
+      t0 = __builtin_amdgcn_s_memtime();
+      st_bar += t0 - t2;
+    }
     const unsigned long long key = keys[i % 3];
     far = (int)(0xffffffffu - (uint32_t)(key & 0xffffffffull));
     cx = sx[far];
     cy = sy[far];
     cz = sz[far];
   }
+#ifdef PK_DEVBUILD
+  if (STAMP && lane == 0 && b < 64) {
+    unsigned long long* g = g_fps_stamps + ((size_t)b * 16 + pk::wave_id()) * 8;
+    g[0] = st_box;
+    g[1] = st_upd;
+    g[2] = st_bar;
+    g[3] = st_nupd;
+    g[4] = (unsigned long long)np;
+  }
+#endif
 }
 
-template <int NT, int PPT>
+template <int NT, int PPT, bool STAMP = false>
 int launch_fps_flat(const float* xyz, const int64_t* offsets, const int32_t* start, const int32_t* npoint,
                     int64_t* out, int out_stride, int B, int nmax, hipStream_t s) {
   const int n_pad = (nmax + 3) & ~3;
   const size_t lds = 4 * sizeof(unsigned long long) + 3 * (size_t)n_pad * sizeof(float);
-  hipLaunchKernelGGL((fps_flat_kernel<NT, PPT>), dim3(B), dim3(NT), lds, s, xyz, offsets, start, npoint, out,
+  hipLaunchKernelGGL((fps_flat_kernel<NT, PPT, STAMP>), dim3(B), dim3(NT), lds, s, xyz, offsets, start, npoint, out,
                      out_stride, pk::side_prio());
   PK_CHECK_LAUNCH();
   return PK_OK;
@@ -642,7 +677,7 @@ extern "C" int pk_fps(const float* xyz, const int64_t* offsets, int B, int nmax,
 
 #ifdef PK_DEVBUILD
 // Development hook (not part of include/posekern.h): force the block size / points
-// per thread, flat (pruned = 4), per-lane buckets (3), pruned (1) or plain (0), for tools/kbench.py's sweeps.
+// per thread, flat with phase stamps (pruned = 6), flat (4), per-lane buckets (3), pruned (1) or plain (0), for tools/kbench.py's sweeps.
 extern "C" int pkdev_fps_cfg(const float* xyz, const int64_t* offsets, int B, int nmax,
                              const int32_t* start, const int32_t* npoint, int64_t* out,
                              int out_stride, int nt, int pruned, void* stream) {
@@ -650,14 +685,22 @@ extern "C" int pkdev_fps_cfg(const float* xyz, const int64_t* offsets, int B, in
   const int ppt = (nmax + nt - 1) / nt;
 #define PK_FPS(NT, PPT)                                                                          \
   if (nt == NT && ppt <= PPT)                                                                    \
-    return pruned == 4 ? launch_fps_flat<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s) \
+    return pruned == 6 ? launch_fps_flat<NT, PPT, true>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s) \
+           : pruned == 4 ? launch_fps_flat<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s) \
            : pruned == 3 ? launch_fps_lane<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, s) \
            : pruned ? launch_fps<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s) \
                   : launch_fps_plain<NT, PPT>(xyz, offsets, start, npoint, out, out_stride, B, nmax, s);
   PK_FPS(256, 4) PK_FPS(256, 8) PK_FPS(256, 16) PK_FPS(256, 32)
   PK_FPS(512, 2) PK_FPS(512, 4) PK_FPS(512, 8) PK_FPS(512, 16) PK_FPS(512, 26)
-  PK_FPS(1024, 2) PK_FPS(1024, 4) PK_FPS(1024, 8) PK_FPS(1024, 13)
+  PK_FPS(1024, 2) PK_FPS(1024, 4) PK_FPS(1024, 8) PK_FPS(1024, 10) PK_FPS(1024, 13)
 #undef PK_FPS
   return PK_ERR_ARG;
+}
+#endif  // PK_DEVBUILD
+
+#ifdef PK_DEVBUILD
+extern "C" int pkdev_fps_stamps(unsigned long long* host, int n) {
+  if (n > 64 * 16 * 8) n = 64 * 16 * 8;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fps_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
 }
 #endif  // PK_DEVBUILD

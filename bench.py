@@ -171,12 +171,13 @@ def ball_query_roofline(dev, probe_launches: int = 10, blocks: int = 7) -> dict:
             "ms_per_launch": round(ms, 4), "bytes_per_launch": byts}
 
 
-def feat_dist_roofline(dev, launches: int = 20) -> dict:
+def feat_dist_roofline(dev, launches: int = 20, topk: int = 1) -> dict:
     """The north-star MFMA gate kernel: pk_feat_dist_topk (fp32 argmin, the naive solver's and the
     IR's feature distance, fmap2pointmap_solvers/naive.py:20,33) at configs[1] (32 crops of
     1024 x 1024, K = 32: 2.147 GFLOP per call), `launches` back-to-back calls in one HIP graph
     between two HIP events on the launch stream (its prep + main passes included), spectral-basis
-    operands."""
+    operands. topk=5: the configured solver's top-5 (spacial_filtering.py:19,32-38; the same
+    contraction, its epilogue and near-tie recompute included in the time)."""
     from dpfm_amd import ops
     from dpfm_amd.dataset.synthetic import lbo_operators
     B, V = 32, 1024
@@ -185,7 +186,7 @@ def feat_dist_roofline(dev, launches: int = 20) -> dict:
     C = (torch.eye(30)[None] + 0.3 * torch.randn(B, 30, 30, generator=torch.Generator().manual_seed(B))).to(dev)
     n = torch.full((B,), V, dtype=torch.int32, device=dev)
     wk = torch.empty(1 << 24, dtype=torch.uint8, device=dev)
-    f = lambda: ops.feat_dist_topk(ex, C, ey, n, n, 1, work=wk)  # noqa: E731
+    f = lambda: ops.feat_dist_topk(ex, C, ey, n, n, topk, work=wk)  # noqa: E731
     for _ in range(3):
         f()
     torch.cuda.synchronize()
@@ -207,7 +208,7 @@ def feat_dist_roofline(dev, launches: int = 20) -> dict:
     ms = sorted(s.elapsed_time(e) for s, e in evs)[2] / launches
     flops = 2.0 * B * V * V * 32
     ach = flops / (ms * 1e-3) / 1e12
-    return {"kernel": "pk_feat_dist_topk (configs[1]: 32 x 1024 x 1024, fp32 top-1, prep + main)", "bound": "mfma",
+    return {"kernel": f"pk_feat_dist_topk (configs[1]: 32 x 1024 x 1024, fp32 top-{topk}, prep + main)", "bound": "mfma",
             "achieved": round(ach, 2), "peak": F32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / F32_MFMA_TFLOPS, 4),
             "ms_per_launch": round(ms, 4), "flops_per_launch": flops, "launches": launches}
 
@@ -1121,6 +1122,10 @@ def main():
         if args.mode == "train" and not args.no_roofline_probe and world == 1:
             out["roofline_ball_query"] = ball_query_roofline(dev)
             out["roofline_feat_dist"] = feat_dist_roofline(dev)
+        if args.mode == "infer" and not args.no_roofline_probe and world == 1 and args.points == 1024:
+            # the configured solver's top-5 timed as the pipeline issues it (graph replays, warm
+            # clocks); roofline_mfma_kernels' entry is the eager per-op probe (host gaps included)
+            out["roofline_feat_dist_top5"] = feat_dist_roofline(dev, topk=5)
         if not args.no_cpu_baseline and world == 1 and not args.ragged:
             if args.mode == "train":
                 out["cpu_baseline"] = cpu_baseline(args.cpu_crops, args.points, args.points)
