@@ -218,6 +218,20 @@ __device__ __forceinline__ uint32_t wave_max_u32_s(uint32_t v) {
   return a > c ? a : c;
 }
 
+// Wave-uniform signed max of an i32 (result is a scalar).
+__device__ __forceinline__ int wave_max_i32_s(int v) {
+  int o;
+  o = (int)PK_DPP(v, 0xB1); v = o > v ? o : v;
+  o = (int)PK_DPP(v, 0x4E); v = o > v ? o : v;
+  o = (int)PK_DPP(v, 0x141); v = o > v ? o : v;
+  o = (int)PK_DPP(v, 0x140); v = o > v ? o : v;
+  int a = (int)readlane((uint32_t)v, 0), b = (int)readlane((uint32_t)v, 16), c = (int)readlane((uint32_t)v, 32),
+      d = (int)readlane((uint32_t)v, 48);
+  a = a > b ? a : b;
+  c = c > d ? c : d;
+  return a > c ? a : c;
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32_s(uint32_t v) {
   v = row_min_u32(v);
   uint32_t a = readlane(v, 0), b = readlane(v, 16), c = readlane(v, 32), d = readlane(v, 48);

@@ -415,12 +415,18 @@ __global__ __launch_bounds__(NT) void fps_lane_kernel(
 // ds_max_u64 of key = (distance bits << 32) | ~index (max distance, then lowest index, torch.max's
 // tie rule) into a triple-buffered word, one barrier, one broadcast read. Round 2's kernels spent
 // ~0.7 us per iteration in per-bucket / per-wave reductions and a 16-slot second stage.
+// Round 6 (phase stamps, profiles/r06_fps_variants.txt): an iteration is paced by the updating
+// wave's dependent chain (distances, max, argmax, wave reduction, key), so that chain was cut:
+// the argmax runs with the whole wave active beside the wave reduction (filling its DPP wait
+// states), its compares write separate SGPR masks, the reduction is a signed max of the distance
+// bits (no validity select), the skip ballot is the bare compare, and the TU is built without the
+// atomic optimizer: 0.49 -> 0.40 us per iteration on the kbench crops, indices unchanged.
 #ifdef PK_DEVBUILD
 // (development: per-wave phase cycle sums of the stamped flat kernel, tools/fps_stamps.py)
 __device__ unsigned long long g_fps_stamps[64 * 16 * 8];
 #endif
 
-template <int NT, int PPT, bool STAMP = false>
+template <int NT, int PPT, bool STAMP = false, bool TRIM = true>
 __global__ __launch_bounds__(NT) void fps_flat_kernel(
     const float* __restrict__ xyz, const int64_t* __restrict__ offsets,
     const int32_t* __restrict__ start, const int32_t* __restrict__ npoint,
@@ -494,7 +500,9 @@ __global__ __launch_bounds__(NT) void fps_flat_kernel(
     const float ddy = fmaxf(fmaxf(by0 - cy, cy - by1), 0.f);
     const float ddz = fmaxf(fmaxf(bz0 - cz, cz - bz1), 0.f);
     const float lb = (ddx * ddx + ddy * ddy) + ddz * ddz;
-    const bool need = lval && !(lb * 0.99999809f >= bd);
+    // an empty lane's bd = -1 fails the test by itself (its box bound is +inf), so the ballot is the
+    // bare compare's mask
+    const bool need = TRIM ? !(lb * 0.99999809f >= bd) : lval && !(lb * 0.99999809f >= bd);
     const uint64_t needm = __ballot(need);
     unsigned long long t1 = 0;
     if (STAMP) {
@@ -519,17 +527,45 @@ __global__ __launch_bounds__(NT) void fps_flat_kernel(
         float m = D[0][0];
 #pragma unroll
         for (int k = 1; k < PPT; ++k) m = fmaxf(m, D[k >> 1][k & 1]);
-        int kk = PPT - 1;
-#pragma unroll
-        for (int k = PPT - 2; k >= 0; --k) kk = D[k >> 1][k & 1] == m ? k : kk;  // first k at the max
         bd = m;
-        bk = kk;
+        if (!TRIM) {  // (development A/B: the round-5 chain, PK_FPS_TRIM=0)
+          int kk = PPT - 1;
+#pragma unroll
+          for (int k = PPT - 2; k >= 0; --k) kk = D[k >> 1][k & 1] == m ? k : kk;
+          bk = kk;
+        }
       }
-      const bool valid = bd >= 0.f;
-      const uint32_t bits = valid ? pk::f32_bits(bd) : 0u;
-      const uint32_t wbits = pk::wave_max_u32_s(bits);
-      const uint64_t at = __ballot(valid && bits == wbits);
-      const uint32_t widx = pk::readlane((uint32_t)(i0 + bk), __ffsll((unsigned long long)at) - 1);
+      uint32_t wbits, widx;
+      if (!TRIM) {
+        const bool valid = bd >= 0.f;
+        const uint32_t bits = valid ? pk::f32_bits(bd) : 0u;
+        wbits = pk::wave_max_u32_s(bits);
+        const uint64_t at = __ballot(valid && bits == wbits);
+        widx = pk::readlane((uint32_t)(i0 + bk), __ffsll((unsigned long long)at) - 1);
+      } else {
+        // the argmax with the whole wave active (a lane that skipped finds its unchanged bk again),
+        // so it can fill the wave reduction's DPP wait states; every compare into its own SGPR mask,
+        // then the select chain (the VCC form pays two wait states per point)
+        {
+          uint64_t eq[PPT];
+#pragma unroll
+          for (int k = 0; k < PPT - 1; ++k) eq[k] = __builtin_amdgcn_fcmpf(D[k >> 1][k & 1], bd, 1 /* OEQ */);
+          int kk = PPT - 1;
+#pragma unroll
+          for (int k = PPT - 2; k >= 0; --k) {
+            int r;
+            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(kk), "I"(k), "s"(eq[k]));
+            kk = r;
+          }
+          bk = kk;
+        }
+        // signed max of the distance bits: an empty lane's -1.0f is negative and never the max; the
+        // valid lanes are a prefix of the wave, so the first lane at the max is a valid one
+        const int bits = __float_as_int(bd);
+        wbits = (uint32_t)pk::wave_max_i32_s(bits);
+        const uint64_t at = __builtin_amdgcn_uicmp((uint32_t)bits, wbits, 32 /* EQ */);
+        widx = pk::readlane((uint32_t)(i0 + bk), __ffsll((unsigned long long)at) - 1);
+      }
       wkey = ((unsigned long long)wbits << 32) | (unsigned long long)(0xffffffffu - widx);
     }
     unsigned long long t2 = 0;
@@ -567,6 +603,15 @@ int launch_fps_flat(const float* xyz, const int64_t* offsets, const int32_t* sta
                     int64_t* out, int out_stride, int B, int nmax, hipStream_t s) {
   const int n_pad = (nmax + 3) & ~3;
   const size_t lds = 4 * sizeof(unsigned long long) + 3 * (size_t)n_pad * sizeof(float);
+#ifdef PK_DEVBUILD
+  static const bool untrimmed = getenv("PK_FPS_TRIM") && atoi(getenv("PK_FPS_TRIM")) == 0;
+  if (untrimmed) {
+    hipLaunchKernelGGL((fps_flat_kernel<NT, PPT, STAMP, false>), dim3(B), dim3(NT), lds, s, xyz, offsets, start,
+                       npoint, out, out_stride, pk::side_prio());
+    PK_CHECK_LAUNCH();
+    return PK_OK;
+  }
+#endif
   hipLaunchKernelGGL((fps_flat_kernel<NT, PPT, STAMP>), dim3(B), dim3(NT), lds, s, xyz, offsets, start, npoint, out,
                      out_stride, pk::side_prio());
   PK_CHECK_LAUNCH();
