@@ -417,10 +417,13 @@ __global__ __launch_bounds__(NT) void fps_lane_kernel(
 // ~0.7 us per iteration in per-bucket / per-wave reductions and a 16-slot second stage.
 // Round 6 (phase stamps, profiles/r06_fps_variants.txt): an iteration is paced by the updating
 // wave's dependent chain (distances, max, argmax, wave reduction, key), so that chain was cut:
-// the argmax runs with the whole wave active beside the wave reduction (filling its DPP wait
-// states), its compares write separate SGPR masks, the reduction is a signed max of the distance
-// bits (no validity select), the skip ballot is the bare compare, and the TU is built without the
-// atomic optimizer: 0.49 -> 0.40 us per iteration on the kbench crops, indices unchanged.
+// the argmax runs with the whole wave active beside the wave reduction (the compiler places its
+// compare -> select wait states under the DPP chain), the reduction is a signed max of the
+// distance bits (no validity select), the skip ballot is the bare compare, and the TU is built
+// without the atomic optimizer: 0.49 -> 0.41 us per iteration on the kbench crops, indices
+// unchanged. (An inline-asm select reading per-compare SGPR masks measured 0.40 but is not kept:
+// hipcc does not pad the VALU-mask-write -> v_cndmask hazard into an asm statement, and it pads
+// two wait states there for its own code.)
 #ifdef PK_DEVBUILD
 // (development: per-wave phase cycle sums of the stamped flat kernel, tools/fps_stamps.py)
 __device__ unsigned long long g_fps_stamps[64 * 16 * 8];
@@ -544,19 +547,12 @@ __global__ __launch_bounds__(NT) void fps_flat_kernel(
         widx = pk::readlane((uint32_t)(i0 + bk), __ffsll((unsigned long long)at) - 1);
       } else {
         // the argmax with the whole wave active (a lane that skipped finds its unchanged bk again),
-        // so it can fill the wave reduction's DPP wait states; every compare into its own SGPR mask,
-        // then the select chain (the VCC form pays two wait states per point)
+        // so the compiler can place its compare -> select wait states under the wave reduction's DPP
+        // chain (plain code: the compiler pads every hazard; an inline-asm select would not be)
         {
-          uint64_t eq[PPT];
-#pragma unroll
-          for (int k = 0; k < PPT - 1; ++k) eq[k] = __builtin_amdgcn_fcmpf(D[k >> 1][k & 1], bd, 1 /* OEQ */);
           int kk = PPT - 1;
 #pragma unroll
-          for (int k = PPT - 2; k >= 0; --k) {
-            int r;
-            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(kk), "I"(k), "s"(eq[k]));
-            kk = r;
-          }
+          for (int k = PPT - 2; k >= 0; --k) kk = D[k >> 1][k & 1] == bd ? k : kk;  // first k at the max
           bk = kk;
         }
         // signed max of the distance bits: an empty lane's -1.0f is negative and never the max; the
